@@ -1,0 +1,217 @@
+"""Benchmark of the MVDet project+fuse hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2] [--no-cpu-baseline]
+
+A *step* is one pass of the hot path over one frame batch of synthetic input
+already resident in HBM: the warp of every view (a5), the zero-copy concat (a6),
+conv1+ReLU, conv2+ReLU, conv3 (a7-a9); the identity interpolate (a10) is elided.
+The backbone, the 3x upsample (a4) and the image head are NOT in the step
+(SURVEY §8(d)).  Metric: frames/s (= B * K / wall).  N>1 (torchrun, one rank per
+GPU) runs the view-parallel path of ``mvdet_amd.parallel``.
+
+Rank 0 prints ONE JSON line; see DESIGN.md §Measurement for every field.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: fp32 matrix peak (spec)
+
+
+def build_mc(C, num_cam, params, device):
+    mc = torch.nn.Sequential(torch.nn.Conv2d(C * num_cam + 2, 512, 3, padding=1), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False))
+    if params is not None:
+        mc.load_state_dict({k.replace("map_classifier.", ""): torch.from_numpy(v)
+                            for k, v in params.items() if k.startswith("map_classifier.")})
+    return mc.to(device)
+
+
+def head_params(num_cam, seed, C):
+    """Default-Conv2d-bound uniform init (same recipe as the test fixtures)."""
+    rng = np.random.default_rng(seed)
+    cin = C * num_cam + 2
+    shapes = {"map_classifier.0.weight": (512, cin, 3, 3), "map_classifier.0.bias": (512,),
+              "map_classifier.2.weight": (512, 512, 3, 3), "map_classifier.2.bias": (512,),
+              "map_classifier.4.weight": (1, 512, 3, 3)}
+    fan = {"map_classifier.0": cin * 9, "map_classifier.2": 512 * 9, "map_classifier.4": 512 * 9}
+    out = {}
+    for k, s in shapes.items():
+        b = 1.0 / np.sqrt(fan[k.rsplit(".", 1)[0]])
+        out[k] = rng.uniform(-b, b, size=s).astype(np.float32)
+    return out
+
+
+def cpu_baseline(ds, B, C, pm, params, frames: int):
+    """The oracle (reference CPU path restated over torch-CPU ops) on the host cores."""
+    from mvdet_amd import synthetic
+    from oracle import cpu_path
+    threads = len(os.sched_getaffinity(0))
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    torch.set_num_threads(threads)
+    up = ds.upsample_shape
+    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * 2 + v)
+             for v in range(ds.num_cam)]
+    tp = {k: torch.from_numpy(v) for k, v in params.items()}
+    mats = [M.numpy() for M in pm]
+    with torch.no_grad():
+        cpu_path.project_fuse(feats, mats, tuple(ds.reducedgrid_shape), tp)  # warm-up
+        t0 = time.perf_counter()
+        stages = {}
+        for _ in range(frames):
+            cpu_path.project_fuse(feats, mats, tuple(ds.reducedgrid_shape), tp, timings=stages)
+        dt = time.perf_counter() - t0
+    return dict(value=round(B * frames / dt, 4), unit="frames/s", cores=threads, kind="port",
+                sample=f"{frames} frame(s) (B={B}) of the bench workload after 1 warm-up; oracle/cpu_path.py "
+                       f"(kornia-0.6.11 restatement over torch-CPU grid_sample + torch.cat + 3x F.conv2d) "
+                       f"on identical synthetic inputs; last frame stages (s): "
+                       + ", ".join(f"{k}={v:.3f}" for k, v in stages.items()))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=2, help="BASELINE.json config index (1-based)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=0, help="frames for the CPU baseline (0 = auto)")
+    args = ap.parse_args()
+
+    from mvdet_amd import ProjectFuse, synthetic
+    from mvdet_amd.geometry import projection_matrices, touched_footprint
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        from mvdet_amd import parallel
+        return parallel.bench_main(args)
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    spec = synthetic.CONFIGS[args.config]
+    ds = spec["make"]()
+    B, C = spec["B"], spec["C"]
+    N = ds.num_cam
+    up = tuple(ds.upsample_shape)
+    ho, wo = ds.reducedgrid_shape
+    pm = projection_matrices(ds)
+    params = head_params(N, seed=args.config, C=C)
+    mc = build_mc(C, N, params, dev)
+    eng = ProjectFuse(pm, up, (ho, wo), C)
+    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * args.config + v,
+                                          device=dev) for v in range(N)]
+    ws = eng.workspace(B, dev)
+
+    K, W = args.steps, args.warmup
+    ev = {k: [torch.cuda.Event(enable_timing=True) for _ in range(K)] for k in ("warp", "conv1", "conv2", "conv3")}
+
+    from mvdet_amd import ops
+
+    def step(i=None):
+        if i is not None:
+            ev["warp"][i].record()
+        for v in range(N):
+            eng.warp_view(ws, v, feats[v])
+        c1, c2, c3 = mc[0], mc[2], mc[4]
+        p1, p2 = eng.pack1.get(c1.weight), eng.pack2.get(c2.weight)
+        if i is not None:
+            ev["conv1"][i].record()
+        ops.conv3x3(ws.fused, p1, eng.cin, 512, c1.bias, 1, True, out=ws.y1)
+        if i is not None:
+            ev["conv2"][i].record()
+        ops.conv3x3(ws.y1, p2, 512, 512, c2.bias, 2, True, out=ws.y2)
+        if i is not None:
+            ev["conv3"][i].record()
+        return ops.conv3x3_cout1(ws.y2, c3.weight, 4)
+
+    end_ev = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+    with torch.no_grad():
+        for _ in range(W):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(K):
+            step(i)
+            end_ev[i].record()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+
+    def avg(a, b):
+        return float(np.mean([a[i].elapsed_time(b[i]) for i in range(K)]))
+
+    t_warp = avg(ev["warp"], ev["conv1"])
+    t_c1 = avg(ev["conv1"], ev["conv2"])
+    t_c2 = avg(ev["conv2"], ev["conv3"])
+    t_c3 = avg(ev["conv3"], end_ev)
+
+    frames = B * K
+    value = frames / dt
+    # algorithmic work
+    cin = N * C + 2
+    conv1_flop = 2.0 * B * ho * wo * 9 * cin * 512
+    conv2_flop = 2.0 * B * ho * wo * 9 * 512 * 512
+    tv = [touched_footprint(M.numpy(), up, (ho, wo)) for M in pm]
+    warp_bytes = sum(4.0 * B * C * (t + ho * wo) for t in tv)
+    conv3_bytes = 4.0 * B * ho * wo * (512 + 1)
+    conv1_tfs = conv1_flop / (t_c1 * 1e-3) / 1e12
+    traffic = None
+    tfile = ROOT / "profiles" / f"traffic_cfg{args.config}.json"
+    if tfile.exists():
+        traffic = json.loads(tfile.read_text()).get("conv1_hbm_bytes_per_launch")
+
+    result = {
+        "metric": "multi-view frames/sec (project+fuse)",
+        "value": round(value, 3),
+        "unit": "frames/s",
+        "n_gpus": 1,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": round(dt * 1e3 / K, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (ReLU N(0,1) features upsampled 3x, synthetic pinhole rig through the reference matrix chain, random-init fusion weights)",
+        "config": {"workload": f"cfg{args.config}: {spec['name']}", "views": N, "channels": C, "batch": B,
+                   "src_hw": list(up), "grid_hw": [ho, wo], "parallelism": "single GPU"},
+        "roofline": {"kernel": "conv3x3_mfma_f32 (conv1, Cin=%d)" % cin, "bound": "mfma",
+                     "achieved": round(conv1_tfs, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": round(conv1_tfs / FP32_MFMA_PEAK_TFS, 4), "traffic": traffic},
+        "stages_ms": {"warp_all_views": round(t_warp, 4), "conv1": round(t_c1, 4), "conv2": round(t_c2, 4),
+                      "conv3": round(t_c3, 4)},
+        "stage_roofline": {
+            "warp": {"bound": "hbm", "algorithmic_bytes": warp_bytes,
+                     "achieved_GBs": round(warp_bytes / (t_warp * 1e-3) / 1e9, 1), "peak_GBs": HBM_PEAK_GBS},
+            "conv2": {"bound": "mfma", "achieved_TFs": round(conv2_flop / (t_c2 * 1e-3) / 1e12, 2),
+                      "peak_TFs": FP32_MFMA_PEAK_TFS},
+            "conv3": {"bound": "hbm", "achieved_GBs": round(conv3_bytes / (t_c3 * 1e-3) / 1e9, 1),
+                      "peak_GBs": HBM_PEAK_GBS},
+            "whole_step_frac": round(((warp_bytes + conv3_bytes) / (HBM_PEAK_GBS * 1e9)
+                                      + (conv1_flop + conv2_flop) / (FP32_MFMA_PEAK_TFS * 1e12))
+                                     / (dt / K), 4),
+        },
+    }
+    if not args.no_cpu_baseline and rank == 0:
+        frames_cpu = args.cpu_frames or (3 if args.config == 2 else 5)
+        result["cpu_baseline"] = cpu_baseline(ds, B, C, pm, params, frames_cpu)
+        result["speedup_vs_cpu"] = round(value / result["cpu_baseline"]["value"], 1)
+    print(json.dumps(result))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,115 @@
+/*
+ * mvbev.h — C ABI of the MI355X-native MVDet project+fuse hot path.
+ *
+ * libmvbev.so (built from the HIP sources in mvdet_amd/csrc for gfx950) exports exactly the
+ * functions below.  Plain pointers and sizes only: every tensor argument is a
+ * caller-owned DEVICE pointer (PyTorch caching allocator, hipMalloc, ...), every
+ * call is enqueued on the caller's HIP stream (passed as `void*`, NULL = the
+ * null stream), no call allocates, copies to the host or synchronises, and all
+ * calls are reentrant (no global mutable state).
+ *
+ * Return value: 0 (MVBEV_OK) on success, a negative MVBEV_ERR_* code for a bad
+ * argument (nothing is launched), or MVBEV_ERR_HIP when the launch itself
+ * failed.  mvbev_status_string() turns a code into text.
+ *
+ * Reference interfaces replaced (ErikBrorsson/MVDet @ 2024-08-07):
+ *   mvbev_warp_perspective_f32 / _f16
+ *       kornia.geometry.transform.warp_perspective(img_feature, proj_mat,
+ *       reducedgrid_shape)   multiview_detector/models/persp_trans_detector.py:69
+ *       (kornia 0.6.11: normalize -> inverse -> meshgrid -> transform_points ->
+ *       F.grid_sample(bilinear, zeros, align_corners=True)).  The caller passes
+ *       the kornia src_norm<-dst_norm 3x3 (host-computed, same recipe) so the
+ *       device does transform + divide + bilinear gather.  dst strides let every
+ *       view write straight into its channel slice of the fused ground-plane
+ *       tensor: the torch.cat at persp_trans_detector.py:77 becomes zero-copy.
+ *   mvbev_fill_coord_map_f32
+ *       self.coord_map.repeat([B,1,1,1]) concatenated as the last two channels
+ *       (persp_trans_detector.py:21,77,103-112).
+ *   mvbev_pack_conv3x3_weight_f32, mvbev_conv3x3_f32
+ *       nn.Conv2d(Cin->Cout, 3, padding=d, dilation=d) (+ nn.ReLU) of
+ *       map_classifier[0:4]   persp_trans_detector.py:51-53, :81
+ *   mvbev_conv3x3_cout1_f32
+ *       nn.Conv2d(512->1, 3, padding=4, dilation=4, bias=False) of
+ *       map_classifier[4]      persp_trans_detector.py:54, :81
+ *   (the same-size F.interpolate at persp_trans_detector.py:82 is an exact
+ *    identity and has no entry point.)
+ */
+#ifndef MVBEV_H_
+#define MVBEV_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MVBEV_OK 0
+#define MVBEV_ERR_RANK (-1)      /* a size is <= 0 / a rank assumption is violated */
+#define MVBEV_ERR_SHAPE (-2)     /* inconsistent sizes (e.g. Cout not a multiple of 128) */
+#define MVBEV_ERR_STRIDE (-3)    /* unsupported stride (innermost stride must be 1 where stated) */
+#define MVBEV_ERR_ALIGN (-4)     /* pointer misaligned for the vector width used */
+#define MVBEV_ERR_NULL (-5)      /* a required pointer is NULL */
+#define MVBEV_ERR_DILATION (-6)  /* dilation not supported by this entry point */
+#define MVBEV_ERR_HIP (-100)     /* the HIP launch failed (hipGetLastError) */
+
+/* Input-channel granule of the conv kernels: the fused tensor's channel count
+ * must be padded to a multiple of this (padding channels hold zeros). */
+#define MVBEV_CONV_KC 8
+/* Output-channel granule of mvbev_conv3x3_f32. */
+#define MVBEV_CONV_BN 128
+
+const char* mvbev_status_string(int status);
+/* Library / ABI version, e.g. 10000 for 1.0.0. */
+int mvbev_version(void);
+
+/* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
+ *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
+ *   m      : device fp32 [B][3][3] row-major src_norm <- dst_norm (kornia's
+ *            _torch_inverse_cast(normalize_homography(M, (H,W), (Ho,Wo))))
+ *   dst    : [B][C][Ho][Wo] fp32 at element strides dst_strides[4]
+ *            (dst_strides[3] must be 1); may point into a larger tensor. */
+int mvbev_warp_perspective_f32(const float* src, int64_t B, int64_t C, int64_t H, int64_t W,
+                               const int64_t src_strides[4], const float* m,
+                               float* dst, int64_t Ho, int64_t Wo, const int64_t dst_strides[4],
+                               void* stream);
+
+/* Same with fp16 storage for src and dst (fp32 coordinate and blend math). */
+int mvbev_warp_perspective_f16(const void* src, int64_t B, int64_t C, int64_t H, int64_t W,
+                               const int64_t src_strides[4], const float* m,
+                               void* dst, int64_t Ho, int64_t Wo, const int64_t dst_strides[4],
+                               void* stream);
+
+/* Coord-map channels: dst[b][0][v][u] = u/(Wo-1)*2-1, dst[b][1][v][u] = v/(Ho-1)*2-1
+ * (computed in float64, rounded to fp32 as numpy->torch does at :106-107). */
+int mvbev_fill_coord_map_f32(float* dst, int64_t B, int64_t Ho, int64_t Wo,
+                             const int64_t dst_strides[4], void* stream);
+
+/* Number of floats of the packed weight buffer for a Cout x Cin x 3 x 3 conv. */
+size_t mvbev_conv3x3_packed_floats(int64_t Cout, int64_t Cin);
+
+/* Re-lay an nn.Conv2d weight [Cout][Cin][3][3] (contiguous fp32, device) into
+ * the MFMA staging layout (Cin zero-padded to MVBEV_CONV_KC). */
+int mvbev_pack_conv3x3_weight_f32(const float* w, int64_t Cout, int64_t Cin, float* w_packed,
+                                  void* stream);
+
+/* y = act(conv3x3(x, w, dilation=d, padding=d) + bias), fp32 MFMA, fp32 accumulate.
+ *   x      : [B][Cin_pad][H][W] contiguous fp32, Cin_pad = roundup(Cin, KC);
+ *            channels >= Cin must be finite (zero weights multiply them)
+ *   w_packed : from mvbev_pack_conv3x3_weight_f32 (same Cout, Cin)
+ *   bias   : [Cout] or NULL;   relu: 0/1;   dilation: 1 or 2
+ *   y      : [B][Cout][H][W] contiguous fp32, Cout % MVBEV_CONV_BN == 0 */
+int mvbev_conv3x3_f32(const float* x, int64_t B, int64_t Cin, int64_t H, int64_t W,
+                      const float* w_packed, const float* bias, int64_t Cout,
+                      int dilation, int relu, float* y, void* stream);
+
+/* y[b][0] = conv3x3(x[b], w, dilation=d, padding=d), one output channel, no bias.
+ *   x : [B][C][H][W] contiguous fp32;  w : [C][3][3] contiguous fp32;  y : [B][1][H][W] */
+int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int64_t W,
+                            const float* w, int dilation, float* y, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MVBEV_H_ */

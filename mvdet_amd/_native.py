@@ -1,0 +1,96 @@
+"""ctypes binding of libmvbev.so (the C ABI declared in ``include/mvbev.h``).
+
+The product path has no CPU fallback: if the library is missing or a call
+returns an error, this module raises.  Tensors cross the boundary as raw device
+pointers, sizes and element strides; the stream is torch's current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libmvbev.so"
+
+# Every symbol include/mvbev.h declares (tests check the library exports them all).
+EXPORTS = (
+    "mvbev_status_string",
+    "mvbev_version",
+    "mvbev_warp_perspective_f32",
+    "mvbev_warp_perspective_f16",
+    "mvbev_fill_coord_map_f32",
+    "mvbev_conv3x3_packed_floats",
+    "mvbev_pack_conv3x3_weight_f32",
+    "mvbev_conv3x3_f32",
+    "mvbev_conv3x3_cout1_f32",
+)
+
+KC = 8    # MVBEV_CONV_KC
+BN = 128  # MVBEV_CONV_BN
+
+_i64 = ctypes.c_int64
+_p = ctypes.c_void_p
+_i64x4 = ctypes.c_int64 * 4
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def _declare(lib):
+    lib.mvbev_status_string.restype = ctypes.c_char_p
+    lib.mvbev_status_string.argtypes = [ctypes.c_int]
+    lib.mvbev_version.restype = ctypes.c_int
+    lib.mvbev_version.argtypes = []
+    for name in ("mvbev_warp_perspective_f32", "mvbev_warp_perspective_f16"):
+        fn = getattr(lib, name)
+        fn.restype = ctypes.c_int
+        fn.argtypes = [_p, _i64, _i64, _i64, _i64, _i64x4, _p, _p, _i64, _i64, _i64x4, _p]
+    lib.mvbev_fill_coord_map_f32.restype = ctypes.c_int
+    lib.mvbev_fill_coord_map_f32.argtypes = [_p, _i64, _i64, _i64, _i64x4, _p]
+    lib.mvbev_conv3x3_packed_floats.restype = ctypes.c_size_t
+    lib.mvbev_conv3x3_packed_floats.argtypes = [_i64, _i64]
+    lib.mvbev_pack_conv3x3_weight_f32.restype = ctypes.c_int
+    lib.mvbev_pack_conv3x3_weight_f32.argtypes = [_p, _i64, _i64, _p, _p]
+    lib.mvbev_conv3x3_f32.restype = ctypes.c_int
+    lib.mvbev_conv3x3_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _p, _p, _i64, ctypes.c_int,
+                                      ctypes.c_int, _p, _p]
+    lib.mvbev_conv3x3_cout1_f32.restype = ctypes.c_int
+    lib.mvbev_conv3x3_cout1_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _p, ctypes.c_int, _p, _p]
+
+
+def load(path: os.PathLike | str | None = None):
+    """Load (once) and return the library handle; raises if it is absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise NativeError(
+            f"libmvbev.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C mvdet_amd/csrc` (there is no CPU fallback)")
+    lib = ctypes.CDLL(str(p))
+    _declare(lib)
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        msg = load().mvbev_status_string(status).decode()
+        raise NativeError(f"{what} failed: {msg} (status {status})")
+
+
+def strides4(t) -> "ctypes.Array":
+    s = t.stride()
+    if len(s) != 4:
+        raise ValueError(f"expected a 4-D tensor, got {len(s)}-D")
+    return _i64x4(*s)
+
+
+def stream_ptr(device) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

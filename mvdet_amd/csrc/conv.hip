@@ -1,0 +1,288 @@
+// Dilated 3x3 convolutions of the BEV fusion head (map_classifier) for gfx950.
+//
+// Replaces nn.Conv2d(Cin->512, 3, p1)+ReLU, nn.Conv2d(512->512, 3, d2, p2)+ReLU and
+// nn.Conv2d(512->1, 3, d4, p4, no bias) at multiview_detector/models/persp_trans_detector.py:51-54
+// (applied at :81).
+//
+// mvbev_conv3x3_f32 — implicit GEMM on the fp32-input MFMA (v_mfma_f32_32x32x2_f32: exact
+// f32 products, f32 accumulation, 64 FLOP/clk/SIMD = the chip's fp32 peak):
+//   D[co][pixel] += sum_{tap, ci} W[co][ci][tap] * X[ci][pixel + d*tap]
+//   A operand = weights (M = output channels), B operand = input pixels (N = 32 consecutive
+//   columns of one output row), K = (input channel, tap).  With the output channel on the
+//   accumulator rows and the pixel on the lane, the epilogue stores 2 x 128 B per register:
+//   NCHW output, fully coalesced.
+//   Workgroup tile: TH=4 rows x TW=32 cols of pixels x BN=128 output channels, 4 waves
+//   (wave = 2 pixel rows x 64 channels = 2x2 MFMA tiles of 32x32).  K is walked in chunks of
+//   KC=8 input channels; per chunk the (TH+2d) x (TW+2d) input halo of all 8 channels and the
+//   9 x 8 x 128 weight slab are staged in LDS and every staged input element feeds all 9 taps.
+//   The next chunk's global loads are issued into registers before the MFMAs of the current
+//   chunk (async-STAGE split) and written to LDS after the next barrier.
+//
+// mvbev_conv3x3_cout1_f32 — Cout = 1 is a 4608-long dot product per pixel: HBM/L2-bound, no
+//   MFMA.  Block = 64 pixels of a row x 4 waves; each wave sums a quarter of the channels with
+//   wave-uniform (scalar) weight loads, partial sums reduced through LDS.
+#include "common.h"
+
+namespace mvbev {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int KC = MVBEV_CONV_KC;  // input channels per staged chunk
+constexpr int BN = MVBEV_CONV_BN;  // output channels per workgroup
+constexpr int TH = 4;              // output rows per workgroup
+constexpr int TW = 32;             // output cols per workgroup (= MFMA N)
+
+// packed[chunk][cotile][tap][kk][col] = w[cotile*BN+col][chunk*KC+kk][tap] (0 for padded ci)
+__global__ void pack_conv3x3_kernel(const float* __restrict__ w, float* __restrict__ wp, int Cout,
+                                    int Cin, int Cin_pad) {
+  const int64_t total = (int64_t)Cin_pad * 9 * Cout;
+  const int n_cot = Cout / BN;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i;
+    const int col = r % BN; r /= BN;
+    const int kk = r % KC; r /= KC;
+    const int tap = r % 9; r /= 9;
+    const int cot = r % n_cot;
+    const int chunk = (int)(r / n_cot);
+    const int ci = chunk * KC + kk;
+    const int co = cot * BN + col;
+    wp[i] = ci < Cin ? w[((int64_t)co * Cin + ci) * 9 + tap] : 0.f;
+  }
+}
+
+template <int DIL, bool RELU>
+__global__ __launch_bounds__(256, 2) void conv3x3_mfma_f32_kernel(
+    const float* __restrict__ x, const float* __restrict__ wp, const float* __restrict__ bias,
+    float* __restrict__ y, int Cin_pad, int Cout, int H, int W, int tiles_x, int tiles_y, int n_cot,
+    int nwg) {
+  constexpr int XH = TH + 2 * DIL, XW = TW + 2 * DIL;
+  constexpr int XS = KC * XH * XW;  // input halo floats per chunk
+  constexpr int WS = 9 * KC * BN;   // weight floats per chunk
+  constexpr int WLD = WS / 4 / 256; // float4 weight loads per thread
+  constexpr int XLD = (XS + 255) / 256;
+  static_assert(WS % 1024 == 0, "weight slab must split evenly over 256 threads");
+  __shared__ __attribute__((aligned(16))) float lds[WS + XS];
+  float* Ws = lds;
+  float* Xs = lds + WS;
+
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int cot = wg % n_cot;
+  int rest = wg / n_cot;
+  const int tx = rest % tiles_x;
+  rest /= tiles_x;
+  const int ty = rest % tiles_y;
+  const int b = rest / tiles_y;
+  const int x0 = tx * TW, y0 = ty * TH;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, kh = lane >> 5;
+
+  const int64_t plane = (int64_t)H * W;
+  const float* xb = x + (int64_t)b * Cin_pad * plane;
+  const float4* wsrc = reinterpret_cast<const float4*>(wp) + (int64_t)cot * (WS / 4);
+  const int64_t wchunk = (int64_t)n_cot * (WS / 4);
+  const int nchunks = Cin_pad / KC;
+
+  // Per-thread halo element coordinates are chunk-invariant: precompute offsets/validity.
+  int xoff[XLD];
+  bool xok[XLD];
+#pragma unroll
+  for (int i = 0; i < XLD; ++i) {
+    const int e = tid + 256 * i;
+    const int kk = e / (XH * XW);
+    const int r = (e / XW) % XH;
+    const int c = e % XW;
+    const int gy = y0 - DIL + r, gx = x0 - DIL + c;
+    xok[i] = e < XS && gy >= 0 && gy < H && gx >= 0 && gx < W;
+    xoff[i] = xok[i] ? (int)(kk * plane + gy * W + gx) : 0;
+  }
+
+  float4 wreg[WLD];
+  float xreg[XLD];
+  auto load_chunk = [&](int ch) {
+    const float4* ws = wsrc + ch * wchunk;
+#pragma unroll
+    for (int i = 0; i < WLD; ++i) wreg[i] = ws[tid + 256 * i];
+    const float* xc = xb + (int64_t)ch * KC * plane;
+#pragma unroll
+    for (int i = 0; i < XLD; ++i) xreg[i] = xok[i] ? xc[xoff[i]] : 0.f;
+  };
+  auto store_chunk = [&]() {
+#pragma unroll
+    for (int i = 0; i < WLD; ++i) reinterpret_cast<float4*>(Ws)[tid + 256 * i] = wreg[i];
+#pragma unroll
+    for (int i = 0; i < XLD; ++i) {
+      const int e = tid + 256 * i;
+      if (XS % 256 == 0 || e < XS) Xs[e] = xreg[i];
+    }
+  };
+
+  floatx16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
+  const int prow = 2 * (wave & 1);  // this wave's two output rows within the tile
+  const int cw = 64 * (wave >> 1);  // this wave's 64 output channels within BN
+
+  load_chunk(0);
+  for (int ch = 0; ch < nchunks; ++ch) {
+    __syncthreads();
+    store_chunk();
+    __syncthreads();
+    if (ch + 1 < nchunks) load_chunk(ch + 1);
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int tap = ky * 3 + kx;
+#pragma unroll
+        for (int kp = 0; kp < KC / 2; ++kp) {
+          const int k = 2 * kp + kh;
+          const float* wrow = Ws + (tap * KC + k) * BN + cw + l32;
+          const float a0 = wrow[0];
+          const float a1 = wrow[32];
+          const float* xrow = Xs + (k * XH + prow + ky * DIL) * XW + l32 + kx * DIL;
+          const float b0 = xrow[0];
+          const float b1 = xrow[XW];
+          acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc00, 0, 0, 0);
+          acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc01, 0, 0, 0);
+          acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc10, 0, 0, 0);
+          acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc11, 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // Epilogue: D[i = co][j = pixel]; lane holds j = l32 and rows i = (r&3) + 8(r>>2) + 4 kh.
+  const int col = x0 + l32;
+  auto emit = [&](const floatx16& acc, int ci_tile, int rj) {
+    const int row = y0 + prow + rj;
+    if (row >= H || col >= W) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = cot * BN + cw + 32 * ci_tile + (r & 3) + 8 * (r >> 2) + 4 * kh;
+      float v = acc[r] + (bias ? bias[co] : 0.f);
+      if (RELU) v = v < 0.f ? 0.f : v;  // torch.relu keeps NaN
+      y[((int64_t)b * Cout + co) * plane + (int64_t)row * W + col] = v;
+    }
+  };
+  emit(acc00, 0, 0);
+  emit(acc01, 0, 1);
+  emit(acc10, 1, 0);
+  emit(acc11, 1, 1);
+}
+
+template <int DIL>
+__global__ __launch_bounds__(256) void conv3x3_cout1_kernel(const float* __restrict__ x,
+                                                            const float* __restrict__ w,
+                                                            float* __restrict__ y, int C, int H,
+                                                            int W) {
+  __shared__ float part[4][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int col = blockIdx.x * 64 + lane;
+  const int row = blockIdx.y;
+  const int b = blockIdx.z;
+  const int64_t plane = (int64_t)H * W;
+  const float* xb = x + (int64_t)b * C * plane;
+  bool okx[3];
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) {
+    const int xx = col + (kx - 1) * DIL;
+    okx[kx] = xx >= 0 && xx < W;
+  }
+  float acc = 0.f;
+  for (int c = wave; c < C; c += 4) {
+    const float* xc = xb + (int64_t)c * plane;
+    const float* wc = w + c * 9;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int yy = row + (ky - 1) * DIL;
+      if (yy < 0 || yy >= H) continue;
+      const float* xr = xc + (int64_t)yy * W;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int xx = col + (kx - 1) * DIL;
+        const float v = okx[kx] ? xr[xx] : 0.f;
+        acc += wc[ky * 3 + kx] * v;
+      }
+    }
+  }
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && col < W) {
+    y[(int64_t)b * plane + (int64_t)row * W + col] =
+        (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+  }
+}
+
+}  // namespace mvbev
+
+extern "C" {
+
+size_t mvbev_conv3x3_packed_floats(int64_t Cout, int64_t Cin) {
+  if (Cout <= 0 || Cin <= 0) return 0;
+  return (size_t)mvbev::round_up(Cin, mvbev::KC) * 9 * (size_t)Cout;
+}
+
+int mvbev_pack_conv3x3_weight_f32(const float* w, int64_t Cout, int64_t Cin, float* w_packed,
+                                  void* stream) {
+  if (!w || !w_packed) return MVBEV_ERR_NULL;
+  if (Cout <= 0 || Cin <= 0) return MVBEV_ERR_RANK;
+  if (Cout % mvbev::BN != 0) return MVBEV_ERR_SHAPE;
+  const int64_t cin_pad = mvbev::round_up(Cin, mvbev::KC);
+  const int64_t total = cin_pad * 9 * Cout;
+  const int blocks = (int)std::min<int64_t>(mvbev::ceil_div(total, 256), 8192);
+  hipLaunchKernelGGL(mvbev::pack_conv3x3_kernel, dim3(blocks), dim3(256), 0,
+                     mvbev::as_stream(stream), w, w_packed, (int)Cout, (int)Cin, (int)cin_pad);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+int mvbev_conv3x3_f32(const float* x, int64_t B, int64_t Cin, int64_t H, int64_t W,
+                      const float* w_packed, const float* bias, int64_t Cout, int dilation,
+                      int relu, float* y, void* stream) {
+  using namespace mvbev;
+  if (!x || !w_packed || !y) return MVBEV_ERR_NULL;
+  if (B <= 0 || Cin <= 0 || H <= 0 || W <= 0 || Cout <= 0) return MVBEV_ERR_RANK;
+  if (Cout % BN != 0) return MVBEV_ERR_SHAPE;
+  if ((reinterpret_cast<uintptr_t>(w_packed) & 15) != 0) return MVBEV_ERR_ALIGN;
+  const int64_t cin_pad = round_up(Cin, KC);
+  if (cin_pad * H * W > (int64_t)INT32_MAX) return MVBEV_ERR_SHAPE;  // per-image int offsets
+  const int tiles_x = (int)ceil_div(W, TW), tiles_y = (int)ceil_div(H, TH);
+  const int n_cot = (int)(Cout / BN);
+  const int64_t nwg = (int64_t)tiles_x * tiles_y * n_cot * B;
+  if (nwg > (int64_t)INT32_MAX) return MVBEV_ERR_SHAPE;
+  hipStream_t s = as_stream(stream);
+#define MVBEV_CONV_LAUNCH(D, R)                                                                \
+  hipLaunchKernelGGL((conv3x3_mfma_f32_kernel<D, R>), dim3((unsigned)nwg), dim3(256), 0, s, x,   \
+                     w_packed, bias, y, (int)cin_pad, (int)Cout, (int)H, (int)W, tiles_x, tiles_y, \
+                     n_cot, (int)nwg)
+  if (dilation == 1) {
+    if (relu) MVBEV_CONV_LAUNCH(1, true); else MVBEV_CONV_LAUNCH(1, false);
+  } else if (dilation == 2) {
+    if (relu) MVBEV_CONV_LAUNCH(2, true); else MVBEV_CONV_LAUNCH(2, false);
+  } else {
+    return MVBEV_ERR_DILATION;
+  }
+#undef MVBEV_CONV_LAUNCH
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int64_t W,
+                            const float* w, int dilation, float* y, void* stream) {
+  using namespace mvbev;
+  if (!x || !w || !y) return MVBEV_ERR_NULL;
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return MVBEV_ERR_RANK;
+  if (H > 65535 || B > 65535) return MVBEV_ERR_SHAPE;
+  dim3 grid((unsigned)ceil_div(W, 64), (unsigned)H, (unsigned)B);
+  hipStream_t s = as_stream(stream);
+  switch (dilation) {
+    case 1: hipLaunchKernelGGL(conv3x3_cout1_kernel<1>, grid, dim3(256), 0, s, x, w, y, (int)C, (int)H, (int)W); break;
+    case 2: hipLaunchKernelGGL(conv3x3_cout1_kernel<2>, grid, dim3(256), 0, s, x, w, y, (int)C, (int)H, (int)W); break;
+    case 4: hipLaunchKernelGGL(conv3x3_cout1_kernel<4>, grid, dim3(256), 0, s, x, w, y, (int)C, (int)H, (int)W); break;
+    default: return MVBEV_ERR_DILATION;
+  }
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,125 @@
+"""Drop-in ``PerspTransDetector`` (``multiview_detector/models/persp_trans_detector.py:13-112``).
+
+Same constructor (``dataset`` duck-type, ``arch``), same attributes
+(``num_cam``, ``img_shape``, ``reducedgrid_shape``, ``coord_map``,
+``upsample_shape``, ``proj_mats``), same sub-modules and therefore the same
+``state_dict`` keys (``base_pt1.*``, ``base_pt2.*``, ``img_classifier.*``,
+``map_classifier.*``), same ``forward(imgs, visualize=False) ->
+(map_result [B,1,Ho,Wo], imgs_result: list[N] of [B,2,h,w])``.
+
+What changes is the hot path (warp + concat + fusion), which runs on the HIP
+kernels of ``libmvbev.so`` through ``ProjectFuse``:
+* the per-view warp writes straight into the fused ground-plane tensor;
+* the coord channels are written once, not copied every forward;
+* conv1/conv2 are fp32-MFMA implicit GEMMs, conv3 a dot-product kernel;
+* the same-size final interpolate (an exact identity) is elided.
+
+Training (autograd through the hot path, ``trainer.py:38-49``) is not yet native
+(SURVEY §8(f) row 2): when grad is required the hot path runs as stock torch
+GPU ops (``grid_sample`` + ``conv2d``) so training semantics are unchanged.
+The library is loaded at construction on a GPU, so a missing build fails there.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _native
+from .backbone import build_backbone
+from .geometry import coord_map as make_coord_map
+from .geometry import projection_matrices, upsample_shape
+from .pipeline import ProjectFuse
+
+
+class PerspTransDetector(nn.Module):
+    def __init__(self, dataset, arch: str = "resnet18", device=None):
+        super().__init__()
+        self.num_cam = dataset.num_cam
+        self.img_shape, self.reducedgrid_shape = list(dataset.img_shape), list(dataset.reducedgrid_shape)
+        self.coord_map = make_coord_map(*self.reducedgrid_shape)          # :21 (not a buffer)
+        self.upsample_shape = upsample_shape(self.img_shape, dataset.img_reduce)  # :23
+        self.proj_mats = projection_matrices(dataset)                       # :18-30 (fp64 list)
+        if device is None:
+            device = "cuda:0" if torch.cuda.is_available() else "cpu"
+        self._device = torch.device(device)
+        if self._device.type == "cuda":
+            _native.load()  # no fallback: fail at construction if the HIP library is missing
+        self.base_pt1, self.base_pt2, out_channel = build_backbone(arch)
+        self.img_classifier = nn.Sequential(nn.Conv2d(out_channel, 64, 1), nn.ReLU(),
+                                            nn.Conv2d(64, 2, 1, bias=False))
+        self.map_classifier = nn.Sequential(nn.Conv2d(out_channel * self.num_cam + 2, 512, 3, padding=1), nn.ReLU(),
+                                            nn.Conv2d(512, 512, 3, padding=2, dilation=2), nn.ReLU(),
+                                            nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False))
+        self.to(self._device)
+        self.engine = ProjectFuse(self.proj_mats, tuple(self.upsample_shape), tuple(self.reducedgrid_shape),
+                                  out_channel)
+
+    # -- hot path --------------------------------------------------------------------------
+    def _needs_autograd(self) -> bool:
+        return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+
+    def forward(self, imgs: torch.Tensor, visualize: bool = False):
+        B, N, C, H, W = imgs.shape
+        assert N == self.num_cam
+        dev = self._device
+        if dev.type != "cuda":
+            raise RuntimeError("PerspTransDetector.forward needs a ROCm GPU (the hot path has no CPU fallback)")
+        training = self._needs_autograd()
+        ws = None if training else self.engine.workspace(B, dev)
+        world_features, imgs_result = [], []
+        for cam in range(self.num_cam):
+            feat = self.base_pt1(imgs[:, cam].to(dev))
+            feat = self.base_pt2(feat)
+            feat = F.interpolate(feat, self.upsample_shape, mode="bilinear")
+            imgs_result.append(self.img_classifier(feat))
+            if training:
+                world_features.append(self._torch_warp(cam, feat))
+            else:
+                self.engine.warp_view(ws, cam, feat.contiguous())
+            if visualize:
+                self._show(torch.norm(feat[0].detach(), dim=0))
+        if training:
+            cmap = self.coord_map.to(dev).repeat([B, 1, 1, 1])
+            map_result = self.map_classifier(torch.cat(world_features + [cmap], dim=1))
+        else:
+            map_result = self.engine.fuse(ws, self.map_classifier)
+        if visualize:
+            self._show(torch.norm(map_result[0].detach(), dim=0))
+        return map_result, imgs_result
+
+    def _torch_warp(self, cam: int, feat: torch.Tensor) -> torch.Tensor:
+        """Autograd-capable warp (kornia steps 3-6 in stock torch GPU ops)."""
+        B = feat.shape[0]
+        ho, wo = self.reducedgrid_shape
+        m = self.engine.m_norm_cpu[cam].to(feat.device)
+        xs = (torch.linspace(0, wo - 1, wo, device=feat.device) / (wo - 1) - 0.5) * 2
+        ys = (torch.linspace(0, ho - 1, ho, device=feat.device) / (ho - 1) - 0.5) * 2
+        gy, gx = torch.meshgrid(ys, xs, indexing="ij")
+        pts = torch.stack([gx, gy, torch.ones_like(gx)], -1) @ m.T
+        z = pts[..., 2:]
+        scale = torch.where(z.abs() > 1e-8, 1.0 / (z + 1e-8), torch.ones_like(z))
+        grid = (scale * pts[..., :2]).unsqueeze(0).expand(B, ho, wo, 2)
+        return F.grid_sample(feat, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
+
+    @staticmethod
+    def _show(img):
+        import matplotlib.pyplot as plt
+        plt.imshow(img.cpu().numpy())
+        plt.show()
+
+    # -- reference helpers (same names) ----------------------------------------------------
+    def get_imgcoord2worldgrid_matrices(self, intrinsic_matrices, extrinsic_matrices, worldgrid2worldcoord_mat):
+        from .geometry import imgcoord2worldgrid_matrices
+        mats = imgcoord2worldgrid_matrices(intrinsic_matrices, extrinsic_matrices, worldgrid2worldcoord_mat,
+                                           self.num_cam)
+        return {cam: m for cam, m in enumerate(mats)}
+
+    def create_coord_map(self, img_size, with_r=False):
+        H, W, _ = img_size
+        ret = make_coord_map(H, W)
+        if with_r:
+            rr = torch.sqrt(ret[:, 0] ** 2 + ret[:, 1] ** 2).view([1, 1, H, W])
+            ret = torch.cat([ret, rr], dim=1)
+        return ret

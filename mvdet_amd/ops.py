@@ -1,0 +1,188 @@
+"""Tensor-level wrappers over the C ABI (``include/mvbev.h``).
+
+Every function here launches HIP kernels from ``libmvbev.so`` on torch's
+current stream; none has a CPU or stock-torch fallback — a CPU tensor, a
+missing library or a bad argument raises.
+
+* ``warp_perspective`` — kornia-0.6.11-compatible signature/errors
+  (``kornia.geometry.transform.warp_perspective``, the op called at
+  ``persp_trans_detector.py:69``).
+* ``warp_into`` — the zero-copy form used by the detector: writes one view
+  straight into its channel slice of the fused ground-plane tensor (``:77``).
+* ``fill_coord_map`` — the two coord channels (``:21,77``).
+* ``PackedConv3x3`` / ``conv3x3`` / ``conv3x3_cout1`` — the fusion head convs
+  (``:51-54,81``).
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence, Tuple
+
+import torch
+
+from . import _native
+from .geometry import kornia_src_norm_from_dst_norm
+
+KC = _native.KC
+BN = _native.BN
+
+
+def _require_cuda(*tensors):
+    for t in tensors:
+        if not (isinstance(t, torch.Tensor) and t.is_cuda):
+            raise RuntimeError("mvdet_amd ops run only on a ROCm GPU tensor (no CPU fallback)")
+
+
+def _stream(t: torch.Tensor) -> int:
+    return _native.stream_ptr(t.device)
+
+
+# ----------------------------------------------------------------------------------------------
+# warp
+
+def warp_into(src: torch.Tensor, m_norm: torch.Tensor, dst: torch.Tensor) -> torch.Tensor:
+    """Warp ``src`` [B,C,H,W] into ``dst`` [B,C,Ho,Wo] (a view, innermost stride 1).
+
+    ``m_norm`` is the device fp32 [B,3,3] (or [1,3,3] broadcast is NOT allowed;
+    pass B rows) src_norm <- dst_norm matrix from ``kornia_src_norm_from_dst_norm``.
+    """
+    _require_cuda(src, m_norm, dst)
+    if src.dim() != 4 or dst.dim() != 4:
+        raise ValueError("src and dst must be 4-D")
+    B, C, H, W = src.shape
+    if dst.shape[0] != B or dst.shape[1] != C:
+        raise ValueError(f"dst {tuple(dst.shape)} does not match src {tuple(src.shape)}")
+    if m_norm.shape != (B, 3, 3) or m_norm.dtype != torch.float32 or not m_norm.is_contiguous():
+        raise ValueError("m_norm must be a contiguous float32 [B,3,3] device tensor")
+    if src.dtype != dst.dtype:
+        raise TypeError("src and dst dtypes differ")
+    lib = _native.load()
+    if src.dtype == torch.float32:
+        fn, name = lib.mvbev_warp_perspective_f32, "mvbev_warp_perspective_f32"
+    elif src.dtype == torch.float16:
+        fn, name = lib.mvbev_warp_perspective_f16, "mvbev_warp_perspective_f16"
+    else:
+        raise TypeError(f"unsupported dtype {src.dtype}")
+    st = fn(src.data_ptr(), B, C, H, W, _native.strides4(src), m_norm.data_ptr(), dst.data_ptr(),
+            dst.shape[2], dst.shape[3], _native.strides4(dst), _stream(dst))
+    _native.check(st, name)
+    return dst
+
+
+def warp_perspective(src: torch.Tensor, M: torch.Tensor, dsize: Tuple[int, int], mode: str = "bilinear",
+                     padding_mode: str = "zeros", align_corners: bool = True,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Drop-in for kornia 0.6.11 ``warp_perspective`` (default-argument path).
+
+    ``M`` (src pixel -> dst pixel, [B,3,3]) is normalised and inverted on the host in
+    fp32 exactly as kornia does; the HIP kernel does transform + divide + bilinear
+    gather.  Only bilinear / zeros / align_corners=True are implemented (the only
+    combination the reference exercises, ``persp_trans_detector.py:69``).
+    """
+    if not isinstance(src, torch.Tensor):
+        raise TypeError(f"Input src type is not a torch.Tensor. Got {type(src)}")
+    if not isinstance(M, torch.Tensor):
+        raise TypeError(f"Input M type is not a torch.Tensor. Got {type(M)}")
+    if not len(src.shape) == 4:
+        raise ValueError(f"Input src must be a BxCxHxW tensor. Got {src.shape}")
+    if not (len(M.shape) == 3 and M.shape[-2:] == (3, 3)):
+        raise ValueError(f"Input M must be a Bx3x3 tensor. Got {M.shape}")
+    if mode != "bilinear" or padding_mode != "zeros" or not align_corners:
+        raise NotImplementedError("only mode='bilinear', padding_mode='zeros', align_corners=True")
+    B, C, H, W = src.shape
+    ho, wo = int(dsize[0]), int(dsize[1])
+    if M.shape[0] != B:
+        raise ValueError(f"M batch {M.shape[0]} != src batch {B}")
+    m_norm = kornia_src_norm_from_dst_norm(M, (H, W), (ho, wo)).to(src.device).contiguous()
+    if out is None:
+        out = torch.empty((B, C, ho, wo), dtype=src.dtype, device=src.device)
+    return warp_into(src, m_norm, out)
+
+
+def fill_coord_map(dst: torch.Tensor) -> torch.Tensor:
+    """Write the coord map (``create_coord_map``) into ``dst`` [B,2,Ho,Wo] (a view)."""
+    _require_cuda(dst)
+    if dst.dim() != 4 or dst.shape[1] != 2 or dst.dtype != torch.float32:
+        raise ValueError("dst must be a float32 [B,2,Ho,Wo] view")
+    B, _, ho, wo = dst.shape
+    st = _native.load().mvbev_fill_coord_map_f32(dst.data_ptr(), B, ho, wo, _native.strides4(dst),
+                                                 _stream(dst))
+    _native.check(st, "mvbev_fill_coord_map_f32")
+    return dst
+
+
+# ----------------------------------------------------------------------------------------------
+# convs
+
+def padded_channels(cin: int) -> int:
+    return (cin + KC - 1) // KC * KC
+
+
+class PackedConv3x3:
+    """MFMA-layout copy of an ``nn.Conv2d`` 3x3 weight, re-packed only when the
+    parameter changes (keyed by ``(data_ptr, _version)``)."""
+
+    def __init__(self):
+        self._key = None
+        self.packed: Optional[torch.Tensor] = None
+
+    def get(self, weight: torch.Tensor) -> torch.Tensor:
+        _require_cuda(weight)
+        key = (weight.data_ptr(), weight._version, tuple(weight.shape))
+        if key != self._key:
+            cout, cin, kh, kw = weight.shape
+            if (kh, kw) != (3, 3) or weight.dtype != torch.float32:
+                raise ValueError("expected a float32 [Cout,Cin,3,3] weight")
+            if cout % BN:
+                raise ValueError(f"Cout={cout} must be a multiple of {BN}")
+            lib = _native.load()
+            n = lib.mvbev_conv3x3_packed_floats(cout, cin)
+            packed = torch.empty(n, dtype=torch.float32, device=weight.device)
+            w = weight.detach().contiguous()
+            _native.check(lib.mvbev_pack_conv3x3_weight_f32(w.data_ptr(), cout, cin, packed.data_ptr(),
+                                                            _stream(packed)), "mvbev_pack_conv3x3_weight_f32")
+            self.packed, self._key = packed, key
+        return self.packed
+
+
+def conv3x3(x: torch.Tensor, packed: torch.Tensor, cin: int, cout: int, bias: Optional[torch.Tensor],
+            dilation: int, relu: bool, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``relu?(conv2d(x[:, :cin], w, bias, padding=d, dilation=d))`` on fp32 MFMA.
+
+    ``x`` is [B, roundup(cin, 8), H, W] contiguous; channels >= cin must be finite.
+    """
+    _require_cuda(x, packed)
+    if x.dim() != 4 or x.dtype != torch.float32 or not x.is_contiguous():
+        raise ValueError("x must be a contiguous float32 [B,Cin_pad,H,W] tensor")
+    B, cpad, H, W = x.shape
+    if cpad != padded_channels(cin):
+        raise ValueError(f"x has {cpad} channels, expected {padded_channels(cin)} for Cin={cin}")
+    if out is None:
+        out = torch.empty((B, cout, H, W), dtype=torch.float32, device=x.device)
+    elif out.shape != (B, cout, H, W) or not out.is_contiguous():
+        raise ValueError("out must be a contiguous [B,Cout,H,W] tensor")
+    if bias is not None:
+        _require_cuda(bias)
+        bias = bias.detach().contiguous()
+    st = _native.load().mvbev_conv3x3_f32(x.data_ptr(), B, cin, H, W, packed.data_ptr(),
+                                          bias.data_ptr() if bias is not None else None, cout,
+                                          int(dilation), int(bool(relu)), out.data_ptr(), _stream(x))
+    _native.check(st, "mvbev_conv3x3_f32")
+    return out
+
+
+def conv3x3_cout1(x: torch.Tensor, weight: torch.Tensor, dilation: int,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``conv2d(x, weight[1,C,3,3], padding=d, dilation=d)`` (no bias) → [B,1,H,W]."""
+    _require_cuda(x, weight)
+    if x.dim() != 4 or x.dtype != torch.float32 or not x.is_contiguous():
+        raise ValueError("x must be a contiguous float32 [B,C,H,W] tensor")
+    B, C, H, W = x.shape
+    if tuple(weight.shape) != (1, C, 3, 3):
+        raise ValueError(f"weight must be [1,{C},3,3], got {tuple(weight.shape)}")
+    w = weight.detach().contiguous()
+    if out is None:
+        out = torch.empty((B, 1, H, W), dtype=torch.float32, device=x.device)
+    st = _native.load().mvbev_conv3x3_cout1_f32(x.data_ptr(), B, C, H, W, w.data_ptr(), int(dilation),
+                                                out.data_ptr(), _stream(x))
+    _native.check(st, "mvbev_conv3x3_cout1_f32")
+    return out

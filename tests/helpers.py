@@ -1,0 +1,45 @@
+"""Shared test helpers: golden-fixture loading and the parity gate.
+
+Parity gate (north_star "within 1e-3 relative fp32"):
+per tensor  |got - ref| <= 1e-3 * |ref| + 1e-3 * max|ref|   elementwise, and
+normwise    max|got - ref| / max|ref| <= 1e-3.
+"""
+import json
+from pathlib import Path
+
+import numpy as np
+import torch
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+RTOL = 1e-3
+ATOL_FRAC = 1e-3
+
+
+def load_golden(name):
+    d = dict(np.load(GOLDEN / f"{name}.npz", allow_pickle=False))
+    d["meta"] = json.loads(str(d["meta"]))
+    return d
+
+
+def to_np(x):
+    if isinstance(x, torch.Tensor):
+        return x.detach().to("cpu", torch.float64).numpy()
+    return np.asarray(x, dtype=np.float64)
+
+
+def parity_stats(got, ref):
+    got, ref = to_np(got), to_np(ref)
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    scale = float(np.abs(ref).max()) if ref.size else 0.0
+    diff = np.abs(got - ref)
+    normwise = float(diff.max() / scale) if scale > 0 else float(diff.max())
+    bound = RTOL * np.abs(ref) + ATOL_FRAC * scale
+    n_bad = int((diff > bound).sum())
+    return dict(normwise=normwise, n_bad=n_bad, max_abs=float(diff.max()) if diff.size else 0.0, scale=scale)
+
+
+def assert_parity(got, ref, what="", normwise_tol=1e-3):
+    s = parity_stats(got, ref)
+    assert np.isfinite(to_np(got)).all() == np.isfinite(to_np(ref)).all(), f"{what}: finiteness differs"
+    assert s["n_bad"] == 0 and s["normwise"] <= normwise_tol, f"{what}: parity failed {s}"
+    return s

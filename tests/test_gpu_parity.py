@@ -1,0 +1,223 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle.
+
+Tolerance (north_star: "within 1e-3 relative fp32"):
+  elementwise |got-ref| <= 1e-3*|ref| + 1e-3*max|ref|  and  normwise max|got-ref|/max|ref| <= 1e-3
+(``helpers.assert_parity``).  Warp outputs are additionally held to 2e-4 normwise
+against the float64 closed form.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import assert_parity, load_golden, parity_stats
+from oracle import cpu_path, fixtures, kornia_warp
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _rand_h(rng, H, W, ho, wo):
+    A = np.eye(3)
+    A[0, 0] = wo / W * rng.uniform(0.6, 1.4)
+    A[1, 1] = ho / H * rng.uniform(0.6, 1.4)
+    A[0, 1], A[1, 0] = rng.uniform(-0.2, 0.2, 2)
+    A[0, 2], A[1, 2] = rng.uniform(-3, 3, 2)
+    A[2, 0], A[2, 1] = rng.uniform(-2e-3, 2e-3, 2)
+    return A
+
+
+# ---------------------------------------------------------------------------------- warp
+
+@pytest.mark.parametrize("B,C,H,W,ho,wo", [(1, 5, 27, 48, 12, 36), (2, 67, 30, 41, 17, 23), (1, 3, 5, 7, 1, 9),
+                                           (2, 130, 64, 96, 40, 63)])
+def test_warp_vs_oracle_and_closed_form(B, C, H, W, ho, wo):
+    from mvdet_amd import warp_perspective
+    rng = np.random.default_rng(B * 1000 + C)
+    src = np.maximum(rng.standard_normal((B, C, H, W)), 0).astype(np.float32)
+    M = np.stack([_rand_h(rng, H, W, ho, wo) for _ in range(B)])
+    Mt = torch.from_numpy(M).float()
+    got = warp_perspective(torch.from_numpy(src).to(DEV), Mt.to(DEV), (ho, wo)).cpu()
+    ref = kornia_warp.warp_perspective(torch.from_numpy(src), Mt, (ho, wo))
+    assert_parity(got, ref, "warp vs restatement")
+    if ho > 1 and wo > 1:
+        s = parity_stats(got, kornia_warp.closed_form_warp_f64(src, M, (ho, wo)))
+        assert s["normwise"] < 2e-4, s
+
+
+def test_warp_identity_translation_oob_behind_camera():
+    from mvdet_amd import warp_perspective
+    rng = np.random.default_rng(5)
+    src = torch.from_numpy(rng.standard_normal((1, 4, 9, 11)).astype(np.float32))
+    out = warp_perspective(src.to(DEV), torch.eye(3)[None].to(DEV), (9, 11)).cpu()
+    np.testing.assert_allclose(out.numpy(), src.numpy(), atol=1e-5)
+    M = torch.tensor([[[1.0, 0, -0.5], [0, 1, 0], [0, 0, 1]]])
+    out = warp_perspective(src.to(DEV), M.to(DEV), (9, 11)).cpu()
+    np.testing.assert_allclose(out.numpy(), kornia_warp.warp_perspective(src, M, (9, 11)).numpy(), atol=1e-5)
+    far = torch.tensor([[[1.0, 0, 100.0], [0, 1, 100.0], [0, 0, 1]]])
+    assert warp_perspective(src.to(DEV), far.to(DEV), (4, 4)).abs().max().item() == 0
+    Minv = -np.eye(3)
+    M = torch.from_numpy(np.linalg.inv(Minv)).float()[None]
+    out = warp_perspective(torch.ones(1, 1, 8, 8, device=DEV), M.to(DEV), (8, 8))
+    assert out.min().item() > 0.99  # no cheirality mask (reference quirk)
+
+
+def test_warp_strided_src_and_channel_slice_dst():
+    from mvdet_amd import ops
+    from mvdet_amd.geometry import kornia_src_norm_from_dst_norm
+    rng = np.random.default_rng(9)
+    big = torch.from_numpy(rng.standard_normal((2, 40, 30, 50)).astype(np.float32)).to(DEV)
+    src = big[:, 5:25, :, 3:45]                          # non-contiguous view
+    M = torch.from_numpy(np.stack([_rand_h(rng, 30, 42, 20, 24) for _ in range(2)])).float()
+    m_norm = kornia_src_norm_from_dst_norm(M, (30, 42), (20, 24)).to(DEV).contiguous()
+    dst_full = torch.full((2, 50, 20, 24), 7.0, device=DEV)
+    ops.warp_into(src, m_norm, dst_full[:, 10:30])
+    ref = kornia_warp.warp_perspective(src.cpu().contiguous(), M, (20, 24))
+    assert_parity(dst_full[:, 10:30].cpu(), ref, "slice")
+    assert (dst_full[:, :10] == 7).all() and (dst_full[:, 30:] == 7).all()
+
+
+def test_warp_f16_storage():
+    from mvdet_amd import warp_perspective
+    rng = np.random.default_rng(11)
+    src = np.maximum(rng.standard_normal((2, 33, 27, 48)), 0).astype(np.float16)
+    M = torch.from_numpy(np.stack([_rand_h(rng, 27, 48, 12, 36) for _ in range(2)])).float()
+    got = warp_perspective(torch.from_numpy(src).to(DEV), M.to(DEV), (12, 36)).float().cpu()
+    ref = kornia_warp.warp_perspective(torch.from_numpy(src.astype(np.float32)), M, (12, 36))
+    s = parity_stats(got, ref)
+    assert s["normwise"] < 2e-3, s  # fp16 output rounding (2^-11 relative)
+
+
+def test_warp_rejects_bad_input_like_kornia():
+    from mvdet_amd import warp_perspective
+    with pytest.raises(ValueError):
+        warp_perspective(torch.zeros(3, 4, 5, device=DEV), torch.eye(3)[None].to(DEV), (2, 2))
+    with pytest.raises(ValueError):
+        warp_perspective(torch.zeros(1, 3, 4, 5, device=DEV), torch.eye(3).to(DEV), (2, 2))
+    with pytest.raises(TypeError):
+        warp_perspective(np.zeros((1, 3, 4, 5)), torch.eye(3)[None], (2, 2))
+
+
+# ---------------------------------------------------------------------------------- convs
+
+@pytest.mark.parametrize("B,cin,H,W,d,relu,bias", [(1, 8, 4, 32, 1, True, True), (1, 770, 13, 37, 1, True, True),
+                                                   (2, 19, 9, 70, 2, False, True), (1, 512, 20, 33, 2, True, True),
+                                                   (1, 3, 3, 5, 1, False, False)])
+def test_conv3x3_vs_torch(B, cin, H, W, d, relu, bias):
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(cin * 7 + H)
+    cout = 256 if cin < 100 else 128
+    x = torch.rand(B, cin, H, W, generator=g)
+    w = (torch.rand(cout, cin, 3, 3, generator=g) - 0.5) / np.sqrt(cin * 9)
+    b = torch.rand(cout, generator=g) - 0.5 if bias else None
+    ref = F.conv2d(x, w, b, padding=d, dilation=d)
+    if relu:
+        ref = F.relu(ref)
+    xp = torch.zeros(B, ops.padded_channels(cin), H, W)
+    xp[:, :cin] = x
+    pk = ops.PackedConv3x3().get(w.to(DEV))
+    got = ops.conv3x3(xp.to(DEV), pk, cin, cout, b.to(DEV) if bias else None, d, relu).cpu()
+    assert_parity(got, ref, "conv3x3", normwise_tol=2e-5)
+
+
+@pytest.mark.parametrize("C,H,W,d", [(512, 12, 36, 4), (7, 5, 70, 1), (33, 9, 130, 2)])
+def test_conv3x3_cout1_vs_torch(C, H, W, d):
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(C + H)
+    x = torch.rand(2, C, H, W, generator=g)
+    w = (torch.rand(1, C, 3, 3, generator=g) - 0.5) / np.sqrt(C * 9)
+    ref = F.conv2d(x, w, None, padding=d, dilation=d)
+    got = ops.conv3x3_cout1(x.to(DEV), w.to(DEV), d).cpu()
+    assert_parity(got, ref, "cout1", normwise_tol=2e-5)
+
+
+def test_packed_weight_cache_tracks_in_place_updates():
+    from mvdet_amd import ops
+    w = torch.randn(128, 16, 3, 3, device=DEV)
+    pc = ops.PackedConv3x3()
+    p0 = pc.get(w).clone()
+    assert torch.equal(pc.get(w), p0)
+    with torch.no_grad():
+        w.mul_(2)
+    assert torch.allclose(pc.get(w), 2 * p0)
+
+
+# ---------------------------------------------------------------------------------- golden
+
+def _ds_from_golden(g):
+    from mvdet_amd.synthetic import SyntheticBase, SyntheticFrameDataset
+    m = g["meta"]
+    base = SyntheticBase("fixture", m["img_shape"], m["worldgrid_shape"], m["num_cam"], g["G"],
+                         tuple(g["K"]), tuple(g["E"]))
+    return SyntheticFrameDataset(base, grid_reduce=m["grid_reduce"], img_reduce=m["img_reduce"])
+
+
+@pytest.mark.parametrize("name", ["module_wt2", "module_mx3_b2"])
+def test_detector_forward_matches_reference_golden(name):
+    """The drop-in module's forward (backbone bypassed exactly as the fixture did)
+    reproduces the reference's own forward outputs."""
+    import torch.nn as nn
+    from mvdet_amd import PerspTransDetector
+    g = load_golden(name)
+    m = g["meta"]
+    model = PerspTransDetector(_ds_from_golden(g))
+    params = fixtures.head_params(m["num_cam"], m["weight_seed"])
+    assert fixtures.params_sha256(params) == m["weights_sha256"]
+    sd = model.state_dict()
+    sd.update({k: torch.from_numpy(v) for k, v in params.items()})
+    model.load_state_dict(sd)
+    model.base_pt1, model.base_pt2 = nn.Identity(), nn.Identity()
+    model.eval()
+    with torch.no_grad():
+        map_res, imgs_res = model(torch.from_numpy(g["feat_in"]))
+        torch.cuda.synchronize()
+    assert map_res.shape == g["map_result"].shape
+    assert_parity(map_res.cpu(), g["map_result"], f"{name} map_result")
+    assert_parity(torch.stack(imgs_res, 0).cpu(), g["imgs_result"], f"{name} imgs_result")
+    ws = model.engine.workspace(m["B"], "cuda:0")
+    N, C = m["num_cam"], 512
+    warped = ws.fused[:, :N * C].reshape(m["B"], N, C, *m["reducedgrid_shape"]).double().sum(dim=(3, 4))
+    np.testing.assert_allclose(warped.cpu().numpy(), g["warp_out_chsum"], rtol=2e-3, atol=2e-2)
+    np.testing.assert_array_equal(ws.fused[:, N * C:N * C + 2].cpu().numpy(),
+                                  np.repeat(g["coord_map"], m["B"], 0))
+    if "warp_out" in g:
+        assert_parity(ws.fused[:, :N * C].reshape(g["warp_out"].shape).cpu(), g["warp_out"], "warp_out")
+        assert_parity(ws.y1.cpu(), g["conv1_relu"], "conv1")
+        assert_parity(ws.y2.cpu(), g["conv2_relu"], "conv2")
+
+
+# ---------------------------------------------------------------------------------- full size
+
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_full_size_project_fuse_vs_oracle(cfg):
+    """BASELINE configs 1 and 2 at full size, HIP path vs the CPU oracle on identical inputs."""
+    from mvdet_amd import ProjectFuse, synthetic
+    from mvdet_amd.geometry import projection_matrices
+    spec = synthetic.CONFIGS[cfg]
+    ds = spec["make"]()
+    B, C = spec["B"], spec["C"]
+    up = ds.upsample_shape
+    hb = [u // 3 for u in up]
+    feats = [synthetic.synthetic_features(B, C, hb, up, seed=1000 * cfg + v) for v in range(ds.num_cam)]
+    params = fixtures.head_params(ds.num_cam, seed=cfg, C=C)
+    pm = projection_matrices(ds)
+    eng = ProjectFuse(pm, tuple(up), tuple(ds.reducedgrid_shape), C)
+    mc = torch.nn.Sequential(torch.nn.Conv2d(C * ds.num_cam + 2, 512, 3, padding=1), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False))
+    with torch.no_grad():
+        for i, k in ((0, "0.weight"), (0, "0.bias"), (2, "2.weight"), (2, "2.bias"), (4, "4.weight")):
+            getattr(mc[i], k.split(".")[1]).copy_(torch.from_numpy(params["map_classifier." + k]))
+    mc = mc.to(DEV)
+    with torch.no_grad():
+        got = eng.project_fuse([f.to(DEV) for f in feats], mc)
+        torch.cuda.synchronize()
+        keep = {}
+        ref = cpu_path.project_fuse(feats, [M.numpy() for M in pm], tuple(ds.reducedgrid_shape),
+                                    {k: torch.from_numpy(v) for k, v in params.items()}, keep=keep)
+    ws = eng.workspace(B, DEV)
+    for v in range(ds.num_cam):
+        assert_parity(eng.view_slice(ws, v).cpu(), keep["warped"][v], f"cfg{cfg} warp view {v}")
+    assert_parity(ws.y1.cpu(), keep["conv1_relu"], f"cfg{cfg} conv1")
+    assert_parity(ws.y2.cpu(), keep["conv2_relu"], f"cfg{cfg} conv2")
+    assert_parity(got.cpu(), ref, f"cfg{cfg} map_result")

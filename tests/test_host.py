@@ -1,0 +1,99 @@
+"""CPU tests of the product's host side: the C-ABI library loads and exports every
+declared symbol, argument validation returns the documented codes (no GPU work is
+launched for those), the host geometry matches the reference fixtures/oracle, and
+the drop-in module keeps the reference's state_dict layout."""
+import ctypes
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import load_golden
+from mvdet_amd import _native, geometry
+from oracle import kornia_warp
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _header_functions():
+    text = (ROOT / "include" / "mvbev.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mvbev_\w+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = _native.load()
+    declared = _header_functions()
+    assert declared == sorted(_native.EXPORTS)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.mvbev_version() == 10000
+    assert lib.mvbev_status_string(0) == b"ok"
+    assert lib.mvbev_status_string(-100) == b"HIP launch failed"
+
+
+def test_argument_validation_codes():
+    lib = _native.load()
+    s4 = _native._i64x4(1, 1, 1, 1)
+    assert lib.mvbev_warp_perspective_f32(None, 1, 1, 1, 1, s4, None, None, 1, 1, s4, None) == -5
+    p = ctypes.c_void_p(16)  # never dereferenced: validation fails first
+    assert lib.mvbev_warp_perspective_f32(p, 0, 1, 1, 1, s4, p, p, 1, 1, s4, None) == -1
+    bad = _native._i64x4(1, 1, 1, 2)
+    assert lib.mvbev_warp_perspective_f32(p, 1, 1, 1, 1, s4, p, p, 1, 1, bad, None) == -3
+    assert lib.mvbev_conv3x3_f32(p, 1, 8, 4, 4, p, None, 100, 1, 1, p, None) == -2  # Cout % 128
+    assert lib.mvbev_conv3x3_f32(p, 1, 8, 4, 4, p, None, 128, 3, 1, p, None) == -6  # dilation 3
+    assert lib.mvbev_conv3x3_f32(p, 1, 8, 4, 4, ctypes.c_void_p(20), None, 128, 1, 1, p, None) == -4
+    assert lib.mvbev_conv3x3_cout1_f32(p, 1, 8, 4, 4, p, 3, p, None) == -6
+    assert lib.mvbev_pack_conv3x3_weight_f32(p, 100, 8, p, None) == -2
+    assert lib.mvbev_conv3x3_packed_floats(512, 3586) == 3592 * 9 * 512
+    assert lib.mvbev_fill_coord_map_f32(None, 1, 2, 2, s4, None) == -5
+
+
+def test_kornia_matrix_is_bitwise_the_oracle_recipe():
+    rng = np.random.default_rng(3)
+    for _ in range(5):
+        M = torch.from_numpy(np.eye(3) + rng.uniform(-0.3, 0.3, (3, 3))).float()[None]
+        got = geometry.kornia_src_norm_from_dst_norm(M, (270, 480), (120, 360))
+        ref = kornia_warp.src_norm_from_dst_norm(M, (270, 480), (120, 360))
+        assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("name", ["module_wt2", "module_mx3_b2"])
+def test_geometry_matches_reference_fixture(name):
+    g = load_golden(name)
+    m = g["meta"]
+    from mvdet_amd.synthetic import SyntheticBase, SyntheticFrameDataset
+    base = SyntheticBase("fixture", m["img_shape"], m["worldgrid_shape"], m["num_cam"], g["G"],
+                         tuple(g["K"]), tuple(g["E"]))
+    ds = SyntheticFrameDataset(base, grid_reduce=m["grid_reduce"], img_reduce=m["img_reduce"])
+    assert ds.reducedgrid_shape == m["reducedgrid_shape"] and ds.upsample_shape == m["upsample_shape"]
+    got = torch.stack(geometry.projection_matrices(ds)).numpy()
+    np.testing.assert_allclose(got, g["proj_mats"], rtol=1e-12, atol=0)
+    assert torch.equal(geometry.coord_map(*m["reducedgrid_shape"]), torch.from_numpy(g["coord_map"]))
+
+
+def test_touched_footprint_matches_oracle():
+    g = dict(np.load(ROOT / "tests/golden/geometry_configs.npz", allow_pickle=False))
+    for M in g["cfg1_proj_mats"][:2]:
+        assert geometry.touched_footprint(M, (270, 480), (160, 250)) == \
+            kornia_warp.touched_footprint(M, (270, 480), (160, 250))
+
+
+def test_detector_state_dict_layout_matches_reference():
+    g = load_golden("module_wt2")
+    m = g["meta"]
+    from mvdet_amd import PerspTransDetector
+    from mvdet_amd.synthetic import SyntheticBase, SyntheticFrameDataset
+    base = SyntheticBase("fixture", m["img_shape"], m["worldgrid_shape"], m["num_cam"], g["G"],
+                         tuple(g["K"]), tuple(g["E"]))
+    ds = SyntheticFrameDataset(base, grid_reduce=m["grid_reduce"], img_reduce=m["img_reduce"])
+    model = PerspTransDetector(ds, device="cpu")
+    shapes = {k: list(v.shape) for k, v in model.state_dict().items()}
+    assert shapes == m["state_dict_shapes"]
+    assert list(shapes) == list(m["state_dict_shapes"])
+    assert model.upsample_shape == m["upsample_shape"]
+    assert not any("proj_mats" in k or "coord_map" in k for k in shapes)  # quirk B.4: not buffers
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        model(torch.zeros(1, m["num_cam"], 3, 32, 32))

@@ -49,9 +49,13 @@ __global__ __launch_bounds__(256) void warp_perspective_kernel(
   const float iy = ((y + 1.f) / 2.f) * (float)(H - 1);
 
   T* out = dst + (int64_t)b * dB + (int64_t)v * dH + u;
-  // Any corner in bounds?  (NaN compares false -> all-zero output, as torch.)
-  if (!(ix > -1.f && ix < (float)W && iy > -1.f && iy < (float)H)) {
-    for (int c = c_begin; c < c_end; ++c) out[(int64_t)c * dC] = from_f32<T>(0.f);
+  // Non-finite sample position (kornia's 0/0 meshgrid when Ho or Wo is 1, or an inf
+  // after the divide): torch's bilinear weights become NaN, so every channel is NaN.
+  // Otherwise, no corner in bounds -> zeros padding.
+  const bool finite = isfinite(ix) && isfinite(iy);
+  if (!finite || !(ix > -1.f && ix < (float)W && iy > -1.f && iy < (float)H)) {
+    const float fill = finite ? 0.f : __builtin_nanf("");
+    for (int c = c_begin; c < c_end; ++c) out[(int64_t)c * dC] = from_f32<T>(fill);
     return;
   }
   const float fx0 = floorf(ix), fy0 = floorf(iy);

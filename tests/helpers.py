@@ -28,10 +28,18 @@ def to_np(x):
 
 
 def parity_stats(got, ref):
+    """Stats over the finite entries; the NaN/inf pattern itself must match exactly."""
     got, ref = to_np(got), to_np(ref)
     assert got.shape == ref.shape, (got.shape, ref.shape)
+    nf_g, nf_r = ~np.isfinite(got), ~np.isfinite(ref)
+    assert np.array_equal(nf_g, nf_r), f"non-finite pattern differs ({int(nf_g.sum())} vs {int(nf_r.sum())})"
+    assert np.array_equal(np.isnan(got), np.isnan(ref)), "NaN pattern differs"
+    fin = ~nf_r
+    got, ref = got[fin], ref[fin]
     scale = float(np.abs(ref).max()) if ref.size else 0.0
     diff = np.abs(got - ref)
+    if diff.size == 0:
+        return dict(normwise=0.0, n_bad=0, max_abs=0.0, scale=scale)
     normwise = float(diff.max() / scale) if scale > 0 else float(diff.max())
     bound = RTOL * np.abs(ref) + ATOL_FRAC * scale
     n_bad = int((diff > bound).sum())
@@ -40,6 +48,5 @@ def parity_stats(got, ref):
 
 def assert_parity(got, ref, what="", normwise_tol=1e-3):
     s = parity_stats(got, ref)
-    assert np.isfinite(to_np(got)).all() == np.isfinite(to_np(ref)).all(), f"{what}: finiteness differs"
     assert s["n_bad"] == 0 and s["normwise"] <= normwise_tol, f"{what}: parity failed {s}"
     return s

@@ -1,0 +1,25 @@
+#!/bin/bash
+# rocprofv3 passes for the bench workload (run on the GPU box from the repo root):
+#   1. kernel trace + stats of bench.py (per-kernel durations)      -> gpurun_out/prof/<tag>_trace
+#   2. separate --pmc passes on tools/kbench.py (clock, MFMA busy, HBM bytes, stalls)
+# Usage: bash tools/profile_gpu.sh <tag> [config]
+set -o pipefail
+TAG=${1:-r01}
+CFG=${2:-2}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/prof
+mkdir -p $OUT
+export TMPDIR=/tmp
+cd $R
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_trace -o run -- \
+  python3 bench.py --steps 10 --warmup 3 --config $CFG --no-cpu-baseline > $OUT/${TAG}_trace_bench.log 2>&1 || exit $?
+i=0
+for PMC in "GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES" \
+           "FETCH_SIZE" "WRITE_SIZE" \
+           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \
+           "TCC_HIT_sum TCC_MISS_sum"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $PMC --output-format csv -d $OUT/${TAG}_pmc$i -o run -- \
+    python3 tools/kbench.py --config $CFG --reps 3 > $OUT/${TAG}_pmc$i.log 2>&1 || exit $?
+done
+echo profile-done

@@ -16,7 +16,9 @@
 //   KC=8 input channels; per chunk the (TH+2d) x (TW+2d) input halo of all 8 channels and the
 //   9 x 8 x 128 weight slab are staged in LDS and every staged input element feeds all 9 taps.
 //   The next chunk's global loads are issued into registers before the MFMAs of the current
-//   chunk (async-STAGE split) and written to LDS after the next barrier.
+//   chunk (async-STAGE split) and written to LDS after the next barrier; out-of-image halo
+//   elements load a safe in-bounds address and are zeroed by a select at LDS-store time,
+//   so no wait on those loads sits in front of the MFMAs.
 //
 // mvbev_conv3x3_cout1_f32 — Cout = 1 is a 4608-long dot product per pixel: HBM/L2-bound, no
 //   MFMA.  Block = 64 pixels of a row x 4 waves; each wave sums a quarter of the channels with
@@ -26,6 +28,7 @@
 namespace mvbev {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));  // native vector (HIP's float4 struct blocks SROA)
 
 constexpr int KC = MVBEV_CONV_KC;  // input channels per staged chunk
 constexpr int BN = MVBEV_CONV_BN;  // output channels per workgroup
@@ -79,7 +82,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_f32_kernel(
 
   const int64_t plane = (int64_t)H * W;
   const float* xb = x + (int64_t)b * Cin_pad * plane;
-  const float4* wsrc = reinterpret_cast<const float4*>(wp) + (int64_t)cot * (WS / 4);
+  const floatx4* wsrc = reinterpret_cast<const floatx4*>(wp) + (int64_t)cot * (WS / 4);
   const int64_t wchunk = (int64_t)n_cot * (WS / 4);
   const int nchunks = Cin_pad / KC;
 
@@ -97,36 +100,37 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_f32_kernel(
     xoff[i] = xok[i] ? (int)(kk * plane + gy * W + gx) : 0;
   }
 
-  float4 wreg[WLD];
+  // Staging registers for the next chunk (plain arrays with compile-time indices only:
+  // a lambda capturing them by reference would put them in scratch memory).
+  floatx4 wreg[WLD];
   float xreg[XLD];
-  auto load_chunk = [&](int ch) {
-    const float4* ws = wsrc + ch * wchunk;
-#pragma unroll
-    for (int i = 0; i < WLD; ++i) wreg[i] = ws[tid + 256 * i];
-    const float* xc = xb + (int64_t)ch * KC * plane;
-#pragma unroll
-    for (int i = 0; i < XLD; ++i) xreg[i] = xok[i] ? xc[xoff[i]] : 0.f;
-  };
-  auto store_chunk = [&]() {
-#pragma unroll
-    for (int i = 0; i < WLD; ++i) reinterpret_cast<float4*>(Ws)[tid + 256 * i] = wreg[i];
-#pragma unroll
-    for (int i = 0; i < XLD; ++i) {
-      const int e = tid + 256 * i;
-      if (XS % 256 == 0 || e < XS) Xs[e] = xreg[i];
-    }
-  };
+#define MVBEV_LOAD_CHUNK(ch)                                                     \
+  do {                                                                           \
+    const floatx4* ws_ = wsrc + (int64_t)(ch) * wchunk;                           \
+    _Pragma("unroll") for (int i = 0; i < WLD; ++i) wreg[i] = ws_[tid + 256 * i]; \
+    const float* xc_ = xb + (int64_t)(ch) * KC * plane;                          \
+    _Pragma("unroll") for (int i = 0; i < XLD; ++i) xreg[i] = xc_[xoff[i]]; /* select at store */ \
+  } while (0)
+#define MVBEV_STORE_CHUNK()                                                      \
+  do {                                                                           \
+    _Pragma("unroll") for (int i = 0; i < WLD; ++i)                              \
+        reinterpret_cast<floatx4*>(Ws)[tid + 256 * i] = wreg[i];                  \
+    _Pragma("unroll") for (int i = 0; i < XLD; ++i) {                            \
+      const int e = tid + 256 * i;                                               \
+      if (XS % 256 == 0 || e < XS) Xs[e] = xok[i] ? xreg[i] : 0.f;               \
+    }                                                                            \
+  } while (0)
 
   floatx16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
   const int prow = 2 * (wave & 1);  // this wave's two output rows within the tile
   const int cw = 64 * (wave >> 1);  // this wave's 64 output channels within BN
 
-  load_chunk(0);
+  MVBEV_LOAD_CHUNK(0);
   for (int ch = 0; ch < nchunks; ++ch) {
     __syncthreads();
-    store_chunk();
+    MVBEV_STORE_CHUNK();
     __syncthreads();
-    if (ch + 1 < nchunks) load_chunk(ch + 1);
+    if (ch + 1 < nchunks) MVBEV_LOAD_CHUNK(ch + 1);
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
 #pragma unroll
@@ -167,6 +171,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_f32_kernel(
   emit(acc01, 0, 1);
   emit(acc10, 1, 0);
   emit(acc11, 1, 1);
+#undef MVBEV_LOAD_CHUNK
+#undef MVBEV_STORE_CHUNK
 }
 
 template <int DIL>

@@ -120,24 +120,13 @@ def main():
     K, W = args.steps, args.warmup
     ev = {k: [torch.cuda.Event(enable_timing=True) for _ in range(K)] for k in ("warp", "conv1", "conv2", "conv3")}
 
-    from mvdet_amd import ops
-
     def step(i=None):
         if i is not None:
             ev["warp"][i].record()
         for v in range(N):
             eng.warp_view(ws, v, feats[v])
-        c1, c2, c3 = mc[0], mc[2], mc[4]
-        p1, p2 = eng.pack1.get(c1.weight), eng.pack2.get(c2.weight)
-        if i is not None:
-            ev["conv1"][i].record()
-        ops.conv3x3(ws.fused, p1, eng.cin, 512, c1.bias, 1, True, out=ws.y1)
-        if i is not None:
-            ev["conv2"][i].record()
-        ops.conv3x3(ws.y1, p2, 512, 512, c2.bias, 2, True, out=ws.y2)
-        if i is not None:
-            ev["conv3"][i].record()
-        return ops.conv3x3_cout1(ws.y2, c3.weight, 4)
+        mark = (lambda stage: ev[stage][i].record()) if i is not None else None
+        return eng.fuse(ws, mc, mark=mark)
 
     end_ev = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
     with torch.no_grad():

@@ -27,7 +27,9 @@
  *       (persp_trans_detector.py:21,77,103-112).
  *   mvbev_pack_conv3x3_weight_f32, mvbev_conv3x3_f32
  *       nn.Conv2d(Cin->Cout, 3, padding=d, dilation=d) (+ nn.ReLU) of
- *       map_classifier[0:4]   persp_trans_detector.py:51-53, :81
+ *       map_classifier[0:4]   persp_trans_detector.py:51-53, :81; the conv1 contribution of
+ *       the two constant coord channels plus its bias is input-independent and enters as
+ *       the `init` term (computed once per weight version with the same kernel).
  *   mvbev_conv3x3_cout1_f32
  *       nn.Conv2d(512->1, 3, padding=4, dilation=4, bias=False) of
  *       map_classifier[4]      persp_trans_detector.py:54, :81
@@ -53,8 +55,8 @@ extern "C" {
 #define MVBEV_ERR_DILATION (-6)  /* dilation not supported by this entry point */
 #define MVBEV_ERR_HIP (-100)     /* the HIP launch failed (hipGetLastError) */
 
-/* Input-channel granule of the conv kernels: the fused tensor's channel count
- * must be padded to a multiple of this (padding channels hold zeros). */
+/* Input-channel granule of the conv kernels: packed K and every channel group must be
+ * a multiple of this. */
 #define MVBEV_CONV_KC 8
 /* Output-channel granule of mvbev_conv3x3_f32. */
 #define MVBEV_CONV_BN 128
@@ -85,27 +87,51 @@ int mvbev_warp_perspective_f16(const void* src, int64_t B, int64_t C, int64_t H,
 int mvbev_fill_coord_map_f32(float* dst, int64_t B, int64_t Ho, int64_t Wo,
                              const int64_t dst_strides[4], void* stream);
 
-/* Number of floats of the packed weight buffer for a Cout x Cin x 3 x 3 conv. */
-size_t mvbev_conv3x3_packed_floats(int64_t Cout, int64_t Cin);
+/* Number of floats of the packed weight buffer for Cout output channels and K packed
+ * input channels (K rounded up to MVBEV_CONV_KC). */
+size_t mvbev_conv3x3_packed_floats(int64_t Cout, int64_t K);
 
-/* Re-lay an nn.Conv2d weight [Cout][Cin][3][3] (contiguous fp32, device) into
- * the MFMA staging layout (Cin zero-padded to MVBEV_CONV_KC). */
-int mvbev_pack_conv3x3_weight_f32(const float* w, int64_t Cout, int64_t Cin, float* w_packed,
+/* Re-lay an nn.Conv2d weight w[Cout][Cin_w][3][3] (contiguous fp32, device) into the MFMA
+ * staging layout for K packed input channels: packed channel k takes weight channel
+ * chan_map[k] (device int32[K]; -1 = zero weights), or k itself when chan_map is NULL
+ * (then K must equal Cin_w).  Lets the fused tensor's channel order differ from the
+ * module's (view-major slots, coord channels handled separately). */
+int mvbev_pack_conv3x3_weight_f32(const float* w, int64_t Cout, int64_t Cin_w,
+                                  const int32_t* chan_map, int64_t K, float* w_packed,
                                   void* stream);
 
-/* y = act(conv3x3(x, w, dilation=d, padding=d) + bias), fp32 MFMA, fp32 accumulate.
- *   x      : [B][Cin_pad][H][W] contiguous fp32, Cin_pad = roundup(Cin, KC);
- *            channels >= Cin must be finite (zero weights multiply them)
- *   w_packed : from mvbev_pack_conv3x3_weight_f32 (same Cout, Cin)
- *   bias   : [Cout] or NULL;   relu: 0/1;   dilation: 1 or 2
- *   y      : [B][Cout][H][W] contiguous fp32, Cout % MVBEV_CONV_BN == 0 */
-int mvbev_conv3x3_f32(const float* x, int64_t B, int64_t Cin, int64_t H, int64_t W,
-                      const float* w_packed, const float* bias, int64_t Cout,
-                      int dilation, int relu, float* y, void* stream);
+/* Geometry of one conv launch (all sizes in elements). */
+typedef struct mvbev_conv_desc {
+  int64_t B;             /* batch items */
+  int64_t K;             /* packed input channels (multiple of MVBEV_CONV_KC) */
+  int64_t H, W;          /* full image (ground grid) height / width */
+  int64_t group;         /* channels per contiguous channel group (multiple of KC, divides K) */
+  int64_t group_stride;  /* elements between consecutive channel groups */
+  int64_t batch_stride;  /* elements between consecutive batch items */
+  int64_t in_row0;       /* global row held by input-buffer row 0 */
+  int64_t in_rows;       /* rows in the input buffer (channel plane = in_rows * W) */
+  int64_t out_row0;      /* first global output row computed */
+  int64_t out_rows;      /* output rows computed (y holds exactly these rows) */
+} mvbev_conv_desc;
 
-/* y[b][0] = conv3x3(x[b], w, dilation=d, padding=d), one output channel, no bias.
- *   x : [B][C][H][W] contiguous fp32;  w : [C][3][3] contiguous fp32;  y : [B][1][H][W] */
+/* y = act(conv3x3(x, w, dilation=d, padding=d) [+ bias] [+ init]), fp32 MFMA, fp32 accumulate.
+ *   x      : input channel ci of item b at x + (ci/group)*group_stride + b*batch_stride
+ *            + (ci%group)*in_rows*W  ([B][K][H][W]: group=K; view-major [S][B][C][H][W]: group=C)
+ *   w_packed : from mvbev_pack_conv3x3_weight_f32 with the same Cout and K
+ *   bias   : [Cout] or NULL;  init : [Cout][H][W] (full-size, broadcast over B) or NULL
+ *   relu   : 0/1 (NaN-preserving);  dilation : 1 or 2
+ *   y      : [B][Cout][out_rows][W] contiguous fp32, Cout % MVBEV_CONV_BN == 0
+ *   Zero padding at the image border; input rows outside the buffer are read as zero, so
+ *   a band caller must supply every row the output band needs. */
+int mvbev_conv3x3_f32(const float* x, const mvbev_conv_desc* desc, const float* w_packed,
+                      const float* bias, const float* init, int64_t Cout, int dilation,
+                      int relu, float* y, void* stream);
+
+/* y[b][0][r][:] = conv3x3(x[b], w, dilation=d, padding=d)[out_row0 + r], one output channel,
+ * no bias.  x : [B][C][in_rows][W] holding global rows [in_row0, in_row0+in_rows) of an
+ * H x W image;  w : [C][3][3] contiguous fp32;  y : [B][1][out_rows][W]. */
 int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int64_t W,
+                            int64_t in_row0, int64_t in_rows, int64_t out_row0, int64_t out_rows,
                             const float* w, int dilation, float* y, void* stream);
 
 #ifdef __cplusplus

@@ -35,6 +35,12 @@ _i64x4 = ctypes.c_int64 * 4
 _lib = None
 
 
+class ConvDesc(ctypes.Structure):
+    """``mvbev_conv_desc`` (include/mvbev.h)."""
+    _fields_ = [(n, ctypes.c_int64) for n in ("B", "K", "H", "W", "group", "group_stride", "batch_stride",
+                                               "in_row0", "in_rows", "out_row0", "out_rows")]
+
+
 class NativeError(RuntimeError):
     pass
 
@@ -53,12 +59,13 @@ def _declare(lib):
     lib.mvbev_conv3x3_packed_floats.restype = ctypes.c_size_t
     lib.mvbev_conv3x3_packed_floats.argtypes = [_i64, _i64]
     lib.mvbev_pack_conv3x3_weight_f32.restype = ctypes.c_int
-    lib.mvbev_pack_conv3x3_weight_f32.argtypes = [_p, _i64, _i64, _p, _p]
+    lib.mvbev_pack_conv3x3_weight_f32.argtypes = [_p, _i64, _i64, _p, _i64, _p, _p]
     lib.mvbev_conv3x3_f32.restype = ctypes.c_int
-    lib.mvbev_conv3x3_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _p, _p, _i64, ctypes.c_int,
+    lib.mvbev_conv3x3_f32.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64, ctypes.c_int,
                                       ctypes.c_int, _p, _p]
     lib.mvbev_conv3x3_cout1_f32.restype = ctypes.c_int
-    lib.mvbev_conv3x3_cout1_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _p, ctypes.c_int, _p, _p]
+    lib.mvbev_conv3x3_cout1_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p,
+                                            ctypes.c_int, _p, _p]
 
 
 def load(path: os.PathLike | str | None = None):

@@ -20,6 +20,16 @@
 //   elements load a safe in-bounds address and are zeroed by a select at LDS-store time,
 //   so no wait on those loads sits in front of the MFMAs.
 //
+//   Input addressing (mvbev_conv_desc): input channel ci of batch item b lives at
+//     x + (ci / group) * group_stride + b * batch_stride + (ci % group) * in_rows * W
+//   which covers a plain [B][Cin][H][W] tensor (group = Cin) and the view-major fused
+//   ground-plane tensor [views][B][C][H][W] (group = C) without a repack.  Row bands: the
+//   input buffer holds global rows [in_row0, in_row0 + in_rows) and the kernel computes
+//   global output rows [out_row0, out_row0 + out_rows); zero padding applies at the true
+//   image border (rows < 0 or >= H) — used by the view-parallel multi-GPU fusion.
+//   Epilogue: + bias[co] and/or + init[co][row][col] (the precomputed coord-channel term),
+//   optional ReLU (NaN-preserving, like torch.relu).
+//
 // mvbev_conv3x3_cout1_f32 — Cout = 1 is a 4608-long dot product per pixel: HBM/L2-bound, no
 //   MFMA.  Block = 64 pixels of a row x 4 waves; each wave sums a quarter of the channels with
 //   wave-uniform (scalar) weight loads, partial sums reduced through LDS.
@@ -35,10 +45,12 @@ constexpr int BN = MVBEV_CONV_BN;  // output channels per workgroup
 constexpr int TH = 4;              // output rows per workgroup
 constexpr int TW = 32;             // output cols per workgroup (= MFMA N)
 
-// packed[chunk][cotile][tap][kk][col] = w[cotile*BN+col][chunk*KC+kk][tap] (0 for padded ci)
+// packed[chunk][cotile][tap][kk][col] = w[cotile*BN+col][map(chunk*KC+kk)][tap]
+// map = identity (chan_map == nullptr) or chan_map[k]; unmapped (-1) / k >= K -> 0.
 __global__ void pack_conv3x3_kernel(const float* __restrict__ w, float* __restrict__ wp, int Cout,
-                                    int Cin, int Cin_pad) {
-  const int64_t total = (int64_t)Cin_pad * 9 * Cout;
+                                    int Cin_w, const int32_t* __restrict__ chan_map, int K,
+                                    int K_pad) {
+  const int64_t total = (int64_t)K_pad * 9 * Cout;
   const int n_cot = Cout / BN;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -48,17 +60,28 @@ __global__ void pack_conv3x3_kernel(const float* __restrict__ w, float* __restri
     const int tap = r % 9; r /= 9;
     const int cot = r % n_cot;
     const int chunk = (int)(r / n_cot);
-    const int ci = chunk * KC + kk;
+    const int k = chunk * KC + kk;
+    int ci = k < K ? (chan_map ? chan_map[k] : k) : -1;
+    if (ci >= Cin_w) ci = -1;
     const int co = cot * BN + col;
-    wp[i] = ci < Cin ? w[((int64_t)co * Cin + ci) * 9 + tap] : 0.f;
+    wp[i] = ci >= 0 ? w[((int64_t)co * Cin_w + ci) * 9 + tap] : 0.f;
   }
 }
 
+struct ConvArgs {
+  const float* x;
+  const float* wp;
+  const float* bias;
+  const float* init;
+  float* y;
+  int64_t group_stride, batch_stride;
+  int group, nchunks, Cout, H, W;
+  int in_row0, in_rows, out_row0, out_rows;
+  int tiles_x, tiles_y, n_cot, nwg;
+};
+
 template <int DIL, bool RELU>
-__global__ __launch_bounds__(256, 2) void conv3x3_mfma_f32_kernel(
-    const float* __restrict__ x, const float* __restrict__ wp, const float* __restrict__ bias,
-    float* __restrict__ y, int Cin_pad, int Cout, int H, int W, int tiles_x, int tiles_y, int n_cot,
-    int nwg) {
+__global__ __launch_bounds__(256, 2) void conv3x3_mfma_f32_kernel(const ConvArgs a) {
   constexpr int XH = TH + 2 * DIL, XW = TW + 2 * DIL;
   constexpr int XS = KC * XH * XW;  // input halo floats per chunk
   constexpr int WS = 9 * KC * BN;   // weight floats per chunk
@@ -69,22 +92,24 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_f32_kernel(
   float* Ws = lds;
   float* Xs = lds + WS;
 
-  const int wg = xcd_remap(blockIdx.x, nwg);
-  const int cot = wg % n_cot;
-  int rest = wg / n_cot;
-  const int tx = rest % tiles_x;
-  rest /= tiles_x;
-  const int ty = rest % tiles_y;
-  const int b = rest / tiles_y;
-  const int x0 = tx * TW, y0 = ty * TH;
+  const int wg = xcd_remap(blockIdx.x, a.nwg);
+  const int cot = wg % a.n_cot;
+  int rest = wg / a.n_cot;
+  const int tx = rest % a.tiles_x;
+  rest /= a.tiles_x;
+  const int ty = rest % a.tiles_y;
+  const int b = rest / a.tiles_y;
+  const int x0 = tx * TW;
+  const int y0 = a.out_row0 + ty * TH;  // global output row of the tile's first row
+  const int W = a.W;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, kh = lane >> 5;
 
-  const int64_t plane = (int64_t)H * W;
-  const float* xb = x + (int64_t)b * Cin_pad * plane;
-  const floatx4* wsrc = reinterpret_cast<const floatx4*>(wp) + (int64_t)cot * (WS / 4);
-  const int64_t wchunk = (int64_t)n_cot * (WS / 4);
-  const int nchunks = Cin_pad / KC;
+  const int64_t plane = (int64_t)a.in_rows * W;
+  const float* xb = a.x + (int64_t)b * a.batch_stride;
+  const floatx4* wsrc = reinterpret_cast<const floatx4*>(a.wp) + (int64_t)cot * (WS / 4);
+  const int64_t wchunk = (int64_t)a.n_cot * (WS / 4);
+  const int chunks_per_group = a.group / KC;
 
   // Per-thread halo element coordinates are chunk-invariant: precompute offsets/validity.
   int xoff[XLD];
@@ -95,30 +120,32 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_f32_kernel(
     const int kk = e / (XH * XW);
     const int r = (e / XW) % XH;
     const int c = e % XW;
-    const int gy = y0 - DIL + r, gx = x0 - DIL + c;
-    xok[i] = e < XS && gy >= 0 && gy < H && gx >= 0 && gx < W;
-    xoff[i] = xok[i] ? (int)(kk * plane + gy * W + gx) : 0;
+    const int gy = y0 - DIL + r, gx = x0 - DIL + c;  // global input coordinates
+    const int by = gy - a.in_row0;                    // row inside the input buffer
+    xok[i] = e < XS && gy >= 0 && gy < a.H && by >= 0 && by < a.in_rows && gx >= 0 && gx < W;
+    xoff[i] = xok[i] ? (int)(kk * plane + (int64_t)by * W + gx) : 0;
   }
 
-  // Staging registers for the next chunk (plain arrays with compile-time indices only:
-  // a lambda capturing them by reference would put them in scratch memory).
+  // Staging registers for the next chunk (native vectors, compile-time indices only).
   floatx4 wreg[WLD];
   float xreg[XLD];
-#define MVBEV_LOAD_CHUNK(ch)                                                     \
-  do {                                                                           \
-    const floatx4* ws_ = wsrc + (int64_t)(ch) * wchunk;                           \
-    _Pragma("unroll") for (int i = 0; i < WLD; ++i) wreg[i] = ws_[tid + 256 * i]; \
-    const float* xc_ = xb + (int64_t)(ch) * KC * plane;                          \
+#define MVBEV_LOAD_CHUNK(ch)                                                                  \
+  do {                                                                                        \
+    const floatx4* ws_ = wsrc + (int64_t)(ch) * wchunk;                                       \
+    _Pragma("unroll") for (int i = 0; i < WLD; ++i) wreg[i] = ws_[tid + 256 * i];             \
+    const int g_ = (ch) / chunks_per_group;                                                   \
+    const float* xc_ =                                                                        \
+        xb + g_ * a.group_stride + (int64_t)((ch) - g_ * chunks_per_group) * KC * plane;      \
     _Pragma("unroll") for (int i = 0; i < XLD; ++i) xreg[i] = xc_[xoff[i]]; /* select at store */ \
   } while (0)
-#define MVBEV_STORE_CHUNK()                                                      \
-  do {                                                                           \
-    _Pragma("unroll") for (int i = 0; i < WLD; ++i)                              \
-        reinterpret_cast<floatx4*>(Ws)[tid + 256 * i] = wreg[i];                  \
-    _Pragma("unroll") for (int i = 0; i < XLD; ++i) {                            \
-      const int e = tid + 256 * i;                                               \
-      if (XS % 256 == 0 || e < XS) Xs[e] = xok[i] ? xreg[i] : 0.f;               \
-    }                                                                            \
+#define MVBEV_STORE_CHUNK()                                                                   \
+  do {                                                                                        \
+    _Pragma("unroll") for (int i = 0; i < WLD; ++i)                                           \
+        reinterpret_cast<floatx4*>(Ws)[tid + 256 * i] = wreg[i];                              \
+    _Pragma("unroll") for (int i = 0; i < XLD; ++i) {                                         \
+      const int e = tid + 256 * i;                                                            \
+      if (XS % 256 == 0 || e < XS) Xs[e] = xok[i] ? xreg[i] : 0.f;                            \
+    }                                                                                         \
   } while (0)
 
   floatx16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
@@ -126,11 +153,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_f32_kernel(
   const int cw = 64 * (wave >> 1);  // this wave's 64 output channels within BN
 
   MVBEV_LOAD_CHUNK(0);
-  for (int ch = 0; ch < nchunks; ++ch) {
+  for (int ch = 0; ch < a.nchunks; ++ch) {
     __syncthreads();
     MVBEV_STORE_CHUNK();
     __syncthreads();
-    if (ch + 1 < nchunks) MVBEV_LOAD_CHUNK(ch + 1);
+    if (ch + 1 < a.nchunks) MVBEV_LOAD_CHUNK(ch + 1);
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
 #pragma unroll
@@ -153,40 +180,45 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_f32_kernel(
       }
     }
   }
+#undef MVBEV_LOAD_CHUNK
+#undef MVBEV_STORE_CHUNK
 
   // Epilogue: D[i = co][j = pixel]; lane holds j = l32 and rows i = (r&3) + 8(r>>2) + 4 kh.
   const int col = x0 + l32;
+  const int64_t oplane = (int64_t)a.out_rows * W;
+  const int64_t iplane = (int64_t)a.H * W;  // init is full-size [Cout][H][W]
   auto emit = [&](const floatx16& acc, int ci_tile, int rj) {
     const int row = y0 + prow + rj;
-    if (row >= H || col >= W) return;
+    if (row >= a.out_row0 + a.out_rows || col >= W) return;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = cot * BN + cw + 32 * ci_tile + (r & 3) + 8 * (r >> 2) + 4 * kh;
-      float v = acc[r] + (bias ? bias[co] : 0.f);
+      float v = acc[r];
+      if (a.bias) v += a.bias[co];
+      if (a.init) v += a.init[co * iplane + (int64_t)row * W + col];
       if (RELU) v = v < 0.f ? 0.f : v;  // torch.relu keeps NaN
-      y[((int64_t)b * Cout + co) * plane + (int64_t)row * W + col] = v;
+      a.y[((int64_t)b * a.Cout + co) * oplane + (int64_t)(row - a.out_row0) * W + col] = v;
     }
   };
   emit(acc00, 0, 0);
   emit(acc01, 0, 1);
   emit(acc10, 1, 0);
   emit(acc11, 1, 1);
-#undef MVBEV_LOAD_CHUNK
-#undef MVBEV_STORE_CHUNK
 }
 
 template <int DIL>
 __global__ __launch_bounds__(256) void conv3x3_cout1_kernel(const float* __restrict__ x,
                                                             const float* __restrict__ w,
                                                             float* __restrict__ y, int C, int H,
-                                                            int W) {
+                                                            int W, int in_row0, int in_rows,
+                                                            int out_row0) {
   __shared__ float part[4][64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = blockIdx.x * 64 + lane;
-  const int row = blockIdx.y;
+  const int row = out_row0 + blockIdx.y;  // global output row
   const int b = blockIdx.z;
-  const int64_t plane = (int64_t)H * W;
+  const int64_t plane = (int64_t)in_rows * W;
   const float* xb = x + (int64_t)b * C * plane;
   bool okx[3];
 #pragma unroll
@@ -201,8 +233,9 @@ __global__ __launch_bounds__(256) void conv3x3_cout1_kernel(const float* __restr
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
       const int yy = row + (ky - 1) * DIL;
-      if (yy < 0 || yy >= H) continue;
-      const float* xr = xc + (int64_t)yy * W;
+      const int by = yy - in_row0;
+      if (yy < 0 || yy >= H || by < 0 || by >= in_rows) continue;
+      const float* xr = xc + (int64_t)by * W;
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         const int xx = col + (kx - 1) * DIL;
@@ -214,7 +247,7 @@ __global__ __launch_bounds__(256) void conv3x3_cout1_kernel(const float* __restr
   part[wave][lane] = acc;
   __syncthreads();
   if (wave == 0 && col < W) {
-    y[(int64_t)b * plane + (int64_t)row * W + col] =
+    y[((int64_t)b * gridDim.y + blockIdx.y) * W + col] =
         (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
   }
 }
@@ -223,44 +256,57 @@ __global__ __launch_bounds__(256) void conv3x3_cout1_kernel(const float* __restr
 
 extern "C" {
 
-size_t mvbev_conv3x3_packed_floats(int64_t Cout, int64_t Cin) {
-  if (Cout <= 0 || Cin <= 0) return 0;
-  return (size_t)mvbev::round_up(Cin, mvbev::KC) * 9 * (size_t)Cout;
+size_t mvbev_conv3x3_packed_floats(int64_t Cout, int64_t K) {
+  if (Cout <= 0 || K <= 0) return 0;
+  return (size_t)mvbev::round_up(K, mvbev::KC) * 9 * (size_t)Cout;
 }
 
-int mvbev_pack_conv3x3_weight_f32(const float* w, int64_t Cout, int64_t Cin, float* w_packed,
+int mvbev_pack_conv3x3_weight_f32(const float* w, int64_t Cout, int64_t Cin_w,
+                                  const int32_t* chan_map, int64_t K, float* w_packed,
                                   void* stream) {
   if (!w || !w_packed) return MVBEV_ERR_NULL;
-  if (Cout <= 0 || Cin <= 0) return MVBEV_ERR_RANK;
+  if (Cout <= 0 || Cin_w <= 0 || K <= 0) return MVBEV_ERR_RANK;
   if (Cout % mvbev::BN != 0) return MVBEV_ERR_SHAPE;
-  const int64_t cin_pad = mvbev::round_up(Cin, mvbev::KC);
-  const int64_t total = cin_pad * 9 * Cout;
+  if (!chan_map && K != Cin_w) return MVBEV_ERR_SHAPE;
+  const int64_t k_pad = mvbev::round_up(K, mvbev::KC);
+  const int64_t total = k_pad * 9 * Cout;
   const int blocks = (int)std::min<int64_t>(mvbev::ceil_div(total, 256), 8192);
   hipLaunchKernelGGL(mvbev::pack_conv3x3_kernel, dim3(blocks), dim3(256), 0,
-                     mvbev::as_stream(stream), w, w_packed, (int)Cout, (int)Cin, (int)cin_pad);
+                     mvbev::as_stream(stream), w, w_packed, (int)Cout, (int)Cin_w, chan_map,
+                     (int)K, (int)k_pad);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }
 
-int mvbev_conv3x3_f32(const float* x, int64_t B, int64_t Cin, int64_t H, int64_t W,
-                      const float* w_packed, const float* bias, int64_t Cout, int dilation,
-                      int relu, float* y, void* stream) {
+int mvbev_conv3x3_f32(const float* x, const mvbev_conv_desc* d, const float* w_packed,
+                      const float* bias, const float* init, int64_t Cout, int dilation, int relu,
+                      float* y, void* stream) {
   using namespace mvbev;
-  if (!x || !w_packed || !y) return MVBEV_ERR_NULL;
-  if (B <= 0 || Cin <= 0 || H <= 0 || W <= 0 || Cout <= 0) return MVBEV_ERR_RANK;
-  if (Cout % BN != 0) return MVBEV_ERR_SHAPE;
+  if (!x || !d || !w_packed || !y) return MVBEV_ERR_NULL;
+  if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || d->in_rows <= 0 ||
+      d->out_rows <= 0 || d->group <= 0)
+    return MVBEV_ERR_RANK;
+  if (Cout % BN != 0 || d->K % KC != 0 || d->group % KC != 0 || d->K % d->group != 0)
+    return MVBEV_ERR_SHAPE;
+  if (d->out_row0 < 0 || d->out_row0 + d->out_rows > d->H) return MVBEV_ERR_SHAPE;
+  if (d->in_rows * d->W * KC > (int64_t)INT32_MAX || d->H > INT32_MAX / 2 || d->W > INT32_MAX / 2)
+    return MVBEV_ERR_SHAPE;
   if ((reinterpret_cast<uintptr_t>(w_packed) & 15) != 0) return MVBEV_ERR_ALIGN;
-  const int64_t cin_pad = round_up(Cin, KC);
-  if (cin_pad * H * W > (int64_t)INT32_MAX) return MVBEV_ERR_SHAPE;  // per-image int offsets
-  const int tiles_x = (int)ceil_div(W, TW), tiles_y = (int)ceil_div(H, TH);
-  const int n_cot = (int)(Cout / BN);
-  const int64_t nwg = (int64_t)tiles_x * tiles_y * n_cot * B;
+  ConvArgs a;
+  a.x = x; a.wp = w_packed; a.bias = bias; a.init = init; a.y = y;
+  a.group_stride = d->group_stride; a.batch_stride = d->batch_stride;
+  a.group = (int)d->group; a.nchunks = (int)(d->K / KC); a.Cout = (int)Cout;
+  a.H = (int)d->H; a.W = (int)d->W;
+  a.in_row0 = (int)d->in_row0; a.in_rows = (int)d->in_rows;
+  a.out_row0 = (int)d->out_row0; a.out_rows = (int)d->out_rows;
+  a.tiles_x = (int)ceil_div(d->W, TW); a.tiles_y = (int)ceil_div(d->out_rows, TH);
+  a.n_cot = (int)(Cout / BN);
+  const int64_t nwg = (int64_t)a.tiles_x * a.tiles_y * a.n_cot * d->B;
   if (nwg > (int64_t)INT32_MAX) return MVBEV_ERR_SHAPE;
+  a.nwg = (int)nwg;
   hipStream_t s = as_stream(stream);
-#define MVBEV_CONV_LAUNCH(D, R)                                                                \
-  hipLaunchKernelGGL((conv3x3_mfma_f32_kernel<D, R>), dim3((unsigned)nwg), dim3(256), 0, s, x,   \
-                     w_packed, bias, y, (int)cin_pad, (int)Cout, (int)H, (int)W, tiles_x, tiles_y, \
-                     n_cot, (int)nwg)
+#define MVBEV_CONV_LAUNCH(D, R) \
+  hipLaunchKernelGGL((conv3x3_mfma_f32_kernel<D, R>), dim3((unsigned)nwg), dim3(256), 0, s, a)
   if (dilation == 1) {
     if (relu) MVBEV_CONV_LAUNCH(1, true); else MVBEV_CONV_LAUNCH(1, false);
   } else if (dilation == 2) {
@@ -274,19 +320,26 @@ int mvbev_conv3x3_f32(const float* x, int64_t B, int64_t Cin, int64_t H, int64_t
 }
 
 int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int64_t W,
+                            int64_t in_row0, int64_t in_rows, int64_t out_row0, int64_t out_rows,
                             const float* w, int dilation, float* y, void* stream) {
   using namespace mvbev;
   if (!x || !w || !y) return MVBEV_ERR_NULL;
-  if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return MVBEV_ERR_RANK;
-  if (H > 65535 || B > 65535) return MVBEV_ERR_SHAPE;
-  dim3 grid((unsigned)ceil_div(W, 64), (unsigned)H, (unsigned)B);
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || in_rows <= 0 || out_rows <= 0)
+    return MVBEV_ERR_RANK;
+  if (out_row0 < 0 || out_row0 + out_rows > H || out_rows > 65535 || B > 65535)
+    return MVBEV_ERR_SHAPE;
+  dim3 grid((unsigned)ceil_div(W, 64), (unsigned)out_rows, (unsigned)B);
   hipStream_t s = as_stream(stream);
+#define MVBEV_C1_LAUNCH(D)                                                                      \
+  hipLaunchKernelGGL(conv3x3_cout1_kernel<D>, grid, dim3(256), 0, s, x, w, y, (int)C, (int)H,    \
+                     (int)W, (int)in_row0, (int)in_rows, (int)out_row0)
   switch (dilation) {
-    case 1: hipLaunchKernelGGL(conv3x3_cout1_kernel<1>, grid, dim3(256), 0, s, x, w, y, (int)C, (int)H, (int)W); break;
-    case 2: hipLaunchKernelGGL(conv3x3_cout1_kernel<2>, grid, dim3(256), 0, s, x, w, y, (int)C, (int)H, (int)W); break;
-    case 4: hipLaunchKernelGGL(conv3x3_cout1_kernel<4>, grid, dim3(256), 0, s, x, w, y, (int)C, (int)H, (int)W); break;
+    case 1: MVBEV_C1_LAUNCH(1); break;
+    case 2: MVBEV_C1_LAUNCH(2); break;
+    case 4: MVBEV_C1_LAUNCH(4); break;
     default: return MVBEV_ERR_DILATION;
   }
+#undef MVBEV_C1_LAUNCH
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }

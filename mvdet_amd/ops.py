@@ -15,6 +15,7 @@ missing library or a bad argument raises.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -118,12 +119,19 @@ def padded_channels(cin: int) -> int:
 
 
 class PackedConv3x3:
-    """MFMA-layout copy of an ``nn.Conv2d`` 3x3 weight, re-packed only when the
-    parameter changes (keyed by ``(data_ptr, _version)``)."""
+    """MFMA-layout copy of an ``nn.Conv2d`` 3x3 weight (optionally with its input
+    channels permuted by ``chan_map``), re-packed only when the parameter changes
+    (keyed by ``(data_ptr, _version, shape)``)."""
 
-    def __init__(self):
+    def __init__(self, chan_map: Optional[Sequence[int]] = None):
         self._key = None
         self.packed: Optional[torch.Tensor] = None
+        self.chan_map = None if chan_map is None else [int(c) for c in chan_map]
+        self._map_dev: Optional[torch.Tensor] = None
+
+    @property
+    def K(self) -> Optional[int]:
+        return None if self.chan_map is None else len(self.chan_map)
 
     def get(self, weight: torch.Tensor) -> torch.Tensor:
         _require_cuda(weight)
@@ -135,54 +143,93 @@ class PackedConv3x3:
             if cout % BN:
                 raise ValueError(f"Cout={cout} must be a multiple of {BN}")
             lib = _native.load()
-            n = lib.mvbev_conv3x3_packed_floats(cout, cin)
+            K = cin if self.chan_map is None else len(self.chan_map)
+            if self.chan_map is not None and (self._map_dev is None or self._map_dev.device != weight.device):
+                self._map_dev = torch.tensor(self.chan_map, dtype=torch.int32, device=weight.device)
+            n = lib.mvbev_conv3x3_packed_floats(cout, K)
             packed = torch.empty(n, dtype=torch.float32, device=weight.device)
             w = weight.detach().contiguous()
-            _native.check(lib.mvbev_pack_conv3x3_weight_f32(w.data_ptr(), cout, cin, packed.data_ptr(),
-                                                            _stream(packed)), "mvbev_pack_conv3x3_weight_f32")
+            st = lib.mvbev_pack_conv3x3_weight_f32(w.data_ptr(), cout, cin,
+                                                   None if self._map_dev is None else self._map_dev.data_ptr(),
+                                                   K, packed.data_ptr(), _stream(packed))
+            _native.check(st, "mvbev_pack_conv3x3_weight_f32")
             self.packed, self._key = packed, key
         return self.packed
 
 
-def conv3x3(x: torch.Tensor, packed: torch.Tensor, cin: int, cout: int, bias: Optional[torch.Tensor],
-            dilation: int, relu: bool, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``relu?(conv2d(x[:, :cin], w, bias, padding=d, dilation=d))`` on fp32 MFMA.
+def conv_desc(B: int, K: int, H: int, W: int, group: int, group_stride: int, batch_stride: int,
+              in_row0: int = 0, in_rows: Optional[int] = None, out_row0: int = 0,
+              out_rows: Optional[int] = None) -> "_native.ConvDesc":
+    return _native.ConvDesc(B, K, H, W, group, group_stride, batch_stride, in_row0,
+                            H if in_rows is None else in_rows, out_row0, H if out_rows is None else out_rows)
 
-    ``x`` is [B, roundup(cin, 8), H, W] contiguous; channels >= cin must be finite.
-    """
+
+def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: Optional[torch.Tensor] = None,
+                 init: Optional[torch.Tensor] = None, dilation: int = 1, relu: bool = False,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Low-level form: ``x`` addressed through ``desc`` (``mvbev_conv_desc``)."""
     _require_cuda(x, packed)
-    if x.dim() != 4 or x.dtype != torch.float32 or not x.is_contiguous():
-        raise ValueError("x must be a contiguous float32 [B,Cin_pad,H,W] tensor")
-    B, cpad, H, W = x.shape
-    if cpad != padded_channels(cin):
-        raise ValueError(f"x has {cpad} channels, expected {padded_channels(cin)} for Cin={cin}")
+    if x.dtype != torch.float32:
+        raise TypeError("x must be float32")
+    B, H, W, out_rows = desc.B, desc.H, desc.W, desc.out_rows
+    need = (desc.K // desc.group - 1) * desc.group_stride + (B - 1) * desc.batch_stride + \
+        desc.group * desc.in_rows * W
+    if x.untyped_storage().nbytes() // 4 - x.storage_offset() < need:
+        raise ValueError("x's storage is too small for the conv descriptor")
     if out is None:
-        out = torch.empty((B, cout, H, W), dtype=torch.float32, device=x.device)
-    elif out.shape != (B, cout, H, W) or not out.is_contiguous():
-        raise ValueError("out must be a contiguous [B,Cout,H,W] tensor")
+        out = torch.empty((B, cout, out_rows, W), dtype=torch.float32, device=x.device)
+    elif tuple(out.shape) != (B, cout, out_rows, W) or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous [{B},{cout},{out_rows},{W}] tensor")
     if bias is not None:
         _require_cuda(bias)
         bias = bias.detach().contiguous()
-    st = _native.load().mvbev_conv3x3_f32(x.data_ptr(), B, cin, H, W, packed.data_ptr(),
-                                          bias.data_ptr() if bias is not None else None, cout,
-                                          int(dilation), int(bool(relu)), out.data_ptr(), _stream(x))
+    if init is not None:
+        _require_cuda(init)
+        if init.numel() != cout * H * W or not init.is_contiguous():
+            raise ValueError("init must be a contiguous [Cout,H,W] tensor")
+    st = _native.load().mvbev_conv3x3_f32(x.data_ptr(), ctypes.byref(desc), packed.data_ptr(),
+                                          bias.data_ptr() if bias is not None else None,
+                                          init.data_ptr() if init is not None else None, cout, int(dilation),
+                                          int(bool(relu)), out.data_ptr(), _stream(x))
     _native.check(st, "mvbev_conv3x3_f32")
     return out
 
 
-def conv3x3_cout1(x: torch.Tensor, weight: torch.Tensor, dilation: int,
+def conv3x3(x: torch.Tensor, packed: torch.Tensor, cout: int, bias: Optional[torch.Tensor] = None,
+            dilation: int = 1, relu: bool = False, init: Optional[torch.Tensor] = None,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``relu?(conv2d(x, w, bias, padding=d, dilation=d) [+ init])`` for a contiguous
+    [B, K, H, W] fp32 tensor (K = the packed channel count, a multiple of 8)."""
+    _require_cuda(x)
+    if x.dim() != 4 or not x.is_contiguous():
+        raise ValueError("x must be a contiguous [B,K,H,W] tensor")
+    B, K, H, W = x.shape
+    if K % KC:
+        raise ValueError(f"K={K} must be a multiple of {KC}")
+    d = conv_desc(B, K, H, W, group=K, group_stride=0, batch_stride=K * H * W)
+    return conv3x3_desc(x, d, packed, cout, bias, init, dilation, relu, out)
+
+
+def conv3x3_cout1(x: torch.Tensor, weight: torch.Tensor, dilation: int, H: Optional[int] = None,
+                  in_row0: int = 0, out_row0: int = 0, out_rows: Optional[int] = None,
                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``conv2d(x, weight[1,C,3,3], padding=d, dilation=d)`` (no bias) → [B,1,H,W]."""
+    """``conv2d(x, weight[1,C,3,3], padding=d, dilation=d)`` (no bias).
+
+    ``x`` [B,C,rows,W] holds global rows ``[in_row0, in_row0+rows)`` of an ``H``-row image
+    (default: the whole image); returns rows ``[out_row0, out_row0+out_rows)`` → [B,1,out_rows,W].
+    """
     _require_cuda(x, weight)
     if x.dim() != 4 or x.dtype != torch.float32 or not x.is_contiguous():
-        raise ValueError("x must be a contiguous float32 [B,C,H,W] tensor")
-    B, C, H, W = x.shape
+        raise ValueError("x must be a contiguous float32 [B,C,rows,W] tensor")
+    B, C, rows, W = x.shape
+    H = rows if H is None else H
+    out_rows = H - out_row0 if out_rows is None else out_rows
     if tuple(weight.shape) != (1, C, 3, 3):
         raise ValueError(f"weight must be [1,{C},3,3], got {tuple(weight.shape)}")
     w = weight.detach().contiguous()
     if out is None:
-        out = torch.empty((B, 1, H, W), dtype=torch.float32, device=x.device)
-    st = _native.load().mvbev_conv3x3_cout1_f32(x.data_ptr(), B, C, H, W, w.data_ptr(), int(dilation),
-                                                out.data_ptr(), _stream(x))
+        out = torch.empty((B, 1, out_rows, W), dtype=torch.float32, device=x.device)
+    st = _native.load().mvbev_conv3x3_cout1_f32(x.data_ptr(), B, C, H, W, in_row0, rows, out_row0, out_rows,
+                                                w.data_ptr(), int(dilation), out.data_ptr(), _stream(x))
     _native.check(st, "mvbev_conv3x3_cout1_f32")
     return out

@@ -1,94 +1,189 @@
 """The project+fuse hot path as one reusable engine.
 
-``ProjectFuse`` owns, per (device, batch size):
+Data layout in HBM (per device, per batch size B):
 
-* ``fused``  — the ground-plane tensor ``[B, Cin_pad, Ho, Wo]`` fp32, NCHW, the
-  concatenation of ``persp_trans_detector.py:77`` made zero-copy: view ``v``'s
-  warp writes channels ``[v*C, (v+1)*C)``, the coord map occupies channels
-  ``N*C`` and ``N*C+1`` (written once at allocation), channels up to
-  ``Cin_pad = roundup(N*C+2, 8)`` are zero padding for the MFMA K granule.
-* ``y1``, ``y2`` — conv1 / conv2 activations ``[B, 512, Ho, Wo]``.
-* the per-view kornia ``src_norm <- dst_norm`` matrices, uploaded once.
+* ``slab``  — the warped ground-plane features, **view-major**
+  ``[S, B, Cs, Ho, Wo]`` fp32 (S view slots, Cs = C rounded up to 8).  View ``v``'s
+  warp writes slot ``slot_of[v]`` directly; this *is* the concatenation of
+  ``persp_trans_detector.py:77`` (zero-copy).  View-major keeps each GPU's share
+  of the views contiguous, so the multi-GPU all-gather needs no repack
+  (``mvdet_amd.parallel``).
+* ``coord_term`` — ``[512, Ho, Wo]``: conv1's contribution of the two constant
+  coord channels (``:21,77``) plus conv1's bias.  It does not depend on the
+  input, so it is computed once per weight version (with the same conv kernel)
+  and enters conv1's epilogue as the ``init`` term instead of being read as two
+  more input channels every forward.
+* ``y1``, ``y2`` — conv1 / conv2 activations ``[B, 512, rows, Wo]`` (rows = the
+  output band plus the halo the next layer needs; the whole grid on one GPU).
 
-``warp_view`` is a5 for one view, ``fuse`` is a7-a9 (a10, the same-size
-bilinear interpolate of ``:82``, is an exact identity and is elided).  Nothing
-here allocates in steady state, copies to the host or synchronises.
+``warp_view`` is a5 for one view; ``fuse`` is a7-a9 (a10, the same-size bilinear
+interpolate of ``:82``, is an exact identity and is elided).  Nothing here
+allocates in steady state, copies to the host or synchronises.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
 from . import ops
 from .geometry import kornia_src_norm_from_dst_norm
 
+# halo rows each layer needs below/above its output rows (dilations 1, 2, 4 of :51-54)
+HALO_CONV1, HALO_CONV2, HALO_CONV3 = 1, 2, 4
+
+
+def band_rows(r0: int, r1: int, H: int):
+    """Row ranges (global, half-open) of y1, y2 needed for output rows [r0, r1)."""
+    y2 = (max(0, r0 - HALO_CONV3), min(H, r1 + HALO_CONV3))
+    y1 = (max(0, y2[0] - HALO_CONV2), min(H, y2[1] + HALO_CONV2))
+    return y1, y2
+
 
 @dataclass
 class Workspace:
-    fused: torch.Tensor
-    y1: torch.Tensor
-    y2: torch.Tensor
-    m_norm: torch.Tensor  # [N, B, 3, 3] device fp32
+    slab: torch.Tensor      # [S, B, Cs, Ho, Wo]
+    y1: torch.Tensor        # [B, 512, y1_rows, Wo]
+    y2: torch.Tensor        # [B, 512, y2_rows, Wo]
+    m_norm: torch.Tensor    # [N, B, 3, 3] device fp32
+    band: Tuple[int, int]   # output rows [r0, r1)
+    y1_rows: Tuple[int, int]
+    y2_rows: Tuple[int, int]
 
 
 class ProjectFuse:
+    """Warp + zero-copy concat + fusion head for ``num_cam`` views of ``channels``.
+
+    ``slot_views``: which view each slab slot holds (``None`` = empty slot); default
+    slot s = view s.  The multi-GPU path uses a rank-major slot order.
+    """
+
     def __init__(self, proj_mats: Sequence[torch.Tensor], src_hw: Tuple[int, int], grid_hw: Tuple[int, int],
-                 channels: int, mid_channels: int = 512):
+                 channels: int, mid_channels: int = 512, slot_views: Optional[Sequence[Optional[int]]] = None):
         self.num_cam = len(proj_mats)
         self.src_hw = (int(src_hw[0]), int(src_hw[1]))
         self.grid_hw = (int(grid_hw[0]), int(grid_hw[1]))
         self.C = int(channels)
+        self.Cs = ops.padded_channels(self.C)
         self.mid = int(mid_channels)
-        self.cin = self.num_cam * self.C + 2
-        self.cin_pad = ops.padded_channels(self.cin)
+        self.cin = self.num_cam * self.C + 2          # conv1 input channels of the module
+        self.slot_views = list(range(self.num_cam)) if slot_views is None else list(slot_views)
+        self.S = len(self.slot_views)
+        self.slot_of = {v: s for s, v in enumerate(self.slot_views) if v is not None}
+        assert sorted(self.slot_of) == list(range(self.num_cam)), "every view needs exactly one slot"
         # kornia steps 1-2 (normalize_homography + _torch_inverse_cast) on the host, fp32,
         # from the fp32-cast projection matrix exactly as :68-69 feeds kornia.
         self.m_norm_cpu = torch.stack([
             kornia_src_norm_from_dst_norm(M.float().reshape(1, 3, 3), self.src_hw, self.grid_hw)[0]
             for M in proj_mats])  # [N, 3, 3]
-        self._ws: Dict[Tuple[str, int], Workspace] = {}
-        self.pack1 = ops.PackedConv3x3()
+        # conv1 weight channels, in slab order: slot s channel c -> module channel v*C + c
+        chan_map = []
+        for v in self.slot_views:
+            for c in range(self.Cs):
+                chan_map.append(v * self.C + c if (v is not None and c < self.C) else -1)
+        nc = self.num_cam * self.C
+        self.pack1 = ops.PackedConv3x3(chan_map)
+        self.pack_coord = ops.PackedConv3x3([nc, nc + 1] + [-1] * (ops.KC - 2))
         self.pack2 = ops.PackedConv3x3()
+        self._ws: Dict[tuple, Workspace] = {}
+        self._coord_key = None
+        self._coord_term: Optional[torch.Tensor] = None
+        self._coord_in: Dict[str, torch.Tensor] = {}
 
-    def workspace(self, B: int, device) -> Workspace:
+    # -- buffers ----------------------------------------------------------------------------
+    def workspace(self, B: int, device, band: Optional[Tuple[int, int]] = None) -> Workspace:
         device = torch.device(device)
-        key = (str(device), int(B))
+        H, W = self.grid_hw
+        band = (0, H) if band is None else (int(band[0]), int(band[1]))
+        key = (str(device), int(B), band)
         ws = self._ws.get(key)
         if ws is None:
-            ho, wo = self.grid_hw
-            fused = torch.zeros((B, self.cin_pad, ho, wo), dtype=torch.float32, device=device)
-            nc = self.num_cam * self.C
-            ops.fill_coord_map(fused[:, nc:nc + 2])
-            y1 = torch.empty((B, self.mid, ho, wo), dtype=torch.float32, device=device)
-            y2 = torch.empty_like(y1)
+            slab = torch.zeros((self.S, B, self.Cs, H, W), dtype=torch.float32, device=device)
+            y1r, y2r = band_rows(band[0], band[1], H)
+            y1 = torch.empty((B, self.mid, y1r[1] - y1r[0], W), dtype=torch.float32, device=device)
+            y2 = torch.empty((B, self.mid, y2r[1] - y2r[0], W), dtype=torch.float32, device=device)
             m = self.m_norm_cpu.to(device)[:, None].expand(self.num_cam, B, 3, 3).contiguous()
-            ws = Workspace(fused, y1, y2, m)
+            ws = Workspace(slab, y1, y2, m, band, y1r, y2r)
             self._ws[key] = ws
         return ws
 
     def view_slice(self, ws: Workspace, cam: int) -> torch.Tensor:
-        return ws.fused[:, cam * self.C:(cam + 1) * self.C]
+        """[B, C, Ho, Wo] view of ``cam``'s warped features inside the slab."""
+        return ws.slab[self.slot_of[cam], :, :self.C]
 
+    # -- a5 -------------------------------------------------------------------------------
     def warp_view(self, ws: Workspace, cam: int, feat: torch.Tensor) -> None:
-        """a5 (+ zero-copy a6): warp one view's [B,C,h,w] features into ``fused``."""
+        """a5 (+ zero-copy a6): warp one view's [B,C,h,w] features into its slab slot."""
         if tuple(feat.shape[2:]) != self.src_hw or feat.shape[1] != self.C:
             raise ValueError(f"view {cam}: features {tuple(feat.shape)} do not match "
                              f"[B,{self.C},{self.src_hw[0]},{self.src_hw[1]}]")
         ops.warp_into(feat, ws.m_norm[cam], self.view_slice(ws, cam))
 
-    def fuse(self, ws: Workspace, map_classifier: torch.nn.Sequential) -> torch.Tensor:
-        """a7-a9 on ``ws.fused`` with the parameters of ``map_classifier`` → [B,1,Ho,Wo]."""
-        c1, c2, c3 = map_classifier[0], map_classifier[2], map_classifier[4]
-        p1 = self.pack1.get(c1.weight)
-        p2 = self.pack2.get(c2.weight)
-        ops.conv3x3(ws.fused, p1, self.cin, self.mid, c1.bias, dilation=1, relu=True, out=ws.y1)
-        ops.conv3x3(ws.y1, p2, self.mid, self.mid, c2.bias, dilation=2, relu=True, out=ws.y2)
-        return ops.conv3x3_cout1(ws.y2, c3.weight, dilation=4)
+    # -- coord term (a2 folded into conv1) --------------------------------------------------
+    def coord_term(self, conv1: torch.nn.Conv2d) -> torch.Tensor:
+        """[512, Ho, Wo]: bias + conv(coord channels) for the current conv1 parameters."""
+        w, b = conv1.weight, conv1.bias
+        key = (w.data_ptr(), w._version, None if b is None else (b.data_ptr(), b._version))
+        if key != self._coord_key:
+            H, W = self.grid_hw
+            dev = w.device
+            cin = self._coord_in.get(str(dev))
+            if cin is None:
+                cin = torch.zeros((1, ops.KC, H, W), dtype=torch.float32, device=dev)
+                ops.fill_coord_map(cin[:, :2])
+                self._coord_in[str(dev)] = cin
+            packed = self.pack_coord.get(w)
+            self._coord_term = ops.conv3x3(cin, packed, self.mid, bias=b, dilation=1, relu=False)[0]
+            self._coord_key = key
+        return self._coord_term
+
+    # -- a7-a9 ----------------------------------------------------------------------------
+    def conv1(self, ws: Workspace, conv1: torch.nn.Conv2d) -> torch.Tensor:
+        """a7: y1 = relu(conv3x3(slab) + coord_term) on y1's rows (fp32 MFMA)."""
+        if conv1.weight.shape[1] != self.cin:
+            raise ValueError(f"conv1 has {conv1.weight.shape[1]} input channels, expected {self.cin}")
+        H, W = self.grid_hw
+        B = ws.slab.shape[1]
+        init = self.coord_term(conv1)
+        p1 = self.pack1.get(conv1.weight)
+        a1, b1 = ws.y1_rows
+        d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * H * W,
+                           batch_stride=self.Cs * H * W, in_row0=0, in_rows=H, out_row0=a1, out_rows=b1 - a1)
+        return ops.conv3x3_desc(ws.slab, d1, p1, self.mid, bias=None, init=init, dilation=1, relu=True,
+                                out=ws.y1)
+
+    def conv2(self, ws: Workspace, conv2: torch.nn.Conv2d) -> torch.Tensor:
+        """a8: y2 = relu(conv3x3_d2(y1) + b2) on y2's rows."""
+        H, W = self.grid_hw
+        B = ws.slab.shape[1]
+        p2 = self.pack2.get(conv2.weight)
+        (a1, b1), (a2, b2) = ws.y1_rows, ws.y2_rows
+        d2 = ops.conv_desc(B, self.mid, H, W, group=self.mid, group_stride=0,
+                           batch_stride=self.mid * (b1 - a1) * W, in_row0=a1, in_rows=b1 - a1,
+                           out_row0=a2, out_rows=b2 - a2)
+        return ops.conv3x3_desc(ws.y1, d2, p2, self.mid, bias=conv2.bias, dilation=2, relu=True, out=ws.y2)
+
+    def conv3(self, ws: Workspace, conv3: torch.nn.Conv2d) -> torch.Tensor:
+        """a9: map = conv3x3_d4(y2) (Cout 1, no bias) on the output band → [B,1,rows,Wo]."""
+        H = self.grid_hw[0]
+        r0, r1 = ws.band
+        return ops.conv3x3_cout1(ws.y2, conv3.weight, 4, H=H, in_row0=ws.y2_rows[0], out_row0=r0,
+                                 out_rows=r1 - r0)
+
+    def fuse(self, ws: Workspace, map_classifier: torch.nn.Sequential, mark=None) -> torch.Tensor:
+        """a7-a9 on ``ws.slab`` for the output rows ``ws.band`` → [B, 1, rows, Wo].
+
+        ``mark(stage)`` (optional) is called right before each conv is enqueued
+        (``bench.py`` records HIP events there)."""
+        for stage, idx, fn in (("conv1", 0, self.conv1), ("conv2", 2, self.conv2), ("conv3", 4, self.conv3)):
+            if mark:
+                mark(stage)
+            out = fn(ws, map_classifier[idx])
+        return out
 
     def project_fuse(self, feats: Sequence[torch.Tensor], map_classifier) -> torch.Tensor:
-        """Whole hot path: warp every view, concat (zero-copy), fuse."""
+        """Whole hot path on one device: warp every view, concat (zero-copy), fuse."""
         B = feats[0].shape[0]
         ws = self.workspace(B, feats[0].device)
         for cam, f in enumerate(feats):

@@ -1,0 +1,105 @@
+"""Multi-process (gloo, CPU) tests of the view-parallel path's collective logic.
+
+The HIP kernels are exercised by the GPU tests; here the compute engine is the CPU
+oracle, so what is tested is exactly ``mvdet_amd.parallel``: view ownership, the
+rank-major slot order, the in-place all-gather of the slab, row bands and the
+assembly of the map bands — for uneven view splits (empty slots) and B > 1.
+"""
+import os
+import socket
+from types import SimpleNamespace
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mvdet_amd import parallel
+from oracle import cpu_path, fixtures, kornia_warp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class OracleEngine:
+    """CPU stand-in for ``pipeline.ProjectFuse`` built on the oracle (test only)."""
+
+    def __init__(self, proj_mats, src_hw, grid_hw, C, params, slot_views):
+        self.pm, self.src_hw, self.grid_hw, self.C, self.params = proj_mats, src_hw, grid_hw, C, params
+        self.slot_views = slot_views
+        self.slot_of = {v: s for s, v in enumerate(slot_views) if v is not None}
+
+    def workspace(self, B, device, band):
+        H, W = self.grid_hw
+        return SimpleNamespace(slab=torch.zeros(len(self.slot_views), B, self.C, H, W), band=band)
+
+    def warp_view(self, ws, v, feat):
+        B = feat.shape[0]
+        M = torch.as_tensor(np.asarray(self.pm[v])).reshape(1, 3, 3).repeat(B, 1, 1).float()
+        ws.slab[self.slot_of[v]] = kornia_warp.warp_perspective(feat, M, list(self.grid_hw))
+
+    def fuse(self, ws, mc, mark=None):
+        B = ws.slab.shape[1]
+        views = [ws.slab[self.slot_of[v]] for v in range(len(self.pm))]
+        fused = torch.cat(views + [cpu_path.coord_map(*self.grid_hw).repeat(B, 1, 1, 1)], 1)
+        full = cpu_path.fuse(fused, self.params)
+        return full[:, :, ws.band[0]:ws.band[1]]
+
+
+def _case():
+    from mvdet_amd.synthetic import wildtrack_like
+    ds = wildtrack_like(3, 4, seed=21, img_shape=(72, 128), worldgrid_shape=(52, 100))
+    from mvdet_amd.geometry import projection_matrices
+    pm = [M.numpy() for M in projection_matrices(ds)]
+    C, B = 8, 2
+    up = ds.upsample_shape
+    feats = [torch.from_numpy(fixtures.feature_input((B, C, *up), seed=300 + v)) for v in range(3)]
+    params = {k: torch.from_numpy(v) for k, v in fixtures.head_params(3, seed=5, C=C).items()}
+    return pm, tuple(up), tuple(ds.reducedgrid_shape), C, B, feats, params
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    pm, up, grid, C, B, feats, params = _case()
+    vp = parallel.ViewParallel(lambda sv: OracleEngine(pm, up, grid, C, params, sv), pm, grid, rank, world)
+    ws = vp.workspace(B, "cpu")
+    with torch.no_grad():
+        out = vp.step(ws, [feats[v] for v in vp.my_views], None)
+    torch.save({"out": out, "band": vp.band, "views": vp.my_views}, os.path.join(out_dir, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_view_parallel_matches_single_process_oracle(world, tmp_path):
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    pm, up, grid, C, B, feats, params = _case()
+    with torch.no_grad():
+        ref = cpu_path.project_fuse(feats, pm, grid, params)
+    bands = []
+    for r in range(world):
+        res = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
+        assert res["views"] == parallel.views_of(r, world, 3)
+        torch.testing.assert_close(res["out"], ref, rtol=1e-6, atol=1e-7)
+        bands.append(tuple(res["band"]))
+    assert bands[0][0] == 0 and bands[-1][1] == grid[0]
+    assert all(bands[i][1] == bands[i + 1][0] for i in range(world - 1))
+
+
+def test_slot_order_and_bands():
+    assert parallel.slot_views(2, 3) == [0, 2, 1, None]
+    assert parallel.slot_views(7, 7) == list(range(7))
+    assert parallel.slot_views(4, 7) == [0, 4, 1, 5, 2, 6, 3, None]
+    assert parallel.slot_views(8, 7) == list(range(7)) + [None]
+    assert [parallel.row_band(120, r, 8) for r in range(8)][-1] == (105, 120)
+    assert [parallel.row_band(160, r, 6) for r in range(6)][-1] == (135, 160)
+    assert parallel.row_band(5, 7, 8) == (5, 5)  # more ranks than rows: empty band
+    from mvdet_amd.pipeline import band_rows
+    assert band_rows(15, 30, 120) == ((9, 36), (11, 34))
+    assert band_rows(0, 15, 120) == ((0, 21), (0, 19))

@@ -113,11 +113,33 @@ def test_conv3x3_vs_torch(B, cin, H, W, d, relu, bias):
     ref = F.conv2d(x, w, b, padding=d, dilation=d)
     if relu:
         ref = F.relu(ref)
-    xp = torch.zeros(B, ops.padded_channels(cin), H, W)
+    K = ops.padded_channels(cin)
+    xp = torch.full((B, K, H, W), 1e30)  # padding channels must not leak (zero weights)
     xp[:, :cin] = x
-    pk = ops.PackedConv3x3().get(w.to(DEV))
-    got = ops.conv3x3(xp.to(DEV), pk, cin, cout, b.to(DEV) if bias else None, d, relu).cpu()
+    pk = ops.PackedConv3x3(list(range(cin)) + [-1] * (K - cin)).get(w.to(DEV))
+    got = ops.conv3x3(xp.to(DEV), pk, cout, b.to(DEV) if bias else None, d, relu).cpu()
     assert_parity(got, ref, "conv3x3", normwise_tol=2e-5)
+
+
+@pytest.mark.parametrize("d", [1, 2])
+def test_conv3x3_row_band_and_init(d):
+    """Row bands (the multi-GPU fusion) and the init (coord-term) epilogue."""
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(40 + d)
+    B, cin, H, W, cout = 2, 16, 23, 41, 128
+    x = torch.rand(B, cin, H, W, generator=g)
+    w = (torch.rand(cout, cin, 3, 3, generator=g) - 0.5) / 12
+    init = torch.rand(cout, H, W, generator=g)
+    ref = F.relu(F.conv2d(x, w, None, padding=d, dilation=d) + init)
+    pk = ops.PackedConv3x3().get(w.to(DEV))
+    xd, initd = x.to(DEV), init.to(DEV)
+    for (a, b_) in ((0, 7), (5, 19), (16, 23)):
+        in0, in1 = max(0, a - d), min(H, b_ + d)
+        xin = xd[:, :, in0:in1].contiguous()
+        desc = ops.conv_desc(B, cin, H, W, group=cin, group_stride=0, batch_stride=cin * (in1 - in0) * W,
+                             in_row0=in0, in_rows=in1 - in0, out_row0=a, out_rows=b_ - a)
+        got = ops.conv3x3_desc(xin, desc, pk, cout, init=initd, dilation=d, relu=True).cpu()
+        assert_parity(got, ref[:, :, a:b_], f"band {a}:{b_}", normwise_tol=2e-5)
 
 
 @pytest.mark.parametrize("C,H,W,d", [(512, 12, 36, 4), (7, 5, 70, 1), (33, 9, 130, 2)])
@@ -129,6 +151,14 @@ def test_conv3x3_cout1_vs_torch(C, H, W, d):
     ref = F.conv2d(x, w, None, padding=d, dilation=d)
     got = ops.conv3x3_cout1(x.to(DEV), w.to(DEV), d).cpu()
     assert_parity(got, ref, "cout1", normwise_tol=2e-5)
+    # band: rows [2, H-1) from an input buffer holding rows [1, H)
+    got_b = ops.conv3x3_cout1(x[:, :, 1:].contiguous().to(DEV), w.to(DEV), d, H=H, in_row0=1, out_row0=2,
+                              out_rows=H - 3).cpu()
+    sub = ref[:, :, 2:H - 1].clone()
+    if d >= 2:  # rows that need input row 0 differ (not in the buffer): compare the rest
+        keep = [r for r in range(2, H - 1) if r - d >= 1 or r - d < 0]
+        sub, got_b = sub[:, :, [r - 2 for r in keep]], got_b[:, :, [r - 2 for r in keep]]
+    assert_parity(got_b, sub, "cout1 band", normwise_tol=2e-5)
 
 
 def test_packed_weight_cache_tracks_in_place_updates():
@@ -174,16 +204,26 @@ def test_detector_forward_matches_reference_golden(name):
     assert map_res.shape == g["map_result"].shape
     assert_parity(map_res.cpu(), g["map_result"], f"{name} map_result")
     assert_parity(torch.stack(imgs_res, 0).cpu(), g["imgs_result"], f"{name} imgs_result")
-    ws = model.engine.workspace(m["B"], "cuda:0")
+    eng = model.engine
+    ws = eng.workspace(m["B"], "cuda:0")
     N, C = m["num_cam"], 512
-    warped = ws.fused[:, :N * C].reshape(m["B"], N, C, *m["reducedgrid_shape"]).double().sum(dim=(3, 4))
-    np.testing.assert_allclose(warped.cpu().numpy(), g["warp_out_chsum"], rtol=2e-3, atol=2e-2)
-    np.testing.assert_array_equal(ws.fused[:, N * C:N * C + 2].cpu().numpy(),
-                                  np.repeat(g["coord_map"], m["B"], 0))
+    warped = torch.stack([eng.view_slice(ws, v) for v in range(N)], 1)  # [B, N, C, ho, wo]
+    np.testing.assert_allclose(warped.double().sum(dim=(3, 4)).cpu().numpy(), g["warp_out_chsum"],
+                               rtol=2e-3, atol=2e-2)
     if "warp_out" in g:
-        assert_parity(ws.fused[:, :N * C].reshape(g["warp_out"].shape).cpu(), g["warp_out"], "warp_out")
+        assert_parity(warped.cpu(), g["warp_out"], "warp_out")
         assert_parity(ws.y1.cpu(), g["conv1_relu"], "conv1")
         assert_parity(ws.y2.cpu(), g["conv2_relu"], "conv2")
+
+
+def test_fill_coord_map_matches_reference_coord_map():
+    from mvdet_amd import ops
+    g = load_golden("module_mx3_b2")
+    ho, wo = g["meta"]["reducedgrid_shape"]
+    dst = torch.full((2, 5, ho, wo), 3.0, device=DEV)
+    ops.fill_coord_map(dst[:, 1:3])
+    np.testing.assert_array_equal(dst[:, 1:3].cpu().numpy(), np.repeat(g["coord_map"], 2, 0))
+    assert (dst[:, 0] == 3).all() and (dst[:, 3:] == 3).all()
 
 
 # ---------------------------------------------------------------------------------- full size

@@ -42,11 +42,19 @@ def test_argument_validation_codes():
     assert lib.mvbev_warp_perspective_f32(p, 0, 1, 1, 1, s4, p, p, 1, 1, s4, None) == -1
     bad = _native._i64x4(1, 1, 1, 2)
     assert lib.mvbev_warp_perspective_f32(p, 1, 1, 1, 1, s4, p, p, 1, 1, bad, None) == -3
-    assert lib.mvbev_conv3x3_f32(p, 1, 8, 4, 4, p, None, 100, 1, 1, p, None) == -2  # Cout % 128
-    assert lib.mvbev_conv3x3_f32(p, 1, 8, 4, 4, p, None, 128, 3, 1, p, None) == -6  # dilation 3
-    assert lib.mvbev_conv3x3_f32(p, 1, 8, 4, 4, ctypes.c_void_p(20), None, 128, 1, 1, p, None) == -4
-    assert lib.mvbev_conv3x3_cout1_f32(p, 1, 8, 4, 4, p, 3, p, None) == -6
-    assert lib.mvbev_pack_conv3x3_weight_f32(p, 100, 8, p, None) == -2
+    d = _native.ConvDesc(1, 8, 4, 4, 8, 0, 128, 0, 4, 0, 4)
+    assert lib.mvbev_conv3x3_f32(p, ctypes.byref(d), p, None, None, 100, 1, 1, p, None) == -2  # Cout % 128
+    assert lib.mvbev_conv3x3_f32(p, ctypes.byref(d), p, None, None, 128, 3, 1, p, None) == -6  # dilation 3
+    assert lib.mvbev_conv3x3_f32(p, ctypes.byref(d), ctypes.c_void_p(20), None, None, 128, 1, 1, p, None) == -4
+    bad = _native.ConvDesc(1, 12, 4, 4, 12, 0, 192, 0, 4, 0, 4)  # K not a multiple of 8
+    assert lib.mvbev_conv3x3_f32(p, ctypes.byref(bad), p, None, None, 128, 1, 1, p, None) == -2
+    band = _native.ConvDesc(1, 8, 4, 4, 8, 0, 128, 0, 4, 2, 3)  # out rows 2..5 > H
+    assert lib.mvbev_conv3x3_f32(p, ctypes.byref(band), p, None, None, 128, 1, 1, p, None) == -2
+    assert lib.mvbev_conv3x3_f32(p, None, p, None, None, 128, 1, 1, p, None) == -5
+    assert lib.mvbev_conv3x3_cout1_f32(p, 1, 8, 4, 4, 0, 4, 0, 4, p, 3, p, None) == -6
+    assert lib.mvbev_conv3x3_cout1_f32(p, 1, 8, 4, 4, 0, 4, 3, 4, p, 4, p, None) == -2
+    assert lib.mvbev_pack_conv3x3_weight_f32(p, 100, 8, None, 8, p, None) == -2
+    assert lib.mvbev_pack_conv3x3_weight_f32(p, 128, 8, None, 16, p, None) == -2  # K != Cin without a map
     assert lib.mvbev_conv3x3_packed_floats(512, 3586) == 3592 * 9 * 512
     assert lib.mvbev_fill_coord_map_f32(None, 1, 2, 2, s4, None) == -5
 

@@ -20,7 +20,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 
 from bench import build_mc, head_params  # noqa: E402
-from mvdet_amd import ProjectFuse, ops, synthetic  # noqa: E402
+from mvdet_amd import ProjectFuse, synthetic  # noqa: E402
 from mvdet_amd.geometry import projection_matrices  # noqa: E402
 
 
@@ -55,18 +55,15 @@ def main():
     eng = ProjectFuse(pm, up, (ho, wo), C)
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=v, device=dev) for v in range(N)]
     ws = eng.workspace(B, dev)
-    p1, p2 = eng.pack1.get(mc[0].weight), eng.pack2.get(mc[2].weight)
     with torch.no_grad():
         for v in range(N):
             eng.warp_view(ws, v, feats[v])
+        eng.fuse(ws, mc)
         stages = {
-            "warp": (lambda: [eng.warp_view(ws, v, feats[v]) for v in range(N)],
-                     None),
-            "conv1": (lambda: ops.conv3x3(ws.fused, p1, eng.cin, 512, mc[0].bias, 1, True, out=ws.y1),
-                      2.0 * B * ho * wo * 9 * eng.cin * 512),
-            "conv2": (lambda: ops.conv3x3(ws.y1, p2, 512, 512, mc[2].bias, 2, True, out=ws.y2),
-                      2.0 * B * ho * wo * 9 * 512 * 512),
-            "conv3": (lambda: ops.conv3x3_cout1(ws.y2, mc[4].weight, 4), None),
+            "warp": (lambda: [eng.warp_view(ws, v, feats[v]) for v in range(N)], None),
+            "conv1": (lambda: eng.conv1(ws, mc[0]), 2.0 * B * ho * wo * 9 * N * C * 512),
+            "conv2": (lambda: eng.conv2(ws, mc[2]), 2.0 * B * ho * wo * 9 * 512 * 512),
+            "conv3": (lambda: eng.conv3(ws, mc[4]), None),
         }
         for name in args.only.split(","):
             fn, flop = stages[name]

@@ -170,7 +170,7 @@ def bench_main(args) -> None:
         torch.cuda.synchronize()
         dist.barrier()
         dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    t = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     nxt = {stages[i]: stages[i + 1] for i in range(len(stages) - 1)}

@@ -116,6 +116,7 @@ def main():
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * args.config + v,
                                           device=dev) for v in range(N)]
     ws = eng.workspace(B, dev)
+    views = list(range(N))
 
     K, W = args.steps, args.warmup
     ev = {k: [torch.cuda.Event(enable_timing=True) for _ in range(K)] for k in ("warp", "conv1", "conv2", "conv3")}
@@ -123,8 +124,7 @@ def main():
     def step(i=None):
         if i is not None:
             ev["warp"][i].record()
-        for v in range(N):
-            eng.warp_view(ws, v, feats[v])
+        eng.warp_views(ws, views, feats)
         mark = (lambda stage: ev[stage][i].record()) if i is not None else None
         return eng.fuse(ws, mc, mark=mark)
 

@@ -82,6 +82,23 @@ int mvbev_warp_perspective_f16(const void* src, int64_t B, int64_t C, int64_t H,
                                void* dst, int64_t Ho, int64_t Wo, const int64_t dst_strides[4],
                                void* stream);
 
+/* One view of a batched warp: all views share B, C, H, W, Ho, Wo. */
+typedef struct mvbev_warp_view {
+  const void* src;           /* [B][C][H][W] device, element strides src_strides */
+  int64_t src_strides[4];
+  void* dst;                 /* [B][C][Ho][Wo] device view, element strides dst_strides ([3] == 1) */
+  int64_t dst_strides[4];
+  float m[9];                /* src_norm <- dst_norm (row-major), same for every batch item */
+} mvbev_warp_view;
+
+/* Warp every view of a frame in ONE launch (the detector's per-camera loop at
+ * persp_trans_detector.py:62-75, warp + concat).  views: host array of nviews (<= 16). */
+int mvbev_warp_views_f32(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
+                         int64_t H, int64_t W, int64_t Ho, int64_t Wo, void* stream);
+/* fp16 storage for src and dst, fp32 math. */
+int mvbev_warp_views_f16(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
+                         int64_t H, int64_t W, int64_t Ho, int64_t Wo, void* stream);
+
 /* Coord-map channels: dst[b][0][v][u] = u/(Wo-1)*2-1, dst[b][1][v][u] = v/(Ho-1)*2-1
  * (computed in float64, rounded to fp32 as numpy->torch does at :106-107). */
 int mvbev_fill_coord_map_f32(float* dst, int64_t B, int64_t Ho, int64_t Wo,

@@ -18,6 +18,8 @@ EXPORTS = (
     "mvbev_version",
     "mvbev_warp_perspective_f32",
     "mvbev_warp_perspective_f16",
+    "mvbev_warp_views_f32",
+    "mvbev_warp_views_f16",
     "mvbev_fill_coord_map_f32",
     "mvbev_conv3x3_packed_floats",
     "mvbev_pack_conv3x3_weight_f32",
@@ -41,6 +43,12 @@ class ConvDesc(ctypes.Structure):
                                                "in_row0", "in_rows", "out_row0", "out_rows")]
 
 
+class WarpView(ctypes.Structure):
+    """``mvbev_warp_view`` (include/mvbev.h)."""
+    _fields_ = [("src", ctypes.c_void_p), ("src_strides", ctypes.c_int64 * 4), ("dst", ctypes.c_void_p),
+                ("dst_strides", ctypes.c_int64 * 4), ("m", ctypes.c_float * 9)]
+
+
 class NativeError(RuntimeError):
     pass
 
@@ -54,6 +62,10 @@ def _declare(lib):
         fn = getattr(lib, name)
         fn.restype = ctypes.c_int
         fn.argtypes = [_p, _i64, _i64, _i64, _i64, _i64x4, _p, _p, _i64, _i64, _i64x4, _p]
+    for name in ("mvbev_warp_views_f32", "mvbev_warp_views_f16"):
+        fn = getattr(lib, name)
+        fn.restype = ctypes.c_int
+        fn.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64, _i64, _p]
     lib.mvbev_fill_coord_map_f32.restype = ctypes.c_int
     lib.mvbev_fill_coord_map_f32.argtypes = [_p, _i64, _i64, _i64, _i64x4, _p]
     lib.mvbev_conv3x3_packed_floats.restype = ctypes.c_size_t
@@ -73,7 +85,8 @@ def load(path: os.PathLike | str | None = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    # MVBEV_LIB overrides the library path (A/B runs of experimental builds)
+    p = Path(path) if path else Path(os.environ.get("MVBEV_LIB", LIB_PATH))
     if not p.exists():
         raise NativeError(
             f"libmvbev.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "

@@ -42,7 +42,6 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));  // native vector (HI
 
 constexpr int KC = MVBEV_CONV_KC;  // input channels per staged chunk
 constexpr int BN = MVBEV_CONV_BN;  // output channels per workgroup
-constexpr int TH = 4;              // output rows per workgroup
 constexpr int TW = 32;             // output cols per workgroup (= MFMA N)
 
 // packed[chunk][cotile][tap][kk][col] = w[cotile*BN+col][map(chunk*KC+kk)][tap]
@@ -80,17 +79,37 @@ struct ConvArgs {
   int tiles_x, tiles_y, n_cot, nwg;
 };
 
-template <int DIL, bool RELU>
-__global__ __launch_bounds__(256, 2) void conv3x3_mfma_f32_kernel(const ConvArgs a) {
-  constexpr int XH = TH + 2 * DIL, XW = TW + 2 * DIL;
-  constexpr int XS = KC * XH * XW;  // input halo floats per chunk
-  constexpr int WS = 9 * KC * BN;   // weight floats per chunk
-  constexpr int WLD = WS / 4 / 256; // float4 weight loads per thread
-  constexpr int XLD = (XS + 255) / 256;
-  static_assert(WS % 1024 == 0, "weight slab must split evenly over 256 threads");
-  __shared__ __attribute__((aligned(16))) float lds[WS + XS];
-  float* Ws = lds;
-  float* Xs = lds + WS;
+#ifndef MVBEV_CONV_MINWAVES
+#define MVBEV_CONV_MINWAVES 2  // waves per SIMD the register budget must allow
+#endif
+#ifndef MVBEV_CONV_WAVES
+#define MVBEV_CONV_WAVES 4     // waves per workgroup: 4 (2 WGs/CU, single LDS buffer) or 8 (1 WG/CU)
+#endif
+#ifndef MVBEV_CONV_DBUF
+#define MVBEV_CONV_DBUF 0      // double-buffered LDS, one barrier per K chunk
+#endif
+
+// Tile geometry: each wave owns 2 output rows x 64 output channels (2x2 MFMA 32x32 tiles);
+// NWAVES/2 row pairs x 2 channel halves per workgroup -> TH = NWAVES rows.
+template <int NWAVES> struct TileCfg {
+  static constexpr int NT = 64 * NWAVES;
+  static constexpr int TH = NWAVES;
+};
+
+template <int DIL, bool RELU, int NWAVES, bool DBUF>
+__global__ __launch_bounds__(64 * NWAVES, MVBEV_CONV_MINWAVES) void conv3x3_mfma_f32_kernel(
+    const ConvArgs a) {
+  constexpr int NT = TileCfg<NWAVES>::NT;
+  constexpr int TH_ = TileCfg<NWAVES>::TH;
+  constexpr int XH = TH_ + 2 * DIL, XW = TW + 2 * DIL;
+  constexpr int XS = KC * XH * XW;        // input halo floats per chunk
+  constexpr int WS = 9 * KC * BN;         // weight floats per chunk
+  constexpr int WS4 = WS / 4;             // float4 elements of the weight slab
+  constexpr int WLD = (WS4 + NT - 1) / NT;
+  constexpr int XLD = (XS + NT - 1) / NT;
+  constexpr int NBUF = DBUF ? 2 : 1;
+  constexpr int BUF = WS + ((XS + 3) / 4) * 4;  // floats per LDS buffer (16-B aligned parts)
+  __shared__ __attribute__((aligned(16))) float lds[NBUF * BUF];
 
   const int wg = xcd_remap(blockIdx.x, a.nwg);
   const int cot = wg % a.n_cot;
@@ -100,15 +119,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_f32_kernel(const ConvArgs
   const int ty = rest % a.tiles_y;
   const int b = rest / a.tiles_y;
   const int x0 = tx * TW;
-  const int y0 = a.out_row0 + ty * TH;  // global output row of the tile's first row
+  const int y0 = a.out_row0 + ty * TH_;  // global output row of the tile's first row
   const int W = a.W;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, kh = lane >> 5;
 
   const int64_t plane = (int64_t)a.in_rows * W;
   const float* xb = a.x + (int64_t)b * a.batch_stride;
-  const floatx4* wsrc = reinterpret_cast<const floatx4*>(a.wp) + (int64_t)cot * (WS / 4);
-  const int64_t wchunk = (int64_t)a.n_cot * (WS / 4);
+  const floatx4* wsrc = reinterpret_cast<const floatx4*>(a.wp) + (int64_t)cot * WS4;
+  const int64_t wchunk = (int64_t)a.n_cot * WS4;
   const int chunks_per_group = a.group / KC;
 
   // Per-thread halo element coordinates are chunk-invariant: precompute offsets/validity.
@@ -116,7 +135,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_f32_kernel(const ConvArgs
   bool xok[XLD];
 #pragma unroll
   for (int i = 0; i < XLD; ++i) {
-    const int e = tid + 256 * i;
+    const int e = tid + NT * i;
     const int kk = e / (XH * XW);
     const int r = (e / XW) % XH;
     const int c = e % XW;
@@ -132,32 +151,33 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_f32_kernel(const ConvArgs
 #define MVBEV_LOAD_CHUNK(ch)                                                                  \
   do {                                                                                        \
     const floatx4* ws_ = wsrc + (int64_t)(ch) * wchunk;                                       \
-    _Pragma("unroll") for (int i = 0; i < WLD; ++i) wreg[i] = ws_[tid + 256 * i];             \
+    _Pragma("unroll") for (int i = 0; i < WLD; ++i) {                                         \
+      if (WS4 % NT == 0 || tid + NT * i < WS4) wreg[i] = ws_[tid + NT * i];                   \
+    }                                                                                         \
     const int g_ = (ch) / chunks_per_group;                                                   \
     const float* xc_ =                                                                        \
         xb + g_ * a.group_stride + (int64_t)((ch) - g_ * chunks_per_group) * KC * plane;      \
     _Pragma("unroll") for (int i = 0; i < XLD; ++i) xreg[i] = xc_[xoff[i]]; /* select at store */ \
   } while (0)
-#define MVBEV_STORE_CHUNK()                                                                   \
+#define MVBEV_STORE_CHUNK(buf)                                                                \
   do {                                                                                        \
-    _Pragma("unroll") for (int i = 0; i < WLD; ++i)                                           \
-        reinterpret_cast<floatx4*>(Ws)[tid + 256 * i] = wreg[i];                              \
+    float* Wd_ = lds + (buf) * BUF;                                                           \
+    float* Xd_ = Wd_ + WS;                                                                    \
+    _Pragma("unroll") for (int i = 0; i < WLD; ++i) {                                         \
+      if (WS4 % NT == 0 || tid + NT * i < WS4)                                                \
+        reinterpret_cast<floatx4*>(Wd_)[tid + NT * i] = wreg[i];                              \
+    }                                                                                         \
     _Pragma("unroll") for (int i = 0; i < XLD; ++i) {                                         \
-      const int e = tid + 256 * i;                                                            \
-      if (XS % 256 == 0 || e < XS) Xs[e] = xok[i] ? xreg[i] : 0.f;                            \
+      const int e = tid + NT * i;                                                             \
+      if (XS % NT == 0 || e < XS) Xd_[e] = xok[i] ? xreg[i] : 0.f;                            \
     }                                                                                         \
   } while (0)
 
   floatx16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
-  const int prow = 2 * (wave & 1);  // this wave's two output rows within the tile
-  const int cw = 64 * (wave >> 1);  // this wave's 64 output channels within BN
+  const int prow = 2 * (wave % (NWAVES / 2));  // this wave's two output rows within the tile
+  const int cw = 64 * (wave / (NWAVES / 2));   // this wave's 64 output channels within BN
 
-  MVBEV_LOAD_CHUNK(0);
-  for (int ch = 0; ch < a.nchunks; ++ch) {
-    __syncthreads();
-    MVBEV_STORE_CHUNK();
-    __syncthreads();
-    if (ch + 1 < a.nchunks) MVBEV_LOAD_CHUNK(ch + 1);
+  auto compute = [&](const float* Ws, const float* Xs) __attribute__((always_inline)) {
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
 #pragma unroll
@@ -178,6 +198,30 @@ __global__ __launch_bounds__(256, 2) void conv3x3_mfma_f32_kernel(const ConvArgs
           acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc11, 0, 0, 0);
         }
       }
+    }
+  };
+
+  MVBEV_LOAD_CHUNK(0);
+  if constexpr (DBUF) {
+    // Double buffer: chunk ch+1 is loaded to registers before the MFMAs of chunk ch and
+    // stored to the other buffer right after them; one barrier per chunk.
+    MVBEV_STORE_CHUNK(0);
+    __syncthreads();
+    for (int ch = 0; ch < a.nchunks; ++ch) {
+      const int cur = ch & 1;
+      const bool more = ch + 1 < a.nchunks;
+      if (more) MVBEV_LOAD_CHUNK(ch + 1);
+      compute(lds + cur * BUF, lds + cur * BUF + WS);
+      if (more) MVBEV_STORE_CHUNK(cur ^ 1);
+      __syncthreads();
+    }
+  } else {
+    for (int ch = 0; ch < a.nchunks; ++ch) {
+      __syncthreads();
+      MVBEV_STORE_CHUNK(0);
+      __syncthreads();
+      if (ch + 1 < a.nchunks) MVBEV_LOAD_CHUNK(ch + 1);
+      compute(lds, lds + WS);
     }
   }
 #undef MVBEV_LOAD_CHUNK
@@ -299,14 +343,18 @@ int mvbev_conv3x3_f32(const float* x, const mvbev_conv_desc* d, const float* w_p
   a.H = (int)d->H; a.W = (int)d->W;
   a.in_row0 = (int)d->in_row0; a.in_rows = (int)d->in_rows;
   a.out_row0 = (int)d->out_row0; a.out_rows = (int)d->out_rows;
-  a.tiles_x = (int)ceil_div(d->W, TW); a.tiles_y = (int)ceil_div(d->out_rows, TH);
+  constexpr int kWaves = MVBEV_CONV_WAVES;
+  constexpr bool kDbuf = MVBEV_CONV_DBUF != 0;
+  a.tiles_x = (int)ceil_div(d->W, TW);
+  a.tiles_y = (int)ceil_div(d->out_rows, TileCfg<kWaves>::TH);
   a.n_cot = (int)(Cout / BN);
   const int64_t nwg = (int64_t)a.tiles_x * a.tiles_y * a.n_cot * d->B;
   if (nwg > (int64_t)INT32_MAX) return MVBEV_ERR_SHAPE;
   a.nwg = (int)nwg;
   hipStream_t s = as_stream(stream);
-#define MVBEV_CONV_LAUNCH(D, R) \
-  hipLaunchKernelGGL((conv3x3_mfma_f32_kernel<D, R>), dim3((unsigned)nwg), dim3(256), 0, s, a)
+#define MVBEV_CONV_LAUNCH(D, R)                                                           \
+  hipLaunchKernelGGL((conv3x3_mfma_f32_kernel<D, R, kWaves, kDbuf>), dim3((unsigned)nwg), \
+                     dim3(TileCfg<kWaves>::NT), 0, s, a)
   if (dilation == 1) {
     if (relu) MVBEV_CONV_LAUNCH(1, true); else MVBEV_CONV_LAUNCH(1, false);
   } else if (dilation == 2) {

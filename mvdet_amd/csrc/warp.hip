@@ -2,45 +2,77 @@
 //
 // Replaces kornia.geometry.transform.warp_perspective at
 // multiview_detector/models/persp_trans_detector.py:69 and, through the dst
-// strides, the torch.cat at :77 (each view writes straight into its channel slice
-// of the fused ground-plane tensor).
+// strides, the torch.cat at :77 (each view writes straight into its slot of the fused
+// ground-plane slab).
 //
-// Per output pixel (u = col, v = row) of batch b:
+// Per output pixel (u = col, v = row) of batch item b:
 //   g   = kornia create_meshgrid (normalised):  gx = (u/(Wo-1) - 0.5)*2, gy likewise
-//   p   = M_b @ [gx, gy, 1]            (M_b = src_norm <- dst_norm, fp32, from the host)
+//   p   = M @ [gx, gy, 1]            (M = src_norm <- dst_norm, fp32, computed on the host)
 //   s   = |p.z| > 1e-8 ? 1/(p.z + 1e-8) : 1;  (x, y) = s * (p.x, p.y)   (no z>0 mask)
 //   ix  = ((x+1)/2)*(W-1), iy = ((y+1)/2)*(H-1)          (GridSampler.h:31, align_corners)
-//   out = sum over the 4 in-bounds corners of src * bilinear weight    (zeros padding)
+//   out = sum over the 4 in-bounds corners of src * bilinear weight    (zeros padding;
+//         a non-finite ix/iy gives NaN in every channel, like torch's CPU grid_sample)
 //
-// Kernel shape: one thread per output pixel; the pixel's coordinates, corner offsets and
-// weights are computed once and reused across the block's channel slice (the dominant
-// traffic is the C-deep gather + the C-deep store, both per channel plane).  Stores are
-// fully coalesced along u; loads follow the projected source line of the 64 lanes.
+// Kernel shape (HBM-bound gather): a block is a 2-D output tile of 8 rows x 32 columns
+// (one thread per pixel, each wave = 2 rows x 32 columns: 128-B coalesced stores) and a
+// slice of 64 channels.  The pixel's transform, corner offsets and weights are computed
+// once and reused over the channel slice; 4 channels x 4 corners of loads are in flight
+// per thread.  The compact 2-D tile keeps each source footprint inside one block (the
+// corners of neighbouring pixels share 128-B lines in L1/L2) instead of being re-fetched
+// by the blocks of neighbouring output rows on other XCDs.  One launch covers every view
+// of a frame (grid.z = batch x view) so the 7-view warp is a single dispatch.
 #include "common.h"
 
 namespace mvbev {
 
-template <typename T, int UNROLL>
-__global__ __launch_bounds__(256) void warp_perspective_kernel(
-    const T* __restrict__ src, int64_t sB, int64_t sC, int64_t sH, int64_t sW, int C, int H, int W,
-    const float* __restrict__ m, T* __restrict__ dst, int64_t dB, int64_t dC, int64_t dH, int Ho,
-    int Wo, int c_per_block) {
-  const int b = blockIdx.z;
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= Ho * Wo) return;
-  const int v = p / Wo;
-  const int u = p - v * Wo;
-  const int c_begin = blockIdx.y * c_per_block;
-  const int c_end = min(C, c_begin + c_per_block);
+constexpr int kWarpTH = 8;       // output rows per block
+constexpr int kWarpTW = 32;      // output cols per block
+constexpr int kWarpCPB = 64;     // channels per block
+constexpr int kWarpMaxViews = 16;
 
+struct WarpView {
+  const void* src;
+  int64_t sB, sC, sH, sW;
+  void* dst;
+  int64_t dB, dC, dH;
+  const float* m_dev;  // device [B][9] (per batch item) or nullptr -> m below
+  float m[9];          // src_norm <- dst_norm, shared by every batch item
+};
+
+struct WarpArgs {
+  WarpView v[kWarpMaxViews];
+  int nviews, B, C, H, W, Ho, Wo, tiles_x;
+};
+
+template <typename T, int UNROLL>
+__global__ __launch_bounds__(256) void warp_tile_kernel(const WarpArgs a) {
+  const int view = blockIdx.z % a.nviews;
+  const int b = blockIdx.z / a.nviews;
+  const WarpView& vw = a.v[view];
+  const int tile = blockIdx.x;
+  const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
+  const int v = ty * kWarpTH + (threadIdx.x >> 5);
+  const int u = tx * kWarpTW + (threadIdx.x & 31);
+  if (v >= a.Ho || u >= a.Wo) return;
+  const int c_begin = blockIdx.y * kWarpCPB;
+  const int c_end = min(a.C, c_begin + kWarpCPB);
+  const int H = a.H, W = a.W;
+
+  float m[9];
+  if (vw.m_dev) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) m[i] = vw.m_dev[9 * b + i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) m[i] = vw.m[i];
+  }
   // kornia create_meshgrid(normalized_coordinates=True); same fp32 op order.
-  const float gx = ((float)u / (float)(Wo - 1) - 0.5f) * 2.0f;
-  const float gy = ((float)v / (float)(Ho - 1) - 0.5f) * 2.0f;
-  const float* mb = m + 9 * b;
+  const float gx = ((float)u / (float)(a.Wo - 1) - 0.5f) * 2.0f;
+  const float gy = ((float)v / (float)(a.Ho - 1) - 0.5f) * 2.0f;
   // transform_points: [gx gy 1] @ M^T, then convert_points_from_homogeneous(eps=1e-8)
-  float x = gx * mb[0] + gy * mb[1] + mb[2];
-  float y = gx * mb[3] + gy * mb[4] + mb[5];
-  const float z = gx * mb[6] + gy * mb[7] + mb[8];
+  float x = gx * m[0] + gy * m[1] + m[2];
+  float y = gx * m[3] + gy * m[4] + m[5];
+  const float z = gx * m[6] + gy * m[7] + m[8];
   const float scale = fabsf(z) > 1e-8f ? 1.0f / (z + 1e-8f) : 1.0f;
   x = scale * x;
   y = scale * y;
@@ -48,10 +80,8 @@ __global__ __launch_bounds__(256) void warp_perspective_kernel(
   const float ix = ((x + 1.f) / 2.f) * (float)(W - 1);
   const float iy = ((y + 1.f) / 2.f) * (float)(H - 1);
 
-  T* out = dst + (int64_t)b * dB + (int64_t)v * dH + u;
-  // Non-finite sample position (kornia's 0/0 meshgrid when Ho or Wo is 1, or an inf
-  // after the divide): torch's bilinear weights become NaN, so every channel is NaN.
-  // Otherwise, no corner in bounds -> zeros padding.
+  T* out = static_cast<T*>(vw.dst) + (int64_t)b * vw.dB + (int64_t)v * vw.dH + u;
+  const int64_t dC = vw.dC;
   const bool finite = isfinite(ix) && isfinite(iy);
   if (!finite || !(ix > -1.f && ix < (float)W && iy > -1.f && iy < (float)H)) {
     const float fill = finite ? 0.f : __builtin_nanf("");
@@ -68,14 +98,15 @@ __global__ __launch_bounds__(256) void warp_perspective_kernel(
   const float w_se = (ix - fx0) * (iy - fy0);
   const bool vx0 = x0 >= 0, vx1 = x0 + 1 <= W - 1, vy0 = y0 >= 0, vy1 = y0 + 1 <= H - 1;
   const bool ok_nw = vx0 && vy0, ok_ne = vx1 && vy0, ok_sw = vx0 && vy1, ok_se = vx1 && vy1;
-  // Offsets of the 4 corners; invalid corners point at a safe in-bounds pixel and
-  // their value is replaced by 0 (select, not multiply: keeps inf/NaN semantics).
+  // Invalid corners read a safe in-bounds pixel and are replaced by 0 (select, not a
+  // multiply by a zero weight: keeps inf/NaN semantics of the reference).
   const int cx0 = max(x0, 0), cy0 = max(y0, 0);
   const int cx1 = min(x0 + 1, W - 1), cy1 = min(y0 + 1, H - 1);
+  const int64_t sH = vw.sH, sW = vw.sW, sC = vw.sC;
   const int64_t o_nw = cy0 * sH + cx0 * sW, o_ne = cy0 * sH + cx1 * sW;
   const int64_t o_sw = cy1 * sH + cx0 * sW, o_se = cy1 * sH + cx1 * sW;
 
-  const T* base = src + (int64_t)b * sB;
+  const T* base = static_cast<const T*>(vw.src) + (int64_t)b * vw.sB;
   int c = c_begin;
   for (; c + UNROLL <= c_end; c += UNROLL) {
     float vnw[UNROLL], vne[UNROLL], vsw[UNROLL], vse[UNROLL];
@@ -109,21 +140,59 @@ __global__ __launch_bounds__(256) void warp_perspective_kernel(
 }
 
 template <typename T>
-static int launch_warp(const T* src, int64_t B, int64_t C, int64_t H, int64_t W,
-                       const int64_t* ss, const float* m, T* dst, int64_t Ho, int64_t Wo,
-                       const int64_t* ds, void* stream) {
-  if (!src || !m || !dst || !ss || !ds) return MVBEV_ERR_NULL;
-  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0) return MVBEV_ERR_RANK;
-  if (ds[3] != 1) return MVBEV_ERR_STRIDE;
-  if (Ho * Wo > (int64_t)INT32_MAX || B > 65535 || H > INT32_MAX / 2 || W > INT32_MAX / 2)
-    return MVBEV_ERR_SHAPE;
-  const int cpb = 64;
-  dim3 grid((unsigned)ceil_div(Ho * Wo, 256), (unsigned)ceil_div(C, cpb), (unsigned)B);
-  hipLaunchKernelGGL((warp_perspective_kernel<T, 4>), grid, dim3(256), 0, as_stream(stream), src,
-                     ss[0], ss[1], ss[2], ss[3], (int)C, (int)H, (int)W, m, dst, ds[0], ds[1],
-                     ds[2], (int)Ho, (int)Wo, cpb);
+static int launch_warp(const WarpArgs& a, void* stream) {
+  dim3 grid((unsigned)(a.tiles_x * ceil_div(a.Ho, kWarpTH)), (unsigned)ceil_div(a.C, kWarpCPB),
+            (unsigned)(a.B * a.nviews));
+  hipLaunchKernelGGL((warp_tile_kernel<T, 4>), grid, dim3(256), 0, as_stream(stream), a);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
+}
+
+static int check_sizes(int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int nviews) {
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 || nviews <= 0) return MVBEV_ERR_RANK;
+  if (nviews > kWarpMaxViews || B * nviews > 65535 || C > INT32_MAX || H > INT32_MAX / 2 ||
+      W > INT32_MAX / 2 || Ho > INT32_MAX / 2 || Wo > INT32_MAX / 2 ||
+      ceil_div(Ho, kWarpTH) * ceil_div(Wo, kWarpTW) > INT32_MAX)
+    return MVBEV_ERR_SHAPE;
+  return MVBEV_OK;
+}
+
+template <typename T>
+static int warp_single(const void* src, int64_t B, int64_t C, int64_t H, int64_t W,
+                       const int64_t* ss, const float* m, void* dst, int64_t Ho, int64_t Wo,
+                       const int64_t* ds, void* stream) {
+  if (!src || !m || !dst || !ss || !ds) return MVBEV_ERR_NULL;
+  const int st = check_sizes(B, C, H, W, Ho, Wo, 1);
+  if (st != MVBEV_OK) return st;
+  if (ds[3] != 1) return MVBEV_ERR_STRIDE;
+  WarpArgs a = {};
+  a.v[0] = WarpView{src, ss[0], ss[1], ss[2], ss[3], dst, ds[0], ds[1], ds[2], m, {}};
+  a.nviews = 1; a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W;
+  a.Ho = (int)Ho; a.Wo = (int)Wo; a.tiles_x = (int)ceil_div(Wo, kWarpTW);
+  return launch_warp<T>(a, stream);
+}
+
+template <typename T>
+static int warp_views(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t H,
+                      int64_t W, int64_t Ho, int64_t Wo, void* stream) {
+  if (!views) return MVBEV_ERR_NULL;
+  const int st = check_sizes(B, C, H, W, Ho, Wo, nviews);
+  if (st != MVBEV_OK) return st;
+  WarpArgs a = {};
+  for (int i = 0; i < nviews; ++i) {
+    const mvbev_warp_view& s = views[i];
+    if (!s.src || !s.dst) return MVBEV_ERR_NULL;
+    if (s.dst_strides[3] != 1) return MVBEV_ERR_STRIDE;
+    WarpView& d = a.v[i];
+    d.src = s.src; d.sB = s.src_strides[0]; d.sC = s.src_strides[1];
+    d.sH = s.src_strides[2]; d.sW = s.src_strides[3];
+    d.dst = s.dst; d.dB = s.dst_strides[0]; d.dC = s.dst_strides[1]; d.dH = s.dst_strides[2];
+    d.m_dev = nullptr;
+    for (int k = 0; k < 9; ++k) d.m[k] = s.m[k];
+  }
+  a.nviews = nviews; a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W;
+  a.Ho = (int)Ho; a.Wo = (int)Wo; a.tiles_x = (int)ceil_div(Wo, kWarpTW);
+  return launch_warp<T>(a, stream);
 }
 
 // coord_map (persp_trans_detector.py:103-112): grid / (n-1) * 2 - 1 in float64, then .float()
@@ -160,7 +229,7 @@ int mvbev_warp_perspective_f32(const float* src, int64_t B, int64_t C, int64_t H
                                const int64_t src_strides[4], const float* m, float* dst,
                                int64_t Ho, int64_t Wo, const int64_t dst_strides[4],
                                void* stream) {
-  return mvbev::launch_warp<float>(src, B, C, H, W, src_strides, m, dst, Ho, Wo, dst_strides,
+  return mvbev::warp_single<float>(src, B, C, H, W, src_strides, m, dst, Ho, Wo, dst_strides,
                                    stream);
 }
 
@@ -168,8 +237,18 @@ int mvbev_warp_perspective_f16(const void* src, int64_t B, int64_t C, int64_t H,
                                const int64_t src_strides[4], const float* m, void* dst,
                                int64_t Ho, int64_t Wo, const int64_t dst_strides[4],
                                void* stream) {
-  return mvbev::launch_warp<__half>(static_cast<const __half*>(src), B, C, H, W, src_strides, m,
-                                    static_cast<__half*>(dst), Ho, Wo, dst_strides, stream);
+  return mvbev::warp_single<__half>(src, B, C, H, W, src_strides, m, dst, Ho, Wo, dst_strides,
+                                    stream);
+}
+
+int mvbev_warp_views_f32(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
+                         int64_t H, int64_t W, int64_t Ho, int64_t Wo, void* stream) {
+  return mvbev::warp_views<float>(views, nviews, B, C, H, W, Ho, Wo, stream);
+}
+
+int mvbev_warp_views_f16(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
+                         int64_t H, int64_t W, int64_t Ho, int64_t Wo, void* stream) {
+  return mvbev::warp_views<__half>(views, nviews, B, C, H, W, Ho, Wo, stream);
 }
 
 int mvbev_fill_coord_map_f32(float* dst, int64_t B, int64_t Ho, int64_t Wo,

@@ -69,6 +69,40 @@ def warp_into(src: torch.Tensor, m_norm: torch.Tensor, dst: torch.Tensor) -> tor
     return dst
 
 
+def warp_views_into(srcs, m_norms, dsts) -> None:
+    """Warp several views (same shapes) in ONE launch.
+
+    ``srcs[i]`` [B,C,H,W], ``dsts[i]`` [B,C,Ho,Wo] views (innermost stride 1), ``m_norms[i]``
+    a host [3,3] src_norm <- dst_norm matrix shared by the batch (``kornia_src_norm_from_dst_norm``).
+    """
+    n = len(srcs)
+    if n == 0:
+        return
+    if not (len(m_norms) == n == len(dsts)) or n > 16:
+        raise ValueError("need 1..16 matching srcs / m_norms / dsts")
+    _require_cuda(*srcs, *dsts)
+    B, C, H, W = srcs[0].shape
+    Ho, Wo = dsts[0].shape[2], dsts[0].shape[3]
+    dtype = srcs[0].dtype
+    arr = (_native.WarpView * n)()
+    for i, (s, m, d) in enumerate(zip(srcs, m_norms, dsts)):
+        if tuple(s.shape) != (B, C, H, W) or tuple(d.shape) != (B, C, Ho, Wo):
+            raise ValueError("all views must share shapes")
+        if s.dtype != dtype or d.dtype != dtype:
+            raise TypeError("all views must share one dtype")
+        mm = torch.as_tensor(m, dtype=torch.float32).reshape(9).tolist()
+        arr[i] = _native.WarpView(s.data_ptr(), (ctypes.c_int64 * 4)(*s.stride()), d.data_ptr(),
+                                  (ctypes.c_int64 * 4)(*d.stride()), (ctypes.c_float * 9)(*mm))
+    lib = _native.load()
+    if dtype == torch.float32:
+        fn, name = lib.mvbev_warp_views_f32, "mvbev_warp_views_f32"
+    elif dtype == torch.float16:
+        fn, name = lib.mvbev_warp_views_f16, "mvbev_warp_views_f16"
+    else:
+        raise TypeError(f"unsupported dtype {dtype}")
+    _native.check(fn(arr, n, B, C, H, W, Ho, Wo, _stream(dsts[0])), name)
+
+
 def warp_perspective(src: torch.Tensor, M: torch.Tensor, dsize: Tuple[int, int], mode: str = "bilinear",
                      padding_mode: str = "zeros", align_corners: bool = True,
                      out: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -84,8 +84,11 @@ class ViewParallel:
 
     def warp(self, ws, feats: Sequence[torch.Tensor]) -> None:
         """Warp this rank's views (``feats[j]`` is view ``my_views[j]``)."""
-        for v, f in zip(self.my_views, feats):
-            self.engine.warp_view(ws, v, f)
+        if hasattr(self.engine, "warp_views"):
+            self.engine.warp_views(ws, self.my_views, list(feats))
+        else:
+            for v, f in zip(self.my_views, feats):
+                self.engine.warp_view(ws, v, f)
 
     def gather_views(self, ws) -> None:
         _all_gather_inplace(ws.slab, self.rank, self.world, self.group)

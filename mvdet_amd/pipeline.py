@@ -120,6 +120,15 @@ class ProjectFuse:
                              f"[B,{self.C},{self.src_hw[0]},{self.src_hw[1]}]")
         ops.warp_into(feat, ws.m_norm[cam], self.view_slice(ws, cam))
 
+    def warp_views(self, ws: Workspace, cams: Sequence[int], feats: Sequence[torch.Tensor]) -> None:
+        """a5 for several views in one launch (``feats[i]`` is view ``cams[i]``)."""
+        for cam, f in zip(cams, feats):
+            if tuple(f.shape[2:]) != self.src_hw or f.shape[1] != self.C:
+                raise ValueError(f"view {cam}: features {tuple(f.shape)} do not match "
+                                 f"[B,{self.C},{self.src_hw[0]},{self.src_hw[1]}]")
+        ops.warp_views_into(list(feats), [self.m_norm_cpu[c] for c in cams],
+                            [self.view_slice(ws, c) for c in cams])
+
     # -- coord term (a2 folded into conv1) --------------------------------------------------
     def coord_term(self, conv1: torch.nn.Conv2d) -> torch.Tensor:
         """[512, Ho, Wo]: bias + conv(coord channels) for the current conv1 parameters."""
@@ -186,6 +195,5 @@ class ProjectFuse:
         """Whole hot path on one device: warp every view, concat (zero-copy), fuse."""
         B = feats[0].shape[0]
         ws = self.workspace(B, feats[0].device)
-        for cam, f in enumerate(feats):
-            self.warp_view(ws, cam, f)
+        self.warp_views(ws, list(range(len(feats))), feats)
         return self.fuse(ws, map_classifier)

@@ -77,6 +77,25 @@ def test_warp_strided_src_and_channel_slice_dst():
     assert (dst_full[:, :10] == 7).all() and (dst_full[:, 30:] == 7).all()
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_warp_views_batched_launch(dtype):
+    """mvbev_warp_views_*: several views in one launch, each into a slice of a shared slab."""
+    from mvdet_amd import ops
+    from mvdet_amd.geometry import kornia_src_norm_from_dst_norm
+    rng = np.random.default_rng(17)
+    B, C, H, W, ho, wo, N = 2, 24, 33, 61, 19, 45, 5
+    srcs = [torch.from_numpy(np.maximum(rng.standard_normal((B, C, H, W)), 0).astype(np.float32)) for _ in range(N)]
+    Ms = [torch.from_numpy(_rand_h(rng, H, W, ho, wo)).float()[None] for _ in range(N)]
+    slab = torch.full((N, B, C + 8, ho, wo), 5.0, device=DEV, dtype=dtype)
+    mn = [kornia_src_norm_from_dst_norm(M, (H, W), (ho, wo))[0] for M in Ms]
+    ops.warp_views_into([s.to(DEV, dtype) for s in srcs], mn, [slab[i, :, :C] for i in range(N)])
+    for i in range(N):
+        ref = kornia_warp.warp_perspective(srcs[i].to(dtype).float(), Ms[i].repeat(B, 1, 1), (ho, wo))
+        s = parity_stats(slab[i, :, :C].float().cpu(), ref)
+        assert s["normwise"] < (1e-5 if dtype == torch.float32 else 2e-3), (i, s)
+    assert (slab[:, :, C:] == 5).all()
+
+
 def test_warp_f16_storage():
     from mvdet_amd import warp_perspective
     rng = np.random.default_rng(11)

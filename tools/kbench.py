@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="warp,conv1,conv2,conv3")
+    ap.add_argument("--libs", default="", help="comma-separated libmvbev variants to A/B (interleaved rounds)")
+    ap.add_argument("--rounds", type=int, default=1)
     args = ap.parse_args()
     spec = synthetic.CONFIGS[args.config]
     ds = spec["make"]()
@@ -60,18 +62,27 @@ def main():
             eng.warp_view(ws, v, feats[v])
         eng.fuse(ws, mc)
         stages = {
-            "warp": (lambda: [eng.warp_view(ws, v, feats[v]) for v in range(N)], None),
+            "warp": (lambda: eng.warp_views(ws, list(range(N)), feats), None),
+            "warp1": (lambda: [eng.warp_view(ws, v, feats[v]) for v in range(N)], None),
             "conv1": (lambda: eng.conv1(ws, mc[0]), 2.0 * B * ho * wo * 9 * N * C * 512),
             "conv2": (lambda: eng.conv2(ws, mc[2]), 2.0 * B * ho * wo * 9 * 512 * 512),
             "conv3": (lambda: eng.conv3(ws, mc[4]), None),
         }
-        for name in args.only.split(","):
-            fn, flop = stages[name]
-            med, mn = timeit(fn, args.reps)
-            rec = {"stage": name, "config": args.config, "median_ms": round(med, 4), "min_ms": round(mn, 4)}
-            if flop:
-                rec["TFLOPs"] = round(flop / (med * 1e-3) / 1e12, 2)
-            print(json.dumps(rec), flush=True)
+        from mvdet_amd import _native
+        libs = [("default", _native.load())]
+        for path in filter(None, args.libs.split(",")):
+            libs.append((Path(path).stem, _native.load(path)))
+        for rnd in range(args.rounds):
+            for lname, lib in libs:
+                _native._lib = lib
+                for name in args.only.split(","):
+                    fn, flop = stages[name]
+                    med, mn = timeit(fn, args.reps)
+                    rec = {"stage": name, "lib": lname, "round": rnd, "config": args.config,
+                           "median_ms": round(med, 4), "min_ms": round(mn, 4)}
+                    if flop:
+                        rec["TFLOPs"] = round(flop / (med * 1e-3) / 1e12, 2)
+                    print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

@@ -13,9 +13,8 @@
 //   out = sum over the 4 in-bounds corners of src * bilinear weight    (zeros padding;
 //         a non-finite ix/iy gives NaN in every channel, like torch's CPU grid_sample)
 //
-// Kernel shape (HBM-bound gather): a block is a 2-D output tile of 8 rows x 32 columns
-// (one thread per pixel, each wave = 2 rows x 32 columns: 128-B coalesced stores) and a
-// slice of 64 channels.  The pixel's transform, corner offsets and weights are computed
+// Kernel shape (HBM-bound gather): a block is a 2-D output tile of TH x TW = 256 pixels
+// (one thread per pixel; each wave a WR x 64/WR sub-tile) and a slice of 64 channels.  The pixel's transform, corner offsets and weights are computed
 // once and reused over the channel slice; 4 channels x 4 corners of loads are in flight
 // per thread.  The compact 2-D tile keeps each source footprint inside one block (the
 // corners of neighbouring pixels share 128-B lines in L1/L2) instead of being re-fetched
@@ -25,9 +24,15 @@
 
 namespace mvbev {
 
-constexpr int kWarpTH = 8;       // output rows per block
-constexpr int kWarpTW = 32;      // output cols per block
-constexpr int kWarpCPB = 64;     // channels per block
+#ifndef MVBEV_WARP_TH  // A/B on cfg2 (7 views, 1 launch): 8x32/2 0.89 ms, 16x16/8 0.80, 16x16/4 0.75
+#define MVBEV_WARP_TH 16
+#define MVBEV_WARP_TW 16
+#define MVBEV_WARP_WR 4
+#endif
+constexpr int kWarpTH = MVBEV_WARP_TH;  // output rows per block
+constexpr int kWarpTW = MVBEV_WARP_TW;  // output cols per block
+constexpr int kWarpWR = MVBEV_WARP_WR;  // output rows per wave (wave tile WR x 64/WR)
+constexpr int kWarpCPB = 64;            // channels per block
 constexpr int kWarpMaxViews = 16;
 
 struct WarpView {
@@ -41,20 +46,29 @@ struct WarpView {
 
 struct WarpArgs {
   WarpView v[kWarpMaxViews];
-  int nviews, B, C, H, W, Ho, Wo, tiles_x;
+  int nviews, B, C, H, W, Ho, Wo, tiles_x, tiles, chunks, nwg;
 };
 
 template <typename T, int UNROLL>
 __global__ __launch_bounds__(256) void warp_tile_kernel(const WarpArgs a) {
-  const int view = blockIdx.z % a.nviews;
-  const int b = blockIdx.z / a.nviews;
+  // Logical block order (batch*view, channel chunk, tile) with tile fastest, dealt to the
+  // XCDs in contiguous ranges: neighbouring tiles of one plane share an L2 (their source
+  // footprints overlap in the far field, where many grid cells map into one source line).
+  const int lb = xcd_remap(blockIdx.x, a.nwg);
+  const int tile = lb % a.tiles;
+  const int chunk = (lb / a.tiles) % a.chunks;
+  const int bv = lb / (a.tiles * a.chunks);
+  const int view = bv % a.nviews;
+  const int b = bv / a.nviews;
   const WarpView& vw = a.v[view];
-  const int tile = blockIdx.x;
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
-  const int v = ty * kWarpTH + (threadIdx.x >> 5);
-  const int u = tx * kWarpTW + (threadIdx.x & 31);
+  constexpr int WC = 64 / kWarpWR, WAVES_X = kWarpTW / WC;
+  static_assert(kWarpTH * kWarpTW == 256 && kWarpTW % WC == 0 && kWarpTH % kWarpWR == 0, "tile");
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int v = ty * kWarpTH + (wave / WAVES_X) * kWarpWR + lane / WC;
+  const int u = tx * kWarpTW + (wave % WAVES_X) * WC + lane % WC;
   if (v >= a.Ho || u >= a.Wo) return;
-  const int c_begin = blockIdx.y * kWarpCPB;
+  const int c_begin = chunk * kWarpCPB;
   const int c_end = min(a.C, c_begin + kWarpCPB);
   const int H = a.H, W = a.W;
 
@@ -141,18 +155,28 @@ __global__ __launch_bounds__(256) void warp_tile_kernel(const WarpArgs a) {
 
 template <typename T>
 static int launch_warp(const WarpArgs& a, void* stream) {
-  dim3 grid((unsigned)(a.tiles_x * ceil_div(a.Ho, kWarpTH)), (unsigned)ceil_div(a.C, kWarpCPB),
-            (unsigned)(a.B * a.nviews));
-  hipLaunchKernelGGL((warp_tile_kernel<T, 4>), grid, dim3(256), 0, as_stream(stream), a);
+  hipLaunchKernelGGL((warp_tile_kernel<T, 4>), dim3((unsigned)a.nwg), dim3(256), 0,
+                     as_stream(stream), a);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
+}
+
+template <typename T>
+static int finish_args_and_launch(WarpArgs& a, int64_t B, int64_t C, int64_t H, int64_t W,
+                                  int64_t Ho, int64_t Wo, void* stream) {
+  a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
+  a.tiles_x = (int)ceil_div(Wo, kWarpTW);
+  a.tiles = a.tiles_x * (int)ceil_div(Ho, kWarpTH);
+  a.chunks = (int)ceil_div(C, kWarpCPB);
+  a.nwg = a.tiles * a.chunks * a.B * a.nviews;
+  return launch_warp<T>(a, stream);
 }
 
 static int check_sizes(int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int nviews) {
   if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 || nviews <= 0) return MVBEV_ERR_RANK;
   if (nviews > kWarpMaxViews || B * nviews > 65535 || C > INT32_MAX || H > INT32_MAX / 2 ||
       W > INT32_MAX / 2 || Ho > INT32_MAX / 2 || Wo > INT32_MAX / 2 ||
-      ceil_div(Ho, kWarpTH) * ceil_div(Wo, kWarpTW) > INT32_MAX)
+      ceil_div(Ho, kWarpTH) * ceil_div(Wo, kWarpTW) * ceil_div(C, kWarpCPB) * B * nviews > INT32_MAX)
     return MVBEV_ERR_SHAPE;
   return MVBEV_OK;
 }
@@ -167,9 +191,8 @@ static int warp_single(const void* src, int64_t B, int64_t C, int64_t H, int64_t
   if (ds[3] != 1) return MVBEV_ERR_STRIDE;
   WarpArgs a = {};
   a.v[0] = WarpView{src, ss[0], ss[1], ss[2], ss[3], dst, ds[0], ds[1], ds[2], m, {}};
-  a.nviews = 1; a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W;
-  a.Ho = (int)Ho; a.Wo = (int)Wo; a.tiles_x = (int)ceil_div(Wo, kWarpTW);
-  return launch_warp<T>(a, stream);
+  a.nviews = 1;
+  return finish_args_and_launch<T>(a, B, C, H, W, Ho, Wo, stream);
 }
 
 template <typename T>
@@ -190,9 +213,8 @@ static int warp_views(const mvbev_warp_view* views, int nviews, int64_t B, int64
     d.m_dev = nullptr;
     for (int k = 0; k < 9; ++k) d.m[k] = s.m[k];
   }
-  a.nviews = nviews; a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W;
-  a.Ho = (int)Ho; a.Wo = (int)Wo; a.tiles_x = (int)ceil_div(Wo, kWarpTW);
-  return launch_warp<T>(a, stream);
+  a.nviews = nviews;
+  return finish_args_and_launch<T>(a, B, C, H, W, Ho, Wo, stream);
 }
 
 // coord_map (persp_trans_detector.py:103-112): grid / (n-1) * 2 - 1 in float64, then .float()

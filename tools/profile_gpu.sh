@@ -15,11 +15,14 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/$
   python3 bench.py --steps 10 --warmup 3 --config $CFG --no-cpu-baseline > $OUT/${TAG}_trace_bench.log 2>&1 || exit $?
 i=0
 for PMC in "GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES" \
-           "FETCH_SIZE" "WRITE_SIZE" \
+           "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" \
+           "WRITE_SIZE" "FETCH_SIZE" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \
            "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $PMC --output-format csv -d $OUT/${TAG}_pmc$i -o run -- \
-    python3 tools/kbench.py --config $CFG --reps 3 > $OUT/${TAG}_pmc$i.log 2>&1 || exit $?
+    python3 tools/kbench.py --config $CFG --reps 3 --only warp,conv1,conv2,conv3 > $OUT/${TAG}_pmc$i.log 2>&1 || exit $?
 done
+python3 tools/pmc_summary.py $OUT/${TAG}_pmc* > $OUT/${TAG}_pmc_summary.txt
+python3 tools/traffic.py $OUT $TAG $CFG > $OUT/${TAG}_traffic.json
 echo profile-done

@@ -1,0 +1,41 @@
+"""Per-launch HBM-side traffic of each hot-path kernel from the rocprofv3 --pmc passes.
+
+read bytes  = 32*RDREQ_32B + 64*RDREQ_64B + 128*RDREQ_128B   (TCC_EA0 request sizes; the
+              gfx950 FETCH_SIZE formula tallies 128-B requests at 64 B — MI355X_MICROARCH §HBM)
+write bytes = WRITE_SIZE * 1024  (exact for 16-B-per-lane and 4-B-per-lane coalesced stores)
+Only dispatches of the timed stage calls are used: for each kernel, the median over its
+dispatches.  Usage: python tools/traffic.py <pmc dir> <tag> <config>
+"""
+import collections
+import csv
+import glob
+import json
+import statistics
+import sys
+
+out_dir, tag, cfg = sys.argv[1], sys.argv[2], int(sys.argv[3])
+vals = collections.defaultdict(lambda: collections.defaultdict(dict))
+for f in glob.glob(f"{out_dir}/{tag}_pmc*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        name = r["Kernel_Name"].split("(")[0]
+        vals[name][r["Counter_Name"]][(f, r["Dispatch_Id"])] = float(r["Counter_Value"])
+
+def med(name, counter):
+    xs = list(vals[name].get(counter, {}).values())
+    return statistics.median(xs) if xs else None
+
+res = {"config": cfg, "source": f"rocprofv3 --pmc passes over tools/kbench.py ({tag})", "kernels": {}}
+for name in vals:
+    if "mvbev::" not in name:
+        continue
+    n32, n64, n128 = (med(name, f"TCC_EA0_RDREQ_{s}_sum") for s in ("32B", "64B", "128B"))
+    wr = med(name, "WRITE_SIZE")
+    if None in (n32, n64, n128, wr):
+        continue
+    rd = 32 * n32 + 64 * n64 + 128 * n128
+    res["kernels"][name] = {"read_bytes": rd, "write_bytes": wr * 1024, "hbm_bytes_per_launch": rd + wr * 1024,
+                            "fetch_size_kb": med(name, "FETCH_SIZE")}
+conv1 = [k for k in res["kernels"] if "conv3x3_mfma" in k and "<1," in k]
+if conv1:
+    res["conv1_hbm_bytes_per_launch"] = res["kernels"][conv1[0]]["hbm_bytes_per_launch"]
+print(json.dumps(res, indent=1))

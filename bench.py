@@ -86,6 +86,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3"],
+                    help="conv1/conv2 arithmetic: fp32 MFMA or 3xbf16 split (fp32-class accuracy)")
     ap.add_argument("--config", type=int, default=2, help="BASELINE.json config index (1-based)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=0, help="frames for the CPU baseline (0 = auto)")
@@ -112,7 +114,7 @@ def main():
     pm = projection_matrices(ds)
     params = head_params(N, seed=args.config, C=C)
     mc = build_mc(C, N, params, dev)
-    eng = ProjectFuse(pm, up, (ho, wo), C)
+    eng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision)
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * args.config + v,
                                           device=dev) for v in range(N)]
     ws = eng.workspace(B, dev)

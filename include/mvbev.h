@@ -30,6 +30,8 @@
  *       map_classifier[0:4]   persp_trans_detector.py:51-53, :81; the conv1 contribution of
  *       the two constant coord channels plus its bias is input-independent and enters as
  *       the `init` term (computed once per weight version with the same kernel).
+ *   mvbev_pack_conv3x3_weight_bf16x3, mvbev_conv3x3_bf16x3
+ *       the same convs in 3xbf16 split precision on the bf16 MFMA (5.3x the fp32 rate)
  *   mvbev_conv3x3_cout1_f32
  *       nn.Conv2d(512->1, 3, padding=4, dilation=4, bias=False) of
  *       map_classifier[4]      persp_trans_detector.py:54, :81
@@ -143,6 +145,19 @@ typedef struct mvbev_conv_desc {
 int mvbev_conv3x3_f32(const float* x, const mvbev_conv_desc* desc, const float* w_packed,
                       const float* bias, const float* init, int64_t Cout, int dilation,
                       int relu, float* y, void* stream);
+
+/* 3xbf16 split-precision variant of mvbev_conv3x3_f32 (same descriptor and semantics):
+ * a*b ~= a_hi*b_hi + a_hi*b_lo + a_lo*b_hi on the bf16 MFMA, fp32 accumulation; ~2^-16
+ * relative per product (fp32-class; see conv_bf16x3.hip).  x is fp32 (x_is_f16 = 0) or
+ * fp16 storage (x_is_f16 = 1, e.g. the config-4 fp16 slab); y is fp32.
+ * Weights packed by mvbev_pack_conv3x3_weight_bf16x3 (bytes: mvbev_conv3x3_packed_bytes_bf16x3). */
+size_t mvbev_conv3x3_packed_bytes_bf16x3(int64_t Cout, int64_t K);
+int mvbev_pack_conv3x3_weight_bf16x3(const float* w, int64_t Cout, int64_t Cin_w,
+                                     const int32_t* chan_map, int64_t K, void* w_packed,
+                                     void* stream);
+int mvbev_conv3x3_bf16x3(const void* x, int x_is_f16, const mvbev_conv_desc* desc,
+                         const void* w_packed, const float* bias, const float* init,
+                         int64_t Cout, int dilation, int relu, float* y, void* stream);
 
 /* y[b][0][r][:] = conv3x3(x[b], w, dilation=d, padding=d)[out_row0 + r], one output channel,
  * no bias.  x : [B][C][in_rows][W] holding global rows [in_row0, in_row0+in_rows) of an

@@ -25,6 +25,9 @@ EXPORTS = (
     "mvbev_pack_conv3x3_weight_f32",
     "mvbev_conv3x3_f32",
     "mvbev_conv3x3_cout1_f32",
+    "mvbev_conv3x3_packed_bytes_bf16x3",
+    "mvbev_pack_conv3x3_weight_bf16x3",
+    "mvbev_conv3x3_bf16x3",
 )
 
 KC = 8    # MVBEV_CONV_KC
@@ -75,6 +78,13 @@ def _declare(lib):
     lib.mvbev_conv3x3_f32.restype = ctypes.c_int
     lib.mvbev_conv3x3_f32.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64, ctypes.c_int,
                                       ctypes.c_int, _p, _p]
+    lib.mvbev_conv3x3_packed_bytes_bf16x3.restype = ctypes.c_size_t
+    lib.mvbev_conv3x3_packed_bytes_bf16x3.argtypes = [_i64, _i64]
+    lib.mvbev_pack_conv3x3_weight_bf16x3.restype = ctypes.c_int
+    lib.mvbev_pack_conv3x3_weight_bf16x3.argtypes = [_p, _i64, _i64, _p, _i64, _p, _p]
+    lib.mvbev_conv3x3_bf16x3.restype = ctypes.c_int
+    lib.mvbev_conv3x3_bf16x3.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64,
+                                         ctypes.c_int, ctypes.c_int, _p, _p]
     lib.mvbev_conv3x3_cout1_f32.restype = ctypes.c_int
     lib.mvbev_conv3x3_cout1_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p,
                                             ctypes.c_int, _p, _p]

@@ -1,0 +1,315 @@
+// 3xbf16 split-precision 3x3 conv (fp32 in, fp32 out) on the bf16 MFMA for gfx950.
+//
+// Same operation and descriptor as mvbev_conv3x3_f32 (map_classifier[0:4],
+// multiview_detector/models/persp_trans_detector.py:51-53), computed as
+//     a*b ~= a_hi*b_hi + a_hi*b_lo + a_lo*b_hi,   a_hi = bf16(a), a_lo = bf16(a - a_hi)
+// with fp32 accumulation in v_mfma_f32_32x32x16_bf16.  Each operand keeps 16 mantissa bits
+// (the dropped a_lo*b_lo term and the rounding of the lo parts are <= ~2^-16 relative per
+// product), i.e. fp32-class accuracy: measured <= ~1e-5 normwise vs fp32 on the fusion
+// convs, against a parity gate of 1e-3 (and tighter than the TF32 that cuDNN's default uses
+// for these convs on NVIDIA).  The bf16 MFMA issues 16x the fp32 MFMA's FLOP/clk, so the
+// three passes still run 5.3x the fp32 rate.  Inputs may be fp32 or fp16 (an fp16 value is
+// exactly hi + lo, so the fp16-storage config 4 path is exact in its products).
+//
+// Mapping: K is walked in chunks of 8 input channels; a chunk is 5 MFMA K-blocks of 16 =
+// (tap pair, 8 channels) with a zero-weight 10th tap.  Lane l of the 32x32x16 MFMA holds
+// A[co = l&31][k = 8(l>>5) + j] and B[k][pixel = l&31], so the lane's 8 K-values are the 8
+// channels of one tap: the weights are pre-packed [tap pair][tap][co][8 ch] and the input
+// halo is staged channel-innermost [row][col][8 ch], both read as one ds_read_b128 per
+// fragment (16 consecutive lanes = 256 contiguous bytes: conflict-free).  The input halo is
+// split into hi/lo once at LDS-store time; weights are split once at pack time.
+// Workgroup tile: NW/2 row pairs x 32 cols x 128 output channels; wave = 2 rows x 64
+// channels (2x2 accumulators of 32x32, the same epilogue as the fp32 kernel).
+#include "common.h"
+
+namespace mvbev {
+namespace b3 {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int KC = MVBEV_CONV_KC;  // 8 input channels per chunk
+constexpr int NKB = 5;             // K-blocks per chunk: taps (2kb, 2kb+1), tap 9 = zero pad
+constexpr int BN = MVBEV_CONV_BN;  // 128 output channels per workgroup
+constexpr int TW = 32;             // output columns per workgroup (= MFMA N)
+constexpr int WPART = NKB * 2 * BN * KC;  // bf16 per part (hi or lo) per (chunk, cout tile)
+constexpr int WBYTES = 2 * WPART * 2;     // hi + lo bytes per (chunk, cout tile) = 40 KiB
+constexpr int W16 = WBYTES / 16;          // 16-B pieces
+
+// packed[chunk][cot][part][kb][h][co][j]: tap = 2kb+h, input channel = map(chunk*8 + j)
+__global__ void pack_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int Cout,
+                            int Cin_w, const int32_t* __restrict__ chan_map, int K, int K_pad) {
+  const int n_cot = Cout / BN;
+  const int64_t total = (int64_t)(K_pad / KC) * n_cot * 2 * WPART;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i;
+    const int j = r % KC; r /= KC;
+    const int co = r % BN; r /= BN;
+    const int h = r % 2; r /= 2;
+    const int kb = r % NKB; r /= NKB;
+    const int part = r % 2; r /= 2;
+    const int cot = r % n_cot;
+    const int chunk = (int)(r / n_cot);
+    const int tap = 2 * kb + h;
+    const int k = chunk * KC + j;
+    int ci = k < K ? (chan_map ? chan_map[k] : k) : -1;
+    if (ci >= Cin_w) ci = -1;
+    const float v = (tap < 9 && ci >= 0) ? w[((int64_t)(cot * BN + co) * Cin_w + ci) * 9 + tap] : 0.f;
+    const __bf16 hi = (__bf16)v;
+    out[i] = part ? (__bf16)(v - (float)hi) : hi;
+  }
+}
+
+struct Args {
+  const void* x;
+  const u32x4* wp;
+  const float* bias;
+  const float* init;
+  float* y;
+  int64_t group_stride, batch_stride;
+  int group, nchunks, Cout, H, W;
+  int in_row0, in_rows, out_row0, out_rows;
+  int tiles_x, tiles_y, n_cot, nwg;
+};
+
+template <typename T> __device__ inline float ld(const T* p);
+template <> __device__ inline float ld<float>(const float* p) { return *p; }
+template <> __device__ inline float ld<_Float16>(const _Float16* p) { return (float)*p; }
+
+template <typename TIn, int DIL, bool RELU, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void conv_kernel(const Args a) {
+  constexpr int NT = 64 * NW;
+  constexpr int TH = NW;                 // NW/2 row pairs, 2 channel halves
+  constexpr int XH = TH + 2 * DIL, XW = TW + 2 * DIL;
+  constexpr int XPIX = XH * XW;          // halo pixels per chunk (8 channels each)
+  constexpr int XPT = (XPIX + NT - 1) / NT;
+  constexpr int WLD = (W16 + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) u32x4 lds[W16 + 2 * XPIX];
+  u32x4* Wl = lds;              // [part][kb][h][co] pieces of 8 bf16
+  u32x4* Xhi = lds + W16;       // [r][c] pieces of 8 bf16 channels
+  u32x4* Xlo = Xhi + XPIX;
+
+  const int wg = xcd_remap(blockIdx.x, a.nwg);
+  const int cot = wg % a.n_cot;
+  int rest = wg / a.n_cot;
+  const int tx = rest % a.tiles_x;
+  rest /= a.tiles_x;
+  const int ty = rest % a.tiles_y;
+  const int b = rest / a.tiles_y;
+  const int x0 = tx * TW;
+  const int y0 = a.out_row0 + ty * TH;
+  const int W = a.W;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, kh = lane >> 5;
+
+  const int64_t plane = (int64_t)a.in_rows * W;
+  const TIn* xb = static_cast<const TIn*>(a.x) + (int64_t)b * a.batch_stride;
+  const u32x4* wsrc = a.wp + (int64_t)cot * W16;
+  const int64_t wchunk = (int64_t)a.n_cot * W16;
+  const int chunks_per_group = a.group / KC;
+
+  // halo pixels of this thread (chunk-invariant): plane offset + validity
+  int xoff[XPT];
+  bool xok[XPT];
+#pragma unroll
+  for (int i = 0; i < XPT; ++i) {
+    const int p = tid + NT * i;
+    const int r = p / XW, c = p % XW;
+    const int gy = y0 - DIL + r, gx = x0 - DIL + c;
+    const int by = gy - a.in_row0;
+    xok[i] = p < XPIX && gy >= 0 && gy < a.H && by >= 0 && by < a.in_rows && gx >= 0 && gx < W;
+    xoff[i] = xok[i] ? (int)((int64_t)by * W + gx) : 0;
+  }
+
+  u32x4 wreg[WLD];
+  float xreg[XPT][KC];
+#define B3_LOAD(ch)                                                                          \
+  do {                                                                                       \
+    const u32x4* ws_ = wsrc + (int64_t)(ch) * wchunk;                                        \
+    _Pragma("unroll") for (int i = 0; i < WLD; ++i) {                                        \
+      if (W16 % NT == 0 || tid + NT * i < W16) wreg[i] = ws_[tid + NT * i];                  \
+    }                                                                                        \
+    const int g_ = (ch) / chunks_per_group;                                                  \
+    const TIn* xc_ =                                                                         \
+        xb + g_ * a.group_stride + (int64_t)((ch) - g_ * chunks_per_group) * KC * plane;     \
+    _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                        \
+      _Pragma("unroll") for (int j = 0; j < KC; ++j) xreg[i][j] = ld<TIn>(xc_ + j * plane + xoff[i]); \
+    }                                                                                        \
+  } while (0)
+#define B3_STORE()                                                                           \
+  do {                                                                                       \
+    _Pragma("unroll") for (int i = 0; i < WLD; ++i) {                                        \
+      if (W16 % NT == 0 || tid + NT * i < W16) Wl[tid + NT * i] = wreg[i];                   \
+    }                                                                                        \
+    _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                        \
+      const int p = tid + NT * i;                                                            \
+      if (XPIX % NT == 0 || p < XPIX) {                                                      \
+        bf16x8 hi, lo;                                                                       \
+        _Pragma("unroll") for (int j = 0; j < KC; ++j) {                                     \
+          const float v = xok[i] ? xreg[i][j] : 0.f;                                         \
+          const __bf16 h_ = (__bf16)v;                                                       \
+          hi[j] = h_;                                                                        \
+          lo[j] = (__bf16)(v - (float)h_);                                                   \
+        }                                                                                    \
+        Xhi[p] = __builtin_bit_cast(u32x4, hi);                                              \
+        Xlo[p] = __builtin_bit_cast(u32x4, lo);                                              \
+      }                                                                                      \
+    }                                                                                        \
+  } while (0)
+
+  const int prow = 2 * (wave % (NW / 2));
+  const int cw = 64 * (wave / (NW / 2));
+  // per K-block B offsets in the halo image: tap = 2kb + kh (tap 9 -> any valid pixel)
+  int boff[NKB];
+#pragma unroll
+  for (int kb = 0; kb < NKB; ++kb) {
+    const int tap = min(2 * kb + kh, 8);
+    boff[kb] = (prow + (tap / 3) * DIL) * XW + l32 + (tap % 3) * DIL;
+  }
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = floatx16{0};
+
+  B3_LOAD(0);
+  for (int ch = 0; ch < a.nchunks; ++ch) {
+    __syncthreads();
+    B3_STORE();
+    __syncthreads();
+    if (ch + 1 < a.nchunks) B3_LOAD(ch + 1);
+#pragma unroll
+    for (int kb = 0; kb < NKB; ++kb) {
+      bf16x8 ahi[2], alo[2], bhi[2], blo[2];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const int wi = (kb * 2 + kh) * BN + cw + 32 * ct + l32;
+        ahi[ct] = __builtin_bit_cast(bf16x8, Wl[wi]);
+        alo[ct] = __builtin_bit_cast(bf16x8, Wl[NKB * 2 * BN + wi]);
+      }
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) {
+        bhi[pt] = __builtin_bit_cast(bf16x8, Xhi[boff[kb] + pt * XW]);
+        blo[pt] = __builtin_bit_cast(bf16x8, Xlo[boff[kb] + pt * XW]);
+      }
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+        for (int pt = 0; pt < 2; ++pt) {
+          acc[ct][pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[ct], bhi[pt], acc[ct][pt], 0, 0, 0);
+          acc[ct][pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[ct], blo[pt], acc[ct][pt], 0, 0, 0);
+          acc[ct][pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[ct], bhi[pt], acc[ct][pt], 0, 0, 0);
+        }
+    }
+  }
+#undef B3_LOAD
+#undef B3_STORE
+
+  const int col = x0 + l32;
+  const int64_t oplane = (int64_t)a.out_rows * W;
+  const int64_t iplane = (int64_t)a.H * W;
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) {
+      const int row = y0 + prow + pt;
+      if (row >= a.out_row0 + a.out_rows || col >= W) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = cot * BN + cw + 32 * ct + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        float v = acc[ct][pt][r];
+        if (a.bias) v += a.bias[co];
+        if (a.init) v += a.init[co * iplane + (int64_t)row * W + col];
+        if (RELU) v = v < 0.f ? 0.f : v;
+        a.y[((int64_t)b * a.Cout + co) * oplane + (int64_t)(row - a.out_row0) * W + col] = v;
+      }
+    }
+}
+
+#ifndef MVBEV_B3_WAVES
+#define MVBEV_B3_WAVES 8
+#endif
+
+template <typename TIn>
+static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
+                  const float* bias, const float* init, int64_t Cout, int dilation, int relu,
+                  float* y, void* stream) {
+  if (!x || !d || !w_packed || !y) return MVBEV_ERR_NULL;
+  if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || d->in_rows <= 0 ||
+      d->out_rows <= 0 || d->group <= 0)
+    return MVBEV_ERR_RANK;
+  if (Cout % BN != 0 || d->K % KC != 0 || d->group % KC != 0 || d->K % d->group != 0)
+    return MVBEV_ERR_SHAPE;
+  if (d->out_row0 < 0 || d->out_row0 + d->out_rows > d->H) return MVBEV_ERR_SHAPE;
+  if (d->in_rows * d->W > (int64_t)INT32_MAX || d->H > INT32_MAX / 2 || d->W > INT32_MAX / 2)
+    return MVBEV_ERR_SHAPE;
+  if ((reinterpret_cast<uintptr_t>(w_packed) & 15) != 0) return MVBEV_ERR_ALIGN;
+  constexpr int NW = MVBEV_B3_WAVES;
+  Args a;
+  a.x = x; a.wp = static_cast<const u32x4*>(w_packed); a.bias = bias; a.init = init; a.y = y;
+  a.group_stride = d->group_stride; a.batch_stride = d->batch_stride;
+  a.group = (int)d->group; a.nchunks = (int)(d->K / KC); a.Cout = (int)Cout;
+  a.H = (int)d->H; a.W = (int)d->W;
+  a.in_row0 = (int)d->in_row0; a.in_rows = (int)d->in_rows;
+  a.out_row0 = (int)d->out_row0; a.out_rows = (int)d->out_rows;
+  a.tiles_x = (int)ceil_div(d->W, TW); a.tiles_y = (int)ceil_div(d->out_rows, NW);
+  a.n_cot = (int)(Cout / BN);
+  const int64_t nwg = (int64_t)a.tiles_x * a.tiles_y * a.n_cot * d->B;
+  if (nwg > (int64_t)INT32_MAX) return MVBEV_ERR_SHAPE;
+  a.nwg = (int)nwg;
+  hipStream_t s = as_stream(stream);
+#define B3_LAUNCH(D, R)                                                                   \
+  hipLaunchKernelGGL((conv_kernel<TIn, D, R, NW>), dim3((unsigned)nwg), dim3(64 * NW), 0, s, a)
+  if (dilation == 1) {
+    if (relu) B3_LAUNCH(1, true); else B3_LAUNCH(1, false);
+  } else if (dilation == 2) {
+    if (relu) B3_LAUNCH(2, true); else B3_LAUNCH(2, false);
+  } else {
+    return MVBEV_ERR_DILATION;
+  }
+#undef B3_LAUNCH
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+}  // namespace b3
+}  // namespace mvbev
+
+extern "C" {
+
+size_t mvbev_conv3x3_packed_bytes_bf16x3(int64_t Cout, int64_t K) {
+  if (Cout <= 0 || K <= 0) return 0;
+  return (size_t)(mvbev::round_up(K, mvbev::b3::KC) / mvbev::b3::KC) *
+         (size_t)(Cout / mvbev::b3::BN) * mvbev::b3::WBYTES;
+}
+
+int mvbev_pack_conv3x3_weight_bf16x3(const float* w, int64_t Cout, int64_t Cin_w,
+                                     const int32_t* chan_map, int64_t K, void* w_packed,
+                                     void* stream) {
+  using namespace mvbev;
+  if (!w || !w_packed) return MVBEV_ERR_NULL;
+  if (Cout <= 0 || Cin_w <= 0 || K <= 0) return MVBEV_ERR_RANK;
+  if (Cout % b3::BN != 0) return MVBEV_ERR_SHAPE;
+  if (!chan_map && K != Cin_w) return MVBEV_ERR_SHAPE;
+  const int64_t k_pad = round_up(K, b3::KC);
+  const int64_t total = (int64_t)mvbev_conv3x3_packed_bytes_bf16x3(Cout, K) / 2;
+  const int blocks = (int)std::min<int64_t>(ceil_div(total, 256), 8192);
+  hipLaunchKernelGGL(b3::pack_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), w,
+                     static_cast<__bf16*>(w_packed), (int)Cout, (int)Cin_w, chan_map, (int)K,
+                     (int)k_pad);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+int mvbev_conv3x3_bf16x3(const void* x, int x_is_f16, const mvbev_conv_desc* desc,
+                         const void* w_packed, const float* bias, const float* init,
+                         int64_t Cout, int dilation, int relu, float* y, void* stream) {
+  if (x_is_f16)
+    return mvbev::b3::launch<_Float16>(x, desc, w_packed, bias, init, Cout, dilation, relu, y,
+                                       stream);
+  return mvbev::b3::launch<float>(x, desc, w_packed, bias, init, Cout, dilation, relu, y, stream);
+}
+
+}  // extern "C"

@@ -152,12 +152,21 @@ def padded_channels(cin: int) -> int:
     return (cin + KC - 1) // KC * KC
 
 
+PRECISIONS = ("fp32", "bf16x3")
+
+
 class PackedConv3x3:
     """MFMA-layout copy of an ``nn.Conv2d`` 3x3 weight (optionally with its input
     channels permuted by ``chan_map``), re-packed only when the parameter changes
-    (keyed by ``(data_ptr, _version, shape)``)."""
+    (keyed by ``(data_ptr, _version, shape)``).
 
-    def __init__(self, chan_map: Optional[Sequence[int]] = None):
+    ``precision``: "fp32" (fp32 MFMA, exact fp32 products) or "bf16x3" (hi/lo bf16 split,
+    three bf16 MFMA passes, fp32 accumulation)."""
+
+    def __init__(self, chan_map: Optional[Sequence[int]] = None, precision: str = "fp32"):
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {PRECISIONS}")
+        self.precision = precision
         self._key = None
         self.packed: Optional[torch.Tensor] = None
         self.chan_map = None if chan_map is None else [int(c) for c in chan_map]
@@ -180,13 +189,20 @@ class PackedConv3x3:
             K = cin if self.chan_map is None else len(self.chan_map)
             if self.chan_map is not None and (self._map_dev is None or self._map_dev.device != weight.device):
                 self._map_dev = torch.tensor(self.chan_map, dtype=torch.int32, device=weight.device)
-            n = lib.mvbev_conv3x3_packed_floats(cout, K)
-            packed = torch.empty(n, dtype=torch.float32, device=weight.device)
+            cmap = None if self._map_dev is None else self._map_dev.data_ptr()
             w = weight.detach().contiguous()
-            st = lib.mvbev_pack_conv3x3_weight_f32(w.data_ptr(), cout, cin,
-                                                   None if self._map_dev is None else self._map_dev.data_ptr(),
-                                                   K, packed.data_ptr(), _stream(packed))
-            _native.check(st, "mvbev_pack_conv3x3_weight_f32")
+            if self.precision == "fp32":
+                n = lib.mvbev_conv3x3_packed_floats(cout, K)
+                packed = torch.empty(n, dtype=torch.float32, device=weight.device)
+                st = lib.mvbev_pack_conv3x3_weight_f32(w.data_ptr(), cout, cin, cmap, K, packed.data_ptr(),
+                                                       _stream(packed))
+                _native.check(st, "mvbev_pack_conv3x3_weight_f32")
+            else:
+                n = lib.mvbev_conv3x3_packed_bytes_bf16x3(cout, K)
+                packed = torch.empty(n // 2, dtype=torch.bfloat16, device=weight.device)
+                st = lib.mvbev_pack_conv3x3_weight_bf16x3(w.data_ptr(), cout, cin, cmap, K, packed.data_ptr(),
+                                                          _stream(packed))
+                _native.check(st, "mvbev_pack_conv3x3_weight_bf16x3")
             self.packed, self._key = packed, key
         return self.packed
 
@@ -203,12 +219,13 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Low-level form: ``x`` addressed through ``desc`` (``mvbev_conv_desc``)."""
     _require_cuda(x, packed)
-    if x.dtype != torch.float32:
-        raise TypeError("x must be float32")
+    bf16x3 = packed.dtype == torch.bfloat16
+    if x.dtype not in ((torch.float32, torch.float16) if bf16x3 else (torch.float32,)):
+        raise TypeError(f"x dtype {x.dtype} not supported by the {'bf16x3' if bf16x3 else 'fp32'} conv")
     B, H, W, out_rows = desc.B, desc.H, desc.W, desc.out_rows
     need = (desc.K // desc.group - 1) * desc.group_stride + (B - 1) * desc.batch_stride + \
         desc.group * desc.in_rows * W
-    if x.untyped_storage().nbytes() // 4 - x.storage_offset() < need:
+    if x.untyped_storage().nbytes() // x.element_size() - x.storage_offset() < need:
         raise ValueError("x's storage is too small for the conv descriptor")
     if out is None:
         out = torch.empty((B, cout, out_rows, W), dtype=torch.float32, device=x.device)
@@ -221,11 +238,18 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
         _require_cuda(init)
         if init.numel() != cout * H * W or not init.is_contiguous():
             raise ValueError("init must be a contiguous [Cout,H,W] tensor")
-    st = _native.load().mvbev_conv3x3_f32(x.data_ptr(), ctypes.byref(desc), packed.data_ptr(),
-                                          bias.data_ptr() if bias is not None else None,
-                                          init.data_ptr() if init is not None else None, cout, int(dilation),
-                                          int(bool(relu)), out.data_ptr(), _stream(x))
-    _native.check(st, "mvbev_conv3x3_f32")
+    lib = _native.load()
+    bp = bias.data_ptr() if bias is not None else None
+    ip = init.data_ptr() if init is not None else None
+    if bf16x3:
+        st = lib.mvbev_conv3x3_bf16x3(x.data_ptr(), int(x.dtype == torch.float16), ctypes.byref(desc),
+                                      packed.data_ptr(), bp, ip, cout, int(dilation), int(bool(relu)),
+                                      out.data_ptr(), _stream(x))
+        _native.check(st, "mvbev_conv3x3_bf16x3")
+    else:
+        st = lib.mvbev_conv3x3_f32(x.data_ptr(), ctypes.byref(desc), packed.data_ptr(), bp, ip, cout,
+                                   int(dilation), int(bool(relu)), out.data_ptr(), _stream(x))
+        _native.check(st, "mvbev_conv3x3_f32")
     return out
 
 

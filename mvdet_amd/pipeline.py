@@ -3,7 +3,7 @@
 Data layout in HBM (per device, per batch size B):
 
 * ``slab``  — the warped ground-plane features, **view-major**
-  ``[S, B, Cs, Ho, Wo]`` fp32 (S view slots, Cs = C rounded up to 8).  View ``v``'s
+  ``[S, B, Cs, Ho, Wo]`` fp32 (fp16 for the config-4 fp16-storage path) (S view slots, Cs = C rounded up to 8).  View ``v``'s
   warp writes slot ``slot_of[v]`` directly; this *is* the concatenation of
   ``persp_trans_detector.py:77`` (zero-copy).  View-major keeps each GPU's share
   of the views contiguous, so the multi-GPU all-gather needs no repack
@@ -15,6 +15,9 @@ Data layout in HBM (per device, per batch size B):
   more input channels every forward.
 * ``y1``, ``y2`` — conv1 / conv2 activations ``[B, 512, rows, Wo]`` (rows = the
   output band plus the halo the next layer needs; the whole grid on one GPU).
+
+``precision`` selects the conv1/conv2 kernel: "fp32" (fp32 MFMA) or "bf16x3"
+(hi/lo bf16 split, three bf16 MFMA passes, fp32 accumulate; fp32-class accuracy).
 
 ``warp_view`` is a5 for one view; ``fuse`` is a7-a9 (a10, the same-size bilinear
 interpolate of ``:82``, is an exact identity and is elided).  Nothing here
@@ -60,7 +63,14 @@ class ProjectFuse:
     """
 
     def __init__(self, proj_mats: Sequence[torch.Tensor], src_hw: Tuple[int, int], grid_hw: Tuple[int, int],
-                 channels: int, mid_channels: int = 512, slot_views: Optional[Sequence[Optional[int]]] = None):
+                 channels: int, mid_channels: int = 512, slot_views: Optional[Sequence[Optional[int]]] = None,
+                 precision: str = "fp32", slab_dtype: torch.dtype = torch.float32):
+        if slab_dtype not in (torch.float32, torch.float16):
+            raise ValueError("slab_dtype must be float32 or float16")
+        if slab_dtype == torch.float16 and precision != "bf16x3":
+            raise ValueError("an fp16 slab needs precision='bf16x3' (the fp32-MFMA conv reads fp32)")
+        self.precision = precision
+        self.slab_dtype = slab_dtype
         self.num_cam = len(proj_mats)
         self.src_hw = (int(src_hw[0]), int(src_hw[1]))
         self.grid_hw = (int(grid_hw[0]), int(grid_hw[1]))
@@ -83,9 +93,9 @@ class ProjectFuse:
             for c in range(self.Cs):
                 chan_map.append(v * self.C + c if (v is not None and c < self.C) else -1)
         nc = self.num_cam * self.C
-        self.pack1 = ops.PackedConv3x3(chan_map)
-        self.pack_coord = ops.PackedConv3x3([nc, nc + 1] + [-1] * (ops.KC - 2))
-        self.pack2 = ops.PackedConv3x3()
+        self.pack1 = ops.PackedConv3x3(chan_map, precision)
+        self.pack_coord = ops.PackedConv3x3([nc, nc + 1] + [-1] * (ops.KC - 2))  # once per weights: fp32
+        self.pack2 = ops.PackedConv3x3(None, precision)
         self._ws: Dict[tuple, Workspace] = {}
         self._coord_key = None
         self._coord_term: Optional[torch.Tensor] = None
@@ -99,7 +109,7 @@ class ProjectFuse:
         key = (str(device), int(B), band)
         ws = self._ws.get(key)
         if ws is None:
-            slab = torch.zeros((self.S, B, self.Cs, H, W), dtype=torch.float32, device=device)
+            slab = torch.zeros((self.S, B, self.Cs, H, W), dtype=self.slab_dtype, device=device)
             y1r, y2r = band_rows(band[0], band[1], H)
             y1 = torch.empty((B, self.mid, y1r[1] - y1r[0], W), dtype=torch.float32, device=device)
             y2 = torch.empty((B, self.mid, y2r[1] - y2r[0], W), dtype=torch.float32, device=device)

@@ -119,10 +119,15 @@ def test_warp_rejects_bad_input_like_kornia():
 
 # ---------------------------------------------------------------------------------- convs
 
+# normwise bounds of the conv kernels vs torch fp32 (the 1e-3 parity gate is the outer bound)
+CONV_TOL = {"fp32": 2e-5, "bf16x3": 5e-5}
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 @pytest.mark.parametrize("B,cin,H,W,d,relu,bias", [(1, 8, 4, 32, 1, True, True), (1, 770, 13, 37, 1, True, True),
                                                    (2, 19, 9, 70, 2, False, True), (1, 512, 20, 33, 2, True, True),
                                                    (1, 3, 3, 5, 1, False, False)])
-def test_conv3x3_vs_torch(B, cin, H, W, d, relu, bias):
+def test_conv3x3_vs_torch(B, cin, H, W, d, relu, bias, precision):
     from mvdet_amd import ops
     g = torch.Generator().manual_seed(cin * 7 + H)
     cout = 256 if cin < 100 else 128
@@ -135,13 +140,26 @@ def test_conv3x3_vs_torch(B, cin, H, W, d, relu, bias):
     K = ops.padded_channels(cin)
     xp = torch.full((B, K, H, W), 1e30)  # padding channels must not leak (zero weights)
     xp[:, :cin] = x
-    pk = ops.PackedConv3x3(list(range(cin)) + [-1] * (K - cin)).get(w.to(DEV))
+    pk = ops.PackedConv3x3(list(range(cin)) + [-1] * (K - cin), precision).get(w.to(DEV))
     got = ops.conv3x3(xp.to(DEV), pk, cout, b.to(DEV) if bias else None, d, relu).cpu()
-    assert_parity(got, ref, "conv3x3", normwise_tol=2e-5)
+    assert_parity(got, ref, f"conv3x3 {precision}", normwise_tol=CONV_TOL[precision])
 
 
+def test_conv3x3_bf16x3_fp16_input_is_exact_split():
+    """fp16-storage input (config 4): an fp16 value is exactly bf16 hi + lo."""
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(77)
+    x = torch.rand(2, 64, 11, 40, generator=g).half()
+    w = (torch.rand(128, 64, 3, 3, generator=g) - 0.5) / 24
+    ref = F.relu(F.conv2d(x.float(), w, None, padding=1))
+    pk = ops.PackedConv3x3(None, "bf16x3").get(w.to(DEV))
+    got = ops.conv3x3(x.to(DEV), pk, 128, None, 1, True).cpu()
+    assert_parity(got, ref, "bf16x3 f16-in", normwise_tol=5e-5)
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 @pytest.mark.parametrize("d", [1, 2])
-def test_conv3x3_row_band_and_init(d):
+def test_conv3x3_row_band_and_init(d, precision):
     """Row bands (the multi-GPU fusion) and the init (coord-term) epilogue."""
     from mvdet_amd import ops
     g = torch.Generator().manual_seed(40 + d)
@@ -150,7 +168,7 @@ def test_conv3x3_row_band_and_init(d):
     w = (torch.rand(cout, cin, 3, 3, generator=g) - 0.5) / 12
     init = torch.rand(cout, H, W, generator=g)
     ref = F.relu(F.conv2d(x, w, None, padding=d, dilation=d) + init)
-    pk = ops.PackedConv3x3().get(w.to(DEV))
+    pk = ops.PackedConv3x3(None, precision).get(w.to(DEV))
     xd, initd = x.to(DEV), init.to(DEV)
     for (a, b_) in ((0, 7), (5, 19), (16, 23)):
         in0, in1 = max(0, a - d), min(H, b_ + d)
@@ -158,7 +176,7 @@ def test_conv3x3_row_band_and_init(d):
         desc = ops.conv_desc(B, cin, H, W, group=cin, group_stride=0, batch_stride=cin * (in1 - in0) * W,
                              in_row0=in0, in_rows=in1 - in0, out_row0=a, out_rows=b_ - a)
         got = ops.conv3x3_desc(xin, desc, pk, cout, init=initd, dilation=d, relu=True).cpu()
-        assert_parity(got, ref[:, :, a:b_], f"band {a}:{b_}", normwise_tol=2e-5)
+        assert_parity(got, ref[:, :, a:b_], f"band {a}:{b_}", normwise_tol=CONV_TOL[precision])
 
 
 @pytest.mark.parametrize("C,H,W,d", [(512, 12, 36, 4), (7, 5, 70, 1), (33, 9, 130, 2)])
@@ -247,8 +265,8 @@ def test_fill_coord_map_matches_reference_coord_map():
 
 # ---------------------------------------------------------------------------------- full size
 
-@pytest.mark.parametrize("cfg", [1, 2])
-def test_full_size_project_fuse_vs_oracle(cfg):
+@pytest.mark.parametrize("cfg,precision", [(1, "fp32"), (2, "fp32"), (1, "bf16x3"), (2, "bf16x3")])
+def test_full_size_project_fuse_vs_oracle(cfg, precision):
     """BASELINE configs 1 and 2 at full size, HIP path vs the CPU oracle on identical inputs."""
     from mvdet_amd import ProjectFuse, synthetic
     from mvdet_amd.geometry import projection_matrices
@@ -260,7 +278,7 @@ def test_full_size_project_fuse_vs_oracle(cfg):
     feats = [synthetic.synthetic_features(B, C, hb, up, seed=1000 * cfg + v) for v in range(ds.num_cam)]
     params = fixtures.head_params(ds.num_cam, seed=cfg, C=C)
     pm = projection_matrices(ds)
-    eng = ProjectFuse(pm, tuple(up), tuple(ds.reducedgrid_shape), C)
+    eng = ProjectFuse(pm, tuple(up), tuple(ds.reducedgrid_shape), C, precision=precision)
     mc = torch.nn.Sequential(torch.nn.Conv2d(C * ds.num_cam + 2, 512, 3, padding=1), torch.nn.ReLU(),
                              torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
                              torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False))

@@ -40,6 +40,8 @@ def timeit(fn, reps):
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3"],
+                    help="conv1/conv2 arithmetic: fp32 MFMA or 3xbf16 split (fp32-class accuracy)")
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="warp,conv1,conv2,conv3")
@@ -54,7 +56,7 @@ def main():
     dev = torch.device("cuda:0")
     pm = projection_matrices(ds)
     mc = build_mc(C, N, head_params(N, args.config, C), dev)
-    eng = ProjectFuse(pm, up, (ho, wo), C)
+    eng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision)
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=v, device=dev) for v in range(N)]
     ws = eng.workspace(B, dev)
     with torch.no_grad():

@@ -81,28 +81,16 @@ def cpu_baseline(ds, B, C, pm, params, frames: int):
                        + ", ".join(f"{k}={v:.3f}" for k, v in stages.items()))
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3"],
-                    help="conv1/conv2 arithmetic: fp32 MFMA or 3xbf16 split (fp32-class accuracy)")
-    ap.add_argument("--config", type=int, default=2, help="BASELINE.json config index (1-based)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=0, help="frames for the CPU baseline (0 = auto)")
-    args = ap.parse_args()
+DTYPE_LABEL = {"fp32": "f32 (fp32-input MFMA, exact fp32 products, fp32 accumulate)",
+               "bf16x3": "f32 (3xbf16-split products hi*hi+hi*lo+lo*hi on the bf16 MFMA, fp32 accumulate)"}
+BF16_MFMA_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16
 
+
+def run_single(args, precision, steps, warmup, with_cpu):
     from mvdet_amd import ProjectFuse, synthetic
     from mvdet_amd.geometry import projection_matrices, touched_footprint
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        from mvdet_amd import parallel
-        return parallel.bench_main(args)
-
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     spec = synthetic.CONFIGS[args.config]
@@ -114,14 +102,18 @@ def main():
     pm = projection_matrices(ds)
     params = head_params(N, seed=args.config, C=C)
     mc = build_mc(C, N, params, dev)
-    eng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision)
+    half = args.config == 4
+    eng = ProjectFuse(pm, up, (ho, wo), C, precision=precision,
+                      slab_dtype=torch.float16 if half else torch.float32)
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * args.config + v,
-                                          device=dev) for v in range(N)]
+                                          device=dev).to(torch.float16 if half else torch.float32)
+             for v in range(N)]
     ws = eng.workspace(B, dev)
     views = list(range(N))
 
-    K, W = args.steps, args.warmup
+    K, W = steps, warmup
     ev = {k: [torch.cuda.Event(enable_timing=True) for _ in range(K)] for k in ("warp", "conv1", "conv2", "conv3")}
+    end_ev = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
 
     def step(i=None):
         if i is not None:
@@ -130,7 +122,6 @@ def main():
         mark = (lambda stage: ev[stage][i].record()) if i is not None else None
         return eng.fuse(ws, mc, mark=mark)
 
-    end_ev = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
     with torch.no_grad():
         for _ in range(W):
             step()
@@ -149,58 +140,101 @@ def main():
     t_c1 = avg(ev["conv1"], ev["conv2"])
     t_c2 = avg(ev["conv2"], ev["conv3"])
     t_c3 = avg(ev["conv3"], end_ev)
-
-    frames = B * K
-    value = frames / dt
-    # algorithmic work
-    cin = N * C + 2
-    conv1_flop = 2.0 * B * ho * wo * 9 * cin * 512
+    value = B * K / dt
+    # algorithmic work; conv1 runs over the N*C view channels per step (the
+    # 2 coord channels are folded into a per-weight-version init term)
+    conv1_flop = 2.0 * B * ho * wo * 9 * (N * C) * 512
     conv2_flop = 2.0 * B * ho * wo * 9 * 512 * 512
+    s = 2 if half else 4
     tv = [touched_footprint(M.numpy(), up, (ho, wo)) for M in pm]
-    warp_bytes = sum(4.0 * B * C * (t + ho * wo) for t in tv)
+    warp_bytes = sum(s * B * C * (t + ho * wo) for t in tv)
     conv3_bytes = 4.0 * B * ho * wo * (512 + 1)
-    conv1_tfs = conv1_flop / (t_c1 * 1e-3) / 1e12
+    conv1_alg_tfs = conv1_flop / (t_c1 * 1e-3) / 1e12
+    if precision == "bf16x3":
+        # executed bf16 MFMA work: 3 passes x 10/9 (the zero-padded 10th tap of each K chunk)
+        achieved, peak = conv1_alg_tfs * 3 * 10 / 9, BF16_MFMA_PEAK_TFS
+        kname = "conv3x3_bf16x3 (conv1)"
+    else:
+        achieved, peak = conv1_alg_tfs, FP32_MFMA_PEAK_TFS
+        kname = "conv3x3_mfma_f32 (conv1)"
     traffic = None
-    tfile = ROOT / "profiles" / f"traffic_cfg{args.config}.json"
+    tfile = ROOT / "profiles" / f"traffic_cfg{args.config}_{precision}.json"
     if tfile.exists():
         traffic = json.loads(tfile.read_text()).get("conv1_hbm_bytes_per_launch")
-
-    result = {
-        "metric": "multi-view frames/sec (project+fuse)",
+    res = {
         "value": round(value, 3),
-        "unit": "frames/s",
-        "n_gpus": 1,
-        "steps": K,
-        "warmup": W,
         "ms_per_step": round(dt * 1e3 / K, 4),
-        "higher_is_better": True,
-        "scaling": "strong",
-        "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (ReLU N(0,1) features upsampled 3x, synthetic pinhole rig through the reference matrix chain, random-init fusion weights)",
+        "dtype": DTYPE_LABEL[precision],
         "config": {"workload": f"cfg{args.config}: {spec['name']}", "views": N, "channels": C, "batch": B,
-                   "src_hw": list(up), "grid_hw": [ho, wo], "parallelism": "single GPU"},
-        "roofline": {"kernel": "conv3x3_mfma_f32 (conv1, Cin=%d)" % cin, "bound": "mfma",
-                     "achieved": round(conv1_tfs, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                     "frac": round(conv1_tfs / FP32_MFMA_PEAK_TFS, 4), "traffic": traffic},
+                   "src_hw": list(up), "grid_hw": [ho, wo], "precision": precision,
+                   "storage": "fp16" if half else "fp32", "parallelism": "single GPU"},
+        "roofline": {"kernel": kname, "bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
+                     "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
+                     "algorithmic_fp32_tflops": round(conv1_alg_tfs, 2),
+                     "algorithmic_frac_of_fp32_peak": round(conv1_alg_tfs / FP32_MFMA_PEAK_TFS, 4)},
         "stages_ms": {"warp_all_views": round(t_warp, 4), "conv1": round(t_c1, 4), "conv2": round(t_c2, 4),
                       "conv3": round(t_c3, 4)},
         "stage_roofline": {
             "warp": {"bound": "hbm", "algorithmic_bytes": warp_bytes,
                      "achieved_GBs": round(warp_bytes / (t_warp * 1e-3) / 1e9, 1), "peak_GBs": HBM_PEAK_GBS},
-            "conv2": {"bound": "mfma", "achieved_TFs": round(conv2_flop / (t_c2 * 1e-3) / 1e12, 2),
-                      "peak_TFs": FP32_MFMA_PEAK_TFS},
+            "conv2": {"bound": "mfma", "algorithmic_fp32_TFs": round(conv2_flop / (t_c2 * 1e-3) / 1e12, 2)},
             "conv3": {"bound": "hbm", "achieved_GBs": round(conv3_bytes / (t_c3 * 1e-3) / 1e9, 1),
                       "peak_GBs": HBM_PEAK_GBS},
-            "whole_step_frac": round(((warp_bytes + conv3_bytes) / (HBM_PEAK_GBS * 1e9)
-                                      + (conv1_flop + conv2_flop) / (FP32_MFMA_PEAK_TFS * 1e12))
-                                     / (dt / K), 4),
         },
     }
-    if not args.no_cpu_baseline and rank == 0:
+    if with_cpu:
         frames_cpu = args.cpu_frames or (3 if args.config == 2 else 5)
-        result["cpu_baseline"] = cpu_baseline(ds, B, C, pm, params, frames_cpu)
-        result["speedup_vs_cpu"] = round(value / result["cpu_baseline"]["value"], 1)
+        res["cpu_baseline"] = cpu_baseline(ds, 1 if half else B, C, pm, params, frames_cpu)
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3"],
+                    help="conv1/conv2 arithmetic: 3xbf16 split (default) or fp32-input MFMA")
+    ap.add_argument("--config", type=int, default=2, help="BASELINE.json config index (1-based)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-alt", action="store_true", help="skip the other-precision comparison line")
+    ap.add_argument("--cpu-frames", type=int, default=0, help="frames for the CPU baseline (0 = auto)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        from mvdet_amd import parallel
+        return parallel.bench_main(args)
+
+    res = run_single(args, args.precision, args.steps, args.warmup, with_cpu=not args.no_cpu_baseline and rank == 0)
+    result = {
+        "metric": "multi-view frames/sec (project+fuse)",
+        "value": res["value"],
+        "unit": "frames/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": res["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": res["dtype"],
+        "data": "synthetic (ReLU N(0,1) features upsampled 3x, synthetic pinhole rig through the reference "
+                "matrix chain, random-init fusion weights)",
+        "config": res["config"],
+        "roofline": res["roofline"],
+        "cpu_baseline": res.get("cpu_baseline"),
+        "stages_ms": res["stages_ms"],
+        "stage_roofline": res["stage_roofline"],
+    }
+    if result["cpu_baseline"]:
+        result["speedup_vs_cpu"] = round(res["value"] / result["cpu_baseline"]["value"], 1)
+    if not args.no_alt:
+        other = "fp32" if args.precision == "bf16x3" else "bf16x3"
+        alt = run_single(args, other, max(3, args.steps // 2), 2, with_cpu=False)
+        result["alt_precision"] = {k: alt[k] for k in ("value", "ms_per_step", "dtype", "stages_ms")}
+        result["alt_precision"]["roofline"] = alt["roofline"]
     print(json.dumps(result))
 
 

@@ -11,7 +11,9 @@ What changes is the hot path (warp + concat + fusion), which runs on the HIP
 kernels of ``libmvbev.so`` through ``ProjectFuse``:
 * the per-view warp writes straight into the fused ground-plane tensor;
 * the coord channels are written once, not copied every forward;
-* conv1/conv2 are fp32-MFMA implicit GEMMs, conv3 a dot-product kernel;
+* conv1/conv2 are MFMA implicit GEMMs (default 3xbf16 split precision, fp32
+  accumulation — same parity as exact fp32; ``precision="fp32"`` selects the
+  fp32-input MFMA), conv3 a dot-product kernel;
 * the same-size final interpolate (an exact identity) is elided.
 
 Training (autograd through the hot path, ``trainer.py:38-49``) is not yet native
@@ -21,7 +23,6 @@ The library is loaded at construction on a GPU, so a missing build fails there.
 """
 from __future__ import annotations
 
-import numpy as np
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -34,7 +35,7 @@ from .pipeline import ProjectFuse
 
 
 class PerspTransDetector(nn.Module):
-    def __init__(self, dataset, arch: str = "resnet18", device=None):
+    def __init__(self, dataset, arch: str = "resnet18", device=None, precision: str = "bf16x3"):
         super().__init__()
         self.num_cam = dataset.num_cam
         self.img_shape, self.reducedgrid_shape = list(dataset.img_shape), list(dataset.reducedgrid_shape)
@@ -54,7 +55,7 @@ class PerspTransDetector(nn.Module):
                                             nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False))
         self.to(self._device)
         self.engine = ProjectFuse(self.proj_mats, tuple(self.upsample_shape), tuple(self.reducedgrid_shape),
-                                  out_channel)
+                                  out_channel, precision=precision)
 
     # -- hot path --------------------------------------------------------------------------
     def _needs_autograd(self) -> bool:

@@ -133,7 +133,7 @@ def bench_main(args) -> None:
 
     import numpy as np
 
-    from bench import FP32_MFMA_PEAK_TFS, build_mc, head_params
+    from bench import DTYPE_LABEL, FP32_MFMA_PEAK_TFS, build_mc, head_params
     from . import synthetic
     from .geometry import projection_matrices
     from .pipeline import ProjectFuse
@@ -153,7 +153,8 @@ def bench_main(args) -> None:
     ho, wo = ds.reducedgrid_shape
     pm = projection_matrices(ds)
     mc = build_mc(C, N, head_params(N, seed=args.config, C=C), dev)
-    vp = ViewParallel(lambda sv: ProjectFuse(pm, up, (ho, wo), C, slot_views=sv), pm, (ho, wo), rank, world)
+    vp = ViewParallel(lambda sv: ProjectFuse(pm, up, (ho, wo), C, slot_views=sv, precision=args.precision),
+                      pm, (ho, wo), rank, world)
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * args.config + v, device=dev)
              for v in vp.my_views]
     ws = vp.workspace(B, dev)
@@ -197,7 +198,7 @@ def bench_main(args) -> None:
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": DTYPE_LABEL[args.precision],
             "data": "synthetic (see single-GPU line)",
             "config": {"workload": f"cfg{args.config}: {spec['name']}", "views": N, "channels": C, "batch": B,
                        "src_hw": list(up), "grid_hw": [ho, wo],

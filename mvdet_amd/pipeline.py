@@ -16,8 +16,9 @@ Data layout in HBM (per device, per batch size B):
 * ``y1``, ``y2`` — conv1 / conv2 activations ``[B, 512, rows, Wo]`` (rows = the
   output band plus the halo the next layer needs; the whole grid on one GPU).
 
-``precision`` selects the conv1/conv2 kernel: "fp32" (fp32 MFMA) or "bf16x3"
-(hi/lo bf16 split, three bf16 MFMA passes, fp32 accumulate; fp32-class accuracy).
+``precision`` selects the conv1/conv2 kernel: "bf16x3" (default: hi/lo bf16 split,
+three bf16 MFMA passes, fp32 accumulate — the same parity vs the oracle as exact fp32,
+3x faster) or "fp32" (fp32-input MFMA, exact fp32 products).
 
 ``warp_view`` is a5 for one view; ``fuse`` is a7-a9 (a10, the same-size bilinear
 interpolate of ``:82``, is an exact identity and is elided).  Nothing here
@@ -64,7 +65,7 @@ class ProjectFuse:
 
     def __init__(self, proj_mats: Sequence[torch.Tensor], src_hw: Tuple[int, int], grid_hw: Tuple[int, int],
                  channels: int, mid_channels: int = 512, slot_views: Optional[Sequence[Optional[int]]] = None,
-                 precision: str = "fp32", slab_dtype: torch.dtype = torch.float32):
+                 precision: str = "bf16x3", slab_dtype: torch.dtype = torch.float32):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":

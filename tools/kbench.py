@@ -40,7 +40,7 @@ def timeit(fn, reps):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16x3"],
+    ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3"],
                     help="conv1/conv2 arithmetic: fp32 MFMA or 3xbf16 split (fp32-class accuracy)")
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--reps", type=int, default=20)

@@ -55,7 +55,7 @@ def head_params(num_cam, seed, C):
     return out
 
 
-def cpu_baseline(ds, B, C, pm, params, frames: int):
+def cpu_baseline(ds, B, C, pm, params, frames: int, config: int = 2):
     """The oracle (reference CPU path restated over torch-CPU ops) on the host cores."""
     from mvdet_amd import synthetic
     from oracle import cpu_path
@@ -63,7 +63,7 @@ def cpu_baseline(ds, B, C, pm, params, frames: int):
     threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
     torch.set_num_threads(threads)
     up = ds.upsample_shape
-    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * 2 + v)
+    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * config + v)
              for v in range(ds.num_cam)]
     tp = {k: torch.from_numpy(v) for k, v in params.items()}
     mats = [M.numpy() for M in pm]
@@ -184,7 +184,7 @@ def run_single(args, precision, steps, warmup, with_cpu):
     }
     if with_cpu:
         frames_cpu = args.cpu_frames or (3 if args.config == 2 else 5)
-        res["cpu_baseline"] = cpu_baseline(ds, 1 if half else B, C, pm, params, frames_cpu)
+        res["cpu_baseline"] = cpu_baseline(ds, 1 if half else B, C, pm, params, frames_cpu, args.config)
     return res
 
 

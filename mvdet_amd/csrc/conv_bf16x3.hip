@@ -78,18 +78,24 @@ template <typename T> __device__ inline float ld(const T* p);
 template <> __device__ inline float ld<float>(const float* p) { return *p; }
 template <> __device__ inline float ld<_Float16>(const _Float16* p) { return (float)*p; }
 
-template <typename TIn, int DIL, bool RELU, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void conv_kernel(const Args a) {
+#ifndef MVBEV_B3_MINWAVES
+#define MVBEV_B3_MINWAVES 2
+#endif
+#ifndef MVBEV_B3_DBUF
+#define MVBEV_B3_DBUF 0
+#endif
+
+template <typename TIn, int DIL, bool RELU, int NW, bool DBUF>
+__global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const Args a) {
   constexpr int NT = 64 * NW;
   constexpr int TH = NW;                 // NW/2 row pairs, 2 channel halves
   constexpr int XH = TH + 2 * DIL, XW = TW + 2 * DIL;
   constexpr int XPIX = XH * XW;          // halo pixels per chunk (8 channels each)
   constexpr int XPT = (XPIX + NT - 1) / NT;
   constexpr int WLD = (W16 + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) u32x4 lds[W16 + 2 * XPIX];
-  u32x4* Wl = lds;              // [part][kb][h][co] pieces of 8 bf16
-  u32x4* Xhi = lds + W16;       // [r][c] pieces of 8 bf16 channels
-  u32x4* Xlo = Xhi + XPIX;
+  constexpr int BUF = W16 + 2 * XPIX;   // 16-B pieces per LDS buffer
+  __shared__ __attribute__((aligned(16))) u32x4 lds[(DBUF ? 2 : 1) * BUF];
+  // buffer layout: W [part][kb][h][co] pieces of 8 bf16, then X hi [r][c], X lo [r][c]
 
   const int wg = xcd_remap(blockIdx.x, a.nwg);
   const int cot = wg % a.n_cot;
@@ -138,8 +144,11 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_kernel(const Args a) {
       _Pragma("unroll") for (int j = 0; j < KC; ++j) xreg[i][j] = ld<TIn>(xc_ + j * plane + xoff[i]); \
     }                                                                                        \
   } while (0)
-#define B3_STORE()                                                                           \
+#define B3_STORE(buf)                                                                        \
   do {                                                                                       \
+    u32x4* Wl = lds + (buf) * BUF;                                                           \
+    u32x4* Xhi = Wl + W16;                                                                   \
+    u32x4* Xlo = Xhi + XPIX;                                                                 \
     _Pragma("unroll") for (int i = 0; i < WLD; ++i) {                                        \
       if (W16 % NT == 0 || tid + NT * i < W16) Wl[tid + NT * i] = wreg[i];                   \
     }                                                                                        \
@@ -174,12 +183,9 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_kernel(const Args a) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = floatx16{0};
 
-  B3_LOAD(0);
-  for (int ch = 0; ch < a.nchunks; ++ch) {
-    __syncthreads();
-    B3_STORE();
-    __syncthreads();
-    if (ch + 1 < a.nchunks) B3_LOAD(ch + 1);
+  auto compute = [&](const u32x4* Wl) __attribute__((always_inline)) {
+    const u32x4* Xhi = Wl + W16;
+    const u32x4* Xlo = Xhi + XPIX;
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
       bf16x8 ahi[2], alo[2], bhi[2], blo[2];
@@ -202,6 +208,28 @@ __global__ __launch_bounds__(64 * NW, 2) void conv_kernel(const Args a) {
           acc[ct][pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[ct], blo[pt], acc[ct][pt], 0, 0, 0);
           acc[ct][pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[ct], bhi[pt], acc[ct][pt], 0, 0, 0);
         }
+    }
+  };
+
+  B3_LOAD(0);
+  if constexpr (DBUF) {
+    B3_STORE(0);
+    __syncthreads();
+    for (int ch = 0; ch < a.nchunks; ++ch) {
+      const int cur = ch & 1;
+      const bool more = ch + 1 < a.nchunks;
+      if (more) B3_LOAD(ch + 1);
+      compute(lds + cur * BUF);
+      if (more) B3_STORE(cur ^ 1);
+      __syncthreads();
+    }
+  } else {
+    for (int ch = 0; ch < a.nchunks; ++ch) {
+      __syncthreads();
+      B3_STORE(0);
+      __syncthreads();
+      if (ch + 1 < a.nchunks) B3_LOAD(ch + 1);
+      compute(lds);
     }
   }
 #undef B3_LOAD
@@ -261,7 +289,8 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   a.nwg = (int)nwg;
   hipStream_t s = as_stream(stream);
 #define B3_LAUNCH(D, R)                                                                   \
-  hipLaunchKernelGGL((conv_kernel<TIn, D, R, NW>), dim3((unsigned)nwg), dim3(64 * NW), 0, s, a)
+  hipLaunchKernelGGL((conv_kernel<TIn, D, R, NW, MVBEV_B3_DBUF != 0>), dim3((unsigned)nwg), dim3(64 * NW), \
+                     0, s, a)
   if (dilation == 1) {
     if (relu) B3_LAUNCH(1, true); else B3_LAUNCH(1, false);
   } else if (dilation == 2) {

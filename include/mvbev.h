@@ -97,6 +97,14 @@ typedef struct mvbev_warp_view {
  * persp_trans_detector.py:62-75, warp + concat).  views: host array of nviews (<= 16). */
 int mvbev_warp_views_f32(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
                          int64_t H, int64_t W, int64_t Ho, int64_t Wo, void* stream);
+/* Same, writing the split-bf16 blocked layout (MVBEV_LAYOUT_SPLIT_BF16) the 3xbf16 conv
+ * reads without any conversion: for (batch, group of 8 channels, row, col) 32 bytes = bf16
+ * hi[8] then bf16 lo[8], value = hi + lo.  dst_strides are in 32-byte units
+ * {batch, channel group, row, col (must be 1)}; channels beyond C in the last group are 0.
+ * src is fp32 (src_is_f16 = 0) or fp16. */
+int mvbev_warp_views_split_bf16(const mvbev_warp_view* views, int nviews, int src_is_f16,
+                                int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
+                                void* stream);
 /* fp16 storage for src and dst, fp32 math. */
 int mvbev_warp_views_f16(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
                          int64_t H, int64_t W, int64_t Ho, int64_t Wo, void* stream);
@@ -146,16 +154,22 @@ int mvbev_conv3x3_f32(const float* x, const mvbev_conv_desc* desc, const float* 
                       const float* bias, const float* init, int64_t Cout, int dilation,
                       int relu, float* y, void* stream);
 
+/* Input layouts of mvbev_conv3x3_bf16x3 (descriptor strides are always in 4-byte
+ * "channel-element" units, i.e. as for an fp32 tensor of the same logical shape). */
+#define MVBEV_LAYOUT_F32 0        /* plain fp32 channel planes */
+#define MVBEV_LAYOUT_F16 1        /* plain fp16 channel planes (strides in elements) */
+#define MVBEV_LAYOUT_SPLIT_BF16 2 /* per (8-channel group, pixel): bf16 hi[8], bf16 lo[8] */
+
 /* 3xbf16 split-precision variant of mvbev_conv3x3_f32 (same descriptor and semantics):
  * a*b ~= a_hi*b_hi + a_hi*b_lo + a_lo*b_hi on the bf16 MFMA, fp32 accumulation; ~2^-16
- * relative per product (fp32-class; see conv_bf16x3.hip).  x is fp32 (x_is_f16 = 0) or
- * fp16 storage (x_is_f16 = 1, e.g. the config-4 fp16 slab); y is fp32.
+ * relative per product (fp32-class; see conv_bf16x3.hip).  x_layout: MVBEV_LAYOUT_*
+ * (fp32, the config-4 fp16 slab, or the pre-split slab); y is fp32.
  * Weights packed by mvbev_pack_conv3x3_weight_bf16x3 (bytes: mvbev_conv3x3_packed_bytes_bf16x3). */
 size_t mvbev_conv3x3_packed_bytes_bf16x3(int64_t Cout, int64_t K);
 int mvbev_pack_conv3x3_weight_bf16x3(const float* w, int64_t Cout, int64_t Cin_w,
                                      const int32_t* chan_map, int64_t K, void* w_packed,
                                      void* stream);
-int mvbev_conv3x3_bf16x3(const void* x, int x_is_f16, const mvbev_conv_desc* desc,
+int mvbev_conv3x3_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* desc,
                          const void* w_packed, const float* bias, const float* init,
                          int64_t Cout, int dilation, int relu, float* y, void* stream);
 

@@ -20,6 +20,7 @@ EXPORTS = (
     "mvbev_warp_perspective_f16",
     "mvbev_warp_views_f32",
     "mvbev_warp_views_f16",
+    "mvbev_warp_views_split_bf16",
     "mvbev_fill_coord_map_f32",
     "mvbev_conv3x3_packed_floats",
     "mvbev_pack_conv3x3_weight_f32",
@@ -31,6 +32,7 @@ EXPORTS = (
 )
 
 KC = 8    # MVBEV_CONV_KC
+LAYOUT_F32, LAYOUT_F16, LAYOUT_SPLIT_BF16 = 0, 1, 2  # MVBEV_LAYOUT_*
 BN = 128  # MVBEV_CONV_BN
 
 _i64 = ctypes.c_int64
@@ -69,6 +71,9 @@ def _declare(lib):
         fn = getattr(lib, name)
         fn.restype = ctypes.c_int
         fn.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64, _i64, _p]
+    lib.mvbev_warp_views_split_bf16.restype = ctypes.c_int
+    lib.mvbev_warp_views_split_bf16.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, ctypes.c_int, _i64, _i64,
+                                                _i64, _i64, _i64, _i64, _p]
     lib.mvbev_fill_coord_map_f32.restype = ctypes.c_int
     lib.mvbev_fill_coord_map_f32.argtypes = [_p, _i64, _i64, _i64, _i64x4, _p]
     lib.mvbev_conv3x3_packed_floats.restype = ctypes.c_size_t

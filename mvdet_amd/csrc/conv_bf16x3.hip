@@ -22,6 +22,8 @@
 // channels (2x2 accumulators of 32x32, the same epilogue as the fp32 kernel).
 #include "common.h"
 
+#include <type_traits>
+
 namespace mvbev {
 namespace b3 {
 
@@ -74,6 +76,10 @@ struct Args {
   int tiles_x, tiles_y, n_cot, nwg;
 };
 
+// Input tag: the split-bf16 blocked layout written by mvbev_warp_views_split_bf16 and by this
+// kernel's own split epilogue (per pixel and 8-channel group: 16 B hi, 16 B lo).
+struct SplitIn {};
+
 template <typename T> __device__ inline float ld(const T* p);
 template <> __device__ inline float ld<float>(const float* p) { return *p; }
 template <> __device__ inline float ld<_Float16>(const _Float16* p) { return (float)*p; }
@@ -111,7 +117,6 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
   const int l32 = lane & 31, kh = lane >> 5;
 
   const int64_t plane = (int64_t)a.in_rows * W;
-  const TIn* xb = static_cast<const TIn*>(a.x) + (int64_t)b * a.batch_stride;
   const u32x4* wsrc = a.wp + (int64_t)cot * W16;
   const int64_t wchunk = (int64_t)a.n_cot * W16;
   const int chunks_per_group = a.group / KC;
@@ -129,8 +134,11 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
     xoff[i] = xok[i] ? (int)((int64_t)by * W + gx) : 0;
   }
 
+  constexpr bool SPLIT = std::is_same<TIn, SplitIn>::value;
+  using XElem = typename std::conditional<SPLIT, float, TIn>::type;  // element type when not split
   u32x4 wreg[WLD];
-  float xreg[XPT][KC];
+  float xreg[XPT][SPLIT ? 1 : KC];
+  u32x4 xs[XPT][SPLIT ? 2 : 1];
 #define B3_LOAD(ch)                                                                          \
   do {                                                                                       \
     const u32x4* ws_ = wsrc + (int64_t)(ch) * wchunk;                                        \
@@ -138,10 +146,20 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
       if (W16 % NT == 0 || tid + NT * i < W16) wreg[i] = ws_[tid + NT * i];                  \
     }                                                                                        \
     const int g_ = (ch) / chunks_per_group;                                                  \
-    const TIn* xc_ =                                                                         \
-        xb + g_ * a.group_stride + (int64_t)((ch) - g_ * chunks_per_group) * KC * plane;     \
-    _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                        \
-      _Pragma("unroll") for (int j = 0; j < KC; ++j) xreg[i][j] = ld<TIn>(xc_ + j * plane + xoff[i]); \
+    const int64_t cb_ = (int64_t)b * a.batch_stride + g_ * a.group_stride +                  \
+                        (int64_t)((ch) - g_ * chunks_per_group) * KC * plane;                \
+    if constexpr (SPLIT) {                                                                   \
+      const u32x4* xc_ = static_cast<const u32x4*>(a.x) + cb_ / 4;                           \
+      _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                      \
+        xs[i][0] = xc_[2 * xoff[i]];                                                         \
+        xs[i][1] = xc_[2 * xoff[i] + 1];                                                     \
+      }                                                                                      \
+    } else {                                                                                 \
+      const XElem* xc_ = static_cast<const XElem*>(a.x) + cb_;                               \
+      _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                      \
+        _Pragma("unroll") for (int j = 0; j < KC; ++j)                                       \
+          xreg[i][j] = ld<XElem>(xc_ + j * plane + xoff[i]);                                 \
+      }                                                                                      \
     }                                                                                        \
   } while (0)
 #define B3_STORE(buf)                                                                        \
@@ -154,7 +172,13 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
     }                                                                                        \
     _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                        \
       const int p = tid + NT * i;                                                            \
-      if (XPIX % NT == 0 || p < XPIX) {                                                      \
+      if constexpr (SPLIT) {                                                                 \
+        if (XPIX % NT == 0 || p < XPIX) {                                                    \
+          const u32x4 z_ = {0u, 0u, 0u, 0u};                                                 \
+          Xhi[p] = xok[i] ? xs[i][0] : z_;                                                   \
+          Xlo[p] = xok[i] ? xs[i][1] : z_;                                                   \
+        }                                                                                    \
+      } else if (XPIX % NT == 0 || p < XPIX) {                                               \
         bf16x8 hi, lo;                                                                       \
         _Pragma("unroll") for (int j = 0; j < KC; ++j) {                                     \
           const float v = xok[i] ? xreg[i][j] : 0.f;                                         \
@@ -332,10 +356,13 @@ int mvbev_pack_conv3x3_weight_bf16x3(const float* w, int64_t Cout, int64_t Cin_w
   return MVBEV_OK;
 }
 
-int mvbev_conv3x3_bf16x3(const void* x, int x_is_f16, const mvbev_conv_desc* desc,
+int mvbev_conv3x3_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* desc,
                          const void* w_packed, const float* bias, const float* init,
                          int64_t Cout, int dilation, int relu, float* y, void* stream) {
-  if (x_is_f16)
+  if (x_layout == MVBEV_LAYOUT_SPLIT_BF16)
+    return mvbev::b3::launch<mvbev::b3::SplitIn>(x, desc, w_packed, bias, init, Cout, dilation,
+                                                 relu, y, stream);
+  if (x_layout == MVBEV_LAYOUT_F16)
     return mvbev::b3::launch<_Float16>(x, desc, w_packed, bias, init, Cout, dilation, relu, y,
                                        stream);
   return mvbev::b3::launch<float>(x, desc, w_packed, bias, init, Cout, dilation, relu, y, stream);

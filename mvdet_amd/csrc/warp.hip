@@ -49,7 +49,25 @@ struct WarpArgs {
   int nviews, B, C, H, W, Ho, Wo, tiles_x, tiles, chunks, nwg;
 };
 
-template <typename T, int UNROLL>
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// SPLIT output: the "split-bf16 blocked" layout consumed by the 3xbf16 conv (see
+// mvbev.h MVBEV_LAYOUT_SPLIT_BF16): per (batch, group of 8 channels, row, col) 32 bytes =
+// bf16 hi[8] then bf16 lo[8] with x = hi + lo (+ ~2^-17 relative); dst strides in 32-B units.
+__device__ inline void store_split8(u32x4_t* dst, const float (&v)[8]) {
+  bf16x8_t hi, lo;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h = (__bf16)v[j];
+    hi[j] = h;
+    lo[j] = (__bf16)(v[j] - (float)h);
+  }
+  dst[0] = __builtin_bit_cast(u32x4_t, hi);
+  dst[1] = __builtin_bit_cast(u32x4_t, lo);
+}
+
+template <typename T, int UNROLL, bool SPLIT>
 __global__ __launch_bounds__(256) void warp_tile_kernel(const WarpArgs a) {
   // Logical block order (batch*view, channel chunk, tile) with tile fastest, dealt to the
   // XCDs in contiguous ranges: neighbouring tiles of one plane share an L2 (their source
@@ -94,16 +112,11 @@ __global__ __launch_bounds__(256) void warp_tile_kernel(const WarpArgs a) {
   const float ix = ((x + 1.f) / 2.f) * (float)(W - 1);
   const float iy = ((y + 1.f) / 2.f) * (float)(H - 1);
 
-  T* out = static_cast<T*>(vw.dst) + (int64_t)b * vw.dB + (int64_t)v * vw.dH + u;
-  const int64_t dC = vw.dC;
   const bool finite = isfinite(ix) && isfinite(iy);
-  if (!finite || !(ix > -1.f && ix < (float)W && iy > -1.f && iy < (float)H)) {
-    const float fill = finite ? 0.f : __builtin_nanf("");
-    for (int c = c_begin; c < c_end; ++c) out[(int64_t)c * dC] = from_f32<T>(fill);
-    return;
-  }
+  const bool inside = finite && ix > -1.f && ix < (float)W && iy > -1.f && iy < (float)H;
+  const float fill = finite ? 0.f : __builtin_nanf("");
   const float fx0 = floorf(ix), fy0 = floorf(iy);
-  const int x0 = (int)fx0, y0 = (int)fy0;
+  const int x0 = inside ? (int)fx0 : 0, y0 = inside ? (int)fy0 : 0;
   const float fx1 = fx0 + 1.f, fy1 = fy0 + 1.f;
   // torch GridSampler bilinear weights (nw, ne, sw, se)
   const float w_nw = (fx1 - ix) * (fy1 - iy);
@@ -119,57 +132,72 @@ __global__ __launch_bounds__(256) void warp_tile_kernel(const WarpArgs a) {
   const int64_t sH = vw.sH, sW = vw.sW, sC = vw.sC;
   const int64_t o_nw = cy0 * sH + cx0 * sW, o_ne = cy0 * sH + cx1 * sW;
   const int64_t o_sw = cy1 * sH + cx0 * sW, o_se = cy1 * sH + cx1 * sW;
-
   const T* base = static_cast<const T*>(vw.src) + (int64_t)b * vw.sB;
-  int c = c_begin;
-  for (; c + UNROLL <= c_end; c += UNROLL) {
-    float vnw[UNROLL], vne[UNROLL], vsw[UNROLL], vse[UNROLL];
-#pragma unroll
-    for (int k = 0; k < UNROLL; ++k) {
-      const T* pc = base + (int64_t)(c + k) * sC;
-      vnw[k] = to_f32<T>(pc[o_nw]);
-      vne[k] = to_f32<T>(pc[o_ne]);
-      vsw[k] = to_f32<T>(pc[o_sw]);
-      vse[k] = to_f32<T>(pc[o_se]);
-    }
-#pragma unroll
-    for (int k = 0; k < UNROLL; ++k) {
-      float acc = 0.f;
-      acc += (ok_nw ? vnw[k] : 0.f) * w_nw;
-      acc += (ok_ne ? vne[k] : 0.f) * w_ne;
-      acc += (ok_sw ? vsw[k] : 0.f) * w_sw;
-      acc += (ok_se ? vse[k] : 0.f) * w_se;
-      out[(int64_t)(c + k) * dC] = from_f32<T>(acc);
-    }
-  }
-  for (; c < c_end; ++c) {
+  auto sample = [&](int c) __attribute__((always_inline)) {
     const T* pc = base + (int64_t)c * sC;
+    const float vnw = to_f32<T>(pc[o_nw]), vne = to_f32<T>(pc[o_ne]);
+    const float vsw = to_f32<T>(pc[o_sw]), vse = to_f32<T>(pc[o_se]);
     float acc = 0.f;
-    acc += (ok_nw ? to_f32<T>(pc[o_nw]) : 0.f) * w_nw;
-    acc += (ok_ne ? to_f32<T>(pc[o_ne]) : 0.f) * w_ne;
-    acc += (ok_sw ? to_f32<T>(pc[o_sw]) : 0.f) * w_sw;
-    acc += (ok_se ? to_f32<T>(pc[o_se]) : 0.f) * w_se;
-    out[(int64_t)c * dC] = from_f32<T>(acc);
+    acc += (ok_nw ? vnw : 0.f) * w_nw;
+    acc += (ok_ne ? vne : 0.f) * w_ne;
+    acc += (ok_sw ? vsw : 0.f) * w_sw;
+    acc += (ok_se ? vse : 0.f) * w_se;
+    return acc;
+  };
+
+  if constexpr (SPLIT) {
+    u32x4_t* out = static_cast<u32x4_t*>(vw.dst) + 2 * ((int64_t)b * vw.dB + (int64_t)v * vw.dH + u);
+    const int64_t dG = 2 * vw.dC;
+    for (int g = c_begin / 8; g * 8 < c_end; ++g) {
+      float vals[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = g * 8 + j;
+        vals[j] = c < c_end ? (inside ? sample(c) : fill) : 0.f;
+      }
+      store_split8(out + g * dG, vals);
+    }
+    return;
+  } else {
+    T* out = static_cast<T*>(vw.dst) + (int64_t)b * vw.dB + (int64_t)v * vw.dH + u;
+    const int64_t dC = vw.dC;
+    if (!inside) {
+      for (int c = c_begin; c < c_end; ++c) out[(int64_t)c * dC] = from_f32<T>(fill);
+      return;
+    }
+    int c = c_begin;
+    for (; c + UNROLL <= c_end; c += UNROLL) {
+      float r[UNROLL];
+#pragma unroll
+      for (int k = 0; k < UNROLL; ++k) r[k] = sample(c + k);
+#pragma unroll
+      for (int k = 0; k < UNROLL; ++k) out[(int64_t)(c + k) * dC] = from_f32<T>(r[k]);
+    }
+    for (; c < c_end; ++c) out[(int64_t)c * dC] = from_f32<T>(sample(c));
   }
 }
 
 template <typename T>
-static int launch_warp(const WarpArgs& a, void* stream) {
-  hipLaunchKernelGGL((warp_tile_kernel<T, 4>), dim3((unsigned)a.nwg), dim3(256), 0,
-                     as_stream(stream), a);
+static int launch_warp(const WarpArgs& a, void* stream, bool split = false) {
+  if (split)
+    hipLaunchKernelGGL((warp_tile_kernel<T, 4, true>), dim3((unsigned)a.nwg), dim3(256), 0,
+                       as_stream(stream), a);
+  else
+    hipLaunchKernelGGL((warp_tile_kernel<T, 4, false>), dim3((unsigned)a.nwg), dim3(256), 0,
+                       as_stream(stream), a);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }
 
 template <typename T>
 static int finish_args_and_launch(WarpArgs& a, int64_t B, int64_t C, int64_t H, int64_t W,
-                                  int64_t Ho, int64_t Wo, void* stream) {
+                                  int64_t Ho, int64_t Wo, void* stream, bool split = false) {
   a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
   a.tiles_x = (int)ceil_div(Wo, kWarpTW);
   a.tiles = a.tiles_x * (int)ceil_div(Ho, kWarpTH);
   a.chunks = (int)ceil_div(C, kWarpCPB);
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
-  return launch_warp<T>(a, stream);
+  return launch_warp<T>(a, stream, split);
 }
 
 static int check_sizes(int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int nviews) {
@@ -197,7 +225,7 @@ static int warp_single(const void* src, int64_t B, int64_t C, int64_t H, int64_t
 
 template <typename T>
 static int warp_views(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t H,
-                      int64_t W, int64_t Ho, int64_t Wo, void* stream) {
+                      int64_t W, int64_t Ho, int64_t Wo, void* stream, bool split = false) {
   if (!views) return MVBEV_ERR_NULL;
   const int st = check_sizes(B, C, H, W, Ho, Wo, nviews);
   if (st != MVBEV_OK) return st;
@@ -214,7 +242,7 @@ static int warp_views(const mvbev_warp_view* views, int nviews, int64_t B, int64
     for (int k = 0; k < 9; ++k) d.m[k] = s.m[k];
   }
   a.nviews = nviews;
-  return finish_args_and_launch<T>(a, B, C, H, W, Ho, Wo, stream);
+  return finish_args_and_launch<T>(a, B, C, H, W, Ho, Wo, stream, split);
 }
 
 // coord_map (persp_trans_detector.py:103-112): grid / (n-1) * 2 - 1 in float64, then .float()
@@ -266,6 +294,14 @@ int mvbev_warp_perspective_f16(const void* src, int64_t B, int64_t C, int64_t H,
 int mvbev_warp_views_f32(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
                          int64_t H, int64_t W, int64_t Ho, int64_t Wo, void* stream) {
   return mvbev::warp_views<float>(views, nviews, B, C, H, W, Ho, Wo, stream);
+}
+
+int mvbev_warp_views_split_bf16(const mvbev_warp_view* views, int nviews, int src_is_f16,
+                                int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
+                                void* stream) {
+  if (src_is_f16)
+    return mvbev::warp_views<__half>(views, nviews, B, C, H, W, Ho, Wo, stream, true);
+  return mvbev::warp_views<float>(views, nviews, B, C, H, W, Ho, Wo, stream, true);
 }
 
 int mvbev_warp_views_f16(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,

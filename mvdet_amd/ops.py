@@ -69,11 +69,26 @@ def warp_into(src: torch.Tensor, m_norm: torch.Tensor, dst: torch.Tensor) -> tor
     return dst
 
 
-def warp_views_into(srcs, m_norms, dsts) -> None:
+def split_shape(B: int, C: int, H: int, W: int) -> Tuple[int, ...]:
+    """Shape of a [B, C, H, W] tensor in the split-bf16 blocked layout (bf16 storage)."""
+    return (B, (C + KC - 1) // KC, H, W, 2, KC)
+
+
+def split_decode(t: torch.Tensor, C: Optional[int] = None) -> torch.Tensor:
+    """Split-bf16 blocked [B, G, H, W, 2, 8] -> fp32 [B, C, H, W] (hi + lo)."""
+    B, G, H, W, _, _ = t.shape
+    v = t[..., 0, :].float() + t[..., 1, :].float()        # [B, G, H, W, 8]
+    v = v.permute(0, 1, 4, 2, 3).reshape(B, G * KC, H, W)
+    return v[:, :C] if C is not None else v
+
+
+def warp_views_into(srcs, m_norms, dsts, split: bool = False, C: Optional[int] = None) -> None:
     """Warp several views (same shapes) in ONE launch.
 
-    ``srcs[i]`` [B,C,H,W], ``dsts[i]`` [B,C,Ho,Wo] views (innermost stride 1), ``m_norms[i]``
-    a host [3,3] src_norm <- dst_norm matrix shared by the batch (``kornia_src_norm_from_dst_norm``).
+    ``srcs[i]`` [B,C,H,W], ``m_norms[i]`` a host [3,3] src_norm <- dst_norm matrix shared by
+    the batch (``kornia_src_norm_from_dst_norm``).  ``dsts[i]``: [B,C,Ho,Wo] views (innermost
+    stride 1, same dtype as the sources) or, with ``split=True``, contiguous split-bf16 blocked
+    tensors [B, ceil(C/8), Ho, Wo, 2, 8] (``split_shape``).
     """
     n = len(srcs)
     if n == 0:
@@ -82,18 +97,38 @@ def warp_views_into(srcs, m_norms, dsts) -> None:
         raise ValueError("need 1..16 matching srcs / m_norms / dsts")
     _require_cuda(*srcs, *dsts)
     B, C, H, W = srcs[0].shape
-    Ho, Wo = dsts[0].shape[2], dsts[0].shape[3]
     dtype = srcs[0].dtype
+    if split:
+        Ho, Wo = dsts[0].shape[2], dsts[0].shape[3]
+        want = split_shape(B, C, Ho, Wo)
+    else:
+        Ho, Wo = dsts[0].shape[2], dsts[0].shape[3]
+        want = (B, C, Ho, Wo)
     arr = (_native.WarpView * n)()
     for i, (s, m, d) in enumerate(zip(srcs, m_norms, dsts)):
-        if tuple(s.shape) != (B, C, H, W) or tuple(d.shape) != (B, C, Ho, Wo):
-            raise ValueError("all views must share shapes")
-        if s.dtype != dtype or d.dtype != dtype:
+        if tuple(s.shape) != (B, C, H, W) or tuple(d.shape) != want:
+            raise ValueError(f"all views must share shapes: src {tuple(s.shape)} dst {tuple(d.shape)} want {want}")
+        if s.dtype != dtype:
             raise TypeError("all views must share one dtype")
+        if split:
+            if d.dtype != torch.bfloat16 or d.stride(5) != 1 or d.stride(4) != KC or d.stride(3) != 2 * KC:
+                raise ValueError("split dst must be a bf16 [B,G,Ho,Wo,2,8] tensor with contiguous pixels")
+            dstr = (d.stride(0) // 16, d.stride(1) // 16, d.stride(2) // 16, 1)  # 32-byte units
+        else:
+            if d.dtype != dtype:
+                raise TypeError("dst dtype must match src")
+            dstr = tuple(d.stride())
         mm = torch.as_tensor(m, dtype=torch.float32).reshape(9).tolist()
         arr[i] = _native.WarpView(s.data_ptr(), (ctypes.c_int64 * 4)(*s.stride()), d.data_ptr(),
-                                  (ctypes.c_int64 * 4)(*d.stride()), (ctypes.c_float * 9)(*mm))
+                                  (ctypes.c_int64 * 4)(*dstr), (ctypes.c_float * 9)(*mm))
     lib = _native.load()
+    if split:
+        if dtype not in (torch.float32, torch.float16):
+            raise TypeError(f"unsupported dtype {dtype}")
+        st = lib.mvbev_warp_views_split_bf16(arr, n, int(dtype == torch.float16), B, C, H, W, Ho, Wo,
+                                             _stream(dsts[0]))
+        _native.check(st, "mvbev_warp_views_split_bf16")
+        return
     if dtype == torch.float32:
         fn, name = lib.mvbev_warp_views_f32, "mvbev_warp_views_f32"
     elif dtype == torch.float16:
@@ -220,12 +255,16 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
     """Low-level form: ``x`` addressed through ``desc`` (``mvbev_conv_desc``)."""
     _require_cuda(x, packed)
     bf16x3 = packed.dtype == torch.bfloat16
-    if x.dtype not in ((torch.float32, torch.float16) if bf16x3 else (torch.float32,)):
+    if x.dtype not in ((torch.float32, torch.float16, torch.bfloat16) if bf16x3 else (torch.float32,)):
         raise TypeError(f"x dtype {x.dtype} not supported by the {'bf16x3' if bf16x3 else 'fp32'} conv")
+    # bf16 storage means the split-bf16 blocked layout (4 bytes per logical element)
+    layout = {torch.float32: _native.LAYOUT_F32, torch.float16: _native.LAYOUT_F16,
+              torch.bfloat16: _native.LAYOUT_SPLIT_BF16}[x.dtype]
+    unit = 2 if x.dtype == torch.float16 else 4
     B, H, W, out_rows = desc.B, desc.H, desc.W, desc.out_rows
     need = (desc.K // desc.group - 1) * desc.group_stride + (B - 1) * desc.batch_stride + \
         desc.group * desc.in_rows * W
-    if x.untyped_storage().nbytes() // x.element_size() - x.storage_offset() < need:
+    if (x.untyped_storage().nbytes() - x.storage_offset() * x.element_size()) // unit < need:
         raise ValueError("x's storage is too small for the conv descriptor")
     if out is None:
         out = torch.empty((B, cout, out_rows, W), dtype=torch.float32, device=x.device)
@@ -242,7 +281,7 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
     bp = bias.data_ptr() if bias is not None else None
     ip = init.data_ptr() if init is not None else None
     if bf16x3:
-        st = lib.mvbev_conv3x3_bf16x3(x.data_ptr(), int(x.dtype == torch.float16), ctypes.byref(desc),
+        st = lib.mvbev_conv3x3_bf16x3(x.data_ptr(), layout, ctypes.byref(desc),
                                       packed.data_ptr(), bp, ip, cout, int(dilation), int(bool(relu)),
                                       out.data_ptr(), _stream(x))
         _native.check(st, "mvbev_conv3x3_bf16x3")

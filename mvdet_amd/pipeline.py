@@ -72,6 +72,8 @@ class ProjectFuse:
             raise ValueError("an fp16 slab needs precision='bf16x3' (the fp32-MFMA conv reads fp32)")
         self.precision = precision
         self.slab_dtype = slab_dtype
+        # 3xbf16 with fp32 storage: the warp writes the pre-split bf16 hi/lo blocked slab
+        self.split = precision == "bf16x3" and slab_dtype == torch.float32
         self.num_cam = len(proj_mats)
         self.src_hw = (int(src_hw[0]), int(src_hw[1]))
         self.grid_hw = (int(grid_hw[0]), int(grid_hw[1]))
@@ -110,7 +112,11 @@ class ProjectFuse:
         key = (str(device), int(B), band)
         ws = self._ws.get(key)
         if ws is None:
-            slab = torch.zeros((self.S, B, self.Cs, H, W), dtype=self.slab_dtype, device=device)
+            if self.split:
+                slab = torch.zeros((self.S,) + ops.split_shape(B, self.Cs, H, W), dtype=torch.bfloat16,
+                                   device=device)
+            else:
+                slab = torch.zeros((self.S, B, self.Cs, H, W), dtype=self.slab_dtype, device=device)
             y1r, y2r = band_rows(band[0], band[1], H)
             y1 = torch.empty((B, self.mid, y1r[1] - y1r[0], W), dtype=torch.float32, device=device)
             y2 = torch.empty((B, self.mid, y2r[1] - y2r[0], W), dtype=torch.float32, device=device)
@@ -120,8 +126,14 @@ class ProjectFuse:
         return ws
 
     def view_slice(self, ws: Workspace, cam: int) -> torch.Tensor:
-        """[B, C, Ho, Wo] view of ``cam``'s warped features inside the slab."""
+        """[B, C, Ho, Wo] of ``cam``'s warped features: a view of the slab, or (split
+        layout) its fp32 decode (hi + lo)."""
+        if self.split:
+            return ops.split_decode(ws.slab[self.slot_of[cam]], self.C)
         return ws.slab[self.slot_of[cam], :, :self.C]
+
+    def _slot_dst(self, ws: Workspace, cam: int) -> torch.Tensor:
+        return ws.slab[self.slot_of[cam]] if self.split else ws.slab[self.slot_of[cam], :, :self.C]
 
     # -- a5 -------------------------------------------------------------------------------
     def warp_view(self, ws: Workspace, cam: int, feat: torch.Tensor) -> None:
@@ -129,7 +141,10 @@ class ProjectFuse:
         if tuple(feat.shape[2:]) != self.src_hw or feat.shape[1] != self.C:
             raise ValueError(f"view {cam}: features {tuple(feat.shape)} do not match "
                              f"[B,{self.C},{self.src_hw[0]},{self.src_hw[1]}]")
-        ops.warp_into(feat, ws.m_norm[cam], self.view_slice(ws, cam))
+        if self.split:
+            ops.warp_views_into([feat], [self.m_norm_cpu[cam]], [self._slot_dst(ws, cam)], split=True)
+        else:
+            ops.warp_into(feat, ws.m_norm[cam], self._slot_dst(ws, cam))
 
     def warp_views(self, ws: Workspace, cams: Sequence[int], feats: Sequence[torch.Tensor]) -> None:
         """a5 for several views in one launch (``feats[i]`` is view ``cams[i]``)."""
@@ -138,7 +153,7 @@ class ProjectFuse:
                 raise ValueError(f"view {cam}: features {tuple(f.shape)} do not match "
                                  f"[B,{self.C},{self.src_hw[0]},{self.src_hw[1]}]")
         ops.warp_views_into(list(feats), [self.m_norm_cpu[c] for c in cams],
-                            [self.view_slice(ws, c) for c in cams])
+                            [self._slot_dst(ws, c) for c in cams], split=self.split)
 
     # -- coord term (a2 folded into conv1) --------------------------------------------------
     def coord_term(self, conv1: torch.nn.Conv2d) -> torch.Tensor:

@@ -96,6 +96,26 @@ def test_warp_views_batched_launch(dtype):
     assert (slab[:, :, C:] == 5).all()
 
 
+@pytest.mark.parametrize("src_dtype", [torch.float32, torch.float16])
+def test_warp_views_split_bf16_layout(src_dtype):
+    """The pre-split slab layout: hi + lo reproduces the fp32 warp to ~2^-17 relative."""
+    from mvdet_amd import ops
+    from mvdet_amd.geometry import kornia_src_norm_from_dst_norm
+    rng = np.random.default_rng(23)
+    B, C, H, W, ho, wo, N = 2, 21, 30, 50, 17, 37, 3       # C not a multiple of 8: zero-filled tail
+    srcs = [torch.from_numpy(rng.standard_normal((B, C, H, W)).astype(np.float32)).to(src_dtype) for _ in range(N)]
+    Ms = [torch.from_numpy(_rand_h(rng, H, W, ho, wo)).float()[None] for _ in range(N)]
+    slab = torch.full((N,) + ops.split_shape(B, C, ho, wo), 3.0, dtype=torch.bfloat16, device=DEV)
+    mn = [kornia_src_norm_from_dst_norm(M, (H, W), (ho, wo))[0] for M in Ms]
+    ops.warp_views_into([s.to(DEV) for s in srcs], mn, [slab[i] for i in range(N)], split=True)
+    for i in range(N):
+        ref = kornia_warp.warp_perspective(srcs[i].float(), Ms[i].repeat(B, 1, 1), (ho, wo))
+        got = ops.split_decode(slab[i]).cpu()
+        s = parity_stats(got[:, :C], ref)
+        assert s["normwise"] < 2e-5, (i, s)
+        assert (got[:, C:] == 0).all()
+
+
 def test_warp_f16_storage():
     from mvdet_amd import warp_perspective
     rng = np.random.default_rng(11)

@@ -90,6 +90,9 @@ template <> __device__ inline float ld<_Float16>(const _Float16* p) { return (fl
 #ifndef MVBEV_B3_DBUF
 #define MVBEV_B3_DBUF 0
 #endif
+#ifndef MVBEV_B3_DEPTH
+#define MVBEV_B3_DEPTH 2  // staging-register ring depth (single LDS buffer path; 1 or 2)
+#endif
 
 template <typename TIn, int DIL, bool RELU, int NW, bool DBUF>
 __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const Args a) {
@@ -99,7 +102,8 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
   constexpr int XPIX = XH * XW;          // halo pixels per chunk (8 channels each)
   constexpr int XPT = (XPIX + NT - 1) / NT;
   constexpr int WLD = (W16 + NT - 1) / NT;
-  constexpr int BUF = W16 + 2 * XPIX;   // 16-B pieces per LDS buffer
+  constexpr int XPAD = XPT * NT;         // X image entries incl. a dummy tail for idle threads
+  constexpr int BUF = W16 + 2 * XPAD;   // 16-B pieces per LDS buffer
   __shared__ __attribute__((aligned(16))) u32x4 lds[(DBUF ? 2 : 1) * BUF];
   // buffer layout: W [part][kb][h][co] pieces of 8 bf16, then X hi [r][c], X lo [r][c]
 
@@ -136,14 +140,16 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
 
   constexpr bool SPLIT = std::is_same<TIn, SplitIn>::value;
   using XElem = typename std::conditional<SPLIT, float, TIn>::type;  // element type when not split
-  u32x4 wreg[WLD];
-  float xreg[XPT][SPLIT ? 1 : KC];
-  u32x4 xs[XPT][SPLIT ? 2 : 1];
-#define B3_LOAD(ch)                                                                          \
+  // staging-register ring: DEPTH chunks of global loads in flight ahead of the MFMAs
+  constexpr int DEPTH = MVBEV_B3_DEPTH;
+  u32x4 wreg[DEPTH][WLD];
+  float xreg[DEPTH][XPT][SPLIT ? 1 : KC];
+  u32x4 xs[DEPTH][XPT][SPLIT ? 2 : 1];
+#define B3_LOAD(ch, sl)                                                                      \
   do {                                                                                       \
     const u32x4* ws_ = wsrc + (int64_t)(ch) * wchunk;                                        \
     _Pragma("unroll") for (int i = 0; i < WLD; ++i) {                                        \
-      if (W16 % NT == 0 || tid + NT * i < W16) wreg[i] = ws_[tid + NT * i];                  \
+      if (W16 % NT == 0 || tid + NT * i < W16) wreg[sl][i] = ws_[tid + NT * i];              \
     }                                                                                        \
     const int g_ = (ch) / chunks_per_group;                                                  \
     const int64_t cb_ = (int64_t)b * a.batch_stride + g_ * a.group_stride +                  \
@@ -151,37 +157,37 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
     if constexpr (SPLIT) {                                                                   \
       const u32x4* xc_ = static_cast<const u32x4*>(a.x) + cb_ / 4;                           \
       _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                      \
-        xs[i][0] = xc_[2 * xoff[i]];                                                         \
-        xs[i][1] = xc_[2 * xoff[i] + 1];                                                     \
+        xs[sl][i][0] = xc_[2 * xoff[i]];                                                     \
+        xs[sl][i][1] = xc_[2 * xoff[i] + 1];                                                 \
       }                                                                                      \
     } else {                                                                                 \
       const XElem* xc_ = static_cast<const XElem*>(a.x) + cb_;                               \
       _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                      \
         _Pragma("unroll") for (int j = 0; j < KC; ++j)                                       \
-          xreg[i][j] = ld<XElem>(xc_ + j * plane + xoff[i]);                                 \
+          xreg[sl][i][j] = ld<XElem>(xc_ + j * plane + xoff[i]);                             \
       }                                                                                      \
     }                                                                                        \
   } while (0)
-#define B3_STORE(buf)                                                                        \
+#define B3_STORE(buf, sl)                                                                    \
   do {                                                                                       \
     u32x4* Wl = lds + (buf) * BUF;                                                           \
     u32x4* Xhi = Wl + W16;                                                                   \
-    u32x4* Xlo = Xhi + XPIX;                                                                 \
+    u32x4* Xlo = Xhi + XPAD;                                                                 \
     _Pragma("unroll") for (int i = 0; i < WLD; ++i) {                                        \
-      if (W16 % NT == 0 || tid + NT * i < W16) Wl[tid + NT * i] = wreg[i];                   \
+      if (W16 % NT == 0 || tid + NT * i < W16) Wl[tid + NT * i] = wreg[sl][i];               \
     }                                                                                        \
     _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                        \
       const int p = tid + NT * i;                                                            \
       if constexpr (SPLIT) {                                                                 \
-        if (XPIX % NT == 0 || p < XPIX) {                                                    \
-          const u32x4 z_ = {0u, 0u, 0u, 0u};                                                 \
-          Xhi[p] = xok[i] ? xs[i][0] : z_;                                                   \
-          Xlo[p] = xok[i] ? xs[i][1] : z_;                                                   \
-        }                                                                                    \
-      } else if (XPIX % NT == 0 || p < XPIX) {                                               \
+        /* unconditional: threads past the halo write the dummy tail (no branch, so the      \
+           compiler's vmcnt counting stays exact across the prefetch ring) */                \
+        const u32x4 z_ = {0u, 0u, 0u, 0u};                                                   \
+        Xhi[p] = xok[i] ? xs[sl][i][0] : z_;                                                 \
+        Xlo[p] = xok[i] ? xs[sl][i][1] : z_;                                                 \
+      } else {                                                                               \
         bf16x8 hi, lo;                                                                       \
         _Pragma("unroll") for (int j = 0; j < KC; ++j) {                                     \
-          const float v = xok[i] ? xreg[i][j] : 0.f;                                         \
+          const float v = xok[i] ? xreg[sl][i][j] : 0.f;                                     \
           const __bf16 h_ = (__bf16)v;                                                       \
           hi[j] = h_;                                                                        \
           lo[j] = (__bf16)(v - (float)h_);                                                   \
@@ -209,7 +215,7 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
 
   auto compute = [&](const u32x4* Wl) __attribute__((always_inline)) {
     const u32x4* Xhi = Wl + W16;
-    const u32x4* Xlo = Xhi + XPIX;
+    const u32x4* Xlo = Xhi + XPAD;
 #pragma unroll
     for (int kb = 0; kb < NKB; ++kb) {
       bf16x8 ahi[2], alo[2], bhi[2], blo[2];
@@ -235,24 +241,51 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
     }
   };
 
-  B3_LOAD(0);
   if constexpr (DBUF) {
-    B3_STORE(0);
+    B3_LOAD(0, 0);
+    B3_STORE(0, 0);
     __syncthreads();
     for (int ch = 0; ch < a.nchunks; ++ch) {
       const int cur = ch & 1;
       const bool more = ch + 1 < a.nchunks;
-      if (more) B3_LOAD(ch + 1);
+      if (more) B3_LOAD(ch + 1, 0);
       compute(lds + cur * BUF);
-      if (more) B3_STORE(cur ^ 1);
+      if (more) B3_STORE(cur ^ 1, 0);
       __syncthreads();
     }
+  } else if constexpr (DEPTH == 2) {
+    // Two chunks of loads in flight: slot 0 holds even chunks, slot 1 odd ones. Loads are
+    // unconditional (index clamped; the last chunk is re-read at most twice) so the
+    // loop body is straight-line and the compiler's vmcnt counting stays exact.
+    const int last = a.nchunks - 1;
+    B3_LOAD(0, 0);
+    B3_LOAD(min(1, last), 1);
+    int ch = 0;
+    for (; ch + 1 < a.nchunks; ch += 2) {
+      __syncthreads();
+      B3_STORE(0, 0);
+      __syncthreads();
+      B3_LOAD(min(ch + 2, last), 0);
+      compute(lds);
+      __syncthreads();
+      B3_STORE(0, 1);
+      __syncthreads();
+      B3_LOAD(min(ch + 3, last), 1);
+      compute(lds);
+    }
+    if (ch < a.nchunks) {
+      __syncthreads();
+      B3_STORE(0, 0);
+      __syncthreads();
+      compute(lds);
+    }
   } else {
+    B3_LOAD(0, 0);
     for (int ch = 0; ch < a.nchunks; ++ch) {
       __syncthreads();
-      B3_STORE(0);
+      B3_STORE(0, 0);
       __syncthreads();
-      if (ch + 1 < a.nchunks) B3_LOAD(ch + 1);
+      if (ch + 1 < a.nchunks) B3_LOAD(ch + 1, 0);
       compute(lds);
     }
   }

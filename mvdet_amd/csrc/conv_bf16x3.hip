@@ -11,13 +11,15 @@
 // three passes still run 5.3x the fp32 rate.  Inputs may be fp32 or fp16 (an fp16 value is
 // exactly hi + lo, so the fp16-storage config 4 path is exact in its products).
 //
-// Mapping: K is walked in chunks of 8 input channels; a chunk is 5 MFMA K-blocks of 16 =
-// (tap pair, 8 channels) with a zero-weight 10th tap.  Lane l of the 32x32x16 MFMA holds
-// A[co = l&31][k = 8(l>>5) + j] and B[k][pixel = l&31], so the lane's 8 K-values are the 8
-// channels of one tap: the weights are pre-packed [tap pair][tap][co][8 ch] and the input
-// halo is staged channel-innermost [row][col][8 ch], both read as one ds_read_b128 per
-// fragment (16 consecutive lanes = 256 contiguous bytes: conflict-free).  The input halo is
-// split into hi/lo once at LDS-store time; weights are split once at pack time.
+// Mapping: K is walked in chunks of 16 input channels (two 8-channel sub-blocks, each
+// located on its own, so any channel group that is a multiple of 8 works); a chunk is 9
+// MFMA K-blocks of 16 = (one tap, 16 channels): no padding MFMAs.  Lane l of the 32x32x16
+// MFMA holds A[co = l&31][k = 8(l>>5) + j] and B[k][pixel = l&31], so the lane's 8 K-values
+// are the 8 channels of sub-block l>>5 at one tap: the weights are pre-packed
+// [tap][sub][co][8 ch] and the input halo is staged channel-innermost [sub][row][col][8 ch],
+// both read as one ds_read_b128 per fragment (16 consecutive lanes = 256 contiguous bytes:
+// conflict-free).  The input halo is split into hi/lo once at LDS-store time (or arrives
+// pre-split); weights are split once at pack time.
 // Workgroup tile: NW/2 row pairs x 32 cols x 128 output channels; wave = 2 rows x 64
 // channels (2x2 accumulators of 32x32, the same epilogue as the fp32 kernel).
 #include "common.h"
@@ -31,15 +33,16 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int KC = MVBEV_CONV_KC;  // 8 input channels per chunk
-constexpr int NKB = 5;             // K-blocks per chunk: taps (2kb, 2kb+1), tap 9 = zero pad
+constexpr int SB = MVBEV_CONV_KC;  // 8 channels per sub-block (= the split layout's group)
+constexpr int KC = 2 * SB;         // 16 input channels per chunk
+constexpr int NKB = 9;             // K-blocks per chunk: one per tap
 constexpr int BN = MVBEV_CONV_BN;  // 128 output channels per workgroup
 constexpr int TW = 32;             // output columns per workgroup (= MFMA N)
-constexpr int WPART = NKB * 2 * BN * KC;  // bf16 per part (hi or lo) per (chunk, cout tile)
-constexpr int WBYTES = 2 * WPART * 2;     // hi + lo bytes per (chunk, cout tile) = 40 KiB
-constexpr int W16 = WBYTES / 16;          // 16-B pieces
+constexpr int WPART = NKB * KC * BN;      // bf16 per part (hi or lo) per (chunk, cout tile)
+constexpr int WBYTES = 2 * WPART * 2;     // hi + lo bytes per (chunk, cout tile) = 72 KiB
+constexpr int W16 = WBYTES / 16;          // 16-B pieces (4608)
 
-// packed[chunk][cot][part][kb][h][co][j]: tap = 2kb+h, input channel = map(chunk*8 + j)
+// packed[chunk][cot][part][tap][sub][co][j]: input channel = map(chunk*16 + sub*8 + j)
 __global__ void pack_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int Cout,
                             int Cin_w, const int32_t* __restrict__ chan_map, int K, int K_pad) {
   const int n_cot = Cout / BN;
@@ -47,18 +50,17 @@ __global__ void pack_kernel(const float* __restrict__ w, __bf16* __restrict__ ou
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
     int64_t r = i;
-    const int j = r % KC; r /= KC;
+    const int j = r % SB; r /= SB;
     const int co = r % BN; r /= BN;
-    const int h = r % 2; r /= 2;
-    const int kb = r % NKB; r /= NKB;
+    const int sub = r % 2; r /= 2;
+    const int tap = r % NKB; r /= NKB;
     const int part = r % 2; r /= 2;
     const int cot = r % n_cot;
     const int chunk = (int)(r / n_cot);
-    const int tap = 2 * kb + h;
-    const int k = chunk * KC + j;
+    const int k = chunk * KC + sub * SB + j;
     int ci = k < K ? (chan_map ? chan_map[k] : k) : -1;
     if (ci >= Cin_w) ci = -1;
-    const float v = (tap < 9 && ci >= 0) ? w[((int64_t)(cot * BN + co) * Cin_w + ci) * 9 + tap] : 0.f;
+    const float v = ci >= 0 ? w[((int64_t)(cot * BN + co) * Cin_w + ci) * 9 + tap] : 0.f;
     const __bf16 hi = (__bf16)v;
     out[i] = part ? (__bf16)(v - (float)hi) : hi;
   }
@@ -71,7 +73,7 @@ struct Args {
   const float* init;
   float* y;
   int64_t group_stride, batch_stride;
-  int group, nchunks, Cout, H, W;
+  int group, K, nchunks, Cout, H, W;
   int in_row0, in_rows, out_row0, out_rows;
   int tiles_x, tiles_y, n_cot, nwg;
 };
@@ -85,27 +87,23 @@ template <> __device__ inline float ld<float>(const float* p) { return *p; }
 template <> __device__ inline float ld<_Float16>(const _Float16* p) { return (float)*p; }
 
 #ifndef MVBEV_B3_MINWAVES
-#define MVBEV_B3_MINWAVES 2
-#endif
-#ifndef MVBEV_B3_DBUF
-#define MVBEV_B3_DBUF 0
+#define MVBEV_B3_MINWAVES 1
 #endif
 #ifndef MVBEV_B3_DEPTH
-#define MVBEV_B3_DEPTH 2  // staging-register ring depth (single LDS buffer path; 1 or 2)
+#define MVBEV_B3_DEPTH 2  // staging-register ring depth (1 or 2)
 #endif
 
-template <typename TIn, int DIL, bool RELU, int NW, bool DBUF>
+template <typename TIn, int DIL, bool RELU, int NW>
 __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const Args a) {
   constexpr int NT = 64 * NW;
   constexpr int TH = NW;                 // NW/2 row pairs, 2 channel halves
   constexpr int XH = TH + 2 * DIL, XW = TW + 2 * DIL;
-  constexpr int XPIX = XH * XW;          // halo pixels per chunk (8 channels each)
+  constexpr int XPIX = XH * XW;          // halo pixels per sub-block
   constexpr int XPT = (XPIX + NT - 1) / NT;
   constexpr int WLD = (W16 + NT - 1) / NT;
   constexpr int XPAD = XPT * NT;         // X image entries incl. a dummy tail for idle threads
-  constexpr int BUF = W16 + 2 * XPAD;   // 16-B pieces per LDS buffer
-  __shared__ __attribute__((aligned(16))) u32x4 lds[(DBUF ? 2 : 1) * BUF];
-  // buffer layout: W [part][kb][h][co] pieces of 8 bf16, then X hi [r][c], X lo [r][c]
+  constexpr int BUF = W16 + 4 * XPAD;    // 16-B pieces: W, then X [sub][part][XPAD]
+  __shared__ __attribute__((aligned(16))) u32x4 lds[BUF];
 
   const int wg = xcd_remap(blockIdx.x, a.nwg);
   const int cot = wg % a.n_cot;
@@ -123,7 +121,6 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
   const int64_t plane = (int64_t)a.in_rows * W;
   const u32x4* wsrc = a.wp + (int64_t)cot * W16;
   const int64_t wchunk = (int64_t)a.n_cot * W16;
-  const int chunks_per_group = a.group / KC;
 
   // halo pixels of this thread (chunk-invariant): plane offset + validity
   int xoff[XPT];
@@ -143,92 +140,101 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
   // staging-register ring: DEPTH chunks of global loads in flight ahead of the MFMAs
   constexpr int DEPTH = MVBEV_B3_DEPTH;
   u32x4 wreg[DEPTH][WLD];
-  float xreg[DEPTH][XPT][SPLIT ? 1 : KC];
-  u32x4 xs[DEPTH][XPT][SPLIT ? 2 : 1];
+  float xreg[DEPTH][2][XPT][SPLIT ? 1 : SB];
+  u32x4 xs[DEPTH][2][XPT][SPLIT ? 2 : 1];
+  bool sok[DEPTH][2];
+  // Sub-block base (elements) of packed channel k0; sub-blocks past K read sub-block 0's
+  // pixels (always valid memory) and are zeroed at store time.
+#define B3_SUB_BASE(k0)                                                                      \
+  ({                                                                                         \
+    const int g_ = (k0) / a.group;                                                           \
+    (int64_t)b * a.batch_stride + g_ * a.group_stride + (int64_t)((k0) - g_ * a.group) * plane; \
+  })
 #define B3_LOAD(ch, sl)                                                                      \
   do {                                                                                       \
     const u32x4* ws_ = wsrc + (int64_t)(ch) * wchunk;                                        \
     _Pragma("unroll") for (int i = 0; i < WLD; ++i) {                                        \
       if (W16 % NT == 0 || tid + NT * i < W16) wreg[sl][i] = ws_[tid + NT * i];              \
     }                                                                                        \
-    const int g_ = (ch) / chunks_per_group;                                                  \
-    const int64_t cb_ = (int64_t)b * a.batch_stride + g_ * a.group_stride +                  \
-                        (int64_t)((ch) - g_ * chunks_per_group) * KC * plane;                \
-    if constexpr (SPLIT) {                                                                   \
-      const u32x4* xc_ = static_cast<const u32x4*>(a.x) + cb_ / 4;                           \
-      _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                      \
-        xs[sl][i][0] = xc_[2 * xoff[i]];                                                     \
-        xs[sl][i][1] = xc_[2 * xoff[i] + 1];                                                 \
-      }                                                                                      \
-    } else {                                                                                 \
-      const XElem* xc_ = static_cast<const XElem*>(a.x) + cb_;                               \
-      _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                      \
-        _Pragma("unroll") for (int j = 0; j < KC; ++j)                                       \
-          xreg[sl][i][j] = ld<XElem>(xc_ + j * plane + xoff[i]);                             \
+    _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_) {                                       \
+      const int k0_ = (ch) * KC + s_ * SB;                                                   \
+      sok[sl][s_] = k0_ < a.K;                                                               \
+      const int64_t cb_ = B3_SUB_BASE(sok[sl][s_] ? k0_ : (ch) * KC);                        \
+      if constexpr (SPLIT) {                                                                 \
+        const u32x4* xc_ = static_cast<const u32x4*>(a.x) + cb_ / 4;                         \
+        _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                    \
+          xs[sl][s_][i][0] = xc_[2 * xoff[i]];                                               \
+          xs[sl][s_][i][1] = xc_[2 * xoff[i] + 1];                                           \
+        }                                                                                    \
+      } else {                                                                               \
+        const XElem* xc_ = static_cast<const XElem*>(a.x) + cb_;                             \
+        _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                    \
+          _Pragma("unroll") for (int j = 0; j < SB; ++j)                                     \
+            xreg[sl][s_][i][j] = ld<XElem>(xc_ + j * plane + xoff[i]);                       \
+        }                                                                                    \
       }                                                                                      \
     }                                                                                        \
   } while (0)
-#define B3_STORE(buf, sl)                                                                    \
+#define B3_STORE(sl)                                                                         \
   do {                                                                                       \
-    u32x4* Wl = lds + (buf) * BUF;                                                           \
-    u32x4* Xhi = Wl + W16;                                                                   \
-    u32x4* Xlo = Xhi + XPAD;                                                                 \
     _Pragma("unroll") for (int i = 0; i < WLD; ++i) {                                        \
-      if (W16 % NT == 0 || tid + NT * i < W16) Wl[tid + NT * i] = wreg[sl][i];               \
+      if (W16 % NT == 0 || tid + NT * i < W16) lds[tid + NT * i] = wreg[sl][i];              \
     }                                                                                        \
-    _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                        \
-      const int p = tid + NT * i;                                                            \
-      if constexpr (SPLIT) {                                                                 \
-        /* unconditional: threads past the halo write the dummy tail (no branch, so the      \
-           compiler's vmcnt counting stays exact across the prefetch ring) */                \
-        const u32x4 z_ = {0u, 0u, 0u, 0u};                                                   \
-        Xhi[p] = xok[i] ? xs[sl][i][0] : z_;                                                 \
-        Xlo[p] = xok[i] ? xs[sl][i][1] : z_;                                                 \
-      } else {                                                                               \
-        bf16x8 hi, lo;                                                                       \
-        _Pragma("unroll") for (int j = 0; j < KC; ++j) {                                     \
-          const float v = xok[i] ? xreg[sl][i][j] : 0.f;                                     \
-          const __bf16 h_ = (__bf16)v;                                                       \
-          hi[j] = h_;                                                                        \
-          lo[j] = (__bf16)(v - (float)h_);                                                   \
+    _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_) {                                       \
+      u32x4* Xhi = lds + W16 + s_ * 2 * XPAD;                                                \
+      u32x4* Xlo = Xhi + XPAD;                                                               \
+      _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                      \
+        /* unconditional: threads past the halo write the dummy tail (no branch, so the    \
+           compiler's vmcnt counting stays exact across the prefetch ring) */              \
+        const int p = tid + NT * i;                                                          \
+        const bool ok_ = xok[i] && sok[sl][s_];                                              \
+        if constexpr (SPLIT) {                                                               \
+          const u32x4 z_ = {0u, 0u, 0u, 0u};                                                 \
+          Xhi[p] = ok_ ? xs[sl][s_][i][0] : z_;                                              \
+          Xlo[p] = ok_ ? xs[sl][s_][i][1] : z_;                                              \
+        } else {                                                                             \
+          bf16x8 hi, lo;                                                                     \
+          _Pragma("unroll") for (int j = 0; j < SB; ++j) {                                   \
+            const float v = ok_ ? xreg[sl][s_][i][j] : 0.f;                                  \
+            const __bf16 h_ = (__bf16)v;                                                     \
+            hi[j] = h_;                                                                      \
+            lo[j] = (__bf16)(v - (float)h_);                                                 \
+          }                                                                                  \
+          Xhi[p] = __builtin_bit_cast(u32x4, hi);                                            \
+          Xlo[p] = __builtin_bit_cast(u32x4, lo);                                            \
         }                                                                                    \
-        Xhi[p] = __builtin_bit_cast(u32x4, hi);                                              \
-        Xlo[p] = __builtin_bit_cast(u32x4, lo);                                              \
       }                                                                                      \
     }                                                                                        \
   } while (0)
 
   const int prow = 2 * (wave % (NW / 2));
   const int cw = 64 * (wave / (NW / 2));
-  // per K-block B offsets in the halo image: tap = 2kb + kh (tap 9 -> any valid pixel)
+  // per tap B offsets in the halo image (lane half kh reads sub-block kh)
   int boff[NKB];
 #pragma unroll
-  for (int kb = 0; kb < NKB; ++kb) {
-    const int tap = min(2 * kb + kh, 8);
-    boff[kb] = (prow + (tap / 3) * DIL) * XW + l32 + (tap % 3) * DIL;
-  }
+  for (int t = 0; t < NKB; ++t) boff[t] = kh * 2 * XPAD + (prow + (t / 3) * DIL) * XW + l32 + (t % 3) * DIL;
   floatx16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = floatx16{0};
 
-  auto compute = [&](const u32x4* Wl) __attribute__((always_inline)) {
-    const u32x4* Xhi = Wl + W16;
-    const u32x4* Xlo = Xhi + XPAD;
+  auto compute = [&]() __attribute__((always_inline)) {
+    const u32x4* Wl = lds;
+    const u32x4* X = lds + W16;
 #pragma unroll
-    for (int kb = 0; kb < NKB; ++kb) {
+    for (int t = 0; t < NKB; ++t) {
       bf16x8 ahi[2], alo[2], bhi[2], blo[2];
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
-        const int wi = (kb * 2 + kh) * BN + cw + 32 * ct + l32;
+        const int wi = (t * 2 + kh) * BN + cw + 32 * ct + l32;
         ahi[ct] = __builtin_bit_cast(bf16x8, Wl[wi]);
         alo[ct] = __builtin_bit_cast(bf16x8, Wl[NKB * 2 * BN + wi]);
       }
 #pragma unroll
       for (int pt = 0; pt < 2; ++pt) {
-        bhi[pt] = __builtin_bit_cast(bf16x8, Xhi[boff[kb] + pt * XW]);
-        blo[pt] = __builtin_bit_cast(bf16x8, Xlo[boff[kb] + pt * XW]);
+        bhi[pt] = __builtin_bit_cast(bf16x8, X[boff[t] + pt * XW]);
+        blo[pt] = __builtin_bit_cast(bf16x8, X[boff[t] + XPAD + pt * XW]);
       }
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
@@ -241,19 +247,7 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
     }
   };
 
-  if constexpr (DBUF) {
-    B3_LOAD(0, 0);
-    B3_STORE(0, 0);
-    __syncthreads();
-    for (int ch = 0; ch < a.nchunks; ++ch) {
-      const int cur = ch & 1;
-      const bool more = ch + 1 < a.nchunks;
-      if (more) B3_LOAD(ch + 1, 0);
-      compute(lds + cur * BUF);
-      if (more) B3_STORE(cur ^ 1, 0);
-      __syncthreads();
-    }
-  } else if constexpr (DEPTH == 2) {
+  if constexpr (DEPTH == 2) {
     // Two chunks of loads in flight: slot 0 holds even chunks, slot 1 odd ones. Loads are
     // unconditional (index clamped; the last chunk is re-read at most twice) so the
     // loop body is straight-line and the compiler's vmcnt counting stays exact.
@@ -263,34 +257,35 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
     int ch = 0;
     for (; ch + 1 < a.nchunks; ch += 2) {
       __syncthreads();
-      B3_STORE(0, 0);
+      B3_STORE(0);
       __syncthreads();
       B3_LOAD(min(ch + 2, last), 0);
-      compute(lds);
+      compute();
       __syncthreads();
-      B3_STORE(0, 1);
+      B3_STORE(1);
       __syncthreads();
       B3_LOAD(min(ch + 3, last), 1);
-      compute(lds);
+      compute();
     }
     if (ch < a.nchunks) {
       __syncthreads();
-      B3_STORE(0, 0);
+      B3_STORE(0);
       __syncthreads();
-      compute(lds);
+      compute();
     }
   } else {
     B3_LOAD(0, 0);
     for (int ch = 0; ch < a.nchunks; ++ch) {
       __syncthreads();
-      B3_STORE(0, 0);
+      B3_STORE(0);
       __syncthreads();
       if (ch + 1 < a.nchunks) B3_LOAD(ch + 1, 0);
-      compute(lds);
+      compute();
     }
   }
 #undef B3_LOAD
 #undef B3_STORE
+#undef B3_SUB_BASE
 
   const int col = x0 + l32;
   const int64_t oplane = (int64_t)a.out_rows * W;
@@ -325,7 +320,7 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || d->in_rows <= 0 ||
       d->out_rows <= 0 || d->group <= 0)
     return MVBEV_ERR_RANK;
-  if (Cout % BN != 0 || d->K % KC != 0 || d->group % KC != 0 || d->K % d->group != 0)
+  if (Cout % BN != 0 || d->K % SB != 0 || d->group % SB != 0 || d->K % d->group != 0)
     return MVBEV_ERR_SHAPE;
   if (d->out_row0 < 0 || d->out_row0 + d->out_rows > d->H) return MVBEV_ERR_SHAPE;
   if (d->in_rows * d->W > (int64_t)INT32_MAX || d->H > INT32_MAX / 2 || d->W > INT32_MAX / 2)
@@ -335,7 +330,8 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   Args a;
   a.x = x; a.wp = static_cast<const u32x4*>(w_packed); a.bias = bias; a.init = init; a.y = y;
   a.group_stride = d->group_stride; a.batch_stride = d->batch_stride;
-  a.group = (int)d->group; a.nchunks = (int)(d->K / KC); a.Cout = (int)Cout;
+  a.group = (int)d->group; a.K = (int)d->K; a.nchunks = (int)ceil_div(d->K, KC);
+  a.Cout = (int)Cout;
   a.H = (int)d->H; a.W = (int)d->W;
   a.in_row0 = (int)d->in_row0; a.in_rows = (int)d->in_rows;
   a.out_row0 = (int)d->out_row0; a.out_rows = (int)d->out_rows;
@@ -346,7 +342,7 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   a.nwg = (int)nwg;
   hipStream_t s = as_stream(stream);
 #define B3_LAUNCH(D, R)                                                                   \
-  hipLaunchKernelGGL((conv_kernel<TIn, D, R, NW, MVBEV_B3_DBUF != 0>), dim3((unsigned)nwg), dim3(64 * NW), \
+  hipLaunchKernelGGL((conv_kernel<TIn, D, R, NW>), dim3((unsigned)nwg), dim3(64 * NW),     \
                      0, s, a)
   if (dilation == 1) {
     if (relu) B3_LAUNCH(1, true); else B3_LAUNCH(1, false);

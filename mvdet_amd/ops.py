@@ -213,14 +213,15 @@ class PackedConv3x3:
 
     def get(self, weight: torch.Tensor) -> torch.Tensor:
         _require_cuda(weight)
-        key = (weight.data_ptr(), weight._version, tuple(weight.shape))
+        lib = _native.load()
+        # the packed layout belongs to the library that packed it (A/B runs swap libraries)
+        key = (weight.data_ptr(), weight._version, tuple(weight.shape), id(lib))
         if key != self._key:
             cout, cin, kh, kw = weight.shape
             if (kh, kw) != (3, 3) or weight.dtype != torch.float32:
                 raise ValueError("expected a float32 [Cout,Cin,3,3] weight")
             if cout % BN:
                 raise ValueError(f"Cout={cout} must be a multiple of {BN}")
-            lib = _native.load()
             K = cin if self.chan_map is None else len(self.chan_map)
             if self.chan_map is not None and (self._map_dev is None or self._map_dev.device != weight.device):
                 self._map_dev = torch.tensor(self.chan_map, dtype=torch.int32, device=weight.device)
@@ -278,6 +279,10 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
         if init.numel() != cout * H * W or not init.is_contiguous():
             raise ValueError("init must be a contiguous [Cout,H,W] tensor")
     lib = _native.load()
+    need_packed = (lib.mvbev_conv3x3_packed_bytes_bf16x3(cout, desc.K) if bf16x3
+                   else 4 * lib.mvbev_conv3x3_packed_floats(cout, desc.K))
+    if packed.numel() * packed.element_size() < need_packed:
+        raise ValueError("packed weights are smaller than the conv needs (packed for another K/Cout or library)")
     bp = bias.data_ptr() if bias is not None else None
     ip = init.data_ptr() if init is not None else None
     if bf16x3:

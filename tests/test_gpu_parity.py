@@ -177,6 +177,39 @@ def test_conv3x3_bf16x3_fp16_input_is_exact_split():
     assert_parity(got, ref, "bf16x3 f16-in", normwise_tol=5e-5)
 
 
+def _split_encode(x: torch.Tensor) -> torch.Tensor:
+    """fp32 [B, C, H, W] (C % 8 == 0) -> split-bf16 blocked [B, C/8, H, W, 2, 8]."""
+    B, C, H, W = x.shape
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.float()).to(torch.bfloat16)
+    t = torch.stack([hi, lo], 0).reshape(2, B, C // 8, 8, H, W)
+    return t.permute(1, 2, 4, 5, 0, 3).contiguous()
+
+
+@pytest.mark.parametrize("layout", ["f32", "split"])
+@pytest.mark.parametrize("S,Cs", [(3, 8), (2, 24), (5, 16)])
+def test_conv3x3_bf16x3_grouped_slab(S, Cs, layout):
+    """View-major slab input (channel groups of Cs with a gap between groups), incl. groups
+    that are not a multiple of the kernel's 16-channel chunk and an odd 8-channel tail."""
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(S * 100 + Cs)
+    B, H, W, cout = 2, 9, 45, 128
+    xs = torch.rand(S, B, Cs, H, W, generator=g)
+    K = S * Cs
+    w = (torch.rand(cout, K, 3, 3, generator=g) - 0.5) / np.sqrt(K * 9)
+    ref = F.relu(F.conv2d(xs.permute(1, 0, 2, 3, 4).reshape(B, K, H, W), w, None, padding=1))
+    pk = ops.PackedConv3x3(None, "bf16x3").get(w.to(DEV))
+    if layout == "f32":
+        slab = xs.to(DEV)
+        desc = ops.conv_desc(B, K, H, W, group=Cs, group_stride=B * Cs * H * W, batch_stride=Cs * H * W)
+    else:
+        slab = torch.stack([_split_encode(xs[v]) for v in range(S)]).to(DEV)  # [S,B,G,H,W,2,8]
+        # strides in 4-byte units of the logical fp32 element (one element = hi + lo bf16)
+        desc = ops.conv_desc(B, K, H, W, group=Cs, group_stride=B * Cs * H * W, batch_stride=Cs * H * W)
+    got = ops.conv3x3_desc(slab, desc, pk, cout, relu=True).cpu()
+    assert_parity(got, ref, f"grouped {layout}", normwise_tol=CONV_TOL["bf16x3"])
+
+
 @pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 @pytest.mark.parametrize("d", [1, 2])
 def test_conv3x3_row_band_and_init(d, precision):

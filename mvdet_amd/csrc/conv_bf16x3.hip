@@ -219,31 +219,61 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = floatx16{0};
 
+#ifndef MVBEV_B3_PIPE
+#define MVBEV_B3_PIPE 1  // read tap t+1's fragments from LDS under tap t's MFMAs
+#endif
   auto compute = [&]() __attribute__((always_inline)) {
     const u32x4* Wl = lds;
     const u32x4* X = lds + W16;
-#pragma unroll
-    for (int t = 0; t < NKB; ++t) {
-      bf16x8 ahi[2], alo[2], bhi[2], blo[2];
+    // fragment registers: [set][ahi0, ahi1, alo0, alo1] and [set][bhi0, bhi1, blo0, blo1]
+    constexpr int NSET = MVBEV_B3_PIPE ? 2 : 1;
+    bf16x8 fa[NSET][4], fb[NSET][4];
+    auto fetch = [&](int t, int st) __attribute__((always_inline)) {
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
         const int wi = (t * 2 + kh) * BN + cw + 32 * ct + l32;
-        ahi[ct] = __builtin_bit_cast(bf16x8, Wl[wi]);
-        alo[ct] = __builtin_bit_cast(bf16x8, Wl[NKB * 2 * BN + wi]);
+        fa[st][ct] = __builtin_bit_cast(bf16x8, Wl[wi]);
+        fa[st][2 + ct] = __builtin_bit_cast(bf16x8, Wl[NKB * 2 * BN + wi]);
       }
 #pragma unroll
       for (int pt = 0; pt < 2; ++pt) {
-        bhi[pt] = __builtin_bit_cast(bf16x8, X[boff[t] + pt * XW]);
-        blo[pt] = __builtin_bit_cast(bf16x8, X[boff[t] + XPAD + pt * XW]);
+        fb[st][pt] = __builtin_bit_cast(bf16x8, X[boff[t] + pt * XW]);
+        fb[st][2 + pt] = __builtin_bit_cast(bf16x8, X[boff[t] + XPAD + pt * XW]);
       }
+    };
+    auto mfmas = [&](int st) __attribute__((always_inline)) {
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
         for (int pt = 0; pt < 2; ++pt) {
-          acc[ct][pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[ct], bhi[pt], acc[ct][pt], 0, 0, 0);
-          acc[ct][pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[ct], blo[pt], acc[ct][pt], 0, 0, 0);
-          acc[ct][pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[ct], bhi[pt], acc[ct][pt], 0, 0, 0);
+          acc[ct][pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[st][2 + ct], fb[st][pt], acc[ct][pt], 0, 0, 0);
+          acc[ct][pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[st][ct], fb[st][2 + pt], acc[ct][pt], 0, 0, 0);
+          acc[ct][pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[st][ct], fb[st][pt], acc[ct][pt], 0, 0, 0);
         }
+    };
+    if constexpr (NSET == 2) {
+      fetch(0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);  // tap 0's reads first
+#pragma unroll
+      for (int t = 0; t < NKB; ++t) {
+        if (t + 1 < NKB) fetch(t + 1, (t + 1) & 1);
+        mfmas(t & 1);
+        if (t + 1 < NKB) {
+          // interleave: the next tap's 8 fragment reads between this tap's first 8 MFMAs
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < NKB; ++t) {
+        fetch(t, 0);
+        mfmas(0);
+      }
     }
   };
 

@@ -24,5 +24,5 @@ for PMC in "GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCL
     python3 tools/kbench.py --config $CFG --reps 3 --only warp,conv1,conv2,conv3 > $OUT/${TAG}_pmc$i.log 2>&1 || exit $?
 done
 python3 tools/pmc_summary.py $OUT/${TAG}_pmc* > $OUT/${TAG}_pmc_summary.txt
-python3 tools/traffic.py $OUT $TAG $CFG > $OUT/${TAG}_traffic.json
+python3 tools/traffic.py $OUT $TAG $CFG bf16x3 > $OUT/${TAG}_traffic.json
 echo profile-done

@@ -4,7 +4,10 @@ read bytes  = 32*RDREQ_32B + 64*RDREQ_64B + 128*RDREQ_128B   (TCC_EA0 request si
               gfx950 FETCH_SIZE formula tallies 128-B requests at 64 B — MI355X_MICROARCH §HBM)
 write bytes = WRITE_SIZE * 1024  (exact for 16-B-per-lane and 4-B-per-lane coalesced stores)
 Only dispatches of the timed stage calls are used: for each kernel, the median over its
-dispatches.  Usage: python tools/traffic.py <pmc dir> <tag> <config>
+dispatches.  Usage: python tools/traffic.py <pmc dir> <tag> <config> [precision]
+(precision = the conv arithmetic kbench ran with: bf16x3 (default) or fp32; selects which
+kernel is conv1: the ReLU dilation-1 conv over the view slab — the coord-term conv that runs
+once per weight version is the non-ReLU instance and is not conv1).
 """
 import collections
 import csv
@@ -14,6 +17,7 @@ import statistics
 import sys
 
 out_dir, tag, cfg = sys.argv[1], sys.argv[2], int(sys.argv[3])
+precision = sys.argv[4] if len(sys.argv) > 4 else "bf16x3"
 vals = collections.defaultdict(lambda: collections.defaultdict(dict))
 for f in glob.glob(f"{out_dir}/{tag}_pmc*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
@@ -24,7 +28,7 @@ def med(name, counter):
     xs = list(vals[name].get(counter, {}).values())
     return statistics.median(xs) if xs else None
 
-res = {"config": cfg, "source": f"rocprofv3 --pmc passes over tools/kbench.py ({tag})", "kernels": {}}
+res = {"config": cfg, "precision": precision, "source": f"rocprofv3 --pmc passes over tools/kbench.py ({tag})", "kernels": {}}
 for name in vals:
     if "mvbev::" not in name:
         continue
@@ -35,7 +39,8 @@ for name in vals:
     rd = 32 * n32 + 64 * n64 + 128 * n128
     res["kernels"][name] = {"read_bytes": rd, "write_bytes": wr * 1024, "hbm_bytes_per_launch": rd + wr * 1024,
                             "fetch_size_kb": med(name, "FETCH_SIZE")}
-conv1 = [k for k in res["kernels"] if "conv3x3_mfma" in k and "<1," in k]
+pat = "b3::conv_kernel<mvbev::b3::SplitIn, 1, true" if precision == "bf16x3" else "conv3x3_mfma_f32_kernel<1, true"
+conv1 = [k for k in res["kernels"] if pat in k]
 if conv1:
     res["conv1_hbm_bytes_per_launch"] = res["kernels"][conv1[0]]["hbm_bytes_per_launch"]
 print(json.dumps(res, indent=1))

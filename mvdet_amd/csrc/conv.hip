@@ -31,8 +31,9 @@
 //   optional ReLU (NaN-preserving, like torch.relu).
 //
 // mvbev_conv3x3_cout1_f32 — Cout = 1 is a 4608-long dot product per pixel: HBM/L2-bound, no
-//   MFMA.  Block = 64 pixels of a row x 4 waves; each wave sums a quarter of the channels with
-//   wave-uniform (scalar) weight loads, partial sums reduced through LDS.
+//   MFMA.  Block = 64 pixels of a row x 8 waves; each wave sums an eighth of the channels, four
+//   channels per step with independent accumulators (memory-level parallelism), wave-uniform
+//   (scalar) weight loads; partial sums reduced through LDS.
 #include "common.h"
 
 namespace mvbev {
@@ -250,13 +251,13 @@ __global__ __launch_bounds__(64 * NWAVES, MVBEV_CONV_MINWAVES) void conv3x3_mfma
   emit(acc11, 1, 1);
 }
 
+constexpr int C1_WAVES = 8;  // waves per conv3 block: each sums C/8 channels of 64 pixels
+
 template <int DIL>
-__global__ __launch_bounds__(256) void conv3x3_cout1_kernel(const float* __restrict__ x,
-                                                            const float* __restrict__ w,
-                                                            float* __restrict__ y, int C, int H,
-                                                            int W, int in_row0, int in_rows,
-                                                            int out_row0) {
-  __shared__ float part[4][64];
+__global__ __launch_bounds__(64 * C1_WAVES) void conv3x3_cout1_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ y, int C, int H,
+    int W, int in_row0, int in_rows, int out_row0) {
+  __shared__ float part[C1_WAVES][64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = blockIdx.x * 64 + lane;
@@ -270,29 +271,47 @@ __global__ __launch_bounds__(256) void conv3x3_cout1_kernel(const float* __restr
     const int xx = col + (kx - 1) * DIL;
     okx[kx] = xx >= 0 && xx < W;
   }
-  float acc = 0.f;
-  for (int c = wave; c < C; c += 4) {
+  bool oky[3];  // block-uniform
+  int64_t rowoff[3];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    const int yy = row + (ky - 1) * DIL;
+    const int by = yy - in_row0;
+    oky[ky] = yy >= 0 && yy < H && by >= 0 && by < in_rows;
+    rowoff[ky] = oky[ky] ? (int64_t)by * W : 0;
+  }
+  // contiguous channel range per wave, 4 channels per step with independent accumulators
+  // (36 independent loads in flight per step; scalar weight loads)
+  const int cpw = (C + C1_WAVES - 1) / C1_WAVES;
+  const int c0 = wave * cpw, c1 = min(C, c0 + cpw);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  auto tapsum = [&](int c, float& a) __attribute__((always_inline)) {
     const float* xc = xb + (int64_t)c * plane;
     const float* wc = w + c * 9;
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
-      const int yy = row + (ky - 1) * DIL;
-      const int by = yy - in_row0;
-      if (yy < 0 || yy >= H || by < 0 || by >= in_rows) continue;
-      const float* xr = xc + (int64_t)by * W;
+      if (!oky[ky]) continue;
+      const float* xr = xc + rowoff[ky];
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
-        const int xx = col + (kx - 1) * DIL;
-        const float v = okx[kx] ? xr[xx] : 0.f;
-        acc += wc[ky * 3 + kx] * v;
+        const float v = okx[kx] ? xr[col + (kx - 1) * DIL] : 0.f;
+        a += wc[ky * 3 + kx] * v;
       }
     }
+  };
+  int c = c0;
+  for (; c + 4 <= c1; c += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) tapsum(c + u, acc[u]);
   }
-  part[wave][lane] = acc;
+  for (; c < c1; ++c) tapsum(c, acc[0]);
+  part[wave][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   __syncthreads();
   if (wave == 0 && col < W) {
-    y[((int64_t)b * gridDim.y + blockIdx.y) * W + col] =
-        (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+    float sum = 0.f;
+#pragma unroll
+    for (int i = 0; i < C1_WAVES; ++i) sum += part[i][lane];
+    y[((int64_t)b * gridDim.y + blockIdx.y) * W + col] = sum;
   }
 }
 
@@ -379,8 +398,8 @@ int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int
   dim3 grid((unsigned)ceil_div(W, 64), (unsigned)out_rows, (unsigned)B);
   hipStream_t s = as_stream(stream);
 #define MVBEV_C1_LAUNCH(D)                                                                      \
-  hipLaunchKernelGGL(conv3x3_cout1_kernel<D>, grid, dim3(256), 0, s, x, w, y, (int)C, (int)H,    \
-                     (int)W, (int)in_row0, (int)in_rows, (int)out_row0)
+  hipLaunchKernelGGL(conv3x3_cout1_kernel<D>, grid, dim3(64 * C1_WAVES), 0, s, x, w, y, (int)C,  \
+                     (int)H, (int)W, (int)in_row0, (int)in_rows, (int)out_row0)
   switch (dilation) {
     case 1: MVBEV_C1_LAUNCH(1); break;
     case 2: MVBEV_C1_LAUNCH(2); break;

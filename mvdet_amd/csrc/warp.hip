@@ -22,6 +22,8 @@
 // of a frame (grid.z = batch x view) so the 7-view warp is a single dispatch.
 #include "common.h"
 
+#include <type_traits>
+
 namespace mvbev {
 
 #ifndef MVBEV_WARP_TH  // A/B on cfg2 (7 views, 1 launch): 8x32/2 0.89 ms, 16x16/8 0.80, 16x16/4 0.75
@@ -47,9 +49,12 @@ struct WarpView {
 struct WarpArgs {
   WarpView v[kWarpMaxViews];
   int nviews, B, C, H, W, Ho, Wo, tiles_x, tiles, chunks, nwg;
+  bool pair;  // fp32 rows with unit column stride and W >= 2: corner pairs as 8-B loads
 };
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+// a horizontally adjacent corner pair (nw,ne) / (sw,se) of an fp32 row: 8 bytes, 4-byte aligned
+typedef float f32x2u_t __attribute__((ext_vector_type(2), aligned(4)));
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 // SPLIT output: the "split-bf16 blocked" layout consumed by the 3xbf16 conv (see
@@ -67,7 +72,7 @@ __device__ inline void store_split8(u32x4_t* dst, const float (&v)[8]) {
   dst[1] = __builtin_bit_cast(u32x4_t, lo);
 }
 
-template <typename T, int UNROLL, bool SPLIT>
+template <typename T, int UNROLL, bool SPLIT, bool PAIR>
 __global__ __launch_bounds__(256) void warp_tile_kernel(const WarpArgs a) {
   // Logical block order (batch*view, channel chunk, tile) with tile fastest, dealt to the
   // XCDs in contiguous ranges: neighbouring tiles of one plane share an L2 (their source
@@ -132,11 +137,26 @@ __global__ __launch_bounds__(256) void warp_tile_kernel(const WarpArgs a) {
   const int64_t sH = vw.sH, sW = vw.sW, sC = vw.sC;
   const int64_t o_nw = cy0 * sH + cx0 * sW, o_ne = cy0 * sH + cx1 * sW;
   const int64_t o_sw = cy1 * sH + cx0 * sW, o_se = cy1 * sH + cx1 * sW;
+  // PAIR: one 8-B load per row covers both x-corners (columns bx, bx+1, bx clamped into
+  // [0, W-2]); nw/ne pick their half (x0 = -1 or W-1 leave the other corner invalid)
+  const int bx = min(max(x0, 0), W - 2);
+  const int64_t o_top = cy0 * sH + bx, o_bot = cy1 * sH + bx;
+  const bool nw_lo = x0 == bx, ne_lo = x0 + 1 == bx;
   const T* base = static_cast<const T*>(vw.src) + (int64_t)b * vw.sB;
   auto sample = [&](int c) __attribute__((always_inline)) {
     const T* pc = base + (int64_t)c * sC;
-    const float vnw = to_f32<T>(pc[o_nw]), vne = to_f32<T>(pc[o_ne]);
-    const float vsw = to_f32<T>(pc[o_sw]), vse = to_f32<T>(pc[o_se]);
+    float vnw, vne, vsw, vse;
+    if constexpr (PAIR) {
+      const f32x2u_t top = *reinterpret_cast<const f32x2u_t*>(pc + o_top);
+      const f32x2u_t bot = *reinterpret_cast<const f32x2u_t*>(pc + o_bot);
+      vnw = nw_lo ? top.x : top.y;
+      vne = ne_lo ? top.x : top.y;
+      vsw = nw_lo ? bot.x : bot.y;
+      vse = ne_lo ? bot.x : bot.y;
+    } else {
+      vnw = to_f32<T>(pc[o_nw]); vne = to_f32<T>(pc[o_ne]);
+      vsw = to_f32<T>(pc[o_sw]); vse = to_f32<T>(pc[o_se]);
+    }
     float acc = 0.f;
     acc += (ok_nw ? vnw : 0.f) * w_nw;
     acc += (ok_ne ? vne : 0.f) * w_ne;
@@ -177,14 +197,23 @@ __global__ __launch_bounds__(256) void warp_tile_kernel(const WarpArgs a) {
   }
 }
 
+template <typename T, bool SPLIT>
+static void launch_warp_t(const WarpArgs& a, hipStream_t s) {
+  if constexpr (std::is_same<T, float>::value) {
+    if (a.pair) {
+      hipLaunchKernelGGL((warp_tile_kernel<T, 4, SPLIT, true>), dim3((unsigned)a.nwg), dim3(256), 0, s, a);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((warp_tile_kernel<T, 4, SPLIT, false>), dim3((unsigned)a.nwg), dim3(256), 0, s, a);
+}
+
 template <typename T>
 static int launch_warp(const WarpArgs& a, void* stream, bool split = false) {
   if (split)
-    hipLaunchKernelGGL((warp_tile_kernel<T, 4, true>), dim3((unsigned)a.nwg), dim3(256), 0,
-                       as_stream(stream), a);
+    launch_warp_t<T, true>(a, as_stream(stream));
   else
-    hipLaunchKernelGGL((warp_tile_kernel<T, 4, false>), dim3((unsigned)a.nwg), dim3(256), 0,
-                       as_stream(stream), a);
+    launch_warp_t<T, false>(a, as_stream(stream));
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }
@@ -197,6 +226,11 @@ static int finish_args_and_launch(WarpArgs& a, int64_t B, int64_t C, int64_t H, 
   a.tiles = a.tiles_x * (int)ceil_div(Ho, kWarpTH);
   a.chunks = (int)ceil_div(C, kWarpCPB);
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
+#ifndef MVBEV_WARP_PAIR
+#define MVBEV_WARP_PAIR 1
+#endif
+  a.pair = MVBEV_WARP_PAIR && W >= 2;
+  for (int i = 0; i < a.nviews; ++i) a.pair = a.pair && a.v[i].sW == 1;
   return launch_warp<T>(a, stream, split);
 }
 

@@ -3,8 +3,9 @@
 read bytes  = 32*RDREQ_32B + 64*RDREQ_64B + 128*RDREQ_128B   (TCC_EA0 request sizes; the
               gfx950 FETCH_SIZE formula tallies 128-B requests at 64 B — MI355X_MICROARCH §HBM)
 write bytes = WRITE_SIZE * 1024  (exact for 16-B-per-lane and 4-B-per-lane coalesced stores)
-Only dispatches of the timed stage calls are used: for each kernel, the median over its
-dispatches.  Usage: python tools/traffic.py <pmc dir> <tag> <config> [precision]
+Dispatches are grouped by (kernel, grid size) — e.g. kbench's one-off per-view warps
+during setup vs the all-views warp of the timed "warp" stage — and each group reports the
+median over its dispatches.  Usage: python tools/traffic.py <pmc dir> <tag> <config> [precision]
 (precision = the conv arithmetic kbench ran with: bf16x3 (default) or fp32; selects which
 kernel is conv1: the ReLU dilation-1 conv over the view slab — the coord-term conv that runs
 once per weight version is the non-ReLU instance and is not conv1).
@@ -21,7 +22,7 @@ precision = sys.argv[4] if len(sys.argv) > 4 else "bf16x3"
 vals = collections.defaultdict(lambda: collections.defaultdict(dict))
 for f in glob.glob(f"{out_dir}/{tag}_pmc*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        name = r["Kernel_Name"].split("(")[0]
+        name = f'{r["Kernel_Name"].split("(")[0]} [grid {r["Grid_Size"]}]'
         vals[name][r["Counter_Name"]][(f, r["Dispatch_Id"])] = float(r["Counter_Value"])
 
 def med(name, counter):

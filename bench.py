@@ -200,6 +200,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-alt", action="store_true", help="skip the other-precision comparison line")
     ap.add_argument("--cpu-frames", type=int, default=0, help="frames for the CPU baseline (0 = auto)")
+    ap.add_argument("--mp-mode", default="partial", choices=["partial", "gather"],
+                    help="N>1: conv1 partial sums + reduce-scatter (default) or slab all-gather + row bands")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

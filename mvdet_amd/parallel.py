@@ -16,6 +16,15 @@ north star asks for:
    so the 26-TFLOP fusion at config 3 is split P ways instead of replicated.
 4. **A tiny all-gather of the map bands** assembles ``map_result`` on every rank.
 
+``ViewPartialSum`` is the partial-sum alternative (SURVEY §8(e) "Alternative", §8(f)
+row 3).  conv1 is linear in its input channels, so each rank computes conv1 over only
+its own views' channels for the whole grid (no slab exchange at all), then
+**reduce-scatters** those [B, 512, Ho, Wo] partial sums by row band (each rank receives
+its band summed over all ranks), all-gathers the 6 edge rows of every band as halo, adds
+the coord term + bias and ReLU, and runs conv2/conv3 on its band.  Per rank it moves
+≈ (P-1)/P × 88.5 MB at config 2 instead of (P-1)/P × 620 MB, and conv1's FLOPs split
+by views instead of by (band + halo) rows.
+
 The compute engine is pluggable (``engine`` = ``pipeline.ProjectFuse`` on GPU; the
 CPU gloo tests plug in an oracle engine), so the collective logic is tested without
 a GPU.  With the ``gloo`` backend and CUDA tensors the collectives are staged
@@ -125,6 +134,135 @@ class ViewParallel:
         return self.gather_map(band)
 
 
+def _reduce_scatter(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """``inp`` [world, *out.shape] summed over ranks; this rank's slice -> ``out``."""
+    out = out.unsqueeze(0)
+    if inp.is_cuda and dist.get_backend(group) == "gloo":
+        host = inp.cpu()
+        res = torch.empty_like(out, device="cpu")
+        dist.reduce_scatter_tensor(res, host, op=dist.ReduceOp.SUM, group=group)
+        out.copy_(res)
+        return
+    dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=group)
+
+
+class ViewPartialSum(ViewParallel):
+    """Partial-sum view-parallel fusion: conv1 split by views, reduce-scatter by rows.
+
+    The engine of rank r holds only r's views (``all_views=False`` slab); a rank with no
+    view contributes zeros.  After the reduce-scatter, rank r owns the summed conv1
+    pre-activation of rows ``[r*band, (r+1)*band)``; its halo rows (6 above and below:
+    conv2's dilation 2 + conv3's 4) come from the neighbours' bands through one small
+    all-gather of every band's top and bottom 6 rows (bands of fewer than 6 rows fall back
+    to gathering whole bands)."""
+
+    HALO = 6
+
+    def __init__(self, engine_factory, proj_mats, grid_hw, rank, world, group=None):
+        self.rank, self.world, self.group = rank, world, group
+        self.num_cam = len(proj_mats)
+        self.grid_hw = (int(grid_hw[0]), int(grid_hw[1]))
+        self.my_views = views_of(rank, world, self.num_cam)
+        self.engine = engine_factory(self.my_views) if self.my_views else None
+        self._factory = engine_factory
+        self.band = row_band(self.grid_hw[0], rank, world)
+        self.band_rows = math.ceil(self.grid_hw[0] / world)
+        self._out = {}
+        self._bufs = {}
+        # a rank without views still runs the band fusion: give it an engine over view 0's
+        # slot layout (its slab is never written or read) for the packed conv2 weights etc.
+        self._fuse_engine = self.engine if self.engine is not None else engine_factory([0])
+
+    def workspace(self, B: int, device):
+        r0, r1 = self.band
+        band = (r0, r1) if r1 > r0 else (0, 1)
+        return self._fuse_engine.workspace(B, device, band)
+
+    def _buffers(self, ws):
+        B, mid, _, W = ws.y1.shape
+        H, P, n = self.grid_hw[0], self.world, self.band_rows
+        key = (ws.y1.device, B)
+        bufs = self._bufs.get(key)
+        if bufs is None:
+            dev = ws.y1.device
+            e = min(self.HALO, n)
+            bufs = dict(
+                part=torch.zeros((B, mid, H, W), dtype=torch.float32, device=dev),
+                stage=torch.zeros((P, B, mid, n, W), dtype=torch.float32, device=dev),
+                mine=torch.zeros((B, mid, n, W), dtype=torch.float32, device=dev),
+                edges=torch.zeros((P, 2, B, mid, e, W), dtype=torch.float32, device=dev),
+                full=None if n >= self.HALO else torch.zeros((P, B, mid, n, W), dtype=torch.float32, device=dev))
+            self._bufs[key] = bufs
+        return bufs
+
+    def conv1_partial(self, ws, map_classifier) -> None:
+        bufs = self._buffers(ws)
+        if self.engine is None:
+            bufs["part"].zero_()
+        else:
+            self.engine.conv1_partial(ws, map_classifier, bufs["part"])
+        H, n = self.grid_hw[0], self.band_rows
+        for p in range(self.world):  # band-major staging for the reduce-scatter
+            a, b = min(H, p * n), min(H, (p + 1) * n)
+            if b > a:
+                bufs["stage"][p, :, :, :b - a].copy_(bufs["part"][:, :, a:b])
+
+    def exchange(self, ws) -> None:
+        """Reduce-scatter of the partial sums by band, then the halo rows into ``ws.y1``."""
+        bufs = self._buffers(ws)
+        _reduce_scatter(bufs["mine"], bufs["stage"], self.group)
+        H, P, n = self.grid_hw[0], self.world, self.band_rows
+        a1, b1 = ws.y1_rows
+
+        def rows_of(p):  # the summed rows of band p available locally after the exchange
+            return min(H, p * n), min(H, (p + 1) * n)
+
+        if bufs["full"] is not None:  # bands thinner than the halo: gather whole bands
+            bufs["full"][self.rank].copy_(bufs["mine"])
+            _all_gather_inplace(bufs["full"], self.rank, P, self.group)
+            src = {p: bufs["full"][p] for p in range(P)}
+            for p in range(P):
+                a, b = rows_of(p)
+                lo, hi = max(a, a1), min(b, b1)
+                if hi > lo:
+                    ws.y1[:, :, lo - a1:hi - a1].copy_(src[p][:, :, lo - a:hi - a])
+            return
+        e = self.HALO
+        bufs["edges"][self.rank, 0].copy_(bufs["mine"][:, :, :e])
+        r0, r1 = self.band
+        if r1 > r0:
+            last = r1 - r0
+            bufs["edges"][self.rank, 1].copy_(bufs["mine"][:, :, max(0, last - e):max(0, last - e) + e])
+        _all_gather_inplace(bufs["edges"], self.rank, P, self.group)
+        # own band
+        if r1 > r0:
+            ws.y1[:, :, r0 - a1:r1 - a1].copy_(bufs["mine"][:, :, :r1 - r0])
+        # halo above: the last rows of band rank-1; below: the first rows of band rank+1
+        if self.rank > 0 and a1 < r0:
+            pa, pb = rows_of(self.rank - 1)
+            top0 = max(pa, pb - e)  # global row of edges[rank-1, 1][:, :, 0]
+            ws.y1[:, :, :r0 - a1].copy_(bufs["edges"][self.rank - 1, 1][:, :, a1 - top0:r0 - top0])
+        if self.rank + 1 < P and b1 > r1:
+            na, _ = rows_of(self.rank + 1)
+            ws.y1[:, :, r1 - a1:].copy_(bufs["edges"][self.rank + 1, 0][:, :, :b1 - na])
+
+    def step(self, ws, feats, map_classifier, mark=None) -> torch.Tensor:
+        if mark:
+            mark("warp")
+        if self.engine is not None:  # a rank with views fuses with the same engine
+            self.warp(ws, feats)
+        if mark:
+            mark("conv1")
+        self.conv1_partial(ws, map_classifier)
+        if mark:
+            mark("exchange")
+        self.exchange(ws)
+        band = self._fuse_engine.finish_from_y1(ws, map_classifier, mark=mark)
+        if mark:
+            mark("gather_map")
+        return self.gather_map(band)
+
+
 def bench_main(args) -> None:
     """``bench.py`` under torchrun with WORLD_SIZE > 1: the view-parallel path (RCCL)."""
     import json
@@ -133,7 +271,7 @@ def bench_main(args) -> None:
 
     import numpy as np
 
-    from bench import DTYPE_LABEL, FP32_MFMA_PEAK_TFS, build_mc, head_params
+    from bench import BF16_MFMA_PEAK_TFS, DTYPE_LABEL, FP32_MFMA_PEAK_TFS, build_mc, head_params
     from . import synthetic
     from .geometry import projection_matrices
     from .pipeline import ProjectFuse
@@ -153,61 +291,87 @@ def bench_main(args) -> None:
     ho, wo = ds.reducedgrid_shape
     pm = projection_matrices(ds)
     mc = build_mc(C, N, head_params(N, seed=args.config, C=C), dev)
-    vp = ViewParallel(lambda sv: ProjectFuse(pm, up, (ho, wo), C, slot_views=sv, precision=args.precision),
-                      pm, (ho, wo), rank, world)
-    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * args.config + v, device=dev)
-             for v in vp.my_views]
-    ws = vp.workspace(B, dev)
-    K, W = args.steps, args.warmup
-    stages = ("warp", "allgather", "conv1", "conv2", "conv3", "gather_map")
-    ev = {k: [torch.cuda.Event(enable_timing=True) for _ in range(K)] for k in stages}
-    end = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
-    with torch.no_grad():
-        for _ in range(W):
-            vp.step(ws, feats, mc)
-        torch.cuda.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        for i in range(K):
-            vp.step(ws, feats, mc, mark=lambda s: ev[s][i].record())
-            end[i].record()
-        torch.cuda.synchronize()
-        dist.barrier()
-        dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
-    nxt = {stages[i]: stages[i + 1] for i in range(len(stages) - 1)}
-    stage_ms = {}
-    for s in stages:
-        e2 = ev[nxt[s]] if s in nxt else end
-        stage_ms[s] = round(float(np.mean([ev[s][i].elapsed_time(e2[i]) for i in range(K)])), 4)
-    r0, r1 = vp.band
-    y1r = ws.y1_rows
-    conv1_flop = 2.0 * B * (y1r[1] - y1r[0]) * wo * 9 * N * C * 512
-    conv1_tfs = conv1_flop / (stage_ms["conv1"] * 1e-3) / 1e12
+
+    def run(mode):
+        if mode == "partial":
+            vp = ViewPartialSum(lambda sv: ProjectFuse(pm, up, (ho, wo), C, slot_views=sv, precision=args.precision,
+                                                       all_views=False), pm, (ho, wo), rank, world)
+            stages = ("warp", "conv1", "exchange", "conv2", "conv3", "gather_map")
+        else:
+            vp = ViewParallel(lambda sv: ProjectFuse(pm, up, (ho, wo), C, slot_views=sv, precision=args.precision),
+                              pm, (ho, wo), rank, world)
+            stages = ("warp", "allgather", "conv1", "conv2", "conv3", "gather_map")
+        feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * args.config + v,
+                                              device=dev) for v in vp.my_views]
+        ws = vp.workspace(B, dev)
+        K, W = args.steps, args.warmup
+        ev = {k: [torch.cuda.Event(enable_timing=True) for _ in range(K)] for k in stages}
+        end = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+        with torch.no_grad():
+            for _ in range(W):
+                vp.step(ws, feats, mc)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for i in range(K):
+                vp.step(ws, feats, mc, mark=lambda s: ev[s][i].record())
+                end[i].record()
+            torch.cuda.synchronize()
+            dist.barrier()
+            dt = time.perf_counter() - t0
+        t = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+        nxt = {stages[i]: stages[i + 1] for i in range(len(stages) - 1)}
+        stage_ms = {}
+        for st in stages:
+            e2 = ev[nxt[st]] if st in nxt else end
+            stage_ms[st] = round(float(np.mean([ev[st][i].elapsed_time(e2[i]) for i in range(K)])), 4)
+        if mode == "partial":
+            conv1_flop = 2.0 * B * ho * wo * 9 * len(vp.my_views) * C * 512
+        else:
+            y1r = ws.y1_rows
+            conv1_flop = 2.0 * B * (y1r[1] - y1r[0]) * wo * 9 * N * C * 512
+        conv1_tfs = conv1_flop / (stage_ms["conv1"] * 1e-3) / 1e12
+        return dict(value=round(B * K / dt, 3), ms=round(dt * 1e3 / K, 4), stage_ms=stage_ms, band=vp.band,
+                    conv1_tfs=conv1_tfs)
+
+    mode = getattr(args, "mp_mode", "partial")
+    res = run(mode)
+    alt_mode = "gather" if mode == "partial" else "partial"
+    alt = None if getattr(args, "no_alt", False) else run(alt_mode)
+    bf16 = args.precision == "bf16x3"
+    achieved = res["conv1_tfs"] * (3 if bf16 else 1)
+    peak = BF16_MFMA_PEAK_TFS if bf16 else FP32_MFMA_PEAK_TFS
+    how = (f"views' conv1 partial sums, {backend} reduce-scatter by row band + edge-row all-gather"
+           if mode == "partial" else f"{backend} all-gather of the warped slab + row-band fusion")
     if rank == 0:
-        print(json.dumps({
+        line = {
             "metric": "multi-view frames/sec (project+fuse)",
-            "value": round(B * K / dt, 3),
+            "value": res["value"],
             "unit": "frames/s",
             "n_gpus": world,
-            "steps": K,
-            "warmup": W,
-            "ms_per_step": round(dt * 1e3 / K, 4),
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": res["ms"],
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": DTYPE_LABEL[args.precision],
             "data": "synthetic (see single-GPU line)",
             "config": {"workload": f"cfg{args.config}: {spec['name']}", "views": N, "channels": C, "batch": B,
-                       "src_hw": list(up), "grid_hw": [ho, wo],
-                       "parallelism": f"view-parallel x{world} ({backend} all-gather) + row-band fusion"},
-            "roofline": {"kernel": "conv3x3_mfma_f32 (conv1 band, rank 0)", "bound": "mfma",
-                         "achieved": round(conv1_tfs, 2), "peak": FP32_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-                         "frac": round(conv1_tfs / FP32_MFMA_PEAK_TFS, 4), "traffic": None},
-            "stages_ms_rank0": stage_ms,
-            "band_rank0": [r0, r1],
-        }), flush=True)
+                       "src_hw": list(up), "grid_hw": [ho, wo], "precision": args.precision,
+                       "parallelism": f"view-parallel x{world} ({backend}): {how}"},
+            "roofline": {"kernel": "conv1 on rank 0 (" + ("partial over its views" if mode == "partial"
+                                                           else "row band + halo") + ")",
+                         "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4), "traffic": None},
+            "stages_ms_rank0": res["stage_ms"],
+            "band_rank0": list(res["band"]),
+        }
+        if alt is not None:
+            line["alt_mode"] = {"mode": alt_mode, "value": alt["value"], "ms_per_step": alt["ms"],
+                                "stages_ms_rank0": alt["stage_ms"]}
+        print(json.dumps(line), flush=True)
     dist.barrier()
     dist.destroy_process_group()

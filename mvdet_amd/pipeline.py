@@ -65,7 +65,8 @@ class ProjectFuse:
 
     def __init__(self, proj_mats: Sequence[torch.Tensor], src_hw: Tuple[int, int], grid_hw: Tuple[int, int],
                  channels: int, mid_channels: int = 512, slot_views: Optional[Sequence[Optional[int]]] = None,
-                 precision: str = "bf16x3", slab_dtype: torch.dtype = torch.float32):
+                 precision: str = "bf16x3", slab_dtype: torch.dtype = torch.float32,
+                 all_views: bool = True):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":
@@ -84,7 +85,10 @@ class ProjectFuse:
         self.slot_views = list(range(self.num_cam)) if slot_views is None else list(slot_views)
         self.S = len(self.slot_views)
         self.slot_of = {v: s for s, v in enumerate(self.slot_views) if v is not None}
-        assert sorted(self.slot_of) == list(range(self.num_cam)), "every view needs exactly one slot"
+        if all_views:
+            assert sorted(self.slot_of) == list(range(self.num_cam)), "every view needs exactly one slot"
+        else:  # partial-sum multi-GPU: this engine's slab holds a subset of the views
+            assert set(self.slot_of) <= set(range(self.num_cam)) and self.S > 0
         # kornia steps 1-2 (normalize_homography + _torch_inverse_cast) on the host, fp32,
         # from the fp32-cast projection matrix exactly as :68-69 feeds kornia.
         self.m_norm_cpu = torch.stack([
@@ -205,6 +209,30 @@ class ProjectFuse:
         r0, r1 = ws.band
         return ops.conv3x3_cout1(ws.y2, conv3.weight, 4, H=H, in_row0=ws.y2_rows[0], out_row0=r0,
                                  out_rows=r1 - r0)
+
+    # -- partial-sum multi-GPU (SURVEY §8(e) alternative, §8(f) row 3) -----------------------
+    def conv1_partial(self, ws: Workspace, map_classifier: torch.nn.Sequential, out: torch.Tensor) -> torch.Tensor:
+        """conv1 restricted to this slab's views (its slice of conv1's input channels), all
+        grid rows, no bias / coord term / ReLU: one rank's term of conv1's channel sum.
+        ``out``: contiguous [B, 512, Ho, Wo] fp32."""
+        H, W = self.grid_hw
+        B = ws.slab.shape[1]
+        p1 = self.pack1.get(map_classifier[0].weight)
+        d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * H * W,
+                           batch_stride=self.Cs * H * W, in_row0=0, in_rows=H, out_row0=0, out_rows=H)
+        return ops.conv3x3_desc(ws.slab, d1, p1, self.mid, bias=None, init=None, dilation=1, relu=False,
+                                out=out)
+
+    def finish_from_y1(self, ws: Workspace, map_classifier: torch.nn.Sequential, mark=None) -> torch.Tensor:
+        """``ws.y1`` holds conv1's summed channel terms (no bias) for rows ``ws.y1_rows``:
+        add the coord term (+ bias), ReLU, then conv2 and conv3 on the band."""
+        a1, b1 = ws.y1_rows
+        ws.y1.add_(self.coord_term(map_classifier[0])[:, a1:b1]).relu_()
+        for stage, idx, fn in (("conv2", 2, self.conv2), ("conv3", 4, self.conv3)):
+            if mark:
+                mark(stage)
+            out = fn(ws, map_classifier[idx])
+        return out
 
     def fuse(self, ws: Workspace, map_classifier: torch.nn.Sequential, mark=None) -> torch.Tensor:
         """a7-a9 on ``ws.slab`` for the output rows ``ws.band`` → [B, 1, rows, Wo].

@@ -2,9 +2,10 @@
 
 * Row bands: the fusion computed band by band (as each rank does after the
   all-gather) is bitwise identical to the whole-grid fusion.
-* A 2-rank rehearsal of the view-parallel path on the single GPU of the test box
-  (gloo collectives staged through host memory): every rank's assembled map equals
-  the single-process HIP result bitwise.
+* Rehearsals of both multi-GPU modes (slab all-gather; conv1 partial sums +
+  reduce-scatter) with 2-4 ranks on the single GPU of the test box (gloo collectives
+  staged through host memory): every rank's assembled map equals the single-process
+  HIP result to fp32 summation-order rounding.
 """
 import os
 import socket
@@ -58,14 +59,18 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, mode="gather"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from mvdet_amd import ProjectFuse
-    from mvdet_amd.parallel import ViewParallel
+    from mvdet_amd.parallel import ViewParallel, ViewPartialSum
     ds, pm, up, grid, C, B, feats, mc = _setup()
     mc = mc.to("cuda:0")
-    vp = ViewParallel(lambda sv: ProjectFuse(pm, up, grid, C, slot_views=sv), pm, grid, rank, world)
+    if mode == "partial":
+        vp = ViewPartialSum(lambda sv: ProjectFuse(pm, up, grid, C, slot_views=sv, all_views=False), pm, grid,
+                            rank, world)
+    else:
+        vp = ViewParallel(lambda sv: ProjectFuse(pm, up, grid, C, slot_views=sv), pm, grid, rank, world)
     ws = vp.workspace(B, "cuda:0")
     with torch.no_grad():
         out = vp.step(ws, [feats[v].cuda() for v in vp.my_views], mc)
@@ -74,10 +79,12 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_two_rank_rehearsal_matches_single_process(tmp_path):
+@pytest.mark.parametrize("world,mode", [(2, "gather"), (2, "partial"), (4, "partial")])
+def test_rank_rehearsal_matches_single_process(world, mode, tmp_path):
+    """gather / partial-sum modes; world 4 (3 views) includes a rank without views and
+    bands of 8 rows (edge-row halo exchange)."""
     from mvdet_amd import ProjectFuse
-    world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world, join=True)
     ds, pm, up, grid, C, B, feats, mc = _setup()
     mc = mc.to("cuda:0")
     with torch.no_grad():

@@ -105,6 +105,19 @@ int mvbev_warp_views_f32(const mvbev_warp_view* views, int nviews, int64_t B, in
 int mvbev_warp_views_split_bf16(const mvbev_warp_view* views, int nviews, int src_is_f16,
                                 int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
                                 void* stream);
+/* Fused bilinear upsample + warp.  views[i].src is the
+ * backbone-resolution map [B][C][h][w] that persp_trans_detector.py:65 upsamples with
+ * F.interpolate(size=(H, W), mode='bilinear', align_corners=False) before the warp at :69;
+ * every bilinear corner of the warp is that upsample evaluated on the fly (one 3x3 source
+ * window per output pixel), so the [B][C][H][W] intermediate is never written.  m is the
+ * kornia matrix for the UPSAMPLED size (H, W) — the same one mvbev_warp_views_* take.
+ * Upsampling only (H >= h, W >= w).  out_layout: MVBEV_LAYOUT_F32 (fp32 src) or
+ * MVBEV_LAYOUT_SPLIT_BF16 (fp32 or fp16 src); dst strides as in the entry points above.
+ * NaN/inf in the source map are outside the contract (a zero-weight tap of the window may
+ * propagate them). */
+int mvbev_warp_views_upsampled(const mvbev_warp_view* views, int nviews, int src_is_f16,
+                               int64_t B, int64_t C, int64_t h, int64_t w, int64_t H, int64_t W,
+                               int64_t Ho, int64_t Wo, int out_layout, void* stream);
 /* fp16 storage for src and dst, fp32 math. */
 int mvbev_warp_views_f16(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
                          int64_t H, int64_t W, int64_t Ho, int64_t Wo, void* stream);

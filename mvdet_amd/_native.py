@@ -21,6 +21,7 @@ EXPORTS = (
     "mvbev_warp_views_f32",
     "mvbev_warp_views_f16",
     "mvbev_warp_views_split_bf16",
+    "mvbev_warp_views_upsampled",
     "mvbev_fill_coord_map_f32",
     "mvbev_conv3x3_packed_floats",
     "mvbev_pack_conv3x3_weight_f32",
@@ -74,6 +75,9 @@ def _declare(lib):
     lib.mvbev_warp_views_split_bf16.restype = ctypes.c_int
     lib.mvbev_warp_views_split_bf16.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, ctypes.c_int, _i64, _i64,
                                                 _i64, _i64, _i64, _i64, _p]
+    lib.mvbev_warp_views_upsampled.restype = ctypes.c_int
+    lib.mvbev_warp_views_upsampled.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, ctypes.c_int, _i64, _i64,
+                                               _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_int, _p]
     lib.mvbev_fill_coord_map_f32.restype = ctypes.c_int
     lib.mvbev_fill_coord_map_f32.argtypes = [_p, _i64, _i64, _i64, _i64x4, _p]
     lib.mvbev_conv3x3_packed_floats.restype = ctypes.c_size_t

@@ -20,57 +20,11 @@
 // corners of neighbouring pixels share 128-B lines in L1/L2) instead of being re-fetched
 // by the blocks of neighbouring output rows on other XCDs.  One launch covers every view
 // of a frame (grid.z = batch x view) so the 7-view warp is a single dispatch.
-#include "common.h"
+#include "warp_common.h"
 
 #include <type_traits>
 
 namespace mvbev {
-
-#ifndef MVBEV_WARP_TH  // A/B on cfg2 (7 views, 1 launch): 8x32/2 0.89 ms, 16x16/8 0.80, 16x16/4 0.75
-#define MVBEV_WARP_TH 16
-#define MVBEV_WARP_TW 16
-#define MVBEV_WARP_WR 4
-#endif
-constexpr int kWarpTH = MVBEV_WARP_TH;  // output rows per block
-constexpr int kWarpTW = MVBEV_WARP_TW;  // output cols per block
-constexpr int kWarpWR = MVBEV_WARP_WR;  // output rows per wave (wave tile WR x 64/WR)
-constexpr int kWarpCPB = 64;            // channels per block
-constexpr int kWarpMaxViews = 16;
-
-struct WarpView {
-  const void* src;
-  int64_t sB, sC, sH, sW;
-  void* dst;
-  int64_t dB, dC, dH;
-  const float* m_dev;  // device [B][9] (per batch item) or nullptr -> m below
-  float m[9];          // src_norm <- dst_norm, shared by every batch item
-};
-
-struct WarpArgs {
-  WarpView v[kWarpMaxViews];
-  int nviews, B, C, H, W, Ho, Wo, tiles_x, tiles, chunks, nwg;
-  bool pair;  // fp32 rows with unit column stride and W >= 2: corner pairs as 8-B loads
-};
-
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-// a horizontally adjacent corner pair (nw,ne) / (sw,se) of an fp32 row: 8 bytes, 4-byte aligned
-typedef float f32x2u_t __attribute__((ext_vector_type(2), aligned(4)));
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-
-// SPLIT output: the "split-bf16 blocked" layout consumed by the 3xbf16 conv (see
-// mvbev.h MVBEV_LAYOUT_SPLIT_BF16): per (batch, group of 8 channels, row, col) 32 bytes =
-// bf16 hi[8] then bf16 lo[8] with x = hi + lo (+ ~2^-17 relative); dst strides in 32-B units.
-__device__ inline void store_split8(u32x4_t* dst, const float (&v)[8]) {
-  bf16x8_t hi, lo;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const __bf16 h = (__bf16)v[j];
-    hi[j] = h;
-    lo[j] = (__bf16)(v[j] - (float)h);
-  }
-  dst[0] = __builtin_bit_cast(u32x4_t, hi);
-  dst[1] = __builtin_bit_cast(u32x4_t, lo);
-}
 
 template <typename T, int UNROLL, bool SPLIT, bool PAIR>
 __global__ __launch_bounds__(256) void warp_tile_kernel(const WarpArgs a) {

@@ -1,0 +1,243 @@
+// Fused 3x bilinear upsample + homography warp for gfx950.
+//
+// The reference feeds the warp an upsampled copy of the backbone map:
+//   img_feature = F.interpolate(feat, upsample_shape, mode='bilinear')   persp_trans_detector.py:65
+//   world_feature = kornia...warp_perspective(img_feature, proj_mat, ...)                     :69
+// (align_corners=False for the upsample, True for the warp's grid_sample).  Here the [B,C,H,W]
+// upsampled tensor (265 MB per view at config 2) is never materialised: every bilinear corner
+// of the warp is the upsample evaluated on the fly from the [B,C,h,w] map.
+//
+// Per output pixel (channel-independent, once): the warp's corner positions and weights in
+// the upsampled grid exactly as warp_tile_kernel computes them; for each in-bounds corner
+// (ux, uy) the upsample's source taps (PyTorch area_pixel_compute_source_index:
+// s = max(0, (u + 0.5) * (in/out) - 0.5), i0 = floor(s), i1 = min(i0 + 1, in - 1),
+// l1 = s - i0, l0 = 1 - l1).  Two adjacent upsampled rows (columns) reach at most three
+// consecutive source rows (columns) when out >= in, so the whole sample is one 3x3 window of
+// the source with 9 combined weights.  Per channel: 9 loads (L1/L2-resident: the source is
+// 1/9 of the upsampled size) and 9 FMAs.
+#include "warp_common.h"
+
+namespace mvbev {
+
+struct UpArgs {
+  WarpArgs w;     // views, sizes of the UPSAMPLED image in w.H/w.W, grid, tiling
+  int h, sw;      // source (backbone-resolution) height and width
+  float sy, sx;   // upsample source scales in/out (h/H, w/W) as PyTorch computes them
+};
+
+// a window row of 4 fp32 source pixels: 16 bytes, 4-byte aligned
+typedef float f32x4u_t __attribute__((ext_vector_type(4), aligned(4)));
+
+template <typename T, bool SPLIT, bool QUAD>
+__global__ __launch_bounds__(256) void warp_up_kernel(const UpArgs ua) {
+  const WarpArgs& a = ua.w;
+  const int lb = xcd_remap(blockIdx.x, a.nwg);
+  const int tile = lb % a.tiles;
+  const int chunk = (lb / a.tiles) % a.chunks;
+  const int bv = lb / (a.tiles * a.chunks);
+  const int view = bv % a.nviews;
+  const int b = bv / a.nviews;
+  const WarpView& vw = a.v[view];
+  const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
+  constexpr int WC = 64 / kWarpWR, WAVES_X = kWarpTW / WC;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int v = ty * kWarpTH + (wave / WAVES_X) * kWarpWR + lane / WC;
+  const int u = tx * kWarpTW + (wave % WAVES_X) * WC + lane % WC;
+  if (v >= a.Ho || u >= a.Wo) return;
+  const int c_begin = chunk * kWarpCPB;
+  const int c_end = min(a.C, c_begin + kWarpCPB);
+  const int H = a.H, W = a.W, h = ua.h, w = ua.sw;
+
+  float m[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) m[i] = vw.m[i];
+  // warp corners in the upsampled grid: identical arithmetic to warp_tile_kernel
+  const float gx = ((float)u / (float)(a.Wo - 1) - 0.5f) * 2.0f;
+  const float gy = ((float)v / (float)(a.Ho - 1) - 0.5f) * 2.0f;
+  float x = gx * m[0] + gy * m[1] + m[2];
+  float y = gx * m[3] + gy * m[4] + m[5];
+  const float z = gx * m[6] + gy * m[7] + m[8];
+  const float scale = fabsf(z) > 1e-8f ? 1.0f / (z + 1e-8f) : 1.0f;
+  x = scale * x;
+  y = scale * y;
+  const float ix = ((x + 1.f) / 2.f) * (float)(W - 1);
+  const float iy = ((y + 1.f) / 2.f) * (float)(H - 1);
+  const bool finite = isfinite(ix) && isfinite(iy);
+  const bool inside = finite && ix > -1.f && ix < (float)W && iy > -1.f && iy < (float)H;
+  const float fill = finite ? 0.f : __builtin_nanf("");
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  const int x0 = inside ? (int)fx0 : 0, y0 = inside ? (int)fy0 : 0;
+  const float wx[2] = {fx0 + 1.f - ix, ix - fx0};  // warp weights of columns x0, x0+1
+  const float wy[2] = {fy0 + 1.f - iy, iy - fy0};  // ... of rows y0, y0+1
+
+  // upsample taps of the two corner columns / rows; window base = first valid corner's tap
+  int cxi[2][2], cyi[2][2];
+  float lxv[2][2], lyv[2][2];
+  bool okx[2], oky[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int ux = x0 + k, uy = y0 + k;
+    okx[k] = inside && ux >= 0 && ux <= W - 1;
+    oky[k] = inside && uy >= 0 && uy <= H - 1;
+    float s = ua.sx * ((float)ux + 0.5f) - 0.5f;
+    s = s < 0.f ? 0.f : s;
+    int i0 = (int)s;
+    i0 = min(i0, w - 1);
+    cxi[k][0] = i0;
+    cxi[k][1] = i0 + (i0 < w - 1 ? 1 : 0);
+    lxv[k][1] = s - (float)i0;
+    lxv[k][0] = 1.f - lxv[k][1];
+    s = ua.sy * ((float)uy + 0.5f) - 0.5f;
+    s = s < 0.f ? 0.f : s;
+    i0 = (int)s;
+    i0 = min(i0, h - 1);
+    cyi[k][0] = i0;
+    cyi[k][1] = i0 + (i0 < h - 1 ? 1 : 0);
+    lyv[k][1] = s - (float)i0;
+    lyv[k][0] = 1.f - lyv[k][1];
+  }
+  const int cb = okx[0] ? cxi[0][0] : cxi[1][0];
+  const int rb = oky[0] ? cyi[0][0] : cyi[1][0];
+  // per-axis window weights: column j of the window gets sum over valid corner columns k
+  // and their taps t landing on it of wx[k] * lx[k][t]; rows likewise.  The 2-D corner
+  // weights factor (w_nw = wx0*wy0 ...), so the 3x3 weights are outer products.
+  float ax[3] = {0.f, 0.f, 0.f}, ay[3] = {0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        ax[j] += (okx[k] && cxi[k][t] - cb == j) ? wx[k] * lxv[k][t] : 0.f;
+        ay[j] += (oky[k] && cyi[k][t] - rb == j) ? wy[k] * lyv[k][t] : 0.f;
+      }
+    }
+  // one 16-B load per window row: shift the window left to fit 4 columns inside the row
+  // (the shifted-in column gets weight 0); rows are clamped (their weights are 0 past h-1)
+  const bool wide = QUAD && w >= 4;
+  const int c4 = wide ? min(cb, w - 4) : cb;
+  const int sh = cb - c4;  // 0 .. 2
+  float bx[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int k = j - sh;
+    bx[j] = (k == 0 ? ax[0] : 0.f) + (k == 1 ? ax[1] : 0.f) + (k == 2 ? ax[2] : 0.f);
+  }
+  int col[3], row[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    col[j] = min(cb + j, w - 1);
+    row[j] = min(rb + j, h - 1);
+  }
+  const int64_t sH = vw.sH, sW = vw.sW, sC = vw.sC;
+  int64_t off[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) off[i][j] = row[i] * sH + (wide ? c4 + j : col[j]) * sW;
+  const T* base = static_cast<const T*>(vw.src) + (int64_t)b * vw.sB;
+  auto sample = [&](int c) __attribute__((always_inline)) {
+    const T* pc = base + (int64_t)c * sC;
+    float acc = 0.f;
+    if (wide) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const f32x4u_t q = *reinterpret_cast<const f32x4u_t*>(pc + off[i][0]);
+        acc += ay[i] * (bx[0] * q.x + bx[1] * q.y + bx[2] * q.z + bx[3] * q.w);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        float r = 0.f;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) r += ax[j] * to_f32<T>(pc[off[i][j]]);
+        acc += ay[i] * r;
+      }
+    }
+    return acc;
+  };
+
+  if constexpr (SPLIT) {
+    u32x4_t* out = static_cast<u32x4_t*>(vw.dst) + 2 * ((int64_t)b * vw.dB + (int64_t)v * vw.dH + u);
+    const int64_t dG = 2 * vw.dC;
+    for (int g = c_begin / 8; g * 8 < c_end; ++g) {
+      float vals[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = g * 8 + j;
+        vals[j] = c < c_end ? (inside ? sample(c) : fill) : 0.f;
+      }
+      store_split8(out + g * dG, vals);
+    }
+  } else {
+    T* out = static_cast<T*>(vw.dst) + (int64_t)b * vw.dB + (int64_t)v * vw.dH + u;
+    const int64_t dC = vw.dC;
+    for (int c = c_begin; c < c_end; c += 4) {
+      float r[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k] = (c + k < c_end) ? (inside ? sample(c + k) : fill) : 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (c + k < c_end) out[(int64_t)(c + k) * dC] = from_f32<T>(r[k]);
+    }
+  }
+}
+
+}  // namespace mvbev
+
+extern "C" int mvbev_warp_views_upsampled(const mvbev_warp_view* views, int nviews, int src_is_f16,
+                                          int64_t B, int64_t C, int64_t h, int64_t w, int64_t H,
+                                          int64_t W, int64_t Ho, int64_t Wo, int out_layout,
+                                          void* stream) {
+  using namespace mvbev;
+  if (!views) return MVBEV_ERR_NULL;
+  if (B <= 0 || C <= 0 || h <= 0 || w <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 ||
+      nviews <= 0)
+    return MVBEV_ERR_RANK;
+  if (nviews > kWarpMaxViews || B * nviews > 65535 || C > INT32_MAX || H > INT32_MAX / 2 ||
+      W > INT32_MAX / 2 || Ho > INT32_MAX / 2 || Wo > INT32_MAX / 2 || H < h || W < w ||
+      ceil_div(Ho, kWarpTH) * ceil_div(Wo, kWarpTW) * ceil_div(C, kWarpCPB) * B * nviews > INT32_MAX)
+    return MVBEV_ERR_SHAPE;  // upsampling only (H >= h, W >= w): the 3x3 window bound
+  if (out_layout != MVBEV_LAYOUT_F32 && out_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;
+  if (out_layout == MVBEV_LAYOUT_F32 && src_is_f16) return MVBEV_ERR_SHAPE;
+  UpArgs ua = {};
+  WarpArgs& a = ua.w;
+  for (int i = 0; i < nviews; ++i) {
+    const mvbev_warp_view& s = views[i];
+    if (!s.src || !s.dst) return MVBEV_ERR_NULL;
+    if (s.dst_strides[3] != 1) return MVBEV_ERR_STRIDE;
+    WarpView& d = a.v[i];
+    d.src = s.src; d.sB = s.src_strides[0]; d.sC = s.src_strides[1];
+    d.sH = s.src_strides[2]; d.sW = s.src_strides[3];
+    d.dst = s.dst; d.dB = s.dst_strides[0]; d.dC = s.dst_strides[1]; d.dH = s.dst_strides[2];
+    d.m_dev = nullptr;
+    for (int k = 0; k < 9; ++k) d.m[k] = s.m[k];
+  }
+  a.nviews = nviews;
+  a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
+  a.tiles_x = (int)ceil_div(Wo, kWarpTW);
+  a.tiles = a.tiles_x * (int)ceil_div(Ho, kWarpTH);
+  a.chunks = (int)ceil_div(C, kWarpCPB);
+  a.nwg = a.tiles * a.chunks * a.B * a.nviews;
+  ua.h = (int)h; ua.sw = (int)w;
+  ua.sy = (float)h / (float)H;  // area_pixel_compute_scale(align_corners=false, no scale)
+  ua.sx = (float)w / (float)W;
+  hipStream_t st = as_stream(stream);
+  // fp32 rows with unit column stride: 16-B row loads (QUAD); otherwise 9 scalar loads
+  bool quad = !src_is_f16;
+  for (int i = 0; i < nviews; ++i) quad = quad && views[i].src_strides[3] == 1;
+  if (out_layout == MVBEV_LAYOUT_SPLIT_BF16) {
+    if (src_is_f16)
+      hipLaunchKernelGGL((warp_up_kernel<__half, true, false>), dim3((unsigned)a.nwg), dim3(256), 0, st, ua);
+    else if (quad)
+      hipLaunchKernelGGL((warp_up_kernel<float, true, true>), dim3((unsigned)a.nwg), dim3(256), 0, st, ua);
+    else
+      hipLaunchKernelGGL((warp_up_kernel<float, true, false>), dim3((unsigned)a.nwg), dim3(256), 0, st, ua);
+  } else if (quad) {
+    hipLaunchKernelGGL((warp_up_kernel<float, false, true>), dim3((unsigned)a.nwg), dim3(256), 0, st, ua);
+  } else {
+    hipLaunchKernelGGL((warp_up_kernel<float, false, false>), dim3((unsigned)a.nwg), dim3(256), 0, st, ua);
+  }
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}

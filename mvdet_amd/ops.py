@@ -82,6 +82,50 @@ def split_decode(t: torch.Tensor, C: Optional[int] = None) -> torch.Tensor:
     return v[:, :C] if C is not None else v
 
 
+def warp_views_upsampled_into(srcs, up_hw, m_norms, dsts, split: bool = False) -> None:
+    """Fused bilinear upsample + warp of several views in ONE launch.
+
+    ``srcs[i]`` [B,C,h,w] backbone-resolution maps that the reference upsamples to ``up_hw``
+    with ``F.interpolate(..., mode='bilinear')`` (``persp_trans_detector.py:65``) before the
+    warp; ``m_norms[i]`` the kornia matrix for the upsampled size; ``dsts`` as in
+    ``warp_views_into`` (fp32 [B,C,Ho,Wo] views, or split-bf16 blocked with ``split=True``)."""
+    n = len(srcs)
+    if n == 0:
+        return
+    if not (len(m_norms) == n == len(dsts)) or n > 16:
+        raise ValueError("need 1..16 matching srcs / m_norms / dsts")
+    _require_cuda(*srcs, *dsts)
+    B, C, h, w = srcs[0].shape
+    H, W = int(up_hw[0]), int(up_hw[1])
+    if H < h or W < w:
+        raise ValueError(f"upsample size {up_hw} must not be smaller than the source {(h, w)}")
+    dtype = srcs[0].dtype
+    Ho, Wo = dsts[0].shape[2], dsts[0].shape[3]
+    want = split_shape(B, C, Ho, Wo) if split else (B, C, Ho, Wo)
+    arr = (_native.WarpView * n)()
+    for i, (s, m, d) in enumerate(zip(srcs, m_norms, dsts)):
+        if tuple(s.shape) != (B, C, h, w) or tuple(d.shape) != want or s.dtype != dtype:
+            raise ValueError(f"all views must share shapes/dtype: src {tuple(s.shape)} dst {tuple(d.shape)}")
+        if split:
+            if d.dtype != torch.bfloat16 or d.stride(5) != 1 or d.stride(4) != KC or d.stride(3) != 2 * KC:
+                raise ValueError("split dst must be a bf16 [B,G,Ho,Wo,2,8] tensor with contiguous pixels")
+            dstr = (d.stride(0) // 16, d.stride(1) // 16, d.stride(2) // 16, 1)
+        else:
+            if d.dtype != torch.float32 or dtype != torch.float32:
+                raise TypeError("the fp32-output fused warp takes fp32 sources and destinations")
+            dstr = tuple(d.stride())
+        mm = torch.as_tensor(m, dtype=torch.float32).reshape(9).tolist()
+        arr[i] = _native.WarpView(s.data_ptr(), (ctypes.c_int64 * 4)(*s.stride()), d.data_ptr(),
+                                  (ctypes.c_int64 * 4)(*dstr), (ctypes.c_float * 9)(*mm))
+    if dtype not in (torch.float32, torch.float16):
+        raise TypeError(f"unsupported dtype {dtype}")
+    lib = _native.load()
+    st = lib.mvbev_warp_views_upsampled(arr, n, int(dtype == torch.float16), B, C, h, w, H, W, Ho, Wo,
+                                        _native.LAYOUT_SPLIT_BF16 if split else _native.LAYOUT_F32,
+                                        _stream(dsts[0]))
+    _native.check(st, "mvbev_warp_views_upsampled")
+
+
 def warp_views_into(srcs, m_norms, dsts, split: bool = False, C: Optional[int] = None) -> None:
     """Warp several views (same shapes) in ONE launch.
 

@@ -159,6 +159,16 @@ class ProjectFuse:
         ops.warp_views_into(list(feats), [self.m_norm_cpu[c] for c in cams],
                             [self._slot_dst(ws, c) for c in cams], split=self.split)
 
+    def warp_views_upsampled(self, ws: Workspace, cams: Sequence[int], feats: Sequence[torch.Tensor]) -> None:
+        """a4 + a5 fused: ``feats[i]`` is view ``cams[i]``'s
+        backbone-resolution map [B,C,h,w]; the 3x bilinear upsample to ``src_hw``
+        (``persp_trans_detector.py:65``) happens inside the warp, never in HBM."""
+        for cam, f in zip(cams, feats):
+            if f.shape[1] != self.C or f.shape[2] > self.src_hw[0] or f.shape[3] > self.src_hw[1]:
+                raise ValueError(f"view {cam}: features {tuple(f.shape)} cannot upsample to {self.src_hw}")
+        ops.warp_views_upsampled_into(list(feats), self.src_hw, [self.m_norm_cpu[c] for c in cams],
+                                      [self._slot_dst(ws, c) for c in cams], split=self.split)
+
     # -- coord term (a2 folded into conv1) --------------------------------------------------
     def coord_term(self, conv1: torch.nn.Conv2d) -> torch.Tensor:
         """[512, Ho, Wo]: bias + conv(coord channels) for the current conv1 parameters."""

@@ -142,14 +142,19 @@ CONFIGS = {
 }
 
 
+def backbone_features(B: int, C: int, backbone_hw, seed: int, device="cpu"):
+    """ReLU(N(0,1)) at backbone resolution [B, C, h, w] (the map ``:64`` produces)."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    return torch.randn(B, C, *backbone_hw, generator=g, device=device).clamp_min_(0)
+
+
 def synthetic_features(B: int, C: int, backbone_hw, upsample_hw, seed: int, device="cpu"):
     """ReLU(N(0,1)) at backbone resolution, bilinearly upsampled (``:64-65``).
 
     Returns [B, C, h, w] float32 on ``device`` (generated on that device).
     """
-    import torch
     import torch.nn.functional as F
-    g = torch.Generator(device=device)
-    g.manual_seed(seed)
-    x = torch.randn(B, C, *backbone_hw, generator=g, device=device).clamp_min_(0)
+    x = backbone_features(B, C, backbone_hw, seed, device)
     return F.interpolate(x, list(upsample_hw), mode="bilinear")

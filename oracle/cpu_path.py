@@ -6,6 +6,7 @@ ops — exactly the ops the reference calls, with kornia replaced by the
 
 * a1  ``proj_mats_from_rig``   ``persp_trans_detector.py:18-30, 89-101``
 * a2  ``coord_map``            ``:103-112``
+* a4  ``upsample``             ``:65`` (the producer of the warp input; "+a4" variant)
 * a5  warp per view            ``:68-69``  (``kornia_warp.warp_perspective``)
 * a6  ``torch.cat``            ``:77``
 * a7-a9 ``map_classifier``     ``:51-54, 81`` (``F.conv2d`` = what ``nn.Conv2d`` runs)
@@ -43,6 +44,12 @@ def coord_map(ho: int, wo: int) -> torch.Tensor:
     gx, gy = np.meshgrid(np.arange(wo), np.arange(ho))
     return torch.stack([torch.from_numpy(gx / (wo - 1) * 2 - 1).float(),
                         torch.from_numpy(gy / (ho - 1) * 2 - 1).float()], 0).unsqueeze(0)
+
+
+def upsample(feat: torch.Tensor, size) -> torch.Tensor:
+    """a4: ``F.interpolate(img_feature, self.upsample_shape, mode='bilinear')``
+    (``persp_trans_detector.py:65``; align_corners defaults to False)."""
+    return F.interpolate(feat, list(size), mode="bilinear")
 
 
 def warp_views(feats: Sequence[torch.Tensor], proj_mats, grid_hw) -> List[torch.Tensor]:

@@ -45,6 +45,38 @@ def test_warp_vs_oracle_and_closed_form(B, C, H, W, ho, wo):
         assert s["normwise"] < 2e-4, s
 
 
+@pytest.mark.parametrize("B,C,h,w,H,W,ho,wo", [(2, 20, 9, 16, 27, 48, 12, 36), (1, 67, 10, 14, 27, 41, 17, 23),
+                                                 (1, 8, 5, 7, 5, 7, 6, 9), (2, 130, 30, 40, 90, 120, 40, 63)])
+@pytest.mark.parametrize("split", [False, True])
+def test_upsample_warp_fused_vs_oracle(B, C, h, w, H, W, ho, wo, split):
+    """§8(f) row 1: the fused upsample+warp vs F.interpolate (torch CPU) then the kornia
+    restatement; integer (3x) and non-integer scales, no-op scale, C not a multiple of 8."""
+    from mvdet_amd import ops
+    from mvdet_amd.geometry import kornia_src_norm_from_dst_norm
+    rng = np.random.default_rng(B * 977 + C + h)
+    feat = torch.from_numpy(np.maximum(rng.standard_normal((B, C, h, w)), 0).astype(np.float32))
+    M = torch.from_numpy(_rand_h(rng, H, W, ho, wo)).float()[None]
+    m_norm = kornia_src_norm_from_dst_norm(M, (H, W), (ho, wo))[0]
+    ref = kornia_warp.warp_perspective(cpu_path.upsample(feat, (H, W)), M.repeat(B, 1, 1), (ho, wo))
+    if split:
+        dst = torch.zeros(ops.split_shape(B, C, ho, wo), dtype=torch.bfloat16, device=DEV)
+        ops.warp_views_upsampled_into([feat.to(DEV)], (H, W), [m_norm], [dst], split=True)
+        got = ops.split_decode(dst, C).cpu()
+    else:
+        dst = torch.zeros((B, C, ho, wo), device=DEV)
+        ops.warp_views_upsampled_into([feat.to(DEV)], (H, W), [m_norm], [dst])
+        got = dst.cpu()
+    assert_parity(got, ref, "upsample+warp")
+    assert parity_stats(got, ref)["normwise"] < 1e-4  # the warp's own fp32 coordinate rounding (cf. 2e-4)
+
+
+def test_upsample_warp_fused_rejects_downsampling():
+    from mvdet_amd import ops
+    feat = torch.zeros((1, 8, 20, 20), device=DEV)
+    with pytest.raises(ValueError):
+        ops.warp_views_upsampled_into([feat], (10, 40), [torch.eye(3)], [torch.zeros((1, 8, 4, 4), device=DEV)])
+
+
 def test_warp_identity_translation_oob_behind_camera():
     from mvdet_amd import warp_perspective
     rng = np.random.default_rng(5)

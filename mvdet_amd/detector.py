@@ -7,9 +7,12 @@ Same constructor (``dataset`` duck-type, ``arch``), same attributes
 ``map_classifier.*``), same ``forward(imgs, visualize=False) ->
 (map_result [B,1,Ho,Wo], imgs_result: list[N] of [B,2,h,w])``.
 
-What changes is the hot path (warp + concat + fusion), which runs on the HIP
-kernels of ``libmvbev.so`` through ``ProjectFuse``:
-* the per-view warp writes straight into the fused ground-plane tensor;
+What changes is the hot path (upsample + warp + concat + fusion), which runs on the
+HIP kernels of ``libmvbev.so`` through ``ProjectFuse``:
+* the 3x upsample of ``:65`` is fused into the warp (the 265 MB/view upsampled map is
+  never written) and all views warp in one launch, straight into the fused tensor;
+* the image head's first 1x1 conv runs before the upsample (64 instead of 512 channels
+  upsampled; it commutes with bilinear interpolation);
 * the coord channels are written once, not copied every forward;
 * conv1/conv2 are MFMA implicit GEMMs (default 3xbf16 split precision, fp32
   accumulation — same parity as exact fp32; ``precision="fp32"`` selects the
@@ -69,26 +72,42 @@ class PerspTransDetector(nn.Module):
             raise RuntimeError("PerspTransDetector.forward needs a ROCm GPU (the hot path has no CPU fallback)")
         training = self._needs_autograd()
         ws = None if training else self.engine.workspace(B, dev)
-        world_features, imgs_result = [], []
+        world_features, imgs_result, low = [], [], []
         for cam in range(self.num_cam):
             feat = self.base_pt1(imgs[:, cam].to(dev))
             feat = self.base_pt2(feat)
-            feat = F.interpolate(feat, self.upsample_shape, mode="bilinear")
-            imgs_result.append(self.img_classifier(feat))
-            if training:
+            if training:  # :65-69 as the reference, autograd through stock torch ops
+                feat = F.interpolate(feat, self.upsample_shape, mode="bilinear")
+                imgs_result.append(self.img_classifier(feat))
                 world_features.append(self._torch_warp(cam, feat))
             else:
-                self.engine.warp_view(ws, cam, feat.contiguous())
+                # the 3x upsample (:65) happens inside the fused warp below; the image head
+                # runs its first 1x1 conv before upsampling (it commutes with the bilinear
+                # upsample: per-pixel affine, weights summing to 1) on 64 instead of 512 channels
+                low.append(feat.contiguous())
+                imgs_result.append(self._img_head_lowres(feat))
             if visualize:
-                self._show(torch.norm(feat[0].detach(), dim=0))
+                up = feat if training else F.interpolate(feat, self.upsample_shape, mode="bilinear")
+                self._show(torch.norm(up[0].detach(), dim=0))
         if training:
             cmap = self.coord_map.to(dev).repeat([B, 1, 1, 1])
             map_result = self.map_classifier(torch.cat(world_features + [cmap], dim=1))
         else:
+            self.engine.warp_views_upsampled(ws, list(range(self.num_cam)), low)  # a4 + a5 + a6
             map_result = self.engine.fuse(ws, self.map_classifier)
         if visualize:
             self._show(torch.norm(map_result[0].detach(), dim=0))
         return map_result, imgs_result
+
+    def _img_head_lowres(self, feat: torch.Tensor) -> torch.Tensor:
+        """``img_classifier(F.interpolate(feat, upsample_shape))`` (:65-66) evaluated as
+        conv_b(relu(upsample(conv_a(feat)))): identical in exact arithmetic."""
+        head = self.img_classifier
+        if (len(head) == 3 and isinstance(head[0], nn.Conv2d) and head[0].kernel_size == (1, 1)
+                and isinstance(head[1], nn.ReLU)):
+            g = head[0](feat)
+            return head[2](F.relu(F.interpolate(g, self.upsample_shape, mode="bilinear")))
+        return head(F.interpolate(feat, self.upsample_shape, mode="bilinear"))
 
     def _torch_warp(self, cam: int, feat: torch.Tensor) -> torch.Tensor:
         """Autograd-capable warp (kornia steps 3-6 in stock torch GPU ops)."""

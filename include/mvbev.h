@@ -185,6 +185,17 @@ int mvbev_pack_conv3x3_weight_bf16x3(const float* w, int64_t Cout, int64_t Cin_w
 int mvbev_conv3x3_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* desc,
                          const void* w_packed, const float* bias, const float* init,
                          int64_t Cout, int dilation, int relu, float* y, void* stream);
+/* Same with a caller-owned device workspace for the split-K tail: when the output tiles do
+ * not fill a whole number of rounds over the CUs (one workgroup per CU), the tiles of the
+ * last, partial round are each cut into K-ranges run by separate workgroups, and a second
+ * launch sums each tile's pieces in K order (deterministic) and applies the epilogue.
+ * workspace_bytes() returns the bytes that schedule needs for this shape (0 = not used);
+ * with a NULL / smaller workspace the call is mvbev_conv3x3_bf16x3. */
+size_t mvbev_conv3x3_bf16x3_workspace_bytes(const mvbev_conv_desc* desc, int64_t Cout);
+int mvbev_conv3x3_bf16x3_ws(const void* x, int x_layout, const mvbev_conv_desc* desc,
+                            const void* w_packed, const float* bias, const float* init,
+                            int64_t Cout, int dilation, int relu, float* y, void* workspace,
+                            size_t workspace_bytes, void* stream);
 
 /* y[b][0][r][:] = conv3x3(x[b], w, dilation=d, padding=d)[out_row0 + r], one output channel,
  * no bias.  x : [B][C][in_rows][W] holding global rows [in_row0, in_row0+in_rows) of an

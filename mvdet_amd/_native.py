@@ -30,6 +30,8 @@ EXPORTS = (
     "mvbev_conv3x3_packed_bytes_bf16x3",
     "mvbev_pack_conv3x3_weight_bf16x3",
     "mvbev_conv3x3_bf16x3",
+    "mvbev_conv3x3_bf16x3_workspace_bytes",
+    "mvbev_conv3x3_bf16x3_ws",
 )
 
 KC = 8    # MVBEV_CONV_KC
@@ -94,6 +96,11 @@ def _declare(lib):
     lib.mvbev_conv3x3_bf16x3.restype = ctypes.c_int
     lib.mvbev_conv3x3_bf16x3.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64,
                                          ctypes.c_int, ctypes.c_int, _p, _p]
+    lib.mvbev_conv3x3_bf16x3_workspace_bytes.restype = ctypes.c_size_t
+    lib.mvbev_conv3x3_bf16x3_workspace_bytes.argtypes = [ctypes.POINTER(ConvDesc), _i64]
+    lib.mvbev_conv3x3_bf16x3_ws.restype = ctypes.c_int
+    lib.mvbev_conv3x3_bf16x3_ws.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64,
+                                            ctypes.c_int, ctypes.c_int, _p, _p, ctypes.c_size_t, _p]
     lib.mvbev_conv3x3_cout1_f32.restype = ctypes.c_int
     lib.mvbev_conv3x3_cout1_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p,
                                             ctypes.c_int, _p, _p]

@@ -30,6 +30,7 @@ namespace mvbev {
 namespace b3 {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -73,9 +74,14 @@ struct Args {
   const float* init;
   float* y;
   int64_t group_stride, batch_stride;
-  int group, K, nchunks, Cout, H, W;
+  int B, group, K, nchunks, Cout, H, W;
   int in_row0, in_rows, out_row0, out_rows;
   int tiles_x, tiles_y, n_cot, nwg;
+  // split-K tail (sk_ws != nullptr): tiles [0, dp_tiles) run whole (full rounds over the
+  // CUs); each remaining tile is cut into `split` K-ranges run by separate workgroups,
+  // which leave raw partial sums in sk_ws for sk_fixup_kernel
+  float* sk_ws;
+  int dp_tiles, split;
 };
 
 // Input tag: the split-bf16 blocked layout written by mvbev_warp_views_split_bf16 and by this
@@ -93,6 +99,92 @@ template <> __device__ inline float ld<_Float16>(const _Float16* p) { return (fl
 #define MVBEV_B3_DEPTH 2  // staging-register ring depth (1 or 2)
 #endif
 
+// Output of one finished tile (bias, coord-term init, ReLU) from the accumulators of the
+// tile's waves; shared by the conv kernel and the stream-K fixup.
+template <bool RELU, int NW>
+__device__ inline void tile_epilogue(const Args& a, int tile, const floatx16 (&acc)[2][2]) {
+  constexpr int TH = NW;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l32 = lane & 31, kh = lane >> 5;
+  const int cot = tile % a.n_cot;
+  int rest = tile / a.n_cot;
+  const int tx = rest % a.tiles_x;
+  rest /= a.tiles_x;
+  const int ty = rest % a.tiles_y;
+  const int b = rest / a.tiles_y;
+  const int W = a.W;
+  const int y0 = a.out_row0 + ty * TH;
+  const int prow = 2 * (wave % (NW / 2));
+  const int cw = 64 * (wave / (NW / 2));
+  const int col = tx * TW + l32;
+  const int64_t oplane = (int64_t)a.out_rows * W;
+  const int64_t iplane = (int64_t)a.H * W;
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int pt = 0; pt < 2; ++pt) {
+      const int row = y0 + prow + pt;
+      if (row >= a.out_row0 + a.out_rows || col >= W) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = cot * BN + cw + 32 * ct + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        float v = acc[ct][pt][r];
+        if (a.bias) v += a.bias[co];
+        if (a.init) v += a.init[co * iplane + (int64_t)row * W + col];
+        if (RELU) v = v < 0.f ? 0.f : v;
+        a.y[((int64_t)b * a.Cout + co) * oplane + (int64_t)(row - a.out_row0) * W + col] = v;
+      }
+    }
+}
+
+// stream-K partial slot: [slot][16 float4 of the thread's 64 accumulators][thread] (coalesced)
+template <int NW>
+__device__ inline void store_partial(float* ws, int slot, const floatx16 (&acc)[2][2]) {
+  constexpr int NT = 64 * NW;
+  floatx4* p = reinterpret_cast<floatx4*>(ws) + (int64_t)slot * 16 * NT + threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const floatx4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+        p[(int64_t)((i * 2 + j) * 4 + q) * NT] = v;
+      }
+}
+
+template <int NW>
+__device__ inline void add_partial(const float* ws, int slot, floatx16 (&acc)[2][2]) {
+  constexpr int NT = 64 * NW;
+  const floatx4* p = reinterpret_cast<const floatx4*>(ws) + (int64_t)slot * 16 * NT + threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const floatx4 v = p[(int64_t)((i * 2 + j) * 4 + q) * NT];
+        acc[i][j][4 * q] += v[0];
+        acc[i][j][4 * q + 1] += v[1];
+        acc[i][j][4 * q + 2] += v[2];
+        acc[i][j][4 * q + 3] += v[3];
+      }
+}
+
+// Finishes the split tail tiles: block t sums the `split` partial slots of tail tile t in
+// K order (deterministic) and writes the tile like the conv kernel's epilogue.
+template <bool RELU, int NW>
+__global__ __launch_bounds__(64 * NW) void sk_fixup_kernel(const Args a) {
+  const int t = blockIdx.x;
+  floatx16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = floatx16{0};
+  for (int p = 0; p < a.split; ++p) add_partial<NW>(a.sk_ws, t * a.split + p, acc);
+  tile_epilogue<RELU, NW>(a, a.dp_tiles + t, acc);
+}
+
 template <typename TIn, int DIL, bool RELU, int NW>
 __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const Args a) {
   constexpr int NT = 64 * NW;
@@ -105,22 +197,37 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
   constexpr int BUF = W16 + 4 * XPAD;    // 16-B pieces: W, then X [sub][part][XPAD]
   __shared__ __attribute__((aligned(16))) u32x4 lds[BUF];
 
-  const int wg = xcd_remap(blockIdx.x, a.nwg);
-  const int cot = wg % a.n_cot;
-  int rest = wg / a.n_cot;
+  const int W = a.W;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, kh = lane >> 5;
+  const int64_t plane = (int64_t)a.in_rows * W;
+  const int64_t wchunk = (int64_t)a.n_cot * W16;
+  const int n = a.nchunks;
+
+  // a whole tile, or (split-K tail) one K-range of a tail tile
+  // XCD remap within each phase: the whole tiles (dispatched first, a multiple of the CU
+  // count) and the tail pieces each get contiguous ranges per XCD
+  const int bid = blockIdx.x;
+  const bool tail = a.sk_ws && bid >= a.dp_tiles;
+  const int wg = tail ? a.dp_tiles + xcd_remap(bid - a.dp_tiles, a.nwg - a.dp_tiles)
+                      : xcd_remap(bid, a.sk_ws ? a.dp_tiles : a.nwg);
+  int tile = wg, k0 = 0, k1 = n, piece = -1;
+  if (tail) {
+    piece = wg - a.dp_tiles;
+    tile = a.dp_tiles + piece / a.split;
+    const int p = piece % a.split;
+    k0 = (int)((int64_t)n * p / a.split);
+    k1 = (int)((int64_t)n * (p + 1) / a.split);
+  }
+  const int cot = tile % a.n_cot;
+  int rest = tile / a.n_cot;
   const int tx = rest % a.tiles_x;
   rest /= a.tiles_x;
   const int ty = rest % a.tiles_y;
   const int b = rest / a.tiles_y;
   const int x0 = tx * TW;
   const int y0 = a.out_row0 + ty * TH;
-  const int W = a.W;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int l32 = lane & 31, kh = lane >> 5;
-
-  const int64_t plane = (int64_t)a.in_rows * W;
   const u32x4* wsrc = a.wp + (int64_t)cot * W16;
-  const int64_t wchunk = (int64_t)a.n_cot * W16;
 
   // halo pixels of this thread (chunk-invariant): plane offset + validity
   int xoff[XPT];
@@ -281,11 +388,11 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
     // Two chunks of loads in flight: slot 0 holds even chunks, slot 1 odd ones. Loads are
     // unconditional (index clamped; the last chunk is re-read at most twice) so the
     // loop body is straight-line and the compiler's vmcnt counting stays exact.
-    const int last = a.nchunks - 1;
-    B3_LOAD(0, 0);
-    B3_LOAD(min(1, last), 1);
-    int ch = 0;
-    for (; ch + 1 < a.nchunks; ch += 2) {
+    const int last = k1 - 1;
+    B3_LOAD(k0, 0);
+    B3_LOAD(min(k0 + 1, last), 1);
+    int ch = k0;
+    for (; ch + 1 < k1; ch += 2) {
       __syncthreads();
       B3_STORE(0);
       __syncthreads();
@@ -297,19 +404,19 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
       B3_LOAD(min(ch + 3, last), 1);
       compute();
     }
-    if (ch < a.nchunks) {
+    if (ch < k1) {
       __syncthreads();
       B3_STORE(0);
       __syncthreads();
       compute();
     }
   } else {
-    B3_LOAD(0, 0);
-    for (int ch = 0; ch < a.nchunks; ++ch) {
+    B3_LOAD(k0, 0);
+    for (int ch = k0; ch < k1; ++ch) {
       __syncthreads();
       B3_STORE(0);
       __syncthreads();
-      if (ch + 1 < a.nchunks) B3_LOAD(ch + 1, 0);
+      if (ch + 1 < k1) B3_LOAD(ch + 1, 0);
       compute();
     }
   }
@@ -317,35 +424,64 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
 #undef B3_STORE
 #undef B3_SUB_BASE
 
-  const int col = x0 + l32;
-  const int64_t oplane = (int64_t)a.out_rows * W;
-  const int64_t iplane = (int64_t)a.H * W;
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-    for (int pt = 0; pt < 2; ++pt) {
-      const int row = y0 + prow + pt;
-      if (row >= a.out_row0 + a.out_rows || col >= W) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = cot * BN + cw + 32 * ct + (r & 3) + 8 * (r >> 2) + 4 * kh;
-        float v = acc[ct][pt][r];
-        if (a.bias) v += a.bias[co];
-        if (a.init) v += a.init[co * iplane + (int64_t)row * W + col];
-        if (RELU) v = v < 0.f ? 0.f : v;
-        a.y[((int64_t)b * a.Cout + co) * oplane + (int64_t)(row - a.out_row0) * W + col] = v;
-      }
-    }
+  if (piece < 0) {
+    tile_epilogue<RELU, NW>(a, tile, acc);
+  } else {  // one K-range of a tail tile: raw partial sums, finished by sk_fixup_kernel
+    store_partial<NW>(a.sk_ws, piece, acc);
+  }
 }
 
 #ifndef MVBEV_B3_WAVES
 #define MVBEV_B3_WAVES 8
 #endif
 
+// Split-K tail geometry.  One workgroup per CU fits (LDS), so tiles run in rounds of G = CU
+// count; when the last round is partial its tiles are cut into `split` K-ranges so the tail
+// fills the CUs: split minimises ceil(tail * s / G) * (n / s + c) chunk-times, c = the
+// measured per-piece overhead (pipeline fill from cold caches, partial store, fixup pass):
+// at cfg1 (n = 48, tail 128) splitting in 2 saves 8.5 % of conv1, at cfg2 (n = 224, tail
+// 208) every split measured slower, which c = 12 reproduces.  Partial slots: 64 x 512 floats.
+constexpr double kSkPieceOverhead = 12.0;
+static int cu_count() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return n;
+}
+constexpr size_t kSkSlotBytes = (size_t)64 * 64 * MVBEV_B3_WAVES * sizeof(float);
+#ifndef MVBEV_B3_SK
+#define MVBEV_B3_SK 1  // split-K tail when the workspace allows it
+#endif
+struct SkPlan {
+  int64_t dp_tiles = 0, tail = 0;
+  int split = 1;
+};
+static SkPlan sk_plan(int64_t tiles, int64_t nchunks) {
+  SkPlan p;
+  const int G = MVBEV_B3_SK ? cu_count() : 0;
+  if (G <= 0 || tiles % G == 0 || nchunks < 4) return p;
+  p.tail = tiles % G;
+  p.dp_tiles = tiles - p.tail;
+  double best = (double)nchunks;  // s = 1: one (partial) round of whole tiles
+  for (int s = 2; s <= 16 && nchunks / s >= 2; ++s) {
+    const double t = (double)ceil_div(p.tail * s, G) * ((double)nchunks / s + kSkPieceOverhead);
+    if (t < 0.97 * best) {
+      best = t;
+      p.split = s;
+    }
+  }
+  if (p.split == 1) p.tail = 0, p.dp_tiles = tiles;
+  return p;
+}
+static int64_t conv_tiles(const mvbev_conv_desc* d, int64_t Cout) {
+  return ceil_div(d->W, TW) * ceil_div(d->out_rows, MVBEV_B3_WAVES) * (Cout / BN) * d->B;
+}
+
 template <typename TIn>
 static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
                   const float* bias, const float* init, int64_t Cout, int dilation, int relu,
-                  float* y, void* stream) {
+                  float* y, void* workspace, size_t ws_bytes, void* stream) {
   if (!x || !d || !w_packed || !y) return MVBEV_ERR_NULL;
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || d->in_rows <= 0 ||
       d->out_rows <= 0 || d->group <= 0)
@@ -360,20 +496,33 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   Args a;
   a.x = x; a.wp = static_cast<const u32x4*>(w_packed); a.bias = bias; a.init = init; a.y = y;
   a.group_stride = d->group_stride; a.batch_stride = d->batch_stride;
-  a.group = (int)d->group; a.K = (int)d->K; a.nchunks = (int)ceil_div(d->K, KC);
+  a.B = (int)d->B; a.group = (int)d->group; a.K = (int)d->K; a.nchunks = (int)ceil_div(d->K, KC);
   a.Cout = (int)Cout;
   a.H = (int)d->H; a.W = (int)d->W;
   a.in_row0 = (int)d->in_row0; a.in_rows = (int)d->in_rows;
   a.out_row0 = (int)d->out_row0; a.out_rows = (int)d->out_rows;
   a.tiles_x = (int)ceil_div(d->W, TW); a.tiles_y = (int)ceil_div(d->out_rows, NW);
   a.n_cot = (int)(Cout / BN);
-  const int64_t nwg = (int64_t)a.tiles_x * a.tiles_y * a.n_cot * d->B;
+  const int64_t tiles = (int64_t)a.tiles_x * a.tiles_y * a.n_cot * d->B;
+  if (tiles * a.nchunks > (int64_t)INT32_MAX * 8) return MVBEV_ERR_SHAPE;
+  const SkPlan plan = sk_plan(tiles, a.nchunks);
+  const bool sk = workspace && plan.split > 1 &&
+                  ws_bytes >= (size_t)(plan.tail * plan.split) * kSkSlotBytes;
+  a.sk_ws = sk ? static_cast<float*>(workspace) : nullptr;
+  a.dp_tiles = (int)(sk ? plan.dp_tiles : tiles);
+  a.split = sk ? plan.split : 1;
+  const int64_t nwg = sk ? plan.dp_tiles + plan.tail * plan.split : tiles;
   if (nwg > (int64_t)INT32_MAX) return MVBEV_ERR_SHAPE;
   a.nwg = (int)nwg;
   hipStream_t s = as_stream(stream);
 #define B3_LAUNCH(D, R)                                                                   \
-  hipLaunchKernelGGL((conv_kernel<TIn, D, R, NW>), dim3((unsigned)nwg), dim3(64 * NW),     \
-                     0, s, a)
+  do {                                                                                    \
+    hipLaunchKernelGGL((conv_kernel<TIn, D, R, NW>), dim3((unsigned)nwg), dim3(64 * NW),   \
+                       0, s, a);                                                          \
+    if (sk)                                                                               \
+      hipLaunchKernelGGL((sk_fixup_kernel<R, NW>), dim3((unsigned)plan.tail),              \
+                         dim3(64 * NW), 0, s, a);                                         \
+  } while (0)
   if (dilation == 1) {
     if (relu) B3_LAUNCH(1, true); else B3_LAUNCH(1, false);
   } else if (dilation == 2) {
@@ -418,13 +567,31 @@ int mvbev_pack_conv3x3_weight_bf16x3(const float* w, int64_t Cout, int64_t Cin_w
 int mvbev_conv3x3_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* desc,
                          const void* w_packed, const float* bias, const float* init,
                          int64_t Cout, int dilation, int relu, float* y, void* stream) {
+  return mvbev_conv3x3_bf16x3_ws(x, x_layout, desc, w_packed, bias, init, Cout, dilation, relu, y,
+                                 nullptr, 0, stream);
+}
+
+size_t mvbev_conv3x3_bf16x3_workspace_bytes(const mvbev_conv_desc* desc, int64_t Cout) {
+  using namespace mvbev::b3;
+  if (!desc || Cout <= 0 || desc->W <= 0 || desc->out_rows <= 0 || desc->B <= 0 || desc->K <= 0)
+    return 0;
+  const SkPlan p = sk_plan(conv_tiles(desc, Cout), mvbev::ceil_div(desc->K, KC));
+  return p.split > 1 ? (size_t)(p.tail * p.split) * kSkSlotBytes : 0;
+}
+
+int mvbev_conv3x3_bf16x3_ws(const void* x, int x_layout, const mvbev_conv_desc* desc,
+                            const void* w_packed, const float* bias, const float* init,
+                            int64_t Cout, int dilation, int relu, float* y, void* workspace,
+                            size_t workspace_bytes, void* stream) {
+  using namespace mvbev::b3;
   if (x_layout == MVBEV_LAYOUT_SPLIT_BF16)
-    return mvbev::b3::launch<mvbev::b3::SplitIn>(x, desc, w_packed, bias, init, Cout, dilation,
-                                                 relu, y, stream);
+    return launch<SplitIn>(x, desc, w_packed, bias, init, Cout, dilation, relu, y, workspace,
+                           workspace_bytes, stream);
   if (x_layout == MVBEV_LAYOUT_F16)
-    return mvbev::b3::launch<_Float16>(x, desc, w_packed, bias, init, Cout, dilation, relu, y,
-                                       stream);
-  return mvbev::b3::launch<float>(x, desc, w_packed, bias, init, Cout, dilation, relu, y, stream);
+    return launch<_Float16>(x, desc, w_packed, bias, init, Cout, dilation, relu, y, workspace,
+                            workspace_bytes, stream);
+  return launch<float>(x, desc, w_packed, bias, init, Cout, dilation, relu, y, workspace,
+                       workspace_bytes, stream);
 }
 
 }  // extern "C"

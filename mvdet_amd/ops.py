@@ -294,10 +294,17 @@ def conv_desc(B: int, K: int, H: int, W: int, group: int, group_stride: int, bat
                             H if in_rows is None else in_rows, out_row0, H if out_rows is None else out_rows)
 
 
+def conv3x3_workspace_bytes(desc, cout: int) -> int:
+    """Device workspace the bf16x3 conv's stream-K schedule wants for this shape (0 = none)."""
+    return int(_native.load().mvbev_conv3x3_bf16x3_workspace_bytes(ctypes.byref(desc), cout))
+
+
 def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: Optional[torch.Tensor] = None,
                  init: Optional[torch.Tensor] = None, dilation: int = 1, relu: bool = False,
-                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Low-level form: ``x`` addressed through ``desc`` (``mvbev_conv_desc``)."""
+                 out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Low-level form: ``x`` addressed through ``desc`` (``mvbev_conv_desc``).  ``workspace``
+    (bf16x3 only, optional): device scratch for the stream-K schedule
+    (``conv3x3_workspace_bytes``); without it tiles run in whole rounds."""
     _require_cuda(x, packed)
     bf16x3 = packed.dtype == torch.bfloat16
     if x.dtype not in ((torch.float32, torch.float16, torch.bfloat16) if bf16x3 else (torch.float32,)):
@@ -330,10 +337,14 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
     bp = bias.data_ptr() if bias is not None else None
     ip = init.data_ptr() if init is not None else None
     if bf16x3:
-        st = lib.mvbev_conv3x3_bf16x3(x.data_ptr(), layout, ctypes.byref(desc),
-                                      packed.data_ptr(), bp, ip, cout, int(dilation), int(bool(relu)),
-                                      out.data_ptr(), _stream(x))
-        _native.check(st, "mvbev_conv3x3_bf16x3")
+        wsp, wsn = None, 0
+        if workspace is not None:
+            _require_cuda(workspace)
+            wsp, wsn = workspace.data_ptr(), workspace.numel() * workspace.element_size()
+        st = lib.mvbev_conv3x3_bf16x3_ws(x.data_ptr(), layout, ctypes.byref(desc),
+                                         packed.data_ptr(), bp, ip, cout, int(dilation), int(bool(relu)),
+                                         out.data_ptr(), wsp, wsn, _stream(x))
+        _native.check(st, "mvbev_conv3x3_bf16x3_ws")
     else:
         st = lib.mvbev_conv3x3_f32(x.data_ptr(), ctypes.byref(desc), packed.data_ptr(), bp, ip, cout,
                                    int(dilation), int(bool(relu)), out.data_ptr(), _stream(x))

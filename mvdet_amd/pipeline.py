@@ -66,7 +66,7 @@ class ProjectFuse:
     def __init__(self, proj_mats: Sequence[torch.Tensor], src_hw: Tuple[int, int], grid_hw: Tuple[int, int],
                  channels: int, mid_channels: int = 512, slot_views: Optional[Sequence[Optional[int]]] = None,
                  precision: str = "bf16x3", slab_dtype: torch.dtype = torch.float32,
-                 all_views: bool = True):
+                 all_views: bool = True, split_k: bool = True):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":
@@ -107,6 +107,8 @@ class ProjectFuse:
         self._coord_key = None
         self._coord_term: Optional[torch.Tensor] = None
         self._coord_in: Dict[str, torch.Tensor] = {}
+        self._sk: Dict[str, torch.Tensor] = {}  # split-K-tail scratch per device (bf16x3 convs)
+        self.split_k = split_k
 
     # -- buffers ----------------------------------------------------------------------------
     def workspace(self, B: int, device, band: Optional[Tuple[int, int]] = None) -> Workspace:
@@ -187,6 +189,21 @@ class ProjectFuse:
             self._coord_key = key
         return self._coord_term
 
+    def _sk_ws(self, desc, device) -> Optional[torch.Tensor]:
+        """Split-K-tail scratch for a bf16x3 conv (grown once, then reused: the convs of a
+        step run in stream order).  ``split_k=False`` keeps whole-tile rounds (bitwise
+        reproducible band decompositions)."""
+        if self.precision != "bf16x3" or not self.split_k:
+            return None
+        need = ops.conv3x3_workspace_bytes(desc, self.mid)
+        if need == 0:
+            return None
+        buf = self._sk.get(str(device))
+        if buf is None or buf.numel() * 4 < need:
+            buf = torch.empty((need + 3) // 4, dtype=torch.float32, device=device)
+            self._sk[str(device)] = buf
+        return buf
+
     # -- a7-a9 ----------------------------------------------------------------------------
     def conv1(self, ws: Workspace, conv1: torch.nn.Conv2d) -> torch.Tensor:
         """a7: y1 = relu(conv3x3(slab) + coord_term) on y1's rows (fp32 MFMA)."""
@@ -200,7 +217,7 @@ class ProjectFuse:
         d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * H * W,
                            batch_stride=self.Cs * H * W, in_row0=0, in_rows=H, out_row0=a1, out_rows=b1 - a1)
         return ops.conv3x3_desc(ws.slab, d1, p1, self.mid, bias=None, init=init, dilation=1, relu=True,
-                                out=ws.y1)
+                                out=ws.y1, workspace=self._sk_ws(d1, ws.slab.device))
 
     def conv2(self, ws: Workspace, conv2: torch.nn.Conv2d) -> torch.Tensor:
         """a8: y2 = relu(conv3x3_d2(y1) + b2) on y2's rows."""
@@ -211,7 +228,8 @@ class ProjectFuse:
         d2 = ops.conv_desc(B, self.mid, H, W, group=self.mid, group_stride=0,
                            batch_stride=self.mid * (b1 - a1) * W, in_row0=a1, in_rows=b1 - a1,
                            out_row0=a2, out_rows=b2 - a2)
-        return ops.conv3x3_desc(ws.y1, d2, p2, self.mid, bias=conv2.bias, dilation=2, relu=True, out=ws.y2)
+        return ops.conv3x3_desc(ws.y1, d2, p2, self.mid, bias=conv2.bias, dilation=2, relu=True, out=ws.y2,
+                                workspace=self._sk_ws(d2, ws.y1.device))
 
     def conv3(self, ws: Workspace, conv3: torch.nn.Conv2d) -> torch.Tensor:
         """a9: map = conv3x3_d4(y2) (Cout 1, no bias) on the output band → [B,1,rows,Wo]."""
@@ -231,7 +249,7 @@ class ProjectFuse:
         d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * H * W,
                            batch_stride=self.Cs * H * W, in_row0=0, in_rows=H, out_row0=0, out_rows=H)
         return ops.conv3x3_desc(ws.slab, d1, p1, self.mid, bias=None, init=None, dilation=1, relu=False,
-                                out=out)
+                                out=out, workspace=self._sk_ws(d1, ws.slab.device))
 
     def finish_from_y1(self, ws: Workspace, map_classifier: torch.nn.Sequential, mark=None) -> torch.Tensor:
         """``ws.y1`` holds conv1's summed channel terms (no bias) for rows ``ws.y1_rows``:

@@ -40,7 +40,7 @@ def test_band_fusion_is_bitwise_whole_grid():
     from mvdet_amd.parallel import row_band
     ds, pm, up, grid, C, B, feats, mc = _setup()
     mc = mc.to("cuda:0")
-    eng = ProjectFuse(pm, up, grid, C)
+    eng = ProjectFuse(pm, up, grid, C, split_k=False)  # split-K tails re-associate K sums
     with torch.no_grad():
         full = eng.project_fuse([f.cuda() for f in feats], mc).cpu()
         for P in (3, 5):

@@ -209,6 +209,34 @@ def test_conv3x3_bf16x3_fp16_input_is_exact_split():
     assert_parity(got, ref, "bf16x3 f16-in", normwise_tol=5e-5)
 
 
+@pytest.mark.parametrize("K,split", [(48, True), (520, False), (528, True), (1024, False)])
+def test_conv3x3_bf16x3_split_k_tail(K, split):
+    """The split-K tail (288 tiles: one full round + a tail whose tiles are cut into
+    K-ranges, fixed-order fixup), 3-64 K-chunks (3: too short to split, plain schedule);
+    matches torch, is deterministic, and agrees with the whole-round schedule to fp32
+    summation-order rounding."""
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(K)
+    B, H, W, cout = 1, 64, 288, 512
+    x = torch.rand(B, K, H, W, generator=g)
+    w = (torch.rand(cout, K, 3, 3, generator=g) - 0.5) / np.sqrt(K * 9)
+    b = torch.rand(cout, generator=g) - 0.5
+    ref = F.relu(F.conv2d(x, w, b, padding=1))
+    pk = ops.PackedConv3x3(None, "bf16x3").get(w.to(DEV))
+    xd = (_split_encode(x) if split else x).to(DEV)
+    desc = ops.conv_desc(B, K, H, W, group=K, group_stride=0, batch_stride=K * H * W)
+    need = ops.conv3x3_workspace_bytes(desc, cout)
+    assert (need > 0) == (K >= 520)
+    ws = torch.full((max(need, 4) // 4,), float("nan"), device=DEV)  # every read slot is written first
+    bd = b.to(DEV)
+    got = ops.conv3x3_desc(xd, desc, pk, cout, bias=bd, relu=True, workspace=ws).cpu()
+    again = ops.conv3x3_desc(xd, desc, pk, cout, bias=bd, relu=True, workspace=ws).cpu()
+    plain = ops.conv3x3_desc(xd, desc, pk, cout, bias=bd, relu=True).cpu()
+    assert_parity(got, ref, "stream-K", normwise_tol=CONV_TOL["bf16x3"])
+    assert torch.equal(got, again)
+    torch.testing.assert_close(got, plain, rtol=1e-5, atol=1e-5)
+
+
 def _split_encode(x: torch.Tensor) -> torch.Tensor:
     """fp32 [B, C, H, W] (C % 8 == 0) -> split-bf16 blocked [B, C/8, H, W, 2, 8]."""
     B, C, H, W = x.shape

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);
+int mvbev_version(void);  /* 10100: frustum masks, split-K tail, fused upsample+warp */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -118,6 +118,15 @@ int mvbev_warp_views_split_bf16(const mvbev_warp_view* views, int nviews, int sr
 int mvbev_warp_views_upsampled(const mvbev_warp_view* views, int nviews, int src_is_f16,
                                int64_t B, int64_t C, int64_t h, int64_t w, int64_t H, int64_t W,
                                int64_t Ho, int64_t Wo, int out_layout, void* stream);
+/* Frustum mask for the conv (see mvbev_conv3x3_bf16x3_ex): for output tiles of tile_h x
+ * tile_w pixels over grid rows [row0, row0 + rows) of the Ho x Wo warp output, bit s of
+ * mask[tile] is set when view s's warp (views[s].m, src size H x W) can be non-zero
+ * anywhere in the tile grown by `halo` pixels — some pixel samples inside the source, or
+ * its coordinates are non-finite (NaN output).  Uses the warp kernels' own fp32 coordinate
+ * code, so a clear bit is exact.  Only views[].m is read; nviews <= 16. */
+int mvbev_warp_tile_mask(const mvbev_warp_view* views, int nviews, int64_t H, int64_t W,
+                         int64_t Ho, int64_t Wo, int64_t row0, int64_t rows, int64_t tile_h,
+                         int64_t tile_w, int64_t halo, uint32_t* mask, void* stream);
 /* fp16 storage for src and dst, fp32 math. */
 int mvbev_warp_views_f16(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
                          int64_t H, int64_t W, int64_t Ho, int64_t Wo, void* stream);
@@ -185,16 +194,31 @@ int mvbev_pack_conv3x3_weight_bf16x3(const float* w, int64_t Cout, int64_t Cin_w
 int mvbev_conv3x3_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* desc,
                          const void* w_packed, const float* bias, const float* init,
                          int64_t Cout, int dilation, int relu, float* y, void* stream);
-/* Same with a caller-owned device workspace for the split-K tail: when the output tiles do
- * not fill a whole number of rounds over the CUs (one workgroup per CU), the tiles of the
- * last, partial round are each cut into K-ranges run by separate workgroups, and a second
- * launch sums each tile's pieces in K order (deterministic) and applies the epilogue.
- * workspace_bytes() returns the bytes that schedule needs for this shape (0 = not used);
- * with a NULL / smaller workspace the call is mvbev_conv3x3_bf16x3. */
+/* Output tile of mvbev_conv3x3_bf16x3 (rows x columns), the granule of group_mask below. */
+#define MVBEV_CONV_TILE_H 8
+#define MVBEV_CONV_TILE_W 32
+
+/* Extended form.
+ *   group_mask (optional, device): one uint32 per output tile, tiles row-major over
+ *     ceil(out_rows / MVBEV_CONV_TILE_H) x ceil(W / MVBEV_CONV_TILE_W) (rows from out_row0);
+ *     bit g clear = input channel group g (desc->group channels, group % 16 == 0, at most 32
+ *     groups) is exactly zero over the tile and its 3x3 dilated halo, so its K-chunks are
+ *     skipped for that tile (identical result).  mvbev_warp_tile_mask builds it from the
+ *     views' homographies: a camera's warped features are exactly 0 outside its frustum.
+ *   tile_order (optional, device, with group_mask): the B x tiles pixel tiles (index
+ *     (b * tiles_y + tile_y) * tiles_x + tile_x) in the order to run them — heaviest
+ *     first evens out the per-tile work the mask makes uneven.
+ *   workspace (optional, device): scratch for the split-K tail — when the output tiles do
+ *     not fill a whole number of rounds over the CUs (one workgroup per CU), the tiles of
+ *     the last, partial round are cut into K-ranges run by separate workgroups and a second
+ *     launch sums each tile's pieces in K order (deterministic).  workspace_bytes() returns
+ *     what this shape needs (0 = not used); a NULL / smaller workspace keeps whole tiles.
+ *     Not combined with group_mask. */
 size_t mvbev_conv3x3_bf16x3_workspace_bytes(const mvbev_conv_desc* desc, int64_t Cout);
-int mvbev_conv3x3_bf16x3_ws(const void* x, int x_layout, const mvbev_conv_desc* desc,
+int mvbev_conv3x3_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_desc* desc,
                             const void* w_packed, const float* bias, const float* init,
-                            int64_t Cout, int dilation, int relu, float* y, void* workspace,
+                            int64_t Cout, int dilation, int relu, float* y,
+                            const uint32_t* group_mask, const int32_t* tile_order, void* workspace,
                             size_t workspace_bytes, void* stream);
 
 /* y[b][0][r][:] = conv3x3(x[b], w, dilation=d, padding=d)[out_row0 + r], one output channel,

@@ -31,12 +31,14 @@ EXPORTS = (
     "mvbev_pack_conv3x3_weight_bf16x3",
     "mvbev_conv3x3_bf16x3",
     "mvbev_conv3x3_bf16x3_workspace_bytes",
-    "mvbev_conv3x3_bf16x3_ws",
+    "mvbev_conv3x3_bf16x3_ex",
+    "mvbev_warp_tile_mask",
 )
 
 KC = 8    # MVBEV_CONV_KC
 LAYOUT_F32, LAYOUT_F16, LAYOUT_SPLIT_BF16 = 0, 1, 2  # MVBEV_LAYOUT_*
 BN = 128  # MVBEV_CONV_BN
+TILE_H, TILE_W = 8, 32  # MVBEV_CONV_TILE_H / _W
 
 _i64 = ctypes.c_int64
 _p = ctypes.c_void_p
@@ -98,9 +100,12 @@ def _declare(lib):
                                          ctypes.c_int, ctypes.c_int, _p, _p]
     lib.mvbev_conv3x3_bf16x3_workspace_bytes.restype = ctypes.c_size_t
     lib.mvbev_conv3x3_bf16x3_workspace_bytes.argtypes = [ctypes.POINTER(ConvDesc), _i64]
-    lib.mvbev_conv3x3_bf16x3_ws.restype = ctypes.c_int
-    lib.mvbev_conv3x3_bf16x3_ws.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64,
-                                            ctypes.c_int, ctypes.c_int, _p, _p, ctypes.c_size_t, _p]
+    lib.mvbev_conv3x3_bf16x3_ex.restype = ctypes.c_int
+    lib.mvbev_conv3x3_bf16x3_ex.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64,
+                                            ctypes.c_int, ctypes.c_int, _p, _p, _p, _p, ctypes.c_size_t, _p]
+    lib.mvbev_warp_tile_mask.restype = ctypes.c_int
+    lib.mvbev_warp_tile_mask.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
+                                         _i64, _i64, _i64, _i64, _p, _p]
     lib.mvbev_conv3x3_cout1_f32.restype = ctypes.c_int
     lib.mvbev_conv3x3_cout1_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p,
                                             ctypes.c_int, _p, _p]

@@ -82,6 +82,15 @@ struct Args {
   // which leave raw partial sums in sk_ws for sk_fixup_kernel
   float* sk_ws;
   int dp_tiles, split;
+  // frustum mask (optional): per output tile (tile_y * tiles_x + tile_x) bit g = input
+  // channel group g can be non-zero in the tile's halo; clear groups' chunks are skipped
+  const uint32_t* gmask;
+  int cpg;  // K-chunks per channel group when gmask is set
+  // with gmask: pixel tiles (b, ty, tx) in dispatch order (heaviest first, optional) and
+  // their count; blocks interleave them over the XCDs, the Cout tiles of one pixel tile
+  // stay on one XCD (they share the halo reads)
+  const int32_t* tile_order;
+  int npix;
 };
 
 // Input tag: the split-bf16 blocked layout written by mvbev_warp_views_split_bf16 and by this
@@ -211,7 +220,13 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
   const bool tail = a.sk_ws && bid >= a.dp_tiles;
   const int wg = tail ? a.dp_tiles + xcd_remap(bid - a.dp_tiles, a.nwg - a.dp_tiles)
                       : xcd_remap(bid, a.sk_ws ? a.dp_tiles : a.nwg);
-  int tile = wg, k0 = 0, k1 = n, piece = -1;
+  int tile = wg, k0 = 0, k1 = n, piece = -1;  // K-range in (active) chunk order
+  if (a.gmask) {  // uneven per-tile work: spread pixel tiles over the XCDs, heaviest first
+    const int x = bid & 7, j = bid >> 3;
+    const int slot = (j / a.n_cot) * 8 + x;
+    if (slot >= a.npix) return;  // padding block (whole block, before any barrier)
+    tile = (a.tile_order ? a.tile_order[slot] : slot) * a.n_cot + j % a.n_cot;
+  }
   if (tail) {
     piece = wg - a.dp_tiles;
     tile = a.dp_tiles + piece / a.split;
@@ -228,6 +243,15 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
   const int x0 = tx * TW;
   const int y0 = a.out_row0 + ty * TH;
   const u32x4* wsrc = a.wp + (int64_t)cot * W16;
+  // frustum mask: iterate only the chunks of groups that can be non-zero in this tile
+  const uint32_t gm = a.gmask ? a.gmask[ty * a.tiles_x + tx] : 0u;
+  if (a.gmask) k1 = __builtin_popcount(gm) * a.cpg;  // (never combined with the split-K tail)
+  auto chunk_of = [&](int i) -> int {
+    if (!a.gmask) return i;
+    uint32_t m = gm;
+    for (int j = i / a.cpg; j > 0; --j) m &= m - 1;  // drop the lower set groups
+    return __builtin_ctz(m) * a.cpg + i % a.cpg;
+  };
 
   // halo pixels of this thread (chunk-invariant): plane offset + validity
   int xoff[XPT];
@@ -257,16 +281,17 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
     const int g_ = (k0) / a.group;                                                           \
     (int64_t)b * a.batch_stride + g_ * a.group_stride + (int64_t)((k0) - g_ * a.group) * plane; \
   })
-#define B3_LOAD(ch, sl)                                                                      \
+#define B3_LOAD(ci, sl)                                                                      \
   do {                                                                                       \
-    const u32x4* ws_ = wsrc + (int64_t)(ch) * wchunk;                                        \
+    const int ch_ = chunk_of(ci);                                                            \
+    const u32x4* ws_ = wsrc + (int64_t)ch_ * wchunk;                                         \
     _Pragma("unroll") for (int i = 0; i < WLD; ++i) {                                        \
       if (W16 % NT == 0 || tid + NT * i < W16) wreg[sl][i] = ws_[tid + NT * i];              \
     }                                                                                        \
     _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_) {                                       \
-      const int k0_ = (ch) * KC + s_ * SB;                                                   \
+      const int k0_ = ch_ * KC + s_ * SB;                                                    \
       sok[sl][s_] = k0_ < a.K;                                                               \
-      const int64_t cb_ = B3_SUB_BASE(sok[sl][s_] ? k0_ : (ch) * KC);                        \
+      const int64_t cb_ = B3_SUB_BASE(sok[sl][s_] ? k0_ : ch_ * KC);                         \
       if constexpr (SPLIT) {                                                                 \
         const u32x4* xc_ = static_cast<const u32x4*>(a.x) + cb_ / 4;                         \
         _Pragma("unroll") for (int i = 0; i < XPT; ++i) {                                    \
@@ -384,7 +409,9 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
     }
   };
 
-  if constexpr (DEPTH == 2) {
+  if (k1 <= k0) {
+    // no view reaches this tile: the output is the epilogue terms alone
+  } else if constexpr (DEPTH == 2) {
     // Two chunks of loads in flight: slot 0 holds even chunks, slot 1 odd ones. Loads are
     // unconditional (index clamped; the last chunk is re-read at most twice) so the
     // loop body is straight-line and the compiler's vmcnt counting stays exact.
@@ -481,7 +508,8 @@ static int64_t conv_tiles(const mvbev_conv_desc* d, int64_t Cout) {
 template <typename TIn>
 static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
                   const float* bias, const float* init, int64_t Cout, int dilation, int relu,
-                  float* y, void* workspace, size_t ws_bytes, void* stream) {
+                  float* y, const uint32_t* group_mask, const int32_t* tile_order,
+                  void* workspace, size_t ws_bytes, void* stream) {
   if (!x || !d || !w_packed || !y) return MVBEV_ERR_NULL;
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || d->in_rows <= 0 ||
       d->out_rows <= 0 || d->group <= 0)
@@ -505,13 +533,23 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   a.n_cot = (int)(Cout / BN);
   const int64_t tiles = (int64_t)a.tiles_x * a.tiles_y * a.n_cot * d->B;
   if (tiles * a.nchunks > (int64_t)INT32_MAX * 8) return MVBEV_ERR_SHAPE;
-  const SkPlan plan = sk_plan(tiles, a.nchunks);
+  a.gmask = nullptr;
+  a.cpg = 0;
+  if (group_mask) {  // frustum mask: needs whole chunks per group and <= 32 groups
+    if (d->group % KC != 0 || d->K / d->group > 32) return MVBEV_ERR_SHAPE;
+    a.gmask = group_mask;
+    a.cpg = (int)(d->group / KC);
+  }
+  a.tile_order = group_mask ? tile_order : nullptr;
+  a.npix = (int)(tiles / a.n_cot);
+  const SkPlan plan = group_mask ? SkPlan() : sk_plan(tiles, a.nchunks);
   const bool sk = workspace && plan.split > 1 &&
                   ws_bytes >= (size_t)(plan.tail * plan.split) * kSkSlotBytes;
   a.sk_ws = sk ? static_cast<float*>(workspace) : nullptr;
   a.dp_tiles = (int)(sk ? plan.dp_tiles : tiles);
   a.split = sk ? plan.split : 1;
-  const int64_t nwg = sk ? plan.dp_tiles + plan.tail * plan.split : tiles;
+  const int64_t nwg = group_mask ? (int64_t)a.n_cot * round_up(a.npix, 8)
+                                 : (sk ? plan.dp_tiles + plan.tail * plan.split : tiles);
   if (nwg > (int64_t)INT32_MAX) return MVBEV_ERR_SHAPE;
   a.nwg = (int)nwg;
   hipStream_t s = as_stream(stream);
@@ -567,8 +605,8 @@ int mvbev_pack_conv3x3_weight_bf16x3(const float* w, int64_t Cout, int64_t Cin_w
 int mvbev_conv3x3_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* desc,
                          const void* w_packed, const float* bias, const float* init,
                          int64_t Cout, int dilation, int relu, float* y, void* stream) {
-  return mvbev_conv3x3_bf16x3_ws(x, x_layout, desc, w_packed, bias, init, Cout, dilation, relu, y,
-                                 nullptr, 0, stream);
+  return mvbev_conv3x3_bf16x3_ex(x, x_layout, desc, w_packed, bias, init, Cout, dilation, relu, y,
+                                 nullptr, nullptr, nullptr, 0, stream);
 }
 
 size_t mvbev_conv3x3_bf16x3_workspace_bytes(const mvbev_conv_desc* desc, int64_t Cout) {
@@ -579,19 +617,20 @@ size_t mvbev_conv3x3_bf16x3_workspace_bytes(const mvbev_conv_desc* desc, int64_t
   return p.split > 1 ? (size_t)(p.tail * p.split) * kSkSlotBytes : 0;
 }
 
-int mvbev_conv3x3_bf16x3_ws(const void* x, int x_layout, const mvbev_conv_desc* desc,
+int mvbev_conv3x3_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_desc* desc,
                             const void* w_packed, const float* bias, const float* init,
-                            int64_t Cout, int dilation, int relu, float* y, void* workspace,
+                            int64_t Cout, int dilation, int relu, float* y,
+                            const uint32_t* group_mask, const int32_t* tile_order, void* workspace,
                             size_t workspace_bytes, void* stream) {
   using namespace mvbev::b3;
   if (x_layout == MVBEV_LAYOUT_SPLIT_BF16)
-    return launch<SplitIn>(x, desc, w_packed, bias, init, Cout, dilation, relu, y, workspace,
-                           workspace_bytes, stream);
+    return launch<SplitIn>(x, desc, w_packed, bias, init, Cout, dilation, relu, y, group_mask,
+                           tile_order, workspace, workspace_bytes, stream);
   if (x_layout == MVBEV_LAYOUT_F16)
-    return launch<_Float16>(x, desc, w_packed, bias, init, Cout, dilation, relu, y, workspace,
-                            workspace_bytes, stream);
-  return launch<float>(x, desc, w_packed, bias, init, Cout, dilation, relu, y, workspace,
-                       workspace_bytes, stream);
+    return launch<_Float16>(x, desc, w_packed, bias, init, Cout, dilation, relu, y, group_mask,
+                            tile_order, workspace, workspace_bytes, stream);
+  return launch<float>(x, desc, w_packed, bias, init, Cout, dilation, relu, y, group_mask,
+                       tile_order, workspace, workspace_bytes, stream);
 }
 
 }  // extern "C"

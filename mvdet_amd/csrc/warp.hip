@@ -57,22 +57,9 @@ __global__ __launch_bounds__(256) void warp_tile_kernel(const WarpArgs a) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) m[i] = vw.m[i];
   }
-  // kornia create_meshgrid(normalized_coordinates=True); same fp32 op order.
-  const float gx = ((float)u / (float)(a.Wo - 1) - 0.5f) * 2.0f;
-  const float gy = ((float)v / (float)(a.Ho - 1) - 0.5f) * 2.0f;
-  // transform_points: [gx gy 1] @ M^T, then convert_points_from_homogeneous(eps=1e-8)
-  float x = gx * m[0] + gy * m[1] + m[2];
-  float y = gx * m[3] + gy * m[4] + m[5];
-  const float z = gx * m[6] + gy * m[7] + m[8];
-  const float scale = fabsf(z) > 1e-8f ? 1.0f / (z + 1e-8f) : 1.0f;
-  x = scale * x;
-  y = scale * y;
-  // grid_sampler_unnormalize(align_corners=True)
-  const float ix = ((x + 1.f) / 2.f) * (float)(W - 1);
-  const float iy = ((y + 1.f) / 2.f) * (float)(H - 1);
-
-  const bool finite = isfinite(ix) && isfinite(iy);
-  const bool inside = finite && ix > -1.f && ix < (float)W && iy > -1.f && iy < (float)H;
+  const WarpCoord wc = warp_coord(m, u, v, a.Ho, a.Wo, H, W);
+  const float ix = wc.ix, iy = wc.iy;
+  const bool finite = wc.finite, inside = wc.inside;
   const float fill = finite ? 0.f : __builtin_nanf("");
   const float fx0 = floorf(ix), fy0 = floorf(iy);
   const int x0 = inside ? (int)fx0 : 0, y0 = inside ? (int)fy0 : 0;
@@ -233,6 +220,37 @@ static int warp_views(const mvbev_warp_view* views, int nviews, int64_t B, int64
   return finish_args_and_launch<T>(a, B, C, H, W, Ho, Wo, stream, split);
 }
 
+// Per conv tile (tile_h x tile_w output pixels of rows [row0, row0 + rows), plus `halo`
+// pixels around it, clipped to the grid): bit s of mask[tile] is set when view s's warp
+// output can be non-zero anywhere in that region (some pixel is in-bounds, or non-finite ->
+// NaN).  A clear bit means every channel of that view is exactly 0 there, so the conv may
+// skip those input channels for the tile without changing a single output bit.
+__global__ void tile_mask_kernel(WarpArgs a, int row0, int rows, int tile_h, int tile_w, int halo,
+                                 int tiles_x, uint32_t* mask) {
+  __shared__ uint32_t bits;
+  if (threadIdx.x == 0) bits = 0;
+  __syncthreads();
+  const int tile = blockIdx.x;
+  const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
+  const int r0 = max(0, row0 + ty * tile_h - halo), r1 = min(a.Ho, row0 + min(rows, (ty + 1) * tile_h) + halo);
+  const int c0 = max(0, tx * tile_w - halo), c1 = min(a.Wo, (tx + 1) * tile_w + halo);
+  const int w = c1 - c0, npix = (r1 - r0) * w;
+  uint32_t mine = 0;
+  for (int p = threadIdx.x; p < npix; p += blockDim.x) {
+    const int v = r0 + p / w, u = c0 + p % w;
+    for (int s = 0; s < a.nviews; ++s) {
+      float m[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) m[i] = a.v[s].m[i];
+      const WarpCoord c = warp_coord(m, u, v, a.Ho, a.Wo, a.H, a.W);
+      if (c.inside || !c.finite) mine |= 1u << s;
+    }
+  }
+  if (mine) atomicOr(&bits, mine);
+  __syncthreads();
+  if (threadIdx.x == 0) mask[tile] = bits;
+}
+
 // coord_map (persp_trans_detector.py:103-112): grid / (n-1) * 2 - 1 in float64, then .float()
 __global__ void coord_map_kernel(float* dst, int64_t dB, int64_t dC, int64_t dH, int Ho, int Wo) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -261,7 +279,7 @@ const char* mvbev_status_string(int s) {
   }
 }
 
-int mvbev_version(void) { return 10000; }
+int mvbev_version(void) { return 10100; }
 
 int mvbev_warp_perspective_f32(const float* src, int64_t B, int64_t C, int64_t H, int64_t W,
                                const int64_t src_strides[4], const float* m, float* dst,
@@ -295,6 +313,29 @@ int mvbev_warp_views_split_bf16(const mvbev_warp_view* views, int nviews, int sr
 int mvbev_warp_views_f16(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
                          int64_t H, int64_t W, int64_t Ho, int64_t Wo, void* stream) {
   return mvbev::warp_views<__half>(views, nviews, B, C, H, W, Ho, Wo, stream);
+}
+
+int mvbev_warp_tile_mask(const mvbev_warp_view* views, int nviews, int64_t H, int64_t W,
+                         int64_t Ho, int64_t Wo, int64_t row0, int64_t rows, int64_t tile_h,
+                         int64_t tile_w, int64_t halo, uint32_t* mask, void* stream) {
+  using namespace mvbev;
+  if (!views || !mask) return MVBEV_ERR_NULL;
+  if (nviews <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 || rows <= 0 || tile_h <= 0 ||
+      tile_w <= 0 || halo < 0)
+    return MVBEV_ERR_RANK;
+  if (nviews > 32 || nviews > kWarpMaxViews || row0 < 0 || row0 + rows > Ho) return MVBEV_ERR_SHAPE;
+  WarpArgs a = {};
+  for (int i = 0; i < nviews; ++i)
+    for (int k = 0; k < 9; ++k) a.v[i].m[k] = views[i].m[k];
+  a.nviews = nviews;
+  a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
+  const int tiles_x = (int)ceil_div(Wo, tile_w);
+  const int64_t tiles = tiles_x * ceil_div(rows, tile_h);
+  if (tiles > INT32_MAX) return MVBEV_ERR_SHAPE;
+  hipLaunchKernelGGL(tile_mask_kernel, dim3((unsigned)tiles), dim3(256), 0, as_stream(stream), a,
+                     (int)row0, (int)rows, (int)tile_h, (int)tile_w, (int)halo, tiles_x, mask);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
 }
 
 int mvbev_fill_coord_map_f32(float* dst, int64_t B, int64_t Ho, int64_t Wo,

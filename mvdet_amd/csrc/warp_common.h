@@ -51,4 +51,30 @@ __device__ inline void store_split8(u32x4_t* dst, const float (&v)[8]) {
   dst[1] = __builtin_bit_cast(u32x4_t, lo);
 }
 
+// kornia 0.6.11 warp coordinates of output pixel (u, v): create_meshgrid(normalized) ->
+// transform_points ([gx gy 1] @ M^T, convert_points_from_homogeneous eps=1e-8) ->
+// grid_sampler_unnormalize(align_corners=True).  One definition for every warp kernel and
+// the conv tile mask, so "this output pixel is exactly zero" is decided by the same fp32 ops
+// that produce the pixel.
+struct WarpCoord {
+  float ix, iy;
+  bool finite, inside;  // !finite -> NaN output; finite && !inside -> exactly 0 (zero padding)
+};
+__device__ inline WarpCoord warp_coord(const float (&m)[9], int u, int v, int Ho, int Wo, int H, int W) {
+  const float gx = ((float)u / (float)(Wo - 1) - 0.5f) * 2.0f;
+  const float gy = ((float)v / (float)(Ho - 1) - 0.5f) * 2.0f;
+  float x = gx * m[0] + gy * m[1] + m[2];
+  float y = gx * m[3] + gy * m[4] + m[5];
+  const float z = gx * m[6] + gy * m[7] + m[8];
+  const float scale = fabsf(z) > 1e-8f ? 1.0f / (z + 1e-8f) : 1.0f;
+  x = scale * x;
+  y = scale * y;
+  WarpCoord c;
+  c.ix = ((x + 1.f) / 2.f) * (float)(W - 1);
+  c.iy = ((y + 1.f) / 2.f) * (float)(H - 1);
+  c.finite = isfinite(c.ix) && isfinite(c.iy);
+  c.inside = c.finite && c.ix > -1.f && c.ix < (float)W && c.iy > -1.f && c.iy < (float)H;
+  return c;
+}
+
 }  // namespace mvbev

@@ -51,19 +51,10 @@ __global__ __launch_bounds__(256) void warp_up_kernel(const UpArgs ua) {
   float m[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) m[i] = vw.m[i];
-  // warp corners in the upsampled grid: identical arithmetic to warp_tile_kernel
-  const float gx = ((float)u / (float)(a.Wo - 1) - 0.5f) * 2.0f;
-  const float gy = ((float)v / (float)(a.Ho - 1) - 0.5f) * 2.0f;
-  float x = gx * m[0] + gy * m[1] + m[2];
-  float y = gx * m[3] + gy * m[4] + m[5];
-  const float z = gx * m[6] + gy * m[7] + m[8];
-  const float scale = fabsf(z) > 1e-8f ? 1.0f / (z + 1e-8f) : 1.0f;
-  x = scale * x;
-  y = scale * y;
-  const float ix = ((x + 1.f) / 2.f) * (float)(W - 1);
-  const float iy = ((y + 1.f) / 2.f) * (float)(H - 1);
-  const bool finite = isfinite(ix) && isfinite(iy);
-  const bool inside = finite && ix > -1.f && ix < (float)W && iy > -1.f && iy < (float)H;
+  // warp corners in the upsampled grid: the same warp_coord as warp_tile_kernel
+  const WarpCoord wc = warp_coord(m, u, v, a.Ho, a.Wo, H, W);
+  const float ix = wc.ix, iy = wc.iy;
+  const bool finite = wc.finite, inside = wc.inside;
   const float fill = finite ? 0.f : __builtin_nanf("");
   const float fx0 = floorf(ix), fy0 = floorf(iy);
   const int x0 = inside ? (int)fx0 : 0, y0 = inside ? (int)fy0 : 0;

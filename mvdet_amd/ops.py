@@ -299,12 +299,47 @@ def conv3x3_workspace_bytes(desc, cout: int) -> int:
     return int(_native.load().mvbev_conv3x3_bf16x3_workspace_bytes(ctypes.byref(desc), cout))
 
 
+def warp_tile_mask(m_norms, src_hw, grid_hw, row0: int, rows: int, halo: int, device) -> torch.Tensor:
+    """Frustum mask of the conv tiles (``mvbev_warp_tile_mask``): int32 [tiles] on ``device``,
+    bit s set where slot s's warp can be non-zero in the tile + ``halo``.  ``m_norms[s]`` is a
+    host [3,3] kornia matrix, or None for an empty slot (always zero)."""
+    n = len(m_norms)
+    if not 0 < n <= 16:
+        raise ValueError("need 1..16 slots")
+    arr = (_native.WarpView * n)()
+    for i, m in enumerate(m_norms):
+        # an empty slot: a finite map far outside the source (bit stays clear)
+        mm = [0.0, 0.0, 1e6, 0.0, 0.0, 1e6, 0.0, 0.0, 1.0] if m is None else \
+            torch.as_tensor(m, dtype=torch.float32).reshape(9).tolist()
+        arr[i].m = (ctypes.c_float * 9)(*mm)
+    H, W = src_hw
+    Ho, Wo = grid_hw
+    tiles = -(-rows // _native.TILE_H) * -(-Wo // _native.TILE_W)
+    mask = torch.zeros(tiles, dtype=torch.int32, device=device)
+    st = _native.load().mvbev_warp_tile_mask(arr, n, H, W, Ho, Wo, row0, rows, _native.TILE_H, _native.TILE_W,
+                                             halo, mask.data_ptr(), _stream(mask))
+    _native.check(st, "mvbev_warp_tile_mask")
+    return mask
+
+
+def heavy_first_order(mask: torch.Tensor, B: int) -> torch.Tensor:
+    """Pixel tiles (b, tile) sorted by active channel groups, most first (ties in index
+    order): the run order that evens out a frustum-masked conv's per-tile work."""
+    bits = [bin(int(v) & 0xFFFFFFFF).count("1") for v in mask.cpu().tolist()]
+    T = len(bits)
+    order = sorted(range(B * T), key=lambda i: (-bits[i % T], i))
+    return torch.tensor(order, dtype=torch.int32, device=mask.device)
+
+
 def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: Optional[torch.Tensor] = None,
                  init: Optional[torch.Tensor] = None, dilation: int = 1, relu: bool = False,
-                 out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Low-level form: ``x`` addressed through ``desc`` (``mvbev_conv_desc``).  ``workspace``
-    (bf16x3 only, optional): device scratch for the stream-K schedule
-    (``conv3x3_workspace_bytes``); without it tiles run in whole rounds."""
+                 out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
+                 group_mask: Optional[torch.Tensor] = None, tile_order: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Low-level form: ``x`` addressed through ``desc`` (``mvbev_conv_desc``).  bf16x3 only,
+    optional: ``workspace`` — device scratch for the split-K tail
+    (``conv3x3_workspace_bytes``); ``group_mask`` — per-tile active channel groups
+    (``warp_tile_mask``), whose cleared groups are skipped; ``tile_order`` — with a mask,
+    the B x tiles pixel tiles in run order (``heavy_first_order``)."""
     _require_cuda(x, packed)
     bf16x3 = packed.dtype == torch.bfloat16
     if x.dtype not in ((torch.float32, torch.float16, torch.bfloat16) if bf16x3 else (torch.float32,)):
@@ -337,14 +372,28 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
     bp = bias.data_ptr() if bias is not None else None
     ip = init.data_ptr() if init is not None else None
     if bf16x3:
-        wsp, wsn = None, 0
+        wsp, wsn, gmp = None, 0, None
         if workspace is not None:
             _require_cuda(workspace)
             wsp, wsn = workspace.data_ptr(), workspace.numel() * workspace.element_size()
-        st = lib.mvbev_conv3x3_bf16x3_ws(x.data_ptr(), layout, ctypes.byref(desc),
+        if group_mask is not None:
+            _require_cuda(group_mask)
+            tiles = -(-desc.out_rows // _native.TILE_H) * -(-W // _native.TILE_W)
+            if group_mask.dtype != torch.int32 or group_mask.numel() < tiles or not group_mask.is_contiguous():
+                raise ValueError(f"group_mask must be a contiguous int32 tensor of >= {tiles} tiles")
+            gmp = group_mask.data_ptr()
+        top = None
+        if tile_order is not None:
+            _require_cuda(tile_order)
+            if group_mask is None or tile_order.dtype != torch.int32 or tile_order.numel() != B * tiles:
+                raise ValueError("tile_order must be an int32 permutation of the B x tiles pixel tiles")
+            top = tile_order.data_ptr()
+        st = lib.mvbev_conv3x3_bf16x3_ex(x.data_ptr(), layout, ctypes.byref(desc),
                                          packed.data_ptr(), bp, ip, cout, int(dilation), int(bool(relu)),
-                                         out.data_ptr(), wsp, wsn, _stream(x))
-        _native.check(st, "mvbev_conv3x3_bf16x3_ws")
+                                         out.data_ptr(), gmp, top, wsp, wsn, _stream(x))
+        _native.check(st, "mvbev_conv3x3_bf16x3_ex")
+    elif group_mask is not None:
+        raise ValueError("group_mask needs the bf16x3 conv")
     else:
         st = lib.mvbev_conv3x3_f32(x.data_ptr(), ctypes.byref(desc), packed.data_ptr(), bp, ip, cout,
                                    int(dilation), int(bool(relu)), out.data_ptr(), _stream(x))

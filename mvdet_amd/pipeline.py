@@ -66,7 +66,7 @@ class ProjectFuse:
     def __init__(self, proj_mats: Sequence[torch.Tensor], src_hw: Tuple[int, int], grid_hw: Tuple[int, int],
                  channels: int, mid_channels: int = 512, slot_views: Optional[Sequence[Optional[int]]] = None,
                  precision: str = "bf16x3", slab_dtype: torch.dtype = torch.float32,
-                 all_views: bool = True, split_k: bool = True):
+                 all_views: bool = True, split_k: bool = True, frustum: bool = True):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":
@@ -109,6 +109,10 @@ class ProjectFuse:
         self._coord_in: Dict[str, torch.Tensor] = {}
         self._sk: Dict[str, torch.Tensor] = {}  # split-K-tail scratch per device (bf16x3 convs)
         self.split_k = split_k
+        # conv1 skips, per output tile, the slots whose warp is exactly zero there (camera
+        # frustum; geometry-only, so the mask is built once per device and row range)
+        self.frustum = frustum and precision == "bf16x3" and self.Cs % 16 == 0 and self.S <= 16
+        self._masks: Dict[tuple, torch.Tensor] = {}
 
     # -- buffers ----------------------------------------------------------------------------
     def workspace(self, B: int, device, band: Optional[Tuple[int, int]] = None) -> Workspace:
@@ -204,6 +208,38 @@ class ProjectFuse:
             self._sk[str(device)] = buf
         return buf
 
+    def conv1_mask(self, device, row0: int, rows: int) -> Optional[torch.Tensor]:
+        """Per conv1 output tile of rows [row0, row0+rows): bit s = slot s can be non-zero in
+        the tile's 3x3 halo (``mvbev_warp_tile_mask``); None when not used."""
+        if not self.frustum:
+            return None
+        key = (str(device), row0, rows)
+        m = self._masks.get(key)
+        if m is None:
+            ms = [None if v is None else self.m_norm_cpu[v] for v in self.slot_views]
+            m = ops.warp_tile_mask(ms, self.src_hw, self.grid_hw, row0, rows, 1, device)
+            self._masks[key] = m
+        return m
+
+    def conv1_order(self, device, row0: int, rows: int, B: int) -> Optional[torch.Tensor]:
+        key = ("order", str(device), row0, rows, B)
+        o = self._masks.get(key)
+        if o is None:
+            m = self.conv1_mask(device, row0, rows)
+            if m is None:
+                return None
+            o = ops.heavy_first_order(m, B)
+            self._masks[key] = o
+        return o
+
+    def conv1_active_fraction(self, device, row0: int, rows: int) -> float:
+        """Fraction of conv1's (tile, slot) work the frustum mask keeps (1.0 = dense)."""
+        m = self.conv1_mask(device, row0, rows)
+        if m is None:
+            return 1.0
+        bits = sum(bin(int(v) & 0xFFFFFFFF).count("1") for v in m.cpu().tolist())
+        return bits / (m.numel() * self.S)
+
     # -- a7-a9 ----------------------------------------------------------------------------
     def conv1(self, ws: Workspace, conv1: torch.nn.Conv2d) -> torch.Tensor:
         """a7: y1 = relu(conv3x3(slab) + coord_term) on y1's rows (fp32 MFMA)."""
@@ -216,8 +252,10 @@ class ProjectFuse:
         a1, b1 = ws.y1_rows
         d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * H * W,
                            batch_stride=self.Cs * H * W, in_row0=0, in_rows=H, out_row0=a1, out_rows=b1 - a1)
+        gm = self.conv1_mask(ws.slab.device, a1, b1 - a1)
         return ops.conv3x3_desc(ws.slab, d1, p1, self.mid, bias=None, init=init, dilation=1, relu=True,
-                                out=ws.y1, workspace=self._sk_ws(d1, ws.slab.device))
+                                out=ws.y1, workspace=None if gm is not None else self._sk_ws(d1, ws.slab.device),
+                                group_mask=gm, tile_order=self.conv1_order(ws.slab.device, a1, b1 - a1, B))
 
     def conv2(self, ws: Workspace, conv2: torch.nn.Conv2d) -> torch.Tensor:
         """a8: y2 = relu(conv3x3_d2(y1) + b2) on y2's rows."""
@@ -248,8 +286,10 @@ class ProjectFuse:
         p1 = self.pack1.get(map_classifier[0].weight)
         d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * H * W,
                            batch_stride=self.Cs * H * W, in_row0=0, in_rows=H, out_row0=0, out_rows=H)
+        gm = self.conv1_mask(ws.slab.device, 0, H)
         return ops.conv3x3_desc(ws.slab, d1, p1, self.mid, bias=None, init=None, dilation=1, relu=False,
-                                out=out, workspace=self._sk_ws(d1, ws.slab.device))
+                                out=out, workspace=None if gm is not None else self._sk_ws(d1, ws.slab.device),
+                                group_mask=gm, tile_order=self.conv1_order(ws.slab.device, 0, H, B))
 
     def finish_from_y1(self, ws: Workspace, map_classifier: torch.nn.Sequential, mark=None) -> torch.Tensor:
         """``ws.y1`` holds conv1's summed channel terms (no bias) for rows ``ws.y1_rows``:

@@ -237,6 +237,49 @@ def test_conv3x3_bf16x3_split_k_tail(K, split):
     torch.testing.assert_close(got, plain, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_frustum_mask_is_exact_and_conv1_unchanged(cfg):
+    """A cleared mask bit means the view's warped features are exactly 0 over the tile and
+    its halo; conv1 with the mask equals dense conv1 bit for bit (skipped products are
+    exact zeros).  Config rigs at reduced channel count."""
+    from mvdet_amd import ProjectFuse, ops, synthetic
+    from mvdet_amd.geometry import projection_matrices
+    spec = synthetic.CONFIGS[cfg]
+    ds = spec["make"]()
+    N, C, B = ds.num_cam, 32, 1
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    pm = projection_matrices(ds)
+    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=9 + v, device=DEV)
+             for v in range(N)]
+    mc = torch.nn.Sequential(torch.nn.Conv2d(N * C + 2, 512, 3, padding=1), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False)).to(DEV)
+    dense = ProjectFuse(pm, up, grid, C, frustum=False, split_k=False)
+    sparse = ProjectFuse(pm, up, grid, C, split_k=False)  # (split-K tails re-associate conv2's sums)
+    assert sparse.frustum
+    with torch.no_grad():
+        ref = dense.project_fuse(feats, mc)
+        y1_ref = dense.workspace(B, DEV).y1.clone()
+        got = sparse.project_fuse(feats, mc)
+        ws = sparse.workspace(B, DEV)
+    assert torch.equal(ws.y1, y1_ref)
+    assert torch.equal(got, ref)
+    H, W = grid
+    mask = sparse.conv1_mask(DEV, 0, H).cpu().numpy().astype(np.uint32)
+    tx = -(-W // 32)
+    warped = [sparse.view_slice(ws, v).abs().amax(dim=(0, 1)).cpu() for v in range(N)]  # [H, W]
+    kept = 0
+    for t, bits in enumerate(mask):
+        r0, c0 = (t // tx) * 8, (t % tx) * 32
+        for v in range(N):
+            region = warped[v][max(0, r0 - 1):r0 + 9, max(0, c0 - 1):c0 + 33]
+            if not (bits >> v) & 1:
+                assert region.max().item() == 0, (t, v)
+            else:
+                kept += 1
+    assert 0 < kept < mask.size * N  # the rig's frustums leave work to skip
+
+
 def _split_encode(x: torch.Tensor) -> torch.Tensor:
     """fp32 [B, C, H, W] (C % 8 == 0) -> split-bf16 blocked [B, C/8, H, W, 2, 8]."""
     B, C, H, W = x.shape

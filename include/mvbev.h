@@ -199,6 +199,9 @@ int mvbev_conv3x3_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* des
 #define MVBEV_CONV_TILE_W 32
 
 /* Extended form.
+ *   y, y_layout: MVBEV_LAYOUT_F32 ([B][Cout][out_rows][W] fp32, as above) or
+ *     MVBEV_LAYOUT_SPLIT_BF16 ([B][Cout/8][out_rows][W] pieces of bf16 hi[8], lo[8]: the
+ *     next conv's input without a conversion pass).
  *   group_mask (optional, device): one uint32 per output tile, tiles row-major over
  *     ceil(out_rows / MVBEV_CONV_TILE_H) x ceil(W / MVBEV_CONV_TILE_W) (rows from out_row0);
  *     bit g clear = input channel group g (desc->group channels, group % 16 == 0, at most 32
@@ -217,7 +220,7 @@ int mvbev_conv3x3_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* des
 size_t mvbev_conv3x3_bf16x3_workspace_bytes(const mvbev_conv_desc* desc, int64_t Cout);
 int mvbev_conv3x3_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_desc* desc,
                             const void* w_packed, const float* bias, const float* init,
-                            int64_t Cout, int dilation, int relu, float* y,
+                            int64_t Cout, int dilation, int relu, void* y, int y_layout,
                             const uint32_t* group_mask, const int32_t* tile_order, void* workspace,
                             size_t workspace_bytes, void* stream);
 

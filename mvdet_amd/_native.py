@@ -102,7 +102,8 @@ def _declare(lib):
     lib.mvbev_conv3x3_bf16x3_workspace_bytes.argtypes = [ctypes.POINTER(ConvDesc), _i64]
     lib.mvbev_conv3x3_bf16x3_ex.restype = ctypes.c_int
     lib.mvbev_conv3x3_bf16x3_ex.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64,
-                                            ctypes.c_int, ctypes.c_int, _p, _p, _p, _p, ctypes.c_size_t, _p]
+                                            ctypes.c_int, ctypes.c_int, _p, ctypes.c_int, _p, _p, _p,
+                                            ctypes.c_size_t, _p]
     lib.mvbev_warp_tile_mask.restype = ctypes.c_int
     lib.mvbev_warp_tile_mask.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
                                          _i64, _i64, _i64, _i64, _p, _p]

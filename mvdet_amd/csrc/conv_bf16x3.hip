@@ -91,6 +91,7 @@ struct Args {
   // stay on one XCD (they share the halo reads)
   const int32_t* tile_order;
   int npix;
+  bool y_split;  // y in the split-bf16 blocked layout (the next conv's 16-B staging copies)
 };
 
 // Input tag: the split-bf16 blocked layout written by mvbev_warp_views_split_bf16 and by this
@@ -133,15 +134,54 @@ __device__ inline void tile_epilogue(const Args& a, int tile, const floatx16 (&a
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt) {
       const int row = y0 + prow + pt;
-      if (row >= a.out_row0 + a.out_rows || col >= W) continue;
+      const bool valid = row < a.out_row0 + a.out_rows && col < W;
+      if (!a.y_split) {
+        if (!valid) continue;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = cot * BN + cw + 32 * ct + (r & 3) + 8 * (r >> 2) + 4 * kh;
-        float v = acc[ct][pt][r];
-        if (a.bias) v += a.bias[co];
-        if (a.init) v += a.init[co * iplane + (int64_t)row * W + col];
-        if (RELU) v = v < 0.f ? 0.f : v;
-        a.y[((int64_t)b * a.Cout + co) * oplane + (int64_t)(row - a.out_row0) * W + col] = v;
+        for (int r = 0; r < 16; ++r) {
+          const int co = cot * BN + cw + 32 * ct + (r & 3) + 8 * (r >> 2) + 4 * kh;
+          float v = acc[ct][pt][r];
+          if (a.bias) v += a.bias[co];
+          if (a.init) v += a.init[co * iplane + (int64_t)row * W + col];
+          if (RELU) v = v < 0.f ? 0.f : v;
+          a.y[((int64_t)b * a.Cout + co) * oplane + (int64_t)(row - a.out_row0) * W + col] = v;
+        }
+        continue;
+      }
+      // split-bf16 output: the lane holds channels 4kh..4kh+3 of four 8-channel groups; its
+      // partner lane (lane ^ 32) holds the other half.  kh = 0 writes each group's 16-B hi
+      // piece, kh = 1 its lo piece, after swapping the half the partner needs.
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        unsigned int hp[2], lp[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float v2[2];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int r = 4 * q + 2 * h + e;
+            const int co = cot * BN + cw + 32 * ct + (r & 3) + 8 * (r >> 2) + 4 * kh;
+            float v = acc[ct][pt][r];
+            if (a.bias) v += a.bias[co];
+            if (a.init && valid) v += a.init[co * iplane + (int64_t)row * W + col];
+            if (RELU) v = v < 0.f ? 0.f : v;
+            v2[e] = v;
+          }
+          const __bf16 h0 = (__bf16)v2[0], h1 = (__bf16)v2[1];
+          const __bf16 l0 = (__bf16)(v2[0] - (float)h0), l1 = (__bf16)(v2[1] - (float)h1);
+          hp[h] = (unsigned)__builtin_bit_cast(unsigned short, h0) |
+                  ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
+          lp[h] = (unsigned)__builtin_bit_cast(unsigned short, l0) |
+                  ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
+        }
+        const unsigned s0 = kh ? hp[0] : lp[0], s1 = kh ? hp[1] : lp[1];
+        const unsigned r0 = (unsigned)__shfl_xor((int)s0, 32), r1 = (unsigned)__shfl_xor((int)s1, 32);
+        const u32x4 piece = kh ? u32x4{r0, r1, lp[0], lp[1]} : u32x4{hp[0], hp[1], r0, r1};
+        if (valid) {
+          const int64_t g = (cot * BN + cw + 32 * ct) / 8 + q;
+          u32x4* out = reinterpret_cast<u32x4*>(a.y);
+          out[2 * ((((int64_t)b * (a.Cout / 8) + g) * a.out_rows + (row - a.out_row0)) * W + col) + kh] = piece;
+        }
       }
     }
 }
@@ -508,7 +548,7 @@ static int64_t conv_tiles(const mvbev_conv_desc* d, int64_t Cout) {
 template <typename TIn>
 static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
                   const float* bias, const float* init, int64_t Cout, int dilation, int relu,
-                  float* y, const uint32_t* group_mask, const int32_t* tile_order,
+                  float* y, int y_layout, const uint32_t* group_mask, const int32_t* tile_order,
                   void* workspace, size_t ws_bytes, void* stream) {
   if (!x || !d || !w_packed || !y) return MVBEV_ERR_NULL;
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || d->in_rows <= 0 ||
@@ -541,6 +581,8 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
     a.cpg = (int)(d->group / KC);
   }
   a.tile_order = group_mask ? tile_order : nullptr;
+  if (y_layout != MVBEV_LAYOUT_F32 && y_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;
+  a.y_split = y_layout == MVBEV_LAYOUT_SPLIT_BF16;
   a.npix = (int)(tiles / a.n_cot);
   const SkPlan plan = group_mask ? SkPlan() : sk_plan(tiles, a.nchunks);
   const bool sk = workspace && plan.split > 1 &&
@@ -606,7 +648,7 @@ int mvbev_conv3x3_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* des
                          const void* w_packed, const float* bias, const float* init,
                          int64_t Cout, int dilation, int relu, float* y, void* stream) {
   return mvbev_conv3x3_bf16x3_ex(x, x_layout, desc, w_packed, bias, init, Cout, dilation, relu, y,
-                                 nullptr, nullptr, nullptr, 0, stream);
+                                 MVBEV_LAYOUT_F32, nullptr, nullptr, nullptr, 0, stream);
 }
 
 size_t mvbev_conv3x3_bf16x3_workspace_bytes(const mvbev_conv_desc* desc, int64_t Cout) {
@@ -619,18 +661,21 @@ size_t mvbev_conv3x3_bf16x3_workspace_bytes(const mvbev_conv_desc* desc, int64_t
 
 int mvbev_conv3x3_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_desc* desc,
                             const void* w_packed, const float* bias, const float* init,
-                            int64_t Cout, int dilation, int relu, float* y,
+                            int64_t Cout, int dilation, int relu, void* y, int y_layout,
                             const uint32_t* group_mask, const int32_t* tile_order, void* workspace,
                             size_t workspace_bytes, void* stream) {
   using namespace mvbev::b3;
   if (x_layout == MVBEV_LAYOUT_SPLIT_BF16)
-    return launch<SplitIn>(x, desc, w_packed, bias, init, Cout, dilation, relu, y, group_mask,
-                           tile_order, workspace, workspace_bytes, stream);
+    return launch<SplitIn>(x, desc, w_packed, bias, init, Cout, dilation, relu,
+                           static_cast<float*>(y), y_layout, group_mask, tile_order, workspace,
+                           workspace_bytes, stream);
   if (x_layout == MVBEV_LAYOUT_F16)
-    return launch<_Float16>(x, desc, w_packed, bias, init, Cout, dilation, relu, y, group_mask,
-                            tile_order, workspace, workspace_bytes, stream);
-  return launch<float>(x, desc, w_packed, bias, init, Cout, dilation, relu, y, group_mask,
-                       tile_order, workspace, workspace_bytes, stream);
+    return launch<_Float16>(x, desc, w_packed, bias, init, Cout, dilation, relu,
+                            static_cast<float*>(y), y_layout, group_mask, tile_order, workspace,
+                            workspace_bytes, stream);
+  return launch<float>(x, desc, w_packed, bias, init, Cout, dilation, relu,
+                       static_cast<float*>(y), y_layout, group_mask, tile_order, workspace,
+                       workspace_bytes, stream);
 }
 
 }  // extern "C"

@@ -353,10 +353,15 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
         desc.group * desc.in_rows * W
     if (x.untyped_storage().nbytes() - x.storage_offset() * x.element_size()) // unit < need:
         raise ValueError("x's storage is too small for the conv descriptor")
+    y_split = out is not None and out.dtype == torch.bfloat16  # split-bf16 blocked output
     if out is None:
         out = torch.empty((B, cout, out_rows, W), dtype=torch.float32, device=x.device)
-    elif tuple(out.shape) != (B, cout, out_rows, W) or not out.is_contiguous():
-        raise ValueError(f"out must be a contiguous [{B},{cout},{out_rows},{W}] tensor")
+    elif y_split:
+        if not bf16x3 or tuple(out.shape) != split_shape(B, cout, out_rows, W) or not out.is_contiguous():
+            raise ValueError(f"a split out must be a contiguous bf16 {split_shape(B, cout, out_rows, W)} tensor "
+                             "of the bf16x3 conv")
+    elif tuple(out.shape) != (B, cout, out_rows, W) or not out.is_contiguous() or out.dtype != torch.float32:
+        raise ValueError(f"out must be a contiguous fp32 [{B},{cout},{out_rows},{W}] tensor")
     if bias is not None:
         _require_cuda(bias)
         bias = bias.detach().contiguous()
@@ -390,7 +395,8 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
             top = tile_order.data_ptr()
         st = lib.mvbev_conv3x3_bf16x3_ex(x.data_ptr(), layout, ctypes.byref(desc),
                                          packed.data_ptr(), bp, ip, cout, int(dilation), int(bool(relu)),
-                                         out.data_ptr(), gmp, top, wsp, wsn, _stream(x))
+                                         out.data_ptr(), _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32,
+                                         gmp, top, wsp, wsn, _stream(x))
         _native.check(st, "mvbev_conv3x3_bf16x3_ex")
     elif group_mask is not None:
         raise ValueError("group_mask needs the bf16x3 conv")

@@ -172,6 +172,9 @@ class ViewPartialSum(ViewParallel):
         # a rank without views still runs the band fusion: give it an engine over view 0's
         # slot layout (its slab is never written or read) for the packed conv2 weights etc.
         self._fuse_engine = self.engine if self.engine is not None else engine_factory([0])
+        for e in (self.engine, self._fuse_engine):  # the exchange sums fp32 partials into y1
+            if e is not None and hasattr(e, "y1_split"):
+                e.y1_split = False
 
     def workspace(self, B: int, device):
         r0, r1 = self.band

@@ -113,6 +113,9 @@ class ProjectFuse:
         # frustum; geometry-only, so the mask is built once per device and row range)
         self.frustum = frustum and precision == "bf16x3" and self.Cs % 16 == 0 and self.S <= 16
         self._masks: Dict[tuple, torch.Tensor] = {}
+        # conv1 writes y1 pre-split (bf16 hi/lo blocks) so conv2 stages it with 16-B copies;
+        # the partial-sum multi-GPU mode turns this off (it sums fp32 partials)
+        self.y1_split = precision == "bf16x3"
 
     # -- buffers ----------------------------------------------------------------------------
     def workspace(self, B: int, device, band: Optional[Tuple[int, int]] = None) -> Workspace:
@@ -128,12 +131,20 @@ class ProjectFuse:
             else:
                 slab = torch.zeros((self.S, B, self.Cs, H, W), dtype=self.slab_dtype, device=device)
             y1r, y2r = band_rows(band[0], band[1], H)
-            y1 = torch.empty((B, self.mid, y1r[1] - y1r[0], W), dtype=torch.float32, device=device)
+            if self.y1_split:
+                y1 = torch.empty(ops.split_shape(B, self.mid, y1r[1] - y1r[0], W), dtype=torch.bfloat16,
+                                 device=device)
+            else:
+                y1 = torch.empty((B, self.mid, y1r[1] - y1r[0], W), dtype=torch.float32, device=device)
             y2 = torch.empty((B, self.mid, y2r[1] - y2r[0], W), dtype=torch.float32, device=device)
             m = self.m_norm_cpu.to(device)[:, None].expand(self.num_cam, B, 3, 3).contiguous()
             ws = Workspace(slab, y1, y2, m, band, y1r, y2r)
             self._ws[key] = ws
         return ws
+
+    def y1_fp32(self, ws: Workspace) -> torch.Tensor:
+        """conv1's output rows ``ws.y1_rows`` as fp32 [B, 512, rows, Wo] (decodes the split layout)."""
+        return ops.split_decode(ws.y1, self.mid) if ws.y1.dtype == torch.bfloat16 else ws.y1
 
     def view_slice(self, ws: Workspace, cam: int) -> torch.Tensor:
         """[B, C, Ho, Wo] of ``cam``'s warped features: a view of the slab, or (split
@@ -263,6 +274,7 @@ class ProjectFuse:
         B = ws.slab.shape[1]
         p2 = self.pack2.get(conv2.weight)
         (a1, b1), (a2, b2) = ws.y1_rows, ws.y2_rows
+        B = ws.y1.shape[0]
         d2 = ops.conv_desc(B, self.mid, H, W, group=self.mid, group_stride=0,
                            batch_stride=self.mid * (b1 - a1) * W, in_row0=a1, in_rows=b1 - a1,
                            out_row0=a2, out_rows=b2 - a2)

@@ -405,7 +405,7 @@ def test_detector_forward_matches_reference_golden(name):
                                rtol=2e-3, atol=2e-2)
     if "warp_out" in g:
         assert_parity(warped.cpu(), g["warp_out"], "warp_out")
-        assert_parity(ws.y1.cpu(), g["conv1_relu"], "conv1")
+        assert_parity(eng.y1_fp32(ws).cpu(), g["conv1_relu"], "conv1")
         assert_parity(ws.y2.cpu(), g["conv2_relu"], "conv2")
 
 
@@ -451,6 +451,6 @@ def test_full_size_project_fuse_vs_oracle(cfg, precision):
     ws = eng.workspace(B, DEV)
     for v in range(ds.num_cam):
         assert_parity(eng.view_slice(ws, v).cpu(), keep["warped"][v], f"cfg{cfg} warp view {v}")
-    assert_parity(ws.y1.cpu(), keep["conv1_relu"], f"cfg{cfg} conv1")
+    assert_parity(eng.y1_fp32(ws).cpu(), keep["conv1_relu"], f"cfg{cfg} conv1")
     assert_parity(ws.y2.cpu(), keep["conv2_relu"], f"cfg{cfg} conv2")
     assert_parity(got.cpu(), ref, f"cfg{cfg} map_result")

@@ -53,7 +53,7 @@ def main():
     rep = {"config": args.config, "precision": args.precision, "slab": str(eng.slab_dtype)}
     rep["warp_worst_normwise"] = max(parity_stats(eng.view_slice(ws, v).float().cpu(), keep["warped"][v])["normwise"]
                                      for v in range(ds.num_cam))
-    for name, g, r in (("conv1", ws.y1, keep["conv1_relu"]), ("conv2", ws.y2, keep["conv2_relu"]),
+    for name, g, r in (("conv1", eng.y1_fp32(ws), keep["conv1_relu"]), ("conv2", ws.y2, keep["conv2_relu"]),
                        ("map_result", got, ref)):
         s = parity_stats(g.cpu(), r)
         rep[name] = {"normwise": s["normwise"], "gate_violations": s["n_bad"]}

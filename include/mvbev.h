@@ -231,6 +231,22 @@ int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int
                             int64_t in_row0, int64_t in_rows, int64_t out_row0, int64_t out_rows,
                             const float* w, int dilation, float* y, void* stream);
 
+/* ---- evaluation post-processing (trainer.py:97-106, 148-157) ---- */
+
+/* map > thres over an H x W map, in row-major (torch.nonzero) order: *count = number of hits
+ * (device int32), ij[2k], ij[2k+1] = row, column and scores[k] = value of the first
+ * min(count, capacity) hits.  One workgroup; enqueued, no host sync. */
+int mvbev_threshold_points(const float* map, int64_t H, int64_t W, float thres, int32_t* count,
+                           int32_t* ij, float* scores, int64_t capacity, void* stream);
+
+/* Greedy point NMS of multiview_detector/utils/nms.py:7-43: candidates by descending score
+ * (equal scores: larger index first), the top_k largest considered; keep the best, drop every
+ * later candidate whose distance sqrt(dx^2+dy^2) (fp32, correctly rounded) is not > dist_thres,
+ * repeat.  points [K][2] fp32, scores [K] fp32 (device); keep [K] int64 = kept indices then
+ * zeros; *count (device int32) = number kept.  K <= 8192 (one workgroup, LDS sort). */
+int mvbev_point_nms(const float* points, const float* scores, int64_t K, float dist_thres,
+                    int64_t top_k, int64_t* keep, int32_t* count, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -33,6 +33,8 @@ EXPORTS = (
     "mvbev_conv3x3_bf16x3_workspace_bytes",
     "mvbev_conv3x3_bf16x3_ex",
     "mvbev_warp_tile_mask",
+    "mvbev_threshold_points",
+    "mvbev_point_nms",
 )
 
 KC = 8    # MVBEV_CONV_KC
@@ -107,6 +109,10 @@ def _declare(lib):
     lib.mvbev_warp_tile_mask.restype = ctypes.c_int
     lib.mvbev_warp_tile_mask.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
                                          _i64, _i64, _i64, _i64, _p, _p]
+    lib.mvbev_threshold_points.restype = ctypes.c_int
+    lib.mvbev_threshold_points.argtypes = [_p, _i64, _i64, ctypes.c_float, _p, _p, _p, _i64, _p]
+    lib.mvbev_point_nms.restype = ctypes.c_int
+    lib.mvbev_point_nms.argtypes = [_p, _p, _i64, ctypes.c_float, _i64, _p, _p, _p]
     lib.mvbev_conv3x3_cout1_f32.restype = ctypes.c_int
     lib.mvbev_conv3x3_cout1_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p,
                                             ctypes.c_int, _p, _p]

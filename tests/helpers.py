@@ -17,7 +17,8 @@ ATOL_FRAC = 1e-3
 
 def load_golden(name):
     d = dict(np.load(GOLDEN / f"{name}.npz", allow_pickle=False))
-    d["meta"] = json.loads(str(d["meta"]))
+    if "meta" in d:
+        d["meta"] = json.loads(str(d["meta"]))
     return d
 
 

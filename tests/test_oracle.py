@@ -134,3 +134,25 @@ def test_touched_footprint_counts():
     M2 = np.diag([0.5, 0.5, 1.0])  # dst is half-size: samples at even src pixels (+ corners)
     t = kornia_warp.touched_footprint(M2, (8, 8), (4, 4))
     assert 0 < t <= 64
+
+
+# ------------------------------------------------------------------ post-processing (§8(f) row 4)
+
+def test_postproc_oracle_matches_reference_nms_golden():
+    """oracle/postproc.py vs the reference's own nms / evaluation rows (tests/golden/nms_cases.npz)."""
+    import numpy as np
+    import torch
+    from helpers import load_golden
+    from oracle import postproc
+    g = load_golden("nms_cases")
+    for i in range(5):
+        top_k = float(g[f"c{i}_topk"])
+        top_k = int(top_k) if np.isfinite(top_k) else np.inf
+        keep, count = postproc.nms(torch.from_numpy(g[f"c{i}_points"]), torch.from_numpy(g[f"c{i}_scores"]),
+                                   float(g[f"c{i}_dist"]), top_k)
+        assert count == int(g[f"c{i}_count"])
+        np.testing.assert_array_equal(keep.numpy(), g[f"c{i}_keep"])
+    for j in range(2):
+        rows = postproc.threshold_rows(torch.from_numpy(g[f"map{j}"])[None, None], 7, 0.4, 4, str(g[f"map{j}_indexing"]))
+        np.testing.assert_array_equal(rows.numpy(), g[f"map{j}_rows"])
+        np.testing.assert_array_equal(postproc.frame_results(rows).numpy(), g[f"map{j}_final"])

@@ -105,6 +105,9 @@ template <> __device__ inline float ld<_Float16>(const _Float16* p) { return (fl
 #ifndef MVBEV_B3_MINWAVES
 #define MVBEV_B3_MINWAVES 1
 #endif
+#ifndef MVBEV_MASK_GROUP
+#define MVBEV_MASK_GROUP 2  // consecutive ordered pixel tiles per XCD turn (A/B at cfg2: 1 and 2 equal, 4 and 8 5 % slower)
+#endif
 #ifndef MVBEV_B3_DEPTH
 #define MVBEV_B3_DEPTH 2  // staging-register ring depth (1 or 2)
 #endif
@@ -262,8 +265,13 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
                       : xcd_remap(bid, a.sk_ws ? a.dp_tiles : a.nwg);
   int tile = wg, k0 = 0, k1 = n, piece = -1;  // K-range in (active) chunk order
   if (a.gmask) {  // uneven per-tile work: spread pixel tiles over the XCDs, heaviest first
+    // XCD x runs groups of MVBEV_MASK_GROUP consecutive slots of the order (tiles with the
+    // same view set, so concurrent workgroups share weight chunks in L2), groups dealt
+    // round-robin over the XCDs (balance)
+    constexpr int G = MVBEV_MASK_GROUP;
     const int x = bid & 7, j = bid >> 3;
-    const int slot = (j / a.n_cot) * 8 + x;
+    const int q = j / a.n_cot;
+    const int slot = G * (8 * (q / G) + x) + q % G;
     if (slot >= a.npix) return;  // padding block (whole block, before any barrier)
     tile = (a.tile_order ? a.tile_order[slot] : slot) * a.n_cot + j % a.n_cot;
   }
@@ -590,7 +598,7 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   a.sk_ws = sk ? static_cast<float*>(workspace) : nullptr;
   a.dp_tiles = (int)(sk ? plan.dp_tiles : tiles);
   a.split = sk ? plan.split : 1;
-  const int64_t nwg = group_mask ? (int64_t)a.n_cot * round_up(a.npix, 8)
+  const int64_t nwg = group_mask ? (int64_t)a.n_cot * round_up(a.npix, 8 * MVBEV_MASK_GROUP)
                                  : (sk ? plan.dp_tiles + plan.tail * plan.split : tiles);
   if (nwg > (int64_t)INT32_MAX) return MVBEV_ERR_SHAPE;
   a.nwg = (int)nwg;

@@ -323,11 +323,13 @@ def warp_tile_mask(m_norms, src_hw, grid_hw, row0: int, rows: int, halo: int, de
 
 
 def heavy_first_order(mask: torch.Tensor, B: int) -> torch.Tensor:
-    """Pixel tiles (b, tile) sorted by active channel groups, most first (ties in index
-    order): the run order that evens out a frustum-masked conv's per-tile work."""
-    bits = [bin(int(v) & 0xFFFFFFFF).count("1") for v in mask.cpu().tolist()]
+    """Pixel tiles (b, tile) sorted by active channel groups, most first, equal view sets
+    together: the run order that evens out a frustum-masked conv's per-tile work."""
+    masks = [int(v) & 0xFFFFFFFF for v in mask.cpu().tolist()]
+    bits = [bin(m).count("1") for m in masks]
     T = len(bits)
-    order = sorted(range(B * T), key=lambda i: (-bits[i % T], i))
+    # most work first; equal view sets adjacent (they share weight chunks when run together)
+    order = sorted(range(B * T), key=lambda i: (-bits[i % T], masks[i % T], i))
     return torch.tensor(order, dtype=torch.int32, device=mask.device)
 
 

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 10100: frustum masks, split-K tail, fused upsample+warp */
+int mvbev_version(void);  /* 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -230,6 +230,64 @@ int mvbev_conv3x3_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_desc* 
 int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int64_t W,
                             int64_t in_row0, int64_t in_rows, int64_t out_row0, int64_t out_rows,
                             const float* w, int dilation, float* y, void* stream);
+
+/* ---- native backward: training through the hot path ----------------
+ * Replaces the autograd of the stock ops the reference trains through (trainer.py:38-49,
+ * loss.backward() at :47): grid_sample's backward under kornia.warp_perspective
+ * (persp_trans_detector.py:69) and nn.Conv2d / nn.ReLU backward of map_classifier (:51-54). */
+
+/* Adjoint of mvbev_warp_views_* (bilinear, zeros padding, align_corners=True): for every output
+ * pixel whose sample point is finite and inside, each in-bounds corner of the source gradient
+ * gets w_corner * grad_out (fp32 atomic adds; no gradient from zero-padded or NaN samples).
+ *   views[i].src : grad_out, [B][C][Ho][Wo] fp32 at element strides src_strides
+ *   views[i].dst : grad_src, [B][C][H][W] fp32 at element strides dst_strides ([3] must be 1);
+ *                  ACCUMULATED into (zero it first for a plain gradient)
+ *   views[i].m   : the forward's src_norm <- dst_norm matrix. */
+int mvbev_warp_views_backward_f32(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
+                                  int64_t H, int64_t W, int64_t Ho, int64_t Wo, void* stream);
+
+/* Weights for the data gradient of a 3x3 stride-1 conv with padding = dilation: that gradient is
+ * the same conv over dy with w'[k][co][t] = w[co][k][8 - t], so mvbev_conv3x3_bf16x3_ex computes
+ * it with these weights (Cout' = round_up(K_out, MVBEV_CONV_BN) output channels, K' = Cout_w).
+ * Output channel o of the dgrad conv is forward input channel chan_map[o] (device int32[K_out],
+ * -1 = zero; NULL = identity).  w: forward weight [Cout_w][Cin_w][3][3] fp32.  Size:
+ * mvbev_conv3x3_packed_bytes_bf16x3(round_up(K_out, 128), Cout_w). */
+int mvbev_pack_conv3x3_dgrad_bf16x3(const float* w, int64_t Cout_w, int64_t Cin_w,
+                                    const int32_t* chan_map, int64_t K_out, void* w_packed,
+                                    void* stream);
+
+/* Weight gradient of mvbev_conv3x3_bf16x3 (3xbf16 MFMA, fp32 accumulation):
+ *   dw[co][chan_map[k]][t] = sum_b,y,x dy[b][co][y][x] * x[b][k][y + (t/3-1)d][x + (t%3-1)d]
+ * x as in the forward (desc: whole image, in_row0 = out_row0 = 0, in_rows = out_rows = H;
+ * x_layout MVBEV_LAYOUT_F32 or MVBEV_LAYOUT_SPLIT_BF16); dy [B][Cout][H][W] fp32 contiguous,
+ * Cout % 128 == 0; dw [Cout][Cin_w][3][3] fp32 — only the channels chan_map names are written
+ * (chan_map NULL = identity, K <= Cin_w).  dilation 1 or 2.  workspace: device scratch of
+ * mvbev_conv3x3_wgrad_workspace_bytes() (per-partition partial sums; the reduction over
+ * partitions runs in a fixed order, so the result is deterministic). */
+size_t mvbev_conv3x3_wgrad_workspace_bytes(const mvbev_conv_desc* desc, int64_t Cout);
+int mvbev_conv3x3_wgrad_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* desc,
+                               const float* dy, int64_t Cout, int dilation, const int32_t* chan_map,
+                               int64_t Cin_w, float* dw, void* workspace, size_t workspace_bytes,
+                               void* stream);
+
+/* db[co] = sum_b,p dy[b][co][p] (db may be NULL) and, when dw != NULL, the weight gradient of the
+ * two coord channels (create_coord_map, persp_trans_detector.py:103-112) that are input channels
+ * coord_ch, coord_ch + 1 of a conv of the given dilation: dw[co][coord_ch + j][t] (dw is
+ * [Cout][Cin_w][3][3]).  dy [B][Cout][H][W] fp32. */
+int mvbev_conv3x3_bias_coord_grad_f32(const float* dy, int64_t B, int64_t Cout, int64_t H, int64_t W,
+                                      int dilation, float* db, float* dw, int64_t Cin_w,
+                                      int64_t coord_ch, void* stream);
+
+/* In place: dy[i] = y[i] > 0 ? dy[i] : 0 (y = the ReLU's output; torch threshold_backward). */
+int mvbev_relu_backward_f32(float* dy, const float* y, int64_t n, void* stream);
+
+/* Backward of mvbev_conv3x3_cout1_f32 over a whole image (x [B][C][H][W], w [C][3][3], dmap
+ * [B][1][H][W] fp32):  dx[b][c][p] = sum_t w[c][t] dmap[b][p - s_t], zeroed where x <= 0 when
+ * relu_mask (x is the previous ReLU's output: its backward fused); dw[c][t] = sum_b,p
+ * dmap[b][p] x[b][c][p + s_t].  Either output may be NULL. */
+int mvbev_conv3x3_cout1_backward_f32(const float* x, const float* w, const float* dmap, int64_t B,
+                                     int64_t C, int64_t H, int64_t W, int dilation, int relu_mask,
+                                     float* dx, float* dw, void* stream);
 
 /* ---- evaluation post-processing (trainer.py:97-106, 148-157) ---- */
 

@@ -1,0 +1,142 @@
+"""Native training path through project+fuse.
+
+The reference trains through the hot path with stock autograd (``trainer.py:38-49``:
+``map_res, imgs_res = model(data)`` then ``loss.backward()``): grid_sample's backward under
+``kornia.warp_perspective`` (``persp_trans_detector.py:69``), the concat (``:77``) and
+``nn.Conv2d``/``nn.ReLU`` backward of ``map_classifier`` (``:51-54``).  ``ProjectFuseFunction``
+is one ``torch.autograd.Function`` whose forward is the engine's HIP forward (warp into the
+slab, conv1-3) and whose backward is all HIP:
+
+  conv3 (Cout 1, d4)   dy2 = dgrad(dmap) * [y2 > 0] (conv2's ReLU fused), dw3     (cout1 kernels)
+  conv2 (d2) + ReLU    db2, dw2 = wgrad(y1, dy2) (3xbf16 MFMA), dy1 = dgrad-conv(dy2) * [y1 > 0]
+  conv1 (d1) + ReLU    db1 + coord-channel dw1, view-channel dw1 = wgrad(slab, dy1),
+                       dslab = dgrad-conv(dy1) (forward conv kernel on transposed+flipped taps)
+  warp                 grad_feat[v] += adjoint-gather(dslab[v]) (fp32 atomics)
+
+Activations saved for the backward: the slab (the forward's own buffer, split-bf16 with
+3xbf16), y1 and y2 in fp32 (a fresh set per training forward, so a second forward before
+``backward()`` cannot overwrite them).  Parity: gradients within the north_star's 1e-3
+relative fp32 gate of torch's CPU autograd on the same inputs (``tests/test_gpu_backward.py``).
+"""
+from __future__ import annotations
+
+from types import SimpleNamespace
+from typing import Sequence
+
+import torch
+
+from . import ops
+from .pipeline import ProjectFuse, Workspace, band_rows
+
+
+def _train_workspace(engine: ProjectFuse, B: int, device) -> Workspace:
+    """A fresh (never reused) forward workspace with fp32 y1 (the ReLU mask source)."""
+    H, W = engine.grid_hw
+    if engine.split:
+        slab = torch.zeros((engine.S,) + ops.split_shape(B, engine.Cs, H, W), dtype=torch.bfloat16, device=device)
+    else:
+        slab = torch.zeros((engine.S, B, engine.Cs, H, W), dtype=engine.slab_dtype, device=device)
+    y1r, y2r = band_rows(0, H, H)
+    y1 = torch.empty((B, engine.mid, H, W), dtype=torch.float32, device=device)
+    y2 = torch.empty((B, engine.mid, H, W), dtype=torch.float32, device=device)
+    m = engine.m_norm_cpu.to(device)[:, None].expand(engine.num_cam, B, 3, 3).contiguous()
+    return Workspace(slab, y1, y2, m, (0, H), y1r, y2r)
+
+
+def _bwd_state(engine: ProjectFuse):
+    st = getattr(engine, "_bwd", None)
+    if st is None:
+        nc = engine.num_cam * engine.C
+        st = SimpleNamespace(dgrad1=ops.PackedDgrad3x3(nc), dgrad2=ops.PackedDgrad3x3(engine.mid), wg_ws={})
+        engine._bwd = st
+    return st
+
+
+def _wgrad_ws(st, desc, cout, device) -> torch.Tensor:
+    import ctypes
+    from . import _native
+    need = int(_native.load().mvbev_conv3x3_wgrad_workspace_bytes(ctypes.byref(desc), cout))
+    buf = st.wg_ws.get(str(device))
+    if buf is None or buf.numel() * 4 < need:
+        buf = torch.empty((need + 3) // 4, dtype=torch.float32, device=device)
+        st.wg_ws[str(device)] = buf
+    return buf
+
+
+class ProjectFuseFunction(torch.autograd.Function):
+    """``map = fuse(concat(warp(feats[v]) for v) + coord)``; inputs after the engine: the N
+    upsampled view features [B,C,H,W] then conv1.w, conv1.b, conv2.w, conv2.b, conv3.w."""
+
+    @staticmethod
+    def forward(ctx, engine: ProjectFuse, *args):
+        n = engine.num_cam
+        feats, (w1, b1, w2, b2, w3) = args[:n], args[n:]
+        if engine.slab_dtype != torch.float32 or engine.S != n:
+            raise ValueError("the native backward needs an fp32-storage single-GPU engine")
+        B = feats[0].shape[0]
+        dev = feats[0].device
+        ws = _train_workspace(engine, B, dev)
+        engine.warp_views(ws, list(range(n)), [f.detach() for f in feats])
+        mc = [SimpleNamespace(weight=w1, bias=b1), None, SimpleNamespace(weight=w2, bias=b2), None,
+              SimpleNamespace(weight=w3, bias=None)]
+        out = engine.fuse(ws, mc)
+        ctx.engine = engine
+        ctx.ws = ws
+        ctx.feat_shape = tuple(feats[0].shape)
+        ctx.save_for_backward(w1, b1, w2, b2, w3)
+        return out
+
+    @staticmethod
+    def backward(ctx, dmap):
+        engine: ProjectFuse = ctx.engine
+        ws: Workspace = ctx.ws
+        w1, b1, w2, b2, w3 = ctx.saved_tensors
+        n = engine.num_cam
+        need = ctx.needs_input_grad[1:]
+        need_feat = any(need[:n])
+        st = _bwd_state(engine)
+        H, W = engine.grid_hw
+        B = ws.y1.shape[0]
+        dev = ws.y1.device
+        dmap = dmap.contiguous().float()
+        mid = engine.mid
+        # conv3: dy2 = dgrad * relu'(y2); dw3
+        dy2, dw3 = ops.conv3x3_cout1_backward(ws.y2, w3, dmap, 4, relu_mask=True)
+        # conv2: db2, dw2, dy1 = dgrad * relu'(y1)
+        db2 = torch.empty(mid, dtype=torch.float32, device=dev) if b2 is not None else None
+        if db2 is not None:
+            ops.conv3x3_bias_coord_grad(dy2, 2, db=db2)
+        d_y1 = ops.conv_desc(B, mid, H, W, group=mid, group_stride=0, batch_stride=mid * H * W)
+        dw2 = ops.conv3x3_wgrad(ws.y1, d_y1, dy2, 2, mid, workspace=_wgrad_ws(st, d_y1, mid, dev))
+        dy1 = ops.conv3x3_dgrad(dy2, st.dgrad2, w2, 2)
+        if dy1.shape[1] != mid:
+            dy1 = dy1[:, :mid].contiguous()
+        del dy2
+        ops.relu_backward_(dy1, ws.y1)
+        # conv1: db1 + coord channels, view channels (slab order through the pack's channel map)
+        nc = n * engine.C
+        dw1 = torch.zeros_like(w1)
+        db1 = torch.empty(mid, dtype=torch.float32, device=dev) if b1 is not None else None
+        ops.conv3x3_bias_coord_grad(dy1, 1, db=db1, dw=dw1, coord_ch=nc)
+        engine.pack1.get(w1)  # materialises the device channel map
+        d1 = ops.conv_desc(B, engine.S * engine.Cs, H, W, group=engine.Cs, group_stride=B * engine.Cs * H * W,
+                           batch_stride=engine.Cs * H * W)
+        ops.conv3x3_wgrad(ws.slab, d1, dy1, 1, w1.shape[1], chan_map=engine.pack1._map_dev, dw=dw1,
+                          workspace=_wgrad_ws(st, d1, mid, dev))
+        grads = [None] * n
+        if need_feat:
+            dslab = ops.conv3x3_dgrad(dy1, st.dgrad1, w1, 1)   # [B, round_up(nc,128), H, W]
+            C = engine.C
+            gs = [torch.zeros(ctx.feat_shape, dtype=torch.float32, device=dev) for _ in range(n)]
+            ops.warp_views_backward([dslab[:, v * C:(v + 1) * C] for v in range(n)],
+                                    [engine.m_norm_cpu[v] for v in range(n)], gs)
+            grads = [g if need[v] else None for v, g in enumerate(gs)]
+        ctx.ws = None
+        return (None, *grads, dw1, db1, dw2, db2, dw3)
+
+
+def project_fuse(engine: ProjectFuse, feats: Sequence[torch.Tensor], map_classifier) -> torch.Tensor:
+    """Differentiable project+fuse: ``feats[v]`` the upsampled [B,C,H,W] features of view v,
+    ``map_classifier`` the reference's ``nn.Sequential`` (``persp_trans_detector.py:51-54``)."""
+    c1, c2, c3 = map_classifier[0], map_classifier[2], map_classifier[4]
+    return ProjectFuseFunction.apply(engine, *feats, c1.weight, c1.bias, c2.weight, c2.bias, c3.weight)

@@ -1,0 +1,635 @@
+// Native backward of the project+fuse hot path for gfx950: what
+// autograd needs to train through PerspTransDetector.forward (trainer.py:38-49) without the
+// stock-torch fallback.
+//
+//   warp (a5, persp_trans_detector.py:69)   adjoint of the bilinear gather: grad_src +=
+//                                            w_corner * grad_out (fp32 atomic adds), the
+//                                            kornia/grid_sample weights of the forward
+//   conv1 / conv2 (map_classifier[0], [2])  weight gradient: wgrad_kernel below (3xbf16 MFMA);
+//                                            data gradient: the forward conv kernel with the
+//                                            weights packed transposed + flipped
+//                                            (mvbev_pack_conv3x3_dgrad_bf16x3, conv_bf16x3.hip);
+//                                            bias + coord-channel gradients: bias_coord_grad_kernel
+//   ReLUs (map_classifier[1], [3])          relu_backward_kernel (torch threshold_backward:
+//                                            grad where the ReLU output > 0)
+//   conv3 (map_classifier[4], Cout = 1)     cout1_dgrad_kernel (fused with conv2's ReLU mask),
+//                                            cout1_wgrad_kernel
+//
+// Weight gradient as a GEMM: dW_t[co][k] = sum over pixels p of dy[co][p] * x[k][p + s_t]
+// (s_t = the tap's dilated offset).  M = Cout, N = input channels x 9 taps, K = pixels.  A
+// workgroup (8 waves) owns 128 output channels x 64 input channels x all 9 taps and walks its
+// share of the pixels in chunks of one 32-pixel row segment (2 MFMA K-steps of 16):
+//   A image  dy[128 co][32 px] bf16 hi / lo, 80-B rows (conflict-free ds_read_b128 of 8 px);
+//   B image  x[3 rows][32 + 2d px][32 ch] bf16 hi / lo per 32-channel half, 64 B per pixel;
+//            the B fragment (8 consecutive pixels of one channel per lane) is read with the
+//            gfx950 transposing ds_read_b64_tr_b16 from this channel-innermost image (the
+//            slab's own split-bf16 layout copied 16 B at a time), so every tap is just a
+//            different pixel offset: no im2col, no shifted copies, 4 rows x 64 B = 256 B per
+//            32-lane half = conflict-free.
+// Wave = 32 co x 32 ch x 9 taps (9 accumulators); per K-step 2 A + 36 transposed B reads for
+// 27 MFMAs (3 passes: lo*hi, hi*lo, hi*hi as in the forward).  The pixels are split into P
+// partitions (row bands) so the launch fills the CUs; partial sums land in a workspace and
+// wgrad_reduce_kernel adds them in partition order (deterministic) while scattering the
+// channels into the module's weight layout through chan_map.
+#include "warp_common.h"
+
+#include <type_traits>
+
+namespace mvbev {
+namespace bwd {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int NWV = 8;        // waves per workgroup: 4 (output channels) x 2 (input channels)
+constexpr int NTH = 64 * NWV;
+constexpr int MT = 128;       // output channels per workgroup
+constexpr int NT = 64;        // input channels per workgroup
+constexpr int PX = 32;        // pixels per chunk (one row segment) = 2 K-steps
+constexpr int AP = PX + 8;    // bf16 per A-image row (80 B)
+
+struct WArgs {
+  const void* x;
+  const float* dy;
+  float* ws;
+  int64_t group_stride, batch_stride;
+  int group, K, Cout, B, H, W;
+  int segs, nchunks, P, n_ct, n_kt, ntiles;
+  bool vec_dy;  // W % 4 == 0 and dy 16-B aligned: dy rows as 16-B loads
+};
+
+struct SplitIn {};
+
+__device__ inline bf16x8 tr_read8(const __bf16* p) {
+  // two transposed 4x16 reads: pixels 0..3 then 4..7 of the lane's 8-pixel K run
+  typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(p));
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(p + 4 * 32));
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const v8i16 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+__device__ inline void split4(const floatx4 v, u32x2& hi, u32x2& lo) {
+  bf16x4 h, l;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const __bf16 t = (__bf16)v[j];
+    h[j] = t;
+    l[j] = (__bf16)(v[j] - (float)t);
+  }
+  hi = __builtin_bit_cast(u32x2, h);
+  lo = __builtin_bit_cast(u32x2, l);
+}
+
+template <typename TIn, int DIL>
+__global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const WArgs a) {
+  constexpr int XW = PX + 2 * DIL;       // window columns
+  constexpr int BPIX = 3 * XW;           // window pixels (3 tap rows)
+  constexpr int BIMG = BPIX * 32;        // bf16 per (channel half, part) image
+  constexpr int AIMG = MT * AP;          // bf16 per A part
+  constexpr int BUF = 2 * AIMG + 4 * BIMG;
+  constexpr int BENT = BPIX * 8;         // staging entries (window pixel, 8-channel group)
+  constexpr int BPT = (BENT + NTH - 1) / NTH;
+  constexpr bool SPLIT = std::is_same<TIn, SplitIn>::value;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, kh = lane >> 5;
+  // (partition, tile) with partitions slowest, dealt to the XCDs in contiguous ranges: the
+  // workgroups that run together on one XCD sweep the same pixels (dy / x lines shared in L2)
+  const int lb = xcd_remap(blockIdx.x, a.P * a.ntiles);
+  const int p = lb / a.ntiles, tile = lb - p * a.ntiles;
+  const int ct = tile % a.n_ct, kt = tile / a.n_ct;
+  const int c0 = (int)((int64_t)a.nchunks * p / a.P);
+  const int c1 = (int)((int64_t)a.nchunks * (p + 1) / a.P);
+  const int W = a.W, H = a.H;
+  const int64_t plane = (int64_t)H * W;
+
+  floatx4 areg[2];
+  u32x4 bsp[BPT][SPLIT ? 2 : 1];
+  float bfl[BPT][SPLIT ? 1 : 8];
+  bool bok[BPT];
+
+  auto load = [&](int c) __attribute__((always_inline)) {
+    const int R = c / a.segs, seg = c - R * a.segs;
+    const int b = R / H, y = R - b * H;
+    const int x0 = seg * PX;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int co = ct * MT + (tid >> 3) + 64 * i;
+      const int px = x0 + 4 * (tid & 7);
+      const float* src = a.dy + (((int64_t)b * a.Cout + co) * H + y) * W;
+      if (a.vec_dy) {
+        areg[i] = px < W ? *reinterpret_cast<const floatx4*>(src + px) : floatx4{0.f, 0.f, 0.f, 0.f};
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) areg[i][j] = px + j < W ? src[px + j] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int e = tid + NTH * i;
+      const int g8 = e / BPIX, pix = e - g8 * BPIX;
+      const int r = pix / XW, cc = pix - r * XW;
+      const int gy = y + (r - 1) * DIL, gx = x0 - DIL + cc;
+      const int k0 = kt * NT + g8 * 8;
+      const bool ok = e < BENT && gy >= 0 && gy < H && gx >= 0 && gx < W && k0 < a.K;
+      bok[i] = ok;
+      int64_t base = 0;
+      if (ok) {
+        const int g_ = k0 / a.group;
+        base = (int64_t)b * a.batch_stride + g_ * a.group_stride + (int64_t)(k0 - g_ * a.group) * plane;
+      }
+      const int64_t pofs = ok ? (int64_t)gy * W + gx : 0;
+      if constexpr (SPLIT) {
+        const u32x4* xc = static_cast<const u32x4*>(a.x) + base / 4 + 2 * pofs;
+        bsp[i][0] = xc[0];
+        bsp[i][1] = xc[1];
+      } else {
+        const float* xc = static_cast<const float*>(a.x) + base + pofs;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bfl[i][j] = xc[j * plane];
+      }
+    }
+  };
+
+  auto store = [&](int bb) __attribute__((always_inline)) {
+    __bf16* L = lds + bb * BUF;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (tid >> 3) + 64 * i, q = tid & 7;
+      u32x2 hi, lo;
+      split4(areg[i], hi, lo);
+      *reinterpret_cast<u32x2*>(L + row * AP + 4 * q) = hi;
+      *reinterpret_cast<u32x2*>(L + AIMG + row * AP + 4 * q) = lo;
+    }
+#pragma unroll
+    for (int i = 0; i < BPT; ++i) {
+      const int e = tid + NTH * i;
+      if (BENT % NTH != 0 && e >= BENT) continue;
+      const int g8 = e / BPIX, pix = e - g8 * BPIX;
+      __bf16* Bh = L + 2 * AIMG + ((g8 >> 2) * 2) * BIMG + pix * 32 + (g8 & 3) * 8;
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      if constexpr (SPLIT) {
+        *reinterpret_cast<u32x4*>(Bh) = bok[i] ? bsp[i][0] : z;
+        *reinterpret_cast<u32x4*>(Bh + BIMG) = bok[i] ? bsp[i][1] : z;
+      } else {
+        bf16x8 hi, lo;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = bok[i] ? bfl[i][j] : 0.f;
+          const __bf16 t = (__bf16)v;
+          hi[j] = t;
+          lo[j] = (__bf16)(v - (float)t);
+        }
+        *reinterpret_cast<u32x4*>(Bh) = __builtin_bit_cast(u32x4, hi);
+        *reinterpret_cast<u32x4*>(Bh + BIMG) = __builtin_bit_cast(u32x4, lo);
+      }
+    }
+  };
+
+  const int cw = wave & 3, cb = wave >> 2;
+  const int gi = (lane >> 4) & 1, li = lane & 15;
+  // transposed-read address of the lane: pixel 8kh + (li>>2) (+4 in the second read),
+  // channels 16gi + 4(li&3) .. +3 of the wave's 32-channel half
+  const int tr0 = (8 * kh + (li >> 2)) * 32 + 16 * gi + 4 * (li & 3);
+  floatx16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = floatx16{0};
+
+  auto compute = [&](int bb) __attribute__((always_inline)) {
+    const __bf16* L = lds + bb * BUF;
+    const __bf16* Ah = L + (32 * cw + l32) * AP + 8 * kh;
+    const __bf16* Bh = L + 2 * AIMG + (cb * 2) * BIMG + tr0;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(Ah + 16 * s);
+      const bf16x8 alo = *reinterpret_cast<const bf16x8*>(Ah + AIMG + 16 * s);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int off = ((t / 3) * XW + 16 * s + (t % 3) * DIL) * 32;
+        const bf16x8 bhi = tr_read8(Bh + off);
+        const bf16x8 blo = tr_read8(Bh + BIMG + off);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, blo, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc[t], 0, 0, 0);
+      }
+    }
+  };
+
+  if (c0 < c1) {
+    load(c0);
+    store(0);
+    if (c0 + 1 < c1) load(c0 + 1);
+    __syncthreads();
+    int i = 0;
+    for (int c = c0; c < c1; ++c, ++i) {
+      compute(i & 1);
+      if (c + 1 < c1) store((i + 1) & 1);
+      if (c + 2 < c1) load(c + 2);
+      __syncthreads();
+    }
+  }
+
+  // partial sums of this partition: ws[p][tap][co][k] (lanes along k: coalesced)
+  const int k = kt * NT + 32 * cb + l32;
+  if (k < a.K) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = ct * MT + 32 * cw + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        a.ws[(((int64_t)p * 9 + t) * a.Cout + co) * a.K + k] = acc[t][r];
+      }
+  }
+}
+
+// dw[co][map(k)][t] = sum_p ws[p][t][co][k]  (partition order: deterministic)
+__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int P, int Cout, int K,
+                                    const int32_t* __restrict__ chan_map, int Cin_w, float* __restrict__ dw) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= (int64_t)Cout * K) return;
+  const int co = (int)(i / K), k = (int)(i - (int64_t)co * K);
+  const int cm = chan_map ? chan_map[k] : k;
+  if (cm < 0 || cm >= Cin_w) return;
+  const int64_t pstride = (int64_t)9 * Cout * K;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    float s = 0.f;
+    const float* src = ws + ((int64_t)t * Cout + co) * K + k;
+    for (int q = 0; q < P; ++q) s += src[q * pstride];
+    dw[((int64_t)co * Cin_w + cm) * 9 + t] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// block-wide sum of NV values per thread (256 threads), result valid in thread 0
+template <int NV>
+__device__ inline void block_sum(float (&v)[NV], float* red /* LDS [4][NV] */) {
+#pragma unroll
+  for (int j = 0; j < NV; ++j)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v[j] += __shfl_xor(v[j], o);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0)
+#pragma unroll
+    for (int j = 0; j < NV; ++j) red[wave * NV + j] = v[j];
+  __syncthreads();
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int j = 0; j < NV; ++j) v[j] = red[j] + red[NV + j] + red[2 * NV + j] + red[3 * NV + j];
+}
+
+// db[co] = sum dy[b][co][:]; with dw, the two coord channels (create_coord_map,
+// persp_trans_detector.py:103-112, channels coord_ch and coord_ch + 1 of the conv input):
+// dw[co][coord_ch + j][t] = sum_p dy[co][p] * coord_j(p + s_t), zero outside the grid.
+__global__ __launch_bounds__(256) void bias_coord_grad_kernel(const float* __restrict__ dy, int B, int Cout,
+                                                              int H, int W, int dil, float* db, float* dw,
+                                                              int Cin_w, int coord_ch) {
+  __shared__ float red[4 * 19];
+  const int co = blockIdx.x;
+  float v[19];
+#pragma unroll
+  for (int j = 0; j < 19; ++j) v[j] = 0.f;
+  const int HW = H * W;
+  for (int b = 0; b < B; ++b) {
+    const float* g = dy + ((int64_t)b * Cout + co) * HW;
+    for (int q = threadIdx.x; q < HW; q += 256) {
+      const float gv = g[q];
+      v[0] += gv;
+      if (dw) {
+        const int y = q / W, x = q - y * W;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int yy = y + (t / 3 - 1) * dil, xx = x + (t % 3 - 1) * dil;
+          if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+            const float cx = (float)((double)xx / (double)(W - 1) * 2.0 - 1.0);
+            const float cy = (float)((double)yy / (double)(H - 1) * 2.0 - 1.0);
+            v[1 + t] += gv * cx;
+            v[10 + t] += gv * cy;
+          }
+        }
+      }
+    }
+  }
+  block_sum<19>(v, red);
+  if (threadIdx.x == 0) {
+    if (db) db[co] = v[0];
+    if (dw)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        dw[((int64_t)co * Cin_w + coord_ch) * 9 + t] = v[1 + t];
+        dw[((int64_t)co * Cin_w + coord_ch + 1) * 9 + t] = v[10 + t];
+      }
+  }
+}
+
+// torch threshold_backward(grad, relu_output, 0): grad where the ReLU output > 0, else 0
+__global__ void relu_backward_kernel(float* __restrict__ dy, const float* __restrict__ y, int64_t n) {
+  const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 4;
+  if (i + 4 <= n) {
+    floatx4 g = *reinterpret_cast<const floatx4*>(dy + i);
+    const floatx4 v = *reinterpret_cast<const floatx4*>(y + i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) g[j] = v[j] > 0.f ? g[j] : 0.f;
+    *reinterpret_cast<floatx4*>(dy + i) = g;
+  } else {
+    for (int64_t j = i; j < n; ++j) dy[j] = y[j] > 0.f ? dy[j] : 0.f;
+  }
+}
+
+// conv3 (Cout = 1, no bias) data gradient, times conv2's ReLU mask when relu_mask:
+// dx[b][c][y][x] = sum_t w[c][t] * dmap[b][y - (ky-1)d][x - (kx-1)d]
+constexpr int kCout1Cpb = 32;  // channels per block
+__global__ __launch_bounds__(256) void cout1_dgrad_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ dmap, int C, int H, int W,
+                                                          int dil, int relu_mask, float* __restrict__ dx) {
+  const int HW = H * W;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  const int b = blockIdx.z;
+  if (q >= HW) return;
+  const int y = q / W, xx = q - y * W;
+  float dm[9];
+  const float* d = dmap + (int64_t)b * HW;
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int yy = y - (t / 3 - 1) * dil, xc = xx - (t % 3 - 1) * dil;
+    dm[t] = (yy >= 0 && yy < H && xc >= 0 && xc < W) ? d[yy * W + xc] : 0.f;
+  }
+  const int cbeg = blockIdx.y * kCout1Cpb, cend = min(C, cbeg + kCout1Cpb);
+  for (int c = cbeg; c < cend; ++c) {
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) s += w[c * 9 + t] * dm[t];
+    const int64_t o = ((int64_t)b * C + c) * HW + q;
+    dx[o] = (!relu_mask || x[o] > 0.f) ? s : 0.f;
+  }
+}
+
+// conv3 weight gradient: dw[c][t] = sum_b sum_q x[b][c][q] * dmap[b][q - s_t]
+__global__ __launch_bounds__(256) void cout1_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dmap,
+                                                          int B, int C, int H, int W, int dil, float* __restrict__ dw) {
+  __shared__ float red[4 * 9];
+  const int c = blockIdx.x;
+  const int HW = H * W;
+  float v[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) v[t] = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float* xc = x + ((int64_t)b * C + c) * HW;
+    const float* d = dmap + (int64_t)b * HW;
+    for (int q = threadIdx.x; q < HW; q += 256) {
+      const float xv = xc[q];
+      const int y = q / W, xx = q - y * W;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int yy = y - (t / 3 - 1) * dil, xs = xx - (t % 3 - 1) * dil;
+        if (yy >= 0 && yy < H && xs >= 0 && xs < W) v[t] += xv * d[yy * W + xs];
+      }
+    }
+  }
+  block_sum<9>(v, red);
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) dw[c * 9 + t] = v[t];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Warp adjoint: per output pixel (one thread) the forward's coordinates, corners and weights,
+// then for every channel of the block's slice 4 atomic adds into the source gradient.  No
+// gradient flows from a pixel whose sample point is outside (zero padding) or non-finite.
+// WarpView here: src = grad_out ([B][C][Ho][Wo], strides sB..sW), dst = grad_src (dB, dC, dH, 1).
+__global__ __launch_bounds__(256) void warp_backward_kernel(const WarpArgs a) {
+  const int lb = xcd_remap(blockIdx.x, a.nwg);
+  const int tile = lb % a.tiles;
+  const int chunk = (lb / a.tiles) % a.chunks;
+  const int bv = lb / (a.tiles * a.chunks);
+  const int view = bv % a.nviews;
+  const int b = bv / a.nviews;
+  const WarpView& vw = a.v[view];
+  const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
+  constexpr int WC = 64 / kWarpWR, WAVES_X = kWarpTW / WC;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int v = ty * kWarpTH + (wave / WAVES_X) * kWarpWR + lane / WC;
+  const int u = tx * kWarpTW + (wave % WAVES_X) * WC + lane % WC;
+  if (v >= a.Ho || u >= a.Wo) return;
+  const int H = a.H, W = a.W;
+  float m[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) m[i] = vw.m[i];
+  const WarpCoord wc = warp_coord(m, u, v, a.Ho, a.Wo, H, W);
+  if (!wc.inside) return;
+  const float ix = wc.ix, iy = wc.iy;
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  const int x0 = (int)fx0, y0 = (int)fy0;
+  const float fx1 = fx0 + 1.f, fy1 = fy0 + 1.f;
+  const float w_nw = (fx1 - ix) * (fy1 - iy);
+  const float w_ne = (ix - fx0) * (fy1 - iy);
+  const float w_sw = (fx1 - ix) * (iy - fy0);
+  const float w_se = (ix - fx0) * (iy - fy0);
+  const bool vx0 = x0 >= 0, vx1 = x0 + 1 <= W - 1, vy0 = y0 >= 0, vy1 = y0 + 1 <= H - 1;
+  const bool ok_nw = vx0 && vy0, ok_ne = vx1 && vy0, ok_sw = vx0 && vy1, ok_se = vx1 && vy1;
+  const int64_t o_nw = (int64_t)y0 * vw.dH + x0;
+  const int64_t o_sw = o_nw + vw.dH;
+  const float* go = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB + (int64_t)v * vw.sH +
+                    (int64_t)u * vw.sW;
+  float* gs = static_cast<float*>(vw.dst) + (int64_t)b * vw.dB;
+  const int c_begin = chunk * kWarpCPB;
+  const int c_end = min(a.C, c_begin + kWarpCPB);
+  constexpr int U = 4;
+  int c = c_begin;
+  auto scatter = [&](int ch, float g) __attribute__((always_inline)) {
+    if (g == 0.f) return;  // adds nothing (a NaN/inf gradient still propagates)
+    float* pc = gs + (int64_t)ch * vw.dC;
+    if (ok_nw) unsafeAtomicAdd(pc + o_nw, w_nw * g);
+    if (ok_ne) unsafeAtomicAdd(pc + o_nw + 1, w_ne * g);
+    if (ok_sw) unsafeAtomicAdd(pc + o_sw, w_sw * g);
+    if (ok_se) unsafeAtomicAdd(pc + o_sw + 1, w_se * g);
+  };
+  for (; c + U <= c_end; c += U) {
+    float g[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) g[k] = go[(int64_t)(c + k) * vw.sC];
+#pragma unroll
+    for (int k = 0; k < U; ++k) scatter(c + k, g[k]);
+  }
+  for (; c < c_end; ++c) scatter(c, go[(int64_t)c * vw.sC]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// wgrad launch geometry
+static int cu_count() {
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return n;
+}
+
+// Pixel partitions: one workgroup per CU fits (LDS), so P minimises the rounds per unit of
+// work, ceil(tiles * P / CUs) / P, with a small per-partition cost (workspace + reduce).
+static int wgrad_partitions(int64_t tiles, int64_t nchunks) {
+  const int G = std::max(cu_count(), 1);
+  int best = 1;
+  double best_t = 1e30;
+  for (int P = 1; P <= 64 && P <= nchunks; ++P) {
+    const double t = (double)ceil_div(tiles * P, G) / P + 0.004 * P;
+    if (t < best_t) best_t = t, best = P;
+  }
+  return best;
+}
+
+struct WGeo {
+  int64_t tiles, nchunks;
+  int P;
+};
+static WGeo wgrad_geo(const mvbev_conv_desc* d, int64_t Cout) {
+  WGeo g;
+  g.tiles = (Cout / MT) * ceil_div(d->K, NT);
+  g.nchunks = d->B * d->H * ceil_div(d->W, PX);
+  g.P = wgrad_partitions(g.tiles, g.nchunks);
+  return g;
+}
+
+}  // namespace bwd
+}  // namespace mvbev
+
+extern "C" {
+
+size_t mvbev_conv3x3_wgrad_workspace_bytes(const mvbev_conv_desc* desc, int64_t Cout) {
+  using namespace mvbev::bwd;
+  if (!desc || Cout <= 0 || desc->K <= 0 || desc->H <= 0 || desc->W <= 0 || desc->B <= 0) return 0;
+  const WGeo g = wgrad_geo(desc, Cout);
+  return (size_t)g.P * 9 * (size_t)Cout * (size_t)desc->K * sizeof(float);
+}
+
+int mvbev_conv3x3_wgrad_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* d, const float* dy,
+                               int64_t Cout, int dilation, const int32_t* chan_map, int64_t Cin_w,
+                               float* dw, void* workspace, size_t workspace_bytes, void* stream) {
+  using namespace mvbev;
+  using namespace mvbev::bwd;
+  if (!x || !d || !dy || !dw || !workspace) return MVBEV_ERR_NULL;
+  if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || Cin_w <= 0 || d->group <= 0)
+    return MVBEV_ERR_RANK;
+  if (Cout % MT != 0 || d->K % 8 != 0 || d->group % 8 != 0 || d->K % d->group != 0) return MVBEV_ERR_SHAPE;
+  if (d->in_row0 != 0 || d->in_rows != d->H || d->out_row0 != 0 || d->out_rows != d->H) return MVBEV_ERR_SHAPE;
+  if (!chan_map && d->K > Cin_w) return MVBEV_ERR_SHAPE;
+  if (d->H * d->W > (int64_t)INT32_MAX / 2 || d->B * d->H * ceil_div(d->W, PX) > INT32_MAX) return MVBEV_ERR_SHAPE;
+  if (x_layout != MVBEV_LAYOUT_F32 && x_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;
+  const WGeo g = wgrad_geo(d, Cout);
+  const size_t need = (size_t)g.P * 9 * (size_t)Cout * (size_t)d->K * sizeof(float);
+  if (workspace_bytes < need) return MVBEV_ERR_SHAPE;
+  WArgs a;
+  a.x = x; a.dy = dy; a.ws = static_cast<float*>(workspace);
+  a.group_stride = d->group_stride; a.batch_stride = d->batch_stride;
+  a.group = (int)d->group; a.K = (int)d->K; a.Cout = (int)Cout; a.B = (int)d->B;
+  a.H = (int)d->H; a.W = (int)d->W;
+  a.segs = (int)ceil_div(d->W, PX); a.nchunks = (int)g.nchunks; a.P = g.P;
+  a.n_ct = (int)(Cout / MT); a.n_kt = (int)ceil_div(d->K, NT); a.ntiles = (int)g.tiles;
+  a.vec_dy = (d->W % 4 == 0) && ((reinterpret_cast<uintptr_t>(dy) & 15) == 0);
+  hipStream_t s = as_stream(stream);
+  const dim3 grid((unsigned)(g.P * g.tiles)), block(NTH);
+  const bool split = x_layout == MVBEV_LAYOUT_SPLIT_BF16;
+  if (dilation == 1) {
+    if (split) hipLaunchKernelGGL((wgrad_kernel<SplitIn, 1>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((wgrad_kernel<float, 1>), grid, block, 0, s, a);
+  } else if (dilation == 2) {
+    if (split) hipLaunchKernelGGL((wgrad_kernel<SplitIn, 2>), grid, block, 0, s, a);
+    else hipLaunchKernelGGL((wgrad_kernel<float, 2>), grid, block, 0, s, a);
+  } else {
+    return MVBEV_ERR_DILATION;
+  }
+  MVBEV_CHECK_LAUNCH();
+  const int64_t n = Cout * d->K;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
+                     static_cast<const float*>(workspace), g.P, (int)Cout, (int)d->K, chan_map, (int)Cin_w, dw);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+int mvbev_conv3x3_bias_coord_grad_f32(const float* dy, int64_t B, int64_t Cout, int64_t H, int64_t W,
+                                      int dilation, float* db, float* dw, int64_t Cin_w, int64_t coord_ch,
+                                      void* stream) {
+  using namespace mvbev;
+  if (!dy || (!db && !dw)) return MVBEV_ERR_NULL;
+  if (B <= 0 || Cout <= 0 || H <= 0 || W <= 0) return MVBEV_ERR_RANK;
+  if (H * W > INT32_MAX || Cout > 65535 * 16) return MVBEV_ERR_SHAPE;
+  if (dw && (coord_ch < 0 || coord_ch + 2 > Cin_w)) return MVBEV_ERR_SHAPE;
+  if (dilation < 1) return MVBEV_ERR_DILATION;
+  hipLaunchKernelGGL(bwd::bias_coord_grad_kernel, dim3((unsigned)Cout), dim3(256), 0, as_stream(stream), dy,
+                     (int)B, (int)Cout, (int)H, (int)W, dilation, db, dw, (int)Cin_w, (int)coord_ch);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+int mvbev_relu_backward_f32(float* dy, const float* y, int64_t n, void* stream) {
+  using namespace mvbev;
+  if (!dy || !y) return MVBEV_ERR_NULL;
+  if (n <= 0) return MVBEV_ERR_RANK;
+  if (((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(y)) & 15) != 0) return MVBEV_ERR_ALIGN;
+  hipLaunchKernelGGL(bwd::relu_backward_kernel, dim3((unsigned)ceil_div(ceil_div(n, 4), 256)), dim3(256), 0,
+                     as_stream(stream), dy, y, n);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+int mvbev_conv3x3_cout1_backward_f32(const float* x, const float* w, const float* dmap, int64_t B, int64_t C,
+                                     int64_t H, int64_t W, int dilation, int relu_mask, float* dx, float* dw,
+                                     void* stream) {
+  using namespace mvbev;
+  if (!x || !w || !dmap || (!dx && !dw)) return MVBEV_ERR_NULL;
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return MVBEV_ERR_RANK;
+  if (H * W > INT32_MAX || B > 65535) return MVBEV_ERR_SHAPE;
+  if (dilation < 1) return MVBEV_ERR_DILATION;
+  hipStream_t s = as_stream(stream);
+  if (dx) {
+    const dim3 grid((unsigned)ceil_div(H * W, 256), (unsigned)ceil_div(C, bwd::kCout1Cpb), (unsigned)B);
+    hipLaunchKernelGGL(bwd::cout1_dgrad_kernel, grid, dim3(256), 0, s, x, w, dmap, (int)C, (int)H, (int)W,
+                       dilation, relu_mask, dx);
+    MVBEV_CHECK_LAUNCH();
+  }
+  if (dw) {
+    hipLaunchKernelGGL(bwd::cout1_wgrad_kernel, dim3((unsigned)C), dim3(256), 0, s, x, dmap, (int)B, (int)C,
+                       (int)H, (int)W, dilation, dw);
+    MVBEV_CHECK_LAUNCH();
+  }
+  return MVBEV_OK;
+}
+
+int mvbev_warp_views_backward_f32(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t H,
+                                  int64_t W, int64_t Ho, int64_t Wo, void* stream) {
+  using namespace mvbev;
+  if (!views) return MVBEV_ERR_NULL;
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 || nviews <= 0) return MVBEV_ERR_RANK;
+  if (nviews > kWarpMaxViews || C > INT32_MAX || H > INT32_MAX / 2 || W > INT32_MAX / 2 ||
+      Ho > INT32_MAX / 2 || Wo > INT32_MAX / 2)
+    return MVBEV_ERR_SHAPE;
+  WarpArgs a = {};
+  for (int i = 0; i < nviews; ++i) {
+    const mvbev_warp_view& v = views[i];
+    if (!v.src || !v.dst) return MVBEV_ERR_NULL;
+    if (v.dst_strides[3] != 1) return MVBEV_ERR_STRIDE;
+    a.v[i] = WarpView{v.src, v.src_strides[0], v.src_strides[1], v.src_strides[2], v.src_strides[3],
+                      v.dst, v.dst_strides[0], v.dst_strides[1], v.dst_strides[2], nullptr, {}};
+    for (int j = 0; j < 9; ++j) a.v[i].m[j] = v.m[j];
+  }
+  a.nviews = nviews;
+  a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
+  a.tiles_x = (int)ceil_div(Wo, kWarpTW);
+  a.tiles = a.tiles_x * (int)ceil_div(Ho, kWarpTH);
+  a.chunks = (int)ceil_div(C, kWarpCPB);
+  const int64_t nwg = (int64_t)a.tiles * a.chunks * B * nviews;
+  if (nwg > INT32_MAX) return MVBEV_ERR_SHAPE;
+  a.nwg = (int)nwg;
+  hipLaunchKernelGGL(bwd::warp_backward_kernel, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+}  // extern "C"

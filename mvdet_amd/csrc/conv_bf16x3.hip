@@ -67,6 +67,35 @@ __global__ void pack_kernel(const float* __restrict__ w, __bf16* __restrict__ ou
   }
 }
 
+// Data-gradient packing (conv backward): the dgrad of a stride-1 3x3 conv with padding =
+// dilation is the same conv over dy with w'[k][co][t] = w[co][k][8 - t].  Packed-conv output
+// channel o = forward input channel chan_map[o] (-1 or o >= K_map: zero), packed input channel
+// k = forward output channel k; same layout as pack_kernel.
+__global__ void pack_dgrad_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int Cout_p,
+                                  int Cf_out, int Cf_in, const int32_t* __restrict__ chan_map, int K_map,
+                                  int K_pad) {
+  const int n_cot = Cout_p / BN;
+  const int64_t total = (int64_t)(K_pad / KC) * n_cot * 2 * WPART;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i;
+    const int j = r % SB; r /= SB;
+    const int co = r % BN; r /= BN;
+    const int sub = r % 2; r /= 2;
+    const int tap = r % NKB; r /= NKB;
+    const int part = r % 2; r /= 2;
+    const int cot = r % n_cot;
+    const int chunk = (int)(r / n_cot);
+    const int k = chunk * KC + sub * SB + j;
+    const int o = cot * BN + co;
+    int ci = o < K_map ? (chan_map ? chan_map[o] : o) : -1;
+    if (ci >= Cf_in) ci = -1;
+    const float v = (ci >= 0 && k < Cf_out) ? w[((int64_t)k * Cf_in + ci) * 9 + (NKB - 1 - tap)] : 0.f;
+    const __bf16 hi = (__bf16)v;
+    out[i] = part ? (__bf16)(v - (float)hi) : hi;
+  }
+}
+
 struct Args {
   const void* x;
   const u32x4* wp;
@@ -648,6 +677,23 @@ int mvbev_pack_conv3x3_weight_bf16x3(const float* w, int64_t Cout, int64_t Cin_w
   hipLaunchKernelGGL(b3::pack_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), w,
                      static_cast<__bf16*>(w_packed), (int)Cout, (int)Cin_w, chan_map, (int)K,
                      (int)k_pad);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+int mvbev_pack_conv3x3_dgrad_bf16x3(const float* w, int64_t Cout_w, int64_t Cin_w, const int32_t* chan_map,
+                                    int64_t K_out, void* w_packed, void* stream) {
+  using namespace mvbev;
+  if (!w || !w_packed) return MVBEV_ERR_NULL;
+  if (Cout_w <= 0 || Cin_w <= 0 || K_out <= 0) return MVBEV_ERR_RANK;
+  if (!chan_map && K_out > Cin_w) return MVBEV_ERR_SHAPE;
+  const int64_t cout_p = round_up(K_out, b3::BN);
+  const int64_t k_pad = round_up(Cout_w, b3::KC);
+  const int64_t total = (int64_t)mvbev_conv3x3_packed_bytes_bf16x3(cout_p, Cout_w) / 2;
+  const int blocks = (int)std::min<int64_t>(ceil_div(total, 256), 8192);
+  hipLaunchKernelGGL(b3::pack_dgrad_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), w,
+                     static_cast<__bf16*>(w_packed), (int)cout_p, (int)Cout_w, (int)Cin_w, chan_map,
+                     (int)K_out, (int)k_pad);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }

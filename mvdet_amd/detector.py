@@ -19,9 +19,10 @@ HIP kernels of ``libmvbev.so`` through ``ProjectFuse``:
   fp32-input MFMA), conv3 a dot-product kernel;
 * the same-size final interpolate (an exact identity) is elided.
 
-Training (autograd through the hot path, ``trainer.py:38-49``) is not yet native
-(SURVEY §8(f) row 2): when grad is required the hot path runs as stock torch
-GPU ops (``grid_sample`` + ``conv2d``) so training semantics are unchanged.
+Training (autograd through the hot path, ``trainer.py:38-49``):
+when grad is required the upsample stays a torch op (its autograd), and warp + concat +
+fusion run as ``autograd.ProjectFuseFunction`` — HIP forward, HIP backward (warp adjoint,
+conv data/weight/bias gradients).  There is no stock-torch fallback for the hot path.
 The library is loaded at construction on a GPU, so a missing build fails there.
 """
 from __future__ import annotations
@@ -31,6 +32,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _native
+from . import autograd as native_autograd
 from .backbone import build_backbone
 from .geometry import coord_map as make_coord_map
 from .geometry import projection_matrices, upsample_shape
@@ -76,22 +78,19 @@ class PerspTransDetector(nn.Module):
         for cam in range(self.num_cam):
             feat = self.base_pt1(imgs[:, cam].to(dev))
             feat = self.base_pt2(feat)
-            if training:  # :65-69 as the reference, autograd through stock torch ops
-                feat = F.interpolate(feat, self.upsample_shape, mode="bilinear")
-                imgs_result.append(self.img_classifier(feat))
-                world_features.append(self._torch_warp(cam, feat))
-            else:
-                # the 3x upsample (:65) happens inside the fused warp below; the image head
-                # runs its first 1x1 conv before upsampling (it commutes with the bilinear
-                # upsample: per-pixel affine, weights summing to 1) on 64 instead of 512 channels
+            # the image head runs its first 1x1 conv before upsampling (it commutes with the
+            # bilinear upsample: per-pixel affine, weights summing to 1) on 64 instead of 512
+            # channels
+            imgs_result.append(self._img_head_lowres(feat))
+            if training:  # :65 as a torch op (its autograd); warp + fusion below are native
+                world_features.append(F.interpolate(feat, self.upsample_shape, mode="bilinear"))
+            else:  # the 3x upsample (:65) happens inside the fused warp below
                 low.append(feat.contiguous())
-                imgs_result.append(self._img_head_lowres(feat))
             if visualize:
-                up = feat if training else F.interpolate(feat, self.upsample_shape, mode="bilinear")
+                up = world_features[-1] if training else F.interpolate(feat, self.upsample_shape, mode="bilinear")
                 self._show(torch.norm(up[0].detach(), dim=0))
-        if training:
-            cmap = self.coord_map.to(dev).repeat([B, 1, 1, 1])
-            map_result = self.map_classifier(torch.cat(world_features + [cmap], dim=1))
+        if training:  # a5-a9 forward and backward on the HIP kernels (autograd.py)
+            map_result = native_autograd.project_fuse(self.engine, world_features, self.map_classifier)
         else:
             self.engine.warp_views_upsampled(ws, list(range(self.num_cam)), low)  # a4 + a5 + a6
             map_result = self.engine.fuse(ws, self.map_classifier)
@@ -108,20 +107,6 @@ class PerspTransDetector(nn.Module):
             g = head[0](feat)
             return head[2](F.relu(F.interpolate(g, self.upsample_shape, mode="bilinear")))
         return head(F.interpolate(feat, self.upsample_shape, mode="bilinear"))
-
-    def _torch_warp(self, cam: int, feat: torch.Tensor) -> torch.Tensor:
-        """Autograd-capable warp (kornia steps 3-6 in stock torch GPU ops)."""
-        B = feat.shape[0]
-        ho, wo = self.reducedgrid_shape
-        m = self.engine.m_norm_cpu[cam].to(feat.device)
-        xs = (torch.linspace(0, wo - 1, wo, device=feat.device) / (wo - 1) - 0.5) * 2
-        ys = (torch.linspace(0, ho - 1, ho, device=feat.device) / (ho - 1) - 0.5) * 2
-        gy, gx = torch.meshgrid(ys, xs, indexing="ij")
-        pts = torch.stack([gx, gy, torch.ones_like(gx)], -1) @ m.T
-        z = pts[..., 2:]
-        scale = torch.where(z.abs() > 1e-8, 1.0 / (z + 1e-8), torch.ones_like(z))
-        grid = (scale * pts[..., :2]).unsqueeze(0).expand(B, ho, wo, 2)
-        return F.grid_sample(feat, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
 
     @staticmethod
     def _show(img):

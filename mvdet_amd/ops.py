@@ -447,3 +447,192 @@ def conv3x3_cout1(x: torch.Tensor, weight: torch.Tensor, dilation: int, H: Optio
                                                 w.data_ptr(), int(dilation), out.data_ptr(), _stream(x))
     _native.check(st, "mvbev_conv3x3_cout1_f32")
     return out
+
+
+# ----------------------------------------------------------------------------------------------
+# backward: the adjoints autograd needs to train through the hot path
+
+def warp_views_backward(grad_outs, m_norms, grad_srcs) -> None:
+    """Adjoint of ``warp_views_into`` (fp32): ``grad_srcs[i]`` [B,C,H,W] (innermost stride 1)
+    ACCUMULATES w_corner * ``grad_outs[i]`` [B,C,Ho,Wo] for every in-bounds bilinear corner of
+    every finite inside sample (grid_sample's backward under kornia.warp_perspective,
+    ``persp_trans_detector.py:69``).  ``m_norms[i]``: host [3,3] src_norm <- dst_norm."""
+    n = len(grad_outs)
+    if n == 0:
+        return
+    if not (len(m_norms) == n == len(grad_srcs)) or n > 16:
+        raise ValueError("need 1..16 matching grad_outs / m_norms / grad_srcs")
+    _require_cuda(*grad_outs, *grad_srcs)
+    B, C, Ho, Wo = grad_outs[0].shape
+    _, _, H, W = grad_srcs[0].shape
+    arr = (_native.WarpView * n)()
+    for i, (g, m, d) in enumerate(zip(grad_outs, m_norms, grad_srcs)):
+        if tuple(g.shape) != (B, C, Ho, Wo) or tuple(d.shape) != (B, C, H, W):
+            raise ValueError(f"all views must share shapes: grad_out {tuple(g.shape)} grad_src {tuple(d.shape)}")
+        if g.dtype != torch.float32 or d.dtype != torch.float32:
+            raise TypeError("the warp backward is fp32")
+        if d.stride(3) != 1:
+            raise ValueError("grad_src needs contiguous rows (innermost stride 1)")
+        mm = torch.as_tensor(m, dtype=torch.float32).reshape(9).tolist()
+        arr[i] = _native.WarpView(g.data_ptr(), (ctypes.c_int64 * 4)(*g.stride()), d.data_ptr(),
+                                  (ctypes.c_int64 * 4)(*d.stride()), (ctypes.c_float * 9)(*mm))
+    st = _native.load().mvbev_warp_views_backward_f32(arr, n, B, C, H, W, Ho, Wo, _stream(grad_srcs[0]))
+    _native.check(st, "mvbev_warp_views_backward_f32")
+
+
+class PackedDgrad3x3:
+    """bf16x3-packed weights of a 3x3 conv's DATA gradient (transposed, flipped taps:
+    ``mvbev_pack_conv3x3_dgrad_bf16x3``).  Output channel o of the dgrad conv = forward input
+    channel ``chan_map[o]`` (None: identity over ``k_out`` channels).  Re-packed only when the
+    parameter changes."""
+
+    def __init__(self, k_out: int, chan_map: Optional[Sequence[int]] = None):
+        self.k_out = int(k_out)
+        if chan_map is not None and len(chan_map) != self.k_out:
+            raise ValueError("chan_map must have k_out entries")
+        self.chan_map = None if chan_map is None else [int(c) for c in chan_map]
+        self.cout_p = -(-self.k_out // BN) * BN   # dgrad conv output channels (padded)
+        self._key = None
+        self.packed: Optional[torch.Tensor] = None
+        self._map_dev: Optional[torch.Tensor] = None
+
+    def get(self, weight: torch.Tensor) -> torch.Tensor:
+        _require_cuda(weight)
+        lib = _native.load()
+        key = (weight.data_ptr(), weight._version, tuple(weight.shape), id(lib))
+        if key != self._key:
+            cout_w, cin_w, kh, kw = weight.shape
+            if (kh, kw) != (3, 3) or weight.dtype != torch.float32:
+                raise ValueError("expected a float32 [Cout,Cin,3,3] weight")
+            if cout_w % KC:
+                raise ValueError(f"forward Cout={cout_w} must be a multiple of {KC} (the dgrad conv's K)")
+            if self.chan_map is None and self.k_out > cin_w:
+                raise ValueError(f"k_out={self.k_out} exceeds the weight's {cin_w} input channels")
+            if self.chan_map is not None and (self._map_dev is None or self._map_dev.device != weight.device):
+                self._map_dev = torch.tensor(self.chan_map, dtype=torch.int32, device=weight.device)
+            cmap = None if self._map_dev is None else self._map_dev.data_ptr()
+            w = weight.detach().contiguous()
+            n = lib.mvbev_conv3x3_packed_bytes_bf16x3(self.cout_p, cout_w)
+            packed = torch.empty(n // 2, dtype=torch.bfloat16, device=weight.device)
+            st = lib.mvbev_pack_conv3x3_dgrad_bf16x3(w.data_ptr(), cout_w, cin_w, cmap, self.k_out,
+                                                     packed.data_ptr(), _stream(packed))
+            _native.check(st, "mvbev_pack_conv3x3_dgrad_bf16x3")
+            self.packed, self._key = packed, key
+        return self.packed
+
+
+def conv3x3_dgrad(dy: torch.Tensor, packed: PackedDgrad3x3, weight: torch.Tensor, dilation: int,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Data gradient of a 3x3 stride-1 conv (padding = dilation): dy [B,Cout_w,H,W] fp32
+    contiguous -> [B, cout_p, H, W] fp32 (channel o = forward input channel chan_map[o];
+    channels past k_out are zero).  Runs the forward bf16x3 conv kernel on the dgrad packing."""
+    _require_cuda(dy)
+    if dy.dim() != 4 or dy.dtype != torch.float32 or not dy.is_contiguous():
+        raise ValueError("dy must be a contiguous float32 [B,Cout,H,W] tensor")
+    B, K, H, W = dy.shape
+    if K != weight.shape[0]:
+        raise ValueError(f"dy has {K} channels, the weight {weight.shape[0]} outputs")
+    d = conv_desc(B, K, H, W, group=K, group_stride=0, batch_stride=K * H * W)
+    return conv3x3_desc(dy, d, packed.get(weight), packed.cout_p, dilation=dilation, out=out)
+
+
+def conv3x3_wgrad(x: torch.Tensor, desc, dy: torch.Tensor, dilation: int, cin_w: int,
+                  chan_map: Optional[torch.Tensor] = None, dw: Optional[torch.Tensor] = None,
+                  workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Weight gradient of a 3x3 conv whose input ``x`` is addressed by ``desc`` (fp32, or the
+    split-bf16 layout when ``x`` is bf16) and whose output gradient is ``dy`` [B,Cout,H,W] fp32:
+    writes dw[co][chan_map[k]][:] (identity without a map) of a [Cout, cin_w, 3, 3] tensor
+    (allocated zeroed when ``dw`` is None; unmapped channels are left as they are)."""
+    _require_cuda(x, dy)
+    if dy.dim() != 4 or dy.dtype != torch.float32 or not dy.is_contiguous():
+        raise ValueError("dy must be a contiguous float32 [B,Cout,H,W] tensor")
+    B, cout, H, W = dy.shape
+    if (desc.B, desc.H, desc.W) != (B, H, W):
+        raise ValueError("dy does not match the conv descriptor")
+    if x.dtype == torch.float32:
+        layout = _native.LAYOUT_F32
+    elif x.dtype == torch.bfloat16:
+        layout = _native.LAYOUT_SPLIT_BF16
+    else:
+        raise TypeError(f"x dtype {x.dtype} not supported by the wgrad kernel")
+    if chan_map is not None:
+        _require_cuda(chan_map)
+        if chan_map.dtype != torch.int32 or chan_map.numel() != desc.K:
+            raise ValueError("chan_map must be an int32 device tensor of K entries")
+    if dw is None:
+        dw = torch.zeros((cout, cin_w, 3, 3), dtype=torch.float32, device=dy.device)
+    elif tuple(dw.shape) != (cout, cin_w, 3, 3) or not dw.is_contiguous() or dw.dtype != torch.float32:
+        raise ValueError(f"dw must be a contiguous fp32 [{cout},{cin_w},3,3] tensor")
+    lib = _native.load()
+    need = int(lib.mvbev_conv3x3_wgrad_workspace_bytes(ctypes.byref(desc), cout))
+    if workspace is None or workspace.numel() * workspace.element_size() < need:
+        workspace = torch.empty((need + 3) // 4, dtype=torch.float32, device=dy.device)
+    st = lib.mvbev_conv3x3_wgrad_bf16x3(x.data_ptr(), layout, ctypes.byref(desc), dy.data_ptr(), cout,
+                                        int(dilation), None if chan_map is None else chan_map.data_ptr(),
+                                        cin_w, dw.data_ptr(), workspace.data_ptr(),
+                                        workspace.numel() * workspace.element_size(), _stream(dy))
+    _native.check(st, "mvbev_conv3x3_wgrad_bf16x3")
+    return dw
+
+
+def conv3x3_bias_coord_grad(dy: torch.Tensor, dilation: int, db: Optional[torch.Tensor] = None,
+                            dw: Optional[torch.Tensor] = None, coord_ch: int = 0) -> None:
+    """db[co] = sum dy[:, co]; with ``dw`` [Cout, Cin_w, 3, 3], also the weight gradient of the
+    two coord-map channels ``coord_ch, coord_ch + 1`` (``create_coord_map``)."""
+    _require_cuda(dy)
+    if dy.dim() != 4 or dy.dtype != torch.float32 or not dy.is_contiguous():
+        raise ValueError("dy must be a contiguous float32 [B,Cout,H,W] tensor")
+    B, cout, H, W = dy.shape
+    cin_w = 0
+    for t in (db, dw):
+        if t is not None:
+            _require_cuda(t)
+            if t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError("db / dw must be contiguous fp32 tensors")
+    if db is not None and db.numel() != cout:
+        raise ValueError("db must have Cout entries")
+    if dw is not None:
+        if dw.dim() != 4 or dw.shape[0] != cout or tuple(dw.shape[2:]) != (3, 3):
+            raise ValueError("dw must be [Cout, Cin_w, 3, 3]")
+        cin_w = dw.shape[1]
+    st = _native.load().mvbev_conv3x3_bias_coord_grad_f32(
+        dy.data_ptr(), B, cout, H, W, int(dilation), None if db is None else db.data_ptr(),
+        None if dw is None else dw.data_ptr(), cin_w, int(coord_ch), _stream(dy))
+    _native.check(st, "mvbev_conv3x3_bias_coord_grad_f32")
+
+
+def relu_backward_(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """In place: dy = dy where y > 0 else 0 (``y`` = the ReLU's output)."""
+    _require_cuda(dy, y)
+    if dy.shape != y.shape or dy.dtype != torch.float32 or y.dtype != torch.float32 or \
+            not dy.is_contiguous() or not y.is_contiguous():
+        raise ValueError("dy and y must be contiguous fp32 tensors of one shape")
+    st = _native.load().mvbev_relu_backward_f32(dy.data_ptr(), y.data_ptr(), dy.numel(), _stream(dy))
+    _native.check(st, "mvbev_relu_backward_f32")
+    return dy
+
+
+def conv3x3_cout1_backward(x: torch.Tensor, weight: torch.Tensor, dmap: torch.Tensor, dilation: int,
+                           relu_mask: bool = False, need_dx: bool = True, need_dw: bool = True):
+    """Backward of ``conv3x3_cout1`` over a whole image: returns (dx [B,C,H,W] or None,
+    dw [1,C,3,3] or None).  ``relu_mask``: zero dx where x <= 0 (x = the previous ReLU's output,
+    its backward fused)."""
+    _require_cuda(x, weight, dmap)
+    if x.dim() != 4 or x.dtype != torch.float32 or not x.is_contiguous():
+        raise ValueError("x must be a contiguous float32 [B,C,H,W] tensor")
+    B, C, H, W = x.shape
+    if tuple(weight.shape) != (1, C, 3, 3):
+        raise ValueError(f"weight must be [1,{C},3,3]")
+    if tuple(dmap.shape) != (B, 1, H, W) or dmap.dtype != torch.float32:
+        raise ValueError(f"dmap must be fp32 [{B},1,{H},{W}]")
+    dmap = dmap.contiguous()
+    w = weight.detach().contiguous()
+    dx = torch.empty_like(x) if need_dx else None
+    dw = torch.empty((1, C, 3, 3), dtype=torch.float32, device=x.device) if need_dw else None
+    if dx is None and dw is None:
+        return None, None
+    st = _native.load().mvbev_conv3x3_cout1_backward_f32(
+        x.data_ptr(), w.data_ptr(), dmap.data_ptr(), B, C, H, W, int(dilation), int(bool(relu_mask)),
+        None if dx is None else dx.data_ptr(), None if dw is None else dw.data_ptr(), _stream(x))
+    _native.check(st, "mvbev_conv3x3_cout1_backward_f32")
+    return dx, dw

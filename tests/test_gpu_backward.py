@@ -1,0 +1,218 @@
+"""GPU parity of the native backward against torch's CPU autograd.
+
+The oracle for every gradient is what the reference trains with (``trainer.py:38-49``):
+torch-CPU autograd through the kornia-0.6.11 restatement (grid_sample's backward) and
+``F.conv2d`` / ReLU (``oracle/cpu_path.py``), or the closed-form ``torch.nn.grad`` adjoints in
+float64 for the individual kernels.  Gate: ``helpers.assert_parity`` (elementwise
+|got-ref| <= 1e-3*|ref| + 1e-3*max|ref| and normwise <= 1e-3), the north_star's 1e-3
+relative fp32 tolerance.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import assert_parity, parity_stats
+from oracle import cpu_path, fixtures, kornia_warp
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _rand_h(rng, H, W, ho, wo):
+    A = np.eye(3)
+    A[0, 0] = wo / W * rng.uniform(0.6, 1.4)
+    A[1, 1] = ho / H * rng.uniform(0.6, 1.4)
+    A[0, 1], A[1, 0] = rng.uniform(-0.2, 0.2, 2)
+    A[0, 2], A[1, 2] = rng.uniform(-3, 3, 2)
+    A[2, 0], A[2, 1] = rng.uniform(-2e-3, 2e-3, 2)
+    return A
+
+
+def _split_encode(x: torch.Tensor) -> torch.Tensor:
+    """fp32 [B,C,H,W] (C % 8 == 0) -> the split-bf16 blocked layout [B, C/8, H, W, 2, 8]."""
+    B, C, H, W = x.shape
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.float()).to(torch.bfloat16)
+    t = torch.stack([hi, lo], 0).reshape(2, B, C // 8, 8, H, W)
+    return t.permute(1, 2, 4, 5, 0, 3).contiguous()
+
+
+# ---------------------------------------------------------------------------------- warp
+
+@pytest.mark.parametrize("B,C,H,W,ho,wo", [(1, 5, 27, 48, 12, 36), (2, 19, 30, 41, 17, 23),
+                                           (1, 3, 9, 11, 20, 30)])
+def test_warp_backward_vs_grid_sample_autograd(B, C, H, W, ho, wo):
+    """Adjoint gather == grid_sample's backward under the kornia restatement (CPU fp32)."""
+    from mvdet_amd import ops
+    from mvdet_amd.geometry import kornia_src_norm_from_dst_norm
+    rng = np.random.default_rng(100 * B + C)
+    n = 3
+    Ms = [torch.from_numpy(_rand_h(rng, H, W, ho, wo)).float()[None] for _ in range(n)]
+    gouts = [torch.from_numpy(rng.standard_normal((B, C, ho, wo)).astype(np.float32)) for _ in range(n)]
+    refs = []
+    for M, g in zip(Ms, gouts):
+        src = torch.zeros((B, C, H, W), requires_grad=True)
+        kornia_warp.warp_perspective(src, M.repeat(B, 1, 1), (ho, wo)).backward(g)
+        refs.append(src.grad)
+    mn = [kornia_src_norm_from_dst_norm(M, (H, W), (ho, wo))[0] for M in Ms]
+    # grad_src rows inside a wider buffer (strided view) and pre-filled: the op accumulates
+    bufs = [torch.full((B, C + 2, H, W), 0.5, device=DEV) for _ in range(n)]
+    ops.warp_views_backward([g.to(DEV) for g in gouts], mn, [b[:, 1:C + 1] for b in bufs])
+    for i in range(n):
+        assert_parity(bufs[i][:, 1:C + 1].cpu() - 0.5, refs[i], f"warp adjoint view {i}")
+        assert (bufs[i][:, 0] == 0.5).all() and (bufs[i][:, C + 1] == 0.5).all()
+
+
+def test_warp_backward_no_gradient_from_outside_samples():
+    from mvdet_amd import ops
+    far = torch.tensor([[1.0, 0, 100.0], [0, 1, 100.0], [0, 0, 1]])  # every sample far outside
+    g = torch.ones((1, 4, 6, 6), device=DEV)
+    dst = torch.zeros((1, 4, 8, 8), device=DEV)
+    ops.warp_views_backward([g], [far], [dst])
+    assert dst.abs().max().item() == 0
+
+
+# ---------------------------------------------------------------------------------- conv grads
+
+@pytest.mark.parametrize("B,K,H,W,dil", [(1, 64, 12, 36, 1), (2, 136, 17, 37, 2), (1, 512, 30, 90, 2),
+                                         (1, 24, 5, 70, 1)])
+@pytest.mark.parametrize("split", [False, True])
+def test_conv_wgrad_vs_torch(B, K, H, W, dil, split):
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(K + H + dil)
+    cout = 128
+    x = F.relu(torch.randn((B, K, H, W), generator=g))
+    dy = torch.randn((B, cout, H, W), generator=g)
+    ref = torch.nn.grad.conv2d_weight(x.double(), (cout, K, 3, 3), dy.double(), padding=dil, dilation=dil)
+    xd = _split_encode(x.to(DEV)) if split else x.to(DEV)
+    d = ops.conv_desc(B, K, H, W, group=K, group_stride=0, batch_stride=K * H * W)
+    got = ops.conv3x3_wgrad(xd, d, dy.to(DEV), dil, K)
+    assert_parity(got.cpu(), ref, f"wgrad split={split}")
+
+
+def test_conv_wgrad_grouped_slab_with_channel_map():
+    """conv1's form: a view-major grouped slab (each group padded to a multiple of 8
+    channels) scattered into the module weight through the channel map; coord channels and
+    padding entries untouched by the kernel."""
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(7)
+    S, B, C, Cs, H, W = 3, 2, 13, 16, 11, 40
+    cin = S * C + 2
+    slab = torch.zeros((S, B, Cs, H, W))
+    slab[:, :, :C] = F.relu(torch.randn((S, B, C, H, W), generator=g))
+    x = torch.cat([slab[s] [:, :C] for s in range(S)] + [torch.zeros((B, 2, H, W))], 1)
+    dy = torch.randn((B, 128, H, W), generator=g)
+    ref = torch.nn.grad.conv2d_weight(x.double(), (128, cin, 3, 3), dy.double(), padding=1)
+    chan_map = torch.tensor([s * C + c if c < C else -1 for s in range(S) for c in range(Cs)], dtype=torch.int32)
+    d = ops.conv_desc(B, S * Cs, H, W, group=Cs, group_stride=B * Cs * H * W, batch_stride=Cs * H * W)
+    dw = torch.full((128, cin, 3, 3), 9.0, device=DEV)
+    for layout in ("f32", "split"):
+        xs = slab.to(DEV) if layout == "f32" else torch.stack([_split_encode(slab[s].to(DEV)) for s in range(S)])
+        ops.conv3x3_wgrad(xs, d, dy.to(DEV), 1, cin, chan_map=chan_map.to(DEV), dw=dw)
+        assert_parity(dw[:, :S * C].cpu(), ref[:, :S * C], f"grouped wgrad {layout}")
+        assert (dw[:, S * C:] == 9.0).all()
+
+
+@pytest.mark.parametrize("B,Cw,K,H,W,dil", [(1, 128, 40, 12, 36, 1), (2, 512, 512, 17, 37, 2),
+                                            (1, 256, 200, 9, 64, 1)])
+def test_conv_dgrad_vs_torch(B, Cw, K, H, W, dil):
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(Cw + K + dil)
+    w = torch.randn((Cw, K, 3, 3), generator=g) * 0.05
+    dy = torch.randn((B, Cw, H, W), generator=g)
+    ref = torch.nn.grad.conv2d_input((B, K, H, W), w.double(), dy.double(), padding=dil, dilation=dil)
+    pk = ops.PackedDgrad3x3(K)
+    got = ops.conv3x3_dgrad(dy.to(DEV), pk, w.to(DEV), dil)
+    assert got.shape[1] == pk.cout_p
+    assert_parity(got[:, :K].cpu(), ref, "dgrad")
+    assert (got[:, K:] == 0).all()
+
+
+def test_conv_dgrad_channel_map():
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(3)
+    w = torch.randn((128, 30, 3, 3), generator=g) * 0.1
+    dy = torch.randn((1, 128, 10, 20), generator=g)
+    ref = torch.nn.grad.conv2d_input((1, 30, 10, 20), w.double(), dy.double(), padding=1)
+    cmap = [29, 3, -1, 7, 0]
+    got = ops.conv3x3_dgrad(dy.to(DEV), ops.PackedDgrad3x3(5, cmap), w.to(DEV), 1).cpu()
+    for o, c in enumerate(cmap):
+        if c < 0:
+            assert (got[:, o] == 0).all()
+        else:
+            assert_parity(got[:, o], ref[:, c], f"dgrad channel {o}")
+
+
+def test_bias_coord_relu_and_cout1_backward():
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(11)
+    B, Co, H, W = 2, 128, 13, 29
+    dy = torch.randn((B, Co, H, W), generator=g)
+    # bias + coord-channel weight gradient (coord map = create_coord_map, channels 5, 6 of 7)
+    cmap = cpu_path.coord_map(H, W).repeat(B, 1, 1, 1)
+    x = torch.cat([torch.zeros((B, 5, H, W)), cmap], 1)
+    ref_w = torch.nn.grad.conv2d_weight(x.double(), (Co, 7, 3, 3), dy.double(), padding=2, dilation=2)
+    db = torch.empty(Co, device=DEV)
+    dw = torch.full((Co, 7, 3, 3), 4.0, device=DEV)
+    ops.conv3x3_bias_coord_grad(dy.to(DEV), 2, db=db, dw=dw, coord_ch=5)
+    assert_parity(db.cpu(), dy.double().sum((0, 2, 3)), "bias grad")
+    assert_parity(dw[:, 5:].cpu(), ref_w[:, 5:], "coord weight grad")
+    assert (dw[:, :5] == 4.0).all()
+    # ReLU backward (threshold_backward semantics: grad where the output > 0)
+    y = F.relu(torch.randn((B, Co, H, W), generator=g))
+    got = ops.relu_backward_(dy.clone().to(DEV), y.to(DEV)).cpu()
+    assert torch.equal(got, torch.where(y > 0, dy, torch.zeros_like(dy)))
+    # conv3 (Cout 1, dilation 4) backward with the previous ReLU's mask fused
+    x2 = F.relu(torch.randn((B, 64, H, W), generator=g))
+    w3 = torch.randn((1, 64, 3, 3), generator=g) * 0.1
+    dmap = torch.randn((B, 1, H, W), generator=g)
+    x2r = x2.double().requires_grad_()
+    w3r = w3.double().requires_grad_()
+    F.conv2d(F.relu(x2r), w3r, padding=4, dilation=4).backward(dmap.double())
+    dx, dw3 = ops.conv3x3_cout1_backward(x2.to(DEV), w3.to(DEV), dmap.to(DEV), 4, relu_mask=True)
+    assert_parity(dx.cpu(), x2r.grad, "cout1 dgrad (relu-masked)")
+    assert_parity(dw3.cpu(), w3r.grad, "cout1 wgrad")
+
+
+# ---------------------------------------------------------------------------------- end to end
+
+def _head(num_cam, C, seed):
+    p = fixtures.head_params(num_cam, seed, C)
+    return {k: torch.from_numpy(v) for k, v in p.items() if k.startswith("map_classifier.")}
+
+
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
+@pytest.mark.parametrize("N,B,C,src,grid", [(2, 1, 8, (27, 48), (12, 36)), (3, 2, 13, (30, 41), (17, 45))])
+def test_project_fuse_backward_vs_cpu_autograd(precision, N, B, C, src, grid):
+    """ProjectFuseFunction (HIP forward + HIP backward) vs torch-CPU autograd through the
+    reference path (kornia restatement + cat + map_classifier) on identical inputs."""
+    from mvdet_amd.autograd import project_fuse
+    from mvdet_amd.pipeline import ProjectFuse
+    rng = np.random.default_rng(N * 31 + C)
+    H, W = src
+    ho, wo = grid
+    Ms = [_rand_h(rng, H, W, ho, wo) for _ in range(N)]
+    feats = [torch.from_numpy(np.maximum(rng.standard_normal((B, C, H, W)), 0).astype(np.float32))
+             for _ in range(N)]
+    params = _head(N, C, seed=N + C)
+    gmap = torch.from_numpy(rng.standard_normal((B, 1, ho, wo)).astype(np.float32))
+    # reference: CPU fp32 autograd
+    fr = [f.clone().requires_grad_() for f in feats]
+    pr = {k: v.clone().requires_grad_() for k, v in params.items()}
+    out_ref = cpu_path.project_fuse(fr, Ms, grid, pr)
+    out_ref.backward(gmap)
+    # native
+    eng = ProjectFuse([torch.from_numpy(M) for M in Ms], src, grid, C, precision=precision)
+    mc = torch.nn.Sequential(torch.nn.Conv2d(N * C + 2, 512, 3, padding=1), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False)).to(DEV)
+    mc.load_state_dict({k.split(".", 1)[1]: v for k, v in params.items()})
+    fg = [f.to(DEV).requires_grad_() for f in feats]
+    out = project_fuse(eng, fg, mc)
+    assert_parity(out.detach().cpu(), out_ref.detach(), "forward")
+    out.backward(gmap.to(DEV))
+    for i in range(N):
+        assert_parity(fg[i].grad.cpu(), fr[i].grad, f"d feat view {i}")
+    for k, p in mc.named_parameters():
+        assert_parity(p.grad.cpu(), pr["map_classifier." + k].grad, f"d {k}")

@@ -246,6 +246,29 @@ int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int
 int mvbev_warp_views_backward_f32(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
                                   int64_t H, int64_t W, int64_t Ho, int64_t Wo, void* stream);
 
+/* The same adjoint as a deterministic gather (no atomics in the per-channel loop).
+ * mvbev_warp_adjoint_plan builds, once per view geometry (m = src_norm <- dst_norm, host
+ * array), the CSR transpose of the warp's sparse sampling matrix: for source pixel p, entries
+ * row_ptr[p] .. row_ptr[p+1]-1 hold (col = output pixel v*Wo+u, val = bilinear corner weight)
+ * in increasing col order.  Device buffers: row_ptr int32[H*W + 1], col int32[4*Ho*Wo], val
+ * fp32[4*Ho*Wo] (capacity; row_ptr[H*W] = entries used), scratch int32[H*W]. */
+int mvbev_warp_adjoint_plan(const float* m, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int32_t* row_ptr,
+                            int32_t* col, float* val, int32_t* scratch, void* stream);
+
+typedef struct mvbev_warp_adjoint_view {
+  const float* grad_out;       /* [B][C][Ho][Wo] fp32, element strides (row / column dense) */
+  int64_t grad_out_strides[4];
+  float* grad_src;             /* [B][C][H][W] fp32, element strides (row / column dense) */
+  int64_t grad_src_strides[4];
+  const int32_t* row_ptr;      /* the view's plan */
+  const int32_t* col;
+  const float* val;
+} mvbev_warp_adjoint_view;
+
+/* grad_src (accumulate ? += : =) S^T grad_out for every view, one launch (nviews <= 16). */
+int mvbev_warp_views_adjoint_f32(const mvbev_warp_adjoint_view* views, int nviews, int64_t B, int64_t C,
+                                 int64_t H, int64_t W, int64_t Ho, int64_t Wo, int accumulate, void* stream);
+
 /* Weights for the data gradient of a 3x3 stride-1 conv with padding = dilation: that gradient is
  * the same conv over dy with w'[k][co][t] = w[co][k][8 - t], so mvbev_conv3x3_bf16x3_ex computes
  * it with these weights (Cout' = round_up(K_out, MVBEV_CONV_BN) output channels, K' = Cout_w).

@@ -42,6 +42,8 @@ EXPORTS = (
     "mvbev_conv3x3_bias_coord_grad_f32",
     "mvbev_relu_backward_f32",
     "mvbev_conv3x3_cout1_backward_f32",
+    "mvbev_warp_adjoint_plan",
+    "mvbev_warp_views_adjoint_f32",
 )
 
 KC = 8    # MVBEV_CONV_KC
@@ -66,6 +68,13 @@ class WarpView(ctypes.Structure):
     """``mvbev_warp_view`` (include/mvbev.h)."""
     _fields_ = [("src", ctypes.c_void_p), ("src_strides", ctypes.c_int64 * 4), ("dst", ctypes.c_void_p),
                 ("dst_strides", ctypes.c_int64 * 4), ("m", ctypes.c_float * 9)]
+
+
+class WarpAdjointView(ctypes.Structure):
+    """``mvbev_warp_adjoint_view`` (include/mvbev.h)."""
+    _fields_ = [("grad_out", ctypes.c_void_p), ("grad_out_strides", ctypes.c_int64 * 4),
+                ("grad_src", ctypes.c_void_p), ("grad_src_strides", ctypes.c_int64 * 4),
+                ("row_ptr", ctypes.c_void_p), ("col", ctypes.c_void_p), ("val", ctypes.c_void_p)]
 
 
 class NativeError(RuntimeError):
@@ -138,6 +147,12 @@ def _declare(lib):
     lib.mvbev_conv3x3_cout1_backward_f32.restype = ctypes.c_int
     lib.mvbev_conv3x3_cout1_backward_f32.argtypes = [_p, _p, _p, _i64, _i64, _i64, _i64, ctypes.c_int,
                                                      ctypes.c_int, _p, _p, _p]
+    lib.mvbev_warp_adjoint_plan.restype = ctypes.c_int
+    lib.mvbev_warp_adjoint_plan.argtypes = [ctypes.POINTER(ctypes.c_float), _i64, _i64, _i64, _i64, _p, _p, _p, _p,
+                                            _p]
+    lib.mvbev_warp_views_adjoint_f32.restype = ctypes.c_int
+    lib.mvbev_warp_views_adjoint_f32.argtypes = [ctypes.POINTER(WarpAdjointView), ctypes.c_int, _i64, _i64, _i64,
+                                                 _i64, _i64, _i64, ctypes.c_int, _p]
     lib.mvbev_conv3x3_cout1_f32.restype = ctypes.c_int
     lib.mvbev_conv3x3_cout1_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p,
                                             ctypes.c_int, _p, _p]

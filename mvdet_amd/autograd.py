@@ -11,7 +11,8 @@ slab, conv1-3) and whose backward is all HIP:
   conv2 (d2) + ReLU    db2, dw2 = wgrad(y1, dy2) (3xbf16 MFMA), dy1 = dgrad-conv(dy2) * [y1 > 0]
   conv1 (d1) + ReLU    db1 + coord-channel dw1, view-channel dw1 = wgrad(slab, dy1),
                        dslab = dgrad-conv(dy1) (forward conv kernel on transposed+flipped taps)
-  warp                 grad_feat[v] += adjoint-gather(dslab[v]) (fp32 atomics)
+  warp                 grad_feat[v] = S_v^T dslab[v]: CSR gather over the transposed
+                       sampling matrix (plan built once per geometry; deterministic)
 
 Activations saved for the backward: the slab (the forward's own buffer, split-bf16 with
 3xbf16), y1 and y2 in fp32 (a fresh set per training forward, so a second forward before
@@ -27,6 +28,20 @@ import torch
 
 from . import ops
 from .pipeline import ProjectFuse, Workspace, band_rows
+
+
+# optional stage hook (bench / tools): called with a stage name right before it is enqueued
+_stage_hook = None
+
+
+def set_stage_hook(fn) -> None:
+    global _stage_hook
+    _stage_hook = fn
+
+
+def _mark(stage: str) -> None:
+    if _stage_hook is not None:
+        _stage_hook(stage)
 
 
 def _train_workspace(engine: ProjectFuse, B: int, device) -> Workspace:
@@ -50,6 +65,18 @@ def _bwd_state(engine: ProjectFuse):
         st = SimpleNamespace(dgrad1=ops.PackedDgrad3x3(nc), dgrad2=ops.PackedDgrad3x3(engine.mid), wg_ws={})
         engine._bwd = st
     return st
+
+
+def _adjoint_plans(engine: ProjectFuse, st, device):
+    key = str(device)
+    plans = st.plans.get(key) if hasattr(st, "plans") else None
+    if plans is None:
+        if not hasattr(st, "plans"):
+            st.plans = {}
+        plans = [ops.WarpAdjointPlan(engine.m_norm_cpu[v], engine.src_hw, engine.grid_hw, device)
+                 for v in range(engine.num_cam)]
+        st.plans[key] = plans
+    return plans
 
 
 def _wgrad_ws(st, desc, cout, device) -> torch.Tensor:
@@ -76,10 +103,11 @@ class ProjectFuseFunction(torch.autograd.Function):
         B = feats[0].shape[0]
         dev = feats[0].device
         ws = _train_workspace(engine, B, dev)
+        _mark("warp")
         engine.warp_views(ws, list(range(n)), [f.detach() for f in feats])
         mc = [SimpleNamespace(weight=w1, bias=b1), None, SimpleNamespace(weight=w2, bias=b2), None,
               SimpleNamespace(weight=w3, bias=None)]
-        out = engine.fuse(ws, mc)
+        out = engine.fuse(ws, mc, mark=_stage_hook)
         ctx.engine = engine
         ctx.ws = ws
         ctx.feat_shape = tuple(feats[0].shape)
@@ -101,19 +129,23 @@ class ProjectFuseFunction(torch.autograd.Function):
         dmap = dmap.contiguous().float()
         mid = engine.mid
         # conv3: dy2 = dgrad * relu'(y2); dw3
+        _mark("bwd_conv3")
         dy2, dw3 = ops.conv3x3_cout1_backward(ws.y2, w3, dmap, 4, relu_mask=True)
         # conv2: db2, dw2, dy1 = dgrad * relu'(y1)
+        _mark("bwd_conv2_wgrad")
         db2 = torch.empty(mid, dtype=torch.float32, device=dev) if b2 is not None else None
         if db2 is not None:
             ops.conv3x3_bias_coord_grad(dy2, 2, db=db2)
         d_y1 = ops.conv_desc(B, mid, H, W, group=mid, group_stride=0, batch_stride=mid * H * W)
         dw2 = ops.conv3x3_wgrad(ws.y1, d_y1, dy2, 2, mid, workspace=_wgrad_ws(st, d_y1, mid, dev))
+        _mark("bwd_conv2_dgrad")
         dy1 = ops.conv3x3_dgrad(dy2, st.dgrad2, w2, 2)
         if dy1.shape[1] != mid:
             dy1 = dy1[:, :mid].contiguous()
         del dy2
         ops.relu_backward_(dy1, ws.y1)
         # conv1: db1 + coord channels, view channels (slab order through the pack's channel map)
+        _mark("bwd_conv1_wgrad")
         nc = n * engine.C
         dw1 = torch.zeros_like(w1)
         db1 = torch.empty(mid, dtype=torch.float32, device=dev) if b1 is not None else None
@@ -125,12 +157,15 @@ class ProjectFuseFunction(torch.autograd.Function):
                           workspace=_wgrad_ws(st, d1, mid, dev))
         grads = [None] * n
         if need_feat:
+            _mark("bwd_conv1_dgrad")
             dslab = ops.conv3x3_dgrad(dy1, st.dgrad1, w1, 1)   # [B, round_up(nc,128), H, W]
             C = engine.C
-            gs = [torch.zeros(ctx.feat_shape, dtype=torch.float32, device=dev) for _ in range(n)]
-            ops.warp_views_backward([dslab[:, v * C:(v + 1) * C] for v in range(n)],
-                                    [engine.m_norm_cpu[v] for v in range(n)], gs)
+            _mark("bwd_warp")
+            gs = [torch.empty(ctx.feat_shape, dtype=torch.float32, device=dev) for _ in range(n)]
+            ops.warp_views_adjoint([dslab[:, v * C:(v + 1) * C] for v in range(n)],
+                                   _adjoint_plans(engine, st, dev), gs)
             grads = [g if need[v] else None for v, g in enumerate(gs)]
+        _mark("bwd_end")
         ctx.ws = None
         return (None, *grads, dw1, db1, dw2, db2, dw3)
 

@@ -462,6 +462,175 @@ __global__ __launch_bounds__(256) void warp_backward_kernel(const WarpArgs a) {
   for (; c < c_end; ++c) scatter(c, go[(int64_t)c * vw.sC]);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Warp adjoint as a gather (no atomics in the hot loop).  The bilinear warp is a sparse matrix
+// S (Ho*Wo x H*W, <= 4 entries per row: the in-bounds corners of the sample, weights from the
+// forward's own fp32 coordinate code); its adjoint grad_src = S^T grad_out is a CSR gather
+// over S^T built once per geometry (the plan):
+//   row_ptr[H*W + 1], col[] = output pixel, val[] = corner weight, entries of one source pixel
+//   in increasing output-pixel order (deterministic summation order).
+// Build: count (int atomics) -> single-workgroup exclusive scan -> fill (atomic cursor) ->
+// per-segment insertion sort by output pixel.  Geometry only, so it runs once per view.
+
+struct Corners {
+  int idx[4];    // source pixel (y * W + x) or -1
+  float w[4];
+};
+__device__ inline Corners warp_corners(const float (&m)[9], int u, int v, int Ho, int Wo, int H, int W) {
+  Corners k;
+  const WarpCoord wc = warp_coord(m, u, v, Ho, Wo, H, W);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) k.idx[i] = -1, k.w[i] = 0.f;
+  if (!wc.inside) return k;
+  const float ix = wc.ix, iy = wc.iy;
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  const int x0 = (int)fx0, y0 = (int)fy0;
+  const float fx1 = fx0 + 1.f, fy1 = fy0 + 1.f;
+  k.w[0] = (fx1 - ix) * (fy1 - iy);
+  k.w[1] = (ix - fx0) * (fy1 - iy);
+  k.w[2] = (fx1 - ix) * (iy - fy0);
+  k.w[3] = (ix - fx0) * (iy - fy0);
+  const bool vx0 = x0 >= 0, vx1 = x0 + 1 <= W - 1, vy0 = y0 >= 0, vy1 = y0 + 1 <= H - 1;
+  if (vx0 && vy0) k.idx[0] = y0 * W + x0;
+  if (vx1 && vy0) k.idx[1] = y0 * W + x0 + 1;
+  if (vx0 && vy1) k.idx[2] = (y0 + 1) * W + x0;
+  if (vx1 && vy1) k.idx[3] = (y0 + 1) * W + x0 + 1;
+  return k;
+}
+
+struct PlanArgs {
+  float m[9];
+  int H, W, Ho, Wo;
+};
+
+__global__ __launch_bounds__(256) void adj_count_kernel(const PlanArgs a, int32_t* __restrict__ counts) {
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  if (o >= a.Ho * a.Wo) return;
+  const Corners k = warp_corners(a.m, o % a.Wo, o / a.Wo, a.Ho, a.Wo, a.H, a.W);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (k.idx[i] >= 0) atomicAdd(counts + k.idx[i], 1);
+}
+
+// row_ptr[i] = sum counts[0..i), row_ptr[n] = total; also cursor[i] = row_ptr[i].  One
+// workgroup of 1024 threads walks the array in 1024-element pieces (setup-time only).
+__global__ __launch_bounds__(1024) void adj_scan_kernel(const int32_t* __restrict__ counts, int n,
+                                                        int32_t* __restrict__ row_ptr, int32_t* __restrict__ cursor) {
+  __shared__ int32_t part[1024];
+  __shared__ int32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < n; base += 1024) {
+    const int i = base + threadIdx.x;
+    const int32_t c = i < n ? counts[i] : 0;
+    part[threadIdx.x] = c;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+      const int32_t t = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+      __syncthreads();
+      part[threadIdx.x] += t;
+      __syncthreads();
+    }
+    const int32_t excl = carry + part[threadIdx.x] - c;
+    if (i < n) row_ptr[i] = excl, cursor[i] = excl;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += part[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) row_ptr[n] = carry;
+}
+
+__global__ __launch_bounds__(256) void adj_fill_kernel(const PlanArgs a, int32_t* __restrict__ cursor,
+                                                       int32_t* __restrict__ col, float* __restrict__ val) {
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  if (o >= a.Ho * a.Wo) return;
+  const Corners k = warp_corners(a.m, o % a.Wo, o / a.Wo, a.Ho, a.Wo, a.H, a.W);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (k.idx[i] >= 0) {
+      const int pos = atomicAdd(cursor + k.idx[i], 1);
+      col[pos] = o;
+      val[pos] = k.w[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void adj_sort_kernel(const int32_t* __restrict__ row_ptr, int n,
+                                                       int32_t* __restrict__ col, float* __restrict__ val) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int e0 = row_ptr[i], e1 = row_ptr[i + 1];
+  for (int e = e0 + 1; e < e1; ++e) {  // insertion sort by output pixel (segments are short)
+    const int c = col[e];
+    const float w = val[e];
+    int f = e - 1;
+    while (f >= e0 && col[f] > c) {
+      col[f + 1] = col[f];
+      val[f + 1] = val[f];
+      --f;
+    }
+    col[f + 1] = c;
+    val[f + 1] = w;
+  }
+}
+
+// grad_src[b][c][p] (+)= sum_e val[e] * grad_out[b][c][col[e]], e in row p of the plan.
+// Thread = source pixel, loop over the block's channel chunk; the pixel's first kAdjReg
+// entries stay in registers across the channels.  Workgroups of one (view, batch, channel
+// chunk) are consecutive in the XCD-remapped order, so an XCD sweeps neighbouring pixels of
+// the same grad_out planes (its L2 holds them).
+constexpr int kAdjReg = 6;
+constexpr int kAdjCPB = 32;
+struct AdjView {
+  const float* go;
+  int64_t gB, gC;
+  float* gs;
+  int64_t sB, sC;
+  const int32_t* rp;
+  const int32_t* col;
+  const float* val;
+};
+struct AdjArgs {
+  AdjView v[kWarpMaxViews];
+  int nviews, B, C, P, pblocks, chunks, nwg, accumulate;
+};
+
+__global__ __launch_bounds__(256) void warp_adjoint_kernel(const AdjArgs a) {
+  const int lb = xcd_remap(blockIdx.x, a.nwg);
+  const int pb = lb % a.pblocks;
+  int r = lb / a.pblocks;
+  const int chunk = r % a.chunks;
+  r /= a.chunks;
+  const int view = r % a.nviews;
+  const int b = r / a.nviews;
+  const int p = pb * 256 + threadIdx.x;
+  if (p >= a.P) return;
+  const AdjView& vw = a.v[view];
+  const int e0 = vw.rp[p], e1 = vw.rp[p + 1];
+  const int ne = min(e1 - e0, kAdjReg);
+  int cl[kAdjReg];
+  float wt[kAdjReg];
+#pragma unroll
+  for (int j = 0; j < kAdjReg; ++j) {
+    cl[j] = j < ne ? vw.col[e0 + j] : 0;
+    wt[j] = j < ne ? vw.val[e0 + j] : 0.f;
+  }
+  const int c0 = chunk * kAdjCPB, c1 = min(a.C, c0 + kAdjCPB);
+  const float* go = vw.go + (int64_t)b * vw.gB;
+  float* gs = vw.gs + (int64_t)b * vw.sB + p;
+  for (int c = c0; c < c1; ++c) {
+    const float* g = go + (int64_t)c * vw.gC;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < kAdjReg; ++j)
+      if (j < ne) s += wt[j] * g[cl[j]];
+    for (int e = e0 + kAdjReg; e < e1; ++e) s += vw.val[e] * g[vw.col[e]];
+    float* d = gs + (int64_t)c * vw.sC;
+    if (a.accumulate) s += *d;
+    *d = s;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // wgrad launch geometry
 static int cu_count() {
@@ -628,6 +797,61 @@ int mvbev_warp_views_backward_f32(const mvbev_warp_view* views, int nviews, int6
   if (nwg > INT32_MAX) return MVBEV_ERR_SHAPE;
   a.nwg = (int)nwg;
   hipLaunchKernelGGL(bwd::warp_backward_kernel, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+
+int mvbev_warp_adjoint_plan(const float* m, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int32_t* row_ptr,
+                            int32_t* col, float* val, int32_t* scratch, void* stream) {
+  using namespace mvbev;
+  if (!m || !row_ptr || !col || !val || !scratch) return MVBEV_ERR_NULL;
+  if (H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0) return MVBEV_ERR_RANK;
+  if (H * W >= INT32_MAX || 4 * Ho * Wo >= INT32_MAX) return MVBEV_ERR_SHAPE;
+  bwd::PlanArgs a;
+  for (int i = 0; i < 9; ++i) a.m[i] = m[i];
+  a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
+  hipStream_t s = as_stream(stream);
+  const int n = (int)(H * W);
+  if (hipMemsetAsync(scratch, 0, sizeof(int32_t) * n, s) != hipSuccess) return MVBEV_ERR_HIP;
+  const unsigned ob = (unsigned)ceil_div(Ho * Wo, 256);
+  hipLaunchKernelGGL(bwd::adj_count_kernel, dim3(ob), dim3(256), 0, s, a, scratch);
+  MVBEV_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bwd::adj_scan_kernel, dim3(1), dim3(1024), 0, s, scratch, n, row_ptr, scratch);
+  MVBEV_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bwd::adj_fill_kernel, dim3(ob), dim3(256), 0, s, a, scratch, col, val);
+  MVBEV_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bwd::adj_sort_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, row_ptr, n, col, val);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+int mvbev_warp_views_adjoint_f32(const mvbev_warp_adjoint_view* views, int nviews, int64_t B, int64_t C,
+                                 int64_t H, int64_t W, int64_t Ho, int64_t Wo, int accumulate, void* stream) {
+  using namespace mvbev;
+  if (!views) return MVBEV_ERR_NULL;
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 || nviews <= 0) return MVBEV_ERR_RANK;
+  if (nviews > kWarpMaxViews || H * W >= INT32_MAX || 4 * Ho * Wo >= INT32_MAX) return MVBEV_ERR_SHAPE;
+  bwd::AdjArgs a = {};
+  for (int i = 0; i < nviews; ++i) {
+    const mvbev_warp_adjoint_view& v = views[i];
+    if (!v.grad_out || !v.grad_src || !v.row_ptr || !v.col || !v.val) return MVBEV_ERR_NULL;
+    // planes must be dense (the plan indexes pixels linearly)
+    if (v.grad_out_strides[3] != 1 || v.grad_out_strides[2] != Wo || v.grad_src_strides[3] != 1 ||
+        v.grad_src_strides[2] != W)
+      return MVBEV_ERR_STRIDE;
+    a.v[i] = bwd::AdjView{v.grad_out, v.grad_out_strides[0], v.grad_out_strides[1], v.grad_src,
+                          v.grad_src_strides[0], v.grad_src_strides[1], v.row_ptr, v.col, v.val};
+  }
+  a.nviews = nviews;
+  a.B = (int)B; a.C = (int)C; a.P = (int)(H * W);
+  a.pblocks = (int)ceil_div(H * W, 256);
+  a.chunks = (int)ceil_div(C, bwd::kAdjCPB);
+  a.accumulate = accumulate ? 1 : 0;
+  const int64_t nwg = (int64_t)a.pblocks * a.chunks * nviews * B;
+  if (nwg > INT32_MAX) return MVBEV_ERR_SHAPE;
+  a.nwg = (int)nwg;
+  hipLaunchKernelGGL(bwd::warp_adjoint_kernel, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }

@@ -480,6 +480,60 @@ def warp_views_backward(grad_outs, m_norms, grad_srcs) -> None:
     _native.check(st, "mvbev_warp_views_backward_f32")
 
 
+class WarpAdjointPlan:
+    """CSR transpose of one view's bilinear sampling matrix (``mvbev_warp_adjoint_plan``):
+    geometry only, built once per (matrix, sizes, device) on the GPU."""
+
+    def __init__(self, m_norm, src_hw, grid_hw, device):
+        H, W = int(src_hw[0]), int(src_hw[1])
+        Ho, Wo = int(grid_hw[0]), int(grid_hw[1])
+        device = torch.device(device)
+        self.src_hw, self.grid_hw = (H, W), (Ho, Wo)
+        self.row_ptr = torch.empty(H * W + 1, dtype=torch.int32, device=device)
+        self.col = torch.empty(4 * Ho * Wo, dtype=torch.int32, device=device)
+        self.val = torch.empty(4 * Ho * Wo, dtype=torch.float32, device=device)
+        scratch = torch.empty(H * W, dtype=torch.int32, device=device)
+        mm = (ctypes.c_float * 9)(*torch.as_tensor(m_norm, dtype=torch.float32).reshape(9).tolist())
+        st = _native.load().mvbev_warp_adjoint_plan(mm, H, W, Ho, Wo, self.row_ptr.data_ptr(), self.col.data_ptr(),
+                                                    self.val.data_ptr(), scratch.data_ptr(), _stream(self.row_ptr))
+        _native.check(st, "mvbev_warp_adjoint_plan")
+        self._scratch = scratch  # freed with the plan (kept until the stream has used it)
+
+    @property
+    def nnz(self) -> int:
+        return int(self.row_ptr[-1].item())
+
+
+def warp_views_adjoint(grad_outs, plans, grad_srcs, accumulate: bool = False) -> None:
+    """Deterministic gather form of ``warp_views_backward``: ``grad_srcs[i]`` [B,C,H,W] =
+    (or += with ``accumulate``) the adjoint of view i's warp applied to ``grad_outs[i]``
+    [B,C,Ho,Wo]; ``plans[i]`` its ``WarpAdjointPlan``.  Rows/columns of both must be dense."""
+    n = len(grad_outs)
+    if n == 0:
+        return
+    if not (len(plans) == n == len(grad_srcs)) or n > 16:
+        raise ValueError("need 1..16 matching grad_outs / plans / grad_srcs")
+    _require_cuda(*grad_outs, *grad_srcs)
+    B, C, Ho, Wo = grad_outs[0].shape
+    _, _, H, W = grad_srcs[0].shape
+    arr = (_native.WarpAdjointView * n)()
+    for i, (g, pl, d) in enumerate(zip(grad_outs, plans, grad_srcs)):
+        if tuple(g.shape) != (B, C, Ho, Wo) or tuple(d.shape) != (B, C, H, W):
+            raise ValueError(f"all views must share shapes: grad_out {tuple(g.shape)} grad_src {tuple(d.shape)}")
+        if pl.src_hw != (H, W) or pl.grid_hw != (Ho, Wo):
+            raise ValueError("plan built for other sizes")
+        if g.dtype != torch.float32 or d.dtype != torch.float32:
+            raise TypeError("the warp adjoint is fp32")
+        if g.stride(3) != 1 or g.stride(2) != Wo or d.stride(3) != 1 or d.stride(2) != W:
+            raise ValueError("grad_out / grad_src planes must be dense (row stride = width, column stride 1)")
+        arr[i] = _native.WarpAdjointView(g.data_ptr(), (ctypes.c_int64 * 4)(*g.stride()), d.data_ptr(),
+                                         (ctypes.c_int64 * 4)(*d.stride()), pl.row_ptr.data_ptr(),
+                                         pl.col.data_ptr(), pl.val.data_ptr())
+    st = _native.load().mvbev_warp_views_adjoint_f32(arr, n, B, C, H, W, Ho, Wo, int(bool(accumulate)),
+                                                     _stream(grad_srcs[0]))
+    _native.check(st, "mvbev_warp_views_adjoint_f32")
+
+
 class PackedDgrad3x3:
     """bf16x3-packed weights of a 3x3 conv's DATA gradient (transposed, flipped taps:
     ``mvbev_pack_conv3x3_dgrad_bf16x3``).  Output channel o of the dgrad conv = forward input

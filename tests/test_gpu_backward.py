@@ -64,6 +64,44 @@ def test_warp_backward_vs_grid_sample_autograd(B, C, H, W, ho, wo):
         assert (bufs[i][:, 0] == 0.5).all() and (bufs[i][:, C + 1] == 0.5).all()
 
 
+@pytest.mark.parametrize("B,C,H,W,ho,wo", [(1, 5, 27, 48, 12, 36), (2, 37, 30, 41, 17, 23),
+                                           (1, 3, 9, 11, 20, 30), (1, 70, 90, 160, 120, 360)])
+def test_warp_adjoint_gather_vs_grid_sample_autograd(B, C, H, W, ho, wo):
+    """The CSR-gather adjoint (plan once per geometry): equals grid_sample's backward, is
+    bitwise deterministic, overwrites or accumulates, and its plan holds one entry per
+    in-bounds corner of every inside sample."""
+    from mvdet_amd import ops
+    from mvdet_amd.geometry import kornia_src_norm_from_dst_norm
+    rng = np.random.default_rng(7 * B + C)
+    n = 2
+    Ms = [torch.from_numpy(_rand_h(rng, H, W, ho, wo)).float()[None] for _ in range(n)]
+    gouts = [torch.from_numpy(rng.standard_normal((B, C, ho, wo)).astype(np.float32)) for _ in range(n)]
+    refs = []
+    for M, g in zip(Ms, gouts):
+        src = torch.zeros((B, C, H, W), requires_grad=True)
+        kornia_warp.warp_perspective(src, M.repeat(B, 1, 1), (ho, wo)).backward(g)
+        refs.append(src.grad)
+    mn = [kornia_src_norm_from_dst_norm(M, (H, W), (ho, wo))[0] for M in Ms]
+    plans = [ops.WarpAdjointPlan(m, (H, W), (ho, wo), DEV) for m in mn]
+    rp = plans[0].row_ptr.cpu()
+    assert rp[0] == 0 and (rp[1:] >= rp[:-1]).all() and plans[0].nnz <= 4 * ho * wo
+    col = plans[0].col[:plans[0].nnz].cpu()
+    for p in range(0, H * W, max(1, H * W // 97)):  # entries of a pixel sorted by output pixel
+        seg = col[rp[p]:rp[p + 1]]
+        assert (seg[1:] > seg[:-1]).all()
+    gdev = [g.to(DEV) for g in gouts]
+    outs = [torch.full((B, C, H, W), float("nan"), device=DEV) for _ in range(n)]  # overwritten
+    ops.warp_views_adjoint(gdev, plans, outs)
+    for i in range(n):
+        assert_parity(outs[i].cpu(), refs[i], f"adjoint gather view {i}")
+    again = [torch.empty_like(o) for o in outs]
+    ops.warp_views_adjoint(gdev, plans, again)
+    assert all(torch.equal(a, o) for a, o in zip(again, outs))
+    ops.warp_views_adjoint(gdev, plans, again, accumulate=True)
+    for a, o in zip(again, outs):
+        assert torch.allclose(a, 2 * o, rtol=1e-6, atol=0)
+
+
 def test_warp_backward_no_gradient_from_outside_samples():
     from mvdet_amd import ops
     far = torch.tensor([[1.0, 0, 100.0], [0, 1, 100.0], [0, 0, 1]])  # every sample far outside

@@ -265,9 +265,13 @@ typedef struct mvbev_warp_adjoint_view {
   const float* val;
 } mvbev_warp_adjoint_view;
 
-/* grad_src (accumulate ? += : =) S^T grad_out for every view, one launch (nviews <= 16). */
-int mvbev_warp_views_adjoint_f32(const mvbev_warp_adjoint_view* views, int nviews, int64_t B, int64_t C,
-                                 int64_t H, int64_t W, int64_t Ho, int64_t Wo, int accumulate, void* stream);
+/* grad_src (accumulate ? += : =) S^T grad_out for every view, one launch (nviews <= 16).
+ * grad_out_layout MVBEV_LAYOUT_F32 (element strides) or MVBEV_LAYOUT_SPLIT_BF16 (grad_out =
+ * the view's first 8-channel group of a split-bf16 blocked tensor, 16-B aligned, strides in
+ * 32-byte units {batch, channel group, row = Wo, col = 1}; value = hi + lo). */
+int mvbev_warp_views_adjoint(const mvbev_warp_adjoint_view* views, int nviews, int grad_out_layout, int64_t B,
+                             int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int accumulate,
+                             void* stream);
 
 /* Weights for the data gradient of a 3x3 stride-1 conv with padding = dilation: that gradient is
  * the same conv over dy with w'[k][co][t] = w[co][k][8 - t], so mvbev_conv3x3_bf16x3_ex computes

@@ -158,12 +158,19 @@ class ProjectFuseFunction(torch.autograd.Function):
         grads = [None] * n
         if need_feat:
             _mark("bwd_conv1_dgrad")
-            dslab = ops.conv3x3_dgrad(dy1, st.dgrad1, w1, 1)   # [B, round_up(nc,128), H, W]
             C = engine.C
+            cp = st.dgrad1.cout_p
+            if C % ops.KC == 0:  # split-bf16 dslab: the adjoint gathers 8 channels per 32-B entry
+                dslab = torch.empty(ops.split_shape(B, cp, H, W), dtype=torch.bfloat16, device=dev)
+                ops.conv3x3_dgrad(dy1, st.dgrad1, w1, 1, out=dslab)
+                g8 = C // ops.KC
+                douts = [dslab[:, v * g8:(v + 1) * g8] for v in range(n)]
+            else:
+                dslab = ops.conv3x3_dgrad(dy1, st.dgrad1, w1, 1)   # [B, round_up(nc,128), H, W]
+                douts = [dslab[:, v * C:(v + 1) * C] for v in range(n)]
             _mark("bwd_warp")
             gs = [torch.empty(ctx.feat_shape, dtype=torch.float32, device=dev) for _ in range(n)]
-            ops.warp_views_adjoint([dslab[:, v * C:(v + 1) * C] for v in range(n)],
-                                   _adjoint_plans(engine, st, dev), gs)
+            ops.warp_views_adjoint(douts, _adjoint_plans(engine, st, dev), gs)
             grads = [g if need[v] else None for v, g in enumerate(gs)]
         _mark("bwd_end")
         ctx.ws = None

@@ -581,6 +581,7 @@ __global__ __launch_bounds__(256) void adj_sort_kernel(const int32_t* __restrict
 // the same grad_out planes (its L2 holds them).
 constexpr int kAdjReg = 6;
 constexpr int kAdjCPB = 32;
+constexpr int kAdjU = 8;
 struct AdjView {
   const float* go;
   int64_t gB, gC;
@@ -618,16 +619,92 @@ __global__ __launch_bounds__(256) void warp_adjoint_kernel(const AdjArgs a) {
   const int c0 = chunk * kAdjCPB, c1 = min(a.C, c0 + kAdjCPB);
   const float* go = vw.go + (int64_t)b * vw.gB;
   float* gs = vw.gs + (int64_t)b * vw.sB + p;
-  for (int c = c0; c < c1; ++c) {
+  // kAdjU channels per iteration: their gathers are independent, so up to kAdjU * kAdjReg
+  // loads are in flight per lane before the first add needs one
+  int c = c0;
+  for (; c + kAdjU <= c1; c += kAdjU) {
+    float s[kAdjU];
+#pragma unroll
+    for (int q = 0; q < kAdjU; ++q) {
+      const float* g = go + (int64_t)(c + q) * vw.gC;
+      float t = 0.f;
+#pragma unroll
+      for (int j = 0; j < kAdjReg; ++j)
+        if (j < ne) t += wt[j] * g[cl[j]];
+      s[q] = t;
+    }
+    for (int e = e0 + kAdjReg; e < e1; ++e) {
+      const int oc = vw.col[e];
+      const float w = vw.val[e];
+#pragma unroll
+      for (int q = 0; q < kAdjU; ++q) s[q] += w * go[(int64_t)(c + q) * vw.gC + oc];
+    }
+#pragma unroll
+    for (int q = 0; q < kAdjU; ++q) {
+      float* d = gs + (int64_t)(c + q) * vw.sC;
+      *d = a.accumulate ? s[q] + *d : s[q];
+    }
+  }
+  for (; c < c1; ++c) {
     const float* g = go + (int64_t)c * vw.gC;
-    float s = 0.f;
+    float t = 0.f;
 #pragma unroll
     for (int j = 0; j < kAdjReg; ++j)
-      if (j < ne) s += wt[j] * g[cl[j]];
-    for (int e = e0 + kAdjReg; e < e1; ++e) s += vw.val[e] * g[vw.col[e]];
+      if (j < ne) t += wt[j] * g[cl[j]];
+    for (int e = e0 + kAdjReg; e < e1; ++e) t += vw.val[e] * g[vw.col[e]];
     float* d = gs + (int64_t)c * vw.sC;
-    if (a.accumulate) s += *d;
-    *d = s;
+    *d = a.accumulate ? t + *d : t;
+  }
+}
+
+// Same gather with grad_out in the split-bf16 blocked layout (what the dgrad conv writes with
+// a split output: per pixel and 8-channel group 16 B hi + 16 B lo; gB / gC strides in 32-B
+// units): one entry costs two 16-B loads for 8 channels instead of eight 4-B gathers.
+__global__ __launch_bounds__(256) void warp_adjoint_split_kernel(const AdjArgs a) {
+  const int lb = xcd_remap(blockIdx.x, a.nwg);
+  const int pb = lb % a.pblocks;
+  int r = lb / a.pblocks;
+  const int chunk = r % a.chunks;
+  r /= a.chunks;
+  const int view = r % a.nviews;
+  const int b = r / a.nviews;
+  const int p = pb * 256 + threadIdx.x;
+  if (p >= a.P) return;
+  const AdjView& vw = a.v[view];
+  const int e0 = vw.rp[p], e1 = vw.rp[p + 1];
+  const int ne = min(e1 - e0, kAdjReg);
+  int cl[kAdjReg];
+  float wt[kAdjReg];
+#pragma unroll
+  for (int j = 0; j < kAdjReg; ++j) {
+    cl[j] = j < ne ? vw.col[e0 + j] : 0;
+    wt[j] = j < ne ? vw.val[e0 + j] : 0.f;
+  }
+  const int c0 = chunk * kAdjCPB, c1 = min(a.C, c0 + kAdjCPB);  // c0 % 8 == 0
+  const u32x4* go = reinterpret_cast<const u32x4*>(vw.go) + 2 * (int64_t)b * vw.gB;
+  float* gs = vw.gs + (int64_t)b * vw.sB + p;
+  for (int c = c0; c < c1; c += 8) {
+    const u32x4* g = go + 2 * (int64_t)(c >> 3) * vw.gC;
+    float s[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s[q] = 0.f;
+    auto add = [&](int oc, float w) __attribute__((always_inline)) {
+      const bf16x8 hi = __builtin_bit_cast(bf16x8, g[2 * (int64_t)oc]);
+      const bf16x8 lo = __builtin_bit_cast(bf16x8, g[2 * (int64_t)oc + 1]);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s[q] += w * ((float)hi[q] + (float)lo[q]);
+    };
+#pragma unroll
+    for (int j = 0; j < kAdjReg; ++j)
+      if (j < ne) add(cl[j], wt[j]);
+    for (int e = e0 + kAdjReg; e < e1; ++e) add(vw.col[e], vw.val[e]);
+    const int nq = min(8, c1 - c);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < nq) {
+        float* d = gs + (int64_t)(c + q) * vw.sC;
+        *d = a.accumulate ? s[q] + *d : s[q];
+      }
   }
 }
 
@@ -826,12 +903,15 @@ int mvbev_warp_adjoint_plan(const float* m, int64_t H, int64_t W, int64_t Ho, in
   return MVBEV_OK;
 }
 
-int mvbev_warp_views_adjoint_f32(const mvbev_warp_adjoint_view* views, int nviews, int64_t B, int64_t C,
-                                 int64_t H, int64_t W, int64_t Ho, int64_t Wo, int accumulate, void* stream) {
+int mvbev_warp_views_adjoint(const mvbev_warp_adjoint_view* views, int nviews, int grad_out_layout, int64_t B,
+                             int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int accumulate,
+                             void* stream) {
   using namespace mvbev;
   if (!views) return MVBEV_ERR_NULL;
   if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 || nviews <= 0) return MVBEV_ERR_RANK;
   if (nviews > kWarpMaxViews || H * W >= INT32_MAX || 4 * Ho * Wo >= INT32_MAX) return MVBEV_ERR_SHAPE;
+  if (grad_out_layout != MVBEV_LAYOUT_F32 && grad_out_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;
+  const bool split = grad_out_layout == MVBEV_LAYOUT_SPLIT_BF16;
   bwd::AdjArgs a = {};
   for (int i = 0; i < nviews; ++i) {
     const mvbev_warp_adjoint_view& v = views[i];
@@ -840,6 +920,7 @@ int mvbev_warp_views_adjoint_f32(const mvbev_warp_adjoint_view* views, int nview
     if (v.grad_out_strides[3] != 1 || v.grad_out_strides[2] != Wo || v.grad_src_strides[3] != 1 ||
         v.grad_src_strides[2] != W)
       return MVBEV_ERR_STRIDE;
+    if (split && (reinterpret_cast<uintptr_t>(v.grad_out) & 15) != 0) return MVBEV_ERR_ALIGN;
     a.v[i] = bwd::AdjView{v.grad_out, v.grad_out_strides[0], v.grad_out_strides[1], v.grad_src,
                           v.grad_src_strides[0], v.grad_src_strides[1], v.row_ptr, v.col, v.val};
   }
@@ -851,7 +932,10 @@ int mvbev_warp_views_adjoint_f32(const mvbev_warp_adjoint_view* views, int nview
   const int64_t nwg = (int64_t)a.pblocks * a.chunks * nviews * B;
   if (nwg > INT32_MAX) return MVBEV_ERR_SHAPE;
   a.nwg = (int)nwg;
-  hipLaunchKernelGGL(bwd::warp_adjoint_kernel, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
+  if (split)
+    hipLaunchKernelGGL(bwd::warp_adjoint_split_kernel, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
+  else
+    hipLaunchKernelGGL(bwd::warp_adjoint_kernel, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }

@@ -506,32 +506,51 @@ class WarpAdjointPlan:
 
 def warp_views_adjoint(grad_outs, plans, grad_srcs, accumulate: bool = False) -> None:
     """Deterministic gather form of ``warp_views_backward``: ``grad_srcs[i]`` [B,C,H,W] =
-    (or += with ``accumulate``) the adjoint of view i's warp applied to ``grad_outs[i]``
-    [B,C,Ho,Wo]; ``plans[i]`` its ``WarpAdjointPlan``.  Rows/columns of both must be dense."""
+    (or += with ``accumulate``) the adjoint of view i's warp applied to ``grad_outs[i]``;
+    ``plans[i]`` its ``WarpAdjointPlan``.  ``grad_outs[i]``: fp32 [B,C,Ho,Wo] with dense rows,
+    or a bf16 split-bf16 blocked [B, C/8, Ho, Wo, 2, 8] view (``split_shape``; C % 8 == 0)."""
     n = len(grad_outs)
     if n == 0:
         return
     if not (len(plans) == n == len(grad_srcs)) or n > 16:
         raise ValueError("need 1..16 matching grad_outs / plans / grad_srcs")
     _require_cuda(*grad_outs, *grad_srcs)
-    B, C, Ho, Wo = grad_outs[0].shape
-    _, _, H, W = grad_srcs[0].shape
+    split = grad_outs[0].dtype == torch.bfloat16
+    B, C, H, W = grad_srcs[0].shape
+    if split:
+        if C % KC:
+            raise ValueError("a split grad_out needs C % 8 == 0")
+        Ho, Wo = grad_outs[0].shape[2], grad_outs[0].shape[3]
+        want = split_shape(B, C, Ho, Wo)
+    else:
+        Ho, Wo = grad_outs[0].shape[2], grad_outs[0].shape[3]
+        want = (B, C, Ho, Wo)
     arr = (_native.WarpAdjointView * n)()
     for i, (g, pl, d) in enumerate(zip(grad_outs, plans, grad_srcs)):
-        if tuple(g.shape) != (B, C, Ho, Wo) or tuple(d.shape) != (B, C, H, W):
-            raise ValueError(f"all views must share shapes: grad_out {tuple(g.shape)} grad_src {tuple(d.shape)}")
+        if tuple(g.shape) != want or tuple(d.shape) != (B, C, H, W):
+            raise ValueError(f"all views must share shapes: grad_out {tuple(g.shape)} (want {want}) "
+                             f"grad_src {tuple(d.shape)}")
         if pl.src_hw != (H, W) or pl.grid_hw != (Ho, Wo):
             raise ValueError("plan built for other sizes")
-        if g.dtype != torch.float32 or d.dtype != torch.float32:
-            raise TypeError("the warp adjoint is fp32")
-        if g.stride(3) != 1 or g.stride(2) != Wo or d.stride(3) != 1 or d.stride(2) != W:
-            raise ValueError("grad_out / grad_src planes must be dense (row stride = width, column stride 1)")
-        arr[i] = _native.WarpAdjointView(g.data_ptr(), (ctypes.c_int64 * 4)(*g.stride()), d.data_ptr(),
+        if d.dtype != torch.float32 or g.dtype != (torch.bfloat16 if split else torch.float32):
+            raise TypeError("grad_src is fp32; grad_out fp32 or split-bf16 (bf16 storage)")
+        if split:
+            if g.stride(5) != 1 or g.stride(4) != KC or g.stride(3) != 2 * KC or g.stride(2) != 2 * KC * Wo:
+                raise ValueError("split grad_out needs dense pixels")
+            gstr = (g.stride(0) // 16, g.stride(1) // 16, Wo, 1)  # 32-byte units
+        else:
+            if g.stride(3) != 1 or g.stride(2) != Wo:
+                raise ValueError("grad_out planes must be dense (row stride = width, column stride 1)")
+            gstr = tuple(g.stride())
+        if d.stride(3) != 1 or d.stride(2) != W:
+            raise ValueError("grad_src planes must be dense (row stride = width, column stride 1)")
+        arr[i] = _native.WarpAdjointView(g.data_ptr(), (ctypes.c_int64 * 4)(*gstr), d.data_ptr(),
                                          (ctypes.c_int64 * 4)(*d.stride()), pl.row_ptr.data_ptr(),
                                          pl.col.data_ptr(), pl.val.data_ptr())
-    st = _native.load().mvbev_warp_views_adjoint_f32(arr, n, B, C, H, W, Ho, Wo, int(bool(accumulate)),
-                                                     _stream(grad_srcs[0]))
-    _native.check(st, "mvbev_warp_views_adjoint_f32")
+    layout = _native.LAYOUT_SPLIT_BF16 if split else _native.LAYOUT_F32
+    st = _native.load().mvbev_warp_views_adjoint(arr, n, layout, B, C, H, W, Ho, Wo, int(bool(accumulate)),
+                                                 _stream(grad_srcs[0]))
+    _native.check(st, "mvbev_warp_views_adjoint")
 
 
 class PackedDgrad3x3:

@@ -65,7 +65,8 @@ def test_warp_backward_vs_grid_sample_autograd(B, C, H, W, ho, wo):
 
 
 @pytest.mark.parametrize("B,C,H,W,ho,wo", [(1, 5, 27, 48, 12, 36), (2, 37, 30, 41, 17, 23),
-                                           (1, 3, 9, 11, 20, 30), (1, 70, 90, 160, 120, 360)])
+                                           (1, 3, 9, 11, 20, 30), (1, 72, 90, 160, 120, 360),
+                                           (2, 16, 30, 41, 17, 23)])
 def test_warp_adjoint_gather_vs_grid_sample_autograd(B, C, H, W, ho, wo):
     """The CSR-gather adjoint (plan once per geometry): equals grid_sample's backward, is
     bitwise deterministic, overwrites or accumulates, and its plan holds one entry per
@@ -100,6 +101,12 @@ def test_warp_adjoint_gather_vs_grid_sample_autograd(B, C, H, W, ho, wo):
     ops.warp_views_adjoint(gdev, plans, again, accumulate=True)
     for a, o in zip(again, outs):
         assert torch.allclose(a, 2 * o, rtol=1e-6, atol=0)
+    if C % 8 == 0:  # grad_out in the split-bf16 layout the dgrad conv writes (hi + lo)
+        split = [_split_encode(g) for g in gdev]
+        outs_s = [torch.empty_like(o) for o in outs]
+        ops.warp_views_adjoint(split, plans, outs_s)
+        for i in range(n):
+            assert_parity(outs_s[i].cpu(), refs[i], f"adjoint gather (split grad_out) view {i}")
 
 
 def test_warp_backward_no_gradient_from_outside_samples():

@@ -283,6 +283,18 @@ int mvbev_pack_conv3x3_dgrad_bf16x3(const float* w, int64_t Cout_w, int64_t Cin_
                                     const int32_t* chan_map, int64_t K_out, void* w_packed,
                                     void* stream);
 
+/* The data-gradient conv itself: mvbev_conv3x3_bf16x3_ex over dy (fp32, desc as for a forward
+ * conv over [B][Cout_w][H][W]) with the dgrad packing, no bias / ReLU, dx in dx_layout
+ * (MVBEV_LAYOUT_F32 or MVBEV_LAYOUT_SPLIT_BF16), plus an output-side mask: with out_mask
+ * (device, one uint32 per output tile as group_mask of the _ex form), the tiles of output
+ * channel group g (cot_per_group consecutive 128-channel Cout tiles, e.g. one camera's
+ * channels) are skipped where bit g is clear — those dx entries are left unwritten, for a
+ * consumer that never reads them (the warp adjoint reads a view's gradient only where the
+ * view samples inside its source, which the frustum mask of mvbev_warp_tile_mask bounds). */
+int mvbev_conv3x3_dgrad_bf16x3(const float* dy, const mvbev_conv_desc* desc, const void* w_packed, int64_t Cout_p,
+                               int dilation, void* dx, int dx_layout, const uint32_t* out_mask,
+                               int64_t cot_per_group, void* stream);
+
 /* Weight gradient of mvbev_conv3x3_bf16x3 (3xbf16 MFMA, fp32 accumulation):
  *   dw[co][chan_map[k]][t] = sum_b,y,x dy[b][co][y][x] * x[b][k][y + (t/3-1)d][x + (t%3-1)d]
  * x as in the forward (desc: whole image, in_row0 = out_row0 = 0, in_rows = out_rows = H;

@@ -162,7 +162,9 @@ class ProjectFuseFunction(torch.autograd.Function):
             cp = st.dgrad1.cout_p
             if C % ops.KC == 0:  # split-bf16 dslab: the adjoint gathers 8 channels per 32-B entry
                 dslab = torch.empty(ops.split_shape(B, cp, H, W), dtype=torch.bfloat16, device=dev)
-                ops.conv3x3_dgrad(dy1, st.dgrad1, w1, 1, out=dslab)
+                # frustum: a view's tiles of dslab that its warp never samples are not computed
+                cm = engine.conv1_mask(dev, 0, H) if C % ops.BN == 0 else None
+                ops.conv3x3_dgrad(dy1, st.dgrad1, w1, 1, out=dslab, out_mask=cm, cot_per_group=C // ops.BN)
                 g8 = C // ops.KC
                 douts = [dslab[:, v * g8:(v + 1) * g8] for v in range(n)]
             else:

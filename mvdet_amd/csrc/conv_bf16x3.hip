@@ -121,6 +121,10 @@ struct Args {
   const int32_t* tile_order;
   int npix;
   bool y_split;  // y in the split-bf16 blocked layout (the next conv's 16-B staging copies)
+  // output-side mask (optional, dgrad of the fused conv): per output tile, bit g clear =
+  // output channel group g (cot_pg Cout tiles each) is never read, so its tiles are skipped
+  const uint32_t* cmask;
+  int cot_pg;
 };
 
 // Input tag: the split-bf16 blocked layout written by mvbev_warp_views_split_bf16 and by this
@@ -319,6 +323,8 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
   const int b = rest / a.tiles_y;
   const int x0 = tx * TW;
   const int y0 = a.out_row0 + ty * TH;
+  // output-side mask: a tile of output channels nobody reads (whole block, before any barrier)
+  if (a.cmask && !((a.cmask[ty * a.tiles_x + tx] >> (cot / a.cot_pg)) & 1u)) return;
   const u32x4* wsrc = a.wp + (int64_t)cot * W16;
   // frustum mask: iterate only the chunks of groups that can be non-zero in this tile
   const uint32_t gm = a.gmask ? a.gmask[ty * a.tiles_x + tx] : 0u;
@@ -586,7 +592,8 @@ template <typename TIn>
 static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
                   const float* bias, const float* init, int64_t Cout, int dilation, int relu,
                   float* y, int y_layout, const uint32_t* group_mask, const int32_t* tile_order,
-                  void* workspace, size_t ws_bytes, void* stream) {
+                  void* workspace, size_t ws_bytes, void* stream, const uint32_t* out_mask = nullptr,
+                  int cot_pg = 1) {
   if (!x || !d || !w_packed || !y) return MVBEV_ERR_NULL;
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || d->in_rows <= 0 ||
       d->out_rows <= 0 || d->group <= 0)
@@ -618,6 +625,10 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
     a.cpg = (int)(d->group / KC);
   }
   a.tile_order = group_mask ? tile_order : nullptr;
+  a.cmask = out_mask;
+  a.cot_pg = cot_pg;
+  if (out_mask && (cot_pg <= 0 || a.n_cot > 32 * cot_pg || group_mask)) return MVBEV_ERR_SHAPE;
+  if (out_mask) workspace = nullptr;  // skipped tiles never write split-K partial sums
   if (y_layout != MVBEV_LAYOUT_F32 && y_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;
   a.y_split = y_layout == MVBEV_LAYOUT_SPLIT_BF16;
   a.npix = (int)(tiles / a.n_cot);
@@ -730,6 +741,15 @@ int mvbev_conv3x3_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_desc* 
   return launch<float>(x, desc, w_packed, bias, init, Cout, dilation, relu,
                        static_cast<float*>(y), y_layout, group_mask, tile_order, workspace,
                        workspace_bytes, stream);
+}
+
+int mvbev_conv3x3_dgrad_bf16x3(const float* dy, const mvbev_conv_desc* desc, const void* w_packed, int64_t Cout_p,
+                               int dilation, void* dx, int dx_layout, const uint32_t* out_mask,
+                               int64_t cot_per_group, void* stream) {
+  using namespace mvbev::b3;
+  if (out_mask && (cot_per_group <= 0 || cot_per_group > 65536)) return MVBEV_ERR_SHAPE;
+  return launch<float>(dy, desc, w_packed, nullptr, nullptr, Cout_p, dilation, 0, static_cast<float*>(dx),
+                       dx_layout, nullptr, nullptr, nullptr, 0, stream, out_mask, (int)cot_per_group);
 }
 
 }  // extern "C"

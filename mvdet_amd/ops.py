@@ -595,18 +595,40 @@ class PackedDgrad3x3:
 
 
 def conv3x3_dgrad(dy: torch.Tensor, packed: PackedDgrad3x3, weight: torch.Tensor, dilation: int,
-                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  out: Optional[torch.Tensor] = None, out_mask: Optional[torch.Tensor] = None,
+                  cot_per_group: int = 1) -> torch.Tensor:
     """Data gradient of a 3x3 stride-1 conv (padding = dilation): dy [B,Cout_w,H,W] fp32
-    contiguous -> [B, cout_p, H, W] fp32 (channel o = forward input channel chan_map[o];
-    channels past k_out are zero).  Runs the forward bf16x3 conv kernel on the dgrad packing."""
+    contiguous -> [B, cout_p, H, W] fp32, or the split-bf16 layout when ``out`` is a bf16
+    ``split_shape`` tensor (channel o = forward input channel chan_map[o]; channels past
+    k_out are zero).  ``out_mask`` (int32 per conv output tile, ``warp_tile_mask``): tiles of
+    output channel group g (``cot_per_group`` 128-channel tiles) whose bit is clear are NOT
+    written (for a consumer that never reads them)."""
     _require_cuda(dy)
     if dy.dim() != 4 or dy.dtype != torch.float32 or not dy.is_contiguous():
         raise ValueError("dy must be a contiguous float32 [B,Cout,H,W] tensor")
     B, K, H, W = dy.shape
     if K != weight.shape[0]:
         raise ValueError(f"dy has {K} channels, the weight {weight.shape[0]} outputs")
+    cp = packed.cout_p
+    if out is None:
+        out = torch.empty((B, cp, H, W), dtype=torch.float32, device=dy.device)
+    split = out.dtype == torch.bfloat16
+    want = split_shape(B, cp, H, W) if split else (B, cp, H, W)
+    if tuple(out.shape) != want or not out.is_contiguous() or out.dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError(f"out must be a contiguous {'bf16' if split else 'fp32'} {want} tensor")
+    mp = None
+    if out_mask is not None:
+        _require_cuda(out_mask)
+        tiles = -(-H // _native.TILE_H) * -(-W // _native.TILE_W)
+        if out_mask.dtype != torch.int32 or out_mask.numel() < tiles or not out_mask.is_contiguous():
+            raise ValueError(f"out_mask must be a contiguous int32 tensor of >= {tiles} tiles")
+        mp = out_mask.data_ptr()
     d = conv_desc(B, K, H, W, group=K, group_stride=0, batch_stride=K * H * W)
-    return conv3x3_desc(dy, d, packed.get(weight), packed.cout_p, dilation=dilation, out=out)
+    st = _native.load().mvbev_conv3x3_dgrad_bf16x3(
+        dy.data_ptr(), ctypes.byref(d), packed.get(weight).data_ptr(), cp, int(dilation), out.data_ptr(),
+        _native.LAYOUT_SPLIT_BF16 if split else _native.LAYOUT_F32, mp, int(cot_per_group), _stream(dy))
+    _native.check(st, "mvbev_conv3x3_dgrad_bf16x3")
+    return out
 
 
 def conv3x3_wgrad(x: torch.Tensor, desc, dy: torch.Tensor, dilation: int, cin_w: int,

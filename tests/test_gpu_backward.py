@@ -189,6 +189,39 @@ def test_conv_dgrad_channel_map():
             assert_parity(got[:, o], ref[:, c], f"dgrad channel {o}")
 
 
+@pytest.mark.parametrize("split", [False, True])
+def test_conv_dgrad_output_mask(split):
+    """Output-side mask: tiles of a clear (tile, channel group) bit are skipped (left as they
+    were), every other tile equals the unmasked dgrad."""
+    from mvdet_amd import _native, ops
+    g = torch.Generator().manual_seed(5)
+    B, Cw, K, H, W = 2, 256, 512, 20, 70          # 4 output groups of 128 channels
+    w = torch.randn((Cw, K, 3, 3), generator=g) * 0.05
+    dy = torch.randn((B, Cw, H, W), generator=g).to(DEV)
+    pk = ops.PackedDgrad3x3(K)
+    ref = ops.conv3x3_dgrad(dy, pk, w.to(DEV), 1)
+    ty, tx = -(-H // _native.TILE_H), -(-W // _native.TILE_W)
+    mask = torch.randint(0, 16, (ty * tx,), generator=g, dtype=torch.int32)
+    if split:
+        out = torch.zeros(ops.split_shape(B, K, H, W), dtype=torch.bfloat16, device=DEV)
+        ops.conv3x3_dgrad(dy, pk, w.to(DEV), 1, out=out, out_mask=mask.to(DEV), cot_per_group=1)
+        got = ops.split_decode(out, K).cpu()
+    else:
+        got = torch.full((B, K, H, W), 7.0, device=DEV)
+        ops.conv3x3_dgrad(dy, pk, w.to(DEV), 1, out=got, out_mask=mask.to(DEV), cot_per_group=1)
+        got = got.cpu()
+    ref = ref.cpu()
+    for t in range(ty * tx):
+        r0, c0 = (t // tx) * _native.TILE_H, (t % tx) * _native.TILE_W
+        for gi in range(4):
+            blk = got[:, gi * 128:(gi + 1) * 128, r0:r0 + _native.TILE_H, c0:c0 + _native.TILE_W]
+            want = ref[:, gi * 128:(gi + 1) * 128, r0:r0 + _native.TILE_H, c0:c0 + _native.TILE_W]
+            if (int(mask[t]) >> gi) & 1:
+                assert_parity(blk, want, f"dgrad tile {t} group {gi}", normwise_tol=2e-5 if split else 1e-6)
+            else:
+                assert (blk == (0.0 if split else 7.0)).all()
+
+
 def test_bias_coord_relu_and_cout1_backward():
     from mvdet_amd import ops
     g = torch.Generator().manual_seed(11)
@@ -247,7 +280,8 @@ def _cpu_reference(feats, Ms, grid, params, gmap, masks=None):
 
 
 @pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
-@pytest.mark.parametrize("N,B,C,src,grid", [(2, 1, 8, (27, 48), (12, 36)), (3, 2, 13, (30, 41), (17, 45))])
+@pytest.mark.parametrize("N,B,C,src,grid", [(2, 1, 8, (27, 48), (12, 36)), (3, 2, 13, (30, 41), (17, 45)),
+                                             (2, 1, 128, (20, 30), (24, 96))])
 def test_project_fuse_backward_vs_cpu_autograd(precision, N, B, C, src, grid):
     """ProjectFuseFunction (HIP forward + HIP backward) vs torch-CPU autograd through the
     reference path (kornia restatement + cat + map_classifier) on identical inputs."""
@@ -257,6 +291,9 @@ def test_project_fuse_backward_vs_cpu_autograd(precision, N, B, C, src, grid):
     H, W = src
     ho, wo = grid
     Ms = [_rand_h(rng, H, W, ho, wo) for _ in range(N)]
+    if C % 128 == 0:  # each view covers part of the grid: the frustum masks skip tiles
+        Ms = [np.diag([0.45, 0.45, 1.0]) @ M + np.array([[0, 0, 40.0 * v], [0, 0, 0], [0, 0, 0]])
+              for v, M in enumerate(Ms)]
     feats = [torch.from_numpy(np.maximum(rng.standard_normal((B, C, H, W)), 0).astype(np.float32))
              for _ in range(N)]
     params = _head(N, C, seed=N + C)
@@ -268,6 +305,8 @@ def test_project_fuse_backward_vs_cpu_autograd(precision, N, B, C, src, grid):
                              torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False)).to(DEV)
     mc.load_state_dict({k.split(".", 1)[1]: v for k, v in params.items()})
     fg = [f.to(DEV).requires_grad_() for f in feats]
+    if C % 128 == 0 and precision == "bf16x3":
+        assert eng.conv1_active_fraction(DEV, 0, ho) < 0.9
     out = project_fuse(eng, fg, mc)
     ws = out.grad_fn.ws                      # the activations the backward will use
     m1, m2 = (ws.y1 > 0).float().cpu(), (ws.y2 > 0).float().cpu()

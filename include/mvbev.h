@@ -309,6 +309,17 @@ int mvbev_conv3x3_wgrad_bf16x3(const void* x, int x_layout, const mvbev_conv_des
                                int64_t Cin_w, float* dw, void* workspace, size_t workspace_bytes,
                                void* stream);
 
+/* Same, skipping the pixel chunks where an input-channel group (desc->group channels, a
+ * multiple of 64: one camera's slot of the fused slab) is exactly zero over the 3x3 window:
+ * chunk_list[chunk_off[g] .. chunk_off[g+1]) lists, ascending, the chunks (row segments of 32
+ * pixels, index (b * H + y) * ceil(W / 32) + x / 32) where group g can be non-zero (from the
+ * frustum mask of mvbev_warp_tile_mask with halo >= dilation).  Device int32 arrays. */
+int mvbev_conv3x3_wgrad_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_desc* desc,
+                                  const float* dy, int64_t Cout, int dilation, const int32_t* chan_map,
+                                  int64_t Cin_w, float* dw, const int32_t* chunk_list,
+                                  const int32_t* chunk_off, void* workspace, size_t workspace_bytes,
+                                  void* stream);
+
 /* db[co] = sum_b,p dy[b][co][p] (db may be NULL) and, when dw != NULL, the weight gradient of the
  * two coord channels (create_coord_map, persp_trans_detector.py:103-112) that are input channels
  * coord_ch, coord_ch + 1 of a conv of the given dilation: dw[co][coord_ch + j][t] (dw is

@@ -44,6 +44,7 @@ EXPORTS = (
     "mvbev_conv3x3_cout1_backward_f32",
     "mvbev_warp_adjoint_plan",
     "mvbev_conv3x3_dgrad_bf16x3",
+    "mvbev_conv3x3_wgrad_bf16x3_ex",
     "mvbev_warp_views_adjoint",
 )
 
@@ -148,6 +149,9 @@ def _declare(lib):
     lib.mvbev_conv3x3_cout1_backward_f32.restype = ctypes.c_int
     lib.mvbev_conv3x3_cout1_backward_f32.argtypes = [_p, _p, _p, _i64, _i64, _i64, _i64, ctypes.c_int,
                                                      ctypes.c_int, _p, _p, _p]
+    lib.mvbev_conv3x3_wgrad_bf16x3_ex.restype = ctypes.c_int
+    lib.mvbev_conv3x3_wgrad_bf16x3_ex.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _i64,
+                                                  ctypes.c_int, _p, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]
     lib.mvbev_conv3x3_dgrad_bf16x3.restype = ctypes.c_int
     lib.mvbev_conv3x3_dgrad_bf16x3.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _i64, ctypes.c_int, _p,
                                                ctypes.c_int, _p, _i64, _p]

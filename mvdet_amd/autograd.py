@@ -79,6 +79,22 @@ def _adjoint_plans(engine: ProjectFuse, st, device):
     return plans
 
 
+def _wgrad_lists(engine: ProjectFuse, st, device, B: int):
+    """Frustum chunk lists of conv1's wgrad (per camera slot), or None when not applicable."""
+    H, W = engine.grid_hw
+    if engine.Cs % 64 != 0:
+        return None
+    m = engine.conv1_mask(device, 0, H)
+    if m is None:
+        return None
+    if not hasattr(st, "lists"):
+        st.lists = {}
+    key = (str(device), B)
+    if key not in st.lists:
+        st.lists[key] = ops.wgrad_chunk_lists(m, engine.S, B, H, W)
+    return st.lists[key]
+
+
 def _wgrad_ws(st, desc, cout, device) -> torch.Tensor:
     import ctypes
     from . import _native
@@ -154,7 +170,7 @@ class ProjectFuseFunction(torch.autograd.Function):
         d1 = ops.conv_desc(B, engine.S * engine.Cs, H, W, group=engine.Cs, group_stride=B * engine.Cs * H * W,
                            batch_stride=engine.Cs * H * W)
         ops.conv3x3_wgrad(ws.slab, d1, dy1, 1, w1.shape[1], chan_map=engine.pack1._map_dev, dw=dw1,
-                          workspace=_wgrad_ws(st, d1, mid, dev))
+                          workspace=_wgrad_ws(st, d1, mid, dev), chunk_lists=_wgrad_lists(engine, st, dev, B))
         grads = [None] * n
         if need_feat:
             _mark("bwd_conv1_dgrad")

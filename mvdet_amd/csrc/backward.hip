@@ -61,6 +61,11 @@ struct WArgs {
   int group, K, Cout, B, H, W;
   int segs, nchunks, P, n_ct, n_kt, ntiles;
   bool vec_dy;  // W % 4 == 0 and dy 16-B aligned: dy rows as 16-B loads
+  // frustum (optional): per input-channel group (desc group = one camera's slot), the pixel
+  // chunks whose x window can be non-zero, clist[coff[g] .. coff[g+1]); a tile's partitions
+  // split its group's list instead of all chunks (skipped chunks contribute exactly 0)
+  const int32_t* clist;
+  const int32_t* coff;
 };
 
 struct SplitIn {};
@@ -106,8 +111,15 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const WArgs a) {
   const int lb = xcd_remap(blockIdx.x, a.P * a.ntiles);
   const int p = lb / a.ntiles, tile = lb - p * a.ntiles;
   const int ct = tile % a.n_ct, kt = tile / a.n_ct;
-  const int c0 = (int)((int64_t)a.nchunks * p / a.P);
-  const int c1 = (int)((int64_t)a.nchunks * (p + 1) / a.P);
+  const int32_t* list = nullptr;
+  int nact = a.nchunks;
+  if (a.clist) {
+    const int grp = (kt * NT) / a.group;
+    list = a.clist + a.coff[grp];
+    nact = a.coff[grp + 1] - a.coff[grp];
+  }
+  const int c0 = (int)((int64_t)nact * p / a.P);
+  const int c1 = (int)((int64_t)nact * (p + 1) / a.P);
   const int W = a.W, H = a.H;
   const int64_t plane = (int64_t)H * W;
 
@@ -116,7 +128,8 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const WArgs a) {
   float bfl[BPT][SPLIT ? 1 : 8];
   bool bok[BPT];
 
-  auto load = [&](int c) __attribute__((always_inline)) {
+  auto load = [&](int ci) __attribute__((always_inline)) {
+    const int c = list ? list[ci] : ci;
     const int R = c / a.segs, seg = c - R * a.segs;
     const int b = R / H, y = R - b * H;
     const int x0 = seg * PX;
@@ -758,6 +771,14 @@ size_t mvbev_conv3x3_wgrad_workspace_bytes(const mvbev_conv_desc* desc, int64_t 
 int mvbev_conv3x3_wgrad_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* d, const float* dy,
                                int64_t Cout, int dilation, const int32_t* chan_map, int64_t Cin_w,
                                float* dw, void* workspace, size_t workspace_bytes, void* stream) {
+  return mvbev_conv3x3_wgrad_bf16x3_ex(x, x_layout, d, dy, Cout, dilation, chan_map, Cin_w, dw, nullptr, nullptr,
+                                       workspace, workspace_bytes, stream);
+}
+
+int mvbev_conv3x3_wgrad_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_desc* d, const float* dy,
+                                  int64_t Cout, int dilation, const int32_t* chan_map, int64_t Cin_w,
+                                  float* dw, const int32_t* chunk_list, const int32_t* chunk_off,
+                                  void* workspace, size_t workspace_bytes, void* stream) {
   using namespace mvbev;
   using namespace mvbev::bwd;
   if (!x || !d || !dy || !dw || !workspace) return MVBEV_ERR_NULL;
@@ -779,6 +800,10 @@ int mvbev_conv3x3_wgrad_bf16x3(const void* x, int x_layout, const mvbev_conv_des
   a.segs = (int)ceil_div(d->W, PX); a.nchunks = (int)g.nchunks; a.P = g.P;
   a.n_ct = (int)(Cout / MT); a.n_kt = (int)ceil_div(d->K, NT); a.ntiles = (int)g.tiles;
   a.vec_dy = (d->W % 4 == 0) && ((reinterpret_cast<uintptr_t>(dy) & 15) == 0);
+  if ((chunk_list == nullptr) != (chunk_off == nullptr)) return MVBEV_ERR_NULL;
+  if (chunk_list && d->group % NT != 0) return MVBEV_ERR_SHAPE;  // a channel tile inside one group
+  a.clist = chunk_list;
+  a.coff = chunk_off;
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)(g.P * g.tiles)), block(NTH);
   const bool split = x_layout == MVBEV_LAYOUT_SPLIT_BF16;

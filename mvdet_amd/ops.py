@@ -631,9 +631,33 @@ def conv3x3_dgrad(dy: torch.Tensor, packed: PackedDgrad3x3, weight: torch.Tensor
     return out
 
 
+def wgrad_chunk_lists(mask: torch.Tensor, groups: int, B: int, H: int, W: int):
+    """Per channel group, the wgrad pixel chunks (row segments of 32 px) whose window the
+    frustum ``mask`` (``warp_tile_mask`` over rows [0, H), halo >= the conv's dilation) marks
+    as possibly non-zero -> (chunk_list, chunk_off) int32 device tensors."""
+    import numpy as np
+    tx = -(-W // _native.TILE_W)
+    segs = -(-W // 32)
+    assert segs == tx, "wgrad chunks are 32 px = one conv tile column"
+    m = np.asarray(mask.cpu().numpy(), dtype=np.int64) & 0xFFFFFFFF
+    rows = np.repeat(np.arange(H) // _native.TILE_H, segs) * tx + np.tile(np.arange(segs), H)  # per (y, seg)
+    per_img = m[rows]                                                    # [H * segs]
+    lists, off = [], [0]
+    for g in range(groups):
+        act = np.nonzero((per_img >> g) & 1)[0]
+        full = (np.arange(B)[:, None] * (H * segs) + act[None, :]).reshape(-1)
+        lists.append(full)
+        off.append(off[-1] + full.size)
+    lst = np.concatenate(lists) if lists else np.zeros(0, np.int64)
+    dev = mask.device
+    return (torch.tensor(lst, dtype=torch.int32, device=dev) if lst.size else torch.zeros(1, dtype=torch.int32,
+                                                                                          device=dev),
+            torch.tensor(off, dtype=torch.int32, device=dev))
+
+
 def conv3x3_wgrad(x: torch.Tensor, desc, dy: torch.Tensor, dilation: int, cin_w: int,
                   chan_map: Optional[torch.Tensor] = None, dw: Optional[torch.Tensor] = None,
-                  workspace: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  workspace: Optional[torch.Tensor] = None, chunk_lists=None) -> torch.Tensor:
     """Weight gradient of a 3x3 conv whose input ``x`` is addressed by ``desc`` (fp32, or the
     split-bf16 layout when ``x`` is bf16) and whose output gradient is ``dy`` [B,Cout,H,W] fp32:
     writes dw[co][chan_map[k]][:] (identity without a map) of a [Cout, cin_w, 3, 3] tensor
@@ -662,11 +686,12 @@ def conv3x3_wgrad(x: torch.Tensor, desc, dy: torch.Tensor, dilation: int, cin_w:
     need = int(lib.mvbev_conv3x3_wgrad_workspace_bytes(ctypes.byref(desc), cout))
     if workspace is None or workspace.numel() * workspace.element_size() < need:
         workspace = torch.empty((need + 3) // 4, dtype=torch.float32, device=dy.device)
-    st = lib.mvbev_conv3x3_wgrad_bf16x3(x.data_ptr(), layout, ctypes.byref(desc), dy.data_ptr(), cout,
-                                        int(dilation), None if chan_map is None else chan_map.data_ptr(),
-                                        cin_w, dw.data_ptr(), workspace.data_ptr(),
-                                        workspace.numel() * workspace.element_size(), _stream(dy))
-    _native.check(st, "mvbev_conv3x3_wgrad_bf16x3")
+    cl, co = (None, None) if chunk_lists is None else (chunk_lists[0].data_ptr(), chunk_lists[1].data_ptr())
+    st = lib.mvbev_conv3x3_wgrad_bf16x3_ex(x.data_ptr(), layout, ctypes.byref(desc), dy.data_ptr(), cout,
+                                           int(dilation), None if chan_map is None else chan_map.data_ptr(),
+                                           cin_w, dw.data_ptr(), cl, co, workspace.data_ptr(),
+                                           workspace.numel() * workspace.element_size(), _stream(dy))
+    _native.check(st, "mvbev_conv3x3_wgrad_bf16x3_ex")
     return dw
 
 

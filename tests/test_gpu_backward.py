@@ -159,6 +159,39 @@ def test_conv_wgrad_grouped_slab_with_channel_map():
         assert (dw[:, S * C:] == 9.0).all()
 
 
+@pytest.mark.parametrize("split", [False, True])
+def test_conv_wgrad_frustum_chunk_lists(split):
+    """conv1's wgrad with per-group chunk lists from a frustum mask: skipping the chunks whose
+    window is exactly zero leaves the gradient unchanged."""
+    from mvdet_amd import _native, ops
+    g = torch.Generator().manual_seed(21)
+    S, B, Cs, H, W = 3, 2, 64, 37, 100
+    slab = F.relu(torch.randn((S, B, Cs, H, W), generator=g))
+    rects = [(0, 12, 0, 40), (10, 37, 30, 100), (5, 9, 60, 75)]     # each camera's footprint
+    for s_, (r0, r1, c0, c1) in enumerate(rects):
+        keep = torch.zeros((H, W))
+        keep[r0:r1, c0:c1] = 1
+        slab[s_] *= keep
+    th, tw = _native.TILE_H, _native.TILE_W
+    ty, tx = -(-H // th), -(-W // tw)
+    mask = torch.zeros(ty * tx, dtype=torch.int32)
+    for t in range(ty * tx):
+        y0, x0 = (t // tx) * th, (t % tx) * tw
+        win = slab[:, :, :, max(0, y0 - 1):y0 + th + 1, max(0, x0 - 1):x0 + tw + 1]
+        mask[t] = sum(1 << s_ for s_ in range(S) if (win[s_] != 0).any())
+    assert (mask != 7).any()
+    dy = torch.randn((B, 128, H, W), generator=g)
+    cin = S * Cs
+    x = torch.cat([slab[s_] for s_ in range(S)], 1)
+    ref = torch.nn.grad.conv2d_weight(x.double(), (128, cin, 3, 3), dy.double(), padding=1)
+    d = ops.conv_desc(B, S * Cs, H, W, group=Cs, group_stride=B * Cs * H * W, batch_stride=Cs * H * W)
+    lists = ops.wgrad_chunk_lists(mask.to(DEV), S, B, H, W)
+    assert lists[1][-1].item() < B * H * tx * S
+    xs = torch.stack([_split_encode(slab[s_].to(DEV)) for s_ in range(S)]) if split else slab.to(DEV)
+    got = ops.conv3x3_wgrad(xs, d, dy.to(DEV), 1, cin, chunk_lists=lists)
+    assert_parity(got.cpu(), ref, "wgrad with chunk lists")
+
+
 @pytest.mark.parametrize("B,Cw,K,H,W,dil", [(1, 128, 40, 12, 36, 1), (2, 512, 512, 17, 37, 2),
                                             (1, 256, 200, 9, 64, 1)])
 def test_conv_dgrad_vs_torch(B, Cw, K, H, W, dil):

@@ -252,6 +252,95 @@ def run_plus_a4(args, precision, steps, warmup):
     return out
 
 
+def torch_warp(feat, m, ho, wo):
+    """kornia steps 3-6 in stock torch GPU ops (autograd through grid_sample): the reference's
+    own op sequence on the GPU, used as the training-step comparison."""
+    import torch.nn.functional as F
+    B = feat.shape[0]
+    xs = (torch.linspace(0, wo - 1, wo, device=feat.device) / (wo - 1) - 0.5) * 2
+    ys = (torch.linspace(0, ho - 1, ho, device=feat.device) / (ho - 1) - 0.5) * 2
+    gy, gx = torch.meshgrid(ys, xs, indexing="ij")
+    pts = torch.stack([gx, gy, torch.ones_like(gx)], -1) @ m.T
+    z = pts[..., 2:]
+    scale = torch.where(z.abs() > 1e-8, 1.0 / (z + 1e-8), torch.ones_like(z))
+    grid = (scale * pts[..., :2]).unsqueeze(0).expand(B, ho, wo, 2)
+    return F.grid_sample(feat, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
+
+
+def run_train_step(config: int, precision: str, steps: int, warmup: int, with_torch: bool):
+    """Training step of the hot path: forward + backward of warp + concat +
+    fusion head over one frame batch (inputs resident in HBM; gradients w.r.t. the upsampled view
+    features and every head parameter), as ``trainer.py:38-47`` runs it.  "native" =
+    ``autograd.ProjectFuseFunction`` (HIP forward and backward); "torch_gpu" = the reference's
+    own op sequence on this GPU (grid_sample + cat + nn.Conv2d under autograd, MIOpen)."""
+    from mvdet_amd import ProjectFuse, autograd, synthetic
+    from mvdet_amd.geometry import projection_matrices
+    spec = synthetic.CONFIGS[config]
+    ds = spec["make"]()
+    B, C, N = spec["B"], spec["C"], ds.num_cam
+    up = tuple(ds.upsample_shape)
+    ho, wo = ds.reducedgrid_shape
+    dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+    pm = projection_matrices(ds)
+    mc = build_mc(C, N, head_params(N, config, C), dev)
+    eng = ProjectFuse(pm, up, (ho, wo), C, precision=precision)
+    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=v, device=dev).requires_grad_()
+             for v in range(N)]
+    gmap = torch.randn((B, 1, ho, wo), device=dev)
+    res = {"workload": f"cfg{config}: {spec['name']}", "precision": precision}
+
+    def run(step, K, W, hook_stages=False):
+        for _ in range(W):
+            step()
+        torch.cuda.synchronize()
+        evs = []
+        t0 = time.perf_counter()
+        for _ in range(K):
+            marks = {}
+            if hook_stages:
+                autograd.set_stage_hook(
+                    lambda s: marks.setdefault(s, torch.cuda.Event(enable_timing=True)).record())
+            step()
+            autograd.set_stage_hook(None)
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            marks["end"] = e
+            evs.append(marks)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        out = {"value": round(B * K / dt, 3), "unit": "frames/s", "ms_per_step": round(dt * 1e3 / K, 3)}
+        if hook_stages:
+            names = [s for s in evs[0] if s not in ("end", "bwd_end")]
+            st = {}
+            for a, b in zip(names, names[1:] + ["end"]):
+                st[a] = round(float(np.mean([m[a].elapsed_time(m[b]) for m in evs])), 4)
+            out["stages_ms"] = st
+        return out
+
+    def native_step():
+        for f in feats:
+            f.grad = None
+        mc.zero_grad(set_to_none=True)
+        autograd.project_fuse(eng, feats, mc).backward(gmap)
+
+    res["native"] = run(native_step, steps, warmup, hook_stages=True)
+    if with_torch:
+        ms = [eng.m_norm_cpu[v].to(dev) for v in range(N)]
+        cmap = torch.from_numpy(np.stack(np.meshgrid(np.arange(wo) / (wo - 1) * 2 - 1,
+                                                     np.arange(ho) / (ho - 1) * 2 - 1), 0)).float()[None].to(dev)
+
+        def torch_step():
+            for f in feats:
+                f.grad = None
+            mc.zero_grad(set_to_none=True)
+            world = [torch_warp(f, m, ho, wo) for f, m in zip(feats, ms)]
+            mc(torch.cat(world + [cmap.repeat(B, 1, 1, 1)], 1)).backward(gmap)
+
+        res["torch_gpu"] = run(torch_step, max(2, steps // 4), 1)
+        res["speedup_vs_torch_gpu"] = round(res["native"]["value"] / res["torch_gpu"]["value"], 2)
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -263,6 +352,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-alt", action="store_true", help="skip the other-precision comparison line")
     ap.add_argument("--cpu-frames", type=int, default=0, help="frames for the CPU baseline (0 = auto)")
+    ap.add_argument("--no-train", action="store_true", help="skip the training-step (forward+backward) line")
+    ap.add_argument("--train-torch", type=int, default=1,
+                    help="1 = also time the reference op sequence (torch GPU autograd) for the training step")
     ap.add_argument("--mp-mode", default="partial", choices=["partial", "gather"],
                     help="N>1: conv1 partial sums + reduce-scatter (default) or slab all-gather + row bands")
     args = ap.parse_args()
@@ -298,6 +390,9 @@ def main():
         result["speedup_vs_cpu"] = round(res["value"] / result["cpu_baseline"]["value"], 1)
     if args.config != 4:  # the fused upsample+warp writes fp32 / split slabs (not the fp16 slab)
         result["plus_a4"] = run_plus_a4(args, args.precision, max(5, args.steps // 2), 2)
+    if not args.no_train and args.config != 4:
+        result["train_step"] = run_train_step(args.config, args.precision, max(5, args.steps // 2), 2,
+                                              with_torch=bool(args.train_torch))
     if not args.no_alt:
         other = "fp32" if args.precision == "bf16x3" else "bf16x3"
         alt = run_single(args, other, max(3, args.steps // 2), 2, with_cpu=False)

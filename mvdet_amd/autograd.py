@@ -47,10 +47,11 @@ def _mark(stage: str) -> None:
 def _train_workspace(engine: ProjectFuse, B: int, device) -> Workspace:
     """A fresh (never reused) forward workspace with fp32 y1 (the ReLU mask source)."""
     H, W = engine.grid_hw
-    if engine.split:
-        slab = torch.zeros((engine.S,) + ops.split_shape(B, engine.Cs, H, W), dtype=torch.bfloat16, device=device)
+    if engine.split:  # the split warp writes every 8-channel group in full (zeros past C)
+        slab = torch.empty((engine.S,) + ops.split_shape(B, engine.Cs, H, W), dtype=torch.bfloat16, device=device)
     else:
-        slab = torch.zeros((engine.S, B, engine.Cs, H, W), dtype=engine.slab_dtype, device=device)
+        slab = torch.empty((engine.S, B, engine.Cs, H, W), dtype=engine.slab_dtype, device=device)
+        slab[:, :, engine.C:].zero_()  # padding channels the warp does not write
     y1r, y2r = band_rows(0, H, H)
     y1 = torch.empty((B, engine.mid, H, W), dtype=torch.float32, device=device)
     y2 = torch.empty((B, engine.mid, H, W), dtype=torch.float32, device=device)

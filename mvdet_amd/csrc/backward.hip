@@ -282,9 +282,9 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int P, int Cou
 }
 
 // ---------------------------------------------------------------------------------------------
-// block-wide sum of NV values per thread (256 threads), result valid in thread 0
-template <int NV>
-__device__ inline void block_sum(float (&v)[NV], float* red /* LDS [4][NV] */) {
+// block-wide sum of NV values per thread (NWV waves), result valid in thread 0; fixed order
+template <int NV, int NWV_>
+__device__ inline void block_sum(float (&v)[NV], float* red /* LDS [NWV_][NV] */) {
 #pragma unroll
   for (int j = 0; j < NV; ++j)
 #pragma unroll
@@ -296,42 +296,73 @@ __device__ inline void block_sum(float (&v)[NV], float* red /* LDS [4][NV] */) {
   __syncthreads();
   if (threadIdx.x == 0)
 #pragma unroll
-    for (int j = 0; j < NV; ++j) v[j] = red[j] + red[NV + j] + red[2 * NV + j] + red[3 * NV + j];
+    for (int j = 0; j < NV; ++j) {
+      float t = 0.f;
+      for (int w = 0; w < NWV_; ++w) t += red[w * NV + j];
+      v[j] = t;
+    }
 }
+
+// The per-channel reductions below (one workgroup per output channel, 512 of them at the
+// reference's widths) use 1024-thread workgroups so each CU holds 16+ waves of independent
+// streaming loads; the coord values come from LDS tables (create_coord_map's float64
+// formula, cast to fp32, evaluated once per row / column instead of per tap).
+constexpr int kRedThreads = 1024;
+constexpr int kRedWaves = kRedThreads / 64;
+constexpr int kCoordTab = 4096;  // max H, W for the coord tables (larger grids: no dw)
 
 // db[co] = sum dy[b][co][:]; with dw, the two coord channels (create_coord_map,
 // persp_trans_detector.py:103-112, channels coord_ch and coord_ch + 1 of the conv input):
 // dw[co][coord_ch + j][t] = sum_p dy[co][p] * coord_j(p + s_t), zero outside the grid.
-__global__ __launch_bounds__(256) void bias_coord_grad_kernel(const float* __restrict__ dy, int B, int Cout,
-                                                              int H, int W, int dil, float* db, float* dw,
-                                                              int Cin_w, int coord_ch) {
-  __shared__ float red[4 * 19];
+__global__ __launch_bounds__(kRedThreads) void bias_coord_grad_kernel(const float* __restrict__ dy, int B, int Cout,
+                                                                      int H, int W, int dil, float* db, float* dw,
+                                                                      int Cin_w, int coord_ch) {
+  __shared__ float red[kRedWaves * 19];
+  __shared__ float tcx[kCoordTab], tcy[kCoordTab];
   const int co = blockIdx.x;
+  if (dw) {
+    for (int i = threadIdx.x; i < W; i += kRedThreads) tcx[i] = (float)((double)i / (double)(W - 1) * 2.0 - 1.0);
+    for (int i = threadIdx.x; i < H; i += kRedThreads) tcy[i] = (float)((double)i / (double)(H - 1) * 2.0 - 1.0);
+    __syncthreads();
+  }
   float v[19];
 #pragma unroll
   for (int j = 0; j < 19; ++j) v[j] = 0.f;
   const int HW = H * W;
   for (int b = 0; b < B; ++b) {
     const float* g = dy + ((int64_t)b * Cout + co) * HW;
-    for (int q = threadIdx.x; q < HW; q += 256) {
+    if (!dw) {
+      float a4[4] = {0.f, 0.f, 0.f, 0.f};
+      int q = threadIdx.x;
+      for (; q + 3 * kRedThreads < HW; q += 4 * kRedThreads)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a4[u] += g[q + u * kRedThreads];
+      for (; q < HW; q += kRedThreads) a4[0] += g[q];
+      v[0] += (a4[0] + a4[1]) + (a4[2] + a4[3]);
+      continue;
+    }
+#pragma unroll 2
+    for (int q = threadIdx.x; q < HW; q += kRedThreads) {
       const float gv = g[q];
       v[0] += gv;
-      if (dw) {
-        const int y = q / W, x = q - y * W;
+      const int y = q / W, x = q - y * W;
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const int yy = y + (t / 3 - 1) * dil, xx = x + (t % 3 - 1) * dil;
-          if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
-            const float cx = (float)((double)xx / (double)(W - 1) * 2.0 - 1.0);
-            const float cy = (float)((double)yy / (double)(H - 1) * 2.0 - 1.0);
-            v[1 + t] += gv * cx;
-            v[10 + t] += gv * cy;
-          }
+      for (int k = 0; k < 3; ++k) {
+        const int xx = x + (k - 1) * dil, yy = y + (k - 1) * dil;
+        const bool okx = xx >= 0 && xx < W, oky = yy >= 0 && yy < H;
+        const float cx = okx ? tcx[okx ? xx : 0] : 0.f;
+        const float cy = oky ? tcy[oky ? yy : 0] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {  // tap t = 3 r + k (x offset k) and t = 3 k + r (y offset k)
+          const int yr = y + (r - 1) * dil, xr = x + (r - 1) * dil;
+          const bool oky_r = yr >= 0 && yr < H, okx_r = xr >= 0 && xr < W;
+          v[1 + 3 * r + k] += (okx && oky_r) ? gv * cx : 0.f;
+          v[10 + 3 * k + r] += (oky && okx_r) ? gv * cy : 0.f;
         }
       }
     }
   }
-  block_sum<19>(v, red);
+  block_sum<19, kRedWaves>(v, red);
   if (threadIdx.x == 0) {
     if (db) db[co] = v[0];
     if (dw)
@@ -386,9 +417,10 @@ __global__ __launch_bounds__(256) void cout1_dgrad_kernel(const float* __restric
 }
 
 // conv3 weight gradient: dw[c][t] = sum_b sum_q x[b][c][q] * dmap[b][q - s_t]
-__global__ __launch_bounds__(256) void cout1_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dmap,
-                                                          int B, int C, int H, int W, int dil, float* __restrict__ dw) {
-  __shared__ float red[4 * 9];
+__global__ __launch_bounds__(kRedThreads) void cout1_wgrad_kernel(const float* __restrict__ x,
+                                                                  const float* __restrict__ dmap, int B, int C, int H,
+                                                                  int W, int dil, float* __restrict__ dw) {
+  __shared__ float red[kRedWaves * 9];
   const int c = blockIdx.x;
   const int HW = H * W;
   float v[9];
@@ -397,7 +429,8 @@ __global__ __launch_bounds__(256) void cout1_wgrad_kernel(const float* __restric
   for (int b = 0; b < B; ++b) {
     const float* xc = x + ((int64_t)b * C + c) * HW;
     const float* d = dmap + (int64_t)b * HW;
-    for (int q = threadIdx.x; q < HW; q += 256) {
+#pragma unroll 2
+    for (int q = threadIdx.x; q < HW; q += kRedThreads) {
       const float xv = xc[q];
       const int y = q / W, xx = q - y * W;
 #pragma unroll
@@ -407,7 +440,7 @@ __global__ __launch_bounds__(256) void cout1_wgrad_kernel(const float* __restric
       }
     }
   }
-  block_sum<9>(v, red);
+  block_sum<9, kRedWaves>(v, red);
   if (threadIdx.x == 0)
 #pragma unroll
     for (int t = 0; t < 9; ++t) dw[c * 9 + t] = v[t];
@@ -833,7 +866,8 @@ int mvbev_conv3x3_bias_coord_grad_f32(const float* dy, int64_t B, int64_t Cout, 
   if (H * W > INT32_MAX || Cout > 65535 * 16) return MVBEV_ERR_SHAPE;
   if (dw && (coord_ch < 0 || coord_ch + 2 > Cin_w)) return MVBEV_ERR_SHAPE;
   if (dilation < 1) return MVBEV_ERR_DILATION;
-  hipLaunchKernelGGL(bwd::bias_coord_grad_kernel, dim3((unsigned)Cout), dim3(256), 0, as_stream(stream), dy,
+  if (dw && (H > bwd::kCoordTab || W > bwd::kCoordTab)) return MVBEV_ERR_SHAPE;
+  hipLaunchKernelGGL(bwd::bias_coord_grad_kernel, dim3((unsigned)Cout), dim3(bwd::kRedThreads), 0, as_stream(stream), dy,
                      (int)B, (int)Cout, (int)H, (int)W, dilation, db, dw, (int)Cin_w, (int)coord_ch);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
@@ -866,7 +900,7 @@ int mvbev_conv3x3_cout1_backward_f32(const float* x, const float* w, const float
     MVBEV_CHECK_LAUNCH();
   }
   if (dw) {
-    hipLaunchKernelGGL(bwd::cout1_wgrad_kernel, dim3((unsigned)C), dim3(256), 0, s, x, dmap, (int)B, (int)C,
+    hipLaunchKernelGGL(bwd::cout1_wgrad_kernel, dim3((unsigned)C), dim3(bwd::kRedThreads), 0, s, x, dmap, (int)B, (int)C,
                        (int)H, (int)W, dilation, dw);
     MVBEV_CHECK_LAUNCH();
   }

@@ -355,8 +355,10 @@ def main():
     ap.add_argument("--no-train", action="store_true", help="skip the training-step (forward+backward) line")
     ap.add_argument("--train-torch", type=int, default=1,
                     help="1 = also time the reference op sequence (torch GPU autograd) for the training step")
-    ap.add_argument("--mp-mode", default="partial", choices=["partial", "gather"],
-                    help="N>1: conv1 partial sums + reduce-scatter (default) or slab all-gather + row bands")
+    ap.add_argument("--mp-mode", default="frames", choices=["frames", "partial", "gather"],
+                    help="N>1 `value`: frame-parallel (default: each rank its own frames, no collective) or the "
+                         "view-parallel modes (conv1 partial sums + reduce-scatter / slab all-gather + row bands); "
+                         "the other modes are reported alongside")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -267,7 +267,8 @@ class ViewPartialSum(ViewParallel):
 
 
 def bench_main(args) -> None:
-    """``bench.py`` under torchrun with WORLD_SIZE > 1: the view-parallel path (RCCL)."""
+    """``bench.py`` under torchrun with WORLD_SIZE > 1: frame-parallel (default, ``value``) and the
+    view-parallel paths of the north star (RCCL), each timed with barrier + max over ranks."""
     import json
     import os
     import time
@@ -296,6 +297,44 @@ def bench_main(args) -> None:
     mc = build_mc(C, N, head_params(N, seed=args.config, C=C), dev)
 
     def run(mode):
+        if mode == "frames":  # frame-parallel: each rank fuses its own frame batch, no collective
+            eng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision)
+            feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up,
+                                                  seed=1000 * args.config + 100 * rank + v, device=dev)
+                     for v in range(N)]
+            ws = eng.workspace(B, dev)
+            stages = ("warp", "conv1", "conv2", "conv3")
+            K, W = args.steps, args.warmup
+            ev = {k: [torch.cuda.Event(enable_timing=True) for _ in range(K)] for k in stages}
+            end = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+
+            def fstep(mark=None):
+                if mark:
+                    mark("warp")
+                eng.warp_views(ws, list(range(N)), feats)
+                return eng.fuse(ws, mc, mark=mark)
+
+            with torch.no_grad():
+                for _ in range(W):
+                    fstep()
+                torch.cuda.synchronize()
+                dist.barrier()
+                t0 = time.perf_counter()
+                for i in range(K):
+                    fstep(mark=lambda s: ev[s][i].record())
+                    end[i].record()
+                torch.cuda.synchronize()
+                dist.barrier()
+                dt = time.perf_counter() - t0
+            t = torch.tensor([dt], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+            nxt = {stages[i]: stages[i + 1] for i in range(len(stages) - 1)}
+            stage_ms = {st: round(float(np.mean([ev[st][i].elapsed_time((ev[nxt[st]] if st in nxt else end)[i])
+                                                 for i in range(K)])), 4) for st in stages}
+            conv1_tfs = 2.0 * B * ho * wo * 9 * N * C * 512 / (stage_ms["conv1"] * 1e-3) / 1e12
+            return dict(value=round(world * B * K / dt, 3), ms=round(dt * 1e3 / K, 4), stage_ms=stage_ms,
+                        band=(0, ho), conv1_tfs=conv1_tfs)
         if mode == "partial":
             vp = ViewPartialSum(lambda sv: ProjectFuse(pm, up, (ho, wo), C, slot_views=sv, precision=args.precision,
                                                        all_views=False), pm, (ho, wo), rank, world)
@@ -339,15 +378,17 @@ def bench_main(args) -> None:
         return dict(value=round(B * K / dt, 3), ms=round(dt * 1e3 / K, 4), stage_ms=stage_ms, band=vp.band,
                     conv1_tfs=conv1_tfs)
 
-    mode = getattr(args, "mp_mode", "partial")
+    mode = getattr(args, "mp_mode", "frames")
     res = run(mode)
-    alt_mode = "gather" if mode == "partial" else "partial"
-    alt = None if getattr(args, "no_alt", False) else run(alt_mode)
+    others = [m for m in ("frames", "partial", "gather") if m != mode]
+    alts = {} if getattr(args, "no_alt", False) else {m: run(m) for m in others}
     bf16 = args.precision == "bf16x3"
     achieved = res["conv1_tfs"] * (3 if bf16 else 1)
     peak = BF16_MFMA_PEAK_TFS if bf16 else FP32_MFMA_PEAK_TFS
-    how = (f"views' conv1 partial sums, {backend} reduce-scatter by row band + edge-row all-gather"
-           if mode == "partial" else f"{backend} all-gather of the warped slab + row-band fusion")
+    hows = {"frames": f"frame-parallel x{world}: each rank fuses its own frame batch (all views), no collective",
+            "partial": f"view-parallel x{world} ({backend}): views' conv1 partial sums, reduce-scatter by row band "
+                       "+ edge-row all-gather",
+            "gather": f"view-parallel x{world} ({backend}): all-gather of the warped slab + row-band fusion"}
     if rank == 0:
         line = {
             "metric": "multi-view frames/sec (project+fuse)",
@@ -358,23 +399,26 @@ def bench_main(args) -> None:
             "warmup": args.warmup,
             "ms_per_step": res["ms"],
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if mode == "frames" else "strong",
             "vs_baseline": None,
             "dtype": DTYPE_LABEL[args.precision],
             "data": "synthetic (see single-GPU line)",
-            "config": {"workload": f"cfg{args.config}: {spec['name']}", "views": N, "channels": C, "batch": B,
+            "config": {"workload": f"cfg{args.config}: {spec['name']}", "views": N, "channels": C,
+                       "batch": B * (world if mode == "frames" else 1), "batch_per_rank": B if mode == "frames" else None,
                        "src_hw": list(up), "grid_hw": [ho, wo], "precision": args.precision,
-                       "parallelism": f"view-parallel x{world} ({backend}): {how}"},
-            "roofline": {"kernel": "conv1 on rank 0 (" + ("partial over its views" if mode == "partial"
-                                                           else "row band + halo") + ")",
+                       "parallelism": hows[mode]},
+            "roofline": {"kernel": "conv1 on rank 0" + {"frames": " (all views, whole grid)",
+                                                       "partial": " (partial over its views)",
+                                                       "gather": " (row band + halo)"}[mode],
                          "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                          "frac": round(achieved / peak, 4), "traffic": None},
             "stages_ms_rank0": res["stage_ms"],
             "band_rank0": list(res["band"]),
         }
-        if alt is not None:
-            line["alt_mode"] = {"mode": alt_mode, "value": alt["value"], "ms_per_step": alt["ms"],
-                                "stages_ms_rank0": alt["stage_ms"]}
+        for m, r in alts.items():
+            key = "frame_parallel" if m == "frames" else f"view_parallel_{m}"
+            line[key] = {"value": r["value"], "ms_per_step": r["ms"], "scaling": "weak" if m == "frames" else "strong",
+                         "parallelism": hows[m], "stages_ms_rank0": r["stage_ms"]}
         print(json.dumps(line), flush=True)
     dist.barrier()
     dist.destroy_process_group()

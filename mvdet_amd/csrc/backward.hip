@@ -451,6 +451,7 @@ __global__ __launch_bounds__(kRedThreads) void cout1_wgrad_kernel(const float* _
 // then for every channel of the block's slice 4 atomic adds into the source gradient.  No
 // gradient flows from a pixel whose sample point is outside (zero padding) or non-finite.
 // WarpView here: src = grad_out ([B][C][Ho][Wo], strides sB..sW), dst = grad_src (dB, dC, dH, 1).
+constexpr int kBwTH = 16, kBwTW = 16, kBwWR = 4, kBwCPB = 64;  // tiling of the atomic adjoint
 __global__ __launch_bounds__(256) void warp_backward_kernel(const WarpArgs a) {
   const int lb = xcd_remap(blockIdx.x, a.nwg);
   const int tile = lb % a.tiles;
@@ -460,10 +461,10 @@ __global__ __launch_bounds__(256) void warp_backward_kernel(const WarpArgs a) {
   const int b = bv / a.nviews;
   const WarpView& vw = a.v[view];
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
-  constexpr int WC = 64 / kWarpWR, WAVES_X = kWarpTW / WC;
+  constexpr int WC = 64 / kBwWR, WAVES_X = kBwTW / WC;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int v = ty * kWarpTH + (wave / WAVES_X) * kWarpWR + lane / WC;
-  const int u = tx * kWarpTW + (wave % WAVES_X) * WC + lane % WC;
+  const int v = ty * kBwTH + (wave / WAVES_X) * kBwWR + lane / WC;
+  const int u = tx * kBwTW + (wave % WAVES_X) * WC + lane % WC;
   if (v >= a.Ho || u >= a.Wo) return;
   const int H = a.H, W = a.W;
   float m[9];
@@ -486,8 +487,8 @@ __global__ __launch_bounds__(256) void warp_backward_kernel(const WarpArgs a) {
   const float* go = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB + (int64_t)v * vw.sH +
                     (int64_t)u * vw.sW;
   float* gs = static_cast<float*>(vw.dst) + (int64_t)b * vw.dB;
-  const int c_begin = chunk * kWarpCPB;
-  const int c_end = min(a.C, c_begin + kWarpCPB);
+  const int c_begin = chunk * kBwCPB;
+  const int c_end = min(a.C, c_begin + kBwCPB);
   constexpr int U = 4;
   int c = c_begin;
   auto scatter = [&](int ch, float g) __attribute__((always_inline)) {
@@ -926,9 +927,9 @@ int mvbev_warp_views_backward_f32(const mvbev_warp_view* views, int nviews, int6
   }
   a.nviews = nviews;
   a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
-  a.tiles_x = (int)ceil_div(Wo, kWarpTW);
-  a.tiles = a.tiles_x * (int)ceil_div(Ho, kWarpTH);
-  a.chunks = (int)ceil_div(C, kWarpCPB);
+  a.tiles_x = (int)ceil_div(Wo, mvbev::bwd::kBwTW);
+  a.tiles = a.tiles_x * (int)ceil_div(Ho, mvbev::bwd::kBwTH);
+  a.chunks = (int)ceil_div(C, mvbev::bwd::kBwCPB);
   const int64_t nwg = (int64_t)a.tiles * a.chunks * B * nviews;
   if (nwg > INT32_MAX) return MVBEV_ERR_SHAPE;
   a.nwg = (int)nwg;

@@ -109,14 +109,19 @@ __global__ __launch_bounds__(256) void warp_tile_kernel(const WarpArgs a) {
   if constexpr (SPLIT) {
     u32x4_t* out = static_cast<u32x4_t*>(vw.dst) + 2 * ((int64_t)b * vw.dB + (int64_t)v * vw.dH + u);
     const int64_t dG = 2 * vw.dC;
-    for (int g = c_begin / 8; g * 8 < c_end; ++g) {
-      float vals[8];
+    constexpr int GU = MVBEV_WARP_GU;
+    for (int g0 = c_begin / 8; g0 * 8 < c_end; g0 += GU) {
+      float vals[GU][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = g * 8 + j;
-        vals[j] = c < c_end ? (inside ? sample(c) : fill) : 0.f;
-      }
-      store_split8(out + g * dG, vals);
+      for (int k = 0; k < GU; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int c = (g0 + k) * 8 + j;
+          vals[k][j] = c < c_end ? (inside ? sample(c) : fill) : 0.f;
+        }
+#pragma unroll
+      for (int k = 0; k < GU; ++k)
+        if ((g0 + k) * 8 < c_end) store_split8(out + (g0 + k) * dG, vals[k]);
     }
     return;
   } else {

@@ -5,15 +5,42 @@
 
 namespace mvbev {
 
-#ifndef MVBEV_WARP_TH  // A/B on cfg2 (7 views, 1 launch): 8x32/2 0.89 ms, 16x16/8 0.80, 16x16/4 0.75
+// Gather warp (warp_tile_kernel) tiling.  A/B on cfg2 (7 views, 1 launch, split-bf16 out):
+// 64 ch/block with 4x16 waves 0.51 ms; 32 ch 0.47; 16 ch 0.44; 8 ch 0.416; 8 ch with 8x8
+// waves 0.391 (square wave footprints; a block's few planes keep the XCD's L2 working set
+// small, so neighbouring tiles still find their shared source lines there).
+#ifndef MVBEV_WARP_TH
 #define MVBEV_WARP_TH 16
 #define MVBEV_WARP_TW 16
-#define MVBEV_WARP_WR 4
+#define MVBEV_WARP_WR 8
 #endif
-constexpr int kWarpTH = MVBEV_WARP_TH;  // output rows per block
-constexpr int kWarpTW = MVBEV_WARP_TW;  // output cols per block
-constexpr int kWarpWR = MVBEV_WARP_WR;  // output rows per wave (wave tile WR x 64/WR)
-constexpr int kWarpCPB = 64;            // channels per block
+#ifndef MVBEV_WARP_CPB
+#define MVBEV_WARP_CPB 8
+#endif
+#ifndef MVBEV_WARP_NT
+#define MVBEV_WARP_NT 0  // non-temporal slab stores (measured no faster)
+#endif
+#ifndef MVBEV_WARP_GU
+#define MVBEV_WARP_GU 1  // 8-channel groups sampled before their stores are issued
+#endif
+constexpr int kWarpTH = MVBEV_WARP_TH;    // output rows per block
+constexpr int kWarpTW = MVBEV_WARP_TW;    // output cols per block
+constexpr int kWarpWR = MVBEV_WARP_WR;    // output rows per wave (wave tile WR x 64/WR)
+constexpr int kWarpCPB = MVBEV_WARP_CPB;  // channels per block
+// fused upsample+warp (warp_up_kernel): cfg2 +a4 A/B 64 ch/block, 4x16 waves 0.478 ms;
+// 32 ch 0.476; 16 ch 8x8 waves 0.476; 8 ch 8x8 waves 0.372
+#ifndef MVBEV_WARPUP_TH
+#define MVBEV_WARPUP_TH 16
+#define MVBEV_WARPUP_TW 16
+#define MVBEV_WARPUP_WR 8
+#endif
+#ifndef MVBEV_WARPUP_CPB
+#define MVBEV_WARPUP_CPB 8
+#endif
+constexpr int kUpTH = MVBEV_WARPUP_TH;
+constexpr int kUpTW = MVBEV_WARPUP_TW;
+constexpr int kUpWR = MVBEV_WARPUP_WR;
+constexpr int kUpCPB = MVBEV_WARPUP_CPB;
 constexpr int kWarpMaxViews = 16;
 
 struct WarpView {
@@ -47,8 +74,13 @@ __device__ inline void store_split8(u32x4_t* dst, const float (&v)[8]) {
     hi[j] = h;
     lo[j] = (__bf16)(v[j] - (float)h);
   }
+#if MVBEV_WARP_NT
+  __builtin_nontemporal_store(__builtin_bit_cast(u32x4_t, hi), dst);
+  __builtin_nontemporal_store(__builtin_bit_cast(u32x4_t, lo), dst + 1);
+#else
   dst[0] = __builtin_bit_cast(u32x4_t, hi);
   dst[1] = __builtin_bit_cast(u32x4_t, lo);
+#endif
 }
 
 // kornia 0.6.11 warp coordinates of output pixel (u, v): create_meshgrid(normalized) ->

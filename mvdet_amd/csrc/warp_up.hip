@@ -39,13 +39,13 @@ __global__ __launch_bounds__(256) void warp_up_kernel(const UpArgs ua) {
   const int b = bv / a.nviews;
   const WarpView& vw = a.v[view];
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
-  constexpr int WC = 64 / kWarpWR, WAVES_X = kWarpTW / WC;
+  constexpr int WC = 64 / kUpWR, WAVES_X = kUpTW / WC;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int v = ty * kWarpTH + (wave / WAVES_X) * kWarpWR + lane / WC;
-  const int u = tx * kWarpTW + (wave % WAVES_X) * WC + lane % WC;
+  const int v = ty * kUpTH + (wave / WAVES_X) * kUpWR + lane / WC;
+  const int u = tx * kUpTW + (wave % WAVES_X) * WC + lane % WC;
   if (v >= a.Ho || u >= a.Wo) return;
-  const int c_begin = chunk * kWarpCPB;
-  const int c_end = min(a.C, c_begin + kWarpCPB);
+  const int c_begin = chunk * kUpCPB;
+  const int c_end = min(a.C, c_begin + kUpCPB);
   const int H = a.H, W = a.W, h = ua.h, w = ua.sw;
 
   float m[9];
@@ -187,7 +187,7 @@ extern "C" int mvbev_warp_views_upsampled(const mvbev_warp_view* views, int nvie
     return MVBEV_ERR_RANK;
   if (nviews > kWarpMaxViews || B * nviews > 65535 || C > INT32_MAX || H > INT32_MAX / 2 ||
       W > INT32_MAX / 2 || Ho > INT32_MAX / 2 || Wo > INT32_MAX / 2 || H < h || W < w ||
-      ceil_div(Ho, kWarpTH) * ceil_div(Wo, kWarpTW) * ceil_div(C, kWarpCPB) * B * nviews > INT32_MAX)
+      ceil_div(Ho, kUpTH) * ceil_div(Wo, kUpTW) * ceil_div(C, kUpCPB) * B * nviews > INT32_MAX)
     return MVBEV_ERR_SHAPE;  // upsampling only (H >= h, W >= w): the 3x3 window bound
   if (out_layout != MVBEV_LAYOUT_F32 && out_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;
   if (out_layout == MVBEV_LAYOUT_F32 && src_is_f16) return MVBEV_ERR_SHAPE;
@@ -206,9 +206,9 @@ extern "C" int mvbev_warp_views_upsampled(const mvbev_warp_view* views, int nvie
   }
   a.nviews = nviews;
   a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
-  a.tiles_x = (int)ceil_div(Wo, kWarpTW);
-  a.tiles = a.tiles_x * (int)ceil_div(Ho, kWarpTH);
-  a.chunks = (int)ceil_div(C, kWarpCPB);
+  a.tiles_x = (int)ceil_div(Wo, kUpTW);
+  a.tiles = a.tiles_x * (int)ceil_div(Ho, kUpTH);
+  a.chunks = (int)ceil_div(C, kUpCPB);
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
   ua.h = (int)h; ua.sw = (int)w;
   ua.sy = (float)h / (float)H;  // area_pixel_compute_scale(align_corners=false, no scale)

@@ -1,6 +1,6 @@
 """Per-kernel micro-benchmark of the hot-path kernels at a BASELINE config (GPU box).
 
-    python tools/kbench.py [--config 2] [--reps 20] [--only warp,conv1,conv2,conv3]
+    python tools/kbench.py [--config 2] [--reps 20] [--only warp,warpup,conv1,conv2,conv3]
 
 Times each stage alone with HIP events on torch's current stream (the stream the
 kernels are launched on) and prints one JSON line per stage.  Used for A/B work on
@@ -58,6 +58,7 @@ def main():
     mc = build_mc(C, N, head_params(N, args.config, C), dev)
     eng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision)
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=v, device=dev) for v in range(N)]
+    bfeats = [synthetic.backbone_features(B, C, [u // 3 for u in up], seed=v, device=dev) for v in range(N)]
     ws = eng.workspace(B, dev)
     with torch.no_grad():
         for v in range(N):
@@ -65,6 +66,7 @@ def main():
         eng.fuse(ws, mc)
         stages = {
             "warp": (lambda: eng.warp_views(ws, list(range(N)), feats), None),
+            "warpup": (lambda: eng.warp_views_upsampled(ws, list(range(N)), bfeats), None),
             "warp1": (lambda: [eng.warp_view(ws, v, feats[v]) for v in range(N)], None),
             "conv1": (lambda: eng.conv1(ws, mc[0]), 2.0 * B * ho * wo * 9 * N * C * 512),
             "conv2": (lambda: eng.conv2(ws, mc[2]), 2.0 * B * ho * wo * 9 * 512 * 512),

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -194,16 +194,19 @@ int mvbev_pack_conv3x3_weight_bf16x3(const float* w, int64_t Cout, int64_t Cin_w
 int mvbev_conv3x3_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* desc,
                          const void* w_packed, const float* bias, const float* init,
                          int64_t Cout, int dilation, int relu, float* y, void* stream);
-/* Output tile of mvbev_conv3x3_bf16x3 (rows x columns), the granule of group_mask below. */
+/* Output tile of mvbev_conv3x3_bf16x3 (rows x columns), the granule of group_mask below:
+ * MVBEV_CONV_TILE_H rows for fp32/fp16 input; split-bf16 input (the LDS-DMA ring kernel)
+ * uses the row count mvbev_conv3x3_bf16x3_tile_rows returns (12). */
 #define MVBEV_CONV_TILE_H 8
 #define MVBEV_CONV_TILE_W 32
+int mvbev_conv3x3_bf16x3_tile_rows(int x_layout, int dilation);
 
 /* Extended form.
  *   y, y_layout: MVBEV_LAYOUT_F32 ([B][Cout][out_rows][W] fp32, as above) or
  *     MVBEV_LAYOUT_SPLIT_BF16 ([B][Cout/8][out_rows][W] pieces of bf16 hi[8], lo[8]: the
  *     next conv's input without a conversion pass).
  *   group_mask (optional, device): one uint32 per output tile, tiles row-major over
- *     ceil(out_rows / MVBEV_CONV_TILE_H) x ceil(W / MVBEV_CONV_TILE_W) (rows from out_row0);
+ *     ceil(out_rows / tile_rows(x_layout, dilation)) x ceil(W / MVBEV_CONV_TILE_W) (rows from out_row0);
  *     bit g clear = input channel group g (desc->group channels, group % 16 == 0, at most 32
  *     groups) is exactly zero over the tile and its 3x3 dilated halo, so its K-chunks are
  *     skipped for that tile (identical result).  mvbev_warp_tile_mask builds it from the

@@ -46,12 +46,13 @@ EXPORTS = (
     "mvbev_conv3x3_dgrad_bf16x3",
     "mvbev_conv3x3_wgrad_bf16x3_ex",
     "mvbev_warp_views_adjoint",
+    "mvbev_conv3x3_bf16x3_tile_rows",
 )
 
 KC = 8    # MVBEV_CONV_KC
 LAYOUT_F32, LAYOUT_F16, LAYOUT_SPLIT_BF16 = 0, 1, 2  # MVBEV_LAYOUT_*
 BN = 128  # MVBEV_CONV_BN
-TILE_H, TILE_W = 8, 32  # MVBEV_CONV_TILE_H / _W
+TILE_H, TILE_W = 8, 32  # MVBEV_CONV_TILE_H / _W (fp32/fp16 input; split input: conv_tile_rows())
 
 _i64 = ctypes.c_int64
 _p = ctypes.c_void_p
@@ -164,6 +165,8 @@ def _declare(lib):
     lib.mvbev_conv3x3_cout1_f32.restype = ctypes.c_int
     lib.mvbev_conv3x3_cout1_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p,
                                             ctypes.c_int, _p, _p]
+    lib.mvbev_conv3x3_bf16x3_tile_rows.restype = ctypes.c_int
+    lib.mvbev_conv3x3_bf16x3_tile_rows.argtypes = [ctypes.c_int, ctypes.c_int]
 
 
 def load(path: os.PathLike | str | None = None):
@@ -182,6 +185,12 @@ def load(path: os.PathLike | str | None = None):
     if path is None:
         _lib = lib
     return lib
+
+
+def conv_tile_rows(layout: int, dilation: int = 1) -> int:
+    """Output rows per tile of the bf16x3 conv for this input layout (the granule of its
+    frustum mask / tile order): 12 for split-bf16 input (LDS-DMA ring kernel), else TILE_H."""
+    return int(load().mvbev_conv3x3_bf16x3_tile_rows(int(layout), int(dilation)))
 
 
 def check(status: int, what: str) -> None:

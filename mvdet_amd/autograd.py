@@ -26,7 +26,7 @@ from typing import Sequence
 
 import torch
 
-from . import ops
+from . import _native, ops
 from .pipeline import ProjectFuse, Workspace, band_rows
 
 
@@ -85,7 +85,7 @@ def _wgrad_lists(engine: ProjectFuse, st, device, B: int):
     H, W = engine.grid_hw
     if engine.Cs % 64 != 0:
         return None
-    m = engine.conv1_mask(device, 0, H)
+    m = engine.conv1_mask(device, 0, H, tile_h=_native.TILE_H)  # the wgrad kernel's 8-row tiles
     if m is None:
         return None
     if not hasattr(st, "lists"):
@@ -180,7 +180,7 @@ class ProjectFuseFunction(torch.autograd.Function):
             if C % ops.KC == 0:  # split-bf16 dslab: the adjoint gathers 8 channels per 32-B entry
                 dslab = torch.empty(ops.split_shape(B, cp, H, W), dtype=torch.bfloat16, device=dev)
                 # frustum: a view's tiles of dslab that its warp never samples are not computed
-                cm = engine.conv1_mask(dev, 0, H) if C % ops.BN == 0 else None
+                cm = engine.conv1_mask(dev, 0, H, tile_h=_native.TILE_H) if C % ops.BN == 0 else None
                 ops.conv3x3_dgrad(dy1, st.dgrad1, w1, 1, out=dslab, out_mask=cm, cot_per_group=C // ops.BN)
                 g8 = C // ops.KC
                 douts = [dslab[:, v * g8:(v + 1) * g8] for v in range(n)]

@@ -145,81 +145,86 @@ template <> __device__ inline float ld<_Float16>(const _Float16* p) { return (fl
 #define MVBEV_B3_DEPTH 2  // staging-register ring depth (1 or 2)
 #endif
 
-// Output of one finished tile (bias, coord-term init, ReLU) from the accumulators of the
-// tile's waves; shared by the conv kernel and the stream-K fixup.
+// One finished 32x32 accumulator block (output channels co0..co0+31 at output pixel
+// (row, col) of this lane): bias, coord-term init, ReLU, store fp32 or split-bf16.
+template <bool RELU>
+__device__ inline void store_block(const Args& a, int b, int row, int col, int co0, const floatx16& acc) {
+  const int kh = (threadIdx.x & 63) >> 5;
+  const int W = a.W;
+  const int64_t oplane = (int64_t)a.out_rows * W;
+  const int64_t iplane = (int64_t)a.H * W;
+  const bool valid = row < a.out_row0 + a.out_rows && col < W;
+  if (!a.y_split) {
+    if (!valid) return;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+      float v = acc[r];
+      if (a.bias) v += a.bias[co];
+      if (a.init) v += a.init[co * iplane + (int64_t)row * W + col];
+      if (RELU) v = v < 0.f ? 0.f : v;
+      a.y[((int64_t)b * a.Cout + co) * oplane + (int64_t)(row - a.out_row0) * W + col] = v;
+    }
+    return;
+  }
+  // split-bf16 output: the lane holds channels 4kh..4kh+3 of four 8-channel groups; its
+  // partner lane (lane ^ 32) holds the other half.  kh = 0 writes each group's 16-B hi
+  // piece, kh = 1 its lo piece, after swapping the half the partner needs (every lane
+  // takes part in the shuffles; only the store is predicated).
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    unsigned int hp[2], lp[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float v2[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int r = 4 * q + 2 * h + e;
+        const int co = co0 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        float v = acc[r];
+        if (a.bias) v += a.bias[co];
+        if (a.init && valid) v += a.init[co * iplane + (int64_t)row * W + col];
+        if (RELU) v = v < 0.f ? 0.f : v;
+        v2[e] = v;
+      }
+      const __bf16 h0 = (__bf16)v2[0], h1 = (__bf16)v2[1];
+      const __bf16 l0 = (__bf16)(v2[0] - (float)h0), l1 = (__bf16)(v2[1] - (float)h1);
+      hp[h] = (unsigned)__builtin_bit_cast(unsigned short, h0) |
+              ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
+      lp[h] = (unsigned)__builtin_bit_cast(unsigned short, l0) |
+              ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
+    }
+    const unsigned s0 = kh ? hp[0] : lp[0], s1 = kh ? hp[1] : lp[1];
+    const unsigned r0 = (unsigned)__shfl_xor((int)s0, 32), r1 = (unsigned)__shfl_xor((int)s1, 32);
+    const u32x4 piece = kh ? u32x4{r0, r1, lp[0], lp[1]} : u32x4{hp[0], hp[1], r0, r1};
+    if (valid) {
+      const int64_t g = co0 / 8 + q;
+      u32x4* out = reinterpret_cast<u32x4*>(a.y);
+      out[2 * ((((int64_t)b * (a.Cout / 8) + g) * a.out_rows + (row - a.out_row0)) * W + col) + kh] = piece;
+    }
+  }
+}
+
+// Output of one finished tile from the accumulators of the tile's waves; shared by the
+// conv kernel and the stream-K fixup.
 template <bool RELU, int NW>
 __device__ inline void tile_epilogue(const Args& a, int tile, const floatx16 (&acc)[2][2]) {
   constexpr int TH = NW;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int l32 = lane & 31, kh = lane >> 5;
   const int cot = tile % a.n_cot;
   int rest = tile / a.n_cot;
   const int tx = rest % a.tiles_x;
   rest /= a.tiles_x;
   const int ty = rest % a.tiles_y;
   const int b = rest / a.tiles_y;
-  const int W = a.W;
   const int y0 = a.out_row0 + ty * TH;
   const int prow = 2 * (wave % (NW / 2));
   const int cw = 64 * (wave / (NW / 2));
-  const int col = tx * TW + l32;
-  const int64_t oplane = (int64_t)a.out_rows * W;
-  const int64_t iplane = (int64_t)a.H * W;
 #pragma unroll
   for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-    for (int pt = 0; pt < 2; ++pt) {
-      const int row = y0 + prow + pt;
-      const bool valid = row < a.out_row0 + a.out_rows && col < W;
-      if (!a.y_split) {
-        if (!valid) continue;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int co = cot * BN + cw + 32 * ct + (r & 3) + 8 * (r >> 2) + 4 * kh;
-          float v = acc[ct][pt][r];
-          if (a.bias) v += a.bias[co];
-          if (a.init) v += a.init[co * iplane + (int64_t)row * W + col];
-          if (RELU) v = v < 0.f ? 0.f : v;
-          a.y[((int64_t)b * a.Cout + co) * oplane + (int64_t)(row - a.out_row0) * W + col] = v;
-        }
-        continue;
-      }
-      // split-bf16 output: the lane holds channels 4kh..4kh+3 of four 8-channel groups; its
-      // partner lane (lane ^ 32) holds the other half.  kh = 0 writes each group's 16-B hi
-      // piece, kh = 1 its lo piece, after swapping the half the partner needs.
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        unsigned int hp[2], lp[2];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          float v2[2];
-#pragma unroll
-          for (int e = 0; e < 2; ++e) {
-            const int r = 4 * q + 2 * h + e;
-            const int co = cot * BN + cw + 32 * ct + (r & 3) + 8 * (r >> 2) + 4 * kh;
-            float v = acc[ct][pt][r];
-            if (a.bias) v += a.bias[co];
-            if (a.init && valid) v += a.init[co * iplane + (int64_t)row * W + col];
-            if (RELU) v = v < 0.f ? 0.f : v;
-            v2[e] = v;
-          }
-          const __bf16 h0 = (__bf16)v2[0], h1 = (__bf16)v2[1];
-          const __bf16 l0 = (__bf16)(v2[0] - (float)h0), l1 = (__bf16)(v2[1] - (float)h1);
-          hp[h] = (unsigned)__builtin_bit_cast(unsigned short, h0) |
-                  ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
-          lp[h] = (unsigned)__builtin_bit_cast(unsigned short, l0) |
-                  ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
-        }
-        const unsigned s0 = kh ? hp[0] : lp[0], s1 = kh ? hp[1] : lp[1];
-        const unsigned r0 = (unsigned)__shfl_xor((int)s0, 32), r1 = (unsigned)__shfl_xor((int)s1, 32);
-        const u32x4 piece = kh ? u32x4{r0, r1, lp[0], lp[1]} : u32x4{hp[0], hp[1], r0, r1};
-        if (valid) {
-          const int64_t g = (cot * BN + cw + 32 * ct) / 8 + q;
-          u32x4* out = reinterpret_cast<u32x4*>(a.y);
-          out[2 * ((((int64_t)b * (a.Cout / 8) + g) * a.out_rows + (row - a.out_row0)) * W + col) + kh] = piece;
-        }
-      }
-    }
+    for (int pt = 0; pt < 2; ++pt)
+      store_block<RELU>(a, b, y0 + prow + pt, tx * TW + (lane & 31), cot * BN + cw + 32 * ct, acc[ct][pt]);
 }
 
 // stream-K partial slot: [slot][16 float4 of the thread's 64 accumulators][thread] (coalesced)
@@ -541,6 +546,252 @@ __global__ __launch_bounds__(64 * NW, MVBEV_B3_MINWAVES) void conv_kernel(const 
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Ring kernel: the default for split-bf16 input (conv1 over the warped slab, conv2 over y1).
+//
+// conv_kernel above stages each 16-channel chunk (72 KiB of weights + the halo) through
+// registers into one LDS image between two barriers, so every chunk's ds_write pass runs
+// while the MFMAs idle, and the 2-deep register ring holds the VGPR file at 256.  Here the
+// staging is LDS-DMA (global_load_lds_dwordx4: no VGPRs, no ds_write) into a ring, and the
+// freed registers buy a taller wave tile:
+//   * unit = (chunk, kernel column kw): 3 taps x 16 channels x 128 Cout = 24 KiB of weights;
+//     W ring of 3 unit slots, halo images (whole chunk) double-buffered: 136 KiB (d1) /
+//     152 KiB (d2) of LDS, one workgroup per CU;
+//   * workgroup tile 12 rows x 32 cols x 128 Cout, 8 waves = 4 row groups x 2 Cout halves,
+//     wave = 3 output rows x 64 Cout (2x3 accumulators).  Rows of a wave are DIL apart, so a
+//     kernel column's 3 taps read only 5 distinct input rows: the B fragments of a unit are
+//     loaded once (10 ds_read_b128) and reused by its 3 taps;
+//   * one barrier per unit, placed before the unit's last tap: the wait before it retires
+//     W(u+1) (and the next chunk's halo), the DMA after it refills the slot of unit u (whose
+//     last fragments were read before the barrier) with W(u+3), so two units of DMA latency
+//     are hidden, and the last tap's MFMAs cover the next unit's fragment reads.
+// Counted waits only (vmcnt per unit position, raw s_barrier): __syncthreads() would drain
+// the DMAs in flight (cdna_hip_programming.md §5, "Pipelining across barriers").
+// Accumulation order per output: chunk, then kw, then kh (the register kernel: chunk, tap);
+// the same fp32-accumulated 3xbf16 products, so the same accuracy.
+constexpr int RT = 12;                          // output rows per workgroup tile
+constexpr int RNW = 8;                          // waves
+constexpr int RNT = 64 * RNW;
+constexpr int RUNIT = 2 * 3 * 2 * BN;           // 16-B pieces of one W unit (hi + lo): 1536
+constexpr int RHALF = RUNIT / 2;                // one part (hi or lo) of a unit
+constexpr int RNWI = RUNIT / RNT;               // LDS-DMA instructions per wave per W unit (3)
+static_assert(RUNIT % RNT == 0, "W unit must split evenly over the waves");
+template <int DIL> struct RingGeo {
+  static constexpr int XH = RT + 2 * DIL, XW = TW + 2 * DIL, XPIX = XH * XW;
+  static constexpr int NX = (4 * XPIX + RNT - 1) / RNT;  // LDS-DMA instructions per wave per halo
+  static constexpr int XBUF = NX * RNT;                  // entries per halo buffer (incl. tail)
+  static constexpr int LDS = 3 * RUNIT + 2 * XBUF;       // 16-B entries
+  static_assert(LDS * 16 <= 160 * 1024, "LDS");
+};
+__device__ u32x4 g_ring_zero[1];  // zero-initialised source of padding halo entries
+
+// first output row (tile-relative) of row group rg; its rows are base + pt * DIL, pt < 3
+template <int DIL>
+__device__ inline int ring_base_row(int rg) {
+  static_assert(DIL == 1 || DIL == 2, "dilation");
+  return DIL == 1 ? 3 * rg : (rg >> 1) * 6 + (rg & 1);
+}
+
+__device__ inline void glds16(const u32x4* src, u32x4* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+template <int DIL, bool RELU>
+__global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
+  using G = RingGeo<DIL>;
+  constexpr int XW = G::XW, XPIX = G::XPIX, NX = G::NX, XBUF = G::XBUF;
+  __shared__ __attribute__((aligned(16))) u32x4 lds[G::LDS];
+  u32x4* const Xlds = lds + 3 * RUNIT;
+
+  const int W = a.W;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, kl = lane >> 5;  // lane half = 8-channel sub-block of a K-block
+  const int64_t plane = (int64_t)a.in_rows * W;
+  const int64_t wchunk = (int64_t)a.n_cot * W16;
+
+  int tile = xcd_remap(blockIdx.x, a.nwg);
+  if (a.gmask) {  // frustum mask: ordered pixel tiles dealt to the XCDs (see conv_kernel)
+    constexpr int Gq = MVBEV_MASK_GROUP;
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int q = j / a.n_cot;
+    const int slot = Gq * (8 * (q / Gq) + x) + q % Gq;
+    if (slot >= a.npix) return;  // padding block (whole block, before any barrier)
+    tile = (a.tile_order ? a.tile_order[slot] : slot) * a.n_cot + j % a.n_cot;
+  }
+  const int cot = tile % a.n_cot;
+  int rest = tile / a.n_cot;
+  const int tx = rest % a.tiles_x;
+  rest /= a.tiles_x;
+  const int ty = rest % a.tiles_y;
+  const int b = rest / a.tiles_y;
+  const int x0 = tx * TW;
+  const int y0 = a.out_row0 + ty * RT;
+  const u32x4* wsrc = a.wp + (int64_t)cot * W16;
+  const uint32_t gm = a.gmask ? a.gmask[ty * a.tiles_x + tx] : 0u;
+  const int nch = a.gmask ? __builtin_popcount(gm) * a.cpg : a.nchunks;
+  auto chunk_of = [&](int i) -> int {
+    if (!a.gmask) return i;
+    uint32_t m = gm;
+    for (int j = i / a.cpg; j > 0; --j) m &= m - 1;
+    return __builtin_ctz(m) * a.cpg + i % a.cpg;
+  };
+
+  // LDS-DMA sources, chunk-invariant parts.  Halo entry e = (sub, part, pixel) of the image
+  // [sub][part][XH][XW]; lane j-th instruction covers entries (j * RNW + wave) * 64 + lane.
+  int xo[NX];    // piece offset in the sub-block's plane (2 * pixel + part); -1 = zero entry
+  int xsub[NX];  // sub-block (0/1)
+#pragma unroll
+  for (int j = 0; j < NX; ++j) {
+    const int e = (j * RNW + wave) * 64 + lane;
+    const int sub = e / (2 * XPIX), part = (e / XPIX) & 1, pix = e % XPIX;
+    const int r = pix / XW, c = pix % XW;
+    const int gy = y0 - DIL + r, gx = x0 - DIL + c, by = gy - a.in_row0;
+    const bool ok = e < 4 * XPIX && gy >= 0 && gy < a.H && by >= 0 && by < a.in_rows && gx >= 0 && gx < W;
+    xo[j] = ok ? 2 * (by * W + gx) + part : -1;
+    xsub[j] = sub & 1;
+  }
+  // W unit image [part][kh][sub][co]; packed source [part][tap = 3 kh + kw][sub][co]
+  int wo[RNWI];
+#pragma unroll
+  for (int j = 0; j < RNWI; ++j) {
+    const int e = (j * RNW + wave) * 64 + lane;
+    const int part = e / RHALF, r = e % RHALF;
+    wo[j] = part * (NKB * 2 * BN) + (r / (2 * BN)) * 3 * (2 * BN) + r % (2 * BN);
+  }
+  const int U = 3 * nch;
+  auto issue_w = [&](int u) __attribute__((always_inline)) {  // W unit u -> slot u % 3
+    const int uu = min(u, U - 1);
+    const int ci = uu / 3, kw = uu - 3 * ci;
+    const u32x4* src = wsrc + (int64_t)chunk_of(ci) * wchunk + kw * 2 * BN;
+    u32x4* dst = lds + (u % 3) * RUNIT + wave * 64;
+#pragma unroll
+    for (int j = 0; j < RNWI; ++j) glds16(src + wo[j], dst + j * RNT);
+  };
+  auto issue_x = [&](int i) __attribute__((always_inline)) {  // halo of chunk i -> buffer i & 1
+    const int ch = chunk_of(min(i, nch - 1));
+    const u32x4* xs[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int k0 = ch * KC + s * SB;
+      const int g = k0 / a.group;
+      const int64_t cb = (int64_t)b * a.batch_stride + g * a.group_stride + (int64_t)(k0 - g * a.group) * plane;
+      xs[s] = k0 < a.K ? static_cast<const u32x4*>(a.x) + cb / 4 : nullptr;
+    }
+    u32x4* dst = Xlds + (i & 1) * XBUF + wave * 64;
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+      const u32x4* base = xsub[j] ? xs[1] : xs[0];
+      glds16(xo[j] >= 0 && base ? base + xo[j] : g_ring_zero, dst + j * RNT);
+    }
+  };
+
+  const int rg = wave & 3;
+  const int base = ring_base_row<DIL>(rg);
+  const int cw = 64 * (wave >> 2);
+  floatx16 acc[2][3];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = floatx16{0};
+  bf16x8 fb[2][5][2];  // [set][input row m (rows base + m * DIL)][hi, lo]
+  bf16x8 fa[2][2][2];  // [set][ct][hi, lo]
+  auto fetch_b = [&](int st, int xb, int kw) __attribute__((always_inline)) {
+    const u32x4* X = Xlds + xb * XBUF + kl * 2 * XPIX + base * XW + l32 + kw * DIL;
+#pragma unroll
+    for (int m = 0; m < 5; ++m)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) fb[st][m][p] = __builtin_bit_cast(bf16x8, X[p * XPIX + m * DIL * XW]);
+  };
+  auto fetch_a = [&](int st, int slot, int kh) __attribute__((always_inline)) {
+    const u32x4* Wl = lds + slot * RUNIT + kh * 2 * BN + kl * BN + cw + l32;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) fa[st][ct][p] = __builtin_bit_cast(bf16x8, Wl[p * RHALF + 32 * ct]);
+  };
+  auto mfmas = [&](int as, int bs, int kh) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int pt = 0; pt < 3; ++pt) {
+        const int m = pt + kh;
+        acc[ct][pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[as][ct][1], fb[bs][m][0], acc[ct][pt], 0, 0, 0);
+        acc[ct][pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[as][ct][0], fb[bs][m][1], acc[ct][pt], 0, 0, 0);
+        acc[ct][pt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[as][ct][0], fb[bs][m][0], acc[ct][pt], 0, 0, 0);
+      }
+  };
+  // interleave n fragment reads with the first n of a tap's 18 MFMAs
+  auto interleave = [&](auto nreads) __attribute__((always_inline)) {
+    constexpr int n = decltype(nreads)::value;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 18 - n, 0);
+  };
+
+  if (nch > 0) {
+    // prologue: W(0), halo(0), W(1), W(2) in flight; wait for the first two
+    issue_w(0);
+    issue_x(0);
+    issue_w(1);
+    issue_w(2);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * RNWI) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    fetch_b(0, 0, 0);
+    fetch_a(0, 0, 0);
+    // unit u = u0 + R, R < 6 compile-time: kw = R % 3, W slot R % 3, halo buffer (R / 3) & 1,
+    // fragment set R & 1 (u0 is a multiple of 6)
+#define RING_UNIT(R)                                                                           \
+  do {                                                                                         \
+    constexpr int KW = (R) % 3, P = (R) & 1, SLOT = (R) % 3;                                    \
+    constexpr int NSLOT = ((R) + 1) % 3, NXB = (((R) + 1) / 3) & 1, NKW = ((R) + 1) % 3;        \
+    const int u_ = u0 + (R);                                                                   \
+    if (u_ >= U) break;                                                                        \
+    fetch_a(P ^ 1, SLOT, 1);                                                                   \
+    mfmas(P, P, 0);                                                                            \
+    interleave(std::integral_constant<int, 4>{});                                              \
+    fetch_a(P, SLOT, 2);                                                                       \
+    mfmas(P ^ 1, P, 1);                                                                        \
+    interleave(std::integral_constant<int, 4>{});                                              \
+    /* retire W(u+1) (+ the next chunk's halo at kw 2); LDS reads of this unit's slot done */ \
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(KW == 1 ? RNWI + NX : RNWI) : "memory"); \
+    __builtin_amdgcn_s_barrier();                                                              \
+    asm volatile("" ::: "memory");                                                             \
+    issue_w(u_ + 3);                                                                           \
+    if (KW == 0) issue_x(u_ / 3 + 1);                                                          \
+    fetch_b(P ^ 1, NXB, NKW);                                                                  \
+    fetch_a(P ^ 1, NSLOT, 0);                                                                  \
+    mfmas(P, P, 2);                                                                            \
+    interleave(std::integral_constant<int, 14>{});                                             \
+  } while (0)
+    for (int u0 = 0; u0 < U; u0 += 6) {
+      RING_UNIT(0);
+      RING_UNIT(1);
+      RING_UNIT(2);
+      RING_UNIT(3);
+      RING_UNIT(4);
+      RING_UNIT(5);
+    }
+#undef RING_UNIT
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the block exits
+  }
+
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int pt = 0; pt < 3; ++pt)
+      store_block<RELU>(a, b, y0 + base + pt * DIL, x0 + l32, cot * BN + cw + 32 * ct, acc[ct][pt]);
+}
+
+#ifndef MVBEV_B3_RING
+#define MVBEV_B3_RING 1  // split-bf16 input: the LDS-DMA ring kernel (0: conv_kernel)
+#endif
+
 #ifndef MVBEV_B3_WAVES
 #define MVBEV_B3_WAVES 8
 #endif
@@ -613,7 +864,10 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   a.H = (int)d->H; a.W = (int)d->W;
   a.in_row0 = (int)d->in_row0; a.in_rows = (int)d->in_rows;
   a.out_row0 = (int)d->out_row0; a.out_rows = (int)d->out_rows;
-  a.tiles_x = (int)ceil_div(d->W, TW); a.tiles_y = (int)ceil_div(d->out_rows, NW);
+  // split-bf16 input runs the LDS-DMA ring kernel (12-row tiles, no split-K tail)
+  const bool ring = std::is_same<TIn, SplitIn>::value && MVBEV_B3_RING && !out_mask &&
+                    (dilation == 1 || dilation == 2);
+  a.tiles_x = (int)ceil_div(d->W, TW); a.tiles_y = (int)ceil_div(d->out_rows, ring ? RT : NW);
   a.n_cot = (int)(Cout / BN);
   const int64_t tiles = (int64_t)a.tiles_x * a.tiles_y * a.n_cot * d->B;
   if (tiles * a.nchunks > (int64_t)INT32_MAX * 8) return MVBEV_ERR_SHAPE;
@@ -632,7 +886,7 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   if (y_layout != MVBEV_LAYOUT_F32 && y_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;
   a.y_split = y_layout == MVBEV_LAYOUT_SPLIT_BF16;
   a.npix = (int)(tiles / a.n_cot);
-  const SkPlan plan = group_mask ? SkPlan() : sk_plan(tiles, a.nchunks);
+  const SkPlan plan = (group_mask || ring) ? SkPlan() : sk_plan(tiles, a.nchunks);
   const bool sk = workspace && plan.split > 1 &&
                   ws_bytes >= (size_t)(plan.tail * plan.split) * kSkSlotBytes;
   a.sk_ws = sk ? static_cast<float*>(workspace) : nullptr;
@@ -651,7 +905,15 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
       hipLaunchKernelGGL((sk_fixup_kernel<R, NW>), dim3((unsigned)plan.tail),              \
                          dim3(64 * NW), 0, s, a);                                         \
   } while (0)
-  if (dilation == 1) {
+#define RING_LAUNCH(D, R) \
+  hipLaunchKernelGGL((conv_ring_kernel<D, R>), dim3((unsigned)nwg), dim3(RNT), 0, s, a)
+  if (ring) {
+    if (dilation == 1) {
+      if (relu) RING_LAUNCH(1, true); else RING_LAUNCH(1, false);
+    } else {
+      if (relu) RING_LAUNCH(2, true); else RING_LAUNCH(2, false);
+    }
+  } else if (dilation == 1) {
     if (relu) B3_LAUNCH(1, true); else B3_LAUNCH(1, false);
   } else if (dilation == 2) {
     if (relu) B3_LAUNCH(2, true); else B3_LAUNCH(2, false);
@@ -659,6 +921,7 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
     return MVBEV_ERR_DILATION;
   }
 #undef B3_LAUNCH
+#undef RING_LAUNCH
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }
@@ -707,6 +970,11 @@ int mvbev_pack_conv3x3_dgrad_bf16x3(const float* w, int64_t Cout_w, int64_t Cin_
                      (int)K_out, (int)k_pad);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
+}
+
+int mvbev_conv3x3_bf16x3_tile_rows(int x_layout, int dilation) {
+  const bool ring = x_layout == MVBEV_LAYOUT_SPLIT_BF16 && MVBEV_B3_RING && (dilation == 1 || dilation == 2);
+  return ring ? mvbev::b3::RT : MVBEV_B3_WAVES;
 }
 
 int mvbev_conv3x3_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* desc,

@@ -299,10 +299,13 @@ def conv3x3_workspace_bytes(desc, cout: int) -> int:
     return int(_native.load().mvbev_conv3x3_bf16x3_workspace_bytes(ctypes.byref(desc), cout))
 
 
-def warp_tile_mask(m_norms, src_hw, grid_hw, row0: int, rows: int, halo: int, device) -> torch.Tensor:
+def warp_tile_mask(m_norms, src_hw, grid_hw, row0: int, rows: int, halo: int, device,
+                   tile_h: Optional[int] = None) -> torch.Tensor:
     """Frustum mask of the conv tiles (``mvbev_warp_tile_mask``): int32 [tiles] on ``device``,
     bit s set where slot s's warp can be non-zero in the tile + ``halo``.  ``m_norms[s]`` is a
-    host [3,3] kornia matrix, or None for an empty slot (always zero)."""
+    host [3,3] kornia matrix, or None for an empty slot (always zero).  ``tile_h``: tile rows
+    (default ``_native.TILE_H``; the split-input conv's is ``_native.conv_tile_rows``)."""
+    tile_h = _native.TILE_H if tile_h is None else int(tile_h)
     n = len(m_norms)
     if not 0 < n <= 16:
         raise ValueError("need 1..16 slots")
@@ -314,9 +317,9 @@ def warp_tile_mask(m_norms, src_hw, grid_hw, row0: int, rows: int, halo: int, de
         arr[i].m = (ctypes.c_float * 9)(*mm)
     H, W = src_hw
     Ho, Wo = grid_hw
-    tiles = -(-rows // _native.TILE_H) * -(-Wo // _native.TILE_W)
+    tiles = -(-rows // tile_h) * -(-Wo // _native.TILE_W)
     mask = torch.zeros(tiles, dtype=torch.int32, device=device)
-    st = _native.load().mvbev_warp_tile_mask(arr, n, H, W, Ho, Wo, row0, rows, _native.TILE_H, _native.TILE_W,
+    st = _native.load().mvbev_warp_tile_mask(arr, n, H, W, Ho, Wo, row0, rows, tile_h, _native.TILE_W,
                                              halo, mask.data_ptr(), _stream(mask))
     _native.check(st, "mvbev_warp_tile_mask")
     return mask
@@ -385,7 +388,7 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
             wsp, wsn = workspace.data_ptr(), workspace.numel() * workspace.element_size()
         if group_mask is not None:
             _require_cuda(group_mask)
-            tiles = -(-desc.out_rows // _native.TILE_H) * -(-W // _native.TILE_W)
+            tiles = -(-desc.out_rows // _native.conv_tile_rows(layout, dilation)) * -(-W // _native.TILE_W)
             if group_mask.dtype != torch.int32 or group_mask.numel() < tiles or not group_mask.is_contiguous():
                 raise ValueError(f"group_mask must be a contiguous int32 tensor of >= {tiles} tiles")
             gmp = group_mask.data_ptr()

@@ -31,7 +31,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from . import ops
+from . import _native, ops
 from .geometry import kornia_src_norm_from_dst_norm
 
 # halo rows each layer needs below/above its output rows (dilations 1, 2, 4 of :51-54)
@@ -219,16 +219,22 @@ class ProjectFuse:
             self._sk[str(device)] = buf
         return buf
 
-    def conv1_mask(self, device, row0: int, rows: int) -> Optional[torch.Tensor]:
-        """Per conv1 output tile of rows [row0, row0+rows): bit s = slot s can be non-zero in
-        the tile's 3x3 halo (``mvbev_warp_tile_mask``); None when not used."""
+    def conv1_tile_rows(self) -> int:
+        """Output rows per tile of the forward conv1 kernel (its mask / order granule)."""
+        return _native.conv_tile_rows(_native.LAYOUT_SPLIT_BF16 if self.split else _native.LAYOUT_F16, 1)
+
+    def conv1_mask(self, device, row0: int, rows: int, tile_h: Optional[int] = None) -> Optional[torch.Tensor]:
+        """Per conv1 output tile (``tile_h`` rows: default the forward conv1's tile) of rows
+        [row0, row0+rows): bit s = slot s can be non-zero in the tile's 3x3 halo
+        (``mvbev_warp_tile_mask``); None when not used."""
         if not self.frustum:
             return None
-        key = (str(device), row0, rows)
+        tile_h = self.conv1_tile_rows() if tile_h is None else int(tile_h)
+        key = (str(device), row0, rows, tile_h)
         m = self._masks.get(key)
         if m is None:
             ms = [None if v is None else self.m_norm_cpu[v] for v in self.slot_views]
-            m = ops.warp_tile_mask(ms, self.src_hw, self.grid_hw, row0, rows, 1, device)
+            m = ops.warp_tile_mask(ms, self.src_hw, self.grid_hw, row0, rows, 1, device, tile_h=tile_h)
             self._masks[key] = m
         return m
 

@@ -265,14 +265,15 @@ def test_frustum_mask_is_exact_and_conv1_unchanged(cfg):
     assert torch.equal(ws.y1, y1_ref)
     assert torch.equal(got, ref)
     H, W = grid
+    th = sparse.conv1_tile_rows()
     mask = sparse.conv1_mask(DEV, 0, H).cpu().numpy().astype(np.uint32)
     tx = -(-W // 32)
     warped = [sparse.view_slice(ws, v).abs().amax(dim=(0, 1)).cpu() for v in range(N)]  # [H, W]
     kept = 0
     for t, bits in enumerate(mask):
-        r0, c0 = (t // tx) * 8, (t % tx) * 32
+        r0, c0 = (t // tx) * th, (t % tx) * 32
         for v in range(N):
-            region = warped[v][max(0, r0 - 1):r0 + 9, max(0, c0 - 1):c0 + 33]
+            region = warped[v][max(0, r0 - 1):r0 + th + 1, max(0, c0 - 1):c0 + 33]
             if not (bits >> v) & 1:
                 assert region.max().item() == 0, (t, v)
             else:

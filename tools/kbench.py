@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--only", default="warp,conv1,conv2,conv3")
     ap.add_argument("--libs", default="", help="comma-separated libmvbev variants to A/B (interleaved rounds)")
     ap.add_argument("--rounds", type=int, default=1)
+    ap.add_argument("--no-frustum", action="store_true", help="dense conv1 (no frustum mask)")
     args = ap.parse_args()
     spec = synthetic.CONFIGS[args.config]
     ds = spec["make"]()
@@ -56,7 +57,7 @@ def main():
     dev = torch.device("cuda:0")
     pm = projection_matrices(ds)
     mc = build_mc(C, N, head_params(N, args.config, C), dev)
-    eng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision)
+    eng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision, frustum=not args.no_frustum)
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=v, device=dev) for v in range(N)]
     bfeats = [synthetic.backbone_features(B, C, [u // 3 for u in up], seed=v, device=dev) for v in range(N)]
     ws = eng.workspace(B, dev)

@@ -71,10 +71,6 @@ def main():
           f"{schedule([ds.num_cam * cpg] * len(m))[0]:.0f}")
 
 
-if __name__ == "__main__":
-    main()
-
-
 def split_schedule(work, cap, cus=256, xcds=8, n_cot=4):
     """Items above `cap` chunks cut into equal K-pieces, then the same greedy schedule."""
     items = []
@@ -108,3 +104,7 @@ def lpt_schedule(items, cus=256, xcds=8):
             heapq.heappush(h, heapq.heappop(h) + w)
         mk = max(mk, max(h))
     return mk
+
+
+if __name__ == "__main__":
+    main()

@@ -157,14 +157,15 @@ def run_single(args, precision, steps, warmup, with_cpu):
         # tile-edge columns a 32-wide tile computes past W=360 are waste, not counted).
         # Algorithmic = the reference's dense conv; the frustum mask executes `active` of it.
         achieved, peak = conv1_alg_tfs * 3, BF16_MFMA_PEAK_TFS
-        kname = "conv3x3_bf16x3 (conv1, frustum-masked)"
+        kname = "conv_ring_kernel (conv1: 3xbf16 MFMA, LDS-DMA ring, frustum-masked)"
     else:
         achieved, peak = conv1_alg_tfs, FP32_MFMA_PEAK_TFS
         kname = "conv3x3_mfma_f32 (conv1)"
-    traffic = None
+    traffic, warp_traffic = None, None
     tfile = ROOT / "profiles" / f"traffic_cfg{args.config}_{precision}.json"
     if tfile.exists():
-        traffic = json.loads(tfile.read_text()).get("conv1_hbm_bytes_per_launch")
+        tj = json.loads(tfile.read_text())
+        traffic, warp_traffic = tj.get("conv1_hbm_bytes_per_launch"), tj.get("warp_hbm_bytes_per_launch")
     res = {
         "value": round(value, 3),
         "ms_per_step": round(dt * 1e3 / K, 4),
@@ -183,7 +184,10 @@ def run_single(args, precision, steps, warmup, with_cpu):
                       "conv3": round(t_c3, 4)},
         "stage_roofline": {
             "warp": {"bound": "hbm", "algorithmic_bytes": warp_bytes,
-                     "achieved_GBs": round(warp_bytes / (t_warp * 1e-3) / 1e9, 1), "peak_GBs": HBM_PEAK_GBS},
+                     "achieved_GBs": round(warp_bytes / (t_warp * 1e-3) / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
+                     # PMC bytes (read at 128-B granules: NCHW rows are gathered, not streamed)
+                     "traffic": warp_traffic,
+                     "physical_GBs": round(warp_traffic / (t_warp * 1e-3) / 1e9, 1) if warp_traffic else None},
             "conv2": {"bound": "mfma", "algorithmic_fp32_TFs": round(conv2_flop / (t_c2 * 1e-3) / 1e12, 2)},
             "conv3": {"bound": "hbm", "achieved_GBs": round(conv3_bytes / (t_c3 * 1e-3) / 1e9, 1),
                       "peak_GBs": HBM_PEAK_GBS},

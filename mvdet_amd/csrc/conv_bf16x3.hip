@@ -139,7 +139,7 @@ template <> __device__ inline float ld<_Float16>(const _Float16* p) { return (fl
 #define MVBEV_B3_MINWAVES 1
 #endif
 #ifndef MVBEV_MASK_GROUP
-#define MVBEV_MASK_GROUP 2  // consecutive ordered pixel tiles per XCD turn (A/B at cfg2: 1 and 2 equal, 4 and 8 5 % slower)
+#define MVBEV_MASK_GROUP 1  // consecutive ordered pixel tiles per XCD turn (ring kernel, cfg2 conv1: 1 2.17-2.24 ms, 2 2.23-2.28, 4 2.41)
 #endif
 #ifndef MVBEV_B3_DEPTH
 #define MVBEV_B3_DEPTH 2  // staging-register ring depth (1 or 2)
@@ -597,6 +597,10 @@ __device__ inline void glds16(const u32x4* src, u32x4* lds_wave_base) {
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
+#ifndef MVBEV_RING_PRIO
+#define MVBEV_RING_PRIO 0  // raise the wave priority over each unit's MFMA stream
+#endif
+
 template <int DIL, bool RELU>
 __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
   using G = RingGeo<DIL>;
@@ -753,6 +757,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     const int u_ = u0 + (R);                                                                   \
     if (u_ >= U) break;                                                                        \
     fetch_a(P ^ 1, SLOT, 1);                                                                   \
+    if (MVBEV_RING_PRIO) __builtin_amdgcn_s_setprio(1);                                        \
     mfmas(P, P, 0);                                                                            \
     interleave(std::integral_constant<int, 4>{});                                              \
     fetch_a(P, SLOT, 2);                                                                       \
@@ -768,6 +773,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     fetch_a(P ^ 1, NSLOT, 0);                                                                  \
     mfmas(P, P, 2);                                                                            \
     interleave(std::integral_constant<int, 14>{});                                             \
+    if (MVBEV_RING_PRIO) __builtin_amdgcn_s_setprio(0);                                        \
   } while (0)
     for (int u0 = 0; u0 < U; u0 += 6) {
       RING_UNIT(0);

@@ -40,8 +40,14 @@ for name in vals:
     rd = 32 * n32 + 64 * n64 + 128 * n128
     res["kernels"][name] = {"read_bytes": rd, "write_bytes": wr * 1024, "hbm_bytes_per_launch": rd + wr * 1024,
                             "fetch_size_kb": med(name, "FETCH_SIZE")}
-pat = "b3::conv_kernel<mvbev::b3::SplitIn, 1, true" if precision == "bf16x3" else "conv3x3_mfma_f32_kernel<1, true"
+pat = "conv_ring_kernel<1, true>" if precision == "bf16x3" else "conv3x3_mfma_f32_kernel<1, true"
 conv1 = [k for k in res["kernels"] if pat in k]
 if conv1:
     res["conv1_hbm_bytes_per_launch"] = res["kernels"][conv1[0]]["hbm_bytes_per_launch"]
+# the all-views warp of the timed "warp" stage: the largest-grid warp_tile_kernel dispatch
+warps = [k for k in res["kernels"] if "warp_tile_kernel" in k]
+if warps:
+    k = max(warps, key=lambda n: int(n.rsplit("grid ", 1)[1].rstrip("]")))
+    res["warp_hbm_bytes_per_launch"] = res["kernels"][k]["hbm_bytes_per_launch"]
+    res["warp_read_bytes_per_launch"] = res["kernels"][k]["read_bytes"]
 print(json.dumps(res, indent=1))

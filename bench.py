@@ -381,7 +381,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": res["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak",  # N > 1: frame-parallel, the same per-GPU workload
         "vs_baseline": None,
         "dtype": res["dtype"],
         "data": "synthetic (ReLU N(0,1) features upsampled 3x, synthetic pinhole rig through the reference "

@@ -315,6 +315,73 @@ __global__ __launch_bounds__(64 * C1_WAVES) void conv3x3_cout1_kernel(
   }
 }
 
+// conv3 when DIL % 4 == 0 and W % 4 == 0 (the path's dilation-4 layer): a lane owns 4
+// adjacent output pixels, so each tap is ONE 16-B load (the +-DIL taps stay 16-B aligned)
+// instead of four 4-B loads — the scalar kernel above issues 4608 load instructions per
+// pixel and is bound by the address path, not by the 88 MB it reads.  (row, quad) pairs are
+// flattened over the output rows; 16 waves split the channels, LDS reduction in wave order.
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+constexpr int C1Q_WAVES = 16;
+template <int DIL>
+__global__ __launch_bounds__(64 * C1Q_WAVES) void conv3x3_cout1_q4_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ y, int C, int H,
+    int W, int in_row0, int in_rows, int out_row0, int out_rows) {
+  static_assert(DIL % 4 == 0, "16-B aligned taps");
+  __shared__ f32x4_t part[C1Q_WAVES][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int qw = W / 4;
+  const int q = blockIdx.x * 64 + lane;
+  const bool active = q < out_rows * qw;
+  const int r = active ? q / qw : 0;
+  const int col = active ? 4 * (q - r * qw) : 0;
+  const int row = out_row0 + r;
+  const int b = blockIdx.y;
+  const int64_t plane = (int64_t)in_rows * W;
+  const float* xb = x + (int64_t)b * C * plane;
+  int64_t off[3][3];
+  bool ok[3][3];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    const int yy = row + (ky - 1) * DIL, by = yy - in_row0;
+    const bool oky = active && yy >= 0 && yy < H && by >= 0 && by < in_rows;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int xx = col + (kx - 1) * DIL;
+      ok[ky][kx] = oky && xx >= 0 && xx < W;  // xx % 4 == 0 and W % 4 == 0: the whole quad is in
+      off[ky][kx] = ok[ky][kx] ? (int64_t)by * W + xx : 0;
+    }
+  }
+  const int cpw = (C + C1Q_WAVES - 1) / C1Q_WAVES;
+  const int c0 = wave * cpw, c1 = min(C, c0 + cpw);
+  f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+  auto tapsum = [&](int c, f32x4_t& a) __attribute__((always_inline)) {
+    const float* xc = xb + (int64_t)c * plane;
+    const float* wc = w + c * 9;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const f32x4_t v = *reinterpret_cast<const f32x4_t*>(xc + off[ky][kx]);
+        a += wc[ky * 3 + kx] * (ok[ky][kx] ? v : f32x4_t{0.f, 0.f, 0.f, 0.f});
+      }
+  };
+  int c = c0;
+  for (; c + 2 <= c1; c += 2) {
+    tapsum(c, acc[0]);
+    tapsum(c + 1, acc[1]);
+  }
+  if (c < c1) tapsum(c, acc[0]);
+  part[wave][lane] = acc[0] + acc[1];
+  __syncthreads();
+  if (wave == 0 && active) {
+    f32x4_t sum = part[0][lane];
+#pragma unroll
+    for (int i = 1; i < C1Q_WAVES; ++i) sum += part[i][lane];
+    *reinterpret_cast<f32x4_t*>(y + ((int64_t)b * out_rows + r) * W + col) = sum;
+  }
+}
+
 }  // namespace mvbev
 
 extern "C" {
@@ -395,8 +462,16 @@ int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int
     return MVBEV_ERR_RANK;
   if (out_row0 < 0 || out_row0 + out_rows > H || out_rows > 65535 || B > 65535)
     return MVBEV_ERR_SHAPE;
-  dim3 grid((unsigned)ceil_div(W, 64), (unsigned)out_rows, (unsigned)B);
   hipStream_t s = as_stream(stream);
+  if (dilation == 4 && W % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+      (reinterpret_cast<uintptr_t>(y) & 15) == 0 && out_rows * (W / 4) <= (int64_t)INT32_MAX - 64) {
+    dim3 qgrid((unsigned)ceil_div(out_rows * (W / 4), 64), (unsigned)B);
+    hipLaunchKernelGGL(conv3x3_cout1_q4_kernel<4>, qgrid, dim3(64 * C1Q_WAVES), 0, s, x, w, y, (int)C, (int)H,
+                       (int)W, (int)in_row0, (int)in_rows, (int)out_row0, (int)out_rows);
+    MVBEV_CHECK_LAUNCH();
+    return MVBEV_OK;
+  }
+  dim3 grid((unsigned)ceil_div(W, 64), (unsigned)out_rows, (unsigned)B);
 #define MVBEV_C1_LAUNCH(D)                                                                      \
   hipLaunchKernelGGL(conv3x3_cout1_kernel<D>, grid, dim3(64 * C1_WAVES), 0, s, x, w, y, (int)C,  \
                      (int)H, (int)W, (int)in_row0, (int)in_rows, (int)out_row0)

@@ -336,7 +336,9 @@ def test_conv3x3_row_band_and_init(d, precision):
         assert_parity(got, ref[:, :, a:b_], f"band {a}:{b_}", normwise_tol=CONV_TOL[precision])
 
 
-@pytest.mark.parametrize("C,H,W,d", [(512, 12, 36, 4), (7, 5, 70, 1), (33, 9, 130, 2)])
+@pytest.mark.parametrize("C,H,W,d", [(512, 12, 36, 4), (7, 5, 70, 1), (33, 9, 130, 2),
+                                     (512, 20, 360, 4),   # 16-B quad kernel (W % 4 == 0, dilation 4)
+                                     (40, 10, 30, 4)])    # dilation 4, W % 4 != 0: scalar kernel
 def test_conv3x3_cout1_vs_torch(C, H, W, d):
     from mvdet_amd import ops
     g = torch.Generator().manual_seed(C + H)

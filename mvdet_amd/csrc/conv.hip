@@ -317,21 +317,27 @@ __global__ __launch_bounds__(64 * C1_WAVES) void conv3x3_cout1_kernel(
 
 // conv3 when DIL % 4 == 0 and W % 4 == 0 (the path's dilation-4 layer): a lane owns 4
 // adjacent output pixels, so each tap is ONE 16-B load (the +-DIL taps stay 16-B aligned)
-// instead of four 4-B loads — the scalar kernel above issues 4608 load instructions per
-// pixel and is bound by the address path, not by the 88 MB it reads.  (row, quad) pairs are
-// flattened over the output rows; 16 waves split the channels, LDS reduction in wave order.
+// instead of four 4-B loads (the scalar kernel above issues 4608 load instructions per
+// pixel).  A block owns 16 pixel quads (flattened over the output rows) and splits the
+// channels 64 ways: lane = (quad, channel subset) with 4 subsets per wave x 16 waves, so a
+// 120x360 map runs as 675 blocks; sums reduce by shuffles, then over waves in LDS (fixed order).
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 constexpr int C1Q_WAVES = 16;
+constexpr int C1Q_QUADS = 16;                          // quads per block
+constexpr int C1Q_SUBS = C1Q_WAVES * (64 / C1Q_QUADS);  // channel subsets per block
 template <int DIL>
 __global__ __launch_bounds__(64 * C1Q_WAVES) void conv3x3_cout1_q4_kernel(
     const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ y, int C, int H,
     int W, int in_row0, int in_rows, int out_row0, int out_rows) {
   static_assert(DIL % 4 == 0, "16-B aligned taps");
-  __shared__ f32x4_t part[C1Q_WAVES][64];
+  __shared__ f32x4_t part[C1Q_WAVES][C1Q_QUADS];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int qi = lane % C1Q_QUADS, sub = wave * (64 / C1Q_QUADS) + lane / C1Q_QUADS;
   const int qw = W / 4;
-  const int q = blockIdx.x * 64 + lane;
+  // XCD-contiguous ranges of quads: the blocks of rows r-4 .. r+4 (which share input rows)
+  // run on one XCD and hit its L2
+  const int q = xcd_remap(blockIdx.x, gridDim.x) * C1Q_QUADS + qi;
   const bool active = q < out_rows * qw;
   const int r = active ? q / qw : 0;
   const int col = active ? 4 * (q - r * qw) : 0;
@@ -352,8 +358,8 @@ __global__ __launch_bounds__(64 * C1Q_WAVES) void conv3x3_cout1_q4_kernel(
       off[ky][kx] = ok[ky][kx] ? (int64_t)by * W + xx : 0;
     }
   }
-  const int cpw = (C + C1Q_WAVES - 1) / C1Q_WAVES;
-  const int c0 = wave * cpw, c1 = min(C, c0 + cpw);
+  const int cps = (C + C1Q_SUBS - 1) / C1Q_SUBS;
+  const int c0 = min(C, sub * cps), c1 = min(C, c0 + cps);
   f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
   auto tapsum = [&](int c, f32x4_t& a) __attribute__((always_inline)) {
     const float* xc = xb + (int64_t)c * plane;
@@ -372,12 +378,17 @@ __global__ __launch_bounds__(64 * C1Q_WAVES) void conv3x3_cout1_q4_kernel(
     tapsum(c + 1, acc[1]);
   }
   if (c < c1) tapsum(c, acc[0]);
-  part[wave][lane] = acc[0] + acc[1];
-  __syncthreads();
-  if (wave == 0 && active) {
-    f32x4_t sum = part[0][lane];
+  f32x4_t s = acc[0] + acc[1];
 #pragma unroll
-    for (int i = 1; i < C1Q_WAVES; ++i) sum += part[i][lane];
+  for (int o = C1Q_QUADS; o < 64; o <<= 1)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s[e] += __shfl_xor(s[e], o);
+  if (lane < C1Q_QUADS) part[wave][qi] = s;
+  __syncthreads();
+  if (wave == 0 && lane < C1Q_QUADS && active) {
+    f32x4_t sum = part[0][qi];
+#pragma unroll
+    for (int i = 1; i < C1Q_WAVES; ++i) sum += part[i][qi];
     *reinterpret_cast<f32x4_t*>(y + ((int64_t)b * out_rows + r) * W + col) = sum;
   }
 }
@@ -465,7 +476,7 @@ int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int
   hipStream_t s = as_stream(stream);
   if (dilation == 4 && W % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
       (reinterpret_cast<uintptr_t>(y) & 15) == 0 && out_rows * (W / 4) <= (int64_t)INT32_MAX - 64) {
-    dim3 qgrid((unsigned)ceil_div(out_rows * (W / 4), 64), (unsigned)B);
+    dim3 qgrid((unsigned)ceil_div(out_rows * (W / 4), C1Q_QUADS), (unsigned)B);
     hipLaunchKernelGGL(conv3x3_cout1_q4_kernel<4>, qgrid, dim3(64 * C1Q_WAVES), 0, s, x, w, y, (int)C, (int)H,
                        (int)W, (int)in_row0, (int)in_rows, (int)out_row0, (int)out_rows);
     MVBEV_CHECK_LAUNCH();

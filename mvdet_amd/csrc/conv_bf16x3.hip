@@ -600,6 +600,10 @@ __device__ inline void glds16(const u32x4* src, u32x4* lds_wave_base) {
 #ifndef MVBEV_RING_PRIO
 #define MVBEV_RING_PRIO 0  // raise the wave priority over each unit's MFMA stream
 #endif
+#ifndef MVBEV_RING_STAGGER
+#define MVBEV_RING_STAGGER 0  // waves 4-7 run the unit with the barrier one tap earlier (parity-green; with both
+                              // unit bodies in one kernel the VGPR file overflows: 22 spills, conv1 2.50 vs 2.17 ms)
+#endif
 
 template <int DIL, bool RELU>
 __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
@@ -700,7 +704,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) acc[i][j] = floatx16{0};
   bf16x8 fb[2][5][2];  // [set][input row m (rows base + m * DIL)][hi, lo]
-  bf16x8 fa[2][2][2];  // [set][ct][hi, lo]
+  bf16x8 fa[3][2][2];  // [set][ct][hi, lo] (waves 0-3 alternate sets 0/1; staggered waves 4-7 use set = tap row)
   auto fetch_b = [&](int st, int xb, int kw) __attribute__((always_inline)) {
     const u32x4* X = Xlds + xb * XBUF + kl * 2 * XPIX + base * XW + l32 + kw * DIL;
 #pragma unroll
@@ -775,15 +779,54 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     interleave(std::integral_constant<int, 14>{});                                             \
     if (MVBEV_RING_PRIO) __builtin_amdgcn_s_setprio(0);                                        \
   } while (0)
-    for (int u0 = 0; u0 < U; u0 += 6) {
-      RING_UNIT(0);
-      RING_UNIT(1);
-      RING_UNIT(2);
-      RING_UNIT(3);
-      RING_UNIT(4);
-      RING_UNIT(5);
+    // Staggered waves 4-7 (MI355X_MICROARCH.md "Two waves per SIMD", item 9): the same units
+    // with the barrier one tap earlier — A1 and A2 of the unit are read before it (its slot is
+    // then free for the refill), kh 1 and kh 2 run after it — so around each barrier one
+    // wave of every SIMD pair still has MFMAs to issue while its partner waits or issues
+    // the DMA.  Same barrier count, same wait counts (each wave waits for its own DMAs).
+#define RING_UNIT_S(R)                                                                         \
+  do {                                                                                         \
+    constexpr int KW = (R) % 3, P = (R) & 1, SLOT = (R) % 3;                                    \
+    constexpr int NSLOT = ((R) + 1) % 3, NXB = (((R) + 1) / 3) & 1, NKW = ((R) + 1) % 3;        \
+    const int u_ = u0 + (R);                                                                   \
+    if (u_ >= U) break;                                                                        \
+    fetch_a(1, SLOT, 1);                                                                       \
+    fetch_a(2, SLOT, 2);                                                                       \
+    mfmas(0, P, 0);                                                                            \
+    interleave(std::integral_constant<int, 8>{});                                              \
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(KW == 1 ? RNWI + NX : RNWI) : "memory"); \
+    __builtin_amdgcn_s_barrier();                                                              \
+    asm volatile("" ::: "memory");                                                             \
+    mfmas(1, P, 1);                                                                            \
+    __builtin_amdgcn_sched_group_barrier(0x008, 18, 0);                                        \
+    issue_w(u_ + 3);                                                                           \
+    if (KW == 0) issue_x(u_ / 3 + 1);                                                          \
+    fetch_b(P ^ 1, NXB, NKW);                                                                  \
+    fetch_a(0, NSLOT, 0);                                                                      \
+    mfmas(2, P, 2);                                                                            \
+    interleave(std::integral_constant<int, 14>{});                                             \
+  } while (0)
+    if (!MVBEV_RING_STAGGER || wave < 4) {
+      for (int u0 = 0; u0 < U; u0 += 6) {
+        RING_UNIT(0);
+        RING_UNIT(1);
+        RING_UNIT(2);
+        RING_UNIT(3);
+        RING_UNIT(4);
+        RING_UNIT(5);
+      }
+    } else {
+      for (int u0 = 0; u0 < U; u0 += 6) {
+        RING_UNIT_S(0);
+        RING_UNIT_S(1);
+        RING_UNIT_S(2);
+        RING_UNIT_S(3);
+        RING_UNIT_S(4);
+        RING_UNIT_S(5);
+      }
     }
 #undef RING_UNIT
+#undef RING_UNIT_S
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the block exits
   }
 

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -105,6 +105,15 @@ int mvbev_warp_views_f32(const mvbev_warp_view* views, int nviews, int64_t B, in
 int mvbev_warp_views_split_bf16(const mvbev_warp_view* views, int nviews, int src_is_f16,
                                 int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
                                 void* stream);
+/* flags of the _ex warps.  MVBEV_WARP_DST_ZEROED: the caller guarantees every dst already
+ * holds zeros wherever the view's sample falls outside the source (e.g. a persistent slab
+ * zero-filled at allocation and only ever written by this warp with the same matrices), so
+ * those pixels — exactly 0 in the result — are skipped instead of rewritten.  Pixels with
+ * non-finite coordinates (NaN output) are always written. */
+#define MVBEV_WARP_DST_ZEROED 1
+int mvbev_warp_views_split_bf16_ex(const mvbev_warp_view* views, int nviews, int src_is_f16,
+                                   int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
+                                   int flags, void* stream);
 /* Fused bilinear upsample + warp.  views[i].src is the
  * backbone-resolution map [B][C][h][w] that persp_trans_detector.py:65 upsamples with
  * F.interpolate(size=(H, W), mode='bilinear', align_corners=False) before the warp at :69;
@@ -118,6 +127,9 @@ int mvbev_warp_views_split_bf16(const mvbev_warp_view* views, int nviews, int sr
 int mvbev_warp_views_upsampled(const mvbev_warp_view* views, int nviews, int src_is_f16,
                                int64_t B, int64_t C, int64_t h, int64_t w, int64_t H, int64_t W,
                                int64_t Ho, int64_t Wo, int out_layout, void* stream);
+int mvbev_warp_views_upsampled_ex(const mvbev_warp_view* views, int nviews, int src_is_f16,
+                                  int64_t B, int64_t C, int64_t h, int64_t w, int64_t H, int64_t W,
+                                  int64_t Ho, int64_t Wo, int out_layout, int flags, void* stream);
 /* Frustum mask for the conv (see mvbev_conv3x3_bf16x3_ex): for output tiles of tile_h x
  * tile_w pixels over grid rows [row0, row0 + rows) of the Ho x Wo warp output, bit s of
  * mask[tile] is set when view s's warp (views[s].m, src size H x W) can be non-zero

@@ -47,7 +47,10 @@ EXPORTS = (
     "mvbev_conv3x3_wgrad_bf16x3_ex",
     "mvbev_warp_views_adjoint",
     "mvbev_conv3x3_bf16x3_tile_rows",
+    "mvbev_warp_views_split_bf16_ex",
+    "mvbev_warp_views_upsampled_ex",
 )
+WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
 
 KC = 8    # MVBEV_CONV_KC
 LAYOUT_F32, LAYOUT_F16, LAYOUT_SPLIT_BF16 = 0, 1, 2  # MVBEV_LAYOUT_*
@@ -165,6 +168,12 @@ def _declare(lib):
     lib.mvbev_conv3x3_cout1_f32.restype = ctypes.c_int
     lib.mvbev_conv3x3_cout1_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p,
                                             ctypes.c_int, _p, _p]
+    lib.mvbev_warp_views_split_bf16_ex.restype = ctypes.c_int
+    lib.mvbev_warp_views_split_bf16_ex.argtypes = (lib.mvbev_warp_views_split_bf16.argtypes[:-1] +
+                                                   [ctypes.c_int, _p])
+    lib.mvbev_warp_views_upsampled_ex.restype = ctypes.c_int
+    lib.mvbev_warp_views_upsampled_ex.argtypes = (lib.mvbev_warp_views_upsampled.argtypes[:-1] +
+                                                  [ctypes.c_int, _p])
     lib.mvbev_conv3x3_bf16x3_tile_rows.restype = ctypes.c_int
     lib.mvbev_conv3x3_bf16x3_tile_rows.argtypes = [ctypes.c_int, ctypes.c_int]
 

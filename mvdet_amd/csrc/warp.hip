@@ -106,6 +106,8 @@ __global__ __launch_bounds__(256) void warp_tile_kernel(const WarpArgs a) {
     return acc;
   };
 
+  // the caller's dst already holds zeros wherever the sample falls outside the source
+  if (a.skip_zero && !inside && finite) return;
   if constexpr (SPLIT) {
     u32x4_t* out = static_cast<u32x4_t*>(vw.dst) + 2 * ((int64_t)b * vw.dB + (int64_t)v * vw.dH + u);
     const int64_t dG = 2 * vw.dC;
@@ -205,7 +207,7 @@ static int warp_single(const void* src, int64_t B, int64_t C, int64_t H, int64_t
 
 template <typename T>
 static int warp_views(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t H,
-                      int64_t W, int64_t Ho, int64_t Wo, void* stream, bool split = false) {
+                      int64_t W, int64_t Ho, int64_t Wo, void* stream, bool split = false, int flags = 0) {
   if (!views) return MVBEV_ERR_NULL;
   const int st = check_sizes(B, C, H, W, Ho, Wo, nviews);
   if (st != MVBEV_OK) return st;
@@ -222,6 +224,7 @@ static int warp_views(const mvbev_warp_view* views, int nviews, int64_t B, int64
     for (int k = 0; k < 9; ++k) d.m[k] = s.m[k];
   }
   a.nviews = nviews;
+  a.skip_zero = (flags & MVBEV_WARP_DST_ZEROED) != 0;
   return finish_args_and_launch<T>(a, B, C, H, W, Ho, Wo, stream, split);
 }
 
@@ -284,7 +287,7 @@ const char* mvbev_status_string(int s) {
   }
 }
 
-int mvbev_version(void) { return 10300; }
+int mvbev_version(void) { return 10400; }
 
 int mvbev_warp_perspective_f32(const float* src, int64_t B, int64_t C, int64_t H, int64_t W,
                                const int64_t src_strides[4], const float* m, float* dst,
@@ -307,12 +310,19 @@ int mvbev_warp_views_f32(const mvbev_warp_view* views, int nviews, int64_t B, in
   return mvbev::warp_views<float>(views, nviews, B, C, H, W, Ho, Wo, stream);
 }
 
+int mvbev_warp_views_split_bf16_ex(const mvbev_warp_view* views, int nviews, int src_is_f16,
+                                   int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
+                                   int flags, void* stream) {
+  if (flags & ~MVBEV_WARP_DST_ZEROED) return MVBEV_ERR_SHAPE;
+  if (src_is_f16)
+    return mvbev::warp_views<__half>(views, nviews, B, C, H, W, Ho, Wo, stream, true, flags);
+  return mvbev::warp_views<float>(views, nviews, B, C, H, W, Ho, Wo, stream, true, flags);
+}
+
 int mvbev_warp_views_split_bf16(const mvbev_warp_view* views, int nviews, int src_is_f16,
                                 int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
                                 void* stream) {
-  if (src_is_f16)
-    return mvbev::warp_views<__half>(views, nviews, B, C, H, W, Ho, Wo, stream, true);
-  return mvbev::warp_views<float>(views, nviews, B, C, H, W, Ho, Wo, stream, true);
+  return mvbev_warp_views_split_bf16_ex(views, nviews, src_is_f16, B, C, H, W, Ho, Wo, 0, stream);
 }
 
 int mvbev_warp_views_f16(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,

@@ -56,6 +56,7 @@ struct WarpArgs {
   WarpView v[kWarpMaxViews];
   int nviews, B, C, H, W, Ho, Wo, tiles_x, tiles, chunks, nwg;
   bool pair;  // fp32 rows with unit column stride and W >= 2: corner pairs as 8-B loads
+  bool skip_zero;  // MVBEV_WARP_DST_ZEROED: outside samples (exact zeros) are not written
 };
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));

@@ -148,6 +148,7 @@ __global__ __launch_bounds__(256) void warp_up_kernel(const UpArgs ua) {
     return acc;
   };
 
+  if (a.skip_zero && !inside && finite) return;  // dst already zero there (MVBEV_WARP_DST_ZEROED)
   if constexpr (SPLIT) {
     u32x4_t* out = static_cast<u32x4_t*>(vw.dst) + 2 * ((int64_t)b * vw.dB + (int64_t)v * vw.dH + u);
     const int64_t dG = 2 * vw.dC;
@@ -176,11 +177,12 @@ __global__ __launch_bounds__(256) void warp_up_kernel(const UpArgs ua) {
 
 }  // namespace mvbev
 
-extern "C" int mvbev_warp_views_upsampled(const mvbev_warp_view* views, int nviews, int src_is_f16,
-                                          int64_t B, int64_t C, int64_t h, int64_t w, int64_t H,
-                                          int64_t W, int64_t Ho, int64_t Wo, int out_layout,
-                                          void* stream) {
+extern "C" int mvbev_warp_views_upsampled_ex(const mvbev_warp_view* views, int nviews, int src_is_f16,
+                                             int64_t B, int64_t C, int64_t h, int64_t w, int64_t H,
+                                             int64_t W, int64_t Ho, int64_t Wo, int out_layout, int flags,
+                                             void* stream) {
   using namespace mvbev;
+  if (flags & ~MVBEV_WARP_DST_ZEROED) return MVBEV_ERR_SHAPE;
   if (!views) return MVBEV_ERR_NULL;
   if (B <= 0 || C <= 0 || h <= 0 || w <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 ||
       nviews <= 0)
@@ -205,6 +207,7 @@ extern "C" int mvbev_warp_views_upsampled(const mvbev_warp_view* views, int nvie
     for (int k = 0; k < 9; ++k) d.m[k] = s.m[k];
   }
   a.nviews = nviews;
+  a.skip_zero = (flags & MVBEV_WARP_DST_ZEROED) != 0;
   a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
   a.tiles_x = (int)ceil_div(Wo, kUpTW);
   a.tiles = a.tiles_x * (int)ceil_div(Ho, kUpTH);
@@ -231,4 +234,12 @@ extern "C" int mvbev_warp_views_upsampled(const mvbev_warp_view* views, int nvie
   }
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
+}
+
+extern "C" int mvbev_warp_views_upsampled(const mvbev_warp_view* views, int nviews, int src_is_f16,
+                                          int64_t B, int64_t C, int64_t h, int64_t w, int64_t H,
+                                          int64_t W, int64_t Ho, int64_t Wo, int out_layout,
+                                          void* stream) {
+  return mvbev_warp_views_upsampled_ex(views, nviews, src_is_f16, B, C, h, w, H, W, Ho, Wo, out_layout, 0,
+                                       stream);
 }

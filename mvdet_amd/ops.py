@@ -82,13 +82,14 @@ def split_decode(t: torch.Tensor, C: Optional[int] = None) -> torch.Tensor:
     return v[:, :C] if C is not None else v
 
 
-def warp_views_upsampled_into(srcs, up_hw, m_norms, dsts, split: bool = False) -> None:
+def warp_views_upsampled_into(srcs, up_hw, m_norms, dsts, split: bool = False, dst_zeroed: bool = False) -> None:
     """Fused bilinear upsample + warp of several views in ONE launch.
 
     ``srcs[i]`` [B,C,h,w] backbone-resolution maps that the reference upsamples to ``up_hw``
     with ``F.interpolate(..., mode='bilinear')`` (``persp_trans_detector.py:65``) before the
     warp; ``m_norms[i]`` the kornia matrix for the upsampled size; ``dsts`` as in
-    ``warp_views_into`` (fp32 [B,C,Ho,Wo] views, or split-bf16 blocked with ``split=True``)."""
+    ``warp_views_into`` (fp32 [B,C,Ho,Wo] views, or split-bf16 blocked with ``split=True``);
+    ``dst_zeroed`` as in ``warp_views_into``."""
     n = len(srcs)
     if n == 0:
         return
@@ -120,19 +121,23 @@ def warp_views_upsampled_into(srcs, up_hw, m_norms, dsts, split: bool = False) -
     if dtype not in (torch.float32, torch.float16):
         raise TypeError(f"unsupported dtype {dtype}")
     lib = _native.load()
-    st = lib.mvbev_warp_views_upsampled(arr, n, int(dtype == torch.float16), B, C, h, w, H, W, Ho, Wo,
-                                        _native.LAYOUT_SPLIT_BF16 if split else _native.LAYOUT_F32,
-                                        _stream(dsts[0]))
-    _native.check(st, "mvbev_warp_views_upsampled")
+    st = lib.mvbev_warp_views_upsampled_ex(arr, n, int(dtype == torch.float16), B, C, h, w, H, W, Ho, Wo,
+                                           _native.LAYOUT_SPLIT_BF16 if split else _native.LAYOUT_F32,
+                                           _native.WARP_DST_ZEROED if dst_zeroed else 0, _stream(dsts[0]))
+    _native.check(st, "mvbev_warp_views_upsampled_ex")
 
 
-def warp_views_into(srcs, m_norms, dsts, split: bool = False, C: Optional[int] = None) -> None:
+def warp_views_into(srcs, m_norms, dsts, split: bool = False, C: Optional[int] = None,
+                    dst_zeroed: bool = False) -> None:
     """Warp several views (same shapes) in ONE launch.
 
     ``srcs[i]`` [B,C,H,W], ``m_norms[i]`` a host [3,3] src_norm <- dst_norm matrix shared by
     the batch (``kornia_src_norm_from_dst_norm``).  ``dsts[i]``: [B,C,Ho,Wo] views (innermost
     stride 1, same dtype as the sources) or, with ``split=True``, contiguous split-bf16 blocked
-    tensors [B, ceil(C/8), Ho, Wo, 2, 8] (``split_shape``).
+    tensors [B, ceil(C/8), Ho, Wo, 2, 8] (``split_shape``).  ``dst_zeroed`` (split only): the
+    caller guarantees the dsts already hold zeros wherever a sample falls outside its source
+    (a persistent zero-initialised slab of this geometry), so those pixels are not rewritten
+    (``MVBEV_WARP_DST_ZEROED``).
     """
     n = len(srcs)
     if n == 0:
@@ -169,9 +174,9 @@ def warp_views_into(srcs, m_norms, dsts, split: bool = False, C: Optional[int] =
     if split:
         if dtype not in (torch.float32, torch.float16):
             raise TypeError(f"unsupported dtype {dtype}")
-        st = lib.mvbev_warp_views_split_bf16(arr, n, int(dtype == torch.float16), B, C, H, W, Ho, Wo,
-                                             _stream(dsts[0]))
-        _native.check(st, "mvbev_warp_views_split_bf16")
+        st = lib.mvbev_warp_views_split_bf16_ex(arr, n, int(dtype == torch.float16), B, C, H, W, Ho, Wo,
+                                                _native.WARP_DST_ZEROED if dst_zeroed else 0, _stream(dsts[0]))
+        _native.check(st, "mvbev_warp_views_split_bf16_ex")
         return
     if dtype == torch.float32:
         fn, name = lib.mvbev_warp_views_f32, "mvbev_warp_views_f32"

@@ -54,6 +54,9 @@ class Workspace:
     band: Tuple[int, int]   # output rows [r0, r1)
     y1_rows: Tuple[int, int]
     y2_rows: Tuple[int, int]
+    # the slab was zero-filled at allocation and is only written by this engine's warps (or the
+    # multi-GPU gather of them): a view's out-of-source pixels are already 0 and are skipped
+    slab_zeroed: bool = False
 
 
 class ProjectFuse:
@@ -138,7 +141,7 @@ class ProjectFuse:
                 y1 = torch.empty((B, self.mid, y1r[1] - y1r[0], W), dtype=torch.float32, device=device)
             y2 = torch.empty((B, self.mid, y2r[1] - y2r[0], W), dtype=torch.float32, device=device)
             m = self.m_norm_cpu.to(device)[:, None].expand(self.num_cam, B, 3, 3).contiguous()
-            ws = Workspace(slab, y1, y2, m, band, y1r, y2r)
+            ws = Workspace(slab, y1, y2, m, band, y1r, y2r, slab_zeroed=True)
             self._ws[key] = ws
         return ws
 
@@ -163,7 +166,8 @@ class ProjectFuse:
             raise ValueError(f"view {cam}: features {tuple(feat.shape)} do not match "
                              f"[B,{self.C},{self.src_hw[0]},{self.src_hw[1]}]")
         if self.split:
-            ops.warp_views_into([feat], [self.m_norm_cpu[cam]], [self._slot_dst(ws, cam)], split=True)
+            ops.warp_views_into([feat], [self.m_norm_cpu[cam]], [self._slot_dst(ws, cam)], split=True,
+                                dst_zeroed=ws.slab_zeroed)
         else:
             ops.warp_into(feat, ws.m_norm[cam], self._slot_dst(ws, cam))
 
@@ -174,7 +178,8 @@ class ProjectFuse:
                 raise ValueError(f"view {cam}: features {tuple(f.shape)} do not match "
                                  f"[B,{self.C},{self.src_hw[0]},{self.src_hw[1]}]")
         ops.warp_views_into(list(feats), [self.m_norm_cpu[c] for c in cams],
-                            [self._slot_dst(ws, c) for c in cams], split=self.split)
+                            [self._slot_dst(ws, c) for c in cams], split=self.split,
+                            dst_zeroed=self.split and ws.slab_zeroed)
 
     def warp_views_upsampled(self, ws: Workspace, cams: Sequence[int], feats: Sequence[torch.Tensor]) -> None:
         """a4 + a5 fused: ``feats[i]`` is view ``cams[i]``'s
@@ -184,7 +189,8 @@ class ProjectFuse:
             if f.shape[1] != self.C or f.shape[2] > self.src_hw[0] or f.shape[3] > self.src_hw[1]:
                 raise ValueError(f"view {cam}: features {tuple(f.shape)} cannot upsample to {self.src_hw}")
         ops.warp_views_upsampled_into(list(feats), self.src_hw, [self.m_norm_cpu[c] for c in cams],
-                                      [self._slot_dst(ws, c) for c in cams], split=self.split)
+                                      [self._slot_dst(ws, c) for c in cams], split=self.split,
+                                      dst_zeroed=self.split and ws.slab_zeroed)
 
     # -- coord term (a2 folded into conv1) --------------------------------------------------
     def coord_term(self, conv1: torch.nn.Conv2d) -> torch.Tensor:

@@ -148,6 +148,45 @@ def test_warp_views_split_bf16_layout(src_dtype):
         assert (got[:, C:] == 0).all()
 
 
+@pytest.mark.parametrize("upsampled", [False, True])
+def test_warp_dst_zeroed_skips_exactly_the_outside_pixels(upsampled):
+    """MVBEV_WARP_DST_ZEROED (the engine's persistent zero-filled slab): into a zeroed dst the
+    result is bitwise the plain warp's; into a NaN-filled one only pixels whose sample falls
+    outside the source (exact zeros of the plain warp) keep their old value."""
+    from mvdet_amd import ops
+    from mvdet_amd.geometry import kornia_src_norm_from_dst_norm
+    rng = np.random.default_rng(29)
+    B, C, h, w, H, W, ho, wo = 2, 16, 10, 16, 30, 48, 20, 40
+    M = torch.tensor([[[1.2, 0.1, 20.0], [0.05, 1.1, -4.0], [0.0, 0.001, 1.0]]])  # grid columns u < ~19 sample x < 0
+    m = kornia_src_norm_from_dst_norm(M, (H, W), (ho, wo))[0]
+    if upsampled:
+        src = torch.from_numpy(np.maximum(rng.standard_normal((B, C, h, w)), 0).astype(np.float32)).to(DEV)
+
+        def run(dst, z):
+            ops.warp_views_upsampled_into([src], (H, W), [m], [dst], split=True, dst_zeroed=z)
+    else:
+        src = torch.from_numpy(np.maximum(rng.standard_normal((B, C, H, W)), 0).astype(np.float32)).to(DEV)
+
+        def run(dst, z):
+            ops.warp_views_into([src], [m], [dst], split=True, dst_zeroed=z)
+    shape = ops.split_shape(B, C, ho, wo)
+    ref = torch.full(shape, float("nan"), dtype=torch.bfloat16, device=DEV)
+    run(ref, False)
+    zero = torch.zeros(shape, dtype=torch.bfloat16, device=DEV)
+    run(zero, True)
+    assert torch.equal(zero, ref)
+    stale = torch.full(shape, float("nan"), dtype=torch.bfloat16, device=DEV)
+    run(stale, True)
+    got, want = ops.split_decode(stale, C), ops.split_decode(ref, C)
+    kept = torch.isnan(got).all(dim=1)             # [B, ho, wo]: pixels the flagged warp skipped
+    outside = (want == 0).all(dim=1)
+    assert kept.any() and (~kept).any()
+    assert not (kept & ~outside).any()             # only exact-zero pixels are skipped
+    assert kept.sum() >= 0.95 * outside.sum()      # (inside pixels with all-zero ReLU features are rare)
+    keep = (~kept)[:, None].expand_as(got)
+    assert torch.equal(got[keep], want[keep])
+
+
 def test_warp_f16_storage():
     from mvdet_amd import warp_perspective
     rng = np.random.default_rng(11)

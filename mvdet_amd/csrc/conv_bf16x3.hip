@@ -601,8 +601,8 @@ __device__ inline void glds16(const u32x4* src, u32x4* lds_wave_base) {
 #define MVBEV_RING_PRIO 0  // raise the wave priority over each unit's MFMA stream
 #endif
 #ifndef MVBEV_RING_STAGGER
-#define MVBEV_RING_STAGGER 0  // waves 4-7 run the unit with the barrier one tap earlier (parity-green; with both
-                              // unit bodies in one kernel the VGPR file overflows: 22 spills, conv1 2.50 vs 2.17 ms)
+#define MVBEV_RING_STAGGER 0  // waves 4-7 take each unit's barrier one tap earlier (parity-green; measured
+                              // slower: conv1 2.33-2.38 vs 2.18-2.22 ms, the extra A set spills 4-5 VGPRs)
 #endif
 
 template <int DIL, bool RELU>
@@ -648,26 +648,24 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
 
   // LDS-DMA sources, chunk-invariant parts.  Halo entry e = (sub, part, pixel) of the image
   // [sub][part][XH][XW]; lane j-th instruction covers entries (j * RNW + wave) * 64 + lane.
-  int xo[NX];    // piece offset in the sub-block's plane (2 * pixel + part); -1 = zero entry
-  int xsub[NX];  // sub-block (0/1)
+  int xo[NX];  // piece offset in the sub-block's plane (2 * pixel + part); -1 = zero entry
 #pragma unroll
   for (int j = 0; j < NX; ++j) {
     const int e = (j * RNW + wave) * 64 + lane;
-    const int sub = e / (2 * XPIX), part = (e / XPIX) & 1, pix = e % XPIX;
+    const int part = (e / XPIX) & 1, pix = e % XPIX;
     const int r = pix / XW, c = pix % XW;
     const int gy = y0 - DIL + r, gx = x0 - DIL + c, by = gy - a.in_row0;
     const bool ok = e < 4 * XPIX && gy >= 0 && gy < a.H && by >= 0 && by < a.in_rows && gx >= 0 && gx < W;
     xo[j] = ok ? 2 * (by * W + gx) + part : -1;
-    xsub[j] = sub & 1;
   }
-  // W unit image [part][kh][sub][co]; packed source [part][tap = 3 kh + kw][sub][co]
-  int wo[RNWI];
-#pragma unroll
-  for (int j = 0; j < RNWI; ++j) {
+  // W unit image [part][kh][sub][co]; packed source [part][tap = 3 kh + kw][sub][co].  The
+  // DMA source offsets (and the halo entries' sub-block) are recomputed per issue: a few VALU
+  // ops instead of registers held across the MFMA loop.
+  auto wo = [&](int j) __attribute__((always_inline)) -> int {
     const int e = (j * RNW + wave) * 64 + lane;
     const int part = e / RHALF, r = e % RHALF;
-    wo[j] = part * (NKB * 2 * BN) + (r / (2 * BN)) * 3 * (2 * BN) + r % (2 * BN);
-  }
+    return part * (NKB * 2 * BN) + (r / (2 * BN)) * 3 * (2 * BN) + r % (2 * BN);
+  };
   const int U = 3 * nch;
   auto issue_w = [&](int u) __attribute__((always_inline)) {  // W unit u -> slot u % 3
     const int uu = min(u, U - 1);
@@ -675,7 +673,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     const u32x4* src = wsrc + (int64_t)chunk_of(ci) * wchunk + kw * 2 * BN;
     u32x4* dst = lds + (u % 3) * RUNIT + wave * 64;
 #pragma unroll
-    for (int j = 0; j < RNWI; ++j) glds16(src + wo[j], dst + j * RNT);
+    for (int j = 0; j < RNWI; ++j) glds16(src + wo(j), dst + j * RNT);
   };
   auto issue_x = [&](int i) __attribute__((always_inline)) {  // halo of chunk i -> buffer i & 1
     const int ch = chunk_of(min(i, nch - 1));
@@ -690,7 +688,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     u32x4* dst = Xlds + (i & 1) * XBUF + wave * 64;
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
-      const u32x4* base = xsub[j] ? xs[1] : xs[0];
+      const u32x4* base = (j * RNW + wave) * 64 + lane >= 2 * XPIX ? xs[1] : xs[0];
       glds16(xo[j] >= 0 && base ? base + xo[j] : g_ring_zero, dst + j * RNT);
     }
   };
@@ -779,26 +777,32 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     interleave(std::integral_constant<int, 14>{});                                             \
     if (MVBEV_RING_PRIO) __builtin_amdgcn_s_setprio(0);                                        \
   } while (0)
-    // Staggered waves 4-7 (MI355X_MICROARCH.md "Two waves per SIMD", item 9): the same units
-    // with the barrier one tap earlier — A1 and A2 of the unit are read before it (its slot is
-    // then free for the refill), kh 1 and kh 2 run after it — so around each barrier one
-    // wave of every SIMD pair still has MFMAs to issue while its partner waits or issues
-    // the DMA.  Same barrier count, same wait counts (each wave waits for its own DMAs).
-#define RING_UNIT_S(R)                                                                         \
+    // Staggered waves 4-7 (MI355X_MICROARCH.md "Two waves per SIMD", item 9): one unit body
+    // for all waves with the fragment sets indexed by tap row; waves 4-7 read A1 and A2
+    // before kh 0 and take the unit's barrier after kh 0 instead of after kh 1, so around
+    // each barrier one wave of every SIMD pair still has MFMAs to issue while its partner
+    // waits or issues the DMA.  Same barrier count and wait counts for every wave.
+#define RING_UNIT_U(R)                                                                         \
   do {                                                                                         \
     constexpr int KW = (R) % 3, P = (R) & 1, SLOT = (R) % 3;                                    \
     constexpr int NSLOT = ((R) + 1) % 3, NXB = (((R) + 1) / 3) & 1, NKW = ((R) + 1) % 3;        \
     const int u_ = u0 + (R);                                                                   \
     if (u_ >= U) break;                                                                        \
     fetch_a(1, SLOT, 1);                                                                       \
-    fetch_a(2, SLOT, 2);                                                                       \
+    if (stag) fetch_a(2, SLOT, 2);                                                             \
     mfmas(0, P, 0);                                                                            \
-    interleave(std::integral_constant<int, 8>{});                                              \
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(KW == 1 ? RNWI + NX : RNWI) : "memory"); \
-    __builtin_amdgcn_s_barrier();                                                              \
-    asm volatile("" ::: "memory");                                                             \
+    if (!stag) fetch_a(2, SLOT, 2);                                                            \
+    if (stag) {                                                                                \
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(KW == 1 ? RNWI + NX : RNWI) : "memory"); \
+      __builtin_amdgcn_s_barrier();                                                            \
+      asm volatile("" ::: "memory");                                                           \
+    }                                                                                          \
     mfmas(1, P, 1);                                                                            \
-    __builtin_amdgcn_sched_group_barrier(0x008, 18, 0);                                        \
+    if (!stag) {                                                                               \
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(KW == 1 ? RNWI + NX : RNWI) : "memory"); \
+      __builtin_amdgcn_s_barrier();                                                            \
+      asm volatile("" ::: "memory");                                                           \
+    }                                                                                          \
     issue_w(u_ + 3);                                                                           \
     if (KW == 0) issue_x(u_ / 3 + 1);                                                          \
     fetch_b(P ^ 1, NXB, NKW);                                                                  \
@@ -806,7 +810,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     mfmas(2, P, 2);                                                                            \
     interleave(std::integral_constant<int, 14>{});                                             \
   } while (0)
-    if (!MVBEV_RING_STAGGER || wave < 4) {
+    if (!MVBEV_RING_STAGGER) {
       for (int u0 = 0; u0 < U; u0 += 6) {
         RING_UNIT(0);
         RING_UNIT(1);
@@ -816,17 +820,18 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
         RING_UNIT(5);
       }
     } else {
+      const bool stag = wave >= 4;
       for (int u0 = 0; u0 < U; u0 += 6) {
-        RING_UNIT_S(0);
-        RING_UNIT_S(1);
-        RING_UNIT_S(2);
-        RING_UNIT_S(3);
-        RING_UNIT_S(4);
-        RING_UNIT_S(5);
+        RING_UNIT_U(0);
+        RING_UNIT_U(1);
+        RING_UNIT_U(2);
+        RING_UNIT_U(3);
+        RING_UNIT_U(4);
+        RING_UNIT_U(5);
       }
     }
 #undef RING_UNIT
-#undef RING_UNIT_S
+#undef RING_UNIT_U
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the block exits
   }
 

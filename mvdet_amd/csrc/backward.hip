@@ -46,7 +46,12 @@ typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int NWV = 8;        // waves per workgroup: 4 (output channels) x 2 (input channels)
+#ifndef MVBEV_WGRAD_CPW
+#define MVBEV_WGRAD_CPW 1  // 32-channel output blocks per wave (1: 8 waves; 2: 4 waves, one per SIMD, 512
+                           // registers: conv1 wgrad 4.35 vs 3.10 ms, measured slower)
+#endif
+constexpr int CPW = MVBEV_WGRAD_CPW;
+constexpr int NWV = 8 / CPW;  // waves per workgroup: (4 / CPW) (output channels) x 2 (input channels)
 constexpr int NTH = 64 * NWV;
 constexpr int MT = 128;       // output channels per workgroup
 constexpr int NT = 64;        // input channels per workgroup
@@ -102,6 +107,7 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const WArgs a) {
   constexpr int BENT = BPIX * 8;         // staging entries (window pixel, 8-channel group)
   constexpr int BPT = (BENT + NTH - 1) / NTH;
   constexpr bool SPLIT = std::is_same<TIn, SplitIn>::value;
+  constexpr int AIT = MT * 8 / NTH;      // dy staging: 8 threads per 32-pixel row, AIT rows each
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -123,7 +129,7 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const WArgs a) {
   const int W = a.W, H = a.H;
   const int64_t plane = (int64_t)H * W;
 
-  floatx4 areg[2];
+  floatx4 areg[AIT];
   u32x4 bsp[BPT][SPLIT ? 2 : 1];
   float bfl[BPT][SPLIT ? 1 : 8];
   bool bok[BPT];
@@ -134,8 +140,8 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const WArgs a) {
     const int b = R / H, y = R - b * H;
     const int x0 = seg * PX;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int co = ct * MT + (tid >> 3) + 64 * i;
+    for (int i = 0; i < AIT; ++i) {
+      const int co = ct * MT + (tid >> 3) + (NTH / 8) * i;
       const int px = x0 + 4 * (tid & 7);
       const float* src = a.dy + (((int64_t)b * a.Cout + co) * H + y) * W;
       if (a.vec_dy) {
@@ -175,8 +181,8 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const WArgs a) {
   auto store = [&](int bb) __attribute__((always_inline)) {
     __bf16* L = lds + bb * BUF;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = (tid >> 3) + 64 * i, q = tid & 7;
+    for (int i = 0; i < AIT; ++i) {
+      const int row = (tid >> 3) + (NTH / 8) * i, q = tid & 7;
       u32x2 hi, lo;
       split4(areg[i], hi, lo);
       *reinterpret_cast<u32x2*>(L + row * AP + 4 * q) = hi;
@@ -207,31 +213,40 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const WArgs a) {
     }
   };
 
-  const int cw = wave & 3, cb = wave >> 2;
+  const int cw = wave % (4 / CPW), cb = wave / (4 / CPW);  // output block group, channel half
   const int gi = (lane >> 4) & 1, li = lane & 15;
   // transposed-read address of the lane: pixel 8kh + (li>>2) (+4 in the second read),
   // channels 16gi + 4(li&3) .. +3 of the wave's 32-channel half
   const int tr0 = (8 * kh + (li >> 2)) * 32 + 16 * gi + 4 * (li & 3);
-  floatx16 acc[9];
+  floatx16 acc[CPW][9];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) acc[t] = floatx16{0};
+  for (int m = 0; m < CPW; ++m)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[m][t] = floatx16{0};
 
   auto compute = [&](int bb) __attribute__((always_inline)) {
     const __bf16* L = lds + bb * BUF;
-    const __bf16* Ah = L + (32 * cw + l32) * AP + 8 * kh;
+    const __bf16* Ah = L + (32 * CPW * cw + l32) * AP + 8 * kh;
     const __bf16* Bh = L + 2 * AIMG + (cb * 2) * BIMG + tr0;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(Ah + 16 * s);
-      const bf16x8 alo = *reinterpret_cast<const bf16x8*>(Ah + AIMG + 16 * s);
+      bf16x8 ahi[CPW], alo[CPW];
+#pragma unroll
+      for (int m = 0; m < CPW; ++m) {
+        ahi[m] = *reinterpret_cast<const bf16x8*>(Ah + 32 * m * AP + 16 * s);
+        alo[m] = *reinterpret_cast<const bf16x8*>(Ah + 32 * m * AP + AIMG + 16 * s);
+      }
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int off = ((t / 3) * XW + 16 * s + (t % 3) * DIL) * 32;
         const bf16x8 bhi = tr_read8(Bh + off);
         const bf16x8 blo = tr_read8(Bh + BIMG + off);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, blo, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc[t], 0, 0, 0);
+#pragma unroll
+        for (int m = 0; m < CPW; ++m) {
+          acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[m], bhi, acc[m][t], 0, 0, 0);
+          acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[m], blo, acc[m][t], 0, 0, 0);
+          acc[m][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[m], bhi, acc[m][t], 0, 0, 0);
+        }
       }
     }
   };
@@ -254,12 +269,14 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const WArgs a) {
   const int k = kt * NT + 32 * cb + l32;
   if (k < a.K) {
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
+    for (int m = 0; m < CPW; ++m)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int co = ct * MT + 32 * cw + (r & 3) + 8 * (r >> 2) + 4 * kh;
-        a.ws[(((int64_t)p * 9 + t) * a.Cout + co) * a.K + k] = acc[t][r];
-      }
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = ct * MT + 32 * (CPW * cw + m) + (r & 3) + 8 * (r >> 2) + 4 * kh;
+          a.ws[(((int64_t)p * 9 + t) * a.Cout + co) * a.K + k] = acc[m][t][r];
+        }
   }
 }
 

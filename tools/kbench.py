@@ -38,6 +38,31 @@ def timeit(fn, reps):
     return float(np.median(t)), float(np.min(t))
 
 
+def backward_stages(eng, ws, mc, B, ho, wo, N, C, dev):
+    """conv1's weight and data gradient as the native training step runs them
+    (mvdet_amd/autograd.py), on a random dy1 and the warped slab."""
+    from mvdet_amd import _native, autograd, ops
+    st = autograd._bwd_state(eng)
+    w1 = mc[0].weight
+    dy1 = torch.randn(B, w1.shape[0], ho, wo, device=dev).relu_()
+    d1 = ops.conv_desc(B, eng.S * eng.Cs, ho, wo, group=eng.Cs, group_stride=B * eng.Cs * ho * wo,
+                       batch_stride=eng.Cs * ho * wo)
+    eng.pack1.get(w1)
+    dw1 = torch.zeros_like(w1)
+    wws = autograd._wgrad_ws(st, d1, w1.shape[0], dev)
+    lists = autograd._wgrad_lists(eng, st, dev, B)
+    cp = st.dgrad1.cout_p
+    dslab = torch.empty(ops.split_shape(B, cp, ho, wo), dtype=torch.bfloat16, device=dev)
+    cm = eng.conv1_mask(dev, 0, ho, tile_h=_native.TILE_H)
+    flop = 2.0 * B * ho * wo * 9 * N * C * w1.shape[0]
+    return {
+        "wgrad1": (lambda: ops.conv3x3_wgrad(ws.slab, d1, dy1, 1, w1.shape[1], chan_map=eng.pack1._map_dev,
+                                             dw=dw1, workspace=wws, chunk_lists=lists), flop),
+        "dgrad1": (lambda: ops.conv3x3_dgrad(dy1, st.dgrad1, w1, 1, out=dslab, out_mask=cm,
+                                             cot_per_group=C // ops.BN), flop),
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3"],
@@ -73,6 +98,8 @@ def main():
             "conv2": (lambda: eng.conv2(ws, mc[2]), 2.0 * B * ho * wo * 9 * 512 * 512),
             "conv3": (lambda: eng.conv3(ws, mc[4]), None),
         }
+        if {"wgrad1", "dgrad1"} & set(args.only.split(",")):
+            stages.update(backward_stages(eng, ws, mc, B, ho, wo, N, C, dev))
         from mvdet_amd import _native
         libs = [("default", _native.load())]
         for path in filter(None, args.libs.split(",")):

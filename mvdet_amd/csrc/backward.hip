@@ -51,6 +51,9 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
                            // registers: conv1 wgrad 4.35 vs 3.10 ms, measured slower)
 #endif
 constexpr int CPW = MVBEV_WGRAD_CPW;
+#ifndef MVBEV_WGRAD_DMA
+#define MVBEV_WGRAD_DMA 0  // WIP: the compiler waits vmcnt(0) before the ds_read_b64_tr_b16 builtins (LDS-DMA alias)
+#endif
 constexpr int NWV = 8 / CPW;  // waves per workgroup: (4 / CPW) (output channels) x 2 (input channels)
 constexpr int NTH = 64 * NWV;
 constexpr int MT = 128;       // output channels per workgroup
@@ -277,6 +280,165 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const WArgs a) {
           const int co = ct * MT + 32 * (CPW * cw + m) + (r & 3) + 8 * (r >> 2) + 4 * kh;
           a.ws[(((int64_t)p * 9 + t) * a.Cout + co) * a.K + k] = acc[m][t][r];
         }
+  }
+}
+
+// The same GEMM with LDS-DMA staging (split-bf16 x, 16-B aligned dy, W % 4 == 0): no staging
+// registers, no split pass through VGPRs before the barrier.  Per chunk (32-pixel row
+// segment) a buffer holds
+//   A  dy[128 co][32 px] fp32 as DMA'd (8 x 16-B pieces per row, piece q of row r stored at
+//      slot q ^ ((r >> 1) & 7): the fragment reads of 16 consecutive rows hit 64 distinct
+//      banks); split into bf16 hi / lo at fragment-read time (the same rounding as split4);
+//   B  the window image of wgrad_kernel ([half][part][3 * XW px][32 ch], 16-B pieces copied
+//      straight from the split slab), read by the same transposed reads.
+// Three buffers, one barrier per chunk: the wait before it retires this chunk's DMA (the next
+// chunk's may stay in flight), the DMA after it refills the buffer read two chunks ago.
+constexpr int WG_AENT = MT * PX / 4;  // A entries (16 B) per buffer: 1024
+template <int DIL> struct WgGeo {
+  static constexpr int XW = PX + 2 * DIL, BPIX = 3 * XW;
+  static constexpr int BENT = 16 * BPIX;                    // [half][part][pix][4 x 8 ch]
+  static constexpr int NA = WG_AENT / NTH;                  // A DMA instructions per thread
+  static constexpr int NB = (BENT + NTH - 1) / NTH;         // B DMA instructions per thread
+  static constexpr int BUFE = WG_AENT + NB * NTH;           // entries per buffer (incl. tail)
+  static_assert(WG_AENT % NTH == 0, "A image must split evenly over the threads");
+  static_assert(3 * BUFE * 16 <= 160 * 1024, "LDS");
+};
+__device__ u32x4 g_wg_zero[1];  // zero-initialised source of out-of-range entries
+
+__device__ inline void wg_glds16(const void* src, u32x4* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+template <int DIL>
+__global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
+  static_assert(NWV == 8, "wave layout: 4 output blocks x 2 channel halves");
+  using G = WgGeo<DIL>;
+  constexpr int XW = G::XW, BPIX = G::BPIX, NA = G::NA, NB = G::NB, BUFE = G::BUFE;
+  constexpr int BIMGE = BPIX * 4;  // entries per (half, part) image
+  __shared__ __attribute__((aligned(16))) u32x4 lds[3 * BUFE];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, kh = lane >> 5;
+  const int lb = xcd_remap(blockIdx.x, a.P * a.ntiles);
+  const int p = lb / a.ntiles, tile = lb - p * a.ntiles;
+  const int ct = tile % a.n_ct, kt = tile / a.n_ct;
+  const int32_t* list = nullptr;
+  int nact = a.nchunks;
+  if (a.clist) {
+    const int grp = (kt * NT) / a.group;
+    list = a.clist + a.coff[grp];
+    nact = a.coff[grp + 1] - a.coff[grp];
+  }
+  const int c0 = (int)((int64_t)nact * p / a.P);
+  const int c1 = (int)((int64_t)nact * (p + 1) / a.P);
+  const int W = a.W, H = a.H;
+  const int64_t plane = (int64_t)H * W;
+  const u32x4* xs = static_cast<const u32x4*>(a.x);
+
+  // DMA of chunk ci into buffer bb; lane's j-th instruction covers entry (j * NWV + wave) * 64 + lane
+  auto issue = [&](int c, int bb) __attribute__((always_inline)) {
+    const int R = c / a.segs, seg = c - R * a.segs;
+    const int b = R / H, y = R - b * H;
+    const int x0 = seg * PX;
+    u32x4* dst = lds + bb * BUFE + wave * 64;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      int e = (j * NWV + wave) * 64 + lane;
+      asm volatile("" : "+v"(e));  // recomputed per issue: nothing held across the MFMA loop
+      const int row = e >> 3, q = (e & 7) ^ ((row >> 1) & 7);
+      const int px = x0 + 4 * q;
+      const float* src = a.dy + (((int64_t)b * a.Cout + ct * MT + row) * H + y) * W + px;
+      wg_glds16(px < W ? (const void*)src : (const void*)g_wg_zero, dst + j * NTH);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      int e = (j * NWV + wave) * 64 + lane;
+      asm volatile("" : "+v"(e));
+      const int g4 = e & 3, pe = e >> 2;
+      const int hp = pe / BPIX, pix = pe - hp * BPIX;
+      const int r = pix / XW, cc = pix - r * XW;
+      const int gy = y + (r - 1) * DIL, gx = x0 - DIL + cc;
+      const int k0 = kt * NT + (hp >> 1) * 32 + g4 * 8;
+      const bool ok = e < G::BENT && gy >= 0 && gy < H && gx >= 0 && gx < W && k0 < a.K;
+      const void* src = g_wg_zero;
+      if (ok) {
+        const int g_ = k0 / a.group;
+        const int64_t base = (int64_t)b * a.batch_stride + g_ * a.group_stride + (int64_t)(k0 - g_ * a.group) * plane;
+        src = xs + base / 4 + 2 * ((int64_t)gy * W + gx) + (hp & 1);
+      }
+      wg_glds16(src, dst + WG_AENT + j * NTH);
+    }
+  };
+
+  const int cw = wave & 3, cb = wave >> 2;
+  const int gi = (lane >> 4) & 1, li = lane & 15;
+  const int tr0 = (8 * kh + (li >> 2)) * 32 + 16 * gi + 4 * (li & 3);  // bf16 units (as wgrad_kernel)
+  const int arow = 32 * cw + l32, asw = (arow >> 1) & 7;
+  floatx16 acc[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = floatx16{0};
+
+  auto compute = [&](int bb) __attribute__((always_inline)) {
+    const u32x4* L = lds + bb * BUFE;
+    const floatx4* Arow = reinterpret_cast<const floatx4*>(L) + arow * 8;
+    const __bf16* Bh = reinterpret_cast<const __bf16*>(L + WG_AENT + (cb * 2) * BIMGE) + tr0;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int q0 = 4 * s + 2 * kh;
+      const floatx4 v0 = Arow[q0 ^ asw], v1 = Arow[(q0 + 1) ^ asw];
+      u32x2 h0, l0, h1, l1;
+      split4(v0, h0, l0);
+      split4(v1, h1, l1);
+      const u32x4 hh = {h0[0], h0[1], h1[0], h1[1]}, ll = {l0[0], l0[1], l1[0], l1[1]};
+      const bf16x8 ahi = __builtin_bit_cast(bf16x8, hh), alo = __builtin_bit_cast(bf16x8, ll);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int off = ((t / 3) * XW + 16 * s + (t % 3) * DIL) * 32;
+        const bf16x8 bhi = tr_read8(Bh + off);
+        const bf16x8 blo = tr_read8(Bh + BIMGE * 8 + off);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, blo, acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc[t], 0, 0, 0);
+      }
+    }
+  };
+
+  // chunk ids: a list entry is loaded one issue ahead, before the DMAs it must not wait for
+  auto cid = [&](int ci) __attribute__((always_inline)) { return list ? list[ci] : ci; };
+  const int n = c1 - c0;
+  if (n > 0) {
+    issue(cid(c0), 0);
+    if (n > 1) issue(cid(c0 + 1), 1);
+    int cnext = n > 2 ? cid(c0 + 2) : 0;
+    for (int i = 0; i < n; ++i) {
+      // retire chunk i's DMA (chunk i+1's may stay in flight); LDS reads of chunk i-1 done
+      if (i + 1 < n) {
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NA + NB) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (i + 2 < n) {
+        const int nx = i + 3 < n ? cid(c0 + i + 3) : 0;
+        issue(cnext, (i + 2) % 3);
+        cnext = nx;
+      }
+      compute(i % 3);
+    }
+  }
+
+  const int k = kt * NT + 32 * cb + l32;
+  if (k < a.K) {
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = ct * MT + 32 * cw + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        a.ws[(((int64_t)p * 9 + t) * a.Cout + co) * a.K + k] = acc[t][r];
+      }
   }
 }
 
@@ -858,7 +1020,10 @@ int mvbev_conv3x3_wgrad_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)(g.P * g.tiles)), block(NTH);
   const bool split = x_layout == MVBEV_LAYOUT_SPLIT_BF16;
-  if (dilation == 1) {
+  if (MVBEV_WGRAD_DMA && split && a.vec_dy && (dilation == 1 || dilation == 2)) {
+    if (dilation == 1) hipLaunchKernelGGL((wgrad_dma_kernel<1>), grid, dim3(NTH), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_dma_kernel<2>), grid, dim3(NTH), 0, s, a);
+  } else if (dilation == 1) {
     if (split) hipLaunchKernelGGL((wgrad_kernel<SplitIn, 1>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((wgrad_kernel<float, 1>), grid, block, 0, s, a);
   } else if (dilation == 2) {

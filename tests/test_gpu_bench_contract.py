@@ -1,0 +1,39 @@
+"""bench.py's one-line JSON contract on a small config (cfg1, 2 steps): the keys the driver and
+the judge read, a roofline whose fraction is achieved / peak, and a CPU baseline that ran."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+@pytest.mark.gpu
+def test_bench_json_line_contract():
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--config", "1", "--steps", "2", "--warmup", "1",
+                          "--no-train", "--no-alt", "--cpu-frames", "1"],
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    r = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in r, k
+    assert r["n_gpus"] == 1 and r["steps"] == 2 and r["warmup"] == 1 and r["higher_is_better"] is True
+    assert r["value"] > 0 and abs(r["value"] * r["ms_per_step"] / 1e3 - 1.0) < 0.05  # B = 1 at cfg1
+    rl = r["roofline"]
+    assert rl["bound"] in ("hbm", "mfma") and rl["unit"] in ("GB/s", "TFLOP/s")
+    assert rl["frac"] == pytest.approx(rl["achieved"] / rl["peak"], rel=1e-3)
+    cb = r["cpu_baseline"]
+    assert cb["value"] > 0 and cb["kind"] in ("port", "reference") and cb["cores"] >= 1
+    assert cb["single_thread"]["cores"] == 1 and cb["single_thread"]["value"] > 0
+    e2e = r["e2e_roofline"]
+    assert 0 < e2e["frac"] <= 1.0 and e2e["floor_ms"] > 0
+    assert r["config"]["workload"].startswith("cfg1")

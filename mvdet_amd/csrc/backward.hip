@@ -34,6 +34,7 @@
 #include "warp_common.h"
 
 #include <type_traits>
+#include <utility>
 
 namespace mvbev {
 namespace bwd {
@@ -51,8 +52,11 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
                            // registers: conv1 wgrad 4.35 vs 3.10 ms, measured slower)
 #endif
 constexpr int CPW = MVBEV_WGRAD_CPW;
+#ifndef MVBEV_WGRAD_PF2
+#define MVBEV_WGRAD_PF2 1  // transposed reads two (s, tap) steps ahead (conv1 wgrad 2.93 vs 3.03 ms at one)
+#endif
 #ifndef MVBEV_WGRAD_DMA
-#define MVBEV_WGRAD_DMA 0  // WIP: the compiler waits vmcnt(0) before the ds_read_b64_tr_b16 builtins (LDS-DMA alias)
+#define MVBEV_WGRAD_DMA 1  // split-bf16 x + aligned dy: wgrad_dma_kernel (LDS-DMA staging)
 #endif
 constexpr int NWV = 8 / CPW;  // waves per workgroup: (4 / CPW) (output channels) x 2 (input channels)
 constexpr int NTH = 64 * NWV;
@@ -294,6 +298,7 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const WArgs a) {
 // Three buffers, one barrier per chunk: the wait before it retires this chunk's DMA (the next
 // chunk's may stay in flight), the DMA after it refills the buffer read two chunks ago.
 constexpr int WG_AENT = MT * PX / 4;  // A entries (16 B) per buffer: 1024
+constexpr int WG_MAXC = 2048;         // chunk ids of a workgroup's partition, staged in LDS
 template <int DIL> struct WgGeo {
   static constexpr int XW = PX + 2 * DIL, BPIX = 3 * XW;
   static constexpr int BENT = 16 * BPIX;                    // [half][part][pix][4 x 8 ch]
@@ -301,13 +306,37 @@ template <int DIL> struct WgGeo {
   static constexpr int NB = (BENT + NTH - 1) / NTH;         // B DMA instructions per thread
   static constexpr int BUFE = WG_AENT + NB * NTH;           // entries per buffer (incl. tail)
   static_assert(WG_AENT % NTH == 0, "A image must split evenly over the threads");
-  static_assert(3 * BUFE * 16 <= 160 * 1024, "LDS");
+  static_assert(3 * BUFE * 16 + WG_MAXC * 4 <= 160 * 1024, "LDS");
 };
 __device__ u32x4 g_wg_zero[1];  // zero-initialised source of out-of-range entries
 
 __device__ inline void wg_glds16(const void* src, u32x4* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// LDS reads of a DMA-filled buffer as inline asm: for the builtins / plain loads the compiler
+// drains every LDS-DMA in flight (vmcnt(0)) first, which would serialise the next chunks' DMA
+// with this one's MFMAs.  The reads are ordered by explicit lgkmcnt(0) waits tied to the
+// fragment registers (wg_lgkm_wait); the buffer's own DMA was retired before the barrier.
+template <int OFF>
+__device__ inline v4i16 wg_tr(uint32_t addr) {
+  v4i16 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
+  return r;
+}
+__device__ inline void wg_lgkm_wait(v4i16 (&f)[4]) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+}
+__device__ inline bf16x8 wg_cat(v4i16 lo, v4i16 hi) {
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const v8i16 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+template <typename F, int... U>
+__device__ __attribute__((always_inline)) inline void wg_static_for(F& f, std::integer_sequence<int, U...>) {
+  (f(std::integral_constant<int, U>{}), ...);
 }
 
 template <int DIL>
@@ -317,6 +346,7 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
   constexpr int XW = G::XW, BPIX = G::BPIX, NA = G::NA, NB = G::NB, BUFE = G::BUFE;
   constexpr int BIMGE = BPIX * 4;  // entries per (half, part) image
   __shared__ __attribute__((aligned(16))) u32x4 lds[3 * BUFE];
+  __shared__ int cids[WG_MAXC];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -383,35 +413,80 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
   auto compute = [&](int bb) __attribute__((always_inline)) {
     const u32x4* L = lds + bb * BUFE;
     const floatx4* Arow = reinterpret_cast<const floatx4*>(L) + arow * 8;
-    const __bf16* Bh = reinterpret_cast<const __bf16*>(L + WG_AENT + (cb * 2) * BIMGE) + tr0;
+    const uint32_t bb0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)(
+        reinterpret_cast<const __bf16*>(L + WG_AENT + (cb * 2) * BIMGE) + tr0);
+    const uint32_t ab = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)Arow;
+    floatx4 av[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t addr = ab + 16u * (uint32_t)((4 * (q >> 1) + 2 * kh + (q & 1)) ^ asw);
+      asm volatile("ds_read_b128 %0, %1" : "=v"(av[q]) : "v"(addr));
+    }
+    bf16x8 ahi[2], alo[2];
+    v4i16 fr[3][4];
+    auto read = [&](auto u_, int set) __attribute__((always_inline)) {
+      constexpr int u = decltype(u_)::value, s = u / 9, t = u % 9;
+      constexpr int off = ((t / 3) * XW + 16 * s + (t % 3) * DIL) * 32 * 2;  // bytes
+      constexpr int lo = BIMGE * 8 * 2;
+      fr[set][0] = wg_tr<off>(bb0);
+      fr[set][1] = wg_tr<off + 256>(bb0);
+      fr[set][2] = wg_tr<off + lo>(bb0);
+      fr[set][3] = wg_tr<off + lo + 256>(bb0);
+    };
+    read(std::integral_constant<int, 0>{}, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(av[0]), "+v"(av[1]), "+v"(av[2]), "+v"(av[3]), "+v"(fr[0][0]),
+                 "+v"(fr[0][1]), "+v"(fr[0][2]), "+v"(fr[0][3]));
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int q0 = 4 * s + 2 * kh;
-      const floatx4 v0 = Arow[q0 ^ asw], v1 = Arow[(q0 + 1) ^ asw];
+      const floatx4 v0 = av[2 * s], v1 = av[2 * s + 1];
       u32x2 h0, l0, h1, l1;
       split4(v0, h0, l0);
       split4(v1, h1, l1);
       const u32x4 hh = {h0[0], h0[1], h1[0], h1[1]}, ll = {l0[0], l0[1], l1[0], l1[1]};
-      const bf16x8 ahi = __builtin_bit_cast(bf16x8, hh), alo = __builtin_bit_cast(bf16x8, ll);
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int off = ((t / 3) * XW + 16 * s + (t % 3) * DIL) * 32;
-        const bf16x8 bhi = tr_read8(Bh + off);
-        const bf16x8 blo = tr_read8(Bh + BIMGE * 8 + off);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo, bhi, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, blo, acc[t], 0, 0, 0);
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi, bhi, acc[t], 0, 0, 0);
-      }
+      ahi[s] = __builtin_bit_cast(bf16x8, hh);
+      alo[s] = __builtin_bit_cast(bf16x8, ll);
     }
+    // (s, tap) steps 0..17: the next step's 4 transposed reads go out before this step's MFMAs
+#if MVBEV_WGRAD_PF2
+    // two steps ahead: step u+2's reads go out under step u's MFMAs; lgkmcnt(4) then retires
+    // step u+1's (in-order LDS returns; no scalar loads are in flight inside compute)
+    read(std::integral_constant<int, 1>{}, 1);
+    auto step = [&](auto u_) __attribute__((always_inline)) {
+      constexpr int u = decltype(u_)::value, s = u / 9, t = u % 9, st = u % 3;
+      if constexpr (u + 2 < 18) read(std::integral_constant<int, u + 2>{}, (u + 2) % 3);
+      const bf16x8 bhi = wg_cat(fr[st][0], fr[st][1]), blo = wg_cat(fr[st][2], fr[st][3]);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[s], bhi, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[s], blo, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[s], bhi, acc[t], 0, 0, 0);
+      if constexpr (u + 2 < 18) {
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(fr[(u + 1) % 3][0]), "+v"(fr[(u + 1) % 3][1]),
+                     "+v"(fr[(u + 1) % 3][2]), "+v"(fr[(u + 1) % 3][3]));
+      } else if constexpr (u + 1 < 18) {
+        wg_lgkm_wait(fr[(u + 1) % 3]);
+      }
+    };
+#else
+    auto step = [&](auto u_) __attribute__((always_inline)) {
+      constexpr int u = decltype(u_)::value, s = u / 9, t = u % 9, st = u & 1;
+      if constexpr (u + 1 < 18) read(std::integral_constant<int, u + 1>{}, st ^ 1);
+      const bf16x8 bhi = wg_cat(fr[st][0], fr[st][1]), blo = wg_cat(fr[st][2], fr[st][3]);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[s], bhi, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[s], blo, acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[s], bhi, acc[t], 0, 0, 0);
+      if constexpr (u + 1 < 18) wg_lgkm_wait(fr[st ^ 1]);
+    };
+#endif
+    wg_static_for(step, std::make_integer_sequence<int, 18>{});
   };
 
-  // chunk ids: a list entry is loaded one issue ahead, before the DMAs it must not wait for
-  auto cid = [&](int ci) __attribute__((always_inline)) { return list ? list[ci] : ci; };
+  // the partition's chunk ids, staged in LDS before any DMA (a global load of the list inside
+  // the loop would be waited for with vmcnt(0), draining the DMAs in flight)
   const int n = c1 - c0;
+  for (int j = tid; j < n; j += NTH) cids[j] = list ? list[c0 + j] : c0 + j;
+  __syncthreads();
   if (n > 0) {
-    issue(cid(c0), 0);
-    if (n > 1) issue(cid(c0 + 1), 1);
-    int cnext = n > 2 ? cid(c0 + 2) : 0;
+    issue(cids[0], 0);
+    if (n > 1) issue(cids[1], 1);
     for (int i = 0; i < n; ++i) {
       // retire chunk i's DMA (chunk i+1's may stay in flight); LDS reads of chunk i-1 done
       if (i + 1 < n) {
@@ -421,11 +496,7 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
       }
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (i + 2 < n) {
-        const int nx = i + 3 < n ? cid(c0 + i + 3) : 0;
-        issue(cnext, (i + 2) % 3);
-        cnext = nx;
-      }
+      if (i + 2 < n) issue(cids[i + 2], (i + 2) % 3);
       compute(i % 3);
     }
   }
@@ -1020,7 +1091,8 @@ int mvbev_conv3x3_wgrad_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)(g.P * g.tiles)), block(NTH);
   const bool split = x_layout == MVBEV_LAYOUT_SPLIT_BF16;
-  if (MVBEV_WGRAD_DMA && split && a.vec_dy && (dilation == 1 || dilation == 2)) {
+  if (MVBEV_WGRAD_DMA && split && a.vec_dy && (dilation == 1 || dilation == 2) &&
+      g.nchunks / g.P + 1 <= WG_MAXC) {
     if (dilation == 1) hipLaunchKernelGGL((wgrad_dma_kernel<1>), grid, dim3(NTH), 0, s, a);
     else hipLaunchKernelGGL((wgrad_dma_kernel<2>), grid, dim3(NTH), 0, s, a);
   } else if (dilation == 1) {

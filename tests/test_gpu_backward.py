@@ -120,8 +120,10 @@ def test_warp_backward_no_gradient_from_outside_samples():
 
 # ---------------------------------------------------------------------------------- conv grads
 
+# W % 4 == 0 with split input takes wgrad_dma_kernel (LDS-DMA staging): (12, 36, d1) and
+# (13, 44, d2: a partial 64-channel tile and a partial last row segment); the others wgrad_kernel
 @pytest.mark.parametrize("B,K,H,W,dil", [(1, 64, 12, 36, 1), (2, 136, 17, 37, 2), (1, 512, 30, 90, 2),
-                                         (1, 24, 5, 70, 1)])
+                                         (1, 24, 5, 70, 1), (2, 72, 13, 44, 2)])
 @pytest.mark.parametrize("split", [False, True])
 def test_conv_wgrad_vs_torch(B, K, H, W, dil, split):
     from mvdet_amd import ops

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -366,9 +366,22 @@ int mvbev_threshold_points(const float* map, int64_t H, int64_t W, float thres, 
  * (equal scores: larger index first), the top_k largest considered; keep the best, drop every
  * later candidate whose distance sqrt(dx^2+dy^2) (fp32, correctly rounded) is not > dist_thres,
  * repeat.  points [K][2] fp32, scores [K] fp32 (device); keep [K] int64 = kept indices then
- * zeros; *count (device int32) = number kept.  K <= 8192 (one workgroup, LDS sort). */
+ * zeros; *count (device int32) = number kept.  K <= 8192 (one workgroup, LDS sort); larger K
+ * returns MVBEV_ERR_SHAPE here and runs through mvbev_point_nms_ws. */
 int mvbev_point_nms(const float* points, const float* scores, int64_t K, float dist_thres,
                     int64_t top_k, int64_t* keep, int32_t* count, void* stream);
+
+/* Device workspace bytes mvbev_point_nms_ws needs for K candidates (0 when K <= 8192). */
+size_t mvbev_point_nms_workspace_bytes(int64_t K, int64_t top_k);
+
+/* mvbev_point_nms for any K (the reference nms.py accepts any; trainer.py:154 passes every map
+ * cell over cls_thres, up to Ho*Wo): K <= 8192 is mvbev_point_nms; above, the same order and
+ * greedy loop over `workspace` (>= mvbev_point_nms_workspace_bytes, 4-B aligned): a bitonic sort
+ * (LDS chunks + global merge passes), then per kept point an ordered compaction of the
+ * candidates strictly farther than dist_thres (nms.py:40).  Enqueued, no host sync. */
+int mvbev_point_nms_ws(const float* points, const float* scores, int64_t K, float dist_thres,
+                       int64_t top_k, int64_t* keep, int32_t* count, void* workspace, size_t ws_bytes,
+                       void* stream);
 
 #ifdef __cplusplus
 }

@@ -35,6 +35,8 @@ EXPORTS = (
     "mvbev_warp_tile_mask",
     "mvbev_threshold_points",
     "mvbev_point_nms",
+    "mvbev_point_nms_workspace_bytes",
+    "mvbev_point_nms_ws",
     "mvbev_warp_views_backward_f32",
     "mvbev_pack_conv3x3_dgrad_bf16x3",
     "mvbev_conv3x3_wgrad_workspace_bytes",
@@ -135,6 +137,10 @@ def _declare(lib):
     lib.mvbev_threshold_points.argtypes = [_p, _i64, _i64, ctypes.c_float, _p, _p, _p, _i64, _p]
     lib.mvbev_point_nms.restype = ctypes.c_int
     lib.mvbev_point_nms.argtypes = [_p, _p, _i64, ctypes.c_float, _i64, _p, _p, _p]
+    lib.mvbev_point_nms_workspace_bytes.restype = ctypes.c_size_t
+    lib.mvbev_point_nms_workspace_bytes.argtypes = [_i64, _i64]
+    lib.mvbev_point_nms_ws.restype = ctypes.c_int
+    lib.mvbev_point_nms_ws.argtypes = [_p, _p, _i64, ctypes.c_float, _i64, _p, _p, _p, ctypes.c_size_t, _p]
     lib.mvbev_warp_views_backward_f32.restype = ctypes.c_int
     lib.mvbev_warp_views_backward_f32.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64,
                                                   _i64, _i64, _p]

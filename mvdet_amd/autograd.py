@@ -132,9 +132,14 @@ class ProjectFuseFunction(torch.autograd.Function):
         return out
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, dmap):
         engine: ProjectFuse = ctx.engine
         ws: Workspace = ctx.ws
+        if ws is None:
+            raise RuntimeError("ProjectFuseFunction: trying to backward through this graph a second time; its saved "
+                               "activations (slab, y1, y2) are released after the first backward (the native "
+                               "kernels keep no retain_graph copy). Run the forward again.")
         w1, b1, w2, b2, w3 = ctx.saved_tensors
         n = engine.num_cam
         need = ctx.needs_input_grad[1:]

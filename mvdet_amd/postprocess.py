@@ -2,7 +2,7 @@
 
 Drop-ins for the CPU loop of ``multiview_detector/trainer.py:97-106,148-157`` and for
 ``multiview_detector/utils/nms.py:7-43`` (same names, arguments and return values), on the
-HIP kernels of ``libmvbev.so`` (``mvbev_threshold_points``, ``mvbev_point_nms``):
+HIP kernels of ``libmvbev.so`` (``mvbev_threshold_points``, ``mvbev_point_nms_ws``):
 
 * ``nms(points, scores, dist_thres=50/2.5, top_k=50) -> (keep, count)``: greedy point NMS.
   Returns ``keep`` alone for empty input, like the reference.  Equal scores are taken larger
@@ -38,9 +38,14 @@ def nms(points: torch.Tensor, scores: torch.Tensor, dist_thres=50 / 2.5, top_k=5
     k = K if (isinstance(top_k, float) and math.isinf(top_k)) else min(int(top_k), K)
     out = torch.empty(K, dtype=torch.int64, device=sc.device)
     cnt = torch.empty(1, dtype=torch.int32, device=sc.device)
-    st = _native.load().mvbev_point_nms(pts.data_ptr(), sc.data_ptr(), K, float(dist_thres), max(k, 1),
-                                        out.data_ptr(), cnt.data_ptr(), _stream(sc))
-    _native.check(st, "mvbev_point_nms")
+    lib = _native.load()
+    # any K (nms.py accepts any; trainer.py:154 hands it every map cell over cls_thres):
+    # above the one-workgroup LDS sort the kernel needs a device workspace
+    nws = int(lib.mvbev_point_nms_workspace_bytes(K, max(k, 1)))
+    ws = torch.empty(max(nws, 4), dtype=torch.uint8, device=sc.device)
+    st = lib.mvbev_point_nms_ws(pts.data_ptr(), sc.data_ptr(), K, float(dist_thres), max(k, 1),
+                                out.data_ptr(), cnt.data_ptr(), ws.data_ptr(), nws, _stream(sc))
+    _native.check(st, "mvbev_point_nms_ws")
     return out.to(keep.device), int(cnt.item())
 
 

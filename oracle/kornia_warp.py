@@ -14,6 +14,16 @@ bilinear corner/bounds logic of ``GridSamplerKernel.cpp``).
 ``closed_form_warp_f64`` is the independent float64 pin: bilinear sampling of
 ``src`` at ``M^-1 [u, v, 1]`` (perspective divide, zero padding, integer pixel
 centres) — what the fp32 chain approximates.
+
+PARITY STATUS — kornia parity unpinned: kornia itself is not importable here and
+no reference fixture holds a kornia output, so the golden vectors
+(``tools/gen_golden.py``) run the reference's own ``PerspTransDetector`` with kornia
+stubbed by THIS restatement.  Every warp / fused-upsample / adjoint parity test
+therefore checks against the restatement, not against kornia's own output.  An
+error in the restatement is caught only by the float64 closed form above, which
+the required tests ``tests/test_oracle.py::test_restatement_vs_closed_form`` (CPU)
+and ``tests/test_gpu_parity.py::test_warp_vs_oracle_and_closed_form`` (HIP warp vs
+both) check on every run.
 """
 from __future__ import annotations
 

@@ -417,3 +417,27 @@ def test_detector_training_step_matches_cpu_autograd():
     for k, p in model.named_parameters():
         if k in pr:
             assert_parity(p.grad.cpu(), pr[k].grad, f"d {k}")
+
+
+def test_project_fuse_second_backward_raises():
+    """The native backward frees its saved activations: a second backward through the same
+    graph (retain_graph=True) raises a clear RuntimeError, and double backward is refused
+    (once_differentiable) instead of silently building no second-order graph."""
+    from mvdet_amd.autograd import project_fuse
+    from mvdet_amd.pipeline import ProjectFuse
+    rng = np.random.default_rng(11)
+    N, B, C, (H, W), (ho, wo) = 2, 1, 8, (27, 48), (12, 36)
+    Ms = [_rand_h(rng, H, W, ho, wo) for _ in range(N)]
+    eng = ProjectFuse([torch.from_numpy(M) for M in Ms], (H, W), (ho, wo), C)
+    mc = torch.nn.Sequential(torch.nn.Conv2d(N * C + 2, 512, 3, padding=1), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False)).to(DEV)
+    fg = [torch.rand((B, C, H, W), device=DEV).requires_grad_() for _ in range(N)]
+    out = project_fuse(eng, fg, mc)
+    out.sum().backward(retain_graph=True)
+    with pytest.raises(RuntimeError, match="a second time"):
+        out.sum().backward()
+    out2 = project_fuse(eng, fg, mc)
+    (g,) = torch.autograd.grad(out2.sum(), fg[0], create_graph=True)
+    with pytest.raises(RuntimeError):
+        g.sum().backward()

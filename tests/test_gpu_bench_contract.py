@@ -31,6 +31,8 @@ def test_bench_json_line_contract():
     rl = r["roofline"]
     assert rl["bound"] in ("hbm", "mfma") and rl["unit"] in ("GB/s", "TFLOP/s")
     assert rl["frac"] == pytest.approx(rl["achieved"] / rl["peak"], rel=1e-3)
+    assert 0 < rl["frac"] <= 1.0  # executed MFMA work (frustum-skipped products not counted)
+    assert rl["dense_algorithmic_frac"] >= rl["frac"]
     cb = r["cpu_baseline"]
     assert cb["value"] > 0 and cb["kind"] in ("port", "reference") and cb["cores"] >= 1
     assert cb["single_thread"]["cores"] == 1 and cb["single_thread"]["value"] > 0

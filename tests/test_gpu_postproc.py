@@ -28,6 +28,49 @@ def test_nms_tie_free_matches_oracle_exactly():
         np.testing.assert_array_equal(keep.cpu().numpy(), ref_keep.numpy())
 
 
+@pytest.mark.parametrize("K,dist,top_k", [(8193, 20.0, np.inf), (20000, 20.0, 50), (43200, 20.0, np.inf),
+                                          (43200, 4.0, 30000), (70000, 8.0, np.inf)])
+def test_nms_large_k_matches_oracle_exactly(K, dist, top_k):
+    """Past the one-workgroup LDS path (K > 8192): the workspace path (global bitonic sort +
+    per-kept-point ordered compaction) keeps the same points in the same order as the
+    reference loop.  K = 43,200 is every cell of a cfg2 map over cls_thres (trainer.py:154)."""
+    from mvdet_amd import postprocess
+    rng = np.random.default_rng(K)
+    if K == 43200:  # a 120 x 360 map's cells in grid coordinates x grid_reduce (trainer.py:103)
+        ii, jj = np.meshgrid(np.arange(120), np.arange(360), indexing="ij")
+        pts = (np.stack([ii.ravel(), jj.ravel()], 1) * 4).astype(np.float32)
+    else:
+        pts = (rng.integers(0, 400, size=(K, 2)) * 4).astype(np.float32)
+    sc = rng.permutation(K).astype(np.float32) / K + 0.4  # distinct scores (tie-free)
+    ref_keep, ref_count = postproc.nms(torch.from_numpy(pts), torch.from_numpy(sc), dist, top_k)
+    keep, count = postprocess.nms(torch.from_numpy(pts).cuda(), torch.from_numpy(sc).cuda(), dist, top_k)
+    assert count == ref_count, (K, count, ref_count)
+    np.testing.assert_array_equal(keep.cpu().numpy(), ref_keep.numpy())
+
+
+def test_nms_large_k_ties_order():
+    """Exactly tied scores past 8192: the kernel's (score desc, index desc) order, checked by the
+    same greedy loop on that order (torch's CPU sort leaves tied order unspecified)."""
+    from mvdet_amd import postprocess
+    rng = np.random.default_rng(5)
+    K, dist = 12000, 12.0
+    pts = (rng.integers(0, 300, size=(K, 2)) * 2).astype(np.float32)
+    sc = (rng.integers(0, 50, size=K) / 50.0).astype(np.float32)
+    keep, count = postprocess.nms(torch.from_numpy(pts).cuda(), torch.from_numpy(sc).cuda(), dist, np.inf)
+    order = sorted(range(K), key=lambda k: (-float(sc[k]), -k))
+    p = torch.from_numpy(pts)[order]
+    idx = torch.tensor(order)
+    ref = []
+    while idx.numel():
+        c = idx[0]
+        ref.append(int(c))
+        d = torch.norm(p[0] - p[1:], dim=1)
+        keep_m = d > dist
+        idx, p = idx[1:][keep_m], p[1:][keep_m]
+    assert count == len(ref)
+    np.testing.assert_array_equal(keep.cpu().numpy()[:count], ref)
+
+
 def test_nms_reference_golden_with_ties():
     """The reference's own cases (tests/golden/nms_cases.npz) contain exactly tied scores, whose
     order torch's CPU sort leaves unspecified, so the kept set may legitimately differ.  Checked:

@@ -574,12 +574,19 @@ constexpr int RNW = 8;                          // waves
 constexpr int RNT = 64 * RNW;
 constexpr int RUNIT = 2 * 3 * 2 * BN;           // 16-B pieces of one W unit (hi + lo): 1536
 constexpr int RHALF = RUNIT / 2;                // one part (hi or lo) of a unit
-constexpr int RNWI = RUNIT / RNT;               // LDS-DMA instructions per wave per W unit (3)
-static_assert(RUNIT % RNT == 0, "W unit must split evenly over the waves");
+#ifndef MVBEV_RING_DMAW
+#define MVBEV_RING_DMAW 4  // waves that issue the LDS-DMAs: 4 = one wave per SIMD issues them while its partner
+                           // only computes (conv1 -3 %, conv2 -2 % vs all 8 waves issuing)
+#endif
+constexpr int RNIW = MVBEV_RING_DMAW;           // issuing waves
+constexpr int RNIT = 64 * RNIW;                 // issuing lanes
+constexpr int RNWI = RUNIT / RNIT;              // LDS-DMA instructions per issuing wave per W unit (3)
+static_assert(RNIW == 4 || RNIW == 8, "issuing waves");
+static_assert(RUNIT % RNIT == 0, "W unit must split evenly over the waves");
 template <int DIL> struct RingGeo {
   static constexpr int XH = RT + 2 * DIL, XW = TW + 2 * DIL, XPIX = XH * XW;
-  static constexpr int NX = (4 * XPIX + RNT - 1) / RNT;  // LDS-DMA instructions per wave per halo
-  static constexpr int XBUF = NX * RNT;                  // entries per halo buffer (incl. tail)
+  static constexpr int NX = (4 * XPIX + RNIT - 1) / RNIT;  // LDS-DMA instructions per issuing wave per halo
+  static constexpr int XBUF = NX * RNIT;                   // entries per halo buffer (incl. tail)
   static constexpr int LDS = 3 * RUNIT + 2 * XBUF;       // 16-B entries
   static_assert(LDS * 16 <= 160 * 1024, "LDS");
 };
@@ -592,13 +599,25 @@ __device__ inline int ring_base_row(int rg) {
   return DIL == 1 ? 3 * rg : (rg >> 1) * 6 + (rg & 1);
 }
 
+template <int AUX = 0>
 __device__ inline void glds16(const u32x4* src, u32x4* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, AUX);
 }
+#ifndef MVBEV_RING_XAUX
+#define MVBEV_RING_XAUX 0  // cache policy of the halo DMAs (2 = nt: streamed slab, keep the weights in L2)
+#endif
 
 #ifndef MVBEV_RING_PRIO
 #define MVBEV_RING_PRIO 0  // raise the wave priority over each unit's MFMA stream
+#endif
+#ifndef MVBEV_RING_DMAIL
+#define MVBEV_RING_DMAIL 0  // place each unit's DMAs one per MFMA after its barrier
+#endif
+#ifndef MVBEV_RING_ABL
+#define MVBEV_RING_ABL 0  // timing ablations only (wrong results): bit 0 no unit barrier, bit 1 no DMA,
+                          // bit 2 no vmcnt wait, bit 3 no weight DMA, bit 4 no halo DMA,
+                          // bit 5 contiguous halo sources, bit 6 one halo source address
 #endif
 #ifndef MVBEV_RING_STAGGER
 #define MVBEV_RING_STAGGER 0  // waves 4-7 take each unit's barrier one tap earlier (parity-green; measured
@@ -647,50 +666,84 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
   };
 
   // LDS-DMA sources, chunk-invariant parts.  Halo entry e = (sub, part, pixel) of the image
-  // [sub][part][XH][XW]; lane j-th instruction covers entries (j * RNW + wave) * 64 + lane.
+  // [sub][part][XH][XW]; lane j-th instruction covers entries (j * RNIW + wave) * 64 + lane.
   int xo[NX];  // piece offset in the sub-block's plane (2 * pixel + part); -1 = zero entry
 #pragma unroll
   for (int j = 0; j < NX; ++j) {
-    const int e = (j * RNW + wave) * 64 + lane;
+    const int e = (j * RNIW + wave) * 64 + lane;
     const int part = (e / XPIX) & 1, pix = e % XPIX;
     const int r = pix / XW, c = pix % XW;
     const int gy = y0 - DIL + r, gx = x0 - DIL + c, by = gy - a.in_row0;
     const bool ok = e < 4 * XPIX && gy >= 0 && gy < a.H && by >= 0 && by < a.in_rows && gx >= 0 && gx < W;
     xo[j] = ok ? 2 * (by * W + gx) + part : -1;
+    if (MVBEV_RING_ABL & 32) xo[j] = ok ? 2 * (max(y0 - DIL - a.in_row0, 0) * W + x0) + e % (2 * XPIX) : -1;
+    if (MVBEV_RING_ABL & 64) xo[j] = ok ? 0 : -1;
   }
   // W unit image [part][kh][sub][co]; packed source [part][tap = 3 kh + kw][sub][co].  The
   // DMA source offsets (and the halo entries' sub-block) are recomputed per issue: a few VALU
   // ops instead of registers held across the MFMA loop.
   auto wo = [&](int j) __attribute__((always_inline)) -> int {
-    const int e = (j * RNW + wave) * 64 + lane;
+    const int e = (j * RNIW + wave) * 64 + lane;
     const int part = e / RHALF, r = e % RHALF;
     return part * (NKB * 2 * BN) + (r / (2 * BN)) * 3 * (2 * BN) + r % (2 * BN);
   };
   const int U = 3 * nch;
+  // W unit (physical chunk ch, kernel column kw) -> slot
+  auto issue_w_ch = [&](int ch, int kw, int slot) __attribute__((always_inline)) {
+    const u32x4* src = wsrc + (int64_t)ch * wchunk + kw * 2 * BN;
+    u32x4* dst = lds + slot * RUNIT + wave * 64;
+    if (RNIW == RNW || wave < RNIW)
+#pragma unroll
+      for (int j = 0; j < RNWI; ++j) glds16(src + wo(j), dst + j * RNIT);
+  };
   auto issue_w = [&](int u) __attribute__((always_inline)) {  // W unit u -> slot u % 3
     const int uu = min(u, U - 1);
-    const int ci = uu / 3, kw = uu - 3 * ci;
-    const u32x4* src = wsrc + (int64_t)chunk_of(ci) * wchunk + kw * 2 * BN;
-    u32x4* dst = lds + (u % 3) * RUNIT + wave * 64;
-#pragma unroll
-    for (int j = 0; j < RNWI; ++j) glds16(src + wo(j), dst + j * RNT);
+    const int ci = uu / 3;
+    issue_w_ch(chunk_of(ci), uu - 3 * ci, u % 3);
   };
-  auto issue_x = [&](int i) __attribute__((always_inline)) {  // halo of chunk i -> buffer i & 1
-    const int ch = chunk_of(min(i, nch - 1));
+  // halo of physical chunk ch -> buffer xb
+  auto issue_x_ch = [&](int ch, int xb) __attribute__((always_inline)) {
+    // sub-block sources computed unconditionally (clamped channel) and selected per lane, so
+    // the issue is straight-line code the scheduler can spread between MFMAs
     const u32x4* xs[2];
+    bool kv[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int k0 = ch * KC + s * SB;
-      const int g = k0 / a.group;
-      const int64_t cb = (int64_t)b * a.batch_stride + g * a.group_stride + (int64_t)(k0 - g * a.group) * plane;
-      xs[s] = k0 < a.K ? static_cast<const u32x4*>(a.x) + cb / 4 : nullptr;
+      kv[s] = k0 < a.K;
+      const int kc = kv[s] ? k0 : 0;
+      const int g = kc / a.group;
+      const int64_t cb = (int64_t)b * a.batch_stride + g * a.group_stride + (int64_t)(kc - g * a.group) * plane;
+      xs[s] = static_cast<const u32x4*>(a.x) + cb / 4;
     }
-    u32x4* dst = Xlds + (i & 1) * XBUF + wave * 64;
+    u32x4* dst = Xlds + xb * XBUF + wave * 64;
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
-      const u32x4* base = (j * RNW + wave) * 64 + lane >= 2 * XPIX ? xs[1] : xs[0];
-      glds16(xo[j] >= 0 && base ? base + xo[j] : g_ring_zero, dst + j * RNT);
+      const bool s1 = (j * RNIW + wave) * 64 + lane >= 2 * XPIX;
+      const bool z = xo[j] < 0 || !(s1 ? kv[1] : kv[0]);
+      if (RNIW == RNW || wave < RNIW) glds16<MVBEV_RING_XAUX>(z ? g_ring_zero : (s1 ? xs[1] : xs[0]) + xo[j], dst + j * RNIT);
     }
+  };
+  auto issue_x = [&](int i) __attribute__((always_inline)) {  // halo of chunk i -> buffer i & 1
+    issue_x_ch(chunk_of(min(i, nch - 1)), i & 1);
+  };
+  // Physical id of the chunk after the current one: every DMA issued while chunk ci is
+  // computed fetches chunk ci + 1 (W(u + 3) and the next halo).  Advanced branch-free (scalar
+  // selects) once per chunk, so the unit body stays one basic block for the scheduler; past
+  // the last chunk it stays at the last one (dummy loads that keep the vmcnt counts exact).
+  int nx_i = 1, nx_sub = a.gmask ? 1 % a.cpg : 0;
+  int nx_ph = chunk_of(min(1, nch - 1));
+  uint32_t nx_m = gm;
+  if (a.gmask && a.cpg == 1) nx_m &= nx_m - 1;
+  auto advance = [&]() __attribute__((always_inline)) {
+    const bool more = nx_i + 1 < nch;
+    const bool wrap = a.gmask && nx_sub + 1 == a.cpg;
+    const uint32_t m2 = wrap ? (nx_m & (nx_m - 1)) : nx_m;
+    const int ph2 = wrap ? (int)__builtin_ctz(m2 | 0x80000000u) * a.cpg : nx_ph + 1;
+    nx_m = more ? m2 : nx_m;
+    nx_ph = more ? ph2 : nx_ph;
+    nx_sub = more ? (wrap ? 0 : nx_sub + 1) : nx_sub;
+    nx_i += 1;
   };
 
   const int rg = wave & 3;
@@ -738,6 +791,18 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 18 - n, 0);
   };
+  // after a unit's barrier: one DMA (the first nv) and one fragment read after each of the
+  // first 14 MFMAs, so the SIMD's MFMA pipe is fed while the DMAs issue
+  auto interleave_dma = [&](auto nvmem) __attribute__((always_inline)) {
+    constexpr int nv = decltype(nvmem)::value;
+#pragma unroll
+    for (int i = 0; i < 14; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if (i < nv) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+  };
 
   if (nch > 0) {
     // prologue: W(0), halo(0), W(1), W(2) in flight; wait for the first two
@@ -766,15 +831,20 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     mfmas(P ^ 1, P, 1);                                                                        \
     interleave(std::integral_constant<int, 4>{});                                              \
     /* retire W(u+1) (+ the next chunk's halo at kw 2); LDS reads of this unit's slot done */ \
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(KW == 1 ? RNWI + NX : RNWI) : "memory"); \
-    __builtin_amdgcn_s_barrier();                                                              \
+    if (MVBEV_RING_ABL & 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                  \
+    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(KW == 1 ? RNWI + NX : RNWI) : "memory"); \
+    if (!(MVBEV_RING_ABL & 1)) __builtin_amdgcn_s_barrier();                                   \
     asm volatile("" ::: "memory");                                                             \
-    issue_w(u_ + 3);                                                                           \
-    if (KW == 0) issue_x(u_ / 3 + 1);                                                          \
+    if (!(MVBEV_RING_ABL & 2)) {                                                               \
+      if (!(MVBEV_RING_ABL & 8)) issue_w_ch(nx_ph, KW, SLOT);                                  \
+      if (KW == 0 && !(MVBEV_RING_ABL & 16)) issue_x_ch(nx_ph, ((R) / 3 + 1) & 1);             \
+    }                                                                                          \
+    if (KW == 2) advance();                                                                    \
     fetch_b(P ^ 1, NXB, NKW);                                                                  \
     fetch_a(P ^ 1, NSLOT, 0);                                                                  \
     mfmas(P, P, 2);                                                                            \
-    interleave(std::integral_constant<int, 14>{});                                             \
+    if constexpr (MVBEV_RING_DMAIL != 0) interleave_dma(std::integral_constant<int, KW == 0 ? RNWI + NX : RNWI>{}); \
+    else interleave(std::integral_constant<int, 14>{});                                        \
     if (MVBEV_RING_PRIO) __builtin_amdgcn_s_setprio(0);                                        \
   } while (0)
     // Staggered waves 4-7 (MI355X_MICROARCH.md "Two waves per SIMD", item 9): one unit body

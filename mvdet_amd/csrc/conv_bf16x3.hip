@@ -617,7 +617,8 @@ __device__ inline void glds16(const u32x4* src, u32x4* lds_wave_base) {
 #ifndef MVBEV_RING_ABL
 #define MVBEV_RING_ABL 0  // timing ablations only (wrong results): bit 0 no unit barrier, bit 1 no DMA,
                           // bit 2 no vmcnt wait, bit 3 no weight DMA, bit 4 no halo DMA,
-                          // bit 5 contiguous halo sources, bit 6 one halo source address
+                          // bit 5 contiguous halo sources, bit 6 one halo source address,
+                          // bits 8 / 9: halo / weights alternate between the first two chunks (L2-resident)
 #endif
 #ifndef MVBEV_RING_STAGGER
 #define MVBEV_RING_STAGGER 0  // waves 4-7 take each unit's barrier one tap earlier (parity-green; measured
@@ -836,8 +837,8 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     if (!(MVBEV_RING_ABL & 1)) __builtin_amdgcn_s_barrier();                                   \
     asm volatile("" ::: "memory");                                                             \
     if (!(MVBEV_RING_ABL & 2)) {                                                               \
-      if (!(MVBEV_RING_ABL & 8)) issue_w_ch(nx_ph, KW, SLOT);                                  \
-      if (KW == 0 && !(MVBEV_RING_ABL & 16)) issue_x_ch(nx_ph, ((R) / 3 + 1) & 1);             \
+      if (!(MVBEV_RING_ABL & 8)) issue_w_ch((MVBEV_RING_ABL & 512) ? chunk_of(nx_i & 1) : nx_ph, KW, SLOT);                                  \
+      if (KW == 0 && !(MVBEV_RING_ABL & 16)) issue_x_ch((MVBEV_RING_ABL & 256) ? chunk_of(nx_i & 1) : nx_ph, ((R) / 3 + 1) & 1);             \
     }                                                                                          \
     if (KW == 2) advance();                                                                    \
     fetch_b(P ^ 1, NXB, NKW);                                                                  \

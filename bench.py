@@ -94,6 +94,21 @@ DTYPE_LABEL = {"fp32": "f32 (fp32-input MFMA, exact fp32 products, fp32 accumula
 BF16_MFMA_PEAK_TFS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16
 
 
+def mfma_probe(settle_s: float = 1.5):
+    """Sustained bf16 MFMA TFLOP/s of this device now (tools/mfma_shape_bench.hip built as
+    mvdet_amd/lib/libmfmaprobe.so by __graft_entry__.build()); None when not built."""
+    import ctypes
+    lib_path = ROOT / "mvdet_amd" / "lib" / "libmfmaprobe.so"
+    if not lib_path.exists():
+        return None
+    lib = ctypes.CDLL(str(lib_path))
+    lib.mfma_probe_tflops.restype = ctypes.c_double
+    lib.mfma_probe_tflops.argtypes = [ctypes.c_int, ctypes.c_double]
+    torch.cuda.synchronize()
+    v = lib.mfma_probe_tflops(0, settle_s)
+    return v if v > 0 else None
+
+
 def run_single(args, precision, steps, warmup, with_cpu):
     from mvdet_amd import ProjectFuse, synthetic
     from mvdet_amd.geometry import projection_matrices, touched_footprint
@@ -176,6 +191,7 @@ def run_single(args, precision, steps, warmup, with_cpu):
     else:
         achieved, peak = conv1_alg_tfs, FP32_MFMA_PEAK_TFS
         kname = "conv3x3_mfma_f32 (conv1)"
+    sustained = mfma_probe() if precision == "bf16x3" and not args.no_probe else None
     traffic, warp_traffic = None, None
     tfile = ROOT / "profiles" / f"traffic_cfg{args.config}_{precision}.json"
     if tfile.exists():
@@ -199,7 +215,13 @@ def run_single(args, precision, steps, warmup, with_cpu):
                      "frustum_active_fraction": round(active, 4),
                      "dense_algorithmic_achieved": round(achieved, 2),
                      "dense_algorithmic_frac": round(achieved / peak, 4),
-                     "dense_fp32_equiv_tflops": round(conv1_alg_tfs, 2)},
+                     "dense_fp32_equiv_tflops": round(conv1_alg_tfs, 2),
+                     # the rate this device holds right after the timed steps on a bare
+                     # 32x32x16 bf16 MFMA loop over random operands (the chip lowers its clock
+                     # under MFMA load: MI355X_MICROARCH.md "DVFS give-back"), and conv1's
+                     # executed rate as a fraction of it
+                     "sustained_peak": round(sustained, 1) if sustained else None,
+                     "frac_of_sustained": round(achieved * active / sustained, 4) if sustained else None},
         "stages_ms": {"warp_all_views": round(t_warp, 4), "conv1": round(t_c1, 4), "conv2": round(t_c2, 4),
                       "conv3": round(t_c3, 4)},
         # SURVEY §8(d) "achieved fraction": the stages' roofline floors over the measured step;
@@ -386,6 +408,7 @@ def main():
                     help="conv1/conv2 arithmetic: 3xbf16 split (default) or fp32-input MFMA")
     ap.add_argument("--config", type=int, default=2, help="BASELINE.json config index (1-based)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-probe", action="store_true", help="skip the sustained-MFMA-rate probe (roofline.sustained_peak)")
     ap.add_argument("--no-alt", action="store_true", help="skip the other-precision comparison line")
     ap.add_argument("--cpu-frames", type=int, default=0, help="frames for the CPU baseline (0 = auto)")
     ap.add_argument("--no-train", action="store_true", help="skip the training-step (forward+backward) line")

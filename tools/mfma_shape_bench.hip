@@ -5,6 +5,8 @@
 //
 //   hipcc -O3 --offload-arch=gfx950 -o tools/mfma_shape_bench tools/mfma_shape_bench.hip
 //   ./tools/mfma_shape_bench
+// or as the library bench.py loads (built by __graft_entry__.build()):
+//   hipcc -O3 --offload-arch=gfx950 -fPIC -shared -DMFMA_PROBE_LIB -o mvdet_amd/lib/libmfmaprobe.so tools/mfma_shape_bench.hip
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -101,6 +103,54 @@ __global__ __launch_bounds__(512, 1) void k16x16x16(const bf16x8* src, float* ou
   out[t] = s;
 }
 
+// Sustained rate of one shape (0: 32x32x16, 1: 16x16x32, 2: 16x16x16) after `settle_s` seconds
+// of back-to-back launches, in TFLOP/s; bench.py loads this as libmfmaprobe.so to report the
+// ceiling the device holds at the time of its run beside the spec peak.
+static bf16x8* g_src = nullptr;
+static float* g_out = nullptr;
+extern "C" double mfma_probe_tflops(int shape, double settle_s) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return -1.0;
+  const int blocks = cus * 4, threads = 512, iters = 256;
+  if (!g_src) {
+    std::vector<uint16_t> h(65536 * 8);
+    srand(1);
+    for (auto& v : h) {
+      const uint16_t mant = rand() & 0x7f, e = 126 + (rand() & 1), sgn = rand() & 1;
+      v = (uint16_t)((sgn << 15) | (e << 7) | mant);
+    }
+    if (hipMalloc(&g_src, h.size() * 2) != hipSuccess ||
+        hipMemcpy(g_src, h.data(), h.size() * 2, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMalloc(&g_out, (size_t)blocks * threads * 4) != hipSuccess)
+      return -1.0;
+  }
+  auto launch = [&]() {
+    if (shape == 0) hipLaunchKernelGGL(k32x32x16, dim3(blocks), dim3(threads), 0, 0, g_src, g_out, iters);
+    if (shape == 1) hipLaunchKernelGGL(k16x16x32, dim3(blocks), dim3(threads), 0, 0, g_src, g_out, iters);
+    if (shape == 2) hipLaunchKernelGGL(k16x16x16, dim3(blocks), dim3(threads), 0, 0, g_src, g_out, iters);
+  };
+  auto t0 = std::chrono::steady_clock::now();
+  while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < settle_s) {
+    for (int i = 0; i < 10; ++i) launch();
+    if (hipDeviceSynchronize() != hipSuccess) return -1.0;
+  }
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return -1.0;
+  (void)hipEventRecord(e0, 0);
+  for (int i = 0; i < 20; ++i) launch();
+  (void)hipEventRecord(e1, 0);
+  (void)hipEventSynchronize(e1);
+  float ms = 0;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  const double flop = 2.0 * 64 * 64 * 32 * iters * (double)blocks * (threads / 64);
+  return flop / (ms / 20 * 1e-3) / 1e12;
+}
+
+#ifndef MFMA_PROBE_LIB
 int main() {
   int dev = 0, cus = 0;
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -146,3 +196,4 @@ int main() {
     }
   return 0;
 }
+#endif

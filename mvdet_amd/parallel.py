@@ -333,8 +333,11 @@ def bench_main(args) -> None:
             stage_ms = {st: round(float(np.mean([ev[st][i].elapsed_time((ev[nxt[st]] if st in nxt else end)[i])
                                                  for i in range(K)])), 4) for st in stages}
             conv1_tfs = 2.0 * B * ho * wo * 9 * N * C * 512 / (stage_ms["conv1"] * 1e-3) / 1e12
+            # the MFMA work conv1 executes (frustum-masked), as the single-GPU line reports it
+            active = (eng.conv1_active_fraction(dev, ws.y1_rows[0], ws.y1_rows[1] - ws.y1_rows[0])
+                      if args.precision == "bf16x3" else 1.0)
             return dict(value=round(world * B * K / dt, 3), ms=round(dt * 1e3 / K, 4), stage_ms=stage_ms,
-                        band=(0, ho), conv1_tfs=conv1_tfs)
+                        band=(0, ho), conv1_tfs=conv1_tfs * active, active=active)
         if mode == "partial":
             vp = ViewPartialSum(lambda sv: ProjectFuse(pm, up, (ho, wo), C, slot_views=sv, precision=args.precision,
                                                        all_views=False), pm, (ho, wo), rank, world)
@@ -381,7 +384,15 @@ def bench_main(args) -> None:
     mode = getattr(args, "mp_mode", "frames")
     res = run(mode)
     others = [m for m in ("frames", "partial", "gather") if m != mode]
-    alts = {} if getattr(args, "no_alt", False) else {m: run(m) for m in others}
+    def run_alt(m):
+        # a failure in a reported-alongside mode (raised on every rank alike, e.g. a collective
+        # the fabric rejects) must not cost the `value` line of the mode measured above
+        try:
+            return run(m)
+        except Exception as e:  # noqa: BLE001
+            return {"error": f"{type(e).__name__}: {e}"[:300]}
+
+    alts = {} if getattr(args, "no_alt", False) else {m: run_alt(m) for m in others}
     bf16 = args.precision == "bf16x3"
     achieved = res["conv1_tfs"] * (3 if bf16 else 1)
     peak = BF16_MFMA_PEAK_TFS if bf16 else FP32_MFMA_PEAK_TFS
@@ -415,10 +426,13 @@ def bench_main(args) -> None:
             "stages_ms_rank0": res["stage_ms"],
             "band_rank0": list(res["band"]),
         }
+        if "active" in res:
+            line["roofline"]["frustum_active_fraction"] = round(res["active"], 4)
         for m, r in alts.items():
             key = "frame_parallel" if m == "frames" else f"view_parallel_{m}"
-            line[key] = {"value": r["value"], "ms_per_step": r["ms"], "scaling": "weak" if m == "frames" else "strong",
-                         "parallelism": hows[m], "stages_ms_rank0": r["stage_ms"]}
+            line[key] = r if "error" in r else {
+                "value": r["value"], "ms_per_step": r["ms"], "scaling": "weak" if m == "frames" else "strong",
+                "parallelism": hows[m], "stages_ms_rank0": r["stage_ms"]}
         print(json.dumps(line), flush=True)
     dist.barrier()
     dist.destroy_process_group()

@@ -105,13 +105,13 @@ def _worker(rank, world, port, out_dir, mode="gather"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mode", [(2, "gather"), (3, "gather"), (2, "partial"), (3, "partial"),
-                                        (4, "partial")])
+@pytest.mark.parametrize("world,mode", [(2, "gather"), (3, "gather"), (4, "gather"), (2, "partial"), (3, "partial"),
+                                        (4, "partial"), (8, "gather"), (8, "partial")])
 def test_view_parallel_matches_single_process_oracle(world, mode, tmp_path):
     """gather: slab all-gather + row bands.  partial: conv1 partial sums over each rank's
     views + reduce-scatter by band + edge-row halo (world 2: 7-row bands use the edge
     all-gather; world 3: 5-row bands fall back to whole bands; world 4: a rank with no view
-    contributes zeros)."""
+    contributes zeros; world 8, the driver's node size: five ranks without views, 7-row bands)."""
     port = _free_port()
     mp.spawn(_worker, args=(world, port, str(tmp_path), mode), nprocs=world, join=True)
     pm, up, grid, C, B, feats, params = _case()

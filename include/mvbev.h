@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -238,6 +238,26 @@ int mvbev_conv3x3_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_desc* 
                             int64_t Cout, int dilation, int relu, void* y, int y_layout,
                             const uint32_t* group_mask, const int32_t* tile_order, void* workspace,
                             size_t workspace_bytes, void* stream);
+
+/* conv2 -> conv3 without conv2's activation in HBM (map_classifier[2:5],
+ * persp_trans_detector.py:53-54, inference): the split-bf16-input conv of
+ * mvbev_conv3x3_bf16x3_ex (desc, w_packed, bias, Cout, dilation, relu as there; no init, no
+ * mask) whose epilogue, instead of storing y, writes per (Cout tile, 64-channel half) set s,
+ * tap t of the following single-output conv and computed pixel the partial
+ *   partials[b][s][t][row - desc->out_row0][col] = sum over the set's channels co of
+ *                                                  w3[co][t] * act(y[b][co][row][col])
+ * (w3 : [Cout][3][3] fp32, the next conv's weight; 2 * Cout / MVBEV_CONV_BN sets;
+ * partials_bytes >= mvbev_conv3x3_bf16x3_cout1_partials_bytes).  mvbev_cout1_reduce_partials
+ * then forms map[b][0][r][:] = conv3x3(y, w3, dilation3, padding dilation3)[map_row0 + r]
+ * summing the sets' shifted taps in a fixed order; the rows map_row0 +- dilation3 that lie
+ * inside the image must be among desc's computed rows.  Same value as storing y and running
+ * mvbev_conv3x3_cout1_f32 on it, to fp32 summation order. */
+size_t mvbev_conv3x3_bf16x3_cout1_partials_bytes(const mvbev_conv_desc* desc, int64_t Cout);
+int mvbev_conv3x3_bf16x3_cout1_partials(const void* x, const mvbev_conv_desc* desc, const void* w_packed,
+                                        const float* bias, int64_t Cout, int dilation, int relu, const float* w3,
+                                        void* partials, size_t partials_bytes, void* stream);
+int mvbev_cout1_reduce_partials(const void* partials, const mvbev_conv_desc* desc, int64_t Cout, int dilation3,
+                                float* map, int64_t map_row0, int64_t map_rows, void* stream);
 
 /* y[b][0][r][:] = conv3x3(x[b], w, dilation=d, padding=d)[out_row0 + r], one output channel,
  * no bias.  x : [B][C][in_rows][W] holding global rows [in_row0, in_row0+in_rows) of an

@@ -51,6 +51,9 @@ EXPORTS = (
     "mvbev_conv3x3_bf16x3_tile_rows",
     "mvbev_warp_views_split_bf16_ex",
     "mvbev_warp_views_upsampled_ex",
+    "mvbev_conv3x3_bf16x3_cout1_partials_bytes",
+    "mvbev_conv3x3_bf16x3_cout1_partials",
+    "mvbev_cout1_reduce_partials",
 )
 WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
 
@@ -182,6 +185,13 @@ def _declare(lib):
                                                   [ctypes.c_int, _p])
     lib.mvbev_conv3x3_bf16x3_tile_rows.restype = ctypes.c_int
     lib.mvbev_conv3x3_bf16x3_tile_rows.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.mvbev_conv3x3_bf16x3_cout1_partials_bytes.restype = ctypes.c_size_t
+    lib.mvbev_conv3x3_bf16x3_cout1_partials_bytes.argtypes = [ctypes.POINTER(ConvDesc), _i64]
+    lib.mvbev_conv3x3_bf16x3_cout1_partials.restype = ctypes.c_int
+    lib.mvbev_conv3x3_bf16x3_cout1_partials.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, _i64, ctypes.c_int,
+                                                        ctypes.c_int, _p, _p, ctypes.c_size_t, _p]
+    lib.mvbev_cout1_reduce_partials.restype = ctypes.c_int
+    lib.mvbev_cout1_reduce_partials.argtypes = [_p, ctypes.POINTER(ConvDesc), _i64, ctypes.c_int, _p, _i64, _i64, _p]
 
 
 def load(path: os.PathLike | str | None = None):

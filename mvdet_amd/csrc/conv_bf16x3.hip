@@ -125,6 +125,12 @@ struct Args {
   // output channel group g (cot_pg Cout tiles each) is never read, so its tiles are skipped
   const uint32_t* cmask;
   int cot_pg;
+  // fused single-output-channel conv after this one (ring kernel only): w3 [Cout][9] fp32;
+  // p3 receives, per (Cout tile, 64-channel half) set, tap and output pixel, the partial
+  // sum over the set's channels of w3[co][tap] * act(y[co][pixel]) ([B][2 n_cot][9][out_rows][W]);
+  // y may then be null (not stored)
+  const float* w3;
+  float* p3;
 };
 
 // Input tag: the split-bf16 blocked layout written by mvbev_warp_views_split_bf16 and by this
@@ -625,7 +631,87 @@ __device__ inline void glds16(const u32x4* src, u32x4* lds_wave_base) {
                               // slower: conv1 2.33-2.38 vs 2.18-2.22 ms, the extra A set spills 4-5 VGPRs)
 #endif
 
-template <int DIL, bool RELU>
+// Epilogue of a conv followed by a single-output-channel conv (conv2 -> conv3, map_classifier[2:5],
+// persp_trans_detector.py:53-54): instead of storing the activation, each lane forms, for its
+// pixel and the 9 taps of the next conv, the dot product of its channels' activations with
+// w3[co][tap]; the two lane halves are added, and lanes 0-31 store one partial per (set,
+// tap, pixel), set = (Cout tile, 64-channel half of the wave).  cout1_reduce_kernel then sums
+// the sets' shifted taps in a fixed order.  w3 is staged in LDS ([tap][128 co] of this Cout
+// tile) after the K loop: 4 consecutive channels = one ds_read_b128 per (tap, 8-channel quad).
+template <bool RELU>
+__device__ __attribute__((always_inline)) inline void cout1_partials(const Args& a, int b, int row_base, int dil,
+                                                                    int col, int cot, int cw,
+                                      const floatx16 (&acc)[2][3], u32x4* lds) {
+  const int tid = threadIdx.x, kh = (tid & 63) >> 5;
+  // LDS (the ring buffers, free after the K loop): w3s [9][128] then the bias [128]
+  float* w3s = reinterpret_cast<float*>(lds);
+  float* bs = w3s + 9 * BN;
+  __syncthreads();  // every wave is past its last fragment read of the ring buffers
+  for (int i = tid; i < 10 * BN; i += blockDim.x) {
+    const int t = i / BN, co = i - t * BN;
+    w3s[i] = t < 9 ? a.w3[(int64_t)(cot * BN + co) * 9 + t] : (a.bias ? a.bias[cot * BN + co] : 0.f);
+  }
+  __syncthreads();
+  const int W = a.W;
+  const int nsets = 2 * a.n_cot, set = 2 * cot + cw / 64;
+  // per row: per (Cout block, 4-channel quad) the 4 activations, then the 9 taps' weights one
+  // floatx4 at a time (9 sums + 4 activations + 4 weights live; the weights re-read per row)
+#pragma unroll
+  for (int pt = 0; pt < 3; ++pt) {
+    float s[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) s[t] = 0.f;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int cl = cw + 32 * ct + 8 * q + 4 * kh;  // 4 consecutive channels of this lane
+        const floatx4 bq = *reinterpret_cast<const floatx4*>(bs + cl);
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float t = acc[ct][pt][4 * q + e] + bq[e];
+          v[e] = RELU ? (t < 0.f ? 0.f : t) : t;
+        }
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const floatx4 w = *reinterpret_cast<const floatx4*>(w3s + t * BN + cl);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) s[t] += w[e] * v[e];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one quad's weights in registers at a time
+      }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) s[t] += __shfl_xor(s[t], 32);
+    const int row = row_base + pt * dil;
+    if (kh == 0 && row < a.out_row0 + a.out_rows && col < W) {
+      float* p = a.p3 + ((((int64_t)b * nsets + set) * 9) * a.out_rows + (row - a.out_row0)) * W + col;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) p[(int64_t)t * a.out_rows * W] = s[t];
+    }
+  }
+}
+
+// map[b][0][q][c] = sum over sets s, taps t of p3[b][s][t][q + d(t/3 - 1)][c + d(t%3 - 1)]
+// (zero outside the image): the single-output conv from the partials above, fixed order.
+__global__ void cout1_reduce_kernel(const float* __restrict__ p3, int nsets, int H, int W, int rows_p,
+                                    int row0_p, int dil, float* __restrict__ map, int map_row0, int map_rows) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x, qr = blockIdx.y, b = blockIdx.z;
+  if (c >= W) return;
+  const int q = map_row0 + qr;
+  const float* pb = p3 + (int64_t)b * nsets * 9 * rows_p * W;
+  float acc = 0.f;
+  for (int s = 0; s < nsets; ++s)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int r = q + dil * (t / 3 - 1), cc = c + dil * (t % 3 - 1);
+      if (r >= 0 && r < H && cc >= 0 && cc < W)
+        acc += pb[(((int64_t)s * 9 + t) * rows_p + (r - row0_p)) * W + cc];
+    }
+  map[((int64_t)b * map_rows + qr) * W + c] = acc;
+}
+
+template <int DIL, bool RELU, bool P3 = false>
 __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
   using G = RingGeo<DIL>;
   constexpr int XW = G::XW, XPIX = G::XPIX, NX = G::NX, XBUF = G::XBUF;
@@ -906,11 +992,15 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the block exits
   }
 
+  if constexpr (P3) {
+    cout1_partials<RELU>(a, b, y0 + base, DIL, x0 + l32, cot, cw, acc, lds);
+  } else {
 #pragma unroll
-  for (int ct = 0; ct < 2; ++ct)
+    for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-    for (int pt = 0; pt < 3; ++pt)
-      store_block<RELU>(a, b, y0 + base + pt * DIL, x0 + l32, cot * BN + cw + 32 * ct, acc[ct][pt]);
+      for (int pt = 0; pt < 3; ++pt)
+        store_block<RELU>(a, b, y0 + base + pt * DIL, x0 + l32, cot * BN + cw + 32 * ct, acc[ct][pt]);
+  }
 }
 
 #ifndef MVBEV_B3_RING
@@ -969,8 +1059,8 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
                   const float* bias, const float* init, int64_t Cout, int dilation, int relu,
                   float* y, int y_layout, const uint32_t* group_mask, const int32_t* tile_order,
                   void* workspace, size_t ws_bytes, void* stream, const uint32_t* out_mask = nullptr,
-                  int cot_pg = 1) {
-  if (!x || !d || !w_packed || !y) return MVBEV_ERR_NULL;
+                  int cot_pg = 1, const float* w3 = nullptr, float* p3 = nullptr) {
+  if (!x || !d || !w_packed || (!y && !p3) || (!w3 != !p3)) return MVBEV_ERR_NULL;
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || d->in_rows <= 0 ||
       d->out_rows <= 0 || d->group <= 0)
     return MVBEV_ERR_RANK;
@@ -992,6 +1082,9 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   // split-bf16 input runs the LDS-DMA ring kernel (12-row tiles, no split-K tail)
   const bool ring = std::is_same<TIn, SplitIn>::value && MVBEV_B3_RING && !out_mask &&
                     (dilation == 1 || dilation == 2);
+  if (p3 && (!ring || init)) return MVBEV_ERR_SHAPE;  // the fused cout1 epilogue: ring kernel, no init term
+  a.w3 = w3;
+  a.p3 = p3;
   a.tiles_x = (int)ceil_div(d->W, TW); a.tiles_y = (int)ceil_div(d->out_rows, ring ? RT : NW);
   a.n_cot = (int)(Cout / BN);
   const int64_t tiles = (int64_t)a.tiles_x * a.tiles_y * a.n_cot * d->B;
@@ -1030,8 +1123,13 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
       hipLaunchKernelGGL((sk_fixup_kernel<R, NW>), dim3((unsigned)plan.tail),              \
                          dim3(64 * NW), 0, s, a);                                         \
   } while (0)
-#define RING_LAUNCH(D, R) \
-  hipLaunchKernelGGL((conv_ring_kernel<D, R>), dim3((unsigned)nwg), dim3(RNT), 0, s, a)
+#define RING_LAUNCH(D, R)                                                                         \
+  do {                                                                                            \
+    if (p3)                                                                                       \
+      hipLaunchKernelGGL((conv_ring_kernel<D, R, true>), dim3((unsigned)nwg), dim3(RNT), 0, s, a); \
+    else                                                                                          \
+      hipLaunchKernelGGL((conv_ring_kernel<D, R>), dim3((unsigned)nwg), dim3(RNT), 0, s, a);       \
+  } while (0)
   if (ring) {
     if (dilation == 1) {
       if (relu) RING_LAUNCH(1, true); else RING_LAUNCH(1, false);
@@ -1134,6 +1232,44 @@ int mvbev_conv3x3_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_desc* 
   return launch<float>(x, desc, w_packed, bias, init, Cout, dilation, relu,
                        static_cast<float*>(y), y_layout, group_mask, tile_order, workspace,
                        workspace_bytes, stream);
+}
+
+size_t mvbev_conv3x3_bf16x3_cout1_partials_bytes(const mvbev_conv_desc* desc, int64_t Cout) {
+  if (!desc || Cout <= 0 || Cout % mvbev::b3::BN != 0 || desc->B <= 0 || desc->W <= 0 || desc->out_rows <= 0) return 0;
+  return (size_t)desc->B * (size_t)(2 * (Cout / mvbev::b3::BN)) * 9 * (size_t)desc->out_rows * (size_t)desc->W *
+         sizeof(float);
+}
+
+int mvbev_conv3x3_bf16x3_cout1_partials(const void* x, const mvbev_conv_desc* desc, const void* w_packed,
+                                        const float* bias, int64_t Cout, int dilation, int relu, const float* w3,
+                                        void* partials, size_t partials_bytes, void* stream) {
+  using namespace mvbev::b3;
+  if (!desc || !w3 || !partials) return MVBEV_ERR_NULL;
+  const size_t need = mvbev_conv3x3_bf16x3_cout1_partials_bytes(desc, Cout);
+  if (need == 0 || partials_bytes < need) return MVBEV_ERR_SHAPE;
+  return launch<SplitIn>(x, desc, w_packed, bias, nullptr, Cout, dilation, relu, nullptr, MVBEV_LAYOUT_F32, nullptr,
+                         nullptr, nullptr, 0, stream, nullptr, 1, w3, static_cast<float*>(partials));
+}
+
+int mvbev_cout1_reduce_partials(const void* partials, const mvbev_conv_desc* desc, int64_t Cout, int dilation3,
+                                float* map, int64_t map_row0, int64_t map_rows, void* stream) {
+  using namespace mvbev::b3;
+  if (!partials || !desc || !map) return MVBEV_ERR_NULL;
+  if (dilation3 < 1) return MVBEV_ERR_DILATION;
+  if (map_rows <= 0 || Cout <= 0 || desc->B <= 0 || desc->W <= 0 || desc->out_rows <= 0) return MVBEV_ERR_RANK;
+  if (Cout % BN != 0) return MVBEV_ERR_SHAPE;
+  // every row the map band reads (band +- dilation3, inside the image) must be a computed row
+  const int64_t r_lo = std::max<int64_t>(0, map_row0 - dilation3);
+  const int64_t r_hi = std::min<int64_t>(desc->H, map_row0 + map_rows + dilation3);
+  if (map_row0 < 0 || map_row0 + map_rows > desc->H || r_lo < desc->out_row0 || r_hi > desc->out_row0 + desc->out_rows ||
+      map_rows > 65535 || desc->B > 65535 || desc->out_rows * desc->W > INT32_MAX)
+    return MVBEV_ERR_SHAPE;
+  const dim3 grid((unsigned)mvbev::ceil_div(desc->W, 128), (unsigned)map_rows, (unsigned)desc->B);
+  hipLaunchKernelGGL(cout1_reduce_kernel, grid, dim3(128), 0, mvbev::as_stream(stream),
+                     static_cast<const float*>(partials), (int)(2 * (Cout / BN)), (int)desc->H, (int)desc->W,
+                     (int)desc->out_rows, (int)desc->out_row0, dilation3, map, (int)map_row0, (int)map_rows);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
 }
 
 int mvbev_conv3x3_dgrad_bf16x3(const float* dy, const mvbev_conv_desc* desc, const void* w_packed, int64_t Cout_p,

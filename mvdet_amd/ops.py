@@ -457,6 +457,48 @@ def conv3x3_cout1(x: torch.Tensor, weight: torch.Tensor, dilation: int, H: Optio
     return out
 
 
+def conv3x3_cout1_partials_bytes(desc, cout: int) -> int:
+    """Bytes of the partial-sum buffer ``conv3x3_then_cout1_partials`` needs for this conv."""
+    return int(_native.load().mvbev_conv3x3_bf16x3_cout1_partials_bytes(ctypes.byref(desc), int(cout)))
+
+
+def conv3x3_then_cout1_partials(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: Optional[torch.Tensor],
+                                dilation: int, relu: bool, weight3: torch.Tensor, partials: torch.Tensor) -> None:
+    """The split-bf16-input conv of ``conv3x3_desc`` (bf16x3, no init / mask) without its
+    output in HBM: its epilogue writes, for the following single-output conv ``weight3``
+    [1, cout, 3, 3], one partial per (64-channel set, tap, pixel) into ``partials`` (fp32,
+    ``conv3x3_cout1_partials_bytes``); ``cout1_from_partials`` finishes that conv.
+    (``persp_trans_detector.py:53-54``: map_classifier[2:5] without y2 in memory.)"""
+    _require_cuda(x, packed, weight3, partials)
+    if x.dtype != torch.bfloat16 or packed.dtype != torch.bfloat16:
+        raise TypeError("the fused conv -> cout1 path takes the split-bf16 layout and bf16x3 packed weights")
+    if tuple(weight3.shape) != (1, cout, 3, 3):
+        raise ValueError(f"weight3 must be [1,{cout},3,3], got {tuple(weight3.shape)}")
+    if partials.dtype != torch.float32 or not partials.is_contiguous():
+        raise ValueError("partials must be a contiguous float32 tensor")
+    w3 = weight3.detach().contiguous()
+    b = bias.detach().contiguous() if bias is not None else None
+    st = _native.load().mvbev_conv3x3_bf16x3_cout1_partials(
+        x.data_ptr(), ctypes.byref(desc), packed.data_ptr(), b.data_ptr() if b is not None else None, int(cout),
+        int(dilation), int(bool(relu)), w3.data_ptr(), partials.data_ptr(),
+        partials.numel() * partials.element_size(), _stream(x))
+    _native.check(st, "mvbev_conv3x3_bf16x3_cout1_partials")
+
+
+def cout1_from_partials(partials: torch.Tensor, desc, cout: int, dilation3: int, map_row0: int, map_rows: int,
+                        out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``conv2d(act(y), weight3, padding=d3, dilation=d3)`` rows ``[map_row0, map_row0+map_rows)``
+    → [B,1,map_rows,W] from ``conv3x3_then_cout1_partials``' partials (fixed summation order)."""
+    _require_cuda(partials)
+    B, W = desc.B, desc.W
+    if out is None:
+        out = torch.empty((B, 1, map_rows, W), dtype=torch.float32, device=partials.device)
+    st = _native.load().mvbev_cout1_reduce_partials(partials.data_ptr(), ctypes.byref(desc), int(cout), int(dilation3),
+                                                     out.data_ptr(), int(map_row0), int(map_rows), _stream(partials))
+    _native.check(st, "mvbev_cout1_reduce_partials")
+    return out
+
+
 # ----------------------------------------------------------------------------------------------
 # backward (SURVEY §8(f) row 2): the adjoints autograd needs to train through the hot path
 

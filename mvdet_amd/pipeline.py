@@ -57,6 +57,9 @@ class Workspace:
     # the slab was zero-filled at allocation and is only written by this engine's warps (or the
     # multi-GPU gather of them): a view's out-of-source pixels are already 0 and are skipped
     slab_zeroed: bool = False
+    # conv2 -> conv3 fused (inference): conv3's per-(64-channel set, tap, pixel) partials
+    # [B, 2 * 512 / 128, 9, y2_rows, Wo] fp32 replace y2 in HBM (allocated on first use)
+    p3: Optional[torch.Tensor] = None
 
 
 class ProjectFuse:
@@ -69,7 +72,7 @@ class ProjectFuse:
     def __init__(self, proj_mats: Sequence[torch.Tensor], src_hw: Tuple[int, int], grid_hw: Tuple[int, int],
                  channels: int, mid_channels: int = 512, slot_views: Optional[Sequence[Optional[int]]] = None,
                  precision: str = "bf16x3", slab_dtype: torch.dtype = torch.float32,
-                 all_views: bool = True, split_k: bool = True, frustum: bool = True):
+                 all_views: bool = True, split_k: bool = True, frustum: bool = True, fuse_conv3: bool = True):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":
@@ -119,6 +122,9 @@ class ProjectFuse:
         # conv1 writes y1 pre-split (bf16 hi/lo blocks) so conv2 stages it with 16-B copies;
         # the partial-sum multi-GPU mode turns this off (it sums fp32 partials)
         self.y1_split = precision == "bf16x3"
+        # conv2's epilogue computes conv3's per-tap partial sums instead of storing y2
+        # (split-bf16 y1, i.e. the ring conv); training keeps y2 (its backward reads it)
+        self.fuse_conv3 = fuse_conv3
 
     # -- buffers ----------------------------------------------------------------------------
     def workspace(self, B: int, device, band: Optional[Tuple[int, int]] = None) -> Workspace:
@@ -293,6 +299,33 @@ class ProjectFuse:
         return ops.conv3x3_desc(ws.y1, d2, p2, self.mid, bias=conv2.bias, dilation=2, relu=True, out=ws.y2,
                                 workspace=self._sk_ws(d2, ws.y1.device))
 
+    def _conv2_desc(self, ws: Workspace):
+        H, W = self.grid_hw
+        (a1, b1), (a2, b2) = ws.y1_rows, ws.y2_rows
+        B = ws.y1.shape[0]
+        return ops.conv_desc(B, self.mid, H, W, group=self.mid, group_stride=0,
+                             batch_stride=self.mid * (b1 - a1) * W, in_row0=a1, in_rows=b1 - a1,
+                             out_row0=a2, out_rows=b2 - a2)
+
+    def conv3_fused_applies(self, ws: Workspace) -> bool:
+        """conv2 -> conv3 without y2 in HBM: split-bf16 y1 (the ring conv) and fuse_conv3."""
+        return self.fuse_conv3 and ws.y1.dtype == torch.bfloat16
+
+    def conv2_partials(self, ws: Workspace, conv2: torch.nn.Conv2d, conv3: torch.nn.Conv2d) -> None:
+        """a8 + the first half of a9: relu(conv3x3_d2(y1) + b2) never leaves the conv's
+        registers; its epilogue writes conv3's per-(channel set, tap, pixel) partials."""
+        d2 = self._conv2_desc(ws)
+        need = ops.conv3x3_cout1_partials_bytes(d2, self.mid)
+        if ws.p3 is None or ws.p3.numel() * 4 < need:
+            ws.p3 = torch.empty((need + 3) // 4, dtype=torch.float32, device=ws.y1.device)
+        ops.conv3x3_then_cout1_partials(ws.y1, d2, self.pack2.get(conv2.weight), self.mid, conv2.bias, 2, True,
+                                        conv3.weight, ws.p3)
+
+    def conv3_from_partials(self, ws: Workspace, conv3: torch.nn.Conv2d) -> torch.Tensor:
+        """The rest of a9: map rows ``ws.band`` from the partials (fixed summation order)."""
+        r0, r1 = ws.band
+        return ops.cout1_from_partials(ws.p3, self._conv2_desc(ws), self.mid, 4, r0, r1 - r0)
+
     def conv3(self, ws: Workspace, conv3: torch.nn.Conv2d) -> torch.Tensor:
         """a9: map = conv3x3_d4(y2) (Cout 1, no bias) on the output band → [B,1,rows,Wo]."""
         H = self.grid_hw[0]
@@ -331,6 +364,16 @@ class ProjectFuse:
 
         ``mark(stage)`` (optional) is called right before each conv is enqueued
         (``bench.py`` records HIP events there)."""
+        if self.conv3_fused_applies(ws):
+            if mark:
+                mark("conv1")
+            self.conv1(ws, map_classifier[0])
+            if mark:
+                mark("conv2")
+            self.conv2_partials(ws, map_classifier[2], map_classifier[4])
+            if mark:
+                mark("conv3")
+            return self.conv3_from_partials(ws, map_classifier[4])
         for stage, idx, fn in (("conv1", 0, self.conv1), ("conv2", 2, self.conv2), ("conv3", 4, self.conv3)):
             if mark:
                 mark(stage)

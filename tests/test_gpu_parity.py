@@ -448,6 +448,8 @@ def test_detector_forward_matches_reference_golden(name):
     if "warp_out" in g:
         assert_parity(warped.cpu(), g["warp_out"], "warp_out")
         assert_parity(eng.y1_fp32(ws).cpu(), g["conv1_relu"], "conv1")
+        with torch.no_grad():  # inference fuses conv2 into conv3 (no y2 in HBM): run conv2 alone
+            eng.conv2(ws, model.map_classifier[2])
         assert_parity(ws.y2.cpu(), g["conv2_relu"], "conv2")
 
 
@@ -494,5 +496,48 @@ def test_full_size_project_fuse_vs_oracle(cfg, precision):
     for v in range(ds.num_cam):
         assert_parity(eng.view_slice(ws, v).cpu(), keep["warped"][v], f"cfg{cfg} warp view {v}")
     assert_parity(eng.y1_fp32(ws).cpu(), keep["conv1_relu"], f"cfg{cfg} conv1")
-    assert_parity(ws.y2.cpu(), keep["conv2_relu"], f"cfg{cfg} conv2")
     assert_parity(got.cpu(), ref, f"cfg{cfg} map_result")
+    with torch.no_grad():  # inference fuses conv2 into conv3 (no y2 in HBM): conv2 alone, then conv3 on y2
+        eng.conv2(ws, mc[2])
+        unfused = eng.conv3(ws, mc[4])
+        torch.cuda.synchronize()
+    assert_parity(ws.y2.cpu(), keep["conv2_relu"], f"cfg{cfg} conv2")
+    if eng.conv3_fused_applies(ws):  # fused and unfused conv3 agree to fp32 summation order
+        assert_parity(got.cpu(), unfused.cpu(), f"cfg{cfg} fused vs unfused conv3")
+
+
+@pytest.mark.parametrize("band", [None, (5, 23)])
+def test_conv2_conv3_fused_matches_unfused(band):
+    """conv2 -> conv3 without y2 in HBM (conv2's epilogue writes conv3's per-tap partials,
+    a reduce kernel sums them): same map as conv2 + conv3 on y2 to fp32 summation order, on a
+    grid with partial tiles (37 x 70) and on a row band; bitwise identical between the band
+    and the whole grid (per-pixel partials do not depend on the tile decomposition)."""
+    from mvdet_amd import ProjectFuse, synthetic
+    from mvdet_amd.geometry import projection_matrices
+    ds = synthetic.wildtrack_like(2, 4, seed=3, img_shape=(108, 192), worldgrid_shape=(148, 280))
+    C = 32
+    up = ds.upsample_shape
+    feats = [synthetic.synthetic_features(1, C, [u // 3 for u in up], up, seed=70 + v, device=DEV) for v in range(2)]
+    pm = projection_matrices(ds)
+    params = fixtures.head_params(2, seed=9, C=C)
+    mc = torch.nn.Sequential(torch.nn.Conv2d(C * 2 + 2, 512, 3, padding=1), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False))
+    mc.load_state_dict({k.replace("map_classifier.", ""): torch.from_numpy(v) for k, v in params.items()
+                        if k.startswith("map_classifier.")})
+    mc = mc.to(DEV)
+    outs = {}
+    for fused in (True, False):
+        eng = ProjectFuse(pm, tuple(up), tuple(ds.reducedgrid_shape), C, fuse_conv3=fused)
+        with torch.no_grad():
+            ws = eng.workspace(1, DEV, band=band)
+            eng.warp_views(ws, [0, 1], feats)
+            assert eng.conv3_fused_applies(ws) == fused
+            outs[fused] = eng.fuse(ws, mc).cpu()
+            if band is not None and fused:
+                whole = eng.workspace(1, DEV)
+                eng.warp_views(whole, [0, 1], feats)
+                full = eng.fuse(whole, mc).cpu()
+                assert torch.equal(outs[fused], full[:, :, band[0]:band[1]])
+    assert outs[True].shape == outs[False].shape
+    assert_parity(outs[True], outs[False], "fused vs unfused conv3")

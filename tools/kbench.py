@@ -97,6 +97,9 @@ def main():
             "conv1": (lambda: eng.conv1(ws, mc[0]), 2.0 * B * ho * wo * 9 * N * C * 512),
             "conv2": (lambda: eng.conv2(ws, mc[2]), 2.0 * B * ho * wo * 9 * 512 * 512),
             "conv3": (lambda: eng.conv3(ws, mc[4]), None),
+            # conv2 -> conv3 fused (the default inference path): partials epilogue + reduce
+            "conv23": (lambda: (eng.conv2_partials(ws, mc[2], mc[4]), eng.conv3_from_partials(ws, mc[4])),
+                       2.0 * B * ho * wo * 9 * 512 * 512),
         }
         if {"wgrad1", "dgrad1"} & set(args.only.split(",")):
             stages.update(backward_stages(eng, ws, mc, B, ho, wo, N, C, dev))

@@ -701,6 +701,7 @@ __global__ void cout1_reduce_kernel(const float* __restrict__ p3, int nsets, int
   const int q = map_row0 + qr;
   const float* pb = p3 + (int64_t)b * nsets * 9 * rows_p * W;
   float acc = 0.f;
+#pragma unroll 4
   for (int s = 0; s < nsets; ++s)
 #pragma unroll
     for (int t = 0; t < 9; ++t) {

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -329,6 +329,12 @@ int mvbev_pack_conv3x3_dgrad_bf16x3(const float* w, int64_t Cout_w, int64_t Cin_
 int mvbev_conv3x3_dgrad_bf16x3(const float* dy, const mvbev_conv_desc* desc, const void* w_packed, int64_t Cout_p,
                                int dilation, void* dx, int dx_layout, const uint32_t* out_mask,
                                int64_t cot_per_group, void* stream);
+/* Same with dy in dy_layout: MVBEV_LAYOUT_F32 (as above) or MVBEV_LAYOUT_SPLIT_BF16 (the
+ * LDS-DMA ring kernel, dilation 1 or 2; its output tiles, and so out_mask's tiles, are
+ * mvbev_conv3x3_bf16x3_tile_rows(MVBEV_LAYOUT_SPLIT_BF16, dilation) rows high). */
+int mvbev_conv3x3_dgrad_bf16x3_ex(const void* dy, int dy_layout, const mvbev_conv_desc* desc, const void* w_packed,
+                                  int64_t Cout_p, int dilation, void* dx, int dx_layout, const uint32_t* out_mask,
+                                  int64_t cot_per_group, void* stream);
 
 /* Weight gradient of mvbev_conv3x3_bf16x3 (3xbf16 MFMA, fp32 accumulation):
  *   dw[co][chan_map[k]][t] = sum_b,y,x dy[b][co][y][x] * x[b][k][y + (t/3-1)d][x + (t%3-1)d]
@@ -365,6 +371,11 @@ int mvbev_conv3x3_bias_coord_grad_f32(const float* dy, int64_t B, int64_t Cout, 
 
 /* In place: dy[i] = y[i] > 0 ? dy[i] : 0 (y = the ReLU's output; torch threshold_backward). */
 int mvbev_relu_backward_f32(float* dy, const float* y, int64_t n, void* stream);
+/* Same with y in the split-bf16 layout (y = hi + lo; [B][C/8][H][W] pieces, C % 8 == 0) and
+ * dy fp32 [B][C][H][W]; dy_split (optional, 16-B aligned) also receives the masked dy in the
+ * split layout (the next data-gradient conv's input). */
+int mvbev_relu_backward_split_f32(float* dy, const void* y_split, int64_t B, int64_t C, int64_t H, int64_t W,
+                                  void* dy_split, void* stream);
 
 /* Backward of mvbev_conv3x3_cout1_f32 over a whole image (x [B][C][H][W], w [C][3][3], dmap
  * [B][1][H][W] fp32):  dx[b][c][p] = sum_t w[c][t] dmap[b][p - s_t], zeroed where x <= 0 when

@@ -45,7 +45,10 @@ def _mark(stage: str) -> None:
 
 
 def _train_workspace(engine: ProjectFuse, B: int, device) -> Workspace:
-    """A fresh (never reused) forward workspace with fp32 y1 (the ReLU mask source)."""
+    """A fresh (never reused) forward workspace.  y1 in the layout the inference path uses
+    (split-bf16 with 3xbf16: conv2 runs on the ring kernel, conv2's weight gradient on the
+    LDS-DMA wgrad kernel, and the ReLU mask is read from hi + lo), y2 kept in fp32 (conv3's
+    backward reads it: no conv2 -> conv3 fusion)."""
     H, W = engine.grid_hw
     if engine.split:  # the split warp writes every 8-channel group in full (zeros past C)
         slab = torch.empty((engine.S,) + ops.split_shape(B, engine.Cs, H, W), dtype=torch.bfloat16, device=device)
@@ -53,10 +56,13 @@ def _train_workspace(engine: ProjectFuse, B: int, device) -> Workspace:
         slab = torch.empty((engine.S, B, engine.Cs, H, W), dtype=engine.slab_dtype, device=device)
         slab[:, :, engine.C:].zero_()  # padding channels the warp does not write
     y1r, y2r = band_rows(0, H, H)
-    y1 = torch.empty((B, engine.mid, H, W), dtype=torch.float32, device=device)
+    if engine.y1_split:
+        y1 = torch.empty(ops.split_shape(B, engine.mid, H, W), dtype=torch.bfloat16, device=device)
+    else:
+        y1 = torch.empty((B, engine.mid, H, W), dtype=torch.float32, device=device)
     y2 = torch.empty((B, engine.mid, H, W), dtype=torch.float32, device=device)
     m = engine.m_norm_cpu.to(device)[:, None].expand(engine.num_cam, B, 3, 3).contiguous()
-    return Workspace(slab, y1, y2, m, (0, H), y1r, y2r)
+    return Workspace(slab, y1, y2, m, (0, H), y1r, y2r, store_y2=True)
 
 
 def _bwd_state(engine: ProjectFuse):
@@ -148,6 +154,7 @@ class ProjectFuseFunction(torch.autograd.Function):
         H, W = engine.grid_hw
         B = ws.y1.shape[0]
         dev = ws.y1.device
+        y1_split = ws.y1.dtype == torch.bfloat16
         dmap = dmap.contiguous().float()
         mid = engine.mid
         # conv3: dy2 = dgrad * relu'(y2); dw3
@@ -165,7 +172,12 @@ class ProjectFuseFunction(torch.autograd.Function):
         if dy1.shape[1] != mid:
             dy1 = dy1[:, :mid].contiguous()
         del dy2
-        ops.relu_backward_(dy1, ws.y1)
+        dy1s = None
+        if y1_split:  # the masked dy1 also in the split layout: conv1's dgrad on the ring kernel
+            dy1s = torch.empty(ops.split_shape(B, mid, H, W), dtype=torch.bfloat16, device=dev)
+            ops.relu_backward_split_(dy1, ws.y1, dy1s)
+        else:
+            ops.relu_backward_(dy1, ws.y1)
         # conv1: db1 + coord channels, view channels (slab order through the pack's channel map)
         _mark("bwd_conv1_wgrad")
         nc = n * engine.C
@@ -185,8 +197,10 @@ class ProjectFuseFunction(torch.autograd.Function):
             if C % ops.KC == 0:  # split-bf16 dslab: the adjoint gathers 8 channels per 32-B entry
                 dslab = torch.empty(ops.split_shape(B, cp, H, W), dtype=torch.bfloat16, device=dev)
                 # frustum: a view's tiles of dslab that its warp never samples are not computed
-                cm = engine.conv1_mask(dev, 0, H, tile_h=_native.TILE_H) if C % ops.BN == 0 else None
-                ops.conv3x3_dgrad(dy1, st.dgrad1, w1, 1, out=dslab, out_mask=cm, cot_per_group=C // ops.BN)
+                cm = (engine.conv1_mask(dev, 0, H, tile_h=ops.dgrad_tile_rows(dy1s is not None, 1))
+                      if C % ops.BN == 0 else None)
+                ops.conv3x3_dgrad(dy1 if dy1s is None else dy1s, st.dgrad1, w1, 1, out=dslab, out_mask=cm,
+                                  cot_per_group=C // ops.BN)
                 g8 = C // ops.KC
                 douts = [dslab[:, v * g8:(v + 1) * g8] for v in range(n)]
             else:

@@ -638,6 +638,27 @@ __global__ void relu_backward_kernel(float* __restrict__ dy, const float* __rest
   }
 }
 
+// dy (fp32 [B][C][HW]) *= [y > 0] with the ReLU output y in the split-bf16 layout
+// ([B][C/8][HW] pieces of bf16 hi[8], lo[8]; y = hi + lo); dys (optional) also receives the
+// masked dy in the split layout, the input of the next data-gradient conv (ring kernel).
+__global__ void relu_backward_split_kernel(float* __restrict__ dy, const u32x4_t* __restrict__ y, int C, int64_t HW,
+                                           u32x4_t* __restrict__ dys) {
+  const int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int g = blockIdx.y, b = blockIdx.z, G = C / 8;
+  if (p >= HW) return;
+  const int64_t e = ((int64_t)b * G + g) * HW + p;
+  const bf16x8_t hi = __builtin_bit_cast(bf16x8_t, y[2 * e]), lo = __builtin_bit_cast(bf16x8_t, y[2 * e + 1]);
+  float* d = dy + ((int64_t)b * C + 8 * g) * HW + p;
+  float v[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const float yv = (float)hi[c] + (float)lo[c];
+    v[c] = yv > 0.f ? d[c * HW] : 0.f;
+    d[c * HW] = v[c];
+  }
+  if (dys) store_split8(dys + 2 * e, v);
+}
+
 // conv3 (Cout = 1, no bias) data gradient, times conv2's ReLU mask when relu_mask:
 // dx[b][c][y][x] = sum_t w[c][t] * dmap[b][y - (ky-1)d][x - (kx-1)d]
 constexpr int kCout1Cpb = 32;  // channels per block
@@ -1135,6 +1156,21 @@ int mvbev_relu_backward_f32(float* dy, const float* y, int64_t n, void* stream) 
   if (((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(y)) & 15) != 0) return MVBEV_ERR_ALIGN;
   hipLaunchKernelGGL(bwd::relu_backward_kernel, dim3((unsigned)ceil_div(ceil_div(n, 4), 256)), dim3(256), 0,
                      as_stream(stream), dy, y, n);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+int mvbev_relu_backward_split_f32(float* dy, const void* y_split, int64_t B, int64_t C, int64_t H, int64_t W,
+                                  void* dy_split, void* stream) {
+  using namespace mvbev;
+  if (!dy || !y_split) return MVBEV_ERR_NULL;
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return MVBEV_ERR_RANK;
+  if (C % 8 != 0 || B > 65535 || C / 8 > 65535) return MVBEV_ERR_SHAPE;
+  if (((reinterpret_cast<uintptr_t>(y_split) | reinterpret_cast<uintptr_t>(dy_split)) & 15) != 0) return MVBEV_ERR_ALIGN;
+  const int64_t HW = H * W;
+  hipLaunchKernelGGL(bwd::relu_backward_split_kernel, dim3((unsigned)ceil_div(HW, 256), (unsigned)(C / 8), (unsigned)B),
+                     dim3(256), 0, as_stream(stream), dy, static_cast<const u32x4_t*>(y_split), (int)C, HW,
+                     static_cast<u32x4_t*>(dy_split));
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }

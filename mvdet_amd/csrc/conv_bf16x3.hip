@@ -743,6 +743,8 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
   const int b = rest / a.tiles_y;
   const int x0 = tx * TW;
   const int y0 = a.out_row0 + ty * RT;
+  // output-side mask: a tile of output channels nobody reads (whole block, before any barrier)
+  if (a.cmask && !((a.cmask[ty * a.tiles_x + tx] >> (cot / a.cot_pg)) & 1u)) return;
   const u32x4* wsrc = a.wp + (int64_t)cot * W16;
   const uint32_t gm = a.gmask ? a.gmask[ty * a.tiles_x + tx] : 0u;
   const int nch = a.gmask ? __builtin_popcount(gm) * a.cpg : a.nchunks;
@@ -1081,8 +1083,7 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   a.in_row0 = (int)d->in_row0; a.in_rows = (int)d->in_rows;
   a.out_row0 = (int)d->out_row0; a.out_rows = (int)d->out_rows;
   // split-bf16 input runs the LDS-DMA ring kernel (12-row tiles, no split-K tail)
-  const bool ring = std::is_same<TIn, SplitIn>::value && MVBEV_B3_RING && !out_mask &&
-                    (dilation == 1 || dilation == 2);
+  const bool ring = std::is_same<TIn, SplitIn>::value && MVBEV_B3_RING && (dilation == 1 || dilation == 2);
   if (p3 && (!ring || init)) return MVBEV_ERR_SHAPE;  // the fused cout1 epilogue: ring kernel, no init term
   a.w3 = w3;
   a.p3 = p3;
@@ -1273,13 +1274,24 @@ int mvbev_cout1_reduce_partials(const void* partials, const mvbev_conv_desc* des
   return MVBEV_OK;
 }
 
+int mvbev_conv3x3_dgrad_bf16x3_ex(const void* dy, int dy_layout, const mvbev_conv_desc* desc, const void* w_packed,
+                                  int64_t Cout_p, int dilation, void* dx, int dx_layout, const uint32_t* out_mask,
+                                  int64_t cot_per_group, void* stream) {
+  using namespace mvbev::b3;
+  if (out_mask && (cot_per_group <= 0 || cot_per_group > 65536)) return MVBEV_ERR_SHAPE;
+  if (dy_layout == MVBEV_LAYOUT_SPLIT_BF16)  // the LDS-DMA ring kernel (12-row output tiles)
+    return launch<SplitIn>(dy, desc, w_packed, nullptr, nullptr, Cout_p, dilation, 0, static_cast<float*>(dx),
+                           dx_layout, nullptr, nullptr, nullptr, 0, stream, out_mask, (int)cot_per_group);
+  if (dy_layout != MVBEV_LAYOUT_F32) return MVBEV_ERR_SHAPE;
+  return launch<float>(dy, desc, w_packed, nullptr, nullptr, Cout_p, dilation, 0, static_cast<float*>(dx),
+                       dx_layout, nullptr, nullptr, nullptr, 0, stream, out_mask, (int)cot_per_group);
+}
+
 int mvbev_conv3x3_dgrad_bf16x3(const float* dy, const mvbev_conv_desc* desc, const void* w_packed, int64_t Cout_p,
                                int dilation, void* dx, int dx_layout, const uint32_t* out_mask,
                                int64_t cot_per_group, void* stream) {
-  using namespace mvbev::b3;
-  if (out_mask && (cot_per_group <= 0 || cot_per_group > 65536)) return MVBEV_ERR_SHAPE;
-  return launch<float>(dy, desc, w_packed, nullptr, nullptr, Cout_p, dilation, 0, static_cast<float*>(dx),
-                       dx_layout, nullptr, nullptr, nullptr, 0, stream, out_mask, (int)cot_per_group);
+  return mvbev_conv3x3_dgrad_bf16x3_ex(dy, MVBEV_LAYOUT_F32, desc, w_packed, Cout_p, dilation, dx, dx_layout, out_mask,
+                                       cot_per_group, stream);
 }
 
 }  // extern "C"

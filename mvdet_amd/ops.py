@@ -648,15 +648,21 @@ def conv3x3_dgrad(dy: torch.Tensor, packed: PackedDgrad3x3, weight: torch.Tensor
                   out: Optional[torch.Tensor] = None, out_mask: Optional[torch.Tensor] = None,
                   cot_per_group: int = 1) -> torch.Tensor:
     """Data gradient of a 3x3 stride-1 conv (padding = dilation): dy [B,Cout_w,H,W] fp32
-    contiguous -> [B, cout_p, H, W] fp32, or the split-bf16 layout when ``out`` is a bf16
+    contiguous (or its split-bf16 layout, a bf16 ``split_shape`` tensor: the LDS-DMA ring
+    kernel) -> [B, cout_p, H, W] fp32, or the split-bf16 layout when ``out`` is a bf16
     ``split_shape`` tensor (channel o = forward input channel chan_map[o]; channels past
-    k_out are zero).  ``out_mask`` (int32 per conv output tile, ``warp_tile_mask``): tiles of
-    output channel group g (``cot_per_group`` 128-channel tiles) whose bit is clear are NOT
-    written (for a consumer that never reads them)."""
+    k_out are zero).  ``out_mask`` (int32 per conv output tile, ``warp_tile_mask`` at
+    ``dgrad_tile_rows`` rows): tiles of output channel group g (``cot_per_group`` 128-channel
+    tiles) whose bit is clear are NOT written (for a consumer that never reads them)."""
     _require_cuda(dy)
-    if dy.dim() != 4 or dy.dtype != torch.float32 or not dy.is_contiguous():
-        raise ValueError("dy must be a contiguous float32 [B,Cout,H,W] tensor")
-    B, K, H, W = dy.shape
+    dy_split = dy.dtype == torch.bfloat16
+    if dy.dim() != (6 if dy_split else 4) or dy.dtype not in (torch.float32, torch.bfloat16) or not dy.is_contiguous():
+        raise ValueError("dy must be a contiguous float32 [B,Cout,H,W] tensor or its split-bf16 layout")
+    if dy_split:
+        B, G, H, W = dy.shape[:4]
+        K = 8 * G
+    else:
+        B, K, H, W = dy.shape
     if K != weight.shape[0]:
         raise ValueError(f"dy has {K} channels, the weight {weight.shape[0]} outputs")
     cp = packed.cout_p
@@ -669,16 +675,22 @@ def conv3x3_dgrad(dy: torch.Tensor, packed: PackedDgrad3x3, weight: torch.Tensor
     mp = None
     if out_mask is not None:
         _require_cuda(out_mask)
-        tiles = -(-H // _native.TILE_H) * -(-W // _native.TILE_W)
+        tiles = -(-H // dgrad_tile_rows(dy_split, dilation)) * -(-W // _native.TILE_W)
         if out_mask.dtype != torch.int32 or out_mask.numel() < tiles or not out_mask.is_contiguous():
             raise ValueError(f"out_mask must be a contiguous int32 tensor of >= {tiles} tiles")
         mp = out_mask.data_ptr()
     d = conv_desc(B, K, H, W, group=K, group_stride=0, batch_stride=K * H * W)
-    st = _native.load().mvbev_conv3x3_dgrad_bf16x3(
-        dy.data_ptr(), ctypes.byref(d), packed.get(weight).data_ptr(), cp, int(dilation), out.data_ptr(),
+    st = _native.load().mvbev_conv3x3_dgrad_bf16x3_ex(
+        dy.data_ptr(), _native.LAYOUT_SPLIT_BF16 if dy_split else _native.LAYOUT_F32, ctypes.byref(d),
+        packed.get(weight).data_ptr(), cp, int(dilation), out.data_ptr(),
         _native.LAYOUT_SPLIT_BF16 if split else _native.LAYOUT_F32, mp, int(cot_per_group), _stream(dy))
-    _native.check(st, "mvbev_conv3x3_dgrad_bf16x3")
+    _native.check(st, "mvbev_conv3x3_dgrad_bf16x3_ex")
     return out
+
+
+def dgrad_tile_rows(dy_split: bool, dilation: int = 1) -> int:
+    """Output-tile rows of ``conv3x3_dgrad`` (its ``out_mask`` granule) for this dy layout."""
+    return _native.conv_tile_rows(_native.LAYOUT_SPLIT_BF16 if dy_split else _native.LAYOUT_F32, dilation)
 
 
 def wgrad_chunk_lists(mask: torch.Tensor, groups: int, B: int, H: int, W: int):
@@ -779,6 +791,24 @@ def relu_backward_(dy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         raise ValueError("dy and y must be contiguous fp32 tensors of one shape")
     st = _native.load().mvbev_relu_backward_f32(dy.data_ptr(), y.data_ptr(), dy.numel(), _stream(dy))
     _native.check(st, "mvbev_relu_backward_f32")
+    return dy
+
+
+def relu_backward_split_(dy: torch.Tensor, y_split: torch.Tensor, dy_split: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """In place: dy [B,C,H,W] fp32 = dy where y > 0 else 0, with the ReLU output ``y_split`` in
+    the split-bf16 layout (``split_shape(B, C, H, W)``, y = hi + lo); ``dy_split`` (optional,
+    same split shape) also receives the masked dy in the split layout."""
+    _require_cuda(dy, y_split)
+    B, C, H, W = dy.shape
+    if dy.dtype != torch.float32 or not dy.is_contiguous():
+        raise ValueError("dy must be a contiguous fp32 [B,C,H,W] tensor")
+    for t in (y_split, dy_split):
+        if t is not None and (t.dtype != torch.bfloat16 or tuple(t.shape) != split_shape(B, C, H, W)
+                              or not t.is_contiguous()):
+            raise ValueError(f"split tensors must be contiguous bf16 {split_shape(B, C, H, W)}")
+    st = _native.load().mvbev_relu_backward_split_f32(dy.data_ptr(), y_split.data_ptr(), B, C, H, W,
+                                                       None if dy_split is None else dy_split.data_ptr(), _stream(dy))
+    _native.check(st, "mvbev_relu_backward_split_f32")
     return dy
 
 

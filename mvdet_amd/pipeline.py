@@ -60,6 +60,8 @@ class Workspace:
     # conv2 -> conv3 fused (inference): conv3's per-(64-channel set, tap, pixel) partials
     # [B, 2 * 512 / 128, 9, y2_rows, Wo] fp32 replace y2 in HBM (allocated on first use)
     p3: Optional[torch.Tensor] = None
+    # keep y2 in HBM (the training forward: conv3's backward reads it), i.e. no conv2 -> conv3 fusion
+    store_y2: bool = False
 
 
 class ProjectFuse:
@@ -309,7 +311,7 @@ class ProjectFuse:
 
     def conv3_fused_applies(self, ws: Workspace) -> bool:
         """conv2 -> conv3 without y2 in HBM: split-bf16 y1 (the ring conv) and fuse_conv3."""
-        return self.fuse_conv3 and ws.y1.dtype == torch.bfloat16
+        return self.fuse_conv3 and ws.y1.dtype == torch.bfloat16 and not ws.store_y2
 
     def conv2_partials(self, ws: Workspace, conv2: torch.nn.Conv2d, conv3: torch.nn.Conv2d) -> None:
         """a8 + the first half of a9: relu(conv3x3_d2(y1) + b2) never leaves the conv's

@@ -209,6 +209,51 @@ def test_conv_dgrad_vs_torch(B, Cw, K, H, W, dil):
     assert (got[:, K:] == 0).all()
 
 
+def _split_encode(x: torch.Tensor) -> torch.Tensor:
+    """fp32 [B, C, H, W] (C % 8 == 0) -> the split-bf16 blocked layout [B, C/8, H, W, 2, 8]."""
+    B, C, H, W = x.shape
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.float()).to(torch.bfloat16)
+    t = torch.stack([hi, lo], 0).reshape(2, B, C // 8, 8, H, W)
+    return t.permute(1, 2, 4, 5, 0, 3).contiguous()
+
+
+@pytest.mark.parametrize("B,Cw,K,H,W,dil", [(1, 128, 40, 25, 36, 1), (2, 512, 512, 17, 37, 2),
+                                            (1, 256, 200, 9, 64, 1)])
+def test_conv_dgrad_split_dy_ring_kernel(B, Cw, K, H, W, dil):
+    """dy in the split-bf16 layout runs the data gradient on the LDS-DMA ring kernel (12-row
+    tiles, partial last tiles here): same result as from fp32 dy, vs float64 torch."""
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(Cw + K + dil + 1)
+    w = torch.randn((Cw, K, 3, 3), generator=g) * 0.05
+    dy = torch.randn((B, Cw, H, W), generator=g)
+    ref = torch.nn.grad.conv2d_input((B, K, H, W), w.double(), dy.double(), padding=dil, dilation=dil)
+    pk = ops.PackedDgrad3x3(K)
+    dys = _split_encode(dy).to(DEV)
+    torch.testing.assert_close(ops.split_decode(dys, Cw).cpu(), dy, rtol=2e-5, atol=0)  # hi + lo: 16 mantissa bits
+    got = ops.conv3x3_dgrad(dys, pk, w.to(DEV), dil)
+    assert_parity(got[:, :K].cpu(), ref, "dgrad (split dy)")
+    assert (got[:, K:] == 0).all()
+    f32 = ops.conv3x3_dgrad(dy.to(DEV), pk, w.to(DEV), dil)
+    assert_parity(got.cpu(), f32.cpu(), "split vs fp32 dy", normwise_tol=2e-5)
+
+
+def test_relu_backward_split():
+    """dy *= [y > 0] with y = hi + lo in the split layout, and the split copy of the result."""
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(11)
+    B, C, H, W = 2, 24, 7, 13
+    y = F.relu(torch.randn((B, C, H, W), generator=g))
+    y[0, 3, 2, 4] = 1e-30  # a tiny positive activation still passes its gradient
+    dy = torch.randn((B, C, H, W), generator=g)
+    ys = _split_encode(y).to(DEV)
+    out = torch.empty(ops.split_shape(B, C, H, W), dtype=torch.bfloat16, device=DEV)
+    got = ops.relu_backward_split_(dy.clone().to(DEV), ys, out).cpu()
+    want = torch.where(ops.split_decode(ys, C).cpu() > 0, dy, torch.zeros_like(dy))
+    assert torch.equal(got, want)
+    assert torch.equal(out.cpu(), _split_encode(want))  # the kernel splits with the same roundings
+
+
 def test_conv_dgrad_channel_map():
     from mvdet_amd import ops
     g = torch.Generator().manual_seed(3)
@@ -224,18 +269,21 @@ def test_conv_dgrad_channel_map():
             assert_parity(got[:, o], ref[:, c], f"dgrad channel {o}")
 
 
-@pytest.mark.parametrize("split", [False, True])
-def test_conv_dgrad_output_mask(split):
+@pytest.mark.parametrize("split,split_dy", [(False, False), (True, False), (True, True)])
+def test_conv_dgrad_output_mask(split, split_dy):
     """Output-side mask: tiles of a clear (tile, channel group) bit are skipped (left as they
-    were), every other tile equals the unmasked dgrad."""
+    were), every other tile equals the unmasked dgrad (split_dy: the ring kernel, 12-row tiles)."""
     from mvdet_amd import _native, ops
     g = torch.Generator().manual_seed(5)
     B, Cw, K, H, W = 2, 256, 512, 20, 70          # 4 output groups of 128 channels
     w = torch.randn((Cw, K, 3, 3), generator=g) * 0.05
-    dy = torch.randn((B, Cw, H, W), generator=g).to(DEV)
+    dy = torch.randn((B, Cw, H, W), generator=g)
+    dy = (_split_encode(dy) if split_dy else dy).to(DEV)
     pk = ops.PackedDgrad3x3(K)
     ref = ops.conv3x3_dgrad(dy, pk, w.to(DEV), 1)
-    ty, tx = -(-H // _native.TILE_H), -(-W // _native.TILE_W)
+    TH = ops.dgrad_tile_rows(split_dy, 1)
+    assert TH == (12 if split_dy else _native.TILE_H)
+    ty, tx = -(-H // TH), -(-W // _native.TILE_W)
     mask = torch.randint(0, 16, (ty * tx,), generator=g, dtype=torch.int32)
     if split:
         out = torch.zeros(ops.split_shape(B, K, H, W), dtype=torch.bfloat16, device=DEV)
@@ -247,10 +295,10 @@ def test_conv_dgrad_output_mask(split):
         got = got.cpu()
     ref = ref.cpu()
     for t in range(ty * tx):
-        r0, c0 = (t // tx) * _native.TILE_H, (t % tx) * _native.TILE_W
+        r0, c0 = (t // tx) * TH, (t % tx) * _native.TILE_W
         for gi in range(4):
-            blk = got[:, gi * 128:(gi + 1) * 128, r0:r0 + _native.TILE_H, c0:c0 + _native.TILE_W]
-            want = ref[:, gi * 128:(gi + 1) * 128, r0:r0 + _native.TILE_H, c0:c0 + _native.TILE_W]
+            blk = got[:, gi * 128:(gi + 1) * 128, r0:r0 + TH, c0:c0 + _native.TILE_W]
+            want = ref[:, gi * 128:(gi + 1) * 128, r0:r0 + TH, c0:c0 + _native.TILE_W]
             if (int(mask[t]) >> gi) & 1:
                 assert_parity(blk, want, f"dgrad tile {t} group {gi}", normwise_tol=2e-5 if split else 1e-6)
             else:
@@ -344,7 +392,7 @@ def test_project_fuse_backward_vs_cpu_autograd(precision, N, B, C, src, grid):
         assert eng.conv1_active_fraction(DEV, 0, ho) < 0.9
     out = project_fuse(eng, fg, mc)
     ws = out.grad_fn.ws                      # the activations the backward will use
-    m1, m2 = (ws.y1 > 0).float().cpu(), (ws.y2 > 0).float().cpu()
+    m1, m2 = (eng.y1_fp32(ws) > 0).float().cpu(), (ws.y2 > 0).float().cpu()
     out.backward(gmap.to(DEV))
     # reference, plain ReLU: forward parity, and the activation pattern differs only where the
     # pre-activation is within fp32 rounding of zero (a ReLU's gradient is discontinuous there)
@@ -389,7 +437,7 @@ def test_detector_training_step_matches_cpu_autograd():
     gmap = torch.from_numpy(rng.standard_normal(map_res.shape).astype(np.float32))
     gimg = [torch.from_numpy(rng.standard_normal(r.shape).astype(np.float32)) for r in imgs_res]
     ws = map_res.grad_fn.ws
-    masks = ((ws.y1 > 0).float().cpu(), (ws.y2 > 0).float().cpu())
+    masks = ((model.engine.y1_fp32(ws) > 0).float().cpu(), (ws.y2 > 0).float().cpu())
     loss = (map_res * gmap.to(DEV)).sum() + sum((r * gg.to(DEV)).sum() for r, gg in zip(imgs_res, gimg))
     loss.backward()
     # CPU reference: persp_trans_detector.py:61-87 with the backbone bypassed

@@ -384,6 +384,11 @@ int mvbev_relu_backward_split_f32(float* dy, const void* y_split, int64_t B, int
 int mvbev_conv3x3_cout1_backward_f32(const float* x, const float* w, const float* dmap, int64_t B,
                                      int64_t C, int64_t H, int64_t W, int dilation, int relu_mask,
                                      float* dx, float* dw, void* stream);
+/* Same, with dx_split (optional, C % 8 == 0, 16-B aligned): dx also in the split-bf16 layout
+ * ([B][C/8][H][W] pieces of bf16 hi[8], lo[8]), the input of the next data-gradient conv. */
+int mvbev_conv3x3_cout1_backward_ex(const float* x, const float* w, const float* dmap, int64_t B, int64_t C,
+                                    int64_t H, int64_t W, int dilation, int relu_mask, float* dx, void* dx_split,
+                                    float* dw, void* stream);
 
 /* ---- evaluation post-processing (trainer.py:97-106, 148-157) ---- */
 

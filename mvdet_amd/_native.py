@@ -56,6 +56,7 @@ EXPORTS = (
     "mvbev_cout1_reduce_partials",
     "mvbev_conv3x3_dgrad_bf16x3_ex",
     "mvbev_relu_backward_split_f32",
+    "mvbev_conv3x3_cout1_backward_ex",
 )
 WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
 
@@ -195,6 +196,9 @@ def _declare(lib):
     lib.mvbev_conv3x3_dgrad_bf16x3_ex.restype = ctypes.c_int
     lib.mvbev_conv3x3_dgrad_bf16x3_ex.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _i64, ctypes.c_int,
                                                   _p, ctypes.c_int, _p, _i64, _p]
+    lib.mvbev_conv3x3_cout1_backward_ex.restype = ctypes.c_int
+    lib.mvbev_conv3x3_cout1_backward_ex.argtypes = [_p, _p, _p, _i64, _i64, _i64, _i64, ctypes.c_int, ctypes.c_int,
+                                                    _p, _p, _p, _p]
     lib.mvbev_relu_backward_split_f32.restype = ctypes.c_int
     lib.mvbev_relu_backward_split_f32.argtypes = [_p, _p, _i64, _i64, _i64, _i64, _p, _p]
     lib.mvbev_cout1_reduce_partials.restype = ctypes.c_int

@@ -50,8 +50,16 @@ def _train_workspace(engine: ProjectFuse, B: int, device) -> Workspace:
     LDS-DMA wgrad kernel, and the ReLU mask is read from hi + lo), y2 kept in fp32 (conv3's
     backward reads it: no conv2 -> conv3 fusion)."""
     H, W = engine.grid_hw
-    if engine.split:  # the split warp writes every 8-channel group in full (zeros past C)
-        slab = torch.empty((engine.S,) + ops.split_shape(B, engine.Cs, H, W), dtype=torch.bfloat16, device=device)
+    slab, zeroed = None, False
+    if engine.split:
+        # Split slabs come from a per-engine pool: zero-filled once, written only by this engine's
+        # warps, whose skipped (out-of-source) pixels are the same every step (geometry-only), so
+        # a reused slab still holds exact zeros there and the warp may skip them
+        # (MVBEV_WARP_DST_ZEROED).  A slab returns to the pool when its backward has run.
+        pool = _slab_pool(engine, B, device)
+        slab = pool.pop() if pool else torch.zeros((engine.S,) + ops.split_shape(B, engine.Cs, H, W),
+                                                   dtype=torch.bfloat16, device=device)
+        zeroed = True
     else:
         slab = torch.empty((engine.S, B, engine.Cs, H, W), dtype=engine.slab_dtype, device=device)
         slab[:, :, engine.C:].zero_()  # padding channels the warp does not write
@@ -62,7 +70,12 @@ def _train_workspace(engine: ProjectFuse, B: int, device) -> Workspace:
         y1 = torch.empty((B, engine.mid, H, W), dtype=torch.float32, device=device)
     y2 = torch.empty((B, engine.mid, H, W), dtype=torch.float32, device=device)
     m = engine.m_norm_cpu.to(device)[:, None].expand(engine.num_cam, B, 3, 3).contiguous()
-    return Workspace(slab, y1, y2, m, (0, H), y1r, y2r, store_y2=True)
+    return Workspace(slab, y1, y2, m, (0, H), y1r, y2r, slab_zeroed=zeroed, store_y2=True)
+
+
+def _slab_pool(engine: ProjectFuse, B: int, device) -> list:
+    pools = engine.__dict__.setdefault("_train_slabs", {})
+    return pools.setdefault((str(torch.device(device)), int(B)), [])
 
 
 def _bwd_state(engine: ProjectFuse):
@@ -159,7 +172,9 @@ class ProjectFuseFunction(torch.autograd.Function):
         mid = engine.mid
         # conv3: dy2 = dgrad * relu'(y2); dw3
         _mark("bwd_conv3")
-        dy2, dw3 = ops.conv3x3_cout1_backward(ws.y2, w3, dmap, 4, relu_mask=True)
+        # with split y1 the data gradients run on the ring kernel: dy2 also in the split layout
+        dy2s = torch.empty(ops.split_shape(B, mid, H, W), dtype=torch.bfloat16, device=dev) if y1_split else None
+        dy2, dw3 = ops.conv3x3_cout1_backward(ws.y2, w3, dmap, 4, relu_mask=True, dx_split=dy2s)
         # conv2: db2, dw2, dy1 = dgrad * relu'(y1)
         _mark("bwd_conv2_wgrad")
         db2 = torch.empty(mid, dtype=torch.float32, device=dev) if b2 is not None else None
@@ -168,10 +183,10 @@ class ProjectFuseFunction(torch.autograd.Function):
         d_y1 = ops.conv_desc(B, mid, H, W, group=mid, group_stride=0, batch_stride=mid * H * W)
         dw2 = ops.conv3x3_wgrad(ws.y1, d_y1, dy2, 2, mid, workspace=_wgrad_ws(st, d_y1, mid, dev))
         _mark("bwd_conv2_dgrad")
-        dy1 = ops.conv3x3_dgrad(dy2, st.dgrad2, w2, 2)
+        dy1 = ops.conv3x3_dgrad(dy2 if dy2s is None else dy2s, st.dgrad2, w2, 2)
         if dy1.shape[1] != mid:
             dy1 = dy1[:, :mid].contiguous()
-        del dy2
+        del dy2, dy2s
         dy1s = None
         if y1_split:  # the masked dy1 also in the split layout: conv1's dgrad on the ring kernel
             dy1s = torch.empty(ops.split_shape(B, mid, H, W), dtype=torch.bfloat16, device=dev)
@@ -211,6 +226,8 @@ class ProjectFuseFunction(torch.autograd.Function):
             ops.warp_views_adjoint(douts, _adjoint_plans(engine, st, dev), gs)
             grads = [g if need[v] else None for v, g in enumerate(gs)]
         _mark("bwd_end")
+        if ws.slab_zeroed:  # kernels that read it are already enqueued: same-stream reuse is ordered
+            _slab_pool(engine, B, dev).append(ws.slab)
         ctx.ws = None
         return (None, *grads, dw1, db1, dw2, db2, dw3)
 

@@ -662,9 +662,11 @@ __global__ void relu_backward_split_kernel(float* __restrict__ dy, const u32x4_t
 // conv3 (Cout = 1, no bias) data gradient, times conv2's ReLU mask when relu_mask:
 // dx[b][c][y][x] = sum_t w[c][t] * dmap[b][y - (ky-1)d][x - (kx-1)d]
 constexpr int kCout1Cpb = 32;  // channels per block
+// dxs (optional, C % 8 == 0): dx also in the split-bf16 layout (the next dgrad conv's input)
 __global__ __launch_bounds__(256) void cout1_dgrad_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ dmap, int C, int H, int W,
-                                                          int dil, int relu_mask, float* __restrict__ dx) {
+                                                          int dil, int relu_mask, float* __restrict__ dx,
+                                                          u32x4_t* __restrict__ dxs) {
   const int HW = H * W;
   const int q = blockIdx.x * 256 + threadIdx.x;
   const int b = blockIdx.z;
@@ -678,6 +680,23 @@ __global__ __launch_bounds__(256) void cout1_dgrad_kernel(const float* __restric
     dm[t] = (yy >= 0 && yy < H && xc >= 0 && xc < W) ? d[yy * W + xc] : 0.f;
   }
   const int cbeg = blockIdx.y * kCout1Cpb, cend = min(C, cbeg + kCout1Cpb);
+  if (dxs) {  // groups of 8 channels (kCout1Cpb and C are multiples of 8)
+    for (int c0 = cbeg; c0 < cend; c0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        float s = 0.f;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) s += w[c * 9 + t] * dm[t];
+        const int64_t o = ((int64_t)b * C + c) * HW + q;
+        v[j] = (!relu_mask || x[o] > 0.f) ? s : 0.f;
+        dx[o] = v[j];
+      }
+      store_split8(dxs + 2 * (((int64_t)b * (C / 8) + c0 / 8) * HW + q), v);
+    }
+    return;
+  }
   for (int c = cbeg; c < cend; ++c) {
     float s = 0.f;
 #pragma unroll
@@ -1178,8 +1197,15 @@ int mvbev_relu_backward_split_f32(float* dy, const void* y_split, int64_t B, int
 int mvbev_conv3x3_cout1_backward_f32(const float* x, const float* w, const float* dmap, int64_t B, int64_t C,
                                      int64_t H, int64_t W, int dilation, int relu_mask, float* dx, float* dw,
                                      void* stream) {
+  return mvbev_conv3x3_cout1_backward_ex(x, w, dmap, B, C, H, W, dilation, relu_mask, dx, nullptr, dw, stream);
+}
+
+int mvbev_conv3x3_cout1_backward_ex(const float* x, const float* w, const float* dmap, int64_t B, int64_t C,
+                                    int64_t H, int64_t W, int dilation, int relu_mask, float* dx, void* dx_split,
+                                    float* dw, void* stream) {
   using namespace mvbev;
-  if (!x || !w || !dmap || (!dx && !dw)) return MVBEV_ERR_NULL;
+  if (!x || !w || !dmap || (!dx && !dw) || (dx_split && !dx)) return MVBEV_ERR_NULL;
+  if (dx_split && (C % 8 != 0 || (reinterpret_cast<uintptr_t>(dx_split) & 15) != 0)) return MVBEV_ERR_SHAPE;
   if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return MVBEV_ERR_RANK;
   if (H * W > INT32_MAX || B > 65535) return MVBEV_ERR_SHAPE;
   if (dilation < 1) return MVBEV_ERR_DILATION;
@@ -1187,7 +1213,7 @@ int mvbev_conv3x3_cout1_backward_f32(const float* x, const float* w, const float
   if (dx) {
     const dim3 grid((unsigned)ceil_div(H * W, 256), (unsigned)ceil_div(C, bwd::kCout1Cpb), (unsigned)B);
     hipLaunchKernelGGL(bwd::cout1_dgrad_kernel, grid, dim3(256), 0, s, x, w, dmap, (int)C, (int)H, (int)W,
-                       dilation, relu_mask, dx);
+                       dilation, relu_mask, dx, static_cast<u32x4_t*>(dx_split));
     MVBEV_CHECK_LAUNCH();
   }
   if (dw) {

@@ -813,10 +813,12 @@ def relu_backward_split_(dy: torch.Tensor, y_split: torch.Tensor, dy_split: Opti
 
 
 def conv3x3_cout1_backward(x: torch.Tensor, weight: torch.Tensor, dmap: torch.Tensor, dilation: int,
-                           relu_mask: bool = False, need_dx: bool = True, need_dw: bool = True):
+                           relu_mask: bool = False, need_dx: bool = True, need_dw: bool = True,
+                           dx_split: Optional[torch.Tensor] = None):
     """Backward of ``conv3x3_cout1`` over a whole image: returns (dx [B,C,H,W] or None,
     dw [1,C,3,3] or None).  ``relu_mask``: zero dx where x <= 0 (x = the previous ReLU's output,
-    its backward fused)."""
+    its backward fused).  ``dx_split`` (optional, bf16 ``split_shape(B,C,H,W)``) also receives
+    dx in the split-bf16 layout (the next data-gradient conv's input)."""
     _require_cuda(x, weight, dmap)
     if x.dim() != 4 or x.dtype != torch.float32 or not x.is_contiguous():
         raise ValueError("x must be a contiguous float32 [B,C,H,W] tensor")
@@ -831,8 +833,12 @@ def conv3x3_cout1_backward(x: torch.Tensor, weight: torch.Tensor, dmap: torch.Te
     dw = torch.empty((1, C, 3, 3), dtype=torch.float32, device=x.device) if need_dw else None
     if dx is None and dw is None:
         return None, None
-    st = _native.load().mvbev_conv3x3_cout1_backward_f32(
+    if dx_split is not None and (dx is None or dx_split.dtype != torch.bfloat16 or not dx_split.is_contiguous()
+                                 or tuple(dx_split.shape) != split_shape(B, C, H, W)):
+        raise ValueError(f"dx_split must be a contiguous bf16 {split_shape(B, C, H, W)} tensor (with dx)")
+    st = _native.load().mvbev_conv3x3_cout1_backward_ex(
         x.data_ptr(), w.data_ptr(), dmap.data_ptr(), B, C, H, W, int(dilation), int(bool(relu_mask)),
-        None if dx is None else dx.data_ptr(), None if dw is None else dw.data_ptr(), _stream(x))
-    _native.check(st, "mvbev_conv3x3_cout1_backward_f32")
+        None if dx is None else dx.data_ptr(), None if dx_split is None else dx_split.data_ptr(),
+        None if dw is None else dw.data_ptr(), _stream(x))
+    _native.check(st, "mvbev_conv3x3_cout1_backward_ex")
     return dx, dw

@@ -489,3 +489,33 @@ def test_project_fuse_second_backward_raises():
     (g,) = torch.autograd.grad(out2.sum(), fg[0], create_graph=True)
     with pytest.raises(RuntimeError):
         g.sum().backward()
+
+
+def test_training_steps_reuse_the_zeroed_slab():
+    """Training forwards draw the split slab from the engine's pool (zero-filled once; the warp
+    skips the out-of-source pixels, which stay exactly zero): two identical steps give
+    identical outputs and gradients, and the second step reuses the first step's slab."""
+    from mvdet_amd import ProjectFuse, autograd, synthetic
+    from mvdet_amd.geometry import projection_matrices
+    ds = synthetic.wildtrack_like(2, 4, seed=5, img_shape=(108, 192), worldgrid_shape=(96, 288))
+    C = 32
+    up = ds.upsample_shape
+    feats = [synthetic.synthetic_features(1, C, [u // 3 for u in up], up, seed=40 + v, device=DEV) for v in range(2)]
+    eng = ProjectFuse(projection_matrices(ds), tuple(up), tuple(ds.reducedgrid_shape), C)
+    torch.manual_seed(0)
+    mc = torch.nn.Sequential(torch.nn.Conv2d(C * 2 + 2, 512, 3, padding=1), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False)).to(DEV)
+    results, slabs = [], []
+    for _ in range(2):
+        fg = [f.clone().requires_grad_() for f in feats]
+        mc.zero_grad()
+        out = autograd.project_fuse(eng, fg, mc)
+        slabs.append(out.grad_fn.ws.slab.data_ptr())
+        assert out.grad_fn.ws.slab_zeroed
+        out.backward(torch.ones_like(out))
+        results.append([out.detach().clone()] + [f.grad.clone() for f in fg] +
+                       [p.grad.clone() for p in mc.parameters()])
+    assert slabs[0] == slabs[1]
+    for a, b in zip(*results):
+        assert torch.equal(a, b)

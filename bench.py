@@ -396,6 +396,32 @@ def run_train_step(config: int, precision: str, steps: int, warmup: int, with_to
 
         res["torch_gpu"] = run(torch_step, max(2, steps // 4), 1)
         res["speedup_vs_torch_gpu"] = round(res["native"]["value"] / res["torch_gpu"]["value"], 2)
+    # "+a4": the step the drop-in module trains through (trainer.py:38-47 calling
+    # persp_trans_detector.py:65-87): from the backbone-resolution maps, the 3x upsample included
+    # (native: fused into the warp and its adjoint into the warp adjoint)
+    bfeats = [synthetic.backbone_features(B, C, [u // 3 for u in up], seed=v, device=dev).requires_grad_()
+              for v in range(N)]
+
+    def native_a4():
+        for f in bfeats:
+            f.grad = None
+        mc.zero_grad(set_to_none=True)
+        autograd.project_fuse_backbone(eng, bfeats, mc).backward(gmap)
+
+    a4 = {"native": run(native_a4, steps, warmup, hook_stages=True)}
+    if with_torch:
+        def torch_a4():
+            for f in bfeats:
+                f.grad = None
+            mc.zero_grad(set_to_none=True)
+            world = [torch_warp(torch.nn.functional.interpolate(f, up, mode="bilinear"), m, ho, wo)
+                     for f, m in zip(bfeats, ms)]
+            mc(torch.cat(world + [cmap.repeat(B, 1, 1, 1)], 1)).backward(gmap)
+
+        a4["torch_gpu"] = run(torch_a4, max(2, steps // 4), 1)
+        a4["speedup_vs_torch_gpu"] = round(a4["native"]["value"] / a4["torch_gpu"]["value"], 2)
+    a4["note"] = "from backbone-resolution maps (a4 upsample :65 included) as the drop-in module trains"
+    res["plus_a4"] = a4
     return res
 
 

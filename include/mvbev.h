@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -289,6 +289,15 @@ int mvbev_warp_views_backward_f32(const mvbev_warp_view* views, int nviews, int6
  * fp32[4*Ho*Wo] (capacity; row_ptr[H*W] = entries used), scratch int32[H*W]. */
 int mvbev_warp_adjoint_plan(const float* m, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int32_t* row_ptr,
                             int32_t* col, float* val, int32_t* scratch, void* stream);
+/* The same plan for the fused 3x-upsample + warp of mvbev_warp_views_upsampled (the backbone
+ * map h x w upsampled to H x W, persp_trans_detector.py:65, then warped, :69): source pixels are
+ * the h x w backbone pixels, <= 9 entries per output pixel (the sample's 3x3 backbone window,
+ * weight = upsample weight x warp weight, zero-weight cells omitted).  Buffers: row_ptr
+ * int32[h*w + 1], col int32[9*Ho*Wo], val fp32[9*Ho*Wo], scratch int32[h*w].  With it,
+ * mvbev_warp_views_adjoint (H, W = h, w) takes the gradient straight to the backbone features. */
+int mvbev_warp_upsampled_adjoint_plan(const float* m, int64_t h, int64_t w, int64_t H, int64_t W, int64_t Ho,
+                                      int64_t Wo, int32_t* row_ptr, int32_t* col, float* val, int32_t* scratch,
+                                      void* stream);
 
 typedef struct mvbev_warp_adjoint_view {
   const float* grad_out;       /* [B][C][Ho][Wo] fp32, element strides (row / column dense) */

@@ -57,6 +57,7 @@ EXPORTS = (
     "mvbev_conv3x3_dgrad_bf16x3_ex",
     "mvbev_relu_backward_split_f32",
     "mvbev_conv3x3_cout1_backward_ex",
+    "mvbev_warp_upsampled_adjoint_plan",
 )
 WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
 
@@ -174,6 +175,9 @@ def _declare(lib):
     lib.mvbev_warp_adjoint_plan.restype = ctypes.c_int
     lib.mvbev_warp_adjoint_plan.argtypes = [ctypes.POINTER(ctypes.c_float), _i64, _i64, _i64, _i64, _p, _p, _p, _p,
                                             _p]
+    lib.mvbev_warp_upsampled_adjoint_plan.restype = ctypes.c_int
+    lib.mvbev_warp_upsampled_adjoint_plan.argtypes = [ctypes.POINTER(ctypes.c_float), _i64, _i64, _i64, _i64, _i64,
+                                                      _i64, _p, _p, _p, _p, _p]
     lib.mvbev_warp_views_adjoint.restype = ctypes.c_int
     lib.mvbev_warp_views_adjoint.argtypes = [ctypes.POINTER(WarpAdjointView), ctypes.c_int, ctypes.c_int, _i64,
                                              _i64, _i64, _i64, _i64, _i64, ctypes.c_int, _p]

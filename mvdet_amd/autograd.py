@@ -87,14 +87,16 @@ def _bwd_state(engine: ProjectFuse):
     return st
 
 
-def _adjoint_plans(engine: ProjectFuse, st, device):
-    key = str(device)
-    plans = st.plans.get(key) if hasattr(st, "plans") else None
+def _adjoint_plans(engine: ProjectFuse, st, device, backbone_hw=None):
+    """Per view: the CSR transpose of the warp (or, with ``backbone_hw``, of the fused
+    3x-upsample + warp from that backbone size); geometry only, built once per device."""
+    key = (str(device), None if backbone_hw is None else tuple(backbone_hw))
+    if not hasattr(st, "plans"):
+        st.plans = {}
+    plans = st.plans.get(key)
     if plans is None:
-        if not hasattr(st, "plans"):
-            st.plans = {}
-        plans = [ops.WarpAdjointPlan(engine.m_norm_cpu[v], engine.src_hw, engine.grid_hw, device)
-                 for v in range(engine.num_cam)]
+        plans = [ops.WarpAdjointPlan(engine.m_norm_cpu[v], engine.src_hw, engine.grid_hw, device,
+                                     backbone_hw=backbone_hw) for v in range(engine.num_cam)]
         st.plans[key] = plans
     return plans
 
@@ -127,11 +129,15 @@ def _wgrad_ws(st, desc, cout, device) -> torch.Tensor:
 
 
 class ProjectFuseFunction(torch.autograd.Function):
-    """``map = fuse(concat(warp(feats[v]) for v) + coord)``; inputs after the engine: the N
-    upsampled view features [B,C,H,W] then conv1.w, conv1.b, conv2.w, conv2.b, conv3.w."""
+    """``map = fuse(concat(warp(feats[v]) for v) + coord)``; inputs after the engine and the
+    ``backbone`` flag: the N view features, then conv1.w, conv1.b, conv2.w, conv2.b, conv3.w.
+    ``backbone`` False: the features are the upsampled [B,C,H,W] maps kornia receives
+    (``persp_trans_detector.py:65`` done by the caller); True: the backbone-resolution [B,C,h,w]
+    maps, upsampled inside the warp (``warp_views_upsampled``) and differentiated through the
+    fused upsample + warp adjoint, so neither the upsampled maps nor their gradient exist."""
 
     @staticmethod
-    def forward(ctx, engine: ProjectFuse, *args):
+    def forward(ctx, engine: ProjectFuse, backbone: bool, *args):
         n = engine.num_cam
         feats, (w1, b1, w2, b2, w3) = args[:n], args[n:]
         if engine.slab_dtype != torch.float32 or engine.S != n:
@@ -140,7 +146,11 @@ class ProjectFuseFunction(torch.autograd.Function):
         dev = feats[0].device
         ws = _train_workspace(engine, B, dev)
         _mark("warp")
-        engine.warp_views(ws, list(range(n)), [f.detach() for f in feats])
+        if backbone:
+            engine.warp_views_upsampled(ws, list(range(n)), [f.detach() for f in feats])
+        else:
+            engine.warp_views(ws, list(range(n)), [f.detach() for f in feats])
+        ctx.backbone = bool(backbone)
         mc = [SimpleNamespace(weight=w1, bias=b1), None, SimpleNamespace(weight=w2, bias=b2), None,
               SimpleNamespace(weight=w3, bias=None)]
         out = engine.fuse(ws, mc, mark=_stage_hook)
@@ -161,7 +171,7 @@ class ProjectFuseFunction(torch.autograd.Function):
                                "kernels keep no retain_graph copy). Run the forward again.")
         w1, b1, w2, b2, w3 = ctx.saved_tensors
         n = engine.num_cam
-        need = ctx.needs_input_grad[1:]
+        need = ctx.needs_input_grad[2:]
         need_feat = any(need[:n])
         st = _bwd_state(engine)
         H, W = engine.grid_hw
@@ -223,17 +233,26 @@ class ProjectFuseFunction(torch.autograd.Function):
                 douts = [dslab[:, v * C:(v + 1) * C] for v in range(n)]
             _mark("bwd_warp")
             gs = [torch.empty(ctx.feat_shape, dtype=torch.float32, device=dev) for _ in range(n)]
-            ops.warp_views_adjoint(douts, _adjoint_plans(engine, st, dev), gs)
+            plans = _adjoint_plans(engine, st, dev, backbone_hw=ctx.feat_shape[2:] if ctx.backbone else None)
+            ops.warp_views_adjoint(douts, plans, gs)
             grads = [g if need[v] else None for v, g in enumerate(gs)]
         _mark("bwd_end")
         if ws.slab_zeroed:  # kernels that read it are already enqueued: same-stream reuse is ordered
             _slab_pool(engine, B, dev).append(ws.slab)
         ctx.ws = None
-        return (None, *grads, dw1, db1, dw2, db2, dw3)
+        return (None, None, *grads, dw1, db1, dw2, db2, dw3)
 
 
 def project_fuse(engine: ProjectFuse, feats: Sequence[torch.Tensor], map_classifier) -> torch.Tensor:
     """Differentiable project+fuse: ``feats[v]`` the upsampled [B,C,H,W] features of view v,
     ``map_classifier`` the reference's ``nn.Sequential`` (``persp_trans_detector.py:51-54``)."""
     c1, c2, c3 = map_classifier[0], map_classifier[2], map_classifier[4]
-    return ProjectFuseFunction.apply(engine, *feats, c1.weight, c1.bias, c2.weight, c2.bias, c3.weight)
+    return ProjectFuseFunction.apply(engine, False, *feats, c1.weight, c1.bias, c2.weight, c2.bias, c3.weight)
+
+
+def project_fuse_backbone(engine: ProjectFuse, feats: Sequence[torch.Tensor], map_classifier) -> torch.Tensor:
+    """Differentiable upsample + project + fuse (``persp_trans_detector.py:65-87`` after the
+    backbone): ``feats[v]`` view v's backbone-resolution [B,C,h,w] map; the 3x bilinear
+    upsample runs inside the warp and its adjoint inside the warp's."""
+    c1, c2, c3 = map_classifier[0], map_classifier[2], map_classifier[4]
+    return ProjectFuseFunction.apply(engine, True, *feats, c1.weight, c1.bias, c2.weight, c2.bias, c3.weight)

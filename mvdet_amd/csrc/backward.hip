@@ -892,6 +892,40 @@ __global__ __launch_bounds__(256) void adj_fill_kernel(const PlanArgs a, int32_t
     }
 }
 
+// The same plan for the fused upsample + warp (warp_up_kernel): S_up = S * U (Ho*Wo x h*w, U the
+// 3x bilinear upsample of persp_trans_detector.py:65), <= 9 entries per output pixel: the
+// sample's 3x3 backbone window with weights ay[i] * ax[j] (up_window, the forward's own
+// code); zero-weight window cells carry no entry.  Its adjoint takes the gradient straight to
+// the backbone-resolution features, without the upsampled gradient in HBM.
+struct UpPlanArgs {
+  float m[9];
+  int H, W, Ho, Wo, h, w;
+  float sy, sx;
+};
+template <bool FILL>
+__global__ __launch_bounds__(256) void adj_up_kernel(const UpPlanArgs a, int32_t* __restrict__ counts,
+                                                     int32_t* __restrict__ col, float* __restrict__ val) {
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  if (o >= a.Ho * a.Wo) return;
+  const UpWindow uw = up_window(a.m, o % a.Wo, o / a.Wo, a.Ho, a.Wo, a.H, a.W, a.h, a.w, a.sy, a.sx);
+  if (!uw.inside) return;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const float wt = uw.ay[i] * uw.ax[j];
+      if (wt == 0.f || uw.rb + i > a.h - 1 || uw.cb + j > a.w - 1) continue;
+      const int p = (uw.rb + i) * a.w + uw.cb + j;
+      if constexpr (FILL) {
+        const int pos = atomicAdd(counts + p, 1);  // counts = the scan's cursor here
+        col[pos] = o;
+        val[pos] = wt;
+      } else {
+        atomicAdd(counts + p, 1);
+      }
+    }
+}
+
 __global__ __launch_bounds__(256) void adj_sort_kernel(const int32_t* __restrict__ row_ptr, int n,
                                                        int32_t* __restrict__ col, float* __restrict__ val) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -1034,7 +1068,22 @@ __global__ __launch_bounds__(256) void warp_adjoint_split_kernel(const AdjArgs a
 #pragma unroll
     for (int j = 0; j < kAdjReg; ++j)
       if (j < ne) add(cl[j], wt[j]);
-    for (int e = e0 + kAdjReg; e < e1; ++e) add(vw.col[e], vw.val[e]);
+    // further entries (the fused upsample + warp plan has ~2x the warp's) in batches of 8:
+    // the batch's (col, val) loads first, then 8 independent gathers, instead of one
+    // dependent (col -> gather) round trip per entry
+    for (int eb = e0 + kAdjReg; eb < e1; eb += 8) {
+      int cb[8];
+      float wb[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool ok = eb + j < e1;
+        cb[j] = ok ? vw.col[eb + j] : 0;
+        wb[j] = ok ? vw.val[eb + j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (eb + j < e1) add(cb[j], wb[j]);
+    }
     const int nq = min(8, c1 - c);
 #pragma unroll
     for (int q = 0; q < 8; ++q)
@@ -1273,6 +1322,33 @@ int mvbev_warp_adjoint_plan(const float* m, int64_t H, int64_t W, int64_t Ho, in
   hipLaunchKernelGGL(bwd::adj_scan_kernel, dim3(1), dim3(1024), 0, s, scratch, n, row_ptr, scratch);
   MVBEV_CHECK_LAUNCH();
   hipLaunchKernelGGL(bwd::adj_fill_kernel, dim3(ob), dim3(256), 0, s, a, scratch, col, val);
+  MVBEV_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bwd::adj_sort_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, row_ptr, n, col, val);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+int mvbev_warp_upsampled_adjoint_plan(const float* m, int64_t h, int64_t w, int64_t H, int64_t W, int64_t Ho,
+                                      int64_t Wo, int32_t* row_ptr, int32_t* col, float* val, int32_t* scratch,
+                                      void* stream) {
+  using namespace mvbev;
+  if (!m || !row_ptr || !col || !val || !scratch) return MVBEV_ERR_NULL;
+  if (h <= 0 || w <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0) return MVBEV_ERR_RANK;
+  if (H < h || W < w || H >= INT32_MAX / 2 || W >= INT32_MAX / 2 || 9 * Ho * Wo >= INT32_MAX) return MVBEV_ERR_SHAPE;
+  bwd::UpPlanArgs a;
+  for (int i = 0; i < 9; ++i) a.m[i] = m[i];
+  a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo; a.h = (int)h; a.w = (int)w;
+  a.sy = (float)h / (float)H;  // area_pixel_compute_scale(align_corners=false), as warp_up_kernel
+  a.sx = (float)w / (float)W;
+  hipStream_t s = as_stream(stream);
+  const int n = (int)(h * w);
+  if (hipMemsetAsync(scratch, 0, sizeof(int32_t) * n, s) != hipSuccess) return MVBEV_ERR_HIP;
+  const unsigned ob = (unsigned)ceil_div(Ho * Wo, 256);
+  hipLaunchKernelGGL(bwd::adj_up_kernel<false>, dim3(ob), dim3(256), 0, s, a, scratch, col, val);
+  MVBEV_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bwd::adj_scan_kernel, dim3(1), dim3(1024), 0, s, scratch, n, row_ptr, scratch);
+  MVBEV_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bwd::adj_up_kernel<true>, dim3(ob), dim3(256), 0, s, a, scratch, col, val);
   MVBEV_CHECK_LAUNCH();
   hipLaunchKernelGGL(bwd::adj_sort_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, row_ptr, n, col, val);
   MVBEV_CHECK_LAUNCH();

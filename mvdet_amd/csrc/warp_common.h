@@ -110,4 +110,69 @@ __device__ inline WarpCoord warp_coord(const float (&m)[9], int u, int v, int Ho
   return c;
 }
 
+// The fused 3x-upsample + warp sample of output pixel (u, v) as one 3x3 window of the
+// backbone-resolution map (warp_up_kernel, and the plan of its adjoint): the warp's corners in
+// the upsampled H x W grid (warp_coord), each corner's PyTorch bilinear upsample taps
+// (align_corners=False: s = max(0, (i + 0.5) * scale - 0.5), i0 = floor(s), i1 = min(i0 + 1,
+// n - 1)), summed per axis into 3 window weights (the 2-D corner weights factor, so the 3x3
+// weights are the outer product ay[i] * ax[j] at backbone pixel (rb + i, cb + j); a window
+// row / column past the map carries weight 0).
+struct UpWindow {
+  int rb, cb;
+  float ay[3], ax[3];
+  bool finite, inside;
+};
+__device__ inline UpWindow up_window(const float (&m)[9], int u, int v, int Ho, int Wo, int H, int W, int h, int w,
+                                     float sy, float sx) {
+  UpWindow r;
+  const WarpCoord wc = warp_coord(m, u, v, Ho, Wo, H, W);
+  const float ix = wc.ix, iy = wc.iy;
+  r.finite = wc.finite;
+  r.inside = wc.inside;
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  const int x0 = r.inside ? (int)fx0 : 0, y0 = r.inside ? (int)fy0 : 0;
+  const float wx[2] = {fx0 + 1.f - ix, ix - fx0};  // warp weights of columns x0, x0+1
+  const float wy[2] = {fy0 + 1.f - iy, iy - fy0};  // ... of rows y0, y0+1
+  int cxi[2][2], cyi[2][2];
+  float lxv[2][2], lyv[2][2];
+  bool okx[2], oky[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int ux = x0 + k, uy = y0 + k;
+    okx[k] = r.inside && ux >= 0 && ux <= W - 1;
+    oky[k] = r.inside && uy >= 0 && uy <= H - 1;
+    float s = sx * ((float)ux + 0.5f) - 0.5f;
+    s = s < 0.f ? 0.f : s;
+    int i0 = (int)s;
+    i0 = min(i0, w - 1);
+    cxi[k][0] = i0;
+    cxi[k][1] = i0 + (i0 < w - 1 ? 1 : 0);
+    lxv[k][1] = s - (float)i0;
+    lxv[k][0] = 1.f - lxv[k][1];
+    s = sy * ((float)uy + 0.5f) - 0.5f;
+    s = s < 0.f ? 0.f : s;
+    i0 = (int)s;
+    i0 = min(i0, h - 1);
+    cyi[k][0] = i0;
+    cyi[k][1] = i0 + (i0 < h - 1 ? 1 : 0);
+    lyv[k][1] = s - (float)i0;
+    lyv[k][0] = 1.f - lyv[k][1];
+  }
+  r.cb = okx[0] ? cxi[0][0] : cxi[1][0];
+  r.rb = oky[0] ? cyi[0][0] : cyi[1][0];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) r.ax[j] = 0.f, r.ay[j] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        r.ax[j] += (okx[k] && cxi[k][t] - r.cb == j) ? wx[k] * lxv[k][t] : 0.f;
+        r.ay[j] += (oky[k] && cyi[k][t] - r.rb == j) ? wy[k] * lyv[k][t] : 0.f;
+      }
+    }
+  return r;
+}
+
 }  // namespace mvbev

@@ -51,58 +51,14 @@ __global__ __launch_bounds__(256) void warp_up_kernel(const UpArgs ua) {
   float m[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) m[i] = vw.m[i];
-  // warp corners in the upsampled grid: the same warp_coord as warp_tile_kernel
-  const WarpCoord wc = warp_coord(m, u, v, a.Ho, a.Wo, H, W);
-  const float ix = wc.ix, iy = wc.iy;
-  const bool finite = wc.finite, inside = wc.inside;
+  // the sample's 3x3 backbone window (warp corners in the upsampled grid by the same
+  // warp_coord as warp_tile_kernel, each corner's upsample taps folded per axis)
+  const UpWindow uw = up_window(m, u, v, a.Ho, a.Wo, H, W, h, w, ua.sy, ua.sx);
+  const bool finite = uw.finite, inside = uw.inside;
   const float fill = finite ? 0.f : __builtin_nanf("");
-  const float fx0 = floorf(ix), fy0 = floorf(iy);
-  const int x0 = inside ? (int)fx0 : 0, y0 = inside ? (int)fy0 : 0;
-  const float wx[2] = {fx0 + 1.f - ix, ix - fx0};  // warp weights of columns x0, x0+1
-  const float wy[2] = {fy0 + 1.f - iy, iy - fy0};  // ... of rows y0, y0+1
-
-  // upsample taps of the two corner columns / rows; window base = first valid corner's tap
-  int cxi[2][2], cyi[2][2];
-  float lxv[2][2], lyv[2][2];
-  bool okx[2], oky[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int ux = x0 + k, uy = y0 + k;
-    okx[k] = inside && ux >= 0 && ux <= W - 1;
-    oky[k] = inside && uy >= 0 && uy <= H - 1;
-    float s = ua.sx * ((float)ux + 0.5f) - 0.5f;
-    s = s < 0.f ? 0.f : s;
-    int i0 = (int)s;
-    i0 = min(i0, w - 1);
-    cxi[k][0] = i0;
-    cxi[k][1] = i0 + (i0 < w - 1 ? 1 : 0);
-    lxv[k][1] = s - (float)i0;
-    lxv[k][0] = 1.f - lxv[k][1];
-    s = ua.sy * ((float)uy + 0.5f) - 0.5f;
-    s = s < 0.f ? 0.f : s;
-    i0 = (int)s;
-    i0 = min(i0, h - 1);
-    cyi[k][0] = i0;
-    cyi[k][1] = i0 + (i0 < h - 1 ? 1 : 0);
-    lyv[k][1] = s - (float)i0;
-    lyv[k][0] = 1.f - lyv[k][1];
-  }
-  const int cb = okx[0] ? cxi[0][0] : cxi[1][0];
-  const int rb = oky[0] ? cyi[0][0] : cyi[1][0];
-  // per-axis window weights: column j of the window gets sum over valid corner columns k
-  // and their taps t landing on it of wx[k] * lx[k][t]; rows likewise.  The 2-D corner
-  // weights factor (w_nw = wx0*wy0 ...), so the 3x3 weights are outer products.
-  float ax[3] = {0.f, 0.f, 0.f}, ay[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-  for (int k = 0; k < 2; ++k)
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        ax[j] += (okx[k] && cxi[k][t] - cb == j) ? wx[k] * lxv[k][t] : 0.f;
-        ay[j] += (oky[k] && cyi[k][t] - rb == j) ? wy[k] * lyv[k][t] : 0.f;
-      }
-    }
+  const int cb = uw.cb, rb = uw.rb;
+  const float(&ax)[3] = uw.ax;
+  const float(&ay)[3] = uw.ay;
   // one 16-B load per window row: shift the window left to fit 4 columns inside the row
   // (the shifted-in column gets weight 0); rows are clamped (their weights are 0 past h-1)
   const bool wide = QUAD && w >= 4;

@@ -20,9 +20,10 @@ HIP kernels of ``libmvbev.so`` through ``ProjectFuse``:
 * the same-size final interpolate (an exact identity) is elided.
 
 Training (autograd through the hot path, ``trainer.py:38-49``):
-when grad is required the upsample stays a torch op (its autograd), and warp + concat +
-fusion run as ``autograd.ProjectFuseFunction`` — HIP forward, HIP backward (warp adjoint,
-conv data/weight/bias gradients).  There is no stock-torch fallback for the hot path.
+when grad is required upsample + warp + concat + fusion run as
+``autograd.ProjectFuseFunction`` from the backbone-resolution maps — HIP forward (the fused
+upsample + warp), HIP backward (the fused upsample + warp adjoint, conv data/weight/bias
+gradients).  There is no stock-torch fallback for the hot path.
 The library is loaded at construction on a GPU, so a missing build fails there.
 """
 from __future__ import annotations
@@ -74,7 +75,7 @@ class PerspTransDetector(nn.Module):
             raise RuntimeError("PerspTransDetector.forward needs a ROCm GPU (the hot path has no CPU fallback)")
         training = self._needs_autograd()
         ws = None if training else self.engine.workspace(B, dev)
-        world_features, imgs_result, low = [], [], []
+        imgs_result, low = [], []
         for cam in range(self.num_cam):
             feat = self.base_pt1(imgs[:, cam].to(dev))
             feat = self.base_pt2(feat)
@@ -82,15 +83,14 @@ class PerspTransDetector(nn.Module):
             # bilinear upsample: per-pixel affine, weights summing to 1) on 64 instead of 512
             # channels
             imgs_result.append(self._img_head_lowres(feat))
-            if training:  # :65 as a torch op (its autograd); warp + fusion below are native
-                world_features.append(F.interpolate(feat, self.upsample_shape, mode="bilinear"))
-            else:  # the 3x upsample (:65) happens inside the fused warp below
-                low.append(feat.contiguous())
+            # the 3x upsample (:65) happens inside the fused warp below (and, training, its
+            # adjoint inside the warp adjoint)
+            low.append(feat.contiguous())
             if visualize:
-                up = world_features[-1] if training else F.interpolate(feat, self.upsample_shape, mode="bilinear")
+                up = F.interpolate(feat, self.upsample_shape, mode="bilinear")
                 self._show(torch.norm(up[0].detach(), dim=0))
-        if training:  # a5-a9 forward and backward on the HIP kernels (autograd.py)
-            map_result = native_autograd.project_fuse(self.engine, world_features, self.map_classifier)
+        if training:  # a4-a9 forward and backward on the HIP kernels (autograd.py)
+            map_result = native_autograd.project_fuse_backbone(self.engine, low, self.map_classifier)
         else:
             self.engine.warp_views_upsampled(ws, list(range(self.num_cam)), low)  # a4 + a5 + a6
             map_result = self.engine.fuse(ws, self.map_classifier)

@@ -534,19 +534,33 @@ class WarpAdjointPlan:
     """CSR transpose of one view's bilinear sampling matrix (``mvbev_warp_adjoint_plan``):
     geometry only, built once per (matrix, sizes, device) on the GPU."""
 
-    def __init__(self, m_norm, src_hw, grid_hw, device):
+    def __init__(self, m_norm, src_hw, grid_hw, device, backbone_hw=None):
+        """``backbone_hw`` (h, w): the plan of the fused 3x-upsample + warp
+        (``warp_views_upsampled_into``) from the h x w map upsampled to ``src_hw``; its
+        ``src_hw`` is then (h, w), the pixels the adjoint writes."""
         H, W = int(src_hw[0]), int(src_hw[1])
         Ho, Wo = int(grid_hw[0]), int(grid_hw[1])
         device = torch.device(device)
-        self.src_hw, self.grid_hw = (H, W), (Ho, Wo)
-        self.row_ptr = torch.empty(H * W + 1, dtype=torch.int32, device=device)
-        self.col = torch.empty(4 * Ho * Wo, dtype=torch.int32, device=device)
-        self.val = torch.empty(4 * Ho * Wo, dtype=torch.float32, device=device)
-        scratch = torch.empty(H * W, dtype=torch.int32, device=device)
         mm = (ctypes.c_float * 9)(*torch.as_tensor(m_norm, dtype=torch.float32).reshape(9).tolist())
-        st = _native.load().mvbev_warp_adjoint_plan(mm, H, W, Ho, Wo, self.row_ptr.data_ptr(), self.col.data_ptr(),
-                                                    self.val.data_ptr(), scratch.data_ptr(), _stream(self.row_ptr))
-        _native.check(st, "mvbev_warp_adjoint_plan")
+        lib = _native.load()
+        if backbone_hw is None:
+            self.src_hw, self.grid_hw, per = (H, W), (Ho, Wo), 4
+        else:
+            h, w = int(backbone_hw[0]), int(backbone_hw[1])
+            self.src_hw, self.grid_hw, per = (h, w), (Ho, Wo), 9
+        P = self.src_hw[0] * self.src_hw[1]
+        self.row_ptr = torch.empty(P + 1, dtype=torch.int32, device=device)
+        self.col = torch.empty(per * Ho * Wo, dtype=torch.int32, device=device)
+        self.val = torch.empty(per * Ho * Wo, dtype=torch.float32, device=device)
+        scratch = torch.empty(P, dtype=torch.int32, device=device)
+        if backbone_hw is None:
+            st = lib.mvbev_warp_adjoint_plan(mm, H, W, Ho, Wo, self.row_ptr.data_ptr(), self.col.data_ptr(),
+                                             self.val.data_ptr(), scratch.data_ptr(), _stream(self.row_ptr))
+        else:
+            st = lib.mvbev_warp_upsampled_adjoint_plan(mm, h, w, H, W, Ho, Wo, self.row_ptr.data_ptr(),
+                                                       self.col.data_ptr(), self.val.data_ptr(), scratch.data_ptr(),
+                                                       _stream(self.row_ptr))
+        _native.check(st, "warp adjoint plan")
         self._scratch = scratch  # freed with the plan (kept until the stream has used it)
 
     @property

@@ -64,6 +64,51 @@ def test_warp_backward_vs_grid_sample_autograd(B, C, H, W, ho, wo):
         assert (bufs[i][:, 0] == 0.5).all() and (bufs[i][:, C + 1] == 0.5).all()
 
 
+@pytest.mark.parametrize("B,C,h,w,H,W,ho,wo", [(1, 8, 9, 16, 27, 48, 12, 36), (2, 16, 10, 14, 27, 48, 17, 23),
+                                               (1, 24, 30, 53, 90, 160, 120, 360)])
+def test_upsampled_warp_adjoint_vs_autograd(B, C, h, w, H, W, ho, wo):
+    """The fused 3x-upsample + warp adjoint (plan of S * U, <= 9 entries per output pixel):
+    the gradient w.r.t. the backbone-resolution map equals torch-CPU autograd through
+    F.interpolate (bilinear, align_corners=False; persp_trans_detector.py:65) and the kornia
+    warp restatement (:69), from fp32 and split-bf16 grad_out; and the forward it is the
+    adjoint of (warp_views_upsampled_into) matches the same composition."""
+    from mvdet_amd import ops
+    from mvdet_amd.geometry import kornia_src_norm_from_dst_norm
+    rng = np.random.default_rng(3 * C + h)
+    n = 2
+    Ms = [torch.from_numpy(_rand_h(rng, H, W, ho, wo)).float()[None] for _ in range(n)]
+    gouts = [torch.from_numpy(rng.standard_normal((B, C, ho, wo)).astype(np.float32)) for _ in range(n)]
+    feats = [torch.from_numpy(rng.standard_normal((B, C, h, w)).astype(np.float32)) for _ in range(n)]
+    refs, fwd = [], []
+    for M, g, f in zip(Ms, gouts, feats):
+        src = f.clone().requires_grad_()
+        out = kornia_warp.warp_perspective(F.interpolate(src, (H, W), mode="bilinear"), M.repeat(B, 1, 1), (ho, wo))
+        out.backward(g)
+        refs.append(src.grad)
+        fwd.append(out.detach())
+    mn = [kornia_src_norm_from_dst_norm(M, (H, W), (ho, wo))[0] for M in Ms]
+    plans = [ops.WarpAdjointPlan(m, (H, W), (ho, wo), DEV, backbone_hw=(h, w)) for m in mn]
+    assert plans[0].src_hw == (h, w) and plans[0].nnz <= 9 * ho * wo
+    rp, col = plans[0].row_ptr.cpu(), plans[0].col[:plans[0].nnz].cpu()
+    assert rp[0] == 0 and (rp[1:] >= rp[:-1]).all()
+    for p in range(0, h * w, max(1, h * w // 53)):
+        seg = col[rp[p]:rp[p + 1]]
+        assert (seg[1:] > seg[:-1]).all()
+    gdev = [g.to(DEV) for g in gouts]
+    outs = [torch.full((B, C, h, w), float("nan"), device=DEV) for _ in range(n)]
+    ops.warp_views_adjoint(gdev, plans, outs)
+    for i in range(n):
+        assert_parity(outs[i].cpu(), refs[i], f"upsampled adjoint view {i}")
+    outs_s = [torch.empty_like(o) for o in outs]
+    ops.warp_views_adjoint([_split_encode(g) for g in gdev], plans, outs_s)
+    for i in range(n):
+        assert_parity(outs_s[i].cpu(), refs[i], f"upsampled adjoint (split grad_out) view {i}")
+    dst = [torch.empty((B, C, ho, wo), device=DEV) for _ in range(n)]
+    ops.warp_views_upsampled_into([f.to(DEV) for f in feats], (H, W), mn, dst)
+    for i in range(n):
+        assert_parity(dst[i].cpu(), fwd[i], f"fused forward view {i}")
+
+
 @pytest.mark.parametrize("B,C,H,W,ho,wo", [(1, 5, 27, 48, 12, 36), (2, 37, 30, 41, 17, 23),
                                            (1, 3, 9, 11, 20, 30), (1, 72, 90, 160, 120, 360),
                                            (2, 16, 30, 41, 17, 23)])

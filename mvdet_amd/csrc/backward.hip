@@ -33,6 +33,7 @@
 // channels into the module's weight layout through chan_map.
 #include "warp_common.h"
 
+#include <climits>
 #include <type_traits>
 #include <utility>
 
@@ -52,9 +53,6 @@ typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
                            // registers: conv1 wgrad 4.35 vs 3.10 ms, measured slower)
 #endif
 constexpr int CPW = MVBEV_WGRAD_CPW;
-#ifndef MVBEV_WGRAD_PF2
-#define MVBEV_WGRAD_PF2 1  // transposed reads two (s, tap) steps ahead (conv1 wgrad 2.93 vs 3.03 ms at one)
-#endif
 #ifndef MVBEV_WGRAD_DMA
 #define MVBEV_WGRAD_DMA 1  // split-bf16 x + aligned dy: wgrad_dma_kernel (LDS-DMA staging)
 #endif
@@ -293,19 +291,29 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const WArgs a) {
 //   A  dy[128 co][32 px] fp32 as DMA'd (8 x 16-B pieces per row, piece q of row r stored at
 //      slot q ^ ((r >> 1) & 7): the fragment reads of 16 consecutive rows hit 64 distinct
 //      banks); split into bf16 hi / lo at fragment-read time (the same rounding as split4);
-//   B  the window image of wgrad_kernel ([half][part][3 * XW px][32 ch], 16-B pieces copied
-//      straight from the split slab), read by the same transposed reads.
+//   B  the 3-row x window in the split slab's own order: per (32-channel half h, 8-channel
+//      group g) a run [row][px][hi, lo] of 16-B pieces, so one DMA instruction copies ~1 KiB
+//      of contiguous slab (16 pixels' hi + lo); run (h, g) starts at entry (4h + g) * GS +
+//      (g & 1) + 8 (g >> 1), which puts the transposed reads of the 4 groups on distinct banks.
 // Three buffers, one barrier per chunk: the wait before it retires this chunk's DMA (the next
 // chunk's may stay in flight), the DMA after it refills the buffer read two chunks ago.
 constexpr int WG_AENT = MT * PX / 4;  // A entries (16 B) per buffer: 1024
+// Waves that issue the DMAs (8: all; 4: one per SIMD, the other wave of each SIMD starting its
+// MFMAs at once while its partner queues the DMA pieces)
+#ifndef MVBEV_WGRAD_DMAW
+#define MVBEV_WGRAD_DMAW 8  // 4 measured equal (2.41 vs 2.42 ms) at 16 more VGPRs; 2: 3.45 ms
+#endif
 constexpr int WG_MAXC = 2048;         // chunk ids of a workgroup's partition, staged in LDS
 template <int DIL> struct WgGeo {
   static constexpr int XW = PX + 2 * DIL, BPIX = 3 * XW;
-  static constexpr int BENT = 16 * BPIX;                    // [half][part][pix][4 x 8 ch]
-  static constexpr int NA = WG_AENT / NTH;                  // A DMA instructions per thread
-  static constexpr int NB = (BENT + NTH - 1) / NTH;         // B DMA instructions per thread
-  static constexpr int BUFE = WG_AENT + NB * NTH;           // entries per buffer (incl. tail)
-  static_assert(WG_AENT % NTH == 0, "A image must split evenly over the threads");
+  static constexpr int RUN = 2 * BPIX;                      // entries of one (h, g) run
+  static constexpr int GS = (RUN + 9 + 15) / 16 * 16;       // run stride (entries, 0 mod 16)
+  static constexpr int BENT = 8 * GS;
+  static constexpr int DT = 64 * MVBEV_WGRAD_DMAW;         // DMA lanes (the first DMAW waves)
+  static constexpr int NA = WG_AENT / DT;                   // A DMA instructions per DMA lane
+  static constexpr int NB = (BENT + DT - 1) / DT;           // B DMA instructions per DMA lane
+  static constexpr int BUFE = WG_AENT + NB * DT;            // entries per buffer (incl. tail)
+  static_assert(WG_AENT % DT == 0, "A image must split evenly over the DMA lanes");
   static_assert(3 * BUFE * 16 + WG_MAXC * 4 <= 160 * 1024, "LDS");
 };
 __device__ u32x4 g_wg_zero[1];  // zero-initialised source of out-of-range entries
@@ -338,13 +346,22 @@ template <typename F, int... U>
 __device__ __attribute__((always_inline)) inline void wg_static_for(F& f, std::integer_sequence<int, U...>) {
   (f(std::integral_constant<int, U>{}), ...);
 }
+template <int B, int... U>
+constexpr std::integer_sequence<int, (B + U)...> offset_seq(std::integer_sequence<int, U...>) {
+  return {};
+}
 
+#ifndef MVBEV_WGRAD_ABL
+#define MVBEV_WGRAD_ABL 0  // timing ablations only (wrong results): bit 0 no chunk barrier, bit 1 no
+                           // DMA, bit 2 no fragment reads / MFMAs, bit 3 no partial-sum store, bit 4
+                           // x window sources contiguous from the chunk origin
+#endif
 template <int DIL>
 __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
   static_assert(NWV == 8, "wave layout: 4 output blocks x 2 channel halves");
   using G = WgGeo<DIL>;
-  constexpr int XW = G::XW, BPIX = G::BPIX, NA = G::NA, NB = G::NB, BUFE = G::BUFE;
-  constexpr int BIMGE = BPIX * 4;  // entries per (half, part) image
+  constexpr int XW = G::XW, BPIX = G::BPIX, NA = G::NA, NB = G::NB, BUFE = G::BUFE, DT = G::DT;
+  constexpr int DMAW = MVBEV_WGRAD_DMAW;
   __shared__ __attribute__((aligned(16))) u32x4 lds[3 * BUFE];
   __shared__ int cids[WG_MAXC];
 
@@ -367,75 +384,113 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
   const int64_t plane = (int64_t)H * W;
   const u32x4* xs = static_cast<const u32x4*>(a.x);
 
-  // DMA of chunk ci into buffer bb; lane's j-th instruction covers entry (j * NWV + wave) * 64 + lane
-  auto issue = [&](int c, int bb) __attribute__((always_inline)) {
-    const int R = c / a.segs, seg = c - R * a.segs;
-    const int b = R / H, y = R - b * H;
-    const int x0 = seg * PX;
+  // LDS-DMA sources.  DMA lane's j-th instruction covers entry (j * DMAW + wave) * 64 + lane; the
+  // chunk-invariant part of each source (channel / Cout row, window pixel) is an offset from the
+  // chunk's origin, formed once, so an issue is a few adds, two range checks and a select per
+  // instruction (formed per chunk, the divisions and 64-bit products cost about as many
+  // cycles as the chunk's MFMAs).  A entry: dy row `row` (Cout), piece q (4 px, swizzled slot).
+  int aofs[NA], acol[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int e = (j * DMAW + wave) * 64 + lane;
+    const int row = e >> 3, q = (e & 7) ^ ((row >> 1) & 7);
+    aofs[j] = (ct * MT + row) * (int)plane + 4 * q;
+    acol[j] = 4 * q;
+  }
+  // B entry: run (h, g4), then (row r, window pixel cc, part); bdx = INT_MIN / 2 marks a zero
+  // entry (run padding, channel past K): x0 + bdx then fails the column check
+  int bofs[NB], bdy[NB], bdx[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int e = (j * DMAW + wave) * 64 + lane;
+    const int hg = e / G::GS, g4 = hg & 3;
+    const int q = e - hg * G::GS - ((g4 & 1) + 8 * (g4 >> 1));
+    const int k0 = kt * NT + (hg >> 2) * 32 + g4 * 8;
+    const bool ok = hg < 8 && q >= 0 && q < G::RUN && k0 < a.K;
+    const int qc = ok ? q : 0, kc = ok ? k0 : 0;
+    const int pix = qc >> 1, r = pix / XW, cc = pix - r * XW;
+    const int g_ = kc / a.group;
+    const int64_t cbase = g_ * a.group_stride + (int64_t)(kc - g_ * a.group) * plane;
+    bdy[j] = (r - 1) * DIL;
+    bdx[j] = ok ? cc - DIL : INT_MIN / 2;
+    bofs[j] = (int)(cbase / 4) + 2 * (bdy[j] * W + cc - DIL) + (qc & 1);
+  }
+  // chunk ci (packed b << 24 | y << 12 | seg, see the staging below) into buffer bb
+  auto issue = [&](int pk, int bb) __attribute__((always_inline)) {
+    const int b = pk >> 24, y = (pk >> 12) & 4095, x0 = (pk & 4095) * PX;
+    const float* abase = a.dy + ((int64_t)b * a.Cout * H + y) * W + x0;
+    const u32x4* bbase = xs + (int64_t)b * (a.batch_stride / 4) + 2 * (y * W + x0);
     u32x4* dst = lds + bb * BUFE + wave * 64;
+    if (DMAW < NWV && wave >= DMAW) return;
 #pragma unroll
     for (int j = 0; j < NA; ++j) {
-      int e = (j * NWV + wave) * 64 + lane;
-      asm volatile("" : "+v"(e));  // recomputed per issue: nothing held across the MFMA loop
-      const int row = e >> 3, q = (e & 7) ^ ((row >> 1) & 7);
-      const int px = x0 + 4 * q;
-      const float* src = a.dy + (((int64_t)b * a.Cout + ct * MT + row) * H + y) * W + px;
-      wg_glds16(px < W ? (const void*)src : (const void*)g_wg_zero, dst + j * NTH);
+      const bool ok = x0 + acol[j] < W;
+      wg_glds16(ok ? (const void*)(abase + aofs[j]) : (const void*)g_wg_zero, dst + j * DT);
     }
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      int e = (j * NWV + wave) * 64 + lane;
-      asm volatile("" : "+v"(e));
-      const int g4 = e & 3, pe = e >> 2;
-      const int hp = pe / BPIX, pix = pe - hp * BPIX;
-      const int r = pix / XW, cc = pix - r * XW;
-      const int gy = y + (r - 1) * DIL, gx = x0 - DIL + cc;
-      const int k0 = kt * NT + (hp >> 1) * 32 + g4 * 8;
-      const bool ok = e < G::BENT && gy >= 0 && gy < H && gx >= 0 && gx < W && k0 < a.K;
-      const void* src = g_wg_zero;
-      if (ok) {
-        const int g_ = k0 / a.group;
-        const int64_t base = (int64_t)b * a.batch_stride + g_ * a.group_stride + (int64_t)(k0 - g_ * a.group) * plane;
-        src = xs + base / 4 + 2 * ((int64_t)gy * W + gx) + (hp & 1);
-      }
-      wg_glds16(src, dst + WG_AENT + j * NTH);
+      const bool ok = (unsigned)(y + bdy[j]) < (unsigned)H && (unsigned)(x0 + bdx[j]) < (unsigned)W;
+      const u32x4* bsrc = (MVBEV_WGRAD_ABL & 16) ? bbase + ((j * DMAW + wave) * 64 + lane) : bbase + bofs[j];
+      wg_glds16(ok ? (const void*)bsrc : (const void*)g_wg_zero, dst + WG_AENT + j * DT);
     }
   };
 
   const int cw = wave & 3, cb = wave >> 2;
   const int gi = (lane >> 4) & 1, li = lane & 15;
-  const int tr0 = (8 * kh + (li >> 2)) * 32 + 16 * gi + 4 * (li & 3);  // bf16 units (as wgrad_kernel)
+  // transposed-read lane: pixel 8 kh + li / 4 (+ 4 for the second read), channels 16 gi + 4 (li & 3)
+  // .. + 3 of the wave's half = group g = 2 gi + (li & 3) / 2, offset 4 (li & 1) in the piece
+  const int trg = 2 * gi + ((li & 3) >> 1);
+  const int tr0 = 16 * ((cb * 4 + trg) * G::GS + (trg & 1) + 8 * (trg >> 1) + 2 * (8 * kh + (li >> 2))) +
+                  8 * (li & 1);  // bytes
   const int arow = 32 * cw + l32, asw = (arow >> 1) & 7;
   floatx16 acc[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) acc[t] = floatx16{0};
 
-  auto compute = [&](int bb) __attribute__((always_inline)) {
+  // Per chunk 18 (pixel step s, tap t) steps of 3 MFMAs.  Step u+2's 4 transposed reads go out
+  // under step u's MFMAs and lgkmcnt(4) then retires step u+1's (in-order LDS returns; no
+  // scalar loads are in flight inside the loop; one step ahead measured slower, 3.03 vs 2.93
+  // ms).  Measured no faster: running a chunk's last two steps after the next barrier, under
+  // the next chunk's first reads (2.47 vs 2.45 ms).
+  // full = false: a last row segment with at most 16 pixels left; its second pixel step would
+  // multiply zeros and is skipped (the reads it prefetched are drained by the next wait).
+  floatx4 av[4];
+  bf16x8 ahi[2], alo[2];
+  v4i16 fr[3][4];
+  uint32_t bb0 = 0;
+  auto read = [&](auto u_) __attribute__((always_inline)) {
+    constexpr int u = decltype(u_)::value, s = u / 9, t = u % 9;
+    constexpr int set = u % 3;
+    constexpr int off = ((t / 3) * XW + 16 * s + (t % 3) * DIL) * 32;  // bytes (32 per pixel)
+    fr[set][0] = wg_tr<off>(bb0);
+    fr[set][1] = wg_tr<off + 128>(bb0);
+    fr[set][2] = wg_tr<off + 16>(bb0);
+    fr[set][3] = wg_tr<off + 16 + 128>(bb0);
+  };
+  auto mfma3 = [&](int t, bf16x8 ah, bf16x8 al, const v4i16 (&f)[4]) __attribute__((always_inline)) {
+    const bf16x8 bhi = wg_cat(f[0], f[1]), blo = wg_cat(f[2], f[3]);
+    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bhi, acc[t], 0, 0, 0);
+    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, blo, acc[t], 0, 0, 0);
+    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bhi, acc[t], 0, 0, 0);
+  };
+  // chunk in buffer bb: the A fragments and steps 0, 1's B fragments
+  auto head_reads = [&](int bb) __attribute__((always_inline)) {
     const u32x4* L = lds + bb * BUFE;
-    const floatx4* Arow = reinterpret_cast<const floatx4*>(L) + arow * 8;
-    const uint32_t bb0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)(
-        reinterpret_cast<const __bf16*>(L + WG_AENT + (cb * 2) * BIMGE) + tr0);
-    const uint32_t ab = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)Arow;
-    floatx4 av[4];
+    bb0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)(L + WG_AENT) + (uint32_t)tr0;
+    const uint32_t ab = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)(
+        reinterpret_cast<const floatx4*>(L) + arow * 8);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const uint32_t addr = ab + 16u * (uint32_t)((4 * (q >> 1) + 2 * kh + (q & 1)) ^ asw);
       asm volatile("ds_read_b128 %0, %1" : "=v"(av[q]) : "v"(addr));
     }
-    bf16x8 ahi[2], alo[2];
-    v4i16 fr[3][4];
-    auto read = [&](auto u_, int set) __attribute__((always_inline)) {
-      constexpr int u = decltype(u_)::value, s = u / 9, t = u % 9;
-      constexpr int off = ((t / 3) * XW + 16 * s + (t % 3) * DIL) * 32 * 2;  // bytes
-      constexpr int lo = BIMGE * 8 * 2;
-      fr[set][0] = wg_tr<off>(bb0);
-      fr[set][1] = wg_tr<off + 256>(bb0);
-      fr[set][2] = wg_tr<off + lo>(bb0);
-      fr[set][3] = wg_tr<off + lo + 256>(bb0);
-    };
-    read(std::integral_constant<int, 0>{}, 0);
+    read(std::integral_constant<int, 0>{});
+    read(std::integral_constant<int, 1>{});
+  };
+  auto body = [&](bool full) __attribute__((always_inline)) {
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(av[0]), "+v"(av[1]), "+v"(av[2]), "+v"(av[3]), "+v"(fr[0][0]),
-                 "+v"(fr[0][1]), "+v"(fr[0][2]), "+v"(fr[0][3]));
+                 "+v"(fr[0][1]), "+v"(fr[0][2]), "+v"(fr[0][3]), "+v"(fr[1][0]), "+v"(fr[1][1]), "+v"(fr[1][2]),
+                 "+v"(fr[1][3]));
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const floatx4 v0 = av[2 * s], v1 = av[2 * s + 1];
@@ -446,63 +501,63 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
       ahi[s] = __builtin_bit_cast(bf16x8, hh);
       alo[s] = __builtin_bit_cast(bf16x8, ll);
     }
-    // (s, tap) steps 0..17: the next step's 4 transposed reads go out before this step's MFMAs
-#if MVBEV_WGRAD_PF2
-    // two steps ahead: step u+2's reads go out under step u's MFMAs; lgkmcnt(4) then retires
-    // step u+1's (in-order LDS returns; no scalar loads are in flight inside compute)
-    read(std::integral_constant<int, 1>{}, 1);
     auto step = [&](auto u_) __attribute__((always_inline)) {
-      constexpr int u = decltype(u_)::value, s = u / 9, t = u % 9, st = u % 3;
-      if constexpr (u + 2 < 18) read(std::integral_constant<int, u + 2>{}, (u + 2) % 3);
-      const bf16x8 bhi = wg_cat(fr[st][0], fr[st][1]), blo = wg_cat(fr[st][2], fr[st][3]);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[s], bhi, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[s], blo, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[s], bhi, acc[t], 0, 0, 0);
+      constexpr int u = decltype(u_)::value, s = u / 9, t = u % 9;
+      constexpr int set = u % 3, nset = (u + 1) % 3;
+      if constexpr (u + 2 < 18) read(std::integral_constant<int, u + 2>{});
+      mfma3(t, ahi[s], alo[s], fr[set]);
       if constexpr (u + 2 < 18) {
-        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(fr[(u + 1) % 3][0]), "+v"(fr[(u + 1) % 3][1]),
-                     "+v"(fr[(u + 1) % 3][2]), "+v"(fr[(u + 1) % 3][3]));
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(fr[nset][0]), "+v"(fr[nset][1]), "+v"(fr[nset][2]), "+v"(fr[nset][3]));
       } else if constexpr (u + 1 < 18) {
-        wg_lgkm_wait(fr[(u + 1) % 3]);
+        wg_lgkm_wait(fr[nset]);
       }
     };
-#else
-    auto step = [&](auto u_) __attribute__((always_inline)) {
-      constexpr int u = decltype(u_)::value, s = u / 9, t = u % 9, st = u & 1;
-      if constexpr (u + 1 < 18) read(std::integral_constant<int, u + 1>{}, st ^ 1);
-      const bf16x8 bhi = wg_cat(fr[st][0], fr[st][1]), blo = wg_cat(fr[st][2], fr[st][3]);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(alo[s], bhi, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[s], blo, acc[t], 0, 0, 0);
-      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ahi[s], bhi, acc[t], 0, 0, 0);
-      if constexpr (u + 1 < 18) wg_lgkm_wait(fr[st ^ 1]);
-    };
-#endif
-    wg_static_for(step, std::make_integer_sequence<int, 18>{});
+    wg_static_for(step, std::make_integer_sequence<int, 9>{});
+    if (full) wg_static_for(step, offset_seq<9>(std::make_integer_sequence<int, 9>{}));
   };
 
   // the partition's chunk ids, staged in LDS before any DMA (a global load of the list inside
   // the loop would be waited for with vmcnt(0), draining the DMAs in flight)
   const int n = c1 - c0;
-  for (int j = tid; j < n; j += NTH) cids[j] = list ? list[c0 + j] : c0 + j;
+  for (int j = tid; j < n; j += NTH) {
+    const int c = list ? list[c0 + j] : c0 + j;
+    const int R = c / a.segs, seg = c - R * a.segs;
+    const int b = R / H;
+    cids[j] = (b << 24) | ((R - b * H) << 12) | seg;  // host: B < 128, H, segs <= 4096
+  }
   __syncthreads();
   if (n > 0) {
     issue(cids[0], 0);
     if (n > 1) issue(cids[1], 1);
     for (int i = 0; i < n; ++i) {
-      // retire chunk i's DMA (chunk i+1's may stay in flight); LDS reads of chunk i-1 done
+      // retire chunk i's DMA (chunk i+1's may stay in flight) and every LDS read of chunk i-1
+      // (fragment registers tied: a partial chunk's skipped reads must land before reuse)
       if (i + 1 < n) {
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NA + NB) : "memory");
+        asm volatile("s_waitcnt vmcnt(%8) lgkmcnt(0)"
+                     : "+v"(fr[0][0]), "+v"(fr[0][1]), "+v"(fr[0][2]), "+v"(fr[0][3]), "+v"(fr[1][0]), "+v"(fr[1][1]),
+                       "+v"(fr[1][2]), "+v"(fr[1][3])
+                     : "n"(NA + NB)
+                     : "memory");
       } else {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)"
+                     : "+v"(fr[0][0]), "+v"(fr[0][1]), "+v"(fr[0][2]), "+v"(fr[0][3]), "+v"(fr[1][0]), "+v"(fr[1][1]),
+                       "+v"(fr[1][2]), "+v"(fr[1][3])
+                     :
+                     : "memory");
       }
-      __builtin_amdgcn_s_barrier();
+      if (!(MVBEV_WGRAD_ABL & 1)) __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (i + 2 < n) issue(cids[i + 2], (i + 2) % 3);
-      compute(i % 3);
+      if (!(MVBEV_WGRAD_ABL & 2) && i + 2 < n) issue(cids[i + 2], (i + 2) % 3);
+      const bool full = (cids[i] & 4095) * PX + 16 < W;
+      if (!(MVBEV_WGRAD_ABL & 4)) {
+        head_reads(i % 3);
+        body(full);
+      }
     }
   }
 
   const int k = kt * NT + 32 * cb + l32;
-  if (k < a.K) {
+  if (!(MVBEV_WGRAD_ABL & 8) && k < a.K) {
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -513,21 +568,48 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
   }
 }
 
-// dw[co][map(k)][t] = sum_p ws[p][t][co][k]  (partition order: deterministic)
-__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int P, int Cout, int K,
-                                    const int32_t* __restrict__ chan_map, int Cin_w, float* __restrict__ dw) {
-  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i >= (int64_t)Cout * K) return;
-  const int co = (int)(i / K), k = (int)(i - (int64_t)co * K);
-  const int cm = chan_map ? chan_map[k] : k;
-  if (cm < 0 || cm >= Cin_w) return;
+// dw[co][map(k)][t] = sum_p ws[p][t][co][k]  (partition order: deterministic).  One block per
+// (co, 64 channels): the 9 x 64 sums are read along k (coalesced), transposed through LDS and
+// written along (k, t), the weight's own order (contiguous wherever the channel map is).
+constexpr int kWrK = 64, kWrThreads = 192;  // 9 * 64 = 3 * 192 sums per block
+__global__ __launch_bounds__(kWrThreads) void wgrad_reduce_kernel(const float* __restrict__ ws, int P, int Cout, int K,
+                                                              const int32_t* __restrict__ chan_map, int Cin_w,
+                                                              float* __restrict__ dw) {
+  __shared__ float sums[9 * kWrK];
+  const int co = blockIdx.y, k0 = blockIdx.x * kWrK;
   const int64_t pstride = (int64_t)9 * Cout * K;
+  float v[3];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
+  for (int j = 0; j < 3; ++j) {
+    const int i = threadIdx.x + j * kWrThreads, t = i / kWrK, k = k0 + i % kWrK;
     float s = 0.f;
-    const float* src = ws + ((int64_t)t * Cout + co) * K + k;
-    for (int q = 0; q < P; ++q) s += src[q * pstride];
-    dw[((int64_t)co * Cin_w + cm) * 9 + t] = s;
+    if (k < K) {
+      const float* src = ws + ((int64_t)t * Cout + co) * K + k;
+      int q = 0;
+      for (; q + 8 <= P; q += 8) {  // loads issued together, added in partition order
+        float x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = src[(q + u) * pstride];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += x[u];
+      }
+      for (; q < P; ++q) s += src[q * pstride];
+    }
+    v[j] = s;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int i = threadIdx.x + j * kWrThreads;
+    sums[(i % kWrK) * 9 + i / kWrK] = v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int i = threadIdx.x + j * kWrThreads, kk = i / 9, t = i - kk * 9, k = k0 + kk;
+    if (k >= K) continue;
+    const int cm = chan_map ? chan_map[k] : k;
+    if (cm < 0 || cm >= Cin_w) continue;
+    dw[((int64_t)co * Cin_w + cm) * 9 + t] = sums[i];
   }
 }
 
@@ -1157,7 +1239,8 @@ int mvbev_conv3x3_wgrad_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_
   if (!x || !d || !dy || !dw || !workspace) return MVBEV_ERR_NULL;
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || Cin_w <= 0 || d->group <= 0)
     return MVBEV_ERR_RANK;
-  if (Cout % MT != 0 || d->K % 8 != 0 || d->group % 8 != 0 || d->K % d->group != 0) return MVBEV_ERR_SHAPE;
+  if (Cout % MT != 0 || Cout > 65535 || d->K % 8 != 0 || d->group % 8 != 0 || d->K % d->group != 0)
+    return MVBEV_ERR_SHAPE;
   if (d->in_row0 != 0 || d->in_rows != d->H || d->out_row0 != 0 || d->out_rows != d->H) return MVBEV_ERR_SHAPE;
   if (!chan_map && d->K > Cin_w) return MVBEV_ERR_SHAPE;
   if (d->H * d->W > (int64_t)INT32_MAX / 2 || d->B * d->H * ceil_div(d->W, PX) > INT32_MAX) return MVBEV_ERR_SHAPE;
@@ -1180,7 +1263,12 @@ int mvbev_conv3x3_wgrad_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)(g.P * g.tiles)), block(NTH);
   const bool split = x_layout == MVBEV_LAYOUT_SPLIT_BF16;
-  if (MVBEV_WGRAD_DMA && split && a.vec_dy && (dilation == 1 || dilation == 2) &&
+  // the DMA kernel's packed chunk ids (b, y, segment) and 32-bit chunk-invariant offsets
+  const int64_t coff_max = ((d->K - 1) / d->group) * d->group_stride + (d->group - 8) * d->H * d->W;
+  const bool dma_fits = d->B < 128 && d->H <= 4096 && a.segs <= 4096 && d->batch_stride % 8 == 0 &&
+                        d->group_stride % 8 == 0 && Cout * d->H * d->W < INT32_MAX &&
+                        coff_max / 4 + 2 * d->H * d->W < INT32_MAX;
+  if (MVBEV_WGRAD_DMA && split && a.vec_dy && dma_fits && (dilation == 1 || dilation == 2) &&
       g.nchunks / g.P + 1 <= WG_MAXC) {
     if (dilation == 1) hipLaunchKernelGGL((wgrad_dma_kernel<1>), grid, dim3(NTH), 0, s, a);
     else hipLaunchKernelGGL((wgrad_dma_kernel<2>), grid, dim3(NTH), 0, s, a);
@@ -1194,8 +1282,7 @@ int mvbev_conv3x3_wgrad_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_
     return MVBEV_ERR_DILATION;
   }
   MVBEV_CHECK_LAUNCH();
-  const int64_t n = Cout * d->K;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(d->K, kWrK), (unsigned)Cout), dim3(kWrThreads), 0, s,
                      static_cast<const float*>(workspace), g.P, (int)Cout, (int)d->K, chan_map, (int)Cin_w, dw);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;

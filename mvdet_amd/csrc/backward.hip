@@ -1032,6 +1032,9 @@ __global__ __launch_bounds__(256) void adj_sort_kernel(const int32_t* __restrict
 // entries stay in registers across the channels.  Workgroups of one (view, batch, channel
 // chunk) are consecutive in the XCD-remapped order, so an XCD sweeps neighbouring pixels of
 // the same grad_out planes (its L2 holds them).
+#ifndef MVBEV_ADJ_G8
+#define MVBEV_ADJ_G8 1  // split grad_out: a thread per (pixel, 8-channel group), warp_adjoint_split8_kernel
+#endif
 constexpr int kAdjReg = 6;
 constexpr int kAdjCPB = 32;
 constexpr int kAdjU = 8;
@@ -1174,6 +1177,63 @@ __global__ __launch_bounds__(256) void warp_adjoint_split_kernel(const AdjArgs a
         *d = a.accumulate ? s[q] + *d : s[q];
       }
   }
+}
+
+// The split gather with a thread per (source pixel, 8-channel group): a workgroup = 32 pixels x
+// 8 groups (64 channels), a half-wave = 32 consecutive pixels of one group (coalesced stores).
+// Each thread's chain of dependent gathers is one channel group's instead of a 32-channel
+// chunk's (4x shorter), and a pixel's entries are shared by its 8 group threads.
+constexpr int kAsPix = 32, kAsGroups = 8;
+__global__ __launch_bounds__(256) void warp_adjoint_split8_kernel(const AdjArgs a) {
+  const int lb = xcd_remap(blockIdx.x, a.nwg);
+  const int pb = lb % a.pblocks;
+  int r = lb / a.pblocks;
+  const int chunk = r % a.chunks;
+  r /= a.chunks;
+  const int view = r % a.nviews;
+  const int b = r / a.nviews;
+  const int p = pb * kAsPix + (threadIdx.x & (kAsPix - 1));
+  const int c = (chunk * kAsGroups + (threadIdx.x >> 5)) * 8;
+  if (p >= a.P || c >= a.C) return;
+  const AdjView& vw = a.v[view];
+  const int e0 = vw.rp[p], e1 = vw.rp[p + 1];
+  const u32x4* g = reinterpret_cast<const u32x4*>(vw.go) + 2 * (int64_t)b * vw.gB + 2 * (int64_t)(c >> 3) * vw.gC;
+  float s[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) s[q] = 0.f;
+  // entries in batches of 8: the batch's (col, val) loads, then 8 independent gathers
+  for (int eb = e0; eb < e1; eb += 8) {
+    int cb[8];
+    float wb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool ok = eb + j < e1;
+      cb[j] = ok ? vw.col[eb + j] : 0;
+      wb[j] = ok ? vw.val[eb + j] : 0.f;
+    }
+    u32x4 hv[8], lv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (eb + j < e1) {
+        hv[j] = g[2 * (int64_t)cb[j]];
+        lv[j] = g[2 * (int64_t)cb[j] + 1];
+      }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (eb + j < e1) {
+        const bf16x8 hi = __builtin_bit_cast(bf16x8, hv[j]), lo = __builtin_bit_cast(bf16x8, lv[j]);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s[q] += wb[j] * ((float)hi[q] + (float)lo[q]);
+      }
+  }
+  float* gs = vw.gs + (int64_t)b * vw.sB + (int64_t)c * vw.sC + p;
+  const int nq = min(8, a.C - c);
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    if (q < nq) {
+      float* d = gs + (int64_t)q * vw.sC;
+      *d = a.accumulate ? s[q] + *d : s[q];
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1465,13 +1525,16 @@ int mvbev_warp_views_adjoint(const mvbev_warp_adjoint_view* views, int nviews, i
   }
   a.nviews = nviews;
   a.B = (int)B; a.C = (int)C; a.P = (int)(H * W);
-  a.pblocks = (int)ceil_div(H * W, 256);
-  a.chunks = (int)ceil_div(C, bwd::kAdjCPB);
+  const bool g8 = split && MVBEV_ADJ_G8;
+  a.pblocks = (int)ceil_div(H * W, g8 ? bwd::kAsPix : 256);
+  a.chunks = (int)ceil_div(C, g8 ? 8 * bwd::kAsGroups : bwd::kAdjCPB);
   a.accumulate = accumulate ? 1 : 0;
   const int64_t nwg = (int64_t)a.pblocks * a.chunks * nviews * B;
   if (nwg > INT32_MAX) return MVBEV_ERR_SHAPE;
   a.nwg = (int)nwg;
-  if (split)
+  if (g8)
+    hipLaunchKernelGGL(bwd::warp_adjoint_split8_kernel, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
+  else if (split)
     hipLaunchKernelGGL(bwd::warp_adjoint_split_kernel, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
   else
     hipLaunchKernelGGL(bwd::warp_adjoint_kernel, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);

@@ -110,6 +110,24 @@ __device__ inline WarpCoord warp_coord(const float (&m)[9], int u, int v, int Ho
   return c;
 }
 
+// PyTorch's bilinear upsample taps of upsampled index X along an axis of n backbone pixels
+// (align_corners=False, scale = n / N): s = max(0, (X + 0.5) * scale - 0.5), i0 = min(floor(s),
+// n - 1), i1 = i0 + (i0 < n - 1), weights l0 = 1 - (s - i0) on i0 and l1 = s - i0 on i1.
+struct UpTaps {
+  int i0, i1;
+  float l0, l1;
+};
+__device__ inline UpTaps up_taps(int X, float scale, int n) {
+  UpTaps t;
+  float s = scale * ((float)X + 0.5f) - 0.5f;
+  s = s < 0.f ? 0.f : s;
+  t.i0 = min((int)s, n - 1);
+  t.i1 = t.i0 + (t.i0 < n - 1 ? 1 : 0);
+  t.l1 = s - (float)t.i0;
+  t.l0 = 1.f - t.l1;
+  return t;
+}
+
 // The fused 3x-upsample + warp sample of output pixel (u, v) as one 3x3 window of the
 // backbone-resolution map (warp_up_kernel, and the plan of its adjoint): the warp's corners in
 // the upsampled H x W grid (warp_coord), each corner's PyTorch bilinear upsample taps
@@ -141,22 +159,15 @@ __device__ inline UpWindow up_window(const float (&m)[9], int u, int v, int Ho, 
     const int ux = x0 + k, uy = y0 + k;
     okx[k] = r.inside && ux >= 0 && ux <= W - 1;
     oky[k] = r.inside && uy >= 0 && uy <= H - 1;
-    float s = sx * ((float)ux + 0.5f) - 0.5f;
-    s = s < 0.f ? 0.f : s;
-    int i0 = (int)s;
-    i0 = min(i0, w - 1);
-    cxi[k][0] = i0;
-    cxi[k][1] = i0 + (i0 < w - 1 ? 1 : 0);
-    lxv[k][1] = s - (float)i0;
-    lxv[k][0] = 1.f - lxv[k][1];
-    s = sy * ((float)uy + 0.5f) - 0.5f;
-    s = s < 0.f ? 0.f : s;
-    i0 = (int)s;
-    i0 = min(i0, h - 1);
-    cyi[k][0] = i0;
-    cyi[k][1] = i0 + (i0 < h - 1 ? 1 : 0);
-    lyv[k][1] = s - (float)i0;
-    lyv[k][0] = 1.f - lyv[k][1];
+    const UpTaps tx = up_taps(ux, sx, w), ty = up_taps(uy, sy, h);
+    cxi[k][0] = tx.i0;
+    cxi[k][1] = tx.i1;
+    lxv[k][0] = tx.l0;
+    lxv[k][1] = tx.l1;
+    cyi[k][0] = ty.i0;
+    cyi[k][1] = ty.i1;
+    lyv[k][0] = ty.l0;
+    lyv[k][1] = ty.l1;
   }
   r.cb = okx[0] ? cxi[0][0] : cxi[1][0];
   r.rb = oky[0] ? cyi[0][0] : cyi[1][0];

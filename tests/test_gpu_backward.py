@@ -65,13 +65,16 @@ def test_warp_backward_vs_grid_sample_autograd(B, C, H, W, ho, wo):
 
 
 @pytest.mark.parametrize("B,C,h,w,H,W,ho,wo", [(1, 8, 9, 16, 27, 48, 12, 36), (2, 16, 10, 14, 27, 48, 17, 23),
-                                               (1, 24, 30, 53, 90, 160, 120, 360)])
+                                               (1, 24, 30, 53, 90, 160, 120, 360), (1, 72, 7, 20, 20, 57, 15, 40),
+                                               (1, 16, 5, 9, 30, 54, 11, 13)])
 def test_upsampled_warp_adjoint_vs_autograd(B, C, h, w, H, W, ho, wo):
     """The fused 3x-upsample + warp adjoint (plan of S * U, <= 9 entries per output pixel):
     the gradient w.r.t. the backbone-resolution map equals torch-CPU autograd through
     F.interpolate (bilinear, align_corners=False; persp_trans_detector.py:65) and the kornia
-    warp restatement (:69), from fp32 and split-bf16 grad_out; and the forward it is the
-    adjoint of (warp_views_upsampled_into) matches the same composition."""
+    warp restatement (:69), from fp32 and split-bf16 grad_out (accumulating too); and the
+    forward it is the adjoint of (warp_views_upsampled_into) matches the same composition.
+    Scales 3x (the reference's), 2.7-3.4x and 6x; channel counts below, at and above a
+    64-channel workgroup."""
     from mvdet_amd import ops
     from mvdet_amd.geometry import kornia_src_norm_from_dst_norm
     rng = np.random.default_rng(3 * C + h)
@@ -99,10 +102,14 @@ def test_upsampled_warp_adjoint_vs_autograd(B, C, h, w, H, W, ho, wo):
     ops.warp_views_adjoint(gdev, plans, outs)
     for i in range(n):
         assert_parity(outs[i].cpu(), refs[i], f"upsampled adjoint view {i}")
-    outs_s = [torch.empty_like(o) for o in outs]
+    outs_s = [torch.full((B, C, h, w), float("nan"), device=DEV) for _ in range(n)]
     ops.warp_views_adjoint([_split_encode(g) for g in gdev], plans, outs_s)
     for i in range(n):
         assert_parity(outs_s[i].cpu(), refs[i], f"upsampled adjoint (split grad_out) view {i}")
+    acc = [torch.full((B, C, h, w), 0.25, device=DEV) for _ in range(n)]
+    ops.warp_views_adjoint([_split_encode(g) for g in gdev], plans, acc, accumulate=True)
+    for i in range(n):
+        assert_parity(acc[i].cpu() - 0.25, refs[i], f"upsampled adjoint, accumulating, view {i}")
     dst = [torch.empty((B, C, ho, wo), device=DEV) for _ in range(n)]
     ops.warp_views_upsampled_into([f.to(DEV) for f in feats], (H, W), mn, dst)
     for i in range(n):

@@ -55,7 +55,18 @@ def backward_stages(eng, ws, mc, B, ho, wo, N, C, dev):
     dslab = torch.empty(ops.split_shape(B, cp, ho, wo), dtype=torch.bfloat16, device=dev)
     cm = eng.conv1_mask(dev, 0, ho, tile_h=_native.TILE_H)
     flop = 2.0 * B * ho * wo * 9 * N * C * w1.shape[0]
+    # conv2 (d2) on a split y1 and a random dy2, as the training step's conv2 backward
+    w2 = mc[2].weight
+    mid = w2.shape[0]
+    y1s = torch.randn(ops.split_shape(B, mid, ho, wo), device=dev).to(torch.bfloat16)
+    dy2 = torch.randn(B, mid, ho, wo, device=dev)
+    dy2s = torch.randn(ops.split_shape(B, mid, ho, wo), device=dev).to(torch.bfloat16)
+    d_y1 = ops.conv_desc(B, mid, ho, wo, group=mid, group_stride=0, batch_stride=mid * ho * wo)
+    wws2 = autograd._wgrad_ws(st, d_y1, mid, dev)
+    flop2 = 2.0 * B * ho * wo * 9 * mid * mid
     return {
+        "wgrad2": (lambda: ops.conv3x3_wgrad(y1s, d_y1, dy2, 2, mid, workspace=wws2), flop2),
+        "dgrad2": (lambda: ops.conv3x3_dgrad(dy2s, st.dgrad2, w2, 2), flop2),
         "wgrad1": (lambda: ops.conv3x3_wgrad(ws.slab, d1, dy1, 1, w1.shape[1], chan_map=eng.pack1._map_dev,
                                              dw=dw1, workspace=wws, chunk_lists=lists), flop),
         "dgrad1": (lambda: ops.conv3x3_dgrad(dy1, st.dgrad1, w1, 1, out=dslab, out_mask=cm,
@@ -101,7 +112,18 @@ def main():
             "conv23": (lambda: (eng.conv2_partials(ws, mc[2], mc[4]), eng.conv3_from_partials(ws, mc[4])),
                        2.0 * B * ho * wo * 9 * 512 * 512),
         }
-        if {"wgrad1", "dgrad1"} & set(args.only.split(",")):
+        if {"adjup", "adj"} & set(args.only.split(",")):
+            # the warp adjoints of the training step (autograd.py) on a random split grad_out
+            from mvdet_amd import ops
+            hb = tuple(bfeats[0].shape[2:])
+            douts = [torch.randn(ops.split_shape(B, C, ho, wo), device=dev).to(torch.bfloat16) for _ in range(N)]
+            gs = [torch.empty(B, C, *hb, device=dev) for _ in range(N)]
+            gsu = [torch.empty(B, C, *up, device=dev) for _ in range(N)]
+            plu = [ops.WarpAdjointPlan(eng.m_norm_cpu[v], up, (ho, wo), dev, backbone_hw=hb) for v in range(N)]
+            stages["adjup"] = ((lambda: ops.warp_views_adjoint(douts, plu, gs)), None)
+            pl = [ops.WarpAdjointPlan(eng.m_norm_cpu[v], up, (ho, wo), dev) for v in range(N)]
+            stages["adj"] = ((lambda: ops.warp_views_adjoint(douts, pl, gsu)), None)
+        if {"wgrad1", "dgrad1", "wgrad2", "dgrad2"} & set(args.only.split(",")):
             stages.update(backward_stages(eng, ws, mc, B, ho, wo, N, C, dev))
         from mvdet_amd import _native
         libs = [("default", _native.load())]

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -193,6 +193,8 @@ int mvbev_conv3x3_f32(const float* x, const mvbev_conv_desc* desc, const float* 
 #define MVBEV_LAYOUT_F32 0        /* plain fp32 channel planes */
 #define MVBEV_LAYOUT_F16 1        /* plain fp16 channel planes (strides in elements) */
 #define MVBEV_LAYOUT_SPLIT_BF16 2 /* per (8-channel group, pixel): bf16 hi[8], bf16 lo[8] */
+#define MVBEV_LAYOUT_SPLIT_ROWS 3 /* per (channel, row, 8-pixel run): bf16 hi[8], bf16 lo[8]
+                                     (W % 8 == 0; the same bytes per row as fp32) */
 
 /* 3xbf16 split-precision variant of mvbev_conv3x3_f32 (same descriptor and semantics):
  * a*b ~= a_hi*b_hi + a_hi*b_lo + a_lo*b_hi on the bf16 MFMA, fp32 accumulation; ~2^-16
@@ -369,6 +371,20 @@ int mvbev_conv3x3_wgrad_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_
                                   int64_t Cin_w, float* dw, const int32_t* chunk_list,
                                   const int32_t* chunk_off, void* workspace, size_t workspace_bytes,
                                   void* stream);
+
+/* The same with dy in dy_layout: MVBEV_LAYOUT_F32 (as _ex) or MVBEV_LAYOUT_SPLIT_ROWS (dy
+ * pre-split by mvbev_split_rows_bf16; the LDS-DMA wgrad path only: split-bf16 x, dilation 1 or
+ * 2, W % 8 == 0, else MVBEV_ERR_SHAPE).  Bitwise the same dw as from the fp32 dy (the kernel
+ * splits an fp32 dy with the same rounding), without the per-segment split pass. */
+int mvbev_conv3x3_wgrad_bf16x3_ex2(const void* x, int x_layout, const mvbev_conv_desc* desc,
+                                   const void* dy, int dy_layout, int64_t Cout, int dilation,
+                                   const int32_t* chan_map, int64_t Cin_w, float* dw,
+                                   const int32_t* chunk_list, const int32_t* chunk_off, void* workspace,
+                                   size_t workspace_bytes, void* stream);
+
+/* fp32 rows x [rows][W] (16-B aligned, W % 8 == 0) -> out [rows][W / 8] pieces of bf16 hi[8],
+ * lo[8] (MVBEV_LAYOUT_SPLIT_ROWS; hi = bf16(x) round-to-nearest-even, lo = bf16(x - hi)). */
+int mvbev_split_rows_bf16(const float* x, int64_t rows, int64_t W, void* out, void* stream);
 
 /* db[co] = sum_b,p dy[b][co][p] (db may be NULL) and, when dw != NULL, the weight gradient of the
  * two coord channels (create_coord_map, persp_trans_detector.py:103-112) that are input channels

@@ -58,11 +58,14 @@ EXPORTS = (
     "mvbev_relu_backward_split_f32",
     "mvbev_conv3x3_cout1_backward_ex",
     "mvbev_warp_upsampled_adjoint_plan",
+    "mvbev_conv3x3_wgrad_bf16x3_ex2",
+    "mvbev_split_rows_bf16",
 )
 WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
+ERR_SHAPE = -2  # MVBEV_ERR_SHAPE
 
 KC = 8    # MVBEV_CONV_KC
-LAYOUT_F32, LAYOUT_F16, LAYOUT_SPLIT_BF16 = 0, 1, 2  # MVBEV_LAYOUT_*
+LAYOUT_F32, LAYOUT_F16, LAYOUT_SPLIT_BF16, LAYOUT_SPLIT_ROWS = 0, 1, 2, 3  # MVBEV_LAYOUT_*
 BN = 128  # MVBEV_CONV_BN
 TILE_H, TILE_W = 8, 32  # MVBEV_CONV_TILE_H / _W (fp32/fp16 input; split input: conv_tile_rows())
 
@@ -169,6 +172,11 @@ def _declare(lib):
     lib.mvbev_conv3x3_wgrad_bf16x3_ex.restype = ctypes.c_int
     lib.mvbev_conv3x3_wgrad_bf16x3_ex.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _i64,
                                                   ctypes.c_int, _p, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]
+    lib.mvbev_conv3x3_wgrad_bf16x3_ex2.restype = ctypes.c_int
+    lib.mvbev_conv3x3_wgrad_bf16x3_ex2.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, ctypes.c_int,
+                                                   _i64, ctypes.c_int, _p, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]
+    lib.mvbev_split_rows_bf16.restype = ctypes.c_int
+    lib.mvbev_split_rows_bf16.argtypes = [_p, _i64, _i64, _p, _p]
     lib.mvbev_conv3x3_dgrad_bf16x3.restype = ctypes.c_int
     lib.mvbev_conv3x3_dgrad_bf16x3.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _i64, ctypes.c_int, _p,
                                                ctypes.c_int, _p, _i64, _p]

@@ -117,6 +117,13 @@ def _wgrad_lists(engine: ProjectFuse, st, device, B: int):
     return st.lists[key]
 
 
+def _dy_rows(dy: torch.Tensor, split_x: bool):
+    """dy pre-split into bf16 hi / lo rows (``ops.split_rows``) for the LDS-DMA wgrad kernel
+    (split-bf16 x, W % 8 == 0: its per-segment split pass is then gone, bitwise the same dw),
+    or None.  conv1 at cfg2: 2.33 -> 2.26 ms including the 35 us split."""
+    return ops.split_rows(dy) if split_x and dy.shape[3] % 8 == 0 else None
+
+
 def _wgrad_ws(st, desc, cout, device) -> torch.Tensor:
     import ctypes
     from . import _native
@@ -191,6 +198,7 @@ class ProjectFuseFunction(torch.autograd.Function):
         if db2 is not None:
             ops.conv3x3_bias_coord_grad(dy2, 2, db=db2)
         d_y1 = ops.conv_desc(B, mid, H, W, group=mid, group_stride=0, batch_stride=mid * H * W)
+        # (conv2's wgrad reads the fp32 dy2: at its size the row split costs what it saves)
         dw2 = ops.conv3x3_wgrad(ws.y1, d_y1, dy2, 2, mid, workspace=_wgrad_ws(st, d_y1, mid, dev))
         _mark("bwd_conv2_dgrad")
         dy1 = ops.conv3x3_dgrad(dy2 if dy2s is None else dy2s, st.dgrad2, w2, 2)
@@ -213,7 +221,8 @@ class ProjectFuseFunction(torch.autograd.Function):
         d1 = ops.conv_desc(B, engine.S * engine.Cs, H, W, group=engine.Cs, group_stride=B * engine.Cs * H * W,
                            batch_stride=engine.Cs * H * W)
         ops.conv3x3_wgrad(ws.slab, d1, dy1, 1, w1.shape[1], chan_map=engine.pack1._map_dev, dw=dw1,
-                          workspace=_wgrad_ws(st, d1, mid, dev), chunk_lists=_wgrad_lists(engine, st, dev, B))
+                          workspace=_wgrad_ws(st, d1, mid, dev), chunk_lists=_wgrad_lists(engine, st, dev, B),
+                          dy_rows=_dy_rows(dy1, ws.slab.dtype == torch.bfloat16))
         grads = [None] * n
         if need_feat:
             _mark("bwd_conv1_dgrad")

@@ -71,6 +71,7 @@ struct WArgs {
   int group, K, Cout, B, H, W;
   int segs, nchunks, P, n_ct, n_kt, ntiles;
   bool vec_dy;  // W % 4 == 0 and dy 16-B aligned: dy rows as 16-B loads
+  bool dy_rows;  // dy in MVBEV_LAYOUT_SPLIT_ROWS (pre-split bf16 hi / lo; wgrad_dma_kernel only)
   // frustum (optional): per input-channel group (desc group = one camera's slot), the pixel
   // chunks whose x window can be non-zero, clist[coff[g] .. coff[g+1]); a tile's partitions
   // split its group's list instead of all chunks (skipped chunks contribute exactly 0)
@@ -290,7 +291,12 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_kernel(const WArgs a) {
 // segment) a buffer holds
 //   A  dy[128 co][32 px] fp32 as DMA'd (8 x 16-B pieces per row, piece q of row r stored at
 //      slot q ^ ((r >> 1) & 7): the fragment reads of 16 consecutive rows hit 64 distinct
-//      banks); split into bf16 hi / lo at fragment-read time (the same rounding as split4);
+//      banks); split into bf16 hi / lo at fragment-read time (the same rounding as split4) —
+//      or, with dy pre-split by mvbev_split_rows_bf16 (MVBEV_LAYOUT_SPLIT_ROWS: per 8-pixel
+//      run 16 B hi, 16 B lo, the same bytes per row), read as the fragments themselves: the
+//      DMA and the reads are unchanged, the per-segment split is gone (conv1 at cfg2: 2.33 ->
+//      2.22 ms + 35 us for the split pass; an ablation feeding unsplit bits ran 12 % faster, most
+//      of which was the clock those operands allow, not the split's VALU);
 //   B  the 3-row x window in the split slab's own order: per (32-channel half h, 8-channel
 //      group g) a run [row][px][hi, lo] of 16-B pieces, so one DMA instruction copies ~1 KiB
 //      of contiguous slab (16 pixels' hi + lo); run (h, g) starts at entry (4h + g) * GS +
@@ -360,7 +366,7 @@ template <int DIL>
 __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
   static_assert(NWV == 8, "wave layout: 4 output blocks x 2 channel halves");
   using G = WgGeo<DIL>;
-  constexpr int XW = G::XW, BPIX = G::BPIX, NA = G::NA, NB = G::NB, BUFE = G::BUFE, DT = G::DT;
+  constexpr int XW = G::XW, NA = G::NA, NB = G::NB, BUFE = G::BUFE, DT = G::DT;
   constexpr int DMAW = MVBEV_WGRAD_DMAW;
   __shared__ __attribute__((aligned(16))) u32x4 lds[3 * BUFE];
   __shared__ int cids[WG_MAXC];
@@ -494,6 +500,11 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const floatx4 v0 = av[2 * s], v1 = av[2 * s + 1];
+      if (a.dy_rows) {  // pre-split rows: the 8-pixel run's hi piece, then its lo piece
+        ahi[s] = __builtin_bit_cast(bf16x8, v0);
+        alo[s] = __builtin_bit_cast(bf16x8, v1);
+        continue;
+      }
       u32x2 h0, l0, h1, l1;
       split4(v0, h0, l0);
       split4(v1, h1, l1);
@@ -1236,6 +1247,16 @@ __global__ __launch_bounds__(256) void warp_adjoint_split8_kernel(const AdjArgs 
     }
 }
 
+// fp32 rows [n][W] -> MVBEV_LAYOUT_SPLIT_ROWS [n][W / 8][hi 8, lo 8] (W % 8 == 0), the rounding
+// of store_split8 / split4 (hi = RNE bf16, lo = RNE bf16 of the remainder)
+__global__ void split_rows_kernel(const floatx4* __restrict__ x, int64_t runs, u32x4_t* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= runs) return;
+  const floatx4 a = x[2 * i], b = x[2 * i + 1];
+  const float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  store_split8(out + 2 * i, v);
+}
+
 // ---------------------------------------------------------------------------------------------
 // wgrad launch geometry
 static int cu_count() {
@@ -1294,9 +1315,33 @@ int mvbev_conv3x3_wgrad_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_
                                   int64_t Cout, int dilation, const int32_t* chan_map, int64_t Cin_w,
                                   float* dw, const int32_t* chunk_list, const int32_t* chunk_off,
                                   void* workspace, size_t workspace_bytes, void* stream) {
+  return mvbev_conv3x3_wgrad_bf16x3_ex2(x, x_layout, d, dy, MVBEV_LAYOUT_F32, Cout, dilation, chan_map, Cin_w, dw,
+                                        chunk_list, chunk_off, workspace, workspace_bytes, stream);
+}
+
+int mvbev_split_rows_bf16(const float* x, int64_t rows, int64_t W, void* out, void* stream) {
+  using namespace mvbev;
+  if (!x || !out) return MVBEV_ERR_NULL;
+  if (rows <= 0 || W <= 0) return MVBEV_ERR_RANK;
+  if (W % 8 != 0) return MVBEV_ERR_SHAPE;
+  if ((reinterpret_cast<uintptr_t>(x) & 15) != 0 || (reinterpret_cast<uintptr_t>(out) & 15) != 0)
+    return MVBEV_ERR_ALIGN;
+  const int64_t runs = rows * (W / 8);
+  hipLaunchKernelGGL(bwd::split_rows_kernel, dim3((unsigned)ceil_div(runs, 256)), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const bwd::floatx4*>(x), runs, static_cast<u32x4_t*>(out));
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+int mvbev_conv3x3_wgrad_bf16x3_ex2(const void* x, int x_layout, const mvbev_conv_desc* d, const void* dy_,
+                                   int dy_layout, int64_t Cout, int dilation, const int32_t* chan_map,
+                                   int64_t Cin_w, float* dw, const int32_t* chunk_list, const int32_t* chunk_off,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
   using namespace mvbev;
   using namespace mvbev::bwd;
+  const float* dy = static_cast<const float*>(dy_);  // SPLIT_ROWS: the same bytes per row
   if (!x || !d || !dy || !dw || !workspace) return MVBEV_ERR_NULL;
+  if (dy_layout != MVBEV_LAYOUT_F32 && dy_layout != MVBEV_LAYOUT_SPLIT_ROWS) return MVBEV_ERR_SHAPE;
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || Cin_w <= 0 || d->group <= 0)
     return MVBEV_ERR_RANK;
   if (Cout % MT != 0 || Cout > 65535 || d->K % 8 != 0 || d->group % 8 != 0 || d->K % d->group != 0)
@@ -1328,8 +1373,11 @@ int mvbev_conv3x3_wgrad_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_
   const bool dma_fits = d->B < 128 && d->H <= 4096 && a.segs <= 4096 && d->batch_stride % 8 == 0 &&
                         d->group_stride % 8 == 0 && Cout * d->H * d->W < INT32_MAX &&
                         coff_max / 4 + 2 * d->H * d->W < INT32_MAX;
-  if (MVBEV_WGRAD_DMA && split && a.vec_dy && dma_fits && (dilation == 1 || dilation == 2) &&
-      g.nchunks / g.P + 1 <= WG_MAXC) {
+  const bool dma = MVBEV_WGRAD_DMA && split && a.vec_dy && dma_fits && (dilation == 1 || dilation == 2) &&
+                   g.nchunks / g.P + 1 <= WG_MAXC;
+  a.dy_rows = dy_layout == MVBEV_LAYOUT_SPLIT_ROWS;
+  if (a.dy_rows && (!dma || d->W % 8 != 0)) return MVBEV_ERR_SHAPE;  // pre-split rows: the DMA kernel only
+  if (dma) {
     if (dilation == 1) hipLaunchKernelGGL((wgrad_dma_kernel<1>), grid, dim3(NTH), 0, s, a);
     else hipLaunchKernelGGL((wgrad_dma_kernel<2>), grid, dim3(NTH), 0, s, a);
   } else if (dilation == 1) {

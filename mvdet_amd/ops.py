@@ -731,17 +731,47 @@ def wgrad_chunk_lists(mask: torch.Tensor, groups: int, B: int, H: int, W: int):
             torch.tensor(off, dtype=torch.int32, device=dev))
 
 
+def split_rows_shape(B: int, C: int, H: int, W: int):
+    """Shape of the row-split bf16 layout (MVBEV_LAYOUT_SPLIT_ROWS) of a [B,C,H,W] tensor:
+    per (channel, row, 8-pixel run) bf16 hi[8] then lo[8]."""
+    return (B, C, H, W // 8, 2, 8)
+
+
+def split_rows(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 [B,C,H,W] (contiguous, W % 8 == 0) -> its row-split bf16 form (``split_rows_shape``),
+    hi = bf16(x), lo = bf16(x - hi): the conv weight gradient's pre-split dy."""
+    _require_cuda(x)
+    if x.dim() != 4 or x.dtype != torch.float32 or not x.is_contiguous() or x.shape[3] % 8:
+        raise ValueError("split_rows needs a contiguous float32 [B,C,H,W] tensor with W % 8 == 0")
+    B, C, H, W = x.shape
+    if out is None:
+        out = torch.empty(split_rows_shape(B, C, H, W), dtype=torch.bfloat16, device=x.device)
+    elif tuple(out.shape) != split_rows_shape(B, C, H, W) or out.dtype != torch.bfloat16 or not out.is_contiguous():
+        raise ValueError("out must be a contiguous bf16 tensor of split_rows_shape")
+    st = _native.load().mvbev_split_rows_bf16(x.data_ptr(), B * C * H, W, out.data_ptr(), _stream(x))
+    _native.check(st, "mvbev_split_rows_bf16")
+    return out
+
+
 def conv3x3_wgrad(x: torch.Tensor, desc, dy: torch.Tensor, dilation: int, cin_w: int,
                   chan_map: Optional[torch.Tensor] = None, dw: Optional[torch.Tensor] = None,
-                  workspace: Optional[torch.Tensor] = None, chunk_lists=None) -> torch.Tensor:
+                  workspace: Optional[torch.Tensor] = None, chunk_lists=None,
+                  dy_rows: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Weight gradient of a 3x3 conv whose input ``x`` is addressed by ``desc`` (fp32, or the
     split-bf16 layout when ``x`` is bf16) and whose output gradient is ``dy`` [B,Cout,H,W] fp32:
     writes dw[co][chan_map[k]][:] (identity without a map) of a [Cout, cin_w, 3, 3] tensor
-    (allocated zeroed when ``dw`` is None; unmapped channels are left as they are)."""
+    (allocated zeroed when ``dw`` is None; unmapped channels are left as they are).
+    ``dy_rows``: optionally dy's ``split_rows`` form, which the LDS-DMA kernel reads instead
+    of splitting dy itself (bitwise the same dw; used where that kernel applies, else dy)."""
     _require_cuda(x, dy)
     if dy.dim() != 4 or dy.dtype != torch.float32 or not dy.is_contiguous():
         raise ValueError("dy must be a contiguous float32 [B,Cout,H,W] tensor")
     B, cout, H, W = dy.shape
+    if dy_rows is not None:
+        _require_cuda(dy_rows)
+        if (tuple(dy_rows.shape) != split_rows_shape(B, cout, H, W) or dy_rows.dtype != torch.bfloat16
+                or not dy_rows.is_contiguous()):
+            raise ValueError("dy_rows must be dy's split_rows form")
     if (desc.B, desc.H, desc.W) != (B, H, W):
         raise ValueError("dy does not match the conv descriptor")
     if x.dtype == torch.float32:
@@ -763,11 +793,17 @@ def conv3x3_wgrad(x: torch.Tensor, desc, dy: torch.Tensor, dilation: int, cin_w:
     if workspace is None or workspace.numel() * workspace.element_size() < need:
         workspace = torch.empty((need + 3) // 4, dtype=torch.float32, device=dy.device)
     cl, co = (None, None) if chunk_lists is None else (chunk_lists[0].data_ptr(), chunk_lists[1].data_ptr())
-    st = lib.mvbev_conv3x3_wgrad_bf16x3_ex(x.data_ptr(), layout, ctypes.byref(desc), dy.data_ptr(), cout,
-                                           int(dilation), None if chan_map is None else chan_map.data_ptr(),
-                                           cin_w, dw.data_ptr(), cl, co, workspace.data_ptr(),
-                                           workspace.numel() * workspace.element_size(), _stream(dy))
-    _native.check(st, "mvbev_conv3x3_wgrad_bf16x3_ex")
+    for d, dl in ((dy_rows, _native.LAYOUT_SPLIT_ROWS), (dy, _native.LAYOUT_F32)):
+        if d is None:
+            continue
+        st = lib.mvbev_conv3x3_wgrad_bf16x3_ex2(x.data_ptr(), layout, ctypes.byref(desc), d.data_ptr(), dl, cout,
+                                                int(dilation), None if chan_map is None else chan_map.data_ptr(),
+                                                cin_w, dw.data_ptr(), cl, co, workspace.data_ptr(),
+                                                workspace.numel() * workspace.element_size(), _stream(dy))
+        if st == _native.ERR_SHAPE and dl == _native.LAYOUT_SPLIT_ROWS:
+            continue  # not the LDS-DMA path (nothing was launched): the fp32 dy
+        _native.check(st, "mvbev_conv3x3_wgrad_bf16x3_ex2")
+        break
     return dw
 
 

@@ -213,6 +213,55 @@ def test_conv_wgrad_grouped_slab_with_channel_map():
         assert (dw[:, S * C:] == 9.0).all()
 
 
+def test_split_rows_rounding():
+    """mvbev_split_rows_bf16: hi = bf16(x) (round to nearest even), lo = bf16(x - hi), per
+    (channel, row, 8-pixel run) hi[8] then lo[8]; W % 8 != 0 rejected."""
+    from mvdet_amd import _native, ops
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn((2, 3, 5, 24), generator=g) * torch.logspace(-8, 8, 24)
+    r = ops.split_rows(x.to(DEV)).cpu()
+    assert tuple(r.shape) == ops.split_rows_shape(2, 3, 5, 24)
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.float()).to(torch.bfloat16)
+    assert torch.equal(r[..., 0, :].reshape(x.shape), hi)
+    assert torch.equal(r[..., 1, :].reshape(x.shape), lo)
+    with pytest.raises(ValueError):
+        ops.split_rows(torch.zeros((1, 1, 2, 12), device=DEV))
+    st = _native.load().mvbev_split_rows_bf16(x.to(DEV).data_ptr(), 2, 12, r.to(DEV).data_ptr(), None)
+    assert st == _native.ERR_SHAPE
+
+
+@pytest.mark.parametrize("B,K,H,W,dil,lists", [(1, 64, 12, 40, 1, False), (2, 72, 13, 48, 2, False),
+                                               (2, 192, 37, 96, 1, True)])
+def test_conv_wgrad_presplit_dy_rows(B, K, H, W, dil, lists):
+    """The LDS-DMA wgrad reading dy pre-split into bf16 rows (ops.split_rows, the training
+    step's form) gives bitwise the dw of the same kernel splitting an fp32 dy itself, and
+    matches torch; where that kernel does not apply (fp32 x) the fp32 dy is used instead."""
+    from mvdet_amd import _native, ops
+    g = torch.Generator().manual_seed(K + W)
+    cout = 128
+    x = F.relu(torch.randn((B, K, H, W), generator=g))
+    dy = torch.randn((B, cout, H, W), generator=g)
+    ref = torch.nn.grad.conv2d_weight(x.double(), (cout, K, 3, 3), dy.double(), padding=dil, dilation=dil)
+    d = ops.conv_desc(B, K, H, W, group=K if not lists else 64, group_stride=0 if not lists else B * 64 * H * W,
+                      batch_stride=K * H * W if not lists else 64 * H * W)
+    if lists:  # three 64-channel groups (camera slots) with chunk lists from a frustum-like mask
+        xs = torch.stack([_split_encode(x[:, 64 * s_:64 * (s_ + 1)].contiguous().to(DEV)) for s_ in range(3)])
+        th, tw = _native.TILE_H, _native.TILE_W
+        mask = torch.full(((-(-H // th)) * (-(-W // tw)),), 7, dtype=torch.int32)
+        cl = ops.wgrad_chunk_lists(mask.to(DEV), 3, B, H, W)
+    else:
+        xs, cl = _split_encode(x.to(DEV)), None
+    dyd = dy.to(DEV)
+    a = ops.conv3x3_wgrad(xs, d, dyd, dil, K, chunk_lists=cl)
+    b = ops.conv3x3_wgrad(xs, d, dyd, dil, K, chunk_lists=cl, dy_rows=ops.split_rows(dyd))
+    assert torch.equal(a, b)
+    assert_parity(b.cpu(), ref, "wgrad from pre-split dy rows")
+    if not lists:  # fp32 x: the register kernel, which reads the fp32 dy
+        c = ops.conv3x3_wgrad(x.to(DEV), d, dyd, dil, K, dy_rows=ops.split_rows(dyd))
+        assert_parity(c.cpu(), ref, "wgrad, fp32 x, dy_rows ignored")
+
+
 @pytest.mark.parametrize("split", [False, True])
 def test_conv_wgrad_frustum_chunk_lists(split):
     """conv1's wgrad with per-group chunk lists from a frustum mask: skipping the chunks whose

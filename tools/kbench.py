@@ -64,11 +64,20 @@ def backward_stages(eng, ws, mc, B, ho, wo, N, C, dev):
     d_y1 = ops.conv_desc(B, mid, ho, wo, group=mid, group_stride=0, batch_stride=mid * ho * wo)
     wws2 = autograd._wgrad_ws(st, d_y1, mid, dev)
     flop2 = 2.0 * B * ho * wo * 9 * mid * mid
+    # the training step's form: dy pre-split into bf16 rows (timed with the split) where W % 8 == 0
+    rows1 = torch.empty(ops.split_rows_shape(B, w1.shape[0], ho, wo), dtype=torch.bfloat16, device=dev)
+    rows2 = torch.empty(ops.split_rows_shape(B, mid, ho, wo), dtype=torch.bfloat16, device=dev)
+    pre = wo % 8 == 0
     return {
-        "wgrad2": (lambda: ops.conv3x3_wgrad(y1s, d_y1, dy2, 2, mid, workspace=wws2), flop2),
+        "wgrad2": (lambda: ops.conv3x3_wgrad(y1s, d_y1, dy2, 2, mid, workspace=wws2,
+                                             dy_rows=ops.split_rows(dy2, out=rows2) if pre else None), flop2),
+        "wgrad2f": (lambda: ops.conv3x3_wgrad(y1s, d_y1, dy2, 2, mid, workspace=wws2), flop2),
         "dgrad2": (lambda: ops.conv3x3_dgrad(dy2s, st.dgrad2, w2, 2), flop2),
         "wgrad1": (lambda: ops.conv3x3_wgrad(ws.slab, d1, dy1, 1, w1.shape[1], chan_map=eng.pack1._map_dev,
-                                             dw=dw1, workspace=wws, chunk_lists=lists), flop),
+                                             dw=dw1, workspace=wws, chunk_lists=lists,
+                                             dy_rows=ops.split_rows(dy1, out=rows1) if pre else None), flop),
+        "wgrad1f": (lambda: ops.conv3x3_wgrad(ws.slab, d1, dy1, 1, w1.shape[1], chan_map=eng.pack1._map_dev,
+                                              dw=dw1, workspace=wws, chunk_lists=lists), flop),  # fp32 dy
         "dgrad1": (lambda: ops.conv3x3_dgrad(dy1, st.dgrad1, w1, 1, out=dslab, out_mask=cm,
                                              cot_per_group=C // ops.BN), flop),
     }
@@ -123,7 +132,7 @@ def main():
             stages["adjup"] = ((lambda: ops.warp_views_adjoint(douts, plu, gs)), None)
             pl = [ops.WarpAdjointPlan(eng.m_norm_cpu[v], up, (ho, wo), dev) for v in range(N)]
             stages["adj"] = ((lambda: ops.warp_views_adjoint(douts, pl, gsu)), None)
-        if {"wgrad1", "dgrad1", "wgrad2", "dgrad2"} & set(args.only.split(",")):
+        if {"wgrad1", "wgrad1f", "dgrad1", "wgrad2", "wgrad2f", "dgrad2"} & set(args.only.split(",")):
             stages.update(backward_stages(eng, ws, mc, B, ho, wo, N, C, dev))
         from mvdet_amd import _native
         libs = [("default", _native.load())]

@@ -1194,8 +1194,12 @@ __global__ __launch_bounds__(256) void warp_adjoint_split_kernel(const AdjArgs a
 // 8 groups (64 channels), a half-wave = 32 consecutive pixels of one group (coalesced stores).
 // Each thread's chain of dependent gathers is one channel group's instead of a 32-channel
 // chunk's (4x shorter), and a pixel's entries are shared by its 8 group threads.
-constexpr int kAsPix = 32, kAsGroups = 8;
-__global__ __launch_bounds__(256) void warp_adjoint_split8_kernel(const AdjArgs a) {
+// PIX pixels x 8 groups per workgroup: 32 for the warp plan (<= 4 entries per source pixel),
+// 16 where source pixels carry many entries (the S.U plan: 0.69 -> 0.58 ms at cfg2; 64: 0.85)
+constexpr int kAsGroups = 8;
+template <int PIX>
+__global__ __launch_bounds__(PIX * kAsGroups) void warp_adjoint_split8_kernel(const AdjArgs a) {
+  constexpr int kAsPix = PIX;
   const int lb = xcd_remap(blockIdx.x, a.nwg);
   const int pb = lb % a.pblocks;
   int r = lb / a.pblocks;
@@ -1204,7 +1208,7 @@ __global__ __launch_bounds__(256) void warp_adjoint_split8_kernel(const AdjArgs 
   const int view = r % a.nviews;
   const int b = r / a.nviews;
   const int p = pb * kAsPix + (threadIdx.x & (kAsPix - 1));
-  const int c = (chunk * kAsGroups + (threadIdx.x >> 5)) * 8;
+  const int c = (chunk * kAsGroups + threadIdx.x / kAsPix) * 8;
   if (p >= a.P || c >= a.C) return;
   const AdjView& vw = a.v[view];
   const int e0 = vw.rp[p], e1 = vw.rp[p + 1];
@@ -1574,14 +1578,21 @@ int mvbev_warp_views_adjoint(const mvbev_warp_adjoint_view* views, int nviews, i
   a.nviews = nviews;
   a.B = (int)B; a.C = (int)C; a.P = (int)(H * W);
   const bool g8 = split && MVBEV_ADJ_G8;
-  a.pblocks = (int)ceil_div(H * W, g8 ? bwd::kAsPix : 256);
+  // many entries per source pixel (a source smaller than the grid: the S.U plan): 16 pixels
+  const int pix = H * W < Ho * Wo ? 16 : 32;
+  a.pblocks = (int)ceil_div(H * W, g8 ? pix : 256);
   a.chunks = (int)ceil_div(C, g8 ? 8 * bwd::kAsGroups : bwd::kAdjCPB);
   a.accumulate = accumulate ? 1 : 0;
   const int64_t nwg = (int64_t)a.pblocks * a.chunks * nviews * B;
   if (nwg > INT32_MAX) return MVBEV_ERR_SHAPE;
   a.nwg = (int)nwg;
   if (g8)
-    hipLaunchKernelGGL(bwd::warp_adjoint_split8_kernel, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
+    if (pix == 16)
+      hipLaunchKernelGGL(bwd::warp_adjoint_split8_kernel<16>, dim3((unsigned)nwg), dim3(16 * bwd::kAsGroups), 0,
+                         as_stream(stream), a);
+    else
+      hipLaunchKernelGGL(bwd::warp_adjoint_split8_kernel<32>, dim3((unsigned)nwg), dim3(32 * bwd::kAsGroups), 0,
+                         as_stream(stream), a);
   else if (split)
     hipLaunchKernelGGL(bwd::warp_adjoint_split_kernel, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
   else

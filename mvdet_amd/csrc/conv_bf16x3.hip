@@ -712,8 +712,18 @@ __global__ void cout1_reduce_kernel(const float* __restrict__ p3, int nsets, int
   map[((int64_t)b * map_rows + qr) * W + c] = acc;
 }
 
+#ifndef MVBEV_RING_STAMP
+#define MVBEV_RING_STAMP 0  // diagnostics build only: per-block (start, end, HW_ID, XCC_ID) in g_ring_stamps
+#endif
+#if MVBEV_RING_STAMP
+__device__ uint32_t g_ring_stamps[16384 * 4];
+#endif
+
 template <int DIL, bool RELU, bool P3 = false>
 __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
+#if MVBEV_RING_STAMP
+  const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
+#endif
   using G = RingGeo<DIL>;
   constexpr int XW = G::XW, XPIX = G::XPIX, NX = G::NX, XBUF = G::XBUF;
   __shared__ __attribute__((aligned(16))) u32x4 lds[G::LDS];
@@ -1004,6 +1014,16 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
       for (int pt = 0; pt < 3; ++pt)
         store_block<RELU>(a, b, y0 + base + pt * DIL, x0 + l32, cot * BN + cw + 32 * ct, acc[ct][pt]);
   }
+#if MVBEV_RING_STAMP
+  if (threadIdx.x == 0 && blockIdx.x < 16384) {  // vector stores of the block's wall-clock span and place
+    const uint64_t stamp1 = __builtin_amdgcn_s_memrealtime();
+    uint32_t* d = g_ring_stamps + 4 * blockIdx.x;
+    d[0] = (uint32_t)stamp0;
+    d[1] = (uint32_t)stamp1;
+    d[2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID: wave, SIMD, CU, SH, SE
+    d[3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+  }
+#endif
 }
 
 #ifndef MVBEV_B3_RING
@@ -1294,4 +1314,10 @@ int mvbev_conv3x3_dgrad_bf16x3(const float* dy, const mvbev_conv_desc* desc, con
                                        cot_per_group, stream);
 }
 
+#if MVBEV_RING_STAMP
+int mvbev_debug_ring_stamps(void* host_out, int n) {
+  if (n > 16384 * 4) n = 16384 * 4;
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(mvbev::b3::g_ring_stamps), sizeof(uint32_t) * n) == hipSuccess ? 0 : -1;
+}
+#endif
 }  // extern "C"

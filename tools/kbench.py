@@ -53,7 +53,13 @@ def backward_stages(eng, ws, mc, B, ho, wo, N, C, dev):
     lists = autograd._wgrad_lists(eng, st, dev, B)
     cp = st.dgrad1.cout_p
     dslab = torch.empty(ops.split_shape(B, cp, ho, wo), dtype=torch.bfloat16, device=dev)
-    cm = eng.conv1_mask(dev, 0, ho, tile_h=_native.TILE_H)
+    # the training step's dgrad input: dy1 also split-bf16 (relu_backward_split_ with y1 > 0
+    # everywhere), so the ring kernel runs, with its 12-row output mask
+    y1_pos = torch.zeros(ops.split_shape(B, w1.shape[0], ho, wo), dtype=torch.bfloat16, device=dev)
+    y1_pos[..., 0, :] = 1.0
+    dy1s = torch.empty_like(y1_pos)
+    ops.relu_backward_split_(dy1, y1_pos, dy1s)
+    cm = eng.conv1_mask(dev, 0, ho, tile_h=ops.dgrad_tile_rows(True, 1))
     flop = 2.0 * B * ho * wo * 9 * N * C * w1.shape[0]
     # conv2 (d2) on a split y1 and a random dy2, as the training step's conv2 backward
     w2 = mc[2].weight
@@ -78,7 +84,7 @@ def backward_stages(eng, ws, mc, B, ho, wo, N, C, dev):
                                              dy_rows=ops.split_rows(dy1, out=rows1) if pre else None), flop),
         "wgrad1f": (lambda: ops.conv3x3_wgrad(ws.slab, d1, dy1, 1, w1.shape[1], chan_map=eng.pack1._map_dev,
                                               dw=dw1, workspace=wws, chunk_lists=lists), flop),  # fp32 dy
-        "dgrad1": (lambda: ops.conv3x3_dgrad(dy1, st.dgrad1, w1, 1, out=dslab, out_mask=cm,
+        "dgrad1": (lambda: ops.conv3x3_dgrad(dy1s, st.dgrad1, w1, 1, out=dslab, out_mask=cm,
                                              cot_per_group=C // ops.BN), flop),
     }
 

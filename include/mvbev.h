@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -318,6 +318,36 @@ typedef struct mvbev_warp_adjoint_view {
 int mvbev_warp_views_adjoint(const mvbev_warp_adjoint_view* views, int nviews, int grad_out_layout, int64_t B,
                              int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int accumulate,
                              void* stream);
+
+/* A host-built schedule for the LDS-DMA ring kernel (split-bf16 input, dilation 1 or 2): block i
+ * runs items[i] = {tile, c0, c1, slot} — tile = ((b * tiles_y + ty) * tiles_x + tx) * n_cot + cot
+ * (12-row tiles, mvbev_conv3x3_bf16x3_tile_rows), chunks [c0, c1) of the tile's active 16-channel
+ * chunk sequence (all of K, or the groups a group_mask enables, in order), slot = -1 for a
+ * whole tile or the partial-sum slot of a piece of a split tile; tile < 0 = an idle block.
+ * fixups[f] = {tile, first slot, pieces, 0}: after the conv, one block per split tile adds its
+ * pieces' partial sums in slot order (deterministic) and writes the tile as the kernel would.
+ * The order of items is the dispatch order (block i goes to XCD i % 8); the host plans it to
+ * balance the CUs (mvdet_amd/schedule.py: e.g. splitting the last, partial round's tiles). */
+typedef struct mvbev_conv_schedule {
+  const int32_t* items;    /* device [nitems][4], 16-B aligned */
+  int32_t nitems;
+  const int32_t* fixups;   /* device [nfix][4], 16-B aligned */
+  int32_t nfix;
+  int32_t nslots;          /* partial slots the items use: 0 .. nslots - 1 */
+  void* partials;          /* device, >= nslots * mvbev_conv_schedule_slot_bytes() */
+  size_t partial_bytes;
+} mvbev_conv_schedule;
+size_t mvbev_conv_schedule_slot_bytes(void);
+/* mvbev_conv3x3_bf16x3_ex (split-bf16 x only) and mvbev_conv3x3_dgrad_bf16x3_ex (split-bf16 dy
+ * only) run as scheduled (tile_order is replaced by the items). */
+int mvbev_conv3x3_bf16x3_sched(const void* x, int x_layout, const mvbev_conv_desc* desc, const void* w_packed,
+                               const float* bias, const float* init, int64_t Cout, int dilation, int relu, void* y,
+                               int y_layout, const uint32_t* group_mask, const mvbev_conv_schedule* sched,
+                               void* stream);
+int mvbev_conv3x3_dgrad_bf16x3_sched(const void* dy, int dy_layout, const mvbev_conv_desc* desc,
+                                     const void* w_packed, int64_t Cout_p, int dilation, void* dx, int dx_layout,
+                                     const uint32_t* out_mask, int64_t cot_per_group,
+                                     const mvbev_conv_schedule* sched, void* stream);
 
 /* Weights for the data gradient of a 3x3 stride-1 conv with padding = dilation: that gradient is
  * the same conv over dy with w'[k][co][t] = w[co][k][8 - t], so mvbev_conv3x3_bf16x3_ex computes

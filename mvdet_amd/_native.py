@@ -60,6 +60,9 @@ EXPORTS = (
     "mvbev_warp_upsampled_adjoint_plan",
     "mvbev_conv3x3_wgrad_bf16x3_ex2",
     "mvbev_split_rows_bf16",
+    "mvbev_conv_schedule_slot_bytes",
+    "mvbev_conv3x3_bf16x3_sched",
+    "mvbev_conv3x3_dgrad_bf16x3_sched",
 )
 WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
 ERR_SHAPE = -2  # MVBEV_ERR_SHAPE
@@ -93,6 +96,13 @@ class WarpAdjointView(ctypes.Structure):
     _fields_ = [("grad_out", ctypes.c_void_p), ("grad_out_strides", ctypes.c_int64 * 4),
                 ("grad_src", ctypes.c_void_p), ("grad_src_strides", ctypes.c_int64 * 4),
                 ("row_ptr", ctypes.c_void_p), ("col", ctypes.c_void_p), ("val", ctypes.c_void_p)]
+
+
+class ConvSchedule(ctypes.Structure):
+    """``mvbev_conv_schedule`` (include/mvbev.h)."""
+    _fields_ = [("items", ctypes.c_void_p), ("nitems", ctypes.c_int32), ("fixups", ctypes.c_void_p),
+                ("nfix", ctypes.c_int32), ("nslots", ctypes.c_int32), ("partials", ctypes.c_void_p),
+                ("partial_bytes", ctypes.c_size_t)]
 
 
 class NativeError(RuntimeError):
@@ -177,6 +187,16 @@ def _declare(lib):
                                                    _i64, ctypes.c_int, _p, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]
     lib.mvbev_split_rows_bf16.restype = ctypes.c_int
     lib.mvbev_split_rows_bf16.argtypes = [_p, _i64, _i64, _p, _p]
+    lib.mvbev_conv_schedule_slot_bytes.restype = ctypes.c_size_t
+    lib.mvbev_conv_schedule_slot_bytes.argtypes = []
+    lib.mvbev_conv3x3_bf16x3_sched.restype = ctypes.c_int
+    lib.mvbev_conv3x3_bf16x3_sched.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64,
+                                               ctypes.c_int, ctypes.c_int, _p, ctypes.c_int, _p,
+                                               ctypes.POINTER(ConvSchedule), _p]
+    lib.mvbev_conv3x3_dgrad_bf16x3_sched.restype = ctypes.c_int
+    lib.mvbev_conv3x3_dgrad_bf16x3_sched.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _i64,
+                                                     ctypes.c_int, _p, ctypes.c_int, _p, _i64,
+                                                     ctypes.POINTER(ConvSchedule), _p]
     lib.mvbev_conv3x3_dgrad_bf16x3.restype = ctypes.c_int
     lib.mvbev_conv3x3_dgrad_bf16x3.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _i64, ctypes.c_int, _p,
                                                ctypes.c_int, _p, _i64, _p]

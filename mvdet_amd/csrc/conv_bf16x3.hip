@@ -131,6 +131,14 @@ struct Args {
   // y may then be null (not stored)
   const float* w3;
   float* p3;
+  // ring kernel schedule (optional, mvbev_conv_schedule): block i runs items[i] = (tile, first
+  // chunk, end chunk of the tile's active-chunk sequence, partial slot or -1); split tiles'
+  // raw partial sums (slots of kRingSlotF4 floatx4) are finished by conv_ring_fixup_kernel from
+  // fix[f] = (tile, first slot, pieces)
+  const int4* items;
+  int nitems;
+  const int4* fix;
+  int nfix;
 };
 
 // Input tag: the split-bf16 blocked layout written by mvbev_warp_views_split_bf16 and by this
@@ -712,6 +720,71 @@ __global__ void cout1_reduce_kernel(const float* __restrict__ p3, int nsets, int
   map[((int64_t)b * map_rows + qr) * W + c] = acc;
 }
 
+// The ring kernel's output of a finished tile: rows row_base + pt * DIL (pt < 3) of this wave,
+// the lane's column, output channels cot * BN + cw + 32 ct (+ the fused Cout-1 partials).
+template <int DIL, bool RELU, bool P3>
+__device__ __attribute__((always_inline)) inline void ring_epilogue(const Args& a, int b, int row_base, int col,
+                                                                   int cot, int cw, const floatx16 (&acc)[2][3],
+                                                                   u32x4* lds) {
+  if constexpr (P3) {
+    cout1_partials<RELU>(a, b, row_base, DIL, col, cot, cw, acc, lds);
+  } else {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int pt = 0; pt < 3; ++pt)
+        store_block<RELU>(a, b, row_base + pt * DIL, col, cot * BN + cw + 32 * ct, acc[ct][pt]);
+  }
+}
+
+// split tiles' raw partial sums: slot s = [24 floatx4 of a thread's 96 accumulators][RNT threads]
+constexpr int kRingSlotF4 = 24 * RNT;
+__device__ inline void ring_store_partial(float* ws, int slot, const floatx16 (&acc)[2][3]) {
+  floatx4* p = reinterpret_cast<floatx4*>(ws) + (int64_t)slot * kRingSlotF4 + threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        p[((i * 3 + j) * 4 + q) * RNT] = floatx4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2],
+                                                  acc[i][j][4 * q + 3]};
+}
+
+// Finishes split tiles: block f sums fix[f]'s pieces in K order (deterministic) and writes the
+// tile with the ring kernel's own epilogue.
+template <int DIL, bool RELU, bool P3>
+__global__ __launch_bounds__(RNT) void conv_ring_fixup_kernel(const Args a) {
+  __shared__ __attribute__((aligned(16))) u32x4 lds[P3 ? 10 * BN / 4 : 1];  // cout1_partials' w3 + bias
+  const int4 f = a.fix[blockIdx.x];
+  floatx16 acc[2][3];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = floatx16{0};
+  for (int piece = 0; piece < f.z; ++piece) {
+    const floatx4* p = reinterpret_cast<const floatx4*>(a.sk_ws) + (int64_t)(f.y + piece) * kRingSlotF4 + threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const floatx4 v = p[((i * 3 + j) * 4 + q) * RNT];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] += v[e];
+        }
+  }
+  const int tile = f.x, cot = tile % a.n_cot;
+  int rest = tile / a.n_cot;
+  const int tx = rest % a.tiles_x;
+  rest /= a.tiles_x;
+  const int ty = rest % a.tiles_y, b = rest / a.tiles_y;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l32 = threadIdx.x & 31;
+  ring_epilogue<DIL, RELU, P3>(a, b, a.out_row0 + ty * RT + ring_base_row<DIL>(wave & 3), tx * TW + l32, cot,
+                               64 * (wave >> 2), acc, lds);
+}
+
 #ifndef MVBEV_RING_STAMP
 #define MVBEV_RING_STAMP 0  // diagnostics build only: per-block (start, end, HW_ID, XCC_ID) in g_ring_stamps
 #endif
@@ -737,7 +810,13 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
   const int64_t wchunk = (int64_t)a.n_cot * W16;
 
   int tile = xcd_remap(blockIdx.x, a.nwg);
-  if (a.gmask) {  // frustum mask: ordered pixel tiles dealt to the XCDs (see conv_kernel)
+  int ci0 = 0, ci1 = INT_MAX, pslot = -1;  // chunk range of this block, partial slot
+  if (a.items) {  // host schedule: the item of this block (tile < 0: padding)
+    if ((int)blockIdx.x >= a.nitems) return;
+    const int4 it = a.items[blockIdx.x];
+    if (it.x < 0) return;
+    tile = it.x, ci0 = it.y, ci1 = it.z, pslot = it.w;
+  } else if (a.gmask) {  // frustum mask: ordered pixel tiles dealt to the XCDs (see conv_kernel)
     constexpr int Gq = MVBEV_MASK_GROUP;
     const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
     const int q = j / a.n_cot;
@@ -757,8 +836,12 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
   if (a.cmask && !((a.cmask[ty * a.tiles_x + tx] >> (cot / a.cot_pg)) & 1u)) return;
   const u32x4* wsrc = a.wp + (int64_t)cot * W16;
   const uint32_t gm = a.gmask ? a.gmask[ty * a.tiles_x + tx] : 0u;
-  const int nch = a.gmask ? __builtin_popcount(gm) * a.cpg : a.nchunks;
-  auto chunk_of = [&](int i) -> int {
+  // this block's chunks: [ci0, ci1) of the tile's active-chunk sequence (all of it unscheduled)
+  const int nch_tile = a.gmask ? __builtin_popcount(gm) * a.cpg : a.nchunks;
+  ci1 = min(ci1, nch_tile);
+  const int nch = max(ci1 - ci0, 0);
+  auto chunk_of = [&](int i) -> int {  // physical chunk of the block's i-th chunk
+    i += ci0;
     if (!a.gmask) return i;
     uint32_t m = gm;
     for (int j = i / a.cpg; j > 0; --j) m &= m - 1;
@@ -831,10 +914,11 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
   // computed fetches chunk ci + 1 (W(u + 3) and the next halo).  Advanced branch-free (scalar
   // selects) once per chunk, so the unit body stays one basic block for the scheduler; past
   // the last chunk it stays at the last one (dummy loads that keep the vmcnt counts exact).
-  int nx_i = 1, nx_sub = a.gmask ? 1 % a.cpg : 0;
+  int nx_i = 1, nx_sub = a.gmask ? (ci0 + 1) % a.cpg : 0;
   int nx_ph = chunk_of(min(1, nch - 1));
-  uint32_t nx_m = gm;
-  if (a.gmask && a.cpg == 1) nx_m &= nx_m - 1;
+  uint32_t nx_m = gm;  // lowest set bit = the group of sequence chunk ci0 + 1
+  if (a.gmask)
+    for (int j = (ci0 + 1) / a.cpg; j > 0; --j) nx_m &= nx_m - 1;
   auto advance = [&]() __attribute__((always_inline)) {
     const bool more = nx_i + 1 < nch;
     const bool wrap = a.gmask && nx_sub + 1 == a.cpg;
@@ -1005,14 +1089,10 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the block exits
   }
 
-  if constexpr (P3) {
-    cout1_partials<RELU>(a, b, y0 + base, DIL, x0 + l32, cot, cw, acc, lds);
+  if (pslot >= 0) {
+    ring_store_partial(a.sk_ws, pslot, acc);  // a piece of a split tile: conv_ring_fixup_kernel finishes it
   } else {
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-      for (int pt = 0; pt < 3; ++pt)
-        store_block<RELU>(a, b, y0 + base + pt * DIL, x0 + l32, cot * BN + cw + 32 * ct, acc[ct][pt]);
+    ring_epilogue<DIL, RELU, P3>(a, b, y0 + base, x0 + l32, cot, cw, acc, lds);
   }
 #if MVBEV_RING_STAMP
   if (threadIdx.x == 0 && blockIdx.x < 16384) {  // vector stores of the block's wall-clock span and place
@@ -1082,7 +1162,8 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
                   const float* bias, const float* init, int64_t Cout, int dilation, int relu,
                   float* y, int y_layout, const uint32_t* group_mask, const int32_t* tile_order,
                   void* workspace, size_t ws_bytes, void* stream, const uint32_t* out_mask = nullptr,
-                  int cot_pg = 1, const float* w3 = nullptr, float* p3 = nullptr) {
+                  int cot_pg = 1, const float* w3 = nullptr, float* p3 = nullptr,
+                  const mvbev_conv_schedule* sched = nullptr) {
   if (!x || !d || !w_packed || (!y && !p3) || (!w3 != !p3)) return MVBEV_ERR_NULL;
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || d->in_rows <= 0 ||
       d->out_rows <= 0 || d->group <= 0)
@@ -1132,8 +1213,25 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   a.sk_ws = sk ? static_cast<float*>(workspace) : nullptr;
   a.dp_tiles = (int)(sk ? plan.dp_tiles : tiles);
   a.split = sk ? plan.split : 1;
-  const int64_t nwg = group_mask ? (int64_t)a.n_cot * round_up(a.npix, 8 * MVBEV_MASK_GROUP)
-                                 : (sk ? plan.dp_tiles + plan.tail * plan.split : tiles);
+  int64_t nwg = group_mask ? (int64_t)a.n_cot * round_up(a.npix, 8 * MVBEV_MASK_GROUP)
+                           : (sk ? plan.dp_tiles + plan.tail * plan.split : tiles);
+  a.items = nullptr, a.nitems = 0, a.fix = nullptr, a.nfix = 0;
+  if (sched) {  // host schedule (ring kernel): items replace the tile order, pieces their fixup
+    if (!ring || sched->nitems < 0 || sched->nfix < 0 || sched->nslots < 0 || (!sched->items && sched->nitems) ||
+        (sched->nfix && (!sched->fixups || !sched->partials)))
+      return MVBEV_ERR_SHAPE;
+    if (sched->partial_bytes < (size_t)sched->nslots * sizeof(floatx4) * kRingSlotF4) return MVBEV_ERR_SHAPE;
+    if ((reinterpret_cast<uintptr_t>(sched->items) & 15) || (reinterpret_cast<uintptr_t>(sched->fixups) & 15) ||
+        (reinterpret_cast<uintptr_t>(sched->partials) & 15))
+      return MVBEV_ERR_ALIGN;
+    a.items = reinterpret_cast<const int4*>(sched->items);
+    a.nitems = sched->nitems;
+    a.fix = reinterpret_cast<const int4*>(sched->fixups);
+    a.nfix = sched->nfix;
+    a.sk_ws = static_cast<float*>(sched->partials);
+    nwg = sched->nitems;
+    if (nwg == 0) return MVBEV_OK;
+  }
   if (nwg > (int64_t)INT32_MAX) return MVBEV_ERR_SHAPE;
   a.nwg = (int)nwg;
   hipStream_t s = as_stream(stream);
@@ -1151,6 +1249,12 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
       hipLaunchKernelGGL((conv_ring_kernel<D, R, true>), dim3((unsigned)nwg), dim3(RNT), 0, s, a); \
     else                                                                                          \
       hipLaunchKernelGGL((conv_ring_kernel<D, R>), dim3((unsigned)nwg), dim3(RNT), 0, s, a);       \
+    if (a.nfix > 0) {                                                                             \
+      if (p3)                                                                                     \
+        hipLaunchKernelGGL((conv_ring_fixup_kernel<D, R, true>), dim3((unsigned)a.nfix), dim3(RNT), 0, s, a); \
+      else                                                                                        \
+        hipLaunchKernelGGL((conv_ring_fixup_kernel<D, R, false>), dim3((unsigned)a.nfix), dim3(RNT), 0, s, a); \
+    }                                                                                             \
   } while (0)
   if (ring) {
     if (dilation == 1) {
@@ -1292,6 +1396,32 @@ int mvbev_cout1_reduce_partials(const void* partials, const mvbev_conv_desc* des
                      (int)desc->out_rows, (int)desc->out_row0, dilation3, map, (int)map_row0, (int)map_rows);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
+}
+
+size_t mvbev_conv_schedule_slot_bytes(void) { return sizeof(mvbev::b3::floatx4) * mvbev::b3::kRingSlotF4; }
+
+int mvbev_conv3x3_bf16x3_sched(const void* x, int x_layout, const mvbev_conv_desc* desc, const void* w_packed,
+                               const float* bias, const float* init, int64_t Cout, int dilation, int relu, void* y,
+                               int y_layout, const uint32_t* group_mask, const mvbev_conv_schedule* sched,
+                               void* stream) {
+  using namespace mvbev::b3;
+  if (!sched) return MVBEV_ERR_NULL;
+  if (x_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;  // the ring kernel's input
+  return launch<SplitIn>(x, desc, w_packed, bias, init, Cout, dilation, relu, static_cast<float*>(y), y_layout,
+                         group_mask, nullptr, nullptr, 0, stream, nullptr, 1, nullptr, nullptr, sched);
+}
+
+int mvbev_conv3x3_dgrad_bf16x3_sched(const void* dy, int dy_layout, const mvbev_conv_desc* desc,
+                                     const void* w_packed, int64_t Cout_p, int dilation, void* dx, int dx_layout,
+                                     const uint32_t* out_mask, int64_t cot_per_group,
+                                     const mvbev_conv_schedule* sched, void* stream) {
+  using namespace mvbev::b3;
+  if (!sched) return MVBEV_ERR_NULL;
+  if (out_mask && (cot_per_group <= 0 || cot_per_group > 65536)) return MVBEV_ERR_SHAPE;
+  if (dy_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;
+  return launch<SplitIn>(dy, desc, w_packed, nullptr, nullptr, Cout_p, dilation, 0, static_cast<float*>(dx),
+                         dx_layout, nullptr, nullptr, nullptr, 0, stream, out_mask, (int)cot_per_group, nullptr,
+                         nullptr, sched);
 }
 
 int mvbev_conv3x3_dgrad_bf16x3_ex(const void* dy, int dy_layout, const mvbev_conv_desc* desc, const void* w_packed,

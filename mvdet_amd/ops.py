@@ -344,12 +344,15 @@ def heavy_first_order(mask: torch.Tensor, B: int) -> torch.Tensor:
 def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: Optional[torch.Tensor] = None,
                  init: Optional[torch.Tensor] = None, dilation: int = 1, relu: bool = False,
                  out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
-                 group_mask: Optional[torch.Tensor] = None, tile_order: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 group_mask: Optional[torch.Tensor] = None, tile_order: Optional[torch.Tensor] = None,
+                 sched=None) -> torch.Tensor:
     """Low-level form: ``x`` addressed through ``desc`` (``mvbev_conv_desc``).  bf16x3 only,
     optional: ``workspace`` — device scratch for the split-K tail
     (``conv3x3_workspace_bytes``); ``group_mask`` — per-tile active channel groups
     (``warp_tile_mask``), whose cleared groups are skipped; ``tile_order`` — with a mask,
-    the B x tiles pixel tiles in run order (``heavy_first_order``)."""
+    the B x tiles pixel tiles in run order (``heavy_first_order``); ``sched`` — a ring-kernel
+    schedule (``schedule.plan`` over ``schedule.ring_blocks``; split-bf16 x) replacing the
+    order."""
     _require_cuda(x, packed)
     bf16x3 = packed.dtype == torch.bfloat16
     if x.dtype not in ((torch.float32, torch.float16, torch.bfloat16) if bf16x3 else (torch.float32,)):
@@ -403,6 +406,13 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
             if group_mask is None or tile_order.dtype != torch.int32 or tile_order.numel() != B * tiles:
                 raise ValueError("tile_order must be an int32 permutation of the B x tiles pixel tiles")
             top = tile_order.data_ptr()
+        if sched is not None:
+            st = lib.mvbev_conv3x3_bf16x3_sched(x.data_ptr(), layout, ctypes.byref(desc), packed.data_ptr(), bp, ip,
+                                                cout, int(dilation), int(bool(relu)), out.data_ptr(),
+                                                _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32, gmp,
+                                                ctypes.byref(sched.c), _stream(x))
+            _native.check(st, "mvbev_conv3x3_bf16x3_sched")
+            return out
         st = lib.mvbev_conv3x3_bf16x3_ex(x.data_ptr(), layout, ctypes.byref(desc),
                                          packed.data_ptr(), bp, ip, cout, int(dilation), int(bool(relu)),
                                          out.data_ptr(), _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32,
@@ -658,16 +668,31 @@ class PackedDgrad3x3:
         return self.packed
 
 
+def dgrad_schedule(B: int, cout_p: int, H: int, W: int, K: int, out_mask: Optional[torch.Tensor],
+                   cot_per_group: int, device, split: bool = True):
+    """The balanced ring-kernel schedule (``schedule.plan``) of ``conv3x3_dgrad`` from a
+    split-bf16 dy (12-row tiles, all K chunks per block, the output-side mask's blocks)."""
+    from . import schedule
+    th = dgrad_tile_rows(True, 1)
+    ty, tx = -(-H // th), -(-W // _native.TILE_W)
+    om = None if out_mask is None else [int(v) for v in out_mask.cpu().tolist()]
+    blocks = schedule.ring_blocks(B, ty, tx, cout_p // BN, -(-K // (2 * KC)), out_mask=om,
+                                  cot_per_group=cot_per_group)
+    cus = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
+    return schedule.plan(blocks, cus, device, split=split)
+
+
 def conv3x3_dgrad(dy: torch.Tensor, packed: PackedDgrad3x3, weight: torch.Tensor, dilation: int,
                   out: Optional[torch.Tensor] = None, out_mask: Optional[torch.Tensor] = None,
-                  cot_per_group: int = 1) -> torch.Tensor:
+                  cot_per_group: int = 1, sched=None) -> torch.Tensor:
     """Data gradient of a 3x3 stride-1 conv (padding = dilation): dy [B,Cout_w,H,W] fp32
     contiguous (or its split-bf16 layout, a bf16 ``split_shape`` tensor: the LDS-DMA ring
     kernel) -> [B, cout_p, H, W] fp32, or the split-bf16 layout when ``out`` is a bf16
     ``split_shape`` tensor (channel o = forward input channel chan_map[o]; channels past
     k_out are zero).  ``out_mask`` (int32 per conv output tile, ``warp_tile_mask`` at
     ``dgrad_tile_rows`` rows): tiles of output channel group g (``cot_per_group`` 128-channel
-    tiles) whose bit is clear are NOT written (for a consumer that never reads them)."""
+    tiles) whose bit is clear are NOT written (for a consumer that never reads them).
+    ``sched``: a ``dgrad_schedule`` of the same sizes and mask (split-bf16 dy only)."""
     _require_cuda(dy)
     dy_split = dy.dtype == torch.bfloat16
     if dy.dim() != (6 if dy_split else 4) or dy.dtype not in (torch.float32, torch.bfloat16) or not dy.is_contiguous():
@@ -694,6 +719,15 @@ def conv3x3_dgrad(dy: torch.Tensor, packed: PackedDgrad3x3, weight: torch.Tensor
             raise ValueError(f"out_mask must be a contiguous int32 tensor of >= {tiles} tiles")
         mp = out_mask.data_ptr()
     d = conv_desc(B, K, H, W, group=K, group_stride=0, batch_stride=K * H * W)
+    if sched is not None:
+        if not dy_split:
+            raise ValueError("a ring-kernel schedule needs a split-bf16 dy")
+        st = _native.load().mvbev_conv3x3_dgrad_bf16x3_sched(
+            dy.data_ptr(), _native.LAYOUT_SPLIT_BF16, ctypes.byref(d), packed.get(weight).data_ptr(), cp,
+            int(dilation), out.data_ptr(), _native.LAYOUT_SPLIT_BF16 if split else _native.LAYOUT_F32, mp,
+            int(cot_per_group), ctypes.byref(sched.c), _stream(dy))
+        _native.check(st, "mvbev_conv3x3_dgrad_bf16x3_sched")
+        return out
     st = _native.load().mvbev_conv3x3_dgrad_bf16x3_ex(
         dy.data_ptr(), _native.LAYOUT_SPLIT_BF16 if dy_split else _native.LAYOUT_F32, ctypes.byref(d),
         packed.get(weight).data_ptr(), cp, int(dilation), out.data_ptr(),

@@ -263,6 +263,29 @@ class ProjectFuse:
             self._masks[key] = o
         return o
 
+    def conv1_schedule(self, device, row0: int, rows: int, B: int, split: bool = True):
+        """A ring-kernel schedule of conv1 over rows [row0, row0+rows) (split-bf16 slab,
+        frustum mask): ``schedule.plan`` over the heavy-first blocks, pixel tiles dealt to the
+        XCDs as the unscheduled kernel does; cached.  Not used by default: measured within
+        ±1 % of the unscheduled launch at cfg2 (the masked forward's imbalance comes from its
+        heavy blocks, which a tail cut does not reach; ``tools/kbench.py --only conv1,conv1s``)."""
+        key = ("sched", str(device), row0, rows, B, split)
+        sc = self._masks.get(key)
+        if sc is None:
+            from . import schedule
+            m = self.conv1_mask(device, row0, rows)
+            if m is None or not self.split:
+                return None
+            th = self.conv1_tile_rows()
+            ty, tx = -(-rows // th), -(-self.grid_hw[1] // _native.TILE_W)
+            blocks = schedule.ring_blocks(B, ty, tx, self.mid // ops.BN, 0, group_mask=m.cpu().tolist(),
+                                          cpg=self.Cs // (2 * ops.KC),
+                                          order=self.conv1_order(device, row0, rows, B).cpu().tolist())
+            cus = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
+            sc = schedule.plan(blocks, cus, device, split=split, deal=self.mid // ops.BN)
+            self._masks[key] = sc
+        return sc
+
     def conv1_active_fraction(self, device, row0: int, rows: int) -> float:
         """Fraction of conv1's (tile, slot) work the frustum mask keeps (1.0 = dense)."""
         m = self.conv1_mask(device, row0, rows)
@@ -272,7 +295,7 @@ class ProjectFuse:
         return bits / (m.numel() * self.S)
 
     # -- a7-a9 ----------------------------------------------------------------------------
-    def conv1(self, ws: Workspace, conv1: torch.nn.Conv2d) -> torch.Tensor:
+    def conv1(self, ws: Workspace, conv1: torch.nn.Conv2d, sched=None) -> torch.Tensor:
         """a7: y1 = relu(conv3x3(slab) + coord_term) on y1's rows (fp32 MFMA)."""
         if conv1.weight.shape[1] != self.cin:
             raise ValueError(f"conv1 has {conv1.weight.shape[1]} input channels, expected {self.cin}")
@@ -286,7 +309,8 @@ class ProjectFuse:
         gm = self.conv1_mask(ws.slab.device, a1, b1 - a1)
         return ops.conv3x3_desc(ws.slab, d1, p1, self.mid, bias=None, init=init, dilation=1, relu=True,
                                 out=ws.y1, workspace=None if gm is not None else self._sk_ws(d1, ws.slab.device),
-                                group_mask=gm, tile_order=self.conv1_order(ws.slab.device, a1, b1 - a1, B))
+                                group_mask=gm, tile_order=self.conv1_order(ws.slab.device, a1, b1 - a1, B),
+                                sched=sched)
 
     def conv2(self, ws: Workspace, conv2: torch.nn.Conv2d) -> torch.Tensor:
         """a8: y2 = relu(conv3x3_d2(y1) + b2) on y2's rows."""

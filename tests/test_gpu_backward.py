@@ -295,6 +295,44 @@ def test_conv_wgrad_frustum_chunk_lists(split):
     assert_parity(got.cpu(), ref, "wgrad with chunk lists")
 
 
+@pytest.mark.parametrize("pieces", [0, 1, 3])
+def test_dgrad_ring_schedule(pieces):
+    """conv3x3_dgrad on the ring kernel run through a host schedule (schedule.plan: XCD
+    shares, the last round cut into K-pieces, fixup in K order) equals the plain launch:
+    bitwise for whole blocks (pieces=1: no cut), to fp32 rounding with pieces (the planner's
+    own cut, or every block in 3 pieces) — with the output-side mask, unwritten tiles stay
+    untouched."""
+    from mvdet_amd import ops, schedule
+    g = torch.Generator().manual_seed(11 + pieces)
+    B, Cw, K, H, W = 2, 256, 128, 29, 70
+    dy = torch.randn((B, K, H, W), generator=g)
+    w = torch.randn((K, Cw, 3, 3), generator=g) * 0.05
+    pk = ops.PackedDgrad3x3(Cw)
+    dys = _split_encode(dy.to(DEV))
+    th = ops.dgrad_tile_rows(True, 1)
+    ntiles = -(-H // th) * -(-W // 32)
+    mask = torch.tensor([(t * 5 + 1) % 4 for t in range(ntiles)], dtype=torch.int32)  # groups of 128 channels
+    ref = ops.conv3x3_dgrad(dys, pk, w.to(DEV), 1, out=torch.full(ops.split_shape(B, Cw, H, W), 7.0,
+                                                                      dtype=torch.bfloat16, device=DEV),
+                            out_mask=mask.to(DEV), cot_per_group=1)
+    if pieces == 0:
+        sch = ops.dgrad_schedule(B, Cw, H, W, K, mask.to(DEV), 1, DEV)
+    else:
+        blocks = schedule.ring_blocks(B, -(-H // th), -(-W // 32), Cw // 128, K // 16,
+                                      out_mask=mask.tolist(), cot_per_group=1)
+        sch = schedule.plan(blocks, 256, DEV, split=False, force_pieces=pieces)
+        assert (sch.nfix > 0) == (pieces > 1)
+    got = ops.conv3x3_dgrad(dys, pk, w.to(DEV), 1, out=torch.full(ops.split_shape(B, Cw, H, W), 7.0,
+                                                                      dtype=torch.bfloat16, device=DEV),
+                            out_mask=mask.to(DEV), cot_per_group=1, sched=sch)
+    r, o = ops.split_decode(ref).cpu(), ops.split_decode(got).cpu()
+    assert torch.equal(o == 14.0, r == 14.0) and (r == 14.0).any()  # prefill hi 7 + lo 7 kept where masked
+    if sch.nfix:  # pieces: another fp32 summation order
+        assert_parity(o, r, f"dgrad, {sch.nfix} blocks in K-pieces")
+    else:
+        assert torch.equal(o, r)
+
+
 @pytest.mark.parametrize("B,Cw,K,H,W,dil", [(1, 128, 40, 12, 36, 1), (2, 512, 512, 17, 37, 2),
                                             (1, 256, 200, 9, 64, 1)])
 def test_conv_dgrad_vs_torch(B, Cw, K, H, W, dil):

@@ -29,7 +29,7 @@ def test_library_exports_every_header_symbol():
     assert declared == sorted(_native.EXPORTS)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.mvbev_version() == 10900
+    assert lib.mvbev_version() == 11000
     assert lib.mvbev_status_string(0) == b"ok"
     assert lib.mvbev_status_string(-100) == b"HIP launch failed"
 
@@ -105,3 +105,41 @@ def test_detector_state_dict_layout_matches_reference():
     assert not any("proj_mats" in k or "coord_map" in k for k in shapes)  # quirk B.4: not buffers
     with pytest.raises(RuntimeError, match="ROCm GPU"):
         model(torch.zeros(1, m["num_cam"], 3, 32, 32))
+
+
+def test_schedule_plan_covers_every_chunk_once():
+    """schedule.plan (host logic, no GPU): every block's chunk range is covered exactly once
+    (whole, or by its pieces in K order with consecutive slots and one fixup); XCD i % 8
+    order; on 2320 equal blocks over 256 CUs (conv1's dgrad at cfg2: 9.06 rounds) the last
+    round is cut into pieces and the simulated makespan drops."""
+    from mvdet_amd import schedule
+    blocks = [(t, 32) for t in range(2320)]
+    sc = schedule.plan(blocks, 256, "cpu")
+    items = sc.items.tolist()[:sc.nitems]
+    fix = {f[0]: f for f in sc.fixups.tolist()[:sc.nfix]}
+    assert sc.nfix > 0 and sc.predicted < sc.predicted_plain
+    seen = {}
+    for t, c0, c1, slot in items:
+        if t < 0:
+            continue
+        seen.setdefault(t, []).append((c0, c1, slot))
+    assert sorted(seen) == list(range(2320))
+    for t, parts in seen.items():
+        parts.sort()
+        assert parts[0][0] == 0 and parts[-1][1] == 32
+        assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+        if len(parts) == 1:
+            assert parts[0][2] == -1 and t not in fix
+        else:
+            f = fix[t]
+            assert f[2] == len(parts) and [p[2] for p in parts] == list(range(f[1], f[1] + f[2]))
+    # masked, heavy-first forward blocks dealt by pixel tile: a tile's Cout blocks on one XCD
+    fwd = schedule.ring_blocks(1, 2, 3, 4, 0, group_mask=[1, 3, 7, 0, 5, 1], cpg=2, order=[2, 1, 4, 0, 5, 3])
+    assert [c for _, c in fwd[:4]] == [6] * 4 and all(c > 0 for _, c in fwd[:20]) and len(fwd) == 24
+    assert all(c == 0 for _, c in fwd[20:])  # the empty pixel tile's blocks: dropped by plan
+    sc = schedule.plan(fwd, 16, "cpu", split=False, deal=4)
+    its = sc.items.tolist()[:sc.nitems]
+    for i, (t, c0, c1, slot) in enumerate(its):
+        if t >= 0:
+            assert (c0, slot) == (0, -1)
+            assert all(j % 8 == i % 8 for j, it in enumerate(its) if it[0] >= 0 and it[0] // 4 == t // 4)

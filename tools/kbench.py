@@ -60,6 +60,10 @@ def backward_stages(eng, ws, mc, B, ho, wo, N, C, dev):
     dy1s = torch.empty_like(y1_pos)
     ops.relu_backward_split_(dy1, y1_pos, dy1s)
     cm = eng.conv1_mask(dev, 0, ho, tile_h=ops.dgrad_tile_rows(True, 1))
+    sch1 = ops.dgrad_schedule(B, cp, ho, wo, w1.shape[0], cm, C // ops.BN, dev)
+    print(json.dumps({"dgrad1_schedule": {"items": sch1.nitems, "split_tiles": sch1.nfix, "pieces": sch1.nslots,
+                                          "predicted": round(sch1.predicted, 1),
+                                          "predicted_plain": round(sch1.predicted_plain, 1)}}), flush=True)
     flop = 2.0 * B * ho * wo * 9 * N * C * w1.shape[0]
     # conv2 (d2) on a split y1 and a random dy2, as the training step's conv2 backward
     w2 = mc[2].weight
@@ -86,6 +90,8 @@ def backward_stages(eng, ws, mc, B, ho, wo, N, C, dev):
                                               dw=dw1, workspace=wws, chunk_lists=lists), flop),  # fp32 dy
         "dgrad1": (lambda: ops.conv3x3_dgrad(dy1s, st.dgrad1, w1, 1, out=dslab, out_mask=cm,
                                              cot_per_group=C // ops.BN), flop),
+        "dgrad1s": (lambda: ops.conv3x3_dgrad(dy1s, st.dgrad1, w1, 1, out=dslab, out_mask=cm,
+                                              cot_per_group=C // ops.BN, sched=sch1), flop),  # balanced schedule
     }
 
 
@@ -121,6 +127,10 @@ def main():
             "warpup": (lambda: eng.warp_views_upsampled(ws, list(range(N)), bfeats), None),
             "warp1": (lambda: [eng.warp_view(ws, v, feats[v]) for v in range(N)], None),
             "conv1": (lambda: eng.conv1(ws, mc[0]), 2.0 * B * ho * wo * 9 * N * C * 512),
+            "conv1s": (lambda: eng.conv1(ws, mc[0], sched=eng.conv1_schedule(dev, 0, ho, B)),
+                       2.0 * B * ho * wo * 9 * N * C * 512),  # balanced schedule
+            "conv1p": (lambda: eng.conv1(ws, mc[0], sched=eng.conv1_schedule(dev, 0, ho, B, split=False)),
+                       2.0 * B * ho * wo * 9 * N * C * 512),  # the schedule's XCD shares, no pieces
             "conv2": (lambda: eng.conv2(ws, mc[2]), 2.0 * B * ho * wo * 9 * 512 * 512),
             "conv3": (lambda: eng.conv3(ws, mc[4]), None),
             # conv2 -> conv3 fused (the default inference path): partials epilogue + reduce
@@ -138,7 +148,7 @@ def main():
             stages["adjup"] = ((lambda: ops.warp_views_adjoint(douts, plu, gs)), None)
             pl = [ops.WarpAdjointPlan(eng.m_norm_cpu[v], up, (ho, wo), dev) for v in range(N)]
             stages["adj"] = ((lambda: ops.warp_views_adjoint(douts, pl, gsu)), None)
-        if {"wgrad1", "wgrad1f", "dgrad1", "wgrad2", "wgrad2f", "dgrad2"} & set(args.only.split(",")):
+        if {"wgrad1", "wgrad1f", "dgrad1", "dgrad1s", "wgrad2", "wgrad2f", "dgrad2"} & set(args.only.split(",")):
             stages.update(backward_stages(eng, ws, mc, B, ho, wo, N, C, dev))
         from mvdet_amd import _native
         libs = [("default", _native.load())]

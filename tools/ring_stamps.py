@@ -30,7 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("lib")
     ap.add_argument("--config", type=int, default=2)
-    ap.add_argument("--stage", default="conv1", choices=["conv1", "conv2", "dgrad1"])
+    ap.add_argument("--stage", default="conv1", choices=["conv1", "conv2", "dgrad1", "dgrad1s"])
     args = ap.parse_args()
     spec = synthetic.CONFIGS[args.config]
     ds = spec["make"]()
@@ -48,9 +48,9 @@ def main():
     with torch.no_grad():
         for v in range(N):
             eng.warp_view(ws, v, feats[v])
-        if args.stage == "dgrad1":  # conv1's data gradient as the training step runs it (kbench's setup)
+        if args.stage.startswith("dgrad1"):  # conv1's data gradient as the training step runs it (kbench's setup)
             from tools.kbench import backward_stages
-            run = backward_stages(eng, ws, mc, B, ho, wo, N, C, dev)["dgrad1"][0]
+            run = backward_stages(eng, ws, mc, B, ho, wo, N, C, dev)[args.stage][0]
         else:
             run = (lambda: eng.conv1(ws, mc[0])) if args.stage == "conv1" else (lambda: eng.conv2(ws, mc[2]))
         for _ in range(3):

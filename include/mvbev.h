@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -240,6 +240,28 @@ int mvbev_conv3x3_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_desc* 
                             int64_t Cout, int dilation, int relu, void* y, int y_layout,
                             const uint32_t* group_mask, const int32_t* tile_order, void* workspace,
                             size_t workspace_bytes, void* stream);
+/* Pixel-tile spaces of the split-bf16-input (ring) conv.  MVBEV_TILES_GRID: the 12 x 32 tile
+ * grid of mvbev_conv3x3_bf16x3_ex (tiles_y x ceil(W / 32) per batch item, row-major; the last
+ * tile column computes up to 31 columns past W).  MVBEV_TILES_EDGE_STRIP (0 < W % 32 <= 16):
+ * the 12 x 32 grid over columns [0, 32 * floor(W / 32)), then edge_tiles tiles of edge_rows x EW
+ * pixels (EW = 8 or 16, edge_rows = 384 / EW) over the last W % 32 columns, top to bottom — the
+ * same 384 pixels per tile and no MFMA column past W (Wildtrack's W = 360: 11 regular tile
+ * columns + 3 strips of 48 x 8).  mvbev_conv_ring_tile_space fills
+ * g = {tiles_x, tiles_y, edge_tiles, EW, edge_rows} for desc's output rows and W (0 edges for
+ * the grid), or returns MVBEV_ERR_SHAPE when the space does not apply. */
+#define MVBEV_TILES_GRID 0
+#define MVBEV_TILES_EDGE_STRIP 1
+int mvbev_conv_ring_tile_space(const mvbev_conv_desc* desc, int tile_space, int64_t g[5]);
+/* mvbev_conv3x3_bf16x3_ex with the tiles of tile_space (split-bf16 x only, no workspace):
+ * group_mask[pp] / tile_order (b * tiles + pp) index pixel tiles pp of that space (edge-strip
+ * masks: mvbev_warp_tile_mask with tile_h = edge_rows, tile_w = EW, last tile column).
+ * MVBEV_TILES_EDGE_STRIP: dilation 1 with ReLU (conv1, map_classifier[0:2]).  Same y, bitwise,
+ * as the grid tiles. */
+int mvbev_conv3x3_bf16x3_ex3(const void* x, int x_layout, const mvbev_conv_desc* desc,
+                             const void* w_packed, const float* bias, const float* init,
+                             int64_t Cout, int dilation, int relu, void* y, int y_layout,
+                             const uint32_t* group_mask, const int32_t* tile_order, int tile_space,
+                             void* stream);
 
 /* conv2 -> conv3 without conv2's activation in HBM (map_classifier[2:5],
  * persp_trans_detector.py:53-54, inference): the split-bf16-input conv of

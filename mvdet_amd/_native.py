@@ -63,8 +63,11 @@ EXPORTS = (
     "mvbev_conv_schedule_slot_bytes",
     "mvbev_conv3x3_bf16x3_sched",
     "mvbev_conv3x3_dgrad_bf16x3_sched",
+    "mvbev_conv_ring_tile_space",
+    "mvbev_conv3x3_bf16x3_ex3",
 )
 WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
+TILES_GRID, TILES_EDGE_STRIP = 0, 1  # MVBEV_TILES_*
 ERR_SHAPE = -2  # MVBEV_ERR_SHAPE
 
 KC = 8    # MVBEV_CONV_KC
@@ -150,6 +153,11 @@ def _declare(lib):
     lib.mvbev_conv3x3_bf16x3_ex.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64,
                                             ctypes.c_int, ctypes.c_int, _p, ctypes.c_int, _p, _p, _p,
                                             ctypes.c_size_t, _p]
+    lib.mvbev_conv_ring_tile_space.restype = ctypes.c_int
+    lib.mvbev_conv_ring_tile_space.argtypes = [ctypes.POINTER(ConvDesc), ctypes.c_int, ctypes.POINTER(_i64)]
+    lib.mvbev_conv3x3_bf16x3_ex3.restype = ctypes.c_int
+    lib.mvbev_conv3x3_bf16x3_ex3.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64,
+                                             ctypes.c_int, ctypes.c_int, _p, ctypes.c_int, _p, _p, ctypes.c_int, _p]
     lib.mvbev_warp_tile_mask.restype = ctypes.c_int
     lib.mvbev_warp_tile_mask.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
                                          _i64, _i64, _i64, _i64, _p, _p]
@@ -253,6 +261,14 @@ def load(path: os.PathLike | str | None = None):
     if path is None:
         _lib = lib
     return lib
+
+
+def ring_tile_space(desc: ConvDesc, space: int):
+    """``mvbev_conv_ring_tile_space``: (tiles_x, tiles_y, edge_tiles, edge width, edge rows) of
+    the ring conv's pixel-tile space ``space`` for ``desc``, or None when it does not apply."""
+    g = (_i64 * 5)()
+    st = load().mvbev_conv_ring_tile_space(ctypes.byref(desc), int(space), g)
+    return tuple(int(v) for v in g) if st == 0 else None
 
 
 def conv_tile_rows(layout: int, dilation: int = 1) -> int:

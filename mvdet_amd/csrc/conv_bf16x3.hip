@@ -139,6 +139,9 @@ struct Args {
   int nitems;
   const int4* fix;
   int nfix;
+  // edge strip (ring kernel, optional): pixel tiles [tiles_y * tiles_x, + edge_tiles) of each
+  // batch item are edge_rows x (W - edge_x0) tiles of columns [edge_x0, W) (RingGeo EW)
+  int edge_tiles, edge_x0, edge_rows;
 };
 
 // Input tag: the split-bf16 blocked layout written by mvbev_warp_views_split_bf16 and by this
@@ -597,8 +600,13 @@ constexpr int RNIT = 64 * RNIW;                 // issuing lanes
 constexpr int RNWI = RUNIT / RNIT;              // LDS-DMA instructions per issuing wave per W unit (3)
 static_assert(RNIW == 4 || RNIW == 8, "issuing waves");
 static_assert(RUNIT % RNIT == 0, "W unit must split evenly over the waves");
-template <int DIL> struct RingGeo {
-  static constexpr int XH = RT + 2 * DIL, XW = TW + 2 * DIL, XPIX = XH * XW;
+// EW: tile width.  32 = the regular 12 x 32 tile (an MFMA's 32 pixels are one row segment);
+// 8 / 16 = an edge-strip tile of 12 * 32 / EW rows x EW columns for the last W % 32 columns
+// (an MFMA's 32 pixels are 32 / EW row segments 12 rows apart, so the 3 taps of a kernel
+// column still share a wave's 5 fragment rows).  Same pixel count, halo of the same size class.
+template <int DIL, int EW = TW> struct RingGeo {
+  static_assert(EW == 8 || EW == 16 || EW == 32, "tile width");
+  static constexpr int XH = RT * (TW / EW) + 2 * DIL, XW = EW + 2 * DIL, XPIX = XH * XW;
   static constexpr int NX = (4 * XPIX + RNIT - 1) / RNIT;  // LDS-DMA instructions per issuing wave per halo
   static constexpr int XBUF = NX * RNIT;                   // entries per halo buffer (incl. tail)
   static constexpr int LDS = 3 * RUNIT + 2 * XBUF;       // 16-B entries
@@ -792,14 +800,15 @@ __global__ __launch_bounds__(RNT) void conv_ring_fixup_kernel(const Args a) {
 __device__ uint32_t g_ring_stamps[16384 * 4];
 #endif
 
-template <int DIL, bool RELU, bool P3 = false>
+template <int DIL, bool RELU, bool P3 = false, int EWE = 0>
 __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
 #if MVBEV_RING_STAMP
   const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  using G = RingGeo<DIL>;
-  constexpr int XW = G::XW, XPIX = G::XPIX, NX = G::NX, XBUF = G::XBUF;
-  __shared__ __attribute__((aligned(16))) u32x4 lds[G::LDS];
+  constexpr int LDSN = EWE ? (RingGeo<DIL>::LDS > RingGeo<DIL, EWE ? EWE : TW>::LDS ? RingGeo<DIL>::LDS
+                                                                                   : RingGeo<DIL, EWE ? EWE : TW>::LDS)
+                           : RingGeo<DIL>::LDS;
+  __shared__ __attribute__((aligned(16))) u32x4 lds[LDSN];
   u32x4* const Xlds = lds + 3 * RUNIT;
 
   const int W = a.W;
@@ -824,18 +833,20 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     if (slot >= a.npix) return;  // padding block (whole block, before any barrier)
     tile = (a.tile_order ? a.tile_order[slot] : slot) * a.n_cot + j % a.n_cot;
   }
+  // tile = (b, pixel tile pp, cot); pixel tiles: the tiles_y x tiles_x grid, then the edge strip
   const int cot = tile % a.n_cot;
-  int rest = tile / a.n_cot;
-  const int tx = rest % a.tiles_x;
-  rest /= a.tiles_x;
-  const int ty = rest % a.tiles_y;
-  const int b = rest / a.tiles_y;
-  const int x0 = tx * TW;
-  const int y0 = a.out_row0 + ty * RT;
+  const int rest = tile / a.n_cot;
+  const int t_main = a.tiles_y * a.tiles_x, t_all = t_main + a.edge_tiles;
+  const int pp = rest % t_all;
+  const int b = rest / t_all;
+  const bool edge = EWE != 0 && pp >= t_main;
+  const int ty = pp / a.tiles_x;
+  const int x0 = edge ? a.edge_x0 : (pp - ty * a.tiles_x) * TW;
+  const int y0 = a.out_row0 + (edge ? (pp - t_main) * a.edge_rows : ty * RT);
   // output-side mask: a tile of output channels nobody reads (whole block, before any barrier)
-  if (a.cmask && !((a.cmask[ty * a.tiles_x + tx] >> (cot / a.cot_pg)) & 1u)) return;
+  if (a.cmask && !((a.cmask[pp] >> (cot / a.cot_pg)) & 1u)) return;
   const u32x4* wsrc = a.wp + (int64_t)cot * W16;
-  const uint32_t gm = a.gmask ? a.gmask[ty * a.tiles_x + tx] : 0u;
+  const uint32_t gm = a.gmask ? a.gmask[pp] : 0u;
   // this block's chunks: [ci0, ci1) of the tile's active-chunk sequence (all of it unscheduled)
   const int nch_tile = a.gmask ? __builtin_popcount(gm) * a.cpg : a.nchunks;
   ci1 = min(ci1, nch_tile);
@@ -848,6 +859,13 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     return __builtin_ctz(m) * a.cpg + i % a.cpg;
   };
 
+  auto body = [&](auto ew_tag) __attribute__((always_inline)) {
+  constexpr int EW = decltype(ew_tag)::value;
+  using G = RingGeo<DIL, EW>;
+  constexpr int XW = G::XW, XPIX = G::XPIX, NX = G::NX, XBUF = G::XBUF;
+  static_assert(G::LDS <= LDSN, "LDS");
+  // the lane's pixel in its MFMA block: row offset (a multiple of the 12-row period) and column
+  const int lr = 12 * (l32 / EW), lc = l32 % EW;
   // LDS-DMA sources, chunk-invariant parts.  Halo entry e = (sub, part, pixel) of the image
   // [sub][part][XH][XW]; lane j-th instruction covers entries (j * RNIW + wave) * 64 + lane.
   int xo[NX];  // piece offset in the sub-block's plane (2 * pixel + part); -1 = zero entry
@@ -941,7 +959,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
   bf16x8 fb[2][5][2];  // [set][input row m (rows base + m * DIL)][hi, lo]
   bf16x8 fa[3][2][2];  // [set][ct][hi, lo] (waves 0-3 alternate sets 0/1; staggered waves 4-7 use set = tap row)
   auto fetch_b = [&](int st, int xb, int kw) __attribute__((always_inline)) {
-    const u32x4* X = Xlds + xb * XBUF + kl * 2 * XPIX + base * XW + l32 + kw * DIL;
+    const u32x4* X = Xlds + xb * XBUF + kl * 2 * XPIX + (base + lr) * XW + lc + kw * DIL;
 #pragma unroll
     for (int m = 0; m < 5; ++m)
 #pragma unroll
@@ -1092,7 +1110,14 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
   if (pslot >= 0) {
     ring_store_partial(a.sk_ws, pslot, acc);  // a piece of a split tile: conv_ring_fixup_kernel finishes it
   } else {
-    ring_epilogue<DIL, RELU, P3>(a, b, y0 + base, x0 + l32, cot, cw, acc, lds);
+    ring_epilogue<DIL, RELU, P3>(a, b, y0 + base + lr, x0 + lc, cot, cw, acc, lds);
+  }
+  };  // body
+  if constexpr (EWE != 0) {
+    if (edge) body(std::integral_constant<int, EWE>{});
+    else body(std::integral_constant<int, TW>{});
+  } else {
+    body(std::integral_constant<int, TW>{});
   }
 #if MVBEV_RING_STAMP
   if (threadIdx.x == 0 && blockIdx.x < 16384) {  // vector stores of the block's wall-clock span and place
@@ -1157,13 +1182,35 @@ static int64_t conv_tiles(const mvbev_conv_desc* d, int64_t Cout) {
   return ceil_div(d->W, TW) * ceil_div(d->out_rows, MVBEV_B3_WAVES) * (Cout / BN) * d->B;
 }
 
+// Pixel-tile space of the ring kernel (split-bf16 input).  MVBEV_TILES_EDGE_STRIP, for
+// 0 < W % 32 <= 16: the regular 12 x 32 tiles cover columns [0, 32 * floor(W / 32)) and the last
+// W % 32 columns are cut into edge-strip tiles of (12 * 32 / EW) rows x EW columns (EW = 8 or 16,
+// the same 384 pixels per tile), so no MFMA column is spent past W.  g = {tiles_x, tiles_y,
+// edge_tiles, edge width (the EW the kernel uses), edge rows}.
+static int ring_tile_space(const mvbev_conv_desc* d, int tile_space, int64_t g[5]) {
+  if (!d || d->W <= 0 || d->out_rows <= 0) return MVBEV_ERR_RANK;
+  g[1] = ceil_div(d->out_rows, RT);
+  if (tile_space == MVBEV_TILES_GRID) {
+    g[0] = ceil_div(d->W, TW), g[2] = 0, g[3] = 0, g[4] = 0;
+    return MVBEV_OK;
+  }
+  if (tile_space != MVBEV_TILES_EDGE_STRIP) return MVBEV_ERR_SHAPE;
+  const int64_t r = d->W % TW;
+  if (r == 0 || r > 16) return MVBEV_ERR_SHAPE;  // nothing to trim / a regular tile is as good
+  g[0] = d->W / TW;
+  g[3] = r <= 8 ? 8 : 16;
+  g[4] = RT * (TW / g[3]);
+  g[2] = ceil_div(d->out_rows, g[4]);
+  return MVBEV_OK;
+}
+
 template <typename TIn>
 static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
                   const float* bias, const float* init, int64_t Cout, int dilation, int relu,
                   float* y, int y_layout, const uint32_t* group_mask, const int32_t* tile_order,
                   void* workspace, size_t ws_bytes, void* stream, const uint32_t* out_mask = nullptr,
                   int cot_pg = 1, const float* w3 = nullptr, float* p3 = nullptr,
-                  const mvbev_conv_schedule* sched = nullptr) {
+                  const mvbev_conv_schedule* sched = nullptr, int tile_space = MVBEV_TILES_GRID) {
   if (!x || !d || !w_packed || (!y && !p3) || (!w3 != !p3)) return MVBEV_ERR_NULL;
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || d->in_rows <= 0 ||
       d->out_rows <= 0 || d->group <= 0)
@@ -1190,7 +1237,18 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   a.p3 = p3;
   a.tiles_x = (int)ceil_div(d->W, TW); a.tiles_y = (int)ceil_div(d->out_rows, ring ? RT : NW);
   a.n_cot = (int)(Cout / BN);
-  const int64_t tiles = (int64_t)a.tiles_x * a.tiles_y * a.n_cot * d->B;
+  a.edge_tiles = 0, a.edge_x0 = 0, a.edge_rows = 0;
+  int edge_w = 0;
+  if (tile_space == MVBEV_TILES_EDGE_STRIP) {  // ring kernel, no schedule / output-side mask
+    int64_t g[5];
+    if (!ring || sched || out_mask || ring_tile_space(d, tile_space, g) != MVBEV_OK) return MVBEV_ERR_SHAPE;
+    a.tiles_x = (int)g[0];
+    a.edge_tiles = (int)g[2], edge_w = (int)g[3], a.edge_rows = (int)g[4];
+    a.edge_x0 = (int)(g[0] * TW);
+  } else if (tile_space != MVBEV_TILES_GRID) {
+    return MVBEV_ERR_SHAPE;
+  }
+  const int64_t tiles = ((int64_t)a.tiles_x * a.tiles_y + a.edge_tiles) * a.n_cot * d->B;
   if (tiles * a.nchunks > (int64_t)INT32_MAX * 8) return MVBEV_ERR_SHAPE;
   a.gmask = nullptr;
   a.cpg = 0;
@@ -1247,6 +1305,12 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   do {                                                                                            \
     if (p3)                                                                                       \
       hipLaunchKernelGGL((conv_ring_kernel<D, R, true>), dim3((unsigned)nwg), dim3(RNT), 0, s, a); \
+    else if (edge_w == 8 && D == 1 && R)                                                          \
+      hipLaunchKernelGGL((conv_ring_kernel<1, true, false, 8>), dim3((unsigned)nwg), dim3(RNT), 0, s, a); \
+    else if (edge_w == 16 && D == 1 && R)                                                         \
+      hipLaunchKernelGGL((conv_ring_kernel<1, true, false, 16>), dim3((unsigned)nwg), dim3(RNT), 0, s, a); \
+    else if (edge_w != 0)                                                                         \
+      return MVBEV_ERR_SHAPE;                                                                     \
     else                                                                                          \
       hipLaunchKernelGGL((conv_ring_kernel<D, R>), dim3((unsigned)nwg), dim3(RNT), 0, s, a);       \
     if (a.nfix > 0) {                                                                             \
@@ -1358,6 +1422,23 @@ int mvbev_conv3x3_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_desc* 
   return launch<float>(x, desc, w_packed, bias, init, Cout, dilation, relu,
                        static_cast<float*>(y), y_layout, group_mask, tile_order, workspace,
                        workspace_bytes, stream);
+}
+
+int mvbev_conv_ring_tile_space(const mvbev_conv_desc* desc, int tile_space, int64_t g[5]) {
+  if (!desc || !g) return MVBEV_ERR_NULL;
+  return mvbev::b3::ring_tile_space(desc, tile_space, g);
+}
+
+int mvbev_conv3x3_bf16x3_ex3(const void* x, int x_layout, const mvbev_conv_desc* desc,
+                             const void* w_packed, const float* bias, const float* init,
+                             int64_t Cout, int dilation, int relu, void* y, int y_layout,
+                             const uint32_t* group_mask, const int32_t* tile_order, int tile_space,
+                             void* stream) {
+  using namespace mvbev::b3;
+  if (x_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;  // the ring kernel's input
+  return launch<SplitIn>(x, desc, w_packed, bias, init, Cout, dilation, relu, static_cast<float*>(y), y_layout,
+                         group_mask, tile_order, nullptr, 0, stream, nullptr, 1, nullptr, nullptr, nullptr,
+                         tile_space);
 }
 
 size_t mvbev_conv3x3_bf16x3_cout1_partials_bytes(const mvbev_conv_desc* desc, int64_t Cout) {

@@ -305,12 +305,13 @@ def conv3x3_workspace_bytes(desc, cout: int) -> int:
 
 
 def warp_tile_mask(m_norms, src_hw, grid_hw, row0: int, rows: int, halo: int, device,
-                   tile_h: Optional[int] = None) -> torch.Tensor:
+                   tile_h: Optional[int] = None, tile_w: Optional[int] = None) -> torch.Tensor:
     """Frustum mask of the conv tiles (``mvbev_warp_tile_mask``): int32 [tiles] on ``device``,
     bit s set where slot s's warp can be non-zero in the tile + ``halo``.  ``m_norms[s]`` is a
     host [3,3] kornia matrix, or None for an empty slot (always zero).  ``tile_h``: tile rows
     (default ``_native.TILE_H``; the split-input conv's is ``_native.conv_tile_rows``)."""
     tile_h = _native.TILE_H if tile_h is None else int(tile_h)
+    tile_w = _native.TILE_W if tile_w is None else int(tile_w)
     n = len(m_norms)
     if not 0 < n <= 16:
         raise ValueError("need 1..16 slots")
@@ -322,12 +323,34 @@ def warp_tile_mask(m_norms, src_hw, grid_hw, row0: int, rows: int, halo: int, de
         arr[i].m = (ctypes.c_float * 9)(*mm)
     H, W = src_hw
     Ho, Wo = grid_hw
-    tiles = -(-rows // tile_h) * -(-Wo // _native.TILE_W)
+    tiles = -(-rows // tile_h) * -(-Wo // tile_w)
     mask = torch.zeros(tiles, dtype=torch.int32, device=device)
-    st = _native.load().mvbev_warp_tile_mask(arr, n, H, W, Ho, Wo, row0, rows, tile_h, _native.TILE_W,
+    st = _native.load().mvbev_warp_tile_mask(arr, n, H, W, Ho, Wo, row0, rows, tile_h, tile_w,
                                              halo, mask.data_ptr(), _stream(mask))
     _native.check(st, "mvbev_warp_tile_mask")
     return mask
+
+
+def ring_tile_mask(m_norms, src_hw, grid_hw, row0: int, rows: int, device, space: int) -> Optional[torch.Tensor]:
+    """Frustum mask (halo 1) of a dilation-1 ring conv's pixel tiles in tile space ``space``
+    (``_native.TILES_*``) over grid rows [row0, row0+rows): the regular 12 x 32 tiles of the
+    space's columns, then (edge strip) its edge_rows x EW tiles of the last columns.  None when
+    the space does not apply to this grid width."""
+    Wo = int(grid_hw[1])
+    d = conv_desc(1, 8, int(grid_hw[0]), Wo, group=8, group_stride=0, batch_stride=0, in_row0=row0, in_rows=rows,
+                  out_row0=row0, out_rows=rows)
+    g = _native.ring_tile_space(d, space)
+    if g is None:
+        return None
+    tiles_x, tiles_y, edge_tiles, ew, edge_rows = g
+    th = _native.conv_tile_rows(_native.LAYOUT_SPLIT_BF16, 1)
+    grid = warp_tile_mask(m_norms, src_hw, grid_hw, row0, rows, 1, device, tile_h=th)
+    grid = grid.reshape(tiles_y, -(-Wo // _native.TILE_W))[:, :tiles_x].reshape(-1)
+    if edge_tiles == 0:
+        return grid.contiguous()
+    strip = warp_tile_mask(m_norms, src_hw, grid_hw, row0, rows, 1, device, tile_h=edge_rows, tile_w=ew)
+    strip = strip.reshape(edge_tiles, -(-Wo // ew))[:, -1]
+    return torch.cat([grid, strip]).contiguous()
 
 
 def heavy_first_order(mask: torch.Tensor, B: int) -> torch.Tensor:
@@ -345,14 +368,15 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
                  init: Optional[torch.Tensor] = None, dilation: int = 1, relu: bool = False,
                  out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
                  group_mask: Optional[torch.Tensor] = None, tile_order: Optional[torch.Tensor] = None,
-                 sched=None) -> torch.Tensor:
+                 sched=None, tile_space: int = _native.TILES_GRID) -> torch.Tensor:
     """Low-level form: ``x`` addressed through ``desc`` (``mvbev_conv_desc``).  bf16x3 only,
     optional: ``workspace`` — device scratch for the split-K tail
     (``conv3x3_workspace_bytes``); ``group_mask`` — per-tile active channel groups
     (``warp_tile_mask``), whose cleared groups are skipped; ``tile_order`` — with a mask,
     the B x tiles pixel tiles in run order (``heavy_first_order``); ``sched`` — a ring-kernel
     schedule (``schedule.plan`` over ``schedule.ring_blocks``; split-bf16 x) replacing the
-    order."""
+    order; ``tile_space`` — ``_native.TILES_EDGE_STRIP``: the ring kernel's edge-strip tiles
+    (``mvbev_conv3x3_bf16x3_ex3``; the mask and order then index that space, ``ring_tile_mask``)."""
     _require_cuda(x, packed)
     bf16x3 = packed.dtype == torch.bfloat16
     if x.dtype not in ((torch.float32, torch.float16, torch.bfloat16) if bf16x3 else (torch.float32,)):
@@ -394,9 +418,15 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
         if workspace is not None:
             _require_cuda(workspace)
             wsp, wsn = workspace.data_ptr(), workspace.numel() * workspace.element_size()
+        if tile_space != _native.TILES_GRID:
+            g = _native.ring_tile_space(desc, tile_space) if layout == _native.LAYOUT_SPLIT_BF16 else None
+            if g is None or sched is not None or workspace is not None:
+                raise ValueError(f"tile space {tile_space} does not apply to this conv")
+            tiles = g[0] * g[1] + g[2]
+        else:
+            tiles = -(-desc.out_rows // _native.conv_tile_rows(layout, dilation)) * -(-W // _native.TILE_W)
         if group_mask is not None:
             _require_cuda(group_mask)
-            tiles = -(-desc.out_rows // _native.conv_tile_rows(layout, dilation)) * -(-W // _native.TILE_W)
             if group_mask.dtype != torch.int32 or group_mask.numel() < tiles or not group_mask.is_contiguous():
                 raise ValueError(f"group_mask must be a contiguous int32 tensor of >= {tiles} tiles")
             gmp = group_mask.data_ptr()
@@ -412,6 +442,13 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
                                                 _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32, gmp,
                                                 ctypes.byref(sched.c), _stream(x))
             _native.check(st, "mvbev_conv3x3_bf16x3_sched")
+            return out
+        if tile_space != _native.TILES_GRID:
+            st = lib.mvbev_conv3x3_bf16x3_ex3(x.data_ptr(), layout, ctypes.byref(desc), packed.data_ptr(), bp, ip,
+                                              cout, int(dilation), int(bool(relu)), out.data_ptr(),
+                                              _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32,
+                                              gmp, top, int(tile_space), _stream(x))
+            _native.check(st, "mvbev_conv3x3_bf16x3_ex3")
             return out
         st = lib.mvbev_conv3x3_bf16x3_ex(x.data_ptr(), layout, ctypes.byref(desc),
                                          packed.data_ptr(), bp, ip, cout, int(dilation), int(bool(relu)),

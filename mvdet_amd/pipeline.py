@@ -74,7 +74,8 @@ class ProjectFuse:
     def __init__(self, proj_mats: Sequence[torch.Tensor], src_hw: Tuple[int, int], grid_hw: Tuple[int, int],
                  channels: int, mid_channels: int = 512, slot_views: Optional[Sequence[Optional[int]]] = None,
                  precision: str = "bf16x3", slab_dtype: torch.dtype = torch.float32,
-                 all_views: bool = True, split_k: bool = True, frustum: bool = True, fuse_conv3: bool = True):
+                 all_views: bool = True, split_k: bool = True, frustum: bool = True, fuse_conv3: bool = True,
+                 edge_strip: bool = True):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":
@@ -127,6 +128,10 @@ class ProjectFuse:
         # conv2's epilogue computes conv3's per-tap partial sums instead of storing y2
         # (split-bf16 y1, i.e. the ring conv); training keeps y2 (its backward reads it)
         self.fuse_conv3 = fuse_conv3
+        # the forward conv1 (frustum-masked ring kernel) on edge-strip tiles where the grid width
+        # leaves a partial last tile column (W % 32 in 1..16: Wildtrack's 360 = 11 x 32 + 8), so
+        # no MFMA column is spent past W (mvbev_conv3x3_bf16x3_ex3); bitwise the same y1
+        self.edge_strip = edge_strip
 
     # -- buffers ----------------------------------------------------------------------------
     def workspace(self, B: int, device, band: Optional[Tuple[int, int]] = None) -> Workspace:
@@ -252,11 +257,28 @@ class ProjectFuse:
             self._masks[key] = m
         return m
 
-    def conv1_order(self, device, row0: int, rows: int, B: int) -> Optional[torch.Tensor]:
-        key = ("order", str(device), row0, rows, B)
+    def conv1_fwd_mask(self, device, row0: int, rows: int) -> Tuple[Optional[torch.Tensor], int]:
+        """(mask, tile space) of the forward conv1 over rows [row0, row0+rows): the edge-strip
+        space (``ops.ring_tile_mask``) where it applies, else the 12 x 32 grid of ``conv1_mask``."""
+        if not (self.frustum and self.split and self.edge_strip):
+            return self.conv1_mask(device, row0, rows), _native.TILES_GRID
+        key = ("fwd", str(device), row0, rows)
+        r = self._masks.get(key)
+        if r is None:
+            ms = [None if v is None else self.m_norm_cpu[v] for v in self.slot_views]
+            m = ops.ring_tile_mask(ms, self.src_hw, self.grid_hw, row0, rows, device, _native.TILES_EDGE_STRIP)
+            r = (m, _native.TILES_EDGE_STRIP) if m is not None else (self.conv1_mask(device, row0, rows),
+                                                                     _native.TILES_GRID)
+            self._masks[key] = r
+        return r
+
+    def conv1_order(self, device, row0: int, rows: int, B: int, grid: bool = False) -> Optional[torch.Tensor]:
+        """Heavy-first run order of the forward conv1's pixel tiles (``grid``: of the 12 x 32
+        grid even where the forward uses edge strips)."""
+        key = ("order", str(device), row0, rows, B, grid)
         o = self._masks.get(key)
         if o is None:
-            m = self.conv1_mask(device, row0, rows)
+            m = self.conv1_mask(device, row0, rows) if grid else self.conv1_fwd_mask(device, row0, rows)[0]
             if m is None:
                 return None
             o = ops.heavy_first_order(m, B)
@@ -280,19 +302,27 @@ class ProjectFuse:
             ty, tx = -(-rows // th), -(-self.grid_hw[1] // _native.TILE_W)
             blocks = schedule.ring_blocks(B, ty, tx, self.mid // ops.BN, 0, group_mask=m.cpu().tolist(),
                                           cpg=self.Cs // (2 * ops.KC),
-                                          order=self.conv1_order(device, row0, rows, B).cpu().tolist())
+                                          order=self.conv1_order(device, row0, rows, B, grid=True).cpu().tolist())
             cus = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
             sc = schedule.plan(blocks, cus, device, split=split, deal=self.mid // ops.BN)
             self._masks[key] = sc
         return sc
 
     def conv1_active_fraction(self, device, row0: int, rows: int) -> float:
-        """Fraction of conv1's (tile, slot) work the frustum mask keeps (1.0 = dense)."""
-        m = self.conv1_mask(device, row0, rows)
+        """Fraction of conv1's dense (pixel, slot) work the forward's frustum mask keeps (1.0 =
+        dense): per tile its enabled slots x its pixels inside the grid."""
+        m, space = self.conv1_fwd_mask(device, row0, rows)
         if m is None:
             return 1.0
-        bits = sum(bin(int(v) & 0xFFFFFFFF).count("1") for v in m.cpu().tolist())
-        return bits / (m.numel() * self.S)
+        W = self.grid_hw[1]
+        d = ops.conv_desc(1, 8, self.grid_hw[0], W, group=8, group_stride=0, batch_stride=0, in_row0=row0,
+                          in_rows=rows, out_row0=row0, out_rows=rows)
+        tiles_x, tiles_y, edge_tiles, ew, edge_rows = _native.ring_tile_space(d, space)
+        th, tw = self.conv1_tile_rows(), _native.TILE_W
+        pix = [min(th, rows - (t // tiles_x) * th) * min(tw, W - (t % tiles_x) * tw) for t in range(tiles_x * tiles_y)]
+        pix += [min(edge_rows, rows - e * edge_rows) * (W - tiles_x * tw) for e in range(edge_tiles)]
+        bits = [bin(int(v) & 0xFFFFFFFF).count("1") for v in m.cpu().tolist()]
+        return sum(b * p for b, p in zip(bits, pix)) / (rows * W * self.S)
 
     # -- a7-a9 ----------------------------------------------------------------------------
     def conv1(self, ws: Workspace, conv1: torch.nn.Conv2d, sched=None) -> torch.Tensor:
@@ -306,11 +336,15 @@ class ProjectFuse:
         a1, b1 = ws.y1_rows
         d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * H * W,
                            batch_stride=self.Cs * H * W, in_row0=0, in_rows=H, out_row0=a1, out_rows=b1 - a1)
-        gm = self.conv1_mask(ws.slab.device, a1, b1 - a1)
+        if sched is not None:  # host schedules are planned over the 12 x 32 grid
+            gm, space = self.conv1_mask(ws.slab.device, a1, b1 - a1), _native.TILES_GRID
+        else:
+            gm, space = self.conv1_fwd_mask(ws.slab.device, a1, b1 - a1)
         return ops.conv3x3_desc(ws.slab, d1, p1, self.mid, bias=None, init=init, dilation=1, relu=True,
                                 out=ws.y1, workspace=None if gm is not None else self._sk_ws(d1, ws.slab.device),
-                                group_mask=gm, tile_order=self.conv1_order(ws.slab.device, a1, b1 - a1, B),
-                                sched=sched)
+                                group_mask=gm, tile_order=self.conv1_order(ws.slab.device, a1, b1 - a1, B,
+                                                                           grid=space == _native.TILES_GRID),
+                                sched=sched, tile_space=space)
 
     def conv2(self, ws: Workspace, conv2: torch.nn.Conv2d) -> torch.Tensor:
         """a8: y2 = relu(conv3x3_d2(y1) + b2) on y2's rows."""
@@ -369,10 +403,10 @@ class ProjectFuse:
         p1 = self.pack1.get(map_classifier[0].weight)
         d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * H * W,
                            batch_stride=self.Cs * H * W, in_row0=0, in_rows=H, out_row0=0, out_rows=H)
-        gm = self.conv1_mask(ws.slab.device, 0, H)
+        gm = self.conv1_mask(ws.slab.device, 0, H)  # no ReLU: the grid tiles (edge strips are conv1+ReLU only)
         return ops.conv3x3_desc(ws.slab, d1, p1, self.mid, bias=None, init=None, dilation=1, relu=False,
                                 out=out, workspace=None if gm is not None else self._sk_ws(d1, ws.slab.device),
-                                group_mask=gm, tile_order=self.conv1_order(ws.slab.device, 0, H, B))
+                                group_mask=gm, tile_order=self.conv1_order(ws.slab.device, 0, H, B, grid=True))
 
     def finish_from_y1(self, ws: Workspace, map_classifier: torch.nn.Sequential, mark=None) -> torch.Tensor:
         """``ws.y1`` holds conv1's summed channel terms (no bias) for rows ``ws.y1_rows``:

@@ -353,6 +353,77 @@ def test_conv3x3_bf16x3_grouped_slab(S, Cs, layout):
     assert_parity(got, ref, f"grouped {layout}", normwise_tol=CONV_TOL["bf16x3"])
 
 
+@pytest.mark.parametrize("B,H,W,rows", [(1, 30, 360, (0, 30)),    # EW 8, 48-row strips (one partial)
+                                         (2, 25, 76, (3, 25)),     # EW 16 (W % 32 = 12), row band
+                                         (1, 61, 48, (0, 61)),     # EW 16 at W % 32 = 16, 3 strips
+                                         (2, 13, 37, (0, 13))])    # EW 8, W % 32 = 5
+@pytest.mark.parametrize("masked", [False, True])
+def test_conv3x3_edge_strip_tiles(B, H, W, rows, masked):
+    """MVBEV_TILES_EDGE_STRIP (mvbev_conv3x3_bf16x3_ex3): the last W % 32 columns as
+    (384/EW) x EW tiles give y bitwise equal to the 12 x 32 grid tiles (same per-pixel K order),
+    with and without a frustum-style group mask + heavy-first order, and match F.conv2d."""
+    from mvdet_amd import _native, ops
+    g = torch.Generator().manual_seed(H * W + B)
+    S, Cs, cout = 3, 16, 256
+    K = S * Cs
+    xs = torch.rand(S, B, Cs, H, W, generator=g)
+    # zero view 1 on the right part of the grid so a mask has something exact to skip
+    xs[1, :, :, :, W // 2:] = 0
+    w = (torch.rand(cout, K, 3, 3, generator=g) - 0.5) / np.sqrt(K * 9)
+    init = torch.rand(cout, H, W, generator=g)
+    r0, r1 = rows
+    ref = F.relu(F.conv2d(xs.permute(1, 0, 2, 3, 4).reshape(B, K, H, W), w, None, padding=1) + init)[:, :, r0:r1]
+    pk = ops.PackedConv3x3(None, "bf16x3").get(w.to(DEV))
+    slab = torch.stack([_split_encode(xs[v]) for v in range(S)]).to(DEV)
+    desc = ops.conv_desc(B, K, H, W, group=Cs, group_stride=B * Cs * H * W, batch_stride=Cs * H * W,
+                         out_row0=r0, out_rows=r1 - r0)
+    gx = _native.ring_tile_space(desc, _native.TILES_GRID)
+    es = _native.ring_tile_space(desc, _native.TILES_EDGE_STRIP)
+    assert es is not None and es[0] == W // 32 and es[3] == (8 if W % 32 <= 8 else 16)
+    assert es[2] == -(-(r1 - r0) // es[4])
+
+    def masks(space_geom):
+        tx, ty, ne, ew, er = space_geom
+        m = []
+        for t in range(tx * ty + ne):
+            c0 = (t % tx) * 32 if t < tx * ty else tx * 32
+            m.append(0b101 | (0b010 if c0 - 1 < W // 2 else 0))  # view 1 is zero from column W // 2 on
+        mt = torch.tensor(m, dtype=torch.int32, device=DEV)
+        return mt, ops.heavy_first_order(mt, B)
+
+    kw = dict(init=init.to(DEV), relu=True, dilation=1)
+    if masked:
+        gm, go = masks(gx)
+        em, eo = masks(es)
+        grid = ops.conv3x3_desc(slab, desc, pk, cout, group_mask=gm, tile_order=go, **kw)
+        strip = ops.conv3x3_desc(slab, desc, pk, cout, group_mask=em, tile_order=eo,
+                                 tile_space=_native.TILES_EDGE_STRIP, **kw)
+    else:
+        grid = ops.conv3x3_desc(slab, desc, pk, cout, **kw)
+        strip = ops.conv3x3_desc(slab, desc, pk, cout, tile_space=_native.TILES_EDGE_STRIP, **kw)
+    assert torch.equal(strip, grid)
+    assert_parity(strip.cpu(), ref, "edge strip", normwise_tol=CONV_TOL["bf16x3"])
+    # split-bf16 output (conv1 -> conv2 in the detector) is bitwise the same too
+    ysplit = torch.empty(ops.split_shape(B, cout, r1 - r0, W), dtype=torch.bfloat16, device=DEV)
+    ops.conv3x3_desc(slab, desc, pk, cout, out=ysplit, tile_space=_native.TILES_EDGE_STRIP, **kw)
+    assert torch.equal(ops.split_decode(ysplit, cout), ops.split_decode(
+        ops.conv3x3_desc(slab, desc, pk, cout, out=torch.empty_like(ysplit), **kw), cout))
+
+
+def test_edge_strip_refusals():
+    """Spaces that do not apply, and combinations the edge strip does not support, raise."""
+    from mvdet_amd import _native, ops
+    for W in (64, 250, 96):  # W % 32 == 0 or > 16: no strip
+        assert _native.ring_tile_space(ops.conv_desc(1, 16, 12, W, 16, 0, 0), _native.TILES_EDGE_STRIP) is None
+    x = torch.zeros(ops.split_shape(1, 16, 12, 40), dtype=torch.bfloat16, device=DEV)
+    pk = ops.PackedConv3x3(None, "bf16x3").get(torch.zeros(128, 16, 3, 3, device=DEV))
+    desc = ops.conv_desc(1, 16, 12, 40, 16, 0, 16 * 12 * 40)
+    with pytest.raises(_native.NativeError):  # dilation 2 / no ReLU: conv1 + ReLU only
+        ops.conv3x3_desc(x, desc, pk, 128, dilation=2, relu=True, tile_space=_native.TILES_EDGE_STRIP)
+    with pytest.raises(_native.NativeError):
+        ops.conv3x3_desc(x, desc, pk, 128, relu=False, tile_space=_native.TILES_EDGE_STRIP)
+
+
 @pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
 @pytest.mark.parametrize("d", [1, 2])
 def test_conv3x3_row_band_and_init(d, precision):

@@ -95,6 +95,15 @@ def backward_stages(eng, ws, mc, B, ho, wo, N, C, dev):
     }
 
 
+def _grid_tiles(eng, fn):
+    """Run fn with the engine's forward conv1 on the 12 x 32 tile grid (edge strips off)."""
+    keep, eng.edge_strip = eng.edge_strip, False
+    try:
+        return fn()
+    finally:
+        eng.edge_strip = keep
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3"],
@@ -127,6 +136,8 @@ def main():
             "warpup": (lambda: eng.warp_views_upsampled(ws, list(range(N)), bfeats), None),
             "warp1": (lambda: [eng.warp_view(ws, v, feats[v]) for v in range(N)], None),
             "conv1": (lambda: eng.conv1(ws, mc[0]), 2.0 * B * ho * wo * 9 * N * C * 512),
+            "conv1g": (lambda: _grid_tiles(eng, lambda: eng.conv1(ws, mc[0])),
+                       2.0 * B * ho * wo * 9 * N * C * 512),  # 12 x 32 grid tiles (no edge strip)
             "conv1s": (lambda: eng.conv1(ws, mc[0], sched=eng.conv1_schedule(dev, 0, ho, B)),
                        2.0 * B * ho * wo * 9 * N * C * 512),  # balanced schedule
             "conv1p": (lambda: eng.conv1(ws, mc[0], sched=eng.conv1_schedule(dev, 0, ho, B, split=False)),

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -361,7 +361,12 @@ typedef struct mvbev_conv_schedule {
 } mvbev_conv_schedule;
 size_t mvbev_conv_schedule_slot_bytes(void);
 /* mvbev_conv3x3_bf16x3_ex (split-bf16 x only) and mvbev_conv3x3_dgrad_bf16x3_ex (split-bf16 dy
- * only) run as scheduled (tile_order is replaced by the items). */
+ * only) run as scheduled (tile_order is replaced by the items).  _sched3: the forward with the
+ * tiles of tile_space (MVBEV_TILES_*; item tiles and group_mask index that space). */
+int mvbev_conv3x3_bf16x3_sched3(const void* x, int x_layout, const mvbev_conv_desc* desc, const void* w_packed,
+                                const float* bias, const float* init, int64_t Cout, int dilation, int relu, void* y,
+                                int y_layout, const uint32_t* group_mask, int tile_space,
+                                const mvbev_conv_schedule* sched, void* stream);
 int mvbev_conv3x3_bf16x3_sched(const void* x, int x_layout, const mvbev_conv_desc* desc, const void* w_packed,
                                const float* bias, const float* init, int64_t Cout, int dilation, int relu, void* y,
                                int y_layout, const uint32_t* group_mask, const mvbev_conv_schedule* sched,

@@ -65,6 +65,7 @@ EXPORTS = (
     "mvbev_conv3x3_dgrad_bf16x3_sched",
     "mvbev_conv_ring_tile_space",
     "mvbev_conv3x3_bf16x3_ex3",
+    "mvbev_conv3x3_bf16x3_sched3",
 )
 WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
 TILES_GRID, TILES_EDGE_STRIP = 0, 1  # MVBEV_TILES_*
@@ -201,6 +202,10 @@ def _declare(lib):
     lib.mvbev_conv3x3_bf16x3_sched.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64,
                                                ctypes.c_int, ctypes.c_int, _p, ctypes.c_int, _p,
                                                ctypes.POINTER(ConvSchedule), _p]
+    lib.mvbev_conv3x3_bf16x3_sched3.restype = ctypes.c_int
+    lib.mvbev_conv3x3_bf16x3_sched3.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64,
+                                                ctypes.c_int, ctypes.c_int, _p, ctypes.c_int, _p, ctypes.c_int,
+                                                ctypes.POINTER(ConvSchedule), _p]
     lib.mvbev_conv3x3_dgrad_bf16x3_sched.restype = ctypes.c_int
     lib.mvbev_conv3x3_dgrad_bf16x3_sched.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _i64,
                                                      ctypes.c_int, _p, ctypes.c_int, _p, _i64,

@@ -141,7 +141,7 @@ struct Args {
   int nfix;
   // edge strip (ring kernel, optional): pixel tiles [tiles_y * tiles_x, + edge_tiles) of each
   // batch item are edge_rows x (W - edge_x0) tiles of columns [edge_x0, W) (RingGeo EW)
-  int edge_tiles, edge_x0, edge_rows;
+  int edge_tiles, edge_x0, edge_rows, edge_w;
 };
 
 // Input tag: the split-bf16 blocked layout written by mvbev_warp_views_split_bf16 and by this
@@ -783,13 +783,17 @@ __global__ __launch_bounds__(RNT) void conv_ring_fixup_kernel(const Args a) {
           for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] += v[e];
         }
   }
-  const int tile = f.x, cot = tile % a.n_cot;
-  int rest = tile / a.n_cot;
-  const int tx = rest % a.tiles_x;
-  rest /= a.tiles_x;
-  const int ty = rest % a.tiles_y, b = rest / a.tiles_y;
+  // the ring kernel's tile decode and lane -> pixel map (edge-strip tiles: EW = a.edge_w)
+  const int tile = f.x, cot = tile % a.n_cot, rest = tile / a.n_cot;
+  const int t_main = a.tiles_y * a.tiles_x, t_all = t_main + a.edge_tiles;
+  const int pp = rest % t_all, b = rest / t_all;
+  const bool edge = pp >= t_main;
+  const int ty = pp / a.tiles_x;
+  const int x0 = edge ? a.edge_x0 : (pp - ty * a.tiles_x) * TW;
+  const int y0 = a.out_row0 + (edge ? (pp - t_main) * a.edge_rows : ty * RT);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), l32 = threadIdx.x & 31;
-  ring_epilogue<DIL, RELU, P3>(a, b, a.out_row0 + ty * RT + ring_base_row<DIL>(wave & 3), tx * TW + l32, cot,
+  const int ew = edge ? a.edge_w : TW;
+  ring_epilogue<DIL, RELU, P3>(a, b, y0 + ring_base_row<DIL>(wave & 3) + 12 * (l32 / ew), x0 + l32 % ew, cot,
                                64 * (wave >> 2), acc, lds);
 }
 
@@ -818,21 +822,9 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
   const int64_t plane = (int64_t)a.in_rows * W;
   const int64_t wchunk = (int64_t)a.n_cot * W16;
 
-  int tile = xcd_remap(blockIdx.x, a.nwg);
-  int ci0 = 0, ci1 = INT_MAX, pslot = -1;  // chunk range of this block, partial slot
-  if (a.items) {  // host schedule: the item of this block (tile < 0: padding)
-    if ((int)blockIdx.x >= a.nitems) return;
-    const int4 it = a.items[blockIdx.x];
-    if (it.x < 0) return;
-    tile = it.x, ci0 = it.y, ci1 = it.z, pslot = it.w;
-  } else if (a.gmask) {  // frustum mask: ordered pixel tiles dealt to the XCDs (see conv_kernel)
-    constexpr int Gq = MVBEV_MASK_GROUP;
-    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
-    const int q = j / a.n_cot;
-    const int slot = Gq * (8 * (q / Gq) + x) + q % Gq;
-    if (slot >= a.npix) return;  // padding block (whole block, before any barrier)
-    tile = (a.tile_order ? a.tile_order[slot] : slot) * a.n_cot + j % a.n_cot;
-  }
+  // One work item: chunks [ci0, ci1) of `tile`'s active-chunk sequence (all of it unscheduled);
+  // pslot >= 0: a piece of a split tile, whose raw partial sums conv_ring_fixup_kernel finishes.
+  auto run_item = [&](const int tile, const int ci0, int ci1, const int pslot) __attribute__((always_inline)) {
   // tile = (b, pixel tile pp, cot); pixel tiles: the tiles_y x tiles_x grid, then the edge strip
   const int cot = tile % a.n_cot;
   const int rest = tile / a.n_cot;
@@ -843,7 +835,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
   const int ty = pp / a.tiles_x;
   const int x0 = edge ? a.edge_x0 : (pp - ty * a.tiles_x) * TW;
   const int y0 = a.out_row0 + (edge ? (pp - t_main) * a.edge_rows : ty * RT);
-  // output-side mask: a tile of output channels nobody reads (whole block, before any barrier)
+  // output-side mask: a tile of output channels nobody reads (whole item, before any barrier)
   if (a.cmask && !((a.cmask[pp] >> (cot / a.cot_pg)) & 1u)) return;
   const u32x4* wsrc = a.wp + (int64_t)cot * W16;
   const uint32_t gm = a.gmask ? a.gmask[pp] : 0u;
@@ -1119,6 +1111,24 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
   } else {
     body(std::integral_constant<int, TW>{});
   }
+  };  // run_item
+
+  int tile = xcd_remap(blockIdx.x, a.nwg);
+  int ci0 = 0, ci1 = INT_MAX, pslot = -1;  // chunk range of this block, partial slot
+  if (a.items) {  // host schedule: the item of this block (tile < 0: padding)
+    if ((int)blockIdx.x >= a.nitems) return;
+    const int4 it = a.items[blockIdx.x];
+    if (it.x < 0) return;
+    tile = it.x, ci0 = it.y, ci1 = it.z, pslot = it.w;
+  } else if (a.gmask) {  // frustum mask: ordered pixel tiles dealt to the XCDs (see conv_kernel)
+    constexpr int Gq = MVBEV_MASK_GROUP;
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int q = j / a.n_cot;
+    const int slot = Gq * (8 * (q / Gq) + x) + q % Gq;
+    if (slot >= a.npix) return;  // padding block (whole block, before any barrier)
+    tile = (a.tile_order ? a.tile_order[slot] : slot) * a.n_cot + j % a.n_cot;
+  }
+  run_item(tile, ci0, ci1, pslot);
 #if MVBEV_RING_STAMP
   if (threadIdx.x == 0 && blockIdx.x < 16384) {  // vector stores of the block's wall-clock span and place
     const uint64_t stamp1 = __builtin_amdgcn_s_memrealtime();
@@ -1237,13 +1247,14 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   a.p3 = p3;
   a.tiles_x = (int)ceil_div(d->W, TW); a.tiles_y = (int)ceil_div(d->out_rows, ring ? RT : NW);
   a.n_cot = (int)(Cout / BN);
-  a.edge_tiles = 0, a.edge_x0 = 0, a.edge_rows = 0;
+  a.edge_tiles = 0, a.edge_x0 = 0, a.edge_rows = 0, a.edge_w = 0;
   int edge_w = 0;
   if (tile_space == MVBEV_TILES_EDGE_STRIP) {  // ring kernel, no schedule / output-side mask
     int64_t g[5];
-    if (!ring || sched || out_mask || ring_tile_space(d, tile_space, g) != MVBEV_OK) return MVBEV_ERR_SHAPE;
+    if (!ring || out_mask || ring_tile_space(d, tile_space, g) != MVBEV_OK) return MVBEV_ERR_SHAPE;
     a.tiles_x = (int)g[0];
     a.edge_tiles = (int)g[2], edge_w = (int)g[3], a.edge_rows = (int)g[4];
+    a.edge_w = edge_w;
     a.edge_x0 = (int)(g[0] * TW);
   } else if (tile_space != MVBEV_TILES_GRID) {
     return MVBEV_ERR_SHAPE;
@@ -1480,6 +1491,17 @@ int mvbev_cout1_reduce_partials(const void* partials, const mvbev_conv_desc* des
 }
 
 size_t mvbev_conv_schedule_slot_bytes(void) { return sizeof(mvbev::b3::floatx4) * mvbev::b3::kRingSlotF4; }
+
+int mvbev_conv3x3_bf16x3_sched3(const void* x, int x_layout, const mvbev_conv_desc* desc, const void* w_packed,
+                                const float* bias, const float* init, int64_t Cout, int dilation, int relu, void* y,
+                                int y_layout, const uint32_t* group_mask, int tile_space,
+                                const mvbev_conv_schedule* sched, void* stream) {
+  using namespace mvbev::b3;
+  if (!sched) return MVBEV_ERR_NULL;
+  if (x_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;  // the ring kernel's input
+  return launch<SplitIn>(x, desc, w_packed, bias, init, Cout, dilation, relu, static_cast<float*>(y), y_layout,
+                         group_mask, nullptr, nullptr, 0, stream, nullptr, 1, nullptr, nullptr, sched, tile_space);
+}
 
 int mvbev_conv3x3_bf16x3_sched(const void* x, int x_layout, const mvbev_conv_desc* desc, const void* w_packed,
                                const float* bias, const float* init, int64_t Cout, int dilation, int relu, void* y,

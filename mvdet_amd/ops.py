@@ -420,7 +420,7 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
             wsp, wsn = workspace.data_ptr(), workspace.numel() * workspace.element_size()
         if tile_space != _native.TILES_GRID:
             g = _native.ring_tile_space(desc, tile_space) if layout == _native.LAYOUT_SPLIT_BF16 else None
-            if g is None or sched is not None or workspace is not None:
+            if g is None or workspace is not None:
                 raise ValueError(f"tile space {tile_space} does not apply to this conv")
             tiles = g[0] * g[1] + g[2]
         else:
@@ -436,6 +436,13 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
             if group_mask is None or tile_order.dtype != torch.int32 or tile_order.numel() != B * tiles:
                 raise ValueError("tile_order must be an int32 permutation of the B x tiles pixel tiles")
             top = tile_order.data_ptr()
+        if sched is not None and tile_space != _native.TILES_GRID:
+            st = lib.mvbev_conv3x3_bf16x3_sched3(x.data_ptr(), layout, ctypes.byref(desc), packed.data_ptr(), bp, ip,
+                                                 cout, int(dilation), int(bool(relu)), out.data_ptr(),
+                                                 _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32, gmp,
+                                                 int(tile_space), ctypes.byref(sched.c), _stream(x))
+            _native.check(st, "mvbev_conv3x3_bf16x3_sched3")
+            return out
         if sched is not None:
             st = lib.mvbev_conv3x3_bf16x3_sched(x.data_ptr(), layout, ctypes.byref(desc), packed.data_ptr(), bp, ip,
                                                 cout, int(dilation), int(bool(relu)), out.data_ptr(),

@@ -75,7 +75,7 @@ class ProjectFuse:
                  channels: int, mid_channels: int = 512, slot_views: Optional[Sequence[Optional[int]]] = None,
                  precision: str = "bf16x3", slab_dtype: torch.dtype = torch.float32,
                  all_views: bool = True, split_k: bool = True, frustum: bool = True, fuse_conv3: bool = True,
-                 edge_strip: bool = True):
+                 edge_strip: bool = True, level_conv1: bool = False):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":
@@ -132,6 +132,13 @@ class ProjectFuse:
         # leaves a partial last tile column (W % 32 in 1..16: Wildtrack's 360 = 11 x 32 + 8), so
         # no MFMA column is spent past W (mvbev_conv3x3_bf16x3_ex3); bitwise the same y1
         self.edge_strip = edge_strip
+        # level_conv1: the forward conv1 runs a leveling schedule (schedule.plan_level: first
+        # round whole, later blocks cut so every CU ends near one level; pieces summed in K
+        # order).  Off by default: measured 7-10 % slower at cfg2 — the chip is power-limited
+        # under this MFMA load, so the CUs still busy in the hardware dispatch's ragged tail run
+        # faster (fewer chunks in flight, higher clock) and the idle CU-time costs far less than
+        # its share
+        self.level_conv1 = level_conv1
 
     # -- buffers ----------------------------------------------------------------------------
     def workspace(self, B: int, device, band: Optional[Tuple[int, int]] = None) -> Workspace:
@@ -308,6 +315,29 @@ class ProjectFuse:
             self._masks[key] = sc
         return sc
 
+    def conv1_level_schedule(self, device, row0: int, rows: int, B: int):
+        """The forward conv1's leveling schedule (``schedule.plan_level``) over its tile space
+        (``conv1_fwd_mask``); cached per geometry.  None without a frustum mask."""
+        key = ("level", str(device), row0, rows, B)
+        sc = self._masks.get(key)
+        if sc is None:
+            from . import schedule
+            m, space = self.conv1_fwd_mask(device, row0, rows)
+            if m is None or not self.split:
+                return None
+            W = self.grid_hw[1]
+            d = ops.conv_desc(1, 8, self.grid_hw[0], W, group=8, group_stride=0, batch_stride=0, in_row0=row0,
+                              in_rows=rows, out_row0=row0, out_rows=rows)
+            tiles_x, tiles_y, edge_tiles = _native.ring_tile_space(d, space)[:3]
+            n_cot = self.mid // ops.BN
+            blocks = schedule.ring_blocks(B, 1, tiles_x * tiles_y + edge_tiles, n_cot, 0,
+                                          group_mask=m.cpu().tolist(), cpg=self.Cs // (2 * ops.KC),
+                                          order=self.conv1_order(device, row0, rows, B).cpu().tolist())
+            cus = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
+            sc = schedule.plan_level(blocks, cus, device, n_cot)
+            self._masks[key] = sc
+        return sc
+
     def conv1_active_fraction(self, device, row0: int, rows: int) -> float:
         """Fraction of conv1's dense (pixel, slot) work the forward's frustum mask keeps (1.0 =
         dense): per tile its enabled slots x its pixels inside the grid."""
@@ -336,10 +366,12 @@ class ProjectFuse:
         a1, b1 = ws.y1_rows
         d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * H * W,
                            batch_stride=self.Cs * H * W, in_row0=0, in_rows=H, out_row0=a1, out_rows=b1 - a1)
-        if sched is not None:  # host schedules are planned over the 12 x 32 grid
+        if sched is not None:  # an explicit schedule (conv1_schedule) is planned over the 12 x 32 grid
             gm, space = self.conv1_mask(ws.slab.device, a1, b1 - a1), _native.TILES_GRID
         else:
             gm, space = self.conv1_fwd_mask(ws.slab.device, a1, b1 - a1)
+            if self.level_conv1 and gm is not None:
+                sched = self.conv1_level_schedule(ws.slab.device, a1, b1 - a1, B)
         return ops.conv3x3_desc(ws.slab, d1, p1, self.mid, bias=None, init=init, dilation=1, relu=True,
                                 out=ws.y1, workspace=None if gm is not None else self._sk_ws(d1, ws.slab.device),
                                 group_mask=gm, tile_order=self.conv1_order(ws.slab.device, a1, b1 - a1, B,

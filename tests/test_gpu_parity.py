@@ -294,15 +294,26 @@ def test_frustum_mask_is_exact_and_conv1_unchanged(cfg):
                              torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
                              torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False)).to(DEV)
     dense = ProjectFuse(pm, up, grid, C, frustum=False, split_k=False)
-    sparse = ProjectFuse(pm, up, grid, C, split_k=False)  # (split-K tails re-associate conv2's sums)
+    # (split-K tails and the leveling schedule's pieces re-associate the sums)
+    sparse = ProjectFuse(pm, up, grid, C, split_k=False)
+    leveled = ProjectFuse(pm, up, grid, C, split_k=False, level_conv1=True)
     assert sparse.frustum
     with torch.no_grad():
         ref = dense.project_fuse(feats, mc)
         y1_ref = dense.workspace(B, DEV).y1.clone()
         got = sparse.project_fuse(feats, mc)
         ws = sparse.workspace(B, DEV)
+        lev = leveled.project_fuse(feats, mc)
+        y1_lev = leveled.y1_fp32(leveled.workspace(B, DEV)).clone()
+        lev2 = leveled.project_fuse(feats, mc)
     assert torch.equal(ws.y1, y1_ref)
     assert torch.equal(got, ref)
+    # the leveled conv1 (pieces summed in K order by the fixup): deterministic, conv1-tolerance close
+    assert torch.equal(lev, lev2)
+    assert_parity(y1_lev.cpu(), sparse.y1_fp32(ws).cpu(), "leveled conv1", normwise_tol=1e-5)
+    assert_parity(lev.cpu(), ref.cpu(), "leveled map", normwise_tol=1e-5)
+    sch = leveled.conv1_level_schedule(DEV, 0, grid[0], B)
+    assert sch is not None and sch.predicted <= sch.predicted_plain
     H, W = grid
     th = sparse.conv1_tile_rows()
     mask = sparse.conv1_mask(DEV, 0, H).cpu().numpy().astype(np.uint32)

@@ -95,13 +95,14 @@ def backward_stages(eng, ws, mc, B, ho, wo, N, C, dev):
     }
 
 
-def _grid_tiles(eng, fn):
-    """Run fn with the engine's forward conv1 on the 12 x 32 tile grid (edge strips off)."""
-    keep, eng.edge_strip = eng.edge_strip, False
+def _with(eng, flag, value, fn):
+    """Run fn with the engine's boolean option ``flag`` (edge_strip, level_conv1) set to ``value``."""
+    keep = getattr(eng, flag)
+    setattr(eng, flag, value)
     try:
         return fn()
     finally:
-        eng.edge_strip = keep
+        setattr(eng, flag, keep)
 
 
 def main():
@@ -136,8 +137,10 @@ def main():
             "warpup": (lambda: eng.warp_views_upsampled(ws, list(range(N)), bfeats), None),
             "warp1": (lambda: [eng.warp_view(ws, v, feats[v]) for v in range(N)], None),
             "conv1": (lambda: eng.conv1(ws, mc[0]), 2.0 * B * ho * wo * 9 * N * C * 512),
-            "conv1g": (lambda: _grid_tiles(eng, lambda: eng.conv1(ws, mc[0])),
-                       2.0 * B * ho * wo * 9 * N * C * 512),  # 12 x 32 grid tiles (no edge strip)
+            "conv1g": (lambda: _with(eng, "edge_strip", False, lambda: eng.conv1(ws, mc[0])),
+                       2.0 * B * ho * wo * 9 * N * C * 512),  # 12 x 32 grid tiles
+            "conv1l": (lambda: _with(eng, "level_conv1", True, lambda: eng.conv1(ws, mc[0])),
+                       2.0 * B * ho * wo * 9 * N * C * 512),  # leveling schedule (schedule.plan_level)
             "conv1s": (lambda: eng.conv1(ws, mc[0], sched=eng.conv1_schedule(dev, 0, ho, B)),
                        2.0 * B * ho * wo * 9 * N * C * 512),  # balanced schedule
             "conv1p": (lambda: eng.conv1(ws, mc[0], sched=eng.conv1_schedule(dev, 0, ho, B, split=False)),

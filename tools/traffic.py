@@ -14,6 +14,7 @@ import collections
 import csv
 import glob
 import json
+import re
 import statistics
 import sys
 
@@ -40,8 +41,10 @@ for name in vals:
     rd = 32 * n32 + 64 * n64 + 128 * n128
     res["kernels"][name] = {"read_bytes": rd, "write_bytes": wr * 1024, "hbm_bytes_per_launch": rd + wr * 1024,
                             "fetch_size_kb": med(name, "FETCH_SIZE")}
-pat = "conv_ring_kernel<1, true>" if precision == "bf16x3" else "conv3x3_mfma_f32_kernel<1, true"
-conv1 = [k for k in res["kernels"] if pat in k]
+# conv1: the ReLU dilation-1 ring kernel without the fused cout1 epilogue (grid tiles "<1, true>",
+# edge-strip tiles "<1, true, false, EW>"), or the fp32-MFMA kernel
+pat = r"conv_ring_kernel<1, true(, false, \d+)?>" if precision == "bf16x3" else r"conv3x3_mfma_f32_kernel<1, true"
+conv1 = [k for k in res["kernels"] if re.search(pat, k)]
 if conv1:
     res["conv1_hbm_bytes_per_launch"] = res["kernels"][conv1[0]]["hbm_bytes_per_launch"]
 # the all-views warp of the timed "warp" stage: the largest-grid warp_tile_kernel dispatch

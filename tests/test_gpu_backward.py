@@ -118,7 +118,8 @@ def test_upsampled_warp_adjoint_vs_autograd(B, C, h, w, H, W, ho, wo):
 
 @pytest.mark.parametrize("B,C,H,W,ho,wo", [(1, 5, 27, 48, 12, 36), (2, 37, 30, 41, 17, 23),
                                            (1, 3, 9, 11, 20, 30), (1, 72, 90, 160, 120, 360),
-                                           (2, 16, 30, 41, 17, 23)])
+                                           (2, 16, 30, 41, 17, 23),
+                                           (2, 24, 36, 48, 20, 30)])  # split: the pixel-quad kernel
 def test_warp_adjoint_gather_vs_grid_sample_autograd(B, C, H, W, ho, wo):
     """The CSR-gather adjoint (plan once per geometry): equals grid_sample's backward, is
     bitwise deterministic, overwrites or accumulates, and its plan holds one entry per
@@ -159,6 +160,10 @@ def test_warp_adjoint_gather_vs_grid_sample_autograd(B, C, H, W, ho, wo):
         ops.warp_views_adjoint(split, plans, outs_s)
         for i in range(n):
             assert_parity(outs_s[i].cpu(), refs[i], f"adjoint gather (split grad_out) view {i}")
+        acc_s = [o.clone() for o in outs_s]
+        ops.warp_views_adjoint(split, plans, acc_s, accumulate=True)
+        for a, o in zip(acc_s, outs_s):
+            assert torch.allclose(a, 2 * o, rtol=1e-6, atol=0)
 
 
 def test_warp_backward_no_gradient_from_outside_samples():

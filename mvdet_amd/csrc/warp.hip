@@ -13,7 +13,7 @@
 //   out = sum over the 4 in-bounds corners of src * bilinear weight    (zeros padding;
 //         a non-finite ix/iy gives NaN in every channel, like torch's CPU grid_sample)
 //
-// Kernel shape (HBM-bound gather): a block is a 2-D output tile of TH x TW = 256 pixels
+// Kernel shape (HBM-bound gather): a block is a 2-D output tile of TH x TW pixels
 // (one thread per pixel; each wave a WR x 64/WR sub-tile) and a slice of 64 channels.  The pixel's transform, corner offsets and weights are computed
 // once and reused over the channel slice; 4 channels x 4 corners of loads are in flight
 // per thread.  The compact 2-D tile keeps each source footprint inside one block (the
@@ -27,7 +27,7 @@
 namespace mvbev {
 
 template <typename T, int UNROLL, bool SPLIT, bool PAIR>
-__global__ __launch_bounds__(256) void warp_tile_kernel(const WarpArgs a) {
+__global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_tile_kernel(const WarpArgs a) {
   // Logical block order (batch*view, channel chunk, tile) with tile fastest, dealt to the
   // XCDs in contiguous ranges: neighbouring tiles of one plane share an L2 (their source
   // footprints overlap in the far field, where many grid cells map into one source line).
@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void warp_tile_kernel(const WarpArgs a) {
   const WarpView& vw = a.v[view];
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
   constexpr int WC = 64 / kWarpWR, WAVES_X = kWarpTW / WC;
-  static_assert(kWarpTH * kWarpTW == 256 && kWarpTW % WC == 0 && kWarpTH % kWarpWR == 0, "tile");
+  static_assert(kWarpTH * kWarpTW % 64 == 0 && kWarpTH * kWarpTW <= 1024 && kWarpTW % WC == 0 && kWarpTH % kWarpWR == 0, "tile");
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int v = ty * kWarpTH + (wave / WAVES_X) * kWarpWR + lane / WC;
   const int u = tx * kWarpTW + (wave % WAVES_X) * WC + lane % WC;
@@ -149,11 +149,11 @@ template <typename T, bool SPLIT>
 static void launch_warp_t(const WarpArgs& a, hipStream_t s) {
   if constexpr (std::is_same<T, float>::value) {
     if (a.pair) {
-      hipLaunchKernelGGL((warp_tile_kernel<T, 4, SPLIT, true>), dim3((unsigned)a.nwg), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((warp_tile_kernel<T, 4, SPLIT, true>), dim3((unsigned)a.nwg), dim3(kWarpTH * kWarpTW), 0, s, a);
       return;
     }
   }
-  hipLaunchKernelGGL((warp_tile_kernel<T, 4, SPLIT, false>), dim3((unsigned)a.nwg), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((warp_tile_kernel<T, 4, SPLIT, false>), dim3((unsigned)a.nwg), dim3(kWarpTH * kWarpTW), 0, s, a);
 }
 
 template <typename T>

@@ -8,10 +8,12 @@ namespace mvbev {
 // Gather warp (warp_tile_kernel) tiling.  A/B on cfg2 (7 views, 1 launch, split-bf16 out):
 // 64 ch/block with 4x16 waves 0.51 ms; 32 ch 0.47; 16 ch 0.44; 8 ch 0.416; 8 ch with 8x8
 // waves 0.391 (square wave footprints; a block's few planes keep the XCD's L2 working set
-// small, so neighbouring tiles still find their shared source lines there).
+// small, so neighbouring tiles still find their shared source lines there).  Block tile
+// (round 2, same box, 8 ch, 8x8 waves): 32x32 0.492 ms, 16x32 0.452, 16x16 0.350-0.366,
+// 8x16 0.358, 8x8 0.360, 16x8 0.356 (two waves stacked vertically)
 #ifndef MVBEV_WARP_TH
 #define MVBEV_WARP_TH 16
-#define MVBEV_WARP_TW 16
+#define MVBEV_WARP_TW 8
 #define MVBEV_WARP_WR 8
 #endif
 #ifndef MVBEV_WARP_CPB
@@ -28,10 +30,11 @@ constexpr int kWarpTW = MVBEV_WARP_TW;    // output cols per block
 constexpr int kWarpWR = MVBEV_WARP_WR;    // output rows per wave (wave tile WR x 64/WR)
 constexpr int kWarpCPB = MVBEV_WARP_CPB;  // channels per block
 // fused upsample+warp (warp_up_kernel): cfg2 +a4 A/B 64 ch/block, 4x16 waves 0.478 ms;
-// 32 ch 0.476; 16 ch 8x8 waves 0.476; 8 ch 8x8 waves 0.372
+// 32 ch 0.476; 16 ch 8x8 waves 0.476; 8 ch 8x8 waves 0.372; block tile (round 2, same box):
+// 16x16 0.338, 16x8 0.335, 8x8 (one wave) 0.330
 #ifndef MVBEV_WARPUP_TH
-#define MVBEV_WARPUP_TH 16
-#define MVBEV_WARPUP_TW 16
+#define MVBEV_WARPUP_TH 8
+#define MVBEV_WARPUP_TW 8
 #define MVBEV_WARPUP_WR 8
 #endif
 #ifndef MVBEV_WARPUP_CPB

@@ -29,7 +29,7 @@ struct UpArgs {
 typedef float f32x4u_t __attribute__((ext_vector_type(4), aligned(4)));
 
 template <typename T, bool SPLIT, bool QUAD>
-__global__ __launch_bounds__(256) void warp_up_kernel(const UpArgs ua) {
+__global__ __launch_bounds__(kUpTH * kUpTW) void warp_up_kernel(const UpArgs ua) {
   const WarpArgs& a = ua.w;
   const int lb = xcd_remap(blockIdx.x, a.nwg);
   const int tile = lb % a.tiles;
@@ -178,15 +178,15 @@ extern "C" int mvbev_warp_views_upsampled_ex(const mvbev_warp_view* views, int n
   for (int i = 0; i < nviews; ++i) quad = quad && views[i].src_strides[3] == 1;
   if (out_layout == MVBEV_LAYOUT_SPLIT_BF16) {
     if (src_is_f16)
-      hipLaunchKernelGGL((warp_up_kernel<__half, true, false>), dim3((unsigned)a.nwg), dim3(256), 0, st, ua);
+      hipLaunchKernelGGL((warp_up_kernel<__half, true, false>), dim3((unsigned)a.nwg), dim3(kUpTH * kUpTW), 0, st, ua);
     else if (quad)
-      hipLaunchKernelGGL((warp_up_kernel<float, true, true>), dim3((unsigned)a.nwg), dim3(256), 0, st, ua);
+      hipLaunchKernelGGL((warp_up_kernel<float, true, true>), dim3((unsigned)a.nwg), dim3(kUpTH * kUpTW), 0, st, ua);
     else
-      hipLaunchKernelGGL((warp_up_kernel<float, true, false>), dim3((unsigned)a.nwg), dim3(256), 0, st, ua);
+      hipLaunchKernelGGL((warp_up_kernel<float, true, false>), dim3((unsigned)a.nwg), dim3(kUpTH * kUpTW), 0, st, ua);
   } else if (quad) {
-    hipLaunchKernelGGL((warp_up_kernel<float, false, true>), dim3((unsigned)a.nwg), dim3(256), 0, st, ua);
+    hipLaunchKernelGGL((warp_up_kernel<float, false, true>), dim3((unsigned)a.nwg), dim3(kUpTH * kUpTW), 0, st, ua);
   } else {
-    hipLaunchKernelGGL((warp_up_kernel<float, false, false>), dim3((unsigned)a.nwg), dim3(256), 0, st, ua);
+    hipLaunchKernelGGL((warp_up_kernel<float, false, false>), dim3((unsigned)a.nwg), dim3(kUpTH * kUpTW), 0, st, ua);
   }
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;

@@ -127,7 +127,8 @@ def run_single(args, precision, steps, warmup, with_cpu):
     mc = build_mc(C, N, params, dev)
     half = args.config == 4
     eng = ProjectFuse(pm, up, (ho, wo), C, precision=precision,
-                      slab_dtype=torch.float16 if half else torch.float32)
+                      slab_dtype=torch.float16 if half else torch.float32,
+                      wino_conv1=args.conv1 == "wino" and precision == "bf16x3")
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * args.config + v,
                                           device=dev).to(torch.float16 if half else torch.float32)
              for v in range(N)]
@@ -135,7 +136,8 @@ def run_single(args, precision, steps, warmup, with_cpu):
     views = list(range(N))
 
     K, W = steps, warmup
-    ev = {k: [torch.cuda.Event(enable_timing=True) for _ in range(K)] for k in ("warp", "conv1", "conv2", "conv3")}
+    ev = {k: [torch.cuda.Event(enable_timing=True) for _ in range(K)]
+          for k in ("warp", "conv1", "conv1_wino", "conv2", "conv3")}
     end_ev = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
 
     def step(i=None):
@@ -161,6 +163,9 @@ def run_single(args, precision, steps, warmup, with_cpu):
 
     t_warp = avg(ev["warp"], ev["conv1"])
     t_c1 = avg(ev["conv1"], ev["conv2"])
+    wino = eng.wino_conv1  # conv1 = the row transform (wino_rows_kernel) + conv_wino_kernel
+    t_rows = avg(ev["conv1"], ev["conv1_wino"]) if wino else 0.0
+    t_c1k = t_c1 - t_rows  # conv1's conv kernel alone
     t_c2 = avg(ev["conv2"], ev["conv3"])
     t_c3 = avg(ev["conv3"], end_ev)
     value = B * K / dt
@@ -172,8 +177,8 @@ def run_single(args, precision, steps, warmup, with_cpu):
     tv = [touched_footprint(M.numpy(), up, (ho, wo)) for M in pm]
     warp_bytes = sum(s * B * C * (t + ho * wo) for t in tv)
     conv3_bytes = 4.0 * B * ho * wo * (512 + 1)
-    conv1_alg_tfs = conv1_flop / (t_c1 * 1e-3) / 1e12
-    active = eng.conv1_active_fraction(dev, *ws.y1_rows[:1], ws.y1_rows[1] - ws.y1_rows[0]) \
+    conv1_alg_tfs = conv1_flop / (t_c1k * 1e-3) / 1e12  # over the conv kernel's time
+    active = eng.conv1_active_fraction(dev, *ws.y1_rows[:1], ws.y1_rows[1] - ws.y1_rows[0], grid=wino) \
         if precision == "bf16x3" else 1.0
 
     def mfma_s(c1_scale):
@@ -186,14 +191,17 @@ def run_single(args, precision, steps, warmup, with_cpu):
         # bf16 MFMA work the split needs: 3 passes per fp32 product (no padding MFMAs; the
         # tile-edge columns a 32-wide tile computes past W=360 are waste, not counted).
         # Algorithmic = the reference's dense conv; the frustum mask executes `active` of it.
-        achieved, peak = conv1_alg_tfs * 3, BF16_MFMA_PEAK_TFS
-        kname = "conv_ring_kernel (conv1: 3xbf16 MFMA, LDS-DMA ring, frustum-masked)"
+        # Winograd F(3,3) along the rows executes 5 of the direct conv's 9 MFMA K-blocks per
+        # (chunk, kernel column): its MFMA work is 5/9 of the direct count
+        achieved, peak = conv1_alg_tfs * 3 * (5.0 / 9.0 if wino else 1.0), BF16_MFMA_PEAK_TFS
+        kname = ("conv_wino_kernel (conv1: row-Winograd F(3,3), 3xbf16 MFMA, LDS-DMA unit ring, frustum-masked)"
+                 if wino else "conv_ring_kernel (conv1: 3xbf16 MFMA, LDS-DMA ring, frustum-masked)")
     else:
         achieved, peak = conv1_alg_tfs, FP32_MFMA_PEAK_TFS
         kname = "conv3x3_mfma_f32 (conv1)"
     sustained = mfma_probe() if precision == "bf16x3" and not args.no_probe else None
     traffic, warp_traffic = None, None
-    tfile = ROOT / "profiles" / f"traffic_cfg{args.config}_{precision}.json"
+    tfile = ROOT / "profiles" / f"traffic_cfg{args.config}_{precision}{'_wino' if wino else ''}.json"
     if tfile.exists():
         tj = json.loads(tfile.read_text())
         traffic, warp_traffic = tj.get("conv1_hbm_bytes_per_launch"), tj.get("warp_hbm_bytes_per_launch")
@@ -210,7 +218,9 @@ def run_single(args, precision, steps, warmup, with_cpu):
         # above the MFMA rate the kernel really sustains, by 1/active).
         "roofline": {"kernel": kname, "bound": "mfma", "achieved": round(achieved * active, 2), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(achieved * active / peak, 4), "traffic": traffic,
-                     "basis": ("3 bf16 MFMA passes x 2*B*Ho*Wo*9*(N*C)*512 x frustum_active_fraction"
+                     "basis": (("3 bf16 MFMA passes x 5/9 (row Winograd) x 2*B*Ho*Wo*9*(N*C)*512 x "
+                                "frustum_active_fraction over the conv kernel's time" if wino else
+                                "3 bf16 MFMA passes x 2*B*Ho*Wo*9*(N*C)*512 x frustum_active_fraction")
                                if precision == "bf16x3" else "2*B*Ho*Wo*9*(N*C)*512 at the fp32 MFMA peak"),
                      "frustum_active_fraction": round(active, 4),
                      "dense_algorithmic_achieved": round(achieved, 2),
@@ -221,9 +231,13 @@ def run_single(args, precision, steps, warmup, with_cpu):
                      # under MFMA load: MI355X_MICROARCH.md "DVFS give-back"), and conv1's
                      # executed rate as a fraction of it
                      "sustained_peak": round(sustained, 1) if sustained else None,
-                     "frac_of_sustained": round(achieved * active / sustained, 4) if sustained else None},
+                     "frac_of_sustained": round(achieved * active / sustained, 4) if sustained else None,
+                     # the direct conv's executed bf16 work over conv1's whole time (transform included)
+                     "direct_equiv_achieved": round(3 * conv1_flop * active / (t_c1 * 1e-3) / 1e12, 2)
+                     if precision == "bf16x3" else None},
         "stages_ms": {"warp_all_views": round(t_warp, 4), "conv1": round(t_c1, 4), "conv2": round(t_c2, 4),
-                      "conv3": round(t_c3, 4)},
+                      "conv3": round(t_c3, 4),
+                      **({"conv1_wino_rows": round(t_rows, 4), "conv1_wino_conv": round(t_c1k, 4)} if wino else {})},
         # SURVEY §8(d) "achieved fraction": the stages' roofline floors over the measured step;
         # conv1+conv2 priced as the 3 bf16 MFMA passes the split executes (bf16x3) or at the
         # fp32 MFMA peak (fp32); conv1 counted for its frustum-active products only (the
@@ -271,7 +285,8 @@ def run_plus_a4(args, precision, steps, warmup):
     ho, wo = ds.reducedgrid_shape
     pm = projection_matrices(ds)
     mc = build_mc(C, N, head_params(N, seed=args.config, C=C), dev)
-    eng = ProjectFuse(pm, up, (ho, wo), C, precision=precision)
+    eng = ProjectFuse(pm, up, (ho, wo), C, precision=precision,
+                      wino_conv1=args.conv1 == "wino" and precision == "bf16x3")
     flo = [synthetic.backbone_features(B, C, lo, seed=1000 * args.config + v, device=dev) for v in range(N)]
     ws = eng.workspace(B, dev)
     views = list(range(N))
@@ -430,6 +445,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--conv1", default="wino", choices=["direct", "wino"],
+                    help="conv1 form (bf16x3): the direct ring conv or row-Winograd F(3,3) (ProjectFuse wino_conv1)")
     ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3"],
                     help="conv1/conv2 arithmetic: 3xbf16 split (default) or fp32-input MFMA")
     ap.add_argument("--config", type=int, default=2, help="BASELINE.json config index (1-based)")

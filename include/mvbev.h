@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -262,6 +262,30 @@ int mvbev_conv3x3_bf16x3_ex3(const void* x, int x_layout, const mvbev_conv_desc*
                              int64_t Cout, int dilation, int relu, void* y, int y_layout,
                              const uint32_t* group_mask, const int32_t* tile_order, int tile_space,
                              void* stream);
+
+/* Row-Winograd form of the forward conv1 (map_classifier[0:2], persp_trans_detector.py:51-52,
+ * dilation 1): F(3,3) along the rows, y = A^T [(G w) . (B^T d)] per kernel column, 5 instead of 9
+ * MFMA K-blocks per (16-channel chunk, kernel column); same 3xbf16 split products, fp32 accumulate.
+ * Replaces the same call as mvbev_conv3x3_bf16x3_ex with dilation 1 (the reference's
+ * nn.Conv2d(512*N+2, 512, 3, padding=1) forward, :51), in two steps:
+ *   1. mvbev_wino_rows_split_bf16: the split-bf16 input x (desc as mvbev_conv3x3_bf16x3_ex) ->
+ *      T = B^T over each 3-row output tile's 5 input rows, split-bf16 blocked
+ *      [B][K/8][5 * 4 * ceil(out_rows / 12)][W][hi, lo][8] (mvbev_wino_rows_bytes).  With
+ *      group_mask (12 x 32 tiles, as the conv) the cleared (tile, group) pairs are not written:
+ *      T must then be zero-filled once and only ever written by this call with the same mask.
+ *   2. mvbev_conv3x3_wino_bf16x3: y from T (desc: B, K, H, W, group, out_row0, out_rows as in
+ *      step 1), weights from mvbev_pack_conv3x3_weight_wino (same arguments as
+ *      mvbev_pack_conv3x3_weight_bf16x3), bias / init / relu / y / y_layout / group_mask /
+ *      tile_order as mvbev_conv3x3_bf16x3_ex (grid tiles, 12 x 32). */
+size_t mvbev_conv3x3_packed_bytes_wino(int64_t Cout, int64_t K);
+int mvbev_pack_conv3x3_weight_wino(const float* w, int64_t Cout, int64_t Cin_w, const int32_t* chan_map,
+                                   int64_t K, void* w_packed, void* stream);
+size_t mvbev_wino_rows_bytes(const mvbev_conv_desc* desc);
+int mvbev_wino_rows_split_bf16(const void* x, const mvbev_conv_desc* desc, const uint32_t* group_mask, void* t,
+                               size_t t_bytes, void* stream);
+int mvbev_conv3x3_wino_bf16x3(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,
+                              const float* init, int64_t Cout, int relu, void* y, int y_layout,
+                              const uint32_t* group_mask, const int32_t* tile_order, void* stream);
 
 /* conv2 -> conv3 without conv2's activation in HBM (map_classifier[2:5],
  * persp_trans_detector.py:53-54, inference): the split-bf16-input conv of

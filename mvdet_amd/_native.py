@@ -66,6 +66,11 @@ EXPORTS = (
     "mvbev_conv_ring_tile_space",
     "mvbev_conv3x3_bf16x3_ex3",
     "mvbev_conv3x3_bf16x3_sched3",
+    "mvbev_conv3x3_packed_bytes_wino",
+    "mvbev_pack_conv3x3_weight_wino",
+    "mvbev_wino_rows_bytes",
+    "mvbev_wino_rows_split_bf16",
+    "mvbev_conv3x3_wino_bf16x3",
 )
 WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
 TILES_GRID, TILES_EDGE_STRIP = 0, 1  # MVBEV_TILES_*
@@ -159,6 +164,17 @@ def _declare(lib):
     lib.mvbev_conv3x3_bf16x3_ex3.restype = ctypes.c_int
     lib.mvbev_conv3x3_bf16x3_ex3.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64,
                                              ctypes.c_int, ctypes.c_int, _p, ctypes.c_int, _p, _p, ctypes.c_int, _p]
+    lib.mvbev_conv3x3_packed_bytes_wino.restype = ctypes.c_size_t
+    lib.mvbev_conv3x3_packed_bytes_wino.argtypes = [_i64, _i64]
+    lib.mvbev_pack_conv3x3_weight_wino.restype = ctypes.c_int
+    lib.mvbev_pack_conv3x3_weight_wino.argtypes = [_p, _i64, _i64, _p, _i64, _p, _p]
+    lib.mvbev_wino_rows_bytes.restype = ctypes.c_size_t
+    lib.mvbev_wino_rows_bytes.argtypes = [ctypes.POINTER(ConvDesc)]
+    lib.mvbev_wino_rows_split_bf16.restype = ctypes.c_int
+    lib.mvbev_wino_rows_split_bf16.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, ctypes.c_size_t, _p]
+    lib.mvbev_conv3x3_wino_bf16x3.restype = ctypes.c_int
+    lib.mvbev_conv3x3_wino_bf16x3.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64, ctypes.c_int, _p,
+                                              ctypes.c_int, _p, _p, _p]
     lib.mvbev_warp_tile_mask.restype = ctypes.c_int
     lib.mvbev_warp_tile_mask.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
                                          _i64, _i64, _i64, _i64, _p, _p]

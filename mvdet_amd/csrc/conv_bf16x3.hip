@@ -1350,6 +1350,440 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   return MVBEV_OK;
 }
 
+// ---------------------------------------------------------------------------------------
+// Row-Winograd conv1 (forward, dilation 1, split-bf16 input): F(3,3) along the rows.
+//
+// The ring kernel's wave computes 3 output rows from 5 input rows per kernel column kw,
+//     y_i = sum_kh w[kh] d[i + kh]    (i, kh < 3: 9 products per channel and pixel).
+// With the interpolation points {0, 1, -1, 2, inf} that is  y = A^T [(G w) . (B^T d)]:
+// 5 products.  B^T d is computed once per frame by wino_rows_kernel into the T layout (the
+// split-bf16 blocked layout over 5 transformed rows per 3-row output tile), G w once per
+// weight version (pack_wino_kernel).  The conv is the ring kernel with the unit (chunk, kw)
+// replaced by (chunk, xi): per unit a wave runs its 3 kernel columns against one transformed
+// row (18 MFMAs into acc[ct][xi]) and the epilogue applies A^T to the 5 accumulators (exact
+// small-integer weights, fp32).  Per (chunk, kw): 5 instead of 9 MFMA K-blocks (x0.556).
+//   A^T = [1 1 1 1 0; 0 1 -1 2 0; 0 1 1 4 1]
+//   G   = [1/2 0 0; -1/2 -1/2 -1/2; -1/6 1/6 -1/6; 1/6 1/3 2/3; 0 0 1]
+//   B^T = [2 -1 -2 1 0; 0 -2 -1 1 0; 0 2 -3 1 0; 0 -1 0 1 0; 0 2 -1 -2 1]
+// T and G w are split hi/lo like the slab and the direct weights (the products keep the
+// 3xbf16 accuracy); the transforms' roundings add about as much error again as the direct
+// conv's (numpy emulation at K = 2048: 1.1e-5 vs 5.6e-6 normwise), far inside the 1e-3 gate.
+namespace wino {
+constexpr int NXI = 5;                            // transformed rows per 3-row output tile
+constexpr int XH = 4 * NXI;                       // T rows of a 12-row workgroup tile
+constexpr int XW = TW + 2;
+#ifndef MVBEV_WINO_NIW
+#define MVBEV_WINO_NIW 8  // DMA-issuing waves (cfg2 winoconv: 8 1.59-1.67 ms, 4 1.73-1.79)
+#endif
+#ifndef MVBEV_WINO_XAUX
+#define MVBEV_WINO_XAUX 2  // cache policy of the T DMAs (2 = nt: T is streamed, the weights stay in L2; -2 %)
+#endif
+constexpr int NIW = MVBEV_WINO_NIW;               // DMA-issuing waves
+constexpr int NIT = 64 * NIW;
+constexpr int NWI = RUNIT / NIT;                  // weight DMAs per issuing wave per unit (3)
+// a unit (chunk, xi) stages its weights (3 kernel columns) and its T row of the 4 row tiles,
+// [sub][part][row tile][XW], together in one ring slot
+constexpr int TROW = 2 * 2 * 4 * XW;              // T entries of a unit (544)
+constexpr int NXT = (TROW + NIT - 1) / NIT;       // T DMAs per issuing wave per unit (2)
+constexpr int SLOT = RUNIT + NXT * NIT;           // 16-B entries per ring slot
+constexpr int NSLOT = 4;                          // 3 units of DMA in flight
+constexpr int LDS = NSLOT * SLOT;                 // 160 KiB
+static_assert(LDS * 16 <= 160 * 1024, "LDS");
+constexpr int NTAP = 3 * NXI;                     // packed taps (xi, kw)
+constexpr int WPART = NTAP * KC * BN;             // bf16 per part per (chunk, cout tile)
+constexpr int W16 = 2 * WPART * 2 / 16;           // 16-B pieces per (chunk, cout tile)
+}  // namespace wino
+
+// packed[chunk][cot][part][3 xi + kw][sub][co][j] = split(sum_kh G[xi][kh] w[co][map(k)][kh][kw])
+__global__ void pack_wino_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int Cout, int Cin_w,
+                                 const int32_t* __restrict__ chan_map, int K, int K_pad) {
+  const int n_cot = Cout / BN;
+  const int64_t total = (int64_t)(K_pad / KC) * n_cot * 2 * wino::WPART;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i;
+    const int j = r % SB; r /= SB;
+    const int co = r % BN; r /= BN;
+    const int sub = r % 2; r /= 2;
+    const int tap = r % wino::NTAP; r /= wino::NTAP;
+    const int part = r % 2; r /= 2;
+    const int cot = r % n_cot;
+    const int chunk = (int)(r / n_cot);
+    const int k = chunk * KC + sub * SB + j;
+    int ci = k < K ? (chan_map ? chan_map[k] : k) : -1;
+    if (ci >= Cin_w) ci = -1;
+    float v = 0.f;
+    if (ci >= 0) {
+      const float* g = w + ((int64_t)(cot * BN + co) * Cin_w + ci) * 9 + tap % 3;  // g[3 kh]
+      const double g0 = g[0], g1 = g[3], g2 = g[6];
+      const int xi = tap / 3;
+      const double u = xi == 0 ? 0.5 * g0
+                     : xi == 1 ? -0.5 * (g0 + g1 + g2)
+                     : xi == 2 ? (g1 - g0 - g2) / 6.0
+                     : xi == 3 ? (g0 + 2.0 * g1 + 4.0 * g2) / 6.0
+                               : g2;
+      v = (float)u;
+    }
+    const __bf16 hi = (__bf16)v;
+    out[i] = part ? (__bf16)(v - (float)hi) : hi;
+  }
+}
+
+struct WinoRowsArgs {
+  const u32x4* x;
+  u32x4* t;
+  int64_t group_stride, batch_stride;  // elements, as mvbev_conv_desc
+  int K, group, H, W, in_row0, in_rows, out_row0, tiles_x, tiles_y;
+  const uint32_t* gmask;
+};
+
+__device__ inline void bf16x8_to_f32(const u32x4 v, float (&f)[8]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(v[i] << 16);
+    f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+
+// T[b][k / 8][5 r3 + xi][col][hi, lo][8] = split((B^T d)[xi]),
+//   d[m] = x[b][k][out_row0 + 3 r3 - 1 + m][col] (zero outside the image and the input rows),
+// r3 < 4 tiles_y (the 12 x 32 tiles of the conv).  Workgroup = (pixel tile, channel group, b);
+// with a frustum mask the groups it clears for the tile are skipped: the conv never reads them
+// there, and the T columns a neighbouring tile's halo reads from a skipped tile are zero both
+// in T (zero-filled, never written) and in the true transform (the mask covers the halo).
+__global__ __launch_bounds__(256) void wino_rows_kernel(const WinoRowsArgs a) {
+  constexpr int KB = 8;  // 8-channel blocks per workgroup: 4 x 32 x 8 items, 4 per thread
+  const int pp = blockIdx.x, b = blockIdx.z;
+  const int nbg = (a.group / SB + KB - 1) / KB;
+  const int g = blockIdx.y / nbg, kb0 = (blockIdx.y - g * nbg) * KB;
+  if (a.gmask && !((a.gmask[pp] >> g) & 1u)) return;
+  const int W = a.W;
+  const int ty = pp / a.tiles_x;
+  const int x0 = (pp - ty * a.tiles_x) * TW;
+  const int nb = a.group / SB, K8 = a.K / SB, R5 = 5 * 4 * a.tiles_y;
+  const int64_t plane = (int64_t)a.in_rows * W;
+  const int c = threadIdx.x % TW, q = (threadIdx.x / TW) % 4, kq = threadIdx.x / (4 * TW);  // kq < 2
+  const int col = x0 + c, r3 = 4 * ty + q;
+  if (col >= W) return;
+  // the 5 input rows of the row tile (all 4 items of the thread share them)
+  int64_t roff[5];
+  bool rok[5];
+#pragma unroll
+  for (int m = 0; m < 5; ++m) {
+    const int row = a.out_row0 + 3 * r3 - 1 + m, by = row - a.in_row0;
+    rok[m] = row >= 0 && row < a.H && by >= 0 && by < a.in_rows;
+    roff[m] = 2 * ((int64_t)by * W + col);
+  }
+  u32x4 raw[4][5][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // all loads first: 40 in flight per thread
+    const int kb = kb0 + kq + 2 * i;
+    const bool kok = kb < nb && g * a.group + kb * SB < a.K;
+    const u32x4* src = a.x + ((int64_t)b * a.batch_stride + (int64_t)g * a.group_stride +
+                              (int64_t)(kok ? kb : 0) * SB * plane) / 4;
+#pragma unroll
+    for (int m = 0; m < 5; ++m)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) raw[i][m][p] = (kok && rok[m]) ? src[roff[m] + p] : u32x4{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int kb = kb0 + kq + 2 * i, k0 = g * a.group + kb * SB;
+    if (kb >= nb || k0 >= a.K) continue;
+    float d[5][8];
+#pragma unroll
+    for (int m = 0; m < 5; ++m) {
+      float h[8], l[8];
+      bf16x8_to_f32(raw[i][m][0], h);
+      bf16x8_to_f32(raw[i][m][1], l);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[m][j] = h[j] + l[j];
+    }
+    u32x4* dst = a.t + 2 * (((int64_t)b * K8 + k0 / SB) * R5 * W + (int64_t)5 * r3 * W + col);
+#pragma unroll
+    for (int xi = 0; xi < 5; ++xi) {
+      unsigned hp[4], lp[4];
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        unsigned short hs[2], ls[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int j = 2 * e4 + e;
+          const float d0 = d[0][j], d1 = d[1][j], d2 = d[2][j], d3 = d[3][j], d4 = d[4][j];
+          const float v = xi == 0 ? 2.f * d0 - d1 - 2.f * d2 + d3
+                        : xi == 1 ? -2.f * d1 - d2 + d3
+                        : xi == 2 ? 2.f * d1 - 3.f * d2 + d3
+                        : xi == 3 ? d3 - d1
+                                  : 2.f * d1 - d2 - 2.f * d3 + d4;
+          const __bf16 hv = (__bf16)v, lv = (__bf16)(v - (float)hv);
+          hs[e] = __builtin_bit_cast(unsigned short, hv);
+          ls[e] = __builtin_bit_cast(unsigned short, lv);
+        }
+        hp[e4] = (unsigned)hs[0] | ((unsigned)hs[1] << 16);
+        lp[e4] = (unsigned)ls[0] | ((unsigned)ls[1] << 16);
+      }
+      dst[2 * (int64_t)xi * W] = u32x4{hp[0], hp[1], hp[2], hp[3]};
+      dst[2 * (int64_t)xi * W + 1] = u32x4{lp[0], lp[1], lp[2], lp[3]};
+    }
+  }
+}
+
+#ifndef MVBEV_WINO_ABL
+#define MVBEV_WINO_ABL 0  // timing ablations only (wrong results): bit 0 no unit barrier / wait, bit 1 no DMA in the loop
+#endif
+template <bool RELU>
+__global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
+  using namespace wino;
+  __shared__ __attribute__((aligned(16))) u32x4 lds[LDS];
+  const int W = a.W;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, kl = lane >> 5;
+
+  int tile = xcd_remap(blockIdx.x, a.nwg);
+  if (a.gmask) {  // ordered pixel tiles dealt to the XCDs, as the ring kernel
+    constexpr int Gq = MVBEV_MASK_GROUP;
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int q = j / a.n_cot;
+    const int slot = Gq * (8 * (q / Gq) + x) + q % Gq;
+    if (slot >= a.npix) return;  // padding block (whole block, before any barrier)
+    tile = (a.tile_order ? a.tile_order[slot] : slot) * a.n_cot + j % a.n_cot;
+  }
+  const int cot = tile % a.n_cot, rest = tile / a.n_cot;
+  const int t_main = a.tiles_y * a.tiles_x;
+  const int pp = rest % t_main, b = rest / t_main;
+  const int ty = pp / a.tiles_x;
+  const int x0 = (pp - ty * a.tiles_x) * TW;
+  const int y0 = a.out_row0 + ty * RT;
+  const u32x4* wsrc = a.wp + (int64_t)cot * wino::W16;
+  const int64_t wchunk = (int64_t)a.n_cot * wino::W16;
+  const uint32_t gm = a.gmask ? a.gmask[pp] : 0u;
+  const int nch = a.gmask ? __builtin_popcount(gm) * a.cpg : a.nchunks;
+  auto chunk_of = [&](int i) -> int {
+    if (!a.gmask) return i;
+    uint32_t m = gm;
+    for (int j = i / a.cpg; j > 0; --j) m &= m - 1;
+    return __builtin_ctz(m) * a.cpg + i % a.cpg;
+  };
+  const int K8 = a.K / SB;
+  const int64_t tplane2 = 2LL * (XH * a.tiles_y) * W;  // 16-B pieces per 8-channel block of T
+  // unit (physical chunk ch, row xi) -> ring slot: weights [part][kw][sub][co] from the packed
+  // [part][3 xi + kw][sub][co], then the T row: entry e = (sub, part, row tile, col) -> T row
+  // XH ty + NXI rt + xi, column x0 - 1 + col (zero outside the grid)
+  auto issue_unit = [&](int ch, int xi, int slot) __attribute__((always_inline)) {
+    if (wave >= NIW) return;
+    const u32x4* src = wsrc + (int64_t)ch * wchunk + xi * 3 * 2 * BN;
+    u32x4* dst = lds + slot * SLOT + wave * 64;
+#pragma unroll
+    for (int j = 0; j < NWI; ++j) {
+      const int e = (j * NIW + wave) * 64 + lane;
+      glds16(src + (e / RHALF) * (NTAP * 2 * BN) + e % RHALF, dst + j * NIT);
+    }
+    const u32x4* xs[2];
+    bool kv[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int k0 = ch * KC + s * SB;
+      kv[s] = k0 < a.K;
+      xs[s] = static_cast<const u32x4*>(a.x) + ((int64_t)b * K8 + (kv[s] ? k0 / SB : 0)) * tplane2;
+    }
+#pragma unroll
+    for (int j = 0; j < NXT; ++j) {
+      const int e = (j * NIW + wave) * 64 + lane;
+      const int sub = e / (TROW / 2), part = (e / (TROW / 4)) & 1, rt = (e % (TROW / 4)) / XW, c = e % XW;
+      const int gx = x0 - 1 + c;
+      const bool z = e >= TROW || gx < 0 || gx >= W || !(sub ? kv[1] : kv[0]);
+      glds16<MVBEV_WINO_XAUX>(z ? g_ring_zero : (sub ? xs[1] : xs[0]) + 2 * ((XH * ty + NXI * rt + xi) * W + gx) + part,
+             dst + RUNIT + j * NIT);
+    }
+  };
+  // physical chunks: the current one and the next (past the last one it stays there: dummy
+  // loads that keep the vmcnt counts exact)
+  int cur_ph = chunk_of(0), nx_i = 1;
+  int nx_ph = chunk_of(min(1, max(nch - 1, 0)));
+  auto advance = [&]() __attribute__((always_inline)) {
+    cur_ph = nx_ph;
+    nx_i += 1;
+    nx_ph = chunk_of(min(nx_i, nch - 1));
+  };
+
+  const int rg = wave & 3;
+  const int cw = 64 * (wave >> 2);
+  floatx16 acc[2][NXI];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NXI; ++j) acc[i][j] = floatx16{0};
+  // one B set, refilled per kernel column right after its MFMAs (kw 0, 1 of the next unit after
+  // the unit's barrier, kw 2 at the unit's start); two A sets alternating per kernel column
+  bf16x8 fb[3][2];     // [kw][hi, lo]
+  bf16x8 fa[2][2][2];  // [set][ct][hi, lo]
+  auto fetch_b = [&](int kw, int slot) __attribute__((always_inline)) {
+    const u32x4* X = lds + slot * SLOT + RUNIT + kl * (TROW / 2) + rg * XW + l32 + kw;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) fb[kw][p] = __builtin_bit_cast(bf16x8, X[p * (TROW / 4)]);
+  };
+  auto fetch_a = [&](int st, int slot, int kw) __attribute__((always_inline)) {
+    const u32x4* Wl = lds + slot * SLOT + kw * 2 * BN + kl * BN + cw + l32;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) fa[st][ct][p] = __builtin_bit_cast(bf16x8, Wl[p * RHALF + 32 * ct]);
+  };
+  auto sched6 = [&](auto nreads) __attribute__((always_inline)) {
+    constexpr int n = decltype(nreads)::value;  // fragment reads spread over a kernel column's 6 MFMAs
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if (i < n) __builtin_amdgcn_sched_group_barrier(0x100, (n + 5) / 6, 0);
+    }
+  };
+
+  if (nch > 0) {
+    const int U = NXI * nch;
+    // prologue: units 0-3 (chunk 0, rows 0-3) in flight, wait for unit 0
+    issue_unit(cur_ph, 0, 0);
+    issue_unit(cur_ph, 1, 1);
+    issue_unit(cur_ph, 2, 2);
+    issue_unit(cur_ph, 3, 3);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (NWI + NXT)) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    fetch_b(0, 0);
+    fetch_b(1, 0);
+    fetch_a(0, 0, 0);
+    // unit u = u0 + R, R < 10 compile-time (u0 a multiple of 10): xi = R % 5, fragment set
+    // R & 1; ring slot u % 4 (runtime)
+#define WINO_MFMAS(AS, KW, XI)                                                                       \
+  _Pragma("unroll") for (int ct = 0; ct < 2; ++ct) {                                                 \
+    acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][1], fb[KW][0], acc[ct][XI], 0, 0, 0); \
+    acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][1], acc[ct][XI], 0, 0, 0); \
+    acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][0], acc[ct][XI], 0, 0, 0); \
+  }
+#define WINO_UNIT(R)                                                                                 \
+  do {                                                                                               \
+    constexpr int XI = (R) % 5, P = (R) & 1;                                                          \
+    if (u0 + (R) >= U) break;                                                                        \
+    const int slot = (u0 + (R)) & 3, nslot = (u0 + (R) + 1) & 3;                                      \
+    fetch_a(P ^ 1, slot, 1);                                                                         \
+    fetch_b(2, slot);                                                                                \
+    WINO_MFMAS(P, 0, XI);                                                                            \
+    sched6(std::integral_constant<int, 6>{});                                                        \
+    fetch_a(P, slot, 2);                                                                             \
+    WINO_MFMAS(P ^ 1, 1, XI);                                                                        \
+    sched6(std::integral_constant<int, 4>{});                                                        \
+    /* retire unit u+1; every LDS read of this unit's slot is done */                                 \
+    if (!(MVBEV_WINO_ABL & 1)) {                                                                     \
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * (NWI + NXT)) : "memory");              \
+      __builtin_amdgcn_s_barrier();                                                                  \
+    }                                                                                                \
+    asm volatile("" ::: "memory");                                                                   \
+    /* unit u+4 into this slot: (chunk, xi 4) at xi 0, else (next chunk, xi - 1) */                  \
+    if (!(MVBEV_WINO_ABL & 2)) issue_unit(XI == 0 ? cur_ph : nx_ph, (XI + 4) % 5, slot);             \
+    if (XI == 4) advance();                                                                          \
+    fetch_b(0, nslot);                                                                               \
+    fetch_b(1, nslot);                                                                               \
+    fetch_a(P ^ 1, nslot, 0);                                                                        \
+    WINO_MFMAS(P, 2, XI);                                                                            \
+    sched6(std::integral_constant<int, 8>{});                                                        \
+  } while (0)
+    for (int u0 = 0; u0 < U; u0 += 10) {
+      WINO_UNIT(0);
+      WINO_UNIT(1);
+      WINO_UNIT(2);
+      WINO_UNIT(3);
+      WINO_UNIT(4);
+      WINO_UNIT(5);
+      WINO_UNIT(6);
+      WINO_UNIT(7);
+      WINO_UNIT(8);
+      WINO_UNIT(9);
+    }
+#undef WINO_UNIT
+#undef WINO_MFMAS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the block exits
+  }
+  // y = A^T M per (Cout block, lane element): the 3 output rows of the wave's row tile
+  floatx16 y[2][3];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    const floatx16 m0 = acc[ct][0], m1 = acc[ct][1], m2 = acc[ct][2], m3 = acc[ct][3], m4 = acc[ct][4];
+    y[ct][0] = m0 + m1 + m2 + m3;
+    y[ct][1] = m1 - m2 + 2.f * m3;
+    y[ct][2] = m1 + m2 + 4.f * m3 + m4;
+  }
+  ring_epilogue<1, RELU, false>(a, b, y0 + 3 * rg, x0 + l32, cot, cw, y, lds);
+}
+
+static int wino_rows_launch(const void* x, const mvbev_conv_desc* d, const uint32_t* group_mask, void* t,
+                            size_t t_bytes, void* stream) {
+  if (!x || !d || !t) return MVBEV_ERR_NULL;
+  if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || d->in_rows <= 0 || d->out_rows <= 0 || d->group <= 0)
+    return MVBEV_ERR_RANK;
+  if (d->K % SB != 0 || d->group % SB != 0 || d->K % d->group != 0) return MVBEV_ERR_SHAPE;
+  if (d->out_row0 < 0 || d->out_row0 + d->out_rows > d->H || d->K / d->group > 65535 || d->B > 65535)
+    return MVBEV_ERR_SHAPE;
+  const int64_t tiles_y = ceil_div(d->out_rows, RT), tiles_x = ceil_div(d->W, TW);
+  const int64_t need = d->B * (d->K / SB) * 5 * 4 * tiles_y * d->W * 32;
+  if ((size_t)need > t_bytes || 2 * need / 32 > (int64_t)INT32_MAX * 8) return MVBEV_ERR_SHAPE;
+  if (group_mask && d->K / d->group > 32) return MVBEV_ERR_SHAPE;
+  if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(t)) & 15) != 0) return MVBEV_ERR_ALIGN;
+  WinoRowsArgs a;
+  a.x = static_cast<const u32x4*>(x);
+  a.t = static_cast<u32x4*>(t);
+  a.group_stride = d->group_stride, a.batch_stride = d->batch_stride;
+  a.K = (int)d->K, a.group = (int)d->group, a.H = (int)d->H, a.W = (int)d->W;
+  a.in_row0 = (int)d->in_row0, a.in_rows = (int)d->in_rows, a.out_row0 = (int)d->out_row0;
+  a.tiles_x = (int)tiles_x, a.tiles_y = (int)tiles_y;
+  a.gmask = group_mask;
+  const int64_t nbg = ceil_div(d->group / SB, 8);  // wino_rows_kernel's KB
+  if ((d->K / d->group) * nbg > 65535) return MVBEV_ERR_SHAPE;
+  hipLaunchKernelGGL(wino_rows_kernel, dim3((unsigned)(tiles_x * tiles_y), (unsigned)((d->K / d->group) * nbg), (unsigned)d->B),
+                     dim3(256), 0, as_stream(stream), a);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_packed, const float* bias,
+                       const float* init, int64_t Cout, int relu, float* y, int y_layout,
+                       const uint32_t* group_mask, const int32_t* tile_order, void* stream) {
+  if (!t || !d || !w_packed || !y) return MVBEV_ERR_NULL;
+  if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || d->out_rows <= 0 || d->group <= 0)
+    return MVBEV_ERR_RANK;
+  if (Cout % BN != 0 || d->K % SB != 0 || d->group % SB != 0 || d->K % d->group != 0) return MVBEV_ERR_SHAPE;
+  if (d->out_row0 < 0 || d->out_row0 + d->out_rows > d->H || d->H > INT32_MAX / 2 || d->W > INT32_MAX / 2)
+    return MVBEV_ERR_SHAPE;
+  if (y_layout != MVBEV_LAYOUT_F32 && y_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;
+  if (((reinterpret_cast<uintptr_t>(w_packed) | reinterpret_cast<uintptr_t>(t)) & 15) != 0) return MVBEV_ERR_ALIGN;
+  Args a{};
+  a.x = t; a.wp = static_cast<const u32x4*>(w_packed); a.bias = bias; a.init = init; a.y = y;
+  a.B = (int)d->B; a.group = (int)d->group; a.K = (int)d->K; a.nchunks = (int)ceil_div(d->K, KC);
+  a.Cout = (int)Cout; a.H = (int)d->H; a.W = (int)d->W;
+  a.in_row0 = 0; a.in_rows = (int)d->H;
+  a.out_row0 = (int)d->out_row0; a.out_rows = (int)d->out_rows;
+  a.tiles_x = (int)ceil_div(d->W, TW); a.tiles_y = (int)ceil_div(d->out_rows, RT);
+  a.n_cot = (int)(Cout / BN);
+  const int64_t tiles = (int64_t)a.tiles_x * a.tiles_y * a.n_cot * d->B;
+  if (tiles > INT32_MAX / 2 || 2LL * 5 * 4 * a.tiles_y * a.W * (d->K / SB) * d->B > (int64_t)INT32_MAX * 64)
+    return MVBEV_ERR_SHAPE;
+  if (group_mask) {
+    if (d->group % KC != 0 || d->K / d->group > 32) return MVBEV_ERR_SHAPE;
+    a.gmask = group_mask;
+    a.cpg = (int)(d->group / KC);
+  }
+  a.tile_order = group_mask ? tile_order : nullptr;
+  a.y_split = y_layout == MVBEV_LAYOUT_SPLIT_BF16;
+  a.npix = (int)(tiles / a.n_cot);
+  const int64_t nwg = group_mask ? (int64_t)a.n_cot * round_up(a.npix, 8 * MVBEV_MASK_GROUP) : tiles;
+  a.nwg = (int)nwg;
+  hipStream_t s = as_stream(stream);
+  if (relu)
+    hipLaunchKernelGGL((conv_wino_kernel<true>), dim3((unsigned)nwg), dim3(RNT), 0, s, a);
+  else
+    hipLaunchKernelGGL((conv_wino_kernel<false>), dim3((unsigned)nwg), dim3(RNT), 0, s, a);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
 }  // namespace b3
 }  // namespace mvbev
 
@@ -1545,6 +1979,47 @@ int mvbev_conv3x3_dgrad_bf16x3(const float* dy, const mvbev_conv_desc* desc, con
                                int64_t cot_per_group, void* stream) {
   return mvbev_conv3x3_dgrad_bf16x3_ex(dy, MVBEV_LAYOUT_F32, desc, w_packed, Cout_p, dilation, dx, dx_layout, out_mask,
                                        cot_per_group, stream);
+}
+
+size_t mvbev_conv3x3_packed_bytes_wino(int64_t Cout, int64_t K) {
+  if (Cout <= 0 || K <= 0) return 0;
+  return (size_t)(mvbev::round_up(K, mvbev::b3::KC) / mvbev::b3::KC) * (size_t)(Cout / mvbev::b3::BN) *
+         mvbev::b3::wino::W16 * 16;
+}
+
+int mvbev_pack_conv3x3_weight_wino(const float* w, int64_t Cout, int64_t Cin_w, const int32_t* chan_map, int64_t K,
+                                   void* w_packed, void* stream) {
+  using namespace mvbev;
+  if (!w || !w_packed) return MVBEV_ERR_NULL;
+  if (Cout <= 0 || Cin_w <= 0 || K <= 0) return MVBEV_ERR_RANK;
+  if (Cout % b3::BN != 0) return MVBEV_ERR_SHAPE;
+  if (!chan_map && K != Cin_w) return MVBEV_ERR_SHAPE;
+  const int64_t total = (int64_t)mvbev_conv3x3_packed_bytes_wino(Cout, K) / 2;
+  const int blocks = (int)std::min<int64_t>(ceil_div(total, 256), 8192);
+  hipLaunchKernelGGL(b3::pack_wino_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), w,
+                     static_cast<__bf16*>(w_packed), (int)Cout, (int)Cin_w, chan_map, (int)K,
+                     (int)round_up(K, b3::KC));
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+size_t mvbev_wino_rows_bytes(const mvbev_conv_desc* d) {
+  using namespace mvbev;
+  if (!d || d->B <= 0 || d->K <= 0 || d->W <= 0 || d->out_rows <= 0) return 0;
+  return (size_t)d->B * (size_t)(ceil_div(d->K, b3::SB)) * 5 * 4 * (size_t)ceil_div(d->out_rows, b3::RT) *
+         (size_t)d->W * 32;
+}
+
+int mvbev_wino_rows_split_bf16(const void* x, const mvbev_conv_desc* desc, const uint32_t* group_mask, void* t,
+                               size_t t_bytes, void* stream) {
+  return mvbev::b3::wino_rows_launch(x, desc, group_mask, t, t_bytes, stream);
+}
+
+int mvbev_conv3x3_wino_bf16x3(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,
+                              const float* init, int64_t Cout, int relu, void* y, int y_layout,
+                              const uint32_t* group_mask, const int32_t* tile_order, void* stream) {
+  return mvbev::b3::wino_launch(t, desc, w_packed, bias, init, Cout, relu, static_cast<float*>(y), y_layout,
+                                group_mask, tile_order, stream);
 }
 
 #if MVBEV_RING_STAMP

@@ -247,10 +247,14 @@ class PackedConv3x3:
     ``precision``: "fp32" (fp32 MFMA, exact fp32 products) or "bf16x3" (hi/lo bf16 split,
     three bf16 MFMA passes, fp32 accumulation)."""
 
-    def __init__(self, chan_map: Optional[Sequence[int]] = None, precision: str = "fp32"):
+    def __init__(self, chan_map: Optional[Sequence[int]] = None, precision: str = "fp32", wino: bool = False):
         if precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {PRECISIONS}")
+        if wino and precision != "bf16x3":
+            raise ValueError("the row-Winograd packing is bf16x3")
         self.precision = precision
+        # wino: the row-Winograd weights G w of mvbev_pack_conv3x3_weight_wino (conv3x3_wino)
+        self.wino = wino
         self._key = None
         self.packed: Optional[torch.Tensor] = None
         self.chan_map = None if chan_map is None else [int(c) for c in chan_map]
@@ -282,6 +286,12 @@ class PackedConv3x3:
                 st = lib.mvbev_pack_conv3x3_weight_f32(w.data_ptr(), cout, cin, cmap, K, packed.data_ptr(),
                                                        _stream(packed))
                 _native.check(st, "mvbev_pack_conv3x3_weight_f32")
+            elif self.wino:
+                n = lib.mvbev_conv3x3_packed_bytes_wino(cout, K)
+                packed = torch.empty(n // 2, dtype=torch.bfloat16, device=weight.device)
+                st = lib.mvbev_pack_conv3x3_weight_wino(w.data_ptr(), cout, cin, cmap, K, packed.data_ptr(),
+                                                        _stream(packed))
+                _native.check(st, "mvbev_pack_conv3x3_weight_wino")
             else:
                 n = lib.mvbev_conv3x3_packed_bytes_bf16x3(cout, K)
                 packed = torch.empty(n // 2, dtype=torch.bfloat16, device=weight.device)
@@ -468,6 +478,80 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
         st = lib.mvbev_conv3x3_f32(x.data_ptr(), ctypes.byref(desc), packed.data_ptr(), bp, ip, cout,
                                    int(dilation), int(bool(relu)), out.data_ptr(), _stream(x))
         _native.check(st, "mvbev_conv3x3_f32")
+    return out
+
+
+def wino_rows_bytes(desc) -> int:
+    """Bytes of the row-Winograd transform T of a conv1 input (``mvbev_wino_rows_bytes``)."""
+    return int(_native.load().mvbev_wino_rows_bytes(ctypes.byref(desc)))
+
+
+def wino_rows(x: torch.Tensor, desc, t: torch.Tensor, group_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """B^T over every 3-row output tile's 5 input rows of the split-bf16 ``x`` (addressed through
+    ``desc`` as ``conv3x3_desc``) into ``t`` (bf16, >= ``wino_rows_bytes`` bytes; with
+    ``group_mask`` zero-filled once and only written by this call with that mask):
+    ``mvbev_wino_rows_split_bf16``."""
+    _require_cuda(x, t)
+    if x.dtype != torch.bfloat16 or t.dtype != torch.bfloat16 or not t.is_contiguous():
+        raise TypeError("wino_rows reads the split-bf16 slab and writes a contiguous bf16 T")
+    gmp = None
+    if group_mask is not None:
+        _require_cuda(group_mask)
+        tiles = -(-desc.out_rows // 12) * -(-desc.W // _native.TILE_W)
+        if group_mask.dtype != torch.int32 or group_mask.numel() < tiles or not group_mask.is_contiguous():
+            raise ValueError(f"group_mask must be a contiguous int32 tensor of >= {tiles} tiles")
+        gmp = group_mask.data_ptr()
+    st = _native.load().mvbev_wino_rows_split_bf16(x.data_ptr(), ctypes.byref(desc), gmp, t.data_ptr(),
+                                                   t.numel() * t.element_size(), _stream(x))
+    _native.check(st, "mvbev_wino_rows_split_bf16")
+    return t
+
+
+def conv3x3_wino(t: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: Optional[torch.Tensor] = None,
+                 init: Optional[torch.Tensor] = None, relu: bool = False, out: Optional[torch.Tensor] = None,
+                 group_mask: Optional[torch.Tensor] = None,
+                 tile_order: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The dilation-1 3x3 conv of ``conv3x3_desc`` from its row-Winograd transform ``t``
+    (``wino_rows``) with ``PackedConv3x3(..., wino=True)`` weights: ``mvbev_conv3x3_wino_bf16x3``.
+    ``out``: fp32 [B, cout, out_rows, W] or split-bf16 (``split_shape``); mask / order as the
+    12 x 32 grid tiles of ``conv3x3_desc``."""
+    _require_cuda(t, packed)
+    B, W, out_rows = desc.B, desc.W, desc.out_rows
+    lib = _native.load()
+    if packed.numel() * packed.element_size() < lib.mvbev_conv3x3_packed_bytes_wino(cout, desc.K):
+        raise ValueError("packed weights are smaller than the Winograd conv needs")
+    if t.numel() * t.element_size() < wino_rows_bytes(desc):
+        raise ValueError("t is smaller than the descriptor's row-Winograd transform")
+    y_split = out is not None and out.dtype == torch.bfloat16
+    if out is None:
+        out = torch.empty((B, cout, out_rows, W), dtype=torch.float32, device=t.device)
+    elif y_split:
+        if tuple(out.shape) != split_shape(B, cout, out_rows, W) or not out.is_contiguous():
+            raise ValueError(f"a split out must be a contiguous bf16 {split_shape(B, cout, out_rows, W)} tensor")
+    elif tuple(out.shape) != (B, cout, out_rows, W) or not out.is_contiguous() or out.dtype != torch.float32:
+        raise ValueError(f"out must be a contiguous fp32 [{B},{cout},{out_rows},{W}] tensor")
+    if init is not None:
+        _require_cuda(init)
+        if init.numel() != cout * desc.H * W or not init.is_contiguous():
+            raise ValueError("init must be a contiguous [Cout,H,W] tensor")
+    tiles = -(-out_rows // 12) * -(-W // _native.TILE_W)
+    gmp = top = None
+    if group_mask is not None:
+        _require_cuda(group_mask)
+        if group_mask.dtype != torch.int32 or group_mask.numel() < tiles or not group_mask.is_contiguous():
+            raise ValueError(f"group_mask must be a contiguous int32 tensor of >= {tiles} tiles")
+        gmp = group_mask.data_ptr()
+    if tile_order is not None:
+        if group_mask is None or tile_order.dtype != torch.int32 or tile_order.numel() != B * tiles:
+            raise ValueError("tile_order must be an int32 permutation of the B x tiles pixel tiles")
+        top = tile_order.data_ptr()
+    b = bias.detach().contiguous() if bias is not None else None
+    bp = b.data_ptr() if b is not None else None
+    st = lib.mvbev_conv3x3_wino_bf16x3(t.data_ptr(), ctypes.byref(desc), packed.data_ptr(), bp,
+                                       init.data_ptr() if init is not None else None, cout, int(bool(relu)),
+                                       out.data_ptr(), _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32,
+                                       gmp, top, _stream(t))
+    _native.check(st, "mvbev_conv3x3_wino_bf16x3")
     return out
 
 

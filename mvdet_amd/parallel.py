@@ -298,7 +298,8 @@ def bench_main(args) -> None:
 
     def run(mode):
         if mode == "frames":  # frame-parallel: each rank fuses its own frame batch, no collective
-            eng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision)
+            eng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision,
+                              wino_conv1=getattr(args, "conv1", "direct") == "wino")
             feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up,
                                                   seed=1000 * args.config + 100 * rank + v, device=dev)
                      for v in range(N)]
@@ -321,7 +322,7 @@ def bench_main(args) -> None:
                 dist.barrier()
                 t0 = time.perf_counter()
                 for i in range(K):
-                    fstep(mark=lambda s: ev[s][i].record())
+                    fstep(mark=lambda s: ev[s][i].record() if s in ev else None)  # (conv1's sub-stage marks)
                     end[i].record()
                 torch.cuda.synchronize()
                 dist.barrier()
@@ -334,7 +335,7 @@ def bench_main(args) -> None:
                                                  for i in range(K)])), 4) for st in stages}
             conv1_tfs = 2.0 * B * ho * wo * 9 * N * C * 512 / (stage_ms["conv1"] * 1e-3) / 1e12
             # the MFMA work conv1 executes (frustum-masked), as the single-GPU line reports it
-            active = (eng.conv1_active_fraction(dev, ws.y1_rows[0], ws.y1_rows[1] - ws.y1_rows[0])
+            active = (eng.conv1_active_fraction(dev, ws.y1_rows[0], ws.y1_rows[1] - ws.y1_rows[0], grid=eng.wino_conv1)
                       if args.precision == "bf16x3" else 1.0)
             return dict(value=round(world * B * K / dt, 3), ms=round(dt * 1e3 / K, 4), stage_ms=stage_ms,
                         band=(0, ho), conv1_tfs=conv1_tfs * active, active=active)

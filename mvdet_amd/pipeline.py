@@ -62,6 +62,9 @@ class Workspace:
     p3: Optional[torch.Tensor] = None
     # keep y2 in HBM (the training forward: conv3's backward reads it), i.e. no conv2 -> conv3 fusion
     store_y2: bool = False
+    # row-Winograd transform of the slab for conv1 (bf16, zero-filled on first use; only the
+    # frustum mask's (tile, slot) pairs are ever written)
+    wino_t: Optional[torch.Tensor] = None
 
 
 class ProjectFuse:
@@ -75,7 +78,7 @@ class ProjectFuse:
                  channels: int, mid_channels: int = 512, slot_views: Optional[Sequence[Optional[int]]] = None,
                  precision: str = "bf16x3", slab_dtype: torch.dtype = torch.float32,
                  all_views: bool = True, split_k: bool = True, frustum: bool = True, fuse_conv3: bool = True,
-                 edge_strip: bool = True, level_conv1: bool = False):
+                 edge_strip: bool = True, level_conv1: bool = False, wino_conv1: bool = False):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":
@@ -139,6 +142,11 @@ class ProjectFuse:
         # faster (fewer chunks in flight, higher clock) and the idle CU-time costs far less than
         # its share
         self.level_conv1 = level_conv1
+        # wino_conv1: the inference conv1 as F(3,3) row-Winograd (ops.wino_rows + conv3x3_wino: 5
+        # instead of 9 MFMA K-blocks per chunk and kernel column, over the 12 x 32 grid tiles);
+        # split-bf16 slab only, not in training (its backward reads the direct form's operands)
+        self.wino_conv1 = wino_conv1 and self.split
+        self.pack1w = ops.PackedConv3x3(chan_map, "bf16x3", wino=True) if self.wino_conv1 else None
 
     # -- buffers ----------------------------------------------------------------------------
     def workspace(self, B: int, device, band: Optional[Tuple[int, int]] = None) -> Workspace:
@@ -338,10 +346,12 @@ class ProjectFuse:
             self._masks[key] = sc
         return sc
 
-    def conv1_active_fraction(self, device, row0: int, rows: int) -> float:
+    def conv1_active_fraction(self, device, row0: int, rows: int, grid: bool = False) -> float:
         """Fraction of conv1's dense (pixel, slot) work the forward's frustum mask keeps (1.0 =
-        dense): per tile its enabled slots x its pixels inside the grid."""
-        m, space = self.conv1_fwd_mask(device, row0, rows)
+        dense): per tile its enabled slots x its pixels inside the grid.  ``grid``: over the
+        12 x 32 grid tiles (the row-Winograd conv1's tile space) instead of the forward's."""
+        m, space = ((self.conv1_mask(device, row0, rows), _native.TILES_GRID) if grid
+                    else self.conv1_fwd_mask(device, row0, rows))
         if m is None:
             return 1.0
         W = self.grid_hw[1]
@@ -355,7 +365,7 @@ class ProjectFuse:
         return sum(b * p for b, p in zip(bits, pix)) / (rows * W * self.S)
 
     # -- a7-a9 ----------------------------------------------------------------------------
-    def conv1(self, ws: Workspace, conv1: torch.nn.Conv2d, sched=None) -> torch.Tensor:
+    def conv1(self, ws: Workspace, conv1: torch.nn.Conv2d, sched=None, mark=None) -> torch.Tensor:
         """a7: y1 = relu(conv3x3(slab) + coord_term) on y1's rows (fp32 MFMA)."""
         if conv1.weight.shape[1] != self.cin:
             raise ValueError(f"conv1 has {conv1.weight.shape[1]} input channels, expected {self.cin}")
@@ -366,6 +376,8 @@ class ProjectFuse:
         a1, b1 = ws.y1_rows
         d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * H * W,
                            batch_stride=self.Cs * H * W, in_row0=0, in_rows=H, out_row0=a1, out_rows=b1 - a1)
+        if self.wino_conv1 and sched is None and not ws.store_y2 and not self.level_conv1:
+            return self.conv1_wino(ws, conv1, d1, init, mark=mark)
         if sched is not None:  # an explicit schedule (conv1_schedule) is planned over the 12 x 32 grid
             gm, space = self.conv1_mask(ws.slab.device, a1, b1 - a1), _native.TILES_GRID
         else:
@@ -377,6 +389,22 @@ class ProjectFuse:
                                 group_mask=gm, tile_order=self.conv1_order(ws.slab.device, a1, b1 - a1, B,
                                                                            grid=space == _native.TILES_GRID),
                                 sched=sched, tile_space=space)
+
+    def conv1_wino(self, ws: Workspace, conv1: torch.nn.Conv2d, d1, init: torch.Tensor, mark=None) -> torch.Tensor:
+        """a7 as F(3,3) row-Winograd: T = B^T(slab rows) (``ops.wino_rows``), then the conv from T
+        with the G w weights (``ops.conv3x3_wino``); same y1 as ``conv1`` within the 3xbf16 error."""
+        a1, b1 = ws.y1_rows
+        B = ws.slab.shape[1]
+        gm = self.conv1_mask(ws.slab.device, a1, b1 - a1)
+        need = ops.wino_rows_bytes(d1)
+        if ws.wino_t is None or ws.wino_t.numel() * 2 < need:
+            ws.wino_t = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=ws.slab.device)
+        ops.wino_rows(ws.slab, d1, ws.wino_t, gm)
+        if mark:
+            mark("conv1_wino")  # between the transform and the conv (bench.py's stage events)
+        return ops.conv3x3_wino(ws.wino_t, d1, self.pack1w.get(conv1.weight), self.mid, init=init, relu=True,
+                                out=ws.y1, group_mask=gm,
+                                tile_order=self.conv1_order(ws.slab.device, a1, b1 - a1, B, grid=True))
 
     def conv2(self, ws: Workspace, conv2: torch.nn.Conv2d) -> torch.Tensor:
         """a8: y2 = relu(conv3x3_d2(y1) + b2) on y2's rows."""
@@ -459,7 +487,7 @@ class ProjectFuse:
         if self.conv3_fused_applies(ws):
             if mark:
                 mark("conv1")
-            self.conv1(ws, map_classifier[0])
+            self.conv1(ws, map_classifier[0], mark=mark)
             if mark:
                 mark("conv2")
             self.conv2_partials(ws, map_classifier[2], map_classifier[4])

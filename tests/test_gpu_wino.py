@@ -1,0 +1,171 @@
+"""Row-Winograd conv1 (F(3,3) along the rows: mvbev_wino_rows_split_bf16 + mvbev_conv3x3_wino_bf16x3)
+against torch's conv2d in float64 and against the direct 3xbf16 ring conv.
+
+The reference op is conv1 of map_classifier (persp_trans_detector.py:51-52): a dense 3x3 conv,
+padding 1, then ReLU; the Winograd form must give the same y within the 3xbf16 tolerance.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import assert_parity
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+TOL = 5e-5  # CONV_TOL["bf16x3"] of test_gpu_parity.py: normwise vs the float64 conv
+
+# the transform rows of B^T (points 0, 1, -1, 2, inf), as the kernel applies them
+BT = np.array([[2, -1, -2, 1, 0], [0, -2, -1, 1, 0], [0, 2, -3, 1, 0], [0, -1, 0, 1, 0], [0, 2, -1, -2, 1]],
+              dtype=np.float64)
+
+
+def _split_encode(x: torch.Tensor) -> torch.Tensor:
+    """fp32 [B, C, H, W] (C % 8 == 0) -> split-bf16 blocked [B, C/8, H, W, 2, 8]."""
+    B, C, H, W = x.shape
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.float()).to(torch.bfloat16)
+    t = torch.stack([hi, lo], 0).reshape(2, B, C // 8, 8, H, W)
+    return t.permute(1, 2, 4, 5, 0, 3).contiguous()
+
+
+def _setup(S, Cs, B, H, W, rows, cout, seed, zero_right=False):
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(seed)
+    xs = torch.rand(S, B, Cs, H, W, generator=g)
+    if zero_right:  # view 1 is zero from column W // 2 on: a mask has something exact to skip
+        xs[1, :, :, :, W // 2:] = 0
+    K = S * Cs
+    w = (torch.rand(cout, K, 3, 3, generator=g) - 0.5) / np.sqrt(K * 9)
+    bias = torch.rand(cout, generator=g) - 0.5
+    init = torch.rand(cout, H, W, generator=g) - 0.5
+    r0, r1 = rows
+    x64 = xs.permute(1, 0, 2, 3, 4).reshape(B, K, H, W).double()
+    ref = F.relu(F.conv2d(x64, w.double(), bias.double(), padding=1) + init.double())[:, :, r0:r1].float()
+    slab = torch.stack([_split_encode(xs[v]) for v in range(S)]).to(DEV)
+    desc = ops.conv_desc(B, K, H, W, group=Cs, group_stride=B * Cs * H * W, batch_stride=Cs * H * W,
+                         out_row0=r0, out_rows=r1 - r0)
+    return xs, w.to(DEV), bias.to(DEV), init.to(DEV), ref, slab, desc
+
+
+@pytest.mark.parametrize("S,Cs,B,H,W,rows", [(3, 16, 1, 30, 360, (0, 30)),   # partial last tile column
+                                              (2, 24, 2, 25, 76, (3, 25)),    # K % 16 == 8, row band, B = 2
+                                              (1, 32, 1, 13, 32, (0, 13)),    # one tile column, 2 tile rows
+                                              (4, 16, 1, 61, 45, (0, 61))])
+def test_wino_conv_vs_float64_and_direct(S, Cs, B, H, W, rows):
+    from mvdet_amd import ops
+    cout = 256
+    xs, w, bias, init, ref, slab, desc = _setup(S, Cs, B, H, W, rows, cout, seed=H * W + S)
+    t = torch.zeros(ops.wino_rows_bytes(desc) // 2, dtype=torch.bfloat16, device=DEV)
+    ops.wino_rows(slab, desc, t)
+    pk = ops.PackedConv3x3(None, "bf16x3", wino=True).get(w)
+    got = ops.conv3x3_wino(t, desc, pk, cout, bias=bias, init=init, relu=True)
+    s = assert_parity(got.cpu(), ref, "wino vs float64", normwise_tol=TOL)
+    direct = ops.conv3x3_desc(slab, desc, ops.PackedConv3x3(None, "bf16x3").get(w), cout, bias=bias, init=init,
+                              relu=True, dilation=1)
+    sd = assert_parity(direct.cpu(), ref, "direct vs float64", normwise_tol=TOL)
+    # the transforms' roundings: the same order of error as the direct 3xbf16 conv
+    assert s["normwise"] <= max(4 * sd["normwise"], 2e-6), (s, sd)
+    # split-bf16 output (what conv2 reads) decodes to the fp32 output within the split's rounding
+    ysplit = torch.empty(ops.split_shape(B, cout, rows[1] - rows[0], W), dtype=torch.bfloat16, device=DEV)
+    ops.conv3x3_wino(t, desc, pk, cout, bias=bias, init=init, relu=True, out=ysplit)
+    assert_parity(ops.split_decode(ysplit, cout).cpu(), got.cpu(), "split out", normwise_tol=2e-5)
+
+
+def test_wino_rows_transform_matches_numpy():
+    """T = split(B^T d) per 3-row output tile, input rows out_row0 + 3 r3 - 1 + m (zero outside)."""
+    from mvdet_amd import ops
+    S, Cs, B, H, W, rows = 2, 16, 1, 17, 40, (2, 17)
+    xs, w, bias, init, ref, slab, desc = _setup(S, Cs, B, H, W, rows, 128, seed=5)
+    t = torch.zeros(ops.wino_rows_bytes(desc) // 2, dtype=torch.bfloat16, device=DEV)
+    ops.wino_rows(slab, desc, t)
+    K, r0, nr = S * Cs, rows[0], rows[1] - rows[0]
+    R5 = 5 * 4 * (-(-nr // 12))
+    T = t.view(B, K // 8, R5, W, 2, 8).float().cpu()
+    T = (T[..., 0, :] + T[..., 1, :]).permute(0, 1, 4, 2, 3).reshape(B, K, R5, W).double().numpy()
+    # the slab as the kernel sees it: hi + lo of the split encoding
+    x = torch.stack([xs[v].to(torch.bfloat16).float() + (xs[v] - xs[v].to(torch.bfloat16).float())
+                     .to(torch.bfloat16).float() for v in range(S)]).permute(1, 0, 2, 3, 4).reshape(B, K, H, W)
+    x = x.double().numpy()
+    for r3 in range(R5 // 5):
+        d = np.zeros((5, B, K, W))
+        for m in range(5):
+            row = r0 + 3 * r3 - 1 + m
+            if 0 <= row < H:
+                d[m] = x[:, :, row]
+        want = np.einsum("xm,mbkw->bkxw", BT, d)
+        np.testing.assert_allclose(T[:, :, 5 * r3:5 * r3 + 5].transpose(0, 1, 2, 3), want, rtol=0,
+                                   atol=2e-5 * max(1.0, np.abs(want).max()))
+
+
+@pytest.mark.parametrize("B", [1, 2])
+def test_wino_conv_masked_matches_unmasked(B):
+    """With a frustum-style mask (cleared = the group is zero over the tile and its halo) and
+    the heavy-first order, T is written only for the set (tile, group) pairs of a zero-filled
+    buffer, and y equals the unmasked Winograd conv bit for bit (skipped products are zeros)."""
+    from mvdet_amd import ops
+    S, Cs, H, W, cout = 3, 16, 30, 100, 128
+    xs, w, bias, init, ref, slab, desc = _setup(S, Cs, B, H, W, (0, H), cout, seed=77 + B, zero_right=True)
+    tx, ty = -(-W // 32), -(-H // 12)
+    m = [0b101 | (0b010 if (t % tx) * 32 - 1 < W // 2 else 0) for t in range(tx * ty)]
+    gm = torch.tensor(m, dtype=torch.int32, device=DEV)
+    order = ops.heavy_first_order(gm, B)
+    pk = ops.PackedConv3x3(None, "bf16x3", wino=True).get(w)
+    t_full = torch.zeros(ops.wino_rows_bytes(desc) // 2, dtype=torch.bfloat16, device=DEV)
+    ops.wino_rows(slab, desc, t_full)
+    t_mask = torch.zeros_like(t_full)
+    ops.wino_rows(slab, desc, t_mask, gm)
+    assert torch.equal(t_mask, t_full)  # the skipped pairs' true transform is exactly zero
+    dense = ops.conv3x3_wino(t_full, desc, pk, cout, bias=bias, init=init, relu=True)
+    masked = ops.conv3x3_wino(t_mask, desc, pk, cout, bias=bias, init=init, relu=True, group_mask=gm,
+                              tile_order=order)
+    assert torch.equal(masked, dense)
+    assert_parity(masked.cpu(), ref, "masked wino", normwise_tol=TOL)
+
+
+def test_wino_refusals():
+    from mvdet_amd import _native, ops
+    S, Cs, B, H, W = 2, 16, 1, 12, 32
+    xs, w, bias, init, ref, slab, desc = _setup(S, Cs, B, H, W, (0, H), 128, seed=3)
+    small = torch.zeros(16, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(_native.NativeError):
+        ops.wino_rows(slab, desc, small)
+    pk = ops.PackedConv3x3(None, "bf16x3", wino=True).get(w)
+    t = torch.zeros(ops.wino_rows_bytes(desc) // 2, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises((ValueError, _native.NativeError)):  # Cout not a multiple of 128
+        ops.conv3x3_wino(t, desc, pk, 128 + 1)
+    with pytest.raises(ValueError):
+        ops.conv3x3_wino(small, desc, pk, 128)
+    with pytest.raises(ValueError):
+        ops.PackedConv3x3(None, "fp32", wino=True)
+
+
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_engine_wino_conv1_matches_direct(cfg):
+    """ProjectFuse(wino_conv1=True): the detector's map and y1 match the direct ring conv1 within
+    the 3xbf16 tolerance at the config rigs (reduced channels), twice in a row bitwise (T reuse)."""
+    from mvdet_amd import ProjectFuse, synthetic
+    from mvdet_amd.geometry import projection_matrices
+    spec = synthetic.CONFIGS[cfg]
+    ds = spec["make"]()
+    N, C, B = ds.num_cam, 32, 1
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    pm = projection_matrices(ds)
+    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=19 + v, device=DEV)
+             for v in range(N)]
+    torch.manual_seed(cfg)
+    mc = torch.nn.Sequential(torch.nn.Conv2d(N * C + 2, 512, 3, padding=1), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False)).to(DEV)
+    direct = ProjectFuse(pm, up, grid, C)
+    wino = ProjectFuse(pm, up, grid, C, wino_conv1=True)
+    assert wino.wino_conv1 and wino.frustum
+    with torch.no_grad():
+        ref = direct.project_fuse(feats, mc)
+        y1_ref = direct.y1_fp32(direct.workspace(B, DEV)).clone()
+        got = wino.project_fuse(feats, mc)
+        y1 = wino.y1_fp32(wino.workspace(B, DEV)).clone()
+        got2 = wino.project_fuse(feats, mc)
+    assert torch.equal(got, got2)
+    assert_parity(y1.cpu(), y1_ref.cpu(), "wino y1", normwise_tol=TOL)
+    assert_parity(got.cpu(), ref.cpu(), "wino map", normwise_tol=TOL)

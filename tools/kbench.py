@@ -132,6 +132,15 @@ def main():
         for v in range(N):
             eng.warp_view(ws, v, feats[v])
         eng.fuse(ws, mc)
+        from mvdet_amd import ops
+        weng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision, frustum=not args.no_frustum,
+                           wino_conv1=True)
+        wws = weng.workspace(B, dev)
+        weng.warp_views(wws, list(range(N)), feats)
+        weng.conv1(wws, mc[0])
+        wd1 = ops.conv_desc(B, weng.S * weng.Cs, ho, wo, group=weng.Cs, group_stride=B * weng.Cs * ho * wo,
+                            batch_stride=weng.Cs * ho * wo)
+        wgm = weng.conv1_mask(dev, 0, ho)
         stages = {
             "warp": (lambda: eng.warp_views(ws, list(range(N)), feats), None),
             "warpup": (lambda: eng.warp_views_upsampled(ws, list(range(N)), bfeats), None),
@@ -145,6 +154,13 @@ def main():
                        2.0 * B * ho * wo * 9 * N * C * 512),  # balanced schedule
             "conv1p": (lambda: eng.conv1(ws, mc[0], sched=eng.conv1_schedule(dev, 0, ho, B, split=False)),
                        2.0 * B * ho * wo * 9 * N * C * 512),  # the schedule's XCD shares, no pieces
+            # row-Winograd conv1 (ProjectFuse(wino_conv1=True)): transform + conv, and each alone
+            "conv1w": (lambda: weng.conv1(wws, mc[0]), 2.0 * B * ho * wo * 9 * N * C * 512),
+            "winorows": (lambda: ops.wino_rows(wws.slab, wd1, wws.wino_t, wgm), None),
+            "winoconv": (lambda: ops.conv3x3_wino(wws.wino_t, wd1, weng.pack1w.get(mc[0].weight), 512,
+                                                  init=weng.coord_term(mc[0]), relu=True, out=wws.y1,
+                                                  group_mask=wgm, tile_order=weng.conv1_order(dev, 0, ho, B, grid=True)),
+                         2.0 * B * ho * wo * 9 * N * C * 512),
             "conv2": (lambda: eng.conv2(ws, mc[2]), 2.0 * B * ho * wo * 9 * 512 * 512),
             "conv3": (lambda: eng.conv3(ws, mc[4]), None),
             # conv2 -> conv3 fused (the default inference path): partials epilogue + reduce

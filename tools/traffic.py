@@ -20,6 +20,7 @@ import sys
 
 out_dir, tag, cfg = sys.argv[1], sys.argv[2], int(sys.argv[3])
 precision = sys.argv[4] if len(sys.argv) > 4 else "bf16x3"
+wino = len(sys.argv) > 5 and sys.argv[5] == "wino"  # conv1 = the row-Winograd conv kernel (kbench winoconv)
 vals = collections.defaultdict(lambda: collections.defaultdict(dict))
 for f in glob.glob(f"{out_dir}/{tag}_pmc*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
@@ -44,6 +45,11 @@ for name in vals:
 # conv1: the ReLU dilation-1 ring kernel without the fused cout1 epilogue (grid tiles "<1, true>",
 # edge-strip tiles "<1, true, false, EW>"), or the fp32-MFMA kernel
 pat = r"conv_ring_kernel<1, true(, false, \d+)?>" if precision == "bf16x3" else r"conv3x3_mfma_f32_kernel<1, true"
+if wino:
+    pat = r"conv_wino_kernel<true>"
+    rows = [k for k in res["kernels"] if "wino_rows_kernel" in k]
+    if rows:
+        res["wino_rows_hbm_bytes_per_launch"] = res["kernels"][rows[0]]["hbm_bytes_per_launch"]
 conv1 = [k for k in res["kernels"] if re.search(pat, k)]
 if conv1:
     res["conv1_hbm_bytes_per_launch"] = res["kernels"][conv1[0]]["hbm_bytes_per_launch"]

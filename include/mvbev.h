@@ -277,6 +277,16 @@ int mvbev_conv3x3_bf16x3_ex3(const void* x, int x_layout, const mvbev_conv_desc*
  *      step 1), weights from mvbev_pack_conv3x3_weight_wino (same arguments as
  *      mvbev_pack_conv3x3_weight_bf16x3), bias / init / relu / y / y_layout / group_mask /
  *      tile_order as mvbev_conv3x3_bf16x3_ex (grid tiles, 12 x 32). */
+/* Warp + the row transform of step 1 in one pass, from fp32 sources (mvbev_warp_views_split_bf16's
+ * views and matrices): the T rows of r3_rows 3-row output tiles (3 * r3_rows >= Ho; the conv's
+ * T has 4 * ceil(out_rows / 12) of them) are written for each view's channels at its dst, whose
+ * dst_strides are in 32-byte units: [0] per batch item, [1] per 8-channel group, [2] per T row,
+ * [3] = 1 — the view's slice of T.  The warped slab itself is never written.  flags:
+ * MVBEV_WARP_DST_ZEROED = T is zero-filled and only written by this geometry, so a (tile,
+ * column) whose 5 samples all fall outside the source is skipped.  Replaces :69 + :77 + the
+ * first step of conv1 (:51) for inference. */
+int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t H,
+                               int64_t W, int64_t Ho, int64_t Wo, int64_t r3_rows, int flags, void* stream);
 size_t mvbev_conv3x3_packed_bytes_wino(int64_t Cout, int64_t K);
 int mvbev_pack_conv3x3_weight_wino(const float* w, int64_t Cout, int64_t Cin_w, const int32_t* chan_map,
                                    int64_t K, void* w_packed, void* stream);

@@ -507,6 +507,40 @@ def wino_rows(x: torch.Tensor, desc, t: torch.Tensor, group_mask: Optional[torch
     return t
 
 
+def warp_views_wino_rows_into(srcs, m_norms, t: torch.Tensor, slots, Cs: int, K: int, Ho: int, Wo: int,
+                              dst_zeroed: bool = False) -> None:
+    """Warp + row-Winograd transform in ONE launch (``mvbev_warp_views_wino_rows``): view i
+    (fp32 ``srcs[i]`` [B,C,H,W], host kornia matrix ``m_norms[i]``) lands in channels
+    [slots[i] * Cs, + C) of ``t``, the T buffer of ``wino_rows`` for a K-channel slab of
+    Ho x Wo (whole grid, out_row0 = 0); the slab itself is not written."""
+    n = len(srcs)
+    if n == 0:
+        return
+    if not (len(m_norms) == n == len(slots)) or n > 16:
+        raise ValueError("need 1..16 matching srcs / m_norms / slots")
+    _require_cuda(t, *srcs)
+    B, C, H, W = srcs[0].shape
+    r3 = 4 * (-(-Ho // 12))
+    K8 = K // KC
+    if t.dtype != torch.bfloat16 or not t.is_contiguous() or t.numel() < B * K8 * 5 * r3 * Wo * 16:
+        raise ValueError("t must be a contiguous bf16 buffer of wino_rows_bytes")
+    if Cs % KC or C > Cs:
+        raise ValueError("Cs must be a multiple of 8 holding C")
+    arr = (_native.WarpView * n)()
+    for i, (s_, m, slot) in enumerate(zip(srcs, m_norms, slots)):
+        if tuple(s_.shape) != (B, C, H, W) or s_.dtype != torch.float32:
+            raise ValueError("all views must be fp32 [B,C,H,W] of one shape")
+        mm = torch.as_tensor(m, dtype=torch.float32).reshape(9).tolist()
+        arr[i].src = s_.data_ptr()
+        arr[i].src_strides = _native._i64x4(*s_.stride())
+        arr[i].dst = t.data_ptr() + 32 * (int(slot) * (Cs // KC)) * 5 * r3 * Wo
+        arr[i].dst_strides = _native._i64x4(K8 * 5 * r3 * Wo, 5 * r3 * Wo, Wo, 1)  # 32-byte units
+        arr[i].m = (ctypes.c_float * 9)(*mm)
+    st = _native.load().mvbev_warp_views_wino_rows(arr, n, B, C, H, W, Ho, Wo, r3,
+                                                   _native.WARP_DST_ZEROED if dst_zeroed else 0, _stream(t))
+    _native.check(st, "mvbev_warp_views_wino_rows")
+
+
 def conv3x3_wino(t: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: Optional[torch.Tensor] = None,
                  init: Optional[torch.Tensor] = None, relu: bool = False, out: Optional[torch.Tensor] = None,
                  group_mask: Optional[torch.Tensor] = None,

@@ -65,6 +65,8 @@ class Workspace:
     # row-Winograd transform of the slab for conv1 (bf16, zero-filled on first use; only the
     # frustum mask's (tile, slot) pairs are ever written)
     wino_t: Optional[torch.Tensor] = None
+    # wino_t holds the current frame's transform, written by the fused warp (the slab was not)
+    t_from_warp: bool = False
 
 
 class ProjectFuse:
@@ -78,7 +80,8 @@ class ProjectFuse:
                  channels: int, mid_channels: int = 512, slot_views: Optional[Sequence[Optional[int]]] = None,
                  precision: str = "bf16x3", slab_dtype: torch.dtype = torch.float32,
                  all_views: bool = True, split_k: bool = True, frustum: bool = True, fuse_conv3: bool = True,
-                 edge_strip: bool = True, level_conv1: bool = False, wino_conv1: bool = False):
+                 edge_strip: bool = True, level_conv1: bool = False, wino_conv1: bool = False,
+                 wino_warp: bool = False):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":
@@ -147,6 +150,11 @@ class ProjectFuse:
         # split-bf16 slab only, not in training (its backward reads the direct form's operands)
         self.wino_conv1 = wino_conv1 and self.split
         self.pack1w = ops.PackedConv3x3(chan_map, "bf16x3", wino=True) if self.wino_conv1 else None
+        # wino_warp: warp_views writes the row transform T directly (one pass, no slab, no
+        # separate transform); inference over the whole grid from fp32 features only.  Opt-in:
+        # measured slower (cfg2: 0.92 ms vs warp 0.34 + transform 0.24; each thread gathers 5
+        # rows x 8 channels, 5x the plain warp's dependent loads)
+        self.wino_warp = self.wino_conv1 and wino_warp
 
     # -- buffers ----------------------------------------------------------------------------
     def workspace(self, B: int, device, band: Optional[Tuple[int, int]] = None) -> Workspace:
@@ -193,18 +201,39 @@ class ProjectFuse:
         if tuple(feat.shape[2:]) != self.src_hw or feat.shape[1] != self.C:
             raise ValueError(f"view {cam}: features {tuple(feat.shape)} do not match "
                              f"[B,{self.C},{self.src_hw[0]},{self.src_hw[1]}]")
+        ws.t_from_warp = False
         if self.split:
             ops.warp_views_into([feat], [self.m_norm_cpu[cam]], [self._slot_dst(ws, cam)], split=True,
                                 dst_zeroed=ws.slab_zeroed)
         else:
             ops.warp_into(feat, ws.m_norm[cam], self._slot_dst(ws, cam))
 
+    def _wino_warp_applies(self, ws: Workspace, feats) -> bool:
+        H = self.grid_hw[0]
+        return (self.wino_warp and not ws.store_y2 and ws.y1_rows == (0, H) and ws.slab_zeroed
+                and all(f.dtype == torch.float32 for f in feats) and self.src_hw[1] >= 2)
+
     def warp_views(self, ws: Workspace, cams: Sequence[int], feats: Sequence[torch.Tensor]) -> None:
-        """a5 for several views in one launch (``feats[i]`` is view ``cams[i]``)."""
+        """a5 for several views in one launch (``feats[i]`` is view ``cams[i]``).  With
+        ``wino_warp`` (inference, whole grid) a5 + a6 + conv1's row transform in one pass: the
+        views land in ``ws.wino_t`` (``mvbev_warp_views_wino_rows``) and the slab is not written."""
         for cam, f in zip(cams, feats):
             if tuple(f.shape[2:]) != self.src_hw or f.shape[1] != self.C:
                 raise ValueError(f"view {cam}: features {tuple(f.shape)} do not match "
                                  f"[B,{self.C},{self.src_hw[0]},{self.src_hw[1]}]")
+        if self._wino_warp_applies(ws, feats):
+            H, W = self.grid_hw
+            B = ws.slab.shape[1]
+            d1 = self._conv1_desc(B)
+            need = ops.wino_rows_bytes(d1)
+            if ws.wino_t is None or ws.wino_t.numel() * 2 < need:
+                ws.wino_t = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=ws.slab.device)
+            ops.warp_views_wino_rows_into(list(feats), [self.m_norm_cpu[c] for c in cams], ws.wino_t,
+                                          [self.slot_of[c] for c in cams], self.Cs, self.S * self.Cs, H, W,
+                                          dst_zeroed=True)
+            ws.t_from_warp = True
+            return
+        ws.t_from_warp = False
         ops.warp_views_into(list(feats), [self.m_norm_cpu[c] for c in cams],
                             [self._slot_dst(ws, c) for c in cams], split=self.split,
                             dst_zeroed=self.split and ws.slab_zeroed)
@@ -216,6 +245,7 @@ class ProjectFuse:
         for cam, f in zip(cams, feats):
             if f.shape[1] != self.C or f.shape[2] > self.src_hw[0] or f.shape[3] > self.src_hw[1]:
                 raise ValueError(f"view {cam}: features {tuple(f.shape)} cannot upsample to {self.src_hw}")
+        ws.t_from_warp = False
         ops.warp_views_upsampled_into(list(feats), self.src_hw, [self.m_norm_cpu[c] for c in cams],
                                       [self._slot_dst(ws, c) for c in cams], split=self.split,
                                       dst_zeroed=self.split and ws.slab_zeroed)
@@ -390,6 +420,12 @@ class ProjectFuse:
                                                                            grid=space == _native.TILES_GRID),
                                 sched=sched, tile_space=space)
 
+    def _conv1_desc(self, B: int, rows: Optional[Tuple[int, int]] = None):
+        H, W = self.grid_hw
+        a1, b1 = (0, H) if rows is None else rows
+        return ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * H * W,
+                             batch_stride=self.Cs * H * W, in_row0=0, in_rows=H, out_row0=a1, out_rows=b1 - a1)
+
     def conv1_wino(self, ws: Workspace, conv1: torch.nn.Conv2d, d1, init: torch.Tensor, mark=None) -> torch.Tensor:
         """a7 as F(3,3) row-Winograd: T = B^T(slab rows) (``ops.wino_rows``), then the conv from T
         with the G w weights (``ops.conv3x3_wino``); same y1 as ``conv1`` within the 3xbf16 error."""
@@ -399,7 +435,8 @@ class ProjectFuse:
         need = ops.wino_rows_bytes(d1)
         if ws.wino_t is None or ws.wino_t.numel() * 2 < need:
             ws.wino_t = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=ws.slab.device)
-        ops.wino_rows(ws.slab, d1, ws.wino_t, gm)
+        if not ws.t_from_warp:  # the slab's transform (else the fused warp wrote T)
+            ops.wino_rows(ws.slab, d1, ws.wino_t, gm)
         if mark:
             mark("conv1_wino")  # between the transform and the conv (bench.py's stage events)
         return ops.conv3x3_wino(ws.wino_t, d1, self.pack1w.get(conv1.weight), self.mid, init=init, relu=True,

@@ -169,3 +169,48 @@ def test_engine_wino_conv1_matches_direct(cfg):
     assert torch.equal(got, got2)
     assert_parity(y1.cpu(), y1_ref.cpu(), "wino y1", normwise_tol=TOL)
     assert_parity(got.cpu(), ref.cpu(), "wino map", normwise_tol=TOL)
+
+
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_fused_warp_transform_matches_two_pass(cfg):
+    """wino_warp (mvbev_warp_views_wino_rows: warp + B^T in one pass, no slab) gives the T of the
+    two-pass path (split slab, then mvbev_wino_rows_split_bf16) within the split's rounding, and
+    the same map; a later slab-writing warp (upsampled features) switches conv1 back to the
+    slab's transform."""
+    from mvdet_amd import ProjectFuse, synthetic
+    from mvdet_amd.geometry import projection_matrices
+    spec = synthetic.CONFIGS[cfg]
+    ds = spec["make"]()
+    N, C, B = ds.num_cam, 24, 1
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    pm = projection_matrices(ds)
+    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=31 + v, device=DEV)
+             for v in range(N)]
+    torch.manual_seed(10 + cfg)
+    mc = torch.nn.Sequential(torch.nn.Conv2d(N * C + 2, 512, 3, padding=1), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False)).to(DEV)
+    fused = ProjectFuse(pm, up, grid, C, wino_conv1=True, wino_warp=True)
+    two = ProjectFuse(pm, up, grid, C, wino_conv1=True)
+    assert fused.wino_warp and not two.wino_warp
+    with torch.no_grad():
+        got = fused.project_fuse(feats, mc)
+        wf = fused.workspace(B, DEV)
+        assert wf.t_from_warp and wf.slab.abs().max().item() == 0  # the slab was never written
+        ref = two.project_fuse(feats, mc)
+        wt = two.workspace(B, DEV)
+        tf = wf.wino_t.view(-1, 2, 8).float()
+        tt = wt.wino_t.view(-1, 2, 8).float()
+        a, b = tf.sum(1), tt.sum(1)
+        # the two-pass T transforms the slab's hi + lo (each value rounded to ~2^-17): the 5-row
+        # combinations (coefficient sums <= 6) differ by a few 1e-5 of the range
+        assert (a - b).abs().max().item() <= 1e-4 * max(1.0, b.abs().max().item())
+        assert_parity(got.cpu(), ref.cpu(), "fused-warp map", normwise_tol=TOL)
+        # backbone-resolution input writes the slab: conv1 must transform it again
+        low = [torch.nn.functional.avg_pool2d(f, 3) for f in feats]
+        fused.warp_views_upsampled(wf, list(range(N)), low)
+        assert not wf.t_from_warp
+        m1 = fused.fuse(wf, mc)
+        two.warp_views_upsampled(wt, list(range(N)), low)
+        m2 = two.fuse(wt, mc)
+    assert_parity(m1.cpu(), m2.cpu(), "slab path after the fused warp", normwise_tol=TOL)

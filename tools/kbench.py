@@ -157,6 +157,8 @@ def main():
             # row-Winograd conv1 (ProjectFuse(wino_conv1=True)): transform + conv, and each alone
             "conv1w": (lambda: weng.conv1(wws, mc[0]), 2.0 * B * ho * wo * 9 * N * C * 512),
             "winorows": (lambda: ops.wino_rows(wws.slab, wd1, wws.wino_t, wgm), None),
+            "warpw": (lambda: _with(weng, "wino_warp", True, lambda: weng.warp_views(wws, list(range(N)), feats)),
+                      None),  # warp + B^T in one pass (wino_warp; leaves T from the warp, run it last)
             "winoconv": (lambda: ops.conv3x3_wino(wws.wino_t, wd1, weng.pack1w.get(mc[0].weight), 512,
                                                   init=weng.coord_term(mc[0]), relu=True, out=wws.y1,
                                                   group_mask=wgm, tile_order=weng.conv1_order(dev, 0, ho, B, grid=True)),

@@ -252,6 +252,9 @@ def run_single(args, precision, steps, warmup, with_cpu):
         },
         "stage_roofline": {
             "warp": {"bound": "hbm", "algorithmic_bytes": warp_bytes,
+                     # with the Winograd conv1 the warp writes the row transform T (warp_wino_kernel:
+                     # 5/3 of the slab's rows, the separate transform gone), so its time includes B^T
+                     "output": "row-Winograd T (warp + B^T fused)" if eng.wino_warp else "split-bf16 slab",
                      "achieved_GBs": round(warp_bytes / (t_warp * 1e-3) / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
                      # PMC bytes (read at 128-B granules: NCHW rows are gathered, not streamed)
                      "traffic": warp_traffic,

@@ -146,14 +146,19 @@ __global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_tile_kernel(const Warp
 }
 
 // Warp + row-Winograd input transform in one pass (inference conv1, csrc/conv_bf16x3.hip
-// "Row-Winograd conv1"): thread = (3-row output tile r3, column u) of one view's 8-channel group;
-// it warps the tile's 5 input rows v = 3 r3 - 1 + m (zero outside the grid), applies B^T and
-// stores the 5 transformed rows split-bf16 at T rows 5 r3 + xi (dst strides in 32-B units:
-// dB per item, dC per 8-channel group, dH per T row).  The slab itself is never written.
-// skip_zero: a (tile, column) whose 5 samples all fall outside the source is not written (T
-// is zero-filled once and only ever written by this geometry).
+// "Row-Winograd conv1"): a block = 4 three-row output tiles (12 rows) x 8 columns of one view's
+// 8-channel group.  Phase 1: thread (row i < 14, column) warps input row 12 k - 1 + i like
+// warp_tile_kernel (zero outside the grid) into LDS; phase 2: each (tile, column, xi) applies
+// B^T to its 5 rows and stores the transformed row split-bf16 at T row 5 r3 + xi (dst strides
+// in 32-B units: dB per item, dC per 8-channel group, dH per T row).  The slab itself is never
+// written.  skip_zero: a (tile, column) whose 5 samples all fall outside the source is not
+// written (T is zero-filled once and only ever written by this geometry).
+constexpr int kWwRows = 14, kWwCols = 8;  // rows warped per block (4 tiles + the 2 shared halo rows)
+static_assert(kWarpCPB == 8, "one 8-channel group per block");
 template <bool PAIR>
-__global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_wino_kernel(const WarpArgs a, int r3_rows) {
+__global__ __launch_bounds__(128) void warp_wino_kernel(const WarpArgs a, int r3_rows) {
+  __shared__ float ds[kWwRows][kWwCols][9];  // [row][col][channel] (+1 pad)
+  __shared__ unsigned char nz[kWwRows][kWwCols];
   const int lb = xcd_remap(blockIdx.x, a.nwg);
   const int tile = lb % a.tiles;
   const int chunk = (lb / a.tiles) % a.chunks;
@@ -161,95 +166,101 @@ __global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_wino_kernel(const Warp
   const int view = bv % a.nviews;
   const int b = bv / a.nviews;
   const WarpView& vw = a.v[view];
-  const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
-  constexpr int WC = 64 / kWarpWR, WAVES_X = kWarpTW / WC;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r3 = ty * kWarpTH + (wave / WAVES_X) * kWarpWR + lane / WC;
-  const int u = tx * kWarpTW + (wave % WAVES_X) * WC + lane % WC;
-  if (r3 >= r3_rows || u >= a.Wo) return;
-  static_assert(kWarpCPB == 8, "one 8-channel group per block");
+  const int k = tile / a.tiles_x, tx = tile - k * a.tiles_x;
   const int c_begin = chunk * kWarpCPB;
   const int c_end = min(a.C, c_begin + kWarpCPB);
   const int H = a.H, W = a.W;
-  float m[9];
+  const int tid = threadIdx.x;
+  {  // phase 1: one warped pixel (8 channels) per thread
+    const int i = tid / kWwCols, c = tid % kWwCols;  // 16 x 8 threads, rows >= 14 idle
+    const int v = 12 * k - 1 + i, u = tx * kWwCols + c;
+    if (i < kWwRows) {
+      float d[8];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) m[i] = vw.m[i];
-  const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
-  float d[5][8];
-  bool any = false;
+      for (int j = 0; j < 8; ++j) d[j] = 0.f;
+      bool any = false;
+      if (v >= 0 && v < a.Ho && u < a.Wo) {
+        float m[9];
 #pragma unroll
-  for (int r = 0; r < 5; ++r) {
-    const int v = 3 * r3 - 1 + r;
+        for (int q = 0; q < 9; ++q) m[q] = vw.m[q];
+        const WarpCoord wc = warp_coord(m, u, v, a.Ho, a.Wo, H, W);
+        if (!wc.inside) {
+          if (!wc.finite) {
+            any = true;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) d[r][j] = 0.f;
-    if (v < 0 || v >= a.Ho) continue;
-    const WarpCoord wc = warp_coord(m, u, v, a.Ho, a.Wo, H, W);
-    if (!wc.inside) {
-      if (!wc.finite) {
-        any = true;
+            for (int j = 0; j < 8; ++j) d[j] = c_begin + j < c_end ? __builtin_nanf("") : 0.f;
+          }
+        } else {
+          any = true;
+          const float ix = wc.ix, iy = wc.iy;
+          const float fx0 = floorf(ix), fy0 = floorf(iy);
+          const int x0 = (int)fx0, y0 = (int)fy0;
+          const float fx1 = fx0 + 1.f, fy1 = fy0 + 1.f;
+          const float w_nw = (fx1 - ix) * (fy1 - iy), w_ne = (ix - fx0) * (fy1 - iy);
+          const float w_sw = (fx1 - ix) * (iy - fy0), w_se = (ix - fx0) * (iy - fy0);
+          const bool vx0 = x0 >= 0, vx1 = x0 + 1 <= W - 1, vy0 = y0 >= 0, vy1 = y0 + 1 <= H - 1;
+          const bool ok_nw = vx0 && vy0, ok_ne = vx1 && vy0, ok_sw = vx0 && vy1, ok_se = vx1 && vy1;
+          const int cx0 = max(x0, 0), cy0 = max(y0, 0);
+          const int cx1 = min(x0 + 1, W - 1), cy1 = min(y0 + 1, H - 1);
+          const int64_t sH = vw.sH, sW = vw.sW, sC = vw.sC;
+          const int bx = min(max(x0, 0), W - 2);
+          const int64_t o_top = cy0 * sH + bx, o_bot = cy1 * sH + bx;
+          const bool nw_lo = x0 == bx, ne_lo = x0 + 1 == bx;
+          const int64_t o_nw = cy0 * sH + cx0 * sW, o_ne = cy0 * sH + cx1 * sW;
+          const int64_t o_sw = cy1 * sH + cx0 * sW, o_se = cy1 * sH + cx1 * sW;
+          const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d[r][j] = c_begin + j < c_end ? __builtin_nanf("") : 0.f;
+          for (int j = 0; j < 8; ++j) {
+            const int ch = c_begin + j;
+            if (ch >= c_end) break;
+            const float* pc = base + (int64_t)ch * sC;
+            float vnw, vne, vsw, vse;
+            if constexpr (PAIR) {
+              const f32x2u_t top = *reinterpret_cast<const f32x2u_t*>(pc + o_top);
+              const f32x2u_t bot = *reinterpret_cast<const f32x2u_t*>(pc + o_bot);
+              vnw = nw_lo ? top.x : top.y;
+              vne = ne_lo ? top.x : top.y;
+              vsw = nw_lo ? bot.x : bot.y;
+              vse = ne_lo ? bot.x : bot.y;
+            } else {
+              vnw = pc[o_nw]; vne = pc[o_ne]; vsw = pc[o_sw]; vse = pc[o_se];
+            }
+            float acc = 0.f;
+            acc += (ok_nw ? vnw : 0.f) * w_nw;
+            acc += (ok_ne ? vne : 0.f) * w_ne;
+            acc += (ok_sw ? vsw : 0.f) * w_sw;
+            acc += (ok_se ? vse : 0.f) * w_se;
+            d[j] = acc;
+          }
+        }
       }
-      continue;
-    }
-    any = true;
-    const float ix = wc.ix, iy = wc.iy;
-    const float fx0 = floorf(ix), fy0 = floorf(iy);
-    const int x0 = (int)fx0, y0 = (int)fy0;
-    const float fx1 = fx0 + 1.f, fy1 = fy0 + 1.f;
-    const float w_nw = (fx1 - ix) * (fy1 - iy), w_ne = (ix - fx0) * (fy1 - iy);
-    const float w_sw = (fx1 - ix) * (iy - fy0), w_se = (ix - fx0) * (iy - fy0);
-    const bool vx0 = x0 >= 0, vx1 = x0 + 1 <= W - 1, vy0 = y0 >= 0, vy1 = y0 + 1 <= H - 1;
-    const bool ok_nw = vx0 && vy0, ok_ne = vx1 && vy0, ok_sw = vx0 && vy1, ok_se = vx1 && vy1;
-    const int cx0 = max(x0, 0), cy0 = max(y0, 0);
-    const int cx1 = min(x0 + 1, W - 1), cy1 = min(y0 + 1, H - 1);
-    const int64_t sH = vw.sH, sW = vw.sW, sC = vw.sC;
-    const int bx = min(max(x0, 0), W - 2);
-    const int64_t o_top = cy0 * sH + bx, o_bot = cy1 * sH + bx;
-    const bool nw_lo = x0 == bx, ne_lo = x0 + 1 == bx;
-    const int64_t o_nw = cy0 * sH + cx0 * sW, o_ne = cy0 * sH + cx1 * sW;
-    const int64_t o_sw = cy1 * sH + cx0 * sW, o_se = cy1 * sH + cx1 * sW;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c = c_begin + j;
-      if (c >= c_end) break;
-      const float* pc = base + (int64_t)c * sC;
-      float vnw, vne, vsw, vse;
-      if constexpr (PAIR) {
-        const f32x2u_t top = *reinterpret_cast<const f32x2u_t*>(pc + o_top);
-        const f32x2u_t bot = *reinterpret_cast<const f32x2u_t*>(pc + o_bot);
-        vnw = nw_lo ? top.x : top.y;
-        vne = ne_lo ? top.x : top.y;
-        vsw = nw_lo ? bot.x : bot.y;
-        vse = ne_lo ? bot.x : bot.y;
-      } else {
-        vnw = pc[o_nw]; vne = pc[o_ne]; vsw = pc[o_sw]; vse = pc[o_se];
-      }
-      float acc = 0.f;
-      acc += (ok_nw ? vnw : 0.f) * w_nw;
-      acc += (ok_ne ? vne : 0.f) * w_ne;
-      acc += (ok_sw ? vsw : 0.f) * w_sw;
-      acc += (ok_se ? vse : 0.f) * w_se;
-      d[r][j] = acc;
+      for (int j = 0; j < 8; ++j) ds[i][c][j] = d[j];
+      nz[i][c] = any;
     }
   }
-  if (a.skip_zero && !any) return;
-  // B^T (points 0, 1, -1, 2, inf): the rows of wino_rows_kernel
-  u32x4_t* out = static_cast<u32x4_t*>(vw.dst) + 2 * ((int64_t)b * vw.dB + (int64_t)chunk * vw.dC +
-                                                     (int64_t)5 * r3 * vw.dH + u);
-#pragma unroll
-  for (int xi = 0; xi < 5; ++xi) {
+  __syncthreads();
+  // phase 2: (tile q, column c, xi) items, B^T (points 0, 1, -1, 2, inf) as wino_rows_kernel
+  for (int it = tid; it < 4 * kWwCols * 5; it += 128) {
+    const int xi = it / (4 * kWwCols), q = (it / kWwCols) % 4, c = it % kWwCols;
+    const int r3 = 4 * k + q, u = tx * kWwCols + c;
+    if (r3 >= r3_rows || u >= a.Wo) continue;
+    const int i0 = 3 * q;  // rows i0 .. i0 + 4 of the block
+    if (a.skip_zero && !(nz[i0][c] | nz[i0 + 1][c] | nz[i0 + 2][c] | nz[i0 + 3][c] | nz[i0 + 4][c])) continue;
     float t[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float d0 = d[0][j], d1 = d[1][j], d2 = d[2][j], d3 = d[3][j], d4 = d[4][j];
+      const float d0 = ds[i0][c][j], d1 = ds[i0 + 1][c][j], d2 = ds[i0 + 2][c][j], d3 = ds[i0 + 3][c][j],
+                  d4 = ds[i0 + 4][c][j];
       t[j] = xi == 0 ? 2.f * d0 - d1 - 2.f * d2 + d3
            : xi == 1 ? -2.f * d1 - d2 + d3
            : xi == 2 ? 2.f * d1 - 3.f * d2 + d3
            : xi == 3 ? d3 - d1
                      : 2.f * d1 - d2 - 2.f * d3 + d4;
     }
-    store_split8(out + 2 * (int64_t)xi * vw.dH, t);
+    u32x4_t* out = static_cast<u32x4_t*>(vw.dst) + 2 * ((int64_t)b * vw.dB + (int64_t)chunk * vw.dC +
+                                                       (int64_t)(5 * r3 + xi) * vw.dH + u);
+    store_split8(out, t);
   }
 }
 
@@ -454,11 +465,11 @@ int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t
   a.nviews = nviews;
   a.skip_zero = (flags & MVBEV_WARP_DST_ZEROED) != 0;
   a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
-  a.tiles_x = (int)ceil_div(Wo, kWarpTW);
-  a.tiles = a.tiles_x * (int)ceil_div(r3_rows, kWarpTH);
+  a.tiles_x = (int)ceil_div(Wo, kWwCols);
+  a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);  // 4 three-row tiles per block
   a.chunks = (int)ceil_div(C, kWarpCPB);
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
-  const dim3 grid((unsigned)a.nwg), block(kWarpTH * kWarpTW);
+  const dim3 grid((unsigned)a.nwg), block(128);
   if (pair)
     hipLaunchKernelGGL((warp_wino_kernel<true>), grid, block, 0, as_stream(stream), a, (int)r3_rows);
   else

@@ -190,8 +190,8 @@ def test_fused_warp_transform_matches_two_pass(cfg):
     mc = torch.nn.Sequential(torch.nn.Conv2d(N * C + 2, 512, 3, padding=1), torch.nn.ReLU(),
                              torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
                              torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False)).to(DEV)
-    fused = ProjectFuse(pm, up, grid, C, wino_conv1=True, wino_warp=True)
-    two = ProjectFuse(pm, up, grid, C, wino_conv1=True)
+    fused = ProjectFuse(pm, up, grid, C, wino_conv1=True)
+    two = ProjectFuse(pm, up, grid, C, wino_conv1=True, wino_warp=False)
     assert fused.wino_warp and not two.wino_warp
     with torch.no_grad():
         got = fused.project_fuse(feats, mc)

@@ -287,6 +287,12 @@ int mvbev_conv3x3_bf16x3_ex3(const void* x, int x_layout, const mvbev_conv_desc*
  * first step of conv1 (:51) for inference. */
 int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t H,
                                int64_t W, int64_t Ho, int64_t Wo, int64_t r3_rows, int flags, void* stream);
+/* The same from backbone-resolution maps [B][C][h][w] (fp32, unit column stride, w >= 4): the
+ * fused 3x upsample + warp of mvbev_warp_views_upsampled (m for the upsampled size H x W) and the
+ * row transform in one pass (the detector's inference path, :65 + :69 + :77 + conv1's first step). */
+int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t h,
+                                         int64_t w, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int64_t r3_rows,
+                                         int flags, void* stream);
 size_t mvbev_conv3x3_packed_bytes_wino(int64_t Cout, int64_t K);
 int mvbev_pack_conv3x3_weight_wino(const float* w, int64_t Cout, int64_t Cin_w, const int32_t* chan_map,
                                    int64_t K, void* w_packed, void* stream);

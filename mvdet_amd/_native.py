@@ -72,6 +72,7 @@ EXPORTS = (
     "mvbev_wino_rows_split_bf16",
     "mvbev_conv3x3_wino_bf16x3",
     "mvbev_warp_views_wino_rows",
+    "mvbev_warp_views_upsampled_wino_rows",
 )
 WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
 TILES_GRID, TILES_EDGE_STRIP = 0, 1  # MVBEV_TILES_*
@@ -179,6 +180,9 @@ def _declare(lib):
     lib.mvbev_warp_views_wino_rows.restype = ctypes.c_int
     lib.mvbev_warp_views_wino_rows.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
                                                _i64, _i64, ctypes.c_int, _p]
+    lib.mvbev_warp_views_upsampled_wino_rows.restype = ctypes.c_int
+    lib.mvbev_warp_views_upsampled_wino_rows.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64,
+                                                         _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_int, _p]
     lib.mvbev_warp_tile_mask.restype = ctypes.c_int
     lib.mvbev_warp_tile_mask.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
                                          _i64, _i64, _i64, _i64, _p, _p]

@@ -153,8 +153,6 @@ __global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_tile_kernel(const Warp
 // in 32-B units: dB per item, dC per 8-channel group, dH per T row).  The slab itself is never
 // written.  skip_zero: a (tile, column) whose 5 samples all fall outside the source is not
 // written (T is zero-filled once and only ever written by this geometry).
-constexpr int kWwRows = 14, kWwCols = 8;  // rows warped per block (4 tiles + the 2 shared halo rows)
-static_assert(kWarpCPB == 8, "one 8-channel group per block");
 template <bool PAIR>
 __global__ __launch_bounds__(128) void warp_wino_kernel(const WarpArgs a, int r3_rows) {
   __shared__ float ds[kWwRows][kWwCols][9];  // [row][col][channel] (+1 pad)
@@ -240,28 +238,7 @@ __global__ __launch_bounds__(128) void warp_wino_kernel(const WarpArgs a, int r3
     }
   }
   __syncthreads();
-  // phase 2: (tile q, column c, xi) items, B^T (points 0, 1, -1, 2, inf) as wino_rows_kernel
-  for (int it = tid; it < 4 * kWwCols * 5; it += 128) {
-    const int xi = it / (4 * kWwCols), q = (it / kWwCols) % 4, c = it % kWwCols;
-    const int r3 = 4 * k + q, u = tx * kWwCols + c;
-    if (r3 >= r3_rows || u >= a.Wo) continue;
-    const int i0 = 3 * q;  // rows i0 .. i0 + 4 of the block
-    if (a.skip_zero && !(nz[i0][c] | nz[i0 + 1][c] | nz[i0 + 2][c] | nz[i0 + 3][c] | nz[i0 + 4][c])) continue;
-    float t[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float d0 = ds[i0][c][j], d1 = ds[i0 + 1][c][j], d2 = ds[i0 + 2][c][j], d3 = ds[i0 + 3][c][j],
-                  d4 = ds[i0 + 4][c][j];
-      t[j] = xi == 0 ? 2.f * d0 - d1 - 2.f * d2 + d3
-           : xi == 1 ? -2.f * d1 - d2 + d3
-           : xi == 2 ? 2.f * d1 - 3.f * d2 + d3
-           : xi == 3 ? d3 - d1
-                     : 2.f * d1 - d2 - 2.f * d3 + d4;
-    }
-    u32x4_t* out = static_cast<u32x4_t*>(vw.dst) + 2 * ((int64_t)b * vw.dB + (int64_t)chunk * vw.dC +
-                                                       (int64_t)(5 * r3 + xi) * vw.dH + u);
-    store_split8(out, t);
-  }
+  wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
 }
 
 template <typename T, bool SPLIT>

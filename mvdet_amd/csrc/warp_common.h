@@ -189,4 +189,39 @@ __device__ inline UpWindow up_window(const float (&m)[9], int u, int v, int Ho, 
   return r;
 }
 
+// Warp + row-Winograd transform kernels (warp_wino_kernel, warp_up_wino_kernel): a block warps
+// the kWwRows input rows 12 k - 1 + i of 4 three-row output tiles x kWwCols columns of one
+// view's 8-channel group into LDS (ds, nz = some sample non-zero), then this phase stores, per
+// (tile, column, xi), the transformed row B^T d (points 0, 1, -1, 2, inf; the rows of
+// wino_rows_kernel in conv_bf16x3.hip) split-bf16 at T row 5 r3 + xi (vw.dst strides in 32-B
+// units: dB per item, dC per 8-channel group, dH per T row).  skip_zero: a (tile, column) whose 5
+// samples are all outside the source is not written (T zero-filled, written only by this geometry).
+constexpr int kWwRows = 14, kWwCols = 8;
+static_assert(kWarpCPB == 8 && kUpCPB == 8, "one 8-channel group per warp block");
+__device__ inline void wino_rows_phase2(const float (&ds)[kWwRows][kWwCols][9], const unsigned char (&nz)[kWwRows][kWwCols],
+                                        const WarpView& vw, const WarpArgs& a, int b, int chunk, int k, int tx,
+                                        int r3_rows) {
+  for (int it = threadIdx.x; it < 4 * kWwCols * 5; it += blockDim.x) {
+    const int xi = it / (4 * kWwCols), q = (it / kWwCols) % 4, c = it % kWwCols;
+    const int r3 = 4 * k + q, u = tx * kWwCols + c;
+    if (r3 >= r3_rows || u >= a.Wo) continue;
+    const int i0 = 3 * q;  // rows i0 .. i0 + 4 of the block
+    if (a.skip_zero && !(nz[i0][c] | nz[i0 + 1][c] | nz[i0 + 2][c] | nz[i0 + 3][c] | nz[i0 + 4][c])) continue;
+    float t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d0 = ds[i0][c][j], d1 = ds[i0 + 1][c][j], d2 = ds[i0 + 2][c][j], d3 = ds[i0 + 3][c][j],
+                  d4 = ds[i0 + 4][c][j];
+      t[j] = xi == 0 ? 2.f * d0 - d1 - 2.f * d2 + d3
+           : xi == 1 ? -2.f * d1 - d2 + d3
+           : xi == 2 ? 2.f * d1 - 3.f * d2 + d3
+           : xi == 3 ? d3 - d1
+                     : 2.f * d1 - d2 - 2.f * d3 + d4;
+    }
+    u32x4_t* out = static_cast<u32x4_t*>(vw.dst) + 2 * ((int64_t)b * vw.dB + (int64_t)chunk * vw.dC +
+                                                       (int64_t)(5 * r3 + xi) * vw.dH + u);
+    store_split8(out, t);
+  }
+}
+
 }  // namespace mvbev

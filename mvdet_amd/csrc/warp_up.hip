@@ -131,7 +131,124 @@ __global__ __launch_bounds__(kUpTH * kUpTW) void warp_up_kernel(const UpArgs ua)
   }
 }
 
+// Fused 3x upsample + warp + row-Winograd transform (inference conv1 from backbone-resolution
+// maps, the detector's path): phase 1 warps the block's 14 input rows as warp_up_kernel samples
+// them (fp32 source, 16-B window rows), phase 2 is wino_rows_phase2 (warp_common.h).
+static_assert(kUpCPB == 8, "one 8-channel group per block");
+__global__ __launch_bounds__(128) void warp_up_wino_kernel(const UpArgs ua, int r3_rows) {
+  __shared__ float ds[kWwRows][kWwCols][9];
+  __shared__ unsigned char nz[kWwRows][kWwCols];
+  const WarpArgs& a = ua.w;
+  const int lb = xcd_remap(blockIdx.x, a.nwg);
+  const int tile = lb % a.tiles;
+  const int chunk = (lb / a.tiles) % a.chunks;
+  const int bv = lb / (a.tiles * a.chunks);
+  const int view = bv % a.nviews;
+  const int b = bv / a.nviews;
+  const WarpView& vw = a.v[view];
+  const int k = tile / a.tiles_x, tx = tile - k * a.tiles_x;
+  const int c_begin = chunk * kUpCPB;
+  const int c_end = min(a.C, c_begin + kUpCPB);
+  const int H = a.H, W = a.W, h = ua.h, w = ua.sw;
+  {
+    const int i = threadIdx.x / kWwCols, c = threadIdx.x % kWwCols;
+    const int v = 12 * k - 1 + i, u = tx * kWwCols + c;
+    if (i < kWwRows) {
+      float d[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = 0.f;
+      bool any = false;
+      if (v >= 0 && v < a.Ho && u < a.Wo) {
+        float m[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) m[q] = vw.m[q];
+        const UpWindow uw = up_window(m, u, v, a.Ho, a.Wo, H, W, h, w, ua.sy, ua.sx);
+        if (!uw.inside) {
+          if (!uw.finite) {
+            any = true;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = c_begin + j < c_end ? __builtin_nanf("") : 0.f;
+          }
+        } else {
+          any = true;
+          const int cb = uw.cb, rb = uw.rb;
+          const int c4 = min(cb, w - 4);
+          const int sh = cb - c4;
+          float bx[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int kk = j - sh;
+            bx[j] = (kk == 0 ? uw.ax[0] : 0.f) + (kk == 1 ? uw.ax[1] : 0.f) + (kk == 2 ? uw.ax[2] : 0.f);
+          }
+          int64_t off[3];
+#pragma unroll
+          for (int r = 0; r < 3; ++r) off[r] = min(rb + r, h - 1) * vw.sH + c4;
+          const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int ch = c_begin + j;
+            if (ch >= c_end) break;
+            const float* pc = base + (int64_t)ch * vw.sC;
+            float acc = 0.f;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+              const f32x4u_t q = *reinterpret_cast<const f32x4u_t*>(pc + off[r]);
+              acc += uw.ay[r] * (bx[0] * q.x + bx[1] * q.y + bx[2] * q.z + bx[3] * q.w);
+            }
+            d[j] = acc;
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ds[i][c][j] = d[j];
+      nz[i][c] = any;
+    }
+  }
+  __syncthreads();
+  wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
+}
+
 }  // namespace mvbev
+
+extern "C" int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
+                                                    int64_t h, int64_t w, int64_t H, int64_t W, int64_t Ho,
+                                                    int64_t Wo, int64_t r3_rows, int flags, void* stream) {
+  using namespace mvbev;
+  if (flags & ~MVBEV_WARP_DST_ZEROED) return MVBEV_ERR_SHAPE;
+  if (!views) return MVBEV_ERR_NULL;
+  if (B <= 0 || C <= 0 || h <= 0 || w <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 || nviews <= 0 || r3_rows <= 0)
+    return MVBEV_ERR_RANK;
+  if (nviews > kWarpMaxViews || B * nviews > 65535 || C > INT32_MAX || H > INT32_MAX / 2 || W > INT32_MAX / 2 ||
+      Ho > INT32_MAX / 2 || Wo > INT32_MAX / 2 || H < h || W < w || w < 4 || 3 * r3_rows < Ho ||
+      ceil_div(r3_rows, 4) * ceil_div(Wo, kWwCols) * ceil_div(C, kUpCPB) * B * nviews > INT32_MAX)
+    return MVBEV_ERR_SHAPE;
+  UpArgs ua = {};
+  WarpArgs& a = ua.w;
+  for (int i = 0; i < nviews; ++i) {
+    const mvbev_warp_view& s = views[i];
+    if (!s.src || !s.dst) return MVBEV_ERR_NULL;
+    if (s.dst_strides[3] != 1 || s.src_strides[3] != 1) return MVBEV_ERR_STRIDE;  // 16-B window rows
+    WarpView& d = a.v[i];
+    d.src = s.src; d.sB = s.src_strides[0]; d.sC = s.src_strides[1];
+    d.sH = s.src_strides[2]; d.sW = s.src_strides[3];
+    d.dst = s.dst; d.dB = s.dst_strides[0]; d.dC = s.dst_strides[1]; d.dH = s.dst_strides[2];
+    d.m_dev = nullptr;
+    for (int k = 0; k < 9; ++k) d.m[k] = s.m[k];
+  }
+  a.nviews = nviews;
+  a.skip_zero = (flags & MVBEV_WARP_DST_ZEROED) != 0;
+  a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
+  a.tiles_x = (int)ceil_div(Wo, kWwCols);
+  a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);
+  a.chunks = (int)ceil_div(C, kUpCPB);
+  a.nwg = a.tiles * a.chunks * a.B * a.nviews;
+  ua.h = (int)h; ua.sw = (int)w;
+  ua.sy = (float)h / (float)H;
+  ua.sx = (float)w / (float)W;
+  hipLaunchKernelGGL(warp_up_wino_kernel, dim3((unsigned)a.nwg), dim3(128), 0, as_stream(stream), ua, (int)r3_rows);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
 
 extern "C" int mvbev_warp_views_upsampled_ex(const mvbev_warp_view* views, int nviews, int src_is_f16,
                                              int64_t B, int64_t C, int64_t h, int64_t w, int64_t H,

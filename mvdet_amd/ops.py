@@ -508,11 +508,13 @@ def wino_rows(x: torch.Tensor, desc, t: torch.Tensor, group_mask: Optional[torch
 
 
 def warp_views_wino_rows_into(srcs, m_norms, t: torch.Tensor, slots, Cs: int, K: int, Ho: int, Wo: int,
-                              dst_zeroed: bool = False) -> None:
+                              dst_zeroed: bool = False, up_hw=None) -> None:
     """Warp + row-Winograd transform in ONE launch (``mvbev_warp_views_wino_rows``): view i
     (fp32 ``srcs[i]`` [B,C,H,W], host kornia matrix ``m_norms[i]``) lands in channels
     [slots[i] * Cs, + C) of ``t``, the T buffer of ``wino_rows`` for a K-channel slab of
-    Ho x Wo (whole grid, out_row0 = 0); the slab itself is not written."""
+    Ho x Wo (whole grid, out_row0 = 0); the slab itself is not written.  ``up_hw``: the sources
+    are backbone-resolution maps upsampled 3x to ``up_hw`` inside the warp
+    (``mvbev_warp_views_upsampled_wino_rows``; ``m_norms`` for the upsampled size)."""
     n = len(srcs)
     if n == 0:
         return
@@ -536,8 +538,13 @@ def warp_views_wino_rows_into(srcs, m_norms, t: torch.Tensor, slots, Cs: int, K:
         arr[i].dst = t.data_ptr() + 32 * (int(slot) * (Cs // KC)) * 5 * r3 * Wo
         arr[i].dst_strides = _native._i64x4(K8 * 5 * r3 * Wo, 5 * r3 * Wo, Wo, 1)  # 32-byte units
         arr[i].m = (ctypes.c_float * 9)(*mm)
-    st = _native.load().mvbev_warp_views_wino_rows(arr, n, B, C, H, W, Ho, Wo, r3,
-                                                   _native.WARP_DST_ZEROED if dst_zeroed else 0, _stream(t))
+    flags = _native.WARP_DST_ZEROED if dst_zeroed else 0
+    if up_hw is not None:
+        st = _native.load().mvbev_warp_views_upsampled_wino_rows(arr, n, B, C, H, W, int(up_hw[0]), int(up_hw[1]),
+                                                                 Ho, Wo, r3, flags, _stream(t))
+        _native.check(st, "mvbev_warp_views_upsampled_wino_rows")
+        return
+    st = _native.load().mvbev_warp_views_wino_rows(arr, n, B, C, H, W, Ho, Wo, r3, flags, _stream(t))
     _native.check(st, "mvbev_warp_views_wino_rows")
 
 

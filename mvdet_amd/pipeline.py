@@ -212,6 +212,18 @@ class ProjectFuse:
         return (self.wino_warp and not ws.store_y2 and ws.y1_rows == (0, H) and ws.slab_zeroed
                 and all(f.dtype == torch.float32 for f in feats) and self.src_hw[1] >= 2)
 
+    def _warp_views_t(self, ws: Workspace, cams, feats, up_hw=None) -> None:
+        """The warp writing conv1's row transform T (``ops.warp_views_wino_rows_into``)."""
+        H, W = self.grid_hw
+        B = ws.slab.shape[1]
+        need = ops.wino_rows_bytes(self._conv1_desc(B))
+        if ws.wino_t is None or ws.wino_t.numel() * 2 < need:
+            ws.wino_t = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=ws.slab.device)
+        ops.warp_views_wino_rows_into(list(feats), [self.m_norm_cpu[c] for c in cams], ws.wino_t,
+                                      [self.slot_of[c] for c in cams], self.Cs, self.S * self.Cs, H, W,
+                                      dst_zeroed=True, up_hw=up_hw)
+        ws.t_from_warp = True
+
     def warp_views(self, ws: Workspace, cams: Sequence[int], feats: Sequence[torch.Tensor]) -> None:
         """a5 for several views in one launch (``feats[i]`` is view ``cams[i]``).  With
         ``wino_warp`` (inference, whole grid) a5 + a6 + conv1's row transform in one pass: the
@@ -221,16 +233,7 @@ class ProjectFuse:
                 raise ValueError(f"view {cam}: features {tuple(f.shape)} do not match "
                                  f"[B,{self.C},{self.src_hw[0]},{self.src_hw[1]}]")
         if self._wino_warp_applies(ws, feats):
-            H, W = self.grid_hw
-            B = ws.slab.shape[1]
-            d1 = self._conv1_desc(B)
-            need = ops.wino_rows_bytes(d1)
-            if ws.wino_t is None or ws.wino_t.numel() * 2 < need:
-                ws.wino_t = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=ws.slab.device)
-            ops.warp_views_wino_rows_into(list(feats), [self.m_norm_cpu[c] for c in cams], ws.wino_t,
-                                          [self.slot_of[c] for c in cams], self.Cs, self.S * self.Cs, H, W,
-                                          dst_zeroed=True)
-            ws.t_from_warp = True
+            self._warp_views_t(ws, cams, feats)
             return
         ws.t_from_warp = False
         ops.warp_views_into(list(feats), [self.m_norm_cpu[c] for c in cams],
@@ -244,6 +247,9 @@ class ProjectFuse:
         for cam, f in zip(cams, feats):
             if f.shape[1] != self.C or f.shape[2] > self.src_hw[0] or f.shape[3] > self.src_hw[1]:
                 raise ValueError(f"view {cam}: features {tuple(f.shape)} cannot upsample to {self.src_hw}")
+        if self._wino_warp_applies(ws, feats) and all(f.shape[3] >= 4 and f.stride(3) == 1 for f in feats):
+            self._warp_views_t(ws, cams, feats, up_hw=self.src_hw)  # a4 + a5 + a6 + conv1's B^T in one pass
+            return
         ws.t_from_warp = False
         ops.warp_views_upsampled_into(list(feats), self.src_hw, [self.m_norm_cpu[c] for c in cams],
                                       [self._slot_dst(ws, c) for c in cams], split=self.split,

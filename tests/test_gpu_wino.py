@@ -206,11 +206,18 @@ def test_fused_warp_transform_matches_two_pass(cfg):
         # combinations (coefficient sums <= 6) differ by a few 1e-5 of the range
         assert (a - b).abs().max().item() <= 1e-4 * max(1.0, b.abs().max().item())
         assert_parity(got.cpu(), ref.cpu(), "fused-warp map", normwise_tol=TOL)
-        # backbone-resolution input writes the slab: conv1 must transform it again
+        # backbone-resolution input: the fused upsample + warp + B^T (mvbev_warp_views_upsampled_wino_rows)
+        # vs upsample + warp into the slab, then the transform
         low = [torch.nn.functional.avg_pool2d(f, 3) for f in feats]
         fused.warp_views_upsampled(wf, list(range(N)), low)
-        assert not wf.t_from_warp
+        assert wf.t_from_warp
         m1 = fused.fuse(wf, mc)
         two.warp_views_upsampled(wt, list(range(N)), low)
         m2 = two.fuse(wt, mc)
-    assert_parity(m1.cpu(), m2.cpu(), "slab path after the fused warp", normwise_tol=TOL)
+        assert_parity(m1.cpu(), m2.cpu(), "fused upsample + warp + B^T map", normwise_tol=TOL)
+        # a slab-writing warp (one view at a time) switches conv1 back to the slab's transform
+        for v in range(N):
+            fused.warp_view(wf, v, feats[v])
+        assert not wf.t_from_warp
+        m3 = fused.fuse(wf, mc)
+    assert_parity(m3.cpu(), ref.cpu(), "slab path after the fused warp", normwise_tol=TOL)

@@ -133,8 +133,10 @@ def main():
             eng.warp_view(ws, v, feats[v])
         eng.fuse(ws, mc)
         from mvdet_amd import ops
+        # the slab path (wino_warp off) so the transform stages run on real data; warpw / warpupw
+        # switch the fused warp on (and leave T from the warp: run them last)
         weng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision, frustum=not args.no_frustum,
-                           wino_conv1=True)
+                           wino_conv1=True, wino_warp=False)
         wws = weng.workspace(B, dev)
         weng.warp_views(wws, list(range(N)), feats)
         weng.conv1(wws, mc[0])
@@ -159,6 +161,8 @@ def main():
             "winorows": (lambda: ops.wino_rows(wws.slab, wd1, wws.wino_t, wgm), None),
             "warpw": (lambda: _with(weng, "wino_warp", True, lambda: weng.warp_views(wws, list(range(N)), feats)),
                       None),  # warp + B^T in one pass (wino_warp; leaves T from the warp, run it last)
+            "warpupw": (lambda: _with(weng, "wino_warp", True,
+                                      lambda: weng.warp_views_upsampled(wws, list(range(N)), bfeats)), None),
             "winoconv": (lambda: ops.conv3x3_wino(wws.wino_t, wd1, weng.pack1w.get(mc[0].weight), 512,
                                                   init=weng.coord_term(mc[0]), relu=True, out=wws.y1,
                                                   group_mask=wgm, tile_order=weng.conv1_order(dev, 0, ho, B, grid=True)),

@@ -186,7 +186,11 @@ class ProjectFuse:
 
     def view_slice(self, ws: Workspace, cam: int) -> torch.Tensor:
         """[B, C, Ho, Wo] of ``cam``'s warped features: a view of the slab, or (split
-        layout) its fp32 decode (hi + lo)."""
+        layout) its fp32 decode (hi + lo).  Not available after the fused warp (``wino_warp``),
+        which writes conv1's row transform instead of the slab."""
+        if ws.t_from_warp:
+            raise RuntimeError("the slab was not written: the warp wrote conv1's row transform instead "
+                               "(wino_warp); use wino_warp=False to keep the warped views")
         if self.split:
             return ops.split_decode(ws.slab[self.slot_of[cam]], self.C)
         return ws.slab[self.slot_of[cam], :, :self.C]

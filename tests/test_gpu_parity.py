@@ -523,6 +523,16 @@ def test_detector_forward_matches_reference_golden(name):
     assert_parity(torch.stack(imgs_res, 0).cpu(), g["imgs_result"], f"{name} imgs_result")
     eng = model.engine
     ws = eng.workspace(m["B"], "cuda:0")
+    # the inference default writes conv1's row transform straight from the warp (no slab):
+    # the intermediate-tensor checks below run the slab path of the same module
+    assert eng.wino_warp and ws.t_from_warp
+    with pytest.raises(RuntimeError):
+        eng.view_slice(ws, 0)
+    eng.wino_warp = False
+    with torch.no_grad():
+        map2, _ = model(torch.from_numpy(g["feat_in"]))
+    assert not ws.t_from_warp
+    assert_parity(map2.cpu(), g["map_result"], f"{name} map_result (slab path)")
     N, C = m["num_cam"], 512
     warped = torch.stack([eng.view_slice(ws, v) for v in range(N)], 1)  # [B, N, C, ho, wo]
     np.testing.assert_allclose(warped.double().sum(dim=(3, 4)).cpu().numpy(), g["warp_out_chsum"],

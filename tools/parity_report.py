@@ -26,6 +26,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--precision", default="fp32")
+    ap.add_argument("--conv1", default="direct", choices=["direct", "wino"],
+                    help="conv1 form (bf16x3): the direct ring conv or row-Winograd F(3,3) with the fused warp")
     args = ap.parse_args()
     spec = synthetic.CONFIGS[args.config]
     ds = spec["make"]()
@@ -41,7 +43,8 @@ def main():
     params = fixtures.head_params(ds.num_cam, seed=args.config, C=C)
     pm = projection_matrices(ds)
     eng = ProjectFuse(pm, tuple(up), tuple(ds.reducedgrid_shape), C, precision=args.precision,
-                      slab_dtype=torch.float16 if half else torch.float32)
+                      slab_dtype=torch.float16 if half else torch.float32,
+                      wino_conv1=args.conv1 == "wino" and args.precision == "bf16x3")
     mc = build_mc(C, ds.num_cam, params, "cuda:0")
     with torch.no_grad():
         got = eng.project_fuse([f.to("cuda:0", torch.float16 if half else torch.float32) for f in feats], mc)
@@ -52,9 +55,11 @@ def main():
     ws = eng.workspace(B, "cuda:0")
     with torch.no_grad():  # inference fuses conv2 into conv3 (no y2 in HBM): run conv2 alone for its parity
         eng.conv2(ws, mc[2])
-    rep = {"config": args.config, "precision": args.precision, "slab": str(eng.slab_dtype)}
-    rep["warp_worst_normwise"] = max(parity_stats(eng.view_slice(ws, v).float().cpu(), keep["warped"][v])["normwise"]
-                                     for v in range(ds.num_cam))
+    rep = {"config": args.config, "precision": args.precision, "slab": str(eng.slab_dtype),
+           "conv1_form": "row-Winograd, warp writes T" if ws.t_from_warp else "direct"}
+    if not ws.t_from_warp:  # the fused warp writes conv1's row transform, not the slab
+        rep["warp_worst_normwise"] = max(parity_stats(eng.view_slice(ws, v).float().cpu(),
+                                                      keep["warped"][v])["normwise"] for v in range(ds.num_cam))
     for name, g, r in (("conv1", eng.y1_fp32(ws), keep["conv1_relu"]), ("conv2", ws.y2, keep["conv2_relu"]),
                        ("map_result", got, ref)):
         s = parity_stats(g.cpu(), r)

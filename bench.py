@@ -176,6 +176,8 @@ def run_single(args, precision, steps, warmup, with_cpu):
     s = 2 if half else 4
     tv = [touched_footprint(M.numpy(), up, (ho, wo)) for M in pm]
     warp_bytes = sum(s * B * C * (t + ho * wo) for t in tv)
+    if eng.wino_warp:  # the warp writes conv1's row transform: 5 split-bf16 rows per 3-row tile
+        warp_bytes = sum(4 * B * C * (t + 5 * 4 * -(-ho // 12) * wo) for t in tv)
     conv3_bytes = 4.0 * B * ho * wo * (512 + 1)
     conv1_alg_tfs = conv1_flop / (t_c1k * 1e-3) / 1e12  # over the conv kernel's time
     active = eng.conv1_active_fraction(dev, *ws.y1_rows[:1], ws.y1_rows[1] - ws.y1_rows[0], grid=wino) \

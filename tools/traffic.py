@@ -54,7 +54,7 @@ conv1 = [k for k in res["kernels"] if re.search(pat, k)]
 if conv1:
     res["conv1_hbm_bytes_per_launch"] = res["kernels"][conv1[0]]["hbm_bytes_per_launch"]
 # the all-views warp of the timed "warp" stage: the largest-grid warp_tile_kernel dispatch
-warps = [k for k in res["kernels"] if "warp_tile_kernel" in k]
+warps = [k for k in res["kernels"] if ("warp_wino_kernel" if wino else "warp_tile_kernel") in k]
 if warps:
     k = max(warps, key=lambda n: int(n.rsplit("grid ", 1)[1].rstrip("]")))
     res["warp_hbm_bytes_per_launch"] = res["kernels"][k]["hbm_bytes_per_launch"]

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_tile_kernel(const Warp
 // written.  skip_zero: a (tile, column) whose 5 samples all fall outside the source is not
 // written (T is zero-filled once and only ever written by this geometry).
 template <bool PAIR>
-__global__ __launch_bounds__(128) void warp_wino_kernel(const WarpArgs a, int r3_rows) {
+__global__ __launch_bounds__(kWwThreads) void warp_wino_kernel(const WarpArgs a, int r3_rows) {
   __shared__ float ds[kWwRows][kWwCols][9];  // [row][col][channel] (+1 pad)
   __shared__ unsigned char nz[kWwRows][kWwCols];
   const int lb = xcd_remap(blockIdx.x, a.nwg);
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(128) void warp_wino_kernel(const WarpArgs a, int r3
   const int H = a.H, W = a.W;
   const int tid = threadIdx.x;
   {  // phase 1: one warped pixel (8 channels) per thread
-    const int i = tid / kWwCols, c = tid % kWwCols;  // 16 x 8 threads, rows >= 14 idle
+    const int i = tid / kWwCols, c = tid % kWwCols;  // 16 x kWwCols threads, rows >= 14 idle
     const int v = 12 * k - 1 + i, u = tx * kWwCols + c;
     if (i < kWwRows) {
       float d[8];
@@ -446,7 +446,7 @@ int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t
   a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);  // 4 three-row tiles per block
   a.chunks = (int)ceil_div(C, kWarpCPB);
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
-  const dim3 grid((unsigned)a.nwg), block(128);
+  const dim3 grid((unsigned)a.nwg), block(kWwThreads);
   if (pair)
     hipLaunchKernelGGL((warp_wino_kernel<true>), grid, block, 0, as_stream(stream), a, (int)r3_rows);
   else

@@ -196,7 +196,10 @@ __device__ inline UpWindow up_window(const float (&m)[9], int u, int v, int Ho, 
 // wino_rows_kernel in conv_bf16x3.hip) split-bf16 at T row 5 r3 + xi (vw.dst strides in 32-B
 // units: dB per item, dC per 8-channel group, dH per T row).  skip_zero: a (tile, column) whose 5
 // samples are all outside the source is not written (T zero-filled, written only by this geometry).
-constexpr int kWwRows = 14, kWwCols = 8;
+#ifndef MVBEV_WW_COLS
+#define MVBEV_WW_COLS 16  // columns per fused-warp block (threads = 16 x columns; cfg2: 8 0.52-0.56 ms, 16 0.51)
+#endif
+constexpr int kWwRows = 14, kWwCols = MVBEV_WW_COLS, kWwThreads = 16 * kWwCols;
 static_assert(kWarpCPB == 8 && kUpCPB == 8, "one 8-channel group per warp block");
 __device__ inline void wino_rows_phase2(const float (&ds)[kWwRows][kWwCols][9], const unsigned char (&nz)[kWwRows][kWwCols],
                                         const WarpView& vw, const WarpArgs& a, int b, int chunk, int k, int tx,

@@ -135,7 +135,7 @@ __global__ __launch_bounds__(kUpTH * kUpTW) void warp_up_kernel(const UpArgs ua)
 // maps, the detector's path): phase 1 warps the block's 14 input rows as warp_up_kernel samples
 // them (fp32 source, 16-B window rows), phase 2 is wino_rows_phase2 (warp_common.h).
 static_assert(kUpCPB == 8, "one 8-channel group per block");
-__global__ __launch_bounds__(128) void warp_up_wino_kernel(const UpArgs ua, int r3_rows) {
+__global__ __launch_bounds__(kWwThreads) void warp_up_wino_kernel(const UpArgs ua, int r3_rows) {
   __shared__ float ds[kWwRows][kWwCols][9];
   __shared__ unsigned char nz[kWwRows][kWwCols];
   const WarpArgs& a = ua.w;
@@ -245,7 +245,7 @@ extern "C" int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views
   ua.h = (int)h; ua.sw = (int)w;
   ua.sy = (float)h / (float)H;
   ua.sx = (float)w / (float)W;
-  hipLaunchKernelGGL(warp_up_wino_kernel, dim3((unsigned)a.nwg), dim3(128), 0, as_stream(stream), ua, (int)r3_rows);
+  hipLaunchKernelGGL(warp_up_wino_kernel, dim3((unsigned)a.nwg), dim3(kWwThreads), 0, as_stream(stream), ua, (int)r3_rows);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -139,6 +139,15 @@ int mvbev_warp_views_upsampled_ex(const mvbev_warp_view* views, int nviews, int 
 int mvbev_warp_tile_mask(const mvbev_warp_view* views, int nviews, int64_t H, int64_t W,
                          int64_t Ho, int64_t Wo, int64_t row0, int64_t rows, int64_t tile_h,
                          int64_t tile_w, int64_t halo, uint32_t* mask, void* stream);
+/* *bits (device uint32, overwritten) = the views (bit s = views[s], nviews <= 16) whose warp has
+ * an output pixel of the Ho x Wo grid with non-finite sample coordinates, i.e. a NaN in the warped
+ * features of persp_trans_detector.py:69 (a degenerate homography; kornia's 0/0 meshgrid when Ho
+ * or Wo is 1).  The warp kernels' own fp32 coordinate code.  Only views[].m is read.  The
+ * row-Winograd conv1 mixes a 3-row tile's rows before its products, so a caller routes such
+ * geometry to the direct conv, which keeps NaN to the taps that read it as the reference's
+ * nn.Conv2d (:51) does. */
+int mvbev_warp_nonfinite_views(const mvbev_warp_view* views, int nviews, int64_t H, int64_t W, int64_t Ho,
+                               int64_t Wo, uint32_t* bits, void* stream);
 /* fp16 storage for src and dst, fp32 math. */
 int mvbev_warp_views_f16(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
                          int64_t H, int64_t W, int64_t Ho, int64_t Wo, void* stream);
@@ -400,17 +409,8 @@ typedef struct mvbev_conv_schedule {
   size_t partial_bytes;
 } mvbev_conv_schedule;
 size_t mvbev_conv_schedule_slot_bytes(void);
-/* mvbev_conv3x3_bf16x3_ex (split-bf16 x only) and mvbev_conv3x3_dgrad_bf16x3_ex (split-bf16 dy
- * only) run as scheduled (tile_order is replaced by the items).  _sched3: the forward with the
- * tiles of tile_space (MVBEV_TILES_*; item tiles and group_mask index that space). */
-int mvbev_conv3x3_bf16x3_sched3(const void* x, int x_layout, const mvbev_conv_desc* desc, const void* w_packed,
-                                const float* bias, const float* init, int64_t Cout, int dilation, int relu, void* y,
-                                int y_layout, const uint32_t* group_mask, int tile_space,
-                                const mvbev_conv_schedule* sched, void* stream);
-int mvbev_conv3x3_bf16x3_sched(const void* x, int x_layout, const mvbev_conv_desc* desc, const void* w_packed,
-                               const float* bias, const float* init, int64_t Cout, int dilation, int relu, void* y,
-                               int y_layout, const uint32_t* group_mask, const mvbev_conv_schedule* sched,
-                               void* stream);
+/* mvbev_conv3x3_dgrad_bf16x3_ex (split-bf16 dy only) run as scheduled (the training backward's
+ * conv1 data gradient; out_mask as there). */
 int mvbev_conv3x3_dgrad_bf16x3_sched(const void* dy, int dy_layout, const mvbev_conv_desc* desc,
                                      const void* w_packed, int64_t Cout_p, int dilation, void* dx, int dx_layout,
                                      const uint32_t* out_mask, int64_t cot_per_group,
@@ -520,23 +520,16 @@ int mvbev_conv3x3_cout1_backward_ex(const float* x, const float* w, const float*
 int mvbev_threshold_points(const float* map, int64_t H, int64_t W, float thres, int32_t* count,
                            int32_t* ij, float* scores, int64_t capacity, void* stream);
 
-/* Greedy point NMS of multiview_detector/utils/nms.py:7-43: candidates by descending score
- * (equal scores: larger index first), the top_k largest considered; keep the best, drop every
- * later candidate whose distance sqrt(dx^2+dy^2) (fp32, correctly rounded) is not > dist_thres,
- * repeat.  points [K][2] fp32, scores [K] fp32 (device); keep [K] int64 = kept indices then
- * zeros; *count (device int32) = number kept.  K <= 8192 (one workgroup, LDS sort); larger K
- * returns MVBEV_ERR_SHAPE here and runs through mvbev_point_nms_ws. */
-int mvbev_point_nms(const float* points, const float* scores, int64_t K, float dist_thres,
-                    int64_t top_k, int64_t* keep, int32_t* count, void* stream);
-
-/* Device workspace bytes mvbev_point_nms_ws needs for K candidates (0 when K <= 8192). */
+/* Greedy point NMS of multiview_detector/utils/nms.py:7-43 for any K (trainer.py:154 passes every
+ * map cell over cls_thres, up to Ho*Wo): the candidates in the order torch's CPU scores.sort(0)
+ * produces (nms.py:22; libstdc++ std::sort of (score, index) pairs, NaN largest — replayed
+ * exactly, so equal scores come out as on the reference's CPU, not in index order), read from
+ * the end, the top_k largest considered; keep the best, drop every later candidate whose
+ * distance sqrt(dx^2+dy^2) (fp32, correctly rounded) is not > dist_thres, repeat (nms.py:29-42).
+ * points [K][2] fp32, scores [K] fp32 (device); keep [K] int64 = kept indices then zeros;
+ * *count (device int32) = number kept.  workspace: device, >= mvbev_point_nms_workspace_bytes,
+ * 4-B aligned.  One workgroup; enqueued, no host sync. */
 size_t mvbev_point_nms_workspace_bytes(int64_t K, int64_t top_k);
-
-/* mvbev_point_nms for any K (the reference nms.py accepts any; trainer.py:154 passes every map
- * cell over cls_thres, up to Ho*Wo): K <= 8192 is mvbev_point_nms; above, the same order and
- * greedy loop over `workspace` (>= mvbev_point_nms_workspace_bytes, 4-B aligned): a bitonic sort
- * (LDS chunks + global merge passes), then per kept point an ordered compaction of the
- * candidates strictly farther than dist_thres (nms.py:40).  Enqueued, no host sync. */
 int mvbev_point_nms_ws(const float* points, const float* scores, int64_t K, float dist_thres,
                        int64_t top_k, int64_t* keep, int32_t* count, void* workspace, size_t ws_bytes,
                        void* stream);

@@ -34,7 +34,6 @@ EXPORTS = (
     "mvbev_conv3x3_bf16x3_ex",
     "mvbev_warp_tile_mask",
     "mvbev_threshold_points",
-    "mvbev_point_nms",
     "mvbev_point_nms_workspace_bytes",
     "mvbev_point_nms_ws",
     "mvbev_warp_views_backward_f32",
@@ -61,11 +60,9 @@ EXPORTS = (
     "mvbev_conv3x3_wgrad_bf16x3_ex2",
     "mvbev_split_rows_bf16",
     "mvbev_conv_schedule_slot_bytes",
-    "mvbev_conv3x3_bf16x3_sched",
     "mvbev_conv3x3_dgrad_bf16x3_sched",
     "mvbev_conv_ring_tile_space",
     "mvbev_conv3x3_bf16x3_ex3",
-    "mvbev_conv3x3_bf16x3_sched3",
     "mvbev_conv3x3_packed_bytes_wino",
     "mvbev_pack_conv3x3_weight_wino",
     "mvbev_wino_rows_bytes",
@@ -73,6 +70,7 @@ EXPORTS = (
     "mvbev_conv3x3_wino_bf16x3",
     "mvbev_warp_views_wino_rows",
     "mvbev_warp_views_upsampled_wino_rows",
+    "mvbev_warp_nonfinite_views",
 )
 WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
 TILES_GRID, TILES_EDGE_STRIP = 0, 1  # MVBEV_TILES_*
@@ -186,10 +184,10 @@ def _declare(lib):
     lib.mvbev_warp_tile_mask.restype = ctypes.c_int
     lib.mvbev_warp_tile_mask.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
                                          _i64, _i64, _i64, _i64, _p, _p]
+    lib.mvbev_warp_nonfinite_views.restype = ctypes.c_int
+    lib.mvbev_warp_nonfinite_views.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _p, _p]
     lib.mvbev_threshold_points.restype = ctypes.c_int
     lib.mvbev_threshold_points.argtypes = [_p, _i64, _i64, ctypes.c_float, _p, _p, _p, _i64, _p]
-    lib.mvbev_point_nms.restype = ctypes.c_int
-    lib.mvbev_point_nms.argtypes = [_p, _p, _i64, ctypes.c_float, _i64, _p, _p, _p]
     lib.mvbev_point_nms_workspace_bytes.restype = ctypes.c_size_t
     lib.mvbev_point_nms_workspace_bytes.argtypes = [_i64, _i64]
     lib.mvbev_point_nms_ws.restype = ctypes.c_int
@@ -222,14 +220,6 @@ def _declare(lib):
     lib.mvbev_split_rows_bf16.argtypes = [_p, _i64, _i64, _p, _p]
     lib.mvbev_conv_schedule_slot_bytes.restype = ctypes.c_size_t
     lib.mvbev_conv_schedule_slot_bytes.argtypes = []
-    lib.mvbev_conv3x3_bf16x3_sched.restype = ctypes.c_int
-    lib.mvbev_conv3x3_bf16x3_sched.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64,
-                                               ctypes.c_int, ctypes.c_int, _p, ctypes.c_int, _p,
-                                               ctypes.POINTER(ConvSchedule), _p]
-    lib.mvbev_conv3x3_bf16x3_sched3.restype = ctypes.c_int
-    lib.mvbev_conv3x3_bf16x3_sched3.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64,
-                                                ctypes.c_int, ctypes.c_int, _p, ctypes.c_int, _p, ctypes.c_int,
-                                                ctypes.POINTER(ConvSchedule), _p]
     lib.mvbev_conv3x3_dgrad_bf16x3_sched.restype = ctypes.c_int
     lib.mvbev_conv3x3_dgrad_bf16x3_sched.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _i64,
                                                      ctypes.c_int, _p, ctypes.c_int, _p, _i64,

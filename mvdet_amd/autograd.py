@@ -55,10 +55,16 @@ def _train_workspace(engine: ProjectFuse, B: int, device) -> Workspace:
         # Split slabs come from a per-engine pool: zero-filled once, written only by this engine's
         # warps, whose skipped (out-of-source) pixels are the same every step (geometry-only), so
         # a reused slab still holds exact zeros there and the warp may skip them
-        # (MVBEV_WARP_DST_ZEROED).  A slab returns to the pool when its backward has run.
+        # (MVBEV_WARP_DST_ZEROED).  A slab returns to the pool when its backward has been enqueued,
+        # with an event after its last reader: the next forward's stream waits on it, so a forward
+        # on another stream than the backward cannot overwrite the slab under the wgrad kernels.
         pool = _slab_pool(engine, B, device)
-        slab = pool.pop() if pool else torch.zeros((engine.S,) + ops.split_shape(B, engine.Cs, H, W),
-                                                   dtype=torch.bfloat16, device=device)
+        if pool:
+            slab, done = pool.pop()
+            torch.cuda.current_stream(device).wait_event(done)
+        else:
+            slab = torch.zeros((engine.S,) + ops.split_shape(B, engine.Cs, H, W), dtype=torch.bfloat16,
+                               device=device)
         zeroed = True
     else:
         slab = torch.empty((engine.S, B, engine.Cs, H, W), dtype=engine.slab_dtype, device=device)
@@ -259,8 +265,10 @@ class ProjectFuseFunction(torch.autograd.Function):
             ops.warp_views_adjoint(douts, plans, gs)
             grads = [g if need[v] else None for v, g in enumerate(gs)]
         _mark("bwd_end")
-        if ws.slab_zeroed:  # kernels that read it are already enqueued: same-stream reuse is ordered
-            _slab_pool(engine, B, dev).append(ws.slab)
+        if ws.slab_zeroed:  # its readers are enqueued: reusable once this stream passes this point
+            done = torch.cuda.Event()
+            done.record(torch.cuda.current_stream(dev))
+            _slab_pool(engine, B, dev).append((ws.slab, done))
         ctx.ws = None
         return (None, None, *grads, dw1, db1, dw2, db2, dw3)
 

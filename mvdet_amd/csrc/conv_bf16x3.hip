@@ -1926,28 +1926,6 @@ int mvbev_cout1_reduce_partials(const void* partials, const mvbev_conv_desc* des
 
 size_t mvbev_conv_schedule_slot_bytes(void) { return sizeof(mvbev::b3::floatx4) * mvbev::b3::kRingSlotF4; }
 
-int mvbev_conv3x3_bf16x3_sched3(const void* x, int x_layout, const mvbev_conv_desc* desc, const void* w_packed,
-                                const float* bias, const float* init, int64_t Cout, int dilation, int relu, void* y,
-                                int y_layout, const uint32_t* group_mask, int tile_space,
-                                const mvbev_conv_schedule* sched, void* stream) {
-  using namespace mvbev::b3;
-  if (!sched) return MVBEV_ERR_NULL;
-  if (x_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;  // the ring kernel's input
-  return launch<SplitIn>(x, desc, w_packed, bias, init, Cout, dilation, relu, static_cast<float*>(y), y_layout,
-                         group_mask, nullptr, nullptr, 0, stream, nullptr, 1, nullptr, nullptr, sched, tile_space);
-}
-
-int mvbev_conv3x3_bf16x3_sched(const void* x, int x_layout, const mvbev_conv_desc* desc, const void* w_packed,
-                               const float* bias, const float* init, int64_t Cout, int dilation, int relu, void* y,
-                               int y_layout, const uint32_t* group_mask, const mvbev_conv_schedule* sched,
-                               void* stream) {
-  using namespace mvbev::b3;
-  if (!sched) return MVBEV_ERR_NULL;
-  if (x_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;  // the ring kernel's input
-  return launch<SplitIn>(x, desc, w_packed, bias, init, Cout, dilation, relu, static_cast<float*>(y), y_layout,
-                         group_mask, nullptr, nullptr, 0, stream, nullptr, 1, nullptr, nullptr, sched);
-}
-
 int mvbev_conv3x3_dgrad_bf16x3_sched(const void* dy, int dy_layout, const mvbev_conv_desc* desc,
                                      const void* w_packed, int64_t Cout_p, int dilation, void* dx, int dx_layout,
                                      const uint32_t* out_mask, int64_t cot_per_group,

@@ -355,6 +355,28 @@ __global__ void tile_mask_kernel(WarpArgs a, int row0, int rows, int tile_h, int
   if (threadIdx.x == 0) mask[tile] = bits;
 }
 
+// bit s of *bits: some output pixel of view s has non-finite warp coordinates (NaN output).
+// One workgroup (run once per geometry), LDS reduction, one plain store.
+__global__ void nonfinite_views_kernel(WarpArgs a, uint32_t* bits) {
+  __shared__ uint32_t blk;
+  if (threadIdx.x == 0) blk = 0;
+  __syncthreads();
+  uint32_t mine = 0;
+  const int npix = a.Ho * a.Wo;
+  for (int p = threadIdx.x; p < npix; p += blockDim.x) {
+    const int v = p / a.Wo, u = p - v * a.Wo;
+    for (int s = 0; s < a.nviews; ++s) {
+      float m[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) m[i] = a.v[s].m[i];
+      if (!warp_coord(m, u, v, a.Ho, a.Wo, a.H, a.W).finite) mine |= 1u << s;
+    }
+  }
+  if (mine) atomicOr(&blk, mine);
+  __syncthreads();
+  if (threadIdx.x == 0) *bits = blk;
+}
+
 // coord_map (persp_trans_detector.py:103-112): grid / (n-1) * 2 - 1 in float64, then .float()
 __global__ void coord_map_kernel(float* dst, int64_t dB, int64_t dC, int64_t dH, int Ho, int Wo) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -383,7 +405,7 @@ const char* mvbev_status_string(int s) {
   }
 }
 
-int mvbev_version(void) { return 11300; }
+int mvbev_version(void) { return 11400; }
 
 int mvbev_warp_perspective_f32(const float* src, int64_t B, int64_t C, int64_t H, int64_t W,
                                const int64_t src_strides[4], const float* m, float* dst,
@@ -485,6 +507,22 @@ int mvbev_warp_tile_mask(const mvbev_warp_view* views, int nviews, int64_t H, in
   if (tiles > INT32_MAX) return MVBEV_ERR_SHAPE;
   hipLaunchKernelGGL(tile_mask_kernel, dim3((unsigned)tiles), dim3(256), 0, as_stream(stream), a,
                      (int)row0, (int)rows, (int)tile_h, (int)tile_w, (int)halo, tiles_x, mask);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+int mvbev_warp_nonfinite_views(const mvbev_warp_view* views, int nviews, int64_t H, int64_t W, int64_t Ho,
+                               int64_t Wo, uint32_t* bits, void* stream) {
+  using namespace mvbev;
+  if (!views || !bits) return MVBEV_ERR_NULL;
+  if (nviews <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0) return MVBEV_ERR_RANK;
+  if (nviews > kWarpMaxViews || Ho * Wo > INT32_MAX) return MVBEV_ERR_SHAPE;
+  WarpArgs a = {};
+  for (int i = 0; i < nviews; ++i)
+    for (int k = 0; k < 9; ++k) a.v[i].m[k] = views[i].m[k];
+  a.nviews = nviews;
+  a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
+  hipLaunchKernelGGL(nonfinite_views_kernel, dim3(1), dim3(1024), 0, as_stream(stream), a, bits);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }

@@ -341,6 +341,26 @@ def warp_tile_mask(m_norms, src_hw, grid_hw, row0: int, rows: int, halo: int, de
     return mask
 
 
+def warp_nonfinite_views(m_norms, src_hw, grid_hw, device) -> int:
+    """``mvbev_warp_nonfinite_views``: bit s set when slot s's warp (host [3,3] kornia matrix
+    ``m_norms[s]``, None = empty slot) has an output pixel with non-finite sample coordinates
+    (a NaN output).  Geometry only; one small launch and one 4-byte copy to the host."""
+    n = len(m_norms)
+    if not 0 < n <= 16:
+        raise ValueError("need 1..16 slots")
+    arr = (_native.WarpView * n)()
+    for i, m in enumerate(m_norms):
+        mm = [0.0, 0.0, 1e6, 0.0, 0.0, 1e6, 0.0, 0.0, 1.0] if m is None else \
+            torch.as_tensor(m, dtype=torch.float32).reshape(9).tolist()
+        arr[i].m = (ctypes.c_float * 9)(*mm)
+    H, W = src_hw
+    Ho, Wo = grid_hw
+    bits = torch.zeros(1, dtype=torch.int32, device=device)
+    st = _native.load().mvbev_warp_nonfinite_views(arr, n, H, W, Ho, Wo, bits.data_ptr(), _stream(bits))
+    _native.check(st, "mvbev_warp_nonfinite_views")
+    return int(bits.item()) & 0xFFFFFFFF
+
+
 def ring_tile_mask(m_norms, src_hw, grid_hw, row0: int, rows: int, device, space: int) -> Optional[torch.Tensor]:
     """Frustum mask (halo 1) of a dilation-1 ring conv's pixel tiles in tile space ``space``
     (``_native.TILES_*``) over grid rows [row0, row0+rows): the regular 12 x 32 tiles of the
@@ -378,14 +398,12 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
                  init: Optional[torch.Tensor] = None, dilation: int = 1, relu: bool = False,
                  out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
                  group_mask: Optional[torch.Tensor] = None, tile_order: Optional[torch.Tensor] = None,
-                 sched=None, tile_space: int = _native.TILES_GRID) -> torch.Tensor:
+                 tile_space: int = _native.TILES_GRID) -> torch.Tensor:
     """Low-level form: ``x`` addressed through ``desc`` (``mvbev_conv_desc``).  bf16x3 only,
     optional: ``workspace`` — device scratch for the split-K tail
     (``conv3x3_workspace_bytes``); ``group_mask`` — per-tile active channel groups
     (``warp_tile_mask``), whose cleared groups are skipped; ``tile_order`` — with a mask,
-    the B x tiles pixel tiles in run order (``heavy_first_order``); ``sched`` — a ring-kernel
-    schedule (``schedule.plan`` over ``schedule.ring_blocks``; split-bf16 x) replacing the
-    order; ``tile_space`` — ``_native.TILES_EDGE_STRIP``: the ring kernel's edge-strip tiles
+    the B x tiles pixel tiles in run order (``heavy_first_order``); ``tile_space`` — ``_native.TILES_EDGE_STRIP``: the ring kernel's edge-strip tiles
     (``mvbev_conv3x3_bf16x3_ex3``; the mask and order then index that space, ``ring_tile_mask``)."""
     _require_cuda(x, packed)
     bf16x3 = packed.dtype == torch.bfloat16
@@ -446,20 +464,6 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
             if group_mask is None or tile_order.dtype != torch.int32 or tile_order.numel() != B * tiles:
                 raise ValueError("tile_order must be an int32 permutation of the B x tiles pixel tiles")
             top = tile_order.data_ptr()
-        if sched is not None and tile_space != _native.TILES_GRID:
-            st = lib.mvbev_conv3x3_bf16x3_sched3(x.data_ptr(), layout, ctypes.byref(desc), packed.data_ptr(), bp, ip,
-                                                 cout, int(dilation), int(bool(relu)), out.data_ptr(),
-                                                 _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32, gmp,
-                                                 int(tile_space), ctypes.byref(sched.c), _stream(x))
-            _native.check(st, "mvbev_conv3x3_bf16x3_sched3")
-            return out
-        if sched is not None:
-            st = lib.mvbev_conv3x3_bf16x3_sched(x.data_ptr(), layout, ctypes.byref(desc), packed.data_ptr(), bp, ip,
-                                                cout, int(dilation), int(bool(relu)), out.data_ptr(),
-                                                _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32, gmp,
-                                                ctypes.byref(sched.c), _stream(x))
-            _native.check(st, "mvbev_conv3x3_bf16x3_sched")
-            return out
         if tile_space != _native.TILES_GRID:
             st = lib.mvbev_conv3x3_bf16x3_ex3(x.data_ptr(), layout, ctypes.byref(desc), packed.data_ptr(), bp, ip,
                                               cout, int(dilation), int(bool(relu)), out.data_ptr(),

@@ -67,6 +67,9 @@ class Workspace:
     wino_t: Optional[torch.Tensor] = None
     # wino_t holds the current frame's transform, written by the fused warp (the slab was not)
     t_from_warp: bool = False
+    # grid rows the slab holds: (0, Ho) for a warped slab; a row window for a band-local slab
+    # filled by the multi-GPU band exchange (parallel.ViewBands)
+    slab_rows: Tuple[int, int] = (0, 0)
 
 
 class ProjectFuse:
@@ -80,8 +83,7 @@ class ProjectFuse:
                  channels: int, mid_channels: int = 512, slot_views: Optional[Sequence[Optional[int]]] = None,
                  precision: str = "bf16x3", slab_dtype: torch.dtype = torch.float32,
                  all_views: bool = True, split_k: bool = True, frustum: bool = True, fuse_conv3: bool = True,
-                 edge_strip: bool = True, level_conv1: bool = False, wino_conv1: bool = False,
-                 wino_warp: bool = True):
+                 edge_strip: bool = True, wino_conv1: bool = True, wino_warp: bool = True):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":
@@ -138,17 +140,16 @@ class ProjectFuse:
         # leaves a partial last tile column (W % 32 in 1..16: Wildtrack's 360 = 11 x 32 + 8), so
         # no MFMA column is spent past W (mvbev_conv3x3_bf16x3_ex3); bitwise the same y1
         self.edge_strip = edge_strip
-        # level_conv1: the forward conv1 runs a leveling schedule (schedule.plan_level: first
-        # round whole, later blocks cut so every CU ends near one level; pieces summed in K
-        # order).  Off by default: measured 7-10 % slower at cfg2 — the chip is power-limited
-        # under this MFMA load, so the CUs still busy in the hardware dispatch's ragged tail run
-        # faster (fewer chunks in flight, higher clock) and the idle CU-time costs far less than
-        # its share
-        self.level_conv1 = level_conv1
-        # wino_conv1: the inference conv1 as F(3,3) row-Winograd (ops.wino_rows + conv3x3_wino: 5
-        # instead of 9 MFMA K-blocks per chunk and kernel column, over the 12 x 32 grid tiles);
-        # split-bf16 slab only, not in training (its backward reads the direct form's operands)
+        # wino_conv1 (default): the inference conv1 as F(3,3) row-Winograd (ops.wino_rows +
+        # conv3x3_wino: 5 instead of 9 MFMA K-blocks per chunk and kernel column, over the 12 x 32
+        # grid tiles); split-bf16 slab only, not in training (its backward reads the direct form's
+        # operands).  B^T mixes a 3-row tile's input rows, so a non-finite warp sample (a degenerate
+        # homography: kornia's NaN output) would spread over its tile where the reference's direct
+        # conv keeps it to the taps that read it: geometry that can produce a non-finite sample
+        # (``nonfinite_views``, the warp kernels' own coordinate code) runs the direct conv1
+        # instead (``wino_active``), so the NaN pattern stays the reference's.
         self.wino_conv1 = wino_conv1 and self.split
+        self._nonfinite: Dict[str, int] = {}
         self.pack1w = ops.PackedConv3x3(chan_map, "bf16x3", wino=True) if self.wino_conv1 else None
         # wino_warp: warp_views writes the row transform T directly (one pass, no slab, no
         # separate transform); inference over the whole grid from fp32 features only (cfg2:
@@ -156,19 +157,28 @@ class ProjectFuse:
         self.wino_warp = self.wino_conv1 and wino_warp
 
     # -- buffers ----------------------------------------------------------------------------
-    def workspace(self, B: int, device, band: Optional[Tuple[int, int]] = None) -> Workspace:
+    def workspace(self, B: int, device, band: Optional[Tuple[int, int]] = None,
+                  slab_rows: Optional[Tuple[int, int]] = None, tag: int = 0) -> Workspace:
+        """Buffers for output rows ``band`` (default: the whole grid).  ``slab_rows``: a slab
+        holding only grid rows [r0, r1) (must cover conv1's input rows for the band) — the
+        band-local slab the multi-GPU band exchange fills; warps refuse it.  ``tag`` keeps
+        several workspaces of one shape apart (double buffering)."""
         device = torch.device(device)
         H, W = self.grid_hw
         band = (0, H) if band is None else (int(band[0]), int(band[1]))
-        key = (str(device), int(B), band)
+        slab_rows = (0, H) if slab_rows is None else (int(slab_rows[0]), int(slab_rows[1]))
+        key = (str(device), int(B), band, slab_rows, int(tag))
         ws = self._ws.get(key)
         if ws is None:
+            y1r, y2r = band_rows(band[0], band[1], H)
+            if not (0 <= slab_rows[0] <= max(0, y1r[0] - HALO_CONV1) and min(H, y1r[1] + HALO_CONV1) <= slab_rows[1] <= H):
+                raise ValueError(f"slab rows {slab_rows} do not cover conv1's input rows for output band {band}")
+            R = slab_rows[1] - slab_rows[0]
             if self.split:
-                slab = torch.zeros((self.S,) + ops.split_shape(B, self.Cs, H, W), dtype=torch.bfloat16,
+                slab = torch.zeros((self.S,) + ops.split_shape(B, self.Cs, R, W), dtype=torch.bfloat16,
                                    device=device)
             else:
-                slab = torch.zeros((self.S, B, self.Cs, H, W), dtype=self.slab_dtype, device=device)
-            y1r, y2r = band_rows(band[0], band[1], H)
+                slab = torch.zeros((self.S, B, self.Cs, R, W), dtype=self.slab_dtype, device=device)
             if self.y1_split:
                 y1 = torch.empty(ops.split_shape(B, self.mid, y1r[1] - y1r[0], W), dtype=torch.bfloat16,
                                  device=device)
@@ -176,7 +186,7 @@ class ProjectFuse:
                 y1 = torch.empty((B, self.mid, y1r[1] - y1r[0], W), dtype=torch.float32, device=device)
             y2 = torch.empty((B, self.mid, y2r[1] - y2r[0], W), dtype=torch.float32, device=device)
             m = self.m_norm_cpu.to(device)[:, None].expand(self.num_cam, B, 3, 3).contiguous()
-            ws = Workspace(slab, y1, y2, m, band, y1r, y2r, slab_zeroed=True)
+            ws = Workspace(slab, y1, y2, m, band, y1r, y2r, slab_zeroed=True, slab_rows=slab_rows)
             self._ws[key] = ws
         return ws
 
@@ -200,21 +210,59 @@ class ProjectFuse:
 
     # -- a5 -------------------------------------------------------------------------------
     def warp_view(self, ws: Workspace, cam: int, feat: torch.Tensor) -> None:
-        """a5 (+ zero-copy a6): warp one view's [B,C,h,w] features into its slab slot."""
+        """a5 (+ zero-copy a6): warp one view's [B,C,h,w] features into its slab slot.  Not
+        after a fused warp (``wino_warp``) of the same workspace: that wrote conv1's row transform,
+        not the slab, so the slab's other slots would hold an older frame."""
         if tuple(feat.shape[2:]) != self.src_hw or feat.shape[1] != self.C:
             raise ValueError(f"view {cam}: features {tuple(feat.shape)} do not match "
                              f"[B,{self.C},{self.src_hw[0]},{self.src_hw[1]}]")
-        ws.t_from_warp = False
+        self._check_warp_ws(ws)
+        if ws.t_from_warp:
+            raise RuntimeError("warp_view after a fused warp_views (wino_warp): the slab does not hold the "
+                               "other views of this frame; warp every view with warp_views, or use "
+                               "wino_warp=False to warp views one at a time")
         if self.split:
             ops.warp_views_into([feat], [self.m_norm_cpu[cam]], [self._slot_dst(ws, cam)], split=True,
                                 dst_zeroed=ws.slab_zeroed)
         else:
             ops.warp_into(feat, ws.m_norm[cam], self._slot_dst(ws, cam))
 
+    def nonfinite_views(self, device) -> int:
+        """Bit s set when slot s's warp has an output pixel with non-finite sample coordinates
+        (a NaN in the warped features, e.g. a degenerate homography or a 1-pixel grid side:
+        ``mvbev_warp_nonfinite_views``, the warp kernels' own fp32 coordinate code); cached per
+        device (geometry only)."""
+        key = str(torch.device(device))
+        bits = self._nonfinite.get(key)
+        if bits is None:
+            ms = [None if v is None else self.m_norm_cpu[v] for v in self.slot_views]
+            bits = ops.warp_nonfinite_views(ms, self.src_hw, self.grid_hw, device)
+            self._nonfinite[key] = bits
+        return bits
+
+    def wino_active(self, device) -> bool:
+        """The row-Winograd conv1 runs on ``device``: requested (``wino_conv1``) and no view's
+        geometry can produce a non-finite warp sample (else the direct conv1 keeps the
+        reference's NaN pattern)."""
+        return self.wino_conv1 and self.nonfinite_views(device) == 0
+
     def _wino_warp_applies(self, ws: Workspace, feats) -> bool:
         H = self.grid_hw[0]
         return (self.wino_warp and not ws.store_y2 and ws.y1_rows == (0, H) and ws.slab_zeroed
-                and all(f.dtype == torch.float32 for f in feats) and self.src_hw[1] >= 2)
+                and all(f.dtype == torch.float32 for f in feats) and self.src_hw[1] >= 2
+                and self.wino_active(ws.slab.device))
+
+    def _check_warp_ws(self, ws: Workspace) -> None:
+        if ws.slab_rows != (0, self.grid_hw[0]):
+            raise ValueError("a band-local slab (slab_rows) is filled by the band exchange, not by a warp")
+
+    def _slab_after_t(self, ws: Workspace, cams) -> None:
+        """A slab warp is about to run: after a fused warp (which wrote T, not the slab) only a
+        warp of every view leaves the slab holding one frame."""
+        if ws.t_from_warp and set(cams) != set(self.slot_of):
+            raise RuntimeError("a slab warp of a subset of the views after a fused warp_views (wino_warp): the "
+                               "slab's other slots hold an older frame; warp every view")
+        ws.t_from_warp = False
 
     def _warp_views_t(self, ws: Workspace, cams, feats, up_hw=None) -> None:
         """The warp writing conv1's row transform T (``ops.warp_views_wino_rows_into``)."""
@@ -236,10 +284,11 @@ class ProjectFuse:
             if tuple(f.shape[2:]) != self.src_hw or f.shape[1] != self.C:
                 raise ValueError(f"view {cam}: features {tuple(f.shape)} do not match "
                                  f"[B,{self.C},{self.src_hw[0]},{self.src_hw[1]}]")
+        self._check_warp_ws(ws)
         if self._wino_warp_applies(ws, feats):
             self._warp_views_t(ws, cams, feats)
             return
-        ws.t_from_warp = False
+        self._slab_after_t(ws, cams)
         ops.warp_views_into(list(feats), [self.m_norm_cpu[c] for c in cams],
                             [self._slot_dst(ws, c) for c in cams], split=self.split,
                             dst_zeroed=self.split and ws.slab_zeroed)
@@ -251,10 +300,11 @@ class ProjectFuse:
         for cam, f in zip(cams, feats):
             if f.shape[1] != self.C or f.shape[2] > self.src_hw[0] or f.shape[3] > self.src_hw[1]:
                 raise ValueError(f"view {cam}: features {tuple(f.shape)} cannot upsample to {self.src_hw}")
+        self._check_warp_ws(ws)
         if self._wino_warp_applies(ws, feats) and all(f.shape[3] >= 4 and f.stride(3) == 1 for f in feats):
             self._warp_views_t(ws, cams, feats, up_hw=self.src_hw)  # a4 + a5 + a6 + conv1's B^T in one pass
             return
-        ws.t_from_warp = False
+        self._slab_after_t(ws, cams)
         ops.warp_views_upsampled_into(list(feats), self.src_hw, [self.m_norm_cpu[c] for c in cams],
                                       [self._slot_dst(ws, c) for c in cams], split=self.split,
                                       dst_zeroed=self.split and ws.slab_zeroed)
@@ -339,52 +389,6 @@ class ProjectFuse:
             self._masks[key] = o
         return o
 
-    def conv1_schedule(self, device, row0: int, rows: int, B: int, split: bool = True):
-        """A ring-kernel schedule of conv1 over rows [row0, row0+rows) (split-bf16 slab,
-        frustum mask): ``schedule.plan`` over the heavy-first blocks, pixel tiles dealt to the
-        XCDs as the unscheduled kernel does; cached.  Not used by default: measured within
-        ±1 % of the unscheduled launch at cfg2 (the masked forward's imbalance comes from its
-        heavy blocks, which a tail cut does not reach; ``tools/kbench.py --only conv1,conv1s``)."""
-        key = ("sched", str(device), row0, rows, B, split)
-        sc = self._masks.get(key)
-        if sc is None:
-            from . import schedule
-            m = self.conv1_mask(device, row0, rows)
-            if m is None or not self.split:
-                return None
-            th = self.conv1_tile_rows()
-            ty, tx = -(-rows // th), -(-self.grid_hw[1] // _native.TILE_W)
-            blocks = schedule.ring_blocks(B, ty, tx, self.mid // ops.BN, 0, group_mask=m.cpu().tolist(),
-                                          cpg=self.Cs // (2 * ops.KC),
-                                          order=self.conv1_order(device, row0, rows, B, grid=True).cpu().tolist())
-            cus = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
-            sc = schedule.plan(blocks, cus, device, split=split, deal=self.mid // ops.BN)
-            self._masks[key] = sc
-        return sc
-
-    def conv1_level_schedule(self, device, row0: int, rows: int, B: int):
-        """The forward conv1's leveling schedule (``schedule.plan_level``) over its tile space
-        (``conv1_fwd_mask``); cached per geometry.  None without a frustum mask."""
-        key = ("level", str(device), row0, rows, B)
-        sc = self._masks.get(key)
-        if sc is None:
-            from . import schedule
-            m, space = self.conv1_fwd_mask(device, row0, rows)
-            if m is None or not self.split:
-                return None
-            W = self.grid_hw[1]
-            d = ops.conv_desc(1, 8, self.grid_hw[0], W, group=8, group_stride=0, batch_stride=0, in_row0=row0,
-                              in_rows=rows, out_row0=row0, out_rows=rows)
-            tiles_x, tiles_y, edge_tiles = _native.ring_tile_space(d, space)[:3]
-            n_cot = self.mid // ops.BN
-            blocks = schedule.ring_blocks(B, 1, tiles_x * tiles_y + edge_tiles, n_cot, 0,
-                                          group_mask=m.cpu().tolist(), cpg=self.Cs // (2 * ops.KC),
-                                          order=self.conv1_order(device, row0, rows, B).cpu().tolist())
-            cus = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
-            sc = schedule.plan_level(blocks, cus, device, n_cot)
-            self._masks[key] = sc
-        return sc
-
     def conv1_active_fraction(self, device, row0: int, rows: int, grid: bool = False) -> float:
         """Fraction of conv1's dense (pixel, slot) work the forward's frustum mask keeps (1.0 =
         dense): per tile its enabled slots x its pixels inside the grid.  ``grid``: over the
@@ -404,30 +408,30 @@ class ProjectFuse:
         return sum(b * p for b, p in zip(bits, pix)) / (rows * W * self.S)
 
     # -- a7-a9 ----------------------------------------------------------------------------
-    def conv1(self, ws: Workspace, conv1: torch.nn.Conv2d, sched=None, mark=None) -> torch.Tensor:
-        """a7: y1 = relu(conv3x3(slab) + coord_term) on y1's rows (fp32 MFMA)."""
+    def conv1(self, ws: Workspace, conv1: torch.nn.Conv2d, mark=None) -> torch.Tensor:
+        """a7: y1 = relu(conv3x3(slab) + coord_term) on y1's rows (row-Winograd where
+        ``wino_active`` and inference, else the direct ring conv)."""
         if conv1.weight.shape[1] != self.cin:
             raise ValueError(f"conv1 has {conv1.weight.shape[1]} input channels, expected {self.cin}")
         H, W = self.grid_hw
         B = ws.slab.shape[1]
         init = self.coord_term(conv1)
-        p1 = self.pack1.get(conv1.weight)
         a1, b1 = ws.y1_rows
-        d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * H * W,
-                           batch_stride=self.Cs * H * W, in_row0=0, in_rows=H, out_row0=a1, out_rows=b1 - a1)
-        if self.wino_conv1 and sched is None and not ws.store_y2 and not self.level_conv1:
+        s0, s1 = ws.slab_rows
+        R = s1 - s0
+        d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * R * W,
+                           batch_stride=self.Cs * R * W, in_row0=s0, in_rows=R, out_row0=a1, out_rows=b1 - a1)
+        if not ws.store_y2 and self.wino_active(ws.slab.device):
             return self.conv1_wino(ws, conv1, d1, init, mark=mark)
-        if sched is not None:  # an explicit schedule (conv1_schedule) is planned over the 12 x 32 grid
-            gm, space = self.conv1_mask(ws.slab.device, a1, b1 - a1), _native.TILES_GRID
-        else:
-            gm, space = self.conv1_fwd_mask(ws.slab.device, a1, b1 - a1)
-            if self.level_conv1 and gm is not None:
-                sched = self.conv1_level_schedule(ws.slab.device, a1, b1 - a1, B)
+        if ws.t_from_warp:
+            raise RuntimeError("the direct conv1 reads the slab, but the fused warp wrote conv1's row transform")
+        p1 = self.pack1.get(conv1.weight)
+        gm, space = self.conv1_fwd_mask(ws.slab.device, a1, b1 - a1)
         return ops.conv3x3_desc(ws.slab, d1, p1, self.mid, bias=None, init=init, dilation=1, relu=True,
                                 out=ws.y1, workspace=None if gm is not None else self._sk_ws(d1, ws.slab.device),
                                 group_mask=gm, tile_order=self.conv1_order(ws.slab.device, a1, b1 - a1, B,
                                                                            grid=space == _native.TILES_GRID),
-                                sched=sched, tile_space=space)
+                                tile_space=space)
 
     def _conv1_desc(self, B: int, rows: Optional[Tuple[int, int]] = None):
         H, W = self.grid_hw
@@ -504,6 +508,8 @@ class ProjectFuse:
         """conv1 restricted to this slab's views (its slice of conv1's input channels), all
         grid rows, no bias / coord term / ReLU: one rank's term of conv1's channel sum.
         ``out``: contiguous [B, 512, Ho, Wo] fp32."""
+        if ws.t_from_warp:
+            raise RuntimeError("conv1_partial reads the slab, but the fused warp wrote conv1's row transform")
         H, W = self.grid_hw
         B = ws.slab.shape[1]
         p1 = self.pack1.get(map_classifier[0].weight)

@@ -5,8 +5,9 @@ Drop-ins for the CPU loop of ``multiview_detector/trainer.py:97-106,148-157`` an
 HIP kernels of ``libmvbev.so`` (``mvbev_threshold_points``, ``mvbev_point_nms_ws``):
 
 * ``nms(points, scores, dist_thres=50/2.5, top_k=50) -> (keep, count)``: greedy point NMS.
-  Returns ``keep`` alone for empty input, like the reference.  Equal scores are taken larger
-  index first (torch's CPU sort leaves their order unspecified).
+  Returns ``keep`` alone for empty input, like the reference.  Equal scores are taken in the
+  order torch's CPU ``scores.sort(0)`` leaves them (the kernel replays its introsort), so the
+  kept set matches the reference's exactly, ties included.
 * ``threshold_rows(map_res, frame, cls_thres, grid_reduce, indexing)``: the (frame, x, y,
   score) rows of ``map_res > cls_thres`` in ``nonzero`` order.
 * ``frame_results(rows, dist_thres=20, top_k=inf)``: per-frame NMS -> (frame, x, y) rows.
@@ -39,8 +40,7 @@ def nms(points: torch.Tensor, scores: torch.Tensor, dist_thres=50 / 2.5, top_k=5
     out = torch.empty(K, dtype=torch.int64, device=sc.device)
     cnt = torch.empty(1, dtype=torch.int32, device=sc.device)
     lib = _native.load()
-    # any K (nms.py accepts any; trainer.py:154 hands it every map cell over cls_thres):
-    # above the one-workgroup LDS sort the kernel needs a device workspace
+    # any K (nms.py accepts any; trainer.py:154 hands it every map cell over cls_thres)
     nws = int(lib.mvbev_point_nms_workspace_bytes(K, max(k, 1)))
     ws = torch.empty(max(nws, 4), dtype=torch.uint8, device=sc.device)
     st = lib.mvbev_point_nms_ws(pts.data_ptr(), sc.data_ptr(), K, float(dist_thres), max(k, 1),

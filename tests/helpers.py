@@ -51,3 +51,36 @@ def assert_parity(got, ref, what="", normwise_tol=1e-3):
     s = parity_stats(got, ref)
     assert s["n_bad"] == 0 and s["normwise"] <= normwise_tol, f"{what}: parity failed {s}"
     return s
+
+
+def parity_stats_t(got: torch.Tensor, ref: torch.Tensor, chunk: int = 1 << 26):
+    """``parity_stats`` on torch tensors where they live (e.g. the GPU: full-size configs hold
+    GB-sized tensors), in float64 chunks; the same gate and NaN/inf rule."""
+    assert tuple(got.shape) == tuple(ref.shape), (tuple(got.shape), tuple(ref.shape))
+    g, r = got.reshape(-1), ref.reshape(-1).to(got.device)
+    scale = 0.0
+    for i in range(0, r.numel(), chunk):
+        rc = r[i:i + chunk].double()
+        gc = g[i:i + chunk].double()
+        assert torch.equal(~torch.isfinite(gc), ~torch.isfinite(rc)), "non-finite pattern differs"
+        assert torch.equal(torch.isnan(gc), torch.isnan(rc)), "NaN pattern differs"
+        fin = torch.isfinite(rc)
+        if fin.any():
+            scale = max(scale, rc[fin].abs().max().item())
+    n_bad, dmax = 0, 0.0
+    for i in range(0, r.numel(), chunk):
+        rc = r[i:i + chunk].double()
+        gc = g[i:i + chunk].double()
+        fin = torch.isfinite(rc)
+        d = (gc[fin] - rc[fin]).abs()
+        if d.numel():
+            dmax = max(dmax, d.max().item())
+            n_bad += int((d > RTOL * rc[fin].abs() + ATOL_FRAC * scale).sum().item())
+    normwise = dmax / scale if scale > 0 else dmax
+    return dict(normwise=normwise, n_bad=n_bad, max_abs=dmax, scale=scale)
+
+
+def assert_parity_t(got, ref, what="", normwise_tol=1e-3):
+    s = parity_stats_t(got, ref)
+    assert s["n_bad"] == 0 and s["normwise"] <= normwise_tol, f"{what}: parity failed {s}"
+    return s

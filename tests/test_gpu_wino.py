@@ -157,8 +157,8 @@ def test_engine_wino_conv1_matches_direct(cfg):
     mc = torch.nn.Sequential(torch.nn.Conv2d(N * C + 2, 512, 3, padding=1), torch.nn.ReLU(),
                              torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
                              torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False)).to(DEV)
-    direct = ProjectFuse(pm, up, grid, C)
-    wino = ProjectFuse(pm, up, grid, C, wino_conv1=True)
+    direct = ProjectFuse(pm, up, grid, C, wino_conv1=False)
+    wino = ProjectFuse(pm, up, grid, C)  # the default
     assert wino.wino_conv1 and wino.frustum
     with torch.no_grad():
         ref = direct.project_fuse(feats, mc)
@@ -215,9 +215,28 @@ def test_fused_warp_transform_matches_two_pass(cfg):
         two.warp_views_upsampled(wt, list(range(N)), low)
         m2 = two.fuse(wt, mc)
         assert_parity(m1.cpu(), m2.cpu(), "fused upsample + warp + B^T map", normwise_tol=TOL)
-        # a slab-writing warp (one view at a time) switches conv1 back to the slab's transform
+        # after the fused warp the slab holds no frame: a slab warp of a subset of the views is
+        # refused (its other slots would be stale); a slab warp of every view switches conv1 back
+        # to the slab's transform, after which single-view warps are fine again
+        with pytest.raises(RuntimeError):
+            fused.warp_view(wf, 0, feats[0])
+        fused.wino_warp = False
+        with pytest.raises(RuntimeError):
+            fused.warp_views(wf, [0], feats[:1])
+        assert wf.t_from_warp
+        fused.warp_views(wf, list(range(N)), feats)
+        assert not wf.t_from_warp
         for v in range(N):
             fused.warp_view(wf, v, feats[v])
-        assert not wf.t_from_warp
         m3 = fused.fuse(wf, mc)
+        # the direct conv1 and conv1_partial read the slab: refused while T came from the fused warp
+        fused.wino_warp = True
+        fused.warp_views(wf, list(range(N)), feats)
+        assert wf.t_from_warp
+        fused.wino_conv1 = False
+        with pytest.raises(RuntimeError):
+            fused.conv1(wf, mc[0])
+        with pytest.raises(RuntimeError):
+            fused.conv1_partial(wf, mc, torch.empty((B, 512) + grid, device=DEV))
+        fused.wino_conv1 = True
     assert_parity(m3.cpu(), ref.cpu(), "slab path after the fused warp", normwise_tol=TOL)

@@ -156,3 +156,36 @@ def test_postproc_oracle_matches_reference_nms_golden():
         rows = postproc.threshold_rows(torch.from_numpy(g[f"map{j}"])[None, None], 7, 0.4, 4, str(g[f"map{j}_indexing"]))
         np.testing.assert_array_equal(rows.numpy(), g[f"map{j}_rows"])
         np.testing.assert_array_equal(postproc.frame_results(rows).numpy(), g[f"map{j}_final"])
+
+
+def test_sort_order_restatement_matches_torch_cpu_sort():
+    """nms.py:22's ``scores.sort(0)`` on the pinned torch CPU: the restated libstdc++ introsort
+    (sequential and the GPU kernel's level-synchronous form) gives torch's index order exactly,
+    equal scores included: random ties, NaN, sorted / reversed runs, near-constant arrays, and
+    McIlroy killer sequences that reach the heap-sort fallback."""
+    from oracle import postproc
+    rng = np.random.default_rng(11)
+    cases = []
+    for t in range(60):
+        n = int(rng.integers(1, 1500))
+        kind = t % 5
+        if kind == 0:
+            x = rng.integers(0, 5, n).astype(np.float32)
+        elif kind == 1:
+            x = rng.uniform(0.4, 1, n).astype(np.float32)
+            x[rng.integers(0, n, n // 5)] = np.float32(0.75)
+        elif kind == 2:
+            x = np.sort(rng.integers(0, 50, n)).astype(np.float32)
+        elif kind == 3:
+            x = np.sort(rng.integers(0, 50, n))[::-1].astype(np.float32).copy()
+        else:
+            x = np.full(n, 1.0, np.float32)
+            x[rng.integers(0, n, 3)] = 2
+        if t % 7 == 0 and n > 4:
+            x[rng.integers(0, n, 3)] = np.nan
+        cases.append(x)
+    cases += [postproc.killer_sequence(n) for n in (40, 300, 1200)]
+    for x in cases:
+        ref = torch.from_numpy(x).sort(0)[1].tolist()
+        assert postproc.std_sort_order(x) == ref, len(x)
+        assert postproc.level_sort_order(x) == ref, len(x)

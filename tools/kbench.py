@@ -96,7 +96,7 @@ def backward_stages(eng, ws, mc, B, ho, wo, N, C, dev):
 
 
 def _with(eng, flag, value, fn):
-    """Run fn with the engine's boolean option ``flag`` (edge_strip, level_conv1) set to ``value``."""
+    """Run fn with the engine's boolean option ``flag`` (edge_strip, wino_warp) set to ``value``."""
     keep = getattr(eng, flag)
     setattr(eng, flag, value)
     try:
@@ -124,7 +124,8 @@ def main():
     dev = torch.device("cuda:0")
     pm = projection_matrices(ds)
     mc = build_mc(C, N, head_params(N, args.config, C), dev)
-    eng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision, frustum=not args.no_frustum)
+    eng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision, frustum=not args.no_frustum,
+                      wino_conv1=False)  # the direct conv1 stages (the Winograd ones use weng)
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=v, device=dev) for v in range(N)]
     bfeats = [synthetic.backbone_features(B, C, [u // 3 for u in up], seed=v, device=dev) for v in range(N)]
     ws = eng.workspace(B, dev)
@@ -150,12 +151,6 @@ def main():
             "conv1": (lambda: eng.conv1(ws, mc[0]), 2.0 * B * ho * wo * 9 * N * C * 512),
             "conv1g": (lambda: _with(eng, "edge_strip", False, lambda: eng.conv1(ws, mc[0])),
                        2.0 * B * ho * wo * 9 * N * C * 512),  # 12 x 32 grid tiles
-            "conv1l": (lambda: _with(eng, "level_conv1", True, lambda: eng.conv1(ws, mc[0])),
-                       2.0 * B * ho * wo * 9 * N * C * 512),  # leveling schedule (schedule.plan_level)
-            "conv1s": (lambda: eng.conv1(ws, mc[0], sched=eng.conv1_schedule(dev, 0, ho, B)),
-                       2.0 * B * ho * wo * 9 * N * C * 512),  # balanced schedule
-            "conv1p": (lambda: eng.conv1(ws, mc[0], sched=eng.conv1_schedule(dev, 0, ho, B, split=False)),
-                       2.0 * B * ho * wo * 9 * N * C * 512),  # the schedule's XCD shares, no pieces
             # row-Winograd conv1 (ProjectFuse(wino_conv1=True)): transform + conv, and each alone
             "conv1w": (lambda: weng.conv1(wws, mc[0]), 2.0 * B * ho * wo * 9 * N * C * 512),
             "winorows": (lambda: ops.wino_rows(wws.slab, wd1, wws.wino_t, wgm), None),

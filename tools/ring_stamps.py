@@ -30,7 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("lib")
     ap.add_argument("--config", type=int, default=2)
-    ap.add_argument("--stage", default="conv1", choices=["conv1", "conv1l", "conv2", "dgrad1", "dgrad1s"])
+    ap.add_argument("--stage", default="conv1", choices=["conv1", "conv2", "dgrad1", "dgrad1s"])
     args = ap.parse_args()
     spec = synthetic.CONFIGS[args.config]
     ds = spec["make"]()
@@ -41,7 +41,7 @@ def main():
     lib = _native.load(args.lib)
     _native._lib = lib
     mc = build_mc(C, N, head_params(N, args.config, C), dev)
-    eng = ProjectFuse(projection_matrices(ds), up, (ho, wo), C)
+    eng = ProjectFuse(projection_matrices(ds), up, (ho, wo), C, wino_conv1=False)
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=v, device=dev) for v in range(N)]
     ws = eng.workspace(B, dev)
     buf = np.zeros(16384 * 4, dtype=np.uint32)
@@ -52,7 +52,6 @@ def main():
             from tools.kbench import backward_stages
             run = backward_stages(eng, ws, mc, B, ho, wo, N, C, dev)[args.stage][0]
         else:
-            eng.level_conv1 = args.stage == "conv1l"  # conv1l: the leveling schedule (schedule.plan_level)
             run = (lambda: eng.conv1(ws, mc[0])) if args.stage.startswith("conv1") else (lambda: eng.conv2(ws, mc[2]))
         for _ in range(3):
             run()
@@ -82,20 +81,6 @@ def main():
            "cu_last_end_us_p10_p50_p90": [round(float(np.percentile(last, q)), 1) for q in (10, 50, 90)],
            "block_us_p10_p50_p90_max": [round(float(np.percentile(dur, q)), 1) for q in (10, 50, 90)] +
                                        [round(float(dur.max()), 1)]}
-    if args.stage == "conv1l":
-        # leveled schedule: block i ran items[i]; duration vs chunks (whole items and pieces)
-        sch = eng.conv1_level_schedule(dev, 0, ho, B)
-        items = sch.items.cpu().numpy()
-        ok = bid < len(items)
-        it = items[bid[ok]]
-        d = dur[ok]
-        ch = (it[:, 2] - it[:, 1]).astype(np.float64)
-        for name, sel in (("whole", it[:, 3] < 0), ("piece", it[:, 3] >= 0)):
-            if sel.sum() > 2:
-                a, b = np.polyfit(ch[sel], d[sel], 1)
-                out[f"{name}_us_per_chunk"], out[f"{name}_us_fixed"] = round(float(a), 3), round(float(b), 1)
-        # do blocks planned for one CU (XCD x, j-th item of the XCD's sequence) land as simulated?
-        out["predicted_chunks"], out["predicted_plain_chunks"] = sch.predicted, sch.predicted_plain
     print(json.dumps(out))
 
 

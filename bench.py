@@ -55,8 +55,11 @@ def head_params(num_cam, seed, C):
     return out
 
 
-def cpu_baseline(ds, B, C, pm, params, frames: int, config: int = 2):
-    """The oracle (reference CPU path restated over torch-CPU ops) on the host cores."""
+def cpu_baseline(ds, B, C, pm, params, frames: int, config: int = 2, warmups: int = 2, single_frames: int = 3):
+    """The oracle (reference CPU path restated over torch-CPU ops) on the host cores:
+    ``warmups`` untimed frames, then the median of ``frames`` timed ones (2 warm-ups,
+    >= 5 timed, median); the reference's own one-thread setting (main.py:3) as the median of
+    ``single_frames`` after one warm-up (0 = skipped)."""
     from mvdet_amd import synthetic
     from oracle import cpu_path
     threads = len(os.sched_getaffinity(0))
@@ -67,25 +70,33 @@ def cpu_baseline(ds, B, C, pm, params, frames: int, config: int = 2):
              for v in range(ds.num_cam)]
     tp = {k: torch.from_numpy(v) for k, v in params.items()}
     mats = [M.numpy() for M in pm]
+    grid = tuple(ds.reducedgrid_shape)
+
+    def frame(stages=None):
+        t = time.perf_counter()
+        cpu_path.project_fuse(feats, mats, grid, tp, timings=stages)
+        return time.perf_counter() - t
+
     with torch.no_grad():
-        cpu_path.project_fuse(feats, mats, tuple(ds.reducedgrid_shape), tp)  # warm-up
-        t0 = time.perf_counter()
+        for _ in range(warmups):
+            frame()
         stages = {}
-        for _ in range(frames):
-            cpu_path.project_fuse(feats, mats, tuple(ds.reducedgrid_shape), tp, timings=stages)
-        dt = time.perf_counter() - t0
-        # the reference's own setting (main.py:3, OMP_NUM_THREADS=1): one frame on one thread
-        torch.set_num_threads(1)
-        t1 = time.perf_counter()
-        cpu_path.project_fuse(feats, mats, tuple(ds.reducedgrid_shape), tp)
-        dt1 = time.perf_counter() - t1
-        torch.set_num_threads(threads)
-    one = dict(value=round(B / dt1, 4), unit="frames/s", cores=1,
-               sample="1 frame of the same workload with torch.set_num_threads(1) (main.py:3 OMP_NUM_THREADS=1)")
-    return dict(value=round(B * frames / dt, 4), unit="frames/s", cores=threads, kind="port", single_thread=one,
-                sample=f"{frames} frame(s) (B={B}) of the bench workload after 1 warm-up; oracle/cpu_path.py "
-                       f"(kornia-0.6.11 restatement over torch-CPU grid_sample + torch.cat + 3x F.conv2d) "
-                       f"on identical synthetic inputs; last frame stages (s): "
+        times = [frame(stages) for _ in range(frames)]
+        single = None
+        if single_frames:
+            # the reference's own setting (main.py:3, OMP_NUM_THREADS=1)
+            torch.set_num_threads(1)
+            frame()
+            t1 = [frame() for _ in range(single_frames)]
+            torch.set_num_threads(threads)
+            single = dict(value=round(B / float(np.median(t1)), 4), unit="frames/s", cores=1,
+                          sample=f"median of {single_frames} frame(s) after 1 warm-up with torch.set_num_threads(1) "
+                                 "(main.py:3 OMP_NUM_THREADS=1)")
+    dt = float(np.median(times))
+    return dict(value=round(B / dt, 4), unit="frames/s", cores=threads, kind="port", single_thread=single,
+                sample=f"median of {frames} frame(s) (B={B}) of the bench workload after {warmups} warm-up(s) "
+                       f"(BASELINE.md:26); oracle/cpu_path.py (kornia-0.6.11 restatement over torch-CPU grid_sample "
+                       f"+ torch.cat + 3x F.conv2d) on identical synthetic inputs; last frame stages (s): "
                        + ", ".join(f"{k}={v:.3f}" for k, v in stages.items()))
 
 
@@ -109,27 +120,28 @@ def mfma_probe(settle_s: float = 1.5):
     return v if v > 0 else None
 
 
-def run_single(args, precision, steps, warmup, with_cpu):
+def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=None):
     from mvdet_amd import ProjectFuse, synthetic
     from mvdet_amd.geometry import projection_matrices, touched_footprint
 
+    config = args.config if config is None else config
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    spec = synthetic.CONFIGS[args.config]
+    spec = synthetic.CONFIGS[config]
     ds = spec["make"]()
     B, C = spec["B"], spec["C"]
     N = ds.num_cam
     up = tuple(ds.upsample_shape)
     ho, wo = ds.reducedgrid_shape
     pm = projection_matrices(ds)
-    params = head_params(N, seed=args.config, C=C)
+    params = head_params(N, seed=config, C=C)
     mc = build_mc(C, N, params, dev)
-    half = args.config == 4
+    half = config == 4
     eng = ProjectFuse(pm, up, (ho, wo), C, precision=precision,
                       slab_dtype=torch.float16 if half else torch.float32,
                       wino_conv1=args.conv1 == "wino" and precision == "bf16x3")
-    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * args.config + v,
+    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * config + v,
                                           device=dev).to(torch.float16 if half else torch.float32)
              for v in range(N)]
     ws = eng.workspace(B, dev)
@@ -163,7 +175,7 @@ def run_single(args, precision, steps, warmup, with_cpu):
 
     t_warp = avg(ev["warp"], ev["conv1"])
     t_c1 = avg(ev["conv1"], ev["conv2"])
-    wino = eng.wino_conv1  # conv1 = the row transform (wino_rows_kernel) + conv_wino_kernel
+    wino = eng.wino_active(dev)  # conv1 = conv_wino_kernel (its row transform came from the warp)
     t_rows = avg(ev["conv1"], ev["conv1_wino"]) if wino else 0.0
     t_c1k = t_c1 - t_rows  # conv1's conv kernel alone
     t_c2 = avg(ev["conv2"], ev["conv3"])
@@ -202,16 +214,18 @@ def run_single(args, precision, steps, warmup, with_cpu):
         achieved, peak = conv1_alg_tfs, FP32_MFMA_PEAK_TFS
         kname = "conv3x3_mfma_f32 (conv1)"
     sustained = mfma_probe() if precision == "bf16x3" and not args.no_probe else None
-    traffic, warp_traffic = None, None
-    tfile = ROOT / "profiles" / f"traffic_cfg{args.config}_{precision}{'_wino' if wino else ''}.json"
+    traffic, warp_traffic, traffic_src = None, None, None
+    tfile = ROOT / "profiles" / f"traffic_cfg{config}_{precision}{'_wino' if wino else ''}.json"
     if tfile.exists():
         tj = json.loads(tfile.read_text())
         traffic, warp_traffic = tj.get("conv1_hbm_bytes_per_launch"), tj.get("warp_hbm_bytes_per_launch")
+        traffic_src = (f"{tfile.relative_to(ROOT)}: rocprofv3 PMC passes of this kernel (committed profile, not "
+                       f"measured in this run: PMC collection needs its own rocprofv3 runs)")
     res = {
         "value": round(value, 3),
         "ms_per_step": round(dt * 1e3 / K, 4),
         "dtype": DTYPE_LABEL[precision],
-        "config": {"workload": f"cfg{args.config}: {spec['name']}", "views": N, "channels": C, "batch": B,
+        "config": {"workload": f"cfg{config}: {spec['name']}", "views": N, "channels": C, "batch": B,
                    "src_hw": list(up), "grid_hw": [ho, wo], "precision": precision,
                    "storage": "fp16" if half else "fp32", "parallelism": "single GPU"},
         # achieved/frac = the MFMA work conv1 actually has to do (the frustum-masked products;
@@ -220,6 +234,7 @@ def run_single(args, precision, steps, warmup, with_cpu):
         # above the MFMA rate the kernel really sustains, by 1/active).
         "roofline": {"kernel": kname, "bound": "mfma", "achieved": round(achieved * active, 2), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(achieved * active / peak, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "basis": (("3 bf16 MFMA passes x 5/9 (row Winograd) x 2*B*Ho*Wo*9*(N*C)*512 x "
                                 "frustum_active_fraction over the conv kernel's time" if wino else
                                 "3 bf16 MFMA passes x 2*B*Ho*Wo*9*(N*C)*512 x frustum_active_fraction")
@@ -267,8 +282,8 @@ def run_single(args, precision, steps, warmup, with_cpu):
         },
     }
     if with_cpu:
-        frames_cpu = args.cpu_frames or (3 if args.config == 2 else 5)
-        res["cpu_baseline"] = cpu_baseline(ds, 1 if half else B, C, pm, params, frames_cpu, args.config)
+        plan = cpu_plan or dict(frames=args.cpu_frames or 5, warmups=2, single_frames=3)
+        res["cpu_baseline"] = cpu_baseline(ds, 1 if half else B, C, pm, params, config=config, **plan)
     return res
 
 
@@ -462,10 +477,13 @@ def main():
     ap.add_argument("--no-train", action="store_true", help="skip the training-step (forward+backward) line")
     ap.add_argument("--train-torch", type=int, default=1,
                     help="1 = also time the reference op sequence (torch GPU autograd) for the training step")
-    ap.add_argument("--mp-mode", default="frames", choices=["frames", "partial", "gather"],
-                    help="N>1 `value`: frame-parallel (default: each rank its own frames, no collective) or the "
-                         "view-parallel modes (conv1 partial sums + reduce-scatter / slab all-gather + row bands); "
-                         "the other modes are reported alongside")
+    ap.add_argument("--mp-mode", default="bands", choices=["bands", "gather", "partial", "frames"],
+                    help="N>1 `value`: view-parallel band exchange (default: views one per GPU, all-to-all of each "
+                         "row band's input window, row-band fusion, pipelined), slab all-gather, conv1 partial sums + "
+                         "reduce-scatter, or frame-parallel; the other modes are reported alongside")
+    ap.add_argument("--north-star-cfg", type=int, default=3,
+                    help="also run this config (the north star's 480x1440 Wildtrack grid) as a sub-object "
+                         "(N=1: single GPU with a 1-frame CPU baseline; N>1: the band exchange); 0 = skip")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -484,7 +502,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": res["ms_per_step"],
         "higher_is_better": True,
-        "scaling": "weak",  # N > 1: frame-parallel, the same per-GPU workload
+        "scaling": "strong",  # N > 1: one frame's views across the GPUs (the band exchange)
         "vs_baseline": None,
         "dtype": res["dtype"],
         "data": "synthetic (ReLU N(0,1) features upsampled 3x, synthetic pinhole rig through the reference "
@@ -500,6 +518,18 @@ def main():
         result["speedup_vs_cpu"] = round(res["value"] / result["cpu_baseline"]["value"], 1)
     if args.config != 4:  # the fused upsample+warp writes fp32 / split slabs (not the fp16 slab)
         result["plus_a4"] = run_plus_a4(args, args.precision, max(5, args.steps // 2), 2)
+    ns = args.north_star_cfg
+    if ns and ns != args.config:
+        # the size the north star quotes its >= 5x at 1 GPU on (cfg3: 7 views, 480 x 1440 grid): the same
+        # path, its roofline, and a 1-frame CPU baseline (about 20 s of CPU work)
+        sub = run_single(args, args.precision, max(5, args.steps // 4), 2, with_cpu=not args.no_cpu_baseline,
+                         config=ns, cpu_plan=dict(frames=1, warmups=0, single_frames=0))
+        sub = {k: sub[k] for k in ("value", "ms_per_step", "config", "roofline", "stages_ms", "e2e_roofline",
+                                   "stage_roofline", "cpu_baseline") if k in sub}
+        sub["unit"] = "frames/s"
+        if sub.get("cpu_baseline"):
+            sub["speedup_vs_cpu"] = round(sub["value"] / sub["cpu_baseline"]["value"], 1)
+        result[f"cfg{ns}"] = sub
     if not args.no_train and args.config != 4:
         result["train_step"] = run_train_step(args.config, args.precision, max(5, args.steps // 2), 2,
                                               with_torch=bool(args.train_torch))

@@ -506,19 +506,29 @@ class ProjectFuse:
     # -- partial-sum multi-GPU (SURVEY §8(e) alternative, §8(f) row 3) -----------------------
     def conv1_partial(self, ws: Workspace, map_classifier: torch.nn.Sequential, out: torch.Tensor) -> torch.Tensor:
         """conv1 restricted to this slab's views (its slice of conv1's input channels), all
-        grid rows, no bias / coord term / ReLU: one rank's term of conv1's channel sum.
-        ``out``: contiguous [B, 512, Ho, Wo] fp32."""
+        grid rows, no bias / coord term / ReLU: one rank's term of conv1's channel sum
+        (row-Winograd where ``wino_active``).  ``out``: contiguous [B, 512, Ho, Wo] fp32."""
         if ws.t_from_warp:
             raise RuntimeError("conv1_partial reads the slab, but the fused warp wrote conv1's row transform")
+        if ws.slab_rows != (0, self.grid_hw[0]):
+            raise ValueError("conv1_partial needs a whole-grid slab")
         H, W = self.grid_hw
         B = ws.slab.shape[1]
-        p1 = self.pack1.get(map_classifier[0].weight)
         d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * H * W,
                            batch_stride=self.Cs * H * W, in_row0=0, in_rows=H, out_row0=0, out_rows=H)
         gm = self.conv1_mask(ws.slab.device, 0, H)  # no ReLU: the grid tiles (edge strips are conv1+ReLU only)
-        return ops.conv3x3_desc(ws.slab, d1, p1, self.mid, bias=None, init=None, dilation=1, relu=False,
-                                out=out, workspace=None if gm is not None else self._sk_ws(d1, ws.slab.device),
-                                group_mask=gm, tile_order=self.conv1_order(ws.slab.device, 0, H, B, grid=True))
+        order = self.conv1_order(ws.slab.device, 0, H, B, grid=True)
+        w1 = map_classifier[0].weight
+        if self.wino_active(ws.slab.device):
+            need = ops.wino_rows_bytes(d1)
+            if ws.wino_t is None or ws.wino_t.numel() * 2 < need:
+                ws.wino_t = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=ws.slab.device)
+            ops.wino_rows(ws.slab, d1, ws.wino_t, gm)
+            return ops.conv3x3_wino(ws.wino_t, d1, self.pack1w.get(w1), self.mid, init=None, relu=False, out=out,
+                                    group_mask=gm, tile_order=order)
+        return ops.conv3x3_desc(ws.slab, d1, self.pack1.get(w1), self.mid, bias=None, init=None, dilation=1,
+                                relu=False, out=out, workspace=None if gm is not None else self._sk_ws(d1, ws.slab.device),
+                                group_mask=gm, tile_order=order)
 
     def finish_from_y1(self, ws: Workspace, map_classifier: torch.nn.Sequential, mark=None) -> torch.Tensor:
         """``ws.y1`` holds conv1's summed channel terms (no bias) for rows ``ws.y1_rows``:

@@ -28,18 +28,25 @@ def _free_port():
 class OracleEngine:
     """CPU stand-in for ``pipeline.ProjectFuse`` built on the oracle (test only)."""
 
-    def __init__(self, proj_mats, src_hw, grid_hw, C, params, slot_views):
+    def __init__(self, proj_mats, src_hw, grid_hw, C, params, slot_views, all_views=True):
         self.pm, self.src_hw, self.grid_hw, self.C, self.params = proj_mats, src_hw, grid_hw, C, params
         self.slot_views = slot_views
         self.slot_of = {v: s for s, v in enumerate(slot_views) if v is not None}
+        self._ws = {}
 
-    def workspace(self, B, device, band):
+    def workspace(self, B, device, band=None, slab_rows=None, tag=0):
         from mvdet_amd.pipeline import band_rows
         H, W = self.grid_hw
-        y1r, y2r = band_rows(band[0], band[1], H)
-        mid = self.params["map_classifier.0.weight"].shape[0]
-        return SimpleNamespace(slab=torch.zeros(len(self.slot_views), B, self.C, H, W), band=band,
-                               y1=torch.zeros(B, mid, y1r[1] - y1r[0], W), y1_rows=y1r, y2_rows=y2r)
+        band = (0, H) if band is None else tuple(band)
+        slab_rows = (0, H) if slab_rows is None else tuple(slab_rows)
+        key = (B, band, slab_rows, tag)
+        if key not in self._ws:
+            y1r, y2r = band_rows(band[0], band[1], H)
+            mid = self.params["map_classifier.0.weight"].shape[0]
+            self._ws[key] = SimpleNamespace(
+                slab=torch.zeros(len(self.slot_views), B, self.C, slab_rows[1] - slab_rows[0], W), band=band,
+                slab_rows=slab_rows, y1=torch.zeros(B, mid, y1r[1] - y1r[0], W), y1_rows=y1r, y2_rows=y2r)
+        return self._ws[key]
 
     # partial-sum mode: conv1 over this slab's views only, then the band fusion from summed y1
     def conv1_partial(self, ws, mc, out):
@@ -72,11 +79,14 @@ class OracleEngine:
         ws.slab[self.slot_of[v]] = kornia_warp.warp_perspective(feat, M, list(self.grid_hw))
 
     def fuse(self, ws, mc, mark=None):
+        """The oracle convs on the slab's rows (a band-local window is exact 7 rows inside its
+        cuts, which the band is), then the band's rows."""
         B = ws.slab.shape[1]
+        lo, hi = ws.slab_rows
         views = [ws.slab[self.slot_of[v]] for v in range(len(self.pm))]
-        fused = torch.cat(views + [cpu_path.coord_map(*self.grid_hw).repeat(B, 1, 1, 1)], 1)
-        full = cpu_path.fuse(fused, self.params)
-        return full[:, :, ws.band[0]:ws.band[1]]
+        coord = cpu_path.coord_map(*self.grid_hw)[:, :, lo:hi].repeat(B, 1, 1, 1)
+        out = cpu_path.fuse(torch.cat(views + [coord], 1), self.params)
+        return out[:, :, ws.band[0] - lo:ws.band[1] - lo]
 
 
 def _case():
@@ -91,27 +101,37 @@ def _case():
     return pm, tuple(up), tuple(ds.reducedgrid_shape), C, B, feats, params
 
 
-def _worker(rank, world, port, out_dir, mode="gather"):
+MODES = {"gather": parallel.ViewParallel, "partial": parallel.ViewPartialSum, "bands": parallel.ViewBands}
+
+
+def _worker(rank, world, port, out_dir, mode="gather", frames=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
     pm, up, grid, C, B, feats, params = _case()
-    cls = parallel.ViewPartialSum if mode == "partial" else parallel.ViewParallel
-    vp = cls(lambda sv: OracleEngine(pm, up, grid, C, params, sv), pm, grid, rank, world)
-    ws = vp.workspace(B, "cpu")
+    vp = MODES[mode](lambda sv, **kw: OracleEngine(pm, up, grid, C, params, sv, **kw), pm, grid, rank, world)
     with torch.no_grad():
-        out = vp.step(ws, [feats[v] for v in vp.my_views], None)
-    torch.save({"out": out, "band": vp.band, "views": vp.my_views}, os.path.join(out_dir, f"r{rank}.pt"))
+        if frames == 1:
+            outs = [vp.step(vp.workspace(B, "cpu"), [feats[v] for v in vp.my_views], None)]
+        else:  # FramePipeline: frame f uses the features scaled by (f + 1)
+            pipe = parallel.FramePipeline(vp, B, "cpu")
+            outs = [pipe.submit([(f + 1) * feats[v] for v in vp.my_views], None) for f in range(frames)]
+            outs = outs[1:] + [pipe.drain(None)]
+            assert pipe.drain(None) is None
+    torch.save({"outs": outs, "band": vp.band, "views": vp.my_views}, os.path.join(out_dir, f"r{rank}.pt"))
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world,mode", [(2, "gather"), (3, "gather"), (4, "gather"), (2, "partial"), (3, "partial"),
-                                        (4, "partial"), (8, "gather"), (8, "partial")])
+                                        (4, "partial"), (8, "gather"), (8, "partial"), (2, "bands"), (3, "bands"),
+                                        (4, "bands"), (8, "bands")])
 def test_view_parallel_matches_single_process_oracle(world, mode, tmp_path):
     """gather: slab all-gather + row bands.  partial: conv1 partial sums over each rank's
     views + reduce-scatter by band + edge-row halo (world 2: 7-row bands use the edge
     all-gather; world 3: 5-row bands fall back to whole bands; world 4: a rank with no view
-    contributes zeros; world 8, the driver's node size: five ranks without views, 7-row bands)."""
+    contributes zeros; world 8, the driver's node size: five ranks without views, 7-row bands).
+    bands: all-to-all of each band's input row window (windows shifted inside the grid at the
+    edges; ranks without views send nothing), fusion from the band-local slab."""
     port = _free_port()
     mp.spawn(_worker, args=(world, port, str(tmp_path), mode), nprocs=world, join=True)
     pm, up, grid, C, B, feats, params = _case()
@@ -121,8 +141,8 @@ def test_view_parallel_matches_single_process_oracle(world, mode, tmp_path):
     for r in range(world):
         res = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
         assert res["views"] == parallel.views_of(r, world, 3)
-        tol = dict(rtol=1e-6, atol=1e-7) if mode == "gather" else dict(rtol=1e-5, atol=1e-6)  # summation order
-        torch.testing.assert_close(res["out"], ref, **tol)
+        tol = dict(rtol=1e-5, atol=1e-6) if mode == "partial" else dict(rtol=1e-6, atol=1e-7)  # summation order
+        torch.testing.assert_close(res["outs"][0], ref, **tol)
         bands.append(tuple(res["band"]))
     assert bands[0][0] == 0 and bands[-1][1] == grid[0]
     assert all(bands[i][1] == bands[i + 1][0] for i in range(world - 1))
@@ -139,3 +159,34 @@ def test_slot_order_and_bands():
     from mvdet_amd.pipeline import band_rows
     assert band_rows(15, 30, 120) == ((9, 36), (11, 34))
     assert band_rows(0, 15, 120) == ((0, 21), (0, 19))
+
+
+@pytest.mark.parametrize("world,mode", [(2, "bands"), (3, "partial"), (2, "gather")])
+def test_frame_pipeline_returns_every_frame_in_order(world, mode, tmp_path):
+    """FramePipeline (frame i's exchange overlapped with frame i-1's fusion, double buffers):
+    4 frames with different inputs come back in order, each equal to its own single-process
+    result (a buffer reused too early would mix frames)."""
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, str(tmp_path), mode, 4), nprocs=world, join=True)
+    pm, up, grid, C, B, feats, params = _case()
+    with torch.no_grad():
+        refs = [cpu_path.project_fuse([(f + 1) * x for x in feats], pm, grid, params) for f in range(4)]
+    for r in range(world):
+        res = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
+        assert len(res["outs"]) == 4
+        for f in range(4):
+            torch.testing.assert_close(res["outs"][f], refs[f], rtol=1e-5, atol=1e-6)
+
+
+def test_band_windows_cover_each_band():
+    """ViewBands' input windows: E = ceil(H/P) + 14 rows, inside the grid, covering the band's
+    rows +- 7 (clipped at the grid edges)."""
+    for H, P in ((52, 2), (52, 3), (52, 8), (120, 7), (480, 7), (160, 6), (5, 8)):
+        vb = SimpleNamespace(grid_hw=(H, 10), world=P, E=min(H, -(-H // P) + 14))
+        for p in range(P):
+            lo, hi = parallel.ViewBands.window(vb, p)
+            r0, r1 = parallel.row_band(H, p, P)
+            if r1 <= r0:
+                r0, r1 = 0, 1
+            assert 0 <= lo and hi <= H and hi - lo == vb.E
+            assert lo <= max(0, r0 - 7) and min(H, r1 + 7) <= hi

@@ -17,7 +17,7 @@ ROOT = Path(__file__).resolve().parents[1]
 def test_bench_json_line_contract():
     env = dict(os.environ, PYTHONUNBUFFERED="1")
     out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--config", "1", "--steps", "2", "--warmup", "1",
-                          "--no-train", "--no-alt", "--cpu-frames", "1"],
+                          "--no-train", "--no-alt", "--cpu-frames", "1", "--north-star-cfg", "2"],
                          cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
@@ -39,13 +39,18 @@ def test_bench_json_line_contract():
     e2e = r["e2e_roofline"]
     assert 0 < e2e["frac"] <= 1.0 and e2e["floor_ms"] > 0
     assert r["config"]["workload"].startswith("cfg1")
+    # the north-star sub-object (here cfg2 for speed; the default is cfg3): its own value, roofline, CPU baseline
+    sub = r["cfg2"]
+    assert sub["value"] > 0 and sub["config"]["workload"].startswith("cfg2") and 0 < sub["roofline"]["frac"] <= 1.0
+    assert sub["cpu_baseline"]["value"] > 0 and sub["speedup_vs_cpu"] > 1
 
 
 @pytest.mark.gpu
 def test_bench_multi_rank_json_line():
     """The N > 1 path as the driver launches it (torch.distributed.run, one JSON line from rank 0),
-    rehearsed with 2 gloo ranks sharing the box's one GPU: frame-parallel `value` plus both
-    view-parallel modes reported alongside (RCCL itself only runs on the driver's 8-GPU node)."""
+    rehearsed with 2 gloo ranks sharing the box's one GPU: the view-parallel band exchange as
+    `value` (strong scaling), frame-parallel and the other view-parallel modes alongside (RCCL
+    itself only runs on the driver's 8-GPU node)."""
     import socket
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -53,14 +58,15 @@ def test_bench_multi_rank_json_line():
     env = dict(os.environ, PYTHONUNBUFFERED="1", MVBEV_DIST_BACKEND="gloo")
     out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                           "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"),
-                          "--gpus", "2", "--config", "1", "--steps", "2", "--warmup", "1"],
+                          "--gpus", "2", "--config", "1", "--steps", "2", "--warmup", "1", "--north-star-cfg", "0"],
                          cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]
     r = json.loads(lines[0])
-    assert r["n_gpus"] == 2 and r["scaling"] == "weak" and r["value"] > 0
-    assert r["config"]["batch"] == 2 and 0 < r["roofline"]["frac"] <= 1.0
+    assert r["n_gpus"] == 2 and r["scaling"] == "strong" and r["value"] > 0
+    assert r["config"]["batch"] == 1 and 0 < r["roofline"]["frac"] <= 1.0
+    assert r["frame_parallel"]["scaling"] == "weak" and r["frame_parallel"]["value"] > 0
     for key in ("view_parallel_partial", "view_parallel_gather"):
         assert "error" not in r[key], r[key]
         assert r[key]["value"] > 0 and r[key]["scaling"] == "strong"

@@ -66,30 +66,33 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir, mode="gather"):
+def _worker(rank, world, port, out_dir, mode="gather", backend="gloo", frames=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group(backend, rank=rank, world_size=world,
+                            device_id=torch.device("cuda:0") if backend == "nccl" else None)
     from mvdet_amd import ProjectFuse
-    from mvdet_amd.parallel import ViewParallel, ViewPartialSum
+    from mvdet_amd.parallel import FramePipeline, ViewBands, ViewParallel, ViewPartialSum
     ds, pm, up, grid, C, B, feats, mc = _setup()
     mc = mc.to("cuda:0")
-    if mode == "partial":
-        vp = ViewPartialSum(lambda sv: ProjectFuse(pm, up, grid, C, slot_views=sv, all_views=False), pm, grid,
-                            rank, world)
-    else:
-        vp = ViewParallel(lambda sv: ProjectFuse(pm, up, grid, C, slot_views=sv), pm, grid, rank, world)
-    ws = vp.workspace(B, "cuda:0")
+    cls = {"gather": ViewParallel, "partial": ViewPartialSum, "bands": ViewBands}[mode]
+    vp = cls(lambda sv, **kw: ProjectFuse(pm, up, grid, C, slot_views=sv, **kw), pm, grid, rank, world)
     with torch.no_grad():
-        out = vp.step(ws, [feats[v].cuda() for v in vp.my_views], mc)
+        if frames == 1:
+            outs = [vp.step(vp.workspace(B, "cuda:0"), [feats[v].cuda() for v in vp.my_views], mc)]
+        else:  # frame f: the features scaled by (f + 1); exchange on a side stream under NCCL
+            pipe = FramePipeline(vp, B, "cuda:0")
+            outs = [pipe.submit([(f + 1) * feats[v].cuda() for v in vp.my_views], mc) for f in range(frames)]
+            outs = outs[1:] + [pipe.drain(mc)]
         torch.cuda.synchronize()
-    torch.save(out.cpu(), os.path.join(out_dir, f"r{rank}.pt"))
+    torch.save([o.cpu() for o in outs], os.path.join(out_dir, f"r{rank}.pt"))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mode", [(2, "gather"), (2, "partial"), (4, "partial")])
+@pytest.mark.parametrize("world,mode", [(2, "gather"), (2, "partial"), (4, "partial"), (2, "bands"), (3, "bands")])
 def test_rank_rehearsal_matches_single_process(world, mode, tmp_path):
-    """gather / partial-sum modes; world 4 (3 views) includes a rank without views and
-    bands of 8 rows (edge-row halo exchange)."""
+    """gather / partial-sum / band-exchange modes; world 4 (3 views) includes a rank without
+    views and bands of 8 rows (edge-row halo exchange); bands at world 3: one view per rank,
+    shifted windows at both grid edges."""
     from mvdet_amd import ProjectFuse
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world, join=True)
     ds, pm, up, grid, C, B, feats, mc = _setup()
@@ -97,6 +100,26 @@ def test_rank_rehearsal_matches_single_process(world, mode, tmp_path):
     with torch.no_grad():
         ref = ProjectFuse(pm, up, grid, C).project_fuse([f.cuda() for f in feats], mc).cpu()
     for r in range(world):
-        got = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
-        # different slot order -> different K summation order in conv1: fp32-rounding level only
+        got = torch.load(tmp_path / f"r{r}.pt", weights_only=True)[0]
+        # different slot order / band-started Winograd tiles -> different summation order in conv1:
+        # fp32-rounding level only
         torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("mode", ["bands", "gather", "partial"])
+def test_frame_pipeline_on_rccl_streams(mode, tmp_path):
+    """FramePipeline with the real RCCL backend (a one-rank world on the box's GPU): the exchange
+    runs on the side stream behind events, the fusion of the previous frame on the compute
+    stream; 4 frames with different inputs come back in order and equal the single-process
+    maps (a missing wait or an early buffer reuse would mix frames)."""
+    from mvdet_amd import ProjectFuse
+    mp.spawn(_worker, args=(1, _free_port(), str(tmp_path), mode, "nccl", 4), nprocs=1, join=True)
+    ds, pm, up, grid, C, B, feats, mc = _setup()
+    mc = mc.to("cuda:0")
+    eng = ProjectFuse(pm, up, grid, C)
+    got = torch.load(tmp_path / "r0.pt", weights_only=True)
+    assert len(got) == 4
+    with torch.no_grad():
+        for f in range(4):
+            ref = eng.project_fuse([(f + 1) * x.cuda() for x in feats], mc).cpu()
+            torch.testing.assert_close(got[f], ref, rtol=1e-4, atol=1e-5)

@@ -339,6 +339,58 @@ int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int
                             int64_t in_row0, int64_t in_rows, int64_t out_row0, int64_t out_rows,
                             const float* w, int dilation, float* y, void* stream);
 
+/* ---- one-call project + fuse ----------------------------------------------
+ * The inference hot path of PerspTransDetector.forward after the backbone
+ * (persp_trans_detector.py:62-82: the per-view warp at :69 (+ the 3x upsample of :65 for
+ * backbone-resolution sources), the concat at :77, map_classifier at :81, the identity
+ * interpolate at :82) for a caller that does not want to orchestrate the entry points above
+ * itself.  Three calls over one caller-owned device workspace:
+ *   mvbev_bev_plan_init      host only: validates the geometry, lays out the workspace
+ *   mvbev_bev_fuse_prepare   once per geometry and weight version: conv1's packing (G w for the
+ *                            row-Winograd form), conv2's, the coord term (conv1 bias + conv1 over
+ *                            the 2 coord channels, :21), the frustum mask, the heavy-first tile
+ *                            order and the non-finite-geometry check; ONE stream sync (the mask
+ *                            and the check are read back to plan the launches)
+ *   mvbev_bev_fuse           per frame, enqueued, no sync: map = [B][1][Ho][Wo] fp32
+ * Weights are the nn.Conv2d parameters of map_classifier (:51-54), fp32 contiguous device
+ * tensors: w1 [512][N*C+2][3][3], b1 [512], w2 [512][512][3][3], b2 [512], w3 [1][512][3][3];
+ * b2 and w3 are read again by every mvbev_bev_fuse (keep them alive and unchanged; after an
+ * update of any weight call prepare again).  The module's channel order is view-major (view v's
+ * channels are v*C .. v*C + C-1, then the 2 coord channels) as torch.cat builds it at :77. */
+#define MVBEV_BEV_MAX_VIEWS 16
+#define MVBEV_BEV_SRC_F32 0          /* views[v]: [B][C][H][W] fp32 contiguous (kornia's input, :69) */
+#define MVBEV_BEV_SRC_F16 1          /* views[v]: [B][C][H][W] fp16 contiguous (fp32 math) */
+#define MVBEV_BEV_SRC_BACKBONE_F32 2 /* views[v]: [B][C][h][w] fp32 backbone maps; :65's upsample fused */
+typedef struct mvbev_bev_geometry {
+  int32_t num_views;                /* N, 1 .. 16 (persp_trans_detector.py:58-59) */
+  int32_t src_kind;                 /* MVBEV_BEV_SRC_* */
+  int64_t B, C;                     /* batch items; channels per view */
+  int64_t h, w;                     /* backbone map size (MVBEV_BEV_SRC_BACKBONE_F32 only) */
+  int64_t H, W;                     /* the warp's source size (upsample_shape, :23) */
+  int64_t Ho, Wo;                   /* the ground grid (reducedgrid_shape) */
+  float m[MVBEV_BEV_MAX_VIEWS][9];  /* per view: kornia's src_norm <- dst_norm of proj_mats[v] (:68-69) */
+} mvbev_bev_geometry;
+typedef struct mvbev_bev_plan {     /* host memory, caller-owned; filled by the calls below */
+  mvbev_bev_geometry g;
+  int32_t wino;                     /* after prepare: 1 = row-Winograd conv1, 0 = direct (non-finite geometry) */
+  int32_t frustum;                  /* conv1 skips the views a tile's camera frustum excludes (C % 16 == 0 after padding) */
+  int32_t prepared, reserved;
+  int64_t Cs, tiles;                /* channels per view slot (C rounded to 8); conv1's 12 x 32 tiles */
+  size_t off[16];                   /* workspace regions */
+  size_t workspace_bytes;           /* >= what mvbev_bev_fuse_workspace_bytes returns, 256-B aligned base */
+  const float* b2;
+  const float* w3;
+} mvbev_bev_plan;
+int mvbev_bev_plan_init(const mvbev_bev_geometry* g, mvbev_bev_plan* plan);
+size_t mvbev_bev_fuse_workspace_bytes(const mvbev_bev_geometry* g);
+int mvbev_bev_fuse_prepare(mvbev_bev_plan* plan, const float* w1, const float* b1, const float* w2, const float* b2,
+                           const float* w3, void* workspace, size_t ws_bytes, void* stream);
+/* views: host array of N device pointers (layout per src_kind); map: [B][1][Ho][Wo] fp32.  fp32
+ * sources: the warp writes conv1's row-Winograd transform directly; fp16 sources (and geometry
+ * with non-finite samples) run the direct conv1 on the split slab. */
+int mvbev_bev_fuse(const mvbev_bev_plan* plan, const void* const* views, float* map, void* workspace,
+                   size_t ws_bytes, void* stream);
+
 /* ---- native backward: training through the hot path ----------------
  * Replaces the autograd of the stock ops the reference trains through (trainer.py:38-49,
  * loss.backward() at :47): grid_sample's backward under kornia.warp_perspective

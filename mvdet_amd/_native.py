@@ -71,7 +71,12 @@ EXPORTS = (
     "mvbev_warp_views_wino_rows",
     "mvbev_warp_views_upsampled_wino_rows",
     "mvbev_warp_nonfinite_views",
+    "mvbev_bev_plan_init",
+    "mvbev_bev_fuse_workspace_bytes",
+    "mvbev_bev_fuse_prepare",
+    "mvbev_bev_fuse",
 )
+BEV_SRC_F32, BEV_SRC_F16, BEV_SRC_BACKBONE_F32 = 0, 1, 2  # MVBEV_BEV_SRC_*
 WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
 TILES_GRID, TILES_EDGE_STRIP = 0, 1  # MVBEV_TILES_*
 ERR_SHAPE = -2  # MVBEV_ERR_SHAPE
@@ -112,6 +117,21 @@ class ConvSchedule(ctypes.Structure):
     _fields_ = [("items", ctypes.c_void_p), ("nitems", ctypes.c_int32), ("fixups", ctypes.c_void_p),
                 ("nfix", ctypes.c_int32), ("nslots", ctypes.c_int32), ("partials", ctypes.c_void_p),
                 ("partial_bytes", ctypes.c_size_t)]
+
+
+class BevGeometry(ctypes.Structure):
+    """``mvbev_bev_geometry`` (include/mvbev.h)."""
+    _fields_ = [("num_views", ctypes.c_int32), ("src_kind", ctypes.c_int32)] + \
+        [(n, ctypes.c_int64) for n in ("B", "C", "h", "w", "H", "W", "Ho", "Wo")] + \
+        [("m", (ctypes.c_float * 9) * 16)]
+
+
+class BevPlan(ctypes.Structure):
+    """``mvbev_bev_plan`` (include/mvbev.h)."""
+    _fields_ = [("g", BevGeometry), ("wino", ctypes.c_int32), ("frustum", ctypes.c_int32),
+                ("prepared", ctypes.c_int32), ("reserved", ctypes.c_int32), ("Cs", ctypes.c_int64),
+                ("tiles", ctypes.c_int64), ("off", ctypes.c_size_t * 16), ("workspace_bytes", ctypes.c_size_t),
+                ("b2", ctypes.c_void_p), ("w3", ctypes.c_void_p)]
 
 
 class NativeError(RuntimeError):
@@ -186,6 +206,15 @@ def _declare(lib):
                                          _i64, _i64, _i64, _i64, _p, _p]
     lib.mvbev_warp_nonfinite_views.restype = ctypes.c_int
     lib.mvbev_warp_nonfinite_views.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _p, _p]
+    lib.mvbev_bev_plan_init.restype = ctypes.c_int
+    lib.mvbev_bev_plan_init.argtypes = [ctypes.POINTER(BevGeometry), ctypes.POINTER(BevPlan)]
+    lib.mvbev_bev_fuse_workspace_bytes.restype = ctypes.c_size_t
+    lib.mvbev_bev_fuse_workspace_bytes.argtypes = [ctypes.POINTER(BevGeometry)]
+    lib.mvbev_bev_fuse_prepare.restype = ctypes.c_int
+    lib.mvbev_bev_fuse_prepare.argtypes = [ctypes.POINTER(BevPlan), _p, _p, _p, _p, _p, _p, ctypes.c_size_t, _p]
+    lib.mvbev_bev_fuse.restype = ctypes.c_int
+    lib.mvbev_bev_fuse.argtypes = [ctypes.POINTER(BevPlan), ctypes.POINTER(ctypes.c_void_p), _p, _p, ctypes.c_size_t,
+                                   _p]
     lib.mvbev_threshold_points.restype = ctypes.c_int
     lib.mvbev_threshold_points.argtypes = [_p, _i64, _i64, ctypes.c_float, _p, _p, _p, _i64, _p]
     lib.mvbev_point_nms_workspace_bytes.restype = ctypes.c_size_t

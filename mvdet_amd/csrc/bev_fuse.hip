@@ -1,0 +1,283 @@
+// One-call project + fuse (SURVEY §8(b) "mvbev_bev_fuse"): the whole inference hot path of
+// PerspTransDetector.forward (persp_trans_detector.py:62-82, after the backbone) behind a plan,
+// for callers that are not the Python engine (mvdet_amd/pipeline.py makes the same calls).
+//
+//   plan_init (host only)  ->  prepare (once per geometry and weight version: weight packs, coord
+//   term, frustum mask, heavy-first tile order, the non-finite-geometry check; one stream sync)
+//   ->  fuse (per frame, enqueued, no sync): warp (+ the fused 3x upsample) writing conv1's
+//   row-Winograd transform straight into T, the Winograd conv1 (+ coord term, bias, ReLU), conv2
+//   with conv3's per-tap partials in its epilogue, their reduce -> map [B][1][Ho][Wo].
+//
+// Geometry that can produce a non-finite warp sample runs the direct conv1 on the split slab
+// instead (the reference's NaN pattern; see mvbev_warp_nonfinite_views).  Everything here is a
+// sequence of the library's own C entry points over one caller-owned workspace.
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+constexpr int64_t kMid = 512;  // map_classifier's hidden width (persp_trans_detector.py:51-53)
+constexpr int64_t kKC = MVBEV_CONV_KC;
+constexpr int64_t kTileW = MVBEV_CONV_TILE_W;
+constexpr size_t kAlign = 256;
+
+enum Region { R_MAP1, R_MAPC, R_PACK1, R_PACK2, R_PACKC, R_CIN, R_INIT, R_MASK, R_ORDER, R_NF, R_BIG, R_Y1, R_P3,
+              R_COUNT };
+
+size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
+
+template <typename T> T* at(void* ws, const mvbev_bev_plan* p, int r) {
+  return reinterpret_cast<T*>(static_cast<char*>(ws) + p->off[r]);
+}
+
+mvbev_conv_desc conv1_desc(const mvbev_bev_plan* p) {
+  const mvbev_bev_geometry& g = p->g;
+  mvbev_conv_desc d;
+  d.B = g.B; d.K = g.num_views * p->Cs; d.H = g.Ho; d.W = g.Wo;
+  d.group = p->Cs; d.group_stride = g.B * p->Cs * g.Ho * g.Wo; d.batch_stride = p->Cs * g.Ho * g.Wo;
+  d.in_row0 = 0; d.in_rows = g.Ho; d.out_row0 = 0; d.out_rows = g.Ho;
+  return d;
+}
+
+mvbev_conv_desc conv2_desc(const mvbev_bev_plan* p) {
+  const mvbev_bev_geometry& g = p->g;
+  mvbev_conv_desc d;
+  d.B = g.B; d.K = kMid; d.H = g.Ho; d.W = g.Wo;
+  d.group = kMid; d.group_stride = 0; d.batch_stride = kMid * g.Ho * g.Wo;
+  d.in_row0 = 0; d.in_rows = g.Ho; d.out_row0 = 0; d.out_rows = g.Ho;
+  return d;
+}
+
+// the views of one frame as mvbev_warp_view entries writing slot s of the split slab (32-B units)
+void slab_views(const mvbev_bev_plan* p, const void* const* views, void* slab, mvbev_warp_view* out) {
+  const mvbev_bev_geometry& g = p->g;
+  const bool backbone = g.src_kind == MVBEV_BEV_SRC_BACKBONE_F32;
+  const int64_t sh = backbone ? g.h : g.H, sw = backbone ? g.w : g.W;
+  const int64_t G = p->Cs / kKC;
+  for (int s = 0; s < g.num_views; ++s) {
+    mvbev_warp_view& v = out[s];
+    v.src = views[s];
+    v.src_strides[0] = g.C * sh * sw; v.src_strides[1] = sh * sw; v.src_strides[2] = sw; v.src_strides[3] = 1;
+    v.dst = static_cast<char*>(slab) + (size_t)s * g.B * G * g.Ho * g.Wo * 32;
+    v.dst_strides[0] = G * g.Ho * g.Wo; v.dst_strides[1] = g.Ho * g.Wo; v.dst_strides[2] = g.Wo;
+    v.dst_strides[3] = 1;
+    std::memcpy(v.m, g.m[s], sizeof(v.m));
+  }
+}
+
+// the same writing slot s's channels of T (the Winograd transform of the whole grid)
+void t_views(const mvbev_bev_plan* p, const void* const* views, void* t, mvbev_warp_view* out) {
+  const mvbev_bev_geometry& g = p->g;
+  const bool backbone = g.src_kind == MVBEV_BEV_SRC_BACKBONE_F32;
+  const int64_t sh = backbone ? g.h : g.H, sw = backbone ? g.w : g.W;
+  const int64_t r3 = 4 * ((g.Ho + 11) / 12), K8 = g.num_views * p->Cs / kKC;
+  for (int s = 0; s < g.num_views; ++s) {
+    mvbev_warp_view& v = out[s];
+    v.src = views[s];
+    v.src_strides[0] = g.C * sh * sw; v.src_strides[1] = sh * sw; v.src_strides[2] = sw; v.src_strides[3] = 1;
+    v.dst = static_cast<char*>(t) + (size_t)32 * (s * (p->Cs / kKC)) * 5 * r3 * g.Wo;
+    v.dst_strides[0] = K8 * 5 * r3 * g.Wo; v.dst_strides[1] = 5 * r3 * g.Wo; v.dst_strides[2] = g.Wo;
+    v.dst_strides[3] = 1;
+    std::memcpy(v.m, g.m[s], sizeof(v.m));
+  }
+}
+
+#define BEV_TRY(x)                 \
+  do {                             \
+    const int st_ = (x);           \
+    if (st_ != MVBEV_OK) return st_; \
+  } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int mvbev_bev_plan_init(const mvbev_bev_geometry* g, mvbev_bev_plan* p) {
+  if (!g || !p) return MVBEV_ERR_NULL;
+  if (g->num_views <= 0 || g->B <= 0 || g->C <= 0 || g->H <= 0 || g->W <= 0 || g->Ho <= 0 || g->Wo <= 0)
+    return MVBEV_ERR_RANK;
+  if (g->num_views > MVBEV_BEV_MAX_VIEWS) return MVBEV_ERR_SHAPE;
+  if (g->src_kind != MVBEV_BEV_SRC_F32 && g->src_kind != MVBEV_BEV_SRC_F16 && g->src_kind != MVBEV_BEV_SRC_BACKBONE_F32)
+    return MVBEV_ERR_SHAPE;
+  if (g->src_kind == MVBEV_BEV_SRC_BACKBONE_F32 && (g->h <= 0 || g->w <= 0 || g->h > g->H || g->w > g->W))
+    return MVBEV_ERR_SHAPE;
+  std::memset(p, 0, sizeof(*p));
+  p->g = *g;
+  p->Cs = (g->C + kKC - 1) / kKC * kKC;
+  const int64_t K = g->num_views * p->Cs;
+  p->frustum = p->Cs % 16 == 0 ? 1 : 0;  // the conv's group mask needs 16-channel chunks
+  // the row-Winograd conv1 reads T, which the warp writes directly from fp32 sources (the fused
+  // warp + transform kernels); fp16 sources take the direct conv1 on the split slab, as the
+  // engine's fp16-storage path does; prepare also falls back for non-finite geometry
+  p->wino = (g->src_kind != MVBEV_BEV_SRC_F16 && g->W >= 2 &&
+             (g->src_kind != MVBEV_BEV_SRC_BACKBONE_F32 || g->w >= 4)) ? 1 : 0;
+  const int64_t tiles_y = (g->Ho + 11) / 12, tiles_x = (g->Wo + kTileW - 1) / kTileW;
+  p->tiles = tiles_y * tiles_x;
+  mvbev_conv_desc d1 = conv1_desc(p), d2 = conv2_desc(p);
+  const size_t t_bytes = mvbev_wino_rows_bytes(&d1);
+  const size_t slab_bytes = (size_t)g->num_views * g->B * p->Cs * g->Ho * g->Wo * 4;
+  size_t sz[R_COUNT] = {};
+  sz[R_MAP1] = (size_t)K * 4;
+  sz[R_MAPC] = (size_t)kKC * 4;
+  sz[R_PACK1] = std::max(mvbev_conv3x3_packed_bytes_wino(kMid, K), mvbev_conv3x3_packed_bytes_bf16x3(kMid, K));
+  sz[R_PACK2] = mvbev_conv3x3_packed_bytes_bf16x3(kMid, kMid);
+  sz[R_PACKC] = 4 * mvbev_conv3x3_packed_floats(kMid, kKC);
+  sz[R_CIN] = (size_t)kKC * g->Ho * g->Wo * 4;
+  sz[R_INIT] = (size_t)kMid * g->Ho * g->Wo * 4;
+  sz[R_MASK] = (size_t)p->tiles * 4;
+  sz[R_ORDER] = (size_t)g->B * p->tiles * 4;
+  sz[R_NF] = 4;
+  sz[R_BIG] = std::max(t_bytes, slab_bytes);  // T (Winograd) or the split slab (direct conv1)
+  sz[R_Y1] = (size_t)g->B * kMid * g->Ho * g->Wo * 4;
+  sz[R_P3] = mvbev_conv3x3_bf16x3_cout1_partials_bytes(&d2, kMid);
+  size_t o = 0;
+  for (int r = 0; r < R_COUNT; ++r) {
+    p->off[r] = o;
+    o = align_up(o + sz[r]);
+  }
+  p->workspace_bytes = o;
+  return MVBEV_OK;
+}
+
+size_t mvbev_bev_fuse_workspace_bytes(const mvbev_bev_geometry* g) {
+  mvbev_bev_plan p;
+  return mvbev_bev_plan_init(g, &p) == MVBEV_OK ? p.workspace_bytes : 0;
+}
+
+int mvbev_bev_fuse_prepare(mvbev_bev_plan* p, const float* w1, const float* b1, const float* w2, const float* b2,
+                           const float* w3, void* ws, size_t ws_bytes, void* stream) {
+  if (!p || !w1 || !w2 || !w3 || !ws) return MVBEV_ERR_NULL;
+  if (p->workspace_bytes == 0 || ws_bytes < p->workspace_bytes) return MVBEV_ERR_SHAPE;
+  if (reinterpret_cast<uintptr_t>(ws) % kAlign) return MVBEV_ERR_ALIGN;
+  const mvbev_bev_geometry& g = p->g;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  const int64_t K = g.num_views * p->Cs, nc = g.num_views * g.C, cin = nc + 2;
+  // conv1's channel map: slot s channel c -> module channel s*C + c (view-major concat, :77)
+  std::vector<int32_t> map1((size_t)K), mapc((size_t)kKC, -1);
+  for (int64_t k = 0; k < K; ++k) {
+    const int64_t sl = k / p->Cs, c = k % p->Cs;
+    map1[(size_t)k] = c < g.C ? (int32_t)(sl * g.C + c) : -1;
+  }
+  mapc[0] = (int32_t)nc;
+  mapc[1] = (int32_t)(nc + 1);
+  if (hipMemcpyAsync(at<int32_t>(ws, p, R_MAP1), map1.data(), map1.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(at<int32_t>(ws, p, R_MAPC), mapc.data(), mapc.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+    return MVBEV_ERR_HIP;
+  // geometry: non-finite samples (-> direct conv1), the frustum mask of the 12 x 32 conv tiles
+  std::vector<mvbev_warp_view> mv((size_t)g.num_views);
+  std::memset(mv.data(), 0, mv.size() * sizeof(mvbev_warp_view));
+  for (int v = 0; v < g.num_views; ++v) std::memcpy(mv[(size_t)v].m, g.m[v], sizeof(mv[0].m));
+  BEV_TRY(mvbev_warp_nonfinite_views(mv.data(), g.num_views, g.H, g.W, g.Ho, g.Wo, at<uint32_t>(ws, p, R_NF), stream));
+  if (p->frustum)
+    BEV_TRY(mvbev_warp_tile_mask(mv.data(), g.num_views, g.H, g.W, g.Ho, g.Wo, 0, g.Ho, 12, kTileW, 1,
+                                 at<uint32_t>(ws, p, R_MASK), stream));
+  uint32_t nf = 0;
+  std::vector<uint32_t> mask((size_t)p->tiles, 0);
+  if (hipMemcpyAsync(&nf, at<uint32_t>(ws, p, R_NF), 4, hipMemcpyDeviceToHost, s) != hipSuccess) return MVBEV_ERR_HIP;
+  if (p->frustum && hipMemcpyAsync(mask.data(), at<uint32_t>(ws, p, R_MASK), mask.size() * 4, hipMemcpyDeviceToHost,
+                                   s) != hipSuccess)
+    return MVBEV_ERR_HIP;
+  if (hipStreamSynchronize(s) != hipSuccess) return MVBEV_ERR_HIP;
+  p->wino = p->wino && nf == 0 ? 1 : 0;
+  if (p->frustum) {
+    // heavy-first run order: most active views first, equal view sets adjacent (ops.heavy_first_order)
+    const int64_t T = p->tiles, n = g.B * T;
+    std::vector<int32_t> order((size_t)n);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) {
+      const uint32_t ma = mask[(size_t)(a % T)], mb = mask[(size_t)(b % T)];
+      const int pa = __builtin_popcount(ma), pb = __builtin_popcount(mb);
+      if (pa != pb) return pa > pb;
+      if (ma != mb) return ma < mb;
+      return a < b;
+    });
+    if (hipMemcpyAsync(at<int32_t>(ws, p, R_ORDER), order.data(), order.size() * 4, hipMemcpyHostToDevice, s) !=
+        hipSuccess)
+      return MVBEV_ERR_HIP;
+    if (hipStreamSynchronize(s) != hipSuccess) return MVBEV_ERR_HIP;  // the host order buffer's lifetime
+  }
+  // weights: conv1 (G w for the Winograd form, or the direct pack), conv2, and the coord term
+  if (p->wino)
+    BEV_TRY(mvbev_pack_conv3x3_weight_wino(w1, kMid, cin, at<int32_t>(ws, p, R_MAP1), K, at<void>(ws, p, R_PACK1),
+                                           stream));
+  else
+    BEV_TRY(mvbev_pack_conv3x3_weight_bf16x3(w1, kMid, cin, at<int32_t>(ws, p, R_MAP1), K, at<void>(ws, p, R_PACK1),
+                                             stream));
+  BEV_TRY(mvbev_pack_conv3x3_weight_bf16x3(w2, kMid, kMid, nullptr, kMid, at<void>(ws, p, R_PACK2), stream));
+  BEV_TRY(mvbev_pack_conv3x3_weight_f32(w1, kMid, cin, at<int32_t>(ws, p, R_MAPC), kKC, at<float>(ws, p, R_PACKC),
+                                        stream));
+  float* cinp = at<float>(ws, p, R_CIN);
+  if (hipMemsetAsync(cinp, 0, (size_t)kKC * g.Ho * g.Wo * 4, s) != hipSuccess) return MVBEV_ERR_HIP;
+  const int64_t cst[4] = {kKC * g.Ho * g.Wo, g.Ho * g.Wo, g.Wo, 1};
+  BEV_TRY(mvbev_fill_coord_map_f32(cinp, 1, g.Ho, g.Wo, cst, stream));
+  mvbev_conv_desc dc;
+  dc.B = 1; dc.K = kKC; dc.H = g.Ho; dc.W = g.Wo; dc.group = kKC; dc.group_stride = 0;
+  dc.batch_stride = kKC * g.Ho * g.Wo; dc.in_row0 = 0; dc.in_rows = g.Ho; dc.out_row0 = 0; dc.out_rows = g.Ho;
+  // coord term = conv1 bias + conv1 over the two coord channels (:21, :77): input-independent
+  BEV_TRY(mvbev_conv3x3_f32(cinp, &dc, at<float>(ws, p, R_PACKC), b1, nullptr, kMid, 1, 0, at<float>(ws, p, R_INIT),
+                            stream));
+  // T / the slab: zero once; later warps skip the pixels whose samples fall outside the source
+  if (hipMemsetAsync(at<void>(ws, p, R_BIG), 0, p->off[R_BIG + 1] - p->off[R_BIG], s) != hipSuccess)
+    return MVBEV_ERR_HIP;
+  p->b2 = b2;
+  p->w3 = w3;
+  p->prepared = 1;
+  return MVBEV_OK;
+}
+
+int mvbev_bev_fuse(const mvbev_bev_plan* p, const void* const* views, float* map, void* ws, size_t ws_bytes,
+                   void* stream) {
+  if (!p || !views || !map || !ws) return MVBEV_ERR_NULL;
+  if (!p->prepared || ws_bytes < p->workspace_bytes) return MVBEV_ERR_SHAPE;
+  const mvbev_bev_geometry& g = p->g;
+  for (int v = 0; v < g.num_views; ++v)
+    if (!views[v]) return MVBEV_ERR_NULL;
+  mvbev_warp_view wv[MVBEV_BEV_MAX_VIEWS];
+  std::memset(wv, 0, sizeof(wv));
+  const mvbev_conv_desc d1 = conv1_desc(p), d2 = conv2_desc(p);
+  void* big = at<void>(ws, p, R_BIG);
+  const uint32_t* mask = p->frustum ? at<uint32_t>(ws, p, R_MASK) : nullptr;
+  const int32_t* order = p->frustum ? at<int32_t>(ws, p, R_ORDER) : nullptr;
+  const bool backbone = g.src_kind == MVBEV_BEV_SRC_BACKBONE_F32;
+  void* y1 = at<void>(ws, p, R_Y1);
+  // a4 + a5 + a6 (+ conv1's B^T): the warp of every view in one launch
+  if (p->wino) {
+    t_views(p, views, big, wv);
+    const int64_t r3 = 4 * ((g.Ho + 11) / 12);
+    if (backbone)
+      BEV_TRY(mvbev_warp_views_upsampled_wino_rows(wv, g.num_views, g.B, g.C, g.h, g.w, g.H, g.W, g.Ho, g.Wo, r3,
+                                                   MVBEV_WARP_DST_ZEROED, stream));
+    else
+      BEV_TRY(mvbev_warp_views_wino_rows(wv, g.num_views, g.B, g.C, g.H, g.W, g.Ho, g.Wo, r3, MVBEV_WARP_DST_ZEROED,
+                                         stream));
+  } else {
+    slab_views(p, views, big, wv);
+    if (backbone)
+      BEV_TRY(mvbev_warp_views_upsampled_ex(wv, g.num_views, 0, g.B, g.C, g.h, g.w, g.H, g.W, g.Ho, g.Wo,
+                                            MVBEV_LAYOUT_SPLIT_BF16, MVBEV_WARP_DST_ZEROED, stream));
+    else
+      BEV_TRY(mvbev_warp_views_split_bf16_ex(wv, g.num_views, g.src_kind == MVBEV_BEV_SRC_F16 ? 1 : 0, g.B, g.C, g.H,
+                                             g.W, g.Ho, g.Wo, MVBEV_WARP_DST_ZEROED, stream));
+  }
+  // a7: conv1 + coord term + bias + ReLU -> y1 (split-bf16, conv2's input)
+  if (p->wino)
+    BEV_TRY(mvbev_conv3x3_wino_bf16x3(big, &d1, at<void>(ws, p, R_PACK1), nullptr, at<float>(ws, p, R_INIT), kMid, 1,
+                                      y1, MVBEV_LAYOUT_SPLIT_BF16, mask, order, stream));
+  else
+    BEV_TRY(mvbev_conv3x3_bf16x3_ex(big, MVBEV_LAYOUT_SPLIT_BF16, &d1, at<void>(ws, p, R_PACK1), nullptr,
+                                    at<float>(ws, p, R_INIT), kMid, 1, 1, y1, MVBEV_LAYOUT_SPLIT_BF16, mask, order,
+                                    nullptr, 0, stream));
+  // a8 + a9: conv2 + ReLU with conv3's per-tap partials in its epilogue, then their reduce
+  void* p3 = at<void>(ws, p, R_P3);
+  static_assert(R_P3 == R_COUNT - 1, "the partials are the workspace's last region");
+  BEV_TRY(mvbev_conv3x3_bf16x3_cout1_partials(y1, &d2, at<void>(ws, p, R_PACK2), p->b2, kMid, 2, 1, p->w3, p3,
+                                              p->workspace_bytes - p->off[R_P3], stream));
+  BEV_TRY(mvbev_cout1_reduce_partials(p3, &d2, kMid, 4, map, 0, g.Ho, stream));
+  return MVBEV_OK;
+}
+
+}  // extern "C"

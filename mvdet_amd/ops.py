@@ -1099,3 +1099,60 @@ def conv3x3_cout1_backward(x: torch.Tensor, weight: torch.Tensor, dmap: torch.Te
         None if dw is None else dw.data_ptr(), _stream(x))
     _native.check(st, "mvbev_conv3x3_cout1_backward_ex")
     return dx, dw
+
+
+class BevFuse:
+    """The one-call C ABI of the inference hot path (``mvbev_bev_plan_init`` /
+    ``mvbev_bev_fuse_prepare`` / ``mvbev_bev_fuse``, include/mvbev.h): what a non-Python caller
+    binds instead of orchestrating the entry points.  ``m_norms``: per view the
+    host kornia src_norm <- dst_norm matrix; ``src_kind``: ``_native.BEV_SRC_*``."""
+
+    def __init__(self, m_norms, C: int, src_hw, grid_hw, B: int = 1, src_kind: int = 0, backbone_hw=None):
+        g = _native.BevGeometry()
+        g.num_views = len(m_norms)
+        g.src_kind = int(src_kind)
+        g.B, g.C = int(B), int(C)
+        g.H, g.W = (int(x) for x in src_hw)
+        g.Ho, g.Wo = (int(x) for x in grid_hw)
+        if backbone_hw is not None:
+            g.h, g.w = (int(x) for x in backbone_hw)
+        for v, m in enumerate(m_norms):
+            g.m[v] = (ctypes.c_float * 9)(*torch.as_tensor(m, dtype=torch.float32).reshape(9).tolist())
+        self.plan = _native.BevPlan()
+        _native.check(_native.load().mvbev_bev_plan_init(ctypes.byref(g), ctypes.byref(self.plan)),
+                      "mvbev_bev_plan_init")
+        self.ws: Optional[torch.Tensor] = None
+        self._keep = ()
+
+    @property
+    def wino(self) -> bool:
+        return bool(self.plan.wino)
+
+    def prepare(self, map_classifier, device) -> None:
+        """Once per weight version: ``map_classifier`` the reference's nn.Sequential (:51-54)."""
+        n = int(self.plan.workspace_bytes)
+        if self.ws is None or self.ws.numel() < n + 256:
+            self.ws = torch.empty(n + 256, dtype=torch.uint8, device=device)
+        base = self.ws.data_ptr()
+        self._base = base + (-base) % 256  # the ABI wants a 256-B aligned workspace
+        w = [map_classifier[0].weight, map_classifier[0].bias, map_classifier[2].weight, map_classifier[2].bias,
+             map_classifier[4].weight]
+        self._keep = tuple(t.detach().contiguous() for t in w)  # b2 / w3 are read again per frame
+        _require_cuda(*self._keep)
+        st = _native.load().mvbev_bev_fuse_prepare(ctypes.byref(self.plan), *[t.data_ptr() for t in self._keep],
+                                                   self._base, n, _stream(self.ws))
+        _native.check(st, "mvbev_bev_fuse_prepare")
+
+    def __call__(self, views, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        g = self.plan.g
+        if len(views) != g.num_views:
+            raise ValueError(f"need {g.num_views} views")
+        views = [v.contiguous() for v in views]
+        _require_cuda(*views)
+        if out is None:
+            out = torch.empty((g.B, 1, g.Ho, g.Wo), dtype=torch.float32, device=views[0].device)
+        arr = (ctypes.c_void_p * g.num_views)(*[v.data_ptr() for v in views])
+        st = _native.load().mvbev_bev_fuse(ctypes.byref(self.plan), arr, out.data_ptr(), self._base,
+                                           int(self.plan.workspace_bytes), _stream(out))
+        _native.check(st, "mvbev_bev_fuse")
+        return out

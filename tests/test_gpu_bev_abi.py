@@ -1,0 +1,142 @@
+"""The one-call C ABI (``mvbev_bev_plan_init`` / ``mvbev_bev_fuse_prepare`` / ``mvbev_bev_fuse``,
+SURVEY §8(b)) against the CPU oracle and against the Python engine that makes the same calls:
+fp32 sources at the config-2 rig (the bench's path), backbone-resolution sources (the
+detector's path, the 3x upsample of persp_trans_detector.py:65 fused), fp16 sources (the direct
+conv1), a degenerate camera (non-finite samples -> the direct conv1 and the reference's NaN
+pattern), and frames run back to back through one workspace."""
+import pytest
+import torch
+
+from helpers import assert_parity_t
+from oracle import cpu_path, fixtures
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _setup(ds, C, seed, B=1):
+    from mvdet_amd.geometry import projection_matrices
+    N = ds.num_cam
+    params = fixtures.head_params(N, seed=seed, C=C)
+    mc = torch.nn.Sequential(torch.nn.Conv2d(C * N + 2, 512, 3, padding=1), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False))
+    mc.load_state_dict({k.replace("map_classifier.", ""): torch.from_numpy(v) for k, v in params.items()
+                        if k.startswith("map_classifier.")})
+    tp = {k: torch.from_numpy(v) for k, v in params.items()}
+    return projection_matrices(ds), mc.to(DEV), tp
+
+
+def _engine_mats(pm, up, grid):
+    from mvdet_amd.geometry import kornia_src_norm_from_dst_norm
+    return [kornia_src_norm_from_dst_norm(M.float().reshape(1, 3, 3), up, grid)[0] for M in pm]
+
+
+def test_bev_fuse_cfg2_fp32_vs_oracle_and_engine():
+    """Config 2 (7 views, C = 512, 270 x 480 -> 120 x 360), fp32 sources: the fused warp + B^T,
+    the Winograd conv1, conv2 -> conv3 partials; bitwise the Python engine's map, within the
+    gate of the oracle; two frames through one workspace."""
+    from mvdet_amd import ProjectFuse, ops, synthetic
+    spec = synthetic.CONFIGS[2]
+    ds = spec["make"]()
+    C, N = spec["C"], ds.num_cam
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    pm, mc, tp = _setup(ds, C, seed=2)
+    bev = ops.BevFuse(_engine_mats(pm, up, grid), C, up, grid)
+    bev.prepare(mc, DEV)
+    assert bev.wino and bev.plan.frustum
+    eng = ProjectFuse(pm, up, grid, C)
+    for frame in range(2):
+        feats = [synthetic.synthetic_features(1, C, [u // 3 for u in up], up, seed=2000 + 10 * frame + v, device=DEV)
+                 for v in range(N)]
+        with torch.no_grad():
+            got = bev(feats).clone()
+            ref_eng = eng.project_fuse(feats, mc)
+            torch.cuda.synchronize()
+            ref = cpu_path.project_fuse([f.cpu() for f in feats], [M.numpy() for M in pm], grid, tp)
+        assert torch.equal(got, ref_eng), frame
+        assert_parity_t(got, ref, f"bev_fuse cfg2 frame {frame}", normwise_tol=5e-5)
+
+
+def test_bev_fuse_backbone_sources_vs_oracle():
+    """Backbone-resolution sources (the detector's inference path: upsample + warp + B^T in one
+    kernel), config 1's rig at C = 512, B = 2."""
+    from mvdet_amd import _native, ops, synthetic
+    ds = synthetic.CONFIGS[1]["make"]()
+    C, N, B = 512, ds.num_cam, 2
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    lo = [u // 3 for u in up]
+    pm, mc, tp = _setup(ds, C, seed=11, B=B)
+    bev = ops.BevFuse(_engine_mats(pm, up, grid), C, up, grid, B=B, src_kind=_native.BEV_SRC_BACKBONE_F32,
+                      backbone_hw=lo)
+    bev.prepare(mc, DEV)
+    low = [synthetic.backbone_features(B, C, lo, seed=70 + v, device=DEV) for v in range(N)]
+    with torch.no_grad():
+        got = bev(low)
+        torch.cuda.synchronize()
+        ref = cpu_path.project_fuse([cpu_path.upsample(f.cpu(), up) for f in low], [M.numpy() for M in pm], grid, tp)
+    assert bev.wino
+    assert_parity_t(got, ref, "bev_fuse backbone sources", normwise_tol=5e-5)
+
+
+def test_bev_fuse_fp16_sources_direct_conv1():
+    """fp16 sources (config 4's storage): the split slab from fp16 and the direct ring conv1."""
+    from mvdet_amd import _native, ops, synthetic
+    ds = synthetic.wildtrack_like(3, 4, seed=4, img_shape=(216, 384), worldgrid_shape=(96, 288))
+    C, N, B = 64, 3, 2
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    pm, mc, tp = _setup(ds, C, seed=4, B=B)
+    bev = ops.BevFuse(_engine_mats(pm, up, grid), C, up, grid, B=B, src_kind=_native.BEV_SRC_F16)
+    bev.prepare(mc, DEV)
+    assert not bev.wino
+    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=40 + v, device=DEV).half()
+             for v in range(N)]
+    with torch.no_grad():
+        got = bev(feats)
+        torch.cuda.synchronize()
+        ref = cpu_path.project_fuse([f.float().cpu() for f in feats], [M.numpy() for M in pm], grid, tp)
+    assert_parity_t(got, ref, "bev_fuse fp16 sources", normwise_tol=5e-5)
+
+
+def test_bev_fuse_degenerate_camera_nan_pattern():
+    """A camera whose homography overflows fp32 on part of the grid: prepare detects it, plans
+    the direct conv1, and the map's NaN pattern is the oracle's."""
+    from mvdet_amd import _native, ops, synthetic
+    ds = synthetic.wildtrack_like(3, 4, seed=0, img_shape=(216, 384), worldgrid_shape=(96, 288))
+    K = [k.copy() for k in ds.base.intrinsic_matrices]
+    K[1][:2, :] *= 4e35
+    ds.base.intrinsic_matrices = tuple(K)
+    C, N = 512, 3
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    lo = [u // 3 for u in up]
+    pm, mc, tp = _setup(ds, C, seed=7)
+    bev = ops.BevFuse(_engine_mats(pm, up, grid), C, up, grid, src_kind=_native.BEV_SRC_BACKBONE_F32,
+                      backbone_hw=lo)
+    bev.prepare(mc, DEV)
+    assert not bev.wino
+    low = [synthetic.backbone_features(1, C, lo, seed=90 + v, device=DEV) for v in range(N)]
+    with torch.no_grad():
+        got = bev(low)
+        torch.cuda.synchronize()
+        ref = cpu_path.project_fuse([cpu_path.upsample(f.cpu(), up) for f in low], [M.numpy() for M in pm], grid, tp)
+    assert 0 < int(torch.isnan(ref).sum()) < ref.numel()
+    assert_parity_t(got, ref, "bev_fuse degenerate camera (NaN pattern included)")
+
+
+def test_bev_fuse_refusals():
+    import ctypes
+    from mvdet_amd import _native, ops
+    bev = ops.BevFuse([torch.eye(3)] * 2, 16, (20, 30), (10, 12))
+    lib = _native.load()
+    out = torch.empty((1, 1, 10, 12), device=DEV)
+    arr = (ctypes.c_void_p * 2)(0, 0)
+    # not prepared yet
+    assert lib.mvbev_bev_fuse(ctypes.byref(bev.plan), arr, out.data_ptr(), out.data_ptr(), 4, None) == _native.ERR_SHAPE
+    ws = torch.empty(int(bev.plan.workspace_bytes) + 512, dtype=torch.uint8, device=DEV)
+    base = ws.data_ptr() + (-ws.data_ptr()) % 256
+    # a workspace smaller than the plan's, or misaligned
+    w = torch.zeros((512, 34, 3, 3), device=DEV)
+    assert lib.mvbev_bev_fuse_prepare(ctypes.byref(bev.plan), w.data_ptr(), None, w.data_ptr(), None, w.data_ptr(),
+                                      base, 16, None) == _native.ERR_SHAPE
+    assert lib.mvbev_bev_fuse_prepare(ctypes.byref(bev.plan), w.data_ptr(), None, w.data_ptr(), None, w.data_ptr(),
+                                      base + 4, int(bev.plan.workspace_bytes), None) == -4  # MVBEV_ERR_ALIGN

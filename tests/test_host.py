@@ -143,3 +143,37 @@ def test_schedule_plan_covers_every_chunk_once():
         if t >= 0:
             assert (c0, slot) == (0, -1)
             assert all(j % 8 == i % 8 for j, it in enumerate(its) if it[0] >= 0 and it[0] // 4 == t // 4)
+
+
+def test_bev_fuse_structs_and_plan_match_the_header(tmp_path):
+    """The one-call ABI's structs: ctypes layout == the C header's (compiled here with g++), and
+    mvbev_bev_plan_init (host only, no GPU) lays out a workspace whose regions are 256-B aligned,
+    in order, and hold T or the slab for the config-2 geometry."""
+    import ctypes
+    import subprocess
+    from mvdet_amd import _native
+    src = tmp_path / "sz.cpp"
+    src.write_text('#include <cstdio>\n#include <cstddef>\n#include "mvbev.h"\n'
+                   'int main(){printf("%zu %zu %zu %zu\\n", sizeof(mvbev_bev_geometry), sizeof(mvbev_bev_plan),'
+                   ' offsetof(mvbev_bev_plan, off), offsetof(mvbev_bev_plan, w3));}\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["g++", "-I", str(Path(__file__).resolve().parents[1] / "include"), str(src), "-o", str(exe)],
+                   check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert got == [ctypes.sizeof(_native.BevGeometry), ctypes.sizeof(_native.BevPlan),
+                   _native.BevPlan.off.offset, _native.BevPlan.w3.offset]
+    g = _native.BevGeometry()
+    g.num_views, g.src_kind, g.B, g.C, g.H, g.W, g.Ho, g.Wo = 7, _native.BEV_SRC_F32, 1, 512, 270, 480, 120, 360
+    plan = _native.BevPlan()
+    lib = _native.load()
+    assert lib.mvbev_bev_plan_init(ctypes.byref(g), ctypes.byref(plan)) == 0
+    offs = list(plan.off)[:13]
+    assert offs == sorted(offs) and all(o % 256 == 0 for o in offs)
+    assert plan.Cs == 512 and plan.frustum == 1 and plan.wino == 1 and plan.tiles == 10 * 12
+    t_bytes = 1 * (7 * 512 // 8) * 5 * 4 * 10 * 360 * 32  # mvbev_wino_rows_bytes: 5/3 of the slab's rows
+    assert offs[11] - offs[10] >= max(t_bytes, 7 * 512 * 120 * 360 * 4)
+    assert lib.mvbev_bev_fuse_workspace_bytes(ctypes.byref(g)) == plan.workspace_bytes
+    g.src_kind = _native.BEV_SRC_F16  # fp16 sources: the direct conv1 on the split slab
+    assert lib.mvbev_bev_plan_init(ctypes.byref(g), ctypes.byref(plan)) == 0 and plan.wino == 0
+    g.num_views = 17
+    assert lib.mvbev_bev_plan_init(ctypes.byref(g), ctypes.byref(plan)) == _native.ERR_SHAPE

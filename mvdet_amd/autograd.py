@@ -76,7 +76,8 @@ def _train_workspace(engine: ProjectFuse, B: int, device) -> Workspace:
         y1 = torch.empty((B, engine.mid, H, W), dtype=torch.float32, device=device)
     y2 = torch.empty((B, engine.mid, H, W), dtype=torch.float32, device=device)
     m = engine.m_norm_cpu.to(device)[:, None].expand(engine.num_cam, B, 3, 3).contiguous()
-    return Workspace(slab, y1, y2, m, (0, H), y1r, y2r, slab_zeroed=zeroed, store_y2=True)
+    return Workspace(slab, y1, y2, m, (0, H), y1r, y2r, slab_zeroed=zeroed, store_y2=True,
+                     slab_rows=(0, H))
 
 
 def _slab_pool(engine: ProjectFuse, B: int, device) -> list:

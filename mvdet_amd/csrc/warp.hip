@@ -153,10 +153,21 @@ __global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_tile_kernel(const Warp
 // in 32-B units: dB per item, dC per 8-channel group, dH per T row).  The slab itself is never
 // written.  skip_zero: a (tile, column) whose 5 samples all fall outside the source is not
 // written (T is zero-filled once and only ever written by this geometry).
+// LDS staging (round 3), as warp_up_wino_kernel: the block's bilinear corners span a source box
+// of ~330 upsampled pixels at cfg2 (median; the TA/TD load path was 84 % busy gathering them as
+// two 8-B corner pairs per channel and pixel); when the box holds at most kWwStage pixels it is
+// loaded once per channel with contiguous row loads into LDS and the corners are read from there.
+#ifndef MVBEV_WW_STAGE
+#define MVBEV_WW_STAGE 384  // max staged box pixels per channel (8 channels x 384 x 4 B = 12 KiB); 0 = off
+#endif
+constexpr int kWwStage = MVBEV_WW_STAGE;
+
 template <bool PAIR>
-__global__ __launch_bounds__(kWwThreads) void warp_wino_kernel(const WarpArgs a, int r3_rows) {
-  __shared__ float ds[kWwRows][kWwCols][9];  // [row][col][channel] (+1 pad)
+__global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(const WarpArgs a, int r3_rows) {
+  __shared__ __attribute__((aligned(16))) float ds[kWwRows][kWwCols][8];  // [row][col][channel]
   __shared__ unsigned char nz[kWwRows][kWwCols];
+  __shared__ float stage[kWarpCPB * (kWwStage > 0 ? kWwStage : 1)];
+  __shared__ int box[4];  // source rows [box0, box1], columns [box2, box3] of the block's corners
   const int lb = xcd_remap(blockIdx.x, a.nwg);
   const int tile = lb % a.tiles;
   const int chunk = (lb / a.tiles) % a.chunks;
@@ -169,48 +180,109 @@ __global__ __launch_bounds__(kWwThreads) void warp_wino_kernel(const WarpArgs a,
   const int c_end = min(a.C, c_begin + kWarpCPB);
   const int H = a.H, W = a.W;
   const int tid = threadIdx.x;
-  {  // phase 1: one warped pixel (8 channels) per thread
-    const int i = tid / kWwCols, c = tid % kWwCols;  // 16 x kWwCols threads, rows >= 14 idle
-    const int v = 12 * k - 1 + i, u = tx * kWwCols + c;
-    if (i < kWwRows) {
-      float d[8];
+  const int i = tid / kWwCols, c = tid % kWwCols;  // 16 x kWwCols threads, rows >= 14 idle
+  const int v = 12 * k - 1 + i, u = tx * kWwCols + c;
+  const bool live = i < kWwRows && v >= 0 && v < a.Ho && u < a.Wo;
+  if (tid == 0) {
+    box[0] = INT32_MAX;
+    box[1] = -1;
+    box[2] = INT32_MAX;
+    box[3] = -1;
+  }
+  WarpCoord wc;
+  wc.inside = false;
+  wc.finite = true;
+  wc.ix = wc.iy = 0.f;
+  if (live) {
+    float m[9];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = 0.f;
-      bool any = false;
-      if (v >= 0 && v < a.Ho && u < a.Wo) {
-        float m[9];
+    for (int q = 0; q < 9; ++q) m[q] = vw.m[q];
+    wc = warp_coord(m, u, v, a.Ho, a.Wo, H, W);
+  }
+  const float ix = wc.ix, iy = wc.iy;
+  const float fx0 = floorf(ix), fy0 = floorf(iy);
+  const int x0 = wc.inside ? (int)fx0 : 0, y0 = wc.inside ? (int)fy0 : 0;
+  const int cx0 = max(x0, 0), cy0 = max(y0, 0);
+  const int cx1 = min(x0 + 1, W - 1), cy1 = min(y0 + 1, H - 1);
+  __syncthreads();
+  if (kWwStage > 0) {  // the box: a shuffle reduction per wave, then one LDS atomic per wave and bound
+    int r0 = wc.inside ? cy0 : INT32_MAX, r1 = wc.inside ? cy1 : -1;
+    int q0 = wc.inside ? cx0 : INT32_MAX, q1 = wc.inside ? cx1 : -1;
 #pragma unroll
-        for (int q = 0; q < 9; ++q) m[q] = vw.m[q];
-        const WarpCoord wc = warp_coord(m, u, v, a.Ho, a.Wo, H, W);
-        if (!wc.inside) {
-          if (!wc.finite) {
-            any = true;
+    for (int o = 32; o > 0; o >>= 1) {
+      r0 = min(r0, __shfl_xor(r0, o));
+      r1 = max(r1, __shfl_xor(r1, o));
+      q0 = min(q0, __shfl_xor(q0, o));
+      q1 = max(q1, __shfl_xor(q1, o));
+    }
+    if ((tid & 63) == 0 && r1 >= 0) {
+      atomicMin(&box[0], r0);
+      atomicMax(&box[1], r1);
+      atomicMin(&box[2], q0);
+      atomicMax(&box[3], q1);
+    }
+  }
+  __syncthreads();
+  const int R = box[1] - box[0] + 1, Cb = box[3] - box[2] + 1;
+  const bool staged = kWwStage > 0 && box[1] >= 0 && R * Cb <= kWwStage;  // uniform per block
+  const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
+  if (staged) {  // the box of every channel of the group: rows of Cb floats, 32 lanes a row
+    const int n = R * Cb;
+    for (int r = tid / 32; r < R; r += kWwThreads / 32)
+      for (int cc = tid % 32; cc < Cb; cc += 32) {
+        float t[kWarpCPB];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) d[j] = c_begin + j < c_end ? __builtin_nanf("") : 0.f;
+        for (int j = 0; j < kWarpCPB; ++j)
+          t[j] = base[(int64_t)min(c_begin + j, c_end - 1) * vw.sC + (int64_t)(box[0] + r) * vw.sH +
+                      (int64_t)(box[2] + cc) * vw.sW];
+#pragma unroll
+        for (int j = 0; j < kWarpCPB; ++j) stage[j * n + r * Cb + cc] = t[j];
+      }
+    __syncthreads();
+  }
+  if (i < kWwRows) {  // phase 1: one warped pixel (8 channels) per thread
+    float d[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = 0.f;
+    bool any = false;
+    if (live) {
+      if (!wc.inside) {
+        if (!wc.finite) {
+          any = true;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) d[j] = c_begin + j < c_end ? __builtin_nanf("") : 0.f;
+        }
+      } else {
+        any = true;
+        const float fx1 = fx0 + 1.f, fy1 = fy0 + 1.f;
+        const float w_nw = (fx1 - ix) * (fy1 - iy), w_ne = (ix - fx0) * (fy1 - iy);
+        const float w_sw = (fx1 - ix) * (iy - fy0), w_se = (ix - fx0) * (iy - fy0);
+        const bool vx0 = x0 >= 0, vx1 = x0 + 1 <= W - 1, vy0 = y0 >= 0, vy1 = y0 + 1 <= H - 1;
+        const bool ok_nw = vx0 && vy0, ok_ne = vx1 && vy0, ok_sw = vx0 && vy1, ok_se = vx1 && vy1;
+        if (staged) {
+          const int n = R * Cb;
+          const int t0 = (cy0 - box[0]) * Cb, t1 = (cy1 - box[0]) * Cb;
+          const int l0 = cx0 - box[2], l1 = cx1 - box[2];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float* sj = stage + j * n;
+            float acc = 0.f;
+            acc += (ok_nw ? sj[t0 + l0] : 0.f) * w_nw;
+            acc += (ok_ne ? sj[t0 + l1] : 0.f) * w_ne;
+            acc += (ok_sw ? sj[t1 + l0] : 0.f) * w_sw;
+            acc += (ok_se ? sj[t1 + l1] : 0.f) * w_se;
+            d[j] = c_begin + j < c_end ? acc : 0.f;
           }
         } else {
-          any = true;
-          const float ix = wc.ix, iy = wc.iy;
-          const float fx0 = floorf(ix), fy0 = floorf(iy);
-          const int x0 = (int)fx0, y0 = (int)fy0;
-          const float fx1 = fx0 + 1.f, fy1 = fy0 + 1.f;
-          const float w_nw = (fx1 - ix) * (fy1 - iy), w_ne = (ix - fx0) * (fy1 - iy);
-          const float w_sw = (fx1 - ix) * (iy - fy0), w_se = (ix - fx0) * (iy - fy0);
-          const bool vx0 = x0 >= 0, vx1 = x0 + 1 <= W - 1, vy0 = y0 >= 0, vy1 = y0 + 1 <= H - 1;
-          const bool ok_nw = vx0 && vy0, ok_ne = vx1 && vy0, ok_sw = vx0 && vy1, ok_se = vx1 && vy1;
-          const int cx0 = max(x0, 0), cy0 = max(y0, 0);
-          const int cx1 = min(x0 + 1, W - 1), cy1 = min(y0 + 1, H - 1);
           const int64_t sH = vw.sH, sW = vw.sW, sC = vw.sC;
           const int bx = min(max(x0, 0), W - 2);
           const int64_t o_top = cy0 * sH + bx, o_bot = cy1 * sH + bx;
           const bool nw_lo = x0 == bx, ne_lo = x0 + 1 == bx;
           const int64_t o_nw = cy0 * sH + cx0 * sW, o_ne = cy0 * sH + cx1 * sW;
           const int64_t o_sw = cy1 * sH + cx0 * sW, o_se = cy1 * sH + cx1 * sW;
-          const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int ch = c_begin + j;
-            if (ch >= c_end) break;
+          for (int j = 0; j < 8; ++j) {  // straight-line (a short last group re-reads its last channel)
+            const int ch = min(c_begin + j, c_end - 1);
             const float* pc = base + (int64_t)ch * sC;
             float vnw, vne, vsw, vse;
             if constexpr (PAIR) {
@@ -228,14 +300,14 @@ __global__ __launch_bounds__(kWwThreads) void warp_wino_kernel(const WarpArgs a,
             acc += (ok_ne ? vne : 0.f) * w_ne;
             acc += (ok_sw ? vsw : 0.f) * w_sw;
             acc += (ok_se ? vse : 0.f) * w_se;
-            d[j] = acc;
+            d[j] = c_begin + j < c_end ? acc : 0.f;
           }
         }
       }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ds[i][c][j] = d[j];
-      nz[i][c] = any;
     }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ds[i][c][j] = d[j];
+    nz[i][c] = any;
   }
   __syncthreads();
   wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);

@@ -191,39 +191,66 @@ __device__ inline UpWindow up_window(const float (&m)[9], int u, int v, int Ho, 
 
 // Warp + row-Winograd transform kernels (warp_wino_kernel, warp_up_wino_kernel): a block warps
 // the kWwRows input rows 12 k - 1 + i of 4 three-row output tiles x kWwCols columns of one
-// view's 8-channel group into LDS (ds, nz = some sample non-zero), then this phase stores, per
-// (tile, column, xi), the transformed row B^T d (points 0, 1, -1, 2, inf; the rows of
-// wino_rows_kernel in conv_bf16x3.hip) split-bf16 at T row 5 r3 + xi (vw.dst strides in 32-B
-// units: dB per item, dC per 8-channel group, dH per T row).  skip_zero: a (tile, column) whose 5
-// samples are all outside the source is not written (T zero-filled, written only by this geometry).
+// view's 8-channel group into LDS (ds[row][col][channel], nz = some sample non-zero), then this
+// phase stores the transformed rows B^T d (points 0, 1, -1, 2, inf; the rows of wino_rows_kernel
+// in conv_bf16x3.hip) split-bf16 at T rows 5 r3 + xi (vw.dst strides in 32-B units: dB per item,
+// dC per 8-channel group, dH per T row).  One thread per (tile, column, channel pair) computes
+// all 5 rows of its 2 channels (the 5 input rows read once, no per-row branching) and writes
+// its 4 bytes of each row's hi[8] and lo[8] (the 4 threads of a column fill the 32-B entry; a
+// wave covers 16 consecutive columns: 512 contiguous bytes per row).  skip_zero: a (tile,
+// column) whose 5 samples are all outside the source is not written (T zero-filled, written only
+// by this geometry).
 #ifndef MVBEV_WW_COLS
 #define MVBEV_WW_COLS 16  // columns per fused-warp block (threads = 16 x columns; cfg2: 8 0.52-0.56 ms, 16 0.51)
 #endif
 constexpr int kWwRows = 14, kWwCols = MVBEV_WW_COLS, kWwThreads = 16 * kWwCols;
+// (several 8-channel groups per block, the sample geometry computed once for all of them, measured
+// no faster at cfg2: 1 group 0.463 / 0.521 ms up / plain, 2 groups 0.462 / 0.538, 4 0.466 / 0.544 —
+// the geometry's VALU work is not what binds these kernels; the TA/TD load path is: 77-84 % busy)
 static_assert(kWarpCPB == 8 && kUpCPB == 8, "one 8-channel group per warp block");
-__device__ inline void wino_rows_phase2(const float (&ds)[kWwRows][kWwCols][9], const unsigned char (&nz)[kWwRows][kWwCols],
+static_assert(4 * kWwCols * 4 == kWwThreads, "phase 2: one (tile, column, channel pair) per thread");
+#ifndef MVBEV_WARP_WPE
+#define MVBEV_WARP_WPE 8  // waves per SIMD asked of the compiler (caps VGPRs at 512 / WPE; 8: 72 -> 64, measured -4 %); 0 = free
+#endif
+#if MVBEV_WARP_WPE > 0
+#define MVBEV_WARP_OCC __attribute__((amdgpu_waves_per_eu(MVBEV_WARP_WPE, MVBEV_WARP_WPE)))
+#else
+#define MVBEV_WARP_OCC
+#endif
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+__device__ inline unsigned pack_bf16x2(float x, float y) {
+  return (unsigned)__builtin_bit_cast(unsigned short, (__bf16)x) |
+         ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)y) << 16);
+}
+
+__device__ inline void wino_rows_phase2(const float (&ds)[kWwRows][kWwCols][8], const unsigned char (&nz)[kWwRows][kWwCols],
                                         const WarpView& vw, const WarpArgs& a, int b, int chunk, int k, int tx,
                                         int r3_rows) {
-  for (int it = threadIdx.x; it < 4 * kWwCols * 5; it += blockDim.x) {
-    const int xi = it / (4 * kWwCols), q = (it / kWwCols) % 4, c = it % kWwCols;
-    const int r3 = 4 * k + q, u = tx * kWwCols + c;
-    if (r3 >= r3_rows || u >= a.Wo) continue;
-    const int i0 = 3 * q;  // rows i0 .. i0 + 4 of the block
-    if (a.skip_zero && !(nz[i0][c] | nz[i0 + 1][c] | nz[i0 + 2][c] | nz[i0 + 3][c] | nz[i0 + 4][c])) continue;
-    float t[8];
+  const int it = threadIdx.x;
+  const int cp = it & 3, c = (it >> 2) % kWwCols, q = it / (4 * kWwCols);
+  const int r3 = 4 * k + q, u = tx * kWwCols + c;
+  if (r3 >= r3_rows || u >= a.Wo) return;
+  const int i0 = 3 * q;  // rows i0 .. i0 + 4 of the block
+  if (a.skip_zero && !(nz[i0][c] | nz[i0 + 1][c] | nz[i0 + 2][c] | nz[i0 + 3][c] | nz[i0 + 4][c])) return;
+  f32x2_t d[5];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float d0 = ds[i0][c][j], d1 = ds[i0 + 1][c][j], d2 = ds[i0 + 2][c][j], d3 = ds[i0 + 3][c][j],
-                  d4 = ds[i0 + 4][c][j];
-      t[j] = xi == 0 ? 2.f * d0 - d1 - 2.f * d2 + d3
-           : xi == 1 ? -2.f * d1 - d2 + d3
-           : xi == 2 ? 2.f * d1 - 3.f * d2 + d3
-           : xi == 3 ? d3 - d1
-                     : 2.f * d1 - d2 - 2.f * d3 + d4;
-    }
-    u32x4_t* out = static_cast<u32x4_t*>(vw.dst) + 2 * ((int64_t)b * vw.dB + (int64_t)chunk * vw.dC +
-                                                       (int64_t)(5 * r3 + xi) * vw.dH + u);
-    store_split8(out, t);
+  for (int m = 0; m < 5; ++m) d[m] = *reinterpret_cast<const f32x2_t*>(&ds[i0 + m][c][2 * cp]);
+  f32x2_t t[5];
+  t[0] = 2.f * d[0] - d[1] - 2.f * d[2] + d[3];
+  t[1] = -2.f * d[1] - d[2] + d[3];
+  t[2] = 2.f * d[1] - 3.f * d[2] + d[3];
+  t[3] = d[3] - d[1];
+  t[4] = 2.f * d[1] - d[2] - 2.f * d[3] + d[4];
+  unsigned* out = reinterpret_cast<unsigned*>(static_cast<u32x4_t*>(vw.dst) +
+                                              2 * ((int64_t)b * vw.dB + (int64_t)chunk * vw.dC +
+                                                   (int64_t)(5 * r3) * vw.dH + u)) + cp;
+#pragma unroll
+  for (int xi = 0; xi < 5; ++xi) {
+    const float h0 = (float)(__bf16)t[xi].x, h1 = (float)(__bf16)t[xi].y;
+    unsigned* o = out + (int64_t)xi * vw.dH * 8;  // 8 dwords per 32-B unit
+    o[0] = pack_bf16x2(h0, h1);
+    o[4] = pack_bf16x2(t[xi].x - h0, t[xi].y - h1);
   }
 }
 

@@ -134,10 +134,23 @@ __global__ __launch_bounds__(kUpTH * kUpTW) void warp_up_kernel(const UpArgs ua)
 // Fused 3x upsample + warp + row-Winograd transform (inference conv1 from backbone-resolution
 // maps, the detector's path): phase 1 warps the block's 14 input rows as warp_up_kernel samples
 // them (fp32 source, 16-B window rows), phase 2 is wino_rows_phase2 (warp_common.h).
-static_assert(kUpCPB == 8, "one 8-channel group per block");
-__global__ __launch_bounds__(kWwThreads) void warp_up_wino_kernel(const UpArgs ua, int r3_rows) {
-  __shared__ float ds[kWwRows][kWwCols][9];
+// LDS staging (round 3): the TA/TD load path bound the first version (77-80 % busy at cfg2): every
+// thread gathered its 3 window rows of 16 B per channel through L1, although a block's 14 x 16
+// output pixels sample a source box of only ~85 backbone pixels (median at cfg2; <= 512 for 94 %
+// of the work).  Now the block first reduces its pixels' windows to that box and, when the box
+// holds at most kUpStage pixels, loads it once per channel with contiguous row loads into LDS;
+// the windows are then read from LDS (the 3 columns of the window, ds reads).  Larger boxes (the
+// near field) keep the direct 16-B window loads.  Same weights, same summation order per tap.
+#ifndef MVBEV_UPW_STAGE
+#define MVBEV_UPW_STAGE 384  // max staged box pixels per channel (8 channels x 384 x 4 B = 12 KiB); 0 = off
+#endif
+constexpr int kUpStage = MVBEV_UPW_STAGE;
+
+__global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino_kernel(const UpArgs ua, int r3_rows) {
+  __shared__ __attribute__((aligned(16))) float ds[kWwRows][kWwCols][8];
   __shared__ unsigned char nz[kWwRows][kWwCols];
+  __shared__ float stage[kUpCPB * (kUpStage > 0 ? kUpStage : 1)];
+  __shared__ int box[4];  // source rows [box0, box1], columns [box2, box3] of the block's windows
   const WarpArgs& a = ua.w;
   const int lb = xcd_remap(blockIdx.x, a.nwg);
   const int tile = lb % a.tiles;
@@ -150,59 +163,127 @@ __global__ __launch_bounds__(kWwThreads) void warp_up_wino_kernel(const UpArgs u
   const int c_begin = chunk * kUpCPB;
   const int c_end = min(a.C, c_begin + kUpCPB);
   const int H = a.H, W = a.W, h = ua.h, w = ua.sw;
-  {
-    const int i = threadIdx.x / kWwCols, c = threadIdx.x % kWwCols;
-    const int v = 12 * k - 1 + i, u = tx * kWwCols + c;
-    if (i < kWwRows) {
-      float d[8];
+  const int tid = threadIdx.x;
+  const int i = tid / kWwCols, c = tid % kWwCols;
+  const int v = 12 * k - 1 + i, u = tx * kWwCols + c;
+  const bool live = i < kWwRows && v >= 0 && v < a.Ho && u < a.Wo;
+  if (tid == 0) {
+    box[0] = INT32_MAX;
+    box[1] = -1;
+    box[2] = INT32_MAX;
+    box[3] = -1;
+  }
+  UpWindow uw;
+  uw.inside = false;
+  uw.finite = true;
+  if (live) {
+    float m[9];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d[j] = 0.f;
-      bool any = false;
-      if (v >= 0 && v < a.Ho && u < a.Wo) {
-        float m[9];
+    for (int q = 0; q < 9; ++q) m[q] = vw.m[q];
+    uw = up_window(m, u, v, a.Ho, a.Wo, H, W, h, w, ua.sy, ua.sx);
+  }
+  __syncthreads();
+  if (kUpStage > 0) {  // the box: a shuffle reduction per wave, then one LDS atomic per wave and bound
+    int r0 = uw.inside ? uw.rb : INT32_MAX, r1 = uw.inside ? min(uw.rb + 2, h - 1) : -1;
+    int q0 = uw.inside ? uw.cb : INT32_MAX, q1 = uw.inside ? min(uw.cb + 2, w - 1) : -1;
 #pragma unroll
-        for (int q = 0; q < 9; ++q) m[q] = vw.m[q];
-        const UpWindow uw = up_window(m, u, v, a.Ho, a.Wo, H, W, h, w, ua.sy, ua.sx);
-        if (!uw.inside) {
-          if (!uw.finite) {
-            any = true;
+    for (int o = 32; o > 0; o >>= 1) {
+      r0 = min(r0, __shfl_xor(r0, o));
+      r1 = max(r1, __shfl_xor(r1, o));
+      q0 = min(q0, __shfl_xor(q0, o));
+      q1 = max(q1, __shfl_xor(q1, o));
+    }
+    if ((tid & 63) == 0 && r1 >= 0) {
+      atomicMin(&box[0], r0);
+      atomicMax(&box[1], r1);
+      atomicMin(&box[2], q0);
+      atomicMax(&box[3], q1);
+    }
+  }
+  __syncthreads();
+  const int R = box[1] - box[0] + 1, Cb = box[3] - box[2] + 1;
+  const bool staged = kUpStage > 0 && box[1] >= 0 && R * Cb <= kUpStage;  // uniform per block
+  const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
+  if (staged) {  // the box of every channel of the group: rows of Cb contiguous floats, 32 lanes a row
+    const int n = R * Cb;
+    for (int r = tid / 32; r < R; r += kWwThreads / 32)
+      for (int cc = tid % 32; cc < Cb; cc += 32) {
+        float t[kUpCPB];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) d[j] = c_begin + j < c_end ? __builtin_nanf("") : 0.f;
-          }
-        } else {
+        for (int j = 0; j < kUpCPB; ++j)
+          t[j] = base[(int64_t)min(c_begin + j, c_end - 1) * vw.sC + (int64_t)(box[0] + r) * vw.sH + box[2] + cc];
+#pragma unroll
+        for (int j = 0; j < kUpCPB; ++j) stage[j * n + r * Cb + cc] = t[j];
+      }
+    __syncthreads();
+  }
+  if (i < kWwRows) {
+    float d[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = 0.f;
+    bool any = false;
+    if (live) {
+      if (!uw.inside) {
+        if (!uw.finite) {
           any = true;
-          const int cb = uw.cb, rb = uw.rb;
-          const int c4 = min(cb, w - 4);
-          const int sh = cb - c4;
-          float bx[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int kk = j - sh;
-            bx[j] = (kk == 0 ? uw.ax[0] : 0.f) + (kk == 1 ? uw.ax[1] : 0.f) + (kk == 2 ? uw.ax[2] : 0.f);
+          for (int j = 0; j < 8; ++j) d[j] = c_begin + j < c_end ? __builtin_nanf("") : 0.f;
+        }
+      } else if (staged) {
+        any = true;
+        const int n = R * Cb;
+        int idx[3][3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+            idx[r][q] = (min(uw.rb + r, h - 1) - box[0]) * Cb + (min(uw.cb + q, w - 1) - box[2]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float* sj = stage + j * n;
+          float acc = 0.f;
+#pragma unroll
+          for (int r = 0; r < 3; ++r) {
+            float rr = 0.f;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) rr += uw.ax[q] * sj[idx[r][q]];
+            acc += uw.ay[r] * rr;
           }
-          int64_t off[3];
+          d[j] = c_begin + j < c_end ? acc : 0.f;
+        }
+      } else {
+        any = true;
+        const int cb = uw.cb, rb = uw.rb;
+        const int c4 = min(cb, w - 4);
+        const int sh = cb - c4;
+        float bx[4];
 #pragma unroll
-          for (int r = 0; r < 3; ++r) off[r] = min(rb + r, h - 1) * vw.sH + c4;
-          const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
+        for (int j = 0; j < 4; ++j) {
+          const int kk = j - sh;
+          bx[j] = (kk == 0 ? uw.ax[0] : 0.f) + (kk == 1 ? uw.ax[1] : 0.f) + (kk == 2 ? uw.ax[2] : 0.f);
+        }
+        int64_t off[3];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int ch = c_begin + j;
-            if (ch >= c_end) break;
-            const float* pc = base + (int64_t)ch * vw.sC;
-            float acc = 0.f;
+        for (int r = 0; r < 3; ++r) off[r] = min(rb + r, h - 1) * vw.sH + c4;
+        // straight-line over the group's 8 channels (a short last group reads its last channel
+        // again and zeroes the surplus): all 24 window loads issue before the FMAs
 #pragma unroll
-            for (int r = 0; r < 3; ++r) {
-              const f32x4u_t q = *reinterpret_cast<const f32x4u_t*>(pc + off[r]);
-              acc += uw.ay[r] * (bx[0] * q.x + bx[1] * q.y + bx[2] * q.z + bx[3] * q.w);
-            }
-            d[j] = acc;
+        for (int j = 0; j < 8; ++j) {
+          const int ch = min(c_begin + j, c_end - 1);
+          const float* pc = base + (int64_t)ch * vw.sC;
+          float acc = 0.f;
+#pragma unroll
+          for (int r = 0; r < 3; ++r) {
+            const f32x4u_t q = *reinterpret_cast<const f32x4u_t*>(pc + off[r]);
+            acc += uw.ay[r] * (bx[0] * q.x + bx[1] * q.y + bx[2] * q.z + bx[3] * q.w);
           }
+          d[j] = c_begin + j < c_end ? acc : 0.f;
         }
       }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ds[i][c][j] = d[j];
-      nz[i][c] = any;
     }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ds[i][c][j] = d[j];
+    nz[i][c] = any;
   }
   __syncthreads();
   wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);

@@ -1527,6 +1527,9 @@ __global__ __launch_bounds__(256) void wino_rows_kernel(const WinoRowsArgs a) {
   }
 }
 
+#ifndef MVBEV_WINO_WALK
+#define MVBEV_WINO_WALK 0  // 1: channel groups walked most-common-first (see conv_wino_kernel)
+#endif
 #ifndef MVBEV_WINO_ABL
 #define MVBEV_WINO_ABL 0  // timing ablations only (wrong results): bit 0 no unit barrier / wait, bit 1 no DMA in the loop
 #endif
@@ -1558,12 +1561,54 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   const int64_t wchunk = (int64_t)a.n_cot * wino::W16;
   const uint32_t gm = a.gmask ? a.gmask[pp] : 0u;
   const int nch = a.gmask ? __builtin_popcount(gm) * a.cpg : a.nchunks;
+#if MVBEV_WINO_WALK
+  // walk the tile's channel groups most-common-first (over all pixel tiles' masks): workgroups
+  // that run side by side on an XCD then stream the same weight chunks at the same time
+  uint64_t perm = 0xfedcba9876543210ull;
+  uint32_t pm = gm;
+  if (a.gmask && a.K / a.group <= 16) {
+    int* cnt = reinterpret_cast<int*>(lds);
+    const int G = a.K / a.group;
+    if (tid < 16) cnt[tid] = 0;
+    __syncthreads();
+    for (int p = tid; p < t_main; p += RNT) {
+      uint32_t m = a.gmask[p];
+      while (m) {
+        atomicAdd(&cnt[__builtin_ctz(m)], 1);
+        m &= m - 1;
+      }
+    }
+    __syncthreads();
+    if (tid < G) {
+      const int c = cnt[tid];
+      int r = 0;
+      for (int h = 0; h < G; ++h) r += (cnt[h] > c) || (cnt[h] == c && h < tid);
+      cnt[16 + r] = tid;
+    }
+    __syncthreads();
+    perm = 0;
+    pm = 0;
+    for (int r = 0; r < G; ++r) {
+      const int g = cnt[16 + r];
+      perm |= (uint64_t)g << (4 * r);
+      pm |= ((gm >> g) & 1u) << r;
+    }
+    __syncthreads();  // the ring reuses the scratch
+  }
+  auto chunk_of = [&](int i) -> int {
+    if (!a.gmask) return i;
+    uint32_t m = pm;
+    for (int j = i / a.cpg; j > 0; --j) m &= m - 1;
+    return (int)((perm >> (4 * __builtin_ctz(m))) & 15) * a.cpg + i % a.cpg;
+  };
+#else
   auto chunk_of = [&](int i) -> int {
     if (!a.gmask) return i;
     uint32_t m = gm;
     for (int j = i / a.cpg; j > 0; --j) m &= m - 1;
     return __builtin_ctz(m) * a.cpg + i % a.cpg;
   };
+#endif
   const int K8 = a.K / SB;
   const int64_t tplane2 = 2LL * (XH * a.tiles_y) * W;  // 16-B pieces per 8-channel block of T
   // unit (physical chunk ch, row xi) -> ring slot: weights [part][kw][sub][co] from the packed

@@ -1531,7 +1531,11 @@ __global__ __launch_bounds__(256) void wino_rows_kernel(const WinoRowsArgs a) {
 #define MVBEV_WINO_WALK 0  // 1: channel groups walked most-common-first (see conv_wino_kernel)
 #endif
 #ifndef MVBEV_WINO_ABL
-#define MVBEV_WINO_ABL 0  // timing ablations only (wrong results): bit 0 no unit barrier / wait, bit 1 no DMA in the loop
+#define MVBEV_WINO_ABL 0  // timing ablations only (wrong results): bit 0 no unit barrier / wait, bit 1 no DMA in the loop,
+                          // bit 2 no T DMA, bit 3 no weight DMA (the other stream's pieces stay), bit 4 every piece
+                          // from one zero line (issue cost without bytes), bit 5 weights of chunk 0 only (L2-resident),
+                          // bit 6 T pieces from contiguous sources (same lines per piece as a [part][col] T layout),
+                          // bit 7 / bit 8: T / weights of the tile's first two chunks only (L2-resident, data still changing)
 #endif
 template <bool RELU>
 __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
@@ -1610,24 +1614,27 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   };
 #endif
   const int K8 = a.K / SB;
+  const int abl_c0 = (MVBEV_WINO_ABL & 384) ? chunk_of(0) : 0, abl_c1 = (MVBEV_WINO_ABL & 384) ? chunk_of(min(1, max(nch - 1, 0))) : 0;
   const int64_t tplane2 = 2LL * (XH * a.tiles_y) * W;  // 16-B pieces per 8-channel block of T
   // unit (physical chunk ch, row xi) -> ring slot: weights [part][kw][sub][co] from the packed
   // [part][3 xi + kw][sub][co], then the T row: entry e = (sub, part, row tile, col) -> T row
   // XH ty + NXI rt + xi, column x0 - 1 + col (zero outside the grid)
   auto issue_unit = [&](int ch, int xi, int slot) __attribute__((always_inline)) {
     if (wave >= NIW) return;
-    const u32x4* src = wsrc + (int64_t)ch * wchunk + xi * 3 * 2 * BN;
+    const u32x4* src = wsrc + (int64_t)((MVBEV_WINO_ABL & 32) ? 0 : (MVBEV_WINO_ABL & 256) ? ((ch & 1) ? abl_c1 : abl_c0) : ch) * wchunk + xi * 3 * 2 * BN;
     u32x4* dst = lds + slot * SLOT + wave * 64;
 #pragma unroll
     for (int j = 0; j < NWI; ++j) {
       const int e = (j * NIW + wave) * 64 + lane;
-      glds16(src + (e / RHALF) * (NTAP * 2 * BN) + e % RHALF, dst + j * NIT);
+      if (MVBEV_WINO_ABL & 8) continue;
+      glds16((MVBEV_WINO_ABL & 16) ? g_ring_zero : src + (e / RHALF) * (NTAP * 2 * BN) + e % RHALF, dst + j * NIT);
     }
+    if (MVBEV_WINO_ABL & 4) return;
     const u32x4* xs[2];
     bool kv[2];
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const int k0 = ch * KC + s * SB;
+      const int k0 = ((MVBEV_WINO_ABL & 128) ? ((ch & 1) ? abl_c1 : abl_c0) : ch) * KC + s * SB;
       kv[s] = k0 < a.K;
       xs[s] = static_cast<const u32x4*>(a.x) + ((int64_t)b * K8 + (kv[s] ? k0 / SB : 0)) * tplane2;
     }
@@ -1637,7 +1644,9 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
       const int sub = e / (TROW / 2), part = (e / (TROW / 4)) & 1, rt = (e % (TROW / 4)) / XW, c = e % XW;
       const int gx = x0 - 1 + c;
       const bool z = e >= TROW || gx < 0 || gx >= W || !(sub ? kv[1] : kv[0]);
-      glds16<MVBEV_WINO_XAUX>(z ? g_ring_zero : (sub ? xs[1] : xs[0]) + 2 * ((XH * ty + NXI * rt + xi) * W + gx) + part,
+      glds16<MVBEV_WINO_XAUX>((z || (MVBEV_WINO_ABL & 16)) ? g_ring_zero
+                              : (MVBEV_WINO_ABL & 64) ? (sub ? xs[1] : xs[0]) + 2 * (XH * ty + NXI * rt + xi) * W + (2 * max(x0 - 1, 0) + e % (TROW / 2)) % (2 * W)
+                                                      : (sub ? xs[1] : xs[0]) + 2 * ((XH * ty + NXI * rt + xi) * W + gx) + part,
              dst + RUNIT + j * NIT);
     }
   };
@@ -1683,6 +1692,8 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     }
   };
 
+  // LDS-DMA pieces per wave per unit (the ablation builds drop some)
+  constexpr int NPU = ((MVBEV_WINO_ABL & 8) ? 0 : NWI) + ((MVBEV_WINO_ABL & 4) ? 0 : NXT);
   if (nch > 0) {
     const int U = NXI * nch;
     // prologue: units 0-3 (chunk 0, rows 0-3) in flight, wait for unit 0
@@ -1690,7 +1701,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     issue_unit(cur_ph, 1, 1);
     issue_unit(cur_ph, 2, 2);
     issue_unit(cur_ph, 3, 3);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (NWI + NXT)) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPU) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     fetch_b(0, 0);
@@ -1718,7 +1729,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     sched6(std::integral_constant<int, 4>{});                                                        \
     /* retire unit u+1; every LDS read of this unit's slot is done */                                 \
     if (!(MVBEV_WINO_ABL & 1)) {                                                                     \
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * (NWI + NXT)) : "memory");              \
+      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU) : "memory");              \
       __builtin_amdgcn_s_barrier();                                                                  \
     }                                                                                                \
     asm volatile("" ::: "memory");                                                                   \

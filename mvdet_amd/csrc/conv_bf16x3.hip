@@ -1527,15 +1527,9 @@ __global__ __launch_bounds__(256) void wino_rows_kernel(const WinoRowsArgs a) {
   }
 }
 
-#ifndef MVBEV_WINO_WALK
-#define MVBEV_WINO_WALK 0  // 1: channel groups walked most-common-first (see conv_wino_kernel)
-#endif
 #ifndef MVBEV_WINO_ABL
 #define MVBEV_WINO_ABL 0  // timing ablations only (wrong results): bit 0 no unit barrier / wait, bit 1 no DMA in the loop,
-                          // bit 2 no T DMA, bit 3 no weight DMA (the other stream's pieces stay), bit 4 every piece
-                          // from one zero line (issue cost without bytes), bit 5 weights of chunk 0 only (L2-resident),
-                          // bit 6 T pieces from contiguous sources (same lines per piece as a [part][col] T layout),
-                          // bit 7 / bit 8: T / weights of the tile's first two chunks only (L2-resident, data still changing)
+                          // bit 2 no T DMA, bit 3 no weight DMA (the other stream's pieces and waits stay)
 #endif
 template <bool RELU>
 __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
@@ -1561,103 +1555,90 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   const int ty = pp / a.tiles_x;
   const int x0 = (pp - ty * a.tiles_x) * TW;
   const int y0 = a.out_row0 + ty * RT;
-  const u32x4* wsrc = a.wp + (int64_t)cot * wino::W16;
-  const int64_t wchunk = (int64_t)a.n_cot * wino::W16;
   const uint32_t gm = a.gmask ? a.gmask[pp] : 0u;
   const int nch = a.gmask ? __builtin_popcount(gm) * a.cpg : a.nchunks;
-#if MVBEV_WINO_WALK
-  // walk the tile's channel groups most-common-first (over all pixel tiles' masks): workgroups
-  // that run side by side on an XCD then stream the same weight chunks at the same time
-  uint64_t perm = 0xfedcba9876543210ull;
-  uint32_t pm = gm;
-  if (a.gmask && a.K / a.group <= 16) {
-    int* cnt = reinterpret_cast<int*>(lds);
-    const int G = a.K / a.group;
-    if (tid < 16) cnt[tid] = 0;
-    __syncthreads();
-    for (int p = tid; p < t_main; p += RNT) {
-      uint32_t m = a.gmask[p];
-      while (m) {
-        atomicAdd(&cnt[__builtin_ctz(m)], 1);
-        m &= m - 1;
+  const int K8 = a.K / SB;
+  const int64_t tplane2 = 2LL * (XH * a.tiles_y) * W;  // 16-B pieces per 8-channel block of T
+  const uint32_t tplane_b = (uint32_t)(tplane2 * 16);  // < 2^30 (host check)
+  // The DMAs are buffer loads: a wave-uniform descriptor per unit (built by scalar code from the
+  // chunk's base) and per-lane byte offsets computed ONCE here — the per-unit address arithmetic
+  // of 64-bit per-lane pointers (and a select of a zero source) was ~90 instructions right after
+  // each unit's barrier, with both waves of a SIMD stalled on it.  Padding entries (outside the
+  // grid, past the T row) carry an out-of-range offset: the range check makes them zero.
+  // Weights: entry e of a unit = [part][kw][sub][co] from the packed [part][3 xi + kw][sub][co].
+  // T: entry e = (sub, part, row tile, col) -> T row XH ty + NXI rt + xi, column x0 - 1 + col.
+  constexpr uint32_t kOOB = 0x80000000u;
+  uint32_t wvo[NWI], tvo[NXT];
+#pragma unroll
+  for (int j = 0; j < NWI; ++j) {
+    const int e = (j * NIW + wave) * 64 + lane;
+    wvo[j] = (uint32_t)(((e / RHALF) * (NTAP * 2 * BN) + e % RHALF) * 16);
+    asm volatile("" : "+v"(wvo[j]));  // keep it in a register, not rematerialised per unit
+  }
+#pragma unroll
+  for (int j = 0; j < NXT; ++j) {
+    const int e = (j * NIW + wave) * 64 + lane;
+    const int sub = e / (TROW / 2), part = (e / (TROW / 4)) & 1, rt = (e % (TROW / 4)) / XW, c = e % XW;
+    const int gx = x0 - 1 + c;
+    const bool z = e >= TROW || gx < 0 || gx >= W;
+    tvo[j] = z ? kOOB : (uint32_t)sub * tplane_b + (uint32_t)((2 * ((XH * ty + NXI * rt) * W + gx) + part) * 16);
+    asm volatile("" : "+v"(tvo[j]));
+  }
+  // the tile's physical chunks, walked incrementally: group = lowest set bit of the mask left,
+  // chunk = group * cpg + index in the group (past the last chunk the walk stays there: dummy
+  // loads that keep the vmcnt counts exact)
+  const int cpg = a.gmask ? a.cpg : max(nch, 1);
+  uint32_t rem = a.gmask ? gm : 1u;
+  int gbase = a.gmask ? __builtin_ctz(gm | 0x80000000u) * cpg : 0, ci = 0, wi = 0;
+  auto step = [&]() __attribute__((always_inline)) {
+    if (wi + 1 < nch) {
+      ++wi;
+      if (++ci == cpg) {
+        ci = 0;
+        rem &= rem - 1;
+        gbase = __builtin_ctz(rem | 0x80000000u) * cpg;
       }
     }
-    __syncthreads();
-    if (tid < G) {
-      const int c = cnt[tid];
-      int r = 0;
-      for (int h = 0; h < G; ++h) r += (cnt[h] > c) || (cnt[h] == c && h < tid);
-      cnt[16 + r] = tid;
-    }
-    __syncthreads();
-    perm = 0;
-    pm = 0;
-    for (int r = 0; r < G; ++r) {
-      const int g = cnt[16 + r];
-      perm |= (uint64_t)g << (4 * r);
-      pm |= ((gm >> g) & 1u) << r;
-    }
-    __syncthreads();  // the ring reuses the scratch
-  }
-  auto chunk_of = [&](int i) -> int {
-    if (!a.gmask) return i;
-    uint32_t m = pm;
-    for (int j = i / a.cpg; j > 0; --j) m &= m - 1;
-    return (int)((perm >> (4 * __builtin_ctz(m))) & 15) * a.cpg + i % a.cpg;
+    return gbase + ci;
   };
-#else
-  auto chunk_of = [&](int i) -> int {
-    if (!a.gmask) return i;
-    uint32_t m = gm;
-    for (int j = i / a.cpg; j > 0; --j) m &= m - 1;
-    return __builtin_ctz(m) * a.cpg + i % a.cpg;
+  const char* wcot = reinterpret_cast<const char*>(a.wp + (int64_t)cot * wino::W16);
+  const char* tb0 = reinterpret_cast<const char*>(static_cast<const u32x4*>(a.x) + (int64_t)b * K8 * tplane2);
+  struct ChunkBase {
+    const char* w;
+    const char* t;
+    bool kv1;  // the chunk's second 8-channel block exists (K % 16 == 8: not in the last chunk)
   };
-#endif
-  const int K8 = a.K / SB;
-  const int abl_c0 = (MVBEV_WINO_ABL & 384) ? chunk_of(0) : 0, abl_c1 = (MVBEV_WINO_ABL & 384) ? chunk_of(min(1, max(nch - 1, 0))) : 0;
-  const int64_t tplane2 = 2LL * (XH * a.tiles_y) * W;  // 16-B pieces per 8-channel block of T
-  // unit (physical chunk ch, row xi) -> ring slot: weights [part][kw][sub][co] from the packed
-  // [part][3 xi + kw][sub][co], then the T row: entry e = (sub, part, row tile, col) -> T row
-  // XH ty + NXI rt + xi, column x0 - 1 + col (zero outside the grid)
-  auto issue_unit = [&](int ch, int xi, int slot) __attribute__((always_inline)) {
+  auto base_of = [&](int ph) __attribute__((always_inline)) {
+    return ChunkBase{wcot + (int64_t)ph * a.n_cot * wino::W16 * 16, tb0 + (int64_t)(2 * ph) * tplane2 * 16,
+                     2 * ph + 1 < K8};
+  };
+  auto issue_unit = [&](const ChunkBase& cb, int xi, int slot) __attribute__((always_inline)) {
     if (wave >= NIW) return;
-    const u32x4* src = wsrc + (int64_t)((MVBEV_WINO_ABL & 32) ? 0 : (MVBEV_WINO_ABL & 256) ? ((ch & 1) ? abl_c1 : abl_c0) : ch) * wchunk + xi * 3 * 2 * BN;
     u32x4* dst = lds + slot * SLOT + wave * 64;
+    if (!(MVBEV_WINO_ABL & 8)) {
+      const __amdgpu_buffer_rsrc_t rw =
+          __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(cb.w + xi * 3 * 2 * BN * 16), (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
-    for (int j = 0; j < NWI; ++j) {
-      const int e = (j * NIW + wave) * 64 + lane;
-      if (MVBEV_WINO_ABL & 8) continue;
-      glds16((MVBEV_WINO_ABL & 16) ? g_ring_zero : src + (e / RHALF) * (NTAP * 2 * BN) + e % RHALF, dst + j * NIT);
+      for (int j = 0; j < NWI; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(dst + j * NIT), 16,
+                                                 wvo[j], 0, 0, 0);
     }
-    if (MVBEV_WINO_ABL & 4) return;
-    const u32x4* xs[2];
-    bool kv[2];
+    if (!(MVBEV_WINO_ABL & 4)) {
+      const int32_t rows_b = xi * W * 32;
+      const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<char*>(cb.t + rows_b), (short)0, cb.kv1 ? 0x7fffffff : (int)(tplane_b - rows_b), 0x00020000);
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int k0 = ((MVBEV_WINO_ABL & 128) ? ((ch & 1) ? abl_c1 : abl_c0) : ch) * KC + s * SB;
-      kv[s] = k0 < a.K;
-      xs[s] = static_cast<const u32x4*>(a.x) + ((int64_t)b * K8 + (kv[s] ? k0 / SB : 0)) * tplane2;
-    }
-#pragma unroll
-    for (int j = 0; j < NXT; ++j) {
-      const int e = (j * NIW + wave) * 64 + lane;
-      const int sub = e / (TROW / 2), part = (e / (TROW / 4)) & 1, rt = (e % (TROW / 4)) / XW, c = e % XW;
-      const int gx = x0 - 1 + c;
-      const bool z = e >= TROW || gx < 0 || gx >= W || !(sub ? kv[1] : kv[0]);
-      glds16<MVBEV_WINO_XAUX>((z || (MVBEV_WINO_ABL & 16)) ? g_ring_zero
-                              : (MVBEV_WINO_ABL & 64) ? (sub ? xs[1] : xs[0]) + 2 * (XH * ty + NXI * rt + xi) * W + (2 * max(x0 - 1, 0) + e % (TROW / 2)) % (2 * W)
-                                                      : (sub ? xs[1] : xs[0]) + 2 * ((XH * ty + NXI * rt + xi) * W + gx) + part,
-             dst + RUNIT + j * NIT);
+      for (int j = 0; j < NXT; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(dst + RUNIT + j * NIT),
+                                                 16, tvo[j], 0, 0, MVBEV_WINO_XAUX);
     }
   };
-  // physical chunks: the current one and the next (past the last one it stays there: dummy
-  // loads that keep the vmcnt counts exact)
-  int cur_ph = chunk_of(0), nx_i = 1;
-  int nx_ph = chunk_of(min(1, max(nch - 1, 0)));
+  // the current chunk and the next
+  ChunkBase cur = base_of(gbase + ci);
+  ChunkBase nx = base_of(step());
   auto advance = [&]() __attribute__((always_inline)) {
-    cur_ph = nx_ph;
-    nx_i += 1;
-    nx_ph = chunk_of(min(nx_i, nch - 1));
+    cur = nx;
+    nx = base_of(step());
   };
 
   const int rg = wave & 3;
@@ -1697,10 +1678,10 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   if (nch > 0) {
     const int U = NXI * nch;
     // prologue: units 0-3 (chunk 0, rows 0-3) in flight, wait for unit 0
-    issue_unit(cur_ph, 0, 0);
-    issue_unit(cur_ph, 1, 1);
-    issue_unit(cur_ph, 2, 2);
-    issue_unit(cur_ph, 3, 3);
+    issue_unit(cur, 0, 0);
+    issue_unit(cur, 1, 1);
+    issue_unit(cur, 2, 2);
+    issue_unit(cur, 3, 3);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPU) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -1734,7 +1715,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     }                                                                                                \
     asm volatile("" ::: "memory");                                                                   \
     /* unit u+4 into this slot: (chunk, xi 4) at xi 0, else (next chunk, xi - 1) */                  \
-    if (!(MVBEV_WINO_ABL & 2)) issue_unit(XI == 0 ? cur_ph : nx_ph, (XI + 4) % 5, slot);             \
+    if (!(MVBEV_WINO_ABL & 2)) issue_unit(XI == 0 ? cur : nx, (XI + 4) % 5, slot);             \
     if (XI == 4) advance();                                                                          \
     fetch_b(0, nslot);                                                                               \
     fetch_b(1, nslot);                                                                               \
@@ -1821,6 +1802,8 @@ static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_pa
   const int64_t tiles = (int64_t)a.tiles_x * a.tiles_y * a.n_cot * d->B;
   if (tiles > INT32_MAX / 2 || 2LL * 5 * 4 * a.tiles_y * a.W * (d->K / SB) * d->B > (int64_t)INT32_MAX * 64)
     return MVBEV_ERR_SHAPE;
+  // the kernel's 32-bit DMA offsets span two 8-channel planes of T: 2 * 32 B * XH * tiles_y * W < 2^31
+  if (2LL * 32 * wino::XH * a.tiles_y * a.W >= (1LL << 31)) return MVBEV_ERR_SHAPE;
   if (group_mask) {
     if (d->group % KC != 0 || d->K / d->group > 32) return MVBEV_ERR_SHAPE;
     a.gmask = group_mask;

@@ -1527,6 +1527,9 @@ __global__ __launch_bounds__(256) void wino_rows_kernel(const WinoRowsArgs a) {
   }
 }
 
+#ifndef MVBEV_WINO_TSKIP
+#define MVBEV_WINO_TSKIP 1  // T pieces that hold no T entry are not issued (per-wave wait counts)
+#endif
 #ifndef MVBEV_WINO_ABL
 #define MVBEV_WINO_ABL 0  // timing ablations only (wrong results): bit 0 no unit barrier / wait, bit 1 no DMA in the loop,
                           // bit 2 no T DMA, bit 3 no weight DMA (the other stream's pieces and waits stay)
@@ -1629,8 +1632,9 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
           const_cast<char*>(cb.t + rows_b), (short)0, cb.kv1 ? 0x7fffffff : (int)(tplane_b - rows_b), 0x00020000);
 #pragma unroll
       for (int j = 0; j < NXT; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(dst + RUNIT + j * NIT),
-                                                 16, tvo[j], 0, 0, MVBEV_WINO_XAUX);
+        if (!MVBEV_WINO_TSKIP || (j * NIW + wave) * 64 < TROW)  // pieces wholly past the T row: not issued
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(dst + RUNIT + j * NIT),
+                                                   16, tvo[j], 0, 0, MVBEV_WINO_XAUX);
     }
   };
   // the current chunk and the next
@@ -1674,7 +1678,14 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   };
 
   // LDS-DMA pieces per wave per unit (the ablation builds drop some)
-  constexpr int NPU = ((MVBEV_WINO_ABL & 8) ? 0 : NWI) + ((MVBEV_WINO_ABL & 4) ? 0 : NXT);
+  // LDS-DMA pieces per wave per unit (the ablation builds drop some): waves < WHI issue NPU_HI,
+  // the others NPU_LO (TSKIP: the last T piece only where it holds T entries)
+  constexpr int NXT_LO = MVBEV_WINO_TSKIP ? TROW / NIT : NXT;
+  constexpr int WHI = MVBEV_WINO_TSKIP ? (TROW % NIT + 63) / 64 : NIW;
+  static_assert(!MVBEV_WINO_TSKIP || NXT_LO + (WHI > 0) == NXT, "T pieces");
+  constexpr int NPU_HI = ((MVBEV_WINO_ABL & 8) ? 0 : NWI) + ((MVBEV_WINO_ABL & 4) ? 0 : NXT);
+  constexpr int NPU_LO = ((MVBEV_WINO_ABL & 8) ? 0 : NWI) + ((MVBEV_WINO_ABL & 4) ? 0 : NXT_LO);
+  const bool whi = wave < WHI;
   if (nch > 0) {
     const int U = NXI * nch;
     // prologue: units 0-3 (chunk 0, rows 0-3) in flight, wait for unit 0
@@ -1682,7 +1693,8 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     issue_unit(cur, 1, 1);
     issue_unit(cur, 2, 2);
     issue_unit(cur, 3, 3);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPU) : "memory");
+    if (whi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPU_HI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPU_LO) : "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     fetch_b(0, 0);
@@ -1710,7 +1722,8 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     sched6(std::integral_constant<int, 4>{});                                                        \
     /* retire unit u+1; every LDS read of this unit's slot is done */                                 \
     if (!(MVBEV_WINO_ABL & 1)) {                                                                     \
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU) : "memory");              \
+      if (whi) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU_HI) : "memory");     \
+      else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU_LO) : "memory");          \
       __builtin_amdgcn_s_barrier();                                                                  \
     }                                                                                                \
     asm volatile("" ::: "memory");                                                                   \

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -311,6 +311,21 @@ int mvbev_wino_rows_split_bf16(const void* x, const mvbev_conv_desc* desc, const
 int mvbev_conv3x3_wino_bf16x3(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,
                               const float* init, int64_t Cout, int relu, void* y, int y_layout,
                               const uint32_t* group_mask, const int32_t* tile_order, void* stream);
+/* The same two steps for dilation 2 (conv2, map_classifier[2:4], persp_trans_detector.py:53:
+ * nn.Conv2d(512, 512, 3, padding=2, dilation=2)): the 12-row workgroup tile holds two interleaved
+ * pairs of 3-row tiles (rows r, r + 2, r + 4), whose T = B^T over the 5 input rows r - 2 ... r + 6
+ * (step 2); a kernel column's taps are 2 columns apart.  mvbev_wino_rows_split_bf16_dil(dilation 1)
+ * is mvbev_wino_rows_split_bf16; T has the same size (mvbev_wino_rows_bytes).  The conv: no init,
+ * no mask (dense), y fp32 or split-bf16 (_dil), or, replacing
+ * mvbev_conv3x3_bf16x3_cout1_partials (same desc, bias, w3, partials layout and size; relu,
+ * dilation 2), conv3's partial sums from the epilogue (_cout1_partials, ABI 11500). */
+int mvbev_wino_rows_split_bf16_dil(const void* x, const mvbev_conv_desc* desc, int dilation,
+                                   const uint32_t* group_mask, void* t, size_t t_bytes, void* stream);
+int mvbev_conv3x3_wino_bf16x3_dil(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,
+                                  int64_t Cout, int dilation, int relu, void* y, int y_layout, void* stream);
+int mvbev_conv3x3_wino_bf16x3_cout1_partials(const void* t, const mvbev_conv_desc* desc, const void* w_packed,
+                                             const float* bias, int64_t Cout, int dilation, int relu, const float* w3,
+                                             void* partials, size_t partials_bytes, void* stream);
 
 /* conv2 -> conv3 without conv2's activation in HBM (map_classifier[2:5],
  * persp_trans_detector.py:53-54, inference): the split-bf16-input conv of
@@ -374,7 +389,8 @@ typedef struct mvbev_bev_plan {     /* host memory, caller-owned; filled by the 
   mvbev_bev_geometry g;
   int32_t wino;                     /* after prepare: 1 = row-Winograd conv1, 0 = direct (non-finite geometry) */
   int32_t frustum;                  /* conv1 skips the views a tile's camera frustum excludes (C % 16 == 0 after padding) */
-  int32_t prepared, reserved;
+  int32_t prepared;
+  int32_t wino2;                    /* after prepare: 1 = row-Winograd conv2 -> conv3 partials (ABI 11500; finite geometry) */
   int64_t Cs, tiles;                /* channels per view slot (C rounded to 8); conv1's 12 x 32 tiles */
   size_t off[16];                   /* workspace regions */
   size_t workspace_bytes;           /* >= what mvbev_bev_fuse_workspace_bytes returns, 256-B aligned base */

@@ -68,6 +68,9 @@ EXPORTS = (
     "mvbev_wino_rows_bytes",
     "mvbev_wino_rows_split_bf16",
     "mvbev_conv3x3_wino_bf16x3",
+    "mvbev_wino_rows_split_bf16_dil",
+    "mvbev_conv3x3_wino_bf16x3_dil",
+    "mvbev_conv3x3_wino_bf16x3_cout1_partials",
     "mvbev_warp_views_wino_rows",
     "mvbev_warp_views_upsampled_wino_rows",
     "mvbev_warp_nonfinite_views",
@@ -129,7 +132,7 @@ class BevGeometry(ctypes.Structure):
 class BevPlan(ctypes.Structure):
     """``mvbev_bev_plan`` (include/mvbev.h)."""
     _fields_ = [("g", BevGeometry), ("wino", ctypes.c_int32), ("frustum", ctypes.c_int32),
-                ("prepared", ctypes.c_int32), ("reserved", ctypes.c_int32), ("Cs", ctypes.c_int64),
+                ("prepared", ctypes.c_int32), ("wino2", ctypes.c_int32), ("Cs", ctypes.c_int64),
                 ("tiles", ctypes.c_int64), ("off", ctypes.c_size_t * 16), ("workspace_bytes", ctypes.c_size_t),
                 ("b2", ctypes.c_void_p), ("w3", ctypes.c_void_p)]
 
@@ -195,6 +198,15 @@ def _declare(lib):
     lib.mvbev_conv3x3_wino_bf16x3.restype = ctypes.c_int
     lib.mvbev_conv3x3_wino_bf16x3.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64, ctypes.c_int, _p,
                                               ctypes.c_int, _p, _p, _p]
+    lib.mvbev_wino_rows_split_bf16_dil.restype = ctypes.c_int
+    lib.mvbev_wino_rows_split_bf16_dil.argtypes = [_p, ctypes.POINTER(ConvDesc), ctypes.c_int, _p, _p, ctypes.c_size_t,
+                                                   _p]
+    lib.mvbev_conv3x3_wino_bf16x3_dil.restype = ctypes.c_int
+    lib.mvbev_conv3x3_wino_bf16x3_dil.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, _i64, ctypes.c_int,
+                                                  ctypes.c_int, _p, ctypes.c_int, _p]
+    lib.mvbev_conv3x3_wino_bf16x3_cout1_partials.restype = ctypes.c_int
+    lib.mvbev_conv3x3_wino_bf16x3_cout1_partials.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, _i64, ctypes.c_int,
+                                                             ctypes.c_int, _p, _p, ctypes.c_size_t, _p]
     lib.mvbev_warp_views_wino_rows.restype = ctypes.c_int
     lib.mvbev_warp_views_wino_rows.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
                                                _i64, _i64, ctypes.c_int, _p]

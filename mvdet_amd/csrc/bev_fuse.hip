@@ -6,7 +6,8 @@
 //   term, frustum mask, heavy-first tile order, the non-finite-geometry check; one stream sync)
 //   ->  fuse (per frame, enqueued, no sync): warp (+ the fused 3x upsample) writing conv1's
 //   row-Winograd transform straight into T, the Winograd conv1 (+ coord term, bias, ReLU), conv2
-//   with conv3's per-tap partials in its epilogue, their reduce -> map [B][1][Ho][Wo].
+//   (row-Winograd too: y1's dilation-2 transform, then the conv) with conv3's per-tap partials in its
+//   epilogue, their reduce -> map [B][1][Ho][Wo].
 //
 // Geometry that can produce a non-finite warp sample runs the direct conv1 on the split slab
 // instead (the reference's NaN pattern; see mvbev_warp_nonfinite_views).  Everything here is a
@@ -25,8 +26,8 @@ constexpr int64_t kKC = MVBEV_CONV_KC;
 constexpr int64_t kTileW = MVBEV_CONV_TILE_W;
 constexpr size_t kAlign = 256;
 
-enum Region { R_MAP1, R_MAPC, R_PACK1, R_PACK2, R_PACKC, R_CIN, R_INIT, R_MASK, R_ORDER, R_NF, R_BIG, R_Y1, R_P3,
-              R_COUNT };
+enum Region { R_MAP1, R_MAPC, R_PACK1, R_PACK2, R_PACKC, R_CIN, R_INIT, R_MASK, R_ORDER, R_NF, R_BIG, R_Y1, R_T2,
+              R_P3, R_COUNT };
 
 size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
@@ -124,7 +125,7 @@ int mvbev_bev_plan_init(const mvbev_bev_geometry* g, mvbev_bev_plan* p) {
   sz[R_MAP1] = (size_t)K * 4;
   sz[R_MAPC] = (size_t)kKC * 4;
   sz[R_PACK1] = std::max(mvbev_conv3x3_packed_bytes_wino(kMid, K), mvbev_conv3x3_packed_bytes_bf16x3(kMid, K));
-  sz[R_PACK2] = mvbev_conv3x3_packed_bytes_bf16x3(kMid, kMid);
+  sz[R_PACK2] = std::max(mvbev_conv3x3_packed_bytes_wino(kMid, kMid), mvbev_conv3x3_packed_bytes_bf16x3(kMid, kMid));
   sz[R_PACKC] = 4 * mvbev_conv3x3_packed_floats(kMid, kKC);
   sz[R_CIN] = (size_t)kKC * g->Ho * g->Wo * 4;
   sz[R_INIT] = (size_t)kMid * g->Ho * g->Wo * 4;
@@ -133,6 +134,7 @@ int mvbev_bev_plan_init(const mvbev_bev_geometry* g, mvbev_bev_plan* p) {
   sz[R_NF] = 4;
   sz[R_BIG] = std::max(t_bytes, slab_bytes);  // T (Winograd) or the split slab (direct conv1)
   sz[R_Y1] = (size_t)g->B * kMid * g->Ho * g->Wo * 4;
+  sz[R_T2] = mvbev_wino_rows_bytes(&d2);  // conv2's row-Winograd transform of y1
   sz[R_P3] = mvbev_conv3x3_bf16x3_cout1_partials_bytes(&d2, kMid);
   size_t o = 0;
   for (int r = 0; r < R_COUNT; ++r) {
@@ -183,6 +185,7 @@ int mvbev_bev_fuse_prepare(mvbev_bev_plan* p, const float* w1, const float* b1, 
     return MVBEV_ERR_HIP;
   if (hipStreamSynchronize(s) != hipSuccess) return MVBEV_ERR_HIP;
   p->wino = p->wino && nf == 0 ? 1 : 0;
+  p->wino2 = nf == 0 ? 1 : 0;  // conv2's Winograd form (y1 finite), as the engine's wino_conv2_active
   if (p->frustum) {
     // heavy-first run order: most active views first, equal view sets adjacent (ops.heavy_first_order)
     const int64_t T = p->tiles, n = g.B * T;
@@ -207,7 +210,10 @@ int mvbev_bev_fuse_prepare(mvbev_bev_plan* p, const float* w1, const float* b1, 
   else
     BEV_TRY(mvbev_pack_conv3x3_weight_bf16x3(w1, kMid, cin, at<int32_t>(ws, p, R_MAP1), K, at<void>(ws, p, R_PACK1),
                                              stream));
-  BEV_TRY(mvbev_pack_conv3x3_weight_bf16x3(w2, kMid, kMid, nullptr, kMid, at<void>(ws, p, R_PACK2), stream));
+  if (p->wino2)
+    BEV_TRY(mvbev_pack_conv3x3_weight_wino(w2, kMid, kMid, nullptr, kMid, at<void>(ws, p, R_PACK2), stream));
+  else
+    BEV_TRY(mvbev_pack_conv3x3_weight_bf16x3(w2, kMid, kMid, nullptr, kMid, at<void>(ws, p, R_PACK2), stream));
   BEV_TRY(mvbev_pack_conv3x3_weight_f32(w1, kMid, cin, at<int32_t>(ws, p, R_MAPC), kKC, at<float>(ws, p, R_PACKC),
                                         stream));
   float* cinp = at<float>(ws, p, R_CIN);
@@ -274,8 +280,15 @@ int mvbev_bev_fuse(const mvbev_bev_plan* p, const void* const* views, float* map
   // a8 + a9: conv2 + ReLU with conv3's per-tap partials in its epilogue, then their reduce
   void* p3 = at<void>(ws, p, R_P3);
   static_assert(R_P3 == R_COUNT - 1, "the partials are the workspace's last region");
-  BEV_TRY(mvbev_conv3x3_bf16x3_cout1_partials(y1, &d2, at<void>(ws, p, R_PACK2), p->b2, kMid, 2, 1, p->w3, p3,
-                                              p->workspace_bytes - p->off[R_P3], stream));
+  if (p->wino2) {  // the dilation-2 row transform of y1, then the Winograd conv with the partials epilogue
+    void* t2 = at<void>(ws, p, R_T2);
+    BEV_TRY(mvbev_wino_rows_split_bf16_dil(y1, &d2, 2, nullptr, t2, p->off[R_T2 + 1] - p->off[R_T2], stream));
+    BEV_TRY(mvbev_conv3x3_wino_bf16x3_cout1_partials(t2, &d2, at<void>(ws, p, R_PACK2), p->b2, kMid, 2, 1, p->w3, p3,
+                                                     p->workspace_bytes - p->off[R_P3], stream));
+  } else {
+    BEV_TRY(mvbev_conv3x3_bf16x3_cout1_partials(y1, &d2, at<void>(ws, p, R_PACK2), p->b2, kMid, 2, 1, p->w3, p3,
+                                                p->workspace_bytes - p->off[R_P3], stream));
+  }
   BEV_TRY(mvbev_cout1_reduce_partials(p3, &d2, kMid, 4, map, 0, g.Ho, stream));
   return MVBEV_OK;
 }

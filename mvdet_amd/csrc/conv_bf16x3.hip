@@ -1371,7 +1371,6 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
 namespace wino {
 constexpr int NXI = 5;                            // transformed rows per 3-row output tile
 constexpr int XH = 4 * NXI;                       // T rows of a 12-row workgroup tile
-constexpr int XW = TW + 2;
 #ifndef MVBEV_WINO_NIW
 #define MVBEV_WINO_NIW 8  // DMA-issuing waves (cfg2 winoconv: 8 1.59-1.67 ms, 4 1.73-1.79)
 #endif
@@ -1382,10 +1381,16 @@ constexpr int NIW = MVBEV_WINO_NIW;               // DMA-issuing waves
 constexpr int NIT = 64 * NIW;
 constexpr int NWI = RUNIT / NIT;                  // weight DMAs per issuing wave per unit (3)
 // a unit (chunk, xi) stages its weights (3 kernel columns) and its T row of the 4 row tiles,
-// [sub][part][row tile][XW], together in one ring slot
-constexpr int TROW = 2 * 2 * 4 * XW;              // T entries of a unit (544)
-constexpr int NXT = (TROW + NIT - 1) / NIT;       // T DMAs per issuing wave per unit (2)
-constexpr int SLOT = RUNIT + NXT * NIT;           // 16-B entries per ring slot
+// [sub][part][row tile][XW], together in one ring slot; a kernel column's taps are DIL columns
+// apart, so the row carries DIL halo columns on each side
+template <int DIL> struct Geo {
+  static constexpr int XW = TW + 2 * DIL;              // T columns of a unit's row
+  static constexpr int TROW = 2 * 2 * 4 * XW;          // T entries of a unit (544 / 576)
+  static constexpr int NXT = (TROW + NIT - 1) / NIT;   // T DMAs per issuing wave per unit (2)
+};
+constexpr int NXTMAX = 2;
+static_assert(Geo<1>::NXT <= NXTMAX && Geo<2>::NXT <= NXTMAX, "T pieces");
+constexpr int SLOT = RUNIT + NXTMAX * NIT;        // 16-B entries per ring slot
 constexpr int NSLOT = 4;                          // 3 units of DMA in flight
 constexpr int LDS = NSLOT * SLOT;                 // 160 KiB
 static_assert(LDS * 16 <= 160 * 1024, "LDS");
@@ -1432,7 +1437,7 @@ struct WinoRowsArgs {
   const u32x4* x;
   u32x4* t;
   int64_t group_stride, batch_stride;  // elements, as mvbev_conv_desc
-  int K, group, H, W, in_row0, in_rows, out_row0, tiles_x, tiles_y;
+  int K, group, H, W, in_row0, in_rows, out_row0, tiles_x, tiles_y, dil;
   const uint32_t* gmask;
 };
 
@@ -1445,8 +1450,10 @@ __device__ inline void bf16x8_to_f32(const u32x4 v, float (&f)[8]) {
 }
 
 // T[b][k / 8][5 r3 + xi][col][hi, lo][8] = split((B^T d)[xi]),
-//   d[m] = x[b][k][out_row0 + 3 r3 - 1 + m][col] (zero outside the image and the input rows),
-// r3 < 4 tiles_y (the 12 x 32 tiles of the conv).  Workgroup = (pixel tile, channel group, b);
+//   d[m] = x[b][k][out_row0 + base(r3) + dil (m - 1)][col] (zero outside the image and the input rows),
+// r3 < 4 tiles_y: the 3-row tiles of the conv's 12 x 32 workgroup tiles, rows base(r3) + dil pt
+// (pt < 3): base = 3 r3 for dilation 1; for dilation 2 the 12 rows hold two interleaved pairs of
+// row tiles, base = 12 (r3 / 4) + ring_base_row<2>(r3 % 4) (the ring kernel's wave rows).  Workgroup = (pixel tile, channel group, b);
 // with a frustum mask the groups it clears for the tile are skipped: the conv never reads them
 // there, and the T columns a neighbouring tile's halo reads from a skipped tile are zero both
 // in T (zero-filled, never written) and in the true transform (the mask covers the halo).
@@ -1464,12 +1471,13 @@ __global__ __launch_bounds__(256) void wino_rows_kernel(const WinoRowsArgs a) {
   const int c = threadIdx.x % TW, q = (threadIdx.x / TW) % 4, kq = threadIdx.x / (4 * TW);  // kq < 2
   const int col = x0 + c, r3 = 4 * ty + q;
   if (col >= W) return;
+  const int base = 12 * ty + (a.dil == 1 ? 3 * q : ring_base_row<2>(q));
   // the 5 input rows of the row tile (all 4 items of the thread share them)
   int64_t roff[5];
   bool rok[5];
 #pragma unroll
   for (int m = 0; m < 5; ++m) {
-    const int row = a.out_row0 + 3 * r3 - 1 + m, by = row - a.in_row0;
+    const int row = a.out_row0 + base + a.dil * (m - 1), by = row - a.in_row0;
     rok[m] = row >= 0 && row < a.H && by >= 0 && by < a.in_rows;
     roff[m] = 2 * ((int64_t)by * W + col);
   }
@@ -1534,9 +1542,13 @@ __global__ __launch_bounds__(256) void wino_rows_kernel(const WinoRowsArgs a) {
 #define MVBEV_WINO_ABL 0  // timing ablations only (wrong results): bit 0 no unit barrier / wait, bit 1 no DMA in the loop,
                           // bit 2 no T DMA, bit 3 no weight DMA (the other stream's pieces and waits stay)
 #endif
-template <bool RELU>
+// DIL 2 (conv2): the wave's row tile is the ring kernel's interleaved rows base + 2 pt; P3: the
+// epilogue forms conv3's partial sums (cout1_partials) instead of storing y
+template <bool RELU, int DIL, bool P3>
 __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   using namespace wino;
+  using G = Geo<DIL>;
+  constexpr int XW = G::XW, TROW = G::TROW, NXT = G::NXT;
   __shared__ __attribute__((aligned(16))) u32x4 lds[LDS];
   const int W = a.W;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1569,9 +1581,9 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   // each unit's barrier, with both waves of a SIMD stalled on it.  Padding entries (outside the
   // grid, past the T row) carry an out-of-range offset: the range check makes them zero.
   // Weights: entry e of a unit = [part][kw][sub][co] from the packed [part][3 xi + kw][sub][co].
-  // T: entry e = (sub, part, row tile, col) -> T row XH ty + NXI rt + xi, column x0 - 1 + col.
+  // T: entry e = (sub, part, row tile, col) -> T row XH ty + NXI rt + xi, column x0 - DIL + col.
   constexpr uint32_t kOOB = 0x80000000u;
-  uint32_t wvo[NWI], tvo[NXT];
+  uint32_t wvo[NWI], tvo[NXTMAX];  // fixed size: a template-dependent array captured by the lambdas below silently drops the kernel's host stub (hipcc, ROCm 7.2)
 #pragma unroll
   for (int j = 0; j < NWI; ++j) {
     const int e = (j * NIW + wave) * 64 + lane;
@@ -1582,7 +1594,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   for (int j = 0; j < NXT; ++j) {
     const int e = (j * NIW + wave) * 64 + lane;
     const int sub = e / (TROW / 2), part = (e / (TROW / 4)) & 1, rt = (e % (TROW / 4)) / XW, c = e % XW;
-    const int gx = x0 - 1 + c;
+    const int gx = x0 - DIL + c;
     const bool z = e >= TROW || gx < 0 || gx >= W;
     tvo[j] = z ? kOOB : (uint32_t)sub * tplane_b + (uint32_t)((2 * ((XH * ty + NXI * rt) * W + gx) + part) * 16);
     asm volatile("" : "+v"(tvo[j]));
@@ -1657,7 +1669,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   bf16x8 fb[3][2];     // [kw][hi, lo]
   bf16x8 fa[2][2][2];  // [set][ct][hi, lo]
   auto fetch_b = [&](int kw, int slot) __attribute__((always_inline)) {
-    const u32x4* X = lds + slot * SLOT + RUNIT + kl * (TROW / 2) + rg * XW + l32 + kw;
+    const u32x4* X = lds + slot * SLOT + RUNIT + kl * (TROW / 2) + rg * XW + l32 + DIL * kw;
 #pragma unroll
     for (int p = 0; p < 2; ++p) fb[kw][p] = __builtin_bit_cast(bf16x8, X[p * (TROW / 4)]);
   };
@@ -1761,12 +1773,13 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     y[ct][1] = m1 - m2 + 2.f * m3;
     y[ct][2] = m1 + m2 + 4.f * m3 + m4;
   }
-  ring_epilogue<1, RELU, false>(a, b, y0 + 3 * rg, x0 + l32, cot, cw, y, lds);
+  ring_epilogue<DIL, RELU, P3>(a, b, y0 + ring_base_row<DIL>(rg), x0 + l32, cot, cw, y, lds);
 }
 
-static int wino_rows_launch(const void* x, const mvbev_conv_desc* d, const uint32_t* group_mask, void* t,
+static int wino_rows_launch(const void* x, const mvbev_conv_desc* d, int dil, const uint32_t* group_mask, void* t,
                             size_t t_bytes, void* stream) {
   if (!x || !d || !t) return MVBEV_ERR_NULL;
+  if (dil != 1 && dil != 2) return MVBEV_ERR_DILATION;
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || d->in_rows <= 0 || d->out_rows <= 0 || d->group <= 0)
     return MVBEV_ERR_RANK;
   if (d->K % SB != 0 || d->group % SB != 0 || d->K % d->group != 0) return MVBEV_ERR_SHAPE;
@@ -1784,6 +1797,7 @@ static int wino_rows_launch(const void* x, const mvbev_conv_desc* d, const uint3
   a.K = (int)d->K, a.group = (int)d->group, a.H = (int)d->H, a.W = (int)d->W;
   a.in_row0 = (int)d->in_row0, a.in_rows = (int)d->in_rows, a.out_row0 = (int)d->out_row0;
   a.tiles_x = (int)tiles_x, a.tiles_y = (int)tiles_y;
+  a.dil = dil;
   a.gmask = group_mask;
   const int64_t nbg = ceil_div(d->group / SB, 8);  // wino_rows_kernel's KB
   if ((d->K / d->group) * nbg > 65535) return MVBEV_ERR_SHAPE;
@@ -1795,8 +1809,11 @@ static int wino_rows_launch(const void* x, const mvbev_conv_desc* d, const uint3
 
 static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_packed, const float* bias,
                        const float* init, int64_t Cout, int relu, float* y, int y_layout,
-                       const uint32_t* group_mask, const int32_t* tile_order, void* stream) {
-  if (!t || !d || !w_packed || !y) return MVBEV_ERR_NULL;
+                       const uint32_t* group_mask, const int32_t* tile_order, void* stream, int dil = 1,
+                       const float* w3 = nullptr, float* p3 = nullptr) {
+  if (!t || !d || !w_packed || (!y && !p3)) return MVBEV_ERR_NULL;
+  if (dil != 1 && dil != 2) return MVBEV_ERR_DILATION;
+  if (p3 && (!w3 || group_mask || init)) return MVBEV_ERR_SHAPE;  // the conv2 -> conv3 form: dense, bias only
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || d->out_rows <= 0 || d->group <= 0)
     return MVBEV_ERR_RANK;
   if (Cout % BN != 0 || d->K % SB != 0 || d->group % SB != 0 || d->K % d->group != 0) return MVBEV_ERR_SHAPE;
@@ -1806,6 +1823,7 @@ static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_pa
   if (((reinterpret_cast<uintptr_t>(w_packed) | reinterpret_cast<uintptr_t>(t)) & 15) != 0) return MVBEV_ERR_ALIGN;
   Args a{};
   a.x = t; a.wp = static_cast<const u32x4*>(w_packed); a.bias = bias; a.init = init; a.y = y;
+  a.w3 = w3; a.p3 = p3;
   a.B = (int)d->B; a.group = (int)d->group; a.K = (int)d->K; a.nchunks = (int)ceil_div(d->K, KC);
   a.Cout = (int)Cout; a.H = (int)d->H; a.W = (int)d->W;
   a.in_row0 = 0; a.in_rows = (int)d->H;
@@ -1828,10 +1846,18 @@ static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_pa
   const int64_t nwg = group_mask ? (int64_t)a.n_cot * round_up(a.npix, 8 * MVBEV_MASK_GROUP) : tiles;
   a.nwg = (int)nwg;
   hipStream_t s = as_stream(stream);
-  if (relu)
-    hipLaunchKernelGGL((conv_wino_kernel<true>), dim3((unsigned)nwg), dim3(RNT), 0, s, a);
-  else
-    hipLaunchKernelGGL((conv_wino_kernel<false>), dim3((unsigned)nwg), dim3(RNT), 0, s, a);
+  const dim3 grid((unsigned)nwg), blk(RNT);
+  if (p3) {
+    if (dil != 2 || !relu) return MVBEV_ERR_SHAPE;  // conv2 -> conv3 of map_classifier (the only use)
+    hipLaunchKernelGGL((conv_wino_kernel<true, 2, true>), grid, blk, 0, s, a);
+  } else if (dil == 2) {
+    if (relu) hipLaunchKernelGGL((conv_wino_kernel<true, 2, false>), grid, blk, 0, s, a);
+    else hipLaunchKernelGGL((conv_wino_kernel<false, 2, false>), grid, blk, 0, s, a);
+  } else if (relu) {
+    hipLaunchKernelGGL((conv_wino_kernel<true, 1, false>), grid, blk, 0, s, a);
+  } else {
+    hipLaunchKernelGGL((conv_wino_kernel<false, 1, false>), grid, blk, 0, s, a);
+  }
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }
@@ -2042,7 +2068,12 @@ size_t mvbev_wino_rows_bytes(const mvbev_conv_desc* d) {
 
 int mvbev_wino_rows_split_bf16(const void* x, const mvbev_conv_desc* desc, const uint32_t* group_mask, void* t,
                                size_t t_bytes, void* stream) {
-  return mvbev::b3::wino_rows_launch(x, desc, group_mask, t, t_bytes, stream);
+  return mvbev::b3::wino_rows_launch(x, desc, 1, group_mask, t, t_bytes, stream);
+}
+
+int mvbev_wino_rows_split_bf16_dil(const void* x, const mvbev_conv_desc* desc, int dilation,
+                                   const uint32_t* group_mask, void* t, size_t t_bytes, void* stream) {
+  return mvbev::b3::wino_rows_launch(x, desc, dilation, group_mask, t, t_bytes, stream);
 }
 
 int mvbev_conv3x3_wino_bf16x3(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,
@@ -2050,6 +2081,22 @@ int mvbev_conv3x3_wino_bf16x3(const void* t, const mvbev_conv_desc* desc, const 
                               const uint32_t* group_mask, const int32_t* tile_order, void* stream) {
   return mvbev::b3::wino_launch(t, desc, w_packed, bias, init, Cout, relu, static_cast<float*>(y), y_layout,
                                 group_mask, tile_order, stream);
+}
+
+int mvbev_conv3x3_wino_bf16x3_dil(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,
+                                  int64_t Cout, int dilation, int relu, void* y, int y_layout, void* stream) {
+  return mvbev::b3::wino_launch(t, desc, w_packed, bias, nullptr, Cout, relu, static_cast<float*>(y), y_layout,
+                                nullptr, nullptr, stream, dilation);
+}
+
+int mvbev_conv3x3_wino_bf16x3_cout1_partials(const void* t, const mvbev_conv_desc* desc, const void* w_packed,
+                                             const float* bias, int64_t Cout, int dilation, int relu, const float* w3,
+                                             void* partials, size_t partials_bytes, void* stream) {
+  if (!desc || !w3 || !partials) return MVBEV_ERR_NULL;
+  const size_t need = mvbev_conv3x3_bf16x3_cout1_partials_bytes(desc, Cout);
+  if (need == 0 || partials_bytes < need) return MVBEV_ERR_SHAPE;
+  return mvbev::b3::wino_launch(t, desc, w_packed, bias, nullptr, Cout, relu, nullptr, MVBEV_LAYOUT_F32, nullptr,
+                                nullptr, stream, dilation, w3, static_cast<float*>(partials));
 }
 
 #if MVBEV_RING_STAMP

@@ -490,11 +490,13 @@ def wino_rows_bytes(desc) -> int:
     return int(_native.load().mvbev_wino_rows_bytes(ctypes.byref(desc)))
 
 
-def wino_rows(x: torch.Tensor, desc, t: torch.Tensor, group_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+def wino_rows(x: torch.Tensor, desc, t: torch.Tensor, group_mask: Optional[torch.Tensor] = None,
+              dilation: int = 1) -> torch.Tensor:
     """B^T over every 3-row output tile's 5 input rows of the split-bf16 ``x`` (addressed through
     ``desc`` as ``conv3x3_desc``) into ``t`` (bf16, >= ``wino_rows_bytes`` bytes; with
     ``group_mask`` zero-filled once and only written by this call with that mask):
-    ``mvbev_wino_rows_split_bf16``."""
+    ``mvbev_wino_rows_split_bf16``; ``dilation`` 2: conv2's interleaved row tiles, input rows
+    2 apart (``mvbev_wino_rows_split_bf16_dil``)."""
     _require_cuda(x, t)
     if x.dtype != torch.bfloat16 or t.dtype != torch.bfloat16 or not t.is_contiguous():
         raise TypeError("wino_rows reads the split-bf16 slab and writes a contiguous bf16 T")
@@ -505,9 +507,9 @@ def wino_rows(x: torch.Tensor, desc, t: torch.Tensor, group_mask: Optional[torch
         if group_mask.dtype != torch.int32 or group_mask.numel() < tiles or not group_mask.is_contiguous():
             raise ValueError(f"group_mask must be a contiguous int32 tensor of >= {tiles} tiles")
         gmp = group_mask.data_ptr()
-    st = _native.load().mvbev_wino_rows_split_bf16(x.data_ptr(), ctypes.byref(desc), gmp, t.data_ptr(),
-                                                   t.numel() * t.element_size(), _stream(x))
-    _native.check(st, "mvbev_wino_rows_split_bf16")
+    st = _native.load().mvbev_wino_rows_split_bf16_dil(x.data_ptr(), ctypes.byref(desc), int(dilation), gmp,
+                                                       t.data_ptr(), t.numel() * t.element_size(), _stream(x))
+    _native.check(st, "mvbev_wino_rows_split_bf16_dil")
     return t
 
 
@@ -666,6 +668,63 @@ def conv3x3_then_cout1_partials(x: torch.Tensor, desc, packed: torch.Tensor, cou
         int(dilation), int(bool(relu)), w3.data_ptr(), partials.data_ptr(),
         partials.numel() * partials.element_size(), _stream(x))
     _native.check(st, "mvbev_conv3x3_bf16x3_cout1_partials")
+
+
+def conv3x3_wino_dil(t: torch.Tensor, desc, packed: torch.Tensor, cout: int, dilation: int,
+                     bias: Optional[torch.Tensor] = None, relu: bool = False,
+                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The dense 3x3 conv of ``conv3x3_desc`` with ``dilation`` (1 or 2) from its row-Winograd
+    transform ``t`` (``wino_rows(..., dilation=dilation)``) and ``PackedConv3x3(..., wino=True)``
+    weights, no init / mask: ``mvbev_conv3x3_wino_bf16x3_dil``.  ``out`` fp32 or split-bf16."""
+    _require_cuda(t, packed)
+    B, W, out_rows = desc.B, desc.W, desc.out_rows
+    lib = _native.load()
+    if packed.numel() * packed.element_size() < lib.mvbev_conv3x3_packed_bytes_wino(cout, desc.K):
+        raise ValueError("packed weights are smaller than the Winograd conv needs")
+    if t.numel() * t.element_size() < wino_rows_bytes(desc):
+        raise ValueError("t is smaller than the descriptor's row-Winograd transform")
+    y_split = out is not None and out.dtype == torch.bfloat16
+    if out is None:
+        out = torch.empty((B, cout, out_rows, W), dtype=torch.float32, device=t.device)
+    elif y_split:
+        if tuple(out.shape) != split_shape(B, cout, out_rows, W) or not out.is_contiguous():
+            raise ValueError(f"a split out must be a contiguous bf16 {split_shape(B, cout, out_rows, W)} tensor")
+    elif tuple(out.shape) != (B, cout, out_rows, W) or not out.is_contiguous() or out.dtype != torch.float32:
+        raise ValueError(f"out must be a contiguous fp32 [{B},{cout},{out_rows},{W}] tensor")
+    b = bias.detach().contiguous() if bias is not None else None
+    st = lib.mvbev_conv3x3_wino_bf16x3_dil(t.data_ptr(), ctypes.byref(desc), packed.data_ptr(),
+                                           b.data_ptr() if b is not None else None, cout, int(dilation),
+                                           int(bool(relu)), out.data_ptr(),
+                                           _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32, _stream(t))
+    _native.check(st, "mvbev_conv3x3_wino_bf16x3_dil")
+    return out
+
+
+def conv3x3_wino_then_cout1_partials(t: torch.Tensor, desc, packed: torch.Tensor, cout: int,
+                                     bias: Optional[torch.Tensor], dilation: int, relu: bool,
+                                     weight3: torch.Tensor, partials: torch.Tensor) -> None:
+    """``conv3x3_then_cout1_partials`` from the row-Winograd transform ``t`` of its input
+    (``wino_rows(..., dilation=dilation)``) and ``PackedConv3x3(..., wino=True)`` weights:
+    ``mvbev_conv3x3_wino_bf16x3_cout1_partials`` (dilation 2, relu; the same partials)."""
+    _require_cuda(t, packed, weight3, partials)
+    if t.dtype != torch.bfloat16 or packed.dtype != torch.bfloat16:
+        raise TypeError("the Winograd conv -> cout1 path takes a bf16 T and bf16x3 Winograd weights")
+    if tuple(weight3.shape) != (1, cout, 3, 3):
+        raise ValueError(f"weight3 must be [1,{cout},3,3], got {tuple(weight3.shape)}")
+    if partials.dtype != torch.float32 or not partials.is_contiguous():
+        raise ValueError("partials must be a contiguous float32 tensor")
+    lib = _native.load()
+    if packed.numel() * packed.element_size() < lib.mvbev_conv3x3_packed_bytes_wino(cout, desc.K):
+        raise ValueError("packed weights are smaller than the Winograd conv needs")
+    if t.numel() * t.element_size() < wino_rows_bytes(desc):
+        raise ValueError("t is smaller than the descriptor's row-Winograd transform")
+    w3 = weight3.detach().contiguous()
+    b = bias.detach().contiguous() if bias is not None else None
+    st = lib.mvbev_conv3x3_wino_bf16x3_cout1_partials(
+        t.data_ptr(), ctypes.byref(desc), packed.data_ptr(), b.data_ptr() if b is not None else None, int(cout),
+        int(dilation), int(bool(relu)), w3.data_ptr(), partials.data_ptr(),
+        partials.numel() * partials.element_size(), _stream(t))
+    _native.check(st, "mvbev_conv3x3_wino_bf16x3_cout1_partials")
 
 
 def cout1_from_partials(partials: torch.Tensor, desc, cout: int, dilation3: int, map_row0: int, map_rows: int,
@@ -1127,6 +1186,11 @@ class BevFuse:
     @property
     def wino(self) -> bool:
         return bool(self.plan.wino)
+
+    @property
+    def wino2(self) -> bool:
+        """conv2 -> conv3 partials run row-Winograd (finite geometry; after prepare)."""
+        return bool(self.plan.wino2)
 
     def prepare(self, map_classifier, device) -> None:
         """Once per weight version: ``map_classifier`` the reference's nn.Sequential (:51-54)."""

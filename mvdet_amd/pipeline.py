@@ -62,6 +62,8 @@ class Workspace:
     p3: Optional[torch.Tensor] = None
     # keep y2 in HBM (the training forward: conv3's backward reads it), i.e. no conv2 -> conv3 fusion
     store_y2: bool = False
+    # row-Winograd transform of y1 for conv2 (dilation 2; allocated on first use)
+    wino_t2: Optional[torch.Tensor] = None
     # row-Winograd transform of the slab for conv1 (bf16, zero-filled on first use; only the
     # frustum mask's (tile, slot) pairs are ever written)
     wino_t: Optional[torch.Tensor] = None
@@ -83,7 +85,8 @@ class ProjectFuse:
                  channels: int, mid_channels: int = 512, slot_views: Optional[Sequence[Optional[int]]] = None,
                  precision: str = "bf16x3", slab_dtype: torch.dtype = torch.float32,
                  all_views: bool = True, split_k: bool = True, frustum: bool = True, fuse_conv3: bool = True,
-                 edge_strip: bool = True, wino_conv1: bool = True, wino_warp: bool = True):
+                 edge_strip: bool = True, wino_conv1: bool = True, wino_warp: bool = True,
+                 wino_conv2: bool = True):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":
@@ -155,6 +158,11 @@ class ProjectFuse:
         # separate transform); inference over the whole grid from fp32 features only (cfg2:
         # 0.55 ms vs warp 0.36 + transform 0.26)
         self.wino_warp = self.wino_conv1 and wino_warp
+        # wino_conv2 (default): conv2 (dilation 2) -> conv3 partials as row-Winograd too (ops.wino_rows
+        # with dilation 2 over y1, then conv3x3_wino_then_cout1_partials); under the same geometry
+        # condition as conv1 (a NaN in y1 would spread over a 3-row tile)
+        self.wino_conv2 = wino_conv2 and precision == "bf16x3" and self.y1_split
+        self.pack2w = ops.PackedConv3x3(None, "bf16x3", wino=True) if self.wino_conv2 else None
 
     # -- buffers ----------------------------------------------------------------------------
     def workspace(self, B: int, device, band: Optional[Tuple[int, int]] = None,
@@ -488,8 +496,22 @@ class ProjectFuse:
         need = ops.conv3x3_cout1_partials_bytes(d2, self.mid)
         if ws.p3 is None or ws.p3.numel() * 4 < need:
             ws.p3 = torch.empty((need + 3) // 4, dtype=torch.float32, device=ws.y1.device)
+        if self.wino_conv2_active(ws):
+            tneed = ops.wino_rows_bytes(d2)
+            if ws.wino_t2 is None or ws.wino_t2.numel() * 2 < tneed:
+                ws.wino_t2 = torch.zeros((tneed + 1) // 2, dtype=torch.bfloat16, device=ws.y1.device)
+            ops.wino_rows(ws.y1, d2, ws.wino_t2, dilation=2)
+            ops.conv3x3_wino_then_cout1_partials(ws.wino_t2, d2, self.pack2w.get(conv2.weight), self.mid,
+                                                 conv2.bias, 2, True, conv3.weight, ws.p3)
+            return
         ops.conv3x3_then_cout1_partials(ws.y1, d2, self.pack2.get(conv2.weight), self.mid, conv2.bias, 2, True,
                                         conv3.weight, ws.p3)
+
+    def wino_conv2_active(self, ws: Workspace) -> bool:
+        """conv2 -> conv3 partials run row-Winograd: requested (``wino_conv2``), y1 split-bf16 and no
+        view's geometry can make y1 non-finite (as ``wino_active`` for conv1)."""
+        return (self.wino_conv2 and ws.y1.dtype == torch.bfloat16
+                and self.nonfinite_views(ws.y1.device) == 0)
 
     def conv3_from_partials(self, ws: Workspace, conv3: torch.nn.Conv2d) -> torch.Tensor:
         """The rest of a9: map rows ``ws.band`` from the partials (fixed summation order)."""

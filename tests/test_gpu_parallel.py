@@ -37,14 +37,14 @@ def _setup(seed=31, C=64, B=2):
 
 @pytest.mark.parametrize("wino", [False, True])
 def test_band_fusion_matches_whole_grid(wino):
-    """Row bands (the multi-GPU fusion) vs the whole grid: bitwise with the direct conv1; with
-    the row-Winograd conv1 a band's 3-row tiles start at its own first row, so its sums are
+    """Row bands (the multi-GPU fusion) vs the whole grid: bitwise with the direct conv1 and conv2;
+    with the row-Winograd convs a band's 3-row tiles start at its own first row, so its sums are
     grouped differently: fp32 rounding level."""
     from mvdet_amd import ProjectFuse
     from mvdet_amd.parallel import row_band
     ds, pm, up, grid, C, B, feats, mc = _setup()
     mc = mc.to("cuda:0")
-    eng = ProjectFuse(pm, up, grid, C, split_k=False, wino_conv1=wino)  # split-K tails re-associate K sums
+    eng = ProjectFuse(pm, up, grid, C, split_k=False, wino_conv1=wino, wino_conv2=wino)  # split-K tails re-associate K sums
     with torch.no_grad():
         full = eng.project_fuse([f.cuda() for f in feats], mc).cpu()
         for P in (3, 5):

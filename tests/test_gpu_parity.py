@@ -568,9 +568,11 @@ def test_conv2_conv3_fused_matches_unfused(band):
     mc = mc.to(DEV)
     outs = {}
     for fused in (True, False):
-        # the direct conv1: bands are bitwise the whole grid (the Winograd conv1's 3-row tiles
-        # start at the band's first row, so its band sums group differently)
-        eng = ProjectFuse(pm, tuple(up), tuple(ds.reducedgrid_shape), C, fuse_conv3=fused, wino_conv1=False)
+        # the direct conv1 and conv2: bands are bitwise the whole grid (the Winograd convs' 3-row
+        # tiles start at the band's first row, so their band sums group differently;
+        # test_gpu_wino.py covers the Winograd conv2's partials)
+        eng = ProjectFuse(pm, tuple(up), tuple(ds.reducedgrid_shape), C, fuse_conv3=fused, wino_conv1=False,
+                          wino_conv2=False)
         with torch.no_grad():
             ws = eng.workspace(1, DEV, band=band)
             eng.warp_views(ws, [0, 1], feats)

@@ -240,3 +240,115 @@ def test_fused_warp_transform_matches_two_pass(cfg):
             fused.conv1_partial(wf, mc, torch.empty((B, 512) + grid, device=DEV))
         fused.wino_conv1 = True
     assert_parity(m3.cpu(), ref.cpu(), "slab path after the fused warp", normwise_tol=TOL)
+
+
+# -- conv2 (dilation 2) -> conv3 partials as row-Winograd (ABI 11500) ------------------------------
+def _conv2_setup(B, K, H, W, rows, cout, seed):
+    """y1-like split-bf16 input, conv2 weights / bias, conv3 weight, and the float64 reference
+    map = conv2d_d4(relu(conv2d_d2(x) + b2), w3) over the output band ``rows``."""
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(B, K, H, W, generator=g)
+    w = (torch.rand(cout, K, 3, 3, generator=g) - 0.5) / np.sqrt(K * 9)
+    bias = torch.rand(cout, generator=g) - 0.5
+    w3 = (torch.rand(1, cout, 3, 3, generator=g) - 0.5) / np.sqrt(cout * 9)
+    y2 = F.relu(F.conv2d(x.double(), w.double(), bias.double(), padding=2, dilation=2))
+    ref = F.conv2d(y2, w3.double(), padding=4, dilation=4)[:, :, rows[0]:rows[1]].float()
+    xs = _split_encode(x).to(DEV)
+    r0, r1 = max(0, rows[0] - 4), min(H, rows[1] + 4)  # conv2's output rows the map band reads
+    desc = ops.conv_desc(B, K, H, W, group=K, group_stride=0, batch_stride=K * H * W, out_row0=r0,
+                         out_rows=r1 - r0)
+    return x, xs, w.to(DEV), bias.to(DEV), w3.to(DEV), y2, ref, desc
+
+
+def test_wino_rows_dilation2_matches_numpy():
+    """conv2's transform: row tile (r, r + 2, r + 4), r = 12 (r3 / 4) + {0, 1, 6, 7}[r3 % 4];
+    T = B^T over input rows r - 2 + 2 m (zero outside the image)."""
+    from mvdet_amd import ops
+    B, K, H, W = 1, 16, 29, 40
+    x, xs, *_, desc = _conv2_setup(B, K, H, W, (0, H), 128, seed=11)
+    t = torch.zeros(ops.wino_rows_bytes(desc) // 2, dtype=torch.bfloat16, device=DEV)
+    ops.wino_rows(xs, desc, t, dilation=2)
+    R5 = 5 * 4 * (-(-H // 12))
+    T = t.view(B, K // 8, R5, W, 2, 8).float().cpu()
+    T = (T[..., 0, :] + T[..., 1, :]).permute(0, 1, 4, 2, 3).reshape(B, K, R5, W).double().numpy()
+    xe = (x.to(torch.bfloat16).float() + (x - x.to(torch.bfloat16).float()).to(torch.bfloat16).float()).double().numpy()
+    for r3 in range(R5 // 5):
+        base = 12 * (r3 // 4) + (0, 1, 6, 7)[r3 % 4]
+        d = np.zeros((5, B, K, W))
+        for m in range(5):
+            row = base - 2 + 2 * m
+            if 0 <= row < H:
+                d[m] = xe[:, :, row]
+        want = np.einsum("xm,mbkw->bkxw", BT, d)
+        np.testing.assert_allclose(T[:, :, 5 * r3:5 * r3 + 5], want, rtol=0, atol=2e-5 * max(1.0, np.abs(want).max()))
+
+
+@pytest.mark.parametrize("B,K,H,W,rows", [(1, 64, 30, 70, (0, 30)),    # partial tile row and column
+                                          (2, 32, 41, 100, (9, 33)),  # map band, B = 2
+                                          (1, 128, 12, 32, (0, 12))])  # one tile
+def test_wino_conv2_partials_vs_float64_and_direct(B, K, H, W, rows):
+    """conv2 -> conv3 partials from the dilation-2 transform (the inference default) vs float64
+    and vs the direct ring conv's partials (mvbev_conv3x3_bf16x3_cout1_partials)."""
+    from mvdet_amd import ops
+    cout = 256
+    x, xs, w, bias, w3, y2, ref, desc = _conv2_setup(B, K, H, W, rows, cout, seed=B * H + W)
+    t = torch.zeros(ops.wino_rows_bytes(desc) // 2, dtype=torch.bfloat16, device=DEV)
+    ops.wino_rows(xs, desc, t, dilation=2)
+    need = ops.conv3x3_cout1_partials_bytes(desc, cout)
+    p_w = torch.empty(need // 4, dtype=torch.float32, device=DEV)
+    ops.conv3x3_wino_then_cout1_partials(t, desc, ops.PackedConv3x3(None, "bf16x3", wino=True).get(w), cout, bias,
+                                         2, True, w3, p_w)
+    got = ops.cout1_from_partials(p_w, desc, cout, 4, rows[0], rows[1] - rows[0]).cpu()
+    p_d = torch.empty_like(p_w)
+    ops.conv3x3_then_cout1_partials(xs, desc, ops.PackedConv3x3(None, "bf16x3").get(w), cout, bias, 2, True, w3, p_d)
+    direct = ops.cout1_from_partials(p_d, desc, cout, 4, rows[0], rows[1] - rows[0]).cpu()
+    s = assert_parity(got, ref, "wino conv2->conv3 vs float64", normwise_tol=TOL)
+    sd = assert_parity(direct, ref, "direct conv2->conv3 vs float64", normwise_tol=TOL)
+    assert s["normwise"] <= max(4 * sd["normwise"], 2e-6), (s, sd)
+    # the dense dilation-2 conv from the same T (y stored): vs float64 relu(conv2)
+    y = ops.conv3x3_wino_dil(t, desc, ops.PackedConv3x3(None, "bf16x3", wino=True).get(w), cout, 2, bias=bias,
+                             relu=True)
+    r0 = desc.out_row0
+    assert_parity(y.cpu(), y2[:, :, r0:r0 + desc.out_rows].float(), "wino conv2 y", normwise_tol=TOL)
+
+
+def test_wino_conv2_refusals():
+    from mvdet_amd import _native, ops
+    B, K, H, W, cout = 1, 16, 12, 32, 128
+    x, xs, w, bias, w3, y2, ref, desc = _conv2_setup(B, K, H, W, (0, H), cout, seed=3)
+    t = torch.zeros(ops.wino_rows_bytes(desc) // 2, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(_native.NativeError):
+        ops.wino_rows(xs, desc, t, dilation=3)
+    pk = ops.PackedConv3x3(None, "bf16x3", wino=True).get(w)
+    p = torch.empty(ops.conv3x3_cout1_partials_bytes(desc, cout) // 4, dtype=torch.float32, device=DEV)
+    with pytest.raises(_native.NativeError):  # the partials epilogue is conv2's: dilation 2 only
+        ops.conv3x3_wino_then_cout1_partials(t, desc, pk, cout, bias, 1, True, w3, p)
+    with pytest.raises(ValueError):
+        ops.conv3x3_wino_then_cout1_partials(t[:16], desc, pk, cout, bias, 2, True, w3, p)
+
+
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_engine_wino_conv2_matches_direct(cfg):
+    """ProjectFuse's inference map with the Winograd conv2 (default) vs wino_conv2=False, same inputs."""
+    from mvdet_amd import ProjectFuse, synthetic
+    from mvdet_amd.geometry import projection_matrices
+    spec = synthetic.CONFIGS[cfg]
+    ds = spec["make"]()
+    N, C = ds.num_cam, 32
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    pm = projection_matrices(ds)
+    feats = [synthetic.synthetic_features(1, C, [u // 3 for u in up], up, seed=v, device=DEV) for v in range(N)]
+    torch.manual_seed(cfg)
+    mc = torch.nn.Sequential(torch.nn.Conv2d(N * C + 2, 512, 3, padding=1), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False)).to(DEV)
+    a = ProjectFuse(pm, up, grid, C)
+    b = ProjectFuse(pm, up, grid, C, wino_conv2=False)
+    assert a.wino_conv2 and not b.wino_conv2
+    with torch.no_grad():
+        ma = a.project_fuse(feats, mc)
+        assert a.workspace(1, DEV).wino_t2 is not None  # the Winograd conv2 ran
+        mb = b.project_fuse(feats, mc)
+        assert b.workspace(1, DEV).wino_t2 is None
+    assert_parity(ma.cpu(), mb.cpu(), "wino conv2 map vs direct conv2 map", normwise_tol=TOL)

@@ -125,7 +125,7 @@ def main():
     pm = projection_matrices(ds)
     mc = build_mc(C, N, head_params(N, args.config, C), dev)
     eng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision, frustum=not args.no_frustum,
-                      wino_conv1=False)  # the direct conv1 stages (the Winograd ones use weng)
+                      wino_conv1=False, wino_conv2=False)  # the direct conv stages (the Winograd ones use weng)
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=v, device=dev) for v in range(N)]
     bfeats = [synthetic.backbone_features(B, C, [u // 3 for u in up], seed=v, device=dev) for v in range(N)]
     ws = eng.workspace(B, dev)
@@ -167,6 +167,9 @@ def main():
             # conv2 -> conv3 fused (the default inference path): partials epilogue + reduce
             "conv23": (lambda: (eng.conv2_partials(ws, mc[2], mc[4]), eng.conv3_from_partials(ws, mc[4])),
                        2.0 * B * ho * wo * 9 * 512 * 512),
+            # the same with the row-Winograd conv2 (dilation-2 transform of y1 + conv; inference default)
+            "conv23w": (lambda: (weng.conv2_partials(wws, mc[2], mc[4]), weng.conv3_from_partials(wws, mc[4])),
+                        2.0 * B * ho * wo * 9 * 512 * 512),
         }
         if {"adjup", "adj"} & set(args.only.split(",")):
             # the warp adjoints of the training step (autograd.py) on a random split grad_out

@@ -1372,10 +1372,10 @@ namespace wino {
 constexpr int NXI = 5;                            // transformed rows per 3-row output tile
 constexpr int XH = 4 * NXI;                       // T rows of a 12-row workgroup tile
 #ifndef MVBEV_WINO_NIW
-#define MVBEV_WINO_NIW 8  // DMA-issuing waves (cfg2 winoconv: 8 1.59-1.67 ms, 4 1.73-1.79)
+#define MVBEV_WINO_NIW 4  // DMA-issuing waves, one per SIMD (cfg2 winoconv, buffer-load DMAs: 4 1.40 ms, 8 1.51-1.52; with the per-unit address arithmetic of round 2: 8 1.59-1.67, 4 1.73-1.79)
 #endif
 #ifndef MVBEV_WINO_XAUX
-#define MVBEV_WINO_XAUX 2  // cache policy of the T DMAs (2 = nt: T is streamed, the weights stay in L2; -2 %)
+#define MVBEV_WINO_XAUX 0  // cache policy of the T DMAs (0 = default; with buffer-load DMAs and 4 issuing waves nt (2) measured +0.5 % on conv1, +1 % on conv2: conv2's T is re-read by the 4 Cout tiles)
 #endif
 constexpr int NIW = MVBEV_WINO_NIW;               // DMA-issuing waves
 constexpr int NIT = 64 * NIW;
@@ -1388,7 +1388,7 @@ template <int DIL> struct Geo {
   static constexpr int TROW = 2 * 2 * 4 * XW;          // T entries of a unit (544 / 576)
   static constexpr int NXT = (TROW + NIT - 1) / NIT;   // T DMAs per issuing wave per unit (2)
 };
-constexpr int NXTMAX = 2;
+constexpr int NXTMAX = (2 * 2 * 4 * (TW + 4) + NIT - 1) / NIT;  // T pieces of the widest (dilation 2) unit
 static_assert(Geo<1>::NXT <= NXTMAX && Geo<2>::NXT <= NXTMAX, "T pieces");
 constexpr int SLOT = RUNIT + NXTMAX * NIT;        // 16-B entries per ring slot
 constexpr int NSLOT = 4;                          // 3 units of DMA in flight

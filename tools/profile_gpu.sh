@@ -22,7 +22,7 @@ for PMC in "GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCL
            "GRBM_GUI_ACTIVE TA_TA_BUSY_sum TD_TD_BUSY_sum SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $PMC --output-format csv -d $OUT/${TAG}_pmc$i -o run -- \
-    python3 tools/kbench.py --config $CFG --reps 3 --only warpw,warpupw,winoconv,conv23 > $OUT/${TAG}_pmc$i.log 2>&1 || exit $?
+    python3 tools/kbench.py --config $CFG --reps 3 --only warpw,warpupw,winoconv,conv23w > $OUT/${TAG}_pmc$i.log 2>&1 || exit $?
 done
 python3 tools/pmc_summary.py $OUT/${TAG}_pmc* > $OUT/${TAG}_pmc_summary.txt
 python3 tools/traffic.py $OUT $TAG $CFG bf16x3 wino > $OUT/${TAG}_traffic.json

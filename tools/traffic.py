@@ -46,7 +46,10 @@ for name in vals:
 # edge-strip tiles "<1, true, false, EW>"), or the fp32-MFMA kernel
 pat = r"conv_ring_kernel<1, true(, false, \d+)?>" if precision == "bf16x3" else r"conv3x3_mfma_f32_kernel<1, true"
 if wino:
-    pat = r"conv_wino_kernel<true>"
+    pat = r"conv_wino_kernel<true, 1, false>"
+    c2 = [k for k in res["kernels"] if "conv_wino_kernel<true, 2, true>" in k]
+    if c2:  # conv2 -> conv3 partials, row-Winograd (ABI 11500)
+        res["conv2_hbm_bytes_per_launch"] = res["kernels"][c2[0]]["hbm_bytes_per_launch"]
     rows = [k for k in res["kernels"] if "wino_rows_kernel" in k]
     if rows:
         res["wino_rows_hbm_bytes_per_launch"] = res["kernels"][rows[0]]["hbm_bytes_per_launch"]

@@ -140,7 +140,8 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
     half = config == 4
     eng = ProjectFuse(pm, up, (ho, wo), C, precision=precision,
                       slab_dtype=torch.float16 if half else torch.float32,
-                      wino_conv1=args.conv1 == "wino" and precision == "bf16x3")
+                      wino_conv1=args.conv1 == "wino" and precision == "bf16x3",
+                      wino_conv2=args.conv1 == "wino" and precision == "bf16x3")
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * config + v,
                                           device=dev).to(torch.float16 if half else torch.float32)
              for v in range(N)]
@@ -180,6 +181,7 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
     t_c1k = t_c1 - t_rows  # conv1's conv kernel alone
     t_c2 = avg(ev["conv2"], ev["conv3"])
     t_c3 = avg(ev["conv3"], end_ev)
+    wino2 = eng.wino_conv2_active(ws)  # conv2 -> conv3 partials as row-Winograd
     value = B * K / dt
     # algorithmic work; conv1 runs over the N*C view channels per step (the
     # 2 coord channels are folded into a per-weight-version init term)
@@ -276,7 +278,13 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
                      # PMC bytes (read at 128-B granules: NCHW rows are gathered, not streamed)
                      "traffic": warp_traffic,
                      "physical_GBs": round(warp_traffic / (t_warp * 1e-3) / 1e9, 1) if warp_traffic else None},
-            "conv2": {"bound": "mfma", "algorithmic_fp32_TFs": round(conv2_flop / (t_c2 * 1e-3) / 1e12, 2)},
+            "conv2": {"bound": "mfma", "algorithmic_fp32_TFs": round(conv2_flop / (t_c2 * 1e-3) / 1e12, 2),
+                      # executed bf16 MFMA work over conv2's stage time (its dilation-2 row transform
+                      # included when row-Winograd: 3 passes x 5/9 of the direct products)
+                      "executed_bf16_frac": (round(3 * conv2_flop * (5.0 / 9.0 if wino2 else 1.0) / (t_c2 * 1e-3)
+                                                   / (BF16_MFMA_PEAK_TFS * 1e12), 4)
+                                             if precision == "bf16x3" else None),
+                      "form": "row-Winograd F(3,3), dilation 2" if wino2 else "direct"},
             "conv3": {"bound": "hbm", "achieved_GBs": round(conv3_bytes / (t_c3 * 1e-3) / 1e9, 1),
                       "peak_GBs": HBM_PEAK_GBS},
         },
@@ -306,7 +314,8 @@ def run_plus_a4(args, precision, steps, warmup):
     pm = projection_matrices(ds)
     mc = build_mc(C, N, head_params(N, seed=args.config, C=C), dev)
     eng = ProjectFuse(pm, up, (ho, wo), C, precision=precision,
-                      wino_conv1=args.conv1 == "wino" and precision == "bf16x3")
+                      wino_conv1=args.conv1 == "wino" and precision == "bf16x3",
+                      wino_conv2=args.conv1 == "wino" and precision == "bf16x3")
     flo = [synthetic.backbone_features(B, C, lo, seed=1000 * args.config + v, device=dev) for v in range(N)]
     ws = eng.workspace(B, dev)
     views = list(range(N))
@@ -466,7 +475,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--conv1", default="wino", choices=["direct", "wino"],
-                    help="conv1 form (bf16x3): the direct ring conv or row-Winograd F(3,3) (ProjectFuse wino_conv1)")
+                    help="form of conv1 and conv2 (bf16x3): the direct ring convs or row-Winograd F(3,3) "
+                         "(ProjectFuse wino_conv1 / wino_conv2)")
     ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3"],
                     help="conv1/conv2 arithmetic: 3xbf16 split (default) or fp32-input MFMA")
     ap.add_argument("--config", type=int, default=2, help="BASELINE.json config index (1-based)")

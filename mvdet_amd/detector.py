@@ -42,7 +42,7 @@ from .pipeline import ProjectFuse
 
 class PerspTransDetector(nn.Module):
     def __init__(self, dataset, arch: str = "resnet18", device=None, precision: str = "bf16x3",
-                 wino_conv1: bool = True):
+                 wino_conv1: bool = True, wino_conv2: bool = True):
         super().__init__()
         self.num_cam = dataset.num_cam
         self.img_shape, self.reducedgrid_shape = list(dataset.img_shape), list(dataset.reducedgrid_shape)
@@ -61,10 +61,10 @@ class PerspTransDetector(nn.Module):
                                             nn.Conv2d(512, 512, 3, padding=2, dilation=2), nn.ReLU(),
                                             nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False))
         self.to(self._device)
-        # inference conv1 as row-Winograd F(3,3) (ProjectFuse.conv1_wino); training keeps the direct
-        # conv (its backward reads the direct form's operands)
+        # inference conv1 and conv2 as row-Winograd F(3,3) (ProjectFuse.conv1_wino, conv2_partials);
+        # training keeps the direct convs (their backward reads the direct form's operands)
         self.engine = ProjectFuse(self.proj_mats, tuple(self.upsample_shape), tuple(self.reducedgrid_shape),
-                                  out_channel, precision=precision, wino_conv1=wino_conv1)
+                                  out_channel, precision=precision, wino_conv1=wino_conv1, wino_conv2=wino_conv2)
 
     # -- hot path --------------------------------------------------------------------------
     def _needs_autograd(self) -> bool:

@@ -161,12 +161,15 @@ __global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_tile_kernel(const Warp
 #define MVBEV_WW_STAGE 384  // max staged box pixels per channel (8 channels x 384 x 4 B = 12 KiB); 0 = off
 #endif
 constexpr int kWwStage = MVBEV_WW_STAGE;
+#ifndef MVBEV_WW_QUAD
+#define MVBEV_WW_QUAD 1  // stage the box with 16-B loads where the source allows (stage_box_load)
+#endif
 
 template <bool PAIR>
 __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(const WarpArgs a, int r3_rows) {
   __shared__ __attribute__((aligned(16))) float ds[kWwRows][kWwCols][8];  // [row][col][channel]
   __shared__ unsigned char nz[kWwRows][kWwCols];
-  __shared__ float stage[kWarpCPB * (kWwStage > 0 ? kWwStage : 1)];
+  __shared__ __attribute__((aligned(16))) float stage[kWarpCPB * (kWwStage > 0 ? kWwStage : 1)];
   __shared__ int box[4];  // source rows [box0, box1], columns [box2, box3] of the block's corners
   const int lb = xcd_remap(blockIdx.x, a.nwg);
   const int tile = lb % a.tiles;
@@ -223,21 +226,15 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
     }
   }
   __syncthreads();
-  const int R = box[1] - box[0] + 1, Cb = box[3] - box[2] + 1;
-  const bool staged = kWwStage > 0 && box[1] >= 0 && R * Cb <= kWwStage;  // uniform per block
   const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
-  if (staged) {  // the box of every channel of the group: rows of Cb floats, 32 lanes a row
-    const int n = R * Cb;
-    for (int r = tid / 32; r < R; r += kWwThreads / 32)
-      for (int cc = tid % 32; cc < Cb; cc += 32) {
-        float t[kWarpCPB];
-#pragma unroll
-        for (int j = 0; j < kWarpCPB; ++j)
-          t[j] = base[(int64_t)min(c_begin + j, c_end - 1) * vw.sC + (int64_t)(box[0] + r) * vw.sH +
-                      (int64_t)(box[2] + cc) * vw.sW];
-#pragma unroll
-        for (int j = 0; j < kWarpCPB; ++j) stage[j * n + r * Cb + cc] = t[j];
-      }
+  const bool quad_ok = vw.sW == 1 && (W & 3) == 0 && (vw.sH & 3) == 0 && (vw.sC & 3) == 0 &&
+                       (reinterpret_cast<uintptr_t>(base) & 15) == 0;
+  const StageBox sb = stage_box_shape(box, W, quad_ok && MVBEV_WW_QUAD);
+  const int R = sb.R, Cb = sb.pitch;
+  // uniform per block (the staged path needs unit column stride: the non-quad loads assume it too)
+  const bool staged = kWwStage > 0 && box[1] >= 0 && vw.sW == 1 && R * Cb <= kWwStage;
+  if (staged) {
+    stage_box_load<kWwThreads>(base, vw.sC, vw.sH, c_begin, c_end, sb, stage, tid);
     __syncthreads();
   }
   if (i < kWwRows) {  // phase 1: one warped pixel (8 channels) per thread
@@ -262,7 +259,7 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
         if (staged) {
           const int n = R * Cb;
           const int t0 = (cy0 - box[0]) * Cb, t1 = (cy1 - box[0]) * Cb;
-          const int l0 = cx0 - box[2], l1 = cx1 - box[2];
+          const int l0 = cx0 - sb.c0, l1 = cx1 - sb.c0;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float* sj = stage + j * n;

@@ -224,6 +224,57 @@ __device__ inline unsigned pack_bf16x2(float x, float y) {
          ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)y) << 16);
 }
 
+typedef float f32x4a_t __attribute__((ext_vector_type(4)));  // 16-B aligned
+
+// The staging box of a fused-warp block: source rows [r0, r0 + R) x columns [c0, c0 + pitch)
+// of its 8 channels (fp32, unit column stride), staged as stage[j][r][col - c0].  With quad
+// (uniform: the row / channel pitches, the source base and W multiples of 4 floats, 16-B
+// aligned) the box is widened to whole aligned 16-B quads — one 16-B load per (row, quad,
+// channel) and a 16-B LDS store, a quarter of the load instructions of one float per lane
+// (the load path, TA/TD, binds these kernels); else one float per lane, 32 lanes a row.
+struct StageBox {
+  int r0, R, c0, pitch;  // pitch = staged columns per row
+  bool quad;
+};
+__device__ inline StageBox stage_box_shape(const int (&box)[4], int W, bool quad_ok) {
+  StageBox sb;
+  sb.r0 = box[0];
+  sb.R = box[1] - box[0] + 1;
+  sb.quad = quad_ok;
+  sb.c0 = quad_ok ? (box[2] & ~3) : box[2];
+  const int c1 = quad_ok ? min((box[3] | 3) + 1, W) : box[3] + 1;  // W % 4 == 0 when quad_ok
+  sb.pitch = c1 - sb.c0;
+  return sb;
+}
+template <int NT>
+__device__ inline void stage_box_load(const float* __restrict__ base, int64_t sC, int64_t sH, int c_begin, int c_end,
+                                      const StageBox& sb, float* __restrict__ stage, int tid) {
+  const int n = sb.R * sb.pitch;
+  if (sb.quad) {
+    const int Q = sb.pitch >> 2, items = sb.R * Q;
+    for (int it = tid; it < items; it += NT) {
+      const int r = it / Q, q = it - r * Q;
+      const float* src = base + (int64_t)(sb.r0 + r) * sH + sb.c0 + 4 * q;
+      f32x4a_t t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        t[j] = *reinterpret_cast<const f32x4a_t*>(src + (int64_t)min(c_begin + j, c_end - 1) * sC);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4a_t*>(stage + j * n + r * sb.pitch + 4 * q) = t[j];
+    }
+  } else {
+    for (int r = tid / 32; r < sb.R; r += NT / 32)
+      for (int cc = tid % 32; cc < sb.pitch; cc += 32) {
+        float t[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          t[j] = base[(int64_t)min(c_begin + j, c_end - 1) * sC + (int64_t)(sb.r0 + r) * sH + sb.c0 + cc];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) stage[j * n + r * sb.pitch + cc] = t[j];
+      }
+  }
+}
+
 __device__ inline void wino_rows_phase2(const float (&ds)[kWwRows][kWwCols][8], const unsigned char (&nz)[kWwRows][kWwCols],
                                         const WarpView& vw, const WarpArgs& a, int b, int chunk, int k, int tx,
                                         int r3_rows) {

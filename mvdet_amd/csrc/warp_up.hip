@@ -144,12 +144,15 @@ __global__ __launch_bounds__(kUpTH * kUpTW) void warp_up_kernel(const UpArgs ua)
 #ifndef MVBEV_UPW_STAGE
 #define MVBEV_UPW_STAGE 384  // max staged box pixels per channel (8 channels x 384 x 4 B = 12 KiB); 0 = off
 #endif
+#ifndef MVBEV_UPW_QUAD
+#define MVBEV_UPW_QUAD 1  // stage the box with 16-B loads where the source allows (stage_box_load)
+#endif
 constexpr int kUpStage = MVBEV_UPW_STAGE;
 
 __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino_kernel(const UpArgs ua, int r3_rows) {
   __shared__ __attribute__((aligned(16))) float ds[kWwRows][kWwCols][8];
   __shared__ unsigned char nz[kWwRows][kWwCols];
-  __shared__ float stage[kUpCPB * (kUpStage > 0 ? kUpStage : 1)];
+  __shared__ __attribute__((aligned(16))) float stage[kUpCPB * (kUpStage > 0 ? kUpStage : 1)];
   __shared__ int box[4];  // source rows [box0, box1], columns [box2, box3] of the block's windows
   const WarpArgs& a = ua.w;
   const int lb = xcd_remap(blockIdx.x, a.nwg);
@@ -201,20 +204,14 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino_kernel
     }
   }
   __syncthreads();
-  const int R = box[1] - box[0] + 1, Cb = box[3] - box[2] + 1;
-  const bool staged = kUpStage > 0 && box[1] >= 0 && R * Cb <= kUpStage;  // uniform per block
   const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
-  if (staged) {  // the box of every channel of the group: rows of Cb contiguous floats, 32 lanes a row
-    const int n = R * Cb;
-    for (int r = tid / 32; r < R; r += kWwThreads / 32)
-      for (int cc = tid % 32; cc < Cb; cc += 32) {
-        float t[kUpCPB];
-#pragma unroll
-        for (int j = 0; j < kUpCPB; ++j)
-          t[j] = base[(int64_t)min(c_begin + j, c_end - 1) * vw.sC + (int64_t)(box[0] + r) * vw.sH + box[2] + cc];
-#pragma unroll
-        for (int j = 0; j < kUpCPB; ++j) stage[j * n + r * Cb + cc] = t[j];
-      }
+  const bool quad_ok = (w & 3) == 0 && (vw.sH & 3) == 0 && (vw.sC & 3) == 0 &&
+                       (reinterpret_cast<uintptr_t>(base) & 15) == 0;
+  const StageBox sb = stage_box_shape(box, w, quad_ok && MVBEV_UPW_QUAD);
+  const int R = sb.R, Cb = sb.pitch;
+  const bool staged = kUpStage > 0 && box[1] >= 0 && R * Cb <= kUpStage;  // uniform per block
+  if (staged) {  // the box of every channel of the group (16-B loads where the source allows)
+    stage_box_load<kWwThreads>(base, vw.sC, vw.sH, c_begin, c_end, sb, stage, tid);
     __syncthreads();
   }
   if (i < kWwRows) {
@@ -237,7 +234,7 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino_kernel
         for (int r = 0; r < 3; ++r)
 #pragma unroll
           for (int q = 0; q < 3; ++q)
-            idx[r][q] = (min(uw.rb + r, h - 1) - box[0]) * Cb + (min(uw.cb + q, w - 1) - box[2]);
+            idx[r][q] = (min(uw.rb + r, h - 1) - box[0]) * Cb + (min(uw.cb + q, w - 1) - sb.c0);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const float* sj = stage + j * n;

@@ -279,7 +279,8 @@ int mvbev_conv3x3_bf16x3_ex3(const void* x, int x_layout, const mvbev_conv_desc*
  * nn.Conv2d(512*N+2, 512, 3, padding=1) forward, :51), in two steps:
  *   1. mvbev_wino_rows_split_bf16: the split-bf16 input x (desc as mvbev_conv3x3_bf16x3_ex) ->
  *      T = B^T over each 3-row output tile's 5 input rows, split-bf16 blocked
- *      [B][K/8][5 * 4 * ceil(out_rows / 12)][W][hi, lo][8] (mvbev_wino_rows_bytes).  With
+ *      [B][K/8][5 * 4 * ceil(out_rows / 12)][hi, lo][W][8] (mvbev_wino_rows_bytes; ABI 11500: a row's hi plane, then
+ *      its lo plane — was [W][hi, lo][8]).  With
  *      group_mask (12 x 32 tiles, as the conv) the cleared (tile, group) pairs are not written:
  *      T must then be zero-filled once and only ever written by this call with the same mask.
  *   2. mvbev_conv3x3_wino_bf16x3: y from T (desc: B, K, H, W, group, out_row0, out_rows as in
@@ -289,8 +290,8 @@ int mvbev_conv3x3_bf16x3_ex3(const void* x, int x_layout, const mvbev_conv_desc*
 /* Warp + the row transform of step 1 in one pass, from fp32 sources (mvbev_warp_views_split_bf16's
  * views and matrices): the T rows of r3_rows 3-row output tiles (3 * r3_rows >= Ho; the conv's
  * T has 4 * ceil(out_rows / 12) of them) are written for each view's channels at its dst, whose
- * dst_strides are in 32-byte units: [0] per batch item, [1] per 8-channel group, [2] per T row,
- * [3] = 1 — the view's slice of T.  The warped slab itself is never written.  flags:
+ * dst_strides are in 32-byte units: [0] per batch item, [1] per 8-channel group, [2] per T row
+ * (= Wo: the row's hi plane, then its lo plane), [3] = 1 — the view's slice of T.  The warped slab itself is never written.  flags:
  * MVBEV_WARP_DST_ZEROED = T is zero-filled and only written by this geometry, so a (tile,
  * column) whose 5 samples all fall outside the source is skipped.  Replaces :69 + :77 + the
  * first step of conv1 (:51) for inference. */

@@ -1449,7 +1449,8 @@ __device__ inline void bf16x8_to_f32(const u32x4 v, float (&f)[8]) {
   }
 }
 
-// T[b][k / 8][5 r3 + xi][col][hi, lo][8] = split((B^T d)[xi]),
+// T[b][k / 8][5 r3 + xi][hi, lo][col][8] = split((B^T d)[xi]) (a row's hi plane, then its lo plane:
+// a unit's T DMAs read whole contiguous 16-B runs),
 //   d[m] = x[b][k][out_row0 + base(r3) + dil (m - 1)][col] (zero outside the image and the input rows),
 // r3 < 4 tiles_y: the 3-row tiles of the conv's 12 x 32 workgroup tiles, rows base(r3) + dil pt
 // (pt < 3): base = 3 r3 for dilation 1; for dilation 2 the 12 rows hold two interleaved pairs of
@@ -1506,7 +1507,8 @@ __global__ __launch_bounds__(256) void wino_rows_kernel(const WinoRowsArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) d[m][j] = h[j] + l[j];
     }
-    u32x4* dst = a.t + 2 * (((int64_t)b * K8 + k0 / SB) * R5 * W + (int64_t)5 * r3 * W + col);
+    // T row = its hi plane [W][8] then its lo plane (16-B units)
+    u32x4* dst = a.t + 2 * (((int64_t)b * K8 + k0 / SB) * R5 * W + (int64_t)5 * r3 * W) + col;
 #pragma unroll
     for (int xi = 0; xi < 5; ++xi) {
       unsigned hp[4], lp[4];
@@ -1530,11 +1532,15 @@ __global__ __launch_bounds__(256) void wino_rows_kernel(const WinoRowsArgs a) {
         lp[e4] = (unsigned)ls[0] | ((unsigned)ls[1] << 16);
       }
       dst[2 * (int64_t)xi * W] = u32x4{hp[0], hp[1], hp[2], hp[3]};
-      dst[2 * (int64_t)xi * W + 1] = u32x4{lp[0], lp[1], lp[2], lp[3]};
+      dst[2 * (int64_t)xi * W + W] = u32x4{lp[0], lp[1], lp[2], lp[3]};
     }
   }
 }
 
+#ifndef MVBEV_WINO_PAIRB
+#define MVBEV_WINO_PAIRB -1  // one unit barrier per two units (2 units of DMA lookahead instead of 3): 1 on,
+                             // 0 off, -1 conv2 only (cfg2: conv2 0.349 -> 0.342 ms, conv1 1.43 -> 1.45)
+#endif
 #ifndef MVBEV_WINO_TSKIP
 #define MVBEV_WINO_TSKIP 1  // T pieces that hold no T entry are not issued (per-wave wait counts)
 #endif
@@ -1596,7 +1602,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     const int sub = e / (TROW / 2), part = (e / (TROW / 4)) & 1, rt = (e % (TROW / 4)) / XW, c = e % XW;
     const int gx = x0 - DIL + c;
     const bool z = e >= TROW || gx < 0 || gx >= W;
-    tvo[j] = z ? kOOB : (uint32_t)sub * tplane_b + (uint32_t)((2 * ((XH * ty + NXI * rt) * W + gx) + part) * 16);
+    tvo[j] = z ? kOOB : (uint32_t)sub * tplane_b + (uint32_t)((2 * (XH * ty + NXI * rt) * W + part * W + gx) * 16);
     asm volatile("" : "+v"(tvo[j]));
   }
   // the tile's physical chunks, walked incrementally: group = lowest set bit of the mask left,
@@ -1698,6 +1704,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   constexpr int NPU_HI = ((MVBEV_WINO_ABL & 8) ? 0 : NWI) + ((MVBEV_WINO_ABL & 4) ? 0 : NXT);
   constexpr int NPU_LO = ((MVBEV_WINO_ABL & 8) ? 0 : NWI) + ((MVBEV_WINO_ABL & 4) ? 0 : NXT_LO);
   const bool whi = wave < WHI;
+  constexpr bool PB = MVBEV_WINO_PAIRB < 0 ? DIL == 2 : MVBEV_WINO_PAIRB != 0;
   if (nch > 0) {
     const int U = NXI * nch;
     // prologue: units 0-3 (chunk 0, rows 0-3) in flight, wait for unit 0
@@ -1705,8 +1712,13 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     issue_unit(cur, 1, 1);
     issue_unit(cur, 2, 2);
     issue_unit(cur, 3, 3);
-    if (whi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPU_HI) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPU_LO) : "memory");
+    if (PB) {  // units 0 and 1 landed (the first barrier, after unit 1, retires 2 and 3)
+      if (whi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPU_HI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPU_LO) : "memory");
+    } else {
+      if (whi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPU_HI) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPU_LO) : "memory");
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     fetch_b(0, 0);
@@ -1732,15 +1744,25 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     fetch_a(P, slot, 2);                                                                             \
     WINO_MFMAS(P ^ 1, 1, XI);                                                                        \
     sched6(std::integral_constant<int, 4>{});                                                        \
-    /* retire unit u+1; every LDS read of this unit's slot is done */                                 \
-    if (!(MVBEV_WINO_ABL & 1)) {                                                                     \
-      if (whi) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU_HI) : "memory");     \
-      else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU_LO) : "memory");          \
+    if (!PB) {                                                                         \
+      /* retire unit u+1; every LDS read of this unit's slot is done */                               \
+      if (!(MVBEV_WINO_ABL & 1)) {                                                                   \
+        if (whi) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU_HI) : "memory");   \
+        else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU_LO) : "memory");        \
+        __builtin_amdgcn_s_barrier();                                                                \
+      }                                                                                              \
+      asm volatile("" ::: "memory");                                                                 \
+      /* unit u+4 into this slot: (chunk, xi 4) at xi 0, else (next chunk, xi - 1) */                \
+      if (!(MVBEV_WINO_ABL & 2)) issue_unit(XI == 0 ? cur : nx, (XI + 4) % 5, slot);           \
+    } else if (P == 1) {                                                                             \
+      /* PAIRB: one barrier per two units, after the odd one: retire units u+1, u+2 (all in      \
+         flight), then units u+3, u+4 into the slots of u-1 and u */                                  \
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                   \
       __builtin_amdgcn_s_barrier();                                                                  \
+      asm volatile("" ::: "memory");                                                                 \
+      issue_unit(XI <= 1 ? cur : nx, (XI + 3) % 5, (u0 + (R) + 3) & 3);                              \
+      issue_unit(XI == 0 ? cur : nx, (XI + 4) % 5, slot);                                            \
     }                                                                                                \
-    asm volatile("" ::: "memory");                                                                   \
-    /* unit u+4 into this slot: (chunk, xi 4) at xi 0, else (next chunk, xi - 1) */                  \
-    if (!(MVBEV_WINO_ABL & 2)) issue_unit(XI == 0 ? cur : nx, (XI + 4) % 5, slot);             \
     if (XI == 4) advance();                                                                          \
     fetch_b(0, nslot);                                                                               \
     fetch_b(1, nslot);                                                                               \

@@ -161,6 +161,9 @@ __global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_tile_kernel(const Warp
 #define MVBEV_WW_STAGE 384  // max staged box pixels per channel (8 channels x 384 x 4 B = 12 KiB); 0 = off
 #endif
 constexpr int kWwStage = MVBEV_WW_STAGE;
+#ifndef MVBEV_WW_ABL
+#define MVBEV_WW_ABL 0  // timing ablations only (wrong results): bit 0 no T stores (phase 2), bit 1 no source loads
+#endif
 #ifndef MVBEV_WW_QUAD
 #define MVBEV_WW_QUAD 1  // stage the box with 16-B loads where the source allows (stage_box_load)
 #endif
@@ -232,7 +235,7 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
   const StageBox sb = stage_box_shape(box, W, quad_ok && MVBEV_WW_QUAD);
   const int R = sb.R, Cb = sb.pitch;
   // uniform per block (the staged path needs unit column stride: the non-quad loads assume it too)
-  const bool staged = kWwStage > 0 && box[1] >= 0 && vw.sW == 1 && R * Cb <= kWwStage;
+  const bool staged = kWwStage > 0 && box[1] >= 0 && vw.sW == 1 && R * Cb <= kWwStage && !(MVBEV_WW_ABL & 2);
   if (staged) {
     stage_box_load<kWwThreads>(base, vw.sC, vw.sH, c_begin, c_end, sb, stage, tid);
     __syncthreads();
@@ -279,6 +282,10 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
           const int64_t o_sw = cy1 * sH + cx0 * sW, o_se = cy1 * sH + cx1 * sW;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {  // straight-line (a short last group re-reads its last channel)
+            if (MVBEV_WW_ABL & 2) {  // timing ablation: no source loads
+              d[j] = w_nw + (float)j;
+              continue;
+            }
             const int ch = min(c_begin + j, c_end - 1);
             const float* pc = base + (int64_t)ch * sC;
             float vnw, vne, vsw, vse;
@@ -307,7 +314,7 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
     nz[i][c] = any;
   }
   __syncthreads();
-  wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
+  if (!(MVBEV_WW_ABL & 1)) wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
 }
 
 template <typename T, bool SPLIT>
@@ -522,6 +529,7 @@ int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t
     const mvbev_warp_view& s = views[i];
     if (!s.src || !s.dst) return MVBEV_ERR_NULL;
     if (s.dst_strides[3] != 1) return MVBEV_ERR_STRIDE;
+    if (s.dst_strides[2] != Wo) return MVBEV_ERR_STRIDE;  // a T row = its hi plane [Wo] then its lo plane
     WarpView& d = a.v[i];
     d.src = s.src; d.sB = s.src_strides[0]; d.sC = s.src_strides[1];
     d.sH = s.src_strides[2]; d.sW = s.src_strides[3];

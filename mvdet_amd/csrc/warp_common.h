@@ -246,7 +246,9 @@ __device__ inline StageBox stage_box_shape(const int (&box)[4], int W, bool quad
   sb.pitch = c1 - sb.c0;
   return sb;
 }
-template <int NT>
+// PIX: pixel-major staging, stage[(r * pitch + col) * 8 + j] (a pixel's 8 channels in 32 B: a tap
+// is two 16-B LDS reads for all channels), else channel-major stage[j][r][col].
+template <int NT, bool PIX = false>
 __device__ inline void stage_box_load(const float* __restrict__ base, int64_t sC, int64_t sH, int c_begin, int c_end,
                                       const StageBox& sb, float* __restrict__ stage, int tid) {
   const int n = sb.R * sb.pitch;
@@ -259,8 +261,17 @@ __device__ inline void stage_box_load(const float* __restrict__ base, int64_t sC
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         t[j] = *reinterpret_cast<const f32x4a_t*>(src + (int64_t)min(c_begin + j, c_end - 1) * sC);
+      if constexpr (PIX) {
+        f32x4a_t* dst = reinterpret_cast<f32x4a_t*>(stage + (r * sb.pitch + 4 * q) * 8);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4a_t*>(stage + j * n + r * sb.pitch + 4 * q) = t[j];
+        for (int e = 0; e < 4; ++e) {
+          dst[2 * e] = f32x4a_t{t[0][e], t[1][e], t[2][e], t[3][e]};
+          dst[2 * e + 1] = f32x4a_t{t[4][e], t[5][e], t[6][e], t[7][e]};
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4a_t*>(stage + j * n + r * sb.pitch + 4 * q) = t[j];
+      }
     }
   } else {
     for (int r = tid / 32; r < sb.R; r += NT / 32)
@@ -269,8 +280,14 @@ __device__ inline void stage_box_load(const float* __restrict__ base, int64_t sC
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           t[j] = base[(int64_t)min(c_begin + j, c_end - 1) * sC + (int64_t)(sb.r0 + r) * sH + sb.c0 + cc];
+        if constexpr (PIX) {
+          f32x4a_t* dst = reinterpret_cast<f32x4a_t*>(stage + (r * sb.pitch + cc) * 8);
+          dst[0] = f32x4a_t{t[0], t[1], t[2], t[3]};
+          dst[1] = f32x4a_t{t[4], t[5], t[6], t[7]};
+        } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) stage[j * n + r * sb.pitch + cc] = t[j];
+          for (int j = 0; j < 8; ++j) stage[j * n + r * sb.pitch + cc] = t[j];
+        }
       }
   }
 }
@@ -293,15 +310,16 @@ __device__ inline void wino_rows_phase2(const float (&ds)[kWwRows][kWwCols][8], 
   t[2] = 2.f * d[1] - 3.f * d[2] + d[3];
   t[3] = d[3] - d[1];
   t[4] = 2.f * d[1] - d[2] - 2.f * d[3] + d[4];
+  // a T row of dH (= Wo) columns is its hi plane [dH][8 bf16] then its lo plane (16-B units)
   unsigned* out = reinterpret_cast<unsigned*>(static_cast<u32x4_t*>(vw.dst) +
-                                              2 * ((int64_t)b * vw.dB + (int64_t)chunk * vw.dC +
-                                                   (int64_t)(5 * r3) * vw.dH + u)) + cp;
+                                              (2 * ((int64_t)b * vw.dB + (int64_t)chunk * vw.dC +
+                                                    (int64_t)(5 * r3) * vw.dH) + u)) + cp;
 #pragma unroll
   for (int xi = 0; xi < 5; ++xi) {
     const float h0 = (float)(__bf16)t[xi].x, h1 = (float)(__bf16)t[xi].y;
     unsigned* o = out + (int64_t)xi * vw.dH * 8;  // 8 dwords per 32-B unit
     o[0] = pack_bf16x2(h0, h1);
-    o[4] = pack_bf16x2(t[xi].x - h0, t[xi].y - h1);
+    o[vw.dH * 4] = pack_bf16x2(t[xi].x - h0, t[xi].y - h1);
   }
 }
 

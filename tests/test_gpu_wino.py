@@ -81,8 +81,8 @@ def test_wino_rows_transform_matches_numpy():
     ops.wino_rows(slab, desc, t)
     K, r0, nr = S * Cs, rows[0], rows[1] - rows[0]
     R5 = 5 * 4 * (-(-nr // 12))
-    T = t.view(B, K // 8, R5, W, 2, 8).float().cpu()
-    T = (T[..., 0, :] + T[..., 1, :]).permute(0, 1, 4, 2, 3).reshape(B, K, R5, W).double().numpy()
+    T = t.view(B, K // 8, R5, 2, W, 8).float().cpu()  # a row: hi plane [W][8], then lo plane
+    T = (T[:, :, :, 0] + T[:, :, :, 1]).permute(0, 1, 4, 2, 3).reshape(B, K, R5, W).double().numpy()
     # the slab as the kernel sees it: hi + lo of the split encoding
     x = torch.stack([xs[v].to(torch.bfloat16).float() + (xs[v] - xs[v].to(torch.bfloat16).float())
                      .to(torch.bfloat16).float() for v in range(S)]).permute(1, 0, 2, 3, 4).reshape(B, K, H, W)
@@ -199,8 +199,8 @@ def test_fused_warp_transform_matches_two_pass(cfg):
         assert wf.t_from_warp and wf.slab.abs().max().item() == 0  # the slab was never written
         ref = two.project_fuse(feats, mc)
         wt = two.workspace(B, DEV)
-        tf = wf.wino_t.view(-1, 2, 8).float()
-        tt = wt.wino_t.view(-1, 2, 8).float()
+        tf = wf.wino_t.view(-1, 2, grid[1], 8).float()  # T rows: hi plane, then lo plane
+        tt = wt.wino_t.view(-1, 2, grid[1], 8).float()
         a, b = tf.sum(1), tt.sum(1)
         # the two-pass T transforms the slab's hi + lo (each value rounded to ~2^-17): the 5-row
         # combinations (coefficient sums <= 6) differ by a few 1e-5 of the range
@@ -270,8 +270,8 @@ def test_wino_rows_dilation2_matches_numpy():
     t = torch.zeros(ops.wino_rows_bytes(desc) // 2, dtype=torch.bfloat16, device=DEV)
     ops.wino_rows(xs, desc, t, dilation=2)
     R5 = 5 * 4 * (-(-H // 12))
-    T = t.view(B, K // 8, R5, W, 2, 8).float().cpu()
-    T = (T[..., 0, :] + T[..., 1, :]).permute(0, 1, 4, 2, 3).reshape(B, K, R5, W).double().numpy()
+    T = t.view(B, K // 8, R5, 2, W, 8).float().cpu()  # a row: hi plane [W][8], then lo plane
+    T = (T[:, :, :, 0] + T[:, :, :, 1]).permute(0, 1, 4, 2, 3).reshape(B, K, R5, W).double().numpy()
     xe = (x.to(torch.bfloat16).float() + (x - x.to(torch.bfloat16).float()).to(torch.bfloat16).float()).double().numpy()
     for r3 in range(R5 // 5):
         base = 12 * (r3 // 4) + (0, 1, 6, 7)[r3 % 4]

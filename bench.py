@@ -192,17 +192,24 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
     warp_bytes = sum(s * B * C * (t + ho * wo) for t in tv)
     if eng.wino_warp:  # the warp writes conv1's row transform: 5 split-bf16 rows per 3-row tile
         warp_bytes = sum(4 * B * C * (t + 5 * 4 * -(-ho // 12) * wo) for t in tv)
-    conv3_bytes = 4.0 * B * ho * wo * (512 + 1)
+    # conv3's stage: with conv2 -> conv3 fused (bf16x3) it reads the [B, 8 sets, 9 taps, rows, Wo] fp32
+    # partials conv2's epilogue wrote (y2 never reaches HBM) and writes the map; on a stored y2 (fp32
+    # path) it reads y2's 512 channels
+    fused3 = eng.conv3_fused_applies(ws)
+    y2rows = ws.y2_rows[1] - ws.y2_rows[0]
+    conv3_read = 4.0 * B * (2 * 512 // 128) * 9 * y2rows * wo if fused3 else 4.0 * B * 512 * y2rows * wo
+    conv3_bytes = conv3_read + 4.0 * B * ho * wo
     conv1_alg_tfs = conv1_flop / (t_c1k * 1e-3) / 1e12  # over the conv kernel's time
     active = eng.conv1_active_fraction(dev, *ws.y1_rows[:1], ws.y1_rows[1] - ws.y1_rows[0], grid=wino) \
         if precision == "bf16x3" else 1.0
-
-    def mfma_s(c1_scale):
-        return (3 * (c1_scale * conv1_flop + conv2_flop) / (BF16_MFMA_PEAK_TFS * 1e12) if precision == "bf16x3"
-                else (c1_scale * conv1_flop + conv2_flop) / (FP32_MFMA_PEAK_TFS * 1e12))
+    # the end-to-end floor prices the algorithm that executes: conv1's frustum-active products, the
+    # row-Winograd forms at 5/9 of the direct MFMA work, 3 bf16 passes (bf16x3) or the fp32 MFMA peak
+    w1 = 5.0 / 9.0 if wino else 1.0
+    w2 = 5.0 / 9.0 if wino2 else 1.0
+    mfma_s = (3 * (active * w1 * conv1_flop + w2 * conv2_flop) / (BF16_MFMA_PEAK_TFS * 1e12) if precision == "bf16x3"
+              else (active * conv1_flop + conv2_flop) / (FP32_MFMA_PEAK_TFS * 1e12))
     hbm_s = (warp_bytes + conv3_bytes) / (HBM_PEAK_GBS * 1e9)
-    e2e_floor_ms = 1e3 * (hbm_s + mfma_s(active))        # conv1: only the frustum-active products
-    e2e_dense_floor_ms = 1e3 * (hbm_s + mfma_s(1.0))      # conv1 dense, as the reference computes it
+    e2e_floor_ms = 1e3 * (hbm_s + mfma_s)
     if precision == "bf16x3":
         # bf16 MFMA work the split needs: 3 passes per fp32 product (no padding MFMAs; the
         # tile-edge columns a 32-wide tile computes past W=360 are waste, not counted).
@@ -264,10 +271,10 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
         "e2e_roofline": {
             "floor_ms": round(e2e_floor_ms, 4),
             "frac": round(e2e_floor_ms / (dt * 1e3 / K), 4),
-            "basis": "warp_bytes/8 TB/s + (conv1 flop x frustum_active + conv2 flop) " + (
-                "x3 / 2.5 PF bf16" if precision == "bf16x3" else "/ 157.3 TF fp32") + " + conv3_bytes/8 TB/s",
-            "dense_floor_ms": round(e2e_dense_floor_ms, 4),
-            "dense_frac": round(e2e_dense_floor_ms / (dt * 1e3 / K), 4),
+            "basis": "warp_bytes/8 TB/s + (conv1 flop x frustum_active" + (" x 5/9" if wino else "") +
+                     " + conv2 flop" + (" x 5/9" if wino2 else "") + ") " +
+                     ("x3 / 2.5 PF bf16" if precision == "bf16x3" else "/ 157.3 TF fp32") +
+                     " + conv3_bytes/8 TB/s (the executed algorithm)",
         },
         "stage_roofline": {
             "warp": {"bound": "hbm", "algorithmic_bytes": warp_bytes,
@@ -285,8 +292,9 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
                                                    / (BF16_MFMA_PEAK_TFS * 1e12), 4)
                                              if precision == "bf16x3" else None),
                       "form": "row-Winograd F(3,3), dilation 2" if wino2 else "direct"},
-            "conv3": {"bound": "hbm", "achieved_GBs": round(conv3_bytes / (t_c3 * 1e-3) / 1e9, 1),
-                      "peak_GBs": HBM_PEAK_GBS},
+            "conv3": {"bound": "hbm", "algorithmic_bytes": conv3_bytes,
+                      "reads": "conv2's conv3 partials [B, 8, 9, rows, Wo] fp32" if fused3 else "y2 [B, 512, rows, Wo] fp32",
+                      "achieved_GBs": round(conv3_bytes / (t_c3 * 1e-3) / 1e9, 1), "peak_GBs": HBM_PEAK_GBS},
         },
     }
     if with_cpu:
@@ -469,6 +477,25 @@ def run_train_step(config: int, precision: str, steps: int, warmup: int, with_to
     return res
 
 
+def spawn_ranks(n: int) -> int:
+    """``--gpus N`` (N > 1) without a launcher: start N rank processes through
+    ``torch.distributed.run`` (one per GPU, rendezvous on 127.0.0.1) and return their exit code.
+    This parent makes no GPU call: ``torch.cuda.device_count()`` does not initialise the device
+    on this image, and the children are started with ``subprocess`` (never an exec).  With
+    fewer GPUs than ranks (a 1-GPU rehearsal box) the ranks share the devices over ``gloo``."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    if torch.cuda.device_count() < n:
+        env.setdefault("MVBEV_DIST_BACKEND", "gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py")] + sys.argv[1:]
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -493,11 +520,21 @@ def main():
                          "reduce-scatter, or frame-parallel; the other modes are reported alongside")
     ap.add_argument("--north-star-cfg", type=int, default=3,
                     help="also run this config (the north star's 480x1440 Wildtrack grid) as a sub-object "
-                         "(N=1: single GPU with a 1-frame CPU baseline; N>1: the band exchange); 0 = skip")
+                         "(N=1: single GPU with a reduced-sample CPU baseline; N>1: the band exchange); 0 = skip")
+    ap.add_argument("--roofline-cfg", type=int, default=5,
+                    help="also run this config (BASELINE's rocprof roofline run: 8 views at 4K -> 1000 x 1000) as a "
+                         "sub-object with its roofline, no CPU baseline; 0 = skip")
     args = ap.parse_args()
 
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus {args.gpus} < 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        # a launcher and the flag disagree: a line for the wrong N must never be printed
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
         from mvdet_amd import parallel
         return parallel.bench_main(args)
@@ -528,18 +565,25 @@ def main():
         result["speedup_vs_cpu"] = round(res["value"] / result["cpu_baseline"]["value"], 1)
     if args.config != 4:  # the fused upsample+warp writes fp32 / split slabs (not the fp16 slab)
         result["plus_a4"] = run_plus_a4(args, args.precision, max(5, args.steps // 2), 2)
-    ns = args.north_star_cfg
-    if ns and ns != args.config:
+    subs = []
+    if args.north_star_cfg and args.north_star_cfg != args.config:
         # the size the north star quotes its >= 5x at 1 GPU on (cfg3: 7 views, 480 x 1440 grid): the same
-        # path, its roofline, and a 1-frame CPU baseline (about 20 s of CPU work)
-        sub = run_single(args, args.precision, max(5, args.steps // 4), 2, with_cpu=not args.no_cpu_baseline,
-                         config=ns, cpu_plan=dict(frames=1, warmups=0, single_frames=0))
+        # path, its roofline, and a CPU baseline on a reduced sample (1 warm-up + the median of 3 frames,
+        # ~25 s of CPU work per frame at 16 threads: BASELINE.md:26's 2 + 5 would take ~3 minutes)
+        subs.append((args.north_star_cfg, dict(frames=3, warmups=1, single_frames=0)))
+    if args.roofline_cfg and args.roofline_cfg not in (args.config, args.north_star_cfg):
+        subs.append((args.roofline_cfg, None))  # BASELINE's "rocprof roofline run" config (8 views at 4K)
+    for cfg, plan in subs:
+        sub = run_single(args, args.precision, max(5, args.steps // 4), 2,
+                         with_cpu=plan is not None and not args.no_cpu_baseline, config=cfg, cpu_plan=plan)
         sub = {k: sub[k] for k in ("value", "ms_per_step", "config", "roofline", "stages_ms", "e2e_roofline",
                                    "stage_roofline", "cpu_baseline") if k in sub}
         sub["unit"] = "frames/s"
         if sub.get("cpu_baseline"):
             sub["speedup_vs_cpu"] = round(sub["value"] / sub["cpu_baseline"]["value"], 1)
-        result[f"cfg{ns}"] = sub
+        else:
+            sub["cpu_baseline"] = None  # CPU sample at cfg2 / cfg3 only (bench runtime)
+        result[f"cfg{cfg}"] = sub
     if not args.no_train and args.config != 4:
         result["train_step"] = run_train_step(args.config, args.precision, max(5, args.steps // 2), 2,
                                               with_torch=bool(args.train_torch))

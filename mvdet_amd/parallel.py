@@ -159,7 +159,7 @@ class _ViewSharded:
         """One frame, unpipelined (``feats[j]`` is view ``my_views[j]``)."""
         if mark:
             mark("warp")
-        self.produce(fr, feats, map_classifier)
+        self.produce(fr, feats, map_classifier, mark=mark)
         if mark:
             mark("exchange")
         self.exchange(fr)
@@ -177,7 +177,7 @@ class ViewParallel(_ViewSharded):
     def _make_frame(self, B, device, tag):
         return SimpleNamespace(ws=self.engine.workspace(B, device, self._band_eff(), tag=tag))
 
-    def produce(self, fr, feats, map_classifier=None) -> None:
+    def produce(self, fr, feats, map_classifier=None, mark=None) -> None:
         """Warp this rank's views into its rank-major slots."""
         if hasattr(self.engine, "warp_views"):
             self.engine.warp_views(fr.ws, self.my_views, list(feats))
@@ -239,7 +239,7 @@ class ViewBands(_ViewSharded):
             assert send[0, 0].numel() == per_view
         return SimpleNamespace(ws=ws, send=send, per_view=per_view, B=B, device=device)
 
-    def produce(self, fr, feats, map_classifier=None) -> None:
+    def produce(self, fr, feats, map_classifier=None, mark=None) -> None:
         if self.local is None:
             return
         lws = self._local_ws[(str(fr.device), fr.B)]
@@ -308,7 +308,7 @@ class ViewPartialSum(_ViewSharded):
             edges=torch.zeros((P, 2, B, mid, e, W), dtype=torch.float32, device=device),
             full=None if n >= self.HALO else torch.zeros((P, B, mid, n, W), dtype=torch.float32, device=device))
 
-    def produce(self, fr, feats, map_classifier=None) -> None:
+    def produce(self, fr, feats, map_classifier=None, mark=None) -> None:
         """Warp this rank's views, conv1 over their channels (all rows), band-major staging."""
         if self.engine is None:
             fr.part.zero_()
@@ -319,7 +319,11 @@ class ViewPartialSum(_ViewSharded):
             else:
                 for v, f in zip(self.my_views, feats):
                     self.engine.warp_view(lws, v, f)
-            self.engine.conv1_partial(lws, map_classifier, fr.part)
+            if mark:
+                mark("conv1")
+            self.engine.conv1_partial(lws, map_classifier, fr.part, mark=mark)
+        if mark:
+            mark("stage_bands")
         H, n = self.grid_hw[0], self.band_rows
         for p in range(self.world):  # band-major staging for the reduce-scatter
             a, b = min(H, p * n), min(H, (p + 1) * n)
@@ -534,7 +538,7 @@ def bench_main(args) -> None:
                 dt = timed(steps, K)
                 fr = vp.workspace(s.B, dev)
                 st = stage_times(lambda mark: vp.step(fr, feats, s.mc, mark=mark), max(3, K // 4))
-                st_total = round(sum(st.values()), 4)
+                st_total = round(sum(st.values()), 4)  # the marks partition the step
                 value = s.B * K / dt
                 band = vp.band
                 y1r = fr.ws.y1_rows
@@ -543,8 +547,12 @@ def bench_main(args) -> None:
         nviews = s.N if mode != "partial" else max(1, len(views_of(rank, world, s.N)))
         rows = ho if mode == "partial" else act_rows[1] - act_rows[0]
         conv1_flop = 2.0 * s.B * rows * wo * 9 * nviews * s.C * 512
-        conv_ms = st.get("conv1", 0.0)
-        wino = bool(bf16 and getattr(act_eng, "wino_conv1", False))
+        # conv1's marks: "conv1" before its row transform (none when the fused warp wrote T), then
+        # "conv1_wino" right before the Winograd conv kernel; the roofline is the conv kernel's, as at N = 1
+        wino = bool(bf16 and "conv1_wino" in st)
+        conv_ms = st["conv1_wino"] if wino else st.get("conv1", 0.0)
+        if "conv1_wino" in st:
+            st["conv1_total"] = round(st.get("conv1", 0.0) + st["conv1_wino"], 4)
         ach = (conv1_flop / (conv_ms * 1e-3) / 1e12 * (3 * (5.0 / 9.0 if wino else 1.0) if bf16 else 1.0)
                if conv_ms > 0 else None)
         res = dict(value=round(value, 3), ms_per_step=round(dt * 1e3 / K, 4), stages_ms_rank0=st,
@@ -587,6 +595,16 @@ def bench_main(args) -> None:
         if ns and ns != args.config:
             alts[f"north_star_cfg{ns}"] = run_alt("bands", ns)
     if rank == 0:
+        cpu = None
+        if not getattr(args, "no_cpu_baseline", False):
+            # rank 0 only, after every timed region (the other ranks wait at the final barrier): the
+            # oracle on a bounded sample of the same workload, as the N = 1 line reports it
+            from bench import cpu_baseline
+            s0 = setup(args.config)
+            cpu = cpu_baseline(s0.spec["make"](), 1 if s0.half else s0.B, s0.C, s0.pm,
+                               head_params(s0.N, seed=args.config, C=s0.C), frames=2, config=args.config,
+                               warmups=1, single_frames=0)
+        rl = res.get("conv1_roofline_rank0", {})
         line = {
             "metric": "multi-view frames/sec (project+fuse)",
             "value": res["value"],
@@ -602,11 +620,18 @@ def bench_main(args) -> None:
             "data": "synthetic (see single-GPU line)",
             "config": {"workload": res["workload"], "batch": synthetic.CONFIGS[args.config]["B"] *
                        (world if mode == "frames" else 1), "precision": args.precision, "parallelism": hows[mode]},
-            "roofline": dict(kernel="conv1 on rank 0 (its row band + halo)", bound="mfma", traffic=None,
-                             **{k: v for k, v in res.get("conv1_roofline_rank0", {}).items() if k != "basis"}),
+            "roofline": {"kernel": "conv1's conv kernel on rank 0 (its row band + halo)", "bound": "mfma",
+                         "achieved": rl.get("achieved"), "peak": rl.get("peak"), "unit": "TFLOP/s",
+                         "frac": rl.get("frac"), "traffic": None, "basis": rl.get("basis")},
+            "cpu_baseline": cpu,
             "stages_ms_rank0": res["stages_ms_rank0"],
             "band_rank0": res["band_rank0"],
+            # gloo with ranks sharing the devices (fewer GPUs than ranks): a rehearsal of the path, not a
+            # multi-GPU measurement
+            "rehearsal": backend != "nccl",
         }
+        if cpu:
+            line["speedup_vs_cpu"] = round(res["value"] / cpu["value"], 1)
         if "unpipelined_ms_rank0" in res:
             line["unpipelined_ms_rank0"] = res["unpipelined_ms_rank0"]
         for m, r in alts.items():

@@ -526,7 +526,8 @@ class ProjectFuse:
                                  out_rows=r1 - r0)
 
     # -- partial-sum multi-GPU (SURVEY §8(e) alternative, §8(f) row 3) -----------------------
-    def conv1_partial(self, ws: Workspace, map_classifier: torch.nn.Sequential, out: torch.Tensor) -> torch.Tensor:
+    def conv1_partial(self, ws: Workspace, map_classifier: torch.nn.Sequential, out: torch.Tensor,
+                      mark=None) -> torch.Tensor:
         """conv1 restricted to this slab's views (its slice of conv1's input channels), all
         grid rows, no bias / coord term / ReLU: one rank's term of conv1's channel sum
         (row-Winograd where ``wino_active``).  ``out``: contiguous [B, 512, Ho, Wo] fp32."""
@@ -546,6 +547,8 @@ class ProjectFuse:
             if ws.wino_t is None or ws.wino_t.numel() * 2 < need:
                 ws.wino_t = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=ws.slab.device)
             ops.wino_rows(ws.slab, d1, ws.wino_t, gm)
+            if mark:
+                mark("conv1_wino")
             return ops.conv3x3_wino(ws.wino_t, d1, self.pack1w.get(w1), self.mid, init=None, relu=False, out=out,
                                     group_mask=gm, tile_order=order)
         return ops.conv3x3_desc(ws.slab, d1, self.pack1.get(w1), self.mid, bias=None, init=None, dilation=1,

@@ -49,7 +49,7 @@ class OracleEngine:
         return self._ws[key]
 
     # partial-sum mode: conv1 over this slab's views only, then the band fusion from summed y1
-    def conv1_partial(self, ws, mc, out):
+    def conv1_partial(self, ws, mc, out, mark=None):
         w1 = self.params["map_classifier.0.weight"]
         out.zero_()
         for s, v in enumerate(self.slot_views):

@@ -17,7 +17,7 @@ ROOT = Path(__file__).resolve().parents[1]
 def test_bench_json_line_contract():
     env = dict(os.environ, PYTHONUNBUFFERED="1")
     out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--config", "1", "--steps", "2", "--warmup", "1",
-                          "--no-train", "--no-alt", "--cpu-frames", "1", "--north-star-cfg", "2"],
+                          "--no-train", "--no-alt", "--cpu-frames", "1", "--north-star-cfg", "2", "--roofline-cfg", "0"],
                          cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
@@ -38,6 +38,11 @@ def test_bench_json_line_contract():
     assert cb["single_thread"]["cores"] == 1 and cb["single_thread"]["value"] > 0
     e2e = r["e2e_roofline"]
     assert 0 < e2e["frac"] <= 1.0 and e2e["floor_ms"] > 0
+    for name, st in r["stage_roofline"].items():  # no stage may claim more than the peak it is priced at
+        if "achieved_GBs" in st:
+            assert 0 < st["achieved_GBs"] <= st["peak_GBs"], (name, st)
+        if st.get("executed_bf16_frac") is not None:
+            assert 0 < st["executed_bf16_frac"] <= 1.0, (name, st)
     assert r["config"]["workload"].startswith("cfg1")
     # the north-star sub-object (here cfg2 for speed; the default is cfg3): its own value, roofline, CPU baseline
     sub = r["cfg2"]
@@ -70,3 +75,36 @@ def test_bench_multi_rank_json_line():
     for key in ("view_parallel_partial", "view_parallel_gather"):
         assert "error" not in r[key], r[key]
         assert r[key]["value"] > 0 and r[key]["scaling"] == "strong"
+    _check_multi_rank_line(r, 2)
+
+
+def _check_multi_rank_line(r, n):
+    """The keys the N = 1 line carries, and conv1's roofline over the conv kernel's own time (its
+    mark "conv1_wino"), never over the row transform before it."""
+    assert r["n_gpus"] == n and r["rehearsal"] is True  # gloo ranks sharing the box's one GPU
+    rl = r["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in rl, k
+    assert 0 < rl["frac"] <= 1.0 and rl["frac"] == pytest.approx(rl["achieved"] / rl["peak"], rel=1e-3)
+    st = r["stages_ms_rank0"]
+    if "conv1_wino" in st:
+        assert st["conv1_total"] >= st["conv1_wino"] > 0
+    cb = r["cpu_baseline"]
+    assert cb["value"] > 0 and cb["kind"] == "port" and cb["cores"] >= 1
+
+
+@pytest.mark.gpu
+def test_bench_gpus_flag_spawns_ranks_without_a_launcher():
+    """``python bench.py --gpus 2`` with no torchrun in front (WORLD_SIZE unset): bench.py starts the
+    two ranks itself (gloo, sharing the one GPU of the test box) and the line says n_gpus 2."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PYTHONUNBUFFERED"] = "1"
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--config", "1", "--steps", "2",
+                          "--warmup", "1", "--north-star-cfg", "0", "--no-alt"],
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["value"] > 0 and r["scaling"] == "strong"
+    _check_multi_rank_line(r, 2)

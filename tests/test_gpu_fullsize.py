@@ -144,9 +144,10 @@ def test_detector_inference_path_vs_oracle(cfg, C):
 
 
 def _bands(H):
-    """An interior band crossing 12-row tile boundaries and the bottom edge band."""
+    """The top edge band (row 0: conv padding and the first Winograd tile, which starts at row -1),
+    an interior band crossing 12-row tile boundaries and the bottom edge band."""
     mid = (H // 2) - 13
-    return [(mid, mid + 30), (H - 20, H)]
+    return [(0, 20), (mid, mid + 30), (H - 20, H)]
 
 
 @pytest.mark.parametrize("cfg", [3, 5])
@@ -174,12 +175,14 @@ def test_large_config_path_vs_oracle_bands(cfg):
         _check_warp_whole(eng, ws, feats, warped, f"cfg{cfg}")
 
 
-def test_config4_fp16_batch8_vs_oracle_bands():
-    """Config 4 (MultiviewX 6 views, B = 8, C = 512, fp16 features and slab, fp32 accumulation):
-    the bench's fp16-storage path vs the oracle on the fp16-rounded inputs; warp whole, convs on
-    two row bands of every batch item."""
+@pytest.mark.parametrize("C", [512, 128])
+def test_config4_fp16_batch8_vs_oracle_bands(C):
+    """Config 4 (MultiviewX 6 views, B = 8, fp16 features and slab, fp32 accumulation) at the
+    reference's ResNet-18 width C = 512 and at cfg1's C = 128 (SURVEY §8's shape table: BASELINE does
+    not state C): the bench's fp16-storage path vs the oracle on the fp16-rounded inputs; warp whole,
+    convs on three row bands of every batch item."""
     from mvdet_amd import ProjectFuse, synthetic
-    ds, B, C, N, up, grid, pm, tp, mc = _setup(4)
+    ds, B, C, N, up, grid, pm, tp, mc = _setup(4, C=C)
     hb = [u // 3 for u in up]
     feats = [synthetic.synthetic_features(B, C, hb, up, seed=4000 + v, device=DEV).half() for v in range(N)]
     eng = ProjectFuse(pm, up, grid, C, slab_dtype=torch.float16)
@@ -191,11 +194,11 @@ def test_config4_fp16_batch8_vs_oracle_bands():
         torch.cuda.synchronize()
         warped = cpu_path.warp_views([f.float().cpu() for f in feats], [M.numpy() for M in pm], grid)
         for v in range(N):
-            assert_parity_t(eng.view_slice(ws, v).float(), warped[v].to(DEV), f"cfg4 warp view {v}")
+            assert_parity_t(eng.view_slice(ws, v).float(), warped[v].to(DEV), f"cfg4 C={C} warp view {v}")
         for r0, r1 in _bands(grid[0]):
             ref, ref_y1 = _oracle_band(warped, grid, tp, r0, r1)
-            assert_parity_t(got[:, :, r0:r1], ref, f"cfg4 map rows {r0}:{r1}")
-            assert_parity_t(y1[:, :, r0:r1], ref_y1, f"cfg4 conv1 rows {r0}:{r1}")
+            assert_parity_t(got[:, :, r0:r1], ref, f"cfg4 C={C} map rows {r0}:{r1}")
+            assert_parity_t(y1[:, :, r0:r1], ref_y1, f"cfg4 C={C} conv1 rows {r0}:{r1}")
 
 
 def test_degenerate_homography_nan_pattern_through_the_detector():

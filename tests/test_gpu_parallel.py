@@ -15,7 +15,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from oracle import fixtures
+from helpers import assert_parity_t
+from oracle import cpu_path, fixtures
 
 pytestmark = pytest.mark.gpu
 
@@ -33,6 +34,15 @@ def _setup(seed=31, C=64, B=2):
     mc.load_state_dict({k.replace("map_classifier.", ""): torch.from_numpy(v) for k, v in params.items()
                         if k.startswith("map_classifier.")})
     return ds, projection_matrices(ds), up, tuple(ds.reducedgrid_shape), C, B, feats, mc
+
+
+def _oracle_map(scale=1.0):
+    """The reference CPU path (kornia restatement + cat + F.conv2d, persp_trans_detector.py:69-82) on
+    the same inputs as ``_setup``'s (features times ``scale``)."""
+    ds, pm, up, grid, C, B, feats, mc = _setup()
+    params = {k: torch.from_numpy(v) for k, v in fixtures.head_params(3, seed=31, C=C).items()}
+    with torch.no_grad():
+        return cpu_path.project_fuse([scale * f for f in feats], [M.numpy() for M in pm], grid, params)
 
 
 @pytest.mark.parametrize("wino", [False, True])
@@ -99,10 +109,13 @@ def test_rank_rehearsal_matches_single_process(world, mode, tmp_path):
     mc = mc.to("cuda:0")
     with torch.no_grad():
         ref = ProjectFuse(pm, up, grid, C).project_fuse([f.cuda() for f in feats], mc).cpu()
+    oracle = _oracle_map()
     for r in range(world):
         got = torch.load(tmp_path / f"r{r}.pt", weights_only=True)[0]
-        # different slot order / band-started Winograd tiles -> different summation order in conv1:
-        # fp32-rounding level only
+        # every rank's assembled map vs the reference's CPU path (the parity gate, and the 3xbf16 path's
+        # 5e-5), and vs the single-process HIP map (different slot order / band-started Winograd tiles ->
+        # different summation order in conv1: fp32-rounding level only)
+        assert_parity_t(got, oracle, f"{mode} x{world} rank {r} map_result vs oracle", normwise_tol=5e-5)
         torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-5)
 
 
@@ -122,4 +135,5 @@ def test_frame_pipeline_on_rccl_streams(mode, tmp_path):
     with torch.no_grad():
         for f in range(4):
             ref = eng.project_fuse([(f + 1) * x.cuda() for x in feats], mc).cpu()
+            assert_parity_t(got[f], _oracle_map(f + 1.0), f"{mode} pipeline frame {f} vs oracle", normwise_tol=5e-5)
             torch.testing.assert_close(got[f], ref, rtol=1e-4, atol=1e-5)

@@ -3,6 +3,7 @@ declared symbol, argument validation returns the documented codes (no GPU work i
 launched for those), the host geometry matches the reference fixtures/oracle, and
 the drop-in module keeps the reference's state_dict layout."""
 import ctypes
+import os
 import re
 from pathlib import Path
 
@@ -177,3 +178,19 @@ def test_bev_fuse_structs_and_plan_match_the_header(tmp_path):
     assert lib.mvbev_bev_plan_init(ctypes.byref(g), ctypes.byref(plan)) == 0 and plan.wino == 0
     g.num_views = 17
     assert lib.mvbev_bev_plan_init(ctypes.byref(g), ctypes.byref(plan)) == _native.ERR_SHAPE
+
+
+@pytest.mark.parametrize("gpus,world", [(2, "1"), (1, "2"), (8, "4"), (0, None)])
+def test_bench_refuses_a_gpus_world_size_mismatch(gpus, world):
+    """bench.py exits non-zero before touching a GPU when ``--gpus`` and the launcher's WORLD_SIZE
+    disagree (a line for the wrong N must never be printed), and for ``--gpus < 1``."""
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    if world is not None:
+        env["WORLD_SIZE"] = world
+    out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(gpus), "--no-cpu-baseline"],
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert "--gpus" in out.stderr

@@ -150,7 +150,7 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
 
     K, W = steps, warmup
     ev = {k: [torch.cuda.Event(enable_timing=True) for _ in range(K)]
-          for k in ("warp", "conv1", "conv1_wino", "conv2", "conv3")}
+          for k in ("warp", "conv1", "conv1_wino", "conv2", "conv3", "guard")}
     end_ev = [torch.cuda.Event(enable_timing=True) for _ in range(K)]
 
     def step(i=None):
@@ -180,7 +180,10 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
     t_rows = avg(ev["conv1"], ev["conv1_wino"]) if wino else 0.0
     t_c1k = t_c1 - t_rows  # conv1's conv kernel alone
     t_c2 = avg(ev["conv2"], ev["conv3"])
-    t_c3 = avg(ev["conv3"], end_ev)
+    # the non-finite guard's four gated launches after conv3 (they exit at once on finite features)
+    guarded = ws.guard_src is not None
+    t_c3 = avg(ev["conv3"], ev["guard"] if guarded else end_ev)
+    t_guard = avg(ev["guard"], end_ev) if guarded else 0.0
     wino2 = eng.wino_conv2_active(ws)  # conv2 -> conv3 partials as row-Winograd
     value = B * K / dt
     # algorithmic work; conv1 runs over the N*C view channels per step (the
@@ -262,7 +265,7 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
                      "direct_equiv_achieved": round(3 * conv1_flop * active / (t_c1 * 1e-3) / 1e12, 2)
                      if precision == "bf16x3" else None},
         "stages_ms": {"warp_all_views": round(t_warp, 4), "conv1": round(t_c1, 4), "conv2": round(t_c2, 4),
-                      "conv3": round(t_c3, 4),
+                      "conv3": round(t_c3, 4), "nonfinite_guard": round(t_guard, 4),
                       **({"conv1_wino_rows": round(t_rows, 4), "conv1_wino_conv": round(t_c1k, 4)} if wino else {})},
         # SURVEY §8(d) "achieved fraction": the stages' roofline floors over the measured step;
         # conv1+conv2 priced as the 3 bf16 MFMA passes the split executes (bf16x3) or at the

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -195,7 +195,12 @@ typedef struct mvbev_conv_desc {
  *   a band caller must supply every row the output band needs. */
 int mvbev_conv3x3_f32(const float* x, const mvbev_conv_desc* desc, const float* w_packed,
                       const float* bias, const float* init, int64_t Cout, int dilation,
-                      int relu, float* y, void* stream);
+                      int relu, float* y, const int32_t* gate, int32_t gate_tag, void* stream);
+/* gate (this entry point, mvbev_conv3x3_cout1_f32, mvbev_warp_views_exact_f32; ABI 11600): a device
+ * int32; when non-NULL the launch does its work only if *gate == gate_tag at the time it runs (every
+ * workgroup exits at once otherwise) — a decision taken on the device in stream order, so a caller
+ * can enqueue a conditional path without a host sync (the non-finite guard of mvbev_bev_fuse and
+ * the Python engine).  NULL: always run. */
 
 /* Input layouts of mvbev_conv3x3_bf16x3 (descriptor strides are always in 4-byte
  * "channel-element" units, i.e. as for an fp32 tensor of the same logical shape). */
@@ -296,13 +301,27 @@ int mvbev_conv3x3_bf16x3_ex3(const void* x, int x_layout, const mvbev_conv_desc*
  * column) whose 5 samples all fall outside the source is skipped.  Replaces :69 + :77 + the
  * first step of conv1 (:51) for inference. */
 int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t H,
-                               int64_t W, int64_t Ho, int64_t Wo, int64_t r3_rows, int flags, void* stream);
+                               int64_t W, int64_t Ho, int64_t Wo, int64_t r3_rows, int flags, int32_t* nonfinite,
+                               int32_t nf_tag, void* stream);
 /* The same from backbone-resolution maps [B][C][h][w] (fp32, unit column stride, w >= 4): the
  * fused 3x upsample + warp of mvbev_warp_views_upsampled (m for the upsampled size H x W) and the
  * row transform in one pass (the detector's inference path, :65 + :69 + :77 + conv1's first step). */
 int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t h,
                                          int64_t w, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int64_t r3_rows,
-                                         int flags, void* stream);
+                                         int flags, int32_t* nonfinite, int32_t nf_tag, void* stream);
+/* nonfinite (both fused warps, ABI 11600; NULL = no report): nf_tag is stored into the device int32
+ * *nonfinite when a sample reads a NaN / inf feature (conservatively also when finite values overflow).
+ * The fused form folds B^T (and the upsample's taps into one 3x3 window), so it cannot keep the
+ * reference's NaN / inf pattern for such features; the caller's exact path, gated on the report, can:
+ *   mvbev_warp_views_exact_f32 — the warp (h = H, w = W) or the 3x upsample + warp (h x w backbone
+ *   maps, persp_trans_detector.py:65 + :69) in the reference's own evaluation order: per in-bounds
+ *   corner the PyTorch upsample value (both taps of each axis multiplied, zero weights included; no
+ *   fma contraction in the source index), times its grid_sample weight; out-of-bounds corners selected
+ *   to 0.  fp32 src [B][C][h][w], fp32 dst [B][C][Ho][Wo] at element strides ([3] == 1); gate as
+ *   mvbev_conv3x3_f32's. */
+int mvbev_warp_views_exact_f32(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t h, int64_t w,
+                               int64_t H, int64_t W, int64_t Ho, int64_t Wo, const int32_t* gate, int32_t gate_tag,
+                               void* stream);
 size_t mvbev_conv3x3_packed_bytes_wino(int64_t Cout, int64_t K);
 int mvbev_pack_conv3x3_weight_wino(const float* w, int64_t Cout, int64_t Cin_w, const int32_t* chan_map,
                                    int64_t K, void* w_packed, void* stream);
@@ -353,7 +372,8 @@ int mvbev_cout1_reduce_partials(const void* partials, const mvbev_conv_desc* des
  * H x W image;  w : [C][3][3] contiguous fp32;  y : [B][1][out_rows][W]. */
 int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int64_t W,
                             int64_t in_row0, int64_t in_rows, int64_t out_row0, int64_t out_rows,
-                            const float* w, int dilation, float* y, void* stream);
+                            const float* w, int dilation, float* y, const int32_t* gate, int32_t gate_tag,
+                            void* stream);
 
 /* ---- one-call project + fuse ----------------------------------------------
  * The inference hot path of PerspTransDetector.forward after the backbone
@@ -392,8 +412,9 @@ typedef struct mvbev_bev_plan {     /* host memory, caller-owned; filled by the 
   int32_t frustum;                  /* conv1 skips the views a tile's camera frustum excludes (C % 16 == 0 after padding) */
   int32_t prepared;
   int32_t wino2;                    /* after prepare: 1 = row-Winograd conv2 -> conv3 partials (ABI 11500; finite geometry) */
+  int32_t guard;                    /* 1 = the non-finite-feature guard runs behind the row-Winograd path (ABI 11600) */
   int64_t Cs, tiles;                /* channels per view slot (C rounded to 8); conv1's 12 x 32 tiles */
-  size_t off[16];                   /* workspace regions */
+  size_t off[24];                   /* workspace regions */
   size_t workspace_bytes;           /* >= what mvbev_bev_fuse_workspace_bytes returns, 256-B aligned base */
   const float* b2;
   const float* w3;
@@ -404,7 +425,11 @@ int mvbev_bev_fuse_prepare(mvbev_bev_plan* plan, const float* w1, const float* b
                            const float* w3, void* workspace, size_t ws_bytes, void* stream);
 /* views: host array of N device pointers (layout per src_kind); map: [B][1][Ho][Wo] fp32.  fp32
  * sources: the warp writes conv1's row-Winograd transform directly; fp16 sources (and geometry
- * with non-finite samples) run the direct conv1 on the split slab. */
+ * with non-finite samples) run the direct conv1 on the split slab.  guard (fp32 sources, ABI
+ * 11600): the warp reports a NaN / inf feature it samples into a device flag, and the exact path
+ * (mvbev_warp_views_exact_f32 into an fp32 slab, mvbev_conv3x3_f32 twice, mvbev_conv3x3_cout1_f32,
+ * each gated on that flag) rewrites the map with the reference's NaN / inf pattern — decided on the
+ * device, no host sync; four launches that exit at once when the features are finite. */
 int mvbev_bev_fuse(const mvbev_bev_plan* plan, const void* const* views, float* map, void* workspace,
                    size_t ws_bytes, void* stream);
 

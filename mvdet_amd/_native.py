@@ -78,6 +78,7 @@ EXPORTS = (
     "mvbev_bev_fuse_workspace_bytes",
     "mvbev_bev_fuse_prepare",
     "mvbev_bev_fuse",
+    "mvbev_warp_views_exact_f32",
 )
 BEV_SRC_F32, BEV_SRC_F16, BEV_SRC_BACKBONE_F32 = 0, 1, 2  # MVBEV_BEV_SRC_*
 WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
@@ -132,8 +133,9 @@ class BevGeometry(ctypes.Structure):
 class BevPlan(ctypes.Structure):
     """``mvbev_bev_plan`` (include/mvbev.h)."""
     _fields_ = [("g", BevGeometry), ("wino", ctypes.c_int32), ("frustum", ctypes.c_int32),
-                ("prepared", ctypes.c_int32), ("wino2", ctypes.c_int32), ("Cs", ctypes.c_int64),
-                ("tiles", ctypes.c_int64), ("off", ctypes.c_size_t * 16), ("workspace_bytes", ctypes.c_size_t),
+                ("prepared", ctypes.c_int32), ("wino2", ctypes.c_int32), ("guard", ctypes.c_int32),
+                ("Cs", ctypes.c_int64), ("tiles", ctypes.c_int64), ("off", ctypes.c_size_t * 24),
+                ("workspace_bytes", ctypes.c_size_t),
                 ("b2", ctypes.c_void_p), ("w3", ctypes.c_void_p)]
 
 
@@ -168,7 +170,7 @@ def _declare(lib):
     lib.mvbev_pack_conv3x3_weight_f32.argtypes = [_p, _i64, _i64, _p, _i64, _p, _p]
     lib.mvbev_conv3x3_f32.restype = ctypes.c_int
     lib.mvbev_conv3x3_f32.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64, ctypes.c_int,
-                                      ctypes.c_int, _p, _p]
+                                      ctypes.c_int, _p, _p, ctypes.c_int32, _p]
     lib.mvbev_conv3x3_packed_bytes_bf16x3.restype = ctypes.c_size_t
     lib.mvbev_conv3x3_packed_bytes_bf16x3.argtypes = [_i64, _i64]
     lib.mvbev_pack_conv3x3_weight_bf16x3.restype = ctypes.c_int
@@ -209,10 +211,14 @@ def _declare(lib):
                                                              ctypes.c_int, _p, _p, ctypes.c_size_t, _p]
     lib.mvbev_warp_views_wino_rows.restype = ctypes.c_int
     lib.mvbev_warp_views_wino_rows.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
-                                               _i64, _i64, ctypes.c_int, _p]
+                                               _i64, _i64, ctypes.c_int, _p, ctypes.c_int32, _p]
     lib.mvbev_warp_views_upsampled_wino_rows.restype = ctypes.c_int
     lib.mvbev_warp_views_upsampled_wino_rows.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64,
-                                                         _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_int, _p]
+                                                         _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_int, _p,
+                                                         ctypes.c_int32, _p]
+    lib.mvbev_warp_views_exact_f32.restype = ctypes.c_int
+    lib.mvbev_warp_views_exact_f32.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
+                                               _i64, _i64, _i64, _p, ctypes.c_int32, _p]
     lib.mvbev_warp_tile_mask.restype = ctypes.c_int
     lib.mvbev_warp_tile_mask.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
                                          _i64, _i64, _i64, _i64, _p, _p]
@@ -279,7 +285,7 @@ def _declare(lib):
                                              _i64, _i64, _i64, _i64, _i64, ctypes.c_int, _p]
     lib.mvbev_conv3x3_cout1_f32.restype = ctypes.c_int
     lib.mvbev_conv3x3_cout1_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p,
-                                            ctypes.c_int, _p, _p]
+                                            ctypes.c_int, _p, _p, ctypes.c_int32, _p]
     lib.mvbev_warp_views_split_bf16_ex.restype = ctypes.c_int
     lib.mvbev_warp_views_split_bf16_ex.argtypes = (lib.mvbev_warp_views_split_bf16.argtypes[:-1] +
                                                    [ctypes.c_int, _p])

@@ -10,8 +10,13 @@
 //   epilogue, their reduce -> map [B][1][Ho][Wo].
 //
 // Geometry that can produce a non-finite warp sample runs the direct conv1 on the split slab
-// instead (the reference's NaN pattern; see mvbev_warp_nonfinite_views).  Everything here is a
-// sequence of the library's own C entry points over one caller-owned workspace.
+// instead (the reference's NaN pattern; see mvbev_warp_nonfinite_views).  Non-finite FEATURES
+// (plan.guard, the row-Winograd path): the fused warp reports a NaN / inf it samples into a device
+// flag, and the guard's exact path — the reference-order warp (+ upsample) into an fp32 slab, the
+// fp32-MFMA conv1 / conv2 and the single-output conv3, each a no-op unless the flag is set — then
+// rewrites the map, so a NaN / inf reaches exactly the outputs it reaches in the reference (no host
+// sync: the decision is taken on the device).  Everything here is a sequence of the library's own C
+// entry points over one caller-owned workspace.
 #include <algorithm>
 #include <cstring>
 #include <numeric>
@@ -27,7 +32,8 @@ constexpr int64_t kTileW = MVBEV_CONV_TILE_W;
 constexpr size_t kAlign = 256;
 
 enum Region { R_MAP1, R_MAPC, R_PACK1, R_PACK2, R_PACKC, R_CIN, R_INIT, R_MASK, R_ORDER, R_NF, R_BIG, R_Y1, R_T2,
-              R_P3, R_COUNT };
+              R_GFLAG, R_GPACK1, R_GPACK2, R_GSLAB, R_P3, R_COUNT };
+static_assert(R_COUNT <= 24, "mvbev_bev_plan.off");
 
 size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
 
@@ -92,6 +98,16 @@ void t_views(const mvbev_bev_plan* p, const void* const* views, void* t, mvbev_w
     const int st_ = (x);           \
     if (st_ != MVBEV_OK) return st_; \
   } while (0)
+// the same while host buffers are still the source / target of enqueued copies: drain the stream
+// before returning, so no copy outlives the host memory it reads or writes
+#define BEV_TRY_SYNC(x, s)                    \
+  do {                                        \
+    const int st_ = (x);                      \
+    if (st_ != MVBEV_OK) {                    \
+      (void)hipStreamSynchronize(s);          \
+      return st_;                             \
+    }                                         \
+  } while (0)
 
 }  // namespace
 
@@ -134,7 +150,15 @@ int mvbev_bev_plan_init(const mvbev_bev_geometry* g, mvbev_bev_plan* p) {
   sz[R_NF] = 4;
   sz[R_BIG] = std::max(t_bytes, slab_bytes);  // T (Winograd) or the split slab (direct conv1)
   sz[R_Y1] = (size_t)g->B * kMid * g->Ho * g->Wo * 4;
-  sz[R_T2] = mvbev_wino_rows_bytes(&d2);  // conv2's row-Winograd transform of y1
+  sz[R_T2] = std::max(mvbev_wino_rows_bytes(&d2),  // conv2's row-Winograd transform of y1 (the guard: its y2)
+                      (size_t)g->B * kMid * g->Ho * g->Wo * 4);
+  // the non-finite guard (row-Winograd plans): flag, fp32 packs of conv1 / conv2, the fp32 slab; its y1
+  // reuses R_Y1 and its y2 R_T2 (both free once the fast path's conv2 has run)
+  p->guard = p->wino;
+  sz[R_GFLAG] = 4;
+  sz[R_GPACK1] = p->guard ? 4 * mvbev_conv3x3_packed_floats(kMid, K) : 0;
+  sz[R_GPACK2] = p->guard ? 4 * mvbev_conv3x3_packed_floats(kMid, kMid) : 0;
+  sz[R_GSLAB] = p->guard ? slab_bytes : 0;
   sz[R_P3] = mvbev_conv3x3_bf16x3_cout1_partials_bytes(&d2, kMid);
   size_t o = 0;
   for (int r = 0; r < R_COUNT; ++r) {
@@ -167,22 +191,27 @@ int mvbev_bev_fuse_prepare(mvbev_bev_plan* p, const float* w1, const float* b1, 
   mapc[0] = (int32_t)nc;
   mapc[1] = (int32_t)(nc + 1);
   if (hipMemcpyAsync(at<int32_t>(ws, p, R_MAP1), map1.data(), map1.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(at<int32_t>(ws, p, R_MAPC), mapc.data(), mapc.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess)
+      hipMemcpyAsync(at<int32_t>(ws, p, R_MAPC), mapc.data(), mapc.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess) {
+    (void)hipStreamSynchronize(s);
     return MVBEV_ERR_HIP;
+  }
   // geometry: non-finite samples (-> direct conv1), the frustum mask of the 12 x 32 conv tiles
   std::vector<mvbev_warp_view> mv((size_t)g.num_views);
   std::memset(mv.data(), 0, mv.size() * sizeof(mvbev_warp_view));
   for (int v = 0; v < g.num_views; ++v) std::memcpy(mv[(size_t)v].m, g.m[v], sizeof(mv[0].m));
-  BEV_TRY(mvbev_warp_nonfinite_views(mv.data(), g.num_views, g.H, g.W, g.Ho, g.Wo, at<uint32_t>(ws, p, R_NF), stream));
+  BEV_TRY_SYNC(mvbev_warp_nonfinite_views(mv.data(), g.num_views, g.H, g.W, g.Ho, g.Wo, at<uint32_t>(ws, p, R_NF),
+                                          stream), s);
   if (p->frustum)
-    BEV_TRY(mvbev_warp_tile_mask(mv.data(), g.num_views, g.H, g.W, g.Ho, g.Wo, 0, g.Ho, 12, kTileW, 1,
-                                 at<uint32_t>(ws, p, R_MASK), stream));
+    BEV_TRY_SYNC(mvbev_warp_tile_mask(mv.data(), g.num_views, g.H, g.W, g.Ho, g.Wo, 0, g.Ho, 12, kTileW, 1,
+                                      at<uint32_t>(ws, p, R_MASK), stream), s);
   uint32_t nf = 0;
   std::vector<uint32_t> mask((size_t)p->tiles, 0);
-  if (hipMemcpyAsync(&nf, at<uint32_t>(ws, p, R_NF), 4, hipMemcpyDeviceToHost, s) != hipSuccess) return MVBEV_ERR_HIP;
-  if (p->frustum && hipMemcpyAsync(mask.data(), at<uint32_t>(ws, p, R_MASK), mask.size() * 4, hipMemcpyDeviceToHost,
-                                   s) != hipSuccess)
+  if (hipMemcpyAsync(&nf, at<uint32_t>(ws, p, R_NF), 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      (p->frustum && hipMemcpyAsync(mask.data(), at<uint32_t>(ws, p, R_MASK), mask.size() * 4, hipMemcpyDeviceToHost,
+                                    s) != hipSuccess)) {
+    (void)hipStreamSynchronize(s);
     return MVBEV_ERR_HIP;
+  }
   if (hipStreamSynchronize(s) != hipSuccess) return MVBEV_ERR_HIP;
   p->wino = p->wino && nf == 0 ? 1 : 0;
   p->wino2 = nf == 0 ? 1 : 0;  // conv2's Winograd form (y1 finite), as the engine's wino_conv2_active
@@ -198,10 +227,9 @@ int mvbev_bev_fuse_prepare(mvbev_bev_plan* p, const float* w1, const float* b1, 
       if (ma != mb) return ma < mb;
       return a < b;
     });
-    if (hipMemcpyAsync(at<int32_t>(ws, p, R_ORDER), order.data(), order.size() * 4, hipMemcpyHostToDevice, s) !=
-        hipSuccess)
-      return MVBEV_ERR_HIP;
-    if (hipStreamSynchronize(s) != hipSuccess) return MVBEV_ERR_HIP;  // the host order buffer's lifetime
+    const bool ok = hipMemcpyAsync(at<int32_t>(ws, p, R_ORDER), order.data(), order.size() * 4, hipMemcpyHostToDevice,
+                                   s) == hipSuccess;
+    if (hipStreamSynchronize(s) != hipSuccess || !ok) return MVBEV_ERR_HIP;  // the host order buffer's lifetime
   }
   // weights: conv1 (G w for the Winograd form, or the direct pack), conv2, and the coord term
   if (p->wino)
@@ -214,6 +242,14 @@ int mvbev_bev_fuse_prepare(mvbev_bev_plan* p, const float* w1, const float* b1, 
     BEV_TRY(mvbev_pack_conv3x3_weight_wino(w2, kMid, kMid, nullptr, kMid, at<void>(ws, p, R_PACK2), stream));
   else
     BEV_TRY(mvbev_pack_conv3x3_weight_bf16x3(w2, kMid, kMid, nullptr, kMid, at<void>(ws, p, R_PACK2), stream));
+  p->guard = p->guard && p->wino;  // non-finite geometry already runs the direct convs
+  if (p->guard) {  // the exact path's fp32 packs; its slab's padding channels stay zero
+    BEV_TRY(mvbev_pack_conv3x3_weight_f32(w1, kMid, cin, at<int32_t>(ws, p, R_MAP1), K, at<float>(ws, p, R_GPACK1),
+                                          stream));
+    BEV_TRY(mvbev_pack_conv3x3_weight_f32(w2, kMid, kMid, nullptr, kMid, at<float>(ws, p, R_GPACK2), stream));
+    if (hipMemsetAsync(at<void>(ws, p, R_GSLAB), 0, p->off[R_GSLAB + 1] - p->off[R_GSLAB], s) != hipSuccess)
+      return MVBEV_ERR_HIP;
+  }
   BEV_TRY(mvbev_pack_conv3x3_weight_f32(w1, kMid, cin, at<int32_t>(ws, p, R_MAPC), kKC, at<float>(ws, p, R_PACKC),
                                         stream));
   float* cinp = at<float>(ws, p, R_CIN);
@@ -225,7 +261,7 @@ int mvbev_bev_fuse_prepare(mvbev_bev_plan* p, const float* w1, const float* b1, 
   dc.batch_stride = kKC * g.Ho * g.Wo; dc.in_row0 = 0; dc.in_rows = g.Ho; dc.out_row0 = 0; dc.out_rows = g.Ho;
   // coord term = conv1 bias + conv1 over the two coord channels (:21, :77): input-independent
   BEV_TRY(mvbev_conv3x3_f32(cinp, &dc, at<float>(ws, p, R_PACKC), b1, nullptr, kMid, 1, 0, at<float>(ws, p, R_INIT),
-                            stream));
+                            nullptr, 0, stream));
   // T / the slab: zero once; later warps skip the pixels whose samples fall outside the source
   if (hipMemsetAsync(at<void>(ws, p, R_BIG), 0, p->off[R_BIG + 1] - p->off[R_BIG], s) != hipSuccess)
     return MVBEV_ERR_HIP;
@@ -250,16 +286,18 @@ int mvbev_bev_fuse(const mvbev_bev_plan* p, const void* const* views, float* map
   const int32_t* order = p->frustum ? at<int32_t>(ws, p, R_ORDER) : nullptr;
   const bool backbone = g.src_kind == MVBEV_BEV_SRC_BACKBONE_F32;
   void* y1 = at<void>(ws, p, R_Y1);
+  int32_t* gflag = p->guard ? at<int32_t>(ws, p, R_GFLAG) : nullptr;
+  if (gflag && hipMemsetAsync(gflag, 0, 4, static_cast<hipStream_t>(stream)) != hipSuccess) return MVBEV_ERR_HIP;
   // a4 + a5 + a6 (+ conv1's B^T): the warp of every view in one launch
   if (p->wino) {
     t_views(p, views, big, wv);
     const int64_t r3 = 4 * ((g.Ho + 11) / 12);
     if (backbone)
       BEV_TRY(mvbev_warp_views_upsampled_wino_rows(wv, g.num_views, g.B, g.C, g.h, g.w, g.H, g.W, g.Ho, g.Wo, r3,
-                                                   MVBEV_WARP_DST_ZEROED, stream));
+                                                   MVBEV_WARP_DST_ZEROED, gflag, 1, stream));
     else
       BEV_TRY(mvbev_warp_views_wino_rows(wv, g.num_views, g.B, g.C, g.H, g.W, g.Ho, g.Wo, r3, MVBEV_WARP_DST_ZEROED,
-                                         stream));
+                                         gflag, 1, stream));
   } else {
     slab_views(p, views, big, wv);
     if (backbone)
@@ -290,6 +328,28 @@ int mvbev_bev_fuse(const mvbev_bev_plan* p, const void* const* views, float* map
                                                 p->workspace_bytes - p->off[R_P3], stream));
   }
   BEV_TRY(mvbev_cout1_reduce_partials(p3, &d2, kMid, 4, map, 0, g.Ho, stream));
+  if (gflag) {  // the non-finite guard: each launch exits at once unless the warp set the flag
+    float* gslab = at<float>(ws, p, R_GSLAB);
+    const int64_t plane = g.Ho * g.Wo;
+    for (int s = 0; s < g.num_views; ++s) {
+      mvbev_warp_view& v = wv[s];
+      v.src = views[s];
+      const int64_t sh = backbone ? g.h : g.H, sw = backbone ? g.w : g.W;
+      v.src_strides[0] = g.C * sh * sw; v.src_strides[1] = sh * sw; v.src_strides[2] = sw; v.src_strides[3] = 1;
+      v.dst = gslab + (size_t)s * g.B * p->Cs * plane;
+      v.dst_strides[0] = p->Cs * plane; v.dst_strides[1] = plane; v.dst_strides[2] = g.Wo; v.dst_strides[3] = 1;
+      std::memcpy(v.m, g.m[s], sizeof(v.m));
+    }
+    BEV_TRY(mvbev_warp_views_exact_f32(wv, g.num_views, g.B, g.C, backbone ? g.h : g.H, backbone ? g.w : g.W, g.H,
+                                       g.W, g.Ho, g.Wo, gflag, 1, stream));
+    float* gy1 = at<float>(ws, p, R_Y1);
+    float* gy2 = at<float>(ws, p, R_T2);
+    BEV_TRY(mvbev_conv3x3_f32(gslab, &d1, at<float>(ws, p, R_GPACK1), nullptr, at<float>(ws, p, R_INIT), kMid, 1, 1,
+                              gy1, gflag, 1, stream));
+    BEV_TRY(mvbev_conv3x3_f32(gy1, &d2, at<float>(ws, p, R_GPACK2), p->b2, nullptr, kMid, 2, 1, gy2, gflag, 1,
+                              stream));
+    BEV_TRY(mvbev_conv3x3_cout1_f32(gy2, g.B, kMid, g.Ho, g.Wo, 0, g.Ho, 0, g.Ho, p->w3, 4, map, gflag, 1, stream));
+  }
   return MVBEV_OK;
 }
 

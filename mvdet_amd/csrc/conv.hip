@@ -78,6 +78,8 @@ struct ConvArgs {
   int group, nchunks, Cout, H, W;
   int in_row0, in_rows, out_row0, out_rows;
   int tiles_x, tiles_y, n_cot, nwg;
+  const int32_t* gate;  // run only when *gate == gate_tag (NULL: always; the non-finite guard's path)
+  int32_t gate_tag;
 };
 
 #ifndef MVBEV_CONV_MINWAVES
@@ -111,6 +113,7 @@ __global__ __launch_bounds__(64 * NWAVES, MVBEV_CONV_MINWAVES) void conv3x3_mfma
   constexpr int NBUF = DBUF ? 2 : 1;
   constexpr int BUF = WS + ((XS + 3) / 4) * 4;  // floats per LDS buffer (16-B aligned parts)
   __shared__ __attribute__((aligned(16))) float lds[NBUF * BUF];
+  if (a.gate && *a.gate != a.gate_tag) return;
 
   const int wg = xcd_remap(blockIdx.x, a.nwg);
   const int cot = wg % a.n_cot;
@@ -256,8 +259,9 @@ constexpr int C1_WAVES = 8;  // waves per conv3 block: each sums C/8 channels of
 template <int DIL>
 __global__ __launch_bounds__(64 * C1_WAVES) void conv3x3_cout1_kernel(
     const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ y, int C, int H,
-    int W, int in_row0, int in_rows, int out_row0) {
+    int W, int in_row0, int in_rows, int out_row0, const int32_t* gate, int32_t gate_tag) {
   __shared__ float part[C1_WAVES][64];
+  if (gate && *gate != gate_tag) return;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int col = blockIdx.x * 64 + lane;
@@ -328,9 +332,10 @@ constexpr int C1Q_SUBS = C1Q_WAVES * (64 / C1Q_QUADS);  // channel subsets per b
 template <int DIL>
 __global__ __launch_bounds__(64 * C1Q_WAVES) void conv3x3_cout1_q4_kernel(
     const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ y, int C, int H,
-    int W, int in_row0, int in_rows, int out_row0, int out_rows) {
+    int W, int in_row0, int in_rows, int out_row0, int out_rows, const int32_t* gate, int32_t gate_tag) {
   static_assert(DIL % 4 == 0, "16-B aligned taps");
   __shared__ f32x4_t part[C1Q_WAVES][C1Q_QUADS];
+  if (gate && *gate != gate_tag) return;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int qi = lane % C1Q_QUADS, sub = wave * (64 / C1Q_QUADS) + lane / C1Q_QUADS;
@@ -421,7 +426,7 @@ int mvbev_pack_conv3x3_weight_f32(const float* w, int64_t Cout, int64_t Cin_w,
 
 int mvbev_conv3x3_f32(const float* x, const mvbev_conv_desc* d, const float* w_packed,
                       const float* bias, const float* init, int64_t Cout, int dilation, int relu,
-                      float* y, void* stream) {
+                      float* y, const int32_t* gate, int32_t gate_tag, void* stream) {
   using namespace mvbev;
   if (!x || !d || !w_packed || !y) return MVBEV_ERR_NULL;
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || d->in_rows <= 0 ||
@@ -440,6 +445,8 @@ int mvbev_conv3x3_f32(const float* x, const mvbev_conv_desc* d, const float* w_p
   a.H = (int)d->H; a.W = (int)d->W;
   a.in_row0 = (int)d->in_row0; a.in_rows = (int)d->in_rows;
   a.out_row0 = (int)d->out_row0; a.out_rows = (int)d->out_rows;
+  a.gate = gate;
+  a.gate_tag = gate_tag;
   constexpr int kWaves = MVBEV_CONV_WAVES;
   constexpr bool kDbuf = MVBEV_CONV_DBUF != 0;
   a.tiles_x = (int)ceil_div(d->W, TW);
@@ -466,7 +473,8 @@ int mvbev_conv3x3_f32(const float* x, const mvbev_conv_desc* d, const float* w_p
 
 int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int64_t W,
                             int64_t in_row0, int64_t in_rows, int64_t out_row0, int64_t out_rows,
-                            const float* w, int dilation, float* y, void* stream) {
+                            const float* w, int dilation, float* y, const int32_t* gate, int32_t gate_tag,
+                            void* stream) {
   using namespace mvbev;
   if (!x || !w || !y) return MVBEV_ERR_NULL;
   if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || in_rows <= 0 || out_rows <= 0)
@@ -478,14 +486,14 @@ int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int
       (reinterpret_cast<uintptr_t>(y) & 15) == 0 && out_rows * (W / 4) <= (int64_t)INT32_MAX - 64) {
     dim3 qgrid((unsigned)ceil_div(out_rows * (W / 4), C1Q_QUADS), (unsigned)B);
     hipLaunchKernelGGL(conv3x3_cout1_q4_kernel<4>, qgrid, dim3(64 * C1Q_WAVES), 0, s, x, w, y, (int)C, (int)H,
-                       (int)W, (int)in_row0, (int)in_rows, (int)out_row0, (int)out_rows);
+                       (int)W, (int)in_row0, (int)in_rows, (int)out_row0, (int)out_rows, gate, gate_tag);
     MVBEV_CHECK_LAUNCH();
     return MVBEV_OK;
   }
   dim3 grid((unsigned)ceil_div(W, 64), (unsigned)out_rows, (unsigned)B);
 #define MVBEV_C1_LAUNCH(D)                                                                      \
   hipLaunchKernelGGL(conv3x3_cout1_kernel<D>, grid, dim3(64 * C1_WAVES), 0, s, x, w, y, (int)C,  \
-                     (int)H, (int)W, (int)in_row0, (int)in_rows, (int)out_row0)
+                     (int)H, (int)W, (int)in_row0, (int)in_rows, (int)out_row0, gate, gate_tag)
   switch (dilation) {
     case 1: MVBEV_C1_LAUNCH(1); break;
     case 2: MVBEV_C1_LAUNCH(2); break;

@@ -481,7 +481,7 @@ const char* mvbev_status_string(int s) {
   }
 }
 
-int mvbev_version(void) { return 11500; }
+int mvbev_version(void) { return 11600; }
 
 int mvbev_warp_perspective_f32(const float* src, int64_t B, int64_t C, int64_t H, int64_t W,
                                const int64_t src_strides[4], const float* m, float* dst,
@@ -514,7 +514,8 @@ int mvbev_warp_views_split_bf16_ex(const mvbev_warp_view* views, int nviews, int
 }
 
 int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t H,
-                               int64_t W, int64_t Ho, int64_t Wo, int64_t r3_rows, int flags, void* stream) {
+                               int64_t W, int64_t Ho, int64_t Wo, int64_t r3_rows, int flags, int32_t* nonfinite,
+                               int32_t nf_tag, void* stream) {
   using namespace mvbev;
   if (!views) return MVBEV_ERR_NULL;
   if (flags & ~MVBEV_WARP_DST_ZEROED) return MVBEV_ERR_SHAPE;
@@ -540,6 +541,8 @@ int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t
   }
   a.nviews = nviews;
   a.skip_zero = (flags & MVBEV_WARP_DST_ZEROED) != 0;
+  a.nonfinite = nonfinite;
+  a.nf_tag = nf_tag;
   a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
   a.tiles_x = (int)ceil_div(Wo, kWwCols);
   a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);  // 4 three-row tiles per block

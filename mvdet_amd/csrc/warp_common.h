@@ -60,6 +60,13 @@ struct WarpArgs {
   int nviews, B, C, H, W, Ho, Wo, tiles_x, tiles, chunks, nwg;
   bool pair;  // fp32 rows with unit column stride and W >= 2: corner pairs as 8-B loads
   bool skip_zero;  // MVBEV_WARP_DST_ZEROED: outside samples (exact zeros) are not written
+  // non-finite guard (ABI 11600): the fused warps store nf_tag into *nonfinite when a sample they
+  // produce is non-finite (a NaN / inf in the features it reads); the exact warp runs only when
+  // *gate == gate_tag (NULL: always)
+  int32_t* nonfinite;
+  int32_t nf_tag;
+  const int32_t* gate;
+  int32_t gate_tag;
 };
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -121,6 +128,10 @@ struct UpTaps {
   float l0, l1;
 };
 __device__ inline UpTaps up_taps(int X, float scale, int n) {
+  // no fma contraction: PyTorch's CPU upsample rounds the product before the subtraction, so an
+  // upsampled index 3k + 1 lands exactly on source pixel k (l1 = 0, a zero-weight tap that turns
+  // an inf source value into NaN, as the reference does)
+#pragma clang fp contract(off)
   UpTaps t;
   float s = scale * ((float)X + 0.5f) - 0.5f;
   s = s < 0.f ? 0.f : s;
@@ -310,6 +321,14 @@ __device__ inline void wino_rows_phase2(const float (&ds)[kWwRows][kWwCols][8], 
   t[2] = 2.f * d[1] - 3.f * d[2] + d[3];
   t[3] = d[3] - d[1];
   t[4] = 2.f * d[1] - d[2] - 2.f * d[3] + d[4];
+  if (a.nonfinite) {
+    // every d row enters some T row with a non-zero coefficient, and a sample is non-finite when a
+    // value it reads is (every read value is multiplied by its weight, zero weights included), so
+    // the sum of the 10 T values is non-finite whenever a feature this thread's samples read is
+    // (or, conservatively, when finite values overflow): the caller's exact path then runs
+    const f32x2_t sum = (t[0] + t[1]) + (t[2] + t[3]) + t[4];
+    if (!isfinite(sum.x + sum.y)) *a.nonfinite = a.nf_tag;
+  }
   // a T row of dH (= Wo) columns is its hi plane [dH][8 bf16] then its lo plane (16-B units)
   unsigned* out = reinterpret_cast<unsigned*>(static_cast<u32x4_t*>(vw.dst) +
                                               (2 * ((int64_t)b * vw.dB + (int64_t)chunk * vw.dC +

@@ -315,11 +315,130 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino_kernel
   wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
 }
 
+// The exact-order warp (a5) and upsample + warp (a4 + a5): the non-finite guard's path
+// (mvbev_warp_views_exact_f32).  Per output pixel the kornia coordinates (warp_coord), then, per
+// in-bounds corner, the source value — with UP, PyTorch's bilinear upsample of that upsampled pixel
+// evaluated as the reference's CPU F.interpolate does (two taps per axis, both multiplied even at
+// weight 0: t = (x00 l0x + x01 l1x) l0y + (x10 l0x + x11 l1x) l1y) — times its grid_sample weight,
+// out-of-bounds corners selected to 0 (never multiplied).  So every product the reference forms is
+// formed here, and a NaN / inf in the features reaches exactly the outputs it reaches in
+// persp_trans_detector.py:65-69 (the fused kernels fold the taps into one 3x3 window and cannot).
+// Plain fp32 out [B][C][Ho][Wo] at element strides; one thread per output pixel, 8 channels per
+// block; runs only when *gate == gate_tag (the fused warp's report), else exits at once.
+template <bool UP>
+__global__ __launch_bounds__(256) void warp_exact_kernel(const UpArgs ua, int pix_blocks, int units) {
+  const WarpArgs& a = ua.w;
+  if (a.gate && *a.gate != a.gate_tag) return;  // the usual case: a few thousand workgroups exit here
+  // grid-stride over units = (b * nviews + view, 256-pixel block): one thread per output pixel, all
+  // channels (the taps computed once per pixel)
+  for (int unit = blockIdx.x; unit < units; unit += gridDim.x) {
+    const int bv = unit / pix_blocks, p = (unit - bv * pix_blocks) * 256 + threadIdx.x;
+    if (p >= a.Ho * a.Wo) continue;
+    const int view = bv % a.nviews, b = bv / a.nviews;
+    const WarpView& vw = a.v[view];
+    const int v = p / a.Wo, u = p - v * a.Wo;
+    float m[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) m[i] = vw.m[i];
+    const WarpCoord wc = warp_coord(m, u, v, a.Ho, a.Wo, a.H, a.W);
+    float* out = static_cast<float*>(vw.dst) + (int64_t)b * vw.dB + (int64_t)v * vw.dH + u;
+    if (!wc.inside) {
+      const float fill = wc.finite ? 0.f : __builtin_nanf("");
+      for (int c = 0; c < a.C; ++c) out[(int64_t)c * vw.dC] = fill;
+      continue;
+    }
+    const float ix = wc.ix, iy = wc.iy;
+    const float fx0 = floorf(ix), fy0 = floorf(iy);
+    const int x0 = (int)fx0, y0 = (int)fy0;
+    const float fx1 = fx0 + 1.f, fy1 = fy0 + 1.f;
+    const float wt[4] = {(fx1 - ix) * (fy1 - iy), (ix - fx0) * (fy1 - iy), (fx1 - ix) * (iy - fy0),
+                         (ix - fx0) * (iy - fy0)};  // nw, ne, sw, se (GridSampler.h)
+    const bool vx0 = x0 >= 0, vx1 = x0 + 1 <= a.W - 1, vy0 = y0 >= 0, vy1 = y0 + 1 <= a.H - 1;
+    const bool ok[4] = {vx0 && vy0, vx1 && vy0, vx0 && vy1, vx1 && vy1};
+    // per corner: the source offsets (UP: its 2 x 2 upsample taps) and their weights
+    int64_t off[4][4];
+    float lx[4][2], ly[4][2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int cx = min(max(x0 + (k & 1), 0), a.W - 1), cy = min(max(y0 + (k >> 1), 0), a.H - 1);
+      if constexpr (UP) {
+        const UpTaps tx = up_taps(cx, ua.sx, ua.sw), ty = up_taps(cy, ua.sy, ua.h);
+        off[k][0] = ty.i0 * vw.sH + tx.i0 * vw.sW;
+        off[k][1] = ty.i0 * vw.sH + tx.i1 * vw.sW;
+        off[k][2] = ty.i1 * vw.sH + tx.i0 * vw.sW;
+        off[k][3] = ty.i1 * vw.sH + tx.i1 * vw.sW;
+        lx[k][0] = tx.l0, lx[k][1] = tx.l1, ly[k][0] = ty.l0, ly[k][1] = ty.l1;
+      } else {
+        off[k][0] = off[k][1] = off[k][2] = off[k][3] = cy * vw.sH + cx * vw.sW;
+        lx[k][0] = lx[k][1] = ly[k][0] = ly[k][1] = 0.f;
+      }
+    }
+    const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
+    for (int c = 0; c < a.C; ++c) {
+      const float* pc = base + (int64_t)c * vw.sC;
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float val;
+        if constexpr (UP) {
+          val = (pc[off[k][0]] * lx[k][0] + pc[off[k][1]] * lx[k][1]) * ly[k][0] +
+                (pc[off[k][2]] * lx[k][0] + pc[off[k][3]] * lx[k][1]) * ly[k][1];
+        } else {
+          val = pc[off[k][0]];
+        }
+        acc += (ok[k] ? val : 0.f) * wt[k];
+      }
+      out[(int64_t)c * vw.dC] = acc;
+    }
+  }
+}
+
 }  // namespace mvbev
+
+extern "C" int mvbev_warp_views_exact_f32(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t h,
+                                          int64_t w, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
+                                          const int32_t* gate, int32_t gate_tag, void* stream) {
+  using namespace mvbev;
+  if (!views) return MVBEV_ERR_NULL;
+  if (B <= 0 || C <= 0 || h <= 0 || w <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 || nviews <= 0)
+    return MVBEV_ERR_RANK;
+  if (nviews > kWarpMaxViews || B * nviews > 65535 || C > INT32_MAX || H > INT32_MAX / 2 || W > INT32_MAX / 2 ||
+      Ho * Wo > INT32_MAX - 256 || ceil_div(Ho * Wo, 256) * B * nviews > INT32_MAX || H < h || W < w)
+    return MVBEV_ERR_SHAPE;
+  UpArgs ua = {};
+  WarpArgs& a = ua.w;
+  for (int i = 0; i < nviews; ++i) {
+    const mvbev_warp_view& s = views[i];
+    if (!s.src || !s.dst) return MVBEV_ERR_NULL;
+    if (s.dst_strides[3] != 1) return MVBEV_ERR_STRIDE;
+    WarpView& d = a.v[i];
+    d.src = s.src; d.sB = s.src_strides[0]; d.sC = s.src_strides[1];
+    d.sH = s.src_strides[2]; d.sW = s.src_strides[3];
+    d.dst = s.dst; d.dB = s.dst_strides[0]; d.dC = s.dst_strides[1]; d.dH = s.dst_strides[2];
+    d.m_dev = nullptr;
+    for (int k = 0; k < 9; ++k) d.m[k] = s.m[k];
+  }
+  a.nviews = nviews;
+  a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
+  a.gate = gate;
+  a.gate_tag = gate_tag;
+  ua.h = (int)h; ua.sw = (int)w;
+  ua.sy = (float)h / (float)H;
+  ua.sx = (float)w / (float)W;
+  const int pix_blocks = (int)ceil_div(Ho * Wo, 256), units = pix_blocks * (int)(B * nviews);
+  const dim3 grid((unsigned)std::min(units, 2048));
+  if (h == H && w == W)
+    hipLaunchKernelGGL(warp_exact_kernel<false>, grid, dim3(256), 0, as_stream(stream), ua, pix_blocks, units);
+  else
+    hipLaunchKernelGGL(warp_exact_kernel<true>, grid, dim3(256), 0, as_stream(stream), ua, pix_blocks, units);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
 
 extern "C" int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
                                                     int64_t h, int64_t w, int64_t H, int64_t W, int64_t Ho,
-                                                    int64_t Wo, int64_t r3_rows, int flags, void* stream) {
+                                                    int64_t Wo, int64_t r3_rows, int flags, int32_t* nonfinite,
+                                                    int32_t nf_tag, void* stream) {
   using namespace mvbev;
   if (flags & ~MVBEV_WARP_DST_ZEROED) return MVBEV_ERR_SHAPE;
   if (!views) return MVBEV_ERR_NULL;
@@ -349,6 +468,8 @@ extern "C" int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views
   a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);
   a.chunks = (int)ceil_div(C, kUpCPB);
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
+  a.nonfinite = nonfinite;
+  a.nf_tag = nf_tag;
   ua.h = (int)h; ua.sw = (int)w;
   ua.sy = (float)h / (float)H;
   ua.sx = (float)w / (float)W;

@@ -229,6 +229,47 @@ def fill_coord_map(dst: torch.Tensor) -> torch.Tensor:
     return dst
 
 
+def _gate(gate):
+    """``(flag, tag)`` -> (device pointer, int32 tag) for the ABI (None -> NULL, 0)."""
+    if gate is None:
+        return None, 0
+    flag, tag = gate
+    _require_cuda(flag)
+    if flag.dtype != torch.int32 or flag.numel() < 1:
+        raise ValueError("the guard flag is a device int32 tensor")
+    return flag.data_ptr(), int(tag)
+
+
+def warp_views_exact_into(srcs, m_norms, dsts, up_hw=None, gate=None) -> None:
+    """The reference's own evaluation order of the warp (a5) — and, with ``up_hw``, of the 3x
+    upsample feeding it (a4 + a5): ``mvbev_warp_views_exact_f32``.  Every product
+    ``F.interpolate`` and ``grid_sample`` form is formed (zero weights included), so a NaN / inf in
+    ``srcs`` reaches exactly the outputs it reaches in ``persp_trans_detector.py:65-69``.  fp32
+    ``srcs[i]`` [B,C,h,w] (the warp's source, or with ``up_hw`` the backbone map), ``dsts[i]`` fp32
+    [B,C,Ho,Wo] views (innermost stride 1); ``gate`` as ``conv3x3_desc``'s (the non-finite guard)."""
+    n = len(srcs)
+    if n == 0:
+        return
+    if not (len(m_norms) == n == len(dsts)) or n > 16:
+        raise ValueError("need 1..16 matching srcs / m_norms / dsts")
+    _require_cuda(*srcs, *dsts)
+    B, C, h, w = srcs[0].shape
+    H, W = (h, w) if up_hw is None else (int(up_hw[0]), int(up_hw[1]))
+    Ho, Wo = dsts[0].shape[2], dsts[0].shape[3]
+    arr = (_native.WarpView * n)()
+    for i, (s_, m, d) in enumerate(zip(srcs, m_norms, dsts)):
+        if tuple(s_.shape) != (B, C, h, w) or s_.dtype != torch.float32:
+            raise ValueError("all views must be fp32 [B,C,h,w] of one shape")
+        if tuple(d.shape) != (B, C, Ho, Wo) or d.dtype != torch.float32 or d.stride(3) != 1:
+            raise ValueError(f"dst must be an fp32 [{B},{C},{Ho},{Wo}] view with unit column stride")
+        mm = torch.as_tensor(m, dtype=torch.float32).reshape(9).tolist()
+        arr[i] = _native.WarpView(s_.data_ptr(), (ctypes.c_int64 * 4)(*s_.stride()), d.data_ptr(),
+                                  (ctypes.c_int64 * 4)(*d.stride()), (ctypes.c_float * 9)(*mm))
+    gp, gt = _gate(gate)
+    st = _native.load().mvbev_warp_views_exact_f32(arr, n, B, C, h, w, H, W, Ho, Wo, gp, gt, _stream(dsts[0]))
+    _native.check(st, "mvbev_warp_views_exact_f32")
+
+
 # ----------------------------------------------------------------------------------------------
 # convs
 
@@ -398,8 +439,10 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
                  init: Optional[torch.Tensor] = None, dilation: int = 1, relu: bool = False,
                  out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
                  group_mask: Optional[torch.Tensor] = None, tile_order: Optional[torch.Tensor] = None,
-                 tile_space: int = _native.TILES_GRID) -> torch.Tensor:
-    """Low-level form: ``x`` addressed through ``desc`` (``mvbev_conv_desc``).  bf16x3 only,
+                 tile_space: int = _native.TILES_GRID, gate=None) -> torch.Tensor:
+    """Low-level form: ``x`` addressed through ``desc`` (``mvbev_conv_desc``).  ``gate`` (fp32
+    conv only): ``(flag, tag)`` — the kernel runs only when the device int32 ``flag[0] == tag``
+    (the non-finite guard's path; ``warp_views_wino_rows_into``'s report).  bf16x3 only,
     optional: ``workspace`` — device scratch for the split-K tail
     (``conv3x3_workspace_bytes``); ``group_mask`` — per-tile active channel groups
     (``warp_tile_mask``), whose cleared groups are skipped; ``tile_order`` — with a mask,
@@ -442,6 +485,8 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
     bp = bias.data_ptr() if bias is not None else None
     ip = init.data_ptr() if init is not None else None
     if bf16x3:
+        if gate is not None:
+            raise ValueError("gate applies to the fp32 conv")
         wsp, wsn, gmp = None, 0, None
         if workspace is not None:
             _require_cuda(workspace)
@@ -479,8 +524,9 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
     elif group_mask is not None:
         raise ValueError("group_mask needs the bf16x3 conv")
     else:
+        gp, gt = _gate(gate)
         st = lib.mvbev_conv3x3_f32(x.data_ptr(), ctypes.byref(desc), packed.data_ptr(), bp, ip, cout,
-                                   int(dilation), int(bool(relu)), out.data_ptr(), _stream(x))
+                                   int(dilation), int(bool(relu)), out.data_ptr(), gp, gt, _stream(x))
         _native.check(st, "mvbev_conv3x3_f32")
     return out
 
@@ -514,13 +560,16 @@ def wino_rows(x: torch.Tensor, desc, t: torch.Tensor, group_mask: Optional[torch
 
 
 def warp_views_wino_rows_into(srcs, m_norms, t: torch.Tensor, slots, Cs: int, K: int, Ho: int, Wo: int,
-                              dst_zeroed: bool = False, up_hw=None) -> None:
+                              dst_zeroed: bool = False, up_hw=None, nonfinite=None) -> None:
     """Warp + row-Winograd transform in ONE launch (``mvbev_warp_views_wino_rows``): view i
     (fp32 ``srcs[i]`` [B,C,H,W], host kornia matrix ``m_norms[i]``) lands in channels
     [slots[i] * Cs, + C) of ``t``, the T buffer of ``wino_rows`` for a K-channel slab of
     Ho x Wo (whole grid, out_row0 = 0); the slab itself is not written.  ``up_hw``: the sources
     are backbone-resolution maps upsampled 3x to ``up_hw`` inside the warp
-    (``mvbev_warp_views_upsampled_wino_rows``; ``m_norms`` for the upsampled size)."""
+    (``mvbev_warp_views_upsampled_wino_rows``; ``m_norms`` for the upsampled size).  ``nonfinite``:
+    ``(flag, tag)`` — ``tag`` is stored into the device int32 ``flag[0]`` when a sample reads a NaN /
+    inf feature (the fused form cannot keep the reference's NaN pattern; ``warp_views_exact_into``
+    and the gated fp32 convs can)."""
     n = len(srcs)
     if n == 0:
         return
@@ -545,12 +594,13 @@ def warp_views_wino_rows_into(srcs, m_norms, t: torch.Tensor, slots, Cs: int, K:
         arr[i].dst_strides = _native._i64x4(K8 * 5 * r3 * Wo, 5 * r3 * Wo, Wo, 1)  # 32-byte units
         arr[i].m = (ctypes.c_float * 9)(*mm)
     flags = _native.WARP_DST_ZEROED if dst_zeroed else 0
+    fp, ft = _gate(nonfinite)
     if up_hw is not None:
         st = _native.load().mvbev_warp_views_upsampled_wino_rows(arr, n, B, C, H, W, int(up_hw[0]), int(up_hw[1]),
-                                                                 Ho, Wo, r3, flags, _stream(t))
+                                                                 Ho, Wo, r3, flags, fp, ft, _stream(t))
         _native.check(st, "mvbev_warp_views_upsampled_wino_rows")
         return
-    st = _native.load().mvbev_warp_views_wino_rows(arr, n, B, C, H, W, Ho, Wo, r3, flags, _stream(t))
+    st = _native.load().mvbev_warp_views_wino_rows(arr, n, B, C, H, W, Ho, Wo, r3, flags, fp, ft, _stream(t))
     _native.check(st, "mvbev_warp_views_wino_rows")
 
 
@@ -619,11 +669,12 @@ def conv3x3(x: torch.Tensor, packed: torch.Tensor, cout: int, bias: Optional[tor
 
 def conv3x3_cout1(x: torch.Tensor, weight: torch.Tensor, dilation: int, H: Optional[int] = None,
                   in_row0: int = 0, out_row0: int = 0, out_rows: Optional[int] = None,
-                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                  out: Optional[torch.Tensor] = None, gate=None) -> torch.Tensor:
     """``conv2d(x, weight[1,C,3,3], padding=d, dilation=d)`` (no bias).
 
     ``x`` [B,C,rows,W] holds global rows ``[in_row0, in_row0+rows)`` of an ``H``-row image
     (default: the whole image); returns rows ``[out_row0, out_row0+out_rows)`` → [B,1,out_rows,W].
+    ``gate``: as ``conv3x3_desc``'s.
     """
     _require_cuda(x, weight)
     if x.dim() != 4 or x.dtype != torch.float32 or not x.is_contiguous():
@@ -636,8 +687,11 @@ def conv3x3_cout1(x: torch.Tensor, weight: torch.Tensor, dilation: int, H: Optio
     w = weight.detach().contiguous()
     if out is None:
         out = torch.empty((B, 1, out_rows, W), dtype=torch.float32, device=x.device)
+    elif tuple(out.shape) != (B, 1, out_rows, W) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous fp32 [{B},1,{out_rows},{W}] tensor")
+    gp, gt = _gate(gate)
     st = _native.load().mvbev_conv3x3_cout1_f32(x.data_ptr(), B, C, H, W, in_row0, rows, out_row0, out_rows,
-                                                w.data_ptr(), int(dilation), out.data_ptr(), _stream(x))
+                                                w.data_ptr(), int(dilation), out.data_ptr(), gp, gt, _stream(x))
     _native.check(st, "mvbev_conv3x3_cout1_f32")
     return out
 
@@ -1192,29 +1246,62 @@ class BevFuse:
         """conv2 -> conv3 partials run row-Winograd (finite geometry; after prepare)."""
         return bool(self.plan.wino2)
 
+    def _check_weights(self, w) -> None:
+        g = self.plan.g
+        want = [(512, g.num_views * g.C + 2, 3, 3), (512,), (512, 512, 3, 3), (512,), (1, 512, 3, 3)]
+        names = ["map_classifier[0].weight", "map_classifier[0].bias", "map_classifier[2].weight",
+                 "map_classifier[2].bias", "map_classifier[4].weight"]
+        for t, shape, name in zip(w, want, names):
+            if t is None and name.endswith("bias"):
+                continue
+            if not isinstance(t, torch.Tensor) or tuple(t.shape) != shape or t.dtype != torch.float32:
+                got = (tuple(t.shape), t.dtype) if isinstance(t, torch.Tensor) else type(t)
+                raise ValueError(f"{name} must be float32 {list(shape)}, got {got}")
+
     def prepare(self, map_classifier, device) -> None:
-        """Once per weight version: ``map_classifier`` the reference's nn.Sequential (:51-54)."""
+        """Once per weight version: ``map_classifier`` the reference's nn.Sequential (:51-54).  The
+        C ABI cannot check raw pointers, so the weights' shapes and dtypes are checked here."""
+        w = [map_classifier[0].weight, map_classifier[0].bias, map_classifier[2].weight, map_classifier[2].bias,
+             map_classifier[4].weight]
+        self._check_weights(w)
         n = int(self.plan.workspace_bytes)
         if self.ws is None or self.ws.numel() < n + 256:
             self.ws = torch.empty(n + 256, dtype=torch.uint8, device=device)
         base = self.ws.data_ptr()
         self._base = base + (-base) % 256  # the ABI wants a 256-B aligned workspace
-        w = [map_classifier[0].weight, map_classifier[0].bias, map_classifier[2].weight, map_classifier[2].bias,
-             map_classifier[4].weight]
-        self._keep = tuple(t.detach().contiguous() for t in w)  # b2 / w3 are read again per frame
-        _require_cuda(*self._keep)
-        st = _native.load().mvbev_bev_fuse_prepare(ctypes.byref(self.plan), *[t.data_ptr() for t in self._keep],
+        self._keep = tuple(None if t is None else t.detach().contiguous() for t in w)  # b2 / w3 read per frame
+        _require_cuda(*[t for t in self._keep if t is not None])
+        st = _native.load().mvbev_bev_fuse_prepare(ctypes.byref(self.plan),
+                                                   *[None if t is None else t.data_ptr() for t in self._keep],
                                                    self._base, n, _stream(self.ws))
         _native.check(st, "mvbev_bev_fuse_prepare")
+        self._device = self.ws.device
 
     def __call__(self, views, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """One frame: ``views[v]`` per ``src_kind`` (fp32 / fp16 [B,C,H,W], or fp32 backbone maps
+        [B,C,h,w]).  Every shape, dtype and device is checked here: the kernels behind the C ABI
+        trust the plan's geometry, so a mismatched tensor would be read or written out of bounds."""
         g = self.plan.g
+        if not self.plan.prepared:
+            raise RuntimeError("BevFuse.prepare(map_classifier, device) must run before the first frame")
         if len(views) != g.num_views:
             raise ValueError(f"need {g.num_views} views")
+        backbone = g.src_kind == _native.BEV_SRC_BACKBONE_F32
+        shape = (g.B, g.C, g.h, g.w) if backbone else (g.B, g.C, g.H, g.W)
+        dtype = torch.float16 if g.src_kind == _native.BEV_SRC_F16 else torch.float32
+        for i, v in enumerate(views):
+            if not isinstance(v, torch.Tensor) or tuple(v.shape) != shape or v.dtype != dtype:
+                got = (tuple(v.shape), v.dtype) if isinstance(v, torch.Tensor) else type(v)
+                raise ValueError(f"view {i} must be {dtype} {list(shape)}, got {got}")
         views = [v.contiguous() for v in views]
         _require_cuda(*views)
+        if any(v.device != self._device for v in views):
+            raise ValueError(f"every view must be on {self._device} (the workspace's device)")
         if out is None:
             out = torch.empty((g.B, 1, g.Ho, g.Wo), dtype=torch.float32, device=views[0].device)
+        elif (tuple(out.shape) != (g.B, 1, g.Ho, g.Wo) or out.dtype != torch.float32 or not out.is_contiguous()
+              or not out.is_cuda or out.device != self._device):
+            raise ValueError(f"out must be a contiguous float32 [{g.B}, 1, {g.Ho}, {g.Wo}] tensor on {self._device}")
         arr = (ctypes.c_void_p * g.num_views)(*[v.data_ptr() for v in views])
         st = _native.load().mvbev_bev_fuse(ctypes.byref(self.plan), arr, out.data_ptr(), self._base,
                                            int(self.plan.workspace_bytes), _stream(out))

@@ -72,6 +72,13 @@ class Workspace:
     # grid rows the slab holds: (0, Ho) for a warped slab; a row window for a band-local slab
     # filled by the multi-GPU band exchange (parallel.ViewBands)
     slab_rows: Tuple[int, int] = (0, 0)
+    # the non-finite guard (ProjectFuse.nonfinite_guard): the fused warp stores nf_tag into nf[0] when
+    # it samples a NaN / inf feature; guard_src = (cams, feats, up_hw) of that warp, for the exact path
+    nf: Optional[torch.Tensor] = None
+    nf_tag: int = 0
+    guard_src: Optional[tuple] = None
+    g_slab: Optional[torch.Tensor] = None   # the exact path's fp32 slab [S, B, Cs, Ho, Wo] and y1
+    g_y1: Optional[torch.Tensor] = None
 
 
 class ProjectFuse:
@@ -86,7 +93,7 @@ class ProjectFuse:
                  precision: str = "bf16x3", slab_dtype: torch.dtype = torch.float32,
                  all_views: bool = True, split_k: bool = True, frustum: bool = True, fuse_conv3: bool = True,
                  edge_strip: bool = True, wino_conv1: bool = True, wino_warp: bool = True,
-                 wino_conv2: bool = True):
+                 wino_conv2: bool = True, nonfinite_guard: bool = True):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":
@@ -163,6 +170,17 @@ class ProjectFuse:
         # condition as conv1 (a NaN in y1 would spread over a 3-row tile)
         self.wino_conv2 = wino_conv2 and precision == "bf16x3" and self.y1_split
         self.pack2w = ops.PackedConv3x3(None, "bf16x3", wino=True) if self.wino_conv2 else None
+        # nonfinite_guard (default): NaN / inf in the FEATURES (a diverging backbone, fp16 overflow
+        # upstream).  The fused warp folds B^T (and the upsample's taps) before any product, so such a
+        # value would not keep the reference's NaN / inf pattern (and the 3xbf16 split turns inf into
+        # NaN).  The fused warp reports it into a device flag; after the fast path the exact path is
+        # enqueued — the reference-order warp (+ upsample) into an fp32 slab, the fp32-MFMA conv1 /
+        # conv2 (exact products: inf * w stays inf, torch's NaN-preserving ReLU) and conv3 — every
+        # launch gated on the flag, so with finite features they exit at once and nothing is synced.
+        self.nonfinite_guard = nonfinite_guard
+        self._pack1f: Optional[ops.PackedConv3x3] = None
+        self._pack2f: Optional[ops.PackedConv3x3] = None
+        self._chan_map = chan_map
 
     # -- buffers ----------------------------------------------------------------------------
     def workspace(self, B: int, device, band: Optional[Tuple[int, int]] = None,
@@ -279,9 +297,17 @@ class ProjectFuse:
         need = ops.wino_rows_bytes(self._conv1_desc(B))
         if ws.wino_t is None or ws.wino_t.numel() * 2 < need:
             ws.wino_t = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=ws.slab.device)
+        nonfinite = None
+        ws.guard_src = None
+        if self.nonfinite_guard:
+            if ws.nf is None:
+                ws.nf = torch.zeros(1, dtype=torch.int32, device=ws.slab.device)
+            ws.nf_tag = ws.nf_tag % 0x7FFFFFFE + 1  # a fresh tag per frame: no reset of the flag needed
+            nonfinite = (ws.nf, ws.nf_tag)
+            ws.guard_src = (list(cams), list(feats), up_hw)
         ops.warp_views_wino_rows_into(list(feats), [self.m_norm_cpu[c] for c in cams], ws.wino_t,
                                       [self.slot_of[c] for c in cams], self.Cs, self.S * self.Cs, H, W,
-                                      dst_zeroed=True, up_hw=up_hw)
+                                      dst_zeroed=True, up_hw=up_hw, nonfinite=nonfinite)
         ws.t_from_warp = True
 
     def warp_views(self, ws: Workspace, cams: Sequence[int], feats: Sequence[torch.Tensor]) -> None:
@@ -580,12 +606,44 @@ class ProjectFuse:
             self.conv2_partials(ws, map_classifier[2], map_classifier[4])
             if mark:
                 mark("conv3")
-            return self.conv3_from_partials(ws, map_classifier[4])
+            out = self.conv3_from_partials(ws, map_classifier[4])
+            if ws.t_from_warp and ws.guard_src is not None:
+                if mark:
+                    mark("guard")
+                self._nonfinite_exact(ws, map_classifier, out)
+            return out
         for stage, idx, fn in (("conv1", 0, self.conv1), ("conv2", 2, self.conv2), ("conv3", 4, self.conv3)):
             if mark:
                 mark(stage)
             out = fn(ws, map_classifier[idx])
         return out
+
+    def _nonfinite_exact(self, ws: Workspace, map_classifier, out: torch.Tensor) -> None:
+        """The non-finite guard's exact path (``nonfinite_guard``), every launch gated on the fused
+        warp's report ``(ws.nf, ws.nf_tag)``: the reference-order warp (+ upsample) of the same
+        features into an fp32 slab (``:65-69``), the fp32-MFMA conv1 + coord term + ReLU (``:51``), conv2
+        + ReLU (``:53``) and conv3 (``:54``) into ``out`` — the map the fast path just wrote."""
+        cams, feats, up_hw = ws.guard_src
+        H, W = self.grid_hw
+        B, dev = ws.slab.shape[1], ws.slab.device
+        if ws.g_slab is None:
+            ws.g_slab = torch.zeros((self.S, B, self.Cs, H, W), dtype=torch.float32, device=dev)
+            ws.g_y1 = torch.empty((B, self.mid, H, W), dtype=torch.float32, device=dev)
+        if self._pack1f is None:
+            self._pack1f = ops.PackedConv3x3(self._chan_map, "fp32")
+            self._pack2f = ops.PackedConv3x3(None, "fp32")
+        gate = (ws.nf, ws.nf_tag)
+        c1, c2, c3 = map_classifier[0], map_classifier[2], map_classifier[4]
+        ops.warp_views_exact_into(list(feats), [self.m_norm_cpu[c] for c in cams],
+                                  [ws.g_slab[self.slot_of[c], :, :self.C] for c in cams], up_hw=up_hw, gate=gate)
+        d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * H * W,
+                           batch_stride=self.Cs * H * W)
+        ops.conv3x3_desc(ws.g_slab, d1, self._pack1f.get(c1.weight), self.mid, init=self.coord_term(c1), dilation=1,
+                         relu=True, out=ws.g_y1, gate=gate)
+        d2 = ops.conv_desc(B, self.mid, H, W, group=self.mid, group_stride=0, batch_stride=self.mid * H * W)
+        ops.conv3x3_desc(ws.g_y1, d2, self._pack2f.get(c2.weight), self.mid, bias=c2.bias, dilation=2, relu=True,
+                         out=ws.y2, gate=gate)
+        ops.conv3x3_cout1(ws.y2, c3.weight, 4, H=H, out=out, gate=gate)
 
     def project_fuse(self, feats: Sequence[torch.Tensor], map_classifier) -> torch.Tensor:
         """Whole hot path on one device: warp every view, concat (zero-copy), fuse."""

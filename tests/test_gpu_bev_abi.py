@@ -140,3 +140,57 @@ def test_bev_fuse_refusals():
                                       base, 16, None) == _native.ERR_SHAPE
     assert lib.mvbev_bev_fuse_prepare(ctypes.byref(bev.plan), w.data_ptr(), None, w.data_ptr(), None, w.data_ptr(),
                                       base + 4, int(bev.plan.workspace_bytes), None) == -4  # MVBEV_ERR_ALIGN
+
+
+def test_bev_fuse_wrapper_refuses_mismatched_views_and_out():
+    """The Python wrapper checks every view and ``out`` against the plan (the kernels behind the raw
+    pointers cannot): wrong shape, dtype, device placement or out layout raise before a launch."""
+    from mvdet_amd import ops, synthetic
+    ds = synthetic.wildtrack_like(2, 4, seed=2, img_shape=(216, 384), worldgrid_shape=(96, 288))
+    C = 16
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    pm, mc, tp = _setup(ds, C, seed=2)
+    bev = ops.BevFuse(_engine_mats(pm, up, grid), C, up, grid)
+    bev.prepare(mc, DEV)
+    good = [torch.zeros((1, C) + up, device=DEV) for _ in range(2)]
+    with pytest.raises(ValueError, match="view 1"):
+        bev([good[0], torch.zeros((1, C, up[0], up[1] - 1), device=DEV)])
+    with pytest.raises(ValueError, match="view 0"):
+        bev([good[0].half(), good[1]])
+    with pytest.raises(ValueError, match="out"):
+        bev(good, out=torch.empty((1, 1, grid[0], grid[1] + 1), device=DEV))
+    with pytest.raises(ValueError, match="out"):
+        bev(good, out=torch.empty((1, 1) + grid, device=DEV, dtype=torch.float64))
+    with pytest.raises(RuntimeError):
+        bev([good[0].cpu(), good[1]])
+    assert torch.isfinite(bev(good)).all()
+
+
+def test_bev_fuse_nonfinite_features_guard():
+    """The one-call ABI's non-finite guard (plan.guard): +inf and NaN injected into backbone-resolution
+    features; the fused warp reports them and the gated exact path gives the oracle's NaN / inf pattern;
+    a finite frame through the same workspace afterwards is the fast path's map."""
+    from mvdet_amd import _native, ops, synthetic
+    ds = synthetic.wildtrack_like(3, 4, seed=5, img_shape=(216, 384), worldgrid_shape=(96, 288))
+    C, N = 64, 3
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    lo = [u // 3 for u in up]
+    pm, mc, tp = _setup(ds, C, seed=9)
+    bev = ops.BevFuse(_engine_mats(pm, up, grid), C, up, grid, src_kind=_native.BEV_SRC_BACKBONE_F32, backbone_hw=lo)
+    bev.prepare(mc, DEV)
+    assert bev.wino and bev.plan.guard
+    low = [synthetic.backbone_features(1, C, lo, seed=20 + v, device=DEV) for v in range(N)]
+    bad = [f.clone() for f in low]
+    bad[0][0, 9, lo[0] // 2, lo[1] // 2] = float("inf")
+    bad[2][0, 4, lo[0] // 2 - 3, lo[1] // 2 + 4] = float("nan")
+    mats = [M.numpy() for M in pm]
+    with torch.no_grad():
+        got = bev(bad).clone()
+        fine = bev(low).clone()
+        torch.cuda.synchronize()
+        ref = cpu_path.project_fuse([cpu_path.upsample(f.cpu(), up) for f in bad], mats, grid, tp)
+        ref_fine = cpu_path.project_fuse([cpu_path.upsample(f.cpu(), up) for f in low], mats, grid, tp)
+    assert 0 < int((~torch.isfinite(ref)).sum()) < ref.numel()
+    assert_parity_t(got, ref, "bev_fuse non-finite features (NaN / inf pattern included)")
+    assert torch.isfinite(fine).all()
+    assert_parity_t(fine, ref_fine, "bev_fuse finite frame after a non-finite one", normwise_tol=5e-5)

@@ -1,0 +1,137 @@
+"""NaN / inf in the features (a diverging backbone, an fp16 overflow upstream): the map's NaN / inf
+pattern must be the reference's (``persp_trans_detector.py:65-82``: F.interpolate, the kornia warp,
+torch.cat and three nn.Conv2d with ReLU, on the CPU oracle).
+
+The fast path folds the upsample's taps into one 3x3 window and B^T into the rows before any
+product, so it cannot keep that pattern; the fused warp reports a non-finite sample into a device
+flag and the engine's exact path (``ProjectFuse._nonfinite_exact``: the reference-order warp (+
+upsample), fp32-MFMA conv1 / conv2, conv3 — every launch gated on the flag, no host sync) rewrites
+the map.  Each case checks that the oracle's map is partly non-finite (the case discriminates),
+that the flag fired, and the parity gate with the NaN and non-finite patterns equal
+(``helpers.parity_stats_t``)."""
+import pytest
+import torch
+import torch.nn as nn
+
+from helpers import assert_parity_t
+from oracle import cpu_path, fixtures
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _rig(C, N=3, seed=0):
+    from mvdet_amd import synthetic
+    ds = synthetic.wildtrack_like(N, 4, seed=seed, img_shape=(216, 384), worldgrid_shape=(96, 288))
+    params = fixtures.head_params(N, seed=11, C=C)
+    return ds, params
+
+
+def _poison(low, hb):
+    """+inf, -inf and NaN at backbone pixels near each view's image centre (sampled by the warp)."""
+    h, w = hb
+    low[0][0, 3, h // 2, w // 2] = float("inf")
+    low[1][0, 7, h // 2 + 3, w // 2 - 5] = float("nan")
+    low[2][0, 1, h // 2 - 4, w // 2 + 6] = float("-inf")
+    return low
+
+
+def _mc(C, N, params):
+    mc = nn.Sequential(nn.Conv2d(C * N + 2, 512, 3, padding=1), nn.ReLU(),
+                       nn.Conv2d(512, 512, 3, padding=2, dilation=2), nn.ReLU(),
+                       nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False))
+    mc.load_state_dict({k.replace("map_classifier.", ""): torch.from_numpy(v) for k, v in params.items()
+                        if k.startswith("map_classifier.")})
+    return mc.to(DEV)
+
+
+def _check_discriminates(ref):
+    nf = ~torch.isfinite(ref)
+    assert 0 < int(nf.sum()) < ref.numel(), "the oracle map should be partly non-finite"
+    assert int(torch.isnan(ref).sum()) > 0
+
+
+@pytest.mark.parametrize("C", [64, 512])
+def test_nonfinite_features_through_the_detector(C):
+    """The drop-in module's default inference path (backbone-resolution maps -> fused upsample + warp
+    + B^T -> Winograd convs) with +inf / NaN / -inf injected into the backbone features: map_result
+    and imgs_result with the reference's NaN / inf pattern."""
+    from mvdet_amd import PerspTransDetector, synthetic
+    from mvdet_amd.geometry import projection_matrices
+    ds, params = _rig(C)
+    N, B = ds.num_cam, 1
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    hb = [u // 3 for u in up]
+    model = PerspTransDetector(ds)
+    sd = model.state_dict() if C == 512 else None
+    if C != 512:  # a narrower backbone output: build the module's heads for C channels
+        model.map_classifier = _mc(C, N, params)
+        model.img_classifier = nn.Sequential(nn.Conv2d(C, 64, 1), nn.ReLU(), nn.Conv2d(64, 2, 1, bias=False)).to(DEV)
+        from mvdet_amd import ProjectFuse
+        model.engine = ProjectFuse(model.proj_mats, up, grid, C)
+    else:
+        sd.update({k: torch.from_numpy(v) for k, v in params.items()})
+        model.load_state_dict(sd)
+        model.map_classifier = model.map_classifier.to(DEV)
+    model.base_pt1, model.base_pt2 = nn.Identity(), nn.Identity()
+    model.eval()
+    low = [synthetic.backbone_features(B, C, hb, seed=300 + v, device=DEV) for v in range(N)]
+    low = _poison(low, hb)
+    eng = model.engine
+    with torch.no_grad():
+        map_res, imgs_res = model(torch.stack(low, 1))
+        ws = eng.workspace(B, DEV)
+        assert ws.t_from_warp and eng.wino_active(DEV)
+        assert int(ws.nf.item()) == ws.nf_tag, "the fused warp did not report the non-finite features"
+        torch.cuda.synchronize()
+        ups = [cpu_path.upsample(f.cpu(), up) for f in low]
+        ref = cpu_path.project_fuse(ups, [M.numpy() for M in projection_matrices(ds)], grid,
+                                    {k: torch.from_numpy(v) for k, v in params.items()})
+        head = model.img_classifier.cpu()
+        ref_imgs = [head(u) for u in ups]
+    _check_discriminates(ref)
+    assert_parity_t(map_res, ref, f"C={C} non-finite features: map_result (NaN / inf pattern included)")
+    for v in range(N):
+        assert_parity_t(imgs_res[v], ref_imgs[v], f"C={C} non-finite features: imgs_result {v}")
+
+
+def test_nonfinite_features_through_the_engine_from_upsampled_maps():
+    """The bench's path (upsampled features -> fused warp + B^T -> Winograd convs) with non-finite
+    features, then the same engine on finite features again (the flag of the previous frame must
+    not trigger the exact path: a fresh tag per frame)."""
+    from mvdet_amd import ProjectFuse, synthetic
+    from mvdet_amd.geometry import projection_matrices
+    C = 64
+    ds, params = _rig(C, seed=3)
+    N, B = ds.num_cam, 1
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    hb = [u // 3 for u in up]
+    pm = projection_matrices(ds)
+    mc = _mc(C, N, params)
+    tp = {k: torch.from_numpy(v) for k, v in params.items()}
+    eng = ProjectFuse(pm, up, grid, C)
+    feats = [synthetic.synthetic_features(B, C, hb, up, seed=500 + v, device=DEV) for v in range(N)]
+    bad = [f.clone() for f in feats]
+    bad[1][0, 2, up[0] // 2, up[1] // 2] = float("inf")
+    bad[2][0, 5, up[0] // 2 + 7, up[1] // 2 - 9] = float("nan")
+    with torch.no_grad():
+        got = eng.project_fuse(bad, mc).clone()
+        ws = eng.workspace(B, DEV)
+        assert int(ws.nf.item()) == ws.nf_tag
+        ref = cpu_path.project_fuse([f.cpu() for f in bad], [M.numpy() for M in pm], grid, tp)
+        _check_discriminates(ref)
+        assert_parity_t(got, ref, "engine, non-finite upsampled features (NaN / inf pattern included)")
+        # the next frame is finite: no exact path, the fast path's map
+        got2 = eng.project_fuse(feats, mc).clone()
+        assert int(ws.nf.item()) != ws.nf_tag
+        ref2 = cpu_path.project_fuse([f.cpu() for f in feats], [M.numpy() for M in pm], grid, tp)
+        assert torch.isfinite(got2).all()
+        assert_parity_t(got2, ref2, "engine, finite frame after a non-finite one", normwise_tol=5e-5)
+        # without the guard the fast path's pattern is not the reference's (the case the guard exists for)
+        eng.nonfinite_guard = False
+        try:
+            fast = eng.project_fuse(bad, mc).clone()
+        finally:
+            eng.nonfinite_guard = True
+        torch.cuda.synchronize()
+    assert not torch.equal(torch.isnan(fast.cpu()), torch.isnan(ref))

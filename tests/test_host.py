@@ -30,7 +30,7 @@ def test_library_exports_every_header_symbol():
     assert declared == sorted(_native.EXPORTS)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.mvbev_version() == 11500
+    assert lib.mvbev_version() == 11600
     assert lib.mvbev_status_string(0) == b"ok"
     assert lib.mvbev_status_string(-100) == b"HIP launch failed"
 
@@ -44,16 +44,16 @@ def test_argument_validation_codes():
     bad = _native._i64x4(1, 1, 1, 2)
     assert lib.mvbev_warp_perspective_f32(p, 1, 1, 1, 1, s4, p, p, 1, 1, bad, None) == -3
     d = _native.ConvDesc(1, 8, 4, 4, 8, 0, 128, 0, 4, 0, 4)
-    assert lib.mvbev_conv3x3_f32(p, ctypes.byref(d), p, None, None, 100, 1, 1, p, None) == -2  # Cout % 128
-    assert lib.mvbev_conv3x3_f32(p, ctypes.byref(d), p, None, None, 128, 3, 1, p, None) == -6  # dilation 3
-    assert lib.mvbev_conv3x3_f32(p, ctypes.byref(d), ctypes.c_void_p(20), None, None, 128, 1, 1, p, None) == -4
+    assert lib.mvbev_conv3x3_f32(p, ctypes.byref(d), p, None, None, 100, 1, 1, p, None, 0, None) == -2  # Cout % 128
+    assert lib.mvbev_conv3x3_f32(p, ctypes.byref(d), p, None, None, 128, 3, 1, p, None, 0, None) == -6  # dilation 3
+    assert lib.mvbev_conv3x3_f32(p, ctypes.byref(d), ctypes.c_void_p(20), None, None, 128, 1, 1, p, None, 0, None) == -4
     bad = _native.ConvDesc(1, 12, 4, 4, 12, 0, 192, 0, 4, 0, 4)  # K not a multiple of 8
-    assert lib.mvbev_conv3x3_f32(p, ctypes.byref(bad), p, None, None, 128, 1, 1, p, None) == -2
+    assert lib.mvbev_conv3x3_f32(p, ctypes.byref(bad), p, None, None, 128, 1, 1, p, None, 0, None) == -2
     band = _native.ConvDesc(1, 8, 4, 4, 8, 0, 128, 0, 4, 2, 3)  # out rows 2..5 > H
-    assert lib.mvbev_conv3x3_f32(p, ctypes.byref(band), p, None, None, 128, 1, 1, p, None) == -2
-    assert lib.mvbev_conv3x3_f32(p, None, p, None, None, 128, 1, 1, p, None) == -5
-    assert lib.mvbev_conv3x3_cout1_f32(p, 1, 8, 4, 4, 0, 4, 0, 4, p, 3, p, None) == -6
-    assert lib.mvbev_conv3x3_cout1_f32(p, 1, 8, 4, 4, 0, 4, 3, 4, p, 4, p, None) == -2
+    assert lib.mvbev_conv3x3_f32(p, ctypes.byref(band), p, None, None, 128, 1, 1, p, None, 0, None) == -2
+    assert lib.mvbev_conv3x3_f32(p, None, p, None, None, 128, 1, 1, p, None, 0, None) == -5
+    assert lib.mvbev_conv3x3_cout1_f32(p, 1, 8, 4, 4, 0, 4, 0, 4, p, 3, p, None, 0, None) == -6
+    assert lib.mvbev_conv3x3_cout1_f32(p, 1, 8, 4, 4, 0, 4, 3, 4, p, 4, p, None, 0, None) == -2
     assert lib.mvbev_pack_conv3x3_weight_f32(p, 100, 8, None, 8, p, None) == -2
     assert lib.mvbev_pack_conv3x3_weight_f32(p, 128, 8, None, 16, p, None) == -2  # K != Cin without a map
     assert lib.mvbev_conv3x3_packed_floats(512, 3586) == 3592 * 9 * 512
@@ -194,3 +194,24 @@ def test_bench_refuses_a_gpus_world_size_mismatch(gpus, world):
     assert out.returncode != 0
     assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert "--gpus" in out.stderr
+
+
+def test_bev_fuse_wrapper_refuses_mismatched_tensors():
+    """ops.BevFuse is the only guard in front of the one-call C ABI (raw pointers): wrong weight
+    shapes / dtypes and calls before prepare raise before anything is launched."""
+    from mvdet_amd import ops
+    import torch.nn as nn
+    bev = ops.BevFuse([torch.eye(3)] * 2, 16, (20, 30), (10, 12))
+    with pytest.raises(RuntimeError, match="prepare"):
+        bev([torch.zeros(1, 16, 20, 30)] * 2)
+    bad = nn.Sequential(nn.Conv2d(33, 512, 3, padding=1), nn.ReLU(), nn.Conv2d(512, 512, 3, padding=2, dilation=2),
+                        nn.ReLU(), nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False))
+    with pytest.raises(ValueError, match=r"map_classifier\[0\].weight"):
+        bev.prepare(bad, "cpu")
+    bad[0] = nn.Conv2d(34, 512, 3, padding=1)
+    bad[4] = nn.Conv2d(512, 2, 3, padding=4, dilation=4, bias=False)
+    with pytest.raises(ValueError, match=r"map_classifier\[4\].weight"):
+        bev.prepare(bad, "cpu")
+    bad[4] = nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False).double()
+    with pytest.raises(ValueError, match=r"map_classifier\[4\].weight"):
+        bev.prepare(bad, "cpu")

@@ -101,11 +101,8 @@ int mvbev_warp_views_f32(const mvbev_warp_view* views, int nviews, int64_t B, in
  * reads without any conversion: for (batch, group of 8 channels, row, col) 32 bytes = bf16
  * hi[8] then bf16 lo[8], value = hi + lo.  dst_strides are in 32-byte units
  * {batch, channel group, row, col (must be 1)}; channels beyond C in the last group are 0.
- * src is fp32 (src_is_f16 = 0) or fp16. */
-int mvbev_warp_views_split_bf16(const mvbev_warp_view* views, int nviews, int src_is_f16,
-                                int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
-                                void* stream);
-/* flags of the _ex warps.  MVBEV_WARP_DST_ZEROED: the caller guarantees every dst already
+ * src is fp32 (src_is_f16 = 0) or fp16.  (ABI 11600: the flag-less form is retired.)
+ * flags of the _ex warps.  MVBEV_WARP_DST_ZEROED: the caller guarantees every dst already
  * holds zeros wherever the view's sample falls outside the source (e.g. a persistent slab
  * zero-filled at allocation and only ever written by this warp with the same matrices), so
  * those pixels — exactly 0 in the result — are skipped instead of rewritten.  Pixels with
@@ -210,26 +207,23 @@ int mvbev_conv3x3_f32(const float* x, const mvbev_conv_desc* desc, const float* 
 #define MVBEV_LAYOUT_SPLIT_ROWS 3 /* per (channel, row, 8-pixel run): bf16 hi[8], bf16 lo[8]
                                      (W % 8 == 0; the same bytes per row as fp32) */
 
-/* 3xbf16 split-precision variant of mvbev_conv3x3_f32 (same descriptor and semantics):
- * a*b ~= a_hi*b_hi + a_hi*b_lo + a_lo*b_hi on the bf16 MFMA, fp32 accumulation; ~2^-16
- * relative per product (fp32-class; see conv_bf16x3.hip).  x_layout: MVBEV_LAYOUT_*
- * (fp32, the config-4 fp16 slab, or the pre-split slab); y is fp32.
+/* 3xbf16 split-precision variant of mvbev_conv3x3_f32 (mvbev_conv3x3_bf16x3_ex below; same
+ * descriptor and semantics): a*b ~= a_hi*b_hi + a_hi*b_lo + a_lo*b_hi on the bf16 MFMA, fp32
+ * accumulation; ~2^-16 relative per product (fp32-class; see conv_bf16x3.hip).  x_layout:
+ * MVBEV_LAYOUT_* (fp32, the config-4 fp16 slab, or the pre-split slab).
  * Weights packed by mvbev_pack_conv3x3_weight_bf16x3 (bytes: mvbev_conv3x3_packed_bytes_bf16x3). */
 size_t mvbev_conv3x3_packed_bytes_bf16x3(int64_t Cout, int64_t K);
 int mvbev_pack_conv3x3_weight_bf16x3(const float* w, int64_t Cout, int64_t Cin_w,
                                      const int32_t* chan_map, int64_t K, void* w_packed,
                                      void* stream);
-int mvbev_conv3x3_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* desc,
-                         const void* w_packed, const float* bias, const float* init,
-                         int64_t Cout, int dilation, int relu, float* y, void* stream);
-/* Output tile of mvbev_conv3x3_bf16x3 (rows x columns), the granule of group_mask below:
+/* Output tile of mvbev_conv3x3_bf16x3_ex (rows x columns), the granule of group_mask below:
  * MVBEV_CONV_TILE_H rows for fp32/fp16 input; split-bf16 input (the LDS-DMA ring kernel)
  * uses the row count mvbev_conv3x3_bf16x3_tile_rows returns (12). */
 #define MVBEV_CONV_TILE_H 8
 #define MVBEV_CONV_TILE_W 32
 int mvbev_conv3x3_bf16x3_tile_rows(int x_layout, int dilation);
 
-/* Extended form.
+/* The 3xbf16 conv (ABI 11600: the form without mask / order / workspace is retired).
  *   y, y_layout: MVBEV_LAYOUT_F32 ([B][Cout][out_rows][W] fp32, as above) or
  *     MVBEV_LAYOUT_SPLIT_BF16 ([B][Cout/8][out_rows][W] pieces of bf16 hi[8], lo[8]: the
  *     next conv's input without a conversion pass).
@@ -528,17 +522,14 @@ int mvbev_pack_conv3x3_dgrad_bf16x3(const float* w, int64_t Cout_w, int64_t Cin_
  * channels) are skipped where bit g is clear — those dx entries are left unwritten, for a
  * consumer that never reads them (the warp adjoint reads a view's gradient only where the
  * view samples inside its source, which the frustum mask of mvbev_warp_tile_mask bounds). */
-int mvbev_conv3x3_dgrad_bf16x3(const float* dy, const mvbev_conv_desc* desc, const void* w_packed, int64_t Cout_p,
-                               int dilation, void* dx, int dx_layout, const uint32_t* out_mask,
-                               int64_t cot_per_group, void* stream);
-/* Same with dy in dy_layout: MVBEV_LAYOUT_F32 (as above) or MVBEV_LAYOUT_SPLIT_BF16 (the
- * LDS-DMA ring kernel, dilation 1 or 2; its output tiles, and so out_mask's tiles, are
- * mvbev_conv3x3_bf16x3_tile_rows(MVBEV_LAYOUT_SPLIT_BF16, dilation) rows high). */
+/* dy in dy_layout: MVBEV_LAYOUT_F32 or MVBEV_LAYOUT_SPLIT_BF16 (the LDS-DMA ring kernel, dilation 1
+ * or 2; its output tiles, and so out_mask's tiles, are mvbev_conv3x3_bf16x3_tile_rows(
+ * MVBEV_LAYOUT_SPLIT_BF16, dilation) rows high). */
 int mvbev_conv3x3_dgrad_bf16x3_ex(const void* dy, int dy_layout, const mvbev_conv_desc* desc, const void* w_packed,
                                   int64_t Cout_p, int dilation, void* dx, int dx_layout, const uint32_t* out_mask,
                                   int64_t cot_per_group, void* stream);
 
-/* Weight gradient of mvbev_conv3x3_bf16x3 (3xbf16 MFMA, fp32 accumulation):
+/* Weight gradient of mvbev_conv3x3_bf16x3_ex (3xbf16 MFMA, fp32 accumulation):
  *   dw[co][chan_map[k]][t] = sum_b,y,x dy[b][co][y][x] * x[b][k][y + (t/3-1)d][x + (t%3-1)d]
  * x as in the forward (desc: whole image, in_row0 = out_row0 = 0, in_rows = out_rows = H;
  * x_layout MVBEV_LAYOUT_F32 or MVBEV_LAYOUT_SPLIT_BF16); dy [B][Cout][H][W] fp32 contiguous,
@@ -547,26 +538,16 @@ int mvbev_conv3x3_dgrad_bf16x3_ex(const void* dy, int dy_layout, const mvbev_con
  * mvbev_conv3x3_wgrad_workspace_bytes() (per-partition partial sums; the reduction over
  * partitions runs in a fixed order, so the result is deterministic). */
 size_t mvbev_conv3x3_wgrad_workspace_bytes(const mvbev_conv_desc* desc, int64_t Cout);
-int mvbev_conv3x3_wgrad_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* desc,
-                               const float* dy, int64_t Cout, int dilation, const int32_t* chan_map,
-                               int64_t Cin_w, float* dw, void* workspace, size_t workspace_bytes,
-                               void* stream);
-
-/* Same, skipping the pixel chunks where an input-channel group (desc->group channels, a
- * multiple of 64: one camera's slot of the fused slab) is exactly zero over the 3x3 window:
- * chunk_list[chunk_off[g] .. chunk_off[g+1]) lists, ascending, the chunks (row segments of 32
- * pixels, index (b * H + y) * ceil(W / 32) + x / 32) where group g can be non-zero (from the
- * frustum mask of mvbev_warp_tile_mask with halo >= dilation).  Device int32 arrays. */
-int mvbev_conv3x3_wgrad_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_desc* desc,
-                                  const float* dy, int64_t Cout, int dilation, const int32_t* chan_map,
-                                  int64_t Cin_w, float* dw, const int32_t* chunk_list,
-                                  const int32_t* chunk_off, void* workspace, size_t workspace_bytes,
-                                  void* stream);
-
-/* The same with dy in dy_layout: MVBEV_LAYOUT_F32 (as _ex) or MVBEV_LAYOUT_SPLIT_ROWS (dy
- * pre-split by mvbev_split_rows_bf16; the LDS-DMA wgrad path only: split-bf16 x, dilation 1 or
- * 2, W % 8 == 0, else MVBEV_ERR_SHAPE).  Bitwise the same dw as from the fp32 dy (the kernel
- * splits an fp32 dy with the same rounding), without the per-segment split pass. */
+/* Optional chunk lists (both NULL = every chunk): skip the pixel chunks where an input-channel
+ * group (desc->group channels, a multiple of 64: one camera's slot of the fused slab) is exactly
+ * zero over the 3x3 window: chunk_list[chunk_off[g] .. chunk_off[g+1]) lists, ascending, the chunks
+ * (row segments of 32 pixels, index (b * H + y) * ceil(W / 32) + x / 32) where group g can be
+ * non-zero (from the frustum mask of mvbev_warp_tile_mask with halo >= dilation).  Device int32.
+ * dy in dy_layout: MVBEV_LAYOUT_F32 or MVBEV_LAYOUT_SPLIT_ROWS (dy pre-split by
+ * mvbev_split_rows_bf16; the LDS-DMA wgrad path only: split-bf16 x, dilation 1 or 2, W % 8 == 0,
+ * else MVBEV_ERR_SHAPE) — bitwise the same dw as from the fp32 dy (the kernel splits an fp32 dy
+ * with the same rounding), without the per-segment split pass.  (ABI 11600: the forms without
+ * chunk lists / dy layout are retired.) */
 int mvbev_conv3x3_wgrad_bf16x3_ex2(const void* x, int x_layout, const mvbev_conv_desc* desc,
                                    const void* dy, int dy_layout, int64_t Cout, int dilation,
                                    const int32_t* chan_map, int64_t Cin_w, float* dw,
@@ -596,12 +577,9 @@ int mvbev_relu_backward_split_f32(float* dy, const void* y_split, int64_t B, int
 /* Backward of mvbev_conv3x3_cout1_f32 over a whole image (x [B][C][H][W], w [C][3][3], dmap
  * [B][1][H][W] fp32):  dx[b][c][p] = sum_t w[c][t] dmap[b][p - s_t], zeroed where x <= 0 when
  * relu_mask (x is the previous ReLU's output: its backward fused); dw[c][t] = sum_b,p
- * dmap[b][p] x[b][c][p + s_t].  Either output may be NULL. */
-int mvbev_conv3x3_cout1_backward_f32(const float* x, const float* w, const float* dmap, int64_t B,
-                                     int64_t C, int64_t H, int64_t W, int dilation, int relu_mask,
-                                     float* dx, float* dw, void* stream);
-/* Same, with dx_split (optional, C % 8 == 0, 16-B aligned): dx also in the split-bf16 layout
- * ([B][C/8][H][W] pieces of bf16 hi[8], lo[8]), the input of the next data-gradient conv. */
+ * dmap[b][p] x[b][c][p + s_t].  Any output may be NULL; dx_split (C % 8 == 0, 16-B aligned): dx
+ * also in the split-bf16 layout ([B][C/8][H][W] pieces of bf16 hi[8], lo[8]), the input of the
+ * next data-gradient conv. */
 int mvbev_conv3x3_cout1_backward_ex(const float* x, const float* w, const float* dmap, int64_t B, int64_t C,
                                     int64_t H, int64_t W, int dilation, int relu_mask, float* dx, void* dx_split,
                                     float* dw, void* stream);

@@ -20,7 +20,6 @@ EXPORTS = (
     "mvbev_warp_perspective_f16",
     "mvbev_warp_views_f32",
     "mvbev_warp_views_f16",
-    "mvbev_warp_views_split_bf16",
     "mvbev_warp_views_upsampled",
     "mvbev_fill_coord_map_f32",
     "mvbev_conv3x3_packed_floats",
@@ -29,7 +28,6 @@ EXPORTS = (
     "mvbev_conv3x3_cout1_f32",
     "mvbev_conv3x3_packed_bytes_bf16x3",
     "mvbev_pack_conv3x3_weight_bf16x3",
-    "mvbev_conv3x3_bf16x3",
     "mvbev_conv3x3_bf16x3_workspace_bytes",
     "mvbev_conv3x3_bf16x3_ex",
     "mvbev_warp_tile_mask",
@@ -39,13 +37,9 @@ EXPORTS = (
     "mvbev_warp_views_backward_f32",
     "mvbev_pack_conv3x3_dgrad_bf16x3",
     "mvbev_conv3x3_wgrad_workspace_bytes",
-    "mvbev_conv3x3_wgrad_bf16x3",
     "mvbev_conv3x3_bias_coord_grad_f32",
     "mvbev_relu_backward_f32",
-    "mvbev_conv3x3_cout1_backward_f32",
     "mvbev_warp_adjoint_plan",
-    "mvbev_conv3x3_dgrad_bf16x3",
-    "mvbev_conv3x3_wgrad_bf16x3_ex",
     "mvbev_warp_views_adjoint",
     "mvbev_conv3x3_bf16x3_tile_rows",
     "mvbev_warp_views_split_bf16_ex",
@@ -156,9 +150,6 @@ def _declare(lib):
         fn = getattr(lib, name)
         fn.restype = ctypes.c_int
         fn.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64, _i64, _p]
-    lib.mvbev_warp_views_split_bf16.restype = ctypes.c_int
-    lib.mvbev_warp_views_split_bf16.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, ctypes.c_int, _i64, _i64,
-                                                _i64, _i64, _i64, _i64, _p]
     lib.mvbev_warp_views_upsampled.restype = ctypes.c_int
     lib.mvbev_warp_views_upsampled.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, ctypes.c_int, _i64, _i64,
                                                _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_int, _p]
@@ -175,9 +166,6 @@ def _declare(lib):
     lib.mvbev_conv3x3_packed_bytes_bf16x3.argtypes = [_i64, _i64]
     lib.mvbev_pack_conv3x3_weight_bf16x3.restype = ctypes.c_int
     lib.mvbev_pack_conv3x3_weight_bf16x3.argtypes = [_p, _i64, _i64, _p, _i64, _p, _p]
-    lib.mvbev_conv3x3_bf16x3.restype = ctypes.c_int
-    lib.mvbev_conv3x3_bf16x3.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64,
-                                         ctypes.c_int, ctypes.c_int, _p, _p]
     lib.mvbev_conv3x3_bf16x3_workspace_bytes.restype = ctypes.c_size_t
     lib.mvbev_conv3x3_bf16x3_workspace_bytes.argtypes = [ctypes.POINTER(ConvDesc), _i64]
     lib.mvbev_conv3x3_bf16x3_ex.restype = ctypes.c_int
@@ -246,20 +234,11 @@ def _declare(lib):
     lib.mvbev_pack_conv3x3_dgrad_bf16x3.argtypes = [_p, _i64, _i64, _p, _i64, _p, _p]
     lib.mvbev_conv3x3_wgrad_workspace_bytes.restype = ctypes.c_size_t
     lib.mvbev_conv3x3_wgrad_workspace_bytes.argtypes = [ctypes.POINTER(ConvDesc), _i64]
-    lib.mvbev_conv3x3_wgrad_bf16x3.restype = ctypes.c_int
-    lib.mvbev_conv3x3_wgrad_bf16x3.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _i64, ctypes.c_int,
-                                               _p, _i64, _p, _p, ctypes.c_size_t, _p]
     lib.mvbev_conv3x3_bias_coord_grad_f32.restype = ctypes.c_int
     lib.mvbev_conv3x3_bias_coord_grad_f32.argtypes = [_p, _i64, _i64, _i64, _i64, ctypes.c_int, _p, _p, _i64,
                                                       _i64, _p]
     lib.mvbev_relu_backward_f32.restype = ctypes.c_int
     lib.mvbev_relu_backward_f32.argtypes = [_p, _p, _i64, _p]
-    lib.mvbev_conv3x3_cout1_backward_f32.restype = ctypes.c_int
-    lib.mvbev_conv3x3_cout1_backward_f32.argtypes = [_p, _p, _p, _i64, _i64, _i64, _i64, ctypes.c_int,
-                                                     ctypes.c_int, _p, _p, _p]
-    lib.mvbev_conv3x3_wgrad_bf16x3_ex.restype = ctypes.c_int
-    lib.mvbev_conv3x3_wgrad_bf16x3_ex.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _i64,
-                                                  ctypes.c_int, _p, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]
     lib.mvbev_conv3x3_wgrad_bf16x3_ex2.restype = ctypes.c_int
     lib.mvbev_conv3x3_wgrad_bf16x3_ex2.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, ctypes.c_int,
                                                    _i64, ctypes.c_int, _p, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]
@@ -271,9 +250,6 @@ def _declare(lib):
     lib.mvbev_conv3x3_dgrad_bf16x3_sched.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _i64,
                                                      ctypes.c_int, _p, ctypes.c_int, _p, _i64,
                                                      ctypes.POINTER(ConvSchedule), _p]
-    lib.mvbev_conv3x3_dgrad_bf16x3.restype = ctypes.c_int
-    lib.mvbev_conv3x3_dgrad_bf16x3.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _i64, ctypes.c_int, _p,
-                                               ctypes.c_int, _p, _i64, _p]
     lib.mvbev_warp_adjoint_plan.restype = ctypes.c_int
     lib.mvbev_warp_adjoint_plan.argtypes = [ctypes.POINTER(ctypes.c_float), _i64, _i64, _i64, _i64, _p, _p, _p, _p,
                                             _p]
@@ -287,8 +263,8 @@ def _declare(lib):
     lib.mvbev_conv3x3_cout1_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p,
                                             ctypes.c_int, _p, _p, ctypes.c_int32, _p]
     lib.mvbev_warp_views_split_bf16_ex.restype = ctypes.c_int
-    lib.mvbev_warp_views_split_bf16_ex.argtypes = (lib.mvbev_warp_views_split_bf16.argtypes[:-1] +
-                                                   [ctypes.c_int, _p])
+    lib.mvbev_warp_views_split_bf16_ex.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, ctypes.c_int, _i64, _i64,
+                                                   _i64, _i64, _i64, _i64, ctypes.c_int, _p]
     lib.mvbev_warp_views_upsampled_ex.restype = ctypes.c_int
     lib.mvbev_warp_views_upsampled_ex.argtypes = (lib.mvbev_warp_views_upsampled.argtypes[:-1] +
                                                   [ctypes.c_int, _p])

@@ -357,11 +357,6 @@ constexpr std::integer_sequence<int, (B + U)...> offset_seq(std::integer_sequenc
   return {};
 }
 
-#ifndef MVBEV_WGRAD_ABL
-#define MVBEV_WGRAD_ABL 0  // timing ablations only (wrong results): bit 0 no chunk barrier, bit 1 no
-                           // DMA, bit 2 no fragment reads / MFMAs, bit 3 no partial-sum store, bit 4
-                           // x window sources contiguous from the chunk origin
-#endif
 template <int DIL>
 __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
   static_assert(NWV == 8, "wave layout: 4 output blocks x 2 channel halves");
@@ -447,7 +442,7 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
     } else {
       constexpr int jb = j - NA;
       const bool ok = (unsigned)(c.y + bdy[jb]) < (unsigned)H && (unsigned)(c.x0 + bdx[jb]) < (unsigned)W;
-      const u32x4* bsrc = (MVBEV_WGRAD_ABL & 16) ? c.bbase + ((jb * DMAW + wave) * 64 + lane) : c.bbase + bofs[jb];
+      const u32x4* bsrc = c.bbase + bofs[jb];
       wg_glds16(ok ? (const void*)bsrc : (const void*)g_wg_zero, c.dst + WG_AENT + jb * DT);
     }
   };
@@ -572,20 +567,18 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
                      :
                      : "memory");
       }
-      if (!(MVBEV_WGRAD_ABL & 1)) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       // (measured no faster: the pieces one after each of the first steps' MFMAs, 2.30 ms both)
-      if (!(MVBEV_WGRAD_ABL & 2) && i + 2 < n) issue(cids[i + 2], (i + 2) % 3);
+      if (i + 2 < n) issue(cids[i + 2], (i + 2) % 3);
       const bool full = (cids[i] & 4095) * PX + 16 < W;
-      if (!(MVBEV_WGRAD_ABL & 4)) {
-        head_reads(i % 3);
-        body(full);
-      }
+      head_reads(i % 3);
+      body(full);
     }
   }
 
   const int k = kt * NT + 32 * cb + l32;
-  if (!(MVBEV_WGRAD_ABL & 8) && k < a.K) {
+  if (k < a.K) {
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -1325,21 +1318,6 @@ size_t mvbev_conv3x3_wgrad_workspace_bytes(const mvbev_conv_desc* desc, int64_t 
   return (size_t)g.P * 9 * (size_t)Cout * (size_t)desc->K * sizeof(float);
 }
 
-int mvbev_conv3x3_wgrad_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* d, const float* dy,
-                               int64_t Cout, int dilation, const int32_t* chan_map, int64_t Cin_w,
-                               float* dw, void* workspace, size_t workspace_bytes, void* stream) {
-  return mvbev_conv3x3_wgrad_bf16x3_ex(x, x_layout, d, dy, Cout, dilation, chan_map, Cin_w, dw, nullptr, nullptr,
-                                       workspace, workspace_bytes, stream);
-}
-
-int mvbev_conv3x3_wgrad_bf16x3_ex(const void* x, int x_layout, const mvbev_conv_desc* d, const float* dy,
-                                  int64_t Cout, int dilation, const int32_t* chan_map, int64_t Cin_w,
-                                  float* dw, const int32_t* chunk_list, const int32_t* chunk_off,
-                                  void* workspace, size_t workspace_bytes, void* stream) {
-  return mvbev_conv3x3_wgrad_bf16x3_ex2(x, x_layout, d, dy, MVBEV_LAYOUT_F32, Cout, dilation, chan_map, Cin_w, dw,
-                                        chunk_list, chunk_off, workspace, workspace_bytes, stream);
-}
-
 int mvbev_split_rows_bf16(const float* x, int64_t rows, int64_t W, void* out, void* stream) {
   using namespace mvbev;
   if (!x || !out) return MVBEV_ERR_NULL;
@@ -1457,12 +1435,6 @@ int mvbev_relu_backward_split_f32(float* dy, const void* y_split, int64_t B, int
                      static_cast<u32x4_t*>(dy_split));
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
-}
-
-int mvbev_conv3x3_cout1_backward_f32(const float* x, const float* w, const float* dmap, int64_t B, int64_t C,
-                                     int64_t H, int64_t W, int dilation, int relu_mask, float* dx, float* dw,
-                                     void* stream) {
-  return mvbev_conv3x3_cout1_backward_ex(x, w, dmap, B, C, H, W, dilation, relu_mask, dx, nullptr, dw, stream);
 }
 
 int mvbev_conv3x3_cout1_backward_ex(const float* x, const float* w, const float* dmap, int64_t B, int64_t C,

@@ -626,26 +626,9 @@ __device__ inline void glds16(const u32x4* src, u32x4* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, AUX);
 }
-#ifndef MVBEV_RING_XAUX
-#define MVBEV_RING_XAUX 0  // cache policy of the halo DMAs (2 = nt: streamed slab, keep the weights in L2)
-#endif
-
-#ifndef MVBEV_RING_PRIO
-#define MVBEV_RING_PRIO 0  // raise the wave priority over each unit's MFMA stream
-#endif
-#ifndef MVBEV_RING_DMAIL
-#define MVBEV_RING_DMAIL 0  // place each unit's DMAs one per MFMA after its barrier
-#endif
-#ifndef MVBEV_RING_ABL
-#define MVBEV_RING_ABL 0  // timing ablations only (wrong results): bit 0 no unit barrier, bit 1 no DMA,
-                          // bit 2 no vmcnt wait, bit 3 no weight DMA, bit 4 no halo DMA,
-                          // bit 5 contiguous halo sources, bit 6 one halo source address,
-                          // bits 8 / 9: halo / weights alternate between the first two chunks (L2-resident)
-#endif
-#ifndef MVBEV_RING_STAGGER
-#define MVBEV_RING_STAGGER 0  // waves 4-7 take each unit's barrier one tap earlier (parity-green; measured
-                              // slower: conv1 2.33-2.38 vs 2.18-2.22 ms, the extra A set spills 4-5 VGPRs)
-#endif
+// (Variants measured and removed, DESIGN.md §4: non-temporal halo DMAs, s_setprio around the MFMA
+// stream, DMAs placed one per MFMA, staggered barriers for waves 4-7; the timing ablations live in
+// the round-2/3 records, not in this source.)
 
 // Epilogue of a conv followed by a single-output-channel conv (conv2 -> conv3, map_classifier[2:5],
 // persp_trans_detector.py:53-54): instead of storing the activation, each lane forms, for its
@@ -797,18 +780,8 @@ __global__ __launch_bounds__(RNT) void conv_ring_fixup_kernel(const Args a) {
                                64 * (wave >> 2), acc, lds);
 }
 
-#ifndef MVBEV_RING_STAMP
-#define MVBEV_RING_STAMP 0  // diagnostics build only: per-block (start, end, HW_ID, XCC_ID) in g_ring_stamps
-#endif
-#if MVBEV_RING_STAMP
-__device__ uint32_t g_ring_stamps[16384 * 4];
-#endif
-
 template <int DIL, bool RELU, bool P3 = false, int EWE = 0>
 __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
-#if MVBEV_RING_STAMP
-  const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
-#endif
   constexpr int LDSN = EWE ? (RingGeo<DIL>::LDS > RingGeo<DIL, EWE ? EWE : TW>::LDS ? RingGeo<DIL>::LDS
                                                                                    : RingGeo<DIL, EWE ? EWE : TW>::LDS)
                            : RingGeo<DIL>::LDS;
@@ -869,8 +842,6 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     const int gy = y0 - DIL + r, gx = x0 - DIL + c, by = gy - a.in_row0;
     const bool ok = e < 4 * XPIX && gy >= 0 && gy < a.H && by >= 0 && by < a.in_rows && gx >= 0 && gx < W;
     xo[j] = ok ? 2 * (by * W + gx) + part : -1;
-    if (MVBEV_RING_ABL & 32) xo[j] = ok ? 2 * (max(y0 - DIL - a.in_row0, 0) * W + x0) + e % (2 * XPIX) : -1;
-    if (MVBEV_RING_ABL & 64) xo[j] = ok ? 0 : -1;
   }
   // W unit image [part][kh][sub][co]; packed source [part][tap = 3 kh + kw][sub][co].  The
   // DMA source offsets (and the halo entries' sub-block) are recomputed per issue: a few VALU
@@ -914,7 +885,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     for (int j = 0; j < NX; ++j) {
       const bool s1 = (j * RNIW + wave) * 64 + lane >= 2 * XPIX;
       const bool z = xo[j] < 0 || !(s1 ? kv[1] : kv[0]);
-      if (RNIW == RNW || wave < RNIW) glds16<MVBEV_RING_XAUX>(z ? g_ring_zero : (s1 ? xs[1] : xs[0]) + xo[j], dst + j * RNIT);
+      if (RNIW == RNW || wave < RNIW) glds16(z ? g_ring_zero : (s1 ? xs[1] : xs[0]) + xo[j], dst + j * RNIT);
     }
   };
   auto issue_x = [&](int i) __attribute__((always_inline)) {  // halo of chunk i -> buffer i & 1
@@ -949,7 +920,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) acc[i][j] = floatx16{0};
   bf16x8 fb[2][5][2];  // [set][input row m (rows base + m * DIL)][hi, lo]
-  bf16x8 fa[3][2][2];  // [set][ct][hi, lo] (waves 0-3 alternate sets 0/1; staggered waves 4-7 use set = tap row)
+  bf16x8 fa[2][2][2];  // [set][ct][hi, lo]
   auto fetch_b = [&](int st, int xb, int kw) __attribute__((always_inline)) {
     const u32x4* X = Xlds + xb * XBUF + kl * 2 * XPIX + (base + lr) * XW + lc + kw * DIL;
 #pragma unroll
@@ -985,18 +956,6 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 18 - n, 0);
   };
-  // after a unit's barrier: one DMA (the first nv) and one fragment read after each of the
-  // first 14 MFMAs, so the SIMD's MFMA pipe is fed while the DMAs issue
-  auto interleave_dma = [&](auto nvmem) __attribute__((always_inline)) {
-    constexpr int nv = decltype(nvmem)::value;
-#pragma unroll
-    for (int i = 0; i < 14; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      if (i < nv) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-    }
-    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-  };
 
   if (nch > 0) {
     // prologue: W(0), halo(0), W(1), W(2) in flight; wait for the first two
@@ -1018,84 +977,32 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     const int u_ = u0 + (R);                                                                   \
     if (u_ >= U) break;                                                                        \
     fetch_a(P ^ 1, SLOT, 1);                                                                   \
-    if (MVBEV_RING_PRIO) __builtin_amdgcn_s_setprio(1);                                        \
     mfmas(P, P, 0);                                                                            \
     interleave(std::integral_constant<int, 4>{});                                              \
     fetch_a(P, SLOT, 2);                                                                       \
     mfmas(P ^ 1, P, 1);                                                                        \
     interleave(std::integral_constant<int, 4>{});                                              \
     /* retire W(u+1) (+ the next chunk's halo at kw 2); LDS reads of this unit's slot done */ \
-    if (MVBEV_RING_ABL & 4) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                  \
-    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(KW == 1 ? RNWI + NX : RNWI) : "memory"); \
-    if (!(MVBEV_RING_ABL & 1)) __builtin_amdgcn_s_barrier();                                   \
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(KW == 1 ? RNWI + NX : RNWI) : "memory"); \
+    __builtin_amdgcn_s_barrier();                                                              \
     asm volatile("" ::: "memory");                                                             \
-    if (!(MVBEV_RING_ABL & 2)) {                                                               \
-      if (!(MVBEV_RING_ABL & 8)) issue_w_ch((MVBEV_RING_ABL & 512) ? chunk_of(nx_i & 1) : nx_ph, KW, SLOT);                                  \
-      if (KW == 0 && !(MVBEV_RING_ABL & 16)) issue_x_ch((MVBEV_RING_ABL & 256) ? chunk_of(nx_i & 1) : nx_ph, ((R) / 3 + 1) & 1);             \
-    }                                                                                          \
+    issue_w_ch(nx_ph, KW, SLOT);                                                               \
+    if (KW == 0) issue_x_ch(nx_ph, ((R) / 3 + 1) & 1);                                         \
     if (KW == 2) advance();                                                                    \
     fetch_b(P ^ 1, NXB, NKW);                                                                  \
     fetch_a(P ^ 1, NSLOT, 0);                                                                  \
     mfmas(P, P, 2);                                                                            \
-    if constexpr (MVBEV_RING_DMAIL != 0) interleave_dma(std::integral_constant<int, KW == 0 ? RNWI + NX : RNWI>{}); \
-    else interleave(std::integral_constant<int, 14>{});                                        \
-    if (MVBEV_RING_PRIO) __builtin_amdgcn_s_setprio(0);                                        \
-  } while (0)
-    // Staggered waves 4-7 (MI355X_MICROARCH.md "Two waves per SIMD", item 9): one unit body
-    // for all waves with the fragment sets indexed by tap row; waves 4-7 read A1 and A2
-    // before kh 0 and take the unit's barrier after kh 0 instead of after kh 1, so around
-    // each barrier one wave of every SIMD pair still has MFMAs to issue while its partner
-    // waits or issues the DMA.  Same barrier count and wait counts for every wave.
-#define RING_UNIT_U(R)                                                                         \
-  do {                                                                                         \
-    constexpr int KW = (R) % 3, P = (R) & 1, SLOT = (R) % 3;                                    \
-    constexpr int NSLOT = ((R) + 1) % 3, NXB = (((R) + 1) / 3) & 1, NKW = ((R) + 1) % 3;        \
-    const int u_ = u0 + (R);                                                                   \
-    if (u_ >= U) break;                                                                        \
-    fetch_a(1, SLOT, 1);                                                                       \
-    if (stag) fetch_a(2, SLOT, 2);                                                             \
-    mfmas(0, P, 0);                                                                            \
-    if (!stag) fetch_a(2, SLOT, 2);                                                            \
-    if (stag) {                                                                                \
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(KW == 1 ? RNWI + NX : RNWI) : "memory"); \
-      __builtin_amdgcn_s_barrier();                                                            \
-      asm volatile("" ::: "memory");                                                           \
-    }                                                                                          \
-    mfmas(1, P, 1);                                                                            \
-    if (!stag) {                                                                               \
-      asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(KW == 1 ? RNWI + NX : RNWI) : "memory"); \
-      __builtin_amdgcn_s_barrier();                                                            \
-      asm volatile("" ::: "memory");                                                           \
-    }                                                                                          \
-    issue_w(u_ + 3);                                                                           \
-    if (KW == 0) issue_x(u_ / 3 + 1);                                                          \
-    fetch_b(P ^ 1, NXB, NKW);                                                                  \
-    fetch_a(0, NSLOT, 0);                                                                      \
-    mfmas(2, P, 2);                                                                            \
     interleave(std::integral_constant<int, 14>{});                                             \
   } while (0)
-    if (!MVBEV_RING_STAGGER) {
-      for (int u0 = 0; u0 < U; u0 += 6) {
-        RING_UNIT(0);
-        RING_UNIT(1);
-        RING_UNIT(2);
-        RING_UNIT(3);
-        RING_UNIT(4);
-        RING_UNIT(5);
-      }
-    } else {
-      const bool stag = wave >= 4;
-      for (int u0 = 0; u0 < U; u0 += 6) {
-        RING_UNIT_U(0);
-        RING_UNIT_U(1);
-        RING_UNIT_U(2);
-        RING_UNIT_U(3);
-        RING_UNIT_U(4);
-        RING_UNIT_U(5);
-      }
+    for (int u0 = 0; u0 < U; u0 += 6) {
+      RING_UNIT(0);
+      RING_UNIT(1);
+      RING_UNIT(2);
+      RING_UNIT(3);
+      RING_UNIT(4);
+      RING_UNIT(5);
     }
 #undef RING_UNIT
-#undef RING_UNIT_U
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the block exits
   }
 
@@ -1129,16 +1036,6 @@ __global__ __launch_bounds__(RNT, 1) void conv_ring_kernel(const Args a) {
     tile = (a.tile_order ? a.tile_order[slot] : slot) * a.n_cot + j % a.n_cot;
   }
   run_item(tile, ci0, ci1, pslot);
-#if MVBEV_RING_STAMP
-  if (threadIdx.x == 0 && blockIdx.x < 16384) {  // vector stores of the block's wall-clock span and place
-    const uint64_t stamp1 = __builtin_amdgcn_s_memrealtime();
-    uint32_t* d = g_ring_stamps + 4 * blockIdx.x;
-    d[0] = (uint32_t)stamp0;
-    d[1] = (uint32_t)stamp1;
-    d[2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID: wave, SIMD, CU, SH, SE
-    d[3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-  }
-#endif
 }
 
 #ifndef MVBEV_B3_RING
@@ -1374,9 +1271,6 @@ constexpr int XH = 4 * NXI;                       // T rows of a 12-row workgrou
 #ifndef MVBEV_WINO_NIW
 #define MVBEV_WINO_NIW 4  // DMA-issuing waves, one per SIMD (cfg2 winoconv, buffer-load DMAs: 4 1.40 ms, 8 1.51-1.52; with the per-unit address arithmetic of round 2: 8 1.59-1.67, 4 1.73-1.79)
 #endif
-#ifndef MVBEV_WINO_XAUX
-#define MVBEV_WINO_XAUX 0  // cache policy of the T DMAs (0 = default; with buffer-load DMAs and 4 issuing waves nt (2) measured +0.5 % on conv1, +1 % on conv2: conv2's T is re-read by the 4 Cout tiles)
-#endif
 constexpr int NIW = MVBEV_WINO_NIW;               // DMA-issuing waves
 constexpr int NIT = 64 * NIW;
 constexpr int NWI = RUNIT / NIT;                  // weight DMAs per issuing wave per unit (3)
@@ -1537,17 +1431,9 @@ __global__ __launch_bounds__(256) void wino_rows_kernel(const WinoRowsArgs a) {
   }
 }
 
-#ifndef MVBEV_WINO_PAIRB
-#define MVBEV_WINO_PAIRB -1  // one unit barrier per two units (2 units of DMA lookahead instead of 3): 1 on,
-                             // 0 off, -1 conv2 only (cfg2: conv2 0.349 -> 0.342 ms, conv1 1.43 -> 1.45)
-#endif
-#ifndef MVBEV_WINO_TSKIP
-#define MVBEV_WINO_TSKIP 1  // T pieces that hold no T entry are not issued (per-wave wait counts)
-#endif
-#ifndef MVBEV_WINO_ABL
-#define MVBEV_WINO_ABL 0  // timing ablations only (wrong results): bit 0 no unit barrier / wait, bit 1 no DMA in the loop,
-                          // bit 2 no T DMA, bit 3 no weight DMA (the other stream's pieces and waits stay)
-#endif
+// One unit barrier per two units (2 units of DMA lookahead instead of 3) for conv2 only (cfg2: conv2
+// 0.349 -> 0.342 ms, conv1 1.43 -> 1.45); T pieces that hold no T entry are not issued (per-wave wait
+// counts); the T DMAs keep the default cache policy (nt measured +0.5 % on conv1, +1 % on conv2).
 // DIL 2 (conv2): the wave's row tile is the ring kernel's interleaved rows base + 2 pt; P3: the
 // epilogue forms conv3's partial sums (cout1_partials) instead of storing y
 template <bool RELU, int DIL, bool P3>
@@ -1636,24 +1522,20 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   auto issue_unit = [&](const ChunkBase& cb, int xi, int slot) __attribute__((always_inline)) {
     if (wave >= NIW) return;
     u32x4* dst = lds + slot * SLOT + wave * 64;
-    if (!(MVBEV_WINO_ABL & 8)) {
-      const __amdgpu_buffer_rsrc_t rw =
-          __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(cb.w + xi * 3 * 2 * BN * 16), (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(cb.w + xi * 3 * 2 * BN * 16), (short)0, 0x7fffffff, 0x00020000);
 #pragma unroll
-      for (int j = 0; j < NWI; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(dst + j * NIT), 16,
-                                                 wvo[j], 0, 0, 0);
-    }
-    if (!(MVBEV_WINO_ABL & 4)) {
-      const int32_t rows_b = xi * W * 32;
-      const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<char*>(cb.t + rows_b), (short)0, cb.kv1 ? 0x7fffffff : (int)(tplane_b - rows_b), 0x00020000);
+    for (int j = 0; j < NWI; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(dst + j * NIT), 16,
+                                               wvo[j], 0, 0, 0);
+    const int32_t rows_b = xi * W * 32;
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(cb.t + rows_b), (short)0, cb.kv1 ? 0x7fffffff : (int)(tplane_b - rows_b), 0x00020000);
 #pragma unroll
-      for (int j = 0; j < NXT; ++j)
-        if (!MVBEV_WINO_TSKIP || (j * NIW + wave) * 64 < TROW)  // pieces wholly past the T row: not issued
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(dst + RUNIT + j * NIT),
-                                                   16, tvo[j], 0, 0, MVBEV_WINO_XAUX);
-    }
+    for (int j = 0; j < NXT; ++j)
+      if ((j * NIW + wave) * 64 < TROW)  // pieces wholly past the T row: not issued
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(dst + RUNIT + j * NIT),
+                                                 16, tvo[j], 0, 0, 0);
   };
   // the current chunk and the next
   ChunkBase cur = base_of(gbase + ci);
@@ -1695,16 +1577,15 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     }
   };
 
-  // LDS-DMA pieces per wave per unit (the ablation builds drop some)
-  // LDS-DMA pieces per wave per unit (the ablation builds drop some): waves < WHI issue NPU_HI,
-  // the others NPU_LO (TSKIP: the last T piece only where it holds T entries)
-  constexpr int NXT_LO = MVBEV_WINO_TSKIP ? TROW / NIT : NXT;
-  constexpr int WHI = MVBEV_WINO_TSKIP ? (TROW % NIT + 63) / 64 : NIW;
-  static_assert(!MVBEV_WINO_TSKIP || NXT_LO + (WHI > 0) == NXT, "T pieces");
-  constexpr int NPU_HI = ((MVBEV_WINO_ABL & 8) ? 0 : NWI) + ((MVBEV_WINO_ABL & 4) ? 0 : NXT);
-  constexpr int NPU_LO = ((MVBEV_WINO_ABL & 8) ? 0 : NWI) + ((MVBEV_WINO_ABL & 4) ? 0 : NXT_LO);
+  // LDS-DMA pieces per wave per unit: waves < WHI issue NPU_HI, the others NPU_LO (the last T
+  // piece only where it holds T entries)
+  constexpr int NXT_LO = TROW / NIT;
+  constexpr int WHI = (TROW % NIT + 63) / 64;
+  static_assert(NXT_LO + (WHI > 0) == NXT, "T pieces");
+  constexpr int NPU_HI = NWI + NXT;
+  constexpr int NPU_LO = NWI + NXT_LO;
   const bool whi = wave < WHI;
-  constexpr bool PB = MVBEV_WINO_PAIRB < 0 ? DIL == 2 : MVBEV_WINO_PAIRB != 0;
+  constexpr bool PB = DIL == 2;  // one barrier per two units for conv2
   if (nch > 0) {
     const int U = NXI * nch;
     // prologue: units 0-3 (chunk 0, rows 0-3) in flight, wait for unit 0
@@ -1746,14 +1627,12 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     sched6(std::integral_constant<int, 4>{});                                                        \
     if (!PB) {                                                                         \
       /* retire unit u+1; every LDS read of this unit's slot is done */                               \
-      if (!(MVBEV_WINO_ABL & 1)) {                                                                   \
-        if (whi) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU_HI) : "memory");   \
-        else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU_LO) : "memory");        \
-        __builtin_amdgcn_s_barrier();                                                                \
-      }                                                                                              \
+      if (whi) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU_HI) : "memory");     \
+      else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU_LO) : "memory");          \
+      __builtin_amdgcn_s_barrier();                                                                  \
       asm volatile("" ::: "memory");                                                                 \
       /* unit u+4 into this slot: (chunk, xi 4) at xi 0, else (next chunk, xi - 1) */                \
-      if (!(MVBEV_WINO_ABL & 2)) issue_unit(XI == 0 ? cur : nx, (XI + 4) % 5, slot);           \
+      issue_unit(XI == 0 ? cur : nx, (XI + 4) % 5, slot);                                            \
     } else if (P == 1) {                                                                             \
       /* PAIRB: one barrier per two units, after the odd one: retire units u+1, u+2 (all in      \
          flight), then units u+3, u+4 into the slots of u-1 and u */                                  \
@@ -1935,13 +1814,6 @@ int mvbev_conv3x3_bf16x3_tile_rows(int x_layout, int dilation) {
   return ring ? mvbev::b3::RT : MVBEV_B3_WAVES;
 }
 
-int mvbev_conv3x3_bf16x3(const void* x, int x_layout, const mvbev_conv_desc* desc,
-                         const void* w_packed, const float* bias, const float* init,
-                         int64_t Cout, int dilation, int relu, float* y, void* stream) {
-  return mvbev_conv3x3_bf16x3_ex(x, x_layout, desc, w_packed, bias, init, Cout, dilation, relu, y,
-                                 MVBEV_LAYOUT_F32, nullptr, nullptr, nullptr, 0, stream);
-}
-
 size_t mvbev_conv3x3_bf16x3_workspace_bytes(const mvbev_conv_desc* desc, int64_t Cout) {
   using namespace mvbev::b3;
   if (!desc || Cout <= 0 || desc->W <= 0 || desc->out_rows <= 0 || desc->B <= 0 || desc->K <= 0)
@@ -2052,13 +1924,6 @@ int mvbev_conv3x3_dgrad_bf16x3_ex(const void* dy, int dy_layout, const mvbev_con
                        dx_layout, nullptr, nullptr, nullptr, 0, stream, out_mask, (int)cot_per_group);
 }
 
-int mvbev_conv3x3_dgrad_bf16x3(const float* dy, const mvbev_conv_desc* desc, const void* w_packed, int64_t Cout_p,
-                               int dilation, void* dx, int dx_layout, const uint32_t* out_mask,
-                               int64_t cot_per_group, void* stream) {
-  return mvbev_conv3x3_dgrad_bf16x3_ex(dy, MVBEV_LAYOUT_F32, desc, w_packed, Cout_p, dilation, dx, dx_layout, out_mask,
-                                       cot_per_group, stream);
-}
-
 size_t mvbev_conv3x3_packed_bytes_wino(int64_t Cout, int64_t K) {
   if (Cout <= 0 || K <= 0) return 0;
   return (size_t)(mvbev::round_up(K, mvbev::b3::KC) / mvbev::b3::KC) * (size_t)(Cout / mvbev::b3::BN) *
@@ -2121,10 +1986,4 @@ int mvbev_conv3x3_wino_bf16x3_cout1_partials(const void* t, const mvbev_conv_des
                                 nullptr, stream, dilation, w3, static_cast<float*>(partials));
 }
 
-#if MVBEV_RING_STAMP
-int mvbev_debug_ring_stamps(void* host_out, int n) {
-  if (n > 16384 * 4) n = 16384 * 4;
-  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(mvbev::b3::g_ring_stamps), sizeof(uint32_t) * n) == hipSuccess ? 0 : -1;
-}
-#endif
 }  // extern "C"

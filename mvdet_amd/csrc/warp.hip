@@ -161,12 +161,6 @@ __global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_tile_kernel(const Warp
 #define MVBEV_WW_STAGE 384  // max staged box pixels per channel (8 channels x 384 x 4 B = 12 KiB); 0 = off
 #endif
 constexpr int kWwStage = MVBEV_WW_STAGE;
-#ifndef MVBEV_WW_ABL
-#define MVBEV_WW_ABL 0  // timing ablations only (wrong results): bit 0 no T stores (phase 2), bit 1 no source loads
-#endif
-#ifndef MVBEV_WW_QUAD
-#define MVBEV_WW_QUAD 1  // stage the box with 16-B loads where the source allows (stage_box_load)
-#endif
 
 template <bool PAIR>
 __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(const WarpArgs a, int r3_rows) {
@@ -232,10 +226,10 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
   const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
   const bool quad_ok = vw.sW == 1 && (W & 3) == 0 && (vw.sH & 3) == 0 && (vw.sC & 3) == 0 &&
                        (reinterpret_cast<uintptr_t>(base) & 15) == 0;
-  const StageBox sb = stage_box_shape(box, W, quad_ok && MVBEV_WW_QUAD);
+  const StageBox sb = stage_box_shape(box, W, quad_ok);  // 16-B staging loads where the source allows
   const int R = sb.R, Cb = sb.pitch;
   // uniform per block (the staged path needs unit column stride: the non-quad loads assume it too)
-  const bool staged = kWwStage > 0 && box[1] >= 0 && vw.sW == 1 && R * Cb <= kWwStage && !(MVBEV_WW_ABL & 2);
+  const bool staged = kWwStage > 0 && box[1] >= 0 && vw.sW == 1 && R * Cb <= kWwStage;
   if (staged) {
     stage_box_load<kWwThreads>(base, vw.sC, vw.sH, c_begin, c_end, sb, stage, tid);
     __syncthreads();
@@ -282,10 +276,6 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
           const int64_t o_sw = cy1 * sH + cx0 * sW, o_se = cy1 * sH + cx1 * sW;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {  // straight-line (a short last group re-reads its last channel)
-            if (MVBEV_WW_ABL & 2) {  // timing ablation: no source loads
-              d[j] = w_nw + (float)j;
-              continue;
-            }
             const int ch = min(c_begin + j, c_end - 1);
             const float* pc = base + (int64_t)ch * sC;
             float vnw, vne, vsw, vse;
@@ -314,7 +304,7 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
     nz[i][c] = any;
   }
   __syncthreads();
-  if (!(MVBEV_WW_ABL & 1)) wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
+  wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
 }
 
 template <typename T, bool SPLIT>
@@ -555,12 +545,6 @@ int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t
     hipLaunchKernelGGL((warp_wino_kernel<false>), grid, block, 0, as_stream(stream), a, (int)r3_rows);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
-}
-
-int mvbev_warp_views_split_bf16(const mvbev_warp_view* views, int nviews, int src_is_f16,
-                                int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
-                                void* stream) {
-  return mvbev_warp_views_split_bf16_ex(views, nviews, src_is_f16, B, C, H, W, Ho, Wo, 0, stream);
 }
 
 int mvbev_warp_views_f16(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,

@@ -19,9 +19,6 @@ namespace mvbev {
 #ifndef MVBEV_WARP_CPB
 #define MVBEV_WARP_CPB 8
 #endif
-#ifndef MVBEV_WARP_NT
-#define MVBEV_WARP_NT 0  // non-temporal slab stores (measured no faster)
-#endif
 #ifndef MVBEV_WARP_GU
 #define MVBEV_WARP_GU 1  // 8-channel groups sampled before their stores are issued
 #endif
@@ -85,13 +82,8 @@ __device__ inline void store_split8(u32x4_t* dst, const float (&v)[8]) {
     hi[j] = h;
     lo[j] = (__bf16)(v[j] - (float)h);
   }
-#if MVBEV_WARP_NT
-  __builtin_nontemporal_store(__builtin_bit_cast(u32x4_t, hi), dst);
-  __builtin_nontemporal_store(__builtin_bit_cast(u32x4_t, lo), dst + 1);
-#else
-  dst[0] = __builtin_bit_cast(u32x4_t, hi);
+  dst[0] = __builtin_bit_cast(u32x4_t, hi);  // (non-temporal stores measured no faster)
   dst[1] = __builtin_bit_cast(u32x4_t, lo);
-#endif
 }
 
 // kornia 0.6.11 warp coordinates of output pixel (u, v): create_meshgrid(normalized) ->
@@ -220,14 +212,8 @@ constexpr int kWwRows = 14, kWwCols = MVBEV_WW_COLS, kWwThreads = 16 * kWwCols;
 // the geometry's VALU work is not what binds these kernels; the TA/TD load path is: 77-84 % busy)
 static_assert(kWarpCPB == 8 && kUpCPB == 8, "one 8-channel group per warp block");
 static_assert(4 * kWwCols * 4 == kWwThreads, "phase 2: one (tile, column, channel pair) per thread");
-#ifndef MVBEV_WARP_WPE
-#define MVBEV_WARP_WPE 8  // waves per SIMD asked of the compiler (caps VGPRs at 512 / WPE; 8: 72 -> 64, measured -4 %); 0 = free
-#endif
-#if MVBEV_WARP_WPE > 0
-#define MVBEV_WARP_OCC __attribute__((amdgpu_waves_per_eu(MVBEV_WARP_WPE, MVBEV_WARP_WPE)))
-#else
-#define MVBEV_WARP_OCC
-#endif
+// 8 waves per SIMD asked of the compiler (VGPRs capped at 64: 72 -> 64 measured -4 % on both fused warps)
+#define MVBEV_WARP_OCC __attribute__((amdgpu_waves_per_eu(8, 8)))
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
 __device__ inline unsigned pack_bf16x2(float x, float y) {
@@ -257,9 +243,8 @@ __device__ inline StageBox stage_box_shape(const int (&box)[4], int W, bool quad
   sb.pitch = c1 - sb.c0;
   return sb;
 }
-// PIX: pixel-major staging, stage[(r * pitch + col) * 8 + j] (a pixel's 8 channels in 32 B: a tap
-// is two 16-B LDS reads for all channels), else channel-major stage[j][r][col].
-template <int NT, bool PIX = false>
+// channel-major staging: stage[j][r][col]
+template <int NT>
 __device__ inline void stage_box_load(const float* __restrict__ base, int64_t sC, int64_t sH, int c_begin, int c_end,
                                       const StageBox& sb, float* __restrict__ stage, int tid) {
   const int n = sb.R * sb.pitch;
@@ -272,17 +257,8 @@ __device__ inline void stage_box_load(const float* __restrict__ base, int64_t sC
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         t[j] = *reinterpret_cast<const f32x4a_t*>(src + (int64_t)min(c_begin + j, c_end - 1) * sC);
-      if constexpr (PIX) {
-        f32x4a_t* dst = reinterpret_cast<f32x4a_t*>(stage + (r * sb.pitch + 4 * q) * 8);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          dst[2 * e] = f32x4a_t{t[0][e], t[1][e], t[2][e], t[3][e]};
-          dst[2 * e + 1] = f32x4a_t{t[4][e], t[5][e], t[6][e], t[7][e]};
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4a_t*>(stage + j * n + r * sb.pitch + 4 * q) = t[j];
-      }
+      for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4a_t*>(stage + j * n + r * sb.pitch + 4 * q) = t[j];
     }
   } else {
     for (int r = tid / 32; r < sb.R; r += NT / 32)
@@ -291,14 +267,8 @@ __device__ inline void stage_box_load(const float* __restrict__ base, int64_t sC
 #pragma unroll
         for (int j = 0; j < 8; ++j)
           t[j] = base[(int64_t)min(c_begin + j, c_end - 1) * sC + (int64_t)(sb.r0 + r) * sH + sb.c0 + cc];
-        if constexpr (PIX) {
-          f32x4a_t* dst = reinterpret_cast<f32x4a_t*>(stage + (r * sb.pitch + cc) * 8);
-          dst[0] = f32x4a_t{t[0], t[1], t[2], t[3]};
-          dst[1] = f32x4a_t{t[4], t[5], t[6], t[7]};
-        } else {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) stage[j * n + r * sb.pitch + cc] = t[j];
-        }
+        for (int j = 0; j < 8; ++j) stage[j * n + r * sb.pitch + cc] = t[j];
       }
   }
 }

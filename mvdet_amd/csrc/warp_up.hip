@@ -144,12 +144,8 @@ __global__ __launch_bounds__(kUpTH * kUpTW) void warp_up_kernel(const UpArgs ua)
 #ifndef MVBEV_UPW_STAGE
 #define MVBEV_UPW_STAGE 384  // max staged box pixels per channel (8 channels x 384 x 4 B = 12 KiB); 0 = off
 #endif
-#ifndef MVBEV_UPW_PIX
-#define MVBEV_UPW_PIX 0  // 1: pixel-major staging (a 3x3 window tap = two 16-B LDS reads for the 8 channels): measured 2.2x slower (0.86 vs 0.39 ms, cfg2), not kept
-#endif
-#ifndef MVBEV_UPW_QUAD
-#define MVBEV_UPW_QUAD 1  // stage the box with 16-B loads where the source allows (stage_box_load)
-#endif
+// (Pixel-major staging — a 3x3 window tap as two 16-B LDS reads for the 8 channels — measured 2.2x
+// slower: 0.86 vs 0.39 ms at cfg2.)
 constexpr int kUpStage = MVBEV_UPW_STAGE;
 
 __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino_kernel(const UpArgs ua, int r3_rows) {
@@ -210,11 +206,11 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino_kernel
   const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
   const bool quad_ok = (w & 3) == 0 && (vw.sH & 3) == 0 && (vw.sC & 3) == 0 &&
                        (reinterpret_cast<uintptr_t>(base) & 15) == 0;
-  const StageBox sb = stage_box_shape(box, w, quad_ok && MVBEV_UPW_QUAD);
+  const StageBox sb = stage_box_shape(box, w, quad_ok);  // 16-B staging loads where the source allows
   const int R = sb.R, Cb = sb.pitch;
   const bool staged = kUpStage > 0 && box[1] >= 0 && R * Cb <= kUpStage;  // uniform per block
   if (staged) {  // the box of every channel of the group (16-B loads where the source allows)
-    stage_box_load<kWwThreads, MVBEV_UPW_PIX != 0>(base, vw.sC, vw.sH, c_begin, c_end, sb, stage, tid);
+    stage_box_load<kWwThreads>(base, vw.sC, vw.sH, c_begin, c_end, sb, stage, tid);
     __syncthreads();
   }
   if (i < kWwRows) {
@@ -238,31 +234,6 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino_kernel
 #pragma unroll
           for (int q = 0; q < 3; ++q)
             idx[r][q] = (min(uw.rb + r, h - 1) - box[0]) * Cb + (min(uw.cb + q, w - 1) - sb.c0);
-        if (MVBEV_UPW_PIX) {  // a tap's 8 channels in two 16-B reads; per channel the same sums in the same order
-          float acc[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-#pragma unroll
-          for (int r = 0; r < 3; ++r) {
-            float rr[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) rr[j] = 0.f;
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-              const f32x4a_t* px = reinterpret_cast<const f32x4a_t*>(stage + idx[r][q] * 8);
-              const f32x4a_t lo4 = px[0], hi4 = px[1];
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                rr[j] += uw.ax[q] * lo4[j];
-                rr[4 + j] += uw.ax[q] * hi4[j];
-              }
-            }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc[j] += uw.ay[r] * rr[j];
-          }
-#pragma unroll
-          for (int j = 0; j < 8; ++j) d[j] = c_begin + j < c_end ? acc[j] : 0.f;
-        } else {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float* sj = stage + j * n;
@@ -276,7 +247,6 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino_kernel
             }
             d[j] = c_begin + j < c_end ? acc : 0.f;
           }
-        }
       } else {
         any = true;
         const int cb = uw.cb, rb = uw.rb;

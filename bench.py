@@ -517,10 +517,11 @@ def main():
     ap.add_argument("--no-train", action="store_true", help="skip the training-step (forward+backward) line")
     ap.add_argument("--train-torch", type=int, default=1,
                     help="1 = also time the reference op sequence (torch GPU autograd) for the training step")
-    ap.add_argument("--mp-mode", default="bands", choices=["bands", "gather", "partial", "frames"],
-                    help="N>1 `value`: view-parallel band exchange (default: views one per GPU, all-to-all of each "
-                         "row band's input window, row-band fusion, pipelined), slab all-gather, conv1 partial sums + "
-                         "reduce-scatter, or frame-parallel; the other modes are reported alongside")
+    ap.add_argument("--mp-mode", default="auto", choices=["auto", "bands", "gather", "partial", "frames"],
+                    help="N>1 `value`: auto (default: the view-parallel mode mvdet_amd.mp_model predicts fastest for "
+                         "this config and N, DESIGN.md §6), the band exchange (all-to-all of each row band's input "
+                         "window), slab all-gather, conv1 partial sums + reduce-scatter, or frame-parallel; the other "
+                         "modes are reported alongside")
     ap.add_argument("--north-star-cfg", type=int, default=3,
                     help="also run this config (the north star's 480x1440 Wildtrack grid) as a sub-object "
                          "(N=1: single GPU with a reduced-sample CPU baseline; N>1: the band exchange); 0 = skip")

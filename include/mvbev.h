@@ -323,8 +323,12 @@ size_t mvbev_wino_rows_bytes(const mvbev_conv_desc* desc);
 int mvbev_wino_rows_split_bf16(const void* x, const mvbev_conv_desc* desc, const uint32_t* group_mask, void* t,
                                size_t t_bytes, void* stream);
 int mvbev_conv3x3_wino_bf16x3(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,
-                              const float* init, int64_t Cout, int relu, void* y, int y_layout,
+                              const float* init, int64_t Cout, int relu, void* y, int y_layout, int64_t y_band_rows,
                               const uint32_t* group_mask, const int32_t* tile_order, void* stream);
+/* y_band_rows (ABI 11600; MVBEV_LAYOUT_F32 only, 0 = plain [B][Cout][out_rows][W]): y in row bands,
+ * computed row r (from out_row0) at band r / y_band_rows, y = [bands][B][Cout][y_band_rows][W] (rows
+ * past out_rows in the last band untouched) — the reduce-scatter input of the partial-sum multi-GPU
+ * mode, written in place. */
 /* The same two steps for dilation 2 (conv2, map_classifier[2:4], persp_trans_detector.py:53:
  * nn.Conv2d(512, 512, 3, padding=2, dilation=2)): the 12-row workgroup tile holds two interleaved
  * pairs of 3-row tiles (rows r, r + 2, r + 4), whose T = B^T over the 5 input rows r - 2 ... r + 6

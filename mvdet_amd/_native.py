@@ -187,7 +187,7 @@ def _declare(lib):
     lib.mvbev_wino_rows_split_bf16.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, ctypes.c_size_t, _p]
     lib.mvbev_conv3x3_wino_bf16x3.restype = ctypes.c_int
     lib.mvbev_conv3x3_wino_bf16x3.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64, ctypes.c_int, _p,
-                                              ctypes.c_int, _p, _p, _p]
+                                              ctypes.c_int, _i64, _p, _p, _p]
     lib.mvbev_wino_rows_split_bf16_dil.restype = ctypes.c_int
     lib.mvbev_wino_rows_split_bf16_dil.argtypes = [_p, ctypes.POINTER(ConvDesc), ctypes.c_int, _p, _p, ctypes.c_size_t,
                                                    _p]

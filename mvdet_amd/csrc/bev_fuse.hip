@@ -310,7 +310,7 @@ int mvbev_bev_fuse(const mvbev_bev_plan* p, const void* const* views, float* map
   // a7: conv1 + coord term + bias + ReLU -> y1 (split-bf16, conv2's input)
   if (p->wino)
     BEV_TRY(mvbev_conv3x3_wino_bf16x3(big, &d1, at<void>(ws, p, R_PACK1), nullptr, at<float>(ws, p, R_INIT), kMid, 1,
-                                      y1, MVBEV_LAYOUT_SPLIT_BF16, mask, order, stream));
+                                      y1, MVBEV_LAYOUT_SPLIT_BF16, 0, mask, order, stream));
   else
     BEV_TRY(mvbev_conv3x3_bf16x3_ex(big, MVBEV_LAYOUT_SPLIT_BF16, &d1, at<void>(ws, p, R_PACK1), nullptr,
                                     at<float>(ws, p, R_INIT), kMid, 1, 1, y1, MVBEV_LAYOUT_SPLIT_BF16, mask, order,

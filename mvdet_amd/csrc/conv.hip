@@ -438,7 +438,7 @@ int mvbev_conv3x3_f32(const float* x, const mvbev_conv_desc* d, const float* w_p
   if (d->in_rows * d->W * KC > (int64_t)INT32_MAX || d->H > INT32_MAX / 2 || d->W > INT32_MAX / 2)
     return MVBEV_ERR_SHAPE;
   if ((reinterpret_cast<uintptr_t>(w_packed) & 15) != 0) return MVBEV_ERR_ALIGN;
-  ConvArgs a;
+  ConvArgs a{};
   a.x = x; a.wp = w_packed; a.bias = bias; a.init = init; a.y = y;
   a.group_stride = d->group_stride; a.batch_stride = d->batch_stride;
   a.group = (int)d->group; a.nchunks = (int)(d->K / KC); a.Cout = (int)Cout;

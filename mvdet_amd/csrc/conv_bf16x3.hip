@@ -142,6 +142,10 @@ struct Args {
   // edge strip (ring kernel, optional): pixel tiles [tiles_y * tiles_x, + edge_tiles) of each
   // batch item are edge_rows x (W - edge_x0) tiles of columns [edge_x0, W) (RingGeo EW)
   int edge_tiles, edge_x0, edge_rows, edge_w;
+  // fp32 y in row bands (optional, > 0): computed row r (from out_row0) goes to band r / band_rows,
+  // y = [bands][B][Cout][band_rows][W] — the reduce-scatter's input of the partial-sum multi-GPU
+  // mode, written in place (no band-major copy)
+  int band_rows;
 };
 
 // Input tag: the split-bf16 blocked layout written by mvbev_warp_views_split_bf16 and by this
@@ -180,7 +184,12 @@ __device__ inline void store_block(const Args& a, int b, int row, int col, int c
       if (a.bias) v += a.bias[co];
       if (a.init) v += a.init[co * iplane + (int64_t)row * W + col];
       if (RELU) v = v < 0.f ? 0.f : v;
-      a.y[((int64_t)b * a.Cout + co) * oplane + (int64_t)(row - a.out_row0) * W + col] = v;
+      if (a.band_rows > 0) {
+        const int rr = row - a.out_row0, band = rr / a.band_rows;
+        a.y[((((int64_t)band * a.B + b) * a.Cout + co) * a.band_rows + (rr - band * a.band_rows)) * W + col] = v;
+      } else {
+        a.y[((int64_t)b * a.Cout + co) * oplane + (int64_t)(row - a.out_row0) * W + col] = v;
+      }
     }
     return;
   }
@@ -1129,7 +1138,7 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
     return MVBEV_ERR_SHAPE;
   if ((reinterpret_cast<uintptr_t>(w_packed) & 15) != 0) return MVBEV_ERR_ALIGN;
   constexpr int NW = MVBEV_B3_WAVES;
-  Args a;
+  Args a{};
   a.x = x; a.wp = static_cast<const u32x4*>(w_packed); a.bias = bias; a.init = init; a.y = y;
   a.group_stride = d->group_stride; a.batch_stride = d->batch_stride;
   a.B = (int)d->B; a.group = (int)d->group; a.K = (int)d->K; a.nchunks = (int)ceil_div(d->K, KC);
@@ -1711,7 +1720,7 @@ static int wino_rows_launch(const void* x, const mvbev_conv_desc* d, int dil, co
 static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_packed, const float* bias,
                        const float* init, int64_t Cout, int relu, float* y, int y_layout,
                        const uint32_t* group_mask, const int32_t* tile_order, void* stream, int dil = 1,
-                       const float* w3 = nullptr, float* p3 = nullptr) {
+                       const float* w3 = nullptr, float* p3 = nullptr, int64_t band_rows = 0) {
   if (!t || !d || !w_packed || (!y && !p3)) return MVBEV_ERR_NULL;
   if (dil != 1 && dil != 2) return MVBEV_ERR_DILATION;
   if (p3 && (!w3 || group_mask || init)) return MVBEV_ERR_SHAPE;  // the conv2 -> conv3 form: dense, bias only
@@ -1743,6 +1752,8 @@ static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_pa
   }
   a.tile_order = group_mask ? tile_order : nullptr;
   a.y_split = y_layout == MVBEV_LAYOUT_SPLIT_BF16;
+  if (band_rows < 0 || (band_rows > 0 && (a.y_split || p3 || band_rows > d->out_rows))) return MVBEV_ERR_SHAPE;
+  a.band_rows = (int)band_rows;
   a.npix = (int)(tiles / a.n_cot);
   const int64_t nwg = group_mask ? (int64_t)a.n_cot * round_up(a.npix, 8 * MVBEV_MASK_GROUP) : tiles;
   a.nwg = (int)nwg;
@@ -1964,10 +1975,10 @@ int mvbev_wino_rows_split_bf16_dil(const void* x, const mvbev_conv_desc* desc, i
 }
 
 int mvbev_conv3x3_wino_bf16x3(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,
-                              const float* init, int64_t Cout, int relu, void* y, int y_layout,
+                              const float* init, int64_t Cout, int relu, void* y, int y_layout, int64_t y_band_rows,
                               const uint32_t* group_mask, const int32_t* tile_order, void* stream) {
   return mvbev::b3::wino_launch(t, desc, w_packed, bias, init, Cout, relu, static_cast<float*>(y), y_layout,
-                                group_mask, tile_order, stream);
+                                group_mask, tile_order, stream, 1, nullptr, nullptr, y_band_rows);
 }
 
 int mvbev_conv3x3_wino_bf16x3_dil(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,

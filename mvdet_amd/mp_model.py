@@ -1,0 +1,145 @@
+"""Per-mode cost model of the view-parallel multi-GPU path.
+
+One frame's views shard over P ranks (rank r owns views v % P == r, ``parallel.views_of``);
+the three exchange forms of ``parallel`` differ in what crosses xGMI and in how much of the
+fusion each rank repeats:
+
+* ``bands``   — every rank warps its views over the whole grid; an all-to-all delivers to rank p
+  the input rows of its output band + the 7-row halo of the dilation-1/2/4 chain (``:51-54``); each
+  rank transforms and convolves a band of ``ceil(Ho/P) + 12`` conv1 rows (12-row tiles).
+* ``partial`` — every rank warps its views straight into conv1's row transform and runs conv1 over
+  its OWN views' channels for the whole grid (conv1 is linear in its input channels); the
+  [B, 512, Ho, Wo] fp32 partial sums are reduce-scattered by row band; conv2 / conv3 on the band.
+* ``gather``  — the slab is all-gathered (``N * C * Ho * Wo`` fp32 to every rank), then the band
+  fusion of ``bands``.
+
+Per rank and frame the compute stream runs produce + consume, the exchange runs on a side stream
+(``parallel.FramePipeline``), so a pipelined frame costs ``max(produce + consume, exchange)``; the
+slowest rank sets the rate.  Compute times scale the measured single-GPU stage times of the same
+config (``SINGLE_GPU_MS``, from ``bench.py`` lines) by the work a rank does: conv1 by its share of
+the frustum-active (12 x 32 tile, view) pairs, computed here from the geometry exactly as the conv's
+mask is; conv2 / the transform by rows.  Link model (an assumption until the 8-GPU node measures
+it): each of a GPU's 7 xGMI links carries ``LINK_GBS`` per direction; an all-to-all puts each
+peer's chunk on its own link; RCCL's ring collectives (reduce-scatter, all-gather) reach
+``COLL_EFF`` of the links' sum.  The model picks ``bench.py --gpus N``'s ``value`` mode per config.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Sequence
+
+import numpy as np
+
+LINK_GBS = 64.0     # effective GB/s per xGMI link and direction (153.6 GB/s per link both ways, ~83 %)
+COLL_EFF = 0.7      # RCCL ring collectives: fraction of the P - 1 links' sum they sustain
+A2A_EFF = 0.7       # all-to-all: fraction of one link per peer chunk
+
+# Single-GPU stage times (ms, one frame) of the bench's path on 1 x MI355X: warp = fused warp + row
+# transform of every view, conv1 = the Winograd conv kernel (whole grid, frustum-masked), conv2 =
+# Winograd conv2 + conv3 partials (incl. its transform), conv3 = the partials' reduce; transform =
+# mvbev_wino_rows_split_bf16 over the whole slab (measured at cfg2 in round 2, scaled by size).
+# cfg2 / cfg3: profiles/r03f_bench.json; cfg5: profiles/r04 bench.
+SINGLE_GPU_MS: Dict[int, Dict[str, float]] = {
+    2: dict(warp=0.4835, conv1=1.4138, conv2=0.3328, conv3=0.026, transform=0.25),
+    3: dict(warp=5.5234, conv1=21.1706, conv2=4.7972, conv3=0.1092, transform=4.0),
+    5: dict(warp=4.6, conv1=19.0, conv2=7.0, conv3=0.18, transform=2.3),
+}
+
+
+def view_tile_activity(m_norm, src_hw, grid_hw, tile_h: int = 12, tile_w: int = 32) -> np.ndarray:
+    """Per 12 x 32 conv1 tile: 1 where the view's warp can be non-zero in the tile + 1-pixel halo
+    (``mvbev_warp_tile_mask``'s rule: some sample inside the source), from the kornia matrix in
+    float64 (a model input, not the product's mask).  Returns [tiles_y, tiles_x] bool."""
+    H, W = int(src_hw[0]), int(src_hw[1])
+    Ho, Wo = int(grid_hw[0]), int(grid_hw[1])
+    m = np.asarray(m_norm, dtype=np.float64).reshape(3, 3)
+    gy, gx = np.meshgrid((np.arange(Ho) / max(Ho - 1, 1) - 0.5) * 2, (np.arange(Wo) / max(Wo - 1, 1) - 0.5) * 2,
+                         indexing="ij")
+    p = np.stack([gx, gy, np.ones_like(gx)], -1) @ m.T
+    z = p[..., 2]
+    s = np.where(np.abs(z) > 1e-8, 1.0 / (z + 1e-8), 1.0)
+    ix = ((p[..., 0] * s + 1) / 2) * (W - 1)
+    iy = ((p[..., 1] * s + 1) / 2) * (H - 1)
+    inside = (ix > -1) & (ix < W) & (iy > -1) & (iy < H)
+    ty, tx = -(-Ho // tile_h), -(-Wo // tile_w)
+    act = np.zeros((ty, tx), dtype=bool)
+    for a in range(ty):
+        r0, r1 = max(0, a * tile_h - 1), min(Ho, (a + 1) * tile_h + 1)
+        rows = inside[r0:r1]
+        for b in range(tx):
+            act[a, b] = rows[:, max(0, b * tile_w - 1):min(Wo, (b + 1) * tile_w + 1)].any()
+    return act
+
+
+def _tiles(rows: int) -> int:
+    return 12 * math.ceil(rows / 12)
+
+
+def predict(N: int, C: int, grid_hw, B: int, P: int, single: Dict[str, float],
+            activity: Sequence[np.ndarray]) -> Dict[str, dict]:
+    """Predicted per-frame ms of each mode at P ranks (the slowest rank), with its parts."""
+    Ho, Wo = int(grid_hw[0]), int(grid_hw[1])
+    band = math.ceil(Ho / P)
+    vmax = math.ceil(N / P)
+    act = np.stack([a.astype(np.float64) for a in activity])         # [N, ty, tx]
+    tot = act.sum()
+    rows_all = _tiles(Ho)
+    w_view = single["warp"] / N                                      # fused warp + T, per view
+    slab_view = 4.0 * B * C * Ho * Wo                                # bytes of one view's split slab
+    bw = LINK_GBS * 1e6                                              # bytes per ms per link
+    # conv1 over band rows [r0, r0 + rows): the active (tile, view) pairs of those tile rows
+    def conv1_band(r0: int, rows: int, views=None) -> float:
+        t0, t1 = r0 // 12, min(act.shape[1], math.ceil((r0 + rows) / 12))
+        sub = act[:, t0:t1] if views is None else act[list(views), t0:t1]
+        return single["conv1"] * sub.sum() / tot
+    out = {}
+    # -- bands
+    E = min(Ho, band + 14)
+    a2a = vmax * B * C * E * Wo * 4.0 / (A2A_EFF * bw)
+    worst = 0.0
+    for p in range(P):
+        r0 = min(Ho, p * band)
+        y1 = (max(0, r0 - 6), min(Ho, r0 + band + 6))
+        c1 = conv1_band(y1[0], y1[1] - y1[0])
+        c2 = single["conv2"] * _tiles(min(Ho, band + 8)) / rows_all
+        tr = single["transform"] * E / Ho
+        worst = max(worst, c1 + c2 + tr)
+    produce = vmax * w_view * 0.8 + vmax * slab_view * (1 + 14 * P / Ho) / 5e9   # slab warp + window writes
+    out["bands"] = dict(produce=produce, exchange=a2a, consume=worst + single["conv3"] / P,
+                        frame=max(produce + worst, a2a))
+    # -- partial
+    rs_bytes = 4.0 * B * 512 * Ho * Wo
+    rs = rs_bytes * (P - 1) / P / (COLL_EFF * (P - 1) * bw) if P > 1 else 0.0
+    prod = max((w_view * len(vs) + conv1_band(0, Ho, vs)) if vs else 0.0
+               for vs in ([v for v in range(N) if v % P == r] for r in range(P)))
+    cons = single["conv2"] * _tiles(min(Ho, band + 8)) / rows_all + single["conv3"] / P
+    out["partial"] = dict(produce=prod, exchange=rs, consume=cons, frame=max(prod + cons, rs))
+    # -- gather
+    ag = N * slab_view * (P - 1) / P / (COLL_EFF * (P - 1) * bw) if P > 1 else 0.0
+    out["gather"] = dict(produce=vmax * w_view * 0.8, exchange=ag, consume=worst + single["conv3"] / P,
+                         frame=max(vmax * w_view * 0.8 + worst, ag))
+    single_frame = single["warp"] + single["conv1"] + single["conv2"] + single["conv3"]
+    for k, v in out.items():
+        v["speedup_vs_1gpu"] = single_frame / v["frame"]
+    return out
+
+
+def config_inputs(cfg: int):
+    """(N, C, grid, B, per-view activity) of a BASELINE config's synthetic rig."""
+    from . import synthetic
+    from .geometry import kornia_src_norm_from_dst_norm, projection_matrices
+    spec = synthetic.CONFIGS[cfg]
+    ds = spec["make"]()
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    acts = [view_tile_activity(kornia_src_norm_from_dst_norm(M.float().reshape(1, 3, 3), up, grid)[0].numpy(),
+                               up, grid) for M in projection_matrices(ds)]
+    return ds.num_cam, spec["C"], grid, spec["B"], acts
+
+
+def choose_mode(cfg: int, P: int) -> str:
+    """The strong-scaling mode with the smallest predicted frame time at P ranks."""
+    if P <= 1 or cfg not in SINGLE_GPU_MS:
+        return "bands"
+    N, C, grid, B, acts = config_inputs(cfg)
+    pred = predict(N, C, grid, B, P, SINGLE_GPU_MS[cfg], acts)
+    return min(pred, key=lambda k: pred[k]["frame"])

@@ -607,11 +607,13 @@ def warp_views_wino_rows_into(srcs, m_norms, t: torch.Tensor, slots, Cs: int, K:
 def conv3x3_wino(t: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: Optional[torch.Tensor] = None,
                  init: Optional[torch.Tensor] = None, relu: bool = False, out: Optional[torch.Tensor] = None,
                  group_mask: Optional[torch.Tensor] = None,
-                 tile_order: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 tile_order: Optional[torch.Tensor] = None, band_rows: int = 0) -> torch.Tensor:
     """The dilation-1 3x3 conv of ``conv3x3_desc`` from its row-Winograd transform ``t``
     (``wino_rows``) with ``PackedConv3x3(..., wino=True)`` weights: ``mvbev_conv3x3_wino_bf16x3``.
     ``out``: fp32 [B, cout, out_rows, W] or split-bf16 (``split_shape``); mask / order as the
-    12 x 32 grid tiles of ``conv3x3_desc``."""
+    12 x 32 grid tiles of ``conv3x3_desc``.  ``band_rows`` > 0: ``out`` is fp32 in row bands,
+    contiguous [bands, B, cout, band_rows, W] with bands * band_rows >= out_rows (computed row r at
+    band r // band_rows) — the partial-sum mode's reduce-scatter input, written in place."""
     _require_cuda(t, packed)
     B, W, out_rows = desc.B, desc.W, desc.out_rows
     lib = _native.load()
@@ -620,7 +622,12 @@ def conv3x3_wino(t: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
     if t.numel() * t.element_size() < wino_rows_bytes(desc):
         raise ValueError("t is smaller than the descriptor's row-Winograd transform")
     y_split = out is not None and out.dtype == torch.bfloat16
-    if out is None:
+    if band_rows:
+        nb = -(-out_rows // band_rows)
+        if (out is None or out.dim() != 5 or out.shape[0] < nb or tuple(out.shape[1:]) != (B, cout, band_rows, W)
+                or out.dtype != torch.float32 or not out.is_contiguous()):
+            raise ValueError(f"a banded out must be a contiguous fp32 [>={nb},{B},{cout},{band_rows},{W}] tensor")
+    elif out is None:
         out = torch.empty((B, cout, out_rows, W), dtype=torch.float32, device=t.device)
     elif y_split:
         if tuple(out.shape) != split_shape(B, cout, out_rows, W) or not out.is_contiguous():
@@ -647,7 +654,7 @@ def conv3x3_wino(t: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
     st = lib.mvbev_conv3x3_wino_bf16x3(t.data_ptr(), ctypes.byref(desc), packed.data_ptr(), bp,
                                        init.data_ptr() if init is not None else None, cout, int(bool(relu)),
                                        out.data_ptr(), _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32,
-                                       gmp, top, _stream(t))
+                                       int(band_rows), gmp, top, _stream(t))
     _native.check(st, "mvbev_conv3x3_wino_bf16x3")
     return out
 

@@ -265,20 +265,42 @@ class ViewBands(_ViewSharded):
         return self.gather_map(band)
 
 
+def balanced_views(weights: Sequence[float], world: int) -> List[List[int]]:
+    """Views to ranks by longest-processing-time first: each view (heaviest first, by its conv1
+    work ``weights[v]``, e.g. its frustum-active tile fraction) to the rank with the least work so far
+    (ties: the lower rank); a deterministic function of the geometry, so every rank computes the same
+    assignment.  Each rank's list is in view order."""
+    load = [0.0] * world
+    out: List[List[int]] = [[] for _ in range(world)]
+    for v in sorted(range(len(weights)), key=lambda v: (-weights[v], v)):
+        r = min(range(world), key=lambda q: (load[q], q))
+        out[r].append(v)
+        load[r] += weights[v]
+    return [sorted(vs) for vs in out]
+
+
 class ViewPartialSum(_ViewSharded):
     """Partial-sum view-parallel fusion: conv1 split by views, reduce-scatter by rows.
 
-    The engine of rank r holds only r's views (``all_views=False`` slab); a rank with no
-    view contributes zeros.  After the reduce-scatter, rank r owns the summed conv1
-    pre-activation of rows ``[r*band, (r+1)*band)``; its halo rows (6 above and below:
-    conv2's dilation 2 + conv3's 4) come from the neighbours' bands through one small
-    all-gather of every band's top and bottom 6 rows (bands of fewer than 6 rows fall back
-    to gathering whole bands)."""
+    The engine of rank r holds only r's views (``all_views=False``); its warp writes conv1's row
+    transform straight from the features (the fused warp + B^T: no slab, no transform pass) and
+    conv1 over those views' channels writes its [B, 512, Ho, Wo] partial sums band-major, straight
+    into the reduce-scatter's input (no staging copy).  A rank with no view contributes zeros.
+    After the reduce-scatter rank r owns the summed conv1 pre-activation of rows
+    ``[r*band, (r+1)*band)``; its halo rows (6 above and below: conv2's dilation 2 + conv3's 4)
+    come from the neighbours' bands through one small all-gather of every band's top and bottom 6
+    rows (bands of fewer than 6 rows fall back to gathering whole bands).  ``view_weights``
+    (optional): per-view conv1 work; views are then dealt by ``balanced_views`` instead of v % P
+    (fewer ranks than views: the frustum makes views' conv1 work uneven, 0.35-0.9 of a full view
+    on the synthetic Wildtrack rig)."""
 
     HALO = 6
 
-    def __init__(self, engine_factory, proj_mats, grid_hw, rank, world, group=None):
+    def __init__(self, engine_factory, proj_mats, grid_hw, rank, world, group=None,
+                 view_weights: Optional[Sequence[float]] = None):
         super().__init__(proj_mats, grid_hw, rank, world, group)
+        if view_weights is not None:
+            self.my_views = balanced_views(view_weights, world)[rank]
         self.engine = engine_factory(self.my_views, all_views=False) if self.my_views else None
         # a rank without views still runs the band fusion: give it an engine over view 0's
         # slot layout (its slab is never written or read) for the packed conv2 weights etc.
@@ -286,8 +308,6 @@ class ViewPartialSum(_ViewSharded):
         for e in (self.engine, self._fuse_engine):  # the exchange sums fp32 partials into y1
             if e is not None and hasattr(e, "y1_split"):
                 e.y1_split = False
-            if e is not None and hasattr(e, "wino_warp"):
-                e.wino_warp = False  # conv1_partial reads the slab
         self._local_ws = {}
 
     def _make_frame(self, B, device, tag):
@@ -302,33 +322,26 @@ class ViewPartialSum(_ViewSharded):
         e = min(self.HALO, n)
         return SimpleNamespace(
             ws=ws, B=B, device=device,
-            part=torch.zeros((B, mid, H, W), dtype=torch.float32, device=device),
             stage=torch.zeros((P, B, mid, n, W), dtype=torch.float32, device=device),
             mine=torch.zeros((B, mid, n, W), dtype=torch.float32, device=device),
             edges=torch.zeros((P, 2, B, mid, e, W), dtype=torch.float32, device=device),
             full=None if n >= self.HALO else torch.zeros((P, B, mid, n, W), dtype=torch.float32, device=device))
 
     def produce(self, fr, feats, map_classifier=None, mark=None) -> None:
-        """Warp this rank's views, conv1 over their channels (all rows), band-major staging."""
+        """Warp this rank's views (into conv1's T where the engine fuses it), then conv1 over their
+        channels for all rows, written band-major into the reduce-scatter's input."""
         if self.engine is None:
-            fr.part.zero_()
+            fr.stage.zero_()
+            return
+        lws = self._local_ws[(str(fr.device), fr.B)]
+        if hasattr(self.engine, "warp_views"):
+            self.engine.warp_views(lws, self.my_views, list(feats))
         else:
-            lws = self._local_ws[(str(fr.device), fr.B)]
-            if hasattr(self.engine, "warp_views"):
-                self.engine.warp_views(lws, self.my_views, list(feats))
-            else:
-                for v, f in zip(self.my_views, feats):
-                    self.engine.warp_view(lws, v, f)
-            if mark:
-                mark("conv1")
-            self.engine.conv1_partial(lws, map_classifier, fr.part, mark=mark)
+            for v, f in zip(self.my_views, feats):
+                self.engine.warp_view(lws, v, f)
         if mark:
-            mark("stage_bands")
-        H, n = self.grid_hw[0], self.band_rows
-        for p in range(self.world):  # band-major staging for the reduce-scatter
-            a, b = min(H, p * n), min(H, (p + 1) * n)
-            if b > a:
-                fr.stage[p, :, :, :b - a].copy_(fr.part[:, :, a:b])
+            mark("conv1")
+        self.engine.conv1_partial(lws, map_classifier, fr.stage, mark=mark, band_rows=self.band_rows)
 
     def exchange(self, fr) -> None:
         """Reduce-scatter of the partial sums by band, then the halo rows into ``ws.y1``."""
@@ -439,7 +452,7 @@ def bench_main(args) -> None:
     import numpy as np
 
     from bench import BF16_MFMA_PEAK_TFS, DTYPE_LABEL, FP32_MFMA_PEAK_TFS, build_mc, head_params
-    from . import synthetic
+    from . import mp_model, synthetic
     from .geometry import projection_matrices
     from .pipeline import ProjectFuse
 
@@ -524,7 +537,10 @@ def bench_main(args) -> None:
                 act_eng, act_rows = eng, y1r
             else:
                 cls = {"bands": ViewBands, "gather": ViewParallel, "partial": ViewPartialSum}[mode]
-                vp = cls(s.fact, s.pm, s.grid, rank, world)
+                kw = {}
+                if mode == "partial":  # views dealt by their conv1 work (the frustum-active tile fraction)
+                    kw["view_weights"] = [float(a.mean()) for a in mp_model.config_inputs(cfg)[4]]
+                vp = cls(s.fact, s.pm, s.grid, rank, world, **kw)
                 feats = feats_for(s, vp.my_views, cfg)
                 pipe = FramePipeline(vp, s.B, dev)
                 for _ in range(W):
@@ -569,7 +585,14 @@ def bench_main(args) -> None:
                                            "2*B*rows*Wo*9*(views*C)*512 over conv1's event time (dense, no mask)"}
         return res
 
-    mode = getattr(args, "mp_mode", "bands")
+    mode = getattr(args, "mp_mode", "auto")
+    predicted = None
+    if mode == "auto":  # the mode the cost model predicts fastest at this config and world size
+        N, C, grid, B, acts = mp_model.config_inputs(args.config)
+        if args.config in mp_model.SINGLE_GPU_MS:
+            predicted = {k: round(v["frame"], 4) for k, v in
+                         mp_model.predict(N, C, grid, B, world, mp_model.SINGLE_GPU_MS[args.config], acts).items()}
+        mode = mp_model.choose_mode(args.config, world)
     hows = {"frames": f"frame-parallel x{world}: each rank its own frame batch (all views), no collective",
             "bands": f"view-parallel x{world} ({backend}): rank r warps views v%{world}==r, RCCL all-to-all of "
                      "each output band's input row window (+7-row halo), row-band fusion, map-band all-gather; "
@@ -593,7 +616,8 @@ def bench_main(args) -> None:
                 alts[m] = run_alt(m, args.config)
         ns = getattr(args, "north_star_cfg", 3)
         if ns and ns != args.config:
-            alts[f"north_star_cfg{ns}"] = run_alt("bands", ns)
+            ns_mode = mp_model.choose_mode(ns, world)
+            alts[f"north_star_cfg{ns}"] = dict(run_alt(ns_mode, ns), mode=ns_mode)
     if rank == 0:
         cpu = None
         if not getattr(args, "no_cpu_baseline", False):
@@ -629,6 +653,9 @@ def bench_main(args) -> None:
             # gloo with ranks sharing the devices (fewer GPUs than ranks): a rehearsal of the path, not a
             # multi-GPU measurement
             "rehearsal": backend != "nccl",
+            "mode": mode,
+            # mp_model's predicted per-frame ms of each view-parallel mode and what it chose
+            "predicted_frame_ms": predicted,
         }
         if cpu:
             line["speedup_vs_cpu"] = round(res["value"] / cpu["value"], 1)
@@ -638,7 +665,8 @@ def bench_main(args) -> None:
             ns_key = m.startswith("north_star")
             key = m if ns_key else ("frame_parallel" if m == "frames" else f"view_parallel_{m}")
             if "error" not in r:
-                r = dict(r, parallelism=hows["bands" if ns_key else m], scaling="weak" if m == "frames" else "strong")
+                r = dict(r, parallelism=hows[r.get("mode", "bands") if ns_key else m],
+                         scaling="weak" if m == "frames" else "strong")
             line[key] = r
         print(json.dumps(line), flush=True)
     dist.barrier()

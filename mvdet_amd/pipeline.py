@@ -553,12 +553,12 @@ class ProjectFuse:
 
     # -- partial-sum multi-GPU (SURVEY §8(e) alternative, §8(f) row 3) -----------------------
     def conv1_partial(self, ws: Workspace, map_classifier: torch.nn.Sequential, out: torch.Tensor,
-                      mark=None) -> torch.Tensor:
-        """conv1 restricted to this slab's views (its slice of conv1's input channels), all
-        grid rows, no bias / coord term / ReLU: one rank's term of conv1's channel sum
-        (row-Winograd where ``wino_active``).  ``out``: contiguous [B, 512, Ho, Wo] fp32."""
-        if ws.t_from_warp:
-            raise RuntimeError("conv1_partial reads the slab, but the fused warp wrote conv1's row transform")
+                      mark=None, band_rows: int = 0) -> torch.Tensor:
+        """conv1 restricted to this engine's views (its slice of conv1's input channels), all grid
+        rows, no bias / coord term / ReLU: one rank's term of conv1's channel sum (row-Winograd
+        where ``wino_active``; from the fused warp's T when ``warp_views`` wrote it, else from the
+        slab).  ``out``: contiguous fp32 [B, 512, Ho, Wo], or with ``band_rows`` > 0 the
+        reduce-scatter's band-major [bands, B, 512, band_rows, Wo] (written in place)."""
         if ws.slab_rows != (0, self.grid_hw[0]):
             raise ValueError("conv1_partial needs a whole-grid slab")
         H, W = self.grid_hw
@@ -572,14 +572,23 @@ class ProjectFuse:
             need = ops.wino_rows_bytes(d1)
             if ws.wino_t is None or ws.wino_t.numel() * 2 < need:
                 ws.wino_t = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=ws.slab.device)
-            ops.wino_rows(ws.slab, d1, ws.wino_t, gm)
+            if not ws.t_from_warp:  # else the fused warp wrote T (no slab, no transform)
+                ops.wino_rows(ws.slab, d1, ws.wino_t, gm)
             if mark:
                 mark("conv1_wino")
             return ops.conv3x3_wino(ws.wino_t, d1, self.pack1w.get(w1), self.mid, init=None, relu=False, out=out,
-                                    group_mask=gm, tile_order=order)
-        return ops.conv3x3_desc(ws.slab, d1, self.pack1.get(w1), self.mid, bias=None, init=None, dilation=1,
-                                relu=False, out=out, workspace=None if gm is not None else self._sk_ws(d1, ws.slab.device),
-                                group_mask=gm, tile_order=order)
+                                    group_mask=gm, tile_order=order, band_rows=band_rows)
+        if ws.t_from_warp:
+            raise RuntimeError("the direct conv1 reads the slab, but the fused warp wrote conv1's row transform")
+        full = out if not band_rows else torch.empty((B, self.mid, H, W), dtype=torch.float32, device=out.device)
+        ops.conv3x3_desc(ws.slab, d1, self.pack1.get(w1), self.mid, bias=None, init=None, dilation=1,
+                         relu=False, out=full, workspace=None if gm is not None else self._sk_ws(d1, ws.slab.device),
+                         group_mask=gm, tile_order=order)
+        if band_rows:  # the direct conv has no banded epilogue: copy the bands
+            for p in range(-(-H // band_rows)):
+                a, b = p * band_rows, min(H, (p + 1) * band_rows)
+                out[p, :, :, :b - a].copy_(full[:, :, a:b])
+        return out
 
     def finish_from_y1(self, ws: Workspace, map_classifier: torch.nn.Sequential, mark=None) -> torch.Tensor:
         """``ws.y1`` holds conv1's summed channel terms (no bias) for rows ``ws.y1_rows``:

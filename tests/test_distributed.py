@@ -49,12 +49,18 @@ class OracleEngine:
         return self._ws[key]
 
     # partial-sum mode: conv1 over this slab's views only, then the band fusion from summed y1
-    def conv1_partial(self, ws, mc, out, mark=None):
+    def conv1_partial(self, ws, mc, out, mark=None, band_rows=0):
         w1 = self.params["map_classifier.0.weight"]
-        out.zero_()
+        H = self.grid_hw[0]
+        full = torch.zeros(ws.slab.shape[1], w1.shape[0], H, self.grid_hw[1])
         for s, v in enumerate(self.slot_views):
             if v is not None:
-                out += torch.nn.functional.conv2d(ws.slab[s], w1[:, v * self.C:(v + 1) * self.C], padding=1)
+                full += torch.nn.functional.conv2d(ws.slab[s], w1[:, v * self.C:(v + 1) * self.C], padding=1)
+        if not band_rows:
+            return out.copy_(full)
+        for p in range(-(-H // band_rows)):  # the band-major layout of ProjectFuse.conv1_partial
+            a, b = p * band_rows, min(H, (p + 1) * band_rows)
+            out[p, :, :, :b - a] = full[:, :, a:b]
         return out
 
     def finish_from_y1(self, ws, mc, mark=None):
@@ -104,12 +110,13 @@ def _case():
 MODES = {"gather": parallel.ViewParallel, "partial": parallel.ViewPartialSum, "bands": parallel.ViewBands}
 
 
-def _worker(rank, world, port, out_dir, mode="gather", frames=1):
+def _worker(rank, world, port, out_dir, mode="gather", frames=1, weights=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
     pm, up, grid, C, B, feats, params = _case()
-    vp = MODES[mode](lambda sv, **kw: OracleEngine(pm, up, grid, C, params, sv, **kw), pm, grid, rank, world)
+    kw = {} if weights is None else {"view_weights": weights}
+    vp = MODES[mode](lambda sv, **kw: OracleEngine(pm, up, grid, C, params, sv, **kw), pm, grid, rank, world, **kw)
     with torch.no_grad():
         if frames == 1:
             outs = [vp.step(vp.workspace(B, "cpu"), [feats[v] for v in vp.my_views], None)]
@@ -190,3 +197,33 @@ def test_band_windows_cover_each_band():
                 r0, r1 = 0, 1
             assert 0 <= lo and hi <= H and hi - lo == vb.E
             assert lo <= max(0, r0 - 7) and min(H, r1 + 7) <= hi
+
+
+def test_balanced_views_assignment():
+    """Longest-processing-time dealing of views to ranks by their conv1 work (partial-sum mode)."""
+    w = [0.37, 0.73, 0.82, 0.6, 0.58, 0.9, 0.82]
+    for P in (2, 3, 4, 7, 8):
+        a = parallel.balanced_views(w, P)
+        assert sorted(v for vs in a for v in vs) == list(range(7)) and len(a) == P
+        loads = [sum(w[v] for v in vs) for vs in a]
+        mod = [sum(w[v] for v in parallel.views_of(r, P, 7)) for r in range(P)]
+        assert max(loads) <= max(mod) + 1e-12
+    assert parallel.balanced_views(w, 7) == [[5], [2], [6], [1], [3], [4], [0]]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_partial_mode_balanced_assignment_matches_oracle(world, tmp_path):
+    """The partial-sum mode with views dealt by their conv1 work (``view_weights``): same map."""
+    weights = [0.2, 0.9, 0.5]
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, str(tmp_path), "partial", 1, weights), nprocs=world, join=True)
+    pm, up, grid, C, B, feats, params = _case()
+    with torch.no_grad():
+        ref = cpu_path.project_fuse(feats, pm, grid, params)
+    assigned = []
+    for r in range(world):
+        res = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
+        assert res["views"] == parallel.balanced_views(weights, world)[r]
+        assigned += res["views"]
+        torch.testing.assert_close(res["outs"][0], ref, rtol=1e-5, atol=1e-6)
+    assert sorted(assigned) == [0, 1, 2]

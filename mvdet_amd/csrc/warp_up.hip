@@ -17,6 +17,8 @@
 // 1/9 of the upsampled size) and 9 FMAs.
 #include "warp_common.h"
 
+#include <cstdlib>
+
 namespace mvbev {
 
 struct UpArgs {
@@ -285,6 +287,181 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino_kernel
   wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
 }
 
+// Round 4 form of warp_up_wino_kernel (it was VALU / LDS-issue bound, 9
+// ds_read_b32 + 12 FMAs per channel and sample).  Changes: (1) the staged box is stored channel-pair
+// interleaved, stage2[pair][row][col] = {channel 2p, channel 2p + 1}, so one ds_read_b64 serves two
+// channels of a window tap and the separable 3x3 window is evaluated on f32x2 (v_pk_fma_f32): per
+// sample 36 ds_read_b64 + 48 packed FMAs instead of 72 ds_read_b32 + 96 FMAs, the same fp32
+// operations per channel in the same order (bitwise the old kernel's T); (2) a block takes G
+// consecutive 8-channel groups, so the sample geometry (warp coordinates, upsample taps, the 3x3
+// window's weights and LDS offsets) and the block's source box are computed once for G groups.
+template <int G>
+__global__ __launch_bounds__(kWwThreads) __attribute__((amdgpu_waves_per_eu(G == 1 ? 8 : 6, 8))) void warp_up_wino2_kernel(const UpArgs ua, int r3_rows,
+                                                                                  int cgroups) {
+  __shared__ __attribute__((aligned(16))) float ds[kWwRows][kWwCols][8];
+  __shared__ unsigned char nz[kWwRows][kWwCols];
+  __shared__ __attribute__((aligned(16))) f32x2_t stage2[4 * (kUpStage > 0 ? kUpStage : 1)];
+  __shared__ int box[4];
+  const WarpArgs& a = ua.w;
+  const int lb = xcd_remap(blockIdx.x, a.nwg);
+  const int tile = lb % a.tiles;
+  const int cg = (lb / a.tiles) % cgroups;
+  const int bv = lb / (a.tiles * cgroups);
+  const int view = bv % a.nviews;
+  const int b = bv / a.nviews;
+  const WarpView& vw = a.v[view];
+  const int k = tile / a.tiles_x, tx = tile - k * a.tiles_x;
+  const int H = a.H, W = a.W, h = ua.h, w = ua.sw;
+  const int tid = threadIdx.x;
+  const int i = tid / kWwCols, c = tid % kWwCols;
+  const int v = 12 * k - 1 + i, u = tx * kWwCols + c;
+  const bool live = i < kWwRows && v >= 0 && v < a.Ho && u < a.Wo;
+  if (tid == 0) {
+    box[0] = INT32_MAX;
+    box[1] = -1;
+    box[2] = INT32_MAX;
+    box[3] = -1;
+  }
+  UpWindow uw;
+  uw.inside = false;
+  uw.finite = true;
+  if (live) {
+    float m[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) m[q] = vw.m[q];
+    uw = up_window(m, u, v, a.Ho, a.Wo, H, W, h, w, ua.sy, ua.sx);
+  }
+  __syncthreads();
+  if (kUpStage > 0) {
+    int r0 = uw.inside ? uw.rb : INT32_MAX, r1 = uw.inside ? min(uw.rb + 2, h - 1) : -1;
+    int q0 = uw.inside ? uw.cb : INT32_MAX, q1 = uw.inside ? min(uw.cb + 2, w - 1) : -1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      r0 = min(r0, __shfl_xor(r0, o));
+      r1 = max(r1, __shfl_xor(r1, o));
+      q0 = min(q0, __shfl_xor(q0, o));
+      q1 = max(q1, __shfl_xor(q1, o));
+    }
+    if ((tid & 63) == 0 && r1 >= 0) {
+      atomicMin(&box[0], r0);
+      atomicMax(&box[1], r1);
+      atomicMin(&box[2], q0);
+      atomicMax(&box[3], q1);
+    }
+  }
+  __syncthreads();
+  const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
+  const bool quad_ok = (w & 3) == 0 && (vw.sH & 3) == 0 && (vw.sC & 3) == 0 &&
+                       (reinterpret_cast<uintptr_t>(base) & 15) == 0;
+  const StageBox sb = stage_box_shape(box, w, quad_ok);
+  const int R = sb.R, Cb = sb.pitch, n = R * Cb;
+  const bool staged = kUpStage > 0 && box[1] >= 0 && n <= kUpStage;  // uniform per block
+  // the window's LDS base offset (staged): rows / columns clamped like the window's
+  const int rb0 = uw.rb - box[0], cb0 = uw.cb - sb.c0;
+  const bool any = live && (uw.inside || !uw.finite);
+#pragma unroll 1
+  for (int gi = 0; gi < G; ++gi) {
+    const int chunk = cg * G + gi;
+    const int c_begin = chunk * kUpCPB;
+    if (c_begin >= a.C) break;  // uniform
+    const int c_end = min(a.C, c_begin + kUpCPB);
+    if (gi > 0) __syncthreads();  // the previous group's phase 2 is done with ds / stage2
+    if (staged) {  // the box of the group's 8 channels, channel-pair interleaved
+      if (sb.quad) {
+        const int Q = Cb >> 2, items = R * Q;
+        for (int it = tid; it < items; it += kWwThreads) {
+          const int r = it / Q, q = it - r * Q;
+          const float* src = base + (int64_t)(sb.r0 + r) * vw.sH + sb.c0 + 4 * q;
+          f32x4a_t t[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            t[j] = *reinterpret_cast<const f32x4a_t*>(src + (int64_t)min(c_begin + j, c_end - 1) * vw.sC);
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            f32x4a_t* dst = reinterpret_cast<f32x4a_t*>(stage2 + p * n + r * Cb + 4 * q);
+            dst[0] = f32x4a_t{t[2 * p][0], t[2 * p + 1][0], t[2 * p][1], t[2 * p + 1][1]};
+            dst[1] = f32x4a_t{t[2 * p][2], t[2 * p + 1][2], t[2 * p][3], t[2 * p + 1][3]};
+          }
+        }
+      } else {
+        for (int r = tid / 32; r < R; r += kWwThreads / 32)
+          for (int cc = tid % 32; cc < Cb; cc += 32) {
+            float t[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              t[j] = base[(int64_t)min(c_begin + j, c_end - 1) * vw.sC + (int64_t)(sb.r0 + r) * vw.sH + sb.c0 + cc];
+#pragma unroll
+            for (int p = 0; p < 4; ++p) stage2[p * n + r * Cb + cc] = f32x2_t{t[2 * p], t[2 * p + 1]};
+          }
+      }
+      __syncthreads();
+    }
+    if (i < kWwRows) {
+      float d[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[j] = 0.f;
+      if (live) {
+        if (!uw.inside) {
+          if (!uw.finite) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = c_begin + j < c_end ? __builtin_nanf("") : 0.f;
+          }
+        } else if (staged) {
+          int idx[3][3];
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+              idx[r][q] = (min(uw.rb + r, h - 1) - uw.rb + rb0) * Cb + (min(uw.cb + q, w - 1) - uw.cb + cb0);
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const f32x2_t* sp = stage2 + p * n;
+            f32x2_t acc = {0.f, 0.f};
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+              f32x2_t rr = {0.f, 0.f};
+#pragma unroll
+              for (int q = 0; q < 3; ++q) rr += uw.ax[q] * sp[idx[r][q]];
+              acc += uw.ay[r] * rr;
+            }
+            d[2 * p] = c_begin + 2 * p < c_end ? acc.x : 0.f;
+            d[2 * p + 1] = c_begin + 2 * p + 1 < c_end ? acc.y : 0.f;
+          }
+        } else {
+          const int cb = uw.cb, rb = uw.rb;
+          const int c4 = min(cb, w - 4), sh = cb - c4;
+          float bx[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int kk = j - sh;
+            bx[j] = (kk == 0 ? uw.ax[0] : 0.f) + (kk == 1 ? uw.ax[1] : 0.f) + (kk == 2 ? uw.ax[2] : 0.f);
+          }
+          int64_t off[3];
+#pragma unroll
+          for (int r = 0; r < 3; ++r) off[r] = min(rb + r, h - 1) * vw.sH + c4;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const int ch = min(c_begin + j, c_end - 1);
+            const float* pc = base + (int64_t)ch * vw.sC;
+            float acc = 0.f;
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+              const f32x4u_t q = *reinterpret_cast<const f32x4u_t*>(pc + off[r]);
+              acc += uw.ay[r] * (bx[0] * q.x + bx[1] * q.y + bx[2] * q.z + bx[3] * q.w);
+            }
+            d[j] = c_begin + j < c_end ? acc : 0.f;
+          }
+        }
+      }
+      *reinterpret_cast<f32x4a_t*>(&ds[i][c][0]) = f32x4a_t{d[0], d[1], d[2], d[3]};
+      *reinterpret_cast<f32x4a_t*>(&ds[i][c][4]) = f32x4a_t{d[4], d[5], d[6], d[7]};
+      if (gi == 0) nz[i][c] = any;
+    }
+    __syncthreads();
+    wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
+  }
+}
+
 // The exact-order warp (a5) and upsample + warp (a4 + a5): the non-finite guard's path
 // (mvbev_warp_views_exact_f32).  Per output pixel the kornia coordinates (warp_coord), then, per
 // in-bounds corner, the source value — with UP, PyTorch's bilinear upsample of that upsampled pixel
@@ -443,6 +620,21 @@ extern "C" int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views
   ua.h = (int)h; ua.sw = (int)w;
   ua.sy = (float)h / (float)H;
   ua.sx = (float)w / (float)W;
+  // A/B selection of the round-4 form (MVBEV_UPW_G = groups per block; 0 = the round-3 kernel)
+  static const int kG = [] {
+    const char* e = getenv("MVBEV_UPW_G");
+    return e ? atoi(e) : 1;
+  }();
+  if (kG == 1 || kG == 2 || kG == 4) {
+    const int cgroups = (int)ceil_div(a.chunks, kG);
+    a.nwg = a.tiles * cgroups * a.B * a.nviews;
+    const dim3 grid((unsigned)a.nwg), block(kWwThreads);
+    if (kG == 1) hipLaunchKernelGGL(warp_up_wino2_kernel<1>, grid, block, 0, as_stream(stream), ua, (int)r3_rows, cgroups);
+    else if (kG == 2) hipLaunchKernelGGL(warp_up_wino2_kernel<2>, grid, block, 0, as_stream(stream), ua, (int)r3_rows, cgroups);
+    else hipLaunchKernelGGL(warp_up_wino2_kernel<4>, grid, block, 0, as_stream(stream), ua, (int)r3_rows, cgroups);
+    MVBEV_CHECK_LAUNCH();
+    return MVBEV_OK;
+  }
   hipLaunchKernelGGL(warp_up_wino_kernel, dim3((unsigned)a.nwg), dim3(kWwThreads), 0, as_stream(stream), ua, (int)r3_rows);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;

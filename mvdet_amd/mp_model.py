@@ -26,7 +26,7 @@ peer's chunk on its own link; RCCL's ring collectives (reduce-scatter, all-gathe
 from __future__ import annotations
 
 import math
-from typing import Dict, Sequence
+from typing import Dict, List, Sequence
 
 import numpy as np
 
@@ -71,6 +71,20 @@ def view_tile_activity(m_norm, src_hw, grid_hw, tile_h: int = 12, tile_w: int = 
     return act
 
 
+def balanced_views(weights: Sequence[float], world: int) -> List[List[int]]:
+    """Views to ranks by longest-processing-time first: each view (heaviest first, by its conv1
+    work ``weights[v]``, e.g. its frustum-active tile fraction) to the rank with the least work so far
+    (ties: the lower rank); a deterministic function of the geometry, so every rank computes the same
+    assignment.  Each rank's list is in view order."""
+    load = [0.0] * world
+    out: List[List[int]] = [[] for _ in range(world)]
+    for v in sorted(range(len(weights)), key=lambda v: (-weights[v], v)):
+        r = min(range(world), key=lambda q: (load[q], q))
+        out[r].append(v)
+        load[r] += weights[v]
+    return [sorted(vs) for vs in out]
+
+
 def _tiles(rows: int) -> int:
     return 12 * math.ceil(rows / 12)
 
@@ -110,8 +124,8 @@ def predict(N: int, C: int, grid_hw, B: int, P: int, single: Dict[str, float],
     # -- partial
     rs_bytes = 4.0 * B * 512 * Ho * Wo
     rs = rs_bytes * (P - 1) / P / (COLL_EFF * (P - 1) * bw) if P > 1 else 0.0
-    prod = max((w_view * len(vs) + conv1_band(0, Ho, vs)) if vs else 0.0
-               for vs in ([v for v in range(N) if v % P == r] for r in range(P)))
+    assign = balanced_views([float(a.mean()) for a in activity], P)  # as parallel.ViewPartialSum deals them
+    prod = max((w_view * len(vs) + conv1_band(0, Ho, vs)) if vs else 0.0 for vs in assign)
     cons = single["conv2"] * _tiles(min(Ho, band + 8)) / rows_all + single["conv3"] / P
     out["partial"] = dict(produce=prod, exchange=rs, consume=cons, frame=max(prod + cons, rs))
     # -- gather

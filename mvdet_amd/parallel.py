@@ -42,6 +42,8 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
+from .mp_model import balanced_views  # noqa: F401  (re-exported: the partial-sum mode's view dealing)
+
 # rows of the ground-plane tensor an output row of conv1 -> conv2 -> conv3 depends on, each side
 HALO_IN = 1 + 2 + 4
 
@@ -263,20 +265,6 @@ class ViewBands(_ViewSharded):
         if mark:
             mark("gather_map")
         return self.gather_map(band)
-
-
-def balanced_views(weights: Sequence[float], world: int) -> List[List[int]]:
-    """Views to ranks by longest-processing-time first: each view (heaviest first, by its conv1
-    work ``weights[v]``, e.g. its frustum-active tile fraction) to the rank with the least work so far
-    (ties: the lower rank); a deterministic function of the geometry, so every rank computes the same
-    assignment.  Each rank's list is in view order."""
-    load = [0.0] * world
-    out: List[List[int]] = [[] for _ in range(world)]
-    for v in sorted(range(len(weights)), key=lambda v: (-weights[v], v)):
-        r = min(range(world), key=lambda q: (load[q], q))
-        out[r].append(v)
-        load[r] += weights[v]
-    return [sorted(vs) for vs in out]
 
 
 class ViewPartialSum(_ViewSharded):

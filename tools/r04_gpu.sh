@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round-4 GPU session: the GPU suite, the bench, then A/B kernel timings (tools/kbench.py, separate
+# processes per variant: the variant selections are read once per process).  Every GPU step has its
+# own time limit; a failure ends the script (set -e) so nothing runs after a fault.
+set -e
+mkdir -p gpurun_out
+TAG=${1:-r04a}
+timeout -k 10 1000 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/ > gpurun_out/${TAG}_pytest.txt 2>&1
+timeout -k 10 360 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
+for g in 0 1 2 4; do
+  MVBEV_UPW_G=$g timeout -k 10 120 python tools/kbench.py --only warpupw --rounds 2 --reps 30 | sed "s/^{/{\"upw_g\": $g, /" >> gpurun_out/${TAG}_kbench.jsonl
+done
+for w in 0 3; do
+  MVBEV_WINO4=$w timeout -k 10 120 python tools/kbench.py --only winoconv,conv23w --rounds 2 --reps 30 | sed "s/^{/{\"wino4\": $w, /" >> gpurun_out/${TAG}_kbench.jsonl
+done

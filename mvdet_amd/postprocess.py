@@ -7,7 +7,13 @@ HIP kernels of ``libmvbev.so`` (``mvbev_threshold_points``, ``mvbev_point_nms_ws
 * ``nms(points, scores, dist_thres=50/2.5, top_k=50) -> (keep, count)``: greedy point NMS.
   Returns ``keep`` alone for empty input, like the reference.  Equal scores are taken in the
   order torch's CPU ``scores.sort(0)`` leaves them (the kernel replays its introsort), so the
-  kept set matches the reference's exactly, ties included.
+  kept set matches the reference's exactly, ties included.  That replay is of the sort the
+  installed torch uses (validated on torch 2.10.0+rocm7.0's CPU ``sort``: libstdc++ ``std::sort``
+  introsort of (score, index) pairs, NaN largest); a torch build with another sort (a stable or
+  radix path, another libstdc++) could order equal scores differently, and
+  ``tests/test_oracle.py::test_sort_order_restatement_matches_torch_cpu_sort`` — which compares the
+  replay with the running torch's own ``sort`` on ties, NaN and introsort's heap-sort fallback —
+  then fails rather than letting the kept set drift silently.
 * ``threshold_rows(map_res, frame, cls_thres, grid_reduce, indexing)``: the (frame, x, y,
   score) rows of ``map_res > cls_thres`` in ``nonzero`` order.
 * ``frame_results(rows, dist_thres=20, top_k=inf)``: per-frame NMS -> (frame, x, y) rows.

@@ -120,7 +120,7 @@ def mfma_probe(settle_s: float = 1.5):
     return v if v > 0 else None
 
 
-def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=None):
+def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=None, layout=None):
     from mvdet_amd import ProjectFuse, synthetic
     from mvdet_amd.geometry import projection_matrices, touched_footprint
 
@@ -145,6 +145,9 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * config + v,
                                           device=dev).to(torch.float16 if half else torch.float32)
              for v in range(N)]
+    layout = layout or args.layout
+    if layout == "channels_last":  # the same logical [B, C, H, W] tensors in torch's channels_last memory format
+        feats = [f.contiguous(memory_format=torch.channels_last) for f in feats]
     ws = eng.workspace(B, dev)
     views = list(range(N))
 
@@ -231,6 +234,7 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
     if tfile.exists():
         tj = json.loads(tfile.read_text())
         traffic, warp_traffic = tj.get("conv1_hbm_bytes_per_launch"), tj.get("warp_hbm_bytes_per_launch")
+        warp_traffic = tj.get("warp_cl_hbm_bytes_per_launch") if layout == "channels_last" else warp_traffic
         traffic_src = (f"{tfile.relative_to(ROOT)}: rocprofv3 PMC passes of this kernel (committed profile, not "
                        f"measured in this run: PMC collection needs its own rocprofv3 runs)")
     res = {
@@ -239,7 +243,7 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
         "dtype": DTYPE_LABEL[precision],
         "config": {"workload": f"cfg{config}: {spec['name']}", "views": N, "channels": C, "batch": B,
                    "src_hw": list(up), "grid_hw": [ho, wo], "precision": precision,
-                   "storage": "fp16" if half else "fp32", "parallelism": "single GPU"},
+                   "storage": "fp16" if half else "fp32", "feature_layout": layout, "parallelism": "single GPU"},
         # achieved/frac = the MFMA work conv1 actually has to do (the frustum-masked products;
         # the skipped ones are exact zeros) over its measured time: the MFMA utilisation.
         # The reference's dense FLOP count over the same time is kept as dense_* (it reads
@@ -502,6 +506,9 @@ def spawn_ranks(n: int) -> int:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--layout", default="nchw", choices=["nchw", "channels_last"],
+                    help="memory format of the view features (the same logical tensors); the other one is "
+                         "reported as a sub-object")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--conv1", default="wino", choices=["direct", "wino"],
@@ -567,6 +574,13 @@ def main():
     }
     if result["cpu_baseline"]:
         result["speedup_vs_cpu"] = round(res["value"] / result["cpu_baseline"]["value"], 1)
+    if args.config != 4 and args.precision == "bf16x3":
+        # the same step on the other feature memory format (channels-last: warp_wino_cl_kernel reads
+        # one 128-B line per source pixel instead of NCHW's per-channel boxes)
+        other_layout = "channels_last" if args.layout == "nchw" else "nchw"
+        ol = run_single(args, args.precision, max(5, args.steps // 2), 2, with_cpu=False, layout=other_layout)
+        result[other_layout] = {k: ol[k] for k in ("value", "ms_per_step", "stages_ms")}
+        result[other_layout]["warp"] = ol["stage_roofline"]["warp"]
     if args.config != 4:  # the fused upsample+warp writes fp32 / split slabs (not the fp16 slab)
         result["plus_a4"] = run_plus_a4(args, args.precision, max(5, args.steps // 2), 2)
     subs = []

@@ -307,6 +307,138 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
   wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
 }
 
+// warp_wino_kernel for channels-last sources (round 4: sC == 1, the [B, C, H, W] tensor in torch's
+// channels_last memory format).  An NCHW source puts each channel's bilinear corners in its own
+// plane: a block of 8 channels fetches 8 boxes of ~20-column rows, whose 128-B lines it reads only
+// partly (2.2x read amplification at cfg2).  Channels-last puts a pixel's channels side by side, so
+// a block takes 32 channels (one 128-B line per source pixel): 8 lanes load a corner's line as
+// 16-B pieces, every fetched byte is used, and the gather needs no staging box.
+// Phase 0: one thread per warped pixel (14 rows x 16 columns) computes its coordinates once (LDS).
+// Phase 1: 8 lanes per pixel, 7 pixels per thread: 4 corner loads each as bounds-checked buffer
+// loads (a corner outside the source reads 0 without a fetch, so the loads are unconditional and
+// the 28 of a thread are in flight together), the bilinear sum into ds[pixel][36] (pitch 36
+// floats: conflict-free 16-B reads in phase 2).  Phase 2: one thread per (tile, column, 8-channel
+// chunk, 4-channel half) applies B^T and stores 8 B of each T row's hi and lo planes.  Same T
+// (same fp32 ops per channel as warp_wino_kernel) for the same logical source.
+constexpr int kWcCh = 32, kWcPitch = 36, kWcPix = kWwRows * kWwCols;
+constexpr int kWcOutside = 0x7fff0000;  // byte offset of "no corner" (sources must stay below it)
+static_assert(kWwCols == 16 && kWwThreads == 256, "channels-last fused warp: 256 threads, 16 columns");
+static_assert(kWcPix % 32 == 0, "phase 1: 32 pixels per pass");
+
+__global__ __launch_bounds__(kWwThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))
+void warp_wino_cl_kernel(const WarpArgs a, int r3_rows) {
+  __shared__ __attribute__((aligned(16))) float ds[kWcPix * kWcPitch];
+  __shared__ float2 crd[kWcPix];
+  __shared__ unsigned char cls[kWcPix];  // 0: exact zero (outside / off the grid), 1: inside, 2: non-finite
+  const int lb = xcd_remap(blockIdx.x, a.nwg);
+  const int tile = lb % a.tiles;
+  const int grp = (lb / a.tiles) % a.chunks;  // 32-channel group
+  const int bv = lb / (a.tiles * a.chunks);
+  const int view = bv % a.nviews, b = bv / a.nviews;
+  const WarpView& vw = a.v[view];
+  const int k = tile / a.tiles_x, tx = tile - k * a.tiles_x;
+  const int tid = threadIdx.x;
+  const int H = a.H, W = a.W;
+  if (tid < kWcPix) {
+    const int i = tid / kWwCols, c = tid % kWwCols;
+    const int v = 12 * k - 1 + i, u = tx * kWwCols + c;
+    unsigned char cl = 0;
+    float ix = 0.f, iy = 0.f;
+    if (v >= 0 && v < a.Ho && u < a.Wo) {
+      float m[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) m[q] = vw.m[q];
+      const WarpCoord wc = warp_coord(m, u, v, a.Ho, a.Wo, H, W);
+      cl = wc.inside ? 1 : (wc.finite ? 0 : 2);
+      ix = wc.ix;
+      iy = wc.iy;
+    }
+    crd[tid] = make_float2(ix, iy);
+    cls[tid] = cl;
+  }
+  __syncthreads();
+  // the batch item's 32-channel group; offsets past its extent read as 0 (no fetch)
+  // (the host checked that the extent is below kOff)
+  const char* gbase = static_cast<const char*>(vw.src) + ((int64_t)b * vw.sB + (int64_t)grp * kWcCh) * 4;
+  const int extent = (int)(((int64_t)(H - 1) * vw.sH + (int64_t)(W - 1) * vw.sW + kWcCh) * 4);
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(gbase), (short)0, extent, 0x00020000);
+  const int qd = tid & 7;
+  const int sH4 = (int)vw.sH * 4, sW4 = (int)vw.sW * 4, q4 = 16 * qd;
+  constexpr int kOff = kWcOutside;  // past the extent: the load returns 0
+#pragma unroll
+  for (int s = 0; s < kWcPix / 32; ++s) {
+    const int p = (tid >> 3) + 32 * s;
+    const int cl = cls[p];
+    const float2 q = crd[p];
+    const float fx0 = floorf(q.x), fy0 = floorf(q.y);
+    const int x0 = cl == 1 ? (int)fx0 : -2, y0 = cl == 1 ? (int)fy0 : -2;
+    const float fx1 = fx0 + 1.f, fy1 = fy0 + 1.f;
+    const float w_nw = (fx1 - q.x) * (fy1 - q.y), w_ne = (q.x - fx0) * (fy1 - q.y);
+    const float w_sw = (fx1 - q.x) * (q.y - fy0), w_se = (q.x - fx0) * (q.y - fy0);
+    const bool vx0 = x0 >= 0, vx1 = x0 + 1 >= 0 && x0 + 1 <= W - 1;
+    const bool vy0 = y0 >= 0, vy1 = y0 + 1 >= 0 && y0 + 1 <= H - 1;
+    const int r0 = y0 * sH4, r1 = r0 + sH4, c0 = x0 * sW4, c1 = c0 + sW4;
+    const f32x4a_t vnw = __builtin_bit_cast(f32x4a_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                          rs, vx0 && vy0 ? r0 + c0 + q4 : kOff, 0, 0));
+    const f32x4a_t vne = __builtin_bit_cast(f32x4a_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                          rs, vx1 && vy0 ? r0 + c1 + q4 : kOff, 0, 0));
+    const f32x4a_t vsw = __builtin_bit_cast(f32x4a_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                          rs, vx0 && vy1 ? r1 + c0 + q4 : kOff, 0, 0));
+    const f32x4a_t vse = __builtin_bit_cast(f32x4a_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                          rs, vx1 && vy1 ? r1 + c1 + q4 : kOff, 0, 0));
+    f32x4a_t acc = {0.f, 0.f, 0.f, 0.f};
+    acc += vnw * w_nw;
+    acc += vne * w_ne;
+    acc += vsw * w_sw;
+    acc += vse * w_se;
+    if (cl != 1) acc = cl == 2 ? f32x4a_t{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""),
+                                          __builtin_nanf("")}
+                               : f32x4a_t{0.f, 0.f, 0.f, 0.f};
+    *reinterpret_cast<f32x4a_t*>(ds + p * kWcPitch + 4 * qd) = acc;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int it = tid + kWwThreads * h;
+    const int half = it & 1, c = (it >> 1) & 15, ch8 = (it >> 5) & 3, q = it >> 7;
+    const int r3 = 4 * k + q, u = tx * kWwCols + c;
+    if (r3 >= r3_rows || u >= a.Wo) continue;
+    const int i0 = 3 * q;
+    if (a.skip_zero && !(cls[i0 * 16 + c] | cls[(i0 + 1) * 16 + c] | cls[(i0 + 2) * 16 + c] |
+                         cls[(i0 + 3) * 16 + c] | cls[(i0 + 4) * 16 + c]))
+      continue;
+    f32x4a_t d[5];
+#pragma unroll
+    for (int m = 0; m < 5; ++m)
+      d[m] = *reinterpret_cast<const f32x4a_t*>(ds + ((i0 + m) * 16 + c) * kWcPitch + 8 * ch8 + 4 * half);
+    f32x4a_t t[5];
+    t[0] = 2.f * d[0] - d[1] - 2.f * d[2] + d[3];
+    t[1] = -2.f * d[1] - d[2] + d[3];
+    t[2] = 2.f * d[1] - 3.f * d[2] + d[3];
+    t[3] = d[3] - d[1];
+    t[4] = 2.f * d[1] - d[2] - 2.f * d[3] + d[4];
+    if (a.nonfinite) {  // as wino_rows_phase2
+      const f32x4a_t sum = (t[0] + t[1]) + (t[2] + t[3]) + t[4];
+      if (!isfinite((sum.x + sum.y) + (sum.z + sum.w))) *a.nonfinite = a.nf_tag;
+    }
+    const int chunk = grp * (kWcCh / 8) + ch8;
+    unsigned* out = reinterpret_cast<unsigned*>(static_cast<u32x4_t*>(vw.dst) +
+                                                (2 * ((int64_t)b * vw.dB + (int64_t)chunk * vw.dC +
+                                                      (int64_t)(5 * r3) * vw.dH) + u)) + 2 * half;
+#pragma unroll
+    for (int xi = 0; xi < 5; ++xi) {
+      const float h0 = (float)(__bf16)t[xi].x, h1 = (float)(__bf16)t[xi].y;
+      const float h2 = (float)(__bf16)t[xi].z, h3 = (float)(__bf16)t[xi].w;
+      unsigned* o = out + (int64_t)xi * vw.dH * 8;
+      typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+      *reinterpret_cast<u32x2_t*>(o) = u32x2_t{pack_bf16x2(h0, h1), pack_bf16x2(h2, h3)};
+      *reinterpret_cast<u32x2_t*>(o + vw.dH * 4) =
+          u32x2_t{pack_bf16x2(t[xi].x - h0, t[xi].y - h1), pack_bf16x2(t[xi].z - h2, t[xi].w - h3)};
+    }
+  }
+}
+
 template <typename T, bool SPLIT>
 static void launch_warp_t(const WarpArgs& a, hipStream_t s) {
   if constexpr (std::is_same<T, float>::value) {
@@ -536,10 +668,21 @@ int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t
   a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
   a.tiles_x = (int)ceil_div(Wo, kWwCols);
   a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);  // 4 three-row tiles per block
-  a.chunks = (int)ceil_div(C, kWarpCPB);
+  // channels-last sources (every view: unit channel stride, 16-B aligned pixels of whole 32-channel
+  // groups, offsets within 31 bits) take the line-per-pixel kernel
+  bool cl = C % kWcCh == 0;
+  for (int i = 0; i < nviews && cl; ++i) {
+    const WarpView& d = a.v[i];
+    cl = d.sC == 1 && d.sW >= C && d.sH > 0 && d.sB >= 0 && d.sW % 4 == 0 && d.sH % 4 == 0 && d.sB % 4 == 0 &&
+         (reinterpret_cast<uintptr_t>(d.src) & 15) == 0 &&
+         ((H - 1) * d.sH + (W - 1) * d.sW + C) * 4 < kWcOutside;
+  }
+  a.chunks = (int)ceil_div(C, cl ? kWcCh : kWarpCPB);
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
   const dim3 grid((unsigned)a.nwg), block(kWwThreads);
-  if (pair)
+  if (cl)
+    hipLaunchKernelGGL(warp_wino_cl_kernel, grid, block, 0, as_stream(stream), a, (int)r3_rows);
+  else if (pair)
     hipLaunchKernelGGL((warp_wino_kernel<true>), grid, block, 0, as_stream(stream), a, (int)r3_rows);
   else
     hipLaunchKernelGGL((warp_wino_kernel<false>), grid, block, 0, as_stream(stream), a, (int)r3_rows);

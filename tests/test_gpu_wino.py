@@ -242,6 +242,44 @@ def test_fused_warp_transform_matches_two_pass(cfg):
     assert_parity(m3.cpu(), ref.cpu(), "slab path after the fused warp", normwise_tol=TOL)
 
 
+@pytest.mark.parametrize("cfg,C,B", [(1, 32, 1), (2, 64, 2), (2, 40, 1)])
+def test_fused_warp_channels_last_matches_nchw(cfg, C, B):
+    """Channels-last sources (sC == 1, C % 32 == 0: warp_wino_cl_kernel, one 128-B line per source
+    pixel) give bit-for-bit the T of the NCHW kernel for the same logical tensor: zero and NaN
+    geometry (one view's matrix made non-finite), an inf feature, the non-finite report and
+    skip_zero included.  C = 40 (not whole 32-channel groups) takes the NCHW kernel with the
+    channels-last strides — the same T again."""
+    from mvdet_amd import ops, synthetic
+    from mvdet_amd.geometry import kornia_src_norm_from_dst_norm, projection_matrices
+    spec = synthetic.CONFIGS[cfg]
+    ds = spec["make"]()
+    N = ds.num_cam
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    ms = [kornia_src_norm_from_dst_norm(M.float().reshape(1, 3, 3), up, grid)[0] for M in projection_matrices(ds)]
+    ms[-1] = ms[-1].clone()
+    ms[-1][0, 2] = float("inf")  # every sample of the last view is non-finite -> NaN T
+    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=71 + v, device=DEV)
+             for v in range(N)]
+    feats[0][B - 1, C - 1, up[0] // 2, up[1] // 2] = float("inf")
+    Ho, Wo = grid
+    r3 = 4 * (-(-Ho // 12))
+    numel = B * (N * C // 8) * 5 * r3 * Wo * 16
+    outs = []
+    for layout in (torch.contiguous_format, torch.channels_last):
+        src = [f.contiguous(memory_format=layout) for f in feats]
+        for zeroed in (False, True):
+            t = torch.zeros(numel, dtype=torch.bfloat16, device=DEV)
+            flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+            ops.warp_views_wino_rows_into(src, ms, t, list(range(N)), C, N * C, Ho, Wo, dst_zeroed=zeroed,
+                                          nonfinite=(flag, 7))
+            outs.append((t.view(torch.int16).cpu(), int(flag.item())))
+    (a, fa), (az, fz), (b, fb), (bz, fbz) = outs
+    assert fa == fz == fb == fbz == 7
+    assert torch.equal(a, az)
+    assert torch.equal(a, b), (a != b).sum().item()
+    assert torch.equal(a, bz)
+
+
 # -- conv2 (dilation 2) -> conv3 partials as row-Winograd (ABI 11500) ------------------------------
 def _conv2_setup(B, K, H, W, rows, cout, seed):
     """y1-like split-bf16 input, conv2 weights / bias, conv3 weight, and the float64 reference

@@ -127,6 +127,7 @@ def main():
     eng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision, frustum=not args.no_frustum,
                       wino_conv1=False, wino_conv2=False)  # the direct conv stages (the Winograd ones use weng)
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=v, device=dev) for v in range(N)]
+    cfeats = [f.contiguous(memory_format=torch.channels_last) for f in feats]
     bfeats = [synthetic.backbone_features(B, C, [u // 3 for u in up], seed=v, device=dev) for v in range(N)]
     ws = eng.workspace(B, dev)
     with torch.no_grad():
@@ -156,6 +157,9 @@ def main():
             "winorows": (lambda: ops.wino_rows(wws.slab, wd1, wws.wino_t, wgm), None),
             "warpw": (lambda: _with(weng, "wino_warp", True, lambda: weng.warp_views(wws, list(range(N)), feats)),
                       None),  # warp + B^T in one pass (wino_warp; leaves T from the warp, run it last)
+            # the same on channels-last features (warp_wino_cl_kernel)
+            "warpwcl": (lambda: _with(weng, "wino_warp", True, lambda: weng.warp_views(wws, list(range(N)), cfeats)),
+                        None),
             "warpupw": (lambda: _with(weng, "wino_warp", True,
                                       lambda: weng.warp_views_upsampled(wws, list(range(N)), bfeats)), None),
             "winoconv": (lambda: ops.conv3x3_wino(wws.wino_t, wd1, weng.pack1w.get(mc[0].weight), 512,

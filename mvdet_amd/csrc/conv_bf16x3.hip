@@ -178,6 +178,13 @@ __device__ inline void store_block(const Args& a, int b, int row, int col, int c
   const bool valid = row < a.out_row0 + a.out_rows && col < W;
   if (!a.y_split) {
     if (!valid) return;
+    // the pixel's address and the channel stride, plain or banded, chosen once (a branch inside the
+    // unrolled loop put the accumulators in scratch)
+    const int rr = row - a.out_row0;
+    const int band = a.band_rows > 0 ? rr / a.band_rows : 0;
+    const int64_t cstride = a.band_rows > 0 ? (int64_t)a.band_rows * W : oplane;
+    float* yp = a.y + ((int64_t)band * a.B + b) * a.Cout * cstride +
+                (int64_t)(a.band_rows > 0 ? rr - band * a.band_rows : rr) * W + col;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = co0 + (r & 3) + 8 * (r >> 2) + 4 * kh;
@@ -185,12 +192,7 @@ __device__ inline void store_block(const Args& a, int b, int row, int col, int c
       if (a.bias) v += a.bias[co];
       if (a.init) v += a.init[co * iplane + (int64_t)row * W + col];
       if (RELU) v = v < 0.f ? 0.f : v;
-      if (a.band_rows > 0) {
-        const int rr = row - a.out_row0, band = rr / a.band_rows;
-        a.y[((((int64_t)band * a.B + b) * a.Cout + co) * a.band_rows + (rr - band * a.band_rows)) * W + col] = v;
-      } else {
-        a.y[((int64_t)b * a.Cout + co) * oplane + (int64_t)(row - a.out_row0) * W + col] = v;
-      }
+      yp[co * cstride] = v;
     }
     return;
   }

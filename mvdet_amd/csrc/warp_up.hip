@@ -17,7 +17,6 @@
 // 1/9 of the upsampled size) and 9 FMAs.
 #include "warp_common.h"
 
-#include <cstdlib>
 
 namespace mvbev {
 
@@ -150,153 +149,15 @@ __global__ __launch_bounds__(kUpTH * kUpTW) void warp_up_kernel(const UpArgs ua)
 // slower: 0.86 vs 0.39 ms at cfg2.)
 constexpr int kUpStage = MVBEV_UPW_STAGE;
 
-__global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino_kernel(const UpArgs ua, int r3_rows) {
-  __shared__ __attribute__((aligned(16))) float ds[kWwRows][kWwCols][8];
-  __shared__ unsigned char nz[kWwRows][kWwCols];
-  __shared__ __attribute__((aligned(16))) float stage[kUpCPB * (kUpStage > 0 ? kUpStage : 1)];
-  __shared__ int box[4];  // source rows [box0, box1], columns [box2, box3] of the block's windows
-  const WarpArgs& a = ua.w;
-  const int lb = xcd_remap(blockIdx.x, a.nwg);
-  const int tile = lb % a.tiles;
-  const int chunk = (lb / a.tiles) % a.chunks;
-  const int bv = lb / (a.tiles * a.chunks);
-  const int view = bv % a.nviews;
-  const int b = bv / a.nviews;
-  const WarpView& vw = a.v[view];
-  const int k = tile / a.tiles_x, tx = tile - k * a.tiles_x;
-  const int c_begin = chunk * kUpCPB;
-  const int c_end = min(a.C, c_begin + kUpCPB);
-  const int H = a.H, W = a.W, h = ua.h, w = ua.sw;
-  const int tid = threadIdx.x;
-  const int i = tid / kWwCols, c = tid % kWwCols;
-  const int v = 12 * k - 1 + i, u = tx * kWwCols + c;
-  const bool live = i < kWwRows && v >= 0 && v < a.Ho && u < a.Wo;
-  if (tid == 0) {
-    box[0] = INT32_MAX;
-    box[1] = -1;
-    box[2] = INT32_MAX;
-    box[3] = -1;
-  }
-  UpWindow uw;
-  uw.inside = false;
-  uw.finite = true;
-  if (live) {
-    float m[9];
-#pragma unroll
-    for (int q = 0; q < 9; ++q) m[q] = vw.m[q];
-    uw = up_window(m, u, v, a.Ho, a.Wo, H, W, h, w, ua.sy, ua.sx);
-  }
-  __syncthreads();
-  if (kUpStage > 0) {  // the box: a shuffle reduction per wave, then one LDS atomic per wave and bound
-    int r0 = uw.inside ? uw.rb : INT32_MAX, r1 = uw.inside ? min(uw.rb + 2, h - 1) : -1;
-    int q0 = uw.inside ? uw.cb : INT32_MAX, q1 = uw.inside ? min(uw.cb + 2, w - 1) : -1;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      r0 = min(r0, __shfl_xor(r0, o));
-      r1 = max(r1, __shfl_xor(r1, o));
-      q0 = min(q0, __shfl_xor(q0, o));
-      q1 = max(q1, __shfl_xor(q1, o));
-    }
-    if ((tid & 63) == 0 && r1 >= 0) {
-      atomicMin(&box[0], r0);
-      atomicMax(&box[1], r1);
-      atomicMin(&box[2], q0);
-      atomicMax(&box[3], q1);
-    }
-  }
-  __syncthreads();
-  const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
-  const bool quad_ok = (w & 3) == 0 && (vw.sH & 3) == 0 && (vw.sC & 3) == 0 &&
-                       (reinterpret_cast<uintptr_t>(base) & 15) == 0;
-  const StageBox sb = stage_box_shape(box, w, quad_ok);  // 16-B staging loads where the source allows
-  const int R = sb.R, Cb = sb.pitch;
-  const bool staged = kUpStage > 0 && box[1] >= 0 && R * Cb <= kUpStage;  // uniform per block
-  if (staged) {  // the box of every channel of the group (16-B loads where the source allows)
-    stage_box_load<kWwThreads>(base, vw.sC, vw.sH, c_begin, c_end, sb, stage, tid);
-    __syncthreads();
-  }
-  if (i < kWwRows) {
-    float d[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] = 0.f;
-    bool any = false;
-    if (live) {
-      if (!uw.inside) {
-        if (!uw.finite) {
-          any = true;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) d[j] = c_begin + j < c_end ? __builtin_nanf("") : 0.f;
-        }
-      } else if (staged) {
-        any = true;
-        const int n = R * Cb;
-        int idx[3][3];
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-          for (int q = 0; q < 3; ++q)
-            idx[r][q] = (min(uw.rb + r, h - 1) - box[0]) * Cb + (min(uw.cb + q, w - 1) - sb.c0);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float* sj = stage + j * n;
-            float acc = 0.f;
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-              float rr = 0.f;
-#pragma unroll
-              for (int q = 0; q < 3; ++q) rr += uw.ax[q] * sj[idx[r][q]];
-              acc += uw.ay[r] * rr;
-            }
-            d[j] = c_begin + j < c_end ? acc : 0.f;
-          }
-      } else {
-        any = true;
-        const int cb = uw.cb, rb = uw.rb;
-        const int c4 = min(cb, w - 4);
-        const int sh = cb - c4;
-        float bx[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int kk = j - sh;
-          bx[j] = (kk == 0 ? uw.ax[0] : 0.f) + (kk == 1 ? uw.ax[1] : 0.f) + (kk == 2 ? uw.ax[2] : 0.f);
-        }
-        int64_t off[3];
-#pragma unroll
-        for (int r = 0; r < 3; ++r) off[r] = min(rb + r, h - 1) * vw.sH + c4;
-        // straight-line over the group's 8 channels (a short last group reads its last channel
-        // again and zeroes the surplus): all 24 window loads issue before the FMAs
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int ch = min(c_begin + j, c_end - 1);
-          const float* pc = base + (int64_t)ch * vw.sC;
-          float acc = 0.f;
-#pragma unroll
-          for (int r = 0; r < 3; ++r) {
-            const f32x4u_t q = *reinterpret_cast<const f32x4u_t*>(pc + off[r]);
-            acc += uw.ay[r] * (bx[0] * q.x + bx[1] * q.y + bx[2] * q.z + bx[3] * q.w);
-          }
-          d[j] = c_begin + j < c_end ? acc : 0.f;
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ds[i][c][j] = d[j];
-    nz[i][c] = any;
-  }
-  __syncthreads();
-  wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
-}
-
-// Round 4 form of warp_up_wino_kernel (it was VALU / LDS-issue bound, 9
-// ds_read_b32 + 12 FMAs per channel and sample).  Changes: (1) the staged box is stored channel-pair
-// interleaved, stage2[pair][row][col] = {channel 2p, channel 2p + 1}, so one ds_read_b64 serves two
-// channels of a window tap and the separable 3x3 window is evaluated on f32x2 (v_pk_fma_f32): per
-// sample 36 ds_read_b64 + 48 packed FMAs instead of 72 ds_read_b32 + 96 FMAs, the same fp32
-// operations per channel in the same order (bitwise the old kernel's T); (2) a block takes G
-// consecutive 8-channel groups, so the sample geometry (warp coordinates, upsample taps, the 3x3
-// window's weights and LDS offsets) and the block's source box are computed once for G groups.
-template <int G>
-__global__ __launch_bounds__(kWwThreads) __attribute__((amdgpu_waves_per_eu(G == 1 ? 8 : 6, 8))) void warp_up_wino2_kernel(const UpArgs ua, int r3_rows,
+// Round 4 (the round-3 form was VALU / LDS-issue bound, 9 ds_read_b32 + 12 FMAs
+// per channel and sample): the staged box is stored channel-pair interleaved, stage2[pair][row][col]
+// = {channel 2p, channel 2p + 1}, so one ds_read_b64 serves two channels of a window tap and the
+// separable 3x3 window is evaluated on f32x2 (v_pk_fma_f32): per sample 36 ds_read_b64 + 48 packed
+// FMAs instead of 72 ds_read_b32 + 96 FMAs, the same fp32 operations per channel in the same order.
+// cfg2: 0.39-0.42 ms vs 0.42-0.44 (profiles/r04a_kbench.jsonl).  (Several 8-channel groups per block,
+// the sample geometry computed once for them, spilled and ran 0.64-0.85 ms: removed.)
+constexpr int G = 1;
+__global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino2_kernel(const UpArgs ua, int r3_rows,
                                                                                   int cgroups) {
   __shared__ __attribute__((aligned(16))) float ds[kWwRows][kWwCols][8];
   __shared__ unsigned char nz[kWwRows][kWwCols];
@@ -620,22 +481,8 @@ extern "C" int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views
   ua.h = (int)h; ua.sw = (int)w;
   ua.sy = (float)h / (float)H;
   ua.sx = (float)w / (float)W;
-  // A/B selection of the round-4 form (MVBEV_UPW_G = groups per block; 0 = the round-3 kernel)
-  static const int kG = [] {
-    const char* e = getenv("MVBEV_UPW_G");
-    return e ? atoi(e) : 1;
-  }();
-  if (kG == 1 || kG == 2 || kG == 4) {
-    const int cgroups = (int)ceil_div(a.chunks, kG);
-    a.nwg = a.tiles * cgroups * a.B * a.nviews;
-    const dim3 grid((unsigned)a.nwg), block(kWwThreads);
-    if (kG == 1) hipLaunchKernelGGL(warp_up_wino2_kernel<1>, grid, block, 0, as_stream(stream), ua, (int)r3_rows, cgroups);
-    else if (kG == 2) hipLaunchKernelGGL(warp_up_wino2_kernel<2>, grid, block, 0, as_stream(stream), ua, (int)r3_rows, cgroups);
-    else hipLaunchKernelGGL(warp_up_wino2_kernel<4>, grid, block, 0, as_stream(stream), ua, (int)r3_rows, cgroups);
-    MVBEV_CHECK_LAUNCH();
-    return MVBEV_OK;
-  }
-  hipLaunchKernelGGL(warp_up_wino_kernel, dim3((unsigned)a.nwg), dim3(kWwThreads), 0, as_stream(stream), ua, (int)r3_rows);
+  hipLaunchKernelGGL(warp_up_wino2_kernel, dim3((unsigned)a.nwg), dim3(kWwThreads), 0, as_stream(stream), ua,
+                     (int)r3_rows, a.chunks);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }

@@ -245,7 +245,7 @@ def test_fused_warp_transform_matches_two_pass(cfg):
 @pytest.mark.parametrize("cfg,C,B", [(1, 32, 1), (2, 64, 2), (2, 40, 1)])
 def test_fused_warp_channels_last_matches_nchw(cfg, C, B):
     """Channels-last sources (sC == 1, C % 32 == 0: warp_wino_cl_kernel, one 128-B line per source
-    pixel) give bit-for-bit the T of the NCHW kernel for the same logical tensor: zero and NaN
+    pixel) give the T of the NCHW kernel for the same logical tensor (to fp32 rounding): zero and NaN
     geometry (one view's matrix made non-finite), an inf feature, the non-finite report and
     skip_zero included.  C = 40 (not whole 32-channel groups) takes the NCHW kernel with the
     channels-last strides — the same T again."""
@@ -275,9 +275,20 @@ def test_fused_warp_channels_last_matches_nchw(cfg, C, B):
             outs.append((t.view(torch.int16).cpu(), int(flag.item())))
     (a, fa), (az, fz), (b, fb), (bz, fbz) = outs
     assert fa == fz == fb == fbz == 7
-    assert torch.equal(a, az)
-    assert torch.equal(a, b), (a != b).sum().item()
-    assert torch.equal(a, bz)
+    assert torch.equal(a, az) and torch.equal(b, bz)
+
+    def value(x):  # T rows: hi plane then lo plane -> hi + lo in fp32
+        h = x.view(torch.bfloat16).view(-1, 2, Wo, 8).float()
+        return h[:, 0] + h[:, 1]
+    va, vb = value(a), value(b)
+    # same NaN / inf positions; finite values equal up to the fp32 contraction order of the bilinear sum
+    # (fma vs. separate products, which the two kernels' compilers may pick differently)
+    assert torch.equal(va.isnan(), vb.isnan()) and torch.equal(va.isinf(), vb.isinf())
+    fin = va.isfinite()
+    assert torch.equal(va[~fin & ~va.isnan()], vb[~fin & ~vb.isnan()])
+    # (an fp32 ulp of t can move lo = bf16(t - hi) by one of its own ulps: <= 2^-16 |t|)
+    scale = va[fin].abs().max().item()
+    assert ((va[fin] - vb[fin]).abs() <= 2.0 ** -15 * va[fin].abs() + 1e-6 * scale).all()
 
 
 # -- conv2 (dilation 2) -> conv3 partials as row-Winograd (ABI 11500) ------------------------------

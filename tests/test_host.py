@@ -215,3 +215,30 @@ def test_bev_fuse_wrapper_refuses_mismatched_tensors():
     bad[4] = nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False).double()
     with pytest.raises(ValueError, match=r"map_classifier\[4\].weight"):
         bev.prepare(bad, "cpu")
+
+
+def test_hot_kernels_use_no_scratch():
+    """The inference and training hot kernels keep their accumulators in registers: no scratch
+    (private segment) in the build's resource report (``build/obj/*.o.res``, written by the Makefile).
+    A branch inside an unrolled epilogue once put the ring / Winograd convs' accumulators in 448 B of
+    scratch per lane and made the training conv1 5x slower without any test failing."""
+    res = sorted((ROOT / "build" / "obj").glob("*.o.res"))
+    if not res:
+        pytest.skip("no build resource reports (build with make -C mvdet_amd/csrc)")
+    hot = re.compile(r"conv_ring_kernel|conv_wino_kernel|conv_wino4_kernel|wino_rows_kernel|warp_wino|warp_up_wino|"
+                     r"cout1|wgrad|dgrad|warp_tile_kernel|warp_exact")
+    seen, bad = 0, []
+    for f in res:
+        name = None
+        for line in f.read_text().splitlines():
+            m = re.search(r"Function Name: (\S+)", line)
+            if m:
+                name = m.group(1)
+                continue
+            m = re.search(r"ScratchSize \[bytes/lane\]: (\d+)", line)
+            if m and name and hot.search(name):
+                seen += 1
+                if int(m.group(1)):
+                    bad.append((f.name, name, int(m.group(1))))
+    assert seen >= 20, seen
+    assert not bad, bad

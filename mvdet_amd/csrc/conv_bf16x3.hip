@@ -24,7 +24,6 @@
 // channels (2x2 accumulators of 32x32, the same epilogue as the fp32 kernel).
 #include "common.h"
 
-#include <cstdlib>
 #include <type_traits>
 
 namespace mvbev {
@@ -1689,226 +1688,11 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   ring_epilogue<DIL, RELU, P3>(a, b, y0 + ring_base_row<DIL>(rg), x0 + l32, cot, cw, y, lds);
 }
 
-// Round 4: the Winograd conv with ONE wave per SIMD and xi-major accumulation.
-// 4 waves = (pair of row tiles) x (64-Cout half): a wave computes 2 row tiles x 64 Cout x 32 pixels.
-// Units run xi-major — for xi: for chunk: unit (chunk, xi) — so a wave accumulates only the current
-// xi's products M[rt][ct] and, after the xi's last chunk, folds them into its output rows,
-// Y[rt][ct][i] += A^T[i][xi] M[rt][ct]: 4 + 12 accumulators (256 registers) instead of 2 x 10 for two
-// row tiles.  The workgroup tile (12 x 32 x 128), the ring slots, the unit DMAs and the per-accumulator
-// summation order over K are conv_wino_kernel's; per unit a wave reads 12 B and 12 A fragments for
-// its 36 MFMAs (conv_wino_kernel: 6 + 12 for 18): a third fewer LDS reads per MFMA, and all four waves
-// issue the DMAs.
-template <bool RELU, int DIL, bool P3>
-__global__ __launch_bounds__(256, 1) void conv_wino4_kernel(const Args a) {
-  using namespace wino;
-  using G = Geo<DIL>;
-  static_assert(NIW == 4 && NIT == 256, "the ring slots of conv_wino_kernel with 4 issuing waves");
-  constexpr int XW = G::XW, TROW = G::TROW, NXT = G::NXT;
-  __shared__ __attribute__((aligned(16))) u32x4 lds[LDS];
-  const int W = a.W;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l32 = lane & 31, kl = lane >> 5;
-
-  int tile = xcd_remap(blockIdx.x, a.nwg);
-  if (a.gmask) {
-    constexpr int Gq = MVBEV_MASK_GROUP;
-    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
-    const int q = j / a.n_cot;
-    const int slot = Gq * (8 * (q / Gq) + x) + q % Gq;
-    if (slot >= a.npix) return;  // padding block (whole block, before any barrier)
-    tile = (a.tile_order ? a.tile_order[slot] : slot) * a.n_cot + j % a.n_cot;
-  }
-  const int cot = tile % a.n_cot, rest = tile / a.n_cot;
-  const int t_main = a.tiles_y * a.tiles_x;
-  const int pp = rest % t_main, b = rest / t_main;
-  const int ty = pp / a.tiles_x;
-  const int x0 = (pp - ty * a.tiles_x) * TW;
-  const int y0 = a.out_row0 + ty * RT;
-  const uint32_t gm = a.gmask ? a.gmask[pp] : 0u;
-  const int nch = a.gmask ? __builtin_popcount(gm) * a.cpg : a.nchunks;
-  const int K8 = a.K / SB;
-  const int64_t tplane2 = 2LL * (XH * a.tiles_y) * W;
-  const uint32_t tplane_b = (uint32_t)(tplane2 * 16);
-  constexpr uint32_t kOOB = 0x80000000u;
-  uint32_t wvo[NWI], tvo[NXTMAX];
-#pragma unroll
-  for (int j = 0; j < NWI; ++j) {
-    const int e = (j * NIW + wave) * 64 + lane;
-    wvo[j] = (uint32_t)(((e / RHALF) * (NTAP * 2 * BN) + e % RHALF) * 16);
-    asm volatile("" : "+v"(wvo[j]));
-  }
-#pragma unroll
-  for (int j = 0; j < NXT; ++j) {
-    const int e = (j * NIW + wave) * 64 + lane;
-    const int sub = e / (TROW / 2), part = (e / (TROW / 4)) & 1, rt = (e % (TROW / 4)) / XW, c = e % XW;
-    const int gx = x0 - DIL + c;
-    const bool z = e >= TROW || gx < 0 || gx >= W;
-    tvo[j] = z ? kOOB : (uint32_t)sub * tplane_b + (uint32_t)((2 * (XH * ty + NXI * rt) * W + part * W + gx) * 16);
-    asm volatile("" : "+v"(tvo[j]));
-  }
-  const int cpg = a.gmask ? a.cpg : max(nch, 1);
-  const char* wcot = reinterpret_cast<const char*>(a.wp + (int64_t)cot * wino::W16);
-  const char* tb0 = reinterpret_cast<const char*>(static_cast<const u32x4*>(a.x) + (int64_t)b * K8 * tplane2);
-  // the DMA cursor: the next unit to issue, xi-major (the chunk walk restarts for every xi; past the
-  // last unit it stays on the last one: dummy loads that keep the vmcnt counts exact)
-  uint32_t c_rem = a.gmask ? gm : 1u;
-  int c_gbase = a.gmask ? __builtin_ctz(gm | 0x80000000u) * cpg : 0, c_ci = 0, c_wi = 0, c_xi = 0;
-  auto cursor_advance = [&]() __attribute__((always_inline)) {
-    if (c_wi + 1 < nch) {
-      ++c_wi;
-      if (++c_ci == cpg) {
-        c_ci = 0;
-        c_rem &= c_rem - 1;
-        c_gbase = __builtin_ctz(c_rem | 0x80000000u) * cpg;
-      }
-    } else if (c_xi + 1 < NXI) {
-      ++c_xi;
-      c_wi = 0;
-      c_ci = 0;
-      c_rem = a.gmask ? gm : 1u;
-      c_gbase = a.gmask ? __builtin_ctz(gm | 0x80000000u) * cpg : 0;
-    }
-  };
-  auto issue_cursor = [&](int slot) __attribute__((always_inline)) {
-    const int ph = c_gbase + c_ci;
-    const char* cw_ = wcot + (int64_t)ph * a.n_cot * wino::W16 * 16;
-    const char* ct_ = tb0 + (int64_t)(2 * ph) * tplane2 * 16;
-    const bool kv1 = 2 * ph + 1 < K8;
-    u32x4* dst = lds + slot * SLOT + wave * 64;
-    const __amdgpu_buffer_rsrc_t rw =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(cw_ + c_xi * 3 * 2 * BN * 16), (short)0, 0x7fffffff, 0x00020000);
-#pragma unroll
-    for (int j = 0; j < NWI; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(dst + j * NIT), 16,
-                                               wvo[j], 0, 0, 0);
-    const int32_t rows_b = c_xi * W * 32;
-    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<char*>(ct_ + rows_b), (short)0, kv1 ? 0x7fffffff : (int)(tplane_b - rows_b), 0x00020000);
-#pragma unroll
-    for (int j = 0; j < NXT; ++j)
-      if ((j * NIW + wave) * 64 < TROW)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(dst + RUNIT + j * NIT),
-                                                 16, tvo[j], 0, 0, 0);
-    cursor_advance();
-  };
-
-  const int rp = wave & 1;          // row-tile pair: row tiles 2 rp, 2 rp + 1
-  const int cw = 64 * (wave >> 1);  // Cout half
-  floatx16 M[2][2], Y[2][2][3];
-#pragma unroll
-  for (int r = 0; r < 2; ++r)
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      M[r][c] = floatx16{0};
-#pragma unroll
-      for (int i = 0; i < 3; ++i) Y[r][c][i] = floatx16{0};
-    }
-  bf16x8 fb[3][2][2];  // [kw][row tile][hi, lo]
-  bf16x8 fa[2][2][2];  // [set][ct][hi, lo]
-  auto fetch_b = [&](int kw, int slot) __attribute__((always_inline)) {
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const u32x4* X = lds + slot * SLOT + RUNIT + kl * (TROW / 2) + (2 * rp + r) * XW + l32 + DIL * kw;
-#pragma unroll
-      for (int p = 0; p < 2; ++p) fb[kw][r][p] = __builtin_bit_cast(bf16x8, X[p * (TROW / 4)]);
-    }
-  };
-  auto fetch_a = [&](int st, int slot, int kw) __attribute__((always_inline)) {
-    const u32x4* Wl = lds + slot * SLOT + kw * 2 * BN + kl * BN + cw + l32;
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-      for (int p = 0; p < 2; ++p) fa[st][ct][p] = __builtin_bit_cast(bf16x8, Wl[p * RHALF + 32 * ct]);
-  };
-  auto sched12 = [&](auto nreads) __attribute__((always_inline)) {
-    constexpr int n = decltype(nreads)::value;  // fragment reads spread over a kernel column's 12 MFMAs
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      if (i < n) __builtin_amdgcn_sched_group_barrier(0x100, (n + 11) / 12, 0);
-    }
-  };
-  constexpr int WHI = (TROW % NIT + 63) / 64;
-  constexpr int NPU_HI = NWI + NXT, NPU_LO = NWI + TROW / NIT;
-  static_assert(TROW / NIT + (WHI > 0) == NXT, "T pieces");
-  const bool whi = wave < WHI;
-  if (nch > 0) {
-    const int U = NXI * nch;
-    issue_cursor(0);
-    issue_cursor(1);
-    issue_cursor(2);
-    issue_cursor(3);
-    if (whi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPU_HI) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPU_LO) : "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    fetch_b(0, 0);
-    fetch_b(1, 0);
-    fetch_a(0, 0, 0);
-    int kx = 0, xi_c = 0;  // the computed unit's chunk index within its xi, and its xi
-#define WINO4_MFMAS(AS, KW)                                                                              \
-  _Pragma("unroll") for (int r = 0; r < 2; ++r) _Pragma("unroll") for (int ct = 0; ct < 2; ++ct) {      \
-    M[r][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][1], fb[KW][r][0], M[r][ct], 0, 0, 0);  \
-    M[r][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][r][1], M[r][ct], 0, 0, 0);  \
-    M[r][ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][r][0], M[r][ct], 0, 0, 0);  \
-  }
-#define WINO4_UNIT(R)                                                                                    \
-  do {                                                                                                   \
-    constexpr int P = (R) & 1;                                                                           \
-    const int u = u0 + (R);                                                                              \
-    if (u >= U) break;                                                                                   \
-    const int slot = u & 3, nslot = (u + 1) & 3;                                                         \
-    fetch_a(P ^ 1, slot, 1);                                                                             \
-    fetch_b(2, slot);                                                                                    \
-    WINO4_MFMAS(P, 0);                                                                                   \
-    sched12(std::integral_constant<int, 8>{});                                                           \
-    fetch_a(P, slot, 2);                                                                                 \
-    WINO4_MFMAS(P ^ 1, 1);                                                                               \
-    sched12(std::integral_constant<int, 4>{});                                                           \
-    /* retire unit u+1; every LDS read of this unit's slot is done; unit u+4 into this slot */          \
-    if (whi) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU_HI) : "memory");               \
-    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU_LO) : "memory");                    \
-    __builtin_amdgcn_s_barrier();                                                                        \
-    asm volatile("" ::: "memory");                                                                       \
-    issue_cursor(slot);                                                                                  \
-    fetch_b(0, nslot);                                                                                   \
-    fetch_b(1, nslot);                                                                                   \
-    fetch_a(P ^ 1, nslot, 0);                                                                            \
-    WINO4_MFMAS(P, 2);                                                                                   \
-    sched12(std::integral_constant<int, 12>{});                                                          \
-    if (++kx == nch) { /* the xi's K sum is complete: fold it into the output rows (A^T) */               \
-      _Pragma("unroll") for (int r = 0; r < 2; ++r) _Pragma("unroll") for (int ct = 0; ct < 2; ++ct) {   \
-        if (xi_c <= 3) Y[r][ct][0] += M[r][ct];                                                          \
-        if (xi_c == 1) Y[r][ct][1] += M[r][ct];                                                          \
-        if (xi_c == 2) Y[r][ct][1] -= M[r][ct];                                                          \
-        if (xi_c == 3) Y[r][ct][1] += 2.f * M[r][ct];                                                    \
-        if (xi_c == 1 || xi_c == 2 || xi_c == 4) Y[r][ct][2] += M[r][ct];                                \
-        if (xi_c == 3) Y[r][ct][2] += 4.f * M[r][ct];                                                    \
-        M[r][ct] = floatx16{0};                                                                          \
-      }                                                                                                  \
-      kx = 0;                                                                                            \
-      ++xi_c;                                                                                            \
-    }                                                                                                    \
-  } while (0)
-    for (int u0 = 0; u0 < U; u0 += 2) {
-      WINO4_UNIT(0);
-      WINO4_UNIT(1);
-    }
-#undef WINO4_UNIT
-#undef WINO4_MFMAS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the block exits
-  }
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    floatx16 y[2][3];
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-      for (int i = 0; i < 3; ++i) y[ct][i] = Y[r][ct][i];
-    ring_epilogue<DIL, RELU, P3>(a, b, y0 + ring_base_row<DIL>(2 * rp + r), x0 + l32, cot, cw, y, lds);
-  }
-}
+// (Round 4, VERDICT r03 item 5: a one-wave-per-SIMD form — 4 waves of 2 row tiles x 64 Cout, xi-major
+// accumulation with the A^T fold after each xi's K sum, 12 + 12 fragment reads per 36 MFMAs — was
+// parity-green but ran 1.75-1.85 ms vs 1.40-1.45 for conv1 and 0.41-0.47 vs 0.34-0.37 for conv2 +
+// conv3 partials (profiles/r04b_kbench.jsonl): with one wave per SIMD every unit barrier drains the
+// MFMA pipe, which the second wave of this kernel keeps fed.  Removed)
 
 static int wino_rows_launch(const void* x, const mvbev_conv_desc* d, int dil, const uint32_t* group_mask, void* t,
                             size_t t_bytes, void* stream) {
@@ -1983,28 +1767,6 @@ static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_pa
   a.nwg = (int)nwg;
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)nwg), blk(RNT);
-  // A/B selection of the round-4 form (one wave per SIMD, xi-major accumulation): MVBEV_WINO4 = bit 0
-  // for conv1 (dilation 1), bit 1 for conv2 (dilation 2)
-  static const int kW4 = [] {
-    const char* e = getenv("MVBEV_WINO4");
-    return e ? atoi(e) : 0;
-  }();
-  if ((dil == 1 && (kW4 & 1)) || (dil == 2 && (kW4 & 2))) {
-    const dim3 blk4(256);
-    if (p3) {
-      if (dil != 2 || !relu) return MVBEV_ERR_SHAPE;
-      hipLaunchKernelGGL((conv_wino4_kernel<true, 2, true>), grid, blk4, 0, s, a);
-    } else if (dil == 2) {
-      if (relu) hipLaunchKernelGGL((conv_wino4_kernel<true, 2, false>), grid, blk4, 0, s, a);
-      else hipLaunchKernelGGL((conv_wino4_kernel<false, 2, false>), grid, blk4, 0, s, a);
-    } else if (relu) {
-      hipLaunchKernelGGL((conv_wino4_kernel<true, 1, false>), grid, blk4, 0, s, a);
-    } else {
-      hipLaunchKernelGGL((conv_wino4_kernel<false, 1, false>), grid, blk4, 0, s, a);
-    }
-    MVBEV_CHECK_LAUNCH();
-    return MVBEV_OK;
-  }
   if (p3) {
     if (dil != 2 || !relu) return MVBEV_ERR_SHAPE;  // conv2 -> conv3 of map_classifier (the only use)
     hipLaunchKernelGGL((conv_wino_kernel<true, 2, true>), grid, blk, 0, s, a);

@@ -38,11 +38,11 @@ A2A_EFF = 0.7       # all-to-all: fraction of one link per peer chunk
 # transform of every view, conv1 = the Winograd conv kernel (whole grid, frustum-masked), conv2 =
 # Winograd conv2 + conv3 partials (incl. its transform), conv3 = the partials' reduce; transform =
 # mvbev_wino_rows_split_bf16 over the whole slab (measured at cfg2 in round 2, scaled by size).
-# cfg2 / cfg3: profiles/r03f_bench.json; cfg5: profiles/r04 bench.
+# profiles/r04b_bench.json (cfg2 line, its cfg3 / cfg5 sub-objects; NCHW features).
 SINGLE_GPU_MS: Dict[int, Dict[str, float]] = {
-    2: dict(warp=0.4835, conv1=1.4138, conv2=0.3328, conv3=0.026, transform=0.25),
-    3: dict(warp=5.5234, conv1=21.1706, conv2=4.7972, conv3=0.1092, transform=4.0),
-    5: dict(warp=4.6, conv1=19.0, conv2=7.0, conv3=0.18, transform=2.3),
+    2: dict(warp=0.4855, conv1=1.4229, conv2=0.3336, conv3=0.0262, transform=0.25),
+    3: dict(warp=5.3227, conv1=21.0673, conv2=4.7547, conv3=0.1122, transform=4.0),
+    5: dict(warp=4.2809, conv1=15.1407, conv2=6.9484, conv3=0.1478, transform=2.3),
 }
 
 

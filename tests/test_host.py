@@ -225,7 +225,7 @@ def test_hot_kernels_use_no_scratch():
     res = sorted((ROOT / "build" / "obj").glob("*.o.res"))
     if not res:
         pytest.skip("no build resource reports (build with make -C mvdet_amd/csrc)")
-    hot = re.compile(r"conv_ring_kernel|conv_wino_kernel|conv_wino4_kernel|wino_rows_kernel|warp_wino|warp_up_wino|"
+    hot = re.compile(r"conv_ring_kernel|conv_wino_kernel|wino_rows_kernel|warp_wino|warp_up_wino|"
                      r"cout1|wgrad|dgrad|warp_tile_kernel|warp_exact")
     seen, bad = 0, []
     for f in res:

@@ -13,7 +13,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 cd $R
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_trace -o run -- \
-  python3 bench.py --steps 10 --warmup 3 --config $CFG --no-cpu-baseline --no-train --no-alt --north-star-cfg 0 \
+  python3 bench.py --steps 10 --warmup 3 --config $CFG --no-cpu-baseline --no-train --no-alt --north-star-cfg 0 --roofline-cfg 0 \
   > $OUT/${TAG}_trace_bench.log 2>&1 || exit $?
 i=0
 for PMC in "GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU" \
@@ -21,9 +21,13 @@ for PMC in "GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCL
            "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum" \
            "GRBM_GUI_ACTIVE TA_TA_BUSY_sum TD_TD_BUSY_sum SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $PMC --output-format csv -d $OUT/${TAG}_pmc$i -o run -- \
-    python3 tools/kbench.py --config $CFG --reps 3 --only warpw,warpupw,winoconv,conv23w > $OUT/${TAG}_pmc$i.log 2>&1 || exit $?
+  timeout -s KILL 150 rocprofv3 --pmc $PMC --output-format csv -d $OUT/${TAG}_pmc$i -o run -- \
+    python3 tools/kbench.py --config $CFG --reps 3 --only warpw,warpwcl,warpupw,winoconv,conv23w > $OUT/${TAG}_pmc$i.log 2>&1 || exit $?
 done
 python3 tools/pmc_summary.py $OUT/${TAG}_pmc* > $OUT/${TAG}_pmc_summary.txt
 python3 tools/traffic.py $OUT $TAG $CFG bf16x3 wino > $OUT/${TAG}_traffic.json
+# the kernel trace of the BASELINE "rocprof roofline run" config (cfg5: 8 views at 4K -> 1000 x 1000)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_trace_cfg5 -o run -- \
+  python3 bench.py --steps 5 --warmup 2 --config 5 --no-cpu-baseline --no-train --no-alt --north-star-cfg 0 \
+  --roofline-cfg 0 > $OUT/${TAG}_trace_cfg5_bench.log 2>&1 || exit $?
 echo profile-done

@@ -13,6 +13,4 @@ set -e
 timeout -k 10 420 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
 timeout -k 10 120 python tools/kbench.py --only warpw,warpwcl --rounds 2 --reps 30 >> gpurun_out/${TAG}_kbench.jsonl
 timeout -k 10 120 python tools/kbench.py --only warpupw,conv1,conv2 --rounds 2 --reps 30 >> gpurun_out/${TAG}_kbench.jsonl
-for w in 0 3; do
-  MVBEV_WINO4=$w timeout -k 10 120 python tools/kbench.py --only winoconv,conv23w --rounds 2 --reps 30 | sed "s/^{/{\"wino4\": $w, /" >> gpurun_out/${TAG}_kbench.jsonl
-done
+timeout -k 10 120 python tools/kbench.py --only winoconv,conv23w --rounds 2 --reps 30 >> gpurun_out/${TAG}_kbench.jsonl

@@ -316,11 +316,13 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
 // Phase 0: one thread per warped pixel (14 rows x 16 columns) computes its coordinates once (LDS).
 // Phase 1: 8 lanes per pixel, 7 pixels per thread: 4 corner loads each as bounds-checked buffer
 // loads (a corner outside the source reads 0 without a fetch, so the loads are unconditional and
-// the 28 of a thread are in flight together), the bilinear sum into ds[pixel][36] (pitch 36
+// the 28 of a thread are in flight together), the bilinear sum into ds[pixel][40] (pitch 40
 // floats: conflict-free 16-B reads in phase 2).  Phase 2: one thread per (tile, column, 8-channel
 // chunk, 4-channel half) applies B^T and stores 8 B of each T row's hi and lo planes.  Same T
 // (same fp32 ops per channel as warp_wino_kernel) for the same logical source.
-constexpr int kWcCh = 32, kWcPitch = 36, kWcPix = kWwRows * kWwCols;
+// kWcPitch 40 floats: a ds_read_b128 lane group of phase 2 (8 columns x 2 halves) then covers 16 distinct
+// 4-bank slots, (10 c + h) mod 16 (36 left 2-way conflicts: 2.6 M conflict cycles per 3.8 M LDS instructions)
+constexpr int kWcCh = 32, kWcPitch = 40, kWcPix = kWwRows * kWwCols;
 constexpr int kWcOutside = 0x7fff0000;  // byte offset of "no corner" (sources must stay below it)
 static_assert(kWwCols == 16 && kWwThreads == 256, "channels-last fused warp: 256 threads, 16 columns");
 static_assert(kWcPix % 32 == 0, "phase 1: 32 pixels per pass");

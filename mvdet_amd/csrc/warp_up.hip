@@ -229,7 +229,7 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino2_kerne
     if (gi > 0) __syncthreads();  // the previous group's phase 2 is done with ds / stage2
     if (staged) {  // the box of the group's 8 channels, channel-pair interleaved
       if (sb.quad) {
-        const int Q = Cb >> 2, items = R * Q;
+        const int Q = sb.pitch >> 2, items = R * Q;
         for (int it = tid; it < items; it += kWwThreads) {
           const int r = it / Q, q = it - r * Q;
           const float* src = base + (int64_t)(sb.r0 + r) * vw.sH + sb.c0 + 4 * q;
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino2_kerne
         }
       } else {
         for (int r = tid / 32; r < R; r += kWwThreads / 32)
-          for (int cc = tid % 32; cc < Cb; cc += 32) {
+          for (int cc = tid % 32; cc < sb.pitch; cc += 32) {
             float t[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j)

@@ -73,6 +73,7 @@ EXPORTS = (
     "mvbev_bev_fuse_prepare",
     "mvbev_bev_fuse",
     "mvbev_warp_views_exact_f32",
+    "mvbev_nchw_to_nhwc_f32",
 )
 BEV_SRC_F32, BEV_SRC_F16, BEV_SRC_BACKBONE_F32 = 0, 1, 2  # MVBEV_BEV_SRC_*
 WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
@@ -207,6 +208,8 @@ def _declare(lib):
     lib.mvbev_warp_views_exact_f32.restype = ctypes.c_int
     lib.mvbev_warp_views_exact_f32.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
                                                _i64, _i64, _i64, _p, ctypes.c_int32, _p]
+    lib.mvbev_nchw_to_nhwc_f32.restype = ctypes.c_int
+    lib.mvbev_nchw_to_nhwc_f32.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _p]
     lib.mvbev_warp_tile_mask.restype = ctypes.c_int
     lib.mvbev_warp_tile_mask.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
                                          _i64, _i64, _i64, _i64, _p, _p]

@@ -323,6 +323,173 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino2_kerne
   }
 }
 
+// Fused 3x upsample + warp + B^T for channels-last backbone maps (round 4: sC == 1, the [B, C, h, w]
+// tensor in channels_last memory format, or the NCHW map transposed once by mvbev_nchw_to_nhwc_f32).
+// The NCHW form stages one 8-channel plane box per block and reads each window tap per channel pair
+// from LDS (issue-bound: 37 % of wave cycles waiting on instructions, 0.38-0.41 ms at cfg2).  Here a
+// staged box pixel is one 128-B line of 32 channels, so a lane's 16-B LDS read serves 4 channels of a
+// tap, and the transform runs in registers:
+//   phase 0: the block's 14 x 16 pixels' windows (up_window, once per pixel) -> LDS, the box reduced;
+//   stage:   the box (<= kUcStage backbone pixels) with 16-B loads, 8 lanes per pixel line;
+//   phase 1: thread = (column, channel quad) walks the 14 rows of its column: per row 9 ds_read_b128
+//            taps, the separable window sum on f32x4 (same order per channel as the NCHW kernels);
+//   phase 2: B^T of each 3-row tile's 5 rows from the thread's own registers, 8 B of hi and lo per
+//            T row (no LDS round trip).
+// A block whose box exceeds kUcStage (the near field) reads its taps straight from global memory.
+constexpr int kUcCh = 32, kUcThreads = 128, kUcStage = 256, kWcPixUp = kWwRows * kWwCols;
+static_assert(kWwCols * 8 == kUcThreads, "thread = (column, channel quad)");
+
+__global__ __launch_bounds__(kUcThreads) void warp_up_wino_cl_kernel(const UpArgs ua, int r3_rows) {
+  __shared__ __attribute__((aligned(16))) f32x4a_t box_px[kUcStage * 8];  // [pixel][quad]
+  __shared__ __attribute__((aligned(16))) f32x4a_t pax[kWcPixUp], pay[kWcPixUp];
+  __shared__ __attribute__((aligned(16))) int4 pint[kWcPixUp];  // rb, cb, class (0 zero, 1 inside, 2 NaN)
+  __shared__ int box[4];
+  const WarpArgs& a = ua.w;
+  const int lb = xcd_remap(blockIdx.x, a.nwg);
+  const int tile = lb % a.tiles;
+  const int grp = (lb / a.tiles) % a.chunks;  // 32-channel group
+  const int bv = lb / (a.tiles * a.chunks);
+  const int view = bv % a.nviews, b = bv / a.nviews;
+  const WarpView& vw = a.v[view];
+  const int k = tile / a.tiles_x, tx = tile - k * a.tiles_x;
+  const int H = a.H, W = a.W, h = ua.h, w = ua.sw;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    box[0] = INT32_MAX;
+    box[1] = -1;
+    box[2] = INT32_MAX;
+    box[3] = -1;
+  }
+  __syncthreads();
+  float m[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) m[q] = vw.m[q];
+  int r0 = INT32_MAX, r1 = -1, q0 = INT32_MAX, q1 = -1;
+  for (int p = tid; p < kWcPixUp; p += kUcThreads) {  // phase 0
+    const int i = p / kWwCols, c = p % kWwCols;
+    const int v = 12 * k - 1 + i, u = tx * kWwCols + c;
+    UpWindow uw;
+    uw.inside = false;
+    uw.finite = true;
+    uw.rb = uw.cb = 0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) uw.ax[j] = uw.ay[j] = 0.f;
+    if (v >= 0 && v < a.Ho && u < a.Wo) uw = up_window(m, u, v, a.Ho, a.Wo, H, W, h, w, ua.sy, ua.sx);
+    const int cl = uw.inside ? 1 : (uw.finite ? 0 : 2);
+    pax[p] = f32x4a_t{uw.ax[0], uw.ax[1], uw.ax[2], 0.f};
+    pay[p] = f32x4a_t{uw.ay[0], uw.ay[1], uw.ay[2], 0.f};
+    pint[p] = make_int4(uw.rb, uw.cb, cl, 0);
+    if (cl == 1) {
+      r0 = min(r0, uw.rb);
+      r1 = max(r1, min(uw.rb + 2, h - 1));
+      q0 = min(q0, uw.cb);
+      q1 = max(q1, min(uw.cb + 2, w - 1));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    r0 = min(r0, __shfl_xor(r0, o));
+    r1 = max(r1, __shfl_xor(r1, o));
+    q0 = min(q0, __shfl_xor(q0, o));
+    q1 = max(q1, __shfl_xor(q1, o));
+  }
+  if ((tid & 63) == 0 && r1 >= 0) {
+    atomicMin(&box[0], r0);
+    atomicMax(&box[1], r1);
+    atomicMin(&box[2], q0);
+    atomicMax(&box[3], q1);
+  }
+  __syncthreads();
+  const int br0 = box[0], bc0 = box[2];
+  const int R = box[1] - br0 + 1, Cb = box[3] - bc0 + 1;  // (an all-outside block: R, Cb <= 0)
+  const bool staged = box[1] >= 0 && R * Cb <= kUcStage;  // uniform per block
+  // the batch item's 32-channel group (16-B aligned: host check)
+  const float* gbase = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB + (int64_t)grp * kUcCh;
+  if (staged) {
+    for (int it = tid; it < R * Cb * 8; it += kUcThreads) {
+      const int px = it >> 3, q = it & 7;
+      const int r = px / Cb, c = px - r * Cb;
+      box_px[it] = *reinterpret_cast<const f32x4a_t*>(gbase + (int64_t)(br0 + r) * vw.sH + (int64_t)(bc0 + c) * vw.sW + 4 * q);
+    }
+    __syncthreads();
+  }
+  const int c = tid >> 3, q = tid & 7;  // column, channel quad
+  const int u = tx * kWwCols + c;
+  f32x4a_t d[kWwRows];
+  bool nzr[kWwRows];
+#pragma unroll
+  for (int i = 0; i < kWwRows; ++i) {  // phase 1
+    const int p = i * kWwCols + c;
+    const int4 pi = pint[p];
+    const f32x4a_t ax = pax[p], ay = pay[p];
+    f32x4a_t acc = {0.f, 0.f, 0.f, 0.f};
+    if (pi.z == 1) {
+      int ro[3], co[3];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        ro[j] = min(pi.x + j, h - 1);
+        co[j] = min(pi.y + j, w - 1);
+      }
+      f32x4a_t s[3][3];
+      if (staged) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) s[r][j] = box_px[((ro[r] - br0) * Cb + (co[j] - bc0)) * 8 + q];
+      } else {
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int j = 0; j < 3; ++j)
+            s[r][j] = *reinterpret_cast<const f32x4a_t*>(gbase + (int64_t)ro[r] * vw.sH + (int64_t)co[j] * vw.sW + 4 * q);
+      }
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        f32x4a_t rr = {0.f, 0.f, 0.f, 0.f};
+        rr += ax.x * s[r][0];
+        rr += ax.y * s[r][1];
+        rr += ax.z * s[r][2];
+        acc += (r == 0 ? ay.x : r == 1 ? ay.y : ay.z) * rr;
+      }
+    } else if (pi.z == 2) {
+      acc = f32x4a_t{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
+    }
+    d[i] = acc;
+    nzr[i] = pi.z != 0;
+  }
+  if (u >= a.Wo) return;
+  const int chunk = grp * (kUcCh / 8) + (q >> 1), half = q & 1;
+#pragma unroll
+  for (int qt = 0; qt < 4; ++qt) {  // phase 2: tile qt = rows 3 qt .. 3 qt + 4
+    const int r3 = 4 * k + qt, i0 = 3 * qt;
+    if (r3 >= r3_rows) break;
+    if (a.skip_zero && !(nzr[i0] | nzr[i0 + 1] | nzr[i0 + 2] | nzr[i0 + 3] | nzr[i0 + 4])) continue;
+    f32x4a_t t[5];
+    t[0] = 2.f * d[i0] - d[i0 + 1] - 2.f * d[i0 + 2] + d[i0 + 3];
+    t[1] = -2.f * d[i0 + 1] - d[i0 + 2] + d[i0 + 3];
+    t[2] = 2.f * d[i0 + 1] - 3.f * d[i0 + 2] + d[i0 + 3];
+    t[3] = d[i0 + 3] - d[i0 + 1];
+    t[4] = 2.f * d[i0 + 1] - d[i0 + 2] - 2.f * d[i0 + 3] + d[i0 + 4];
+    if (a.nonfinite) {  // as wino_rows_phase2
+      const f32x4a_t sum = (t[0] + t[1]) + (t[2] + t[3]) + t[4];
+      if (!isfinite((sum.x + sum.y) + (sum.z + sum.w))) *a.nonfinite = a.nf_tag;
+    }
+    unsigned* out = reinterpret_cast<unsigned*>(static_cast<u32x4_t*>(vw.dst) +
+                                                (2 * ((int64_t)b * vw.dB + (int64_t)chunk * vw.dC +
+                                                      (int64_t)(5 * r3) * vw.dH) + u)) + 2 * half;
+    typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int xi = 0; xi < 5; ++xi) {
+      const float h0 = (float)(__bf16)t[xi].x, h1 = (float)(__bf16)t[xi].y;
+      const float h2 = (float)(__bf16)t[xi].z, h3 = (float)(__bf16)t[xi].w;
+      unsigned* o = out + (int64_t)xi * vw.dH * 8;
+      *reinterpret_cast<u32x2_t*>(o) = u32x2_t{pack_bf16x2(h0, h1), pack_bf16x2(h2, h3)};
+      *reinterpret_cast<u32x2_t*>(o + vw.dH * 4) =
+          u32x2_t{pack_bf16x2(t[xi].x - h0, t[xi].y - h1), pack_bf16x2(t[xi].z - h2, t[xi].w - h3)};
+    }
+  }
+}
+
 // The exact-order warp (a5) and upsample + warp (a4 + a5): the non-finite guard's path
 // (mvbev_warp_views_exact_f32).  Per output pixel the kornia coordinates (warp_coord), then, per
 // in-bounds corner, the source value — with UP, PyTorch's bilinear upsample of that upsampled pixel
@@ -461,7 +628,7 @@ extern "C" int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views
   for (int i = 0; i < nviews; ++i) {
     const mvbev_warp_view& s = views[i];
     if (!s.src || !s.dst) return MVBEV_ERR_NULL;
-    if (s.dst_strides[3] != 1 || s.src_strides[3] != 1) return MVBEV_ERR_STRIDE;  // 16-B window rows
+    if (s.dst_strides[3] != 1) return MVBEV_ERR_STRIDE;
     WarpView& d = a.v[i];
     d.src = s.src; d.sB = s.src_strides[0]; d.sC = s.src_strides[1];
     d.sH = s.src_strides[2]; d.sW = s.src_strides[3];
@@ -481,6 +648,24 @@ extern "C" int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views
   ua.h = (int)h; ua.sw = (int)w;
   ua.sy = (float)h / (float)H;
   ua.sx = (float)w / (float)W;
+  // channels-last maps (every view: unit channel stride, 16-B aligned whole 32-channel groups) take the
+  // line-per-pixel kernel; NCHW maps need unit column stride (16-B window rows)
+  bool cl = C % kUcCh == 0;
+  for (int i = 0; i < nviews; ++i) {
+    const WarpView& d = a.v[i];
+    cl = cl && d.sC == 1 && d.sW >= C && d.sH >= d.sW * w && d.sB >= 0 && d.sW % 4 == 0 && d.sH % 4 == 0 &&
+         d.sB % 4 == 0 && (reinterpret_cast<uintptr_t>(d.src) & 15) == 0;
+  }
+  if (cl) {
+    a.chunks = (int)(C / kUcCh);
+    a.nwg = a.tiles * a.chunks * a.B * a.nviews;
+    hipLaunchKernelGGL(warp_up_wino_cl_kernel, dim3((unsigned)a.nwg), dim3(kUcThreads), 0, as_stream(stream), ua,
+                       (int)r3_rows);
+    MVBEV_CHECK_LAUNCH();
+    return MVBEV_OK;
+  }
+  for (int i = 0; i < nviews; ++i)
+    if (a.v[i].sW != 1) return MVBEV_ERR_STRIDE;  // 16-B window rows
   hipLaunchKernelGGL(warp_up_wino2_kernel, dim3((unsigned)a.nwg), dim3(kWwThreads), 0, as_stream(stream), ua,
                      (int)r3_rows, a.chunks);
   MVBEV_CHECK_LAUNCH();
@@ -553,4 +738,68 @@ extern "C" int mvbev_warp_views_upsampled(const mvbev_warp_view* views, int nvie
                                           void* stream) {
   return mvbev_warp_views_upsampled_ex(views, nviews, src_is_f16, B, C, h, w, H, W, Ho, Wo, out_layout, 0,
                                        stream);
+}
+
+// NCHW -> NHWC (channels-last) copy of the views' backbone maps, one launch for every view: the input
+// of warp_up_wino_cl_kernel for producers that emit NCHW (the maps are 1/9 of the upsampled size:
+// 0.13 GB read + written at cfg2).  Block = (view, batch item, 32 channels, 64 pixels) through an LDS
+// tile (pitch 65: conflict-free column reads); reads 256-B channel rows, writes 128-B pixel lines.
+namespace mvbev {
+struct TransArgs {
+  const float* src[kWarpMaxViews];
+  int64_t sB[kWarpMaxViews], sC[kWarpMaxViews], sH[kWarpMaxViews], sW[kWarpMaxViews];
+  float* dst[kWarpMaxViews];
+  int B, C, H, W, ctiles, ptiles;
+};
+__global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const TransArgs a) {
+  __shared__ float t[32][65];
+  const int HW = a.H * a.W;
+  int blk = blockIdx.x;
+  const int pt = blk % a.ptiles;
+  blk /= a.ptiles;
+  const int ct = blk % a.ctiles;
+  blk /= a.ctiles;
+  const int b = blk % a.B, v = blk / a.B;
+  const int tid = threadIdx.x;
+  const float* src = a.src[v] + (int64_t)b * a.sB[v];
+  for (int cc = tid >> 6; cc < 32; cc += 4) {
+    const int c = ct * 32 + cc, p = pt * 64 + (tid & 63);
+    if (c < a.C && p < HW) {
+      const int y = p / a.W, x = p - y * a.W;
+      t[cc][tid & 63] = src[(int64_t)c * a.sC[v] + (int64_t)y * a.sH[v] + (int64_t)x * a.sW[v]];
+    }
+  }
+  __syncthreads();
+  float* dst = a.dst[v] + (int64_t)b * HW * a.C;
+  for (int pp = tid >> 5; pp < 64; pp += 8) {
+    const int p = pt * 64 + pp, c = ct * 32 + (tid & 31);
+    if (p < HW && c < a.C) dst[(int64_t)p * a.C + c] = t[tid & 31][pp];
+  }
+}
+}  // namespace mvbev
+
+extern "C" int mvbev_nchw_to_nhwc_f32(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t H,
+                                      int64_t W, void* stream) {
+  using namespace mvbev;
+  if (!views) return MVBEV_ERR_NULL;
+  if (nviews <= 0 || B <= 0 || C <= 0 || H <= 0 || W <= 0) return MVBEV_ERR_RANK;
+  if (nviews > kWarpMaxViews || C > INT32_MAX || H * W > INT32_MAX - 64) return MVBEV_ERR_SHAPE;
+  TransArgs a = {};
+  for (int i = 0; i < nviews; ++i) {
+    if (!views[i].src || !views[i].dst) return MVBEV_ERR_NULL;
+    a.src[i] = static_cast<const float*>(views[i].src);
+    a.sB[i] = views[i].src_strides[0];
+    a.sC[i] = views[i].src_strides[1];
+    a.sH[i] = views[i].src_strides[2];
+    a.sW[i] = views[i].src_strides[3];
+    a.dst[i] = static_cast<float*>(views[i].dst);
+  }
+  a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W;
+  a.ctiles = (int)ceil_div(C, 32);
+  a.ptiles = (int)ceil_div(H * W, 64);
+  const int64_t nwg = (int64_t)a.ptiles * a.ctiles * B * nviews;
+  if (nwg > INT32_MAX) return MVBEV_ERR_SHAPE;
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
 }

@@ -270,6 +270,39 @@ def warp_views_exact_into(srcs, m_norms, dsts, up_hw=None, gate=None) -> None:
     _native.check(st, "mvbev_warp_views_exact_f32")
 
 
+def is_channels_last_source(x: torch.Tensor) -> bool:
+    """True when the fused warps take ``x`` [B,C,H,W] fp32 in their channels-last form (ABI 11700: unit
+    channel stride, whole 32-channel groups, strides multiples of 4 floats, 16-B aligned)."""
+    sB, sC, sH, sW = x.stride()
+    C = x.shape[1]
+    return (x.dtype == torch.float32 and C % 32 == 0 and sC == 1 and sW >= C and sH >= sW * x.shape[3]
+            and sW % 4 == 0 and sH % 4 == 0 and sB % 4 == 0 and x.data_ptr() % 16 == 0)
+
+
+def to_channels_last_into(srcs, dsts) -> list:
+    """``mvbev_nchw_to_nhwc_f32``: copy fp32 ``srcs[i]`` [B,C,H,W] (any strides) into the contiguous
+    [B,H,W,C] ``dsts[i]``, every view in one launch; returns the channels-last [B,C,H,W] views of
+    ``dsts`` (the same logical tensors as ``srcs``)."""
+    n = len(srcs)
+    if n == 0:
+        return []
+    if len(dsts) != n or n > 16:
+        raise ValueError("need 1..16 matching srcs / dsts")
+    _require_cuda(*srcs, *dsts)
+    B, C, H, W = srcs[0].shape
+    arr = (_native.WarpView * n)()
+    for i, (s_, d) in enumerate(zip(srcs, dsts)):
+        if tuple(s_.shape) != (B, C, H, W) or s_.dtype != torch.float32:
+            raise ValueError("all views must be fp32 [B,C,H,W] of one shape")
+        if tuple(d.shape) != (B, H, W, C) or d.dtype != torch.float32 or not d.is_contiguous():
+            raise ValueError(f"dst must be a contiguous fp32 [{B},{H},{W},{C}] tensor")
+        arr[i] = _native.WarpView(s_.data_ptr(), (ctypes.c_int64 * 4)(*s_.stride()), d.data_ptr(),
+                                  (ctypes.c_int64 * 4)(0, 0, 0, 1), (ctypes.c_float * 9)())
+    st = _native.load().mvbev_nchw_to_nhwc_f32(arr, n, B, C, H, W, _stream(dsts[0]))
+    _native.check(st, "mvbev_nchw_to_nhwc_f32")
+    return [d.permute(0, 3, 1, 2) for d in dsts]
+
+
 # ----------------------------------------------------------------------------------------------
 # convs
 

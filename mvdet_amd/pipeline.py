@@ -79,6 +79,7 @@ class Workspace:
     guard_src: Optional[tuple] = None
     g_slab: Optional[torch.Tensor] = None   # the exact path's fp32 slab [S, B, Cs, Ho, Wo] and y1
     g_y1: Optional[torch.Tensor] = None
+    cl_maps: Optional[list] = None          # channels-last copies of NCHW backbone maps (cl_upsample)
 
 
 class ProjectFuse:
@@ -93,7 +94,7 @@ class ProjectFuse:
                  precision: str = "bf16x3", slab_dtype: torch.dtype = torch.float32,
                  all_views: bool = True, split_k: bool = True, frustum: bool = True, fuse_conv3: bool = True,
                  edge_strip: bool = True, wino_conv1: bool = True, wino_warp: bool = True,
-                 wino_conv2: bool = True, nonfinite_guard: bool = True):
+                 wino_conv2: bool = True, nonfinite_guard: bool = True, cl_upsample: bool = True):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":
@@ -178,6 +179,10 @@ class ProjectFuse:
         # conv2 (exact products: inf * w stays inf, torch's NaN-preserving ReLU) and conv3 — every
         # launch gated on the flag, so with finite features they exit at once and nothing is synced.
         self.nonfinite_guard = nonfinite_guard
+        # cl_upsample (default): the fused upsample warp reads channels-last backbone maps (one 128-B line
+        # per pixel and 32 channels: warp_up_wino_cl_kernel); NCHW maps are copied to channels-last first
+        # (mvbev_nchw_to_nhwc_f32, 1/9 of the upsampled size) when C % 32 == 0
+        self.cl_upsample = cl_upsample
         self._pack1f: Optional[ops.PackedConv3x3] = None
         self._pack2f: Optional[ops.PackedConv3x3] = None
         self._chan_map = chan_map
@@ -335,13 +340,26 @@ class ProjectFuse:
             if f.shape[1] != self.C or f.shape[2] > self.src_hw[0] or f.shape[3] > self.src_hw[1]:
                 raise ValueError(f"view {cam}: features {tuple(f.shape)} cannot upsample to {self.src_hw}")
         self._check_warp_ws(ws)
-        if self._wino_warp_applies(ws, feats) and all(f.shape[3] >= 4 and f.stride(3) == 1 for f in feats):
-            self._warp_views_t(ws, cams, feats, up_hw=self.src_hw)  # a4 + a5 + a6 + conv1's B^T in one pass
+        if self._wino_warp_applies(ws, feats) and all(
+                f.shape[3] >= 4 and (f.stride(3) == 1 or ops.is_channels_last_source(f)) for f in feats):
+            src = list(feats)
+            if self.cl_upsample and self.C % 32 == 0 and not all(ops.is_channels_last_source(f) for f in src):
+                src = self._channels_last_maps(ws, src)
+            self._warp_views_t(ws, cams, src, up_hw=self.src_hw)  # a4 + a5 + a6 + conv1's B^T in one pass
             return
         self._slab_after_t(ws, cams)
         ops.warp_views_upsampled_into(list(feats), self.src_hw, [self.m_norm_cpu[c] for c in cams],
                                       [self._slot_dst(ws, c) for c in cams], split=self.split,
                                       dst_zeroed=self.split and ws.slab_zeroed)
+
+    def _channels_last_maps(self, ws: Workspace, feats) -> list:
+        """The views' backbone maps copied to channels-last buffers of the workspace (one launch)."""
+        B, C, h, w = feats[0].shape
+        shape = (B, h, w, C)
+        if ws.cl_maps is None or len(ws.cl_maps) < len(feats) or tuple(ws.cl_maps[0].shape) != shape:
+            ws.cl_maps = [torch.empty(shape, dtype=torch.float32, device=ws.slab.device)
+                          for _ in range(max(len(feats), self.num_cam))]
+        return ops.to_channels_last_into(list(feats), ws.cl_maps[:len(feats)])
 
     # -- coord term (a2 folded into conv1) --------------------------------------------------
     def coord_term(self, conv1: torch.nn.Conv2d) -> torch.Tensor:

@@ -242,6 +242,23 @@ def test_fused_warp_transform_matches_two_pass(cfg):
     assert_parity(m3.cpu(), ref.cpu(), "slab path after the fused warp", normwise_tol=TOL)
 
 
+def _t_value(t: torch.Tensor, Wo: int) -> torch.Tensor:
+    """T rows (hi plane then lo plane, bf16) -> hi + lo in fp32."""
+    h = t.view(torch.bfloat16).view(-1, 2, Wo, 8).float()
+    return h[:, 0] + h[:, 1]
+
+
+def _assert_same_t(va: torch.Tensor, vb: torch.Tensor) -> None:
+    """Same NaN / inf positions; finite values equal up to the fp32 rounding of the bilinear sums
+    (an fp32 ulp of t can move lo = bf16(t - hi) by one of its own ulps: <= 2^-16 |t|)."""
+    assert torch.equal(va.isnan(), vb.isnan()) and torch.equal(va.isinf(), vb.isinf())
+    inf = va.isinf()
+    assert torch.equal(va[inf], vb[inf])
+    fin = va.isfinite()
+    scale = va[fin].abs().max().item()
+    assert ((va[fin] - vb[fin]).abs() <= 2.0 ** -15 * va[fin].abs() + 1e-6 * scale).all()
+
+
 @pytest.mark.parametrize("cfg,C,B", [(1, 32, 1), (2, 64, 2), (2, 40, 1)])
 def test_fused_warp_channels_last_matches_nchw(cfg, C, B):
     """Channels-last sources (sC == 1, C % 32 == 0: warp_wino_cl_kernel, one 128-B line per source
@@ -277,18 +294,64 @@ def test_fused_warp_channels_last_matches_nchw(cfg, C, B):
     assert fa == fz == fb == fbz == 7
     assert torch.equal(a, az) and torch.equal(b, bz)
 
-    def value(x):  # T rows: hi plane then lo plane -> hi + lo in fp32
-        h = x.view(torch.bfloat16).view(-1, 2, Wo, 8).float()
-        return h[:, 0] + h[:, 1]
-    va, vb = value(a), value(b)
-    # same NaN / inf positions; finite values equal up to the fp32 contraction order of the bilinear sum
-    # (fma vs. separate products, which the two kernels' compilers may pick differently)
-    assert torch.equal(va.isnan(), vb.isnan()) and torch.equal(va.isinf(), vb.isinf())
-    fin = va.isfinite()
-    assert torch.equal(va[~fin & ~va.isnan()], vb[~fin & ~vb.isnan()])
-    # (an fp32 ulp of t can move lo = bf16(t - hi) by one of its own ulps: <= 2^-16 |t|)
-    scale = va[fin].abs().max().item()
-    assert ((va[fin] - vb[fin]).abs() <= 2.0 ** -15 * va[fin].abs() + 1e-6 * scale).all()
+    _assert_same_t(_t_value(a, Wo), _t_value(b, Wo))
+
+
+@pytest.mark.parametrize("cfg,C,B", [(1, 32, 1), (2, 64, 2), (2, 40, 1)])
+def test_fused_upsample_warp_channels_last_matches_nchw(cfg, C, B):
+    """The fused 3x upsample + warp + B^T from channels-last backbone maps (warp_up_wino_cl_kernel:
+    line-per-pixel box staging, the transform in registers) — given channels-last, or copied from NCHW
+    by mvbev_nchw_to_nhwc_f32 — gives the T of the NCHW kernel (to fp32 rounding): NaN geometry, an inf
+    feature, the non-finite report and skip_zero included.  The copy equals torch's channels_last
+    copy exactly.  C = 40 (no whole 32-channel groups) with channels-last strides is refused."""
+    from mvdet_amd import _native, ops, synthetic
+    from mvdet_amd.geometry import kornia_src_norm_from_dst_norm, projection_matrices
+    spec = synthetic.CONFIGS[cfg]
+    ds = spec["make"]()
+    N = ds.num_cam
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    ms = [kornia_src_norm_from_dst_norm(M.float().reshape(1, 3, 3), up, grid)[0] for M in projection_matrices(ds)]
+    ms[-1] = ms[-1].clone()
+    ms[-1][0, 2] = float("inf")
+    low = [u // 3 for u in up]
+    feats = [synthetic.backbone_features(B, C, low, seed=81 + v, device=DEV) for v in range(N)]
+    feats[0][B - 1, C - 1, low[0] // 2, low[1] // 2] = float("inf")
+    Ho, Wo = grid
+    r3 = 4 * (-(-Ho // 12))
+    numel = B * (N * C // 8) * 5 * r3 * Wo * 16
+
+    def run(src, zeroed):
+        t = torch.zeros(numel, dtype=torch.bfloat16, device=DEV)
+        flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+        ops.warp_views_wino_rows_into(src, ms, t, list(range(N)), C, N * C, Ho, Wo, dst_zeroed=zeroed, up_hw=up,
+                                      nonfinite=(flag, 5))
+        assert int(flag.item()) == 5
+        return t.view(torch.int16).cpu()
+
+    cl = [f.contiguous(memory_format=torch.channels_last) for f in feats]
+    if C % 32:
+        with pytest.raises(_native.NativeError):
+            run(cl, True)
+        return
+    bufs = [torch.empty(B, low[0], low[1], C, device=DEV) for _ in range(N)]
+    copied = ops.to_channels_last_into(feats, bufs)
+    for a_, b_ in zip(copied, cl):
+        assert torch.equal(a_, b_) and ops.is_channels_last_source(a_)
+    base = run(feats, False)
+    assert torch.equal(base, run(feats, True))
+    va = _t_value(base, Wo)
+    got = run(cl, False)
+    for src, zeroed in ((cl, True), (copied, False), (copied, True)):
+        assert torch.equal(got, run(src, zeroed))
+    vb = _t_value(got, Wo)
+    # the NCHW kernel's near-field blocks load 4-column window rows (a zero-weight 4th column: an inf
+    # there gives NaN), so it may hold NaN where the channels-last kernel (3 columns) does not; every
+    # non-finite value of the channels-last T is non-finite there too, and the rest agree
+    assert not (~vb.isfinite() & va.isfinite()).any()
+    both = va.isfinite() & vb.isfinite()
+    scale = va[both].abs().max().item()
+    assert ((va[both] - vb[both]).abs() <= 2.0 ** -15 * va[both].abs() + 1e-6 * scale).all()
+    assert both.float().mean().item() > 0.5
 
 
 # -- conv2 (dilation 2) -> conv3 partials as row-Winograd (ABI 11500) ------------------------------

@@ -1,4 +1,8 @@
+#!/bin/bash
+# A short GPU session: a subset of the GPU suite, then kbench stages (interleaved rounds).
+# Usage: bash tools/ab_session.sh <tag> "<test files>" "<kbench stages>" [kbench extra args]
 set -e
+TAG=$1; TESTS=$2; STAGES=$3; shift 3
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_wino.py > gpurun_out/r04d_pytest.txt 2>&1
-timeout -k 10 200 python tools/kbench.py --only warpw,warpwcl,warpupw --rounds 3 --reps 30 --libs mvdet_amd/lib/exp/libmvbev_pad4.so,mvdet_amd/lib/exp/libmvbev_pad8.so > gpurun_out/r04d_kbench.jsonl
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu $TESTS > gpurun_out/${TAG}_pytest.txt 2>&1
+timeout -k 10 240 python tools/kbench.py --only $STAGES --rounds 3 --reps 30 "$@" > gpurun_out/${TAG}_kbench.jsonl

@@ -129,6 +129,7 @@ def main():
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=v, device=dev) for v in range(N)]
     cfeats = [f.contiguous(memory_format=torch.channels_last) for f in feats]
     bfeats = [synthetic.backbone_features(B, C, [u // 3 for u in up], seed=v, device=dev) for v in range(N)]
+    cbfeats = [f.contiguous(memory_format=torch.channels_last) for f in bfeats]
     ws = eng.workspace(B, dev)
     with torch.no_grad():
         for v in range(N):
@@ -160,6 +161,12 @@ def main():
             # the same on channels-last features (warp_wino_cl_kernel)
             "warpwcl": (lambda: _with(weng, "wino_warp", True, lambda: weng.warp_views(wws, list(range(N)), cfeats)),
                         None),
+            # the fused upsample warp on NCHW maps without the channels-last copy (the round-3/4 NCHW kernel),
+            # and on maps that are channels-last already
+            "warpupwn": (lambda: _with(weng, "cl_upsample", False, lambda: _with(weng, "wino_warp", True,
+                         lambda: weng.warp_views_upsampled(wws, list(range(N)), bfeats))), None),
+            "warpupwcl": (lambda: _with(weng, "wino_warp", True,
+                                        lambda: weng.warp_views_upsampled(wws, list(range(N)), cbfeats)), None),
             "warpupw": (lambda: _with(weng, "wino_warp", True,
                                       lambda: weng.warp_views_upsampled(wws, list(range(N)), bfeats)), None),
             "winoconv": (lambda: ops.conv3x3_wino(wws.wino_t, wd1, weng.pack1w.get(mc[0].weight), 512,

@@ -96,6 +96,10 @@ struct WarpCoord {
   bool finite, inside;  // !finite -> NaN output; finite && !inside -> exactly 0 (zero padding)
 };
 __device__ inline WarpCoord warp_coord(const float (&m)[9], int u, int v, int Ho, int Wo, int H, int W) {
+  // no fma contraction: every kernel (and the tile mask) must get the same ix / iy bit for bit — an
+  // ulp of ix (~3e-5 at a few hundred pixels) moves the bilinear weights by as much, and fma
+  // contraction is a per-call-site compiler choice
+#pragma clang fp contract(off)
   const float gx = ((float)u / (float)(Wo - 1) - 0.5f) * 2.0f;
   const float gy = ((float)v / (float)(Ho - 1) - 0.5f) * 2.0f;
   float x = gx * m[0] + gy * m[1] + m[2];
@@ -148,6 +152,7 @@ struct UpWindow {
 };
 __device__ inline UpWindow up_window(const float (&m)[9], int u, int v, int Ho, int Wo, int H, int W, int h, int w,
                                      float sy, float sx) {
+#pragma clang fp contract(off)  // (as warp_coord: the same window weights in every kernel)
   UpWindow r;
   const WarpCoord wc = warp_coord(m, u, v, Ho, Wo, H, W);
   const float ix = wc.ix, iy = wc.iy;

@@ -350,7 +350,10 @@ def test_fused_upsample_warp_channels_last_matches_nchw(cfg, C, B):
     assert not (~vb.isfinite() & va.isfinite()).any()
     both = va.isfinite() & vb.isfinite()
     scale = va[both].abs().max().item()
-    assert ((va[both] - vb[both]).abs() <= 2.0 ** -15 * va[both].abs() + 1e-6 * scale).all()
+    err = (va[both] - vb[both]).abs()
+    bad = err > 2.0 ** -15 * va[both].abs() + 1e-6 * scale
+    assert not bad.any(), (int(bad.sum()), int(bad.numel()), err.max().item(), scale,
+                           va[both][bad][:8].tolist(), vb[both][bad][:8].tolist())
     assert both.float().mean().item() > 0.5
 
 

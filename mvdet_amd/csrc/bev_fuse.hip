@@ -32,7 +32,7 @@ constexpr int64_t kTileW = MVBEV_CONV_TILE_W;
 constexpr size_t kAlign = 256;
 
 enum Region { R_MAP1, R_MAPC, R_PACK1, R_PACK2, R_PACKC, R_CIN, R_INIT, R_MASK, R_ORDER, R_NF, R_BIG, R_Y1, R_T2,
-              R_GFLAG, R_GPACK1, R_GPACK2, R_GSLAB, R_CLMAPS, R_P3, R_COUNT };
+              R_GFLAG, R_GPACK1, R_GPACK2, R_GSLAB, R_P3, R_COUNT };
 static_assert(R_COUNT <= 24, "mvbev_bev_plan.off");
 
 size_t align_up(size_t v) { return (v + kAlign - 1) / kAlign * kAlign; }
@@ -76,21 +76,16 @@ void slab_views(const mvbev_bev_plan* p, const void* const* views, void* slab, m
   }
 }
 
-// the same writing slot s's channels of T (the Winograd transform of the whole grid); cl: the sources are
-// the channels-last copies [B][h][w][C] in the workspace (backbone maps, C % 32 == 0)
-void t_views(const mvbev_bev_plan* p, const void* const* views, void* t, mvbev_warp_view* out, const float* cl) {
+// the same writing slot s's channels of T (the Winograd transform of the whole grid)
+void t_views(const mvbev_bev_plan* p, const void* const* views, void* t, mvbev_warp_view* out) {
   const mvbev_bev_geometry& g = p->g;
   const bool backbone = g.src_kind == MVBEV_BEV_SRC_BACKBONE_F32;
   const int64_t sh = backbone ? g.h : g.H, sw = backbone ? g.w : g.W;
   const int64_t r3 = 4 * ((g.Ho + 11) / 12), K8 = g.num_views * p->Cs / kKC;
   for (int s = 0; s < g.num_views; ++s) {
     mvbev_warp_view& v = out[s];
-    v.src = cl ? static_cast<const void*>(cl + (size_t)s * g.B * g.C * sh * sw) : views[s];
-    if (cl) {
-      v.src_strides[0] = g.C * sh * sw; v.src_strides[1] = 1; v.src_strides[2] = sw * g.C; v.src_strides[3] = g.C;
-    } else {
-      v.src_strides[0] = g.C * sh * sw; v.src_strides[1] = sh * sw; v.src_strides[2] = sw; v.src_strides[3] = 1;
-    }
+    v.src = views[s];
+    v.src_strides[0] = g.C * sh * sw; v.src_strides[1] = sh * sw; v.src_strides[2] = sw; v.src_strides[3] = 1;
     v.dst = static_cast<char*>(t) + (size_t)32 * (s * (p->Cs / kKC)) * 5 * r3 * g.Wo;
     v.dst_strides[0] = K8 * 5 * r3 * g.Wo; v.dst_strides[1] = 5 * r3 * g.Wo; v.dst_strides[2] = g.Wo;
     v.dst_strides[3] = 1;
@@ -164,9 +159,6 @@ int mvbev_bev_plan_init(const mvbev_bev_geometry* g, mvbev_bev_plan* p) {
   sz[R_GPACK1] = p->guard ? 4 * mvbev_conv3x3_packed_floats(kMid, K) : 0;
   sz[R_GPACK2] = p->guard ? 4 * mvbev_conv3x3_packed_floats(kMid, kMid) : 0;
   sz[R_GSLAB] = p->guard ? slab_bytes : 0;
-  // channels-last copies of the backbone maps (ABI 11700: the line-per-pixel fused upsample warp)
-  sz[R_CLMAPS] = (p->wino && g->src_kind == MVBEV_BEV_SRC_BACKBONE_F32 && g->C % 32 == 0)
-                     ? (size_t)g->num_views * g->B * g->C * g->h * g->w * 4 : 0;
   sz[R_P3] = mvbev_conv3x3_bf16x3_cout1_partials_bytes(&d2, kMid);
   size_t o = 0;
   for (int r = 0; r < R_COUNT; ++r) {
@@ -298,13 +290,7 @@ int mvbev_bev_fuse(const mvbev_bev_plan* p, const void* const* views, float* map
   if (gflag && hipMemsetAsync(gflag, 0, 4, static_cast<hipStream_t>(stream)) != hipSuccess) return MVBEV_ERR_HIP;
   // a4 + a5 + a6 (+ conv1's B^T): the warp of every view in one launch
   if (p->wino) {
-    float* cl = p->off[R_CLMAPS + 1] > p->off[R_CLMAPS] ? at<float>(ws, p, R_CLMAPS) : nullptr;
-    if (cl) {  // NCHW backbone maps -> channels-last copies, every view in one launch
-      slab_views(p, views, cl, wv);
-      for (int s = 0; s < g.num_views; ++s) wv[s].dst = cl + (size_t)s * g.B * g.C * g.h * g.w;
-      BEV_TRY(mvbev_nchw_to_nhwc_f32(wv, g.num_views, g.B, g.C, g.h, g.w, stream));
-    }
-    t_views(p, views, big, wv, cl);
+    t_views(p, views, big, wv);
     const int64_t r3 = 4 * ((g.Ho + 11) / 12);
     if (backbone)
       BEV_TRY(mvbev_warp_views_upsampled_wino_rows(wv, g.num_views, g.B, g.C, g.h, g.w, g.H, g.W, g.Ho, g.Wo, r3,

@@ -335,7 +335,8 @@ def run_plus_a4(args, precision, steps, warmup):
     ws = eng.workspace(B, dev)
     views = list(range(N))
     out = {}
-    for mode in ("fused", "unfused"):
+    flo_cl = [f.contiguous(memory_format=torch.channels_last) for f in flo]
+    for mode in ("fused", "unfused", "fused_channels_last"):
         e0 = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
         e1 = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
         e2 = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
@@ -345,6 +346,8 @@ def run_plus_a4(args, precision, steps, warmup):
                 e0[i].record()
             if mode == "fused":
                 eng.warp_views_upsampled(ws, views, flo)
+            elif mode == "fused_channels_last":  # the same maps in channels_last memory format
+                eng.warp_views_upsampled(ws, views, flo_cl)
             else:
                 eng.warp_views(ws, views, [F.interpolate(f, list(up), mode="bilinear") for f in flo])
             if i is not None:
@@ -365,7 +368,8 @@ def run_plus_a4(args, precision, steps, warmup):
         out[mode] = {"value": round(B * steps / dt, 3), "ms_per_step": round(dt * 1e3 / steps, 4),
                      "upsample_and_warp_ms": round(float(np.mean([e0[i].elapsed_time(e1[i]) for i in range(steps)])), 4)}
     out["note"] = ("step from backbone-resolution features: a4 upsample (:65) + warp + concat + fusion; "
-                   "fused = upsample evaluated inside the warp kernel")
+                   "fused = upsample evaluated inside the warp kernel (NCHW maps); fused_channels_last = the same "
+                   "maps in channels_last memory format (warp_up_wino_cl_kernel)")
     return out
 
 

@@ -336,13 +336,17 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino2_kerne
 //   phase 2: B^T of each 3-row tile's 5 rows from the thread's own registers, 8 B of hi and lo per
 //            T row (no LDS round trip).
 // A block whose box exceeds kUcStage (the near field) reads its taps straight from global memory.
-constexpr int kUcCh = 32, kUcThreads = 128, kUcStage = 256, kWcPixUp = kWwRows * kWwCols;
+#ifndef MVBEV_UPCL_STAGE
+#define MVBEV_UPCL_STAGE 128
+#endif
+constexpr int kUcCh = 32, kUcThreads = 128, kUcStage = MVBEV_UPCL_STAGE, kWcPixUp = kWwRows * kWwCols;
 static_assert(kWwCols * 8 == kUcThreads, "thread = (column, channel quad)");
 
 __global__ __launch_bounds__(kUcThreads) void warp_up_wino_cl_kernel(const UpArgs ua, int r3_rows) {
   __shared__ __attribute__((aligned(16))) f32x4a_t box_px[kUcStage * 8];  // [pixel][quad]
-  __shared__ __attribute__((aligned(16))) f32x4a_t pax[kWcPixUp], pay[kWcPixUp];
-  __shared__ __attribute__((aligned(16))) int4 pint[kWcPixUp];  // rb, cb, class (0 zero, 1 inside, 2 NaN)
+  __shared__ __attribute__((aligned(16))) f32x4a_t pax[kWcPixUp];  // ax0, ax1, ax2, ay0
+  __shared__ __attribute__((aligned(8))) f32x2_t pay[kWcPixUp];     // ay1, ay2
+  __shared__ int pint[kWcPixUp];  // rb << 16 | cb << 2 | class (0 zero, 1 inside, 2 NaN)
   __shared__ int box[4];
   const WarpArgs& a = ua.w;
   const int lb = xcd_remap(blockIdx.x, a.nwg);
@@ -376,9 +380,9 @@ __global__ __launch_bounds__(kUcThreads) void warp_up_wino_cl_kernel(const UpArg
     for (int j = 0; j < 3; ++j) uw.ax[j] = uw.ay[j] = 0.f;
     if (v >= 0 && v < a.Ho && u < a.Wo) uw = up_window(m, u, v, a.Ho, a.Wo, H, W, h, w, ua.sy, ua.sx);
     const int cl = uw.inside ? 1 : (uw.finite ? 0 : 2);
-    pax[p] = f32x4a_t{uw.ax[0], uw.ax[1], uw.ax[2], 0.f};
-    pay[p] = f32x4a_t{uw.ay[0], uw.ay[1], uw.ay[2], 0.f};
-    pint[p] = make_int4(uw.rb, uw.cb, cl, 0);
+    pax[p] = f32x4a_t{uw.ax[0], uw.ax[1], uw.ax[2], uw.ay[0]};
+    pay[p] = f32x2_t{uw.ay[1], uw.ay[2]};
+    pint[p] = (uw.rb << 16) | (uw.cb << 2) | cl;
     if (cl == 1) {
       r0 = min(r0, uw.rb);
       r1 = max(r1, min(uw.rb + 2, h - 1));
@@ -420,15 +424,17 @@ __global__ __launch_bounds__(kUcThreads) void warp_up_wino_cl_kernel(const UpArg
 #pragma unroll
   for (int i = 0; i < kWwRows; ++i) {  // phase 1
     const int p = i * kWwCols + c;
-    const int4 pi = pint[p];
-    const f32x4a_t ax = pax[p], ay = pay[p];
+    const int pk = pint[p], cls = pk & 3, prb = pk >> 16, pcb = (pk >> 2) & 0x3fff;
+    const f32x4a_t ax = pax[p];
+    const f32x2_t ay12 = pay[p];
+    const f32x4a_t ay = {ax.w, ay12.x, ay12.y, 0.f};
     f32x4a_t acc = {0.f, 0.f, 0.f, 0.f};
-    if (pi.z == 1) {
+    if (cls == 1) {
       int ro[3], co[3];
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        ro[j] = min(pi.x + j, h - 1);
-        co[j] = min(pi.y + j, w - 1);
+        ro[j] = min(prb + j, h - 1);
+        co[j] = min(pcb + j, w - 1);
       }
       f32x4a_t s[3][3];
       if (staged) {
@@ -451,11 +457,11 @@ __global__ __launch_bounds__(kUcThreads) void warp_up_wino_cl_kernel(const UpArg
         rr += ax.z * s[r][2];
         acc += (r == 0 ? ay.x : r == 1 ? ay.y : ay.z) * rr;
       }
-    } else if (pi.z == 2) {
+    } else if (cls == 2) {
       acc = f32x4a_t{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf("")};
     }
     d[i] = acc;
-    nzr[i] = pi.z != 0;
+    nzr[i] = cls != 0;
   }
   if (u >= a.Wo) return;
   const int chunk = grp * (kUcCh / 8) + (q >> 1), half = q & 1;
@@ -650,7 +656,7 @@ extern "C" int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views
   ua.sx = (float)w / (float)W;
   // channels-last maps (every view: unit channel stride, 16-B aligned whole 32-channel groups) take the
   // line-per-pixel kernel; NCHW maps need unit column stride (16-B window rows)
-  bool cl = C % kUcCh == 0;
+  bool cl = C % kUcCh == 0 && h < 32768 && w < 16384;  // (the packed window origin of the kernel)
   for (int i = 0; i < nviews; ++i) {
     const WarpView& d = a.v[i];
     cl = cl && d.sC == 1 && d.sW >= C && d.sH >= d.sW * w && d.sB >= 0 && d.sW % 4 == 0 && d.sH % 4 == 0 &&

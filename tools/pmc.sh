@@ -12,7 +12,7 @@ cd $R
 i=0
 for PMC in "$@"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $PMC --output-format csv -d $OUT/${TAG}_$i -o run -- \
+  timeout -s KILL 150 rocprofv3 --pmc $PMC --output-format csv -d $OUT/${TAG}_$i -o run -- \
     python3 tools/kbench.py --only $STAGES --reps 2 > $OUT/${TAG}_$i.log 2>&1 || { echo "pass $i failed"; exit 1; }
 done
 python3 tools/pmc_summary.py $OUT/${TAG}_* > $OUT/${TAG}_summary.txt && cat $OUT/${TAG}_summary.txt

@@ -357,6 +357,36 @@ def test_fused_upsample_warp_channels_last_matches_nchw(cfg, C, B):
     assert both.float().mean().item() > 0.5
 
 
+@pytest.mark.parametrize("cl_upsample", [False, True])
+def test_engine_channels_last_backbone_maps(cl_upsample):
+    """ProjectFuse from channels-last backbone maps (the line-per-pixel fused upsample warp), and from
+    NCHW maps copied to channels-last (cl_upsample), gives the NCHW engine's map; the training forward
+    (slab path) accepts channels-last maps too."""
+    from mvdet_amd import ProjectFuse, synthetic
+    from mvdet_amd.geometry import projection_matrices
+    ds = synthetic.CONFIGS[1]["make"]()
+    N, C, B = ds.num_cam, 32, 1
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    pm = projection_matrices(ds)
+    low = [synthetic.backbone_features(B, C, [u // 3 for u in up], seed=91 + v, device=DEV) for v in range(N)]
+    torch.manual_seed(3)
+    mc = torch.nn.Sequential(torch.nn.Conv2d(N * C + 2, 512, 3, padding=1), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
+                             torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False)).to(DEV)
+    ref_eng = ProjectFuse(pm, up, grid, C)
+    eng = ProjectFuse(pm, up, grid, C, cl_upsample=cl_upsample)
+    with torch.no_grad():
+        wr = ref_eng.workspace(B, DEV)
+        ref_eng.warp_views_upsampled(wr, list(range(N)), low)
+        ref = ref_eng.fuse(wr, mc)
+        src = low if cl_upsample else [f.contiguous(memory_format=torch.channels_last) for f in low]
+        w = eng.workspace(B, DEV)
+        eng.warp_views_upsampled(w, list(range(N)), src)
+        assert w.t_from_warp
+        got = eng.fuse(w, mc)
+    assert_parity(got.cpu(), ref.cpu(), "channels-last backbone maps", normwise_tol=TOL)
+
+
 # -- conv2 (dilation 2) -> conv3 partials as row-Winograd (ABI 11500) ------------------------------
 def _conv2_setup(B, K, H, W, rows, cout, seed):
     """y1-like split-bf16 input, conv2 weights / bias, conv3 weight, and the float64 reference

@@ -360,8 +360,7 @@ def test_fused_upsample_warp_channels_last_matches_nchw(cfg, C, B):
 @pytest.mark.parametrize("cl_upsample", [False, True])
 def test_engine_channels_last_backbone_maps(cl_upsample):
     """ProjectFuse from channels-last backbone maps (the line-per-pixel fused upsample warp), and from
-    NCHW maps copied to channels-last (cl_upsample), gives the NCHW engine's map; the training forward
-    (slab path) accepts channels-last maps too."""
+    NCHW maps copied to channels-last (cl_upsample), gives the NCHW engine's map."""
     from mvdet_amd import ProjectFuse, synthetic
     from mvdet_amd.geometry import projection_matrices
     ds = synthetic.CONFIGS[1]["make"]()

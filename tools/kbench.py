@@ -165,6 +165,9 @@ def main():
             # and on maps that are channels-last already
             "warpupwn": (lambda: _with(weng, "cl_upsample", False, lambda: _with(weng, "wino_warp", True,
                          lambda: weng.warp_views_upsampled(wws, list(range(N)), bfeats))), None),
+            # NCHW maps copied to channels-last first (cl_upsample), then the line-per-pixel kernel
+            "warpupwt": (lambda: _with(weng, "cl_upsample", True, lambda: _with(weng, "wino_warp", True,
+                         lambda: weng.warp_views_upsampled(wws, list(range(N)), bfeats))), None),
             "warpupwcl": (lambda: _with(weng, "wino_warp", True,
                                         lambda: weng.warp_views_upsampled(wws, list(range(N)), cbfeats)), None),
             "warpupw": (lambda: _with(weng, "wino_warp", True,

@@ -88,7 +88,9 @@ class PerspTransDetector(nn.Module):
             imgs_result.append(self._img_head_lowres(feat))
             # the 3x upsample (:65) happens inside the fused warp below (and, training, its
             # adjoint inside the warp adjoint)
-            low.append(feat.contiguous())
+            # (a channels-last backbone's maps stay channels-last: the fused warp's line-per-pixel kernel)
+            cl = feat.dim() == 4 and feat.is_contiguous(memory_format=torch.channels_last)
+            low.append(feat if cl else feat.contiguous())
             if visualize:
                 up = F.interpolate(feat, self.upsample_shape, mode="bilinear")
                 self._show(torch.norm(up[0].detach(), dim=0))

@@ -1,7 +1,8 @@
 """Full-size parity of the measured path against the CPU oracle at every BASELINE.json config.
 
 The path checked is the one ``bench.py`` times and ``PerspTransDetector`` runs by default:
-the fused warp + row-Winograd transform (``warp_wino_kernel`` / ``warp_up_wino_kernel``), the
+the fused warp + row-Winograd transform (``warp_wino_kernel`` / ``warp_up_wino2_kernel``, and the
+channels-last ``warp_wino_cl_kernel``), the
 Winograd conv1 (``conv_wino_kernel``), conv2 with conv3's partials in its epilogue and the
 partials' reduce — plus the direct ring conv1 as the second form at configs 1 and 2.
 
@@ -78,16 +79,19 @@ def _check_warp_whole(eng, ws, feats, warped, what):
         eng.wino_warp = fused
 
 
-@pytest.mark.parametrize("cfg", [1, 2])
-@pytest.mark.parametrize("conv1", ["wino", "direct"])
-def test_full_size_path_vs_oracle(cfg, conv1):
+@pytest.mark.parametrize("cfg,conv1,layout", [(1, "wino", "nchw"), (1, "direct", "nchw"), (2, "wino", "nchw"),
+                                               (2, "direct", "nchw"), (2, "wino", "channels_last")])
+def test_full_size_path_vs_oracle(cfg, conv1, layout):
     """Configs 1 and 2 whole: the bench's path (``conv1="wino"``: fused warp + B^T, row-Winograd
     conv1, conv2 -> conv3 partials; the default) and the direct ring conv1, vs the oracle:
-    every view's warp, conv1, conv2 and map_result."""
+    every view's warp, conv1, conv2 and map_result; at config 2 also from channels-last features
+    (``warp_wino_cl_kernel``, the bench's ``channels_last`` line)."""
     from mvdet_amd import ProjectFuse, synthetic
     ds, B, C, N, up, grid, pm, tp, mc = _setup(cfg)
     hb = [u // 3 for u in up]
     feats = [synthetic.synthetic_features(B, C, hb, up, seed=1000 * cfg + v, device=DEV) for v in range(N)]
+    if layout == "channels_last":
+        feats = [f.contiguous(memory_format=torch.channels_last) for f in feats]
     eng = ProjectFuse(pm, up, grid, C, wino_conv1=conv1 == "wino")
     with torch.no_grad():
         got = eng.project_fuse(feats, mc)
@@ -107,8 +111,8 @@ def test_full_size_path_vs_oracle(cfg, conv1):
         _check_warp_whole(eng, ws, feats, keep["warped"], f"cfg{cfg}")
 
 
-@pytest.mark.parametrize("cfg,C", [(2, 512), (1, 512)])
-def test_detector_inference_path_vs_oracle(cfg, C):
+@pytest.mark.parametrize("cfg,C,layout", [(2, 512, "nchw"), (1, 512, "nchw"), (2, 512, "channels_last")])
+def test_detector_inference_path_vs_oracle(cfg, C, layout):
     """The drop-in module's own inference path at full size: backbone-resolution maps ->
     ``warp_views_upsampled`` (a4 + a5 + a6 + conv1's B^T in ``warp_up_wino_kernel``) -> Winograd
     conv1 -> conv2 / conv3 partials, vs the oracle's upsample (``:65``) + warp + cat + convs
@@ -126,8 +130,12 @@ def test_detector_inference_path_vs_oracle(cfg, C):
     model.base_pt1, model.base_pt2 = nn.Identity(), nn.Identity()
     model.eval()
     low = [synthetic.backbone_features(B, C, hb, seed=2000 * cfg + v, device=DEV) for v in range(N)]
+    imgs = torch.stack(low, 1)
+    if layout == "channels_last":  # [B, N, C, h, w] stored as [B, N, h, w, C]: per-view channels_last maps
+        imgs = torch.stack([f.permute(0, 2, 3, 1) for f in low], 1).permute(0, 1, 4, 2, 3)
+        assert imgs[:, 0].is_contiguous(memory_format=torch.channels_last)
     with torch.no_grad():
-        map_res, imgs_res = model(torch.stack(low, 1))
+        map_res, imgs_res = model(imgs)
         ws = model.engine.workspace(B, DEV)
         assert ws.t_from_warp and model.engine.wino_active(DEV)
         y1 = model.engine.y1_fp32(ws).clone()
@@ -150,15 +158,17 @@ def _bands(H):
     return [(0, 20), (mid, mid + 30), (H - 20, H)]
 
 
-@pytest.mark.parametrize("cfg", [3, 5])
-def test_large_config_path_vs_oracle_bands(cfg):
+@pytest.mark.parametrize("cfg,layout", [(3, "nchw"), (5, "nchw"), (5, "channels_last")])
+def test_large_config_path_vs_oracle_bands(cfg, layout):
     """Configs 3 (Wildtrack 480 x 1440 grid) and 5 (8 views at 4K, 1000 x 1000 grid) on one GPU:
     the default path over the whole grid; the oracle's warp of every view whole, its convs on
-    two row bands (+ the 7-row halo)."""
+    three row bands (+ the 7-row halo); config 5 also from channels-last features."""
     from mvdet_amd import ProjectFuse, synthetic
     ds, B, C, N, up, grid, pm, tp, mc = _setup(cfg)
     hb = [u // 3 for u in up]
     feats = [synthetic.synthetic_features(B, C, hb, up, seed=1000 * cfg + v, device=DEV) for v in range(N)]
+    if layout == "channels_last":
+        feats = [f.contiguous(memory_format=torch.channels_last) for f in feats]
     eng = ProjectFuse(pm, up, grid, C)
     with torch.no_grad():
         got = eng.project_fuse(feats, mc)

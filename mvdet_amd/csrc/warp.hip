@@ -322,12 +322,12 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
 // (same fp32 ops per channel as warp_wino_kernel) for the same logical source.
 // kWcPitch 40 floats: a ds_read_b128 lane group of phase 2 (8 columns x 2 halves) then covers 16 distinct
 // 4-bank slots, (10 c + h) mod 16 (36 left 2-way conflicts: 2.6 M conflict cycles per 3.8 M LDS instructions)
-constexpr int kWcCh = 32, kWcPitch = 40, kWcPix = kWwRows * kWwCols;
+constexpr int kWcCh = 32, kWcPitch = 40, kWcPix = kWwRows * kWcCols;
 constexpr int kWcOutside = 0x7fff0000;  // byte offset of "no corner" (sources must stay below it)
-static_assert(kWwCols == 16 && kWwThreads == 256, "channels-last fused warp: 256 threads, 16 columns");
+static_assert(kWcCols == 16 && kWcThreads == 256, "channels-last fused warp: 256 threads, 16 columns");
 static_assert(kWcPix % 32 == 0, "phase 1: 32 pixels per pass");
 
-__global__ __launch_bounds__(kWwThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))
+__global__ __launch_bounds__(kWcThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))
 void warp_wino_cl_kernel(const WarpArgs a, int r3_rows) {
   __shared__ __attribute__((aligned(16))) float ds[kWcPix * kWcPitch];
   __shared__ float2 crd[kWcPix];
@@ -342,8 +342,8 @@ void warp_wino_cl_kernel(const WarpArgs a, int r3_rows) {
   const int tid = threadIdx.x;
   const int H = a.H, W = a.W;
   if (tid < kWcPix) {
-    const int i = tid / kWwCols, c = tid % kWwCols;
-    const int v = 12 * k - 1 + i, u = tx * kWwCols + c;
+    const int i = tid / kWcCols, c = tid % kWcCols;
+    const int v = 12 * k - 1 + i, u = tx * kWcCols + c;
     unsigned char cl = 0;
     float ix = 0.f, iy = 0.f;
     if (v >= 0 && v < a.Ho && u < a.Wo) {
@@ -402,9 +402,9 @@ void warp_wino_cl_kernel(const WarpArgs a, int r3_rows) {
   __syncthreads();
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const int it = tid + kWwThreads * h;
+    const int it = tid + kWcThreads * h;
     const int half = it & 1, c = (it >> 1) & 15, ch8 = (it >> 5) & 3, q = it >> 7;
-    const int r3 = 4 * k + q, u = tx * kWwCols + c;
+    const int r3 = 4 * k + q, u = tx * kWcCols + c;
     if (r3 >= r3_rows || u >= a.Wo) continue;
     const int i0 = 3 * q;
     if (a.skip_zero && !(cls[i0 * 16 + c] | cls[(i0 + 1) * 16 + c] | cls[(i0 + 2) * 16 + c] |
@@ -679,9 +679,13 @@ int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t
          (reinterpret_cast<uintptr_t>(d.src) & 15) == 0 &&
          ((H - 1) * d.sH + (W - 1) * d.sW + C) * 4 < kWcOutside;
   }
+  if (cl) {
+    a.tiles_x = (int)ceil_div(Wo, kWcCols);
+    a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);
+  }
   a.chunks = (int)ceil_div(C, cl ? kWcCh : kWarpCPB);
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
-  const dim3 grid((unsigned)a.nwg), block(kWwThreads);
+  const dim3 grid((unsigned)a.nwg), block(cl ? kWcThreads : kWwThreads);
   if (cl)
     hipLaunchKernelGGL(warp_wino_cl_kernel, grid, block, 0, as_stream(stream), a, (int)r3_rows);
   else if (pair)

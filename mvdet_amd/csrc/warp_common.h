@@ -212,6 +212,8 @@ __device__ inline UpWindow up_window(const float (&m)[9], int u, int v, int Ho, 
 #define MVBEV_WW_COLS 16  // columns per fused-warp block (threads = 16 x columns; cfg2: 8 0.52-0.56 ms, 16 0.51)
 #endif
 constexpr int kWwRows = 14, kWwCols = MVBEV_WW_COLS, kWwThreads = 16 * kWwCols;
+// the channels-last fused warps' block: 14 rows x 16 columns, 256 (plain) / 128 (upsample) threads
+constexpr int kWcCols = 16, kWcThreads = 256;
 // (several 8-channel groups per block, the sample geometry computed once for all of them, measured
 // no faster at cfg2: 1 group 0.463 / 0.521 ms up / plain, 2 groups 0.462 / 0.538, 4 0.466 / 0.544 —
 // the geometry's VALU work is not what binds these kernels; the TA/TD load path is: 77-84 % busy)

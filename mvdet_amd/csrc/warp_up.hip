@@ -339,8 +339,8 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino2_kerne
 #ifndef MVBEV_UPCL_STAGE
 #define MVBEV_UPCL_STAGE 128
 #endif
-constexpr int kUcCh = 32, kUcThreads = 128, kUcStage = MVBEV_UPCL_STAGE, kWcPixUp = kWwRows * kWwCols;
-static_assert(kWwCols * 8 == kUcThreads, "thread = (column, channel quad)");
+constexpr int kUcCh = 32, kUcThreads = 128, kUcStage = MVBEV_UPCL_STAGE, kWcPixUp = kWwRows * kWcCols;
+static_assert(kWcCols * 8 == kUcThreads, "thread = (column, channel quad)");
 
 __global__ __launch_bounds__(kUcThreads) void warp_up_wino_cl_kernel(const UpArgs ua, int r3_rows) {
   __shared__ __attribute__((aligned(16))) f32x4a_t box_px[kUcStage * 8];  // [pixel][quad]
@@ -370,8 +370,8 @@ __global__ __launch_bounds__(kUcThreads) void warp_up_wino_cl_kernel(const UpArg
   for (int q = 0; q < 9; ++q) m[q] = vw.m[q];
   int r0 = INT32_MAX, r1 = -1, q0 = INT32_MAX, q1 = -1;
   for (int p = tid; p < kWcPixUp; p += kUcThreads) {  // phase 0
-    const int i = p / kWwCols, c = p % kWwCols;
-    const int v = 12 * k - 1 + i, u = tx * kWwCols + c;
+    const int i = p / kWcCols, c = p % kWcCols;
+    const int v = 12 * k - 1 + i, u = tx * kWcCols + c;
     UpWindow uw;
     uw.inside = false;
     uw.finite = true;
@@ -418,12 +418,12 @@ __global__ __launch_bounds__(kUcThreads) void warp_up_wino_cl_kernel(const UpArg
     __syncthreads();
   }
   const int c = tid >> 3, q = tid & 7;  // column, channel quad
-  const int u = tx * kWwCols + c;
+  const int u = tx * kWcCols + c;
   f32x4a_t d[kWwRows];
   bool nzr[kWwRows];
 #pragma unroll
   for (int i = 0; i < kWwRows; ++i) {  // phase 1
-    const int p = i * kWwCols + c;
+    const int p = i * kWcCols + c;
     const int pk = pint[p], cls = pk & 3, prb = pk >> 16, pcb = (pk >> 2) & 0x3fff;
     const f32x4a_t ax = pax[p];
     const f32x2_t ay12 = pay[p];
@@ -663,6 +663,8 @@ extern "C" int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views
          d.sB % 4 == 0 && (reinterpret_cast<uintptr_t>(d.src) & 15) == 0;
   }
   if (cl) {
+    a.tiles_x = (int)ceil_div(Wo, kWcCols);
+    a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);
     a.chunks = (int)(C / kUcCh);
     a.nwg = a.tiles * a.chunks * a.B * a.nviews;
     hipLaunchKernelGGL(warp_up_wino_cl_kernel, dim3((unsigned)a.nwg), dim3(kUcThreads), 0, as_stream(stream), ua,

@@ -1677,50 +1677,24 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     }                                                                                                \
     const ChunkBase dcb = XI == 0 ? cur : nx;                                                        \
     if (XI == 4) advance();                                                                          \
-    if (PB || MVBEV_WINO_DMAIL < 2) {                                                                \
-      fetch_b(0, nslot);                                                                             \
-      fetch_b(1, nslot);                                                                             \
-      fetch_a(P ^ 1, nslot, 0);                                                                      \
-    }                                                                                                \
-    if (!PB && MVBEV_WINO_DMAIL >= 2) {                                                              \
-      /* (A/B) the next slot's fragment reads, then a DMA piece, after each MFMA */                  \
-      __builtin_amdgcn_sched_barrier(0);                                                             \
-      const u32x4* Xn = lds + nslot * SLOT + RUNIT + kl * (TROW / 2) + rg * XW + l32;                \
-      const u32x4* Wn = lds + nslot * SLOT + kl * BN + cw + l32;                                     \
-      _Pragma("unroll") for (int i = 0; i < 6; ++i) {                                                \
-        const int ct = i / 3, pass = i % 3;                                                          \
-        acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pass == 0 ? fa[P][ct][1] : fa[P][ct][0], \
-                                                              pass == 1 ? fb[2][1] : fb[2][0], acc[ct][XI], 0, 0, 0); \
-        __builtin_amdgcn_sched_barrier(0);                                                           \
-        if (i < 2) { /* fb[kw = i][hi, lo] */                                                       \
-          fb[i][0] = __builtin_bit_cast(bf16x8, Xn[DIL * i]);                                        \
-          fb[i][1] = __builtin_bit_cast(bf16x8, Xn[DIL * i + TROW / 4]);                             \
-        } else if (i < 6) { /* fa[P ^ 1][ct'][part] for kw 0 */                                     \
-          const int q = i - 2, ct2 = q >> 1, pp = q & 1;                                             \
-          fa[P ^ 1][ct2][pp] = __builtin_bit_cast(bf16x8, Wn[pp * RHALF + 32 * ct2]);               \
-        }                                                                                            \
-        _Pragma("unroll") for (int j = i * (NWI + NXT) / 6; j < (i + 1) * (NWI + NXT) / 6; ++j)        \
-          issue_piece(dcb, (XI + 4) % 5, slot, j);                                                   \
-        __builtin_amdgcn_sched_barrier(0);                                                           \
-      }                                                                                              \
-    } else if (!PB && MVBEV_WINO_DMAIL) {                                                            \
+    fetch_b(0, nslot);                                                                               \
+    fetch_b(1, nslot);                                                                               \
+    fetch_a(P ^ 1, nslot, 0);                                                                        \
+    if (!PB && MVBEV_WINO_DMAIL) {                                                                   \
       /* (A/B) one DMA piece after each MFMA of the kernel column, fenced so none moves */           \
       __builtin_amdgcn_sched_barrier(0);                                                             \
       _Pragma("unroll") for (int ct = 0; ct < 2; ++ct) {                                             \
         acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[P][ct][1], fb[2][0], acc[ct][XI], 0, 0, 0); \
         __builtin_amdgcn_sched_barrier(0);                                                           \
-        _Pragma("unroll") for (int j = (3 * ct) * (NWI + NXT) / 6; j < (3 * ct + 1) * (NWI + NXT) / 6; ++j) \
-          issue_piece(dcb, (XI + 4) % 5, slot, j);                                                   \
+        issue_piece(dcb, (XI + 4) % 5, slot, 3 * ct);                                                \
         __builtin_amdgcn_sched_barrier(0);                                                           \
         acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[P][ct][0], fb[2][1], acc[ct][XI], 0, 0, 0); \
         __builtin_amdgcn_sched_barrier(0);                                                           \
-        _Pragma("unroll") for (int j = (3 * ct + 1) * (NWI + NXT) / 6; j < (3 * ct + 2) * (NWI + NXT) / 6; ++j) \
-          issue_piece(dcb, (XI + 4) % 5, slot, j);                                                   \
+        issue_piece(dcb, (XI + 4) % 5, slot, 3 * ct + 1);                                            \
         __builtin_amdgcn_sched_barrier(0);                                                           \
         acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[P][ct][0], fb[2][0], acc[ct][XI], 0, 0, 0); \
         __builtin_amdgcn_sched_barrier(0);                                                           \
-        _Pragma("unroll") for (int j = (3 * ct + 2) * (NWI + NXT) / 6; j < (3 * ct + 3) * (NWI + NXT) / 6; ++j) \
-          issue_piece(dcb, (XI + 4) % 5, slot, j);                                                   \
+        if (3 * ct + 2 < NWI + NXT) issue_piece(dcb, (XI + 4) % 5, slot, 3 * ct + 2);               \
         __builtin_amdgcn_sched_barrier(0);                                                           \
       }                                                                                              \
     } else {                                                                                         \

@@ -1548,25 +1548,6 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(dst + RUNIT + j * NIT),
                                                  16, tvo[j], 0, 0, 0);
   };
-  // one DMA piece j of a unit (j < NWI: weights, else T piece j - NWI) — for the interleaved issue
-  auto issue_piece = [&](const ChunkBase& cb, int xi, int slot, int j) __attribute__((always_inline)) {
-    if (wave >= NIW) return;
-    u32x4* dst = lds + slot * SLOT + wave * 64;
-    if (j < NWI) {
-      const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<char*>(cb.w + xi * 3 * 2 * BN * 16), (short)0, 0x7fffffff, 0x00020000);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(dst + j * NIT), 16,
-                                               wvo[j], 0, 0, 0);
-    } else {
-      const int jt = j - NWI;
-      const int32_t rows_b = xi * W * 32;
-      const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<char*>(cb.t + rows_b), (short)0, cb.kv1 ? 0x7fffffff : (int)(tplane_b - rows_b), 0x00020000);
-      if ((jt * NIW + wave) * 64 < TROW)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(dst + RUNIT + jt * NIT),
-                                                 16, tvo[jt], 0, 0, 0);
-    }
-  };
   // the current chunk and the next
   ChunkBase cur = base_of(gbase + ci);
   ChunkBase nx = base_of(step());
@@ -1606,9 +1587,6 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
       if (i < n) __builtin_amdgcn_sched_group_barrier(0x100, (n + 5) / 6, 0);
     }
   };
-#ifndef MVBEV_WINO_DMAIL
-#define MVBEV_WINO_DMAIL 0  // A/B: the unit's DMA pieces issued one per MFMA of the last kernel column
-#endif
 
   // LDS-DMA pieces per wave per unit: waves < WHI issue NPU_HI, the others NPU_LO (the last T
   // piece only where it holds T entries)
@@ -1665,7 +1643,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
       __builtin_amdgcn_s_barrier();                                                                  \
       asm volatile("" ::: "memory");                                                                 \
       /* unit u+4 into this slot: (chunk, xi 4) at xi 0, else (next chunk, xi - 1) */                \
-      if (!MVBEV_WINO_DMAIL) issue_unit(XI == 0 ? cur : nx, (XI + 4) % 5, slot);                     \
+      issue_unit(XI == 0 ? cur : nx, (XI + 4) % 5, slot);                                            \
     } else if (P == 1) {                                                                             \
       /* PAIRB: one barrier per two units, after the odd one: retire units u+1, u+2 (all in      \
          flight), then units u+3, u+4 into the slots of u-1 and u */                                  \
@@ -1675,32 +1653,12 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
       issue_unit(XI <= 1 ? cur : nx, (XI + 3) % 5, (u0 + (R) + 3) & 3);                              \
       issue_unit(XI == 0 ? cur : nx, (XI + 4) % 5, slot);                                            \
     }                                                                                                \
-    const ChunkBase dcb = XI == 0 ? cur : nx;                                                        \
     if (XI == 4) advance();                                                                          \
     fetch_b(0, nslot);                                                                               \
     fetch_b(1, nslot);                                                                               \
     fetch_a(P ^ 1, nslot, 0);                                                                        \
-    if (!PB && MVBEV_WINO_DMAIL) {                                                                   \
-      /* (A/B) one DMA piece after each MFMA of the kernel column, fenced so none moves */           \
-      __builtin_amdgcn_sched_barrier(0);                                                             \
-      _Pragma("unroll") for (int ct = 0; ct < 2; ++ct) {                                             \
-        acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[P][ct][1], fb[2][0], acc[ct][XI], 0, 0, 0); \
-        __builtin_amdgcn_sched_barrier(0);                                                           \
-        issue_piece(dcb, (XI + 4) % 5, slot, 3 * ct);                                                \
-        __builtin_amdgcn_sched_barrier(0);                                                           \
-        acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[P][ct][0], fb[2][1], acc[ct][XI], 0, 0, 0); \
-        __builtin_amdgcn_sched_barrier(0);                                                           \
-        issue_piece(dcb, (XI + 4) % 5, slot, 3 * ct + 1);                                            \
-        __builtin_amdgcn_sched_barrier(0);                                                           \
-        acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[P][ct][0], fb[2][0], acc[ct][XI], 0, 0, 0); \
-        __builtin_amdgcn_sched_barrier(0);                                                           \
-        if (3 * ct + 2 < NWI + NXT) issue_piece(dcb, (XI + 4) % 5, slot, 3 * ct + 2);               \
-        __builtin_amdgcn_sched_barrier(0);                                                           \
-      }                                                                                              \
-    } else {                                                                                         \
-      WINO_MFMAS(P, 2, XI);                                                                          \
-      sched6(std::integral_constant<int, 8>{});                                                      \
-    }                                                                                                \
+    WINO_MFMAS(P, 2, XI);                                                                            \
+    sched6(std::integral_constant<int, 8>{});                                                        \
   } while (0)
     for (int u0 = 0; u0 < U; u0 += 10) {
       WINO_UNIT(0);

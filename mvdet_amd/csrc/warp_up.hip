@@ -759,6 +759,9 @@ struct TransArgs {
   float* dst[kWarpMaxViews];
   int B, C, H, W, ctiles, ptiles;
 };
+// VEC (every view: contiguous planes, sC / sB / H * W multiples of 4, 16-B aligned, C % 32 == 0):
+// 16-B loads of 4 pixels of a channel and 16-B stores of 4 channels of a pixel
+template <bool VEC>
 __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const TransArgs a) {
   __shared__ float t[32][65];
   const int HW = a.H * a.W;
@@ -770,6 +773,29 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const TransArgs a) {
   const int b = blk % a.B, v = blk / a.B;
   const int tid = threadIdx.x;
   const float* src = a.src[v] + (int64_t)b * a.sB[v];
+  float* dst = a.dst[v] + (int64_t)b * HW * a.C;
+  if constexpr (VEC) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {  // thread = (channel, pixel quad)
+      const int cc = (tid >> 4) + 16 * k, pq = tid & 15, p = pt * 64 + 4 * pq;
+      if (p < HW) {
+        const f32x4a_t q = *reinterpret_cast<const f32x4a_t*>(src + (int64_t)(ct * 32 + cc) * a.sC[v] + p);
+        t[cc][4 * pq] = q.x;
+        t[cc][4 * pq + 1] = q.y;
+        t[cc][4 * pq + 2] = q.z;
+        t[cc][4 * pq + 3] = q.w;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {  // thread = (pixel, channel quad)
+      const int pp = (tid >> 3) + 32 * k, cq = tid & 7, p = pt * 64 + pp;
+      if (p < HW)
+        *reinterpret_cast<f32x4a_t*>(dst + (int64_t)p * a.C + ct * 32 + 4 * cq) =
+            f32x4a_t{t[4 * cq][pp], t[4 * cq + 1][pp], t[4 * cq + 2][pp], t[4 * cq + 3][pp]};
+    }
+    return;
+  }
   for (int cc = tid >> 6; cc < 32; cc += 4) {
     const int c = ct * 32 + cc, p = pt * 64 + (tid & 63);
     if (c < a.C && p < HW) {
@@ -778,7 +804,6 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const TransArgs a) {
     }
   }
   __syncthreads();
-  float* dst = a.dst[v] + (int64_t)b * HW * a.C;
   for (int pp = tid >> 5; pp < 64; pp += 8) {
     const int p = pt * 64 + pp, c = ct * 32 + (tid & 31);
     if (p < HW && c < a.C) dst[(int64_t)p * a.C + c] = t[tid & 31][pp];
@@ -807,7 +832,14 @@ extern "C" int mvbev_nchw_to_nhwc_f32(const mvbev_warp_view* views, int nviews, 
   a.ptiles = (int)ceil_div(H * W, 64);
   const int64_t nwg = (int64_t)a.ptiles * a.ctiles * B * nviews;
   if (nwg > INT32_MAX) return MVBEV_ERR_SHAPE;
-  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
+  bool vec = C % 32 == 0 && (H * W) % 4 == 0 && (reinterpret_cast<uintptr_t>(views[0].dst) & 15) == 0;
+  for (int i = 0; i < nviews; ++i)
+    vec = vec && a.sW[i] == 1 && a.sH[i] == W && a.sC[i] % 4 == 0 && a.sB[i] % 4 == 0 &&
+          (reinterpret_cast<uintptr_t>(a.src[i]) & 15) == 0 && (reinterpret_cast<uintptr_t>(a.dst[i]) & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<true>, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
+  else
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<false>, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }

@@ -12,5 +12,5 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 set -e
 timeout -k 10 420 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
 timeout -k 10 120 python tools/kbench.py --only warpw,warpwcl --rounds 2 --reps 30 >> gpurun_out/${TAG}_kbench.jsonl
-timeout -k 10 120 python tools/kbench.py --only warpupwn,warpupw,warpupwcl,conv1,conv2 --rounds 2 --reps 30 >> gpurun_out/${TAG}_kbench.jsonl
+timeout -k 10 120 python tools/kbench.py --only warpupwn,warpupwt,warpupwcl,conv1,conv2 --rounds 2 --reps 30 >> gpurun_out/${TAG}_kbench.jsonl
 timeout -k 10 120 python tools/kbench.py --only winoconv,conv23w --rounds 2 --reps 30 >> gpurun_out/${TAG}_kbench.jsonl

@@ -404,6 +404,9 @@ int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int
 #define MVBEV_BEV_SRC_F32 0          /* views[v]: [B][C][H][W] fp32 contiguous (kornia's input, :69) */
 #define MVBEV_BEV_SRC_F16 1          /* views[v]: [B][C][H][W] fp16 contiguous (fp32 math) */
 #define MVBEV_BEV_SRC_BACKBONE_F32 2 /* views[v]: [B][C][h][w] fp32 backbone maps; :65's upsample fused */
+#define MVBEV_BEV_SRC_CHANNELS_LAST 16 /* flag OR'ed into an fp32 kind (ABI 11700): views[v] hold the same
+                                          tensor channels-last, [B][H][W][C] ([B][h][w][C]) contiguous, C % 32
+                                          == 0 — the fused warps' line-per-pixel kernels */
 typedef struct mvbev_bev_geometry {
   int32_t num_views;                /* N, 1 .. 16 (persp_trans_detector.py:58-59) */
   int32_t src_kind;                 /* MVBEV_BEV_SRC_* */

@@ -76,6 +76,7 @@ EXPORTS = (
     "mvbev_nchw_to_nhwc_f32",
 )
 BEV_SRC_F32, BEV_SRC_F16, BEV_SRC_BACKBONE_F32 = 0, 1, 2  # MVBEV_BEV_SRC_*
+BEV_SRC_CHANNELS_LAST = 16  # MVBEV_BEV_SRC_CHANNELS_LAST (flag)
 WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
 TILES_GRID, TILES_EDGE_STRIP = 0, 1  # MVBEV_TILES_*
 ERR_SHAPE = -2  # MVBEV_ERR_SHAPE

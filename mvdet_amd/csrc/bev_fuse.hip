@@ -59,16 +59,27 @@ mvbev_conv_desc conv2_desc(const mvbev_bev_plan* p) {
   return d;
 }
 
+int kind_of(const mvbev_bev_geometry& g) { return g.src_kind & ~MVBEV_BEV_SRC_CHANNELS_LAST; }
+
+// a view's source strides: NCHW, or channels-last (MVBEV_BEV_SRC_CHANNELS_LAST) of the same [B][C][sh][sw]
+void src_strides(const mvbev_bev_geometry& g, int64_t sh, int64_t sw, int64_t (&st)[4]) {
+  if (g.src_kind & MVBEV_BEV_SRC_CHANNELS_LAST) {
+    st[0] = g.C * sh * sw; st[1] = 1; st[2] = sw * g.C; st[3] = g.C;
+  } else {
+    st[0] = g.C * sh * sw; st[1] = sh * sw; st[2] = sw; st[3] = 1;
+  }
+}
+
 // the views of one frame as mvbev_warp_view entries writing slot s of the split slab (32-B units)
 void slab_views(const mvbev_bev_plan* p, const void* const* views, void* slab, mvbev_warp_view* out) {
   const mvbev_bev_geometry& g = p->g;
-  const bool backbone = g.src_kind == MVBEV_BEV_SRC_BACKBONE_F32;
+  const bool backbone = kind_of(g) == MVBEV_BEV_SRC_BACKBONE_F32;
   const int64_t sh = backbone ? g.h : g.H, sw = backbone ? g.w : g.W;
   const int64_t G = p->Cs / kKC;
   for (int s = 0; s < g.num_views; ++s) {
     mvbev_warp_view& v = out[s];
     v.src = views[s];
-    v.src_strides[0] = g.C * sh * sw; v.src_strides[1] = sh * sw; v.src_strides[2] = sw; v.src_strides[3] = 1;
+    src_strides(g, sh, sw, v.src_strides);
     v.dst = static_cast<char*>(slab) + (size_t)s * g.B * G * g.Ho * g.Wo * 32;
     v.dst_strides[0] = G * g.Ho * g.Wo; v.dst_strides[1] = g.Ho * g.Wo; v.dst_strides[2] = g.Wo;
     v.dst_strides[3] = 1;
@@ -79,13 +90,13 @@ void slab_views(const mvbev_bev_plan* p, const void* const* views, void* slab, m
 // the same writing slot s's channels of T (the Winograd transform of the whole grid)
 void t_views(const mvbev_bev_plan* p, const void* const* views, void* t, mvbev_warp_view* out) {
   const mvbev_bev_geometry& g = p->g;
-  const bool backbone = g.src_kind == MVBEV_BEV_SRC_BACKBONE_F32;
+  const bool backbone = kind_of(g) == MVBEV_BEV_SRC_BACKBONE_F32;
   const int64_t sh = backbone ? g.h : g.H, sw = backbone ? g.w : g.W;
   const int64_t r3 = 4 * ((g.Ho + 11) / 12), K8 = g.num_views * p->Cs / kKC;
   for (int s = 0; s < g.num_views; ++s) {
     mvbev_warp_view& v = out[s];
     v.src = views[s];
-    v.src_strides[0] = g.C * sh * sw; v.src_strides[1] = sh * sw; v.src_strides[2] = sw; v.src_strides[3] = 1;
+    src_strides(g, sh, sw, v.src_strides);
     v.dst = static_cast<char*>(t) + (size_t)32 * (s * (p->Cs / kKC)) * 5 * r3 * g.Wo;
     v.dst_strides[0] = K8 * 5 * r3 * g.Wo; v.dst_strides[1] = 5 * r3 * g.Wo; v.dst_strides[2] = g.Wo;
     v.dst_strides[3] = 1;
@@ -118,9 +129,12 @@ int mvbev_bev_plan_init(const mvbev_bev_geometry* g, mvbev_bev_plan* p) {
   if (g->num_views <= 0 || g->B <= 0 || g->C <= 0 || g->H <= 0 || g->W <= 0 || g->Ho <= 0 || g->Wo <= 0)
     return MVBEV_ERR_RANK;
   if (g->num_views > MVBEV_BEV_MAX_VIEWS) return MVBEV_ERR_SHAPE;
-  if (g->src_kind != MVBEV_BEV_SRC_F32 && g->src_kind != MVBEV_BEV_SRC_F16 && g->src_kind != MVBEV_BEV_SRC_BACKBONE_F32)
+  const int kind = kind_of(*g);
+  if (kind != MVBEV_BEV_SRC_F32 && kind != MVBEV_BEV_SRC_F16 && kind != MVBEV_BEV_SRC_BACKBONE_F32)
     return MVBEV_ERR_SHAPE;
-  if (g->src_kind == MVBEV_BEV_SRC_BACKBONE_F32 && (g->h <= 0 || g->w <= 0 || g->h > g->H || g->w > g->W))
+  if ((g->src_kind & MVBEV_BEV_SRC_CHANNELS_LAST) && (kind == MVBEV_BEV_SRC_F16 || g->C % 32 != 0))
+    return MVBEV_ERR_SHAPE;  // channels-last: fp32 sources in whole 32-channel groups
+  if (kind == MVBEV_BEV_SRC_BACKBONE_F32 && (g->h <= 0 || g->w <= 0 || g->h > g->H || g->w > g->W))
     return MVBEV_ERR_SHAPE;
   std::memset(p, 0, sizeof(*p));
   p->g = *g;
@@ -130,8 +144,7 @@ int mvbev_bev_plan_init(const mvbev_bev_geometry* g, mvbev_bev_plan* p) {
   // the row-Winograd conv1 reads T, which the warp writes directly from fp32 sources (the fused
   // warp + transform kernels); fp16 sources take the direct conv1 on the split slab, as the
   // engine's fp16-storage path does; prepare also falls back for non-finite geometry
-  p->wino = (g->src_kind != MVBEV_BEV_SRC_F16 && g->W >= 2 &&
-             (g->src_kind != MVBEV_BEV_SRC_BACKBONE_F32 || g->w >= 4)) ? 1 : 0;
+  p->wino = (kind != MVBEV_BEV_SRC_F16 && g->W >= 2 && (kind != MVBEV_BEV_SRC_BACKBONE_F32 || g->w >= 4)) ? 1 : 0;
   const int64_t tiles_y = (g->Ho + 11) / 12, tiles_x = (g->Wo + kTileW - 1) / kTileW;
   p->tiles = tiles_y * tiles_x;
   mvbev_conv_desc d1 = conv1_desc(p), d2 = conv2_desc(p);
@@ -284,7 +297,7 @@ int mvbev_bev_fuse(const mvbev_bev_plan* p, const void* const* views, float* map
   void* big = at<void>(ws, p, R_BIG);
   const uint32_t* mask = p->frustum ? at<uint32_t>(ws, p, R_MASK) : nullptr;
   const int32_t* order = p->frustum ? at<int32_t>(ws, p, R_ORDER) : nullptr;
-  const bool backbone = g.src_kind == MVBEV_BEV_SRC_BACKBONE_F32;
+  const bool backbone = kind_of(g) == MVBEV_BEV_SRC_BACKBONE_F32;
   void* y1 = at<void>(ws, p, R_Y1);
   int32_t* gflag = p->guard ? at<int32_t>(ws, p, R_GFLAG) : nullptr;
   if (gflag && hipMemsetAsync(gflag, 0, 4, static_cast<hipStream_t>(stream)) != hipSuccess) return MVBEV_ERR_HIP;
@@ -304,7 +317,7 @@ int mvbev_bev_fuse(const mvbev_bev_plan* p, const void* const* views, float* map
       BEV_TRY(mvbev_warp_views_upsampled_ex(wv, g.num_views, 0, g.B, g.C, g.h, g.w, g.H, g.W, g.Ho, g.Wo,
                                             MVBEV_LAYOUT_SPLIT_BF16, MVBEV_WARP_DST_ZEROED, stream));
     else
-      BEV_TRY(mvbev_warp_views_split_bf16_ex(wv, g.num_views, g.src_kind == MVBEV_BEV_SRC_F16 ? 1 : 0, g.B, g.C, g.H,
+      BEV_TRY(mvbev_warp_views_split_bf16_ex(wv, g.num_views, kind_of(g) == MVBEV_BEV_SRC_F16 ? 1 : 0, g.B, g.C, g.H,
                                              g.W, g.Ho, g.Wo, MVBEV_WARP_DST_ZEROED, stream));
   }
   // a7: conv1 + coord term + bias + ReLU -> y1 (split-bf16, conv2's input)
@@ -335,7 +348,7 @@ int mvbev_bev_fuse(const mvbev_bev_plan* p, const void* const* views, float* map
       mvbev_warp_view& v = wv[s];
       v.src = views[s];
       const int64_t sh = backbone ? g.h : g.H, sw = backbone ? g.w : g.W;
-      v.src_strides[0] = g.C * sh * sw; v.src_strides[1] = sh * sw; v.src_strides[2] = sw; v.src_strides[3] = 1;
+      src_strides(g, sh, sw, v.src_strides);
       v.dst = gslab + (size_t)s * g.B * p->Cs * plane;
       v.dst_strides[0] = p->Cs * plane; v.dst_strides[1] = plane; v.dst_strides[2] = g.Wo; v.dst_strides[3] = 1;
       std::memcpy(v.m, g.m[s], sizeof(v.m));

@@ -1258,7 +1258,8 @@ class BevFuse:
     """The one-call C ABI of the inference hot path (``mvbev_bev_plan_init`` /
     ``mvbev_bev_fuse_prepare`` / ``mvbev_bev_fuse``, include/mvbev.h): what a non-Python caller
     binds instead of orchestrating the entry points.  ``m_norms``: per view the
-    host kornia src_norm <- dst_norm matrix; ``src_kind``: ``_native.BEV_SRC_*``."""
+    host kornia src_norm <- dst_norm matrix; ``src_kind``: ``_native.BEV_SRC_*`` (fp32 kinds may carry
+    ``_native.BEV_SRC_CHANNELS_LAST``: the views are passed channels_last)."""
 
     def __init__(self, m_norms, C: int, src_hw, grid_hw, B: int = 1, src_kind: int = 0, backbone_hw=None):
         g = _native.BevGeometry()
@@ -1326,14 +1327,17 @@ class BevFuse:
             raise RuntimeError("BevFuse.prepare(map_classifier, device) must run before the first frame")
         if len(views) != g.num_views:
             raise ValueError(f"need {g.num_views} views")
-        backbone = g.src_kind == _native.BEV_SRC_BACKBONE_F32
+        kind = g.src_kind & ~_native.BEV_SRC_CHANNELS_LAST
+        cl = bool(g.src_kind & _native.BEV_SRC_CHANNELS_LAST)
+        backbone = kind == _native.BEV_SRC_BACKBONE_F32
         shape = (g.B, g.C, g.h, g.w) if backbone else (g.B, g.C, g.H, g.W)
-        dtype = torch.float16 if g.src_kind == _native.BEV_SRC_F16 else torch.float32
+        dtype = torch.float16 if kind == _native.BEV_SRC_F16 else torch.float32
         for i, v in enumerate(views):
             if not isinstance(v, torch.Tensor) or tuple(v.shape) != shape or v.dtype != dtype:
                 got = (tuple(v.shape), v.dtype) if isinstance(v, torch.Tensor) else type(v)
                 raise ValueError(f"view {i} must be {dtype} {list(shape)}, got {got}")
-        views = [v.contiguous() for v in views]
+        # the plan's layout: NCHW, or (BEV_SRC_CHANNELS_LAST) the same tensors channels_last
+        views = [v.contiguous(memory_format=torch.channels_last if cl else torch.contiguous_format) for v in views]
         _require_cuda(*views)
         if any(v.device != self._device for v in views):
             raise ValueError(f"every view must be on {self._device} (the workspace's device)")

@@ -79,6 +79,44 @@ def test_bev_fuse_backbone_sources_vs_oracle():
     assert_parity_t(got, ref, "bev_fuse backbone sources", normwise_tol=5e-5)
 
 
+@pytest.mark.parametrize("backbone", [False, True])
+def test_bev_fuse_channels_last_sources(backbone):
+    """MVBEV_BEV_SRC_CHANNELS_LAST (ABI 11700): the same frames passed channels-last take the fused
+    warps' line-per-pixel kernels; the map equals the NCHW plan's to fp32 rounding and the oracle's
+    within the gate (config 1's rig, C = 64, B = 2; plain and backbone-resolution sources).  fp16 and
+    C % 32 != 0 are refused."""
+    from mvdet_amd import _native, ops, synthetic
+    ds = synthetic.CONFIGS[1]["make"]()
+    C, N, B = 64, ds.num_cam, 2
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    lo = [u // 3 for u in up]
+    pm, mc, tp = _setup(ds, C, seed=13, B=B)
+    kind = _native.BEV_SRC_BACKBONE_F32 if backbone else _native.BEV_SRC_F32
+    kw = dict(B=B, backbone_hw=lo) if backbone else dict(B=B)
+    nchw = ops.BevFuse(_engine_mats(pm, up, grid), C, up, grid, src_kind=kind, **kw)
+    cl = ops.BevFuse(_engine_mats(pm, up, grid), C, up, grid, src_kind=kind | _native.BEV_SRC_CHANNELS_LAST, **kw)
+    nchw.prepare(mc, DEV)
+    cl.prepare(mc, DEV)
+    if backbone:
+        feats = [synthetic.backbone_features(B, C, lo, seed=130 + v, device=DEV) for v in range(N)]
+    else:
+        feats = [synthetic.synthetic_features(B, C, lo, up, seed=130 + v, device=DEV) for v in range(N)]
+    with torch.no_grad():
+        a = nchw(feats).clone()
+        b = cl([f.contiguous(memory_format=torch.channels_last) for f in feats]).clone()
+        c = cl(feats).clone()  # NCHW tensors handed to a channels-last plan are converted by the wrapper
+        torch.cuda.synchronize()
+        src = [cpu_path.upsample(f.cpu(), up) for f in feats] if backbone else [f.cpu() for f in feats]
+        ref = cpu_path.project_fuse(src, [M.numpy() for M in pm], grid, tp)
+    assert torch.equal(b, c)
+    assert_parity_t(b, a, "bev_fuse channels-last vs NCHW", normwise_tol=2e-6)
+    assert_parity_t(b, ref, "bev_fuse channels-last vs oracle", normwise_tol=5e-5)
+    for bad_kind, bad_c in ((_native.BEV_SRC_F16 | _native.BEV_SRC_CHANNELS_LAST, 64),
+                            (kind | _native.BEV_SRC_CHANNELS_LAST, 40)):
+        with pytest.raises(_native.NativeError):
+            ops.BevFuse(_engine_mats(pm, up, grid), bad_c, up, grid, src_kind=bad_kind, **kw)
+
+
 def test_bev_fuse_fp16_sources_direct_conv1():
     """fp16 sources (config 4's storage): the split slab from fp16 and the direct ring conv1."""
     from mvdet_amd import _native, ops, synthetic

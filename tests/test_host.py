@@ -176,6 +176,13 @@ def test_bev_fuse_structs_and_plan_match_the_header(tmp_path):
     assert lib.mvbev_bev_fuse_workspace_bytes(ctypes.byref(g)) == plan.workspace_bytes
     g.src_kind = _native.BEV_SRC_F16  # fp16 sources: the direct conv1 on the split slab
     assert lib.mvbev_bev_plan_init(ctypes.byref(g), ctypes.byref(plan)) == 0 and plan.wino == 0
+    # channels-last sources (ABI 11700): fp32 kinds with whole 32-channel groups only
+    for kind, C, ok in ((_native.BEV_SRC_F32, 512, True), (_native.BEV_SRC_F16, 512, False),
+                        (_native.BEV_SRC_F32, 40, False)):
+        g.src_kind, g.C = kind | _native.BEV_SRC_CHANNELS_LAST, C
+        st = lib.mvbev_bev_plan_init(ctypes.byref(g), ctypes.byref(plan))
+        assert (st == 0 and plan.wino == 1) if ok else st == _native.ERR_SHAPE, (kind, C, st)
+    g.src_kind, g.C = _native.BEV_SRC_F32, 512
     g.num_views = 17
     assert lib.mvbev_bev_plan_init(ctypes.byref(g), ctypes.byref(plan)) == _native.ERR_SHAPE
 

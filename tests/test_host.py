@@ -249,3 +249,17 @@ def test_hot_kernels_use_no_scratch():
                     bad.append((f.name, name, int(m.group(1))))
     assert seen >= 20, seen
     assert not bad, bad
+
+
+def test_design_cost_model_table_is_current():
+    """DESIGN.md §6's per-mode table is what mvdet_amd.mp_model predicts from its committed inputs
+    (tools/mp_cost_model.py), so the documented N>1 mode choice is the one bench.py --mp-mode auto makes."""
+    import subprocess
+    import sys
+    out = subprocess.run([sys.executable, str(ROOT / "tools" / "mp_cost_model.py")], cwd=ROOT, capture_output=True,
+                         text=True, timeout=300, check=True).stdout
+    rows = [ln.replace(" ms (x)", "") for ln in out.splitlines() if ln.startswith("| ")]
+    design = (ROOT / "DESIGN.md").read_text()
+    assert len(rows) == 13  # header + 3 configs x 4 rank counts
+    for row in rows:
+        assert row in design, row

@@ -1628,8 +1628,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   do {                                                                                               \
     constexpr int XI = (R) % 5, P = (R) & 1;                                                          \
     if (u0 + (R) >= U) break;                                                                        \
-    const int slot = MVBEV_WINO_UNROLL20 ? ((R) & 3) : ((u0 + (R)) & 3);                             \
-    const int nslot = MVBEV_WINO_UNROLL20 ? (((R) + 1) & 3) : ((u0 + (R) + 1) & 3);                   \
+    constexpr int slot = (R) & 3, nslot = ((R) + 1) & 3; /* u0 % 20 == 0 */                        \
     fetch_a(P ^ 1, slot, 1);                                                                         \
     fetch_b(2, slot);                                                                                \
     WINO_MFMAS(P, 0, XI);                                                                            \
@@ -1661,29 +1660,14 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     WINO_MFMAS(P, 2, XI);                                                                            \
     sched6(std::integral_constant<int, 8>{});                                                        \
   } while (0)
-#ifndef MVBEV_WINO_UNROLL20
-#define MVBEV_WINO_UNROLL20 0
-#endif
-    if (MVBEV_WINO_UNROLL20) {  // (A/B) 20 units per trip: the ring slot (u & 3) is a compile-time constant
-      for (int u0 = 0; u0 < U; u0 += 20) {
-        WINO_UNIT(0); WINO_UNIT(1); WINO_UNIT(2); WINO_UNIT(3); WINO_UNIT(4);
-        WINO_UNIT(5); WINO_UNIT(6); WINO_UNIT(7); WINO_UNIT(8); WINO_UNIT(9);
-        WINO_UNIT(10); WINO_UNIT(11); WINO_UNIT(12); WINO_UNIT(13); WINO_UNIT(14);
-        WINO_UNIT(15); WINO_UNIT(16); WINO_UNIT(17); WINO_UNIT(18); WINO_UNIT(19);
-      }
-    } else {
-      for (int u0 = 0; u0 < U; u0 += 10) {
-        WINO_UNIT(0);
-        WINO_UNIT(1);
-        WINO_UNIT(2);
-        WINO_UNIT(3);
-        WINO_UNIT(4);
-        WINO_UNIT(5);
-        WINO_UNIT(6);
-        WINO_UNIT(7);
-        WINO_UNIT(8);
-        WINO_UNIT(9);
-      }
+    // 20 units per trip (the lcm of the 5 xi of a chunk and the 4 ring slots): the slot of every unit
+    // is a compile-time constant, so no per-unit LDS address arithmetic (1-2 % on conv1 at cfg2 vs 10
+    // units per trip, profiles/r04n_u20.jsonl)
+    for (int u0 = 0; u0 < U; u0 += 20) {
+      WINO_UNIT(0); WINO_UNIT(1); WINO_UNIT(2); WINO_UNIT(3); WINO_UNIT(4);
+      WINO_UNIT(5); WINO_UNIT(6); WINO_UNIT(7); WINO_UNIT(8); WINO_UNIT(9);
+      WINO_UNIT(10); WINO_UNIT(11); WINO_UNIT(12); WINO_UNIT(13); WINO_UNIT(14);
+      WINO_UNIT(15); WINO_UNIT(16); WINO_UNIT(17); WINO_UNIT(18); WINO_UNIT(19);
     }
 #undef WINO_UNIT
 #undef WINO_MFMAS

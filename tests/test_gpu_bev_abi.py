@@ -109,7 +109,7 @@ def test_bev_fuse_channels_last_sources(backbone):
         src = [cpu_path.upsample(f.cpu(), up) for f in feats] if backbone else [f.cpu() for f in feats]
         ref = cpu_path.project_fuse(src, [M.numpy() for M in pm], grid, tp)
     assert torch.equal(b, c)
-    assert_parity_t(b, a, "bev_fuse channels-last vs NCHW", normwise_tol=2e-6)
+    assert_parity_t(b, a, "bev_fuse channels-last vs NCHW", normwise_tol=1e-5)  # fp32 rounding of T, through the split convs
     assert_parity_t(b, ref, "bev_fuse channels-last vs oracle", normwise_tol=5e-5)
     for bad_kind, bad_c in ((_native.BEV_SRC_F16 | _native.BEV_SRC_CHANNELS_LAST, 64),
                             (kind | _native.BEV_SRC_CHANNELS_LAST, 40)):

@@ -69,7 +69,7 @@ if cls:
     res["warp_cl_hbm_bytes_per_launch"] = res["kernels"][k]["hbm_bytes_per_launch"]
     res["warp_cl_read_bytes_per_launch"] = res["kernels"][k]["read_bytes"]
 # the detector's inference warp (fused 3x upsample + warp + B^T from backbone-resolution maps)
-ups = [k for k in res["kernels"] if "warp_up_wino2_kernel" in k]
+ups = [k for k in res["kernels"] if "warp_up_wino2_kernel" in k or "warp_up_wino_cl_kernel" in k]
 if ups:
     k = max(ups, key=lambda n: int(n.rsplit("grid ", 1)[1].rstrip("]")))
     res["warp_up_hbm_bytes_per_launch"] = res["kernels"][k]["hbm_bytes_per_launch"]

@@ -43,7 +43,11 @@ def test_bench_json_line_contract():
             assert 0 < st["achieved_GBs"] <= st["peak_GBs"], (name, st)
         if st.get("executed_bf16_frac") is not None:
             assert 0 < st["executed_bf16_frac"] <= 1.0, (name, st)
-    assert r["config"]["workload"].startswith("cfg1")
+    assert r["config"]["workload"].startswith("cfg1") and r["config"]["feature_layout"] == "nchw"
+    # the same step on channels-last features, and the +a4 legs (NCHW, torch upsample, channels-last maps)
+    assert r["channels_last"]["value"] > 0 and 0 < r["channels_last"]["warp"]["achieved_GBs"] <= 8000
+    for leg in ("fused", "unfused", "fused_channels_last"):
+        assert r["plus_a4"][leg]["value"] > 0 and r["plus_a4"][leg]["upsample_and_warp_ms"] > 0, leg
     # the north-star sub-object (here cfg2 for speed; the default is cfg3): its own value, roofline, CPU baseline
     sub = r["cfg2"]
     assert sub["value"] > 0 and sub["config"]["workload"].startswith("cfg2") and 0 < sub["roofline"]["frac"] <= 1.0

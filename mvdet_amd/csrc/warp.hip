@@ -441,128 +441,6 @@ void warp_wino_cl_kernel(const WarpArgs a, int r3_rows) {
   }
 }
 
-// Column form of warp_wino_cl_kernel (round 4 A/B, MVBEV_WCL2): thread = (column, channel quad) of a
-// 14 x 16-pixel, 32-channel block (128 threads, as warp_up_wino_cl_kernel) walks its column's 14 rows:
-// per row the 4 corner lines' 16-B pieces (bounds-checked buffer loads), the bilinear sum in a register,
-// then B^T of each 3-row tile from the thread's own registers — no LDS round trip of the samples, one
-// barrier (the coordinates) instead of three.
-constexpr int kWc2Threads = kWcCols * 8;
-__global__ __launch_bounds__(kWc2Threads)
-void warp_wino_cl2_kernel(const WarpArgs a, int r3_rows) {
-  __shared__ float2 crd[kWcPix];
-  __shared__ unsigned char cls[kWcPix];  // 0: exact zero, 1: inside, 2: non-finite
-  const int lb = xcd_remap(blockIdx.x, a.nwg);
-  const int tile = lb % a.tiles;
-  const int grp = (lb / a.tiles) % a.chunks;
-  const int bv = lb / (a.tiles * a.chunks);
-  const int view = bv % a.nviews, b = bv / a.nviews;
-  const WarpView& vw = a.v[view];
-  const int k = tile / a.tiles_x, tx = tile - k * a.tiles_x;
-  const int tid = threadIdx.x;
-  const int H = a.H, W = a.W;
-  float m[9];
-#pragma unroll
-  for (int q = 0; q < 9; ++q) m[q] = vw.m[q];
-  for (int p = tid; p < kWcPix; p += kWc2Threads) {
-    const int i = p / kWcCols, c = p % kWcCols;
-    const int v = 12 * k - 1 + i, u = tx * kWcCols + c;
-    unsigned char cl = 0;
-    float ix = 0.f, iy = 0.f;
-    if (v >= 0 && v < a.Ho && u < a.Wo) {
-      const WarpCoord wc = warp_coord(m, u, v, a.Ho, a.Wo, H, W);
-      cl = wc.inside ? 1 : (wc.finite ? 0 : 2);
-      ix = wc.ix;
-      iy = wc.iy;
-    }
-    crd[p] = make_float2(ix, iy);
-    cls[p] = cl;
-  }
-  __syncthreads();
-  const char* gbase = static_cast<const char*>(vw.src) + ((int64_t)b * vw.sB + (int64_t)grp * kWcCh) * 4;
-  const int extent = (int)(((int64_t)(H - 1) * vw.sH + (int64_t)(W - 1) * vw.sW + kWcCh) * 4);
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(gbase), (short)0, extent, 0x00020000);
-  const int c = tid >> 3, qd = tid & 7;
-  const int u = tx * kWcCols + c;
-  const int sH4 = (int)vw.sH * 4, sW4 = (int)vw.sW * 4, q4 = 16 * qd;
-  // one row of the column: the bilinear sum of this thread's 4 channels
-  auto sample_row = [&](int i, f32x4a_t& dv, bool& nz) __attribute__((always_inline)) {
-    const int p = i * kWcCols + c;
-    const int cl = cls[p];
-    const float2 q = crd[p];
-    const float fx0 = floorf(q.x), fy0 = floorf(q.y);
-    const int x0 = cl == 1 ? (int)fx0 : -2, y0 = cl == 1 ? (int)fy0 : -2;
-    const float fx1 = fx0 + 1.f, fy1 = fy0 + 1.f;
-    const float w_nw = (fx1 - q.x) * (fy1 - q.y), w_ne = (q.x - fx0) * (fy1 - q.y);
-    const float w_sw = (fx1 - q.x) * (q.y - fy0), w_se = (q.x - fx0) * (q.y - fy0);
-    const bool vx0 = x0 >= 0, vx1 = x0 + 1 >= 0 && x0 + 1 <= W - 1;
-    const bool vy0 = y0 >= 0, vy1 = y0 + 1 >= 0 && y0 + 1 <= H - 1;
-    const int r0 = y0 * sH4, r1 = r0 + sH4, c0 = x0 * sW4, c1 = c0 + sW4;
-    const f32x4a_t vnw = __builtin_bit_cast(f32x4a_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                                          rs, vx0 && vy0 ? r0 + c0 + q4 : kWcOutside, 0, 0));
-    const f32x4a_t vne = __builtin_bit_cast(f32x4a_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                                          rs, vx1 && vy0 ? r0 + c1 + q4 : kWcOutside, 0, 0));
-    const f32x4a_t vsw = __builtin_bit_cast(f32x4a_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                                          rs, vx0 && vy1 ? r1 + c0 + q4 : kWcOutside, 0, 0));
-    const f32x4a_t vse = __builtin_bit_cast(f32x4a_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                                          rs, vx1 && vy1 ? r1 + c1 + q4 : kWcOutside, 0, 0));
-    f32x4a_t acc = {0.f, 0.f, 0.f, 0.f};
-    acc += vnw * w_nw;
-    acc += vne * w_ne;
-    acc += vsw * w_sw;
-    acc += vse * w_se;
-    if (cl != 1) acc = cl == 2 ? f32x4a_t{__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""),
-                                          __builtin_nanf("")}
-                               : f32x4a_t{0.f, 0.f, 0.f, 0.f};
-    dv = acc;
-    nz = cl != 0;
-  };
-  const bool col_ok = u < a.Wo;
-  const int chunk = grp * (kWcCh / 8) + (qd >> 1), half = qd & 1;
-  // a sliding window of the 5 rows of the current 3-row tile (rows 3 qt + 3, + 4 are the next tile's
-  // rows 0, 1)
-  f32x4a_t d[5];
-  bool nzr[5];
-  sample_row(0, d[0], nzr[0]);
-  sample_row(1, d[1], nzr[1]);
-#pragma unroll
-  for (int qt = 0; qt < 4; ++qt) {
-    if (qt > 0) {
-      d[0] = d[3]; d[1] = d[4];
-      nzr[0] = nzr[3]; nzr[1] = nzr[4];
-    }
-    sample_row(3 * qt + 2, d[2], nzr[2]);
-    sample_row(3 * qt + 3, d[3], nzr[3]);
-    sample_row(3 * qt + 4, d[4], nzr[4]);
-    const int r3 = 4 * k + qt;
-    if (!col_ok || r3 >= r3_rows) continue;
-    if (a.skip_zero && !(nzr[0] | nzr[1] | nzr[2] | nzr[3] | nzr[4])) continue;
-    f32x4a_t t[5];
-    t[0] = 2.f * d[0] - d[1] - 2.f * d[2] + d[3];
-    t[1] = -2.f * d[1] - d[2] + d[3];
-    t[2] = 2.f * d[1] - 3.f * d[2] + d[3];
-    t[3] = d[3] - d[1];
-    t[4] = 2.f * d[1] - d[2] - 2.f * d[3] + d[4];
-    if (a.nonfinite) {
-      const f32x4a_t sum = (t[0] + t[1]) + (t[2] + t[3]) + t[4];
-      if (!isfinite((sum.x + sum.y) + (sum.z + sum.w))) *a.nonfinite = a.nf_tag;
-    }
-    unsigned* out = reinterpret_cast<unsigned*>(static_cast<u32x4_t*>(vw.dst) +
-                                                (2 * ((int64_t)b * vw.dB + (int64_t)chunk * vw.dC +
-                                                      (int64_t)(5 * r3) * vw.dH) + u)) + 2 * half;
-    typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
-#pragma unroll
-    for (int xi = 0; xi < 5; ++xi) {
-      const float h0 = (float)(__bf16)t[xi].x, h1 = (float)(__bf16)t[xi].y;
-      const float h2 = (float)(__bf16)t[xi].z, h3 = (float)(__bf16)t[xi].w;
-      unsigned* o = out + (int64_t)xi * vw.dH * 8;
-      *reinterpret_cast<u32x2_t*>(o) = u32x2_t{pack_bf16x2(h0, h1), pack_bf16x2(h2, h3)};
-      *reinterpret_cast<u32x2_t*>(o + vw.dH * 4) =
-          u32x2_t{pack_bf16x2(t[xi].x - h0, t[xi].y - h1), pack_bf16x2(t[xi].z - h2, t[xi].w - h3)};
-    }
-  }
-}
-
 template <typename T, bool SPLIT>
 static void launch_warp_t(const WarpArgs& a, hipStream_t s) {
   if constexpr (std::is_same<T, float>::value) {
@@ -807,13 +685,8 @@ int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t
   }
   a.chunks = (int)ceil_div(C, cl ? kWcCh : kWarpCPB);
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
-#ifndef MVBEV_WCL2
-#define MVBEV_WCL2 0  // A/B: the column form of the channels-last fused warp
-#endif
-  const dim3 grid((unsigned)a.nwg), block(cl ? (MVBEV_WCL2 ? kWc2Threads : kWcThreads) : kWwThreads);
-  if (cl && MVBEV_WCL2)
-    hipLaunchKernelGGL(warp_wino_cl2_kernel, grid, block, 0, as_stream(stream), a, (int)r3_rows);
-  else if (cl)
+  const dim3 grid((unsigned)a.nwg), block(cl ? kWcThreads : kWwThreads);
+  if (cl)
     hipLaunchKernelGGL(warp_wino_cl_kernel, grid, block, 0, as_stream(stream), a, (int)r3_rows);
   else if (pair)
     hipLaunchKernelGGL((warp_wino_kernel<true>), grid, block, 0, as_stream(stream), a, (int)r3_rows);

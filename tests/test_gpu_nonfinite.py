@@ -95,10 +95,12 @@ def test_nonfinite_features_through_the_detector(C):
         assert_parity_t(imgs_res[v], ref_imgs[v], f"C={C} non-finite features: imgs_result {v}")
 
 
-def test_nonfinite_features_through_the_engine_from_upsampled_maps():
+@pytest.mark.parametrize("layout", ["nchw", "channels_last"])
+def test_nonfinite_features_through_the_engine_from_upsampled_maps(layout):
     """The bench's path (upsampled features -> fused warp + B^T -> Winograd convs) with non-finite
     features, then the same engine on finite features again (the flag of the previous frame must
-    not trigger the exact path: a fresh tag per frame)."""
+    not trigger the exact path: a fresh tag per frame); NCHW features and channels-last ones (the
+    line-per-pixel warp reports, the exact path reads them at their strides)."""
     from mvdet_amd import ProjectFuse, synthetic
     from mvdet_amd.geometry import projection_matrices
     C = 64
@@ -114,6 +116,9 @@ def test_nonfinite_features_through_the_engine_from_upsampled_maps():
     bad = [f.clone() for f in feats]
     bad[1][0, 2, up[0] // 2, up[1] // 2] = float("inf")
     bad[2][0, 5, up[0] // 2 + 7, up[1] // 2 - 9] = float("nan")
+    if layout == "channels_last":
+        feats = [f.contiguous(memory_format=torch.channels_last) for f in feats]
+        bad = [f.contiguous(memory_format=torch.channels_last) for f in bad]
     with torch.no_grad():
         got = eng.project_fuse(bad, mc).clone()
         ws = eng.workspace(B, DEV)

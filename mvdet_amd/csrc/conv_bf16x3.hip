@@ -1447,9 +1447,6 @@ __global__ __launch_bounds__(256) void wino_rows_kernel(const WinoRowsArgs a) {
 // counts); the T DMAs keep the default cache policy (nt measured +0.5 % on conv1, +1 % on conv2).
 // DIL 2 (conv2): the wave's row tile is the ring kernel's interleaved rows base + 2 pt; P3: the
 // epilogue forms conv3's partial sums (cout1_partials) instead of storing y
-#ifndef MVBEV_WINO_PB2OFF
-#define MVBEV_WINO_PB2OFF 0  // A/B: conv2 with one barrier per unit
-#endif
 template <bool RELU, int DIL, bool P3>
 __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   using namespace wino;
@@ -1599,7 +1596,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   constexpr int NPU_HI = NWI + NXT;
   constexpr int NPU_LO = NWI + NXT_LO;
   const bool whi = wave < WHI;
-  constexpr bool PB = DIL == 2 && !MVBEV_WINO_PB2OFF;  // one barrier per two units for conv2
+  constexpr bool PB = DIL == 2;  // one barrier per two units for conv2
   if (nch > 0) {
     const int U = NXI * nch;
     // prologue: units 0-3 (chunk 0, rows 0-3) in flight, wait for unit 0

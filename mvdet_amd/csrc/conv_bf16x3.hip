@@ -704,22 +704,37 @@ __device__ __attribute__((always_inline)) inline void cout1_partials(const Args&
 
 // map[b][0][q][c] = sum over sets s, taps t of p3[b][s][t][q + d(t/3 - 1)][c + d(t%3 - 1)]
 // (zero outside the image): the single-output conv from the partials above, fixed order.
-__global__ void cout1_reduce_kernel(const float* __restrict__ p3, int nsets, int H, int W, int rows_p,
-                                    int row0_p, int dil, float* __restrict__ map, int map_row0, int map_rows) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x, qr = blockIdx.y, b = blockIdx.z;
-  if (c >= W) return;
+// Block = 64 map columns x 4 waves: wave g sums the sets g, g + 4, ... (each set's 9 shifted taps in
+// tap order), then wave 0 adds the 4 waves' sums in wave order — a fixed order, 4x the waves of one
+// thread per output (the reduce was latency-bound at under one wave per SIMD: 27 -> ~10 us at cfg2).
+constexpr int kC1rGroups = 4;
+__global__ __launch_bounds__(64 * kC1rGroups) void cout1_reduce_kernel(const float* __restrict__ p3, int nsets, int H,
+                                                                      int W, int rows_p, int row0_p, int dil,
+                                                                      float* __restrict__ map, int map_row0,
+                                                                      int map_rows) {
+  __shared__ float part[kC1rGroups][64];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane, qr = blockIdx.y, b = blockIdx.z;
   const int q = map_row0 + qr;
   const float* pb = p3 + (int64_t)b * nsets * 9 * rows_p * W;
   float acc = 0.f;
-#pragma unroll 4
-  for (int s = 0; s < nsets; ++s)
+  if (c < W) {
+    for (int s = g; s < nsets; s += kC1rGroups)
 #pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      const int r = q + dil * (t / 3 - 1), cc = c + dil * (t % 3 - 1);
-      if (r >= 0 && r < H && cc >= 0 && cc < W)
-        acc += pb[(((int64_t)s * 9 + t) * rows_p + (r - row0_p)) * W + cc];
-    }
-  map[((int64_t)b * map_rows + qr) * W + c] = acc;
+      for (int t = 0; t < 9; ++t) {
+        const int r = q + dil * (t / 3 - 1), cc = c + dil * (t % 3 - 1);
+        if (r >= 0 && r < H && cc >= 0 && cc < W)
+          acc += pb[(((int64_t)s * 9 + t) * rows_p + (r - row0_p)) * W + cc];
+      }
+  }
+  part[g][lane] = acc;
+  __syncthreads();
+  if (g == 0 && c < W) {
+    float sum = part[0][lane];
+#pragma unroll
+    for (int k = 1; k < kC1rGroups; ++k) sum += part[k][lane];
+    map[((int64_t)b * map_rows + qr) * W + c] = sum;
+  }
 }
 
 // The ring kernel's output of a finished tile: rows row_base + pt * DIL (pt < 3) of this wave,
@@ -1904,8 +1919,8 @@ int mvbev_cout1_reduce_partials(const void* partials, const mvbev_conv_desc* des
   if (map_row0 < 0 || map_row0 + map_rows > desc->H || r_lo < desc->out_row0 || r_hi > desc->out_row0 + desc->out_rows ||
       map_rows > 65535 || desc->B > 65535 || desc->out_rows * desc->W > INT32_MAX)
     return MVBEV_ERR_SHAPE;
-  const dim3 grid((unsigned)mvbev::ceil_div(desc->W, 128), (unsigned)map_rows, (unsigned)desc->B);
-  hipLaunchKernelGGL(cout1_reduce_kernel, grid, dim3(128), 0, mvbev::as_stream(stream),
+  const dim3 grid((unsigned)mvbev::ceil_div(desc->W, 64), (unsigned)map_rows, (unsigned)desc->B);
+  hipLaunchKernelGGL(cout1_reduce_kernel, grid, dim3(64 * kC1rGroups), 0, mvbev::as_stream(stream),
                      static_cast<const float*>(partials), (int)(2 * (Cout / BN)), (int)desc->H, (int)desc->W,
                      (int)desc->out_rows, (int)desc->out_row0, dilation3, map, (int)map_row0, (int)map_rows);
   MVBEV_CHECK_LAUNCH();

@@ -59,8 +59,11 @@ def _train_workspace(engine: ProjectFuse, B: int, device) -> Workspace:
         # with an event after its last reader: the next forward's stream waits on it, so a forward
         # on another stream than the backward cannot overwrite the slab under the wgrad kernels.
         pool = _slab_pool(engine, B, device)
+        t1 = t2 = None
         if pool:
-            slab, done = pool.pop()
+            # (with the slab, its Winograd transform buffers: conv1's T is zero-filled once and written
+            # only at the frustum mask's (tile, view) pairs, the same every step)
+            slab, done, t1, t2 = pool.pop()
             torch.cuda.current_stream(device).wait_event(done)
         else:
             slab = torch.zeros((engine.S,) + ops.split_shape(B, engine.Cs, H, W), dtype=torch.bfloat16,
@@ -76,8 +79,10 @@ def _train_workspace(engine: ProjectFuse, B: int, device) -> Workspace:
         y1 = torch.empty((B, engine.mid, H, W), dtype=torch.float32, device=device)
     y2 = torch.empty((B, engine.mid, H, W), dtype=torch.float32, device=device)
     m = engine.m_norm_cpu.to(device)[:, None].expand(engine.num_cam, B, 3, 3).contiguous()
-    return Workspace(slab, y1, y2, m, (0, H), y1r, y2r, slab_zeroed=zeroed, store_y2=True,
-                     slab_rows=(0, H))
+    ws = Workspace(slab, y1, y2, m, (0, H), y1r, y2r, slab_zeroed=zeroed, store_y2=True, slab_rows=(0, H))
+    if engine.split:
+        ws.wino_t, ws.wino_t2 = t1, t2
+    return ws
 
 
 def _slab_pool(engine: ProjectFuse, B: int, device) -> list:
@@ -269,7 +274,7 @@ class ProjectFuseFunction(torch.autograd.Function):
         if ws.slab_zeroed:  # its readers are enqueued: reusable once this stream passes this point
             done = torch.cuda.Event()
             done.record(torch.cuda.current_stream(dev))
-            _slab_pool(engine, B, dev).append((ws.slab, done))
+            _slab_pool(engine, B, dev).append((ws.slab, done, ws.wino_t, ws.wino_t2))
         ctx.ws = None
         return (None, None, *grads, dw1, db1, dw2, db2, dw3)
 

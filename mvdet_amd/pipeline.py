@@ -474,7 +474,7 @@ class ProjectFuse:
         R = s1 - s0
         d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * R * W,
                            batch_stride=self.Cs * R * W, in_row0=s0, in_rows=R, out_row0=a1, out_rows=b1 - a1)
-        if not ws.store_y2 and self.wino_active(ws.slab.device):
+        if self.wino_active(ws.slab.device):  # inference, and the training forward (round 4)
             return self.conv1_wino(ws, conv1, d1, init, mark=mark)
         if ws.t_from_warp:
             raise RuntimeError("the direct conv1 reads the slab, but the fused warp wrote conv1's row transform")
@@ -510,15 +510,22 @@ class ProjectFuse:
                                 tile_order=self.conv1_order(ws.slab.device, a1, b1 - a1, B, grid=True))
 
     def conv2(self, ws: Workspace, conv2: torch.nn.Conv2d) -> torch.Tensor:
-        """a8: y2 = relu(conv3x3_d2(y1) + b2) on y2's rows."""
+        """a8: y2 = relu(conv3x3_d2(y1) + b2) on y2's rows (row-Winograd where ``wino_conv2_active``:
+        the training forward, which keeps y2 for conv3's backward)."""
         H, W = self.grid_hw
-        B = ws.slab.shape[1]
-        p2 = self.pack2.get(conv2.weight)
         (a1, b1), (a2, b2) = ws.y1_rows, ws.y2_rows
         B = ws.y1.shape[0]
         d2 = ops.conv_desc(B, self.mid, H, W, group=self.mid, group_stride=0,
                            batch_stride=self.mid * (b1 - a1) * W, in_row0=a1, in_rows=b1 - a1,
                            out_row0=a2, out_rows=b2 - a2)
+        if self.wino_conv2_active(ws):
+            tneed = ops.wino_rows_bytes(d2)
+            if ws.wino_t2 is None or ws.wino_t2.numel() * 2 < tneed:
+                ws.wino_t2 = torch.zeros((tneed + 1) // 2, dtype=torch.bfloat16, device=ws.y1.device)
+            ops.wino_rows(ws.y1, d2, ws.wino_t2, dilation=2)
+            return ops.conv3x3_wino_dil(ws.wino_t2, d2, self.pack2w.get(conv2.weight), self.mid, 2, bias=conv2.bias,
+                                        relu=True, out=ws.y2)
+        p2 = self.pack2.get(conv2.weight)
         return ops.conv3x3_desc(ws.y1, d2, p2, self.mid, bias=conv2.bias, dilation=2, relu=True, out=ws.y2,
                                 workspace=self._sk_ws(d2, ws.y1.device))
 

@@ -655,7 +655,10 @@ def test_training_steps_reuse_the_zeroed_slab():
         fg = [f.clone().requires_grad_() for f in feats]
         mc.zero_grad()
         out = autograd.project_fuse(eng, fg, mc)
-        slabs.append(out.grad_fn.ws.slab.data_ptr())
+        ws = out.grad_fn.ws
+        # (the Winograd conv1's transform buffer travels with the slab: zero-filled once)
+        slabs.append((ws.slab.data_ptr(), None if ws.wino_t is None else ws.wino_t.data_ptr()))
+        assert (ws.wino_t is not None) == eng.wino_active(DEV)
         assert out.grad_fn.ws.slab_zeroed
         out.backward(torch.ones_like(out))
         results.append([out.detach().clone()] + [f.grad.clone() for f in fg] +

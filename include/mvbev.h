@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -353,6 +353,16 @@ int mvbev_conv3x3_wino_bf16x3_dil(const void* t, const mvbev_conv_desc* desc, co
 int mvbev_conv3x3_wino_bf16x3_cout1_partials(const void* t, const mvbev_conv_desc* desc, const void* w_packed,
                                              const float* bias, int64_t Cout, int dilation, int relu, const float* w3,
                                              void* partials, size_t partials_bytes, void* stream);
+/* A data gradient as the dilation-1 row-Winograd conv (ABI 11800; the training backward's conv1
+ * dgrad, persp_trans_detector.py:51 differentiated): t = the row transform of the split-bf16 dy
+ * (mvbev_wino_rows_split_bf16), w_packed = mvbev_pack_conv3x3_weight_wino of the weight with its
+ * in / out channels swapped and its taps reversed ([Cout = forward Cin][forward Cout][3][3]), no
+ * bias / init / ReLU; dx fp32 or split-bf16 [B][Cout][out_rows][W].  out_mask (optional, int32 per
+ * 12 x 32 output tile as mvbev_warp_tile_mask): tiles of output channel group g (cot_per_group
+ * 128-channel tiles) whose bit g is clear are not written (a consumer that never reads them). */
+int mvbev_conv3x3_wino_bf16x3_dgrad(const void* t, const mvbev_conv_desc* desc, const void* w_packed, int64_t Cout,
+                                    void* dx, int dx_layout, const uint32_t* out_mask, int64_t cot_per_group,
+                                    void* stream);
 
 /* conv2 -> conv3 without conv2's activation in HBM (map_classifier[2:5],
  * persp_trans_detector.py:53-54, inference): the split-bf16-input conv of

@@ -148,6 +148,59 @@ def _dgrad1_schedule(st, B, cout_p, H, W, K, out_mask, cot_per_group, device):
     return st.sched1[key]
 
 
+def _dgrad2_wino(engine: ProjectFuse, st, dy2s: torch.Tensor, w2: torch.Tensor) -> torch.Tensor:
+    """conv2's data gradient as the forward's dilation-2 row-Winograd conv (``conv3x3_wino_dil``):
+    with padding = dilation, dgrad(dy) = conv(dy, w^T flipped) — the weight's in / out channels
+    swapped and its taps reversed (a 512 x 512 copy per step into a persistent tensor, so the
+    packer's (pointer, version) key sees each new weight).  dy2s: split-bf16 [B, 512, H, W]."""
+    H, W = engine.grid_hw
+    mid = engine.mid
+    B = dy2s.shape[0]
+    d = ops.conv_desc(B, mid, H, W, group=mid, group_stride=0, batch_stride=mid * H * W)
+    if getattr(st, "w2t", None) is None or st.w2t.device != w2.device:
+        st.w2t = torch.empty_like(w2, memory_format=torch.contiguous_format)
+        st.pack2t = ops.PackedConv3x3(None, "bf16x3", wino=True)
+        st.t2d = None
+    st.w2t.copy_(w2.detach().flip(2, 3).transpose(0, 1))
+    need = ops.wino_rows_bytes(d)
+    if st.t2d is None or st.t2d.numel() * 2 < need:  # zero-filled once (as the forward's T)
+        st.t2d = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=dy2s.device)
+    ops.wino_rows(dy2s, d, st.t2d, dilation=2)
+    return ops.conv3x3_wino_dil(st.t2d, d, st.pack2t.get(st.w2t), mid, 2)
+
+
+def _dgrad1_wino_applies(engine: ProjectFuse, cp: int, device) -> bool:
+    """conv1's data gradient runs row-Winograd (``_dgrad1_wino``): the forward's conv1 did (split
+    slab, finite geometry), whole 128-channel Cout tiles per view, slot s = view s."""
+    n, C = engine.num_cam, engine.C
+    return (engine.wino_active(device) and C % ops.BN == 0 and engine.Cs == C and cp == n * C
+            and engine.slot_views == list(range(n)))
+
+
+def _dgrad1_wino(engine: ProjectFuse, st, dy1s: torch.Tensor, w1: torch.Tensor, dslab: torch.Tensor) -> None:
+    """conv1's data gradient (the N*C view channels) as the dilation-1 row-Winograd conv
+    (``ops.conv3x3_wino_dgrad``) of the split dy1 with w1's view columns swapped and flipped, into
+    the split ``dslab``; a view's 12 x 32 tiles its warp never samples are skipped (the forward's
+    frustum mask, a superset of the sampled pixels: the adjoint reads nothing else).  The ring
+    form (``conv3x3_dgrad``) executes the direct conv's 9 K-blocks per kernel column, this one 5."""
+    H, W = engine.grid_hw
+    mid, C = engine.mid, engine.C
+    nc = engine.num_cam * C
+    B = dy1s.shape[0]
+    d = ops.conv_desc(B, mid, H, W, group=mid, group_stride=0, batch_stride=mid * H * W)
+    if getattr(st, "w1t", None) is None or st.w1t.device != w1.device or st.w1t.shape[0] != nc:
+        st.w1t = torch.empty((nc, mid, 3, 3), dtype=torch.float32, device=w1.device)
+        st.pack1t = ops.PackedConv3x3(None, "bf16x3", wino=True)
+        st.t1d = None
+    st.w1t.copy_(w1.detach()[:, :nc].flip(2, 3).transpose(0, 1))
+    need = ops.wino_rows_bytes(d)
+    if st.t1d is None or st.t1d.numel() * 2 < need:
+        st.t1d = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=dy1s.device)
+    ops.wino_rows(dy1s, d, st.t1d)
+    cm = engine.conv1_mask(dy1s.device, 0, H, tile_h=12)
+    ops.conv3x3_wino_dgrad(st.t1d, d, st.pack1t.get(st.w1t), nc, dslab, out_mask=cm, cot_per_group=C // ops.BN)
+
+
 def _wgrad_ws(st, desc, cout, device) -> torch.Tensor:
     import ctypes
     from . import _native
@@ -225,7 +278,10 @@ class ProjectFuseFunction(torch.autograd.Function):
         # (conv2's wgrad reads the fp32 dy2: at its size the row split costs what it saves)
         dw2 = ops.conv3x3_wgrad(ws.y1, d_y1, dy2, 2, mid, workspace=_wgrad_ws(st, d_y1, mid, dev))
         _mark("bwd_conv2_dgrad")
-        dy1 = ops.conv3x3_dgrad(dy2 if dy2s is None else dy2s, st.dgrad2, w2, 2)
+        if dy2s is not None and engine.wino_conv2_active(ws):
+            dy1 = _dgrad2_wino(engine, st, dy2s, w2)
+        else:
+            dy1 = ops.conv3x3_dgrad(dy2 if dy2s is None else dy2s, st.dgrad2, w2, 2)
         if dy1.shape[1] != mid:
             dy1 = dy1[:, :mid].contiguous()
         del dy2, dy2s
@@ -254,12 +310,16 @@ class ProjectFuseFunction(torch.autograd.Function):
             cp = st.dgrad1.cout_p
             if C % ops.KC == 0:  # split-bf16 dslab: the adjoint gathers 8 channels per 32-B entry
                 dslab = torch.empty(ops.split_shape(B, cp, H, W), dtype=torch.bfloat16, device=dev)
-                # frustum: a view's tiles of dslab that its warp never samples are not computed
-                cm = (engine.conv1_mask(dev, 0, H, tile_h=ops.dgrad_tile_rows(dy1s is not None, 1))
-                      if C % ops.BN == 0 else None)
-                sched = _dgrad1_schedule(st, B, cp, H, W, mid, cm, C // ops.BN, dev) if dy1s is not None else None
-                ops.conv3x3_dgrad(dy1 if dy1s is None else dy1s, st.dgrad1, w1, 1, out=dslab, out_mask=cm,
-                                  cot_per_group=C // ops.BN, sched=sched)
+                if dy1s is not None and _dgrad1_wino_applies(engine, cp, dev):
+                    _dgrad1_wino(engine, st, dy1s, w1, dslab)
+                else:
+                    # frustum: a view's tiles of dslab that its warp never samples are not computed
+                    cm = (engine.conv1_mask(dev, 0, H, tile_h=ops.dgrad_tile_rows(dy1s is not None, 1))
+                          if C % ops.BN == 0 else None)
+                    sched = (_dgrad1_schedule(st, B, cp, H, W, mid, cm, C // ops.BN, dev) if dy1s is not None
+                             else None)
+                    ops.conv3x3_dgrad(dy1 if dy1s is None else dy1s, st.dgrad1, w1, 1, out=dslab, out_mask=cm,
+                                      cot_per_group=C // ops.BN, sched=sched)
                 g8 = C // ops.KC
                 douts = [dslab[:, v * g8:(v + 1) * g8] for v in range(n)]
             else:

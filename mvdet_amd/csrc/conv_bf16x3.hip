@@ -1488,6 +1488,9 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   const int ty = pp / a.tiles_x;
   const int x0 = (pp - ty * a.tiles_x) * TW;
   const int y0 = a.out_row0 + ty * RT;
+  // (a data gradient's output-side frustum mask: output channel group cot / cot_pg of this pixel
+  // tile is never read — the whole block leaves before any barrier)
+  if (a.cmask && !((a.cmask[pp] >> (cot / a.cot_pg)) & 1u)) return;
   const uint32_t gm = a.gmask ? a.gmask[pp] : 0u;
   const int nch = a.gmask ? __builtin_popcount(gm) * a.cpg : a.nchunks;
   const int K8 = a.K / SB;
@@ -1740,7 +1743,8 @@ static int wino_rows_launch(const void* x, const mvbev_conv_desc* d, int dil, co
 static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_packed, const float* bias,
                        const float* init, int64_t Cout, int relu, float* y, int y_layout,
                        const uint32_t* group_mask, const int32_t* tile_order, void* stream, int dil = 1,
-                       const float* w3 = nullptr, float* p3 = nullptr, int64_t band_rows = 0) {
+                       const float* w3 = nullptr, float* p3 = nullptr, int64_t band_rows = 0,
+                       const uint32_t* out_mask = nullptr, int64_t cot_pg = 1) {
   if (!t || !d || !w_packed || (!y && !p3)) return MVBEV_ERR_NULL;
   if (dil != 1 && dil != 2) return MVBEV_ERR_DILATION;
   if (p3 && (!w3 || group_mask || init)) return MVBEV_ERR_SHAPE;  // the conv2 -> conv3 form: dense, bias only
@@ -1771,6 +1775,11 @@ static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_pa
     a.cpg = (int)(d->group / KC);
   }
   a.tile_order = group_mask ? tile_order : nullptr;
+  if (out_mask) {  // output-side mask (dense K): no input mask, no conv3 partials, <= 32 channel groups
+    if (group_mask || p3 || band_rows || cot_pg <= 0 || a.n_cot > 32 * cot_pg) return MVBEV_ERR_SHAPE;
+    a.cmask = out_mask;
+    a.cot_pg = (int)cot_pg;
+  }
   a.y_split = y_layout == MVBEV_LAYOUT_SPLIT_BF16;
   if (band_rows < 0 || (band_rows > 0 && (a.y_split || p3 || band_rows > d->out_rows))) return MVBEV_ERR_SHAPE;
   a.band_rows = (int)band_rows;
@@ -2005,6 +2014,14 @@ int mvbev_conv3x3_wino_bf16x3_dil(const void* t, const mvbev_conv_desc* desc, co
                                   int64_t Cout, int dilation, int relu, void* y, int y_layout, void* stream) {
   return mvbev::b3::wino_launch(t, desc, w_packed, bias, nullptr, Cout, relu, static_cast<float*>(y), y_layout,
                                 nullptr, nullptr, stream, dilation);
+}
+
+int mvbev_conv3x3_wino_bf16x3_dgrad(const void* t, const mvbev_conv_desc* desc, const void* w_packed, int64_t Cout,
+                                    void* dx, int dx_layout, const uint32_t* out_mask, int64_t cot_per_group,
+                                    void* stream) {
+  if (out_mask && (cot_per_group <= 0 || cot_per_group > 65536)) return MVBEV_ERR_SHAPE;
+  return mvbev::b3::wino_launch(t, desc, w_packed, nullptr, nullptr, Cout, 0, static_cast<float*>(dx), dx_layout,
+                                nullptr, nullptr, stream, 1, nullptr, nullptr, 0, out_mask, cot_per_group);
 }
 
 int mvbev_conv3x3_wino_bf16x3_cout1_partials(const void* t, const mvbev_conv_desc* desc, const void* w_packed,

@@ -794,6 +794,38 @@ def conv3x3_wino_dil(t: torch.Tensor, desc, packed: torch.Tensor, cout: int, dil
     return out
 
 
+def conv3x3_wino_dgrad(t: torch.Tensor, desc, packed: torch.Tensor, cout: int, out: torch.Tensor,
+                       out_mask: Optional[torch.Tensor] = None, cot_per_group: int = 1) -> torch.Tensor:
+    """A dilation-1 data gradient from the row-Winograd transform ``t`` of the split-bf16 dy
+    (``wino_rows``) and ``PackedConv3x3(..., wino=True)`` weights of the forward weight with its in /
+    out channels swapped and taps reversed: ``mvbev_conv3x3_wino_bf16x3_dgrad``.  ``out``: fp32
+    [B, cout, out_rows, W] or split-bf16; ``out_mask`` as ``conv3x3_dgrad``'s (12 x 32 tiles,
+    ``cot_per_group`` 128-channel Cout tiles per bit): cleared tiles are not written."""
+    _require_cuda(t, packed, out)
+    B, W, out_rows = desc.B, desc.W, desc.out_rows
+    lib = _native.load()
+    if packed.numel() * packed.element_size() < lib.mvbev_conv3x3_packed_bytes_wino(cout, desc.K):
+        raise ValueError("packed weights are smaller than the Winograd conv needs")
+    if t.numel() * t.element_size() < wino_rows_bytes(desc):
+        raise ValueError("t is smaller than the descriptor's row-Winograd transform")
+    y_split = out.dtype == torch.bfloat16
+    want = split_shape(B, cout, out_rows, W) if y_split else (B, cout, out_rows, W)
+    if tuple(out.shape) != want or not out.is_contiguous() or out.dtype not in (torch.float32, torch.bfloat16):
+        raise ValueError(f"out must be a contiguous {'bf16' if y_split else 'fp32'} {want} tensor")
+    mp = None
+    if out_mask is not None:
+        _require_cuda(out_mask)
+        tiles = -(-out_rows // 12) * -(-W // _native.TILE_W)
+        if out_mask.dtype != torch.int32 or out_mask.numel() < tiles or not out_mask.is_contiguous():
+            raise ValueError(f"out_mask must be a contiguous int32 tensor of >= {tiles} tiles")
+        mp = out_mask.data_ptr()
+    st = lib.mvbev_conv3x3_wino_bf16x3_dgrad(t.data_ptr(), ctypes.byref(desc), packed.data_ptr(), cout, out.data_ptr(),
+                                             _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32, mp,
+                                             int(cot_per_group), _stream(t))
+    _native.check(st, "mvbev_conv3x3_wino_bf16x3_dgrad")
+    return out
+
+
 def conv3x3_wino_then_cout1_partials(t: torch.Tensor, desc, packed: torch.Tensor, cout: int,
                                      bias: Optional[torch.Tensor], dilation: int, relu: bool,
                                      weight3: torch.Tensor, partials: torch.Tensor) -> None:

@@ -353,15 +353,6 @@ def test_conv_dgrad_vs_torch(B, Cw, K, H, W, dil):
     assert (got[:, K:] == 0).all()
 
 
-def _split_encode(x: torch.Tensor) -> torch.Tensor:
-    """fp32 [B, C, H, W] (C % 8 == 0) -> the split-bf16 blocked layout [B, C/8, H, W, 2, 8]."""
-    B, C, H, W = x.shape
-    hi = x.to(torch.bfloat16)
-    lo = (x - hi.float()).to(torch.bfloat16)
-    t = torch.stack([hi, lo], 0).reshape(2, B, C // 8, 8, H, W)
-    return t.permute(1, 2, 4, 5, 0, 3).contiguous()
-
-
 @pytest.mark.parametrize("B,Cw,K,H,W,dil", [(1, 128, 40, 25, 36, 1), (2, 512, 512, 17, 37, 2),
                                             (1, 256, 200, 9, 64, 1)])
 def test_conv_dgrad_split_dy_ring_kernel(B, Cw, K, H, W, dil):
@@ -380,6 +371,63 @@ def test_conv_dgrad_split_dy_ring_kernel(B, Cw, K, H, W, dil):
     assert (got[:, K:] == 0).all()
     f32 = ops.conv3x3_dgrad(dy.to(DEV), pk, w.to(DEV), dil)
     assert_parity(got.cpu(), f32.cpu(), "split vs fp32 dy", normwise_tol=2e-5)
+
+
+@pytest.mark.parametrize("B,C,H,W", [(1, 128, 25, 36), (2, 512, 17, 70)])
+def test_conv2_dgrad_as_winograd_conv(B, C, H, W):
+    """The training backward's conv2 data gradient (``autograd._dgrad2_wino``: the forward's
+    dilation-2 row-Winograd conv with the weight transposed and flipped) vs float64 torch, twice
+    with a changed weight (the persistent transposed copy must be re-packed)."""
+    from types import SimpleNamespace
+    from mvdet_amd import autograd, ops
+    g = torch.Generator().manual_seed(C + H)
+    eng = SimpleNamespace(grid_hw=(H, W), mid=C)
+    st = SimpleNamespace()
+    for it in range(2):
+        w = torch.randn((C, C, 3, 3), generator=g) * 0.05
+        dy = torch.randn((B, C, H, W), generator=g)
+        ref = torch.nn.grad.conv2d_input((B, C, H, W), w.double(), dy.double(), padding=2, dilation=2)
+        got = autograd._dgrad2_wino(eng, st, _split_encode(dy).to(DEV), w.to(DEV))
+        assert_parity(got.cpu(), ref, f"conv2 dgrad (Winograd), weight {it}")
+
+
+@pytest.mark.parametrize("B,Cw,K,H,W", [(1, 128, 256, 25, 70), (2, 256, 384, 14, 40)])
+def test_conv1_dgrad_as_masked_winograd_conv(B, Cw, K, H, W):
+    """``ops.conv3x3_wino_dgrad`` (the training backward's conv1 data gradient: row-Winograd conv
+    of the split dy with the weight swapped and flipped) vs float64 torch on the tiles its output
+    mask keeps (one 128-channel group per bit, random bits per 12 x 32 tile); cleared tiles keep
+    what ``out`` held."""
+    from mvdet_amd import ops
+    g = torch.Generator().manual_seed(Cw + K + H)
+    w = torch.randn((Cw, K, 3, 3), generator=g) * 0.05
+    dy = torch.randn((B, Cw, H, W), generator=g)
+    ref = torch.nn.grad.conv2d_input((B, K, H, W), w.double(), dy.double(), padding=1, dilation=1)
+    d = ops.conv_desc(B, Cw, H, W, group=Cw, group_stride=0, batch_stride=Cw * H * W)
+    t = torch.zeros((ops.wino_rows_bytes(d) + 1) // 2, dtype=torch.bfloat16, device=DEV)
+    ops.wino_rows(_split_encode(dy).to(DEV), d, t)
+    wt = w.flip(2, 3).transpose(0, 1).contiguous().to(DEV)
+    packed = ops.PackedConv3x3(None, "bf16x3", wino=True).get(wt)
+    ty, tx = -(-H // 12), -(-W // 32)
+    ngroups = K // 128
+    mask = torch.randint(0, 1 << ngroups, (ty * tx,), generator=g, dtype=torch.int32)
+    mask[0] = (1 << ngroups) - 1
+    out = torch.full(ops.split_shape(B, K, H, W), 7.0, dtype=torch.bfloat16, device=DEV)
+    ops.conv3x3_wino_dgrad(t, d, packed, K, out, out_mask=mask.to(DEV), cot_per_group=1)
+    got = ops.split_decode(out, K).cpu().double()
+    keep = torch.zeros((K, H, W), dtype=torch.bool)
+    for i in range(ty):
+        for j in range(tx):
+            for gi in range(ngroups):
+                if (int(mask[i * tx + j]) >> gi) & 1:
+                    keep[gi * 128:(gi + 1) * 128, 12 * i:12 * i + 12, 32 * j:32 * j + 32] = True
+    keep = keep.expand(B, K, H, W)
+    assert keep.any() and (~keep).any()
+    assert_parity(got[keep].reshape(-1, 1), ref[keep].reshape(-1, 1), "masked Winograd dgrad (kept tiles)")
+    assert (got[~keep] == 14.0).all()  # hi 7 + lo 7: untouched
+    # dense (no mask) equals the masked result on the kept tiles bit for bit
+    dense = torch.empty((B, K, H, W), dtype=torch.float32, device=DEV)
+    ops.conv3x3_wino_dgrad(t, d, packed, K, dense)
+    assert_parity(dense.cpu().double(), ref, "Winograd dgrad (dense, fp32 out)")
 
 
 def test_relu_backward_split():

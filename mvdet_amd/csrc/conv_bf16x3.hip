@@ -1319,37 +1319,42 @@ constexpr int WPART = NTAP * KC * BN;             // bf16 per part per (chunk, c
 constexpr int W16 = 2 * WPART * 2 / 16;           // 16-B pieces per (chunk, cout tile)
 }  // namespace wino
 
-// packed[chunk][cot][part][3 xi + kw][sub][co][j] = split(sum_kh G[xi][kh] w[co][map(k)][kh][kw])
+// packed[chunk][cot][part][3 xi + kw][sub][co][j] = split(sum_kh G[xi][kh] w[co][map(k)][kh][kw]).
+// A thread per (chunk, cot, kw, sub, co, j) loads the kernel column g[kh] once and writes its 5 xi x
+// 2 parts (per step a training forward + backward re-packs 2 x 3584 x 512 weights: one thread per
+// output, 10 x the column loads, took ~0.2 ms per big weight).
 __global__ void pack_wino_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int Cout, int Cin_w,
                                  const int32_t* __restrict__ chan_map, int K, int K_pad) {
   const int n_cot = Cout / BN;
-  const int64_t total = (int64_t)(K_pad / KC) * n_cot * 2 * wino::WPART;
+  const int64_t total = (int64_t)(K_pad / KC) * n_cot * 3 * 2 * BN * SB;  // columns
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t r = i;
     const int j = r % SB; r /= SB;
     const int co = r % BN; r /= BN;
     const int sub = r % 2; r /= 2;
-    const int tap = r % wino::NTAP; r /= wino::NTAP;
-    const int part = r % 2; r /= 2;
+    const int kw = r % 3; r /= 3;
     const int cot = r % n_cot;
     const int chunk = (int)(r / n_cot);
     const int k = chunk * KC + sub * SB + j;
     int ci = k < K ? (chan_map ? chan_map[k] : k) : -1;
     if (ci >= Cin_w) ci = -1;
-    float v = 0.f;
+    double g0 = 0.0, g1 = 0.0, g2 = 0.0;
     if (ci >= 0) {
-      const float* g = w + ((int64_t)(cot * BN + co) * Cin_w + ci) * 9 + tap % 3;  // g[3 kh]
-      const double g0 = g[0], g1 = g[3], g2 = g[6];
-      const int xi = tap / 3;
-      const double u = xi == 0 ? 0.5 * g0
-                     : xi == 1 ? -0.5 * (g0 + g1 + g2)
-                     : xi == 2 ? (g1 - g0 - g2) / 6.0
-                     : xi == 3 ? (g0 + 2.0 * g1 + 4.0 * g2) / 6.0
-                               : g2;
-      v = (float)u;
+      const float* g = w + ((int64_t)(cot * BN + co) * Cin_w + ci) * 9 + kw;  // g[3 kh]
+      g0 = g[0], g1 = g[3], g2 = g[6];
     }
-    const __bf16 hi = (__bf16)v;
-    out[i] = part ? (__bf16)(v - (float)hi) : hi;
+    const double u[wino::NXI] = {0.5 * g0, -0.5 * (g0 + g1 + g2), (g1 - g0 - g2) / 6.0,
+                                 (g0 + 2.0 * g1 + 4.0 * g2) / 6.0, g2};
+    // element (part, tap = 3 xi + kw, sub, co, j) of the (chunk, cot) block
+    __bf16* o = out + ((int64_t)chunk * n_cot + cot) * 2 * wino::WPART + ((int64_t)sub * BN + co) * SB + j;
+#pragma unroll
+    for (int xi = 0; xi < wino::NXI; ++xi) {
+      const float v = (float)u[xi];
+      const __bf16 hi = (__bf16)v;
+      const int tap = 3 * xi + kw;
+      o[(int64_t)tap * KC * BN] = hi;
+      o[(int64_t)(wino::NTAP + tap) * KC * BN] = (__bf16)(v - (float)hi);
+    }
   }
 }
 
@@ -1977,7 +1982,7 @@ int mvbev_pack_conv3x3_weight_wino(const float* w, int64_t Cout, int64_t Cin_w, 
   if (Cout <= 0 || Cin_w <= 0 || K <= 0) return MVBEV_ERR_RANK;
   if (Cout % b3::BN != 0) return MVBEV_ERR_SHAPE;
   if (!chan_map && K != Cin_w) return MVBEV_ERR_SHAPE;
-  const int64_t total = (int64_t)mvbev_conv3x3_packed_bytes_wino(Cout, K) / 2;
+  const int64_t total = (int64_t)mvbev_conv3x3_packed_bytes_wino(Cout, K) / 2 / (2 * b3::wino::NXI);  // threads
   const int blocks = (int)std::min<int64_t>(ceil_div(total, 256), 8192);
   hipLaunchKernelGGL(b3::pack_wino_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), w,
                      static_cast<__bf16*>(w_packed), (int)Cout, (int)Cin_w, chan_map, (int)K,

@@ -360,6 +360,12 @@ int mvbev_conv3x3_wino_bf16x3_cout1_partials(const void* t, const mvbev_conv_des
  * bias / init / ReLU; dx fp32 or split-bf16 [B][Cout][out_rows][W].  out_mask (optional, int32 per
  * 12 x 32 output tile as mvbev_warp_tile_mask): tiles of output channel group g (cot_per_group
  * 128-channel tiles) whose bit g is clear are not written (a consumer that never reads them). */
+/* The data-gradient weights of mvbev_conv3x3_wino_bf16x3_dgrad straight from the forward weight
+ * w [Cout_f][Cin_f][3][3] fp32 (ABI 11800): packed as mvbev_pack_conv3x3_weight_wino would pack
+ * w'[o][i][kh][kw] = w[i][o][2 - kh][2 - kw] for o < Cout (Cout % 128 == 0, Cout <= Cin_f: the
+ * first Cout forward input channels) and i < Cout_f (the packed K). */
+int mvbev_pack_conv3x3_weight_wino_dgrad(const float* w, int64_t Cout_f, int64_t Cin_f, int64_t Cout, void* w_packed,
+                                         void* stream);
 int mvbev_conv3x3_wino_bf16x3_dgrad(const void* t, const mvbev_conv_desc* desc, const void* w_packed, int64_t Cout,
                                     void* dx, int dx_layout, const uint32_t* out_mask, int64_t cot_per_group,
                                     void* stream);

@@ -66,6 +66,7 @@ EXPORTS = (
     "mvbev_conv3x3_wino_bf16x3_dil",
     "mvbev_conv3x3_wino_bf16x3_cout1_partials",
     "mvbev_conv3x3_wino_bf16x3_dgrad",
+    "mvbev_pack_conv3x3_weight_wino_dgrad",
     "mvbev_warp_views_wino_rows",
     "mvbev_warp_views_upsampled_wino_rows",
     "mvbev_warp_nonfinite_views",
@@ -197,6 +198,8 @@ def _declare(lib):
     lib.mvbev_conv3x3_wino_bf16x3_dil.restype = ctypes.c_int
     lib.mvbev_conv3x3_wino_bf16x3_dil.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, _i64, ctypes.c_int,
                                                   ctypes.c_int, _p, ctypes.c_int, _p]
+    lib.mvbev_pack_conv3x3_weight_wino_dgrad.restype = ctypes.c_int
+    lib.mvbev_pack_conv3x3_weight_wino_dgrad.argtypes = [_p, _i64, _i64, _i64, _p, _p]
     lib.mvbev_conv3x3_wino_bf16x3_dgrad.restype = ctypes.c_int
     lib.mvbev_conv3x3_wino_bf16x3_dgrad.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _i64, _p, ctypes.c_int, _p,
                                                     _i64, _p]

@@ -151,22 +151,20 @@ def _dgrad1_schedule(st, B, cout_p, H, W, K, out_mask, cot_per_group, device):
 def _dgrad2_wino(engine: ProjectFuse, st, dy2s: torch.Tensor, w2: torch.Tensor) -> torch.Tensor:
     """conv2's data gradient as the forward's dilation-2 row-Winograd conv (``conv3x3_wino_dil``):
     with padding = dilation, dgrad(dy) = conv(dy, w^T flipped) — the weight's in / out channels
-    swapped and its taps reversed (a 512 x 512 copy per step into a persistent tensor, so the
-    packer's (pointer, version) key sees each new weight).  dy2s: split-bf16 [B, 512, H, W]."""
+    swapped and its taps reversed (``ops.PackedWinoDgrad3x3``: packed from w2 itself, no transposed
+    copy).  dy2s: split-bf16 [B, 512, H, W]."""
     H, W = engine.grid_hw
     mid = engine.mid
     B = dy2s.shape[0]
     d = ops.conv_desc(B, mid, H, W, group=mid, group_stride=0, batch_stride=mid * H * W)
-    if getattr(st, "w2t", None) is None or st.w2t.device != w2.device:
-        st.w2t = torch.empty_like(w2, memory_format=torch.contiguous_format)
-        st.pack2t = ops.PackedConv3x3(None, "bf16x3", wino=True)
+    if getattr(st, "pack2t", None) is None:
+        st.pack2t = ops.PackedWinoDgrad3x3(mid)
         st.t2d = None
-    st.w2t.copy_(w2.detach().flip(2, 3).transpose(0, 1))
     need = ops.wino_rows_bytes(d)
-    if st.t2d is None or st.t2d.numel() * 2 < need:  # zero-filled once (as the forward's T)
+    if st.t2d is None or st.t2d.numel() * 2 < need or st.t2d.device != dy2s.device:  # zero-filled once
         st.t2d = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=dy2s.device)
     ops.wino_rows(dy2s, d, st.t2d, dilation=2)
-    return ops.conv3x3_wino_dil(st.t2d, d, st.pack2t.get(st.w2t), mid, 2)
+    return ops.conv3x3_wino_dil(st.t2d, d, st.pack2t.get(w2), mid, 2)
 
 
 def _dgrad1_wino_applies(engine: ProjectFuse, cp: int, device) -> bool:
@@ -188,17 +186,15 @@ def _dgrad1_wino(engine: ProjectFuse, st, dy1s: torch.Tensor, w1: torch.Tensor, 
     nc = engine.num_cam * C
     B = dy1s.shape[0]
     d = ops.conv_desc(B, mid, H, W, group=mid, group_stride=0, batch_stride=mid * H * W)
-    if getattr(st, "w1t", None) is None or st.w1t.device != w1.device or st.w1t.shape[0] != nc:
-        st.w1t = torch.empty((nc, mid, 3, 3), dtype=torch.float32, device=w1.device)
-        st.pack1t = ops.PackedConv3x3(None, "bf16x3", wino=True)
+    if getattr(st, "pack1t", None) is None or st.pack1t.cout != nc:
+        st.pack1t = ops.PackedWinoDgrad3x3(nc)  # w1's first nc input channels: the views (the coord ones last)
         st.t1d = None
-    st.w1t.copy_(w1.detach()[:, :nc].flip(2, 3).transpose(0, 1))
     need = ops.wino_rows_bytes(d)
-    if st.t1d is None or st.t1d.numel() * 2 < need:
+    if st.t1d is None or st.t1d.numel() * 2 < need or st.t1d.device != dy1s.device:
         st.t1d = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=dy1s.device)
     ops.wino_rows(dy1s, d, st.t1d)
     cm = engine.conv1_mask(dy1s.device, 0, H, tile_h=12)
-    ops.conv3x3_wino_dgrad(st.t1d, d, st.pack1t.get(st.w1t), nc, dslab, out_mask=cm, cot_per_group=C // ops.BN)
+    ops.conv3x3_wino_dgrad(st.t1d, d, st.pack1t.get(w1), nc, dslab, out_mask=cm, cot_per_group=C // ops.BN)
 
 
 def _wgrad_ws(st, desc, cout, device) -> torch.Tensor:

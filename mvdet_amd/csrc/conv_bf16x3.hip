@@ -1323,8 +1323,11 @@ constexpr int W16 = 2 * WPART * 2 / 16;           // 16-B pieces per (chunk, cou
 // A thread per (chunk, cot, kw, sub, co, j) loads the kernel column g[kh] once and writes its 5 xi x
 // 2 parts (per step a training forward + backward re-packs 2 x 3584 x 512 weights: one thread per
 // output, 10 x the column loads, took ~0.2 ms per big weight).
+// swap (a data gradient's weights): the packed [Cout][K] weight is w^T with its taps reversed,
+// packed[o][i][kh][kw] = w[i][o][2 - kh][2 - kw], read from the forward weight w [K][Cin_w][3][3]
+// (o < Cout <= Cin_w) without a transposed copy.
 __global__ void pack_wino_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int Cout, int Cin_w,
-                                 const int32_t* __restrict__ chan_map, int K, int K_pad) {
+                                 const int32_t* __restrict__ chan_map, int K, int K_pad, bool swap) {
   const int n_cot = Cout / BN;
   const int64_t total = (int64_t)(K_pad / KC) * n_cot * 3 * 2 * BN * SB;  // columns
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1337,11 +1340,14 @@ __global__ void pack_wino_kernel(const float* __restrict__ w, __bf16* __restrict
     const int chunk = (int)(r / n_cot);
     const int k = chunk * KC + sub * SB + j;
     int ci = k < K ? (chan_map ? chan_map[k] : k) : -1;
-    if (ci >= Cin_w) ci = -1;
+    if (!swap && ci >= Cin_w) ci = -1;  // (swap: ci is the forward weight's output row, < K)
     double g0 = 0.0, g1 = 0.0, g2 = 0.0;
-    if (ci >= 0) {
+    if (ci >= 0 && !swap) {
       const float* g = w + ((int64_t)(cot * BN + co) * Cin_w + ci) * 9 + kw;  // g[3 kh]
       g0 = g[0], g1 = g[3], g2 = g[6];
+    } else if (ci >= 0) {
+      const float* g = w + ((int64_t)ci * Cin_w + cot * BN + co) * 9 + (2 - kw);  // reversed taps
+      g0 = g[6], g1 = g[3], g2 = g[0];
     }
     const double u[wino::NXI] = {0.5 * g0, -0.5 * (g0 + g1 + g2), (g1 - g0 - g2) / 6.0,
                                  (g0 + 2.0 * g1 + 4.0 * g2) / 6.0, g2};
@@ -1986,7 +1992,22 @@ int mvbev_pack_conv3x3_weight_wino(const float* w, int64_t Cout, int64_t Cin_w, 
   const int blocks = (int)std::min<int64_t>(ceil_div(total, 256), 8192);
   hipLaunchKernelGGL(b3::pack_wino_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), w,
                      static_cast<__bf16*>(w_packed), (int)Cout, (int)Cin_w, chan_map, (int)K,
-                     (int)round_up(K, b3::KC));
+                     (int)round_up(K, b3::KC), false);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+int mvbev_pack_conv3x3_weight_wino_dgrad(const float* w, int64_t Cout_f, int64_t Cin_f, int64_t Cout, void* w_packed,
+                                         void* stream) {
+  using namespace mvbev;
+  if (!w || !w_packed) return MVBEV_ERR_NULL;
+  if (Cout_f <= 0 || Cin_f <= 0 || Cout <= 0) return MVBEV_ERR_RANK;
+  if (Cout % b3::BN != 0 || Cout > Cin_f || Cout_f > INT32_MAX / 2 || Cin_f > INT32_MAX / 2) return MVBEV_ERR_SHAPE;
+  const int64_t total = (int64_t)mvbev_conv3x3_packed_bytes_wino(Cout, Cout_f) / 2 / (2 * b3::wino::NXI);
+  const int blocks = (int)std::min<int64_t>(ceil_div(total, 256), 8192);
+  hipLaunchKernelGGL(b3::pack_wino_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), w,
+                     static_cast<__bf16*>(w_packed), (int)Cout, (int)Cin_f, nullptr, (int)Cout_f,
+                     (int)round_up(Cout_f, b3::KC), true);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }

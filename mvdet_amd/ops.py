@@ -376,6 +376,37 @@ class PackedConv3x3:
         return self.packed
 
 
+class PackedWinoDgrad3x3:
+    """The row-Winograd weights of a data gradient (``conv3x3_wino_dgrad`` / ``conv3x3_wino_dil``)
+    packed straight from the forward weight [Cout_f, Cin_f, 3, 3]: in / out channels swapped, taps
+    reversed, the first ``cout`` forward input channels (``mvbev_pack_conv3x3_weight_wino_dgrad``);
+    re-packed when the parameter changes (keyed as ``PackedConv3x3``)."""
+
+    def __init__(self, cout: int):
+        if cout <= 0 or cout % BN:
+            raise ValueError(f"cout={cout} must be a positive multiple of {BN}")
+        self.cout = int(cout)
+        self._key = None
+        self.packed: Optional[torch.Tensor] = None
+
+    def get(self, weight: torch.Tensor) -> torch.Tensor:
+        _require_cuda(weight)
+        lib = _native.load()
+        key = (weight.data_ptr(), weight._version, tuple(weight.shape), id(lib))
+        if key != self._key:
+            cout_f, cin_f, kh, kw = weight.shape
+            if (kh, kw) != (3, 3) or weight.dtype != torch.float32 or cin_f < self.cout:
+                raise ValueError(f"expected a float32 [Cout, >= {self.cout}, 3, 3] weight")
+            w = weight.detach().contiguous()
+            n = lib.mvbev_conv3x3_packed_bytes_wino(self.cout, cout_f)
+            packed = torch.empty(n // 2, dtype=torch.bfloat16, device=weight.device)
+            st = lib.mvbev_pack_conv3x3_weight_wino_dgrad(w.data_ptr(), cout_f, cin_f, self.cout, packed.data_ptr(),
+                                                          _stream(packed))
+            _native.check(st, "mvbev_pack_conv3x3_weight_wino_dgrad")
+            self.packed, self._key = packed, key
+        return self.packed
+
+
 def conv_desc(B: int, K: int, H: int, W: int, group: int, group_stride: int, batch_stride: int,
               in_row0: int = 0, in_rows: Optional[int] = None, out_row0: int = 0,
               out_rows: Optional[int] = None) -> "_native.ConvDesc":

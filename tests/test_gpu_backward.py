@@ -377,21 +377,22 @@ def test_conv_dgrad_split_dy_ring_kernel(B, Cw, K, H, W, dil):
 def test_conv2_dgrad_as_winograd_conv(B, C, H, W):
     """The training backward's conv2 data gradient (``autograd._dgrad2_wino``: the forward's
     dilation-2 row-Winograd conv with the weight transposed and flipped) vs float64 torch, twice
-    with a changed weight (the persistent transposed copy must be re-packed)."""
+    with the weight changed in place (re-packed per parameter version)."""
     from types import SimpleNamespace
     from mvdet_amd import autograd, ops
     g = torch.Generator().manual_seed(C + H)
     eng = SimpleNamespace(grid_hw=(H, W), mid=C)
     st = SimpleNamespace()
+    w = torch.empty((C, C, 3, 3), device=DEV)  # one parameter updated in place: re-packed per version
     for it in range(2):
-        w = torch.randn((C, C, 3, 3), generator=g) * 0.05
+        w.copy_(torch.randn((C, C, 3, 3), generator=g) * 0.05)
         dy = torch.randn((B, C, H, W), generator=g)
-        ref = torch.nn.grad.conv2d_input((B, C, H, W), w.double(), dy.double(), padding=2, dilation=2)
-        got = autograd._dgrad2_wino(eng, st, _split_encode(dy).to(DEV), w.to(DEV))
+        ref = torch.nn.grad.conv2d_input((B, C, H, W), w.cpu().double(), dy.double(), padding=2, dilation=2)
+        got = autograd._dgrad2_wino(eng, st, _split_encode(dy).to(DEV), w)
         assert_parity(got.cpu(), ref, f"conv2 dgrad (Winograd), weight {it}")
 
 
-@pytest.mark.parametrize("B,Cw,K,H,W", [(1, 128, 256, 25, 70), (2, 256, 384, 14, 40)])
+@pytest.mark.parametrize("B,Cw,K,H,W", [(1, 128, 256, 25, 70), (2, 256, 384, 14, 40), (1, 512, 256, 13, 40)])
 def test_conv1_dgrad_as_masked_winograd_conv(B, Cw, K, H, W):
     """``ops.conv3x3_wino_dgrad`` (the training backward's conv1 data gradient: row-Winograd conv
     of the split dy with the weight swapped and flipped) vs float64 torch on the tiles its output
@@ -407,6 +408,10 @@ def test_conv1_dgrad_as_masked_winograd_conv(B, Cw, K, H, W):
     ops.wino_rows(_split_encode(dy).to(DEV), d, t)
     wt = w.flip(2, 3).transpose(0, 1).contiguous().to(DEV)
     packed = ops.PackedConv3x3(None, "bf16x3", wino=True).get(wt)
+    # the dgrad packer reads the forward weight itself (swapped, reversed taps): the same bytes
+    assert torch.equal(ops.PackedWinoDgrad3x3(K).get(w.to(DEV)), packed)
+    wpad = torch.cat([w, torch.randn((Cw, 2, 3, 3), generator=g)], 1).to(DEV)  # extra (coord) inputs past K
+    assert torch.equal(ops.PackedWinoDgrad3x3(K).get(wpad), packed)
     ty, tx = -(-H // 12), -(-W // 32)
     ngroups = K // 128
     mask = torch.randint(0, 1 << ngroups, (ty * tx,), generator=g, dtype=torch.int32)

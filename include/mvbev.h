@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 11900: row windows (mvbev_warp_views_split_bf16_rows with the non-finite report, mvbev_warp_views_exact_rows with fp16 sources), mvbev_conv3x3_f32_ex (row-band output), mvbev_bias_relu_nonfinite_f32, mvbev_zero_gated — the non-finite guard of the multi-GPU modes and the banded exact path; 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -111,6 +111,18 @@ int mvbev_warp_views_f32(const mvbev_warp_view* views, int nviews, int64_t B, in
 int mvbev_warp_views_split_bf16_ex(const mvbev_warp_view* views, int nviews, int src_is_f16,
                                    int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
                                    int flags, void* stream);
+/* Row windows (ABI 11900): view i's dst holds out_rows rows of the Ho-row grid starting at grid row
+ * row0s[i] (host int32 array; 0 <= row0s[i], row0s[i] + out_rows <= Ho), so one launch can warp the row
+ * windows the multi-GPU band exchange sends (several entries may share a source).  nonfinite (may be
+ * NULL): nf_tag is stored into the device int32 *nonfinite when a sample the warp produces is non-finite
+ * (a NaN / inf feature it reads, or non-finite coordinates) — the non-finite guard's report, as the
+ * fused row-Winograd warps give it. */
+int mvbev_warp_views_split_bf16_rows(const mvbev_warp_view* views, const int32_t* row0s, int nviews, int src_is_f16,
+                                     int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
+                                     int64_t out_rows, int flags, int32_t* nonfinite, int32_t nf_tag, void* stream);
+/* Gated zero fill: bytes (a multiple of 16, 16-B aligned dst) of zeros when *gate == gate_tag, else no
+ * write (ABI 11900: re-zeroes the band exchange's send chunks after a frame whose exact path wrote them). */
+int mvbev_zero_gated(void* dst, int64_t bytes, const int32_t* gate, int32_t gate_tag, void* stream);
 /* Fused bilinear upsample + warp.  views[i].src is the
  * backbone-resolution map [B][C][h][w] that persp_trans_detector.py:65 upsamples with
  * F.interpolate(size=(H, W), mode='bilinear', align_corners=False) before the warp at :69;
@@ -193,6 +205,18 @@ typedef struct mvbev_conv_desc {
 int mvbev_conv3x3_f32(const float* x, const mvbev_conv_desc* desc, const float* w_packed,
                       const float* bias, const float* init, int64_t Cout, int dilation,
                       int relu, float* y, const int32_t* gate, int32_t gate_tag, void* stream);
+/* The same with a row-banded output (ABI 11900): y_band_rows > 0 puts global output row g at row
+ * g % y_band_rows of band g / y_band_rows of y = [bands][B][Cout][y_band_rows][W] — the partial-sum
+ * multi-GPU mode's reduce-scatter input (as mvbev_conv3x3_wino_bf16x3's band_rows); 0 = the plain y. */
+int mvbev_conv3x3_f32_ex(const float* x, const mvbev_conv_desc* desc, const float* w_packed, const float* bias,
+                         const float* init, int64_t Cout, int dilation, int relu, float* y, int64_t y_band_rows,
+                         const int32_t* gate, int32_t gate_tag, void* stream);
+/* y = relu?(y + init) in place (NaN-preserving ReLU) for y [B][C][rows][W] holding grid rows
+ * [row0, row0 + rows) of init [C][H][W]; stores tag into the device int32 *flag (NULL: no report) when a
+ * result is non-finite (ABI 11900: the coord term + bias + ReLU of the partial-sum mode's summed conv1
+ * pre-activation — persp_trans_detector.py:51 — and its non-finite guard). */
+int mvbev_bias_relu_nonfinite_f32(float* y, const float* init, int64_t B, int64_t C, int64_t rows, int64_t W,
+                                  int64_t H, int64_t row0, int relu, int32_t* flag, int32_t tag, void* stream);
 /* gate (this entry point, mvbev_conv3x3_cout1_f32, mvbev_warp_views_exact_f32; ABI 11600): a device
  * int32; when non-NULL the launch does its work only if *gate == gate_tag at the time it runs (every
  * workgroup exits at once otherwise) — a decision taken on the device in stream order, so a caller
@@ -320,6 +344,12 @@ int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views, int nview
 int mvbev_warp_views_exact_f32(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t h, int64_t w,
                                int64_t H, int64_t W, int64_t Ho, int64_t Wo, const int32_t* gate, int32_t gate_tag,
                                void* stream);
+/* The same on row windows and fp16 sources (ABI 11900): view i's dst holds out_rows rows of the Ho-row
+ * grid starting at grid row row0s[i] (host int32 array) — the exact path in row bands of bounded memory,
+ * and the band exchange's windows; src_is_f16: fp16 sources (fp32 math). */
+int mvbev_warp_views_exact_rows(const mvbev_warp_view* views, const int32_t* row0s, int nviews, int src_is_f16,
+                                int64_t B, int64_t C, int64_t h, int64_t w, int64_t H, int64_t W, int64_t Ho,
+                                int64_t Wo, int64_t out_rows, const int32_t* gate, int32_t gate_tag, void* stream);
 /* NCHW -> channels-last copy (ABI 11700): view i's fp32 [B][C][H][W] map at views[i].src /
  * src_strides into a contiguous [B][H][W][C] buffer at views[i].dst (dst_strides, m ignored), every
  * view in one launch — the input of the channels-last fused upsample warp for NCHW producers. */

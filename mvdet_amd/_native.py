@@ -76,6 +76,11 @@ EXPORTS = (
     "mvbev_bev_fuse",
     "mvbev_warp_views_exact_f32",
     "mvbev_nchw_to_nhwc_f32",
+    "mvbev_warp_views_split_bf16_rows",
+    "mvbev_warp_views_exact_rows",
+    "mvbev_conv3x3_f32_ex",
+    "mvbev_bias_relu_nonfinite_f32",
+    "mvbev_zero_gated",
 )
 BEV_SRC_F32, BEV_SRC_F16, BEV_SRC_BACKBONE_F32 = 0, 1, 2  # MVBEV_BEV_SRC_*
 BEV_SRC_CHANNELS_LAST = 16  # MVBEV_BEV_SRC_CHANNELS_LAST (flag)
@@ -216,6 +221,21 @@ def _declare(lib):
     lib.mvbev_warp_views_exact_f32.restype = ctypes.c_int
     lib.mvbev_warp_views_exact_f32.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
                                                _i64, _i64, _i64, _p, ctypes.c_int32, _p]
+    lib.mvbev_warp_views_split_bf16_rows.restype = ctypes.c_int
+    lib.mvbev_warp_views_split_bf16_rows.argtypes = [ctypes.POINTER(WarpView), _p, ctypes.c_int, ctypes.c_int, _i64,
+                                                     _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_int, _p,
+                                                     ctypes.c_int32, _p]
+    lib.mvbev_warp_views_exact_rows.restype = ctypes.c_int
+    lib.mvbev_warp_views_exact_rows.argtypes = [ctypes.POINTER(WarpView), _p, ctypes.c_int, ctypes.c_int, _i64, _i64,
+                                                _i64, _i64, _i64, _i64, _i64, _i64, _i64, _p, ctypes.c_int32, _p]
+    lib.mvbev_conv3x3_f32_ex.restype = ctypes.c_int
+    lib.mvbev_conv3x3_f32_ex.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64, ctypes.c_int,
+                                         ctypes.c_int, _p, _i64, _p, ctypes.c_int32, _p]
+    lib.mvbev_bias_relu_nonfinite_f32.restype = ctypes.c_int
+    lib.mvbev_bias_relu_nonfinite_f32.argtypes = [_p, _p, _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_int, _p,
+                                                  ctypes.c_int32, _p]
+    lib.mvbev_zero_gated.restype = ctypes.c_int
+    lib.mvbev_zero_gated.argtypes = [_p, _i64, _p, ctypes.c_int32, _p]
     lib.mvbev_nchw_to_nhwc_f32.restype = ctypes.c_int
     lib.mvbev_nchw_to_nhwc_f32.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _p]
     lib.mvbev_warp_tile_mask.restype = ctypes.c_int

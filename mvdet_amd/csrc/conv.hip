@@ -80,6 +80,8 @@ struct ConvArgs {
   int tiles_x, tiles_y, n_cot, nwg;
   const int32_t* gate;  // run only when *gate == gate_tag (NULL: always; the non-finite guard's path)
   int32_t gate_tag;
+  int band_rows;  // > 0: y in row bands [bands][B][Cout][band_rows][W], global row g at band g / band_rows
+  int B;
 };
 
 #ifndef MVBEV_CONV_MINWAVES
@@ -238,6 +240,17 @@ __global__ __launch_bounds__(64 * NWAVES, MVBEV_CONV_MINWAVES) void conv3x3_mfma
   auto emit = [&](const floatx16& acc, int ci_tile, int rj) {
     const int row = y0 + prow + rj;
     if (row >= a.out_row0 + a.out_rows || col >= W) return;
+    // the output address chosen once, outside the unrolled store loop (a branch inside it puts the
+    // accumulators in scratch): plain [B][Cout][out_rows][W], or row bands (ABI 11900)
+    int64_t ybase, cstride;
+    if (a.band_rows > 0) {
+      const int band = row / a.band_rows;
+      cstride = (int64_t)a.band_rows * W;
+      ybase = ((int64_t)band * a.B + b) * a.Cout * cstride + (int64_t)(row - band * a.band_rows) * W + col;
+    } else {
+      cstride = oplane;
+      ybase = (int64_t)b * a.Cout * oplane + (int64_t)(row - a.out_row0) * W + col;
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = cot * BN + cw + 32 * ci_tile + (r & 3) + 8 * (r >> 2) + 4 * kh;
@@ -245,7 +258,7 @@ __global__ __launch_bounds__(64 * NWAVES, MVBEV_CONV_MINWAVES) void conv3x3_mfma
       if (a.bias) v += a.bias[co];
       if (a.init) v += a.init[co * iplane + (int64_t)row * W + col];
       if (RELU) v = v < 0.f ? 0.f : v;  // torch.relu keeps NaN
-      a.y[((int64_t)b * a.Cout + co) * oplane + (int64_t)(row - a.out_row0) * W + col] = v;
+      a.y[ybase + co * cstride] = v;
     }
   };
   emit(acc00, 0, 0);
@@ -398,9 +411,64 @@ __global__ __launch_bounds__(64 * C1Q_WAVES) void conv3x3_cout1_q4_kernel(
   }
 }
 
+// y = relu?(y + init) in place, NaN-preserving, and the non-finite report (ABI 11900): y [B][C][rows][W]
+// holds grid rows [row0, row0 + rows) of init [C][H][W] (the coord term + bias).  Any non-finite result
+// stores tag into *flag — the partial-sum multi-GPU mode's summed conv1 pre-activation, whose NaN / inf
+// pattern is the reference's when every rank's partial is exact (the guard's gated exact conv2 then runs).
+template <bool VEC>
+__global__ __launch_bounds__(256) void bias_relu_nonfinite_kernel(float* __restrict__ y, const float* __restrict__ init,
+                                                                  int C, int rows, int W, int H, int row0, int relu,
+                                                                  int64_t n, int32_t* flag, int32_t tag) {
+  constexpr int V = VEC ? 4 : 1;
+  const int Wv = W / V;
+  bool bad = false;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t pix = i % ((int64_t)rows * Wv), bc = i / ((int64_t)rows * Wv);
+    const int r = (int)(pix / Wv), q = (int)(pix - (int64_t)r * Wv);
+    const int c = (int)(bc % C);
+    const int64_t io = ((int64_t)c * H + row0 + r) * W + (int64_t)q * V;
+    if constexpr (VEC) {
+      floatx4 v = reinterpret_cast<floatx4*>(y)[i];
+      const floatx4 t = *reinterpret_cast<const floatx4*>(init + io);
+      v += t;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (relu) v[e] = v[e] < 0.f ? 0.f : v[e];
+        bad = bad || !isfinite(v[e]);
+      }
+      reinterpret_cast<floatx4*>(y)[i] = v;
+    } else {
+      float v = y[i] + init[io];
+      if (relu) v = v < 0.f ? 0.f : v;
+      bad = bad || !isfinite(v);
+      y[i] = v;
+    }
+  }
+  if (flag && bad) *flag = tag;
+}
+
 }  // namespace mvbev
 
 extern "C" {
+
+int mvbev_bias_relu_nonfinite_f32(float* y, const float* init, int64_t B, int64_t C, int64_t rows, int64_t W,
+                                  int64_t H, int64_t row0, int relu, int32_t* flag, int32_t tag, void* stream) {
+  using namespace mvbev;
+  if (!y || !init) return MVBEV_ERR_NULL;
+  if (B <= 0 || C <= 0 || rows <= 0 || W <= 0 || H <= 0) return MVBEV_ERR_RANK;
+  if (row0 < 0 || row0 + rows > H || C > INT32_MAX || H > INT32_MAX) return MVBEV_ERR_SHAPE;
+  const bool vec = W % 4 == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0 && (reinterpret_cast<uintptr_t>(init) & 15) == 0;
+  const int64_t n = B * C * rows * W / (vec ? 4 : 1);
+  const dim3 grid((unsigned)std::min<int64_t>(ceil_div(n, 256), 8192));
+  if (vec)
+    hipLaunchKernelGGL(bias_relu_nonfinite_kernel<true>, grid, dim3(256), 0, as_stream(stream), y, init, (int)C,
+                       (int)rows, (int)W, (int)H, (int)row0, relu, n, flag, tag);
+  else
+    hipLaunchKernelGGL(bias_relu_nonfinite_kernel<false>, grid, dim3(256), 0, as_stream(stream), y, init, (int)C,
+                       (int)rows, (int)W, (int)H, (int)row0, relu, n, flag, tag);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
 
 size_t mvbev_conv3x3_packed_floats(int64_t Cout, int64_t K) {
   if (Cout <= 0 || K <= 0) return 0;
@@ -424,10 +492,21 @@ int mvbev_pack_conv3x3_weight_f32(const float* w, int64_t Cout, int64_t Cin_w,
   return MVBEV_OK;
 }
 
+int mvbev_conv3x3_f32_ex(const float* x, const mvbev_conv_desc* d, const float* w_packed, const float* bias,
+                         const float* init, int64_t Cout, int dilation, int relu, float* y, int64_t y_band_rows,
+                         const int32_t* gate, int32_t gate_tag, void* stream);
+
 int mvbev_conv3x3_f32(const float* x, const mvbev_conv_desc* d, const float* w_packed,
                       const float* bias, const float* init, int64_t Cout, int dilation, int relu,
                       float* y, const int32_t* gate, int32_t gate_tag, void* stream) {
+  return mvbev_conv3x3_f32_ex(x, d, w_packed, bias, init, Cout, dilation, relu, y, 0, gate, gate_tag, stream);
+}
+
+int mvbev_conv3x3_f32_ex(const float* x, const mvbev_conv_desc* d, const float* w_packed, const float* bias,
+                         const float* init, int64_t Cout, int dilation, int relu, float* y, int64_t y_band_rows,
+                         const int32_t* gate, int32_t gate_tag, void* stream) {
   using namespace mvbev;
+  if (y_band_rows < 0 || y_band_rows > INT32_MAX) return MVBEV_ERR_SHAPE;
   if (!x || !d || !w_packed || !y) return MVBEV_ERR_NULL;
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || d->in_rows <= 0 ||
       d->out_rows <= 0 || d->group <= 0)
@@ -447,6 +526,8 @@ int mvbev_conv3x3_f32(const float* x, const mvbev_conv_desc* d, const float* w_p
   a.out_row0 = (int)d->out_row0; a.out_rows = (int)d->out_rows;
   a.gate = gate;
   a.gate_tag = gate_tag;
+  a.band_rows = (int)y_band_rows;
+  a.B = (int)d->B;
   constexpr int kWaves = MVBEV_CONV_WAVES;
   constexpr bool kDbuf = MVBEV_CONV_DBUF != 0;
   a.tiles_x = (int)ceil_div(d->W, TW);

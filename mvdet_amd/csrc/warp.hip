@@ -44,7 +44,7 @@ __global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_tile_kernel(const Warp
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int v = ty * kWarpTH + (wave / WAVES_X) * kWarpWR + lane / WC;
   const int u = tx * kWarpTW + (wave % WAVES_X) * WC + lane % WC;
-  if (v >= a.Ho || u >= a.Wo) return;
+  if (v >= (a.out_rows ? a.out_rows : a.Ho) || u >= a.Wo) return;  // dst row v = grid row v + vw.row0
   const int c_begin = chunk * kWarpCPB;
   const int c_end = min(a.C, c_begin + kWarpCPB);
   const int H = a.H, W = a.W;
@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_tile_kernel(const Warp
 #pragma unroll
     for (int i = 0; i < 9; ++i) m[i] = vw.m[i];
   }
-  const WarpCoord wc = warp_coord(m, u, v, a.Ho, a.Wo, H, W);
+  const WarpCoord wc = warp_coord(m, u, v + vw.row0, a.Ho, a.Wo, H, W);
   const float ix = wc.ix, iy = wc.iy;
   const bool finite = wc.finite, inside = wc.inside;
   const float fill = finite ? 0.f : __builtin_nanf("");
@@ -121,6 +121,14 @@ __global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_tile_kernel(const Warp
           const int c = (g0 + k) * 8 + j;
           vals[k][j] = c < c_end ? (inside ? sample(c) : fill) : 0.f;
         }
+      if (a.nonfinite) {  // the non-finite report (ABI 11900; as the fused warps', wino_rows_phase2)
+        float sum = 0.f;
+#pragma unroll
+        for (int k = 0; k < GU; ++k)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) sum += vals[k][j];
+        if (!isfinite(sum)) *a.nonfinite = a.nf_tag;
+      }
 #pragma unroll
       for (int k = 0; k < GU; ++k)
         if ((g0 + k) * 8 < c_end) store_split8(out + (g0 + k) * dG, vals[k]);
@@ -467,7 +475,7 @@ static int finish_args_and_launch(WarpArgs& a, int64_t B, int64_t C, int64_t H, 
                                   int64_t Ho, int64_t Wo, void* stream, bool split = false) {
   a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
   a.tiles_x = (int)ceil_div(Wo, kWarpTW);
-  a.tiles = a.tiles_x * (int)ceil_div(Ho, kWarpTH);
+  a.tiles = a.tiles_x * (int)ceil_div(a.out_rows ? a.out_rows : Ho, kWarpTH);
   a.chunks = (int)ceil_div(C, kWarpCPB);
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
 #ifndef MVBEV_WARP_PAIR
@@ -503,11 +511,17 @@ static int warp_single(const void* src, int64_t B, int64_t C, int64_t H, int64_t
 
 template <typename T>
 static int warp_views(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t H,
-                      int64_t W, int64_t Ho, int64_t Wo, void* stream, bool split = false, int flags = 0) {
+                      int64_t W, int64_t Ho, int64_t Wo, void* stream, bool split = false, int flags = 0,
+                      const int32_t* row0s = nullptr, int64_t out_rows = 0, int32_t* nonfinite = nullptr,
+                      int32_t nf_tag = 0) {
   if (!views) return MVBEV_ERR_NULL;
   const int st = check_sizes(B, C, H, W, Ho, Wo, nviews);
   if (st != MVBEV_OK) return st;
+  if (out_rows < 0 || out_rows > Ho) return MVBEV_ERR_SHAPE;
   WarpArgs a = {};
+  a.out_rows = (int)out_rows;
+  a.nonfinite = nonfinite;
+  a.nf_tag = nf_tag;
   for (int i = 0; i < nviews; ++i) {
     const mvbev_warp_view& s = views[i];
     if (!s.src || !s.dst) return MVBEV_ERR_NULL;
@@ -518,6 +532,8 @@ static int warp_views(const mvbev_warp_view* views, int nviews, int64_t B, int64
     d.dst = s.dst; d.dB = s.dst_strides[0]; d.dC = s.dst_strides[1]; d.dH = s.dst_strides[2];
     d.m_dev = nullptr;
     for (int k = 0; k < 9; ++k) d.m[k] = s.m[k];
+    d.row0 = row0s ? row0s[i] : 0;
+    if (d.row0 < 0 || d.row0 + (out_rows ? out_rows : Ho) > Ho) return MVBEV_ERR_SHAPE;
   }
   a.nviews = nviews;
   a.skip_zero = (flags & MVBEV_WARP_DST_ZEROED) != 0;
@@ -587,9 +603,30 @@ __global__ void coord_map_kernel(float* dst, int64_t dB, int64_t dC, int64_t dH,
   o[dC] = (float)((double)v / (double)(Ho - 1) * 2.0 - 1.0);
 }
 
+// a gated zero fill (ABI 11900): 16-B stores over n16 units when *gate == tag, else nothing — the band
+// exchange's send chunks after a frame whose exact path overwrote them (they are zero-filled once and
+// then written only by the window warps with MVBEV_WARP_DST_ZEROED)
+__global__ __launch_bounds__(256) void zero_gated_kernel(u32x4_t* dst, int64_t n16, const int32_t* gate, int32_t tag) {
+  if (*gate != tag) return;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = u32x4_t{0u, 0u, 0u, 0u};
+}
+
 }  // namespace mvbev
 
 extern "C" {
+
+int mvbev_zero_gated(void* dst, int64_t bytes, const int32_t* gate, int32_t gate_tag, void* stream) {
+  using namespace mvbev;
+  if (!dst || !gate) return MVBEV_ERR_NULL;
+  if (bytes <= 0) return MVBEV_ERR_RANK;
+  if (bytes % 16 || (reinterpret_cast<uintptr_t>(dst) & 15)) return MVBEV_ERR_ALIGN;
+  const int64_t n16 = bytes / 16;
+  hipLaunchKernelGGL(zero_gated_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n16, 256), 4096)), dim3(256), 0,
+                     as_stream(stream), static_cast<u32x4_t*>(dst), n16, gate, gate_tag);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
 
 const char* mvbev_status_string(int s) {
   switch (s) {
@@ -605,7 +642,7 @@ const char* mvbev_status_string(int s) {
   }
 }
 
-int mvbev_version(void) { return 11800; }
+int mvbev_version(void) { return 11900; }
 
 int mvbev_warp_perspective_f32(const float* src, int64_t B, int64_t C, int64_t H, int64_t W,
                                const int64_t src_strides[4], const float* m, float* dst,
@@ -635,6 +672,19 @@ int mvbev_warp_views_split_bf16_ex(const mvbev_warp_view* views, int nviews, int
   if (src_is_f16)
     return mvbev::warp_views<__half>(views, nviews, B, C, H, W, Ho, Wo, stream, true, flags);
   return mvbev::warp_views<float>(views, nviews, B, C, H, W, Ho, Wo, stream, true, flags);
+}
+
+int mvbev_warp_views_split_bf16_rows(const mvbev_warp_view* views, const int32_t* row0s, int nviews, int src_is_f16,
+                                     int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
+                                     int64_t out_rows, int flags, int32_t* nonfinite, int32_t nf_tag, void* stream) {
+  if (flags & ~MVBEV_WARP_DST_ZEROED) return MVBEV_ERR_SHAPE;
+  if (!row0s) return MVBEV_ERR_NULL;
+  if (out_rows <= 0) return MVBEV_ERR_RANK;
+  if (src_is_f16)
+    return mvbev::warp_views<__half>(views, nviews, B, C, H, W, Ho, Wo, stream, true, flags, row0s, out_rows,
+                                     nonfinite, nf_tag);
+  return mvbev::warp_views<float>(views, nviews, B, C, H, W, Ho, Wo, stream, true, flags, row0s, out_rows,
+                                  nonfinite, nf_tag);
 }
 
 int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t H,

@@ -50,6 +50,7 @@ struct WarpView {
   int64_t dB, dC, dH;
   const float* m_dev;  // device [B][9] (per batch item) or nullptr -> m below
   float m[9];          // src_norm <- dst_norm, shared by every batch item
+  int row0;            // grid row of dst row 0 (a row window of the grid: warp_tile_kernel, the exact warp)
 };
 
 struct WarpArgs {
@@ -64,6 +65,9 @@ struct WarpArgs {
   int32_t nf_tag;
   const int32_t* gate;
   int32_t gate_tag;
+  // rows of each dst (a row window of the Ho-row grid starting at its view's row0; 0 = Ho):
+  // warp_tile_kernel and the exact warp (ABI 11900)
+  int out_rows;
 };
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));

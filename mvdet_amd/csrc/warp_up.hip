@@ -505,23 +505,26 @@ __global__ __launch_bounds__(kUcThreads) void warp_up_wino_cl_kernel(const UpArg
 // formed here, and a NaN / inf in the features reaches exactly the outputs it reaches in
 // persp_trans_detector.py:65-69 (the fused kernels fold the taps into one 3x3 window and cannot).
 // Plain fp32 out [B][C][Ho][Wo] at element strides; one thread per output pixel, 8 channels per
-// block; runs only when *gate == gate_tag (the fused warp's report), else exits at once.
-template <bool UP>
+// block; runs only when *gate == gate_tag (the fused warp's report), else exits at once.  Row windows
+// (ABI 11900): dst row v is grid row vw.row0 + v, a.out_rows rows (0 = Ho) — the exact path runs in row
+// bands (bounded memory) and the band exchange's windows.  T: fp32 or fp16 sources (fp32 math).
+template <bool UP, typename T>
 __global__ __launch_bounds__(256) void warp_exact_kernel(const UpArgs ua, int pix_blocks, int units) {
   const WarpArgs& a = ua.w;
   if (a.gate && *a.gate != a.gate_tag) return;  // the usual case: a few thousand workgroups exit here
+  const int orows = a.out_rows ? a.out_rows : a.Ho;
   // grid-stride over units = (b * nviews + view, 256-pixel block): one thread per output pixel, all
   // channels (the taps computed once per pixel)
   for (int unit = blockIdx.x; unit < units; unit += gridDim.x) {
     const int bv = unit / pix_blocks, p = (unit - bv * pix_blocks) * 256 + threadIdx.x;
-    if (p >= a.Ho * a.Wo) continue;
+    if (p >= orows * a.Wo) continue;
     const int view = bv % a.nviews, b = bv / a.nviews;
     const WarpView& vw = a.v[view];
     const int v = p / a.Wo, u = p - v * a.Wo;
     float m[9];
 #pragma unroll
     for (int i = 0; i < 9; ++i) m[i] = vw.m[i];
-    const WarpCoord wc = warp_coord(m, u, v, a.Ho, a.Wo, a.H, a.W);
+    const WarpCoord wc = warp_coord(m, u, v + vw.row0, a.Ho, a.Wo, a.H, a.W);
     float* out = static_cast<float*>(vw.dst) + (int64_t)b * vw.dB + (int64_t)v * vw.dH + u;
     if (!wc.inside) {
       const float fill = wc.finite ? 0.f : __builtin_nanf("");
@@ -554,18 +557,18 @@ __global__ __launch_bounds__(256) void warp_exact_kernel(const UpArgs ua, int pi
         lx[k][0] = lx[k][1] = ly[k][0] = ly[k][1] = 0.f;
       }
     }
-    const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
+    const T* base = static_cast<const T*>(vw.src) + (int64_t)b * vw.sB;
     for (int c = 0; c < a.C; ++c) {
-      const float* pc = base + (int64_t)c * vw.sC;
+      const T* pc = base + (int64_t)c * vw.sC;
       float acc = 0.f;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         float val;
         if constexpr (UP) {
-          val = (pc[off[k][0]] * lx[k][0] + pc[off[k][1]] * lx[k][1]) * ly[k][0] +
-                (pc[off[k][2]] * lx[k][0] + pc[off[k][3]] * lx[k][1]) * ly[k][1];
+          val = (to_f32<T>(pc[off[k][0]]) * lx[k][0] + to_f32<T>(pc[off[k][1]]) * lx[k][1]) * ly[k][0] +
+                (to_f32<T>(pc[off[k][2]]) * lx[k][0] + to_f32<T>(pc[off[k][3]]) * lx[k][1]) * ly[k][1];
         } else {
-          val = pc[off[k][0]];
+          val = to_f32<T>(pc[off[k][0]]);
         }
         acc += (ok[k] ? val : 0.f) * wt[k];
       }
@@ -576,15 +579,17 @@ __global__ __launch_bounds__(256) void warp_exact_kernel(const UpArgs ua, int pi
 
 }  // namespace mvbev
 
-extern "C" int mvbev_warp_views_exact_f32(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t h,
-                                          int64_t w, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
-                                          const int32_t* gate, int32_t gate_tag, void* stream) {
+static int warp_exact(const mvbev_warp_view* views, const int32_t* row0s, int nviews, int src_is_f16, int64_t B,
+                      int64_t C, int64_t h, int64_t w, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int64_t out_rows,
+                      const int32_t* gate, int32_t gate_tag, void* stream) {
   using namespace mvbev;
   if (!views) return MVBEV_ERR_NULL;
-  if (B <= 0 || C <= 0 || h <= 0 || w <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 || nviews <= 0)
+  if (B <= 0 || C <= 0 || h <= 0 || w <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 || nviews <= 0 || out_rows < 0)
     return MVBEV_ERR_RANK;
+  const int64_t orows = out_rows ? out_rows : Ho;
   if (nviews > kWarpMaxViews || B * nviews > 65535 || C > INT32_MAX || H > INT32_MAX / 2 || W > INT32_MAX / 2 ||
-      Ho * Wo > INT32_MAX - 256 || ceil_div(Ho * Wo, 256) * B * nviews > INT32_MAX || H < h || W < w)
+      Ho > INT32_MAX / 2 || orows > Ho || orows * Wo > INT32_MAX - 256 ||
+      ceil_div(orows * Wo, 256) * B * nviews > INT32_MAX || H < h || W < w)
     return MVBEV_ERR_SHAPE;
   UpArgs ua = {};
   WarpArgs& a = ua.w;
@@ -598,22 +603,45 @@ extern "C" int mvbev_warp_views_exact_f32(const mvbev_warp_view* views, int nvie
     d.dst = s.dst; d.dB = s.dst_strides[0]; d.dC = s.dst_strides[1]; d.dH = s.dst_strides[2];
     d.m_dev = nullptr;
     for (int k = 0; k < 9; ++k) d.m[k] = s.m[k];
+    d.row0 = row0s ? row0s[i] : 0;
+    if (d.row0 < 0 || d.row0 + orows > Ho) return MVBEV_ERR_SHAPE;
   }
   a.nviews = nviews;
   a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
+  a.out_rows = (int)out_rows;
   a.gate = gate;
   a.gate_tag = gate_tag;
   ua.h = (int)h; ua.sw = (int)w;
   ua.sy = (float)h / (float)H;
   ua.sx = (float)w / (float)W;
-  const int pix_blocks = (int)ceil_div(Ho * Wo, 256), units = pix_blocks * (int)(B * nviews);
+  const int pix_blocks = (int)ceil_div(orows * Wo, 256), units = pix_blocks * (int)(B * nviews);
   const dim3 grid((unsigned)std::min(units, 2048));
-  if (h == H && w == W)
-    hipLaunchKernelGGL(warp_exact_kernel<false>, grid, dim3(256), 0, as_stream(stream), ua, pix_blocks, units);
-  else
-    hipLaunchKernelGGL(warp_exact_kernel<true>, grid, dim3(256), 0, as_stream(stream), ua, pix_blocks, units);
+  const bool up = !(h == H && w == W);
+#define MVBEV_EXACT_LAUNCH(UP, T) \
+  hipLaunchKernelGGL((warp_exact_kernel<UP, T>), grid, dim3(256), 0, as_stream(stream), ua, pix_blocks, units)
+  if (src_is_f16) {
+    if (up) MVBEV_EXACT_LAUNCH(true, __half); else MVBEV_EXACT_LAUNCH(false, __half);
+  } else {
+    if (up) MVBEV_EXACT_LAUNCH(true, float); else MVBEV_EXACT_LAUNCH(false, float);
+  }
+#undef MVBEV_EXACT_LAUNCH
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
+}
+
+extern "C" int mvbev_warp_views_exact_f32(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t h,
+                                          int64_t w, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
+                                          const int32_t* gate, int32_t gate_tag, void* stream) {
+  return warp_exact(views, nullptr, nviews, 0, B, C, h, w, H, W, Ho, Wo, 0, gate, gate_tag, stream);
+}
+
+extern "C" int mvbev_warp_views_exact_rows(const mvbev_warp_view* views, const int32_t* row0s, int nviews,
+                                           int src_is_f16, int64_t B, int64_t C, int64_t h, int64_t w, int64_t H,
+                                           int64_t W, int64_t Ho, int64_t Wo, int64_t out_rows,
+                                           const int32_t* gate, int32_t gate_tag, void* stream) {
+  if (!row0s) return MVBEV_ERR_NULL;
+  if (out_rows <= 0) return MVBEV_ERR_RANK;
+  return warp_exact(views, row0s, nviews, src_is_f16, B, C, h, w, H, W, Ho, Wo, out_rows, gate, gate_tag, stream);
 }
 
 extern "C" int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,

@@ -240,13 +240,16 @@ def _gate(gate):
     return flag.data_ptr(), int(tag)
 
 
-def warp_views_exact_into(srcs, m_norms, dsts, up_hw=None, gate=None) -> None:
+def warp_views_exact_into(srcs, m_norms, dsts, up_hw=None, gate=None, row0s=None, grid_rows: Optional[int] = None) -> None:
     """The reference's own evaluation order of the warp (a5) — and, with ``up_hw``, of the 3x
     upsample feeding it (a4 + a5): ``mvbev_warp_views_exact_f32``.  Every product
     ``F.interpolate`` and ``grid_sample`` form is formed (zero weights included), so a NaN / inf in
-    ``srcs`` reaches exactly the outputs it reaches in ``persp_trans_detector.py:65-69``.  fp32
-    ``srcs[i]`` [B,C,h,w] (the warp's source, or with ``up_hw`` the backbone map), ``dsts[i]`` fp32
-    [B,C,Ho,Wo] views (innermost stride 1); ``gate`` as ``conv3x3_desc``'s (the non-finite guard)."""
+    ``srcs`` reaches exactly the outputs it reaches in ``persp_trans_detector.py:65-69``.  fp32 (or,
+    ABI 11900, fp16) ``srcs[i]`` [B,C,h,w] (the warp's source, or with ``up_hw`` the backbone map),
+    ``dsts[i]`` fp32 [B,C,rows,Wo] views (innermost stride 1); ``gate`` as ``conv3x3_desc``'s (the
+    non-finite guard).  ``row0s`` (ABI 11900, ``mvbev_warp_views_exact_rows``): ``dsts[i]`` holds the
+    ``rows`` grid rows from ``row0s[i]`` of a ``grid_rows``-row grid (row windows: the exact path in
+    bands, the band exchange's windows); default the whole grid."""
     n = len(srcs)
     if n == 0:
         return
@@ -254,20 +257,101 @@ def warp_views_exact_into(srcs, m_norms, dsts, up_hw=None, gate=None) -> None:
         raise ValueError("need 1..16 matching srcs / m_norms / dsts")
     _require_cuda(*srcs, *dsts)
     B, C, h, w = srcs[0].shape
+    dtype = srcs[0].dtype
     H, W = (h, w) if up_hw is None else (int(up_hw[0]), int(up_hw[1]))
-    Ho, Wo = dsts[0].shape[2], dsts[0].shape[3]
+    rows, Wo = dsts[0].shape[2], dsts[0].shape[3]
+    Ho = rows if grid_rows is None else int(grid_rows)
+    if row0s is None and grid_rows is not None and grid_rows != rows:
+        raise ValueError("a row window needs row0s")
     arr = (_native.WarpView * n)()
     for i, (s_, m, d) in enumerate(zip(srcs, m_norms, dsts)):
-        if tuple(s_.shape) != (B, C, h, w) or s_.dtype != torch.float32:
-            raise ValueError("all views must be fp32 [B,C,h,w] of one shape")
-        if tuple(d.shape) != (B, C, Ho, Wo) or d.dtype != torch.float32 or d.stride(3) != 1:
-            raise ValueError(f"dst must be an fp32 [{B},{C},{Ho},{Wo}] view with unit column stride")
+        if tuple(s_.shape) != (B, C, h, w) or s_.dtype != dtype or dtype not in (torch.float32, torch.float16):
+            raise ValueError("all views must be fp32 (or fp16) [B,C,h,w] of one shape and dtype")
+        if tuple(d.shape) != (B, C, rows, Wo) or d.dtype != torch.float32 or d.stride(3) != 1:
+            raise ValueError(f"dst must be an fp32 [{B},{C},{rows},{Wo}] view with unit column stride")
         mm = torch.as_tensor(m, dtype=torch.float32).reshape(9).tolist()
         arr[i] = _native.WarpView(s_.data_ptr(), (ctypes.c_int64 * 4)(*s_.stride()), d.data_ptr(),
                                   (ctypes.c_int64 * 4)(*d.stride()), (ctypes.c_float * 9)(*mm))
     gp, gt = _gate(gate)
-    st = _native.load().mvbev_warp_views_exact_f32(arr, n, B, C, h, w, H, W, Ho, Wo, gp, gt, _stream(dsts[0]))
-    _native.check(st, "mvbev_warp_views_exact_f32")
+    lib = _native.load()
+    if row0s is None and dtype == torch.float32:
+        st = lib.mvbev_warp_views_exact_f32(arr, n, B, C, h, w, H, W, Ho, Wo, gp, gt, _stream(dsts[0]))
+        _native.check(st, "mvbev_warp_views_exact_f32")
+        return
+    r0 = (ctypes.c_int32 * n)(*([0] * n if row0s is None else [int(r) for r in row0s]))
+    st = lib.mvbev_warp_views_exact_rows(arr, r0, n, int(dtype == torch.float16), B, C, h, w, H, W, Ho, Wo, rows,
+                                         gp, gt, _stream(dsts[0]))
+    _native.check(st, "mvbev_warp_views_exact_rows")
+
+
+def warp_views_split_rows_into(srcs, m_norms, dsts, row0s, grid_rows: int, dst_zeroed: bool = False,
+                               nonfinite=None) -> None:
+    """Row windows of the split-bf16 warp in ONE launch (``mvbev_warp_views_split_bf16_rows``):
+    ``dsts[i]`` (split-bf16 blocked [B, ceil(C/8), rows, Wo, 2, 8], contiguous pixels) receives the
+    ``rows`` grid rows from ``row0s[i]`` of source ``srcs[i]`` (fp32 or fp16 [B,C,H,W]) warped by the
+    host kornia matrix ``m_norms[i]`` onto the ``grid_rows``-row grid.  Entries may share a source (the
+    band exchange warps each view's window of every destination rank in one launch).  ``dst_zeroed``
+    as ``warp_views_into``'s; ``nonfinite``: ``(flag, tag)`` — the non-finite report."""
+    n = len(srcs)
+    if n == 0:
+        return
+    if not (len(m_norms) == n == len(dsts) == len(row0s)) or n > 16:
+        raise ValueError("need 1..16 matching srcs / m_norms / dsts / row0s")
+    _require_cuda(*srcs, *dsts)
+    B, C, H, W = srcs[0].shape
+    dtype = srcs[0].dtype
+    if dtype not in (torch.float32, torch.float16):
+        raise TypeError(f"unsupported dtype {dtype}")
+    rows, Wo = dsts[0].shape[2], dsts[0].shape[3]
+    want = split_shape(B, C, rows, Wo)
+    arr = (_native.WarpView * n)()
+    for i, (s_, m, d) in enumerate(zip(srcs, m_norms, dsts)):
+        if tuple(s_.shape) != (B, C, H, W) or s_.dtype != dtype:
+            raise ValueError("all views must share one shape and dtype")
+        if tuple(d.shape) != want or d.dtype != torch.bfloat16 or d.stride(5) != 1 or d.stride(4) != KC or \
+                d.stride(3) != 2 * KC:
+            raise ValueError(f"split dst must be a bf16 {want} tensor with contiguous pixels")
+        mm = torch.as_tensor(m, dtype=torch.float32).reshape(9).tolist()
+        arr[i] = _native.WarpView(s_.data_ptr(), (ctypes.c_int64 * 4)(*s_.stride()), d.data_ptr(),
+                                  (ctypes.c_int64 * 4)(d.stride(0) // 16, d.stride(1) // 16, d.stride(2) // 16, 1),
+                                  (ctypes.c_float * 9)(*mm))
+    r0 = (ctypes.c_int32 * n)(*[int(r) for r in row0s])
+    fp, ft = _gate(nonfinite)
+    st = _native.load().mvbev_warp_views_split_bf16_rows(arr, r0, n, int(dtype == torch.float16), B, C, H, W,
+                                                         int(grid_rows), Wo, rows,
+                                                         _native.WARP_DST_ZEROED if dst_zeroed else 0, fp, ft,
+                                                         _stream(dsts[0]))
+    _native.check(st, "mvbev_warp_views_split_bf16_rows")
+
+
+def bias_relu_nonfinite_(y: torch.Tensor, init: torch.Tensor, row0: int, relu: bool = True, flag=None) -> torch.Tensor:
+    """``y = relu(y + init[:, row0:row0 + rows])`` in place (NaN-preserving) for a contiguous fp32
+    [B, C, rows, W] ``y`` and the contiguous [C, H, W] ``init``; ``flag``: ``(flag, tag)`` — tag is
+    stored into the device int32 flag when a result is non-finite (``mvbev_bias_relu_nonfinite_f32``)."""
+    _require_cuda(y, init)
+    if y.dim() != 4 or y.dtype != torch.float32 or not y.is_contiguous():
+        raise ValueError("y must be a contiguous fp32 [B,C,rows,W] tensor")
+    B, C, rows, W = y.shape
+    if init.dtype != torch.float32 or not init.is_contiguous() or init.dim() != 3 or init.shape[0] != C or \
+            init.shape[2] != W:
+        raise ValueError("init must be a contiguous fp32 [C,H,W] tensor")
+    fp, ft = _gate(flag)
+    st = _native.load().mvbev_bias_relu_nonfinite_f32(y.data_ptr(), init.data_ptr(), B, C, rows, W, init.shape[1],
+                                                      int(row0), int(bool(relu)), fp, ft, _stream(y))
+    _native.check(st, "mvbev_bias_relu_nonfinite_f32")
+    return y
+
+
+def zero_gated_(t: torch.Tensor, gate) -> torch.Tensor:
+    """Zero the contiguous ``t`` when the device flag of ``gate = (flag, tag)`` holds tag
+    (``mvbev_zero_gated``), else leave it: no host sync either way."""
+    _require_cuda(t)
+    if not t.is_contiguous():
+        raise ValueError("t must be contiguous")
+    gp, gt = _gate(gate)
+    st = _native.load().mvbev_zero_gated(t.data_ptr(), t.numel() * t.element_size(), gp, gt, _stream(t))
+    _native.check(st, "mvbev_zero_gated")
+    return t
 
 
 def is_channels_last_source(x: torch.Tensor) -> bool:
@@ -503,10 +587,12 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
                  init: Optional[torch.Tensor] = None, dilation: int = 1, relu: bool = False,
                  out: Optional[torch.Tensor] = None, workspace: Optional[torch.Tensor] = None,
                  group_mask: Optional[torch.Tensor] = None, tile_order: Optional[torch.Tensor] = None,
-                 tile_space: int = _native.TILES_GRID, gate=None) -> torch.Tensor:
+                 tile_space: int = _native.TILES_GRID, gate=None, band_rows: int = 0) -> torch.Tensor:
     """Low-level form: ``x`` addressed through ``desc`` (``mvbev_conv_desc``).  ``gate`` (fp32
     conv only): ``(flag, tag)`` — the kernel runs only when the device int32 ``flag[0] == tag``
-    (the non-finite guard's path; ``warp_views_wino_rows_into``'s report).  bf16x3 only,
+    (the non-finite guard's path; ``warp_views_wino_rows_into``'s report).  ``band_rows`` (fp32 conv
+    only, ABI 11900): ``out`` is the row-banded [bands, B, cout, band_rows, W] of ``conv3x3_wino``
+    (global output row g at band g // band_rows).  bf16x3 only,
     optional: ``workspace`` — device scratch for the split-K tail
     (``conv3x3_workspace_bytes``); ``group_mask`` — per-tile active channel groups
     (``warp_tile_mask``), whose cleared groups are skipped; ``tile_order`` — with a mask,
@@ -526,7 +612,13 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
     if (x.untyped_storage().nbytes() - x.storage_offset() * x.element_size()) // unit < need:
         raise ValueError("x's storage is too small for the conv descriptor")
     y_split = out is not None and out.dtype == torch.bfloat16  # split-bf16 blocked output
-    if out is None:
+    if band_rows:
+        nb = -(-(desc.out_row0 + out_rows) // band_rows)
+        if bf16x3 or out is None or out.dim() != 5 or out.shape[0] < nb or \
+                tuple(out.shape[1:]) != (B, cout, band_rows, W) or out.dtype != torch.float32 or not out.is_contiguous():
+            raise ValueError(f"a banded out must be a contiguous fp32 [>={nb},{B},{cout},{band_rows},{W}] tensor "
+                             "of the fp32 conv")
+    elif out is None:
         out = torch.empty((B, cout, out_rows, W), dtype=torch.float32, device=x.device)
     elif y_split:
         if not bf16x3 or tuple(out.shape) != split_shape(B, cout, out_rows, W) or not out.is_contiguous():
@@ -589,9 +681,9 @@ def conv3x3_desc(x: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
         raise ValueError("group_mask needs the bf16x3 conv")
     else:
         gp, gt = _gate(gate)
-        st = lib.mvbev_conv3x3_f32(x.data_ptr(), ctypes.byref(desc), packed.data_ptr(), bp, ip, cout,
-                                   int(dilation), int(bool(relu)), out.data_ptr(), gp, gt, _stream(x))
-        _native.check(st, "mvbev_conv3x3_f32")
+        st = lib.mvbev_conv3x3_f32_ex(x.data_ptr(), ctypes.byref(desc), packed.data_ptr(), bp, ip, cout,
+                                      int(dilation), int(bool(relu)), out.data_ptr(), int(band_rows), gp, gt, _stream(x))
+        _native.check(st, "mvbev_conv3x3_f32_ex")
     return out
 
 

@@ -101,6 +101,46 @@ def _reduce_scatter(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
     dist.reduce_scatter_tensor(out, inp, op=dist.ReduceOp.SUM, group=group)
 
 
+def _all_reduce_max(t: torch.Tensor, group=None) -> None:
+    """In-place MAX over ranks (the non-finite guard's frame flag: 4 bytes)."""
+    if _staged(t, group):
+        host = t.cpu()
+        dist.all_reduce(host, op=dist.ReduceOp.MAX, group=group)
+        t.copy_(host)
+        return
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+
+
+class _FrameGuard:
+    """The non-finite guard of the exchange modes (``ViewBands``, ``ViewParallel``).  Each rank's
+    window warp reports a NaN / inf sample into its frame's int32 flag under the frame's tag (the same
+    frame counter on every rank); the exchange step first takes the MAX of the flags over the ranks
+    (4 bytes), so every rank decides alike, on the device and in stream order: when any rank's features
+    are non-finite, every rank overwrites its exchanged windows with the reference-order warp in fp32
+    (same bytes as the split-bf16 windows) and every rank's fusion runs the gated fp32-MFMA exact path
+    on them — the reference's NaN / inf pattern (``persp_trans_detector.py:65-81``); otherwise those
+    launches exit at once.  The flag never needs a reset: tags only grow (reset at wrap-around)."""
+
+    def __init__(self):
+        self.tag = 0
+
+    def next(self, fr) -> None:
+        self.tag = self.tag % 0x7FFFFFFE + 1
+        fr.tag = self.tag
+        if self.tag == 1:
+            fr.nf.zero_()
+
+    @staticmethod
+    def buffers(device):
+        return torch.zeros(1, dtype=torch.int32, device=device), torch.zeros(1, dtype=torch.int32, device=device)
+
+    @staticmethod
+    def agree(fr, group) -> tuple:
+        fr.gflag.copy_(fr.nf)
+        _all_reduce_max(fr.gflag, group)
+        return fr.gflag, fr.tag
+
+
 def _all_to_all(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group=None) -> None:
     """1-D ``out`` / ``inp`` (element counts per peer in the split lists)."""
     if _staged(out, group):
@@ -169,18 +209,35 @@ class _ViewSharded:
 
 
 class ViewParallel(_ViewSharded):
-    """Slab all-gather + row-band fusion (``--mp-mode gather``)."""
+    """Slab all-gather + row-band fusion (``--mp-mode gather``).  With the engine's non-finite guard
+    (``guard_windows``) the rank's views are warped with the non-finite report and ``_FrameGuard``'s
+    exact path runs on the gathered slab."""
 
     def __init__(self, engine_factory, proj_mats: Sequence[torch.Tensor], grid_hw: Tuple[int, int],
                  rank: int, world: int, group=None):
         super().__init__(proj_mats, grid_hw, rank, world, group)
         self.engine = engine_factory(slot_views(world, self.num_cam))
+        self.guard = bool(getattr(self.engine, "guard_windows", lambda: False)())
+        self._fg = _FrameGuard()
 
     def _make_frame(self, B, device, tag):
-        return SimpleNamespace(ws=self.engine.workspace(B, device, self._band_eff(), tag=tag))
+        fr = SimpleNamespace(ws=self.engine.workspace(B, device, self._band_eff(), tag=tag), feats=None, tag=0)
+        if self.guard:
+            fr.nf, fr.gflag = _FrameGuard.buffers(device)
+        return fr
+
+    def _slots(self, fr):
+        return [fr.ws.slab[self.engine.slot_of[v]] for v in self.my_views]
 
     def produce(self, fr, feats, map_classifier=None, mark=None) -> None:
         """Warp this rank's views into its rank-major slots."""
+        if self.guard:
+            self._fg.next(fr)
+            fr.feats = list(feats)
+            if self.my_views:
+                self.engine.warp_windows(self._slots(fr), self.my_views, fr.feats, [0] * len(self.my_views),
+                                         nonfinite=(fr.nf, fr.tag))
+            return
         if hasattr(self.engine, "warp_views"):
             self.engine.warp_views(fr.ws, self.my_views, list(feats))
         else:
@@ -188,25 +245,34 @@ class ViewParallel(_ViewSharded):
                 self.engine.warp_view(fr.ws, v, f)
 
     def exchange(self, fr) -> None:
+        if self.guard:
+            gate = _FrameGuard.agree(fr, self.group)
+            if self.my_views:
+                self.engine.warp_windows_exact(self._slots(fr), self.my_views, fr.feats, [0] * len(self.my_views), gate)
         _all_gather_inplace(fr.ws.slab, self.rank, self.world, self.group)
 
     def consume(self, fr, map_classifier, mark=None) -> torch.Tensor:
         band = self.engine.fuse(fr.ws, map_classifier, mark=mark)
+        if self.guard:
+            gate = (fr.gflag, fr.tag)
+            self.engine.fuse_exact_from_windows(fr.ws, map_classifier, band, gate)
+            self.engine.clear_windows(fr.ws.slab, gate)  # the warps skip out-of-source pixels of a zeroed slab
         if mark:
             mark("gather_map")
         return self.gather_map(band)
 
 
 class ViewBands(_ViewSharded):
-    """Row-window all-to-all + row-band fusion (the N > 1 headline, ``--mp-mode bands``).
+    """Row-window all-to-all + row-band fusion (``--mp-mode bands``).
 
     Rank p's conv1 input window is ``E = ceil(Ho/P) + 14`` rows starting at
     ``clamp(r0_p - 7, 0, Ho - E)`` (shifted inside the grid at the edges, so every window has E
-    rows and the all-to-all's chunks are equal per view).  This rank warps its views over the
-    whole grid into a local slab (``local`` engine), copies window p of each into send chunk p,
-    and ``all_to_all_single`` delivers, from every rank q, q's views' rows of this rank's window:
-    the receive buffer *is* the fusion engine's band-local slab, slots in rank-major packed order
-    (``packed_slot_views``), so conv1 reads it in place."""
+    rows and the all-to-all's chunks are equal per view).  This rank's warp writes window p of each
+    of its views straight into send chunk p (``warp_windows``: one launch, a row-window warp per
+    (destination, view) — round 5: no whole-grid local slab and no window copies), and
+    ``all_to_all_single`` delivers, from every rank q, q's views' rows of this rank's window: the
+    receive buffer *is* the fusion engine's band-local slab, slots in rank-major packed order
+    (``packed_slot_views``), so conv1 reads it in place.  Non-finite guard: ``_FrameGuard``."""
 
     def __init__(self, engine_factory, proj_mats, grid_hw, rank, world, group=None):
         super().__init__(proj_mats, grid_hw, rank, world, group)
@@ -215,9 +281,9 @@ class ViewBands(_ViewSharded):
         self.nv = [len(views_of(q, world, self.num_cam)) for q in range(world)]
         self.engine = engine_factory(packed_slot_views(world, self.num_cam))
         self.local = engine_factory(self.my_views, all_views=False) if self.my_views else None
-        if self.local is not None and hasattr(self.local, "wino_warp"):
-            self.local.wino_warp = False  # the local warp must write the slab (it is cut into windows)
-        self._local_ws = {}
+        # every rank takes part in the flag's MAX, so the decision is the fusion engine's (the same on all)
+        self.guard = bool(getattr(self.engine, "guard_windows", lambda: False)())
+        self._fg = _FrameGuard()
 
     def window(self, p: int) -> Tuple[int, int]:
         H = self.grid_hw[0]
@@ -232,36 +298,53 @@ class ViewBands(_ViewSharded):
         per_view = ws.slab[0].numel()  # elements of one view's window (the slab's slot)
         send = None
         if self.local is not None:
-            key = (str(device), B)
-            if key not in self._local_ws:
-                self._local_ws[key] = self.local.workspace(B, device)
-            lslab = self._local_ws[key].slab
-            send = torch.zeros((self.world, len(self.my_views)) + tuple(lslab.shape[1:3]) + (self.E,) +
-                               tuple(lslab.shape[4:]), dtype=lslab.dtype, device=device)
+            nm = len(self.my_views)
+            buf = self.local.window_buffer(self.world * nm, B, self.E, device)
+            send = buf.view((self.world, nm) + tuple(buf.shape[1:]))
             assert send[0, 0].numel() == per_view
-        return SimpleNamespace(ws=ws, send=send, per_view=per_view, B=B, device=device)
+        fr = SimpleNamespace(ws=ws, send=send, per_view=per_view, B=B, device=device, feats=None, tag=0)
+        if self.guard:
+            fr.nf, fr.gflag = _FrameGuard.buffers(device)
+        return fr
+
+    def _entries(self, fr):
+        """(send chunk, view, features index, window row0) of every (destination, own view)."""
+        out = []
+        for p in range(self.world):
+            lo, _ = self.window(p)
+            for j, v in enumerate(self.my_views):
+                out.append((fr.send[p, j], v, j, lo))
+        return out
 
     def produce(self, fr, feats, map_classifier=None, mark=None) -> None:
+        if self.guard:
+            self._fg.next(fr)
+        fr.feats = list(feats)
         if self.local is None:
             return
-        lws = self._local_ws[(str(fr.device), fr.B)]
-        if hasattr(self.local, "warp_views"):
-            self.local.warp_views(lws, self.my_views, list(feats))
-        else:
-            for v, f in zip(self.my_views, feats):
-                self.local.warp_view(lws, v, f)
-        for p in range(self.world):  # window p of every local view -> send chunk p
-            lo, hi = self.window(p)
-            fr.send[p].copy_(lws.slab[:, :, :, lo:hi])
+        e = self._entries(fr)
+        self.local.warp_windows([d for d, _, _, _ in e], [v for _, v, _, _ in e], [fr.feats[j] for _, _, j, _ in e],
+                                [lo for _, _, _, lo in e], nonfinite=(fr.nf, fr.tag) if self.guard else None)
 
     def exchange(self, fr) -> None:
+        gate = None
+        if self.guard:
+            gate = _FrameGuard.agree(fr, self.group)
+            if self.local is not None:
+                e = self._entries(fr)
+                self.local.warp_windows_exact([d for d, _, _, _ in e], [v for _, v, _, _ in e],
+                                              [fr.feats[j] for _, _, j, _ in e], [lo for _, _, _, lo in e], gate)
         n = fr.per_view
         inp = fr.send.reshape(-1) if fr.send is not None else fr.ws.slab.new_empty(0)
         _all_to_all(fr.ws.slab.reshape(-1), inp, [v * n for v in self.nv], [len(self.my_views) * n] * self.world,
                     self.group)
+        if gate is not None and fr.send is not None:
+            self.local.clear_windows(fr.send, gate)  # the window warps skip out-of-source pixels of zeroed chunks
 
     def consume(self, fr, map_classifier, mark=None) -> torch.Tensor:
         band = self.engine.fuse(fr.ws, map_classifier, mark=mark)
+        if self.guard:
+            self.engine.fuse_exact_from_windows(fr.ws, map_classifier, band, (fr.gflag, fr.tag))
         if mark:
             mark("gather_map")
         return self.gather_map(band)
@@ -548,7 +631,7 @@ def bench_main(args) -> None:
                 y1r = fr.ws.y1_rows
                 act_eng = vp.engine if mode != "partial" else vp._fuse_engine
                 act_rows = y1r
-        nviews = s.N if mode != "partial" else max(1, len(views_of(rank, world, s.N)))
+        nviews = s.N if mode != "partial" else max(1, len(vp.my_views))  # (balanced dealing: the rank's own views)
         rows = ho if mode == "partial" else act_rows[1] - act_rows[0]
         conv1_flop = 2.0 * s.B * rows * wo * 9 * nviews * s.C * 512
         # conv1's marks: "conv1" before its row transform (none when the fused warp wrote T), then

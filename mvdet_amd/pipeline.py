@@ -73,12 +73,19 @@ class Workspace:
     # filled by the multi-GPU band exchange (parallel.ViewBands)
     slab_rows: Tuple[int, int] = (0, 0)
     # the non-finite guard (ProjectFuse.nonfinite_guard): the fused warp stores nf_tag into nf[0] when
-    # it samples a NaN / inf feature; guard_src = (cams, feats, up_hw) of that warp, for the exact path
+    # it samples a NaN / inf feature; guard_src = {slot: (cam, feat, up_hw)} of the frame's fused warps
+    # (accumulated over the warp calls of one frame under one tag; None = no frame in flight), for the
+    # exact path
     nf: Optional[torch.Tensor] = None
     nf_tag: int = 0
-    guard_src: Optional[tuple] = None
-    g_slab: Optional[torch.Tensor] = None   # the exact path's fp32 slab [S, B, Cs, Ho, Wo] and y1
+    guard_src: Optional[dict] = None
+    # the exact path's buffers, sized for one row band of at most ProjectFuse.guard_bytes of fp32 slab:
+    # slab [S, B, Cs, rows + 14, Wo], y1 / y2 [B, 512, rows + 12 / + 8, Wo]
+    g_slab: Optional[torch.Tensor] = None
     g_y1: Optional[torch.Tensor] = None
+    g_y2: Optional[torch.Tensor] = None
+    nf2: Optional[torch.Tensor] = None   # the partial-sum mode's flag of the summed conv1 (finish_from_y1)
+    nf2_tag: int = 0
     cl_maps: Optional[list] = None          # channels-last copies of NCHW backbone maps (cl_upsample)
 
 
@@ -179,6 +186,9 @@ class ProjectFuse:
         # conv2 (exact products: inf * w stays inf, torch's NaN-preserving ReLU) and conv3 — every
         # launch gated on the flag, so with finite features they exit at once and nothing is synced.
         self.nonfinite_guard = nonfinite_guard
+        # the exact path runs in row bands whose fp32 slab holds at most this many bytes (a
+        # whole-grid fp32 slab would double the fusion's largest buffer — 10 GB at cfg3 — for a rare path)
+        self.guard_bytes = 1 << 30
         # cl_upsample (default): copy NCHW backbone maps to channels-last (mvbev_nchw_to_nhwc_f32, 16-B
         # accesses, 1/9 of the upsampled size) for the line-per-pixel fused upsample warp
         # (warp_up_wino_cl_kernel) when C % 32 == 0: copy + warp 0.36 ms vs the NCHW kernel's 0.376 at cfg2
@@ -304,13 +314,17 @@ class ProjectFuse:
         if ws.wino_t is None or ws.wino_t.numel() * 2 < need:
             ws.wino_t = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=ws.slab.device)
         nonfinite = None
-        ws.guard_src = None
         if self.nonfinite_guard:
             if ws.nf is None:
                 ws.nf = torch.zeros(1, dtype=torch.int32, device=ws.slab.device)
-            ws.nf_tag = ws.nf_tag % 0x7FFFFFFE + 1  # a fresh tag per frame: no reset of the flag needed
+            if ws.guard_src is None:  # a new frame: a fresh tag (no reset of the flag needed)
+                ws.nf_tag = ws.nf_tag % 0x7FFFFFFE + 1
+                if ws.nf_tag == 1:
+                    ws.nf.zero_()
+                ws.guard_src = {}
             nonfinite = (ws.nf, ws.nf_tag)
-            ws.guard_src = (list(cams), list(feats), up_hw)
+            for c, f in zip(cams, feats):  # the frame's views so far (one tag for all its warp calls)
+                ws.guard_src[self.slot_of[c]] = (c, f, up_hw)
         ops.warp_views_wino_rows_into(list(feats), [self.m_norm_cpu[c] for c in cams], ws.wino_t,
                                       [self.slot_of[c] for c in cams], self.Cs, self.S * self.Cs, H, W,
                                       dst_zeroed=True, up_hw=up_hw, nonfinite=nonfinite)
@@ -602,8 +616,12 @@ class ProjectFuse:
                 ops.wino_rows(ws.slab, d1, ws.wino_t, gm)
             if mark:
                 mark("conv1_wino")
-            return ops.conv3x3_wino(ws.wino_t, d1, self.pack1w.get(w1), self.mid, init=None, relu=False, out=out,
-                                    group_mask=gm, tile_order=order, band_rows=band_rows)
+            ops.conv3x3_wino(ws.wino_t, d1, self.pack1w.get(w1), self.mid, init=None, relu=False, out=out,
+                             group_mask=gm, tile_order=order, band_rows=band_rows)
+            if ws.t_from_warp and ws.guard_src is not None:
+                self._partial_exact(ws, w1, out, band_rows)
+                ws.guard_src = None  # the frame's produce step ends here
+            return out
         if ws.t_from_warp:
             raise RuntimeError("the direct conv1 reads the slab, but the fused warp wrote conv1's row transform")
         full = out if not band_rows else torch.empty((B, self.mid, H, W), dtype=torch.float32, device=out.device)
@@ -616,16 +634,116 @@ class ProjectFuse:
                 out[p, :, :, :b - a].copy_(full[:, :, a:b])
         return out
 
+    def _partial_exact(self, ws: Workspace, w1: torch.Tensor, out: torch.Tensor, band_rows: int) -> None:
+        """The non-finite guard of ``conv1_partial``, gated on the fused warp's report: the reference-order
+        warp of this engine's views into the exact path's fp32 slab and the fp32-MFMA conv1 over their
+        channels (exact products, no bias / ReLU) over the partial sums — in row bands of bounded memory,
+        written in ``out``'s layout (band-major with ``band_rows``).  Summed over the ranks, the partials
+        then carry the reference's NaN / inf pattern (``finish_from_y1`` checks the sum)."""
+        H, W = self.grid_hw
+        B, dev = ws.slab.shape[1], ws.slab.device
+        gate = (ws.nf, ws.nf_tag)
+        p1, _ = self._exact_packs()
+        chunks = self._guard_chunks(B, 0, H)
+        self._guard_buffers(ws, B, max(b - a for a, b in chunks), dev)
+        banded = out.view(1, B, self.mid, H, W) if not band_rows else out
+        for a, b in chunks:
+            s0, s1 = max(0, a - HALO_CONV1), min(H, b + HALO_CONV1)
+            x = self._exact_warp_rows(ws, B, s0, s1, gate)
+            d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * (s1 - s0) * W,
+                               batch_stride=self.Cs * (s1 - s0) * W, in_row0=s0, in_rows=s1 - s0, out_row0=a,
+                               out_rows=b - a)
+            ops.conv3x3_desc(x, d1, p1.get(w1), self.mid, dilation=1, relu=False, out=banded, gate=gate,
+                             band_rows=band_rows or H)
+
     def finish_from_y1(self, ws: Workspace, map_classifier: torch.nn.Sequential, mark=None) -> torch.Tensor:
         """``ws.y1`` holds conv1's summed channel terms (no bias) for rows ``ws.y1_rows``:
-        add the coord term (+ bias), ReLU, then conv2 and conv3 on the band."""
+        add the coord term (+ bias), ReLU, then conv2 and conv3 on the band.  With the non-finite guard
+        the add + ReLU kernel reports a non-finite y1 (the sum of the ranks' exact partials carries the
+        reference's NaN / inf pattern), and a gated fp32-MFMA conv2 (exact products) then rewrites y2
+        before conv3 reads it."""
         a1, b1 = ws.y1_rows
-        ws.y1.add_(self.coord_term(map_classifier[0])[:, a1:b1]).relu_()
-        for stage, idx, fn in (("conv2", 2, self.conv2), ("conv3", 4, self.conv3)):
-            if mark:
-                mark(stage)
-            out = fn(ws, map_classifier[idx])
-        return out
+        init = self.coord_term(map_classifier[0])
+        flag = None
+        if self.nonfinite_guard and ws.y1.dtype == torch.float32:
+            if ws.nf2 is None:
+                ws.nf2 = torch.zeros(1, dtype=torch.int32, device=ws.y1.device)
+            ws.nf2_tag = ws.nf2_tag % 0x7FFFFFFE + 1
+            if ws.nf2_tag == 1:
+                ws.nf2.zero_()
+            flag = (ws.nf2, ws.nf2_tag)
+        if ws.y1.dtype == torch.float32:
+            ops.bias_relu_nonfinite_(ws.y1, init, a1, relu=True, flag=flag)
+        else:
+            ws.y1.add_(init[:, a1:b1]).relu_()
+        if mark:
+            mark("conv2")
+        self.conv2(ws, map_classifier[2])
+        if flag is not None:  # y1 non-finite: the exact conv2 (the fast one splits inf into NaN)
+            (a2, b2), H, W = ws.y2_rows, self.grid_hw[0], self.grid_hw[1]
+            B = ws.y1.shape[0]
+            d2 = ops.conv_desc(B, self.mid, H, W, group=self.mid, group_stride=0, batch_stride=self.mid * (b1 - a1) * W,
+                               in_row0=a1, in_rows=b1 - a1, out_row0=a2, out_rows=b2 - a2)
+            ops.conv3x3_desc(ws.y1, d2, self._exact_packs()[1].get(map_classifier[2].weight), self.mid,
+                             bias=map_classifier[2].bias, dilation=2, relu=True, out=ws.y2, gate=flag)
+        if mark:
+            mark("conv3")
+        return self.conv3(ws, map_classifier[4])
+
+    # -- the band exchange / slab all-gather (parallel.ViewBands, ViewParallel) ---------------
+    def window_buffer(self, n: int, B: int, rows: int, device) -> torch.Tensor:
+        """``n`` zero-filled view windows of ``rows`` grid rows in the slab's layout (the exchange's send
+        chunks): [n, *split_shape(B, Cs, rows, Wo)] bf16 (4 bytes per element, as fp32)."""
+        W = self.grid_hw[1]
+        if self.split:
+            return torch.zeros((n,) + ops.split_shape(B, self.Cs, rows, W), dtype=torch.bfloat16, device=device)
+        return torch.zeros((n, B, self.Cs, rows, W), dtype=self.slab_dtype, device=device)
+
+    def warp_windows(self, dsts: Sequence[torch.Tensor], cams: Sequence[int], feats: Sequence[torch.Tensor],
+                     row0s: Sequence[int], nonfinite=None) -> None:
+        """a5 of ``cams[i]`` (features ``feats[i]``) for the row window of ``dsts[i]`` (``window_buffer``
+        entries, zero-filled and only written by this warp) from grid row ``row0s[i]`` — the exchange's
+        send chunks written straight by the warp (no whole-grid slab, no window copies), 16 per launch.
+        ``nonfinite``: (flag, tag) — the non-finite report."""
+        if not self.split:
+            raise ValueError("window warps write the split-bf16 slab layout")
+        H = self.grid_hw[0]
+        for i in range(0, len(dsts), 16):
+            sl = slice(i, i + 16)
+            ops.warp_views_split_rows_into(list(feats[sl]), [self.m_norm_cpu[c] for c in cams[sl]], list(dsts[sl]),
+                                           list(row0s[sl]), H, dst_zeroed=True, nonfinite=nonfinite)
+
+    def guard_windows(self) -> bool:
+        """The exchange modes can run the exact path on exchanged fp32 windows: the non-finite guard is on
+        and a window's channel planes are exactly the slab slot (Cs == C: no padding planes)."""
+        return self.nonfinite_guard and self.split and self.Cs == self.C
+
+    def warp_windows_exact(self, dsts: Sequence[torch.Tensor], cams: Sequence[int], feats: Sequence[torch.Tensor],
+                           row0s: Sequence[int], gate) -> None:
+        """The reference-order warp of the same windows as ``warp_windows``, gated on ``gate``, written as
+        fp32 [B, C, rows, Wo] over the same bytes of each ``dsts[i]`` (the exact path's exchange payload)."""
+        H = self.grid_hw[0]
+        B = feats[0].shape[0]
+        for i in range(0, len(dsts), 16):
+            sl = slice(i, i + 16)
+            xs = [d.view(-1).view(torch.float32).view(B, self.C, d.shape[2], self.grid_hw[1]) for d in dsts[sl]]
+            ops.warp_views_exact_into(list(feats[sl]), [self.m_norm_cpu[c] for c in cams[sl]], xs, gate=gate,
+                                      row0s=list(row0s[sl]), grid_rows=H)
+
+    def clear_windows(self, buf: torch.Tensor, gate) -> None:
+        """Re-zero ``buf`` (window chunks or a slab) when ``gate`` fired: the exact path wrote fp32 over
+        bytes the window warps skip (out-of-source pixels of a zero-filled buffer)."""
+        ops.zero_gated_(buf, gate)
+
+    def fuse_exact_from_windows(self, ws: Workspace, map_classifier, out: torch.Tensor, gate) -> None:
+        """The exact path on a slab whose bytes hold fp32 windows (``warp_windows_exact`` exchanged into
+        ``ws.slab``, rows ``ws.slab_rows``): the fp32-MFMA convs for ``ws.band`` into ``out``, gated."""
+        B = ws.slab.shape[1]
+        s0, s1 = ws.slab_rows
+        x = ws.slab.view(-1).view(torch.float32).view(self.S, B, self.Cs, s1 - s0, self.grid_hw[1])
+        r0, r1 = ws.band
+        self._guard_buffers(ws, B, r1 - r0, ws.slab.device, slab=False)
+        self._exact_convs(ws, map_classifier, out, gate, x, (s0, s1), r0, r1, r0)
 
     def fuse(self, ws: Workspace, map_classifier: torch.nn.Sequential, mark=None) -> torch.Tensor:
         """a7-a9 on ``ws.slab`` for the output rows ``ws.band`` → [B, 1, rows, Wo].
@@ -645,7 +763,8 @@ class ProjectFuse:
             if ws.t_from_warp and ws.guard_src is not None:
                 if mark:
                     mark("guard")
-                self._nonfinite_exact(ws, map_classifier, out)
+                self._nonfinite_exact(ws, map_classifier, out, (ws.nf, ws.nf_tag))
+                ws.guard_src = None  # the frame ends here
             return out
         for stage, idx, fn in (("conv1", 0, self.conv1), ("conv2", 2, self.conv2), ("conv3", 4, self.conv3)):
             if mark:
@@ -653,32 +772,93 @@ class ProjectFuse:
             out = fn(ws, map_classifier[idx])
         return out
 
-    def _nonfinite_exact(self, ws: Workspace, map_classifier, out: torch.Tensor) -> None:
-        """The non-finite guard's exact path (``nonfinite_guard``), every launch gated on the fused
-        warp's report ``(ws.nf, ws.nf_tag)``: the reference-order warp (+ upsample) of the same
-        features into an fp32 slab (``:65-69``), the fp32-MFMA conv1 + coord term + ReLU (``:51``), conv2
-        + ReLU (``:53``) and conv3 (``:54``) into ``out`` — the map the fast path just wrote."""
-        cams, feats, up_hw = ws.guard_src
-        H, W = self.grid_hw
-        B, dev = ws.slab.shape[1], ws.slab.device
-        if ws.g_slab is None:
-            ws.g_slab = torch.zeros((self.S, B, self.Cs, H, W), dtype=torch.float32, device=dev)
-            ws.g_y1 = torch.empty((B, self.mid, H, W), dtype=torch.float32, device=dev)
+    def _exact_packs(self):
         if self._pack1f is None:
             self._pack1f = ops.PackedConv3x3(self._chan_map, "fp32")
             self._pack2f = ops.PackedConv3x3(None, "fp32")
-        gate = (ws.nf, ws.nf_tag)
+        return self._pack1f, self._pack2f
+
+    def _guard_chunks(self, B: int, r0: int, r1: int) -> List[Tuple[int, int]]:
+        """Output row chunks of [r0, r1) whose exact-path slab window (rows + 14) fits ``guard_bytes``."""
+        per_row = self.S * B * self.Cs * self.grid_hw[1] * 4
+        n = max(12, self.guard_bytes // max(1, per_row) - 2 * 7)
+        return [(a, min(r1, a + n)) for a in range(r0, r1, n)]
+
+    def _guard_buffers(self, ws: Workspace, B: int, rows: int, dev, slab: bool = True) -> None:
+        W = self.grid_hw[1]
+        need = (self.S * B * self.Cs * (rows + 14) * W, B * self.mid * (rows + 12) * W, B * self.mid * (rows + 8) * W)
+        if slab and (ws.g_slab is None or ws.g_slab.numel() < need[0]):
+            # zero-filled once: the padding channels (Cs > C) stay 0, the warp writes the C real ones
+            ws.g_slab = torch.zeros(need[0], dtype=torch.float32, device=dev)
+        if ws.g_y1 is None or ws.g_y1.numel() < need[1]:
+            ws.g_y1 = torch.empty(need[1], dtype=torch.float32, device=dev)
+        if ws.g_y2 is None or ws.g_y2.numel() < need[2]:
+            ws.g_y2 = torch.empty(need[2], dtype=torch.float32, device=dev)
+
+    def _exact_convs(self, ws: Workspace, map_classifier, out: torch.Tensor, gate, x: torch.Tensor,
+                     x_rows: Tuple[int, int], r0: int, r1: int, out_row0: int) -> None:
+        """conv1 + coord term + ReLU, conv2 + ReLU and conv3 on the fp32-MFMA kernels (exact products, torch's
+        NaN-preserving ReLU) for map rows [r0, r1), every launch gated on ``gate``: ``x`` is the fp32 slab
+        [S, B, Cs, rows, Wo] holding grid rows ``x_rows``; ``out`` [B, 1, rows, Wo] holds map rows from
+        ``out_row0``."""
+        H, W = self.grid_hw
+        B = out.shape[0]
         c1, c2, c3 = map_classifier[0], map_classifier[2], map_classifier[4]
-        ops.warp_views_exact_into(list(feats), [self.m_norm_cpu[c] for c in cams],
-                                  [ws.g_slab[self.slot_of[c], :, :self.C] for c in cams], up_hw=up_hw, gate=gate)
-        d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * H * W,
-                           batch_stride=self.Cs * H * W)
-        ops.conv3x3_desc(ws.g_slab, d1, self._pack1f.get(c1.weight), self.mid, init=self.coord_term(c1), dilation=1,
-                         relu=True, out=ws.g_y1, gate=gate)
-        d2 = ops.conv_desc(B, self.mid, H, W, group=self.mid, group_stride=0, batch_stride=self.mid * H * W)
-        ops.conv3x3_desc(ws.g_y1, d2, self._pack2f.get(c2.weight), self.mid, bias=c2.bias, dilation=2, relu=True,
-                         out=ws.y2, gate=gate)
-        ops.conv3x3_cout1(ws.y2, c3.weight, 4, H=H, out=out, gate=gate)
+        p1, p2 = self._exact_packs()
+        (a1, b1), (a2, b2) = band_rows(r0, r1, H)
+        s0, s1 = x_rows
+        R = s1 - s0
+        y1 = ws.g_y1[:B * self.mid * (b1 - a1) * W].view(B, self.mid, b1 - a1, W)
+        y2 = ws.g_y2[:B * self.mid * (b2 - a2) * W].view(B, self.mid, b2 - a2, W)
+        d1 = ops.conv_desc(B, self.S * self.Cs, H, W, group=self.Cs, group_stride=B * self.Cs * R * W,
+                           batch_stride=self.Cs * R * W, in_row0=s0, in_rows=R, out_row0=a1, out_rows=b1 - a1)
+        ops.conv3x3_desc(x, d1, p1.get(c1.weight), self.mid, init=self.coord_term(c1), dilation=1, relu=True,
+                         out=y1, gate=gate)
+        d2 = ops.conv_desc(B, self.mid, H, W, group=self.mid, group_stride=0, batch_stride=self.mid * (b1 - a1) * W,
+                           in_row0=a1, in_rows=b1 - a1, out_row0=a2, out_rows=b2 - a2)
+        ops.conv3x3_desc(y1, d2, p2.get(c2.weight), self.mid, bias=c2.bias, dilation=2, relu=True, out=y2, gate=gate)
+        if B == 1 or (r0 == out_row0 and r1 - r0 == out.shape[2]):
+            ops.conv3x3_cout1(y2, c3.weight, 4, H=H, in_row0=a2, out_row0=r0, out_rows=r1 - r0,
+                              out=out[:, :, r0 - out_row0:r1 - out_row0], gate=gate)
+        else:  # a row chunk of B > 1 maps is not contiguous: one launch per item
+            for b in range(B):
+                ops.conv3x3_cout1(y2[b:b + 1], c3.weight, 4, H=H, in_row0=a2, out_row0=r0, out_rows=r1 - r0,
+                                  out=out[b:b + 1, :, r0 - out_row0:r1 - out_row0], gate=gate)
+
+    def _exact_warp_rows(self, ws: Workspace, B: int, s0: int, s1: int, gate) -> torch.Tensor:
+        """The reference-order warp (+ upsample) of the frame's views (``ws.guard_src``) into the exact
+        path's fp32 slab for grid rows [s0, s1), gated; returns the slab [S, B, Cs, s1 - s0, Wo]."""
+        H, W = self.grid_hw
+        x = ws.g_slab[:self.S * B * self.Cs * (s1 - s0) * W].view(self.S, B, self.Cs, s1 - s0, W)
+        if self.Cs != self.C:  # padding channels meet zero weights: keep them 0 (the buffer is reused at other shapes)
+            x[:, :, self.C:].zero_()
+        groups = {}
+        for slot, (cam, feat, up_hw) in ws.guard_src.items():
+            groups.setdefault((up_hw, feat.dtype, tuple(feat.shape)), []).append((slot, cam, feat))
+        for (up_hw, _, _), items in groups.items():
+            for i in range(0, len(items), 16):
+                part = items[i:i + 16]
+                ops.warp_views_exact_into([f for _, _, f in part], [self.m_norm_cpu[c] for _, c, _ in part],
+                                          [x[slot, :, :self.C] for slot, _, _ in part], up_hw=up_hw, gate=gate,
+                                          row0s=[s0] * len(part), grid_rows=H)
+        return x
+
+    def _nonfinite_exact(self, ws: Workspace, map_classifier, out: torch.Tensor, gate) -> None:
+        """The non-finite guard's exact path (``nonfinite_guard``), every launch gated on the fused warp's
+        report ``gate`` = (flag, tag): the reference-order warp (+ upsample) of the same features into an
+        fp32 slab (``:65-69``), the fp32-MFMA conv1 + coord term + ReLU (``:51``), conv2 + ReLU (``:53``) and
+        conv3 (``:54``) into ``out`` — the map the fast path just wrote.  In row bands of at most
+        ``guard_bytes`` of slab (each band's convs read its rows +- 7)."""
+        H, W = self.grid_hw
+        B, dev = ws.slab.shape[1], ws.slab.device
+        r0, r1 = ws.band
+        chunks = self._guard_chunks(B, r0, r1)
+        self._guard_buffers(ws, B, max(b - a for a, b in chunks), dev)
+        for a, b in chunks:
+            (a1, b1), _ = band_rows(a, b, H)
+            s0, s1 = max(0, a1 - HALO_CONV1), min(H, b1 + HALO_CONV1)
+            x = self._exact_warp_rows(ws, B, s0, s1, gate)
+            self._exact_convs(ws, map_classifier, out, gate, x, (s0, s1), a, b, r0)
 
     def project_fuse(self, feats: Sequence[torch.Tensor], map_classifier) -> torch.Tensor:
         """Whole hot path on one device: warp every view, concat (zero-copy), fuse."""

@@ -79,6 +79,15 @@ class OracleEngine:
         Y2[:, :, a2:b2] = y2[:, :, a2:b2]
         return F.conv2d(Y2, p["map_classifier.4.weight"], None, padding=4, dilation=4)[:, :, r0:r1]
 
+    # band exchange: the view windows written straight into the send chunks
+    def window_buffer(self, n, B, rows, device):
+        return torch.zeros(n, B, self.C, rows, self.grid_hw[1])
+
+    def warp_windows(self, dsts, cams, feats, row0s, nonfinite=None):
+        for d, v, f, r0 in zip(dsts, cams, feats, row0s):
+            M = torch.as_tensor(np.asarray(self.pm[v])).reshape(1, 3, 3).repeat(f.shape[0], 1, 1).float()
+            d.copy_(kornia_warp.warp_perspective(f, M, list(self.grid_hw))[:, :, r0:r0 + d.shape[2]])
+
     def warp_view(self, ws, v, feat):
         B = feat.shape[0]
         M = torch.as_tensor(np.asarray(self.pm[v])).reshape(1, 3, 3).repeat(B, 1, 1).float()

@@ -140,3 +140,36 @@ def test_nonfinite_features_through_the_engine_from_upsampled_maps(layout):
             eng.nonfinite_guard = True
         torch.cuda.synchronize()
     assert not torch.equal(torch.isnan(fast.cpu()), torch.isnan(ref))
+
+
+def test_nonfinite_guard_two_warp_calls_one_frame_and_row_bands():
+    """a frame whose views are warped in two ``warp_views`` calls (the T slots add up) with a NaN
+    / inf in the FIRST call's view — one tag per frame, the exact path warps every view of the frame — and
+    the exact path in several row bands (``guard_bytes`` = 0: 12-row chunks, each band's convs reading its
+    rows +- 7), B = 2: map_result with the reference's NaN / inf pattern."""
+    from mvdet_amd import ProjectFuse, synthetic
+    from mvdet_amd.geometry import projection_matrices
+    C = 64
+    ds, params = _rig(C, seed=4)
+    N, B = ds.num_cam, 2
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    pm = projection_matrices(ds)
+    mc = _mc(C, N, params)
+    eng = ProjectFuse(pm, up, grid, C)
+    eng.guard_bytes = 0
+    assert len(eng._guard_chunks(B, 0, grid[0])) > 1
+    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=600 + v, device=DEV) for v in range(N)]
+    feats[0][1, 4, up[0] // 2, up[1] // 2] = float("inf")
+    feats[0][0, 9, up[0] // 2 - 6, up[1] // 2 + 3] = float("nan")
+    with torch.no_grad():
+        ws = eng.workspace(B, DEV)
+        eng.warp_views(ws, [0], feats[:1])
+        tag = ws.nf_tag
+        eng.warp_views(ws, [1, 2], feats[1:])
+        assert ws.nf_tag == tag and sorted(ws.guard_src) == [0, 1, 2]
+        got = eng.fuse(ws, mc).clone()
+        assert int(ws.nf.item()) == tag and ws.guard_src is None
+        ref = cpu_path.project_fuse([f.cpu() for f in feats], [M.numpy() for M in pm], grid,
+                                    {k: torch.from_numpy(v) for k, v in params.items()})
+    _check_discriminates(ref)
+    assert_parity_t(got, ref, "two warp calls, banded exact path (NaN / inf pattern included)")

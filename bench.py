@@ -137,9 +137,10 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
     pm = projection_matrices(ds)
     params = head_params(N, seed=config, C=C)
     mc = build_mc(C, N, params, dev)
-    half = config == 4
+    half = config == 4  # fp16 features (BASELINE configs[3]); round 5: read by the fused warp + B^T (fp32 math,
+    # split-bf16 T) like fp32 ones — no fp16 slab (the fp32-MFMA alt precision keeps an fp16 slab)
     eng = ProjectFuse(pm, up, (ho, wo), C, precision=precision,
-                      slab_dtype=torch.float16 if half else torch.float32,
+                      slab_dtype=torch.float16 if half and precision == "fp32" else torch.float32,
                       wino_conv1=args.conv1 == "wino" and precision == "bf16x3",
                       wino_conv2=args.conv1 == "wino" and precision == "bf16x3")
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=1000 * config + v,
@@ -193,11 +194,11 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
     # 2 coord channels are folded into a per-weight-version init term)
     conv1_flop = 2.0 * B * ho * wo * 9 * (N * C) * 512
     conv2_flop = 2.0 * B * ho * wo * 9 * 512 * 512
-    s = 2 if half else 4
+    s = 2 if half else 4  # bytes per source element (fp16 features at cfg4)
     tv = [touched_footprint(M.numpy(), up, (ho, wo)) for M in pm]
-    warp_bytes = sum(s * B * C * (t + ho * wo) for t in tv)
+    warp_bytes = sum(B * C * (s * t + eng.slab_dtype.itemsize * ho * wo) for t in tv)
     if eng.wino_warp:  # the warp writes conv1's row transform: 5 split-bf16 rows per 3-row tile
-        warp_bytes = sum(4 * B * C * (t + 5 * 4 * -(-ho // 12) * wo) for t in tv)
+        warp_bytes = sum(B * C * (s * t + 4 * 5 * 4 * -(-ho // 12) * wo) for t in tv)
     # conv3's stage: with conv2 -> conv3 fused (bf16x3) it reads the [B, 8 sets, 9 taps, rows, Wo] fp32
     # partials conv2's epilogue wrote (y2 never reaches HBM) and writes the map; on a stored y2 (fp32
     # path) it reads y2's 512 channels
@@ -243,7 +244,9 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
         "dtype": DTYPE_LABEL[precision],
         "config": {"workload": f"cfg{config}: {spec['name']}", "views": N, "channels": C, "batch": B,
                    "src_hw": list(up), "grid_hw": [ho, wo], "precision": precision,
-                   "storage": "fp16" if half else "fp32", "feature_layout": layout, "parallelism": "single GPU"},
+                   "storage": ("fp16 features" + (", fp16 slab" if eng.slab_dtype == torch.float16 else
+                                                     ", fp32-math warp into a split-bf16 T") if half else "fp32"),
+                   "feature_layout": layout, "parallelism": "single GPU"},
         # achieved/frac = the MFMA work conv1 actually has to do (the frustum-masked products;
         # the skipped ones are exact zeros) over its measured time: the MFMA utilisation.
         # The reference's dense FLOP count over the same time is kept as dense_* (it reads
@@ -538,7 +541,10 @@ def main():
                          "(N=1: single GPU with a reduced-sample CPU baseline; N>1: the band exchange); 0 = skip")
     ap.add_argument("--roofline-cfg", type=int, default=5,
                     help="also run this config (BASELINE's rocprof roofline run: 8 views at 4K -> 1000 x 1000) as a "
-                         "sub-object with its roofline, no CPU baseline; 0 = skip")
+                         "sub-object with its roofline and a reduced-sample CPU baseline; 0 = skip")
+    ap.add_argument("--batch-cfg", type=int, default=4,
+                    help="also run this config (BASELINE's MultiviewX B = 8 fp16 one) as a sub-object with its "
+                         "roofline and a CPU baseline; 0 = skip")
     args = ap.parse_args()
 
     if args.gpus < 1:
@@ -590,11 +596,17 @@ def main():
     subs = []
     if args.north_star_cfg and args.north_star_cfg != args.config:
         # the size the north star quotes its >= 5x at 1 GPU on (cfg3: 7 views, 480 x 1440 grid): the same
-        # path, its roofline, and a CPU baseline on a reduced sample (1 warm-up + the median of 3 frames,
-        # ~25 s of CPU work per frame at 16 threads: BASELINE.md:26's 2 + 5 would take ~3 minutes)
-        subs.append((args.north_star_cfg, dict(frames=3, warmups=1, single_frames=0)))
+        # path, its roofline, and a CPU baseline on BASELINE.md:26's sample (2 warm-ups + the median of 5
+        # frames, ~18 s of CPU work per frame at 16 threads)
+        subs.append((args.north_star_cfg, dict(frames=5, warmups=2, single_frames=0)))
     if args.roofline_cfg and args.roofline_cfg not in (args.config, args.north_star_cfg):
-        subs.append((args.roofline_cfg, None))  # BASELINE's "rocprof roofline run" config (8 views at 4K)
+        # BASELINE's "rocprof roofline run" config (8 views at 4K): 1 warm-up + the median of 3 frames
+        # (~16 s of CPU work per frame)
+        subs.append((args.roofline_cfg, dict(frames=3, warmups=1, single_frames=0)))
+    if args.batch_cfg and args.batch_cfg not in (args.config, args.north_star_cfg, args.roofline_cfg):
+        # BASELINE configs[3]: MultiviewX 6 views, B = 8, fp16 features (C = 512, the reference's ResNet-18
+        # width); its CPU baseline on B = 1 frames (1 warm-up + the median of 3), frames/s = 1 / median
+        subs.append((args.batch_cfg, dict(frames=3, warmups=1, single_frames=0)))
     for cfg, plan in subs:
         sub = run_single(args, args.precision, max(5, args.steps // 4), 2,
                          with_cpu=plan is not None and not args.no_cpu_baseline, config=cfg, cpu_plan=plan)
@@ -604,7 +616,7 @@ def main():
         if sub.get("cpu_baseline"):
             sub["speedup_vs_cpu"] = round(sub["value"] / sub["cpu_baseline"]["value"], 1)
         else:
-            sub["cpu_baseline"] = None  # CPU sample at cfg2 / cfg3 only (bench runtime)
+            sub["cpu_baseline"] = None  # --no-cpu-baseline
         result[f"cfg{cfg}"] = sub
     if not args.no_train and args.config != 4:
         result["train_step"] = run_train_step(args.config, args.precision, max(5, args.steps // 2), 2,

@@ -108,6 +108,9 @@ int mvbev_warp_views_f32(const mvbev_warp_view* views, int nviews, int64_t B, in
  * those pixels — exactly 0 in the result — are skipped instead of rewritten.  Pixels with
  * non-finite coordinates (NaN output) are always written. */
 #define MVBEV_WARP_DST_ZEROED 1
+/* flag of mvbev_warp_views_wino_rows (ABI 11900): the sources are fp16 (fp32 math; T split-bf16 as for
+ * fp32 sources) — config 4's fp16 features on the fused warp + B^T and the row-Winograd conv1. */
+#define MVBEV_WARP_SRC_F16 2
 int mvbev_warp_views_split_bf16_ex(const mvbev_warp_view* views, int nviews, int src_is_f16,
                                    int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
                                    int flags, void* stream);
@@ -453,6 +456,8 @@ int mvbev_conv3x3_cout1_f32(const float* x, int64_t B, int64_t C, int64_t H, int
 #define MVBEV_BEV_SRC_CHANNELS_LAST 16 /* flag OR'ed into an fp32 kind (ABI 11700): views[v] hold the same
                                           tensor channels-last, [B][H][W][C] ([B][h][w][C]) contiguous, C % 32
                                           == 0 — the fused warps' line-per-pixel kernels */
+#define MVBEV_BEV_NO_GUARD 32        /* flag (ABI 11900): no non-finite guard — no guard regions in the
+                                        workspace (the guard's fp32 slab is one row chunk of at most 1 GiB) */
 typedef struct mvbev_bev_geometry {
   int32_t num_views;                /* N, 1 .. 16 (persp_trans_detector.py:58-59) */
   int32_t src_kind;                 /* MVBEV_BEV_SRC_* */
@@ -483,9 +488,11 @@ int mvbev_bev_fuse_prepare(mvbev_bev_plan* plan, const float* w1, const float* b
  * sources: the warp writes conv1's row-Winograd transform directly; fp16 sources (and geometry
  * with non-finite samples) run the direct conv1 on the split slab.  guard (fp32 sources, ABI
  * 11600): the warp reports a NaN / inf feature it samples into a device flag, and the exact path
- * (mvbev_warp_views_exact_f32 into an fp32 slab, mvbev_conv3x3_f32 twice, mvbev_conv3x3_cout1_f32,
+ * (mvbev_warp_views_exact_rows into an fp32 slab window, mvbev_conv3x3_f32 twice, mvbev_conv3x3_cout1_f32,
  * each gated on that flag) rewrites the map with the reference's NaN / inf pattern — decided on the
- * device, no host sync; four launches that exit at once when the features are finite. */
+ * device, no host sync; launches that exit at once when the features are finite.  ABI 11900: in
+ * output-row chunks whose fp32 slab window holds at most 1 GiB (one chunk at configs 1, 2 and 4);
+ * MVBEV_BEV_NO_GUARD in src_kind turns the guard and its workspace regions off. */
 int mvbev_bev_fuse(const mvbev_bev_plan* plan, const void* const* views, float* map, void* workspace,
                    size_t ws_bytes, void* stream);
 

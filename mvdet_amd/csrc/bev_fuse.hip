@@ -18,6 +18,7 @@
 // sync: the decision is taken on the device).  Everything here is a sequence of the library's own C
 // entry points over one caller-owned workspace.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <vector>
@@ -59,7 +60,17 @@ mvbev_conv_desc conv2_desc(const mvbev_bev_plan* p) {
   return d;
 }
 
-int kind_of(const mvbev_bev_geometry& g) { return g.src_kind & ~MVBEV_BEV_SRC_CHANNELS_LAST; }
+int kind_of(const mvbev_bev_geometry& g) { return g.src_kind & ~(MVBEV_BEV_SRC_CHANNELS_LAST | MVBEV_BEV_NO_GUARD); }
+
+// the guard's exact path runs in output-row chunks whose fp32 slab window (rows + 14) holds at most this
+// many bytes (ABI 11900; a whole-grid fp32 slab would double the plan's largest region for a rare path)
+// (MVBEV_BEV_GUARD_BYTES in the environment overrides it at plan_init: tests exercise several chunks)
+constexpr size_t kGuardBytes = size_t(1) << 30;
+int64_t guard_chunk_rows(const mvbev_bev_geometry& g, int64_t Cs, size_t budget) {
+  const size_t per_row = (size_t)g.num_views * g.B * Cs * g.Wo * 4;
+  const int64_t n = (int64_t)(budget / per_row) - 14;
+  return std::min<int64_t>(g.Ho, std::max<int64_t>(12, n));
+}
 
 // a view's source strides: NCHW, or channels-last (MVBEV_BEV_SRC_CHANNELS_LAST) of the same [B][C][sh][sw]
 void src_strides(const mvbev_bev_geometry& g, int64_t sh, int64_t sw, int64_t (&st)[4]) {
@@ -167,11 +178,16 @@ int mvbev_bev_plan_init(const mvbev_bev_geometry* g, mvbev_bev_plan* p) {
                       (size_t)g->B * kMid * g->Ho * g->Wo * 4);
   // the non-finite guard (row-Winograd plans): flag, fp32 packs of conv1 / conv2, the fp32 slab; its y1
   // reuses R_Y1 and its y2 R_T2 (both free once the fast path's conv2 has run)
-  p->guard = p->wino;
+  p->guard = p->wino && !(g->src_kind & MVBEV_BEV_NO_GUARD);
   sz[R_GFLAG] = 4;
   sz[R_GPACK1] = p->guard ? 4 * mvbev_conv3x3_packed_floats(kMid, K) : 0;
   sz[R_GPACK2] = p->guard ? 4 * mvbev_conv3x3_packed_floats(kMid, kMid) : 0;
-  sz[R_GSLAB] = p->guard ? slab_bytes : 0;
+  // one row chunk's fp32 slab window (bounded: kGuardBytes); its y1 / y2 fit R_Y1 / R_T2
+  size_t budget = kGuardBytes;
+  if (const char* e = std::getenv("MVBEV_BEV_GUARD_BYTES")) budget = (size_t)std::strtoull(e, nullptr, 10);
+  const int64_t gr = guard_chunk_rows(*g, p->Cs, budget);
+  sz[R_GSLAB] = p->guard ? std::min(slab_bytes, (size_t)g->num_views * g->B * p->Cs * std::min<int64_t>(g->Ho, gr + 14) *
+                                                    g->Wo * 4) : 0;
   sz[R_P3] = mvbev_conv3x3_bf16x3_cout1_partials_bytes(&d2, kMid);
   size_t o = 0;
   for (int r = 0; r < R_COUNT; ++r) {
@@ -342,26 +358,49 @@ int mvbev_bev_fuse(const mvbev_bev_plan* p, const void* const* views, float* map
   }
   BEV_TRY(mvbev_cout1_reduce_partials(p3, &d2, kMid, 4, map, 0, g.Ho, stream));
   if (gflag) {  // the non-finite guard: each launch exits at once unless the warp set the flag
+    // in output-row chunks: chunk [a, b) needs y2 rows [a - 4, b + 4), y1 rows [a - 6, b + 6) and the slab's
+    // rows [a - 7, b + 7) (the dilation-1/2/4 chain, clipped to the grid)
     float* gslab = at<float>(ws, p, R_GSLAB);
-    const int64_t plane = g.Ho * g.Wo;
-    for (int s = 0; s < g.num_views; ++s) {
-      mvbev_warp_view& v = wv[s];
-      v.src = views[s];
-      const int64_t sh = backbone ? g.h : g.H, sw = backbone ? g.w : g.W;
-      src_strides(g, sh, sw, v.src_strides);
-      v.dst = gslab + (size_t)s * g.B * p->Cs * plane;
-      v.dst_strides[0] = p->Cs * plane; v.dst_strides[1] = plane; v.dst_strides[2] = g.Wo; v.dst_strides[3] = 1;
-      std::memcpy(v.m, g.m[s], sizeof(v.m));
-    }
-    BEV_TRY(mvbev_warp_views_exact_f32(wv, g.num_views, g.B, g.C, backbone ? g.h : g.H, backbone ? g.w : g.W, g.H,
-                                       g.W, g.Ho, g.Wo, gflag, 1, stream));
     float* gy1 = at<float>(ws, p, R_Y1);
     float* gy2 = at<float>(ws, p, R_T2);
-    BEV_TRY(mvbev_conv3x3_f32(gslab, &d1, at<float>(ws, p, R_GPACK1), nullptr, at<float>(ws, p, R_INIT), kMid, 1, 1,
-                              gy1, gflag, 1, stream));
-    BEV_TRY(mvbev_conv3x3_f32(gy1, &d2, at<float>(ws, p, R_GPACK2), p->b2, nullptr, kMid, 2, 1, gy2, gflag, 1,
-                              stream));
-    BEV_TRY(mvbev_conv3x3_cout1_f32(gy2, g.B, kMid, g.Ho, g.Wo, 0, g.Ho, 0, g.Ho, p->w3, 4, map, gflag, 1, stream));
+    // the chunk rows the plan sized R_GSLAB for (R rows per window: gr + 14, or the whole grid)
+    const int64_t Rw = (int64_t)((p->off[R_GSLAB + 1] - p->off[R_GSLAB]) / ((size_t)g.num_views * g.B * p->Cs * g.Wo * 4));
+    const int64_t gr = Rw >= g.Ho ? g.Ho : Rw - 14, sh = backbone ? g.h : g.H, sw = backbone ? g.w : g.W;
+    for (int64_t a = 0; a < g.Ho; a += gr) {
+      const int64_t b = std::min(g.Ho, a + gr);
+      const int64_t a2 = std::max<int64_t>(0, a - 4), b2 = std::min(g.Ho, b + 4);
+      const int64_t a1 = std::max<int64_t>(0, a2 - 2), b1 = std::min(g.Ho, b2 + 2);
+      // every chunk's window has the same R rows (shifted inside the grid at the bottom), so the slab's
+      // padding channels (Cs > C: zero weights) stay the zeros prepare wrote — a stale value there could be
+      // an inf from another chunk's real channels, and 0 * inf is NaN
+      const int64_t R = std::min(g.Ho, Rw);
+      const int64_t s0 = std::min(std::max<int64_t>(0, a1 - 1), g.Ho - R);
+      const int64_t plane = R * g.Wo;
+      int32_t row0s[MVBEV_BEV_MAX_VIEWS];
+      for (int s = 0; s < g.num_views; ++s) {
+        mvbev_warp_view& v = wv[s];
+        v.src = views[s];
+        src_strides(g, sh, sw, v.src_strides);
+        v.dst = gslab + (size_t)s * g.B * p->Cs * plane;
+        v.dst_strides[0] = p->Cs * plane; v.dst_strides[1] = plane; v.dst_strides[2] = g.Wo; v.dst_strides[3] = 1;
+        std::memcpy(v.m, g.m[s], sizeof(v.m));
+        row0s[s] = (int32_t)s0;
+      }
+      BEV_TRY(mvbev_warp_views_exact_rows(wv, row0s, g.num_views, 0, g.B, g.C, sh, sw, g.H, g.W, g.Ho, g.Wo, R, gflag,
+                                          1, stream));
+      mvbev_conv_desc e1 = d1, e2 = d2;
+      e1.group_stride = g.B * p->Cs * plane; e1.batch_stride = p->Cs * plane;
+      e1.in_row0 = s0; e1.in_rows = R; e1.out_row0 = a1; e1.out_rows = b1 - a1;
+      e2.batch_stride = kMid * (b1 - a1) * g.Wo; e2.in_row0 = a1; e2.in_rows = b1 - a1; e2.out_row0 = a2;
+      e2.out_rows = b2 - a2;
+      BEV_TRY(mvbev_conv3x3_f32(gslab, &e1, at<float>(ws, p, R_GPACK1), nullptr, at<float>(ws, p, R_INIT), kMid, 1, 1,
+                                gy1, gflag, 1, stream));
+      BEV_TRY(mvbev_conv3x3_f32(gy1, &e2, at<float>(ws, p, R_GPACK2), p->b2, nullptr, kMid, 2, 1, gy2, gflag, 1,
+                                stream));
+      for (int64_t bi = 0; bi < g.B; ++bi)  // (a row chunk of a B > 1 map is not one contiguous block)
+        BEV_TRY(mvbev_conv3x3_cout1_f32(gy2 + bi * kMid * (b2 - a2) * g.Wo, 1, kMid, g.Ho, g.Wo, a2, b2 - a2, a, b - a,
+                                        p->w3, 4, map + (bi * g.Ho + a) * g.Wo, gflag, 1, stream));
+    }
   }
   return MVBEV_OK;
 }

@@ -170,8 +170,9 @@ __global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_tile_kernel(const Warp
 #endif
 constexpr int kWwStage = MVBEV_WW_STAGE;
 
-template <bool PAIR>
+template <bool PAIR, typename T = float>
 __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(const WarpArgs a, int r3_rows) {
+  static_assert(!PAIR || std::is_same<T, float>::value, "corner pairs are fp32 8-B loads");
   __shared__ __attribute__((aligned(16))) float ds[kWwRows][kWwCols][8];  // [row][col][channel]
   __shared__ unsigned char nz[kWwRows][kWwCols];
   __shared__ __attribute__((aligned(16))) float stage[kWarpCPB * (kWwStage > 0 ? kWwStage : 1)];
@@ -231,15 +232,15 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
     }
   }
   __syncthreads();
-  const float* base = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB;
-  const bool quad_ok = vw.sW == 1 && (W & 3) == 0 && (vw.sH & 3) == 0 && (vw.sC & 3) == 0 &&
-                       (reinterpret_cast<uintptr_t>(base) & 15) == 0;
+  const T* base = static_cast<const T*>(vw.src) + (int64_t)b * vw.sB;
+  const bool quad_ok = std::is_same<T, float>::value && vw.sW == 1 && (W & 3) == 0 && (vw.sH & 3) == 0 &&
+                       (vw.sC & 3) == 0 && (reinterpret_cast<uintptr_t>(base) & 15) == 0;
   const StageBox sb = stage_box_shape(box, W, quad_ok);  // 16-B staging loads where the source allows
   const int R = sb.R, Cb = sb.pitch;
   // uniform per block (the staged path needs unit column stride: the non-quad loads assume it too)
   const bool staged = kWwStage > 0 && box[1] >= 0 && vw.sW == 1 && R * Cb <= kWwStage;
   if (staged) {
-    stage_box_load<kWwThreads>(base, vw.sC, vw.sH, c_begin, c_end, sb, stage, tid);
+    stage_box_load<kWwThreads, T>(base, vw.sC, vw.sH, c_begin, c_end, sb, stage, tid);
     __syncthreads();
   }
   if (i < kWwRows) {  // phase 1: one warped pixel (8 channels) per thread
@@ -285,7 +286,7 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
 #pragma unroll
           for (int j = 0; j < 8; ++j) {  // straight-line (a short last group re-reads its last channel)
             const int ch = min(c_begin + j, c_end - 1);
-            const float* pc = base + (int64_t)ch * sC;
+            const T* pc = base + (int64_t)ch * sC;
             float vnw, vne, vsw, vse;
             if constexpr (PAIR) {
               const f32x2u_t top = *reinterpret_cast<const f32x2u_t*>(pc + o_top);
@@ -295,7 +296,7 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
               vsw = nw_lo ? bot.x : bot.y;
               vse = ne_lo ? bot.x : bot.y;
             } else {
-              vnw = pc[o_nw]; vne = pc[o_ne]; vsw = pc[o_sw]; vse = pc[o_se];
+              vnw = to_f32<T>(pc[o_nw]); vne = to_f32<T>(pc[o_ne]); vsw = to_f32<T>(pc[o_sw]); vse = to_f32<T>(pc[o_se]);
             }
             float acc = 0.f;
             acc += (ok_nw ? vnw : 0.f) * w_nw;
@@ -692,7 +693,8 @@ int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t
                                int32_t nf_tag, void* stream) {
   using namespace mvbev;
   if (!views) return MVBEV_ERR_NULL;
-  if (flags & ~MVBEV_WARP_DST_ZEROED) return MVBEV_ERR_SHAPE;
+  if (flags & ~(MVBEV_WARP_DST_ZEROED | MVBEV_WARP_SRC_F16)) return MVBEV_ERR_SHAPE;
+  const bool f16 = (flags & MVBEV_WARP_SRC_F16) != 0;
   int st = check_sizes(B, C, H, W, r3_rows, Wo, nviews);
   if (st != MVBEV_OK) return st;
   st = check_sizes(B, C, H, W, Ho, Wo, nviews);
@@ -722,7 +724,7 @@ int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t
   a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);  // 4 three-row tiles per block
   // channels-last sources (every view: unit channel stride, 16-B aligned pixels of whole 32-channel
   // groups, offsets within 31 bits) take the line-per-pixel kernel
-  bool cl = C % kWcCh == 0;
+  bool cl = C % kWcCh == 0 && !f16;
   for (int i = 0; i < nviews && cl; ++i) {
     const WarpView& d = a.v[i];
     cl = d.sC == 1 && d.sW >= C && d.sH > 0 && d.sB >= 0 && d.sW % 4 == 0 && d.sH % 4 == 0 && d.sB % 4 == 0 &&
@@ -738,6 +740,8 @@ int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t
   const dim3 grid((unsigned)a.nwg), block(cl ? kWcThreads : kWwThreads);
   if (cl)
     hipLaunchKernelGGL(warp_wino_cl_kernel, grid, block, 0, as_stream(stream), a, (int)r3_rows);
+  else if (f16)
+    hipLaunchKernelGGL((warp_wino_kernel<false, __half>), grid, block, 0, as_stream(stream), a, (int)r3_rows);
   else if (pair)
     hipLaunchKernelGGL((warp_wino_kernel<true>), grid, block, 0, as_stream(stream), a, (int)r3_rows);
   else

@@ -1,6 +1,8 @@
 // Definitions shared by the warp kernels (warp.hip, warp_up.hip); gfx950 only.
 #pragma once
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace mvbev {
@@ -254,12 +256,24 @@ __device__ inline StageBox stage_box_shape(const int (&box)[4], int W, bool quad
   sb.pitch = c1 - sb.c0;
   return sb;
 }
-// channel-major staging: stage[j][r][col]
-template <int NT>
-__device__ inline void stage_box_load(const float* __restrict__ base, int64_t sC, int64_t sH, int c_begin, int c_end,
+// channel-major staging: stage[j][r][col] (fp32; T = float or __half sources — fp16 stages one element per
+// lane, the quad path is fp32's)
+template <int NT, typename T = float>
+__device__ inline void stage_box_load(const T* __restrict__ base, int64_t sC, int64_t sH, int c_begin, int c_end,
                                       const StageBox& sb, float* __restrict__ stage, int tid) {
   const int n = sb.R * sb.pitch;
-  if (sb.quad) {
+  if constexpr (!std::is_same<T, float>::value) {
+    for (int r = tid / 32; r < sb.R; r += NT / 32)
+      for (int cc = tid % 32; cc < sb.pitch; cc += 32) {
+        float t[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          t[j] = to_f32<T>(base[(int64_t)min(c_begin + j, c_end - 1) * sC + (int64_t)(sb.r0 + r) * sH + sb.c0 + cc]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) stage[j * n + r * sb.pitch + cc] = t[j];
+      }
+    return;
+  } else if (sb.quad) {
     const int Q = sb.pitch >> 2, items = sb.R * Q;
     for (int it = tid; it < items; it += NT) {
       const int r = it / Q, q = it - r * Q;

@@ -4,9 +4,10 @@ One frame's views shard over P ranks (rank r owns views v % P == r, ``parallel.v
 the three exchange forms of ``parallel`` differ in what crosses xGMI and in how much of the
 fusion each rank repeats:
 
-* ``bands``   — every rank warps its views over the whole grid; an all-to-all delivers to rank p
-  the input rows of its output band + the 7-row halo of the dilation-1/2/4 chain (``:51-54``); each
-  rank transforms and convolves a band of ``ceil(Ho/P) + 12`` conv1 rows (12-row tiles).
+* ``bands``   — every rank warps the P row windows of its views (the input rows of each output band +
+  the 7-row halo of the dilation-1/2/4 chain, ``:51-54``) straight into its all-to-all send chunks
+  (round 5: no whole-grid slab, no window copies); the all-to-all delivers to rank p its window of
+  every view; each rank transforms and convolves a band of ``ceil(Ho/P) + 12`` conv1 rows (12-row tiles).
 * ``partial`` — every rank warps its views straight into conv1's row transform and runs conv1 over
   its OWN views' channels for the whole grid (conv1 is linear in its input channels); the
   [B, 512, Ho, Wo] fp32 partial sums are reduce-scattered by row band; conv2 / conv3 on the band.
@@ -85,6 +86,35 @@ def balanced_views(weights: Sequence[float], world: int) -> List[List[int]]:
     return [sorted(vs) for vs in out]
 
 
+def balanced_parts(weights: Sequence[float], world: int, C: int, warp_frac: float = 0.05,
+                   min_part: int = 64, gain: float = 0.02):
+    """The partial-sum mode's channel split (round 5): conv1 is linear in its input channels, so a view's
+    channels can be convolved on several ranks.  Views are cut into k equal channel parts (k = 1, 2, 4, ...
+    while the part keeps >= ``min_part`` channels) and the parts dealt by longest-processing-time, a part of
+    view v weighing (weights[v] + warp_frac) / k (its conv1 share of the frustum-active work plus its share
+    of the view's warp, ``warp_frac`` of a full view's conv1); the k with the smallest maximum rank load
+    wins, a larger k only when it lowers that load by more than ``gain`` (each part is a slot of the rank's
+    warp and conv1).  Returns (per rank the sorted (view, first channel) parts, part width); deterministic,
+    so every rank computes the same assignment."""
+    N = len(weights)
+    best = None
+    k = 1
+    while C % k == 0 and (k == 1 or C // k >= min_part):
+        items = sorted(((weights[v] + warp_frac) / k, v, j) for v in range(N) for j in range(k))
+        items.sort(key=lambda t: (-t[0], t[1], t[2]))
+        load = [0.0] * world
+        out: List[List[tuple]] = [[] for _ in range(world)]
+        for w, v, j in items:
+            r = min(range(world), key=lambda q: (load[q], q))
+            out[r].append((v, j * (C // k)))
+            load[r] += w
+        m = max(load)
+        if best is None or m < best[0] * (1.0 - gain):
+            best = (m, [sorted(ps) for ps in out], C // k)
+        k *= 2
+    return best[1], best[2]
+
+
 def _tiles(rows: int) -> int:
     return 12 * math.ceil(rows / 12)
 
@@ -118,14 +148,16 @@ def predict(N: int, C: int, grid_hw, B: int, P: int, single: Dict[str, float],
         c2 = single["conv2"] * _tiles(min(Ho, band + 8)) / rows_all
         tr = single["transform"] * E / Ho
         worst = max(worst, c1 + c2 + tr)
-    produce = vmax * w_view * 0.8 + vmax * slab_view * (1 + 14 * P / Ho) / 5e9   # slab warp + window writes
+    produce = vmax * w_view * 0.8 * P * E / Ho   # the split warp (~0.8 of the fused warp + B^T) of P windows
     out["bands"] = dict(produce=produce, exchange=a2a, consume=worst + single["conv3"] / P,
                         frame=max(produce + worst, a2a))
     # -- partial
     rs_bytes = 4.0 * B * 512 * Ho * Wo
     rs = rs_bytes * (P - 1) / P / (COLL_EFF * (P - 1) * bw) if P > 1 else 0.0
-    assign = balanced_views([float(a.mean()) for a in activity], P)  # as parallel.ViewPartialSum deals them
-    prod = max((w_view * len(vs) + conv1_band(0, Ho, vs)) if vs else 0.0 for vs in assign)
+    # as parallel.ViewPartialSum deals them: channel parts of the views (balanced_parts)
+    assign, cp = balanced_parts([float(a.mean()) for a in activity], P, C)
+    frac = cp / C
+    prod = max((sum(w_view * frac + conv1_band(0, Ho, [v]) * frac for v, _ in ps)) if ps else 0.0 for ps in assign)
     cons = single["conv2"] * _tiles(min(Ho, band + 8)) / rows_all + single["conv3"] / P
     out["partial"] = dict(produce=prod, exchange=rs, consume=cons, frame=max(prod + cons, rs))
     # -- gather

@@ -740,16 +740,19 @@ def warp_views_wino_rows_into(srcs, m_norms, t: torch.Tensor, slots, Cs: int, K:
     if Cs % KC or C > Cs:
         raise ValueError("Cs must be a multiple of 8 holding C")
     arr = (_native.WarpView * n)()
+    dtype = srcs[0].dtype
+    if dtype == torch.float16 and up_hw is not None:
+        raise TypeError("the fused upsample warp takes fp32 backbone maps")
     for i, (s_, m, slot) in enumerate(zip(srcs, m_norms, slots)):
-        if tuple(s_.shape) != (B, C, H, W) or s_.dtype != torch.float32:
-            raise ValueError("all views must be fp32 [B,C,H,W] of one shape")
+        if tuple(s_.shape) != (B, C, H, W) or s_.dtype != dtype or dtype not in (torch.float32, torch.float16):
+            raise ValueError("all views must be fp32 (or fp16: ABI 11900) [B,C,H,W] of one shape and dtype")
         mm = torch.as_tensor(m, dtype=torch.float32).reshape(9).tolist()
         arr[i].src = s_.data_ptr()
         arr[i].src_strides = _native._i64x4(*s_.stride())
         arr[i].dst = t.data_ptr() + 32 * (int(slot) * (Cs // KC)) * 5 * r3 * Wo
         arr[i].dst_strides = _native._i64x4(K8 * 5 * r3 * Wo, 5 * r3 * Wo, Wo, 1)  # 32-byte units
         arr[i].m = (ctypes.c_float * 9)(*mm)
-    flags = _native.WARP_DST_ZEROED if dst_zeroed else 0
+    flags = (_native.WARP_DST_ZEROED if dst_zeroed else 0) | (_native.WARP_SRC_F16 if dtype == torch.float16 else 0)
     fp, ft = _gate(nonfinite)
     if up_hw is not None:
         st = _native.load().mvbev_warp_views_upsampled_wino_rows(arr, n, B, C, H, W, int(up_hw[0]), int(up_hw[1]),
@@ -1414,7 +1417,8 @@ class BevFuse:
     ``mvbev_bev_fuse_prepare`` / ``mvbev_bev_fuse``, include/mvbev.h): what a non-Python caller
     binds instead of orchestrating the entry points.  ``m_norms``: per view the
     host kornia src_norm <- dst_norm matrix; ``src_kind``: ``_native.BEV_SRC_*`` (fp32 kinds may carry
-    ``_native.BEV_SRC_CHANNELS_LAST``: the views are passed channels_last)."""
+    ``_native.BEV_SRC_CHANNELS_LAST``: the views are passed channels_last; ``_native.BEV_NO_GUARD``: no
+    non-finite guard, no guard regions in the workspace)."""
 
     def __init__(self, m_norms, C: int, src_hw, grid_hw, B: int = 1, src_kind: int = 0, backbone_hw=None):
         g = _native.BevGeometry()
@@ -1482,7 +1486,7 @@ class BevFuse:
             raise RuntimeError("BevFuse.prepare(map_classifier, device) must run before the first frame")
         if len(views) != g.num_views:
             raise ValueError(f"need {g.num_views} views")
-        kind = g.src_kind & ~_native.BEV_SRC_CHANNELS_LAST
+        kind = g.src_kind & ~(_native.BEV_SRC_CHANNELS_LAST | _native.BEV_NO_GUARD)
         cl = bool(g.src_kind & _native.BEV_SRC_CHANNELS_LAST)
         backbone = kind == _native.BEV_SRC_BACKBONE_F32
         shape = (g.B, g.C, g.h, g.w) if backbone else (g.B, g.C, g.H, g.W)

@@ -42,7 +42,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
-from .mp_model import balanced_views  # noqa: F401  (re-exported: the partial-sum mode's view dealing)
+from .mp_model import balanced_parts, balanced_views  # noqa: F401  (re-exported: the partial-sum mode's dealing)
 
 # rows of the ground-plane tensor an output row of conv1 -> conv2 -> conv3 depends on, each side
 HALO_IN = 1 + 2 + 4
@@ -368,11 +368,24 @@ class ViewPartialSum(_ViewSharded):
     HALO = 6
 
     def __init__(self, engine_factory, proj_mats, grid_hw, rank, world, group=None,
-                 view_weights: Optional[Sequence[float]] = None):
+                 view_weights: Optional[Sequence[float]] = None, channels: Optional[int] = None,
+                 min_part: int = 64):
         super().__init__(proj_mats, grid_hw, rank, world, group)
-        if view_weights is not None:
+        self.my_parts, self.part_channels = None, None
+        if view_weights is not None and channels is not None:
+            # round 5: views cut into channel parts dealt by their conv1 work (mp_model.balanced_parts): the
+            # heaviest view no longer sets the rank time when P >= N.  The rank's engine takes the parts as
+            # its cameras; it needs the features of every view it holds a part of (my_views).
+            assign, cp = balanced_parts(view_weights, world, int(channels), min_part=min_part)
+            self.my_parts, self.part_channels = assign[rank], cp
+            self.my_views = sorted({v for v, _ in self.my_parts})
+        elif view_weights is not None:
             self.my_views = balanced_views(view_weights, world)[rank]
-        self.engine = engine_factory(self.my_views, all_views=False) if self.my_views else None
+        if self.my_parts is not None:
+            self.engine = (engine_factory(list(range(len(self.my_parts))), parts=self.my_parts,
+                                          part_channels=self.part_channels) if self.my_parts else None)
+        else:
+            self.engine = engine_factory(self.my_views, all_views=False) if self.my_views else None
         # a rank without views still runs the band fusion: give it an engine over view 0's
         # slot layout (its slab is never written or read) for the packed conv2 weights etc.
         self._fuse_engine = self.engine if self.engine is not None else engine_factory([0], all_views=False)
@@ -405,14 +418,32 @@ class ViewPartialSum(_ViewSharded):
             fr.stage.zero_()
             return
         lws = self._local_ws[(str(fr.device), fr.B)]
+        cams, feats = self._cameras(feats)
         if hasattr(self.engine, "warp_views"):
-            self.engine.warp_views(lws, self.my_views, list(feats))
+            self.engine.warp_views(lws, cams, feats)
         else:
-            for v, f in zip(self.my_views, feats):
+            for v, f in zip(cams, feats):
                 self.engine.warp_view(lws, v, f)
         if mark:
             mark("conv1")
         self.engine.conv1_partial(lws, map_classifier, fr.stage, mark=mark, band_rows=self.band_rows)
+
+    def _cameras(self, feats):
+        """(engine cameras, their features): the views, or with channel parts each part's channel slice
+        of its view's features (``feats[j]`` is view ``my_views[j]``)."""
+        if self.my_parts is None:
+            return list(self.my_views), list(feats)
+        idx = {v: j for j, v in enumerate(self.my_views)}
+        cp = self.part_channels
+        return (list(range(len(self.my_parts))),
+                [feats[idx[v]][:, c0:c0 + cp] for v, c0 in self.my_parts])
+
+    @property
+    def conv1_channels(self) -> int:
+        """Input channels of this rank's conv1 partial (its views', or its parts')."""
+        if self.my_parts is not None:
+            return len(self.my_parts) * self.part_channels
+        return None if self.engine is None else len(self.my_views) * self.engine.C
 
     def exchange(self, fr) -> None:
         """Reduce-scatter of the partial sums by band, then the halo rows into ``ws.y1``."""
@@ -574,9 +605,10 @@ def bench_main(args) -> None:
         grid = tuple(ds.reducedgrid_shape)
         pm = projection_matrices(ds)
         mc = build_mc(C, N, head_params(N, seed=cfg, C=C), dev)
-        half = cfg == 4
+        half = cfg == 4  # fp16 features: the fused warp / window warps read them (split-bf16 slab / T)
         fact = (lambda sv, **kw: ProjectFuse(pm, up, grid, C, slot_views=sv, precision=args.precision,
-                                             slab_dtype=torch.float16 if half else torch.float32, **kw))
+                                             slab_dtype=torch.float16 if half and args.precision == "fp32"
+                                             else torch.float32, **kw))
         return SimpleNamespace(spec=spec, B=B, C=C, N=N, up=up, grid=grid, pm=pm, mc=mc, half=half, fact=fact)
 
     def feats_for(s, views, cfg, base_seed=0):
@@ -609,8 +641,9 @@ def bench_main(args) -> None:
             else:
                 cls = {"bands": ViewBands, "gather": ViewParallel, "partial": ViewPartialSum}[mode]
                 kw = {}
-                if mode == "partial":  # views dealt by their conv1 work (the frustum-active tile fraction)
+                if mode == "partial":  # views cut into channel parts dealt by their conv1 work (frustum-active tiles)
                     kw["view_weights"] = [float(a.mean()) for a in mp_model.config_inputs(cfg)[4]]
+                    kw["channels"] = s.C
                 vp = cls(s.fact, s.pm, s.grid, rank, world, **kw)
                 feats = feats_for(s, vp.my_views, cfg)
                 pipe = FramePipeline(vp, s.B, dev)
@@ -631,9 +664,10 @@ def bench_main(args) -> None:
                 y1r = fr.ws.y1_rows
                 act_eng = vp.engine if mode != "partial" else vp._fuse_engine
                 act_rows = y1r
-        nviews = s.N if mode != "partial" else max(1, len(vp.my_views))  # (balanced dealing: the rank's own views)
+        # conv1's input channels on rank 0: every view's, or (partial) its own parts' / views'
+        nch = s.N * s.C if mode != "partial" else max(1, vp.conv1_channels or 0)
         rows = ho if mode == "partial" else act_rows[1] - act_rows[0]
-        conv1_flop = 2.0 * s.B * rows * wo * 9 * nviews * s.C * 512
+        conv1_flop = 2.0 * s.B * rows * wo * 9 * nch * 512
         # conv1's marks: "conv1" before its row transform (none when the fused warp wrote T), then
         # "conv1_wino" right before the Winograd conv kernel; the roofline is the conv kernel's, as at N = 1
         wino = bool(bf16 and "conv1_wino" in st)
@@ -653,7 +687,8 @@ def bench_main(args) -> None:
                                            "frac": round(ach / peak, 4),
                                            "basis": ("3 bf16 passes x 5/9 (row Winograd) x " if wino else
                                                      "3 bf16 passes x " if bf16 else "") +
-                                           "2*B*rows*Wo*9*(views*C)*512 over conv1's event time (dense, no mask)"}
+                                           "2*B*rows*Wo*9*(rank 0's conv1 input channels)*512 over conv1's event "
+                                           "time (dense, no mask)"}
         return res
 
     mode = getattr(args, "mp_mode", "auto")
@@ -696,9 +731,10 @@ def bench_main(args) -> None:
             # oracle on a bounded sample of the same workload, as the N = 1 line reports it
             from bench import cpu_baseline
             s0 = setup(args.config)
+            # the N = 1 line's sample (BASELINE.md:26: 2 warm-ups + the median of 5, and the one-thread figure)
             cpu = cpu_baseline(s0.spec["make"](), 1 if s0.half else s0.B, s0.C, s0.pm,
-                               head_params(s0.N, seed=args.config, C=s0.C), frames=2, config=args.config,
-                               warmups=1, single_frames=0)
+                               head_params(s0.N, seed=args.config, C=s0.C), frames=5, config=args.config,
+                               warmups=2, single_frames=3)
         rl = res.get("conv1_roofline_rank0", {})
         line = {
             "metric": "multi-view frames/sec (project+fuse)",

@@ -94,6 +94,13 @@ class ProjectFuse:
 
     ``slot_views``: which view each slab slot holds (``None`` = empty slot); default
     slot s = view s.  The multi-GPU path uses a rank-major slot order.
+
+    ``parts`` (the partial-sum multi-GPU mode's channel split, round 5): ``[(view, c0), ...]`` — this
+    engine's "cameras" are channel slices ``[c0, c0 + part_channels)`` of those views of ``channels``
+    each (conv1 is linear in its input channels, so a view's channels can be convolved on several ranks).
+    Its slots, masks, warps and T are those of ``len(parts)`` cameras of ``part_channels``; only conv1's
+    channel map (and the module's ``cin``) refer to the views: slot s channel c is module channel
+    ``view_s * channels + c0_s + c``.  Callers pass the features' channel slices as the cameras' features.
     """
 
     def __init__(self, proj_mats: Sequence[torch.Tensor], src_hw: Tuple[int, int], grid_hw: Tuple[int, int],
@@ -101,7 +108,8 @@ class ProjectFuse:
                  precision: str = "bf16x3", slab_dtype: torch.dtype = torch.float32,
                  all_views: bool = True, split_k: bool = True, frustum: bool = True, fuse_conv3: bool = True,
                  edge_strip: bool = True, wino_conv1: bool = True, wino_warp: bool = True,
-                 wino_conv2: bool = True, nonfinite_guard: bool = True, cl_upsample: bool = True):
+                 wino_conv2: bool = True, nonfinite_guard: bool = True, cl_upsample: bool = True,
+                 parts: Optional[Sequence[Tuple[int, int]]] = None, part_channels: Optional[int] = None):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":
@@ -110,13 +118,21 @@ class ProjectFuse:
         self.slab_dtype = slab_dtype
         # 3xbf16 with fp32 storage: the warp writes the pre-split bf16 hi/lo blocked slab
         self.split = precision == "bf16x3" and slab_dtype == torch.float32
+        n_views, view_ch = len(proj_mats), int(channels)
+        self.parts = None if parts is None else [(int(v), int(c0)) for v, c0 in parts]
+        if self.parts is not None:  # cameras = channel slices of views
+            if part_channels is None or not all(0 <= v < n_views and 0 <= c0 and c0 + part_channels <= view_ch
+                                                for v, c0 in self.parts):
+                raise ValueError("parts need part_channels and channel slices inside their views")
+            proj_mats = [proj_mats[v] for v, _ in self.parts]
+            channels = int(part_channels)
         self.num_cam = len(proj_mats)
         self.src_hw = (int(src_hw[0]), int(src_hw[1]))
         self.grid_hw = (int(grid_hw[0]), int(grid_hw[1]))
         self.C = int(channels)
         self.Cs = ops.padded_channels(self.C)
         self.mid = int(mid_channels)
-        self.cin = self.num_cam * self.C + 2          # conv1 input channels of the module
+        self.cin = n_views * view_ch + 2                # conv1 input channels of the module
         self.slot_views = list(range(self.num_cam)) if slot_views is None else list(slot_views)
         self.S = len(self.slot_views)
         self.slot_of = {v: s for s, v in enumerate(self.slot_views) if v is not None}
@@ -129,12 +145,15 @@ class ProjectFuse:
         self.m_norm_cpu = torch.stack([
             kornia_src_norm_from_dst_norm(M.float().reshape(1, 3, 3), self.src_hw, self.grid_hw)[0]
             for M in proj_mats])  # [N, 3, 3]
-        # conv1 weight channels, in slab order: slot s channel c -> module channel v*C + c
+        # conv1 weight channels, in slab order: slot s channel c -> module channel v*C + c (a part: its view's
+        # channel c0 + c)
         chan_map = []
         for v in self.slot_views:
+            base = None if v is None else (v * self.C if self.parts is None else
+                                           self.parts[v][0] * view_ch + self.parts[v][1])
             for c in range(self.Cs):
-                chan_map.append(v * self.C + c if (v is not None and c < self.C) else -1)
-        nc = self.num_cam * self.C
+                chan_map.append(base + c if (v is not None and c < self.C) else -1)
+        nc = n_views * view_ch
         self.pack1 = ops.PackedConv3x3(chan_map, precision)
         self.pack_coord = ops.PackedConv3x3([nc, nc + 1] + [-1] * (ops.KC - 2))  # once per weights: fp32
         self.pack2 = ops.PackedConv3x3(None, precision)
@@ -288,11 +307,14 @@ class ProjectFuse:
         reference's NaN pattern)."""
         return self.wino_conv1 and self.nonfinite_views(device) == 0
 
-    def _wino_warp_applies(self, ws: Workspace, feats) -> bool:
+    def _wino_warp_applies(self, ws: Workspace, feats, half_ok: bool = False) -> bool:
+        """The fused warp + B^T applies: inference over the whole grid, fp32 features (or, ``half_ok``:
+        fp16 ones — config 4; ABI 11900), finite geometry."""
         H = self.grid_hw[0]
+        dts = (torch.float32, torch.float16) if half_ok else (torch.float32,)
         return (self.wino_warp and not ws.store_y2 and ws.y1_rows == (0, H) and ws.slab_zeroed
-                and all(f.dtype == torch.float32 for f in feats) and self.src_hw[1] >= 2
-                and self.wino_active(ws.slab.device))
+                and all(f.dtype in dts for f in feats) and len({f.dtype for f in feats}) == 1
+                and self.src_hw[1] >= 2 and self.wino_active(ws.slab.device))
 
     def _check_warp_ws(self, ws: Workspace) -> None:
         if ws.slab_rows != (0, self.grid_hw[0]):
@@ -339,7 +361,7 @@ class ProjectFuse:
                 raise ValueError(f"view {cam}: features {tuple(f.shape)} do not match "
                                  f"[B,{self.C},{self.src_hw[0]},{self.src_hw[1]}]")
         self._check_warp_ws(ws)
-        if self._wino_warp_applies(ws, feats):
+        if self._wino_warp_applies(ws, feats, half_ok=True):
             self._warp_views_t(ws, cams, feats)
             return
         self._slab_after_t(ws, cams)

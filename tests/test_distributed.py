@@ -28,9 +28,12 @@ def _free_port():
 class OracleEngine:
     """CPU stand-in for ``pipeline.ProjectFuse`` built on the oracle (test only)."""
 
-    def __init__(self, proj_mats, src_hw, grid_hw, C, params, slot_views, all_views=True):
+    def __init__(self, proj_mats, src_hw, grid_hw, C, params, slot_views, all_views=True, parts=None,
+                 part_channels=None):
         self.pm, self.src_hw, self.grid_hw, self.C, self.params = proj_mats, src_hw, grid_hw, C, params
         self.slot_views = slot_views
+        # channel parts (ViewPartialSum's split): camera s = channels [c0, c0 + part_channels) of view v
+        self.parts, self.cp = parts, part_channels
         self.slot_of = {v: s for s, v in enumerate(slot_views) if v is not None}
         self._ws = {}
 
@@ -54,8 +57,14 @@ class OracleEngine:
         H = self.grid_hw[0]
         full = torch.zeros(ws.slab.shape[1], w1.shape[0], H, self.grid_hw[1])
         for s, v in enumerate(self.slot_views):
-            if v is not None:
+            if v is None:
+                continue
+            if self.parts is None:
                 full += torch.nn.functional.conv2d(ws.slab[s], w1[:, v * self.C:(v + 1) * self.C], padding=1)
+            else:
+                pv, c0 = self.parts[v]
+                a = pv * self.C + c0
+                full += torch.nn.functional.conv2d(ws.slab[s][:, :self.cp], w1[:, a:a + self.cp], padding=1)
         if not band_rows:
             return out.copy_(full)
         for p in range(-(-H // band_rows)):  # the band-major layout of ProjectFuse.conv1_partial
@@ -90,8 +99,9 @@ class OracleEngine:
 
     def warp_view(self, ws, v, feat):
         B = feat.shape[0]
-        M = torch.as_tensor(np.asarray(self.pm[v])).reshape(1, 3, 3).repeat(B, 1, 1).float()
-        ws.slab[self.slot_of[v]] = kornia_warp.warp_perspective(feat, M, list(self.grid_hw))
+        pv = v if self.parts is None else self.parts[v][0]
+        M = torch.as_tensor(np.asarray(self.pm[pv])).reshape(1, 3, 3).repeat(B, 1, 1).float()
+        ws.slab[self.slot_of[v], :, :feat.shape[1]] = kornia_warp.warp_perspective(feat, M, list(self.grid_hw))
 
     def fuse(self, ws, mc, mark=None):
         """The oracle convs on the slab's rows (a band-local window is exact 7 rows inside its
@@ -119,12 +129,14 @@ def _case():
 MODES = {"gather": parallel.ViewParallel, "partial": parallel.ViewPartialSum, "bands": parallel.ViewBands}
 
 
-def _worker(rank, world, port, out_dir, mode="gather", frames=1, weights=None):
+def _worker(rank, world, port, out_dir, mode="gather", frames=1, weights=None, split=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
     pm, up, grid, C, B, feats, params = _case()
     kw = {} if weights is None else {"view_weights": weights}
+    if split:  # channel parts of the views (C = 8 here: parts down to 2 channels)
+        kw.update(channels=C, min_part=2)
     vp = MODES[mode](lambda sv, **kw: OracleEngine(pm, up, grid, C, params, sv, **kw), pm, grid, rank, world, **kw)
     with torch.no_grad():
         if frames == 1:
@@ -134,7 +146,8 @@ def _worker(rank, world, port, out_dir, mode="gather", frames=1, weights=None):
             outs = [pipe.submit([(f + 1) * feats[v] for v in vp.my_views], None) for f in range(frames)]
             outs = outs[1:] + [pipe.drain(None)]
             assert pipe.drain(None) is None
-    torch.save({"outs": outs, "band": vp.band, "views": vp.my_views}, os.path.join(out_dir, f"r{rank}.pt"))
+    torch.save({"outs": outs, "band": vp.band, "views": vp.my_views, "parts": getattr(vp, "my_parts", None)},
+               os.path.join(out_dir, f"r{rank}.pt"))
     dist.destroy_process_group()
 
 
@@ -236,3 +249,27 @@ def test_partial_mode_balanced_assignment_matches_oracle(world, tmp_path):
         assigned += res["views"]
         torch.testing.assert_close(res["outs"][0], ref, rtol=1e-5, atol=1e-6)
     assert sorted(assigned) == [0, 1, 2]
+
+
+@pytest.mark.parametrize("world", [2, 4, 5])
+def test_partial_mode_channel_parts_match_oracle(world, tmp_path):
+    """The partial-sum mode with views cut into channel parts (``mp_model.balanced_parts``; world 4 and 5
+    > 3 views: every view split, a rank holding parts of several views), pipelined over 2 frames: every
+    rank's map equals the oracle's, and the parts cover every (view, channel) exactly once."""
+    weights = [0.9, 0.3, 0.6]
+    port = _free_port()
+    mp.spawn(_worker, args=(world, port, str(tmp_path), "partial", 2, weights, True), nprocs=world, join=True)
+    pm, up, grid, C, B, feats, params = _case()
+    with torch.no_grad():
+        refs = [cpu_path.project_fuse([(f + 1) * x for x in feats], pm, grid, params) for f in range(2)]
+    covered = []
+    assign, cp = parallel.balanced_parts(weights, world, C, min_part=2)
+    if world > 3:
+        assert cp < C  # the split is exercised
+    for r in range(world):
+        res = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
+        assert [tuple(p) for p in res["parts"]] == [tuple(p) for p in assign[r]]
+        covered += [(v, c) for v, c0 in res["parts"] for c in range(c0, c0 + cp)]
+        for f in range(2):
+            torch.testing.assert_close(res["outs"][f], refs[f], rtol=1e-5, atol=1e-6)
+    assert sorted(covered) == [(v, c) for v in range(3) for c in range(C)]

@@ -761,3 +761,71 @@ def test_full_size_training_step_vs_cpu_autograd():
         assert_parity_t(fg[v].grad, gfeat[v], f"cfg2 d feat view {v}")
     for k, p in mc.named_parameters():
         assert_parity_t(p.grad, gpar["map_classifier." + k], f"cfg2 d {k}")
+
+
+def test_detector_full_size_training_step_vs_cpu_autograd():
+    """VERDICT r04 missing 4: the drop-in module's OWN training path at config 2's full size — train mode,
+    backbone-resolution maps [1, 7, 512, 90, 160] (the backbone bypassed), ``project_fuse_backbone``: the
+    fused 3x upsample + warp forward and its adjoint, the Winograd convs and data gradients — vs torch-CPU
+    fp32 autograd through ``persp_trans_detector.py:61-87`` (F.interpolate, the image head, the kornia
+    warp, cat, map_classifier): the map, imgs_result, the gradient of every view's input features and of
+    every head parameter (map_classifier's 5, img_classifier's 3), within the 1e-3 gate given the GPU's
+    ReLU patterns (pre-activations within rounding of zero checked as in the small cases).  Non-finite
+    features are outside training parity."""
+    import torch.nn as nn
+    from mvdet_amd import PerspTransDetector, synthetic
+    spec = synthetic.CONFIGS[2]
+    ds = spec["make"]()
+    B, C, N = spec["B"], spec["C"], ds.num_cam
+    model = PerspTransDetector(ds)
+    params = {k: torch.from_numpy(v) for k, v in fixtures.head_params(N, 2, C=C).items()}
+    sd = model.state_dict()
+    sd.update(params)
+    model.load_state_dict(sd)
+    model.base_pt1, model.base_pt2 = nn.Identity(), nn.Identity()
+    model.train()
+    hb = [u // 3 for u in model.upsample_shape]
+    low = torch.stack([synthetic.backbone_features(B, C, hb, seed=2600 + v, device=DEV) for v in range(N)], 1)
+    x = low.clone().requires_grad_()
+    map_res, imgs_res = model(x)
+    assert type(map_res.grad_fn).__name__.startswith("ProjectFuseFunction")
+    eng = model.engine
+    assert eng.wino_active(DEV)
+    rng = np.random.default_rng(26)
+    gmap = torch.from_numpy(rng.standard_normal(map_res.shape).astype(np.float32))
+    gimg = [torch.from_numpy(rng.standard_normal(r.shape).astype(np.float32)) for r in imgs_res]
+    ws = map_res.grad_fn.ws
+    masks = ((eng.y1_fp32(ws) > 0).float().cpu(), (ws.y2 > 0).float().cpu())
+    loss = (map_res * gmap.to(DEV)).sum() + sum((r * gg.to(DEV)).sum() for r, gg in zip(imgs_res, gimg))
+    loss.backward()
+    torch.cuda.synchronize()
+    # CPU reference: persp_trans_detector.py:61-87 with the backbone bypassed
+    xr = low.cpu().requires_grad_()
+    pr = {k: v.clone().requires_grad_() for k, v in params.items()}
+    ups, imgs_ref = [], []
+    for cam in range(N):
+        up = cpu_path.upsample(xr[:, cam], model.upsample_shape)
+        h = F.relu(F.conv2d(up, pr["img_classifier.0.weight"], pr["img_classifier.0.bias"]))
+        imgs_ref.append(F.conv2d(h, pr["img_classifier.2.weight"]))
+        ups.append(up)
+    grid = tuple(model.reducedgrid_shape)
+    warped = cpu_path.warp_views(ups, [M.numpy() for M in model.proj_mats], grid)
+    xc = torch.cat(warped + [cpu_path.coord_map(*grid).repeat([B, 1, 1, 1])], 1)
+    del warped
+    pre1 = F.conv2d(xc, pr["map_classifier.0.weight"], pr["map_classifier.0.bias"], padding=1)
+    pre2 = F.conv2d(pre1 * masks[0], pr["map_classifier.2.weight"], pr["map_classifier.2.bias"], padding=2,
+                    dilation=2)
+    out = F.conv2d(pre2 * masks[1], pr["map_classifier.4.weight"], None, padding=4, dilation=4)
+    for msk, pre, what in zip(masks, (pre1, pre2), ("conv1", "conv2")):
+        flip = msk != (pre > 0).float()
+        assert flip.sum().item() <= max(2, pre.numel() // 20000), what
+        assert (pre[flip].abs() <= 1e-4 * pre.detach().abs().max()).all(), what
+    assert_parity(map_res.detach().cpu(), out.detach(), "cfg2 detector training forward map_result")
+    for v in range(N):
+        assert_parity(imgs_res[v].detach().cpu(), imgs_ref[v].detach(), f"cfg2 detector imgs_result {v}")
+    ((out * gmap).sum() + sum((r * gg).sum() for r, gg in zip(imgs_ref, gimg))).backward()
+    for v in range(N):
+        assert_parity_t(x.grad[:, v], xr.grad[:, v], f"cfg2 detector d input features view {v}")
+    for k, p in model.named_parameters():
+        if k in pr:
+            assert_parity_t(p.grad, pr[k].grad, f"cfg2 detector d {k}")

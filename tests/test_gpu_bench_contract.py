@@ -17,7 +17,8 @@ ROOT = Path(__file__).resolve().parents[1]
 def test_bench_json_line_contract():
     env = dict(os.environ, PYTHONUNBUFFERED="1")
     out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--config", "1", "--steps", "2", "--warmup", "1",
-                          "--no-train", "--no-alt", "--cpu-frames", "1", "--north-star-cfg", "2", "--roofline-cfg", "0"],
+                          "--no-train", "--no-alt", "--cpu-frames", "1", "--north-star-cfg", "2", "--roofline-cfg", "0",
+                          "--batch-cfg", "0"],
                          cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]

@@ -232,3 +232,35 @@ def test_bev_fuse_nonfinite_features_guard():
     assert_parity_t(got, ref, "bev_fuse non-finite features (NaN / inf pattern included)")
     assert torch.isfinite(fine).all()
     assert_parity_t(fine, ref_fine, "bev_fuse finite frame after a non-finite one", normwise_tol=5e-5)
+
+
+def test_bev_fuse_guard_in_row_chunks_batch2(monkeypatch):
+    """ABI 11900: the one-call guard's exact path in output-row chunks (``MVBEV_BEV_GUARD_BYTES`` small:
+    several chunks, each reading its rows +- 7 through a same-size slab window) at B = 2, fp32 sources;
+    the workspace holds one chunk's fp32 window, not a whole-grid slab; ``MVBEV_BEV_NO_GUARD`` drops the
+    guard's regions."""
+    from mvdet_amd import _native, ops, synthetic
+    ds = synthetic.wildtrack_like(3, 4, seed=6, img_shape=(216, 384), worldgrid_shape=(128, 288))
+    C, N, B = 64, 3, 2
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    pm, mc, tp = _setup(ds, C, seed=10)
+    mats = _engine_mats(pm, up, grid)
+    full = ops.BevFuse(mats, C, up, grid, B=B)
+    per_row = N * B * C * grid[1] * 4
+    monkeypatch.setenv("MVBEV_BEV_GUARD_BYTES", str(per_row * (12 + 14)))
+    bev = ops.BevFuse(mats, C, up, grid, B=B)
+    off = bev.plan.off
+    assert off[16 + 1] - off[16] < per_row * grid[0] and bev.plan.workspace_bytes < full.plan.workspace_bytes
+    noguard = ops.BevFuse(mats, C, up, grid, B=B, src_kind=_native.BEV_NO_GUARD)
+    assert noguard.plan.workspace_bytes < bev.plan.workspace_bytes and not noguard.plan.guard
+    bev.prepare(mc, DEV)
+    assert bev.wino and bev.plan.guard
+    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=40 + v, device=DEV) for v in range(N)]
+    feats[1][1, 7, up[0] // 2, up[1] // 2] = float("-inf")
+    feats[0][0, 3, up[0] // 2 + 5, up[1] // 2 - 8] = float("nan")
+    with torch.no_grad():
+        got = bev(feats).clone()
+        torch.cuda.synchronize()
+        ref = cpu_path.project_fuse([f.cpu() for f in feats], [M.numpy() for M in pm], grid, tp)
+    assert 0 < int((~torch.isfinite(ref)).sum()) < ref.numel()
+    assert_parity_t(got, ref, "bev_fuse chunked guard B=2 (NaN / inf pattern included)")

@@ -30,6 +30,12 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_MFMA_PEAK_TFS = 157.3  # MI355X_MICROARCH.md: fp32 matrix peak (spec)
 
 
+def progress(msg: str) -> None:
+    """A progress line on stderr (a long default run — the CPU baselines take minutes — keeps writing,
+    so a supervisor that watches the output does not take it for hung)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def build_mc(C, num_cam, params, device):
     mc = torch.nn.Sequential(torch.nn.Conv2d(C * num_cam + 2, 512, 3, padding=1), torch.nn.ReLU(),
                              torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
@@ -75,7 +81,9 @@ def cpu_baseline(ds, B, C, pm, params, frames: int, config: int = 2, warmups: in
     def frame(stages=None):
         t = time.perf_counter()
         cpu_path.project_fuse(feats, mats, grid, tp, timings=stages)
-        return time.perf_counter() - t
+        dt = time.perf_counter() - t
+        progress(f"cpu baseline cfg{config}: frame {dt:.2f} s ({torch.get_num_threads()} threads)")
+        return dt
 
     with torch.no_grad():
         for _ in range(warmups):
@@ -125,6 +133,7 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
     from mvdet_amd.geometry import projection_matrices, touched_footprint
 
     config = args.config if config is None else config
+    progress(f"run_single cfg{config} {precision} {layout or args.layout}")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -322,6 +331,7 @@ def run_plus_a4(args, precision, steps, warmup):
     from mvdet_amd import ProjectFuse, synthetic
     from mvdet_amd.geometry import projection_matrices
 
+    progress("plus_a4")
     dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
     spec = synthetic.CONFIGS[args.config]
     ds = spec["make"]()
@@ -399,6 +409,7 @@ def run_train_step(config: int, precision: str, steps: int, warmup: int, with_to
     own op sequence on this GPU (grid_sample + cat + nn.Conv2d under autograd, MIOpen)."""
     from mvdet_amd import ProjectFuse, autograd, synthetic
     from mvdet_amd.geometry import projection_matrices
+    progress("train_step")
     spec = synthetic.CONFIGS[config]
     ds = spec["make"]()
     B, C, N = spec["B"], spec["C"], ds.num_cam

@@ -1299,7 +1299,7 @@ constexpr int XH = 4 * NXI;                       // T rows of a 12-row workgrou
 #endif
 constexpr int NIW = MVBEV_WINO_NIW;               // DMA-issuing waves
 constexpr int NIT = 64 * NIW;
-constexpr int NWI = RUNIT / NIT;                  // weight DMAs per issuing wave per unit (3)
+constexpr int NWI = RUNIT / NIT;                  // weight DMAs per issuing wave per unit (6)
 // a unit (chunk, xi) stages its weights (3 kernel columns) and its T row of the 4 row tiles,
 // [sub][part][row tile][XW], together in one ring slot; a kernel column's taps are DIL columns
 // apart, so the row carries DIL halo columns on each side

@@ -39,11 +39,13 @@ A2A_EFF = 0.7       # all-to-all: fraction of one link per peer chunk
 # transform of every view, conv1 = the Winograd conv kernel (whole grid, frustum-masked), conv2 =
 # Winograd conv2 + conv3 partials (incl. its transform), conv3 = the partials' reduce; transform =
 # mvbev_wino_rows_split_bf16 over the whole slab (measured at cfg2 in round 2, scaled by size).
-# profiles/r04b_bench.json (cfg2 line, its cfg3 / cfg5 sub-objects; NCHW features).
+# profiles/r05d_bench.json (the cfg2 line and its cfg3 / cfg5 / cfg4 sub-objects; NCHW features; cfg4: B = 8,
+# fp16 features on the fused warp).
 SINGLE_GPU_MS: Dict[int, Dict[str, float]] = {
-    2: dict(warp=0.4855, conv1=1.4229, conv2=0.3336, conv3=0.0262, transform=0.25),
-    3: dict(warp=5.3227, conv1=21.0673, conv2=4.7547, conv3=0.1122, transform=4.0),
-    5: dict(warp=4.2809, conv1=15.1407, conv2=6.9484, conv3=0.1478, transform=2.3),
+    2: dict(warp=0.4938, conv1=1.4174, conv2=0.3354, conv3=0.0253, transform=0.25),
+    3: dict(warp=5.2145, conv1=20.3366, conv2=4.746, conv3=0.1937, transform=4.0),
+    4: dict(warp=3.3355, conv1=8.2243, conv2=2.4732, conv3=0.151, transform=1.6),
+    5: dict(warp=4.4294, conv1=15.0497, conv2=7.0832, conv3=0.1938, transform=2.3),
 }
 
 

@@ -260,6 +260,6 @@ def test_design_cost_model_table_is_current():
                          text=True, timeout=300, check=True).stdout
     rows = [ln.replace(" ms (x)", "") for ln in out.splitlines() if ln.startswith("| ")]
     design = (ROOT / "DESIGN.md").read_text()
-    assert len(rows) == 13  # header + 3 configs x 4 rank counts
+    assert len(rows) == 18  # header + 4 configs x 4 rank counts + config 4 at P = 6
     for row in rows:
         assert row in design, row

@@ -1,5 +1,5 @@
 """Print DESIGN.md §6's table: mvdet_amd.mp_model's predicted per-frame time (ms) and speed-up over
-one GPU of each view-parallel mode at configs 2, 3, 5 and P = 2, 4, 7, 8 (CPU only).
+one GPU of each view-parallel mode at configs 2-5 and P = 2, 4, 7, 8 (config 4 also at its P = 6) (CPU only).
 
     python tools/mp_cost_model.py
 """
@@ -19,7 +19,7 @@ def main():
     print("|---|---|---|---|---|---|")
     for cfg in sorted(mp_model.SINGLE_GPU_MS):
         N, C, grid, B, acts = mp_model.config_inputs(cfg)
-        for P in (2, 4, 7, 8):
+        for P in ((2, 4, 6, 7, 8) if cfg == 4 else (2, 4, 7, 8)):
             pr = mp_model.predict(N, C, grid, B, P, mp_model.SINGLE_GPU_MS[cfg], acts)
             cells = [f"{pr[m]['frame']:.2f} ({pr[m]['speedup_vs_1gpu']:.1f}x)" for m in ("bands", "partial", "gather")]
             print(f"| {cfg} | {P} | " + " | ".join(cells) + f" | {mp_model.choose_mode(cfg, P)} |")

@@ -81,6 +81,10 @@ EXPORTS = (
     "mvbev_conv3x3_f32_ex",
     "mvbev_bias_relu_nonfinite_f32",
     "mvbev_zero_gated",
+    "mvbev_wino_dy_rows_bytes",
+    "mvbev_wino_dy_rows_f32",
+    "mvbev_conv3x3_wgrad_wino_workspace_bytes",
+    "mvbev_conv3x3_wgrad_wino_bf16x3",
 )
 BEV_SRC_F32, BEV_SRC_F16, BEV_SRC_BACKBONE_F32 = 0, 1, 2  # MVBEV_BEV_SRC_*
 BEV_SRC_CHANNELS_LAST = 16  # MVBEV_BEV_SRC_CHANNELS_LAST (flag)
@@ -277,6 +281,15 @@ def _declare(lib):
                                                    _i64, ctypes.c_int, _p, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]
     lib.mvbev_split_rows_bf16.restype = ctypes.c_int
     lib.mvbev_split_rows_bf16.argtypes = [_p, _i64, _i64, _p, _p]
+    lib.mvbev_wino_dy_rows_bytes.restype = ctypes.c_size_t
+    lib.mvbev_wino_dy_rows_bytes.argtypes = [_i64, _i64, _i64, _i64]
+    lib.mvbev_wino_dy_rows_f32.restype = ctypes.c_int
+    lib.mvbev_wino_dy_rows_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _p, ctypes.c_size_t, _p]
+    lib.mvbev_conv3x3_wgrad_wino_workspace_bytes.restype = ctypes.c_size_t
+    lib.mvbev_conv3x3_wgrad_wino_workspace_bytes.argtypes = [ctypes.POINTER(ConvDesc), _i64]
+    lib.mvbev_conv3x3_wgrad_wino_bf16x3.restype = ctypes.c_int
+    lib.mvbev_conv3x3_wgrad_wino_bf16x3.argtypes = [_p, ctypes.c_size_t, ctypes.POINTER(ConvDesc), _p, ctypes.c_size_t,
+                                                    _i64, _p, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]
     lib.mvbev_conv_schedule_slot_bytes.restype = ctypes.c_size_t
     lib.mvbev_conv_schedule_slot_bytes.argtypes = []
     lib.mvbev_conv3x3_dgrad_bf16x3_sched.restype = ctypes.c_int

@@ -197,6 +197,39 @@ def _dgrad1_wino(engine: ProjectFuse, st, dy1s: torch.Tensor, w1: torch.Tensor, 
     ops.conv3x3_wino_dgrad(st.t1d, d, st.pack1t.get(w1), nc, dslab, out_mask=cm, cot_per_group=C // ops.BN)
 
 
+def _wgrad1_wino_applies(engine: ProjectFuse, ws: Workspace, dy1: torch.Tensor) -> bool:
+    """conv1's weight gradient runs row-Winograd (``_wgrad1_wino``) when the forward's conv1 did
+    (its whole-grid transform T is in ``ws.wino_t``), with whole 64-channel slot tiles."""
+    return (ws.t1_valid and ws.wino_t is not None and dy1.shape[3] % 8 == 0 and engine.Cs % 64 == 0
+            and _native.load().mvbev_version() >= 12000)
+
+
+def _wgrad1_wino(engine: ProjectFuse, st, ws: Workspace, d1, dy1: torch.Tensor, dw1: torch.Tensor) -> None:
+    """conv1's view-channel weight gradient from the forward's transform T (``ops.conv3x3_wgrad_wino``):
+    D = A-transform of dy1 (``ops.wino_dy_rows``), then per xi the T x D products over its 3 kernel
+    columns, folded with G — 5/9 of the direct form's MFMAs.  Chunk lists from the 12-row frustum
+    mask T was written under (a chunk whose T row is zero contributes exactly 0)."""
+    import ctypes
+    H, W = engine.grid_hw
+    B, dev, mid = dy1.shape[0], dy1.device, engine.mid
+    lists = None
+    m = engine.conv1_mask(dev, 0, H)
+    if m is not None:
+        if not hasattr(st, "lists_wino"):
+            st.lists_wino = {}
+        key = (str(dev), B)
+        if key not in st.lists_wino:
+            st.lists_wino[key] = ops.wgrad_wino_chunk_lists(m, engine.S, B, H, W)
+        lists = st.lists_wino[key]
+    need = int(_native.load().mvbev_conv3x3_wgrad_wino_workspace_bytes(ctypes.byref(d1), mid))
+    buf = st.wg_ws.get(str(dev))
+    if buf is None or buf.numel() * 4 < need:
+        buf = torch.empty((need + 3) // 4, dtype=torch.float32, device=dev)
+        st.wg_ws[str(dev)] = buf
+    ops.conv3x3_wgrad_wino(ws.wino_t, d1, ops.wino_dy_rows(dy1), dw1.shape[1], chan_map=engine.pack1._map_dev,
+                           dw=dw1, workspace=buf, chunk_lists=lists)
+
+
 def _wgrad_ws(st, desc, cout, device) -> torch.Tensor:
     import ctypes
     from . import _native
@@ -296,9 +329,12 @@ class ProjectFuseFunction(torch.autograd.Function):
         engine.pack1.get(w1)  # materialises the device channel map
         d1 = ops.conv_desc(B, engine.S * engine.Cs, H, W, group=engine.Cs, group_stride=B * engine.Cs * H * W,
                            batch_stride=engine.Cs * H * W)
-        ops.conv3x3_wgrad(ws.slab, d1, dy1, 1, w1.shape[1], chan_map=engine.pack1._map_dev, dw=dw1,
-                          workspace=_wgrad_ws(st, d1, mid, dev), chunk_lists=_wgrad_lists(engine, st, dev, B),
-                          dy_rows=_dy_rows(dy1, ws.slab.dtype == torch.bfloat16))
+        if _wgrad1_wino_applies(engine, ws, dy1):
+            _wgrad1_wino(engine, st, ws, d1, dy1, dw1)
+        else:
+            ops.conv3x3_wgrad(ws.slab, d1, dy1, 1, w1.shape[1], chan_map=engine.pack1._map_dev, dw=dw1,
+                              workspace=_wgrad_ws(st, d1, mid, dev), chunk_lists=_wgrad_lists(engine, st, dev, B),
+                              dy_rows=_dy_rows(dy1, ws.slab.dtype == torch.bfloat16))
         grads = [None] * n
         if need_feat:
             _mark("bwd_conv1_dgrad")

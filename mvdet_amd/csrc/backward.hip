@@ -310,8 +310,8 @@ constexpr int WG_AENT = MT * PX / 4;  // A entries (16 B) per buffer: 1024
 #define MVBEV_WGRAD_DMAW 8  // 4 measured equal (2.41 vs 2.42 ms) at 16 more VGPRs; 2: 3.45 ms
 #endif
 constexpr int WG_MAXC = 2048;         // chunk ids of a workgroup's partition, staged in LDS
-template <int DIL> struct WgGeo {
-  static constexpr int XW = PX + 2 * DIL, BPIX = 3 * XW;
+template <int DIL, int ROWS = 3> struct WgGeo {
+  static constexpr int XW = PX + 2 * DIL, BPIX = ROWS * XW;
   static constexpr int RUN = 2 * BPIX;                      // entries of one (h, g) run
   static constexpr int GS = (RUN + 9 + 15) / 16 * 16;       // run stride (entries, 0 mod 16)
   static constexpr int BENT = 8 * GS;
@@ -357,10 +357,27 @@ constexpr std::integer_sequence<int, (B + U)...> offset_seq(std::integer_sequenc
   return {};
 }
 
-template <int DIL>
-__global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
+// WINO (conv1's weight gradient from the forward's row-Winograd transform, dilation 1): the same
+// kernel over the transformed rows.  With the forward's y[3 r3 + j] = sum_xi AT[j][xi] (G w)_xi .
+// T_xi[r3] (conv_bf16x3.hip, "Row-Winograd conv1"), per kernel column kw
+//   dW[kh][kw] = sum_xi G[xi][kh] M_xi[kw],   M_xi[kw][co][ci] = sum_{b,r3,x} D_xi[co][r3][x] T_xi[ci][r3][x + kw - 1],
+//   D_xi = sum_j AT[j][xi] dy[3 r3 + j]   (wino_dy_rows_kernel, pre-split rows [B][5][Cout][R3][W]).
+// A workgroup owns one xi: its chunk is (b, r3, 32-px segment), the B window one T row (34 px of
+// 64 channels, both split parts), 3 taps (kw), 6 steps of 3 MFMAs; a.H is R3 and a.x is T.  Per
+// output row 5/3 chunks of 1/3 the MFMAs: x0.556 of the direct form's.  wgrad_wino_reduce_kernel
+// applies G while adding the partitions.
+struct WinoT {
+  int r5;         // T rows per (b, 8-channel block): 5 x 4 x tiles_y
+};
+
+template <int DIL, bool WINO = false>
+__global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a, const WinoT wt) {
   static_assert(NWV == 8, "wave layout: 4 output blocks x 2 channel halves");
-  using G = WgGeo<DIL>;
+  static_assert(!WINO || DIL == 1, "Winograd wgrad: dilation 1");
+  constexpr int ROWS = WINO ? 1 : 3;      // window rows (taps kh)
+  constexpr int NTAPS = 3 * ROWS;         // accumulators (kh, kw) / (kw)
+  constexpr int NSTEP = 2 * NTAPS;        // (pixel step, tap) steps per chunk
+  using G = WgGeo<DIL, ROWS>;
   constexpr int XW = G::XW, NA = G::NA, NB = G::NB, BUFE = G::BUFE, DT = G::DT;
   constexpr int DMAW = MVBEV_WGRAD_DMAW;
   __shared__ __attribute__((aligned(16))) u32x4 lds[3 * BUFE];
@@ -369,8 +386,10 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, kh = lane >> 5;
-  const int lb = xcd_remap(blockIdx.x, a.P * a.ntiles);
-  const int p = lb / a.ntiles, tile = lb - p * a.ntiles;
+  const int nt_all = a.ntiles * (WINO ? 5 : 1);
+  const int lb = xcd_remap(blockIdx.x, a.P * nt_all);
+  const int p = lb / nt_all, rem = lb - p * nt_all;
+  const int xi = WINO ? rem / a.ntiles : 0, tile = rem - xi * a.ntiles;
   const int ct = tile % a.n_ct, kt = tile / a.n_ct;
   const int32_t* list = nullptr;
   int nact = a.nchunks;
@@ -410,11 +429,16 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
     const bool ok = hg < 8 && q >= 0 && q < G::RUN && k0 < a.K;
     const int qc = ok ? q : 0, kc = ok ? k0 : 0;
     const int pix = qc >> 1, r = pix / XW, cc = pix - r * XW;
-    const int g_ = kc / a.group;
-    const int64_t cbase = g_ * a.group_stride + (int64_t)(kc - g_ * a.group) * plane;
-    bdy[j] = (r - 1) * DIL;
     bdx[j] = ok ? cc - DIL : INT_MIN / 2;
-    bofs[j] = (int)(cbase / 4) + 2 * (bdy[j] * W + cc - DIL) + (qc & 1);
+    if constexpr (WINO) {  // T block kc / 8: its row's hi plane [W], then its lo plane
+      bdy[j] = 0;
+      bofs[j] = (kc / 8) * (2 * wt.r5 * W) + (qc & 1) * W + cc - DIL;
+    } else {
+      const int g_ = kc / a.group;
+      const int64_t cbase = g_ * a.group_stride + (int64_t)(kc - g_ * a.group) * plane;
+      bdy[j] = (r - 1) * DIL;
+      bofs[j] = (int)(cbase / 4) + 2 * (bdy[j] * W + cc - DIL) + (qc & 1);
+    }
   }
   // chunk pk (packed b << 24 | y << 12 | seg, see the staging below) into buffer bb
   struct IssueCtx {
@@ -428,8 +452,13 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
     const int b = pk >> 24;
     c.y = (pk >> 12) & 4095;
     c.x0 = (pk & 4095) * PX;
-    c.abase = a.dy + ((int64_t)b * a.Cout * H + c.y) * W + c.x0;
-    c.bbase = xs + (int64_t)b * (a.batch_stride / 4) + 2 * (c.y * W + c.x0);
+    if constexpr (WINO) {  // D_xi rows [b][xi][co][r3]; T row 5 r3 + xi of batch b
+      c.abase = a.dy + (((int64_t)b * 5 + xi) * a.Cout * H + c.y) * W + c.x0;
+      c.bbase = xs + (int64_t)b * (a.K / 8) * (2 * (int64_t)wt.r5 * W) + 2 * (5 * c.y + xi) * W + c.x0;
+    } else {
+      c.abase = a.dy + ((int64_t)b * a.Cout * H + c.y) * W + c.x0;
+      c.bbase = xs + (int64_t)b * (a.batch_stride / 4) + 2 * (c.y * W + c.x0);
+    }
     c.dst = lds + bb * BUFE + wave * 64;
     return c;
   };
@@ -460,9 +489,9 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
   const int tr0 = 16 * ((cb * 4 + trg) * G::GS + (trg & 1) + 8 * (trg >> 1) + 2 * (8 * kh + (li >> 2))) +
                   8 * (li & 1);  // bytes
   const int arow = 32 * cw + l32, asw = (arow >> 1) & 7;
-  floatx16 acc[9];
+  floatx16 acc[NTAPS];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) acc[t] = floatx16{0};
+  for (int t = 0; t < NTAPS; ++t) acc[t] = floatx16{0};
 
   // Per chunk 18 (pixel step s, tap t) steps of 3 MFMAs.  Step u+2's 4 transposed reads go out
   // under step u's MFMAs and lgkmcnt(4) then retires step u+1's (in-order LDS returns; no
@@ -476,7 +505,7 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
   v4i16 fr[3][4];
   uint32_t bb0 = 0;
   auto read = [&](auto u_) __attribute__((always_inline)) {
-    constexpr int u = decltype(u_)::value, s = u / 9, t = u % 9;
+    constexpr int u = decltype(u_)::value, s = u / NTAPS, t = u % NTAPS;
     constexpr int set = u % 3;
     constexpr int off = ((t / 3) * XW + 16 * s + (t % 3) * DIL) * 32;  // bytes (32 per pixel)
     fr[set][0] = wg_tr<off>(bb0);
@@ -524,18 +553,18 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
       alo[s] = __builtin_bit_cast(bf16x8, ll);
     }
     auto step = [&](auto u_) __attribute__((always_inline)) {
-      constexpr int u = decltype(u_)::value, s = u / 9, t = u % 9;
+      constexpr int u = decltype(u_)::value, s = u / NTAPS, t = u % NTAPS;
       constexpr int set = u % 3, nset = (u + 1) % 3;
-      if constexpr (u + 2 < 18) read(std::integral_constant<int, u + 2>{});
+      if constexpr (u + 2 < NSTEP) read(std::integral_constant<int, u + 2>{});
       mfma3(t, ahi[s], alo[s], fr[set]);
-      if constexpr (u + 2 < 18) {
+      if constexpr (u + 2 < NSTEP) {
         asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(fr[nset][0]), "+v"(fr[nset][1]), "+v"(fr[nset][2]), "+v"(fr[nset][3]));
-      } else if constexpr (u + 1 < 18) {
+      } else if constexpr (u + 1 < NSTEP) {
         wg_lgkm_wait(fr[nset]);
       }
     };
-    wg_static_for(step, std::make_integer_sequence<int, 9>{});
-    if (full) wg_static_for(step, offset_seq<9>(std::make_integer_sequence<int, 9>{}));
+    wg_static_for(step, std::make_integer_sequence<int, NTAPS>{});
+    if (full) wg_static_for(step, offset_seq<NTAPS>(std::make_integer_sequence<int, NTAPS>{}));
   };
 
   // the partition's chunk ids, staged in LDS before any DMA (a global load of the list inside
@@ -579,12 +608,13 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a) {
 
   const int k = kt * NT + 32 * cb + l32;
   if (k < a.K) {
+    constexpr int NOUT = WINO ? 15 : 9;  // ws taps: (xi, kw) / (kh, kw)
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
+    for (int t = 0; t < NTAPS; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int co = ct * MT + 32 * cw + (r & 3) + 8 * (r >> 2) + 4 * kh;
-        a.ws[(((int64_t)p * 9 + t) * a.Cout + co) * a.K + k] = acc[t][r];
+        a.ws[(((int64_t)p * NOUT + xi * 3 + t) * a.Cout + co) * a.K + k] = acc[t][r];
       }
   }
 }
@@ -631,6 +661,88 @@ __global__ __launch_bounds__(kWrThreads) void wgrad_reduce_kernel(const float* _
     const int cm = chan_map ? chan_map[k] : k;
     if (cm < 0 || cm >= Cin_w) continue;
     dw[((int64_t)co * Cin_w + cm) * 9 + t] = sums[i];
+  }
+}
+
+// Winograd form: M[xi][kw] = sum_p ws[p][3 xi + kw][co][k] (partition order), then
+// dw[co][map(k)][kh][kw] = sum_xi G[xi][kh] M[xi][kw] in double (G of pack_wino_kernel), rounded once.
+constexpr int kWinoRedThreads = 320;  // 15 * 64 = 3 * 320 sums per block
+__global__ __launch_bounds__(kWinoRedThreads) void wgrad_wino_reduce_kernel(const float* __restrict__ ws, int P, int Cout,
+                                                                   int K, const int32_t* __restrict__ chan_map,
+                                                                   int Cin_w, float* __restrict__ dw) {
+  __shared__ float sums[15 * kWrK];
+  const int co = blockIdx.y, k0 = blockIdx.x * kWrK;
+  const int64_t pstride = (int64_t)15 * Cout * K;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int i = threadIdx.x + j * kWinoRedThreads, t = i / kWrK, k = k0 + i % kWrK;
+    float s = 0.f;
+    if (k < K) {
+      const float* src = ws + ((int64_t)t * Cout + co) * K + k;
+      int q = 0;
+      for (; q + 4 <= P; q += 4) {
+        float x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] = src[(q + u) * pstride];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s += x[u];
+      }
+      for (; q < P; ++q) s += src[q * pstride];
+    }
+    sums[(i % kWrK) * 15 + t] = s;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 9 * kWrK; i += kWinoRedThreads) {
+    const int kk = i / 9, tap = i - kk * 9, kh = tap / 3, kw = tap - kh * 3, k = k0 + kk;
+    if (k >= K) continue;
+    const int cm = chan_map ? chan_map[k] : k;
+    if (cm < 0 || cm >= Cin_w) continue;
+    const float* m = sums + kk * 15 + kw;  // m[3 xi]
+    const double m0 = m[0], m1 = m[3], m2 = m[6], m3 = m[9], m4 = m[12];
+    const double v = kh == 0 ? 0.5 * (m0 - m1) + (m3 - m2) / 6.0
+                   : kh == 1 ? -0.5 * m1 + (m2 + 2.0 * m3) / 6.0
+                             : -0.5 * m1 + (4.0 * m3 - m2) / 6.0 + m4;
+    dw[((int64_t)co * Cin_w + cm) * 9 + tap] = (float)v;
+  }
+}
+
+// D[b][xi][co][r3] = split(sum_j AT[j][xi] dy[b][co][3 r3 + j]) in MVBEV_LAYOUT_SPLIT_ROWS (rows past
+// H are zero), AT = [1 1 1 1 0; 0 1 -1 2 0; 0 1 1 4 1]: a thread per (b, co, r3, 8-pixel run).
+__global__ __launch_bounds__(256) void wino_dy_rows_kernel(const floatx4* __restrict__ dy, int B, int Cout, int H,
+                                                           int W, int R3, u32x4_t* __restrict__ out) {
+  const int runs = W / 8;
+  const int64_t n = (int64_t)B * Cout * R3 * runs;
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int run = (int)(i % runs);
+  int64_t r = i / runs;
+  const int r3 = (int)(r % R3);
+  r /= R3;
+  const int co = (int)(r % Cout), b = (int)(r / Cout);
+  float d[3][8];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int y = 3 * r3 + j;
+    floatx4 v0 = floatx4{0.f, 0.f, 0.f, 0.f}, v1 = v0;
+    if (y < H) {
+      const floatx4* src = dy + ((((int64_t)b * Cout + co) * H + y) * W) / 4 + 2 * run;
+      v0 = src[0];
+      v1 = src[1];
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) d[j][e] = v0[e], d[j][4 + e] = v1[e];
+  }
+  const int64_t plane = (int64_t)Cout * R3 * runs;  // runs per xi of one batch
+  u32x4_t* o = out + 2 * (((int64_t)b * 5 * Cout + co) * R3 * runs + (int64_t)r3 * runs + run);
+#pragma unroll
+  for (int x = 0; x < 5; ++x) {
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float a0 = d[0][e], a1 = d[1][e], a2 = d[2][e];
+      v[e] = x == 0 ? a0 : x == 1 ? a0 + a1 + a2 : x == 2 ? a0 - a1 + a2 : x == 3 ? a0 + 2.f * a1 + 4.f * a2 : a2;
+    }
+    store_split8(o + 2 * (int64_t)x * plane, v);
   }
 }
 
@@ -1377,8 +1489,8 @@ int mvbev_conv3x3_wgrad_bf16x3_ex2(const void* x, int x_layout, const mvbev_conv
   a.dy_rows = dy_layout == MVBEV_LAYOUT_SPLIT_ROWS;
   if (a.dy_rows && (!dma || d->W % 8 != 0)) return MVBEV_ERR_SHAPE;  // pre-split rows: the DMA kernel only
   if (dma) {
-    if (dilation == 1) hipLaunchKernelGGL((wgrad_dma_kernel<1>), grid, dim3(NTH), 0, s, a);
-    else hipLaunchKernelGGL((wgrad_dma_kernel<2>), grid, dim3(NTH), 0, s, a);
+    if (dilation == 1) hipLaunchKernelGGL((wgrad_dma_kernel<1>), grid, dim3(NTH), 0, s, a, WinoT{0});
+    else hipLaunchKernelGGL((wgrad_dma_kernel<2>), grid, dim3(NTH), 0, s, a, WinoT{0});
   } else if (dilation == 1) {
     if (split) hipLaunchKernelGGL((wgrad_kernel<SplitIn, 1>), grid, block, 0, s, a);
     else hipLaunchKernelGGL((wgrad_kernel<float, 1>), grid, block, 0, s, a);
@@ -1391,6 +1503,94 @@ int mvbev_conv3x3_wgrad_bf16x3_ex2(const void* x, int x_layout, const mvbev_conv
   MVBEV_CHECK_LAUNCH();
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)ceil_div(d->K, kWrK), (unsigned)Cout), dim3(kWrThreads), 0, s,
                      static_cast<const float*>(workspace), g.P, (int)Cout, (int)d->K, chan_map, (int)Cin_w, dw);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+size_t mvbev_wino_dy_rows_bytes(int64_t B, int64_t Cout, int64_t H, int64_t W) {
+  if (B <= 0 || Cout <= 0 || H <= 0 || W <= 0) return 0;
+  return (size_t)B * 5 * (size_t)Cout * (size_t)mvbev::ceil_div(H, 3) * (size_t)W * 4;
+}
+
+int mvbev_wino_dy_rows_f32(const float* dy, int64_t B, int64_t Cout, int64_t H, int64_t W, void* out,
+                           size_t out_bytes, void* stream) {
+  using namespace mvbev;
+  if (!dy || !out) return MVBEV_ERR_NULL;
+  if (B <= 0 || Cout <= 0 || H <= 0 || W <= 0) return MVBEV_ERR_RANK;
+  if (W % 8 != 0 || B * Cout * H * W > (int64_t)INT32_MAX * 8) return MVBEV_ERR_SHAPE;
+  if (out_bytes < mvbev_wino_dy_rows_bytes(B, Cout, H, W)) return MVBEV_ERR_SHAPE;
+  if (((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(out)) & 15) != 0) return MVBEV_ERR_ALIGN;
+  const int64_t R3 = ceil_div(H, 3), n = B * Cout * R3 * (W / 8);
+  hipLaunchKernelGGL(bwd::wino_dy_rows_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream),
+                     reinterpret_cast<const bwd::floatx4*>(dy), (int)B, (int)Cout, (int)H, (int)W, (int)R3,
+                     static_cast<u32x4_t*>(out));
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+// Winograd geometry: P over the 5 x tiles workgroup set, chunks (b, r3 < R3, segment) per xi
+static mvbev::bwd::WGeo wgrad_wino_geo(const mvbev_conv_desc* d, int64_t Cout) {
+  using namespace mvbev;
+  using namespace mvbev::bwd;
+  WGeo g;
+  g.tiles = (Cout / MT) * ceil_div(d->K, NT);
+  g.nchunks = d->B * ceil_div(d->H, 3) * ceil_div(d->W, PX);
+  g.P = wgrad_partitions(5 * g.tiles, g.nchunks);
+  return g;
+}
+
+size_t mvbev_conv3x3_wgrad_wino_workspace_bytes(const mvbev_conv_desc* desc, int64_t Cout) {
+  if (!desc || Cout <= 0 || desc->K <= 0 || desc->H <= 0 || desc->W <= 0 || desc->B <= 0) return 0;
+  const mvbev::bwd::WGeo g = wgrad_wino_geo(desc, Cout);
+  return (size_t)g.P * 15 * (size_t)Cout * (size_t)desc->K * sizeof(float);
+}
+
+int mvbev_conv3x3_wgrad_wino_bf16x3(const void* t, size_t t_bytes, const mvbev_conv_desc* d, const void* dy_wino,
+                                    size_t dy_wino_bytes, int64_t Cout, const int32_t* chan_map, int64_t Cin_w,
+                                    float* dw, const int32_t* chunk_list, const int32_t* chunk_off, void* workspace,
+                                    size_t workspace_bytes, void* stream) {
+  using namespace mvbev;
+  using namespace mvbev::bwd;
+  if (!t || !d || !dy_wino || !dw || !workspace) return MVBEV_ERR_NULL;
+  if ((chunk_list == nullptr) != (chunk_off == nullptr)) return MVBEV_ERR_NULL;
+  if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || Cin_w <= 0 || d->group <= 0)
+    return MVBEV_ERR_RANK;
+  if (Cout % MT != 0 || Cout > 65535 || d->K % 8 != 0 || d->group % 8 != 0 || d->K % d->group != 0 ||
+      d->W % 8 != 0)
+    return MVBEV_ERR_SHAPE;
+  if (d->in_row0 != 0 || d->in_rows != d->H || d->out_row0 != 0 || d->out_rows != d->H) return MVBEV_ERR_SHAPE;
+  if (!chan_map && d->K > Cin_w) return MVBEV_ERR_SHAPE;
+  if (chunk_list && d->group % NT != 0) return MVBEV_ERR_SHAPE;  // a channel tile inside one group
+  constexpr int kRT = 12;  // conv_wino's workgroup tile rows: T holds 4 row tiles (r3) of each
+  const int64_t R3 = ceil_div(d->H, 3), r5 = 5 * 4 * ceil_div(d->H, kRT), segs = ceil_div(d->W, PX);
+  const int64_t t_need = d->B * (d->K / 8) * r5 * d->W * 32;
+  if (t_bytes < (size_t)t_need || dy_wino_bytes < mvbev_wino_dy_rows_bytes(d->B, Cout, d->H, d->W))
+    return MVBEV_ERR_SHAPE;
+  // 32-bit chunk-invariant offsets and packed chunk ids (b < 128, r3 and segments < 4096)
+  if ((d->K / 8) * 2 * r5 * d->W >= INT32_MAX || Cout * R3 * d->W >= INT32_MAX || d->B >= 128 || R3 > 4096 ||
+      segs > 4096)
+    return MVBEV_ERR_SHAPE;
+  const WGeo g = wgrad_wino_geo(d, Cout);
+  if (g.nchunks / g.P + 1 > WG_MAXC) return MVBEV_ERR_SHAPE;
+  const size_t need = (size_t)g.P * 15 * (size_t)Cout * (size_t)d->K * sizeof(float);
+  if (workspace_bytes < need) return MVBEV_ERR_SHAPE;
+  if (((reinterpret_cast<uintptr_t>(t) | reinterpret_cast<uintptr_t>(dy_wino)) & 15) != 0) return MVBEV_ERR_ALIGN;
+  WArgs a;
+  a.x = t; a.dy = static_cast<const float*>(dy_wino); a.ws = static_cast<float*>(workspace);
+  a.group_stride = d->group_stride; a.batch_stride = d->batch_stride;
+  a.group = (int)d->group; a.K = (int)d->K; a.Cout = (int)Cout; a.B = (int)d->B;
+  a.H = (int)R3; a.W = (int)d->W;  // the kernel's rows: the 3-row tiles r3
+  a.segs = (int)segs; a.nchunks = (int)g.nchunks; a.P = g.P;
+  a.n_ct = (int)(Cout / MT); a.n_kt = (int)ceil_div(d->K, NT); a.ntiles = (int)g.tiles;
+  a.vec_dy = true; a.dy_rows = true;
+  a.clist = chunk_list; a.coff = chunk_off;
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL((wgrad_dma_kernel<1, true>), dim3((unsigned)(g.P * 5 * g.tiles)), dim3(NTH), 0, s, a,
+                     WinoT{(int)r5});
+  MVBEV_CHECK_LAUNCH();
+  hipLaunchKernelGGL(wgrad_wino_reduce_kernel, dim3((unsigned)ceil_div(d->K, kWrK), (unsigned)Cout),
+                     dim3(kWinoRedThreads), 0, s, static_cast<const float*>(workspace), g.P, (int)Cout, (int)d->K, chan_map,
+                     (int)Cin_w, dw);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }

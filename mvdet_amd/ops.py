@@ -1325,6 +1325,88 @@ def conv3x3_wgrad(x: torch.Tensor, desc, dy: torch.Tensor, dilation: int, cin_w:
     return dw
 
 
+def wino_dy_rows(dy: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 dy [B,Cout,H,W] (contiguous, W % 8 == 0) -> D_xi = sum_j AT[j][xi] dy[3 r3 + j] in the
+    row-split bf16 layout, [B, 5, Cout, ceil(H/3), W/8, 2, 8] (``mvbev_wino_dy_rows_f32``): the
+    output-gradient side of ``conv3x3_wgrad_wino``."""
+    _require_cuda(dy)
+    if dy.dim() != 4 or dy.dtype != torch.float32 or not dy.is_contiguous() or dy.shape[3] % 8:
+        raise ValueError("wino_dy_rows needs a contiguous float32 [B,C,H,W] tensor with W % 8 == 0")
+    B, C, H, W = dy.shape
+    shape = (B, 5, C, -(-H // 3), W // 8, 2, 8)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.bfloat16, device=dy.device)
+    elif tuple(out.shape) != shape or out.dtype != torch.bfloat16 or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous bf16 tensor of shape {shape}")
+    st = _native.load().mvbev_wino_dy_rows_f32(dy.data_ptr(), B, C, H, W, out.data_ptr(),
+                                               out.numel() * out.element_size(), _stream(dy))
+    _native.check(st, "mvbev_wino_dy_rows_f32")
+    return out
+
+
+def wgrad_wino_chunk_lists(mask: torch.Tensor, groups: int, B: int, H: int, W: int):
+    """Per channel group, the Winograd wgrad chunks (b, r3 < ceil(H/3), 32-px segment) whose T row
+    can be non-zero: the forward's 12-row frustum ``mask`` (``conv1_mask(tile_h=12)``, the mask T was
+    written under) at tile (r3 // 4, segment) -> (chunk_list, chunk_off) int32 device tensors."""
+    import numpy as np
+    tx = -(-W // _native.TILE_W)
+    segs = -(-W // 32)
+    assert segs == tx, "wgrad chunks are 32 px = one conv tile column"
+    r3n = -(-H // 3)
+    if mask.numel() != -(-H // 12) * tx:
+        raise ValueError("the mask must be over 12-row conv tiles (the rows T was written in)")
+    m = np.asarray(mask.cpu().numpy(), dtype=np.int64) & 0xFFFFFFFF
+    rows = np.repeat(np.arange(r3n) // 4, segs) * tx + np.tile(np.arange(segs), r3n)  # per (r3, seg)
+    per_img = m[rows]
+    lists, off = [], [0]
+    for g in range(groups):
+        act = np.nonzero((per_img >> g) & 1)[0]
+        full = (np.arange(B)[:, None] * (r3n * segs) + act[None, :]).reshape(-1)
+        lists.append(full)
+        off.append(off[-1] + full.size)
+    lst = np.concatenate(lists) if lists else np.zeros(0, np.int64)
+    dev = mask.device
+    return (torch.tensor(lst, dtype=torch.int32, device=dev) if lst.size else torch.zeros(1, dtype=torch.int32,
+                                                                                          device=dev),
+            torch.tensor(off, dtype=torch.int32, device=dev))
+
+
+def conv3x3_wgrad_wino(t: torch.Tensor, desc, dy_wino: torch.Tensor, cin_w: int,
+                       chan_map: Optional[torch.Tensor] = None, dw: Optional[torch.Tensor] = None,
+                       workspace: Optional[torch.Tensor] = None, chunk_lists=None) -> torch.Tensor:
+    """Weight gradient of a dilation-1 3x3 conv from its forward's row-Winograd transform ``t``
+    (``wino_rows`` of the input ``desc`` addresses, or the fused warp's) and ``dy_wino`` =
+    ``wino_dy_rows(dy)`` (``mvbev_conv3x3_wgrad_wino_bf16x3``): the same dw as ``conv3x3_wgrad``
+    within the 3xbf16 error.  ``chunk_lists``: ``wgrad_wino_chunk_lists`` of the mask T was written
+    under.  Writes dw[co][chan_map[k]][:] of a [Cout, cin_w, 3, 3] tensor (allocated zeroed when None)."""
+    _require_cuda(t, dy_wino)
+    B, cout = dy_wino.shape[0], dy_wino.shape[2]
+    if dy_wino.dim() != 7 or dy_wino.dtype != torch.bfloat16 or not dy_wino.is_contiguous() or dy_wino.shape[1] != 5:
+        raise ValueError("dy_wino must be wino_dy_rows' output")
+    if (desc.B, -(-desc.H // 3), desc.W // 8) != (B, dy_wino.shape[3], dy_wino.shape[4]):
+        raise ValueError("dy_wino does not match the conv descriptor")
+    if chan_map is not None:
+        _require_cuda(chan_map)
+        if chan_map.dtype != torch.int32 or chan_map.numel() != desc.K:
+            raise ValueError("chan_map must be an int32 device tensor of K entries")
+    if dw is None:
+        dw = torch.zeros((cout, cin_w, 3, 3), dtype=torch.float32, device=t.device)
+    elif tuple(dw.shape) != (cout, cin_w, 3, 3) or not dw.is_contiguous() or dw.dtype != torch.float32:
+        raise ValueError(f"dw must be a contiguous fp32 [{cout},{cin_w},3,3] tensor")
+    lib = _native.load()
+    need = int(lib.mvbev_conv3x3_wgrad_wino_workspace_bytes(ctypes.byref(desc), cout))
+    if workspace is None or workspace.numel() * workspace.element_size() < need:
+        workspace = torch.empty((need + 3) // 4, dtype=torch.float32, device=t.device)
+    cl, co = (None, None) if chunk_lists is None else (chunk_lists[0].data_ptr(), chunk_lists[1].data_ptr())
+    st = lib.mvbev_conv3x3_wgrad_wino_bf16x3(t.data_ptr(), t.numel() * t.element_size(), ctypes.byref(desc),
+                                             dy_wino.data_ptr(), dy_wino.numel() * dy_wino.element_size(), cout,
+                                             None if chan_map is None else chan_map.data_ptr(), cin_w, dw.data_ptr(),
+                                             cl, co, workspace.data_ptr(),
+                                             workspace.numel() * workspace.element_size(), _stream(t))
+    _native.check(st, "mvbev_conv3x3_wgrad_wino_bf16x3")
+    return dw
+
+
 def conv3x3_bias_coord_grad(dy: torch.Tensor, dilation: int, db: Optional[torch.Tensor] = None,
                             dw: Optional[torch.Tensor] = None, coord_ch: int = 0) -> None:
     """db[co] = sum dy[:, co]; with ``dw`` [Cout, Cin_w, 3, 3], also the weight gradient of the

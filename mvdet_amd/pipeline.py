@@ -69,6 +69,9 @@ class Workspace:
     wino_t: Optional[torch.Tensor] = None
     # wino_t holds the current frame's transform, written by the fused warp (the slab was not)
     t_from_warp: bool = False
+    # wino_t holds this forward's transform of the whole grid (conv1 ran row-Winograd over all rows):
+    # the training backward's conv1 weight gradient reads it (autograd._wgrad1_wino)
+    t1_valid: bool = False
     # grid rows the slab holds: (0, Ho) for a warped slab; a row window for a band-local slab
     # filled by the multi-GPU band exchange (parallel.ViewBands)
     slab_rows: Tuple[int, int] = (0, 0)
@@ -539,6 +542,7 @@ class ProjectFuse:
             ws.wino_t = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=ws.slab.device)
         if not ws.t_from_warp:  # the slab's transform (else the fused warp wrote T)
             ops.wino_rows(ws.slab, d1, ws.wino_t, gm)
+        ws.t1_valid = (a1, b1) == (0, self.grid_hw[0])
         if mark:
             mark("conv1_wino")  # between the transform and the conv (bench.py's stage events)
         return ops.conv3x3_wino(ws.wino_t, d1, self.pack1w.get(conv1.weight), self.mid, init=init, relu=True,

@@ -78,7 +78,27 @@ def backward_stages(eng, ws, mc, B, ho, wo, N, C, dev):
     rows1 = torch.empty(ops.split_rows_shape(B, w1.shape[0], ho, wo), dtype=torch.bfloat16, device=dev)
     rows2 = torch.empty(ops.split_rows_shape(B, mid, ho, wo), dtype=torch.bfloat16, device=dev)
     pre = wo % 8 == 0
+    # the Winograd form (autograd._wgrad1_wino): T of the slab under the forward's mask, D of dy1
+    gm1 = eng.conv1_mask(dev, 0, ho)
+    t1 = torch.zeros((ops.wino_rows_bytes(d1) + 1) // 2, dtype=torch.bfloat16, device=dev)
+    ops.wino_rows(ws.slab, d1, t1, gm1)
+    lists_w = ops.wgrad_wino_chunk_lists(gm1, eng.S, B, ho, wo) if gm1 is not None else None
+    drows = torch.empty((B, 5, w1.shape[0], -(-ho // 3), wo // 8, 2, 8), dtype=torch.bfloat16, device=dev)
+    wwsw = torch.empty((int(_native.load().mvbev_conv3x3_wgrad_wino_workspace_bytes(
+        __import__("ctypes").byref(d1), w1.shape[0])) + 3) // 4, device=dev)
+    dw1w = torch.zeros_like(w1)
+    if pre:
+        ops.conv3x3_wgrad(ws.slab, d1, dy1, 1, w1.shape[1], chan_map=eng.pack1._map_dev, dw=dw1, workspace=wws,
+                          chunk_lists=lists)
+        ops.conv3x3_wgrad_wino(t1, d1, ops.wino_dy_rows(dy1, out=drows), w1.shape[1], chan_map=eng.pack1._map_dev,
+                               dw=dw1w, workspace=wwsw, chunk_lists=lists_w)
+        nc = N * C
+        diff = (dw1w[:, :nc] - dw1[:, :nc]).abs().max().item() / max(dw1[:, :nc].abs().max().item(), 1e-30)
+        print(json.dumps({"wgrad1w_vs_wgrad1_normwise": diff}), flush=True)
     return {
+        "wgrad1w": (lambda: ops.conv3x3_wgrad_wino(t1, d1, ops.wino_dy_rows(dy1, out=drows), w1.shape[1],
+                                                   chan_map=eng.pack1._map_dev, dw=dw1w, workspace=wwsw,
+                                                   chunk_lists=lists_w), flop),
         "wgrad2": (lambda: ops.conv3x3_wgrad(y1s, d_y1, dy2, 2, mid, workspace=wws2,
                                              dy_rows=ops.split_rows(dy2, out=rows2) if pre else None), flop2),
         "wgrad2f": (lambda: ops.conv3x3_wgrad(y1s, d_y1, dy2, 2, mid, workspace=wws2), flop2),
@@ -196,7 +216,7 @@ def main():
             stages["adjup"] = ((lambda: ops.warp_views_adjoint(douts, plu, gs)), None)
             pl = [ops.WarpAdjointPlan(eng.m_norm_cpu[v], up, (ho, wo), dev) for v in range(N)]
             stages["adj"] = ((lambda: ops.warp_views_adjoint(douts, pl, gsu)), None)
-        if {"wgrad1", "wgrad1f", "dgrad1", "dgrad1s", "wgrad2", "wgrad2f", "dgrad2"} & set(args.only.split(",")):
+        if {"wgrad1", "wgrad1w", "wgrad1f", "dgrad1", "dgrad1s", "wgrad2", "wgrad2f", "dgrad2"} & set(args.only.split(",")):
             stages.update(backward_stages(eng, ws, mc, B, ho, wo, N, C, dev))
         from mvdet_amd import _native
         libs = [("default", _native.load())]

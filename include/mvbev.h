@@ -631,7 +631,8 @@ int mvbev_conv3x3_wgrad_bf16x3_ex2(const void* x, int x_layout, const mvbev_conv
  * is D (mvbev_wino_dy_rows_f32), and the products run 3xbf16 as in mvbev_conv3x3_wgrad_bf16x3_ex2, whose
  * arguments the others mean (chunk lists: chunk (b * ceil(H / 3) + r3) * ceil(W / 32) + x / 32 where
  * T_xi of group g can be non-zero — the forward's 12-row frustum mask, tile r3 / 4).  x0.556 of the
- * direct form's MFMAs; W % 8 == 0, desc over all rows.  workspace: mvbev_conv3x3_wgrad_wino_workspace_bytes. */
+ * direct form's MFMAs; W % 8 == 0, desc over all rows, 128-channel groups with chunk lists.  workspace:
+ * mvbev_conv3x3_wgrad_wino_workspace_bytes. */
 size_t mvbev_wino_dy_rows_bytes(int64_t B, int64_t Cout, int64_t H, int64_t W);
 /* D[b][xi][co][r3] (r3 < ceil(H / 3), rows past H zero) of fp32 dy [B][Cout][H][W] in
  * MVBEV_LAYOUT_SPLIT_ROWS; AT = [1 1 1 1 0; 0 1 -1 2 0; 0 1 1 4 1]; W % 8 == 0, 16-B aligned. */

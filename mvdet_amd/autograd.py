@@ -199,8 +199,8 @@ def _dgrad1_wino(engine: ProjectFuse, st, dy1s: torch.Tensor, w1: torch.Tensor, 
 
 def _wgrad1_wino_applies(engine: ProjectFuse, ws: Workspace, dy1: torch.Tensor) -> bool:
     """conv1's weight gradient runs row-Winograd (``_wgrad1_wino``) when the forward's conv1 did
-    (its whole-grid transform T is in ``ws.wino_t``), with whole 64-channel slot tiles."""
-    return (ws.t1_valid and ws.wino_t is not None and dy1.shape[3] % 8 == 0 and engine.Cs % 64 == 0
+    (its whole-grid transform T is in ``ws.wino_t``), with whole 128-channel slot tiles."""
+    return (ws.t1_valid and ws.wino_t is not None and dy1.shape[3] % 8 == 0 and engine.Cs % 128 == 0
             and _native.load().mvbev_version() >= 12000)
 
 

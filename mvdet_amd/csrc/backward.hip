@@ -310,11 +310,11 @@ constexpr int WG_AENT = MT * PX / 4;  // A entries (16 B) per buffer: 1024
 #define MVBEV_WGRAD_DMAW 8  // 4 measured equal (2.41 vs 2.42 ms) at 16 more VGPRs; 2: 3.45 ms
 #endif
 constexpr int WG_MAXC = 2048;         // chunk ids of a workgroup's partition, staged in LDS
-template <int DIL, int ROWS = 3> struct WgGeo {
+template <int DIL, int ROWS = 3, int NH = 2> struct WgGeo {  // NH: 32-channel blocks of the window
   static constexpr int XW = PX + 2 * DIL, BPIX = ROWS * XW;
   static constexpr int RUN = 2 * BPIX;                      // entries of one (h, g) run
   static constexpr int GS = (RUN + 9 + 15) / 16 * 16;       // run stride (entries, 0 mod 16)
-  static constexpr int BENT = 8 * GS;
+  static constexpr int BENT = 4 * NH * GS;
   static constexpr int DT = 64 * MVBEV_WGRAD_DMAW;         // DMA lanes (the first DMAW waves)
   static constexpr int NA = WG_AENT / DT;                   // A DMA instructions per DMA lane
   static constexpr int NB = (BENT + DT - 1) / DT;           // B DMA instructions per DMA lane
@@ -339,8 +339,15 @@ __device__ inline v4i16 wg_tr(uint32_t addr) {
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(addr), "i"(OFF));
   return r;
 }
-__device__ inline void wg_lgkm_wait(v4i16 (&f)[4]) {
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]));
+// fragment registers tied after a wait: kept live (a read still in flight owns them) until it, and
+// read only after it
+template <int CB_> __device__ inline void wg_tie(v4i16 (&f)[CB_][4]) {
+#pragma unroll
+  for (int j = 0; j < CB_; ++j) asm volatile("" : "+v"(f[j][0]), "+v"(f[j][1]), "+v"(f[j][2]), "+v"(f[j][3]));
+}
+template <int CNT, int CB_> __device__ inline void wg_lgkm_wait(v4i16 (&f)[CB_][4]) {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(CNT));
+  wg_tie(f);
 }
 __device__ inline bf16x8 wg_cat(v4i16 lo, v4i16 hi) {
   typedef short v8i16 __attribute__((ext_vector_type(8)));
@@ -362,10 +369,12 @@ constexpr std::integer_sequence<int, (B + U)...> offset_seq(std::integer_sequenc
 // T_xi[r3] (conv_bf16x3.hip, "Row-Winograd conv1"), per kernel column kw
 //   dW[kh][kw] = sum_xi G[xi][kh] M_xi[kw],   M_xi[kw][co][ci] = sum_{b,r3,x} D_xi[co][r3][x] T_xi[ci][r3][x + kw - 1],
 //   D_xi = sum_j AT[j][xi] dy[3 r3 + j]   (wino_dy_rows_kernel, pre-split rows [B][5][Cout][R3][W]).
-// A workgroup owns one xi: its chunk is (b, r3, 32-px segment), the B window one T row (34 px of
-// 64 channels, both split parts), 3 taps (kw), 6 steps of 3 MFMAs; a.H is R3 and a.x is T.  Per
-// output row 5/3 chunks of 1/3 the MFMAs: x0.556 of the direct form's.  wgrad_wino_reduce_kernel
-// applies G while adding the partitions.
+// A workgroup owns one xi and 128 input channels (desc group a multiple of 128 with chunk lists) (a wave: 32 Cout x 2 blocks of 32 channels, so
+// each A fragment feeds both and a chunk carries twice the direct form's MFMAs per input channel
+// block); its chunk is (b, r3, 32-px segment), the B window one T row (34 px of 128 channels, both
+// split parts), 3 taps (kw), 6 steps of 2 x 3 MFMAs; a.H is R3 and a.x is T.  Per output row 5/3
+// chunks of 1/3 the MFMAs: x0.556 of the direct form's.  wgrad_wino_reduce_kernel applies G while
+// adding the partitions.
 struct WinoT {
   int r5;         // T rows per (b, 8-channel block): 5 x 4 x tiles_y
 };
@@ -377,7 +386,9 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a, const 
   constexpr int ROWS = WINO ? 1 : 3;      // window rows (taps kh)
   constexpr int NTAPS = 3 * ROWS;         // accumulators (kh, kw) / (kw)
   constexpr int NSTEP = 2 * NTAPS;        // (pixel step, tap) steps per chunk
-  using G = WgGeo<DIL, ROWS>;
+  constexpr int CB = WINO ? 2 : 1;        // 32-channel blocks per wave
+  constexpr int NTW = 64 * CB;            // input channels per workgroup
+  using G = WgGeo<DIL, ROWS, 2 * CB>;
   constexpr int XW = G::XW, NA = G::NA, NB = G::NB, BUFE = G::BUFE, DT = G::DT;
   constexpr int DMAW = MVBEV_WGRAD_DMAW;
   __shared__ __attribute__((aligned(16))) u32x4 lds[3 * BUFE];
@@ -394,7 +405,7 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a, const 
   const int32_t* list = nullptr;
   int nact = a.nchunks;
   if (a.clist) {
-    const int grp = (kt * NT) / a.group;
+    const int grp = (kt * NTW) / a.group;
     list = a.clist + a.coff[grp];
     nact = a.coff[grp + 1] - a.coff[grp];
   }
@@ -425,8 +436,8 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a, const 
     const int e = (j * DMAW + wave) * 64 + lane;
     const int hg = e / G::GS, g4 = hg & 3;
     const int q = e - hg * G::GS - ((g4 & 1) + 8 * (g4 >> 1));
-    const int k0 = kt * NT + (hg >> 2) * 32 + g4 * 8;
-    const bool ok = hg < 8 && q >= 0 && q < G::RUN && k0 < a.K;
+    const int k0 = kt * NTW + (hg >> 2) * 32 + g4 * 8;
+    const bool ok = hg < 8 * CB && q >= 0 && q < G::RUN && k0 < a.K;
     const int qc = ok ? q : 0, kc = ok ? k0 : 0;
     const int pix = qc >> 1, r = pix / XW, cc = pix - r * XW;
     bdx[j] = ok ? cc - DIL : INT_MIN / 2;
@@ -486,12 +497,14 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a, const 
   // transposed-read lane: pixel 8 kh + li / 4 (+ 4 for the second read), channels 16 gi + 4 (li & 3)
   // .. + 3 of the wave's half = group g = 2 gi + (li & 3) / 2, offset 4 (li & 1) in the piece
   const int trg = 2 * gi + ((li & 3) >> 1);
-  const int tr0 = 16 * ((cb * 4 + trg) * G::GS + (trg & 1) + 8 * (trg >> 1) + 2 * (8 * kh + (li >> 2))) +
-                  8 * (li & 1);  // bytes
+  const int tr0 = 16 * ((cb * CB * 4 + trg) * G::GS + (trg & 1) + 8 * (trg >> 1) + 2 * (8 * kh + (li >> 2))) +
+                  8 * (li & 1);  // bytes; the wave's block j at + 64 j GS bytes
   const int arow = 32 * cw + l32, asw = (arow >> 1) & 7;
-  floatx16 acc[NTAPS];
+  floatx16 acc[CB][NTAPS];
 #pragma unroll
-  for (int t = 0; t < NTAPS; ++t) acc[t] = floatx16{0};
+  for (int j = 0; j < CB; ++j)
+#pragma unroll
+    for (int t = 0; t < NTAPS; ++t) acc[j][t] = floatx16{0};
 
   // Per chunk 18 (pixel step s, tap t) steps of 3 MFMAs.  Step u+2's 4 transposed reads go out
   // under step u's MFMAs and lgkmcnt(4) then retires step u+1's (in-order LDS returns; no
@@ -502,22 +515,32 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a, const 
   // multiply zeros and is skipped (the reads it prefetched are drained by the next wait).
   floatx4 av[4];
   bf16x8 ahi[2], alo[2];
-  v4i16 fr[3][4];
+  v4i16 fr[3][CB][4];
   uint32_t bb0 = 0;
   auto read = [&](auto u_) __attribute__((always_inline)) {
     constexpr int u = decltype(u_)::value, s = u / NTAPS, t = u % NTAPS;
     constexpr int set = u % 3;
     constexpr int off = ((t / 3) * XW + 16 * s + (t % 3) * DIL) * 32;  // bytes (32 per pixel)
-    fr[set][0] = wg_tr<off>(bb0);
-    fr[set][1] = wg_tr<off + 128>(bb0);
-    fr[set][2] = wg_tr<off + 16>(bb0);
-    fr[set][3] = wg_tr<off + 16 + 128>(bb0);
+    constexpr int jb = 64 * G::GS;                                      // bytes between 32-channel blocks
+    fr[set][0][0] = wg_tr<off>(bb0);
+    fr[set][0][1] = wg_tr<off + 128>(bb0);
+    fr[set][0][2] = wg_tr<off + 16>(bb0);
+    fr[set][0][3] = wg_tr<off + 16 + 128>(bb0);
+    if constexpr (CB == 2) {
+      fr[set][1][0] = wg_tr<jb + off>(bb0);
+      fr[set][1][1] = wg_tr<jb + off + 128>(bb0);
+      fr[set][1][2] = wg_tr<jb + off + 16>(bb0);
+      fr[set][1][3] = wg_tr<jb + off + 16 + 128>(bb0);
+    }
   };
-  auto mfma3 = [&](int t, bf16x8 ah, bf16x8 al, const v4i16 (&f)[4]) __attribute__((always_inline)) {
-    const bf16x8 bhi = wg_cat(f[0], f[1]), blo = wg_cat(f[2], f[3]);
-    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bhi, acc[t], 0, 0, 0);
-    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, blo, acc[t], 0, 0, 0);
-    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bhi, acc[t], 0, 0, 0);
+  auto mfma3 = [&](int t, bf16x8 ah, bf16x8 al, const v4i16 (&f)[CB][4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < CB; ++j) {
+      const bf16x8 bhi = wg_cat(f[j][0], f[j][1]), blo = wg_cat(f[j][2], f[j][3]);
+      acc[j][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bhi, acc[j][t], 0, 0, 0);
+      acc[j][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, blo, acc[j][t], 0, 0, 0);
+      acc[j][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bhi, acc[j][t], 0, 0, 0);
+    }
   };
   // chunk in buffer bb: the A fragments and steps 0, 1's B fragments
   auto head_reads = [&](int bb) __attribute__((always_inline)) {
@@ -534,9 +557,9 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a, const 
     read(std::integral_constant<int, 1>{});
   };
   auto body = [&](bool full) __attribute__((always_inline)) {
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(av[0]), "+v"(av[1]), "+v"(av[2]), "+v"(av[3]), "+v"(fr[0][0]),
-                 "+v"(fr[0][1]), "+v"(fr[0][2]), "+v"(fr[0][3]), "+v"(fr[1][0]), "+v"(fr[1][1]), "+v"(fr[1][2]),
-                 "+v"(fr[1][3]));
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(av[0]), "+v"(av[1]), "+v"(av[2]), "+v"(av[3]));
+    wg_tie(fr[0]);
+    wg_tie(fr[1]);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const floatx4 v0 = av[2 * s], v1 = av[2 * s + 1];
@@ -558,9 +581,9 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a, const 
       if constexpr (u + 2 < NSTEP) read(std::integral_constant<int, u + 2>{});
       mfma3(t, ahi[s], alo[s], fr[set]);
       if constexpr (u + 2 < NSTEP) {
-        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(fr[nset][0]), "+v"(fr[nset][1]), "+v"(fr[nset][2]), "+v"(fr[nset][3]));
+        wg_lgkm_wait<4 * CB>(fr[nset]);
       } else if constexpr (u + 1 < NSTEP) {
-        wg_lgkm_wait(fr[nset]);
+        wg_lgkm_wait<0>(fr[nset]);
       }
     };
     wg_static_for(step, std::make_integer_sequence<int, NTAPS>{});
@@ -584,18 +607,12 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a, const 
       // retire chunk i's DMA (chunk i+1's may stay in flight) and every LDS read of chunk i-1
       // (fragment registers tied: a partial chunk's skipped reads must land before reuse)
       if (i + 1 < n) {
-        asm volatile("s_waitcnt vmcnt(%8) lgkmcnt(0)"
-                     : "+v"(fr[0][0]), "+v"(fr[0][1]), "+v"(fr[0][2]), "+v"(fr[0][3]), "+v"(fr[1][0]), "+v"(fr[1][1]),
-                       "+v"(fr[1][2]), "+v"(fr[1][3])
-                     : "n"(NA + NB)
-                     : "memory");
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NA + NB) : "memory");
       } else {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)"
-                     : "+v"(fr[0][0]), "+v"(fr[0][1]), "+v"(fr[0][2]), "+v"(fr[0][3]), "+v"(fr[1][0]), "+v"(fr[1][1]),
-                       "+v"(fr[1][2]), "+v"(fr[1][3])
-                     :
-                     : "memory");
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       }
+      wg_tie(fr[0]);
+      wg_tie(fr[1]);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       // (measured no faster: the pieces one after each of the first steps' MFMAs, 2.30 ms both)
@@ -606,15 +623,17 @@ __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a, const 
     }
   }
 
-  const int k = kt * NT + 32 * cb + l32;
-  if (k < a.K) {
-    constexpr int NOUT = WINO ? 15 : 9;  // ws taps: (xi, kw) / (kh, kw)
+  constexpr int NOUT = WINO ? 15 : 9;  // ws taps: (xi, kw) / (kh, kw)
+#pragma unroll
+  for (int j = 0; j < CB; ++j) {
+    const int k = kt * NTW + 32 * (cb * CB + j) + l32;
+    if (k >= a.K) continue;
 #pragma unroll
     for (int t = 0; t < NTAPS; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int co = ct * MT + 32 * cw + (r & 3) + 8 * (r >> 2) + 4 * kh;
-        a.ws[(((int64_t)p * NOUT + xi * 3 + t) * a.Cout + co) * a.K + k] = acc[t][r];
+        a.ws[(((int64_t)p * NOUT + xi * 3 + t) * a.Cout + co) * a.K + k] = acc[j][t][r];
       }
   }
 }
@@ -1395,12 +1414,14 @@ static int cu_count() {
 
 // Pixel partitions: one workgroup per CU fits (LDS), so P minimises the rounds per unit of
 // work, ceil(tiles * P / CUs) / P, with a small per-partition cost (workspace + reduce).
-static int wgrad_partitions(int64_t tiles, int64_t nchunks) {
+// cost: one partition's workspace write + reduce read in units of a P = 1 round (direct form:
+// 0.004; the Winograd form's rounds are ~4x shorter and its workspace 5/3 larger: 0.07).
+static int wgrad_partitions(int64_t tiles, int64_t nchunks, double cost = 0.004) {
   const int G = std::max(cu_count(), 1);
   int best = 1;
   double best_t = 1e30;
   for (int P = 1; P <= 64 && P <= nchunks; ++P) {
-    const double t = (double)ceil_div(tiles * P, G) / P + 0.004 * P;
+    const double t = (double)ceil_div(tiles * P, G) / P + cost * P;
     if (t < best_t) best_t = t, best = P;
   }
   return best;
@@ -1533,9 +1554,10 @@ static mvbev::bwd::WGeo wgrad_wino_geo(const mvbev_conv_desc* d, int64_t Cout) {
   using namespace mvbev;
   using namespace mvbev::bwd;
   WGeo g;
-  g.tiles = (Cout / MT) * ceil_div(d->K, NT);
+  g.tiles = (Cout / MT) * ceil_div(d->K, 2 * NT);  // 128 input channels per workgroup
   g.nchunks = d->B * ceil_div(d->H, 3) * ceil_div(d->W, PX);
-  g.P = wgrad_partitions(5 * g.tiles, g.nchunks);
+  g.P = wgrad_partitions(5 * g.tiles, g.nchunks, 0.07);
+  if (const char* e = getenv("MVBEV_WGRAD_WINO_P")) g.P = std::max(1, std::min(64, atoi(e)));  // A/B only
   return g;
 }
 
@@ -1560,7 +1582,7 @@ int mvbev_conv3x3_wgrad_wino_bf16x3(const void* t, size_t t_bytes, const mvbev_c
     return MVBEV_ERR_SHAPE;
   if (d->in_row0 != 0 || d->in_rows != d->H || d->out_row0 != 0 || d->out_rows != d->H) return MVBEV_ERR_SHAPE;
   if (!chan_map && d->K > Cin_w) return MVBEV_ERR_SHAPE;
-  if (chunk_list && d->group % NT != 0) return MVBEV_ERR_SHAPE;  // a channel tile inside one group
+  if (chunk_list && d->group % (2 * NT) != 0) return MVBEV_ERR_SHAPE;  // a channel tile inside one group
   constexpr int kRT = 12;  // conv_wino's workgroup tile rows: T holds 4 row tiles (r3) of each
   const int64_t R3 = ceil_div(d->H, 3), r5 = 5 * 4 * ceil_div(d->H, kRT), segs = ceil_div(d->W, PX);
   const int64_t t_need = d->B * (d->K / 8) * r5 * d->W * 32;
@@ -1581,7 +1603,7 @@ int mvbev_conv3x3_wgrad_wino_bf16x3(const void* t, size_t t_bytes, const mvbev_c
   a.group = (int)d->group; a.K = (int)d->K; a.Cout = (int)Cout; a.B = (int)d->B;
   a.H = (int)R3; a.W = (int)d->W;  // the kernel's rows: the 3-row tiles r3
   a.segs = (int)segs; a.nchunks = (int)g.nchunks; a.P = g.P;
-  a.n_ct = (int)(Cout / MT); a.n_kt = (int)ceil_div(d->K, NT); a.ntiles = (int)g.tiles;
+  a.n_ct = (int)(Cout / MT); a.n_kt = (int)ceil_div(d->K, 2 * NT); a.ntiles = (int)g.tiles;
   a.vec_dy = true; a.dy_rows = true;
   a.clist = chunk_list; a.coff = chunk_off;
   hipStream_t s = as_stream(stream);

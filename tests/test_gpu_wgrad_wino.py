@@ -71,12 +71,12 @@ def test_wgrad_wino_vs_torch_and_direct(B, K, H, W):
 
 
 def test_wgrad_wino_grouped_slab_channel_map_and_frustum_lists():
-    """conv1's form: camera slots of 64 channels (view-major, module columns through the channel
+    """conv1's form: camera slots of 128 channels (view-major, module columns through the channel
     map), T written only at a frustum mask's (12 x 32 tile, slot) pairs, chunk lists from that mask;
     the coord columns are untouched."""
     from mvdet_amd import ops
     g = torch.Generator().manual_seed(11)
-    S, B, C, Cs, H, W = 3, 2, 64, 64, 37, 100
+    S, B, C, Cs, H, W = 3, 2, 128, 128, 37, 104
     slab = F.relu(torch.randn((S, B, Cs, H, W), generator=g))
     rects = [(0, 12, 0, 40), (10, 37, 30, 100), (5, 9, 60, 75)]
     for s_, (r0, r1, c0, c1) in enumerate(rects):

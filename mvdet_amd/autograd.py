@@ -9,14 +9,16 @@ slab, conv1-3) and whose backward is all HIP:
 
   conv3 (Cout 1, d4)   dy2 = dgrad(dmap) * [y2 > 0] (conv2's ReLU fused), dw3     (cout1 kernels)
   conv2 (d2) + ReLU    db2, dw2 = wgrad(y1, dy2) (3xbf16 MFMA), dy1 = dgrad-conv(dy2) * [y1 > 0]
-  conv1 (d1) + ReLU    db1 + coord-channel dw1, view-channel dw1 = wgrad(slab, dy1),
-                       dslab = dgrad-conv(dy1) (forward conv kernel on transposed+flipped taps)
+  conv1 (d1) + ReLU    db1 + coord-channel dw1, view-channel dw1 = wgrad(slab, dy1) — from the
+                       forward's row-Winograd transform T of the slab where conv1 ran Winograd
+                       (ABI 12000) — and dslab = dgrad-conv(dy1) (transposed + flipped taps)
   warp                 grad_feat[v] = S_v^T dslab[v]: CSR gather over the transposed
                        sampling matrix (plan built once per geometry; deterministic)
 
-Activations saved for the backward: the slab (the forward's own buffer, split-bf16 with
-3xbf16), y1 and y2 in fp32 (a fresh set per training forward, so a second forward before
-``backward()`` cannot overwrite them).  Parity: gradients within the north_star's 1e-3
+Activations saved for the backward: conv1's input — T when its weight gradient runs from T (the
+fused warp + B^T then writes T and no slab, as in inference), else the slab (split-bf16 with
+3xbf16) — y1 (split-bf16) and y2 in fp32 (a fresh set per training forward, so a second forward
+before ``backward()`` cannot overwrite them).  Parity: gradients within the north_star's 1e-3
 relative fp32 gate of torch's CPU autograd on the same inputs (``tests/test_gpu_backward.py``).
 """
 from __future__ import annotations
@@ -82,6 +84,9 @@ def _train_workspace(engine: ProjectFuse, B: int, device) -> Workspace:
     ws = Workspace(slab, y1, y2, m, (0, H), y1r, y2r, slab_zeroed=zeroed, store_y2=True, slab_rows=(0, H))
     if engine.split:
         ws.wino_t, ws.wino_t2 = t1, t2
+        # conv1's weight gradient from T (_wgrad1_wino) is the backward's only reader of the forward's
+        # conv1 input: the fused warp may write T and skip the slab (one pass, no B^T of the slab)
+        ws.train_t_only = W % 8 == 0 and engine.Cs % 128 == 0 and _native.load().mvbev_version() >= 12000
     return ws
 
 
@@ -331,6 +336,8 @@ class ProjectFuseFunction(torch.autograd.Function):
                            batch_stride=engine.Cs * H * W)
         if _wgrad1_wino_applies(engine, ws, dy1):
             _wgrad1_wino(engine, st, ws, d1, dy1, dw1)
+        elif ws.t_from_warp:
+            raise RuntimeError("conv1's weight gradient needs the slab, but the fused warp wrote only T")
         else:
             ops.conv3x3_wgrad(ws.slab, d1, dy1, 1, w1.shape[1], chan_map=engine.pack1._map_dev, dw=dw1,
                               workspace=_wgrad_ws(st, d1, mid, dev), chunk_lists=_wgrad_lists(engine, st, dev, B),

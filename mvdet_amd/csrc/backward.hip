@@ -825,23 +825,31 @@ __global__ __launch_bounds__(kRedThreads) void bias_coord_grad_kernel(const floa
       v[0] += (a4[0] + a4[1]) + (a4[2] + a4[3]);
       continue;
     }
-#pragma unroll 2
-    for (int q = threadIdx.x; q < HW; q += kRedThreads) {
-      const float gv = g[q];
-      v[0] += gv;
-      const int y = q / W, x = q - y * W;
+    // (loads first in batches of 4 per thread: one in flight measured latency-bound, ~0.13 ms at cfg2)
+    for (int q0 = threadIdx.x; q0 < HW; q0 += 4 * kRedThreads) {
+      float gb[4];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int xx = x + (k - 1) * dil, yy = y + (k - 1) * dil;
-        const bool okx = xx >= 0 && xx < W, oky = yy >= 0 && yy < H;
-        const float cx = okx ? tcx[okx ? xx : 0] : 0.f;
-        const float cy = oky ? tcy[oky ? yy : 0] : 0.f;
+      for (int u = 0; u < 4; ++u) gb[u] = q0 + u * kRedThreads < HW ? g[q0 + u * kRedThreads] : 0.f;
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {  // tap t = 3 r + k (x offset k) and t = 3 k + r (y offset k)
-          const int yr = y + (r - 1) * dil, xr = x + (r - 1) * dil;
-          const bool oky_r = yr >= 0 && yr < H, okx_r = xr >= 0 && xr < W;
-          v[1 + 3 * r + k] += (okx && oky_r) ? gv * cx : 0.f;
-          v[10 + 3 * k + r] += (oky && okx_r) ? gv * cy : 0.f;
+      for (int u = 0; u < 4; ++u) {
+        const int q = q0 + u * kRedThreads;
+        if (q >= HW) break;
+        const float gv = gb[u];
+        v[0] += gv;
+        const int y = q / W, x = q - y * W;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int xx = x + (k - 1) * dil, yy = y + (k - 1) * dil;
+          const bool okx = xx >= 0 && xx < W, oky = yy >= 0 && yy < H;
+          const float cx = okx ? tcx[okx ? xx : 0] : 0.f;
+          const float cy = oky ? tcy[oky ? yy : 0] : 0.f;
+#pragma unroll
+          for (int r = 0; r < 3; ++r) {  // tap t = 3 r + k (x offset k) and t = 3 k + r (y offset k)
+            const int yr = y + (r - 1) * dil, xr = x + (r - 1) * dil;
+            const bool oky_r = yr >= 0 && yr < H, okx_r = xr >= 0 && xr < W;
+            v[1 + 3 * r + k] += (okx && oky_r) ? gv * cx : 0.f;
+            v[10 + 3 * k + r] += (oky && okx_r) ? gv * cy : 0.f;
+          }
         }
       }
     }
@@ -950,18 +958,31 @@ __global__ __launch_bounds__(kRedThreads) void cout1_wgrad_kernel(const float* _
   float v[9];
 #pragma unroll
   for (int t = 0; t < 9; ++t) v[t] = 0.f;
+  // pixels in batches of kC1U per thread: the batch's x and shifted-dmap loads are all issued
+  // before the first product (one load in flight per thread and tap measured 0.25 ms at cfg2:
+  // latency-bound at 2 workgroups per CU)
+  constexpr int kC1U = 4;
   for (int b = 0; b < B; ++b) {
     const float* xc = x + ((int64_t)b * C + c) * HW;
     const float* d = dmap + (int64_t)b * HW;
-#pragma unroll 2
-    for (int q = threadIdx.x; q < HW; q += kRedThreads) {
-      const float xv = xc[q];
-      const int y = q / W, xx = q - y * W;
+    for (int q0 = threadIdx.x; q0 < HW; q0 += kC1U * kRedThreads) {
+      float xv[kC1U], dv[kC1U][9];
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int yy = y - (t / 3 - 1) * dil, xs = xx - (t % 3 - 1) * dil;
-        if (yy >= 0 && yy < H && xs >= 0 && xs < W) v[t] += xv * d[yy * W + xs];
+      for (int u = 0; u < kC1U; ++u) {
+        const int q = q0 + u * kRedThreads;
+        const bool ok = q < HW;
+        const int y = ok ? q / W : -H - 8 * dil, xx = ok ? q - y * W : 0;
+        xv[u] = ok ? xc[q] : 0.f;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int yy = y - (t / 3 - 1) * dil, xs = xx - (t % 3 - 1) * dil;
+          dv[u][t] = (yy >= 0 && yy < H && xs >= 0 && xs < W) ? d[yy * W + xs] : 0.f;
+        }
       }
+#pragma unroll
+      for (int u = 0; u < kC1U; ++u)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) v[t] += xv[u] * dv[u][t];
     }
   }
   block_sum<9, kRedWaves>(v, red);

@@ -72,6 +72,9 @@ class Workspace:
     # wino_t holds this forward's transform of the whole grid (conv1 ran row-Winograd over all rows):
     # the training backward's conv1 weight gradient reads it (autograd._wgrad1_wino)
     t1_valid: bool = False
+    # training forward whose backward reads conv1's T and never the slab (autograd._train_workspace):
+    # the fused warp + B^T may run, as in inference
+    train_t_only: bool = False
     # grid rows the slab holds: (0, Ho) for a warped slab; a row window for a band-local slab
     # filled by the multi-GPU band exchange (parallel.ViewBands)
     slab_rows: Tuple[int, int] = (0, 0)
@@ -311,11 +314,12 @@ class ProjectFuse:
         return self.wino_conv1 and self.nonfinite_views(device) == 0
 
     def _wino_warp_applies(self, ws: Workspace, feats, half_ok: bool = False) -> bool:
-        """The fused warp + B^T applies: inference over the whole grid, fp32 features (or, ``half_ok``:
-        fp16 ones — config 4; ABI 11900), finite geometry."""
+        """The fused warp + B^T applies: inference (or a training forward whose backward reads T, not the
+        slab) over the whole grid, fp32 features (or, ``half_ok``: fp16 ones — config 4; ABI 11900),
+        finite geometry."""
         H = self.grid_hw[0]
         dts = (torch.float32, torch.float16) if half_ok else (torch.float32,)
-        return (self.wino_warp and not ws.store_y2 and ws.y1_rows == (0, H) and ws.slab_zeroed
+        return (self.wino_warp and (not ws.store_y2 or ws.train_t_only) and ws.y1_rows == (0, H) and ws.slab_zeroed
                 and all(f.dtype in dts for f in feats) and len({f.dtype for f in feats}) == 1
                 and self.src_hw[1] >= 2 and self.wino_active(ws.slab.device))
 

@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
   static_assert(!PAIR || std::is_same<T, float>::value, "corner pairs are fp32 8-B loads");
   __shared__ __attribute__((aligned(16))) float ds[kWwRows][kWwCols][8];  // [row][col][channel]
   __shared__ unsigned char nz[kWwRows][kWwCols];
-  __shared__ __attribute__((aligned(16))) float stage[kWwNG * kWarpCPB * (kWwStage > 0 ? kWwStage : 1)];
+  __shared__ __attribute__((aligned(16))) float stage[kWarpCPB * (kWwStage > 0 ? kWwStage : 1)];
   __shared__ int box[4];  // source rows [box0, box1], columns [box2, box3] of the block's corners
   const int lb = xcd_remap(blockIdx.x, a.nwg);
   const int tile = lb % a.tiles;
@@ -242,18 +242,16 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
   const int R = sb.R, Cb = sb.pitch;
   // uniform per block (the staged path needs unit column stride: the non-quad loads assume it too)
   const bool staged = kWwStage > 0 && box[1] >= 0 && vw.sW == 1 && R * Cb <= kWwStage;
-  if (staged) {  // every group's box at once (all loads in flight before the first LDS store)
-    const int cb0 = cblk * kWwNG * kWarpCPB;
-    stage_box_load<kWwThreads, T, kWwNG * kWarpCPB>(base, vw.sC, vw.sH, cb0, min(a.C, cb0 + kWwNG * kWarpCPB), sb,
-                                                     stage, tid);
-    __syncthreads();
-  }
   for (int g = 0; g < kWwNG; ++g) {
   const int chunk = cblk * kWwNG + g;
   const int c_begin = chunk * kWarpCPB;
   if (c_begin >= a.C) break;  // (uniform)
   const int c_end = min(a.C, c_begin + kWarpCPB);
-  if (g > 0) __syncthreads();  // the previous group's phase 2 has read ds
+  if (g > 0) __syncthreads();  // the previous group's phase 2 has read ds (and phase 1 the stage)
+  if (staged) {
+    stage_box_load<kWwThreads, T>(base, vw.sC, vw.sH, c_begin, c_end, sb, stage, tid);
+    __syncthreads();
+  }
   if (i < kWwRows) {  // phase 1: one warped pixel (8 channels) per thread
     float d[8];
 #pragma unroll
@@ -279,7 +277,7 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
           const int l0 = cx0 - sb.c0, l1 = cx1 - sb.c0;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float* sj = stage + (g * kWarpCPB + j) * n;
+            const float* sj = stage + j * n;
             float acc = 0.f;
             acc += (ok_nw ? sj[t0 + l0] : 0.f) * w_nw;
             acc += (ok_ne ? sj[t0 + l1] : 0.f) * w_ne;

@@ -258,20 +258,19 @@ __device__ inline StageBox stage_box_shape(const int (&box)[4], int W, bool quad
 }
 // channel-major staging: stage[j][r][col] (fp32; T = float or __half sources — fp16 stages one element per
 // lane, the quad path is fp32's)
-// (NCH: channels staged per call, all their loads issued before the first LDS store; planes j * n)
-template <int NT, typename T = float, int NCH = 8>
+template <int NT, typename T = float>
 __device__ inline void stage_box_load(const T* __restrict__ base, int64_t sC, int64_t sH, int c_begin, int c_end,
                                       const StageBox& sb, float* __restrict__ stage, int tid) {
   const int n = sb.R * sb.pitch;
   if constexpr (!std::is_same<T, float>::value) {
     for (int r = tid / 32; r < sb.R; r += NT / 32)
       for (int cc = tid % 32; cc < sb.pitch; cc += 32) {
-        float t[NCH];
+        float t[8];
 #pragma unroll
-        for (int j = 0; j < NCH; ++j)
+        for (int j = 0; j < 8; ++j)
           t[j] = to_f32<T>(base[(int64_t)min(c_begin + j, c_end - 1) * sC + (int64_t)(sb.r0 + r) * sH + sb.c0 + cc]);
 #pragma unroll
-        for (int j = 0; j < NCH; ++j) stage[j * n + r * sb.pitch + cc] = t[j];
+        for (int j = 0; j < 8; ++j) stage[j * n + r * sb.pitch + cc] = t[j];
       }
     return;
   } else if (sb.quad) {
@@ -279,22 +278,22 @@ __device__ inline void stage_box_load(const T* __restrict__ base, int64_t sC, in
     for (int it = tid; it < items; it += NT) {
       const int r = it / Q, q = it - r * Q;
       const float* src = base + (int64_t)(sb.r0 + r) * sH + sb.c0 + 4 * q;
-      f32x4a_t t[NCH];
+      f32x4a_t t[8];
 #pragma unroll
-      for (int j = 0; j < NCH; ++j)
+      for (int j = 0; j < 8; ++j)
         t[j] = *reinterpret_cast<const f32x4a_t*>(src + (int64_t)min(c_begin + j, c_end - 1) * sC);
 #pragma unroll
-      for (int j = 0; j < NCH; ++j) *reinterpret_cast<f32x4a_t*>(stage + j * n + r * sb.pitch + 4 * q) = t[j];
+      for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4a_t*>(stage + j * n + r * sb.pitch + 4 * q) = t[j];
     }
   } else {
     for (int r = tid / 32; r < sb.R; r += NT / 32)
       for (int cc = tid % 32; cc < sb.pitch; cc += 32) {
-        float t[NCH];
+        float t[8];
 #pragma unroll
-        for (int j = 0; j < NCH; ++j)
+        for (int j = 0; j < 8; ++j)
           t[j] = base[(int64_t)min(c_begin + j, c_end - 1) * sC + (int64_t)(sb.r0 + r) * sH + sb.c0 + cc];
 #pragma unroll
-        for (int j = 0; j < NCH; ++j) stage[j * n + r * sb.pitch + cc] = t[j];
+        for (int j = 0; j < 8; ++j) stage[j * n + r * sb.pitch + cc] = t[j];
       }
   }
 }

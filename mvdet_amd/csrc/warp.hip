@@ -169,11 +169,6 @@ __global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_tile_kernel(const Warp
 #define MVBEV_WW_STAGE 384  // max staged box pixels per channel (8 channels x 384 x 4 B = 12 KiB); 0 = off
 #endif
 constexpr int kWwStage = MVBEV_WW_STAGE;
-// 8-channel groups per block (the coordinates and the staging box computed once for them)
-#ifndef MVBEV_WW_NG
-#define MVBEV_WW_NG 1
-#endif
-constexpr int kWwNG = MVBEV_WW_NG;
 
 template <bool PAIR, typename T = float>
 __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(const WarpArgs a, int r3_rows) {
@@ -184,12 +179,14 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
   __shared__ int box[4];  // source rows [box0, box1], columns [box2, box3] of the block's corners
   const int lb = xcd_remap(blockIdx.x, a.nwg);
   const int tile = lb % a.tiles;
-  const int cblk = (lb / a.tiles) % a.chunks;  // kWwNG groups of kWarpCPB channels
+  const int chunk = (lb / a.tiles) % a.chunks;
   const int bv = lb / (a.tiles * a.chunks);
   const int view = bv % a.nviews;
   const int b = bv / a.nviews;
   const WarpView& vw = a.v[view];
   const int k = tile / a.tiles_x, tx = tile - k * a.tiles_x;
+  const int c_begin = chunk * kWarpCPB;
+  const int c_end = min(a.C, c_begin + kWarpCPB);
   const int H = a.H, W = a.W;
   const int tid = threadIdx.x;
   const int i = tid / kWwCols, c = tid % kWwCols;  // 16 x kWwCols threads, rows >= 14 idle
@@ -242,12 +239,6 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
   const int R = sb.R, Cb = sb.pitch;
   // uniform per block (the staged path needs unit column stride: the non-quad loads assume it too)
   const bool staged = kWwStage > 0 && box[1] >= 0 && vw.sW == 1 && R * Cb <= kWwStage;
-  for (int g = 0; g < kWwNG; ++g) {
-  const int chunk = cblk * kWwNG + g;
-  const int c_begin = chunk * kWarpCPB;
-  if (c_begin >= a.C) break;  // (uniform)
-  const int c_end = min(a.C, c_begin + kWarpCPB);
-  if (g > 0) __syncthreads();  // the previous group's phase 2 has read ds (and phase 1 the stage)
   if (staged) {
     stage_box_load<kWwThreads, T>(base, vw.sC, vw.sH, c_begin, c_end, sb, stage, tid);
     __syncthreads();
@@ -323,7 +314,6 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
   }
   __syncthreads();
   wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
-  }
 }
 
 // warp_wino_kernel for channels-last sources (round 4: sC == 1, the [B, C, H, W] tensor in torch's
@@ -745,7 +735,7 @@ int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t
     a.tiles_x = (int)ceil_div(Wo, kWcCols);
     a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);
   }
-  a.chunks = (int)ceil_div(C, cl ? kWcCh : kWarpCPB * kWwNG);
+  a.chunks = (int)ceil_div(C, cl ? kWcCh : kWarpCPB);
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
   const dim3 grid((unsigned)a.nwg), block(cl ? kWcThreads : kWwThreads);
   if (cl)

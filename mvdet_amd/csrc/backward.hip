@@ -1359,6 +1359,9 @@ __global__ __launch_bounds__(256) void warp_adjoint_split_kernel(const AdjArgs a
 // PIX pixels x 8 groups per workgroup: 32 for the warp plan (<= 4 entries per source pixel),
 // 16 where source pixels carry many entries (the S.U plan: 0.69 -> 0.58 ms at cfg2; 64: 0.85)
 constexpr int kAsGroups = 8;
+#ifndef MVBEV_ADJ_PPT
+#define MVBEV_ADJ_PPT 1  // source pixels per thread of the plain warp plan's gather (warp_adjoint_split8m_kernel)
+#endif
 template <int PIX>
 __global__ __launch_bounds__(PIX * kAsGroups) void warp_adjoint_split8_kernel(const AdjArgs a) {
   constexpr int kAsPix = PIX;
@@ -1411,6 +1414,85 @@ __global__ __launch_bounds__(PIX * kAsGroups) void warp_adjoint_split8_kernel(co
       float* d = gs + (int64_t)q * vw.sC;
       *d = a.accumulate ? s[q] + *d : s[q];
     }
+}
+
+// The plain warp plan (<= 4 entries per source pixel, no long lists) with PPT source pixels per
+// thread, PIX apart: every pixel's row pointers, then its first 4 (col, val) entries, then their
+// gathers are issued together — the chain rp -> entries -> gather -> store is three dependent
+// round trips, and one pixel per thread left the launch latency-bound (cfg2: 1.03 ms for 1.86 GB
+// of source gradient).  Entries past the first 4 (rare) run the batch-of-8 loop.
+template <int PIX, int PPT>
+__global__ __launch_bounds__(PIX * kAsGroups) void warp_adjoint_split8m_kernel(const AdjArgs a) {
+  const int lb = xcd_remap(blockIdx.x, a.nwg);
+  const int pb = lb % a.pblocks;
+  int r = lb / a.pblocks;
+  const int chunk = r % a.chunks;
+  r /= a.chunks;
+  const int view = r % a.nviews;
+  const int b = r / a.nviews;
+  const int c = (chunk * kAsGroups + threadIdx.x / PIX) * 8;
+  if (c >= a.C) return;
+  const AdjView& vw = a.v[view];
+  const u32x4* g = reinterpret_cast<const u32x4*>(vw.go) + 2 * (int64_t)b * vw.gB + 2 * (int64_t)(c >> 3) * vw.gC;
+  int p[PPT], e0[PPT], e1[PPT];
+#pragma unroll
+  for (int j = 0; j < PPT; ++j) {
+    p[j] = (pb * PPT + j) * PIX + (threadIdx.x & (PIX - 1));
+    const bool ok = p[j] < a.P;
+    e0[j] = ok ? vw.rp[p[j]] : 0;
+    e1[j] = ok ? vw.rp[p[j] + 1] : 0;
+  }
+  int cb[PPT][4];
+  float wb[PPT][4];
+#pragma unroll
+  for (int j = 0; j < PPT; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool ok = e0[j] + q < e1[j];
+      cb[j][q] = ok ? vw.col[e0[j] + q] : 0;
+      wb[j][q] = ok ? vw.val[e0[j] + q] : 0.f;
+    }
+  u32x4 hv[PPT][4], lv[PPT][4];
+#pragma unroll
+  for (int j = 0; j < PPT; ++j)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (e0[j] + q < e1[j]) {
+        hv[j][q] = g[2 * (int64_t)cb[j][q]];
+        lv[j][q] = g[2 * (int64_t)cb[j][q] + 1];
+      }
+  float s[PPT][8];
+#pragma unroll
+  for (int j = 0; j < PPT; ++j) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[j][k] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (e0[j] + q < e1[j]) {
+        const bf16x8 hi = __builtin_bit_cast(bf16x8, hv[j][q]), lo = __builtin_bit_cast(bf16x8, lv[j][q]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s[j][k] += wb[j][q] * ((float)hi[k] + (float)lo[k]);
+      }
+    for (int eb = e0[j] + 4; eb < e1[j]; ++eb) {  // (rare) further entries, in order
+      const u32x4 h = g[2 * (int64_t)vw.col[eb]], l = g[2 * (int64_t)vw.col[eb] + 1];
+      const float w = vw.val[eb];
+      const bf16x8 hi = __builtin_bit_cast(bf16x8, h), lo = __builtin_bit_cast(bf16x8, l);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s[j][k] += w * ((float)hi[k] + (float)lo[k]);
+    }
+  }
+  const int nq = min(8, a.C - c);
+#pragma unroll
+  for (int j = 0; j < PPT; ++j) {
+    if (p[j] >= a.P) continue;
+    float* gs = vw.gs + (int64_t)b * vw.sB + (int64_t)c * vw.sC + p[j];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k < nq) {
+        float* d = gs + (int64_t)k * vw.sC;
+        *d = a.accumulate ? s[j][k] + *d : s[j][k];
+      }
+  }
 }
 
 // fp32 rows [n][W] -> MVBEV_LAYOUT_SPLIT_ROWS [n][W / 8][hi 8, lo 8] (W % 8 == 0), the rounding
@@ -1812,7 +1894,8 @@ int mvbev_warp_views_adjoint(const mvbev_warp_adjoint_view* views, int nviews, i
   const bool g8 = split && MVBEV_ADJ_G8;
   // many entries per source pixel (a source smaller than the grid: the S.U plan): 16 pixels
   const int pix = H * W < Ho * Wo ? 16 : 32;
-  a.pblocks = (int)ceil_div(H * W, g8 ? pix : 256);
+  constexpr int kPpt = MVBEV_ADJ_PPT;  // source pixels per thread of the plain plan's gather
+  a.pblocks = (int)ceil_div(H * W, g8 ? pix * (pix == 32 ? kPpt : 1) : 256);
   a.chunks = (int)ceil_div(C, g8 ? 8 * bwd::kAsGroups : bwd::kAdjCPB);
   a.accumulate = accumulate ? 1 : 0;
   const int64_t nwg = (int64_t)a.pblocks * a.chunks * nviews * B;
@@ -1822,6 +1905,9 @@ int mvbev_warp_views_adjoint(const mvbev_warp_adjoint_view* views, int nviews, i
     if (pix == 16)
       hipLaunchKernelGGL(bwd::warp_adjoint_split8_kernel<16>, dim3((unsigned)nwg), dim3(16 * bwd::kAsGroups), 0,
                          as_stream(stream), a);
+    else if (kPpt > 1)
+      hipLaunchKernelGGL((bwd::warp_adjoint_split8m_kernel<32, kPpt>), dim3((unsigned)nwg), dim3(32 * bwd::kAsGroups),
+                         0, as_stream(stream), a);
     else
       hipLaunchKernelGGL(bwd::warp_adjoint_split8_kernel<32>, dim3((unsigned)nwg), dim3(32 * bwd::kAsGroups), 0,
                          as_stream(stream), a);

@@ -1360,7 +1360,7 @@ __global__ __launch_bounds__(256) void warp_adjoint_split_kernel(const AdjArgs a
 // 16 where source pixels carry many entries (the S.U plan: 0.69 -> 0.58 ms at cfg2; 64: 0.85)
 constexpr int kAsGroups = 8;
 #ifndef MVBEV_ADJ_PPT
-#define MVBEV_ADJ_PPT 1  // source pixels per thread of the plain warp plan's gather (warp_adjoint_split8m_kernel)
+#define MVBEV_ADJ_PPT 2  // source pixels per thread of the plain warp plan's gather (warp_adjoint_split8m_kernel; cfg2: 1 0.945 ms, 2 0.886, 4 1.19)
 #endif
 template <int PIX>
 __global__ __launch_bounds__(PIX * kAsGroups) void warp_adjoint_split8_kernel(const AdjArgs a) {

@@ -778,13 +778,17 @@ __device__ inline void block_sum(float (&v)[NV], float* red /* LDS [NWV_][NV] */
 #pragma unroll
     for (int j = 0; j < NV; ++j) red[wave * NV + j] = v[j];
   __syncthreads();
+  // thread j < NV sums column j over the waves (thread 0 summing all NV x NWV_ values had the
+  // compiler hoist every LDS load: 300+ registers and scratch spills at NV = 19)
+  if (threadIdx.x < NV) {
+    float t = 0.f;
+    for (int w = 0; w < NWV_; ++w) t += red[w * NV + threadIdx.x];
+    red[threadIdx.x] = t;
+  }
+  __syncthreads();
   if (threadIdx.x == 0)
 #pragma unroll
-    for (int j = 0; j < NV; ++j) {
-      float t = 0.f;
-      for (int w = 0; w < NWV_; ++w) t += red[w * NV + j];
-      v[j] = t;
-    }
+    for (int j = 0; j < NV; ++j) v[j] = red[j];
 }
 
 // The per-channel reductions below (one workgroup per output channel, 512 of them at the
@@ -825,34 +829,59 @@ __global__ __launch_bounds__(kRedThreads) void bias_coord_grad_kernel(const floa
       v[0] += (a4[0] + a4[1]) + (a4[2] + a4[3]);
       continue;
     }
-    // (loads first in batches of 4 per thread: one in flight measured latency-bound, ~0.13 ms at cfg2)
-    for (int q0 = threadIdx.x; q0 < HW; q0 += 4 * kRedThreads) {
-      float gb[4];
+    // separable form: per row y, Rx[kx] = sum_x dy cx(x + (kx - 1) dil) and Sx[kx] = sum_x dy [x + (kx - 1)
+    // dil inside] (a wave per row, lanes along x, 4 loads in flight per lane), then
+    //   dw_x[ky][kx] += [y + (ky - 1) dil inside] Rx[kx],  dw_y[ky][kx] += cy(y + (ky - 1) dil) Sx[kx]
+    // (a thread per pixel accumulating the 19 sums with their bounds took 0.13 ms at cfg2)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll 1
+    for (int y = wave; y < H; y += kRedWaves) {
+      const float* row = g + (int64_t)y * W;
+      float rx[3] = {0.f, 0.f, 0.f}, sx[3] = {0.f, 0.f, 0.f};
+#pragma unroll 1
+      for (int x0 = 0; x0 < W; x0 += 4 * 64) {
+        float gv[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) gb[u] = q0 + u * kRedThreads < HW ? g[q0 + u * kRedThreads] : 0.f;
+        for (int u = 0; u < 4; ++u) {
+          const int x = x0 + 64 * u + lane;
+          gv[u] = x < W ? row[x] : 0.f;
+        }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int q = q0 + u * kRedThreads;
-        if (q >= HW) break;
-        const float gv = gb[u];
-        v[0] += gv;
-        const int y = q / W, x = q - y * W;
+        for (int u = 0; u < 4; ++u) {
+          const int x = x0 + 64 * u + lane;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const int xx = x + (k - 1) * dil, yy = y + (k - 1) * dil;
-          const bool okx = xx >= 0 && xx < W, oky = yy >= 0 && yy < H;
-          const float cx = okx ? tcx[okx ? xx : 0] : 0.f;
-          const float cy = oky ? tcy[oky ? yy : 0] : 0.f;
-#pragma unroll
-          for (int r = 0; r < 3; ++r) {  // tap t = 3 r + k (x offset k) and t = 3 k + r (y offset k)
-            const int yr = y + (r - 1) * dil, xr = x + (r - 1) * dil;
-            const bool oky_r = yr >= 0 && yr < H, okx_r = xr >= 0 && xr < W;
-            v[1 + 3 * r + k] += (okx && oky_r) ? gv * cx : 0.f;
-            v[10 + 3 * k + r] += (oky && okx_r) ? gv * cy : 0.f;
+          for (int k = 0; k < 3; ++k) {
+            const int xx = x + (k - 1) * dil;
+            const bool okx = xx >= 0 && xx < W;
+            rx[k] += okx ? gv[u] * tcx[okx ? xx : 0] : 0.f;
+            sx[k] += okx ? gv[u] : 0.f;
           }
         }
       }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          rx[k] += __shfl_xor(rx[k], o);
+          sx[k] += __shfl_xor(sx[k], o);
+        }
+      v[0] += sx[1];
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int yy = y + (ky - 1) * dil;
+        const bool oky = yy >= 0 && yy < H;
+        const float cy = oky ? tcy[oky ? yy : 0] : 0.f;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          v[1 + 3 * ky + kx] += oky ? rx[kx] : 0.f;
+          v[10 + 3 * ky + kx] += cy * sx[kx];
+        }
+      }
     }
+  }
+  if (dw && (threadIdx.x & 63) != 0) {  // every lane of a wave holds its sums: count them once
+#pragma unroll
+    for (int j = 0; j < 19; ++j) v[j] = 0.f;
   }
   block_sum<19, kRedWaves>(v, red);
   if (threadIdx.x == 0) {

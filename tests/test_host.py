@@ -232,8 +232,10 @@ def test_hot_kernels_use_no_scratch():
     res = sorted((ROOT / "build" / "obj").glob("*.o.res"))
     if not res:
         pytest.skip("no build resource reports (build with make -C mvdet_amd/csrc)")
-    hot = re.compile(r"conv_ring_kernel|conv_wino_kernel|wino_rows_kernel|warp_wino|warp_up_wino|"
-                     r"cout1|wgrad|dgrad|warp_tile_kernel|warp_exact")
+    # every kernel but the register-tiled bf16x3 conv (b3::conv_kernel: the fallback form, no longer on
+    # the product path, keeps a 12-36 B spill); round 5 found the bias / coord-gradient reduction
+    # spilling 676 B per lane (block_sum's hoisted LDS loads), 2x slower, outside the old list
+    legacy = re.compile(r"2b311conv_kernel")
     seen, bad = 0, []
     for f in res:
         name = None
@@ -243,7 +245,7 @@ def test_hot_kernels_use_no_scratch():
                 name = m.group(1)
                 continue
             m = re.search(r"ScratchSize \[bytes/lane\]: (\d+)", line)
-            if m and name and hot.search(name):
+            if m and name and not legacy.search(name):
                 seen += 1
                 if int(m.group(1)):
                     bad.append((f.name, name, int(m.group(1))))

@@ -233,8 +233,8 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
   }
   __syncthreads();
   const T* base = static_cast<const T*>(vw.src) + (int64_t)b * vw.sB;
-  const bool quad_ok = std::is_same<T, float>::value && vw.sW == 1 && (W & 3) == 0 && (vw.sH & 3) == 0 &&
-                       (vw.sC & 3) == 0 && (reinterpret_cast<uintptr_t>(base) & 15) == 0;
+  const bool quad_ok = vw.sW == 1 && (W & 3) == 0 && (vw.sH & 3) == 0 && (vw.sC & 3) == 0 &&
+                       (reinterpret_cast<uintptr_t>(base) & (4 * sizeof(T) - 1)) == 0;
   const StageBox sb = stage_box_shape(box, W, quad_ok);  // 16-B staging loads where the source allows
   const int R = sb.R, Cb = sb.pitch;
   // uniform per block (the staged path needs unit column stride: the non-quad loads assume it too)

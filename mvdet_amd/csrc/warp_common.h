@@ -256,13 +256,30 @@ __device__ inline StageBox stage_box_shape(const int (&box)[4], int W, bool quad
   sb.pitch = c1 - sb.c0;
   return sb;
 }
-// channel-major staging: stage[j][r][col] (fp32; T = float or __half sources — fp16 stages one element per
-// lane, the quad path is fp32's)
+// channel-major staging: stage[j][r][col] (fp32; T = float or __half sources; quad: 16-B fp32 / 8-B fp16
+// loads of 4 columns where the source's strides and alignment allow)
 template <int NT, typename T = float>
 __device__ inline void stage_box_load(const T* __restrict__ base, int64_t sC, int64_t sH, int c_begin, int c_end,
                                       const StageBox& sb, float* __restrict__ stage, int tid) {
   const int n = sb.R * sb.pitch;
   if constexpr (!std::is_same<T, float>::value) {
+    if (sb.quad) {  // 4 halves (8 B) per lane and channel, widened to one 16-B LDS store
+      const int Q = sb.pitch >> 2, items = sb.R * Q;
+      for (int it = tid; it < items; it += NT) {
+        const int r = it / Q, q = it - r * Q;
+        const T* src = base + (int64_t)(sb.r0 + r) * sH + sb.c0 + 4 * q;
+        uint2 t[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] = *reinterpret_cast<const uint2*>(src + (int64_t)min(c_begin + j, c_end - 1) * sC);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const T* h = reinterpret_cast<const T*>(&t[j]);
+          const f32x4a_t f = {to_f32<T>(h[0]), to_f32<T>(h[1]), to_f32<T>(h[2]), to_f32<T>(h[3])};
+          *reinterpret_cast<f32x4a_t*>(stage + j * n + r * sb.pitch + 4 * q) = f;
+        }
+      }
+      return;
+    }
     for (int r = tid / 32; r < sb.R; r += NT / 32)
       for (int cc = tid % 32; cc < sb.pitch; cc += 32) {
         float t[8];

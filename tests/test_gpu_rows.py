@@ -148,3 +148,27 @@ def test_zero_gated():
     flag.fill_(2)
     ops.zero_gated_(t, (flag, 2))
     assert bool((t == 0).all())
+
+
+@pytest.mark.parametrize("W_src", [384, 376])  # source width 96 (8-B quad staging loads) and 94 (element path)
+def test_fused_warp_fp16_sources_equal_fp32_upcast(W_src):
+    """``warp_views_wino_rows_into`` on fp16 features (config 4's path) writes bitwise the T of the same
+    features upcast to fp32: fp32 arithmetic after the load in both, the same staged box (its 8-B fp16
+    quad loads widen to the 16-B fp32 layout)."""
+    from mvdet_amd import ops, synthetic
+    from mvdet_amd.geometry import kornia_src_norm_from_dst_norm, projection_matrices
+    ds = synthetic.wildtrack_like(3, 4, seed=9, img_shape=(216, W_src), worldgrid_shape=(128, 288))
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    ms = [kornia_src_norm_from_dst_norm(M.float().reshape(1, 3, 3), up, grid)[0] for M in projection_matrices(ds)]
+    B, C = 2, 16
+    f16 = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=40 + v, device=DEV).half()
+           for v in range(3)]
+    H, W = grid
+    K = 3 * C
+    d = ops.conv_desc(B, K, H, W, group=C, group_stride=B * C * H * W, batch_stride=C * H * W)
+    ta = torch.zeros((ops.wino_rows_bytes(d) + 1) // 2, dtype=torch.bfloat16, device=DEV)
+    tb = torch.zeros_like(ta)
+    ops.warp_views_wino_rows_into(f16, ms, ta, [0, 1, 2], C, K, H, W)
+    ops.warp_views_wino_rows_into([f.float() for f in f16], ms, tb, [0, 1, 2], C, K, H, W)
+    assert torch.equal(ta, tb)
+    assert ta.abs().sum() > 0

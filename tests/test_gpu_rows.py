@@ -151,10 +151,11 @@ def test_zero_gated():
 
 
 @pytest.mark.parametrize("W_src", [384, 376])  # source width 96 (8-B quad staging loads) and 94 (element path)
-def test_fused_warp_fp16_sources_equal_fp32_upcast(W_src):
-    """``warp_views_wino_rows_into`` on fp16 features (config 4's path) writes bitwise the T of the same
-    features upcast to fp32: fp32 arithmetic after the load in both, the same staged box (its 8-B fp16
-    quad loads widen to the 16-B fp32 layout)."""
+def test_fused_warp_fp16_sources_match_fp32_upcast(W_src):
+    """``warp_views_wino_rows_into`` on fp16 features (config 4's path) writes the T of the same features
+    upcast to fp32: fp32 arithmetic after the load in both (its 8-B fp16 quad loads widen to the 16-B fp32
+    staging layout).  Not bitwise: the two kernel instantiations contract the bilinear sums into FMAs
+    differently, so ~0.5 % of the transformed values differ by an fp32 ulp before the hi / lo split."""
     from mvdet_amd import ops, synthetic
     from mvdet_amd.geometry import kornia_src_norm_from_dst_norm, projection_matrices
     ds = synthetic.wildtrack_like(3, 4, seed=9, img_shape=(216, W_src), worldgrid_shape=(128, 288))
@@ -170,5 +171,11 @@ def test_fused_warp_fp16_sources_equal_fp32_upcast(W_src):
     tb = torch.zeros_like(ta)
     ops.warp_views_wino_rows_into(f16, ms, ta, [0, 1, 2], C, K, H, W)
     ops.warp_views_wino_rows_into([f.float() for f in f16], ms, tb, [0, 1, 2], C, K, H, W)
-    assert torch.equal(ta, tb)
-    assert ta.abs().sum() > 0
+    R5 = 5 * 4 * (-(-H // 12))
+    n = B * (K // 8) * R5 * 2 * W * 8
+    va = ta[:n].float().view(B, K // 8, R5, 2, W, 8).sum(3)  # hi + lo
+    vb = tb[:n].float().view(B, K // 8, R5, 2, W, 8).sum(3)
+    scale = float(vb.abs().max())
+    assert scale > 0
+    # an fp32-ulp difference of a transformed value can flip its hi / lo split: hi + lo keeps ~16 bits
+    assert float((va - vb).abs().max()) <= 1e-5 * scale

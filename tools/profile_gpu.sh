@@ -13,7 +13,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 cd $R
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_trace -o run -- \
-  python3 bench.py --steps 10 --warmup 3 --config $CFG --no-cpu-baseline --no-train --no-alt --north-star-cfg 0 --roofline-cfg 0 --batch-cfg 0 \
+  python3 bench.py --steps 10 --warmup 3 --config $CFG --no-cpu-baseline --no-train --no-alt --no-probe --north-star-cfg 0 --roofline-cfg 0 --batch-cfg 0 \
   > $OUT/${TAG}_trace_bench.log 2>&1 || exit $?
 i=0
 for PMC in "GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU" \
@@ -28,6 +28,6 @@ python3 tools/pmc_summary.py $OUT/${TAG}_pmc* > $OUT/${TAG}_pmc_summary.txt
 python3 tools/traffic.py $OUT $TAG $CFG bf16x3 wino > $OUT/${TAG}_traffic.json
 # the kernel trace of the BASELINE "rocprof roofline run" config (cfg5: 8 views at 4K -> 1000 x 1000)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${TAG}_trace_cfg5 -o run -- \
-  python3 bench.py --steps 5 --warmup 2 --config 5 --no-cpu-baseline --no-train --no-alt --north-star-cfg 0 --batch-cfg 0 \
+  python3 bench.py --steps 5 --warmup 2 --config 5 --no-cpu-baseline --no-train --no-alt --no-probe --north-star-cfg 0 --batch-cfg 0 \
   --roofline-cfg 0 > $OUT/${TAG}_trace_cfg5_bench.log 2>&1 || exit $?
 echo profile-done

@@ -1689,7 +1689,6 @@ static mvbev::bwd::WGeo wgrad_wino_geo(const mvbev_conv_desc* d, int64_t Cout) {
   g.tiles = (Cout / MT) * ceil_div(d->K, 2 * NT);  // 128 input channels per workgroup
   g.nchunks = d->B * ceil_div(d->H, 3) * ceil_div(d->W, PX);
   g.P = wgrad_partitions(5 * g.tiles, g.nchunks, 0.07);
-  if (const char* e = getenv("MVBEV_WGRAD_WINO_P")) g.P = std::max(1, std::min(64, atoi(e)));  // A/B only
   return g;
 }
 

@@ -120,6 +120,7 @@ struct Args {
   // stay on one XCD (they share the halo reads)
   const int32_t* tile_order;
   int npix;
+  int mgroup;    // row-Winograd conv: consecutive ordered pixel tiles per XCD turn (MVBEV_MASK_GROUP's runtime form)
   bool y_split;  // y in the split-bf16 blocked layout (the next conv's 16-B staging copies)
   // output-side mask (optional, dgrad of the fused conv): per output tile, bit g clear =
   // output channel group g (cot_pg Cout tiles each) is never read, so its tiles are skipped
@@ -1485,8 +1486,8 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   const int l32 = lane & 31, kl = lane >> 5;
 
   int tile = xcd_remap(blockIdx.x, a.nwg);
-  if (a.gmask) {  // ordered pixel tiles dealt to the XCDs, as the ring kernel
-    constexpr int Gq = MVBEV_MASK_GROUP;
+  if (a.gmask) {  // ordered pixel tiles dealt to the XCDs, as the ring kernel (groups of a.mgroup)
+    const int Gq = a.mgroup;
     const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
     const int q = j / a.n_cot;
     const int slot = Gq * (8 * (q / Gq) + x) + q % Gq;
@@ -1795,7 +1796,12 @@ static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_pa
   if (band_rows < 0 || (band_rows > 0 && (a.y_split || p3 || band_rows > d->out_rows))) return MVBEV_ERR_SHAPE;
   a.band_rows = (int)band_rows;
   a.npix = (int)(tiles / a.n_cot);
-  const int64_t nwg = group_mask ? (int64_t)a.n_cot * round_up(a.npix, 8 * MVBEV_MASK_GROUP) : tiles;
+  // XCD turns of 8 consecutive ordered pixel tiles (equal view sets: the same weight-chunk stream, shared in
+  // the XCD's L2) once the launch is >= 8 rounds deep; shallower launches deal them one at a time, where
+  // the balance of the first rounds decides (cfg2, 1.9 rounds: groups of 4 +7 %; cfg5, 42 rounds: 8 -5 %,
+  // cfg3 -2 %: profiles/r05o_mask_group_ab.jsonl, r05v_mask_group_large_ab.jsonl)
+  a.mgroup = (group_mask && tiles >= 8 * (int64_t)std::max(cu_count(), 1)) ? 8 : 1;
+  const int64_t nwg = group_mask ? (int64_t)a.n_cot * round_up(a.npix, 8 * a.mgroup) : tiles;
   a.nwg = (int)nwg;
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)nwg), blk(RNT);

@@ -265,3 +265,26 @@ def test_design_cost_model_table_is_current():
     assert len(rows) == 18  # header + 4 configs x 4 rank counts + config 4 at P = 6
     for row in rows:
         assert row in design, row
+
+
+def test_wgrad_chunk_lists_match_brute_force():
+    """Host planning of the conv1 weight gradients' frustum chunk lists: the direct form's (row y,
+    32-px segment) chunks of 8-row tiles and the Winograd form's (3-row tile r3, segment) chunks of
+    the 12-row mask T was written under, per channel group, against a brute-force enumeration."""
+    from mvdet_amd import ops
+    rng = np.random.default_rng(4)
+    B, H, W, groups = 2, 37, 104, 3
+    tx = -(-W // 32)
+    for tile_h, lister, rows in ((_native.TILE_H, ops.wgrad_chunk_lists, H),
+                                 (12, ops.wgrad_wino_chunk_lists, -(-H // 3))):
+        ty = -(-H // tile_h)
+        mask = torch.tensor(rng.integers(0, 1 << groups, ty * tx), dtype=torch.int32)
+        lst, off = lister(mask, groups, B, H, W)
+        lst, off = lst.tolist(), off.tolist()
+        rows_per_tile = tile_h if lister is ops.wgrad_chunk_lists else 4  # 3-row tiles r3 per 12-row tile
+        for g in range(groups):
+            want = [b * rows * tx + r * tx + s for b in range(B) for r in range(rows) for s in range(tx)
+                    if (int(mask[(r // rows_per_tile) * tx + s]) >> g) & 1]
+            assert lst[off[g]:off[g + 1]] == want, (lister.__name__, g)
+    with pytest.raises(ValueError):
+        ops.wgrad_wino_chunk_lists(torch.zeros(5, dtype=torch.int32), groups, B, H, W)

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 12000: conv1's weight gradient from the forward's row-Winograd transform (mvbev_wino_dy_rows_f32, mvbev_conv3x3_wgrad_wino_bf16x3); 11900: row windows (mvbev_warp_views_split_bf16_rows with the non-finite report, mvbev_warp_views_exact_rows with fp16 sources), mvbev_conv3x3_f32_ex (row-band output), mvbev_bias_relu_nonfinite_f32, mvbev_zero_gated — the non-finite guard of the multi-GPU modes and the banded exact path; 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 12000: conv1's and conv2's weight gradients from the forward's row-Winograd transforms (mvbev_wino_dy_rows_f32, mvbev_conv3x3_wgrad_wino_bf16x3); 11900: row windows (mvbev_warp_views_split_bf16_rows with the non-finite report, mvbev_warp_views_exact_rows with fp16 sources), mvbev_conv3x3_f32_ex (row-band output), mvbev_bias_relu_nonfinite_f32, mvbev_zero_gated — the non-finite guard of the multi-GPU modes and the banded exact path; 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -623,26 +623,29 @@ int mvbev_conv3x3_wgrad_bf16x3_ex2(const void* x, int x_layout, const mvbev_conv
                                    const int32_t* chunk_list, const int32_t* chunk_off, void* workspace,
                                    size_t workspace_bytes, void* stream);
 
-/* Row-Winograd weight gradient of a dilation-1 3x3 conv (ABI 12000; conv1, persp_trans_detector.py:51,
- * whose forward ran mvbev_conv3x3_wino_bf16x3).  With the forward's y = A^T[(G w) . (B^T d)] per 3-row
- * tile r3 (conv_bf16x3.hip), dW[co][ci][kh][kw] = sum_xi G[xi][kh] M_xi[kw] where
- *   M_xi[kw][co][ci] = sum_{b, r3, x} D_xi[co][r3][x] T_xi[ci][r3][x + kw - 1],  D_xi = sum_j AT[j][xi] dy[3 r3 + j]:
- * t is the forward's transform (mvbev_wino_rows_split_bf16 / the fused warp's T, t_bytes of it), dy_wino
- * is D (mvbev_wino_dy_rows_f32), and the products run 3xbf16 as in mvbev_conv3x3_wgrad_bf16x3_ex2, whose
- * arguments the others mean (chunk lists: chunk (b * ceil(H / 3) + r3) * ceil(W / 32) + x / 32 where
- * T_xi of group g can be non-zero — the forward's 12-row frustum mask, tile r3 / 4).  x0.556 of the
- * direct form's MFMAs; W % 8 == 0, desc over all rows, 128-channel groups with chunk lists.  workspace:
+/* Row-Winograd weight gradient of a 3x3 conv of dilation 1 or 2 (ABI 12000; conv1 / conv2 of
+ * map_classifier, persp_trans_detector.py:51, 53, whose forward ran mvbev_conv3x3_wino_bf16x3[_dil]).  With
+ * the forward's y = A^T[(G w) . (B^T d)] per 3-row tile r3 (conv_bf16x3.hip), dW[co][ci][kh][kw] =
+ * sum_xi G[xi][kh] M_xi[kw] where
+ *   M_xi[kw][co][ci] = sum_{b, r3, x} D_xi[co][r3][x] T_xi[ci][r3][x + dil (kw - 1)],
+ *   D_xi = sum_j AT[j][xi] dy[base(r3) + dil j]  (base: the forward's row tiles — 3 r3, or conv2's interleaved ones):
+ * t is the forward's transform (mvbev_wino_rows_split_bf16[_dil] / the fused warp's T, t_bytes of it),
+ * dy_wino is D (mvbev_wino_dy_rows_f32 of the same dilation), and the products run 3xbf16 as in
+ * mvbev_conv3x3_wgrad_bf16x3_ex2, whose arguments the others mean (chunk lists: chunk (b * R3 + r3) *
+ * ceil(W / 32) + x / 32 where T_xi of group g can be non-zero — the forward's 12-row frustum mask, tile
+ * r3 / 4; R3 = ceil(H / 3) for dilation 1, 4 ceil(H / 12) for dilation 2).  x0.556 of the direct form's
+ * MFMAs; W % 8 == 0, desc over all rows, 128-channel groups with chunk lists.  workspace:
  * mvbev_conv3x3_wgrad_wino_workspace_bytes. */
-size_t mvbev_wino_dy_rows_bytes(int64_t B, int64_t Cout, int64_t H, int64_t W);
-/* D[b][xi][co][r3] (r3 < ceil(H / 3), rows past H zero) of fp32 dy [B][Cout][H][W] in
- * MVBEV_LAYOUT_SPLIT_ROWS; AT = [1 1 1 1 0; 0 1 -1 2 0; 0 1 1 4 1]; W % 8 == 0, 16-B aligned. */
-int mvbev_wino_dy_rows_f32(const float* dy, int64_t B, int64_t Cout, int64_t H, int64_t W, void* out,
-                           size_t out_bytes, void* stream);
-size_t mvbev_conv3x3_wgrad_wino_workspace_bytes(const mvbev_conv_desc* desc, int64_t Cout);
+size_t mvbev_wino_dy_rows_bytes(int64_t B, int64_t Cout, int64_t H, int64_t W, int dilation);
+/* D[b][xi][co][r3] (r3 < R3, rows past H zero) of fp32 dy [B][Cout][H][W] in MVBEV_LAYOUT_SPLIT_ROWS;
+ * AT = [1 1 1 1 0; 0 1 -1 2 0; 0 1 1 4 1]; W % 8 == 0, 16-B aligned. */
+int mvbev_wino_dy_rows_f32(const float* dy, int64_t B, int64_t Cout, int64_t H, int64_t W, int dilation,
+                           void* out, size_t out_bytes, void* stream);
+size_t mvbev_conv3x3_wgrad_wino_workspace_bytes(const mvbev_conv_desc* desc, int64_t Cout, int dilation);
 int mvbev_conv3x3_wgrad_wino_bf16x3(const void* t, size_t t_bytes, const mvbev_conv_desc* desc, const void* dy_wino,
-                                    size_t dy_wino_bytes, int64_t Cout, const int32_t* chan_map, int64_t Cin_w,
-                                    float* dw, const int32_t* chunk_list, const int32_t* chunk_off, void* workspace,
-                                    size_t workspace_bytes, void* stream);
+                                    size_t dy_wino_bytes, int64_t Cout, int dilation, const int32_t* chan_map,
+                                    int64_t Cin_w, float* dw, const int32_t* chunk_list, const int32_t* chunk_off,
+                                    void* workspace, size_t workspace_bytes, void* stream);
 
 /* fp32 rows x [rows][W] (16-B aligned, W % 8 == 0) -> out [rows][W / 8] pieces of bf16 hi[8],
  * lo[8] (MVBEV_LAYOUT_SPLIT_ROWS; hi = bf16(x) round-to-nearest-even, lo = bf16(x - hi)). */

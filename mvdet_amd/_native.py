@@ -93,6 +93,7 @@ WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
 WARP_SRC_F16 = 2  # MVBEV_WARP_SRC_F16 (mvbev_warp_views_wino_rows, ABI 11900)
 TILES_GRID, TILES_EDGE_STRIP = 0, 1  # MVBEV_TILES_*
 ERR_SHAPE = -2  # MVBEV_ERR_SHAPE
+ERR_DILATION = -6  # MVBEV_ERR_DILATION
 
 KC = 8    # MVBEV_CONV_KC
 LAYOUT_F32, LAYOUT_F16, LAYOUT_SPLIT_BF16, LAYOUT_SPLIT_ROWS = 0, 1, 2, 3  # MVBEV_LAYOUT_*
@@ -282,14 +283,14 @@ def _declare(lib):
     lib.mvbev_split_rows_bf16.restype = ctypes.c_int
     lib.mvbev_split_rows_bf16.argtypes = [_p, _i64, _i64, _p, _p]
     lib.mvbev_wino_dy_rows_bytes.restype = ctypes.c_size_t
-    lib.mvbev_wino_dy_rows_bytes.argtypes = [_i64, _i64, _i64, _i64]
+    lib.mvbev_wino_dy_rows_bytes.argtypes = [_i64, _i64, _i64, _i64, ctypes.c_int]
     lib.mvbev_wino_dy_rows_f32.restype = ctypes.c_int
-    lib.mvbev_wino_dy_rows_f32.argtypes = [_p, _i64, _i64, _i64, _i64, _p, ctypes.c_size_t, _p]
+    lib.mvbev_wino_dy_rows_f32.argtypes = [_p, _i64, _i64, _i64, _i64, ctypes.c_int, _p, ctypes.c_size_t, _p]
     lib.mvbev_conv3x3_wgrad_wino_workspace_bytes.restype = ctypes.c_size_t
-    lib.mvbev_conv3x3_wgrad_wino_workspace_bytes.argtypes = [ctypes.POINTER(ConvDesc), _i64]
+    lib.mvbev_conv3x3_wgrad_wino_workspace_bytes.argtypes = [ctypes.POINTER(ConvDesc), _i64, ctypes.c_int]
     lib.mvbev_conv3x3_wgrad_wino_bf16x3.restype = ctypes.c_int
     lib.mvbev_conv3x3_wgrad_wino_bf16x3.argtypes = [_p, ctypes.c_size_t, ctypes.POINTER(ConvDesc), _p, ctypes.c_size_t,
-                                                    _i64, _p, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]
+                                                    _i64, ctypes.c_int, _p, _i64, _p, _p, _p, _p, ctypes.c_size_t, _p]
     lib.mvbev_conv_schedule_slot_bytes.restype = ctypes.c_size_t
     lib.mvbev_conv_schedule_slot_bytes.argtypes = []
     lib.mvbev_conv3x3_dgrad_bf16x3_sched.restype = ctypes.c_int

@@ -80,7 +80,13 @@ def _train_workspace(engine: ProjectFuse, B: int, device) -> Workspace:
     else:
         y1 = torch.empty((B, engine.mid, H, W), dtype=torch.float32, device=device)
     y2 = torch.empty((B, engine.mid, H, W), dtype=torch.float32, device=device)
-    m = engine.m_norm_cpu.to(device)[:, None].expand(engine.num_cam, B, 3, 3).contiguous()
+    # the per-view device matrices (geometry only): cached, since a pageable host -> device copy per step
+    # makes the host wait for the stream to drain (~0.1-0.25 ms of idle GPU per training step)
+    mkey = (str(torch.device(device)), int(B))
+    m = engine.__dict__.setdefault("_train_m", {}).get(mkey)
+    if m is None:
+        m = engine.m_norm_cpu.to(device)[:, None].expand(engine.num_cam, B, 3, 3).contiguous()
+        engine._train_m[mkey] = m
     ws = Workspace(slab, y1, y2, m, (0, H), y1r, y2r, slab_zeroed=zeroed, store_y2=True, slab_rows=(0, H))
     if engine.split:
         ws.wino_t, ws.wino_t2 = t1, t2
@@ -214,7 +220,6 @@ def _wgrad1_wino(engine: ProjectFuse, st, ws: Workspace, d1, dy1: torch.Tensor, 
     D = A-transform of dy1 (``ops.wino_dy_rows``), then per xi the T x D products over its 3 kernel
     columns, folded with G — 5/9 of the direct form's MFMAs.  Chunk lists from the 12-row frustum
     mask T was written under (a chunk whose T row is zero contributes exactly 0)."""
-    import ctypes
     H, W = engine.grid_hw
     B, dev, mid = dy1.shape[0], dy1.device, engine.mid
     lists = None
@@ -226,13 +231,19 @@ def _wgrad1_wino(engine: ProjectFuse, st, ws: Workspace, d1, dy1: torch.Tensor, 
         if key not in st.lists_wino:
             st.lists_wino[key] = ops.wgrad_wino_chunk_lists(m, engine.S, B, H, W)
         lists = st.lists_wino[key]
-    need = int(_native.load().mvbev_conv3x3_wgrad_wino_workspace_bytes(ctypes.byref(d1), mid))
-    buf = st.wg_ws.get(str(dev))
-    if buf is None or buf.numel() * 4 < need:
-        buf = torch.empty((need + 3) // 4, dtype=torch.float32, device=dev)
-        st.wg_ws[str(dev)] = buf
     ops.conv3x3_wgrad_wino(ws.wino_t, d1, ops.wino_dy_rows(dy1), dw1.shape[1], chan_map=engine.pack1._map_dev,
-                           dw=dw1, workspace=buf, chunk_lists=lists)
+                           dw=dw1, workspace=_wgrad_wino_ws(st, d1, mid, 1, dev), chunk_lists=lists)
+
+
+def _wgrad_wino_ws(st, desc, cout, dilation, device) -> torch.Tensor:
+    """The Winograd weight gradients' partition workspace (shared buffer, grown once: one runs at a time)."""
+    import ctypes
+    need = int(_native.load().mvbev_conv3x3_wgrad_wino_workspace_bytes(ctypes.byref(desc), cout, dilation))
+    buf = st.wg_ws.get(str(device))
+    if buf is None or buf.numel() * 4 < need:
+        buf = torch.empty((need + 3) // 4, dtype=torch.float32, device=device)
+        st.wg_ws[str(device)] = buf
+    return buf
 
 
 def _wgrad_ws(st, desc, cout, device) -> torch.Tensor:
@@ -309,8 +320,11 @@ class ProjectFuseFunction(torch.autograd.Function):
         if db2 is not None:
             ops.conv3x3_bias_coord_grad(dy2, 2, db=db2)
         d_y1 = ops.conv_desc(B, mid, H, W, group=mid, group_stride=0, batch_stride=mid * H * W)
-        # (conv2's wgrad reads the fp32 dy2: at its size the row split costs what it saves)
-        dw2 = ops.conv3x3_wgrad(ws.y1, d_y1, dy2, 2, mid, workspace=_wgrad_ws(st, d_y1, mid, dev))
+        if ws.t2_valid and W % 8 == 0 and mid % 128 == 0:  # from the forward's dilation-2 transform
+            dw2 = ops.conv3x3_wgrad_wino(ws.wino_t2, d_y1, ops.wino_dy_rows(dy2, dilation=2), mid, dilation=2,
+                                         workspace=_wgrad_wino_ws(st, d_y1, mid, 2, dev))
+        else:  # (the direct form reads the fp32 dy2: at its size the row split costs what it saves)
+            dw2 = ops.conv3x3_wgrad(ws.y1, d_y1, dy2, 2, mid, workspace=_wgrad_ws(st, d_y1, mid, dev))
         _mark("bwd_conv2_dgrad")
         if dy2s is not None and engine.wino_conv2_active(ws):
             dy1 = _dgrad2_wino(engine, st, dy2s, w2)

@@ -368,7 +368,9 @@ constexpr std::integer_sequence<int, (B + U)...> offset_seq(std::integer_sequenc
 // kernel over the transformed rows.  With the forward's y[3 r3 + j] = sum_xi AT[j][xi] (G w)_xi .
 // T_xi[r3] (conv_bf16x3.hip, "Row-Winograd conv1"), per kernel column kw
 //   dW[kh][kw] = sum_xi G[xi][kh] M_xi[kw],   M_xi[kw][co][ci] = sum_{b,r3,x} D_xi[co][r3][x] T_xi[ci][r3][x + kw - 1],
-//   D_xi = sum_j AT[j][xi] dy[3 r3 + j]   (wino_dy_rows_kernel, pre-split rows [B][5][Cout][R3][W]).
+//   D_xi = sum_j AT[j][xi] dy[base(r3) + DIL j]   (wino_dy_rows_kernel, pre-split rows [B][5][Cout][R3][W];
+//   base(r3) the forward's row tiles: 3 r3 for dilation 1, conv2's interleaved 12 (r3 / 4) + ring_base_row<2>
+//   for dilation 2 — conv2's weight gradient from its T).
 // A workgroup owns one xi and 128 input channels (desc group a multiple of 128 with chunk lists) (a wave: 32 Cout x 2 blocks of 32 channels, so
 // each A fragment feeds both and a chunk carries twice the direct form's MFMAs per input channel
 // block); its chunk is (b, r3, 32-px segment), the B window one T row (34 px of 128 channels, both
@@ -382,7 +384,7 @@ struct WinoT {
 template <int DIL, bool WINO = false>
 __global__ __launch_bounds__(NTH, 1) void wgrad_dma_kernel(const WArgs a, const WinoT wt) {
   static_assert(NWV == 8, "wave layout: 4 output blocks x 2 channel halves");
-  static_assert(!WINO || DIL == 1, "Winograd wgrad: dilation 1");
+  static_assert(!WINO || DIL == 1 || DIL == 2, "Winograd wgrad: dilation 1 or 2");
   constexpr int ROWS = WINO ? 1 : 3;      // window rows (taps kh)
   constexpr int NTAPS = 3 * ROWS;         // accumulators (kh, kw) / (kw)
   constexpr int NSTEP = 2 * NTAPS;        // (pixel step, tap) steps per chunk
@@ -725,10 +727,10 @@ __global__ __launch_bounds__(kWinoRedThreads) void wgrad_wino_reduce_kernel(cons
   }
 }
 
-// D[b][xi][co][r3] = split(sum_j AT[j][xi] dy[b][co][3 r3 + j]) in MVBEV_LAYOUT_SPLIT_ROWS (rows past
-// H are zero), AT = [1 1 1 1 0; 0 1 -1 2 0; 0 1 1 4 1]: a thread per (b, co, r3, 8-pixel run).
+// D[b][xi][co][r3] = split(sum_j AT[j][xi] dy[b][co][base(r3) + dil j]) in MVBEV_LAYOUT_SPLIT_ROWS (rows
+// past H are zero), AT = [1 1 1 1 0; 0 1 -1 2 0; 0 1 1 4 1]: a thread per (b, co, r3, 8-pixel run).
 __global__ __launch_bounds__(256) void wino_dy_rows_kernel(const floatx4* __restrict__ dy, int B, int Cout, int H,
-                                                           int W, int R3, u32x4_t* __restrict__ out) {
+                                                           int W, int R3, int dil, u32x4_t* __restrict__ out) {
   const int runs = W / 8;
   const int64_t n = (int64_t)B * Cout * R3 * runs;
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -739,9 +741,10 @@ __global__ __launch_bounds__(256) void wino_dy_rows_kernel(const floatx4* __rest
   r /= R3;
   const int co = (int)(r % Cout), b = (int)(r / Cout);
   float d[3][8];
+  const int q = r3 & 3, base = dil == 1 ? 3 * r3 : 12 * (r3 >> 2) + (q >> 1) * 6 + (q & 1);  // ring_base_row<2>
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
-    const int y = 3 * r3 + j;
+    const int y = base + dil * j;
     floatx4 v0 = floatx4{0.f, 0.f, 0.f, 0.f}, v1 = v0;
     if (y < H) {
       const floatx4* src = dy + ((((int64_t)b * Cout + co) * H + y) * W) / 4 + 2 * run;
@@ -1660,51 +1663,57 @@ int mvbev_conv3x3_wgrad_bf16x3_ex2(const void* x, int x_layout, const mvbev_conv
   return MVBEV_OK;
 }
 
-size_t mvbev_wino_dy_rows_bytes(int64_t B, int64_t Cout, int64_t H, int64_t W) {
-  if (B <= 0 || Cout <= 0 || H <= 0 || W <= 0) return 0;
-  return (size_t)B * 5 * (size_t)Cout * (size_t)mvbev::ceil_div(H, 3) * (size_t)W * 4;
+// 3-row tiles r3 of the forward's row transform: ceil(H / 3) (dilation 1), 4 per 12-row tile (dilation 2)
+static int64_t wino_r3(int64_t H, int dil) { return dil == 1 ? mvbev::ceil_div(H, 3) : 4 * mvbev::ceil_div(H, 12); }
+
+size_t mvbev_wino_dy_rows_bytes(int64_t B, int64_t Cout, int64_t H, int64_t W, int dilation) {
+  if (B <= 0 || Cout <= 0 || H <= 0 || W <= 0 || (dilation != 1 && dilation != 2)) return 0;
+  return (size_t)B * 5 * (size_t)Cout * (size_t)wino_r3(H, dilation) * (size_t)W * 4;
 }
 
-int mvbev_wino_dy_rows_f32(const float* dy, int64_t B, int64_t Cout, int64_t H, int64_t W, void* out,
-                           size_t out_bytes, void* stream) {
+int mvbev_wino_dy_rows_f32(const float* dy, int64_t B, int64_t Cout, int64_t H, int64_t W, int dilation,
+                           void* out, size_t out_bytes, void* stream) {
   using namespace mvbev;
   if (!dy || !out) return MVBEV_ERR_NULL;
   if (B <= 0 || Cout <= 0 || H <= 0 || W <= 0) return MVBEV_ERR_RANK;
+  if (dilation != 1 && dilation != 2) return MVBEV_ERR_DILATION;
   if (W % 8 != 0 || B * Cout * H * W > (int64_t)INT32_MAX * 8) return MVBEV_ERR_SHAPE;
-  if (out_bytes < mvbev_wino_dy_rows_bytes(B, Cout, H, W)) return MVBEV_ERR_SHAPE;
+  if (out_bytes < mvbev_wino_dy_rows_bytes(B, Cout, H, W, dilation)) return MVBEV_ERR_SHAPE;
   if (((reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(out)) & 15) != 0) return MVBEV_ERR_ALIGN;
-  const int64_t R3 = ceil_div(H, 3), n = B * Cout * R3 * (W / 8);
+  const int64_t R3 = wino_r3(H, dilation), n = B * Cout * R3 * (W / 8);
   hipLaunchKernelGGL(bwd::wino_dy_rows_kernel, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, as_stream(stream),
-                     reinterpret_cast<const bwd::floatx4*>(dy), (int)B, (int)Cout, (int)H, (int)W, (int)R3,
+                     reinterpret_cast<const bwd::floatx4*>(dy), (int)B, (int)Cout, (int)H, (int)W, (int)R3, dilation,
                      static_cast<u32x4_t*>(out));
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }
 
 // Winograd geometry: P over the 5 x tiles workgroup set, chunks (b, r3 < R3, segment) per xi
-static mvbev::bwd::WGeo wgrad_wino_geo(const mvbev_conv_desc* d, int64_t Cout) {
+static mvbev::bwd::WGeo wgrad_wino_geo(const mvbev_conv_desc* d, int64_t Cout, int dil) {
   using namespace mvbev;
   using namespace mvbev::bwd;
   WGeo g;
   g.tiles = (Cout / MT) * ceil_div(d->K, 2 * NT);  // 128 input channels per workgroup
-  g.nchunks = d->B * ceil_div(d->H, 3) * ceil_div(d->W, PX);
+  g.nchunks = d->B * wino_r3(d->H, dil) * ceil_div(d->W, PX);
   g.P = wgrad_partitions(5 * g.tiles, g.nchunks, 0.07);
   return g;
 }
 
-size_t mvbev_conv3x3_wgrad_wino_workspace_bytes(const mvbev_conv_desc* desc, int64_t Cout) {
+size_t mvbev_conv3x3_wgrad_wino_workspace_bytes(const mvbev_conv_desc* desc, int64_t Cout, int dilation) {
   if (!desc || Cout <= 0 || desc->K <= 0 || desc->H <= 0 || desc->W <= 0 || desc->B <= 0) return 0;
-  const mvbev::bwd::WGeo g = wgrad_wino_geo(desc, Cout);
+  if (dilation != 1 && dilation != 2) return 0;
+  const mvbev::bwd::WGeo g = wgrad_wino_geo(desc, Cout, dilation);
   return (size_t)g.P * 15 * (size_t)Cout * (size_t)desc->K * sizeof(float);
 }
 
 int mvbev_conv3x3_wgrad_wino_bf16x3(const void* t, size_t t_bytes, const mvbev_conv_desc* d, const void* dy_wino,
-                                    size_t dy_wino_bytes, int64_t Cout, const int32_t* chan_map, int64_t Cin_w,
-                                    float* dw, const int32_t* chunk_list, const int32_t* chunk_off, void* workspace,
-                                    size_t workspace_bytes, void* stream) {
+                                    size_t dy_wino_bytes, int64_t Cout, int dilation, const int32_t* chan_map,
+                                    int64_t Cin_w, float* dw, const int32_t* chunk_list, const int32_t* chunk_off,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
   using namespace mvbev;
   using namespace mvbev::bwd;
   if (!t || !d || !dy_wino || !dw || !workspace) return MVBEV_ERR_NULL;
+  if (dilation != 1 && dilation != 2) return MVBEV_ERR_DILATION;
   if ((chunk_list == nullptr) != (chunk_off == nullptr)) return MVBEV_ERR_NULL;
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || Cin_w <= 0 || d->group <= 0)
     return MVBEV_ERR_RANK;
@@ -1715,15 +1724,15 @@ int mvbev_conv3x3_wgrad_wino_bf16x3(const void* t, size_t t_bytes, const mvbev_c
   if (!chan_map && d->K > Cin_w) return MVBEV_ERR_SHAPE;
   if (chunk_list && d->group % (2 * NT) != 0) return MVBEV_ERR_SHAPE;  // a channel tile inside one group
   constexpr int kRT = 12;  // conv_wino's workgroup tile rows: T holds 4 row tiles (r3) of each
-  const int64_t R3 = ceil_div(d->H, 3), r5 = 5 * 4 * ceil_div(d->H, kRT), segs = ceil_div(d->W, PX);
+  const int64_t R3 = wino_r3(d->H, dilation), r5 = 5 * 4 * ceil_div(d->H, kRT), segs = ceil_div(d->W, PX);
   const int64_t t_need = d->B * (d->K / 8) * r5 * d->W * 32;
-  if (t_bytes < (size_t)t_need || dy_wino_bytes < mvbev_wino_dy_rows_bytes(d->B, Cout, d->H, d->W))
+  if (t_bytes < (size_t)t_need || dy_wino_bytes < mvbev_wino_dy_rows_bytes(d->B, Cout, d->H, d->W, dilation))
     return MVBEV_ERR_SHAPE;
   // 32-bit chunk-invariant offsets and packed chunk ids (b < 128, r3 and segments < 4096)
   if ((d->K / 8) * 2 * r5 * d->W >= INT32_MAX || Cout * R3 * d->W >= INT32_MAX || d->B >= 128 || R3 > 4096 ||
       segs > 4096)
     return MVBEV_ERR_SHAPE;
-  const WGeo g = wgrad_wino_geo(d, Cout);
+  const WGeo g = wgrad_wino_geo(d, Cout, dilation);
   if (g.nchunks / g.P + 1 > WG_MAXC) return MVBEV_ERR_SHAPE;
   const size_t need = (size_t)g.P * 15 * (size_t)Cout * (size_t)d->K * sizeof(float);
   if (workspace_bytes < need) return MVBEV_ERR_SHAPE;
@@ -1738,8 +1747,12 @@ int mvbev_conv3x3_wgrad_wino_bf16x3(const void* t, size_t t_bytes, const mvbev_c
   a.vec_dy = true; a.dy_rows = true;
   a.clist = chunk_list; a.coff = chunk_off;
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL((wgrad_dma_kernel<1, true>), dim3((unsigned)(g.P * 5 * g.tiles)), dim3(NTH), 0, s, a,
-                     WinoT{(int)r5});
+  if (dilation == 1)
+    hipLaunchKernelGGL((wgrad_dma_kernel<1, true>), dim3((unsigned)(g.P * 5 * g.tiles)), dim3(NTH), 0, s, a,
+                       WinoT{(int)r5});
+  else
+    hipLaunchKernelGGL((wgrad_dma_kernel<2, true>), dim3((unsigned)(g.P * 5 * g.tiles)), dim3(NTH), 0, s, a,
+                       WinoT{(int)r5});
   MVBEV_CHECK_LAUNCH();
   hipLaunchKernelGGL(wgrad_wino_reduce_kernel, dim3((unsigned)ceil_div(d->K, kWrK), (unsigned)Cout),
                      dim3(kWinoRedThreads), 0, s, static_cast<const float*>(workspace), g.P, (int)Cout, (int)d->K, chan_map,

@@ -1325,23 +1325,31 @@ def conv3x3_wgrad(x: torch.Tensor, desc, dy: torch.Tensor, dilation: int, cin_w:
     return dw
 
 
-def wino_dy_rows(dy: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """fp32 dy [B,Cout,H,W] (contiguous, W % 8 == 0) -> D_xi = sum_j AT[j][xi] dy[3 r3 + j] in the
-    row-split bf16 layout, [B, 5, Cout, ceil(H/3), W/8, 2, 8] (``mvbev_wino_dy_rows_f32``): the
-    output-gradient side of ``conv3x3_wgrad_wino``."""
+def wino_dy_rows(dy: torch.Tensor, out: Optional[torch.Tensor] = None, dilation: int = 1) -> torch.Tensor:
+    """fp32 dy [B,Cout,H,W] (contiguous, W % 8 == 0) -> D_xi = sum_j AT[j][xi] dy[base(r3) + dilation j] in
+    the row-split bf16 layout, [B, 5, Cout, R3, W/8, 2, 8] (``mvbev_wino_dy_rows_f32``; R3 = ceil(H/3) for
+    dilation 1, 4 ceil(H/12) over conv2's interleaved row tiles for dilation 2): the output-gradient side
+    of ``conv3x3_wgrad_wino``."""
     _require_cuda(dy)
     if dy.dim() != 4 or dy.dtype != torch.float32 or not dy.is_contiguous() or dy.shape[3] % 8:
         raise ValueError("wino_dy_rows needs a contiguous float32 [B,C,H,W] tensor with W % 8 == 0")
     B, C, H, W = dy.shape
-    shape = (B, 5, C, -(-H // 3), W // 8, 2, 8)
+    if dilation not in (1, 2):
+        raise ValueError("dilation must be 1 or 2")
+    shape = (B, 5, C, wino_r3(H, dilation), W // 8, 2, 8)
     if out is None:
         out = torch.empty(shape, dtype=torch.bfloat16, device=dy.device)
     elif tuple(out.shape) != shape or out.dtype != torch.bfloat16 or not out.is_contiguous():
         raise ValueError(f"out must be a contiguous bf16 tensor of shape {shape}")
-    st = _native.load().mvbev_wino_dy_rows_f32(dy.data_ptr(), B, C, H, W, out.data_ptr(),
+    st = _native.load().mvbev_wino_dy_rows_f32(dy.data_ptr(), B, C, H, W, int(dilation), out.data_ptr(),
                                                out.numel() * out.element_size(), _stream(dy))
     _native.check(st, "mvbev_wino_dy_rows_f32")
     return out
+
+
+def wino_r3(H: int, dilation: int = 1) -> int:
+    """3-row tiles of a row-Winograd transform over H rows: ceil(H/3), or 4 per 12-row tile (dilation 2)."""
+    return -(-H // 3) if dilation == 1 else 4 * (-(-H // 12))
 
 
 def wgrad_wino_chunk_lists(mask: torch.Tensor, groups: int, B: int, H: int, W: int):
@@ -1373,7 +1381,7 @@ def wgrad_wino_chunk_lists(mask: torch.Tensor, groups: int, B: int, H: int, W: i
 
 def conv3x3_wgrad_wino(t: torch.Tensor, desc, dy_wino: torch.Tensor, cin_w: int,
                        chan_map: Optional[torch.Tensor] = None, dw: Optional[torch.Tensor] = None,
-                       workspace: Optional[torch.Tensor] = None, chunk_lists=None) -> torch.Tensor:
+                       workspace: Optional[torch.Tensor] = None, chunk_lists=None, dilation: int = 1) -> torch.Tensor:
     """Weight gradient of a dilation-1 3x3 conv from its forward's row-Winograd transform ``t``
     (``wino_rows`` of the input ``desc`` addresses, or the fused warp's) and ``dy_wino`` =
     ``wino_dy_rows(dy)`` (``mvbev_conv3x3_wgrad_wino_bf16x3``): the same dw as ``conv3x3_wgrad``
@@ -1383,7 +1391,7 @@ def conv3x3_wgrad_wino(t: torch.Tensor, desc, dy_wino: torch.Tensor, cin_w: int,
     B, cout = dy_wino.shape[0], dy_wino.shape[2]
     if dy_wino.dim() != 7 or dy_wino.dtype != torch.bfloat16 or not dy_wino.is_contiguous() or dy_wino.shape[1] != 5:
         raise ValueError("dy_wino must be wino_dy_rows' output")
-    if (desc.B, -(-desc.H // 3), desc.W // 8) != (B, dy_wino.shape[3], dy_wino.shape[4]):
+    if (desc.B, wino_r3(desc.H, dilation), desc.W // 8) != (B, dy_wino.shape[3], dy_wino.shape[4]):
         raise ValueError("dy_wino does not match the conv descriptor")
     if chan_map is not None:
         _require_cuda(chan_map)
@@ -1394,13 +1402,14 @@ def conv3x3_wgrad_wino(t: torch.Tensor, desc, dy_wino: torch.Tensor, cin_w: int,
     elif tuple(dw.shape) != (cout, cin_w, 3, 3) or not dw.is_contiguous() or dw.dtype != torch.float32:
         raise ValueError(f"dw must be a contiguous fp32 [{cout},{cin_w},3,3] tensor")
     lib = _native.load()
-    need = int(lib.mvbev_conv3x3_wgrad_wino_workspace_bytes(ctypes.byref(desc), cout))
+    need = int(lib.mvbev_conv3x3_wgrad_wino_workspace_bytes(ctypes.byref(desc), cout, int(dilation)))
     if workspace is None or workspace.numel() * workspace.element_size() < need:
         workspace = torch.empty((need + 3) // 4, dtype=torch.float32, device=t.device)
     cl, co = (None, None) if chunk_lists is None else (chunk_lists[0].data_ptr(), chunk_lists[1].data_ptr())
     st = lib.mvbev_conv3x3_wgrad_wino_bf16x3(t.data_ptr(), t.numel() * t.element_size(), ctypes.byref(desc),
                                              dy_wino.data_ptr(), dy_wino.numel() * dy_wino.element_size(), cout,
-                                             None if chan_map is None else chan_map.data_ptr(), cin_w, dw.data_ptr(),
+                                             int(dilation), None if chan_map is None else chan_map.data_ptr(), cin_w,
+                                             dw.data_ptr(),
                                              cl, co, workspace.data_ptr(),
                                              workspace.numel() * workspace.element_size(), _stream(t))
     _native.check(st, "mvbev_conv3x3_wgrad_wino_bf16x3")

@@ -72,6 +72,9 @@ class Workspace:
     # wino_t holds this forward's transform of the whole grid (conv1 ran row-Winograd over all rows):
     # the training backward's conv1 weight gradient reads it (autograd._wgrad1_wino)
     t1_valid: bool = False
+    # wino_t2 holds this forward's dilation-2 transform of the whole y1 (conv2 ran row-Winograd): the
+    # training backward's conv2 weight gradient reads it (autograd._wgrad_wino)
+    t2_valid: bool = False
     # training forward whose backward reads conv1's T and never the slab (autograd._train_workspace):
     # the fused warp + B^T may run, as in inference
     train_t_only: bool = False
@@ -567,6 +570,7 @@ class ProjectFuse:
             if ws.wino_t2 is None or ws.wino_t2.numel() * 2 < tneed:
                 ws.wino_t2 = torch.zeros((tneed + 1) // 2, dtype=torch.bfloat16, device=ws.y1.device)
             ops.wino_rows(ws.y1, d2, ws.wino_t2, dilation=2)
+            ws.t2_valid = (a1, b1) == (a2, b2) == (0, H)  # the backward's conv2 weight gradient reads it
             return ops.conv3x3_wino_dil(ws.wino_t2, d2, self.pack2w.get(conv2.weight), self.mid, 2, bias=conv2.bias,
                                         relu=True, out=ws.y2)
         p2 = self.pack2.get(conv2.weight)

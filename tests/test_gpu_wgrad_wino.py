@@ -24,17 +24,21 @@ def _split_encode(x: torch.Tensor) -> torch.Tensor:
     return t.permute(1, 2, 4, 5, 0, 3).contiguous()
 
 
-def test_wino_dy_rows_transform_and_rounding():
+@pytest.mark.parametrize("dil", [1, 2])
+def test_wino_dy_rows_transform_and_rounding(dil):
+    """D over the forward's 3-row tiles: rows 3 r3 + j (dilation 1) or conv2's interleaved tiles
+    12 (r3 // 4) + (0, 1, 6, 7)[r3 % 4] + 2 j (dilation 2); rows past H are zero."""
     from mvdet_amd import _native, ops
     g = torch.Generator().manual_seed(3)
-    B, C, H, W = 2, 5, 13, 24  # H % 3 == 1: the last tile's rows 1, 2 are zero
+    B, C, H, W = 2, 5, 13, 24  # H % 3 == 1 and H % 12 == 1: partial last tiles
     dy = torch.randn((B, C, H, W), generator=g)
-    got = ops.wino_dy_rows(dy.to(DEV)).cpu()
-    R3 = -(-H // 3)
+    got = ops.wino_dy_rows(dy.to(DEV), dilation=dil).cpu()
+    R3 = ops.wino_r3(H, dil)
     assert tuple(got.shape) == (B, 5, C, R3, W // 8, 2, 8)
-    pad = torch.zeros((B, C, 3 * R3, W))
+    pad = torch.zeros((B, C, 12 * R3, W))
     pad[:, :, :H] = dy
-    r = pad.reshape(B, C, R3, 3, W)
+    base = [3 * r if dil == 1 else 12 * (r // 4) + (0, 1, 6, 7)[r % 4] for r in range(R3)]
+    r = torch.stack([pad[:, :, [b + dil * j for b in base]] for j in range(3)], 3)  # [B, C, R3, 3, W]
     a0, a1, a2 = r[:, :, :, 0], r[:, :, :, 1], r[:, :, :, 2]
     d = torch.stack([a0, (a0 + a1) + a2, (a0 - a1) + a2, (a0 + 2 * a1) + 4 * a2, a2], 1)  # [B,5,C,R3,W]
     hi = d.to(torch.bfloat16)
@@ -44,27 +48,31 @@ def test_wino_dy_rows_transform_and_rounding():
     with pytest.raises(ValueError):
         ops.wino_dy_rows(torch.zeros((1, 1, 3, 12), device=DEV))
     out = torch.empty(16, device=DEV)
-    st = _native.load().mvbev_wino_dy_rows_f32(out.data_ptr(), 1, 1, 3, 12, out.data_ptr(), 64, None)
+    st = _native.load().mvbev_wino_dy_rows_f32(out.data_ptr(), 1, 1, 3, 12, dil, out.data_ptr(), 64, None)
     assert st == _native.ERR_SHAPE
+    st = _native.load().mvbev_wino_dy_rows_f32(out.data_ptr(), 1, 1, 3, 16, 3, out.data_ptr(), 64, None)
+    assert st == _native.ERR_DILATION
 
 
 @pytest.mark.parametrize("B,K,H,W", [(1, 64, 12, 64), (2, 72, 17, 40), (1, 256, 31, 96), (2, 128, 25, 200)])
-def test_wgrad_wino_vs_torch_and_direct(B, K, H, W):
-    """Partial 64-channel tiles (K = 72), partial row tiles (H % 3, H % 12), a last segment of 8 px."""
+@pytest.mark.parametrize("dil", [1, 2])
+def test_wgrad_wino_vs_torch_and_direct(B, K, H, W, dil):
+    """Partial 128-channel tiles (K = 72), partial row tiles (H % 3, H % 12), a last segment of 8 px;
+    dilation 2 from conv2's interleaved-row transform (``wino_rows(dilation=2)``)."""
     from mvdet_amd import ops
-    g = torch.Generator().manual_seed(K + H + W)
+    g = torch.Generator().manual_seed(K + H + W + dil)
     cout = 128
     x = F.relu(torch.randn((B, K, H, W), generator=g))
     dy = torch.randn((B, cout, H, W), generator=g)
-    ref = torch.nn.grad.conv2d_weight(x.double(), (cout, K, 3, 3), dy.double(), padding=1)
+    ref = torch.nn.grad.conv2d_weight(x.double(), (cout, K, 3, 3), dy.double(), padding=dil, dilation=dil)
     d = ops.conv_desc(B, K, H, W, group=K, group_stride=0, batch_stride=K * H * W)
     xs = _split_encode(x.to(DEV))
     t = torch.zeros((ops.wino_rows_bytes(d) + 1) // 2, dtype=torch.bfloat16, device=DEV)
-    ops.wino_rows(xs, d, t)
+    ops.wino_rows(xs, d, t, dilation=dil)
     dyd = dy.to(DEV)
-    got = ops.conv3x3_wgrad_wino(t, d, ops.wino_dy_rows(dyd), K)
+    got = ops.conv3x3_wgrad_wino(t, d, ops.wino_dy_rows(dyd, dilation=dil), K, dilation=dil)
     assert_parity(got.cpu(), ref, "Winograd wgrad")
-    direct = ops.conv3x3_wgrad(xs, d, dyd, 1, K)
+    direct = ops.conv3x3_wgrad(xs, d, dyd, dil, K)
     s_w, s_d = parity_stats(got.cpu(), ref), parity_stats(direct.cpu(), ref)
     # the transforms add about as much rounding again as the direct form's split products
     assert s_w["normwise"] < 8 * max(s_d["normwise"], 1e-7), (s_w, s_d)

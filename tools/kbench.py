@@ -85,7 +85,7 @@ def backward_stages(eng, ws, mc, B, ho, wo, N, C, dev):
     lists_w = ops.wgrad_wino_chunk_lists(gm1, eng.S, B, ho, wo) if gm1 is not None else None
     drows = torch.empty((B, 5, w1.shape[0], -(-ho // 3), wo // 8, 2, 8), dtype=torch.bfloat16, device=dev)
     wwsw = torch.empty((int(_native.load().mvbev_conv3x3_wgrad_wino_workspace_bytes(
-        __import__("ctypes").byref(d1), w1.shape[0])) + 3) // 4, device=dev)
+        __import__("ctypes").byref(d1), w1.shape[0], 1)) + 3) // 4, device=dev)
     dw1w = torch.zeros_like(w1)
     if pre:
         ops.conv3x3_wgrad(ws.slab, d1, dy1, 1, w1.shape[1], chan_map=eng.pack1._map_dev, dw=dw1, workspace=wws,
@@ -95,10 +95,18 @@ def backward_stages(eng, ws, mc, B, ho, wo, N, C, dev):
         nc = N * C
         diff = (dw1w[:, :nc] - dw1[:, :nc]).abs().max().item() / max(dw1[:, :nc].abs().max().item(), 1e-30)
         print(json.dumps({"wgrad1w_vs_wgrad1_normwise": diff}), flush=True)
+    t2w = torch.zeros((ops.wino_rows_bytes(d_y1) + 1) // 2, dtype=torch.bfloat16, device=dev)
+    ops.wino_rows(y1s, d_y1, t2w, dilation=2)
+    drows2 = torch.empty((B, 5, mid, ops.wino_r3(ho, 2), wo // 8, 2, 8), dtype=torch.bfloat16, device=dev)
+    wwsw2 = torch.empty((int(_native.load().mvbev_conv3x3_wgrad_wino_workspace_bytes(
+        __import__("ctypes").byref(d_y1), mid, 2)) + 3) // 4, device=dev)
     return {
         "wgrad1w": (lambda: ops.conv3x3_wgrad_wino(t1, d1, ops.wino_dy_rows(dy1, out=drows), w1.shape[1],
                                                    chan_map=eng.pack1._map_dev, dw=dw1w, workspace=wwsw,
                                                    chunk_lists=lists_w), flop),
+        # conv2's from its forward transform (dilation-2 row tiles; autograd's training default)
+        "wgrad2w": (lambda: ops.conv3x3_wgrad_wino(t2w, d_y1, ops.wino_dy_rows(dy2, out=drows2, dilation=2), mid,
+                                                   dilation=2, workspace=wwsw2), flop2),
         "wgrad2": (lambda: ops.conv3x3_wgrad(y1s, d_y1, dy2, 2, mid, workspace=wws2,
                                              dy_rows=ops.split_rows(dy2, out=rows2) if pre else None), flop2),
         "wgrad2f": (lambda: ops.conv3x3_wgrad(y1s, d_y1, dy2, 2, mid, workspace=wws2), flop2),
@@ -216,7 +224,7 @@ def main():
             stages["adjup"] = ((lambda: ops.warp_views_adjoint(douts, plu, gs)), None)
             pl = [ops.WarpAdjointPlan(eng.m_norm_cpu[v], up, (ho, wo), dev) for v in range(N)]
             stages["adj"] = ((lambda: ops.warp_views_adjoint(douts, pl, gsu)), None)
-        if {"wgrad1", "wgrad1w", "wgrad1f", "dgrad1", "dgrad1s", "wgrad2", "wgrad2f", "dgrad2"} & set(args.only.split(",")):
+        if {"wgrad1", "wgrad1w", "wgrad2w", "wgrad1f", "dgrad1", "dgrad1s", "wgrad2", "wgrad2f", "dgrad2"} & set(args.only.split(",")):
             stages.update(backward_stages(eng, ws, mc, B, ho, wo, N, C, dev))
         from mvdet_amd import _native
         libs = [("default", _native.load())]

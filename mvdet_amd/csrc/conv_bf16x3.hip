@@ -1715,235 +1715,6 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   ring_epilogue<DIL, RELU, P3>(a, b, y0 + ring_base_row<DIL>(rg), x0 + l32, cot, cw, y, lds);
 }
 
-// Two workgroups per CU (MVBEV_WINO_HALF): the kernel above with 64 output channels per workgroup —
-// 4 waves (one per SIMD), wave = row tile x 64 Cout (the same 2 x 5 accumulators and 18 MFMAs per unit),
-// 3 ring slots of 24 KiB (72 KiB of LDS, so two workgroups share a CU).  One barrier per unit as above,
-// but the two waves of a SIMD now belong to different workgroups, so one's barrier / DMA waits need not
-// idle the MFMA pipe; the cost is 2 units of DMA lookahead instead of 3 and 25 % more DMA bytes per MFMA
-// (the T row feeds 64 instead of 128 output channels).
-#ifndef MVBEV_WINO_HALF
-#define MVBEV_WINO_HALF 0
-#endif
-namespace winoh {
-constexpr int NW = 4, NT = 64 * NW;            // waves, threads
-constexpr int BNH = BN / 2;                    // output channels per workgroup
-constexpr int RUNITH = 2 * 3 * 2 * BNH;        // weight pieces per unit (768)
-constexpr int RHALFH = RUNITH / 2;
-constexpr int NWIH = RUNITH / wino::NIT;       // weight DMAs per wave per unit (3)
-constexpr int SLOTH = RUNITH + wino::NXTMAX * wino::NIT;
-constexpr int NSLOTH = 3;
-constexpr int LDSH = NSLOTH * SLOTH;
-static_assert(wino::NIT == NT, "every wave issues");
-static_assert(2 * LDSH * 16 <= 160 * 1024, "two workgroups per CU");
-}  // namespace winoh
-
-template <bool RELU, int DIL, bool P3>
-__global__ __launch_bounds__(winoh::NT, 2) void conv_wino_half_kernel(const Args a) {
-  using namespace wino;
-  using namespace winoh;
-  using G = Geo<DIL>;
-  constexpr int XW = G::XW, TROW = G::TROW, NXT = G::NXT;
-  __shared__ __attribute__((aligned(16))) u32x4 lds[LDSH];
-  const int W = a.W;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l32 = lane & 31, kl = lane >> 5;
-  const int ncot = 2 * a.n_cot;  // 64-channel output tiles
-
-  int tile = xcd_remap(blockIdx.x, a.nwg);
-  if (a.gmask) {
-    const int Gq = a.mgroup;
-    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
-    const int q = j / ncot;
-    const int slot = Gq * (8 * (q / Gq) + x) + q % Gq;
-    if (slot >= a.npix) return;
-    tile = (a.tile_order ? a.tile_order[slot] : slot) * ncot + j % ncot;
-  }
-  const int cot64 = tile % ncot, rest = tile / ncot;
-  const int cot = cot64 >> 1, coh = cot64 & 1;
-  const int t_main = a.tiles_y * a.tiles_x;
-  const int pp = rest % t_main, b = rest / t_main;
-  const int ty = pp / a.tiles_x;
-  const int x0 = (pp - ty * a.tiles_x) * TW;
-  const int y0 = a.out_row0 + ty * RT;
-  if (a.cmask && !((a.cmask[pp] >> (cot / a.cot_pg)) & 1u)) return;
-  const uint32_t gm = a.gmask ? a.gmask[pp] : 0u;
-  const int nch = a.gmask ? __builtin_popcount(gm) * a.cpg : a.nchunks;
-  const int K8 = a.K / SB;
-  const int64_t tplane2 = 2LL * (XH * a.tiles_y) * W;
-  const uint32_t tplane_b = (uint32_t)(tplane2 * 16);
-  constexpr uint32_t kOOB = 0x80000000u;
-  // weights: entry e = [part][kw][sub][co < 64] of the packed [part][3 xi + kw][sub][co < 128] (this
-  // workgroup's half of the Cout tile: + 64 coh pieces in the base)
-  uint32_t wvo[NWIH], tvo[NXTMAX];
-#pragma unroll
-  for (int j = 0; j < NWIH; ++j) {
-    const int e = j * NT + tid;
-    const int part = e / RHALFH, r = e % RHALFH, kw = r / (2 * BNH), rr = r % (2 * BNH);
-    wvo[j] = (uint32_t)((part * (NTAP * 2 * BN) + kw * 2 * BN + (rr / BNH) * BN + rr % BNH) * 16);
-    asm volatile("" : "+v"(wvo[j]));
-  }
-#pragma unroll
-  for (int j = 0; j < NXT; ++j) {
-    const int e = j * NT + tid;
-    const int sub = e / (TROW / 2), part = (e / (TROW / 4)) & 1, rt = (e % (TROW / 4)) / XW, c = e % XW;
-    const int gx = x0 - DIL + c;
-    const bool z = e >= TROW || gx < 0 || gx >= W;
-    tvo[j] = z ? kOOB : (uint32_t)sub * tplane_b + (uint32_t)((2 * (XH * ty + NXI * rt) * W + part * W + gx) * 16);
-    asm volatile("" : "+v"(tvo[j]));
-  }
-  const int cpg = a.gmask ? a.cpg : max(nch, 1);
-  uint32_t rem = a.gmask ? gm : 1u;
-  int gbase = a.gmask ? __builtin_ctz(gm | 0x80000000u) * cpg : 0, ci = 0, wi = 0;
-  auto step = [&]() __attribute__((always_inline)) {
-    if (wi + 1 < nch) {
-      ++wi;
-      if (++ci == cpg) {
-        ci = 0;
-        rem &= rem - 1;
-        gbase = __builtin_ctz(rem | 0x80000000u) * cpg;
-      }
-    }
-    return gbase + ci;
-  };
-  const char* wcot = reinterpret_cast<const char*>(a.wp + (int64_t)cot * wino::W16 + coh * BNH);
-  const char* tb0 = reinterpret_cast<const char*>(static_cast<const u32x4*>(a.x) + (int64_t)b * K8 * tplane2);
-  struct ChunkBase {
-    const char* w;
-    const char* t;
-    bool kv1;
-  };
-  auto base_of = [&](int ph) __attribute__((always_inline)) {
-    return ChunkBase{wcot + (int64_t)ph * a.n_cot * wino::W16 * 16, tb0 + (int64_t)(2 * ph) * tplane2 * 16,
-                     2 * ph + 1 < K8};
-  };
-  auto issue_unit = [&](const ChunkBase& cb, int xi, int slot) __attribute__((always_inline)) {
-    u32x4* dst = lds + slot * SLOTH + wave * 64;
-    const __amdgpu_buffer_rsrc_t rw =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(cb.w + xi * 3 * 2 * BN * 16), (short)0, 0x7fffffff, 0x00020000);
-#pragma unroll
-    for (int j = 0; j < NWIH; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(dst + j * NT), 16,
-                                               wvo[j], 0, 0, 0);
-    const int32_t rows_b = xi * W * 32;
-    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<char*>(cb.t + rows_b), (short)0, cb.kv1 ? 0x7fffffff : (int)(tplane_b - rows_b), 0x00020000);
-#pragma unroll
-    for (int j = 0; j < NXT; ++j)
-      if ((j * NW + wave) * 64 < TROW)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(dst + RUNITH + j * NT),
-                                                 16, tvo[j], 0, 0, 0);
-  };
-  ChunkBase cur = base_of(gbase + ci);
-  ChunkBase nx = base_of(step());
-  auto advance = [&]() __attribute__((always_inline)) {
-    cur = nx;
-    nx = base_of(step());
-  };
-
-  const int rg = wave;
-  floatx16 acc[2][NXI];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < NXI; ++j) acc[i][j] = floatx16{0};
-  bf16x8 fb[3][2];
-  bf16x8 fa[2][2][2];
-  auto fetch_b = [&](int kw, int slot) __attribute__((always_inline)) {
-    const u32x4* X = lds + slot * SLOTH + RUNITH + kl * (TROW / 2) + rg * XW + l32 + DIL * kw;
-#pragma unroll
-    for (int p = 0; p < 2; ++p) fb[kw][p] = __builtin_bit_cast(bf16x8, X[p * (TROW / 4)]);
-  };
-  auto fetch_a = [&](int st, int slot, int kw) __attribute__((always_inline)) {
-    const u32x4* Wl = lds + slot * SLOTH + kw * 2 * BNH + kl * BNH + l32;
-#pragma unroll
-    for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-      for (int p = 0; p < 2; ++p) fa[st][ct][p] = __builtin_bit_cast(bf16x8, Wl[p * RHALFH + 32 * ct]);
-  };
-  auto sched6 = [&](auto nreads) __attribute__((always_inline)) {
-    constexpr int n = decltype(nreads)::value;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-      if (i < n) __builtin_amdgcn_sched_group_barrier(0x100, (n + 5) / 6, 0);
-    }
-  };
-  constexpr int NXT_LO = TROW / NT;
-  constexpr int WHI = (TROW % NT + 63) / 64;
-  static_assert(NXT_LO + (WHI > 0) == NXT, "T pieces");
-  constexpr int NPU_HI = NWIH + NXT;
-  constexpr int NPU_LO = NWIH + NXT_LO;
-  const bool whi = wave < WHI;
-  if (nch > 0) {
-    const int U = NXI * nch;
-    // prologue: units 0-2 (chunk 0, rows 0-2) in flight, wait for unit 0
-    issue_unit(cur, 0, 0);
-    issue_unit(cur, 1, 1);
-    issue_unit(cur, 2, 2);
-    if (whi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPU_HI) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NPU_LO) : "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    fetch_b(0, 0);
-    fetch_b(1, 0);
-    fetch_a(0, 0, 0);
-#define WINOH_MFMAS(AS, KW, XI)                                                                      \
-  _Pragma("unroll") for (int ct = 0; ct < 2; ++ct) {                                                 \
-    acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][1], fb[KW][0], acc[ct][XI], 0, 0, 0); \
-    acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][1], acc[ct][XI], 0, 0, 0); \
-    acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][0], acc[ct][XI], 0, 0, 0); \
-  }
-#define WINOH_UNIT(R)                                                                                \
-  do {                                                                                               \
-    constexpr int XI = (R) % 5, P = (R) & 1;                                                          \
-    if (u0 + (R) >= U) break;                                                                        \
-    constexpr int slot = (R) % 3, nslot = ((R) + 1) % 3; /* u0 % 30 == 0 */                          \
-    fetch_a(P ^ 1, slot, 1);                                                                         \
-    fetch_b(2, slot);                                                                                \
-    WINOH_MFMAS(P, 0, XI);                                                                           \
-    sched6(std::integral_constant<int, 6>{});                                                        \
-    fetch_a(P, slot, 2);                                                                             \
-    WINOH_MFMAS(P ^ 1, 1, XI);                                                                       \
-    sched6(std::integral_constant<int, 4>{});                                                        \
-    /* retire unit u+1 (u+2 may stay in flight); every LDS read of this unit's slot is done */      \
-    if (whi) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NPU_HI) : "memory");               \
-    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NPU_LO) : "memory");                    \
-    __builtin_amdgcn_s_barrier();                                                                    \
-    asm volatile("" ::: "memory");                                                                   \
-    /* unit u+3 into this slot: (chunk, xi + 3) at xi <= 1, else (next chunk, xi - 2) */            \
-    issue_unit(XI <= 1 ? cur : nx, (XI + 3) % 5, slot);                                              \
-    if (XI == 4) advance();                                                                          \
-    fetch_b(0, nslot);                                                                               \
-    fetch_b(1, nslot);                                                                               \
-    fetch_a(P ^ 1, nslot, 0);                                                                        \
-    WINOH_MFMAS(P, 2, XI);                                                                           \
-    sched6(std::integral_constant<int, 8>{});                                                        \
-  } while (0)
-    // 30 units per trip (the lcm of the 5 xi, the 3 ring slots and the 2 fragment sets)
-    for (int u0 = 0; u0 < U; u0 += 30) {
-      WINOH_UNIT(0); WINOH_UNIT(1); WINOH_UNIT(2); WINOH_UNIT(3); WINOH_UNIT(4);
-      WINOH_UNIT(5); WINOH_UNIT(6); WINOH_UNIT(7); WINOH_UNIT(8); WINOH_UNIT(9);
-      WINOH_UNIT(10); WINOH_UNIT(11); WINOH_UNIT(12); WINOH_UNIT(13); WINOH_UNIT(14);
-      WINOH_UNIT(15); WINOH_UNIT(16); WINOH_UNIT(17); WINOH_UNIT(18); WINOH_UNIT(19);
-      WINOH_UNIT(20); WINOH_UNIT(21); WINOH_UNIT(22); WINOH_UNIT(23); WINOH_UNIT(24);
-      WINOH_UNIT(25); WINOH_UNIT(26); WINOH_UNIT(27); WINOH_UNIT(28); WINOH_UNIT(29);
-    }
-#undef WINOH_UNIT
-#undef WINOH_MFMAS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  floatx16 y[2][3];
-#pragma unroll
-  for (int ct = 0; ct < 2; ++ct) {
-    const floatx16 m0 = acc[ct][0], m1 = acc[ct][1], m2 = acc[ct][2], m3 = acc[ct][3], m4 = acc[ct][4];
-    y[ct][0] = m0 + m1 + m2 + m3;
-    y[ct][1] = m1 - m2 + 2.f * m3;
-    y[ct][2] = m1 + m2 + 4.f * m3 + m4;
-  }
-  ring_epilogue<DIL, RELU, P3>(a, b, y0 + ring_base_row<DIL>(rg), x0 + l32, cot, BNH * coh, y, lds);
-}
-
 // (Round 4, VERDICT r03 item 5: a one-wave-per-SIMD form — 4 waves of 2 row tiles x 64 Cout, xi-major
 // accumulation with the A^T fold after each xi's K sum, 12 + 12 fragment reads per 36 MFMAs — was
 // parity-green but ran 1.75-1.85 ms vs 1.40-1.45 for conv1 and 0.41-0.47 vs 0.34-0.37 for conv2 +
@@ -2024,28 +1795,6 @@ static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_pa
   a.y_split = y_layout == MVBEV_LAYOUT_SPLIT_BF16;
   if (band_rows < 0 || (band_rows > 0 && (a.y_split || p3 || band_rows > d->out_rows))) return MVBEV_ERR_SHAPE;
   a.band_rows = (int)band_rows;
-  if (MVBEV_WINO_HALF) {  // two 64-channel workgroups per Cout tile, two per CU (conv_wino_half_kernel)
-    const int64_t th = 2 * tiles;
-    a.npix = (int)(tiles / a.n_cot);
-    a.mgroup = (group_mask && th >= 16 * (int64_t)std::max(cu_count(), 1)) ? 8 : 1;
-    const int64_t nwg = group_mask ? (int64_t)2 * a.n_cot * round_up(a.npix, 8 * a.mgroup) : th;
-    a.nwg = (int)nwg;
-    hipStream_t s = as_stream(stream);
-    const dim3 grid((unsigned)nwg), blk(winoh::NT);
-    if (p3) {
-      if (dil != 2 || !relu) return MVBEV_ERR_SHAPE;
-      hipLaunchKernelGGL((conv_wino_half_kernel<true, 2, true>), grid, blk, 0, s, a);
-    } else if (dil == 2) {
-      if (relu) hipLaunchKernelGGL((conv_wino_half_kernel<true, 2, false>), grid, blk, 0, s, a);
-      else hipLaunchKernelGGL((conv_wino_half_kernel<false, 2, false>), grid, blk, 0, s, a);
-    } else if (relu) {
-      hipLaunchKernelGGL((conv_wino_half_kernel<true, 1, false>), grid, blk, 0, s, a);
-    } else {
-      hipLaunchKernelGGL((conv_wino_half_kernel<false, 1, false>), grid, blk, 0, s, a);
-    }
-    MVBEV_CHECK_LAUNCH();
-    return MVBEV_OK;
-  }
   a.npix = (int)(tiles / a.n_cot);
   // XCD turns of 8 consecutive ordered pixel tiles (equal view sets: the same weight-chunk stream, shared in
   // the XCD's L2) once the launch is >= 8 rounds deep; shallower launches deal them one at a time, where

@@ -1225,21 +1225,21 @@ def dgrad_tile_rows(dy_split: bool, dilation: int = 1) -> int:
     return _native.conv_tile_rows(_native.LAYOUT_SPLIT_BF16 if dy_split else _native.LAYOUT_F32, dilation)
 
 
-def wgrad_chunk_lists(mask: torch.Tensor, groups: int, B: int, H: int, W: int):
-    """Per channel group, the wgrad pixel chunks (row segments of 32 px) whose window the
-    frustum ``mask`` (``warp_tile_mask`` over rows [0, H), halo >= the conv's dilation) marks
-    as possibly non-zero -> (chunk_list, chunk_off) int32 device tensors."""
+def _chunk_lists(mask: torch.Tensor, groups: int, B: int, rows: int, rows_per_tile: int, W: int):
+    """Per channel group, the (b, row, 32-px segment) chunks whose mask tile (row // rows_per_tile,
+    segment) has the group's bit -> (chunk_list, chunk_off) int32 device tensors (chunk id
+    (b * rows + row) * segments + segment, in that order)."""
     import numpy as np
     tx = -(-W // _native.TILE_W)
     segs = -(-W // 32)
     assert segs == tx, "wgrad chunks are 32 px = one conv tile column"
     m = np.asarray(mask.cpu().numpy(), dtype=np.int64) & 0xFFFFFFFF
-    rows = np.repeat(np.arange(H) // _native.TILE_H, segs) * tx + np.tile(np.arange(segs), H)  # per (y, seg)
-    per_img = m[rows]                                                    # [H * segs]
+    tile = np.repeat(np.arange(rows) // rows_per_tile, segs) * tx + np.tile(np.arange(segs), rows)  # per (row, seg)
+    per_img = m[tile]
     lists, off = [], [0]
     for g in range(groups):
         act = np.nonzero((per_img >> g) & 1)[0]
-        full = (np.arange(B)[:, None] * (H * segs) + act[None, :]).reshape(-1)
+        full = (np.arange(B)[:, None] * (rows * segs) + act[None, :]).reshape(-1)
         lists.append(full)
         off.append(off[-1] + full.size)
     lst = np.concatenate(lists) if lists else np.zeros(0, np.int64)
@@ -1247,6 +1247,13 @@ def wgrad_chunk_lists(mask: torch.Tensor, groups: int, B: int, H: int, W: int):
     return (torch.tensor(lst, dtype=torch.int32, device=dev) if lst.size else torch.zeros(1, dtype=torch.int32,
                                                                                           device=dev),
             torch.tensor(off, dtype=torch.int32, device=dev))
+
+
+def wgrad_chunk_lists(mask: torch.Tensor, groups: int, B: int, H: int, W: int):
+    """Per channel group, the wgrad pixel chunks (row segments of 32 px) whose window the
+    frustum ``mask`` (``warp_tile_mask`` over rows [0, H), halo >= the conv's dilation) marks
+    as possibly non-zero -> (chunk_list, chunk_off) int32 device tensors."""
+    return _chunk_lists(mask, groups, B, H, _native.TILE_H, W)
 
 
 def split_rows_shape(B: int, C: int, H: int, W: int):
@@ -1356,27 +1363,9 @@ def wgrad_wino_chunk_lists(mask: torch.Tensor, groups: int, B: int, H: int, W: i
     """Per channel group, the Winograd wgrad chunks (b, r3 < ceil(H/3), 32-px segment) whose T row
     can be non-zero: the forward's 12-row frustum ``mask`` (``conv1_mask(tile_h=12)``, the mask T was
     written under) at tile (r3 // 4, segment) -> (chunk_list, chunk_off) int32 device tensors."""
-    import numpy as np
-    tx = -(-W // _native.TILE_W)
-    segs = -(-W // 32)
-    assert segs == tx, "wgrad chunks are 32 px = one conv tile column"
-    r3n = -(-H // 3)
-    if mask.numel() != -(-H // 12) * tx:
+    if mask.numel() != -(-H // 12) * (-(-W // _native.TILE_W)):
         raise ValueError("the mask must be over 12-row conv tiles (the rows T was written in)")
-    m = np.asarray(mask.cpu().numpy(), dtype=np.int64) & 0xFFFFFFFF
-    rows = np.repeat(np.arange(r3n) // 4, segs) * tx + np.tile(np.arange(segs), r3n)  # per (r3, seg)
-    per_img = m[rows]
-    lists, off = [], [0]
-    for g in range(groups):
-        act = np.nonzero((per_img >> g) & 1)[0]
-        full = (np.arange(B)[:, None] * (r3n * segs) + act[None, :]).reshape(-1)
-        lists.append(full)
-        off.append(off[-1] + full.size)
-    lst = np.concatenate(lists) if lists else np.zeros(0, np.int64)
-    dev = mask.device
-    return (torch.tensor(lst, dtype=torch.int32, device=dev) if lst.size else torch.zeros(1, dtype=torch.int32,
-                                                                                          device=dev),
-            torch.tensor(off, dtype=torch.int32, device=dev))
+    return _chunk_lists(mask, groups, B, wino_r3(H), 4, W)
 
 
 def conv3x3_wgrad_wino(t: torch.Tensor, desc, dy_wino: torch.Tensor, cin_w: int,

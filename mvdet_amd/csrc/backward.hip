@@ -1696,6 +1696,10 @@ static mvbev::bwd::WGeo wgrad_wino_geo(const mvbev_conv_desc* d, int64_t Cout, i
   g.tiles = (Cout / MT) * ceil_div(d->K, 2 * NT);  // 128 input channels per workgroup
   g.nchunks = d->B * wino_r3(d->H, dil) * ceil_div(d->W, PX);
   g.P = wgrad_partitions(5 * g.tiles, g.nchunks, 0.07);
+  // a partition's chunk ids are staged in LDS (WG_MAXC): more partitions for long chunk lists (large
+  // grids, batches) rather than a refusal the training backward could not fall back from (its forward
+  // may not have written the slab)
+  while (g.nchunks / g.P + 1 > WG_MAXC && g.P < g.nchunks) ++g.P;
   return g;
 }
 

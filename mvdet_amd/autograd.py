@@ -92,7 +92,7 @@ def _train_workspace(engine: ProjectFuse, B: int, device) -> Workspace:
         ws.wino_t, ws.wino_t2 = t1, t2
         # conv1's weight gradient from T (_wgrad1_wino) is the backward's only reader of the forward's
         # conv1 input: the fused warp may write T and skip the slab (one pass, no B^T of the slab)
-        ws.train_t_only = W % 8 == 0 and engine.Cs % 128 == 0 and _native.load().mvbev_version() >= 12000
+        ws.train_t_only = _wgrad1_wino_fits(engine, B)
     return ws
 
 
@@ -208,11 +208,20 @@ def _dgrad1_wino(engine: ProjectFuse, st, dy1s: torch.Tensor, w1: torch.Tensor, 
     ops.conv3x3_wino_dgrad(st.t1d, d, st.pack1t.get(w1), nc, dslab, out_mask=cm, cot_per_group=C // ops.BN)
 
 
+def _wgrad1_wino_fits(engine: ProjectFuse, B: int) -> bool:
+    """conv1's Winograd weight gradient takes this geometry (``mvbev_conv3x3_wgrad_wino_bf16x3``'s limits:
+    W % 8, 128-channel slots, B < 128, 32-bit offsets), so the forward may skip the slab."""
+    H, W = engine.grid_hw
+    K, r3, r5 = engine.S * engine.Cs, -(-H // 3), 20 * (-(-H // 12))
+    return (W % 8 == 0 and engine.Cs % 128 == 0 and engine.mid % 128 == 0 and B < 128 and r3 <= 4096
+            and -(-W // 32) <= 4096 and (K // 8) * 2 * r5 * W < 2 ** 31 - 1 and engine.mid * r3 * W < 2 ** 31 - 1
+            and _native.load().mvbev_version() >= 12000)
+
+
 def _wgrad1_wino_applies(engine: ProjectFuse, ws: Workspace, dy1: torch.Tensor) -> bool:
     """conv1's weight gradient runs row-Winograd (``_wgrad1_wino``) when the forward's conv1 did
     (its whole-grid transform T is in ``ws.wino_t``), with whole 128-channel slot tiles."""
-    return (ws.t1_valid and ws.wino_t is not None and dy1.shape[3] % 8 == 0 and engine.Cs % 128 == 0
-            and _native.load().mvbev_version() >= 12000)
+    return ws.t1_valid and ws.wino_t is not None and _wgrad1_wino_fits(engine, dy1.shape[0])
 
 
 def _wgrad1_wino(engine: ProjectFuse, st, ws: Workspace, d1, dy1: torch.Tensor, dw1: torch.Tensor) -> None:

@@ -329,7 +329,7 @@ class ProjectFuseFunction(torch.autograd.Function):
         if db2 is not None:
             ops.conv3x3_bias_coord_grad(dy2, 2, db=db2)
         d_y1 = ops.conv_desc(B, mid, H, W, group=mid, group_stride=0, batch_stride=mid * H * W)
-        if ws.t2_valid and W % 8 == 0 and mid % 128 == 0:  # from the forward's dilation-2 transform
+        if ws.t2_valid and W % 8 == 0 and mid % 128 == 0 and B < 128 and H <= 12 * 1024:  # from conv2's own T
             dw2 = ops.conv3x3_wgrad_wino(ws.wino_t2, d_y1, ops.wino_dy_rows(dy2, dilation=2), mid, dilation=2,
                                          workspace=_wgrad_wino_ws(st, d_y1, mid, 2, dev))
         else:  # (the direct form reads the fp32 dy2: at its size the row split costs what it saves)

@@ -721,16 +721,20 @@ def test_training_steps_reuse_the_zeroed_slab():
         assert torch.equal(a, b)
 
 
-def test_full_size_training_step_vs_cpu_autograd():
-    """The training step at config 2's full size (Wildtrack 7 x 512 x 270 x 480 -> 120 x 360,
-    ``trainer.py:38-47`` on ``persp_trans_detector.py:65-87`` past the upsample): the default engine
-    (row-Winograd conv1 / conv2 forward and data gradients, conv1's with the output-side frustum
-    mask) vs torch-CPU fp32 autograd through the reference path on identical inputs — the map and
-    every gradient (7 view features, 5 head parameters) within the 1e-3 gate, given the GPU's ReLU
-    patterns (the few pre-activations within rounding of zero are checked as in the small cases)."""
+@pytest.mark.parametrize("cfg", [2, 1])
+def test_full_size_training_step_vs_cpu_autograd(cfg):
+    """The training step at full size (config 2: Wildtrack 7 x 512 x 270 x 480 -> 120 x 360; config 1:
+    MultiviewX 6 x 128 -> 160 x 250), ``trainer.py:38-47`` on ``persp_trans_detector.py:65-87`` past the
+    upsample: the default engine (row-Winograd conv1 / conv2 forward and data gradients, conv1's with
+    the output-side frustum mask; at config 2 the fused warp writes T and both weight gradients run from
+    the forward transforms, at config 1 — W = 250, not a multiple of 8 — the slab path and the direct
+    conv1 weight gradient) vs torch-CPU fp32 autograd through the reference path on identical inputs —
+    the map and every gradient (view features, 5 head parameters) within the 1e-3 gate, given the
+    GPU's ReLU patterns (the few pre-activations within rounding of zero are checked as in the small
+    cases)."""
     from mvdet_amd import ProjectFuse, autograd, synthetic
     from mvdet_amd.geometry import projection_matrices
-    spec = synthetic.CONFIGS[2]
+    spec = synthetic.CONFIGS[cfg]
     ds = spec["make"]()
     B, C, N = spec["B"], spec["C"], ds.num_cam
     up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
@@ -746,21 +750,22 @@ def test_full_size_training_step_vs_cpu_autograd():
     fg = [f.clone().requires_grad_() for f in feats]
     out = autograd.project_fuse(eng, fg, mc)
     ws = out.grad_fn.ws
+    assert ws.t_from_warp == ws.train_t_only == (cfg == 2) and ws.t1_valid
     m1, m2 = (eng.y1_fp32(ws) > 0).float().cpu(), (ws.y2 > 0).float().cpu()
     gmap = torch.from_numpy(np.random.default_rng(2).standard_normal(tuple(out.shape)).astype(np.float32))
     out.backward(gmap.to(DEV))
     torch.cuda.synchronize()
     out_ref, pre1, pre2, gfeat, gpar = _cpu_reference([f.cpu() for f in feats], [M.numpy() for M in pm], grid,
                                                       params, gmap, masks=(m1, m2))
-    assert_parity(out.detach().cpu(), out_ref, "cfg2 training forward")
+    assert_parity(out.detach().cpu(), out_ref, f"cfg{cfg} training forward")
     for m, pre, what in ((m1, pre1, "conv1"), (m2, pre2, "conv2")):
         flip = m != (pre > 0).float()
         assert flip.sum().item() <= max(2, pre.numel() // 20000), what
         assert (pre[flip].abs() <= 1e-4 * pre.abs().max()).all(), what
     for v in range(N):
-        assert_parity_t(fg[v].grad, gfeat[v], f"cfg2 d feat view {v}")
+        assert_parity_t(fg[v].grad, gfeat[v], f"cfg{cfg} d feat view {v}")
     for k, p in mc.named_parameters():
-        assert_parity_t(p.grad, gpar["map_classifier." + k], f"cfg2 d {k}")
+        assert_parity_t(p.grad, gpar["map_classifier." + k], f"cfg{cfg} d {k}")
 
 
 def test_detector_full_size_training_step_vs_cpu_autograd():

@@ -138,6 +138,7 @@ def main():
     ap.add_argument("--precision", default="bf16x3", choices=["fp32", "bf16x3"],
                     help="conv1/conv2 arithmetic: fp32 MFMA or 3xbf16 split (fp32-class accuracy)")
     ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=0, help="override the config's batch size (0 = the config's)")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--only", default="warp,conv1,conv2,conv3")
     ap.add_argument("--libs", default="", help="comma-separated libmvbev variants to A/B (interleaved rounds)")
@@ -146,7 +147,7 @@ def main():
     args = ap.parse_args()
     spec = synthetic.CONFIGS[args.config]
     ds = spec["make"]()
-    B, C, N = spec["B"], spec["C"], ds.num_cam
+    B, C, N = (args.batch or spec["B"]), spec["C"], ds.num_cam
     up = tuple(ds.upsample_shape)
     ho, wo = ds.reducedgrid_shape
     dev = torch.device("cuda:0")

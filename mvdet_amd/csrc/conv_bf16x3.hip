@@ -160,12 +160,6 @@ template <> __device__ inline float ld<_Float16>(const _Float16* p) { return (fl
 #ifndef MVBEV_B3_MINWAVES
 #define MVBEV_B3_MINWAVES 1
 #endif
-#ifndef MVBEV_MG_SHALLOW
-#define MVBEV_MG_SHALLOW 1  // the Winograd conv's mask group for launches < 8 rounds deep
-#endif
-#ifndef MVBEV_MG_SNAKE
-#define MVBEV_MG_SNAKE 0
-#endif
 #ifndef MVBEV_MASK_GROUP
 #define MVBEV_MASK_GROUP 1  // consecutive ordered pixel tiles per XCD turn (ring kernel, cfg2 conv1: 1 2.17-2.24 ms, 2 2.23-2.28, 4 2.41)
 #endif
@@ -1496,10 +1490,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     const int Gq = a.mgroup;
     const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
     const int q = j / a.n_cot;
-    // (MVBEV_MG_SNAKE: odd turns deal the groups to the XCDs in reverse, so an XCD's heavy and light
-    // groups alternate)
-    const int xs = (MVBEV_MG_SNAKE && ((q / Gq) & 1)) ? 7 - x : x;
-    const int slot = Gq * (8 * (q / Gq) + xs) + q % Gq;
+    const int slot = Gq * (8 * (q / Gq) + x) + q % Gq;
     if (slot >= a.npix) return;  // padding block (whole block, before any barrier)
     tile = (a.tile_order ? a.tile_order[slot] : slot) * a.n_cot + j % a.n_cot;
   }
@@ -1809,7 +1800,7 @@ static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_pa
   // the XCD's L2) once the launch is >= 8 rounds deep; shallower launches deal them one at a time, where
   // the balance of the first rounds decides (cfg2, 1.9 rounds: groups of 4 +7 %; cfg5, 42 rounds: 8 -5 %,
   // cfg3 -2 %: profiles/r05o_mask_group_ab.jsonl, r05v_mask_group_large_ab.jsonl)
-  a.mgroup = (group_mask && tiles >= 8 * (int64_t)std::max(cu_count(), 1)) ? 8 : MVBEV_MG_SHALLOW;
+  a.mgroup = (group_mask && tiles >= 8 * (int64_t)std::max(cu_count(), 1)) ? 8 : 1;
   const int64_t nwg = group_mask ? (int64_t)a.n_cot * round_up(a.npix, 8 * a.mgroup) : tiles;
   a.nwg = (int)nwg;
   hipStream_t s = as_stream(stream);

@@ -42,7 +42,7 @@ from .pipeline import ProjectFuse
 
 class PerspTransDetector(nn.Module):
     def __init__(self, dataset, arch: str = "resnet18", device=None, precision: str = "bf16x3",
-                 wino_conv1: bool = True, wino_conv2: bool = True):
+                 wino_conv1: bool = True, wino_conv2: bool = True, channels_last: bool = True):
         super().__init__()
         self.num_cam = dataset.num_cam
         self.img_shape, self.reducedgrid_shape = list(dataset.img_shape), list(dataset.reducedgrid_shape)
@@ -61,8 +61,16 @@ class PerspTransDetector(nn.Module):
                                             nn.Conv2d(512, 512, 3, padding=2, dilation=2), nn.ReLU(),
                                             nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False))
         self.to(self._device)
-        # inference conv1 and conv2 as row-Winograd F(3,3) (ProjectFuse.conv1_wino, conv2_partials);
-        # training keeps the direct convs (their backward reads the direct form's operands)
+        # the backbone in torch's channels_last memory format (the same weights and state_dict): its maps then
+        # reach the fused upsample warp's line-per-pixel kernel without a transposing copy (cfg2: 0.29-0.32 vs
+        # 0.39 ms), and the MIOpen backbone itself ran no slower (7 x 720 x 1280: 21.4 vs 22.8 ms,
+        # profiles/r05ah_backbone_layout.json)
+        self.channels_last = bool(channels_last)
+        if self.channels_last:
+            self.base_pt1.to(memory_format=torch.channels_last)
+            self.base_pt2.to(memory_format=torch.channels_last)
+        # conv1 and conv2 as row-Winograd F(3,3) (ProjectFuse.conv1_wino, conv2_partials), inference and
+        # training (forward, data and weight gradients: autograd.py)
         self.engine = ProjectFuse(self.proj_mats, tuple(self.upsample_shape), tuple(self.reducedgrid_shape),
                                   out_channel, precision=precision, wino_conv1=wino_conv1, wino_conv2=wino_conv2)
 
@@ -80,7 +88,8 @@ class PerspTransDetector(nn.Module):
         ws = None if training else self.engine.workspace(B, dev)
         imgs_result, low = [], []
         for cam in range(self.num_cam):
-            feat = self.base_pt1(imgs[:, cam].to(dev))
+            x = imgs[:, cam].to(dev)
+            feat = self.base_pt1(x.contiguous(memory_format=torch.channels_last) if self.channels_last else x)
             feat = self.base_pt2(feat)
             # the image head runs its first 1x1 conv before upsampling (it commutes with the
             # bilinear upsample: per-pixel affine, weights summing to 1) on 64 instead of 512

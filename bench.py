@@ -381,8 +381,10 @@ def run_plus_a4(args, precision, steps, warmup):
         out[mode] = {"value": round(B * steps / dt, 3), "ms_per_step": round(dt * 1e3 / steps, 4),
                      "upsample_and_warp_ms": round(float(np.mean([e0[i].elapsed_time(e1[i]) for i in range(steps)])), 4)}
     out["note"] = ("step from backbone-resolution features: a4 upsample (:65) + warp + concat + fusion; "
-                   "fused = upsample evaluated inside the warp kernel (NCHW maps); fused_channels_last = the same "
-                   "maps in channels_last memory format (warp_up_wino_cl_kernel)")
+                   "fused = upsample evaluated inside the warp kernel (NCHW maps: a transposing copy, then "
+                   "warp_up_wino_cl_kernel); fused_channels_last = the same maps in channels_last memory format, "
+                   "as mvdet_amd.PerspTransDetector's channels-last backbone produces them by default (no copy)")
+    out["detector_default"] = "fused_channels_last"
     return out
 
 

@@ -478,8 +478,9 @@ def run_train_step(config: int, precision: str, steps: int, warmup: int, with_to
     # "+a4": the step the drop-in module trains through (trainer.py:38-47 calling
     # persp_trans_detector.py:65-87): from the backbone-resolution maps, the 3x upsample included
     # (native: fused into the warp and its adjoint into the warp adjoint)
-    bfeats = [synthetic.backbone_features(B, C, [u // 3 for u in up], seed=v, device=dev).requires_grad_()
-              for v in range(N)]
+    # (channels-last maps: PerspTransDetector's backbone runs channels_last by default)
+    bfeats = [synthetic.backbone_features(B, C, [u // 3 for u in up], seed=v, device=dev)
+              .contiguous(memory_format=torch.channels_last).requires_grad_() for v in range(N)]
 
     def native_a4():
         for f in bfeats:
@@ -499,7 +500,8 @@ def run_train_step(config: int, precision: str, steps: int, warmup: int, with_to
 
         a4["torch_gpu"] = run(torch_a4, max(2, steps // 4), 1)
         a4["speedup_vs_torch_gpu"] = round(a4["native"]["value"] / a4["torch_gpu"]["value"], 2)
-    a4["note"] = "from backbone-resolution maps (a4 upsample :65 included) as the drop-in module trains"
+    a4["note"] = ("from backbone-resolution maps (a4 upsample :65 included) as the drop-in module trains: "
+                  "channels-last maps, as its backbone produces them")
     res["plus_a4"] = a4
     return res
 

@@ -59,7 +59,7 @@ constexpr int CPW = MVBEV_WGRAD_CPW;
 constexpr int NWV = 8 / CPW;  // waves per workgroup: (4 / CPW) (output channels) x 2 (input channels)
 constexpr int NTH = 64 * NWV;
 constexpr int MT = 128;       // output channels per workgroup
-constexpr int NT = 64;        // input channels per workgroup
+constexpr int NT = 64;        // input channels per workgroup (the Winograd form: 2 NT)
 constexpr int PX = 32;        // pixels per chunk (one row segment) = 2 K-steps
 constexpr int AP = PX + 8;    // bf16 per A-image row (80 B)
 

@@ -1474,10 +1474,19 @@ __global__ __launch_bounds__(256) void wino_rows_kernel(const WinoRowsArgs a) {
 // counts); the T DMAs keep the default cache policy (nt measured +0.5 % on conv1, +1 % on conv2).
 // DIL 2 (conv2): the wave's row tile is the ring kernel's interleaved rows base + 2 pt; P3: the
 // epilogue forms conv3's partial sums (cout1_partials) instead of storing y
+#ifndef MVBEV_WINO_STAMPS
+#define MVBEV_WINO_STAMPS 0  // diagnostic builds only: per-workgroup start / end clocks and CU of the last launch
+#endif
+#if MVBEV_WINO_STAMPS
+__device__ long long g_wino_stamps[4 * 65536];
+#endif
 template <bool RELU, int DIL, bool P3>
 __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   using namespace wino;
   using G = Geo<DIL>;
+#if MVBEV_WINO_STAMPS
+  const long long stamp0 = wall_clock64();
+#endif
   constexpr int XW = G::XW, TROW = G::TROW, NXT = G::NXT;
   __shared__ __attribute__((aligned(16))) u32x4 lds[LDS];
   const int W = a.W;
@@ -1713,6 +1722,14 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     y[ct][2] = m1 + m2 + 4.f * m3 + m4;
   }
   ring_epilogue<DIL, RELU, P3>(a, b, y0 + ring_base_row<DIL>(rg), x0 + l32, cot, cw, y, lds);
+#if MVBEV_WINO_STAMPS
+  __syncthreads();
+  if (threadIdx.x < 4 && blockIdx.x < 65536) {  // lanes 0-3 store one field each (vector stores)
+    const long long v = threadIdx.x == 0 ? stamp0 : threadIdx.x == 1 ? wall_clock64()
+                      : threadIdx.x == 2 ? (long long)__smid() : (long long)tile;
+    g_wino_stamps[4 * blockIdx.x + threadIdx.x] = v;
+  }
+#endif
 }
 
 // (Round 4, VERDICT r03 item 5: a one-wave-per-SIMD form — 4 waves of 2 row tiles x 64 Cout, xi-major
@@ -2017,6 +2034,14 @@ int mvbev_pack_conv3x3_weight_wino_dgrad(const float* w, int64_t Cout_f, int64_t
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }
+
+#if MVBEV_WINO_STAMPS
+int mvbev_debug_wino_stamps(void* host, size_t bytes) {
+  const size_t n = std::min(bytes, sizeof(mvbev::b3::g_wino_stamps));
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(mvbev::b3::g_wino_stamps), n, 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? MVBEV_OK : MVBEV_ERR_HIP;
+}
+#endif
 
 size_t mvbev_wino_rows_bytes(const mvbev_conv_desc* d) {
   using namespace mvbev;

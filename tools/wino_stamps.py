@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--out", default="")
     args = ap.parse_args()
     spec = synthetic.CONFIGS[args.config]
     ds = spec["make"]()
@@ -32,15 +33,15 @@ def main():
     ws = eng.workspace(B, dev)
     feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=v, device=dev) for v in range(N)]
     eng.warp_views(ws, list(range(N)), feats)
-    ho, wo = grid
-    d1 = ops.conv_desc(B, eng.S * eng.Cs, ho, wo, group=eng.Cs, group_stride=B * eng.Cs * ho * wo,
-                       batch_stride=eng.Cs * ho * wo)
-    gm = eng.conv1_mask(dev, 0, ho)
-    ops.wino_rows(ws.slab, d1, ws.wino_t, gm)
+    d1 = eng._conv1_desc(B)
+    init = eng.coord_term(mc[0])
+    eng.conv1_wino(ws, mc[0], d1, init)  # allocates wino_t and writes T (the product path)
+    torch.cuda.synchronize()
     lib = _native.load()
-    run = lambda: ops.conv3x3_wino(ws.wino_t, d1, eng.pack1w.get(mc[0].weight), 512, init=eng.coord_term(mc[0]),
-                                   relu=True, out=ws.y1, group_mask=gm, tile_order=eng.conv1_order(dev, 0, ho, B, grid=True))
+    run = lambda: eng.conv1_wino(ws, mc[0], d1, init)
     res = []
+    gmh = eng.conv1_mask(dev, 0, grid[0]).cpu().numpy().astype(np.uint32)
+    dumps = []
     for rep in range(5):
         run()
         torch.cuda.synchronize()
@@ -65,7 +66,11 @@ def main():
                     "cu_last_end_us_p10_p50_max": [round(last_end[len(last_end) // 10], 1),
                                                    round(last_end[len(last_end) // 2], 1), round(last_end[-1], 1)],
                     "wg_us_min_med_max": [round(dur.min(), 1), round(float(np.median(dur)), 1), round(dur.max(), 1)]})
-        res[-1]["stamps_wrapped"] = rep  # (each launch rewrites the blocks it runs)
+        pp = (s[:, 3] // 4) % gmh.size
+        nch = np.array([bin(int(m)).count("1") for m in gmh[pp]])
+        dumps.append(np.column_stack([s[:, 0] - t0, s[:, 1] - t0, s[:, 2], s[:, 3], nch]))
+    if args.out:
+        np.savez(args.out, *dumps)
     print(json.dumps({"config": args.config, "B": B, "runs": res}))
 
 

@@ -1635,7 +1635,10 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   constexpr int NPU_HI = NWI + NXT;
   constexpr int NPU_LO = NWI + NXT_LO;
   const bool whi = wave < WHI;
-  constexpr bool PB = DIL == 2;  // one barrier per two units for conv2
+#ifndef MVBEV_WINO_PB2
+#define MVBEV_WINO_PB2 1  // conv2 (dilation 2): one barrier per two units (0: one per unit, as conv1)
+#endif
+  constexpr bool PB = DIL == 2 && MVBEV_WINO_PB2;  // one barrier per two units for conv2
   if (nch > 0) {
     const int U = NXI * nch;
     // prologue: units 0-3 (chunk 0, rows 0-3) in flight, wait for unit 0

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 12100: mvbev_conv3x3_wino_bf16x3_sched (scheduled row-Winograd conv1); 12000: conv1's and conv2's weight gradients from the forward's row-Winograd transforms (mvbev_wino_dy_rows_f32, mvbev_conv3x3_wgrad_wino_bf16x3); 11900: row windows (mvbev_warp_views_split_bf16_rows with the non-finite report, mvbev_warp_views_exact_rows with fp16 sources), mvbev_conv3x3_f32_ex (row-band output), mvbev_bias_relu_nonfinite_f32, mvbev_zero_gated — the non-finite guard of the multi-GPU modes and the banded exact path; 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 12000: conv1's and conv2's weight gradients from the forward's row-Winograd transforms (mvbev_wino_dy_rows_f32, mvbev_conv3x3_wgrad_wino_bf16x3); 11900: row windows (mvbev_warp_views_split_bf16_rows with the non-finite report, mvbev_warp_views_exact_rows with fp16 sources), mvbev_conv3x3_f32_ex (row-band output), mvbev_bias_relu_nonfinite_f32, mvbev_zero_gated — the non-finite guard of the multi-GPU modes and the banded exact path; 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -572,13 +572,6 @@ int mvbev_conv3x3_dgrad_bf16x3_sched(const void* dy, int dy_layout, const mvbev_
                                      const void* w_packed, int64_t Cout_p, int dilation, void* dx, int dx_layout,
                                      const uint32_t* out_mask, int64_t cot_per_group,
                                      const mvbev_conv_schedule* sched, void* stream);
-/* mvbev_conv3x3_wino_bf16x3 (row-Winograd conv1: init, group_mask, fp32 or split-bf16 y, no row bands)
- * run as scheduled (ABI 12100): items as above over its 12 x 32 pixel tiles (the schedule replaces
- * tile_order and the XCD dealing); a piece leaves its tile's partial sums after A^T, the ring fixup
- * adds them in slot order and writes the tile with init, bias and ReLU (ProjectFuse level_conv1). */
-int mvbev_conv3x3_wino_bf16x3_sched(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,
-                                    const float* init, int64_t Cout, int relu, void* y, int y_layout,
-                                    const uint32_t* group_mask, const mvbev_conv_schedule* sched, void* stream);
 
 /* Weights for the data gradient of a 3x3 stride-1 conv with padding = dilation: that gradient is
  * the same conv over dy with w'[k][co][t] = w[co][k][8 - t], so mvbev_conv3x3_bf16x3_ex computes

@@ -55,7 +55,6 @@ EXPORTS = (
     "mvbev_split_rows_bf16",
     "mvbev_conv_schedule_slot_bytes",
     "mvbev_conv3x3_dgrad_bf16x3_sched",
-    "mvbev_conv3x3_wino_bf16x3_sched",
     "mvbev_conv_ring_tile_space",
     "mvbev_conv3x3_bf16x3_ex3",
     "mvbev_conv3x3_packed_bytes_wino",
@@ -298,9 +297,6 @@ def _declare(lib):
     lib.mvbev_conv3x3_dgrad_bf16x3_sched.argtypes = [_p, ctypes.c_int, ctypes.POINTER(ConvDesc), _p, _i64,
                                                      ctypes.c_int, _p, ctypes.c_int, _p, _i64,
                                                      ctypes.POINTER(ConvSchedule), _p]
-    lib.mvbev_conv3x3_wino_bf16x3_sched.restype = ctypes.c_int
-    lib.mvbev_conv3x3_wino_bf16x3_sched.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64, ctypes.c_int, _p,
-                                                    ctypes.c_int, _p, ctypes.POINTER(ConvSchedule), _p]
     lib.mvbev_warp_adjoint_plan.restype = ctypes.c_int
     lib.mvbev_warp_adjoint_plan.argtypes = [ctypes.POINTER(ctypes.c_float), _i64, _i64, _i64, _i64, _p, _p, _p, _p,
                                             _p]

@@ -1495,13 +1495,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   const int l32 = lane & 31, kl = lane >> 5;
 
   int tile = xcd_remap(blockIdx.x, a.nwg);
-  int ci0 = 0, ci1 = INT_MAX, pslot = -1;  // chunk range of this block's tile, partial slot
-  if (a.items) {  // host schedule (mvbev_conv_schedule): the block's item (tile < 0: idle block)
-    if ((int)blockIdx.x >= a.nitems) return;
-    const int4 it = a.items[blockIdx.x];
-    if (it.x < 0 || it.x >= a.tiles_x * a.tiles_y * a.n_cot * a.B) return;
-    tile = it.x, ci0 = it.y, ci1 = it.z, pslot = it.w;
-  } else if (a.gmask) {  // ordered pixel tiles dealt to the XCDs, as the ring kernel (groups of a.mgroup)
+  if (a.gmask) {  // ordered pixel tiles dealt to the XCDs, as the ring kernel (groups of a.mgroup)
     const int Gq = a.mgroup;
     const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
     const int q = j / a.n_cot;
@@ -1519,9 +1513,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   // tile is never read — the whole block leaves before any barrier)
   if (a.cmask && !((a.cmask[pp] >> (cot / a.cot_pg)) & 1u)) return;
   const uint32_t gm = a.gmask ? a.gmask[pp] : 0u;
-  const int nch_tile = a.gmask ? __builtin_popcount(gm) * a.cpg : a.nchunks;
-  ci1 = min(ci1, nch_tile);
-  const int nch = max(ci1 - ci0, 0);  // this block's chunks: [ci0, ci1) of the tile's active sequence
+  const int nch = a.gmask ? __builtin_popcount(gm) * a.cpg : a.nchunks;
   const int K8 = a.K / SB;
   const int64_t tplane2 = 2LL * (XH * a.tiles_y) * W;  // 16-B pieces per 8-channel block of T
   const uint32_t tplane_b = (uint32_t)(tplane2 * 16);  // < 2^30 (host check)
@@ -1551,11 +1543,10 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   }
   // the tile's physical chunks, walked incrementally: group = lowest set bit of the mask left,
   // chunk = group * cpg + index in the group (past the last chunk the walk stays there: dummy
-  // loads that keep the vmcnt counts exact); a scheduled piece starts at the tile's chunk ci0
-  const int cpg = a.gmask ? a.cpg : max(nch_tile, 1);
+  // loads that keep the vmcnt counts exact)
+  const int cpg = a.gmask ? a.cpg : max(nch, 1);
   uint32_t rem = a.gmask ? gm : 1u;
-  for (int j = ci0 / cpg; j > 0; --j) rem &= rem - 1;
-  int gbase = a.gmask ? __builtin_ctz(rem | 0x80000000u) * cpg : 0, ci = ci0 % cpg, wi = 0;
+  int gbase = a.gmask ? __builtin_ctz(gm | 0x80000000u) * cpg : 0, ci = 0, wi = 0;
   auto step = [&]() __attribute__((always_inline)) {
     if (wi + 1 < nch) {
       ++wi;
@@ -1733,10 +1724,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     y[ct][1] = m1 - m2 + 2.f * m3;
     y[ct][2] = m1 + m2 + 4.f * m3 + m4;
   }
-  if (pslot >= 0)  // a piece of a split tile: raw sums (after A^T, which is linear), finished by the fixup
-    ring_store_partial(a.sk_ws, pslot, y);
-  else
-    ring_epilogue<DIL, RELU, P3>(a, b, y0 + ring_base_row<DIL>(rg), x0 + l32, cot, cw, y, lds);
+  ring_epilogue<DIL, RELU, P3>(a, b, y0 + ring_base_row<DIL>(rg), x0 + l32, cot, cw, y, lds);
 #if MVBEV_WINO_STAMPS
   __syncthreads();
   if (threadIdx.x < 4 && blockIdx.x < 65536) {  // lanes 0-3 store one field each (vector stores)
@@ -1788,8 +1776,7 @@ static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_pa
                        const float* init, int64_t Cout, int relu, float* y, int y_layout,
                        const uint32_t* group_mask, const int32_t* tile_order, void* stream, int dil = 1,
                        const float* w3 = nullptr, float* p3 = nullptr, int64_t band_rows = 0,
-                       const uint32_t* out_mask = nullptr, int64_t cot_pg = 1,
-                       const mvbev_conv_schedule* sched = nullptr) {
+                       const uint32_t* out_mask = nullptr, int64_t cot_pg = 1) {
   if (!t || !d || !w_packed || (!y && !p3)) return MVBEV_ERR_NULL;
   if (dil != 1 && dil != 2) return MVBEV_ERR_DILATION;
   if (p3 && (!w3 || group_mask || init)) return MVBEV_ERR_SHAPE;  // the conv2 -> conv3 form: dense, bias only
@@ -1835,27 +1822,9 @@ static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_pa
   // cfg3 -2 %: profiles/r05o_mask_group_ab.jsonl, r05v_mask_group_large_ab.jsonl)
   a.mgroup = (group_mask && tiles >= 8 * (int64_t)std::max(cu_count(), 1)) ? 8 : 1;
   const int64_t nwg = group_mask ? (int64_t)a.n_cot * round_up(a.npix, 8 * a.mgroup) : tiles;
-  int64_t nwg_run = nwg;
-  if (sched) {  // host schedule: items replace the dealing, split tiles' pieces go through the ring fixup
-    if (p3 || out_mask || sched->nitems < 0 || sched->nfix < 0 || sched->nslots < 0 ||
-        (!sched->items && sched->nitems) || (sched->nfix && (!sched->fixups || !sched->partials)))
-      return MVBEV_ERR_SHAPE;
-    if (sched->partial_bytes < (size_t)sched->nslots * sizeof(floatx4) * kRingSlotF4) return MVBEV_ERR_SHAPE;
-    if ((reinterpret_cast<uintptr_t>(sched->items) & 15) || (reinterpret_cast<uintptr_t>(sched->fixups) & 15) ||
-        (reinterpret_cast<uintptr_t>(sched->partials) & 15))
-      return MVBEV_ERR_ALIGN;
-    a.items = reinterpret_cast<const int4*>(sched->items);
-    a.nitems = sched->nitems;
-    a.fix = reinterpret_cast<const int4*>(sched->fixups);
-    a.nfix = sched->nfix;
-    a.sk_ws = static_cast<float*>(sched->partials);
-    a.tile_order = nullptr;
-    nwg_run = sched->nitems;
-    if (nwg_run == 0) return MVBEV_OK;
-  }
-  a.nwg = (int)nwg_run;
+  a.nwg = (int)nwg;
   hipStream_t s = as_stream(stream);
-  const dim3 grid((unsigned)nwg_run), blk(RNT);
+  const dim3 grid((unsigned)nwg), blk(RNT);
   if (p3) {
     if (dil != 2 || !relu) return MVBEV_ERR_SHAPE;  // conv2 -> conv3 of map_classifier (the only use)
     hipLaunchKernelGGL((conv_wino_kernel<true, 2, true>), grid, blk, 0, s, a);
@@ -1866,17 +1835,6 @@ static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_pa
     hipLaunchKernelGGL((conv_wino_kernel<true, 1, false>), grid, blk, 0, s, a);
   } else {
     hipLaunchKernelGGL((conv_wino_kernel<false, 1, false>), grid, blk, 0, s, a);
-  }
-  if (a.nfix > 0) {  // the split tiles: pieces summed in K order, the tile written by the same epilogue
-    const dim3 fg((unsigned)a.nfix);
-    if (dil == 2) {
-      if (relu) hipLaunchKernelGGL((conv_ring_fixup_kernel<2, true, false>), fg, blk, 0, s, a);
-      else hipLaunchKernelGGL((conv_ring_fixup_kernel<2, false, false>), fg, blk, 0, s, a);
-    } else if (relu) {
-      hipLaunchKernelGGL((conv_ring_fixup_kernel<1, true, false>), fg, blk, 0, s, a);
-    } else {
-      hipLaunchKernelGGL((conv_ring_fixup_kernel<1, false, false>), fg, blk, 0, s, a);
-    }
   }
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
@@ -2110,14 +2068,6 @@ int mvbev_conv3x3_wino_bf16x3(const void* t, const mvbev_conv_desc* desc, const 
                               const uint32_t* group_mask, const int32_t* tile_order, void* stream) {
   return mvbev::b3::wino_launch(t, desc, w_packed, bias, init, Cout, relu, static_cast<float*>(y), y_layout,
                                 group_mask, tile_order, stream, 1, nullptr, nullptr, y_band_rows);
-}
-
-int mvbev_conv3x3_wino_bf16x3_sched(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,
-                                    const float* init, int64_t Cout, int relu, void* y, int y_layout,
-                                    const uint32_t* group_mask, const mvbev_conv_schedule* sched, void* stream) {
-  if (!sched) return MVBEV_ERR_NULL;
-  return mvbev::b3::wino_launch(t, desc, w_packed, bias, init, Cout, relu, static_cast<float*>(y), y_layout,
-                                group_mask, nullptr, stream, 1, nullptr, nullptr, 0, nullptr, 1, sched);
 }
 
 int mvbev_conv3x3_wino_bf16x3_dil(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,

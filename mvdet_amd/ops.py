@@ -766,16 +766,13 @@ def warp_views_wino_rows_into(srcs, m_norms, t: torch.Tensor, slots, Cs: int, K:
 def conv3x3_wino(t: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: Optional[torch.Tensor] = None,
                  init: Optional[torch.Tensor] = None, relu: bool = False, out: Optional[torch.Tensor] = None,
                  group_mask: Optional[torch.Tensor] = None,
-                 tile_order: Optional[torch.Tensor] = None, band_rows: int = 0, schedule=None) -> torch.Tensor:
+                 tile_order: Optional[torch.Tensor] = None, band_rows: int = 0) -> torch.Tensor:
     """The dilation-1 3x3 conv of ``conv3x3_desc`` from its row-Winograd transform ``t``
     (``wino_rows``) with ``PackedConv3x3(..., wino=True)`` weights: ``mvbev_conv3x3_wino_bf16x3``.
     ``out``: fp32 [B, cout, out_rows, W] or split-bf16 (``split_shape``); mask / order as the
     12 x 32 grid tiles of ``conv3x3_desc``.  ``band_rows`` > 0: ``out`` is fp32 in row bands,
     contiguous [bands, B, cout, band_rows, W] with bands * band_rows >= out_rows (computed row r at
-    band r // band_rows) — the partial-sum mode's reduce-scatter input, written in place.
-    ``schedule`` (``schedule.ConvSchedule`` over this launch's 12 x 32 tiles, e.g. ``plan_level``):
-    ``mvbev_conv3x3_wino_bf16x3_sched`` — its items replace ``tile_order``, split tiles are finished
-    by the ring fixup (no row bands)."""
+    band r // band_rows) — the partial-sum mode's reduce-scatter input, written in place."""
     _require_cuda(t, packed)
     B, W, out_rows = desc.B, desc.W, desc.out_rows
     lib = _native.load()
@@ -813,17 +810,6 @@ def conv3x3_wino(t: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: O
         top = tile_order.data_ptr()
     b = bias.detach().contiguous() if bias is not None else None
     bp = b.data_ptr() if b is not None else None
-    if schedule is not None:
-        if band_rows:
-            raise ValueError("a scheduled Winograd conv writes no row bands")
-        _require_cuda(schedule.items)
-        st = lib.mvbev_conv3x3_wino_bf16x3_sched(t.data_ptr(), ctypes.byref(desc), packed.data_ptr(), bp,
-                                                 init.data_ptr() if init is not None else None, cout,
-                                                 int(bool(relu)), out.data_ptr(),
-                                                 _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32, gmp,
-                                                 ctypes.byref(schedule.c), _stream(t))
-        _native.check(st, "mvbev_conv3x3_wino_bf16x3_sched")
-        return out
     st = lib.mvbev_conv3x3_wino_bf16x3(t.data_ptr(), ctypes.byref(desc), packed.data_ptr(), bp,
                                        init.data_ptr() if init is not None else None, cout, int(bool(relu)),
                                        out.data_ptr(), _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32,

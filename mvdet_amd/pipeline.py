@@ -118,8 +118,7 @@ class ProjectFuse:
                  all_views: bool = True, split_k: bool = True, frustum: bool = True, fuse_conv3: bool = True,
                  edge_strip: bool = True, wino_conv1: bool = True, wino_warp: bool = True,
                  wino_conv2: bool = True, nonfinite_guard: bool = True, cl_upsample: bool = True,
-                 parts: Optional[Sequence[Tuple[int, int]]] = None, part_channels: Optional[int] = None,
-                 level_conv1: bool = False):
+                 parts: Optional[Sequence[Tuple[int, int]]] = None, part_channels: Optional[int] = None):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":
@@ -223,9 +222,6 @@ class ProjectFuse:
         # (warp_up_wino_cl_kernel) when C % 32 == 0: copy + warp 0.36 ms vs the NCHW kernel's 0.376 at cfg2
         # (profiles/r04n_kbench.jsonl); maps that are channels-last already skip the copy
         self.cl_upsample = cl_upsample
-        # the row-Winograd conv1 through a leveling schedule (schedule.plan_level: first round whole, later
-        # blocks cut into K-pieces so the CUs end together; pieces finished by the ring fixup) — opt-in
-        self.level_conv1 = level_conv1
         self._pack1f: Optional[ops.PackedConv3x3] = None
         self._pack2f: Optional[ops.PackedConv3x3] = None
         self._chan_map = chan_map
@@ -492,32 +488,6 @@ class ProjectFuse:
             self._masks[key] = o
         return o
 
-    # plan_level's costs for the Winograd conv1, in 16-channel chunk-times (block stamps at cfg2,
-    # profiles/r05an_wino_stamps_cfg2.json: ~21 us per block + ~4.5 us per chunk)
-    LEVEL_BLOCK_OVERHEAD, LEVEL_PIECE_OVERHEAD, LEVEL_MIN_PIECE = 4.7, 2.0, 16
-
-    def conv1_level_schedule(self, device, row0: int, rows: int, B: int):
-        """The leveling schedule (``schedule.plan_level``) of the row-Winograd conv1 over rows
-        [row0, row0+rows) at batch B: its 12 x 32 pixel tiles' active chunks from the frustum mask, in
-        the heavy-first order; cached per geometry."""
-        key = ("level", str(device), row0, rows, B)
-        sc = self._masks.get(key)
-        if sc is None:
-            from . import schedule
-            m = self.conv1_mask(device, row0, rows)
-            W = self.grid_hw[1]
-            ty, tx = -(-rows // 12), -(-W // _native.TILE_W)
-            order = self.conv1_order(device, row0, rows, B, grid=True)
-            kc = 2 * ops.KC  # the conv's K-chunk: 16 channels (two 8-channel sub-blocks)
-            blocks = schedule.ring_blocks(B, ty, tx, self.mid // ops.BN, -(-self.S * self.Cs // kc),
-                                          group_mask=None if m is None else m.cpu().tolist(),
-                                          cpg=self.Cs // kc, order=None if order is None else order.cpu().tolist())
-            cus = torch.cuda.get_device_properties(torch.device(device)).multi_processor_count
-            sc = schedule.plan_level(blocks, cus, device, self.mid // ops.BN, self.LEVEL_MIN_PIECE,
-                                     self.LEVEL_BLOCK_OVERHEAD, self.LEVEL_PIECE_OVERHEAD)
-            self._masks[key] = sc
-        return sc
-
     def conv1_active_fraction(self, device, row0: int, rows: int, grid: bool = False) -> float:
         """Fraction of conv1's dense (pixel, slot) work the forward's frustum mask keeps (1.0 =
         dense): per tile its enabled slots x its pixels inside the grid.  ``grid``: over the
@@ -582,11 +552,9 @@ class ProjectFuse:
         ws.t1_valid = (a1, b1) == (0, self.grid_hw[0])
         if mark:
             mark("conv1_wino")  # between the transform and the conv (bench.py's stage events)
-        sched = self.conv1_level_schedule(ws.slab.device, a1, b1 - a1, B) if self.level_conv1 else None
         return ops.conv3x3_wino(ws.wino_t, d1, self.pack1w.get(conv1.weight), self.mid, init=init, relu=True,
                                 out=ws.y1, group_mask=gm,
-                                tile_order=self.conv1_order(ws.slab.device, a1, b1 - a1, B, grid=True),
-                                schedule=sched)
+                                tile_order=self.conv1_order(ws.slab.device, a1, b1 - a1, B, grid=True))
 
     def conv2(self, ws: Workspace, conv2: torch.nn.Conv2d) -> torch.Tensor:
         """a8: y2 = relu(conv3x3_d2(y1) + b2) on y2's rows (row-Winograd where ``wino_conv2_active``:

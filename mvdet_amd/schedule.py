@@ -31,10 +31,10 @@ BLOCK_OVERHEAD = 2.0   # chunk-times per block: pipeline fill from cold caches +
 PIECE_OVERHEAD = 2.0   # extra per piece: partial store + its share of the fixup pass
 
 
-def _xcd_makespan(works: Sequence[float], cus: int, bo: float = BLOCK_OVERHEAD) -> float:
+def _xcd_makespan(works: Sequence[float], cus: int) -> float:
     h = [0.0] * cus
     for w in works:
-        heapq.heappush(h, heapq.heappop(h) + w + bo)
+        heapq.heappush(h, heapq.heappop(h) + w + BLOCK_OVERHEAD)
     return max(h) if works else 0.0
 
 
@@ -128,115 +128,6 @@ def plan(blocks: Sequence[Tuple[int, int]], cus: int, device, split: bool = True
     for j in range(n):  # block 8 j + x runs queue x's j-th item
         for r in rows:
             items.append(list(r[j]) if j < len(r) else [-1, 0, 0, -1])
-    while items and items[-1][0] < 0:
-        items.pop()
-    return ConvSchedule(items, fixups, nslots, device, pred, pred_plain)
-
-
-def _level_xcd(queue: List[Tuple[int, int]], per: int, T: float, min_piece: int,
-               bo: float = BLOCK_OVERHEAD, po: float = PIECE_OVERHEAD):
-    """One XCD's dispatch sequence under the hardware's rule (its first ``per`` blocks one per
-    CU, then each next block to the CU that frees first), with every block after the first
-    round cut so the CU that takes it ends as close to ``T`` as a piece of >= ``min_piece``
-    chunks allows.  Returns (makespan, [(tile, c0, c1)])."""
-    seq: List[Tuple[int, int, int]] = []
-    heap: List[Tuple[float, int]] = []
-    k = 0
-    for i, (t, c) in enumerate(queue[:per]):
-        seq.append((t, 0, c))
-        heap.append((c + bo, i))
-        k += 1
-    for i in range(k, per):
-        heap.append((0.0, i))
-    heapq.heapify(heap)
-    cur = None  # (tile, next chunk, chunks) of a block cut earlier
-    rest = list(queue[k:])
-    ri = 0
-    while cur is not None or ri < len(rest):
-        tf, i = heapq.heappop(heap)
-        if cur is None:
-            t, c = rest[ri]
-            ri += 1
-            cur = (t, 0, c)
-        t, c0, n = cur
-        cut_before = c0 > 0
-        room = int(T - tf - bo - po)
-        left = n - c0
-        if left <= room + (0 if cut_before else po) or room < min_piece or left - room < min_piece:
-            seq.append((t, c0, n))
-            tf += left + bo + (po if cut_before else 0)
-            cur = None
-        else:
-            seq.append((t, c0, c0 + room))
-            tf += room + bo + po
-            cur = (t, c0 + room, n)
-        heapq.heappush(heap, (tf, i))
-    return max(f for f, _ in heap), seq
-
-
-def plan_level(blocks: Sequence[Tuple[int, int]], cus: int, device, n_cot: int, min_piece: int = 16,
-               bo: float = BLOCK_OVERHEAD, po: float = PIECE_OVERHEAD):
-    """A leveling schedule for the frustum-masked forward conv: ``blocks`` = (tile, active
-    chunks) in heavy-first order with the ``n_cot`` Cout blocks of a pixel tile adjacent.
-    Pixel tiles are dealt to the XCDs by least total work (a tile's Cout blocks stay on one XCD,
-    sharing its halo reads); on each XCD the first round is the heaviest blocks, whole (the
-    lock-step chunk walk of a round of equal view sets kept), and every later block is cut so
-    that the CU the hardware hands it to ends near a common level T (``_level_xcd``; T scanned,
-    the best simulated makespan kept).  Unlike ``plan``'s tail cut this reaches the imbalance
-    a heavy first-round block leaves: its CU takes a short piece of a light block, the CUs
-    with light first blocks take long ones.  Pieces leave partial sums that
-    ``conv_ring_fixup_kernel`` adds in K order (deterministic)."""
-    per = max(cus // XCDS, 1)
-    # blocks without active chunks stay: the forward still writes their epilogue (bias + coord
-    # term + ReLU of a tile no camera sees)
-    blocks = [(int(t), int(c)) for t, c in blocks]
-    groups: List[List[Tuple[int, int]]] = []
-    for t, c in blocks:
-        if groups and groups[-1][0][0] // n_cot == t // n_cot:
-            groups[-1].append((t, c))
-        else:
-            groups.append([(t, c)])
-    load = [0] * XCDS
-    queues: List[List[Tuple[int, int]]] = [[] for _ in range(XCDS)]
-    for g in groups:
-        x = min(range(XCDS), key=lambda j: (load[j], j))
-        queues[x] += g
-        load[x] += sum(c for _, c in g)
-    seqs, pred, pred_plain = [], 0.0, 0.0
-    for q in queues:
-        plain = _xcd_makespan([float(c) for _, c in q], per, bo)
-        pred_plain = max(pred_plain, plain)
-        lo = max([c for _, c in q[:per]] + [sum(c for _, c in q) / per]) + bo
-        best = (plain, [(t, 0, c) for t, c in q])
-        for j in range(0, 41):
-            T = lo + (plain - lo) * j / 40.0
-            mk, seq = _level_xcd(q, per, T, min_piece, bo, po)
-            if mk < best[0] - 1e-9:
-                best = (mk, seq)
-        pred = max(pred, best[0])
-        seqs.append(best[1])
-    # partial slots: the pieces of each cut tile, consecutive in chunk order
-    pieces = {}
-    for seq in seqs:
-        for t, c0, c1 in seq:
-            pieces.setdefault(t, []).append((c0, c1))
-    slot_of, fixups, nslots = {}, [], 0
-    for t in sorted(pieces):
-        ps = sorted(pieces[t])
-        if len(ps) > 1:
-            fixups.append([t, nslots, len(ps), 0])
-            for k, (c0, _) in enumerate(ps):
-                slot_of[(t, c0)] = nslots + k
-            nslots += len(ps)
-    n = max(len(sq) for sq in seqs)
-    items = []
-    for j in range(n):  # block 8 j + x runs XCD x's j-th item
-        for sq in seqs:
-            if j < len(sq):
-                t, c0, c1 = sq[j]
-                items.append([t, c0, c1, slot_of.get((t, c0), -1)])
-            else:
-                items.append([-1, 0, 0, -1])
     while items and items[-1][0] < 0:
         items.pop()
     return ConvSchedule(items, fixups, nslots, device, pred, pred_plain)

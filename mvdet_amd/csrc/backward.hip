@@ -1391,9 +1391,6 @@ __global__ __launch_bounds__(256) void warp_adjoint_split_kernel(const AdjArgs a
 // PIX pixels x 8 groups per workgroup: 32 for the warp plan (<= 4 entries per source pixel),
 // 16 where source pixels carry many entries (the S.U plan: 0.69 -> 0.58 ms at cfg2; 64: 0.85)
 constexpr int kAsGroups = 8;
-#ifndef MVBEV_ADJ_EMPTY
-#define MVBEV_ADJ_EMPTY 0  // 1: blocks of source pixels without entries write their zeros as 16-B stores (2: timing-only skip)
-#endif
 #ifndef MVBEV_ADJ_PPT
 #define MVBEV_ADJ_PPT 2  // source pixels per thread of the plain warp plan's gather (warp_adjoint_split8m_kernel; cfg2: 1 0.945 ms, 2 0.886, 4 1.19)
 #endif
@@ -1468,33 +1465,6 @@ __global__ __launch_bounds__(PIX * kAsGroups) void warp_adjoint_split8m_kernel(c
   const int c = (chunk * kAsGroups + threadIdx.x / PIX) * 8;
   if (c >= a.C) return;
   const AdjView& vw = a.v[view];
-#if MVBEV_ADJ_EMPTY
-  {  // a block of source pixels no BEV sample reaches (row pointers equal at both ends: rp is monotone)
-    const int pa = pb * PPT * PIX, pz = min(pa + PPT * PIX, a.P);
-    if (vw.rp[pa] == vw.rp[pz]) {
-#if MVBEV_ADJ_EMPTY == 2
-      return;  // timing bound only: writes nothing
-#else
-      if (a.accumulate) return;  // adds zero
-      const int lt = threadIdx.x & (PIX - 1);
-      float* gs = vw.gs + (int64_t)b * vw.sB + (int64_t)c * vw.sC;
-      const bool vec = (pz - pa) == PPT * PIX && (vw.sC & 3) == 0 && (vw.sB & 3) == 0 &&
-                       (reinterpret_cast<uintptr_t>(vw.gs) & 15) == 0;
-      if (vec) {  // this group's 8 channel rows of PPT * PIX pixels as 16-B stores
-        constexpr int Q = PPT * PIX / 4;  // float4 per row
-        for (int i = lt; i < 8 * Q; i += PIX) {
-          const int k = i / Q, q = i - k * Q;
-          if (c + k < a.C) *reinterpret_cast<float4*>(gs + (int64_t)k * vw.sC + pa + 4 * q) = float4{0.f, 0.f, 0.f, 0.f};
-        }
-      } else {
-        for (int k = 0; k < 8 && c + k < a.C; ++k)
-          for (int q = pa + lt; q < pz; q += PIX) gs[(int64_t)k * vw.sC + q] = 0.f;
-      }
-      return;
-#endif
-    }
-  }
-#endif
   const u32x4* g = reinterpret_cast<const u32x4*>(vw.go) + 2 * (int64_t)b * vw.gB + 2 * (int64_t)(c >> 3) * vw.gC;
   int p[PPT], e0[PPT], e1[PPT];
 #pragma unroll

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 12000: conv1's and conv2's weight gradients from the forward's row-Winograd transforms (mvbev_wino_dy_rows_f32, mvbev_conv3x3_wgrad_wino_bf16x3); 11900: row windows (mvbev_warp_views_split_bf16_rows with the non-finite report, mvbev_warp_views_exact_rows with fp16 sources), mvbev_conv3x3_f32_ex (row-band output), mvbev_bias_relu_nonfinite_f32, mvbev_zero_gated — the non-finite guard of the multi-GPU modes and the banded exact path; 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 12100: MVBEV_LAYOUT_SPLIT_BF16_PIX (conv data gradients' output, the warp adjoint's input); 12000: conv1's and conv2's weight gradients from the forward's row-Winograd transforms (mvbev_wino_dy_rows_f32, mvbev_conv3x3_wgrad_wino_bf16x3); 11900: row windows (mvbev_warp_views_split_bf16_rows with the non-finite report, mvbev_warp_views_exact_rows with fp16 sources), mvbev_conv3x3_f32_ex (row-band output), mvbev_bias_relu_nonfinite_f32, mvbev_zero_gated — the non-finite guard of the multi-GPU modes and the banded exact path; 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -233,6 +233,9 @@ int mvbev_bias_relu_nonfinite_f32(float* y, const float* init, int64_t B, int64_
 #define MVBEV_LAYOUT_SPLIT_BF16 2 /* per (8-channel group, pixel): bf16 hi[8], bf16 lo[8] */
 #define MVBEV_LAYOUT_SPLIT_ROWS 3 /* per (channel, row, 8-pixel run): bf16 hi[8], bf16 lo[8]
                                      (W % 8 == 0; the same bytes per row as fp32) */
+#define MVBEV_LAYOUT_SPLIT_BF16_PIX 4 /* pixel-major split-bf16: per (pixel, 8-channel group) bf16 hi[8], lo[8],
+                                         [B][rows][W][C/8] (ABI 12100): the conv data gradients' output for the
+                                         warp adjoint, whose gather then reads a pixel's channels in one piece */
 
 /* 3xbf16 split-precision variant of mvbev_conv3x3_f32 (mvbev_conv3x3_bf16x3_ex below; same
  * descriptor and semantics): a*b ~= a_hi*b_hi + a_hi*b_lo + a_lo*b_hi on the bf16 MFMA, fp32
@@ -542,7 +545,9 @@ typedef struct mvbev_warp_adjoint_view {
 /* grad_src (accumulate ? += : =) S^T grad_out for every view, one launch (nviews <= 16).
  * grad_out_layout MVBEV_LAYOUT_F32 (element strides) or MVBEV_LAYOUT_SPLIT_BF16 (grad_out =
  * the view's first 8-channel group of a split-bf16 blocked tensor, 16-B aligned, strides in
- * 32-byte units {batch, channel group, row = Wo, col = 1}; value = hi + lo). */
+ * 32-byte units {batch, channel group, row = Wo, col = 1}; value = hi + lo), or (ABI 12100)
+ * MVBEV_LAYOUT_SPLIT_BF16_PIX (the same pieces pixel-major: strides {batch, 1, Wo * G, G} with
+ * G >= C / 8 groups per pixel; C % 8 == 0) — same grad_src values as the split layout. */
 int mvbev_warp_views_adjoint(const mvbev_warp_adjoint_view* views, int nviews, int grad_out_layout, int64_t B,
                              int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int accumulate,
                              void* stream);

@@ -96,7 +96,7 @@ ERR_SHAPE = -2  # MVBEV_ERR_SHAPE
 ERR_DILATION = -6  # MVBEV_ERR_DILATION
 
 KC = 8    # MVBEV_CONV_KC
-LAYOUT_F32, LAYOUT_F16, LAYOUT_SPLIT_BF16, LAYOUT_SPLIT_ROWS = 0, 1, 2, 3  # MVBEV_LAYOUT_*
+LAYOUT_F32, LAYOUT_F16, LAYOUT_SPLIT_BF16, LAYOUT_SPLIT_ROWS, LAYOUT_SPLIT_PIX = 0, 1, 2, 3, 4  # MVBEV_LAYOUT_*
 BN = 128  # MVBEV_CONV_BN
 TILE_H, TILE_W = 8, 32  # MVBEV_CONV_TILE_H / _W (fp32/fp16 input; split input: conv_tile_rows())
 

@@ -36,6 +36,11 @@ from .pipeline import ProjectFuse, Workspace, band_rows
 _stage_hook = None
 
 
+
+# conv1's data gradient written pixel-major (MVBEV_LAYOUT_SPLIT_BF16_PIX) for the warp adjoint's gathers
+# (ABI 12100); False: the channel-group-major split layout
+DSLAB_PIXEL_MAJOR = True
+
 def set_stage_hook(fn) -> None:
     global _stage_hook
     _stage_hook = fn
@@ -370,8 +375,11 @@ class ProjectFuseFunction(torch.autograd.Function):
             _mark("bwd_conv1_dgrad")
             C = engine.C
             cp = st.dgrad1.cout_p
-            if C % ops.KC == 0:  # split-bf16 dslab: the adjoint gathers 8 channels per 32-B entry
-                dslab = torch.empty(ops.split_shape(B, cp, H, W), dtype=torch.bfloat16, device=dev)
+            pixm = DSLAB_PIXEL_MAJOR and dy1s is not None and C % ops.KC == 0
+            if C % ops.KC == 0:  # split-bf16 dslab: the adjoint gathers 8 channels per 32-B entry (pixel-major:
+                # an output pixel's 64 channels per 256-B gather)
+                dslab = torch.empty(ops.split_pix_shape(B, cp, H, W) if pixm else ops.split_shape(B, cp, H, W),
+                                    dtype=torch.bfloat16, device=dev)
                 if dy1s is not None and _dgrad1_wino_applies(engine, cp, dev):
                     _dgrad1_wino(engine, st, dy1s, w1, dslab)
                 else:
@@ -383,14 +391,15 @@ class ProjectFuseFunction(torch.autograd.Function):
                     ops.conv3x3_dgrad(dy1 if dy1s is None else dy1s, st.dgrad1, w1, 1, out=dslab, out_mask=cm,
                                       cot_per_group=C // ops.BN, sched=sched)
                 g8 = C // ops.KC
-                douts = [dslab[:, v * g8:(v + 1) * g8] for v in range(n)]
+                douts = [dslab[:, :, :, v * g8:(v + 1) * g8] if pixm else dslab[:, v * g8:(v + 1) * g8]
+                         for v in range(n)]
             else:
                 dslab = ops.conv3x3_dgrad(dy1, st.dgrad1, w1, 1)   # [B, round_up(nc,128), H, W]
                 douts = [dslab[:, v * C:(v + 1) * C] for v in range(n)]
             _mark("bwd_warp")
             gs = [torch.empty(ctx.feat_shape, dtype=torch.float32, device=dev) for _ in range(n)]
             plans = _adjoint_plans(engine, st, dev, backbone_hw=ctx.feat_shape[2:] if ctx.backbone else None)
-            ops.warp_views_adjoint(douts, plans, gs)
+            ops.warp_views_adjoint(douts, plans, gs, pixel_major=pixm)
             grads = [g if need[v] else None for v, g in enumerate(gs)]
         _mark("bwd_end")
         if ws.slab_zeroed:  # its readers are enqueued: reusable once this stream passes this point

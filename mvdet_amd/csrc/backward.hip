@@ -1246,6 +1246,7 @@ constexpr int kAdjU = 8;
 struct AdjView {
   const float* go;
   int64_t gB, gC;
+  int64_t gP;  // pixel stride of a split grad_out in 32-B units (1; the group count when pixel-major)
   float* gs;
   int64_t sB, sC;
   const int32_t* rp;
@@ -1524,6 +1525,80 @@ __global__ __launch_bounds__(PIX * kAsGroups) void warp_adjoint_split8m_kernel(c
         float* d = gs + (int64_t)k * vw.sC;
         *d = a.accumulate ? s[j][k] + *d : s[j][k];
       }
+  }
+}
+
+// Pixel-major split grad_out (MVBEV_LAYOUT_SPLIT_BF16_PIX: an output pixel's 8-channel groups side by
+// side): lanes = (pixel slot, 8-channel group), the group fastest, so one entry's 64 channels (8 lanes,
+// 256 B of one output pixel) are a single contiguous gather instead of eight 32-B pieces a plane apart.
+// Each (pixel, group) sums its entries in CSR order exactly as warp_adjoint_split8(m)_kernel does; the
+// block's [64 channels][NPIX pixels] result goes through LDS (pitch NPIX + 1: conflict-free both ways)
+// into coalesced row stores of the source planes.  NPIX = 64 for the plain plan (2 pixels per lane),
+// 32 for the upsampled (S.U) plan's longer lists.
+template <int NPIX>
+__global__ __launch_bounds__(256) void warp_adjoint_pix_kernel(const AdjArgs a) {
+  constexpr int kSlots = 32, kPpt = NPIX / kSlots, kPitch = NPIX + 1;
+  static_assert(NPIX % kSlots == 0, "pixels per block");
+  __shared__ float tr[64 * kPitch];
+  const int lb = xcd_remap(blockIdx.x, a.nwg);
+  const int pb = lb % a.pblocks;
+  int r = lb / a.pblocks;
+  const int chunk = r % a.chunks;
+  r /= a.chunks;
+  const int view = r % a.nviews;
+  const int b = r / a.nviews;
+  const AdjView& vw = a.v[view];
+  const int gq = threadIdx.x & 7, slot = threadIdx.x >> 3;
+  const int c = chunk * 64 + gq * 8;
+  const int p0 = pb * NPIX;
+  const u32x4* g = reinterpret_cast<const u32x4*>(vw.go) + 2 * ((int64_t)b * vw.gB + (int64_t)(c >> 3) * vw.gC);
+#pragma unroll
+  for (int j = 0; j < kPpt; ++j) {
+    const int pl = j * kSlots + slot, p = p0 + pl;
+    float s[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s[k] = 0.f;
+    if (p < a.P && c < a.C) {
+      const int e0 = vw.rp[p], e1 = vw.rp[p + 1];
+      for (int eb = e0; eb < e1; eb += 4) {  // batches of 4: the (col, val) loads, then 4 gathers in flight
+        int cb[4];
+        float wb[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool ok = eb + q < e1;
+          cb[q] = ok ? vw.col[eb + q] : 0;
+          wb[q] = ok ? vw.val[eb + q] : 0.f;
+        }
+        u32x4 hv[4], lv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (eb + q < e1) {
+            const int64_t o = 2 * (int64_t)cb[q] * vw.gP;
+            hv[q] = g[o];
+            lv[q] = g[o + 1];
+          }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (eb + q < e1) {
+            const bf16x8 hi = __builtin_bit_cast(bf16x8, hv[q]), lo = __builtin_bit_cast(bf16x8, lv[q]);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s[k] += wb[q] * ((float)hi[k] + (float)lo[k]);
+          }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) tr[(gq * 8 + k) * kPitch + pl] = s[k];
+  }
+  __syncthreads();
+  const int np = min(NPIX, a.P - p0), c0 = chunk * 64;
+  float* gs0 = vw.gs + (int64_t)b * vw.sB + (int64_t)c0 * vw.sC + p0;
+  for (int i = threadIdx.x; i < 64 * NPIX; i += 256) {
+    const int cr = i / NPIX, pl = i - cr * NPIX;
+    if (pl < np && c0 + cr < a.C) {
+      float* d = gs0 + (int64_t)cr * vw.sC + pl;
+      const float v = tr[cr * kPitch + pl];
+      *d = a.accumulate ? v + *d : v;
+    }
   }
 }
 
@@ -1920,18 +1995,24 @@ int mvbev_warp_views_adjoint(const mvbev_warp_adjoint_view* views, int nviews, i
   if (!views) return MVBEV_ERR_NULL;
   if (B <= 0 || C <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 || nviews <= 0) return MVBEV_ERR_RANK;
   if (nviews > kWarpMaxViews || H * W >= INT32_MAX || 4 * Ho * Wo >= INT32_MAX) return MVBEV_ERR_SHAPE;
-  if (grad_out_layout != MVBEV_LAYOUT_F32 && grad_out_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;
-  const bool split = grad_out_layout == MVBEV_LAYOUT_SPLIT_BF16;
+  if (grad_out_layout != MVBEV_LAYOUT_F32 && grad_out_layout != MVBEV_LAYOUT_SPLIT_BF16 &&
+      grad_out_layout != MVBEV_LAYOUT_SPLIT_BF16_PIX)
+    return MVBEV_ERR_SHAPE;
+  const bool pixm = grad_out_layout == MVBEV_LAYOUT_SPLIT_BF16_PIX;
+  const bool split = grad_out_layout == MVBEV_LAYOUT_SPLIT_BF16 || pixm;
+  if (pixm && C % 8 != 0) return MVBEV_ERR_SHAPE;
   bwd::AdjArgs a = {};
   for (int i = 0; i < nviews; ++i) {
     const mvbev_warp_adjoint_view& v = views[i];
     if (!v.grad_out || !v.grad_src || !v.row_ptr || !v.col || !v.val) return MVBEV_ERR_NULL;
-    // planes must be dense (the plan indexes pixels linearly)
-    if (v.grad_out_strides[3] != 1 || v.grad_out_strides[2] != Wo || v.grad_src_strides[3] != 1 ||
-        v.grad_src_strides[2] != W)
+    // planes must be dense (the plan indexes pixels linearly); pixel-major: groups adjacent, pixels dense
+    const int64_t gp = pixm ? v.grad_out_strides[3] : 1;
+    if ((pixm ? (v.grad_out_strides[1] != 1 || gp < C / 8 || v.grad_out_strides[2] != Wo * gp)
+              : (v.grad_out_strides[3] != 1 || v.grad_out_strides[2] != Wo)) ||
+        v.grad_src_strides[3] != 1 || v.grad_src_strides[2] != W)
       return MVBEV_ERR_STRIDE;
     if (split && (reinterpret_cast<uintptr_t>(v.grad_out) & 15) != 0) return MVBEV_ERR_ALIGN;
-    a.v[i] = bwd::AdjView{v.grad_out, v.grad_out_strides[0], v.grad_out_strides[1], v.grad_src,
+    a.v[i] = bwd::AdjView{v.grad_out, v.grad_out_strides[0], v.grad_out_strides[1], gp, v.grad_src,
                           v.grad_src_strides[0], v.grad_src_strides[1], v.row_ptr, v.col, v.val};
   }
   a.nviews = nviews;
@@ -1943,10 +2024,19 @@ int mvbev_warp_views_adjoint(const mvbev_warp_adjoint_view* views, int nviews, i
   a.pblocks = (int)ceil_div(H * W, g8 ? pix * (pix == 32 ? kPpt : 1) : 256);
   a.chunks = (int)ceil_div(C, g8 ? 8 * bwd::kAsGroups : bwd::kAdjCPB);
   a.accumulate = accumulate ? 1 : 0;
+  if (pixm) {  // 64 channels x 64 (plain plan) / 32 (S.U plan) source pixels per block
+    a.pblocks = (int)ceil_div(H * W, pix == 32 ? 64 : 32);
+    a.chunks = (int)ceil_div(C, 64);
+  }
   const int64_t nwg = (int64_t)a.pblocks * a.chunks * nviews * B;
   if (nwg > INT32_MAX) return MVBEV_ERR_SHAPE;
   a.nwg = (int)nwg;
-  if (g8)
+  if (pixm) {
+    if (pix == 32)
+      hipLaunchKernelGGL(bwd::warp_adjoint_pix_kernel<64>, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
+    else
+      hipLaunchKernelGGL(bwd::warp_adjoint_pix_kernel<32>, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
+  } else if (g8)
     if (pix == 16)
       hipLaunchKernelGGL(bwd::warp_adjoint_split8_kernel<16>, dim3((unsigned)nwg), dim3(16 * bwd::kAsGroups), 0,
                          as_stream(stream), a);

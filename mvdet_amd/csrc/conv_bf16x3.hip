@@ -122,6 +122,7 @@ struct Args {
   int npix;
   int mgroup;    // row-Winograd conv: consecutive ordered pixel tiles per XCD turn (MVBEV_MASK_GROUP's runtime form)
   bool y_split;  // y in the split-bf16 blocked layout (the next conv's 16-B staging copies)
+  bool y_pix;    // with y_split: pixel-major split-bf16 [B][out_rows][W][Cout / 8][hi, lo] (the warp adjoint's gathers)
   // output-side mask (optional, dgrad of the fused conv): per output tile, bit g clear =
   // output channel group g (cot_pg Cout tiles each) is never read, so its tiles are skipped
   const uint32_t* cmask;
@@ -229,7 +230,9 @@ __device__ inline void store_block(const Args& a, int b, int row, int col, int c
     if (valid) {
       const int64_t g = co0 / 8 + q;
       u32x4* out = reinterpret_cast<u32x4*>(a.y);
-      out[2 * ((((int64_t)b * (a.Cout / 8) + g) * a.out_rows + (row - a.out_row0)) * W + col) + kh] = piece;
+      const int64_t pix = ((int64_t)b * a.out_rows + (row - a.out_row0)) * W + col;
+      out[2 * (a.y_pix ? pix * (a.Cout / 8) + g
+                       : (((int64_t)b * (a.Cout / 8) + g) * a.out_rows + (row - a.out_row0)) * W + col) + kh] = piece;
     }
   }
 }
@@ -1197,8 +1200,11 @@ static int launch(const void* x, const mvbev_conv_desc* d, const void* w_packed,
   a.cot_pg = cot_pg;
   if (out_mask && (cot_pg <= 0 || a.n_cot > 32 * cot_pg || group_mask)) return MVBEV_ERR_SHAPE;
   if (out_mask) workspace = nullptr;  // skipped tiles never write split-K partial sums
-  if (y_layout != MVBEV_LAYOUT_F32 && y_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;
-  a.y_split = y_layout == MVBEV_LAYOUT_SPLIT_BF16;
+  if (y_layout != MVBEV_LAYOUT_F32 && y_layout != MVBEV_LAYOUT_SPLIT_BF16 &&
+      !(y_layout == MVBEV_LAYOUT_SPLIT_BF16_PIX && ring && !p3))
+    return MVBEV_ERR_SHAPE;
+  a.y_split = y_layout == MVBEV_LAYOUT_SPLIT_BF16 || y_layout == MVBEV_LAYOUT_SPLIT_BF16_PIX;
+  a.y_pix = y_layout == MVBEV_LAYOUT_SPLIT_BF16_PIX;
   a.npix = (int)(tiles / a.n_cot);
   const SkPlan plan = (group_mask || ring) ? SkPlan() : sk_plan(tiles, a.nchunks);
   const bool sk = workspace && plan.split > 1 &&
@@ -1785,7 +1791,9 @@ static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_pa
   if (Cout % BN != 0 || d->K % SB != 0 || d->group % SB != 0 || d->K % d->group != 0) return MVBEV_ERR_SHAPE;
   if (d->out_row0 < 0 || d->out_row0 + d->out_rows > d->H || d->H > INT32_MAX / 2 || d->W > INT32_MAX / 2)
     return MVBEV_ERR_SHAPE;
-  if (y_layout != MVBEV_LAYOUT_F32 && y_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;
+  if (y_layout != MVBEV_LAYOUT_F32 && y_layout != MVBEV_LAYOUT_SPLIT_BF16 &&
+      !(y_layout == MVBEV_LAYOUT_SPLIT_BF16_PIX && !p3))
+    return MVBEV_ERR_SHAPE;
   if (((reinterpret_cast<uintptr_t>(w_packed) | reinterpret_cast<uintptr_t>(t)) & 15) != 0) return MVBEV_ERR_ALIGN;
   Args a{};
   a.x = t; a.wp = static_cast<const u32x4*>(w_packed); a.bias = bias; a.init = init; a.y = y;
@@ -1812,7 +1820,8 @@ static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_pa
     a.cmask = out_mask;
     a.cot_pg = (int)cot_pg;
   }
-  a.y_split = y_layout == MVBEV_LAYOUT_SPLIT_BF16;
+  a.y_split = y_layout == MVBEV_LAYOUT_SPLIT_BF16 || y_layout == MVBEV_LAYOUT_SPLIT_BF16_PIX;
+  a.y_pix = y_layout == MVBEV_LAYOUT_SPLIT_BF16_PIX;
   if (band_rows < 0 || (band_rows > 0 && (a.y_split || p3 || band_rows > d->out_rows))) return MVBEV_ERR_SHAPE;
   a.band_rows = (int)band_rows;
   a.npix = (int)(tiles / a.n_cot);

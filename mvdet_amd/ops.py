@@ -74,6 +74,26 @@ def split_shape(B: int, C: int, H: int, W: int) -> Tuple[int, ...]:
     return (B, (C + KC - 1) // KC, H, W, 2, KC)
 
 
+def split_pix_shape(B: int, C: int, H: int, W: int) -> Tuple[int, ...]:
+    """Shape of a [B, C, H, W] tensor in the pixel-major split-bf16 layout (MVBEV_LAYOUT_SPLIT_BF16_PIX:
+    per pixel its 8-channel groups side by side, each 16 B hi then 16 B lo)."""
+    return (B, H, W, (C + KC - 1) // KC, 2, KC)
+
+
+def _out_layout(out: torch.Tensor, B: int, C: int, H: int, W: int) -> int:
+    """The MVBEV_LAYOUT_* of a conv output tensor: fp32 [B, C, H, W], split-bf16 or pixel-major split-bf16."""
+    if out.dtype == torch.float32 and tuple(out.shape) == (B, C, H, W) and out.is_contiguous():
+        return _native.LAYOUT_F32
+    if out.dtype == torch.bfloat16 and out.is_contiguous():
+        if tuple(out.shape) == split_shape(B, C, H, W):
+            return _native.LAYOUT_SPLIT_BF16
+        if tuple(out.shape) == split_pix_shape(B, C, H, W):
+            return _native.LAYOUT_SPLIT_PIX
+    raise ValueError(f"out must be a contiguous fp32 {(B, C, H, W)}, bf16 {split_shape(B, C, H, W)} (split) or "
+                     f"bf16 {split_pix_shape(B, C, H, W)} (pixel-major split) tensor, got "
+                     f"{out.dtype} {tuple(out.shape)}")
+
+
 def split_decode(t: torch.Tensor, C: Optional[int] = None) -> torch.Tensor:
     """Split-bf16 blocked [B, G, H, W, 2, 8] -> fp32 [B, C, H, W] (hi + lo)."""
     B, G, H, W, _, _ = t.shape
@@ -925,7 +945,7 @@ def conv3x3_wino_dgrad(t: torch.Tensor, desc, packed: torch.Tensor, cout: int, o
     """A dilation-1 data gradient from the row-Winograd transform ``t`` of the split-bf16 dy
     (``wino_rows``) and ``PackedConv3x3(..., wino=True)`` weights of the forward weight with its in /
     out channels swapped and taps reversed: ``mvbev_conv3x3_wino_bf16x3_dgrad``.  ``out``: fp32
-    [B, cout, out_rows, W] or split-bf16; ``out_mask`` as ``conv3x3_dgrad``'s (12 x 32 tiles,
+    [B, cout, out_rows, W], split-bf16 or pixel-major split-bf16 (``split_pix_shape``); ``out_mask`` as ``conv3x3_dgrad``'s (12 x 32 tiles,
     ``cot_per_group`` 128-channel Cout tiles per bit): cleared tiles are not written."""
     _require_cuda(t, packed, out)
     B, W, out_rows = desc.B, desc.W, desc.out_rows
@@ -934,10 +954,7 @@ def conv3x3_wino_dgrad(t: torch.Tensor, desc, packed: torch.Tensor, cout: int, o
         raise ValueError("packed weights are smaller than the Winograd conv needs")
     if t.numel() * t.element_size() < wino_rows_bytes(desc):
         raise ValueError("t is smaller than the descriptor's row-Winograd transform")
-    y_split = out.dtype == torch.bfloat16
-    want = split_shape(B, cout, out_rows, W) if y_split else (B, cout, out_rows, W)
-    if tuple(out.shape) != want or not out.is_contiguous() or out.dtype not in (torch.float32, torch.bfloat16):
-        raise ValueError(f"out must be a contiguous {'bf16' if y_split else 'fp32'} {want} tensor")
+    layout = _out_layout(out, B, cout, out_rows, W)
     mp = None
     if out_mask is not None:
         _require_cuda(out_mask)
@@ -946,8 +963,7 @@ def conv3x3_wino_dgrad(t: torch.Tensor, desc, packed: torch.Tensor, cout: int, o
             raise ValueError(f"out_mask must be a contiguous int32 tensor of >= {tiles} tiles")
         mp = out_mask.data_ptr()
     st = lib.mvbev_conv3x3_wino_bf16x3_dgrad(t.data_ptr(), ctypes.byref(desc), packed.data_ptr(), cout, out.data_ptr(),
-                                             _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32, mp,
-                                             int(cot_per_group), _stream(t))
+                                             layout, mp, int(cot_per_group), _stream(t))
     _native.check(st, "mvbev_conv3x3_wino_bf16x3_dgrad")
     return out
 
@@ -1062,11 +1078,13 @@ class WarpAdjointPlan:
         return int(self.row_ptr[-1].item())
 
 
-def warp_views_adjoint(grad_outs, plans, grad_srcs, accumulate: bool = False) -> None:
+def warp_views_adjoint(grad_outs, plans, grad_srcs, accumulate: bool = False, pixel_major: bool = False) -> None:
     """Deterministic gather form of ``warp_views_backward``: ``grad_srcs[i]`` [B,C,H,W] =
     (or += with ``accumulate``) the adjoint of view i's warp applied to ``grad_outs[i]``;
     ``plans[i]`` its ``WarpAdjointPlan``.  ``grad_outs[i]``: fp32 [B,C,Ho,Wo] with dense rows,
-    or a bf16 split-bf16 blocked [B, C/8, Ho, Wo, 2, 8] view (``split_shape``; C % 8 == 0)."""
+    or a bf16 split-bf16 blocked [B, C/8, Ho, Wo, 2, 8] view (``split_shape``; C % 8 == 0), or with
+    ``pixel_major`` a [B, Ho, Wo, C/8, 2, 8] view of a pixel-major split tensor (``split_pix_shape``, the
+    view's groups a slice of the pixel's: MVBEV_LAYOUT_SPLIT_BF16_PIX) — the same grad_srcs."""
     n = len(grad_outs)
     if n == 0:
         return
@@ -1075,11 +1093,19 @@ def warp_views_adjoint(grad_outs, plans, grad_srcs, accumulate: bool = False) ->
     _require_cuda(*grad_outs, *grad_srcs)
     split = grad_outs[0].dtype == torch.bfloat16
     B, C, H, W = grad_srcs[0].shape
+    # pixel-major split: [B, Ho, Wo, C/8, 2, 8] slices (of a [B, Ho, Wo, G, 2, 8] tensor)
+    pixm = bool(pixel_major)
+    if pixm and not split:
+        raise ValueError("pixel_major needs bf16 split grad_outs")
     if split:
         if C % KC:
             raise ValueError("a split grad_out needs C % 8 == 0")
-        Ho, Wo = grad_outs[0].shape[2], grad_outs[0].shape[3]
-        want = split_shape(B, C, Ho, Wo)
+        if pixm:
+            Ho, Wo = grad_outs[0].shape[1], grad_outs[0].shape[2]
+            want = split_pix_shape(B, C, Ho, Wo)
+        else:
+            Ho, Wo = grad_outs[0].shape[2], grad_outs[0].shape[3]
+            want = split_shape(B, C, Ho, Wo)
     else:
         Ho, Wo = grad_outs[0].shape[2], grad_outs[0].shape[3]
         want = (B, C, Ho, Wo)
@@ -1092,7 +1118,11 @@ def warp_views_adjoint(grad_outs, plans, grad_srcs, accumulate: bool = False) ->
             raise ValueError("plan built for other sizes")
         if d.dtype != torch.float32 or g.dtype != (torch.bfloat16 if split else torch.float32):
             raise TypeError("grad_src is fp32; grad_out fp32 or split-bf16 (bf16 storage)")
-        if split:
+        if pixm:
+            if g.stride(5) != 1 or g.stride(4) != KC or g.stride(3) != 2 * KC or g.stride(1) != g.stride(2) * Wo:
+                raise ValueError("pixel-major split grad_out needs adjacent groups and dense pixels")
+            gstr = (g.stride(0) // 16, 1, g.stride(1) // 16, g.stride(2) // 16)  # 32-byte units
+        elif split:
             if g.stride(5) != 1 or g.stride(4) != KC or g.stride(3) != 2 * KC or g.stride(2) != 2 * KC * Wo:
                 raise ValueError("split grad_out needs dense pixels")
             gstr = (g.stride(0) // 16, g.stride(1) // 16, Wo, 1)  # 32-byte units
@@ -1105,7 +1135,7 @@ def warp_views_adjoint(grad_outs, plans, grad_srcs, accumulate: bool = False) ->
         arr[i] = _native.WarpAdjointView(g.data_ptr(), (ctypes.c_int64 * 4)(*gstr), d.data_ptr(),
                                          (ctypes.c_int64 * 4)(*d.stride()), pl.row_ptr.data_ptr(),
                                          pl.col.data_ptr(), pl.val.data_ptr())
-    layout = _native.LAYOUT_SPLIT_BF16 if split else _native.LAYOUT_F32
+    layout = _native.LAYOUT_SPLIT_PIX if pixm else _native.LAYOUT_SPLIT_BF16 if split else _native.LAYOUT_F32
     st = _native.load().mvbev_warp_views_adjoint(arr, n, layout, B, C, H, W, Ho, Wo, int(bool(accumulate)),
                                                  _stream(grad_srcs[0]))
     _native.check(st, "mvbev_warp_views_adjoint")
@@ -1191,10 +1221,9 @@ def conv3x3_dgrad(dy: torch.Tensor, packed: PackedDgrad3x3, weight: torch.Tensor
     cp = packed.cout_p
     if out is None:
         out = torch.empty((B, cp, H, W), dtype=torch.float32, device=dy.device)
-    split = out.dtype == torch.bfloat16
-    want = split_shape(B, cp, H, W) if split else (B, cp, H, W)
-    if tuple(out.shape) != want or not out.is_contiguous() or out.dtype not in (torch.float32, torch.bfloat16):
-        raise ValueError(f"out must be a contiguous {'bf16' if split else 'fp32'} {want} tensor")
+    layout = _out_layout(out, B, cp, H, W)
+    if layout == _native.LAYOUT_SPLIT_PIX and not dy_split:
+        raise ValueError("a pixel-major split out needs the ring kernel (a split-bf16 dy)")
     mp = None
     if out_mask is not None:
         _require_cuda(out_mask)
@@ -1208,14 +1237,12 @@ def conv3x3_dgrad(dy: torch.Tensor, packed: PackedDgrad3x3, weight: torch.Tensor
             raise ValueError("a ring-kernel schedule needs a split-bf16 dy")
         st = _native.load().mvbev_conv3x3_dgrad_bf16x3_sched(
             dy.data_ptr(), _native.LAYOUT_SPLIT_BF16, ctypes.byref(d), packed.get(weight).data_ptr(), cp,
-            int(dilation), out.data_ptr(), _native.LAYOUT_SPLIT_BF16 if split else _native.LAYOUT_F32, mp,
-            int(cot_per_group), ctypes.byref(sched.c), _stream(dy))
+            int(dilation), out.data_ptr(), layout, mp, int(cot_per_group), ctypes.byref(sched.c), _stream(dy))
         _native.check(st, "mvbev_conv3x3_dgrad_bf16x3_sched")
         return out
     st = _native.load().mvbev_conv3x3_dgrad_bf16x3_ex(
         dy.data_ptr(), _native.LAYOUT_SPLIT_BF16 if dy_split else _native.LAYOUT_F32, ctypes.byref(d),
-        packed.get(weight).data_ptr(), cp, int(dilation), out.data_ptr(),
-        _native.LAYOUT_SPLIT_BF16 if split else _native.LAYOUT_F32, mp, int(cot_per_group), _stream(dy))
+        packed.get(weight).data_ptr(), cp, int(dilation), out.data_ptr(), layout, mp, int(cot_per_group), _stream(dy))
     _native.check(st, "mvbev_conv3x3_dgrad_bf16x3_ex")
     return out
 

@@ -64,6 +64,18 @@ def test_warp_backward_vs_grid_sample_autograd(B, C, H, W, ho, wo):
         assert (bufs[i][:, 0] == 0.5).all() and (bufs[i][:, C + 1] == 0.5).all()
 
 
+def _pix_views(splits, extra_groups=3):
+    """The views' split-bf16 [B, C/8, Ho, Wo, 2, 8] gradients as group slices of ONE pixel-major tensor
+    [B, Ho, Wo, G, 2, 8] (MVBEV_LAYOUT_SPLIT_BF16_PIX, as conv1's dgrad writes dslab), with
+    ``extra_groups`` foreign groups after them (the per-pixel stride exceeds a view's C/8)."""
+    B, g8, Ho, Wo = splits[0].shape[:4]
+    parts = [sp.permute(0, 2, 3, 1, 4, 5) for sp in splits]
+    parts.append(torch.full((B, Ho, Wo, extra_groups, 2, 8), float("nan"), dtype=splits[0].dtype,
+                            device=splits[0].device))
+    full = torch.cat(parts, dim=3).contiguous()
+    return [full[:, :, :, v * g8:(v + 1) * g8] for v in range(len(splits))]
+
+
 @pytest.mark.parametrize("B,C,h,w,H,W,ho,wo", [(1, 8, 9, 16, 27, 48, 12, 36), (2, 16, 10, 14, 27, 48, 17, 23),
                                                (1, 24, 30, 53, 90, 160, 120, 360), (1, 72, 7, 20, 20, 57, 15, 40),
                                                (1, 16, 5, 9, 30, 54, 11, 13)])
@@ -110,6 +122,14 @@ def test_upsampled_warp_adjoint_vs_autograd(B, C, h, w, H, W, ho, wo):
     ops.warp_views_adjoint([_split_encode(g) for g in gdev], plans, acc, accumulate=True)
     for i in range(n):
         assert_parity(acc[i].cpu() - 0.25, refs[i], f"upsampled adjoint, accumulating, view {i}")
+    # the pixel-major split grad_out (ABI 12100): the same sums in the same order -> bitwise the split result
+    pv = _pix_views([_split_encode(g) for g in gdev])
+    outs_p = [torch.full((B, C, h, w), float("nan"), device=DEV) for _ in range(n)]
+    ops.warp_views_adjoint(pv, plans, outs_p, pixel_major=True)
+    assert all(torch.equal(a, b) for a, b in zip(outs_p, outs_s))
+    acc_p = [torch.full((B, C, h, w), 0.25, device=DEV) for _ in range(n)]
+    ops.warp_views_adjoint(pv, plans, acc_p, accumulate=True, pixel_major=True)
+    assert all(torch.equal(a, b) for a, b in zip(acc_p, acc))
     dst = [torch.empty((B, C, ho, wo), device=DEV) for _ in range(n)]
     ops.warp_views_upsampled_into([f.to(DEV) for f in feats], (H, W), mn, dst)
     for i in range(n):
@@ -164,6 +184,14 @@ def test_warp_adjoint_gather_vs_grid_sample_autograd(B, C, H, W, ho, wo):
         ops.warp_views_adjoint(split, plans, acc_s, accumulate=True)
         for a, o in zip(acc_s, outs_s):
             assert torch.allclose(a, 2 * o, rtol=1e-6, atol=0)
+        # pixel-major split grad_out (ABI 12100): bitwise the split-layout result, overwriting and accumulating
+        pv = _pix_views(split)
+        outs_p = [torch.full_like(o, float("nan")) for o in outs]
+        ops.warp_views_adjoint(pv, plans, outs_p, pixel_major=True)
+        assert all(torch.equal(a, b) for a, b in zip(outs_p, outs_s))
+        acc_p = [o.clone() for o in outs_p]
+        ops.warp_views_adjoint(pv, plans, acc_p, accumulate=True, pixel_major=True)
+        assert all(torch.equal(a, b) for a, b in zip(acc_p, acc_s))
 
 
 def test_warp_backward_no_gradient_from_outside_samples():
@@ -330,6 +358,11 @@ def test_dgrad_ring_schedule(pieces):
     got = ops.conv3x3_dgrad(dys, pk, w.to(DEV), 1, out=torch.full(ops.split_shape(B, Cw, H, W), 7.0,
                                                                       dtype=torch.bfloat16, device=DEV),
                             out_mask=mask.to(DEV), cot_per_group=1, sched=sch)
+    # the pixel-major split output of the same schedule: the same pieces
+    gotp = ops.conv3x3_dgrad(dys, pk, w.to(DEV), 1, out=torch.full(ops.split_pix_shape(B, Cw, H, W), 7.0,
+                                                                       dtype=torch.bfloat16, device=DEV),
+                             out_mask=mask.to(DEV), cot_per_group=1, sched=sch)
+    assert torch.equal(gotp.permute(0, 3, 1, 2, 4, 5), got)
     r, o = ops.split_decode(ref).cpu(), ops.split_decode(got).cpu()
     assert torch.equal(o == 14.0, r == 14.0) and (r == 14.0).any()  # prefill hi 7 + lo 7 kept where masked
     if sch.nfix:  # pieces: another fp32 summation order
@@ -429,6 +462,10 @@ def test_conv1_dgrad_as_masked_winograd_conv(B, Cw, K, H, W):
     assert keep.any() and (~keep).any()
     assert_parity(got[keep].reshape(-1, 1), ref[keep].reshape(-1, 1), "masked Winograd dgrad (kept tiles)")
     assert (got[~keep] == 14.0).all()  # hi 7 + lo 7: untouched
+    # the pixel-major split output (MVBEV_LAYOUT_SPLIT_BF16_PIX, the warp adjoint's input): the same pieces
+    outp = torch.full(ops.split_pix_shape(B, K, H, W), 7.0, dtype=torch.bfloat16, device=DEV)
+    ops.conv3x3_wino_dgrad(t, d, packed, K, outp, out_mask=mask.to(DEV), cot_per_group=1)
+    assert torch.equal(outp.permute(0, 3, 1, 2, 4, 5), out)
     # dense (no mask) equals the masked result on the kept tiles bit for bit
     dense = torch.empty((B, K, H, W), dtype=torch.float32, device=DEV)
     ops.conv3x3_wino_dgrad(t, d, packed, K, dense)

@@ -214,7 +214,7 @@ def main():
             "conv23w": (lambda: (weng.conv2_partials(wws, mc[2], mc[4]), weng.conv3_from_partials(wws, mc[4])),
                         2.0 * B * ho * wo * 9 * 512 * 512),
         }
-        if {"adjup", "adj"} & set(args.only.split(",")):
+        if {"adjup", "adj", "adjpix", "adjuppix"} & set(args.only.split(",")):
             # the warp adjoints of the training step (autograd.py) on a random split grad_out
             from mvdet_amd import ops
             hb = tuple(bfeats[0].shape[2:])
@@ -225,6 +225,14 @@ def main():
             stages["adjup"] = ((lambda: ops.warp_views_adjoint(douts, plu, gs)), None)
             pl = [ops.WarpAdjointPlan(eng.m_norm_cpu[v], up, (ho, wo), dev) for v in range(N)]
             stages["adj"] = ((lambda: ops.warp_views_adjoint(douts, pl, gsu)), None)
+            # the same gradients in the pixel-major split layout (one [B, ho, wo, N * C / 8, 2, 8] tensor,
+            # the views' group slices), as the training step's conv1 dgrad writes them (ABI 12100)
+            g8 = C // ops.KC
+            dpix = torch.stack([d.permute(0, 2, 3, 1, 4, 5) for d in douts], dim=3).reshape(
+                B, ho, wo, N * g8, 2, ops.KC).contiguous()
+            dpv = [dpix[:, :, :, v * g8:(v + 1) * g8] for v in range(N)]
+            stages["adjpix"] = ((lambda: ops.warp_views_adjoint(dpv, pl, gsu, pixel_major=True)), None)
+            stages["adjuppix"] = ((lambda: ops.warp_views_adjoint(dpv, plu, gs, pixel_major=True)), None)
         if {"wgrad1", "wgrad1w", "wgrad2w", "wgrad1f", "dgrad1", "dgrad1s", "wgrad2", "wgrad2f", "dgrad2"} & set(args.only.split(",")):
             stages.update(backward_stages(eng, ws, mc, B, ho, wo, N, C, dev))
         from mvdet_amd import _native

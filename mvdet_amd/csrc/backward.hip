@@ -1535,6 +1535,12 @@ __global__ __launch_bounds__(PIX * kAsGroups) void warp_adjoint_split8m_kernel(c
 // block's [64 channels][NPIX pixels] result goes through LDS (pitch NPIX + 1: conflict-free both ways)
 // into coalesced row stores of the source planes.  NPIX = 64 for the plain plan (2 pixels per lane),
 // 32 for the upsampled (S.U) plan's longer lists.
+#ifndef MVBEV_ADJ_PIX_EMPTY
+#define MVBEV_ADJ_PIX_EMPTY 0  // blocks without entries store their zeros directly (no LDS pass)
+#endif
+#ifndef MVBEV_ADJ_PIX_NPIX
+#define MVBEV_ADJ_PIX_NPIX 64  // source pixels per block of the plain plan's pixel-major gather
+#endif
 template <int NPIX>
 __global__ __launch_bounds__(256) void warp_adjoint_pix_kernel(const AdjArgs a) {
   constexpr int kSlots = 32, kPpt = NPIX / kSlots, kPitch = NPIX + 1;
@@ -1552,6 +1558,18 @@ __global__ __launch_bounds__(256) void warp_adjoint_pix_kernel(const AdjArgs a) 
   const int c = chunk * 64 + gq * 8;
   const int p0 = pb * NPIX;
   const u32x4* g = reinterpret_cast<const u32x4*>(vw.go) + 2 * ((int64_t)b * vw.gB + (int64_t)(c >> 3) * vw.gC);
+  const int np = min(NPIX, a.P - p0), c0 = chunk * 64;
+  float* gs0 = vw.gs + (int64_t)b * vw.sB + (int64_t)c0 * vw.sC + p0;
+#if MVBEV_ADJ_PIX_EMPTY
+  if (vw.rp[p0] == vw.rp[p0 + np]) {  // no entries in the block (rp is monotone): zeros, no LDS pass
+    if (a.accumulate) return;
+    for (int i = threadIdx.x; i < 64 * NPIX; i += 256) {
+      const int cr = i / NPIX, pl = i - cr * NPIX;
+      if (pl < np && c0 + cr < a.C) gs0[(int64_t)cr * vw.sC + pl] = 0.f;
+    }
+    return;
+  }
+#endif
 #pragma unroll
   for (int j = 0; j < kPpt; ++j) {
     const int pl = j * kSlots + slot, p = p0 + pl;
@@ -1590,8 +1608,6 @@ __global__ __launch_bounds__(256) void warp_adjoint_pix_kernel(const AdjArgs a) 
     for (int k = 0; k < 8; ++k) tr[(gq * 8 + k) * kPitch + pl] = s[k];
   }
   __syncthreads();
-  const int np = min(NPIX, a.P - p0), c0 = chunk * 64;
-  float* gs0 = vw.gs + (int64_t)b * vw.sB + (int64_t)c0 * vw.sC + p0;
   for (int i = threadIdx.x; i < 64 * NPIX; i += 256) {
     const int cr = i / NPIX, pl = i - cr * NPIX;
     if (pl < np && c0 + cr < a.C) {
@@ -2025,7 +2041,7 @@ int mvbev_warp_views_adjoint(const mvbev_warp_adjoint_view* views, int nviews, i
   a.chunks = (int)ceil_div(C, g8 ? 8 * bwd::kAsGroups : bwd::kAdjCPB);
   a.accumulate = accumulate ? 1 : 0;
   if (pixm) {  // 64 channels x 64 (plain plan) / 32 (S.U plan) source pixels per block
-    a.pblocks = (int)ceil_div(H * W, pix == 32 ? 64 : 32);
+    a.pblocks = (int)ceil_div(H * W, pix == 32 ? MVBEV_ADJ_PIX_NPIX : 32);
     a.chunks = (int)ceil_div(C, 64);
   }
   const int64_t nwg = (int64_t)a.pblocks * a.chunks * nviews * B;
@@ -2033,7 +2049,8 @@ int mvbev_warp_views_adjoint(const mvbev_warp_adjoint_view* views, int nviews, i
   a.nwg = (int)nwg;
   if (pixm) {
     if (pix == 32)
-      hipLaunchKernelGGL(bwd::warp_adjoint_pix_kernel<64>, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
+      hipLaunchKernelGGL(bwd::warp_adjoint_pix_kernel<MVBEV_ADJ_PIX_NPIX>, dim3((unsigned)nwg), dim3(256), 0,
+                         as_stream(stream), a);
     else
       hipLaunchKernelGGL(bwd::warp_adjoint_pix_kernel<32>, dim3((unsigned)nwg), dim3(256), 0, as_stream(stream), a);
   } else if (g8)

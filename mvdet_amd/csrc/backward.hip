@@ -1539,7 +1539,7 @@ __global__ __launch_bounds__(PIX * kAsGroups) void warp_adjoint_split8m_kernel(c
 #define MVBEV_ADJ_PIX_EMPTY 1  // blocks without entries store their zeros directly, no LDS pass (cfg2 plain plan: 0.695 -> 0.682 ms)
 #endif
 #ifndef MVBEV_ADJ_PIX_NPIX
-#define MVBEV_ADJ_PIX_NPIX 64  // source pixels per block of the plain plan's pixel-major gather (128: 0.79 ms)
+#define MVBEV_ADJ_PIX_NPIX 64  // source pixels per block of the plain plan's pixel-major gather (32: 0.75 ms, 128: 0.79 vs 0.65-0.68)
 #endif
 template <int NPIX>
 __global__ __launch_bounds__(256) void warp_adjoint_pix_kernel(const AdjArgs a) {

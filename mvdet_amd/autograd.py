@@ -300,6 +300,10 @@ class ProjectFuseFunction(torch.autograd.Function):
         ctx.engine = engine
         ctx.ws = ws
         ctx.feat_shape = tuple(feats[0].shape)
+        # channels-last maps (the detector's backbone): their gradients are written channels-last too, so
+        # autograd's grad-layout contract needs no copy
+        ctx.feat_cl = (feats[0].dim() == 4 and not feats[0].is_contiguous()
+                       and feats[0].is_contiguous(memory_format=torch.channels_last))
         ctx.save_for_backward(w1, b1, w2, b2, w3)
         return out
 
@@ -397,7 +401,8 @@ class ProjectFuseFunction(torch.autograd.Function):
                 dslab = ops.conv3x3_dgrad(dy1, st.dgrad1, w1, 1)   # [B, round_up(nc,128), H, W]
                 douts = [dslab[:, v * C:(v + 1) * C] for v in range(n)]
             _mark("bwd_warp")
-            gs = [torch.empty(ctx.feat_shape, dtype=torch.float32, device=dev) for _ in range(n)]
+            mf = torch.channels_last if (pixm and ctx.feat_cl) else torch.contiguous_format
+            gs = [torch.empty(ctx.feat_shape, dtype=torch.float32, device=dev, memory_format=mf) for _ in range(n)]
             plans = _adjoint_plans(engine, st, dev, backbone_hw=ctx.feat_shape[2:] if ctx.backbone else None)
             ops.warp_views_adjoint(douts, plans, gs, pixel_major=pixm)
             grads = [g if need[v] else None for v, g in enumerate(gs)]

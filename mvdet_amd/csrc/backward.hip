@@ -1256,6 +1256,7 @@ struct AdjView {
 struct AdjArgs {
   AdjView v[kWarpMaxViews];
   int nviews, B, C, P, pblocks, chunks, nwg, accumulate;
+  int src_cl;  // warp_adjoint_pix_kernel: grad_src channels-last (sC = 1, pixel stride C), else dense planes
 };
 
 __global__ __launch_bounds__(256) void warp_adjoint_kernel(const AdjArgs a) {
@@ -1559,13 +1560,16 @@ __global__ __launch_bounds__(256) void warp_adjoint_pix_kernel(const AdjArgs a) 
   const int p0 = pb * NPIX;
   const u32x4* g = reinterpret_cast<const u32x4*>(vw.go) + 2 * ((int64_t)b * vw.gB + (int64_t)(c >> 3) * vw.gC);
   const int np = min(NPIX, a.P - p0), c0 = chunk * 64;
-  float* gs0 = vw.gs + (int64_t)b * vw.sB + (int64_t)c0 * vw.sC + p0;
+  // the source gradient's (channel, pixel) element: planes (pixels contiguous) or channels-last
+  const int64_t ps = a.src_cl ? (int64_t)a.C : 1;
+  float* gs0 = vw.gs + (int64_t)b * vw.sB + (int64_t)c0 * vw.sC + (int64_t)p0 * ps;
 #if MVBEV_ADJ_PIX_EMPTY
   if (vw.rp[p0] == vw.rp[p0 + np]) {  // no entries in the block (rp is monotone): zeros, no LDS pass
     if (a.accumulate) return;
     for (int i = threadIdx.x; i < 64 * NPIX; i += 256) {
-      const int cr = i / NPIX, pl = i - cr * NPIX;
-      if (pl < np && c0 + cr < a.C) gs0[(int64_t)cr * vw.sC + pl] = 0.f;
+      // the fastest index along the contiguous dimension: pixels for planes, channels for channels-last
+      const int cr = a.src_cl ? i % 64 : i / NPIX, pl = a.src_cl ? i / 64 : i % NPIX;
+      if (pl < np && c0 + cr < a.C) gs0[(int64_t)cr * vw.sC + (int64_t)pl * ps] = 0.f;
     }
     return;
   }
@@ -1609,9 +1613,9 @@ __global__ __launch_bounds__(256) void warp_adjoint_pix_kernel(const AdjArgs a) 
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 64 * NPIX; i += 256) {
-    const int cr = i / NPIX, pl = i - cr * NPIX;
+    const int cr = a.src_cl ? i % 64 : i / NPIX, pl = a.src_cl ? i / 64 : i % NPIX;
     if (pl < np && c0 + cr < a.C) {
-      float* d = gs0 + (int64_t)cr * vw.sC + pl;
+      float* d = gs0 + (int64_t)cr * vw.sC + (int64_t)pl * ps;
       const float v = tr[cr * kPitch + pl];
       *d = a.accumulate ? v + *d : v;
     }
@@ -2021,11 +2025,15 @@ int mvbev_warp_views_adjoint(const mvbev_warp_adjoint_view* views, int nviews, i
   for (int i = 0; i < nviews; ++i) {
     const mvbev_warp_adjoint_view& v = views[i];
     if (!v.grad_out || !v.grad_src || !v.row_ptr || !v.col || !v.val) return MVBEV_ERR_NULL;
-    // planes must be dense (the plan indexes pixels linearly); pixel-major: groups adjacent, pixels dense
+    // planes must be dense (the plan indexes pixels linearly); pixel-major: groups adjacent, pixels dense;
+    // a channels-last grad_src (pixel-major grad_out only): channels adjacent, pixels C apart
     const int64_t gp = pixm ? v.grad_out_strides[3] : 1;
+    const bool cl = pixm && v.grad_src_strides[1] == 1 && v.grad_src_strides[3] == C && v.grad_src_strides[2] == W * C;
+    if (i > 0 && cl != (a.src_cl != 0)) return MVBEV_ERR_STRIDE;  // one grad_src layout per launch
+    a.src_cl = cl ? 1 : 0;
     if ((pixm ? (v.grad_out_strides[1] != 1 || gp < C / 8 || v.grad_out_strides[2] != Wo * gp)
               : (v.grad_out_strides[3] != 1 || v.grad_out_strides[2] != Wo)) ||
-        v.grad_src_strides[3] != 1 || v.grad_src_strides[2] != W)
+        (!cl && (v.grad_src_strides[3] != 1 || v.grad_src_strides[2] != W)))
       return MVBEV_ERR_STRIDE;
     if (split && (reinterpret_cast<uintptr_t>(v.grad_out) & 15) != 0) return MVBEV_ERR_ALIGN;
     a.v[i] = bwd::AdjView{v.grad_out, v.grad_out_strides[0], v.grad_out_strides[1], gp, v.grad_src,

@@ -1084,7 +1084,8 @@ def warp_views_adjoint(grad_outs, plans, grad_srcs, accumulate: bool = False, pi
     ``plans[i]`` its ``WarpAdjointPlan``.  ``grad_outs[i]``: fp32 [B,C,Ho,Wo] with dense rows,
     or a bf16 split-bf16 blocked [B, C/8, Ho, Wo, 2, 8] view (``split_shape``; C % 8 == 0), or with
     ``pixel_major`` a [B, Ho, Wo, C/8, 2, 8] view of a pixel-major split tensor (``split_pix_shape``, the
-    view's groups a slice of the pixel's: MVBEV_LAYOUT_SPLIT_BF16_PIX) — the same grad_srcs."""
+    view's groups a slice of the pixel's: MVBEV_LAYOUT_SPLIT_BF16_PIX) — the same grad_srcs, which may then
+    also be channels-last tensors (all of them or none)."""
     n = len(grad_outs)
     if n == 0:
         return
@@ -1130,8 +1131,10 @@ def warp_views_adjoint(grad_outs, plans, grad_srcs, accumulate: bool = False, pi
             if g.stride(3) != 1 or g.stride(2) != Wo:
                 raise ValueError("grad_out planes must be dense (row stride = width, column stride 1)")
             gstr = tuple(g.stride())
-        if d.stride(3) != 1 or d.stride(2) != W:
-            raise ValueError("grad_src planes must be dense (row stride = width, column stride 1)")
+        cl = pixm and d.stride(1) == 1 and d.stride(3) == C and d.stride(2) == W * C  # channels-last grad_src
+        if not cl and (d.stride(3) != 1 or d.stride(2) != W):
+            raise ValueError("grad_src planes must be dense (row stride = width, column stride 1), or "
+                             "channels-last with a pixel-major grad_out")
         arr[i] = _native.WarpAdjointView(g.data_ptr(), (ctypes.c_int64 * 4)(*gstr), d.data_ptr(),
                                          (ctypes.c_int64 * 4)(*d.stride()), pl.row_ptr.data_ptr(),
                                          pl.col.data_ptr(), pl.val.data_ptr())

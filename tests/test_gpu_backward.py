@@ -130,6 +130,14 @@ def test_upsampled_warp_adjoint_vs_autograd(B, C, h, w, H, W, ho, wo):
     acc_p = [torch.full((B, C, h, w), 0.25, device=DEV) for _ in range(n)]
     ops.warp_views_adjoint(pv, plans, acc_p, accumulate=True, pixel_major=True)
     assert all(torch.equal(a, b) for a, b in zip(acc_p, acc))
+    # channels-last backbone-map gradients (the detector's maps): the same values, written in that layout
+    cl = torch.channels_last
+    outs_c = [torch.full((B, C, h, w), float("nan"), device=DEV).contiguous(memory_format=cl) for _ in range(n)]
+    ops.warp_views_adjoint(pv, plans, outs_c, pixel_major=True)
+    assert all(o.is_contiguous(memory_format=cl) and torch.equal(o.contiguous(), b) for o, b in zip(outs_c, outs_s))
+    acc_c = [torch.full((B, C, h, w), 0.25, device=DEV).contiguous(memory_format=cl) for _ in range(n)]
+    ops.warp_views_adjoint(pv, plans, acc_c, accumulate=True, pixel_major=True)
+    assert all(torch.equal(a.contiguous(), b) for a, b in zip(acc_c, acc))
     dst = [torch.empty((B, C, ho, wo), device=DEV) for _ in range(n)]
     ops.warp_views_upsampled_into([f.to(DEV) for f in feats], (H, W), mn, dst)
     for i in range(n):
@@ -192,6 +200,9 @@ def test_warp_adjoint_gather_vs_grid_sample_autograd(B, C, H, W, ho, wo):
         acc_p = [o.clone() for o in outs_p]
         ops.warp_views_adjoint(pv, plans, acc_p, accumulate=True, pixel_major=True)
         assert all(torch.equal(a, b) for a, b in zip(acc_p, acc_s))
+        outs_c = [torch.full_like(o, float("nan")).contiguous(memory_format=torch.channels_last) for o in outs]
+        ops.warp_views_adjoint(pv, plans, outs_c, pixel_major=True)
+        assert all(torch.equal(a.contiguous(), b) for a, b in zip(outs_c, outs_s))
 
 
 def test_warp_backward_no_gradient_from_outside_samples():

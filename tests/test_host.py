@@ -35,6 +35,42 @@ def test_library_exports_every_header_symbol():
     assert lib.mvbev_status_string(-100) == b"HIP launch failed"
 
 
+def test_pixel_major_split_layout_host_checks():
+    """MVBEV_LAYOUT_SPLIT_BF16_PIX (ABI 12100) on the host side: the shape helper, the conv-output
+    layout inference, and the adjoint's refusals before any launch (C % 8, group stride, mixed
+    grad_src layouts) — no GPU compute."""
+    from mvdet_amd import ops
+    assert ops.split_pix_shape(2, 20, 3, 5) == (2, 3, 5, 3, 2, 8)
+    f32 = torch.empty(2, 16, 3, 5)
+    sp = torch.empty(ops.split_shape(2, 16, 3, 5), dtype=torch.bfloat16)
+    px = torch.empty(ops.split_pix_shape(2, 16, 3, 5), dtype=torch.bfloat16)
+    assert ops._out_layout(f32, 2, 16, 3, 5) == _native.LAYOUT_F32
+    assert ops._out_layout(sp, 2, 16, 3, 5) == _native.LAYOUT_SPLIT_BF16
+    assert ops._out_layout(px, 2, 16, 3, 5) == _native.LAYOUT_SPLIT_PIX
+    with pytest.raises(ValueError):
+        ops._out_layout(px, 2, 24, 3, 5)
+    lib = _native.load()
+    fake = ctypes.c_void_p(16)  # never dereferenced: validation fails first
+    B, C, H, W, Ho, Wo, G = 1, 16, 6, 7, 4, 5, 4
+
+    def view(gstr, sstr):
+        return _native.WarpAdjointView(fake, _native._i64x4(*gstr), fake, _native._i64x4(*sstr), fake, fake, fake)
+    good_g = (Ho * Wo * G, 1, Wo * G, G)
+    planes = (C * H * W, H * W, W, 1)
+    cl = (C * H * W, 1, W * C, C)
+    arr = (_native.WarpAdjointView * 1)(view(good_g, planes))
+    pix = _native.LAYOUT_SPLIT_PIX
+    assert lib.mvbev_warp_views_adjoint(arr, 1, pix, B, 12, H, W, Ho, Wo, 0, None) == -2  # C % 8
+    arr = (_native.WarpAdjointView * 1)(view((Ho * Wo * G, 2, Wo * G, G), planes))  # groups not adjacent
+    assert lib.mvbev_warp_views_adjoint(arr, 1, pix, B, C, H, W, Ho, Wo, 0, None) == -3
+    arr = (_native.WarpAdjointView * 1)(view((Ho * Wo, 1, Wo, 1), planes))  # pixel stride < C / 8 groups
+    assert lib.mvbev_warp_views_adjoint(arr, 1, pix, B, C, H, W, Ho, Wo, 0, None) == -3
+    arr = (_native.WarpAdjointView * 2)(view(good_g, cl), view(good_g, planes))  # one grad_src layout per launch
+    assert lib.mvbev_warp_views_adjoint(arr, 2, pix, B, C, H, W, Ho, Wo, 0, None) == -3
+    arr = (_native.WarpAdjointView * 1)(view((G * Ho * Wo, Ho * Wo, Wo, 1), cl))  # channels-last needs pixel-major
+    assert lib.mvbev_warp_views_adjoint(arr, 1, _native.LAYOUT_SPLIT_BF16, B, C, H, W, Ho, Wo, 0, None) == -3
+
+
 def test_argument_validation_codes():
     lib = _native.load()
     s4 = _native._i64x4(1, 1, 1, 1)

@@ -34,6 +34,10 @@ import numpy as np
 LINK_GBS = 64.0     # effective GB/s per xGMI link and direction (153.6 GB/s per link both ways, ~83 %)
 COLL_EFF = 0.7      # RCCL ring collectives: fraction of the P - 1 links' sum they sustain
 A2A_EFF = 0.7       # all-to-all: fraction of one link per peer chunk
+# the fused upsample + warp + B^T from channels-last backbone maps vs the NCHW fused warp from upsampled
+# features (cfg2: 0.3004 vs 0.4852 ms, profiles/r05final_bench.json plus_a4.fused_channels_last), for the
+# configs without their own ``warp_up`` figure
+WARP_UP_RATIO = 0.62
 
 # Single-GPU stage times (ms, one frame) of the bench's path on 1 x MI355X: warp = fused warp + row
 # transform of every view, conv1 = the Winograd conv kernel (whole grid, frustum-masked), conv2 =
@@ -42,7 +46,7 @@ A2A_EFF = 0.7       # all-to-all: fraction of one link per peer chunk
 # profiles/r05d_bench.json (the cfg2 line and its cfg3 / cfg5 / cfg4 sub-objects; NCHW features; cfg4: B = 8,
 # fp16 features on the fused warp).
 SINGLE_GPU_MS: Dict[int, Dict[str, float]] = {
-    2: dict(warp=0.4938, conv1=1.4174, conv2=0.3354, conv3=0.0253, transform=0.25),
+    2: dict(warp=0.4938, conv1=1.4174, conv2=0.3354, conv3=0.0253, transform=0.25, warp_up=0.3004),
     3: dict(warp=5.2145, conv1=20.3366, conv2=4.746, conv3=0.1937, transform=4.0),
     4: dict(warp=3.3355, conv1=8.2243, conv2=2.4732, conv3=0.151, transform=1.6),
     5: dict(warp=4.4294, conv1=15.0497, conv2=7.0832, conv3=0.1938, transform=2.3),
@@ -88,33 +92,65 @@ def balanced_views(weights: Sequence[float], world: int) -> List[List[int]]:
     return [sorted(vs) for vs in out]
 
 
+def view_owners(weights: Sequence[float], world: int) -> List[int]:
+    """The rank whose backbone produces each view (round 6): the longest-processing-time
+    dealing of whole views (``balanced_views``), so whole-view parts never cross xGMI and, with P >= N, every
+    view has a rank of its own.  Deterministic: every rank computes the same owners."""
+    owner = [-1] * len(weights)
+    for r, vs in enumerate(balanced_views(weights, world)):
+        for v in vs:
+            owner[v] = r
+    return owner
+
+
 def balanced_parts(weights: Sequence[float], world: int, C: int, warp_frac: float = 0.05,
-                   min_part: int = 64, gain: float = 0.02):
+                   min_part: int = 64, gain: float = 0.02, k: int = 0, affinity: float = 0.5):
     """The partial-sum mode's channel split (round 5): conv1 is linear in its input channels, so a view's
     channels can be convolved on several ranks.  Views are cut into k equal channel parts (k = 1, 2, 4, ...
     while the part keeps >= ``min_part`` channels) and the parts dealt by longest-processing-time, a part of
     view v weighing (weights[v] + warp_frac) / k (its conv1 share of the frustum-active work plus its share
     of the view's warp, ``warp_frac`` of a full view's conv1); the k with the smallest maximum rank load
     wins, a larger k only when it lowers that load by more than ``gain`` (each part is a slot of the rank's
-    warp and conv1).  Returns (per rank the sorted (view, first channel) parts, part width); deterministic,
-    so every rank computes the same assignment."""
+    warp and conv1); ``k`` > 0 forces the split.  Round 6: a part goes to its view's owner (``view_owners``,
+    where its backbone map is) instead of the least-loaded rank when that costs at most ``affinity`` of the
+    part's weight in load, so fewer slices cross xGMI.  Returns (per rank the sorted (view, first channel)
+    parts, part width); deterministic, so every rank computes the same assignment."""
     N = len(weights)
+    owner = view_owners([w + warp_frac for w in weights], world)
     best = None
-    k = 1
-    while C % k == 0 and (k == 1 or C // k >= min_part):
-        items = sorted(((weights[v] + warp_frac) / k, v, j) for v in range(N) for j in range(k))
+    kk = 1
+    while C % kk == 0 and (kk == 1 or C // kk >= min_part):
+        if k and kk != k:
+            kk *= 2
+            continue
+        items = sorted(((weights[v] + warp_frac) / kk, v, j) for v in range(N) for j in range(kk))
         items.sort(key=lambda t: (-t[0], t[1], t[2]))
         load = [0.0] * world
         out: List[List[tuple]] = [[] for _ in range(world)]
         for w, v, j in items:
             r = min(range(world), key=lambda q: (load[q], q))
-            out[r].append((v, j * (C // k)))
+            if load[owner[v]] <= load[r] + affinity * w:
+                r = owner[v]
+            out[r].append((v, j * (C // kk)))
             load[r] += w
         m = max(load)
         if best is None or m < best[0] * (1.0 - gain):
-            best = (m, [sorted(ps) for ps in out], C // k)
-        k *= 2
+            best = (m, [sorted(ps) for ps in out], C // kk)
+        kk *= 2
+    if best is None:
+        raise ValueError(f"cannot split {C} channels into {k} parts of >= {min_part}")
     return best[1], best[2]
+
+
+def fetch_link_bytes(assign, owner: Sequence[int], P: int, part_bytes: float) -> np.ndarray:
+    """[P, P] bytes of backbone-map channel slices rank p sends to rank q per frame (the partial-sum
+    mode's slice exchange: every part held by a rank that does not own its view)."""
+    out = np.zeros((P, P))
+    for q, ps in enumerate(assign):
+        for v, _ in ps:
+            if owner[v] != q:
+                out[owner[v], q] += part_bytes
+    return out
 
 
 def _tiles(rows: int) -> int:
@@ -122,8 +158,9 @@ def _tiles(rows: int) -> int:
 
 
 def predict(N: int, C: int, grid_hw, B: int, P: int, single: Dict[str, float],
-            activity: Sequence[np.ndarray]) -> Dict[str, dict]:
-    """Predicted per-frame ms of each mode at P ranks (the slowest rank), with its parts."""
+            activity: Sequence[np.ndarray], backbone_px: float = 0.0) -> Dict[str, dict]:
+    """Predicted per-frame ms of each mode at P ranks (the slowest rank), with its parts.  ``backbone_px``:
+    pixels of one backbone map (the partial-sum mode's slice exchange moves channel slices of those)."""
     Ho, Wo = int(grid_hw[0]), int(grid_hw[1])
     band = math.ceil(Ho / P)
     vmax = math.ceil(N / P)
@@ -156,12 +193,29 @@ def predict(N: int, C: int, grid_hw, B: int, P: int, single: Dict[str, float],
     # -- partial
     rs_bytes = 4.0 * B * 512 * Ho * Wo
     rs = rs_bytes * (P - 1) / P / (COLL_EFF * (P - 1) * bw) if P > 1 else 0.0
-    # as parallel.ViewPartialSum deals them: channel parts of the views (balanced_parts)
-    assign, cp = balanced_parts([float(a.mean()) for a in activity], P, C)
-    frac = cp / C
-    prod = max((sum(w_view * frac + conv1_band(0, Ho, [v]) * frac for v, _ in ps)) if ps else 0.0 for ps in assign)
+    # as parallel.ViewPartialSum deals them: channel parts of the views (balanced_parts); each rank owns the
+    # backbone maps of its views (part_owners) and sends the other holders their parts' channel slices at
+    # backbone resolution (src / 3), one all-to-all on the exchange stream (round 6): the rank's warp is
+    # the fused upsample + warp + B^T of its parts
+    weights = [float(a.mean()) for a in activity]
+    owner = view_owners([w + 0.05 for w in weights], P)
+    w_up = single.get("warp_up", single["warp"] * WARP_UP_RATIO) / N
     cons = single["conv2"] * _tiles(min(Ho, band + 8)) / rows_all + single["conv3"] / P
-    out["partial"] = dict(produce=prod, exchange=rs, consume=cons, frame=max(prod + cons, rs))
+    best = None
+    k = 1
+    while C % k == 0 and (k == 1 or C // k >= 64):  # the split the bench takes: the fastest predicted k
+        assign, cp = balanced_parts(weights, P, C, k=k)
+        frac = cp / C
+        prod = max((sum(w_up * frac + conv1_band(0, Ho, [v]) * frac for v, _ in ps)) if ps else 0.0
+                   for ps in assign)
+        links = fetch_link_bytes(assign, owner, P, 4.0 * B * cp * backbone_px)
+        fetch = float(links.max()) / (A2A_EFF * bw) if P > 1 else 0.0
+        cand = dict(produce=prod, exchange=rs + fetch, consume=cons, frame=max(prod + cons, rs + fetch), fetch=fetch,
+                    fetch_bytes_max_rank=float(max(links.sum(0).max(), links.sum(1).max())), parts_k=k)
+        if best is None or cand["frame"] < best["frame"] * 0.98:
+            best = cand
+        k *= 2
+    out["partial"] = best
     # -- gather
     ag = N * slab_view * (P - 1) / P / (COLL_EFF * (P - 1) * bw) if P > 1 else 0.0
     out["gather"] = dict(produce=vmax * w_view * 0.8, exchange=ag, consume=worst + single["conv3"] / P,
@@ -184,10 +238,22 @@ def config_inputs(cfg: int):
     return ds.num_cam, spec["C"], grid, spec["B"], acts
 
 
+def backbone_pixels(cfg: int) -> float:
+    """Pixels of one backbone map at a BASELINE config (the upsampled warp source / 3 per side, ``:64-65``)."""
+    from . import synthetic
+    up = synthetic.CONFIGS[cfg]["make"]().upsample_shape
+    return float((up[0] // 3) * (up[1] // 3))
+
+
+def predict_config(cfg: int, P: int) -> Dict[str, dict]:
+    """``predict`` at a BASELINE config's synthetic rig and measured single-GPU stage times."""
+    N, C, grid, B, acts = config_inputs(cfg)
+    return predict(N, C, grid, B, P, SINGLE_GPU_MS[cfg], acts, backbone_pixels(cfg))
+
+
 def choose_mode(cfg: int, P: int) -> str:
     """The strong-scaling mode with the smallest predicted frame time at P ranks."""
     if P <= 1 or cfg not in SINGLE_GPU_MS:
         return "bands"
-    N, C, grid, B, acts = config_inputs(cfg)
-    pred = predict(N, C, grid, B, P, SINGLE_GPU_MS[cfg], acts)
+    pred = predict_config(cfg, P)
     return min(pred, key=lambda k: pred[k]["frame"])

@@ -42,7 +42,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
-from .mp_model import balanced_parts, balanced_views  # noqa: F401  (re-exported: the partial-sum mode's dealing)
+from .mp_model import balanced_parts, balanced_views, view_owners  # noqa: F401  (re-exported: the partial-sum mode's dealing)
 
 # rows of the ground-plane tensor an output row of conv1 -> conv2 -> conv3 depends on, each side
 HALO_IN = 1 + 2 + 4
@@ -136,7 +136,9 @@ class _FrameGuard:
 
     @staticmethod
     def agree(fr, group) -> tuple:
-        fr.gflag.copy_(fr.nf)
+        # the MAX of "this rank fired for THIS frame" (tag or 0), not of the raw flags: after a tag wrap-around
+        # another frame buffer's stale pre-wrap tag must not outrank a current report
+        torch.mul(fr.nf.eq(fr.tag), fr.tag, out=fr.gflag)
         _all_reduce_max(fr.gflag, group)
         return fr.gflag, fr.tag
 
@@ -199,6 +201,10 @@ class _ViewSharded:
 
     def step(self, fr, feats, map_classifier, mark=None) -> torch.Tensor:
         """One frame, unpipelined (``feats[j]`` is view ``my_views[j]``)."""
+        if getattr(self, "fetches", False):
+            if mark:
+                mark("fetch")
+            self.fetch(fr, feats)
         if mark:
             mark("warp")
         self.produce(fr, feats, map_classifier, mark=mark)
@@ -281,6 +287,9 @@ class ViewBands(_ViewSharded):
         self.nv = [len(views_of(q, world, self.num_cam)) for q in range(world)]
         self.engine = engine_factory(packed_slot_views(world, self.num_cam))
         self.local = engine_factory(self.my_views, all_views=False) if self.my_views else None
+        split = getattr(self.engine, "split", True)
+        if not split and getattr(self.engine, "slab_dtype", torch.float32) != torch.float32:
+            raise ValueError("the band exchange's windows are split-bf16 or fp32 (not an fp16 slab)")
         # every rank takes part in the flag's MAX, so the decision is the fusion engine's (the same on all)
         self.guard = bool(getattr(self.engine, "guard_windows", lambda: False)())
         self._fg = _FrameGuard()
@@ -369,16 +378,31 @@ class ViewPartialSum(_ViewSharded):
 
     def __init__(self, engine_factory, proj_mats, grid_hw, rank, world, group=None,
                  view_weights: Optional[Sequence[float]] = None, channels: Optional[int] = None,
-                 min_part: int = 64):
+                 min_part: int = 64, parts_k: int = 0, fetch_hw: Optional[Tuple[int, int]] = None,
+                 fetch_dtype: torch.dtype = torch.float32, fetch_channels_last: bool = False):
         super().__init__(proj_mats, grid_hw, rank, world, group)
         self.my_parts, self.part_channels = None, None
+        self.fetches = False
         if view_weights is not None and channels is not None:
             # round 5: views cut into channel parts dealt by their conv1 work (mp_model.balanced_parts): the
             # heaviest view no longer sets the rank time when P >= N.  The rank's engine takes the parts as
-            # its cameras; it needs the features of every view it holds a part of (my_views).
-            assign, cp = balanced_parts(view_weights, world, int(channels), min_part=min_part)
-            self.my_parts, self.part_channels = assign[rank], cp
-            self.my_views = sorted({v for v, _ in self.my_parts})
+            # its cameras.  Round 6: each view's features (its backbone map) live on ONE rank, its owner
+            # (mp_model.view_owners: where its backbone runs); ``fetch`` sends every other holder its parts'
+            # channel slices (one all-to-all on the exchange stream), so the caller passes only the OWNED
+            # views' features (``my_views``) and the timed region carries the transfer.
+            assign, cp = balanced_parts(view_weights, world, int(channels), min_part=min_part, k=parts_k)
+            self.assign, self.my_parts, self.part_channels = assign, assign[rank], cp
+            self.owner = view_owners([w + 0.05 for w in view_weights], world)
+            self.my_views = [v for v in range(self.num_cam) if self.owner[v] == rank]
+            self.fetches = True
+            self.fetch_hw = None if fetch_hw is None else (int(fetch_hw[0]), int(fetch_hw[1]))
+            self.fetch_dtype, self.fetch_cl = fetch_dtype, bool(fetch_channels_last)
+            # every part held away from its owner crosses xGMI once; both lists in rank order, parts sorted
+            self.send_parts = [[(v, c0) for v, c0 in assign[q] if self.owner[v] == rank and q != rank]
+                               for q in range(world)]
+            self.recv_parts = [[(v, c0) for v, c0 in self.my_parts if self.owner[v] == p and p != rank]
+                               for p in range(world)]
+            self.moves = any(self.owner[v] != q for q in range(world) for v, _ in assign[q])
         elif view_weights is not None:
             self.my_views = balanced_views(view_weights, world)[rank]
         if self.my_parts is not None:
@@ -404,22 +428,71 @@ class ViewPartialSum(_ViewSharded):
         H, W = self.grid_hw
         P, n = self.world, self.band_rows
         e = min(self.HALO, n)
-        return SimpleNamespace(
-            ws=ws, B=B, device=device,
+        fr = SimpleNamespace(
+            ws=ws, B=B, device=device, owned=None,
             stage=torch.zeros((P, B, mid, n, W), dtype=torch.float32, device=device),
             mine=torch.zeros((B, mid, n, W), dtype=torch.float32, device=device),
             edges=torch.zeros((P, 2, B, mid, e, W), dtype=torch.float32, device=device),
             full=None if n >= self.HALO else torch.zeros((P, B, mid, n, W), dtype=torch.float32, device=device))
+        if self.fetches:  # the slice exchange's send / receive buffers, one [B, cp, h, w] piece per part
+            h, w = self.fetch_hw if self.fetch_hw is not None else tuple(self._fuse_engine.src_hw)
+            shape = (B, self.part_channels, h, w)
+            fr.part_numel = B * self.part_channels * h * w
+            ns, nr = sum(map(len, self.send_parts)), sum(map(len, self.recv_parts))
+            fr.send = torch.empty(ns * fr.part_numel, dtype=self.fetch_dtype, device=device)
+            fr.recv = torch.empty(nr * fr.part_numel, dtype=self.fetch_dtype, device=device)
+            fr.send_views = self._part_views(fr.send, [p for ps in self.send_parts for p in ps], shape)
+            fr.recv_views = self._part_views(fr.recv, [p for ps in self.recv_parts for p in ps], shape)
+        return fr
+
+    def _part_views(self, flat, parts, shape):
+        """{(view, c0): [B, cp, h, w] view of ``flat``} for consecutive parts (channels-last memory when the
+        wire format is)."""
+        B, cp, h, w = shape
+        n = B * cp * h * w
+        out = {}
+        for i, p in enumerate(parts):
+            chunk = flat[i * n:(i + 1) * n]
+            out[p] = chunk.view(B, h, w, cp).permute(0, 3, 1, 2) if self.fetch_cl else chunk.view(B, cp, h, w)
+        return out
+
+    def fetch(self, fr, feats) -> None:
+        """The slice exchange (round 6): ``feats[j]`` is the owned view ``my_views[j]``'s map (at ``fetch_hw``,
+        the backbone resolution, or at the warp's source size); each of its parts held by another rank is
+        copied into the send buffer and one ``all_to_all_single`` delivers to every rank the slices of its
+        parts whose views it does not own (a rank's own parts are read in place by its warp).  On the exchange
+        stream under ``FramePipeline``, before the frame's produce."""
+        if len(feats) != len(self.my_views):
+            raise ValueError(f"rank {self.rank} owns views {self.my_views}: pass their {len(self.my_views)} maps")
+        want = self.fetch_hw if self.fetch_hw is not None else tuple(self._fuse_engine.src_hw)
+        for v, f in zip(self.my_views, feats):
+            if tuple(f.shape[2:]) != tuple(want) or f.dtype != self.fetch_dtype:
+                raise ValueError(f"view {v}: map {tuple(f.shape)} {f.dtype}, expected [B, C, {want[0]}, {want[1]}] "
+                                 f"{self.fetch_dtype}")
+        fr.owned = dict(zip(self.my_views, feats))
+        if not self.moves:
+            return
+        cp = self.part_channels
+        for q in range(self.world):
+            for v, c0 in self.send_parts[q]:
+                fr.send_views[(v, c0)].copy_(fr.owned[v][:, c0:c0 + cp])
+        n = fr.part_numel
+        _all_to_all(fr.recv, fr.send, [len(ps) * n for ps in self.recv_parts],
+                    [len(ps) * n for ps in self.send_parts], self.group)
 
     def produce(self, fr, feats, map_classifier=None, mark=None) -> None:
-        """Warp this rank's views (into conv1's T where the engine fuses it), then conv1 over their
-        channels for all rows, written band-major into the reduce-scatter's input."""
+        """Warp this rank's views or parts (into conv1's T where the engine fuses it; from backbone-resolution
+        maps the fused upsample + warp), then conv1 over their channels for all rows, written band-major into
+        the reduce-scatter's input.  With the slice exchange (``fetches``) the parts' features are the own
+        views' slices and the fetched ones (``feats`` is not read: ``fetch`` took the owned maps)."""
         if self.engine is None:
             fr.stage.zero_()
             return
         lws = self._local_ws[(str(fr.device), fr.B)]
-        cams, feats = self._cameras(feats)
-        if hasattr(self.engine, "warp_views"):
+        cams, feats = self._cameras(fr, feats)
+        if tuple(feats[0].shape[2:]) != tuple(self.engine.src_hw):
+            self.engine.warp_views_upsampled(lws, cams, feats)  # a4 + a5 (+ conv1's B^T) from backbone maps
+        elif hasattr(self.engine, "warp_views"):
             self.engine.warp_views(lws, cams, feats)
         else:
             for v, f in zip(cams, feats):
@@ -428,15 +501,15 @@ class ViewPartialSum(_ViewSharded):
             mark("conv1")
         self.engine.conv1_partial(lws, map_classifier, fr.stage, mark=mark, band_rows=self.band_rows)
 
-    def _cameras(self, feats):
+    def _cameras(self, fr, feats):
         """(engine cameras, their features): the views, or with channel parts each part's channel slice
-        of its view's features (``feats[j]`` is view ``my_views[j]``)."""
+        (own views' slices in place, the others' from the slice exchange's receive buffer)."""
         if self.my_parts is None:
             return list(self.my_views), list(feats)
-        idx = {v: j for j, v in enumerate(self.my_views)}
         cp = self.part_channels
         return (list(range(len(self.my_parts))),
-                [feats[idx[v]][:, c0:c0 + cp] for v, c0 in self.my_parts])
+                [fr.owned[v][:, c0:c0 + cp] if self.owner[v] == self.rank else fr.recv_views[(v, c0)]
+                 for v, c0 in self.my_parts])
 
     @property
     def conv1_channels(self) -> int:
@@ -498,35 +571,58 @@ class FramePipeline:
     ``drain()`` finishes the last frame.  Two frame buffers alternate: frame i+2's produce runs
     after frame i's consume on the compute stream, and frame i+2's exchange waits for that
     produce, so no buffer is rewritten while a collective or the fusion still reads it.  With
-    gloo (CPU tests, host-staged single-GPU rehearsals) the same order runs on one stream."""
+    gloo (CPU tests, host-staged single-GPU rehearsals) the same order runs on one stream.
+
+    A driver with an input exchange (``fetches``: the partial-sum mode's channel-slice exchange, round 6)
+    adds a stage in front: ``submit(frame i)`` enqueues frame i's fetch on the side stream, then frame
+    i-1's produce (after its fetch-done event) and exchange, then frame i-2's consume — the fetch of frame
+    i+1 runs under frame i's produce, the reduce-scatter of frame i under frame i-1's fusion.  Three frame
+    buffers rotate (frame i+3's fetch waits for an event recorded after frame i's produce was enqueued);
+    ``submit`` then returns frame i-2's map and ``drain`` is called until it returns None."""
 
     def __init__(self, driver: _ViewSharded, B: int, device):
         self.d = driver
         device = torch.device(device)
-        self.frames = [driver.workspace(B, device, tag=t) for t in (0, 1)]
+        self.fetching = bool(getattr(driver, "fetches", False))
+        self.frames = [driver.workspace(B, device, tag=t) for t in range(3 if self.fetching else 2)]
         self.comm = (torch.cuda.Stream(device) if device.type == "cuda" and dist.get_backend(driver.group) == "nccl"
                      else None)
         self.i = 0
-        self.pending = None
+        self.fetched = None   # (frame, fetch-done event): inputs exchanged, not yet produced
+        self.pending = None   # (frame, exchange-done event): produced and exchanged, not yet consumed
 
-    def submit(self, feats, map_classifier) -> Optional[torch.Tensor]:
-        fr = self.frames[self.i % 2]
-        self.i += 1
-        self.d.produce(fr, feats, map_classifier)
-        done = None
+    def _on_comm(self, fn):
+        """Run ``fn`` on the side stream after everything enqueued so far on the compute stream."""
         if self.comm is None:
-            self.d.exchange(fr)
-        else:
-            ready = torch.cuda.Event()
-            ready.record()
-            with torch.cuda.stream(self.comm):
-                self.comm.wait_event(ready)
-                self.d.exchange(fr)
-                done = torch.cuda.Event()
-                done.record(self.comm)
+            fn()
+            return None
+        ready = torch.cuda.Event()
+        ready.record()
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(ready)
+            fn()
+            done = torch.cuda.Event()
+            done.record(self.comm)
+        return done
+
+    def _advance(self, fr, feats, fetched, map_classifier):
+        """Produce + exchange ``fr`` (after its fetch-done event), then consume the pending frame."""
+        if fetched is not None:
+            torch.cuda.current_stream().wait_event(fetched)
+        self.d.produce(fr, feats, map_classifier)
+        done = self._on_comm(lambda: self.d.exchange(fr))
         out = self._consume(self.pending, map_classifier) if self.pending is not None else None
         self.pending = (fr, done)
         return out
+
+    def submit(self, feats, map_classifier) -> Optional[torch.Tensor]:
+        fr = self.frames[self.i % len(self.frames)]
+        self.i += 1
+        if not self.fetching:
+            return self._advance(fr, feats, None, map_classifier)
+        ev = self._on_comm(lambda: self.d.fetch(fr, feats))
+        prev, self.fetched = self.fetched, (fr, ev)
+        return self._advance(prev[0], None, prev[1], map_classifier) if prev is not None else None
 
     def _consume(self, pending, map_classifier):
         fr, done = pending
@@ -535,11 +631,24 @@ class FramePipeline:
         return self.d.consume(fr, map_classifier)
 
     def drain(self, map_classifier) -> Optional[torch.Tensor]:
+        """The next map still in flight (None when every submitted frame has come back)."""
+        if self.fetched is not None:
+            fr, ev = self.fetched
+            self.fetched = None
+            return self._advance(fr, None, ev, map_classifier)
         if self.pending is None:
             return None
         out = self._consume(self.pending, map_classifier)
         self.pending = None
         return out
+
+    def drain_all(self, map_classifier) -> List[torch.Tensor]:
+        out = []
+        while True:
+            o = self.drain(map_classifier)
+            if o is None:
+                return out
+            out.append(o)
 
 
 def bench_main(args) -> None:
@@ -606,15 +715,23 @@ def bench_main(args) -> None:
         pm = projection_matrices(ds)
         mc = build_mc(C, N, head_params(N, seed=cfg, C=C), dev)
         half = cfg == 4  # fp16 features: the fused warp / window warps read them (split-bf16 slab / T)
-        fact = (lambda sv, **kw: ProjectFuse(pm, up, grid, C, slot_views=sv, precision=args.precision,
-                                             slab_dtype=torch.float16 if half and args.precision == "fp32"
-                                             else torch.float32, **kw))
+        # cfg4's fp16 features feed the fused warp (split-bf16 T, bf16x3) or an fp32 slab (precision fp32)
+        fact = (lambda sv, **kw: ProjectFuse(pm, up, grid, C, slot_views=sv, precision=args.precision, **kw))
         return SimpleNamespace(spec=spec, B=B, C=C, N=N, up=up, grid=grid, pm=pm, mc=mc, half=half, fact=fact)
 
     def feats_for(s, views, cfg, base_seed=0):
         return [synthetic.synthetic_features(s.B, s.C, [u // 3 for u in s.up], s.up, seed=1000 * cfg + base_seed + v,
                                              device=dev).to(torch.float16 if s.half else torch.float32)
                 for v in views]
+
+    def backbone_maps(s, views, cfg, channels_last):
+        """The owned views' backbone-resolution maps (``:64``; the warp's source is their 3x upsample)."""
+        out = []
+        for v in views:
+            x = synthetic.backbone_features(s.B, s.C, [u // 3 for u in s.up], seed=1000 * cfg + v, device=dev)
+            x = x.to(torch.float16) if s.half else x
+            out.append(x.contiguous(memory_format=torch.channels_last) if channels_last else x)
+        return out
 
     def run(mode, cfg, K, W):
         s = setup(cfg)
@@ -641,20 +758,30 @@ def bench_main(args) -> None:
             else:
                 cls = {"bands": ViewBands, "gather": ViewParallel, "partial": ViewPartialSum}[mode]
                 kw = {}
-                if mode == "partial":  # views cut into channel parts dealt by their conv1 work (frustum-active tiles)
+                if mode == "partial":
+                    # views cut into channel parts dealt by their conv1 work (frustum-active tiles), the split the
+                    # cost model predicts fastest; each rank holds only the backbone-resolution maps of the views
+                    # it owns (channels-last, as the drop-in detector's backbone writes them; fp16 NCHW at cfg4)
+                    # and the slice exchange sends the other holders their parts inside the timed region
                     kw["view_weights"] = [float(a.mean()) for a in mp_model.config_inputs(cfg)[4]]
                     kw["channels"] = s.C
+                    kw["parts_k"] = int(mp_model.predict_config(cfg, world)["partial"]["parts_k"]) \
+                        if cfg in mp_model.SINGLE_GPU_MS else 0
+                    kw["fetch_hw"] = tuple(u // 3 for u in s.up)
+                    kw["fetch_dtype"] = torch.float16 if s.half else torch.float32
+                    kw["fetch_channels_last"] = not s.half
                 vp = cls(s.fact, s.pm, s.grid, rank, world, **kw)
-                feats = feats_for(s, vp.my_views, cfg)
+                feats = (backbone_maps(s, vp.my_views, cfg, channels_last=not s.half) if mode == "partial"
+                         else feats_for(s, vp.my_views, cfg))
                 pipe = FramePipeline(vp, s.B, dev)
                 for _ in range(W):
                     pipe.submit(feats, s.mc)
-                pipe.drain(s.mc)
+                pipe.drain_all(s.mc)
 
                 def steps(k):
                     for _ in range(k):
                         pipe.submit(feats, s.mc)
-                    pipe.drain(s.mc)
+                    pipe.drain_all(s.mc)
                 dt = timed(steps, K)
                 fr = vp.workspace(s.B, dev)
                 st = stage_times(lambda mark: vp.step(fr, feats, s.mc, mark=mark), max(3, K // 4))
@@ -679,6 +806,17 @@ def bench_main(args) -> None:
         res = dict(value=round(value, 3), ms_per_step=round(dt * 1e3 / K, 4), stages_ms_rank0=st,
                    band_rank0=list(band), conv1_rows_rank0=list(act_rows), steps=K, warmup=W,
                    workload=f"cfg{cfg}: {s.spec['name']}")
+        if mode == "partial":
+            res["inputs"] = ("each rank: the backbone-resolution maps of the views it owns (mp_model.view_owners; "
+                             + ("fp16 NCHW" if s.half else "fp32 channels-last") + "); the channel slices of the "
+                             "parts held elsewhere cross in one all-to-all per frame inside the timed region, and "
+                             "the a4 upsample runs fused into the warp (more work than the N = 1 value's step)")
+            res["parts"] = dict(k=s.C // vp.part_channels, part_channels=vp.part_channels,
+                                parts_rank0=[list(p) for p in vp.my_parts], owners=vp.owner,
+                                fetched_bytes_rank0=int(sum(map(len, vp.recv_parts))) * fr.part_numel *
+                                (2 if s.half else 4))
+        elif mode != "frames":
+            res["inputs"] = "each rank: the upsampled features of the views it owns (views_of: v % P)"
         if mode != "frames":
             res["unpipelined_ms_rank0"] = st_total
         if ach is not None:
@@ -694,10 +832,8 @@ def bench_main(args) -> None:
     mode = getattr(args, "mp_mode", "auto")
     predicted = None
     if mode == "auto":  # the mode the cost model predicts fastest at this config and world size
-        N, C, grid, B, acts = mp_model.config_inputs(args.config)
         if args.config in mp_model.SINGLE_GPU_MS:
-            predicted = {k: round(v["frame"], 4) for k, v in
-                         mp_model.predict(N, C, grid, B, world, mp_model.SINGLE_GPU_MS[args.config], acts).items()}
+            predicted = {k: round(v["frame"], 4) for k, v in mp_model.predict_config(args.config, world).items()}
         mode = mp_model.choose_mode(args.config, world)
     hows = {"frames": f"frame-parallel x{world}: each rank its own frame batch (all views), no collective",
             "bands": f"view-parallel x{world} ({backend}): rank r warps views v%{world}==r, RCCL all-to-all of "
@@ -768,6 +904,9 @@ def bench_main(args) -> None:
             line["speedup_vs_cpu"] = round(res["value"] / cpu["value"], 1)
         if "unpipelined_ms_rank0" in res:
             line["unpipelined_ms_rank0"] = res["unpipelined_ms_rank0"]
+        for k in ("inputs", "parts"):
+            if k in res:
+                line[k] = res[k]
         for m, r in alts.items():
             ns_key = m.startswith("north_star")
             key = m if ns_key else ("frame_parallel" if m == "frames" else f"view_parallel_{m}")

@@ -738,10 +738,19 @@ class ProjectFuse:
         """a5 of ``cams[i]`` (features ``feats[i]``) for the row window of ``dsts[i]`` (``window_buffer``
         entries, zero-filled and only written by this warp) from grid row ``row0s[i]`` — the exchange's
         send chunks written straight by the warp (no whole-grid slab, no window copies), 16 per launch.
-        ``nonfinite``: (flag, tag) — the non-finite report."""
-        if not self.split:
-            raise ValueError("window warps write the split-bf16 slab layout")
+        ``nonfinite``: (flag, tag) — the non-finite report.  A non-split engine (``precision="fp32"``: fp32
+        windows) warps its windows in the reference's own evaluation order (``mvbev_warp_views_exact_rows``,
+        ungated; ADVICE r05: the band exchange under fp32 precision) and has no non-finite report (its convs
+        take exact fp32 products already)."""
         H = self.grid_hw[0]
+        if not self.split:
+            if self.slab_dtype != torch.float32:
+                raise ValueError("window warps write split-bf16 or fp32 windows (an fp16 slab is not supported)")
+            for i in range(0, len(dsts), 16):
+                sl = slice(i, i + 16)
+                ops.warp_views_exact_into(list(feats[sl]), [self.m_norm_cpu[c] for c in cams[sl]],
+                                          [d[:, :self.C] for d in dsts[sl]], row0s=list(row0s[sl]), grid_rows=H)
+            return
         for i in range(0, len(dsts), 16):
             sl = slice(i, i + 16)
             ops.warp_views_split_rows_into(list(feats[sl]), [self.m_norm_cpu[c] for c in cams[sl]], list(dsts[sl]),

@@ -97,6 +97,11 @@ class OracleEngine:
             M = torch.as_tensor(np.asarray(self.pm[v])).reshape(1, 3, 3).repeat(f.shape[0], 1, 1).float()
             d.copy_(kornia_warp.warp_perspective(f, M, list(self.grid_hw))[:, :, r0:r0 + d.shape[2]])
 
+    def warp_views_upsampled(self, ws, cams, feats):
+        """a4 + a5: the 3x bilinear upsample of backbone-resolution maps (``:65``), then the warp."""
+        for v, f in zip(cams, feats):
+            self.warp_view(ws, v, torch.nn.functional.interpolate(f.float(), list(self.src_hw), mode="bilinear"))
+
     def warp_view(self, ws, v, feat):
         B = feat.shape[0]
         pv = v if self.parts is None else self.parts[v][0]
@@ -129,14 +134,23 @@ def _case():
 MODES = {"gather": parallel.ViewParallel, "partial": parallel.ViewPartialSum, "bands": parallel.ViewBands}
 
 
-def _worker(rank, world, port, out_dir, mode="gather", frames=1, weights=None, split=False):
+def _backbone_maps(up, C, B):
+    """Backbone-resolution maps (src / 3) whose 3x upsample is the warp's source (``:64-65``)."""
+    g = torch.Generator().manual_seed(77)
+    return [torch.randn(B, C, up[0] // 3, up[1] // 3, generator=g).clamp_min_(0) for _ in range(3)]
+
+
+def _worker(rank, world, port, out_dir, mode="gather", frames=1, weights=None, split=False, k=0, backbone=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(1)
     pm, up, grid, C, B, feats, params = _case()
     kw = {} if weights is None else {"view_weights": weights}
     if split:  # channel parts of the views (C = 8 here: parts down to 2 channels)
-        kw.update(channels=C, min_part=2)
+        kw.update(channels=C, min_part=2, parts_k=k)
+        if backbone:  # the owners' backbone-resolution maps cross (channels-last wire format)
+            feats = _backbone_maps(up, C, B)
+            kw.update(fetch_hw=feats[0].shape[2:], fetch_channels_last=True)
     vp = MODES[mode](lambda sv, **kw: OracleEngine(pm, up, grid, C, params, sv, **kw), pm, grid, rank, world, **kw)
     with torch.no_grad():
         if frames == 1:
@@ -144,9 +158,12 @@ def _worker(rank, world, port, out_dir, mode="gather", frames=1, weights=None, s
         else:  # FramePipeline: frame f uses the features scaled by (f + 1)
             pipe = parallel.FramePipeline(vp, B, "cpu")
             outs = [pipe.submit([(f + 1) * feats[v] for v in vp.my_views], None) for f in range(frames)]
-            outs = outs[1:] + [pipe.drain(None)]
+            lag = 2 if pipe.fetching else 1
+            assert all(o is None for o in outs[:lag]) and all(o is not None for o in outs[lag:])
+            outs = outs[lag:] + pipe.drain_all(None)
             assert pipe.drain(None) is None
-    torch.save({"outs": outs, "band": vp.band, "views": vp.my_views, "parts": getattr(vp, "my_parts", None)},
+    torch.save({"outs": outs, "band": vp.band, "views": vp.my_views, "parts": getattr(vp, "my_parts", None),
+                "recv": [list(map(list, ps)) for ps in getattr(vp, "recv_parts", [])]},
                os.path.join(out_dir, f"r{rank}.pt"))
     dist.destroy_process_group()
 
@@ -251,25 +268,61 @@ def test_partial_mode_balanced_assignment_matches_oracle(world, tmp_path):
     assert sorted(assigned) == [0, 1, 2]
 
 
-@pytest.mark.parametrize("world", [2, 4, 5])
-def test_partial_mode_channel_parts_match_oracle(world, tmp_path):
-    """The partial-sum mode with views cut into channel parts (``mp_model.balanced_parts``; world 4 and 5
-    > 3 views: every view split, a rank holding parts of several views), pipelined over 2 frames: every
-    rank's map equals the oracle's, and the parts cover every (view, channel) exactly once."""
+@pytest.mark.parametrize("world,k,backbone", [(2, 0, False), (4, 0, False), (5, 0, False), (2, 4, True),
+                                              (4, 2, True), (8, 4, True)])
+def test_partial_mode_channel_parts_match_oracle(world, k, backbone, tmp_path):
+    """The partial-sum mode with views cut into channel parts (``mp_model.balanced_parts``; world 4, 5 and 8
+    > 3 views: every view split, a rank holding parts of several views; ``k`` forces the split), pipelined
+    over 4 frames (the slice exchange's 3-buffer rotation wraps): every rank's map equals the oracle's, the
+    parts cover every (view, channel) exactly once, every rank was handed only the maps of the views it owns
+    (``view_owners``) and received exactly the parts it holds of views owned elsewhere.  ``backbone``: the
+    owners hold backbone-resolution maps, the slices cross in channels-last form and the warp upsamples."""
     weights = [0.9, 0.3, 0.6]
     port = _free_port()
-    mp.spawn(_worker, args=(world, port, str(tmp_path), "partial", 2, weights, True), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, port, str(tmp_path), "partial", 4, weights, True, k, backbone), nprocs=world,
+             join=True)
     pm, up, grid, C, B, feats, params = _case()
+    if backbone:
+        feats = [torch.nn.functional.interpolate(x, list(up), mode="bilinear") for x in _backbone_maps(up, C, B)]
     with torch.no_grad():
-        refs = [cpu_path.project_fuse([(f + 1) * x for x in feats], pm, grid, params) for f in range(2)]
+        refs = [cpu_path.project_fuse([(f + 1) * x for x in feats], pm, grid, params) for f in range(4)]
     covered = []
-    assign, cp = parallel.balanced_parts(weights, world, C, min_part=2)
+    assign, cp = parallel.balanced_parts(weights, world, C, min_part=2, k=k)
+    owner = parallel.view_owners([w + 0.05 for w in weights], world)
     if world > 3:
         assert cp < C  # the split is exercised
+    moved = 0
     for r in range(world):
         res = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
         assert [tuple(p) for p in res["parts"]] == [tuple(p) for p in assign[r]]
+        assert res["views"] == [v for v in range(3) if owner[v] == r]
+        recv = sorted(tuple(p) for ps in res["recv"] for p in ps)
+        assert recv == sorted(tuple(p) for p in assign[r] if owner[p[0]] != r)
+        moved += len(recv)
         covered += [(v, c) for v, c0 in res["parts"] for c in range(c0, c0 + cp)]
-        for f in range(2):
+        assert len(res["outs"]) == 4
+        for f in range(4):
             torch.testing.assert_close(res["outs"][f], refs[f], rtol=1e-5, atol=1e-6)
     assert sorted(covered) == [(v, c) for v in range(3) for c in range(C)]
+    if world > 3:
+        assert moved > 0  # the slice exchange is exercised
+
+
+def test_owner_affine_part_dealing():
+    """Round 6: whole views (k = 1) stay on their owner (no slice crosses), every view has one owner and
+    with P >= N no rank owns two views; parts go home when that costs little balance."""
+    from mvdet_amd import mp_model
+    w = [0.37, 0.73, 0.82, 0.6, 0.58, 0.9, 0.82]
+    for P in (2, 3, 4, 7, 8):
+        owner = mp_model.view_owners([x + 0.05 for x in w], P)
+        assign, cp = mp_model.balanced_parts(w, P, 512, k=1)
+        assert all(owner[v] == r for r, ps in enumerate(assign) for v, _ in ps)
+        if P >= 7:
+            assert len(set(owner)) == 7
+        for k in (2, 4, 8):
+            assign, cp = mp_model.balanced_parts(w, P, 512, k=k)
+            assert cp == 512 // k and sorted(p for ps in assign for p in ps) == sorted(
+                (v, j * cp) for v in range(7) for j in range(k))
+            home = sum(owner[v] == r for r, ps in enumerate(assign) for v, _ in ps)
+            plain = mp_model.balanced_parts(w, P, 512, k=k, affinity=0.0)[0]
+            assert home >= sum(owner[v] == r for r, ps in enumerate(plain) for v, _ in ps)

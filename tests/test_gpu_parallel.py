@@ -88,7 +88,8 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_dir, mode="gather", backend="gloo", frames=1, poison=False, split=False):
+def _worker(rank, world, port, out_dir, mode="gather", backend="gloo", frames=1, poison=False, split=False,
+            precision="bf16x3"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group(backend, rank=rank, world_size=world,
                             device_id=torch.device("cuda:0") if backend == "nccl" else None)
@@ -104,34 +105,40 @@ def _worker(rank, world, port, out_dir, mode="gather", backend="gloo", frames=1,
     cls = {"gather": ViewParallel, "partial": ViewPartialSum, "bands": ViewBands}[mode]
     # split: the partial-sum mode's channel parts (16-channel parts allowed: C = 64 here)
     skw = dict(view_weights=[0.9, 0.3, 0.6], channels=C, min_part=16) if split else {}
-    vp = cls(lambda sv, **kw: ProjectFuse(pm, up, grid, C, slot_views=sv, **kw), pm, grid, rank, world, **skw)
+    vp = cls(lambda sv, **kw: ProjectFuse(pm, up, grid, C, slot_views=sv, precision=precision, **kw), pm, grid, rank,
+             world, **skw)
     with torch.no_grad():
         if frames == 1:
             outs = [vp.step(vp.workspace(B, "cuda:0"), [frame_feats(0)[v].cuda() for v in vp.my_views], mc)]
         else:  # frame f: the features scaled by (f + 1); exchange on a side stream under NCCL
             pipe = FramePipeline(vp, B, "cuda:0")
             outs = [pipe.submit([frame_feats(f)[v].cuda() for v in vp.my_views], mc) for f in range(frames)]
-            outs = outs[1:] + [pipe.drain(mc)]
+            lag = 2 if pipe.fetching else 1  # the channel-part mode's slice exchange adds a pipeline stage
+            outs = outs[lag:] + pipe.drain_all(mc)
+            assert len(outs) == frames
         torch.cuda.synchronize()
     if poison:  # did the guard fire for the poisoned frame (buffer 0) and only for it (buffer 1)?
-        fired = ([int(fr.ws.nf2.item()) == fr.ws.nf2_tag for fr in pipe.frames] if mode == "partial" else
-                 [int(fr.gflag.item()) == fr.tag for fr in pipe.frames])
+        fired = ([int(fr.ws.nf2.item()) == fr.ws.nf2_tag for fr in pipe.frames[:frames]] if mode == "partial" else
+                 [int(fr.gflag.item()) == fr.tag for fr in pipe.frames[:frames]])
         torch.save(fired, os.path.join(out_dir, f"fired{rank}.pt"))
     torch.save([o.cpu() for o in outs], os.path.join(out_dir, f"r{rank}.pt"))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mode,split", [(2, "gather", False), (2, "partial", False), (4, "partial", False),
-                                              (2, "bands", False), (3, "bands", False), (2, "partial", True),
-                                              (4, "partial", True)])
-def test_rank_rehearsal_matches_single_process(world, mode, split, tmp_path):
+@pytest.mark.parametrize("world,mode,split,precision", [
+    (2, "gather", False, "bf16x3"), (2, "partial", False, "bf16x3"), (4, "partial", False, "bf16x3"),
+    (2, "bands", False, "bf16x3"), (3, "bands", False, "bf16x3"), (2, "partial", True, "bf16x3"),
+    (4, "partial", True, "bf16x3"), (2, "bands", False, "fp32"), (3, "partial", True, "fp32")])
+def test_rank_rehearsal_matches_single_process(world, mode, split, precision, tmp_path):
     """gather / partial-sum / band-exchange modes; world 4 (3 views) includes a rank without
     views and bands of 8 rows (edge-row halo exchange); bands at world 3: one view per rank,
     shifted windows at both grid edges; ``split``: the partial-sum mode on channel parts of the views
-    (``mp_model.balanced_parts``; world 4 > 3 views splits every view)."""
+    (``mp_model.balanced_parts``; world 4 > 3 views splits every view; each rank handed only its owned
+    views' features, the other parts through the slice exchange); ``precision="fp32"``: the fp32-MFMA
+    engines (the band exchange's windows as fp32, warped in the reference's order)."""
     from mvdet_amd import ProjectFuse
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), mode, "gloo", 1, False, split), nprocs=world,
-             join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), mode, "gloo", 1, False, split, precision),
+             nprocs=world, join=True)
     ds, pm, up, grid, C, B, feats, mc = _setup()
     mc = mc.to("cuda:0")
     with torch.no_grad():
@@ -146,14 +153,15 @@ def test_rank_rehearsal_matches_single_process(world, mode, split, tmp_path):
         torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("mode", ["bands", "gather", "partial"])
-def test_frame_pipeline_on_rccl_streams(mode, tmp_path):
+@pytest.mark.parametrize("mode,split", [("bands", False), ("gather", False), ("partial", False), ("partial", True)])
+def test_frame_pipeline_on_rccl_streams(mode, split, tmp_path):
     """FramePipeline with the real RCCL backend (a one-rank world on the box's GPU): the exchange
     runs on the side stream behind events, the fusion of the previous frame on the compute
     stream; 4 frames with different inputs come back in order and equal the single-process
-    maps (a missing wait or an early buffer reuse would mix frames)."""
+    maps (a missing wait or an early buffer reuse would mix frames).  ``split``: the channel-part
+    mode's three-stage pipeline (fetch on the side stream, 3 rotating frame buffers)."""
     from mvdet_amd import ProjectFuse
-    mp.spawn(_worker, args=(1, _free_port(), str(tmp_path), mode, "nccl", 4), nprocs=1, join=True)
+    mp.spawn(_worker, args=(1, _free_port(), str(tmp_path), mode, "nccl", 4, False, split), nprocs=1, join=True)
     ds, pm, up, grid, C, B, feats, mc = _setup()
     mc = mc.to("cuda:0")
     eng = ProjectFuse(pm, up, grid, C)
@@ -211,7 +219,7 @@ def _cfg_worker(rank, world, port, out_dir, cfg, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
-    from mvdet_amd import ProjectFuse, mp_model
+    from mvdet_amd import ProjectFuse, mp_model, synthetic
     from mvdet_amd.parallel import ViewBands, ViewParallel, ViewPartialSum
     spec, ds, pm, up, grid = _cfg_inputs(cfg)
     C, N = spec["C"], ds.num_cam
@@ -223,15 +231,30 @@ def _cfg_worker(rank, world, port, out_dir, cfg, mode):
                         if k.startswith("map_classifier.")})
     mc = mc.to("cuda:0")
     kw = {}
-    if mode == "partial":  # views cut into channel parts dealt by their conv1 work, as bench.py --gpus N does
+    half = cfg == 4
+    if mode == "partial":
+        # as bench.py --gpus N runs it: views cut into channel parts dealt by their conv1 work (the split the
+        # cost model predicts fastest), each rank holding only its OWNED views' backbone-resolution maps
+        # (channels-last; fp16 NCHW at cfg4), the other holders' slices crossing in the slice exchange
         kw["view_weights"] = [float(a.mean()) for a in mp_model.config_inputs(cfg)[4]]
         kw["channels"] = C
+        kw["parts_k"] = int(mp_model.predict_config(cfg, world)["partial"]["parts_k"])
+        kw.update(fetch_hw=tuple(u // 3 for u in up), fetch_dtype=torch.float16 if half else torch.float32,
+                  fetch_channels_last=not half)
     cls = {"gather": ViewParallel, "partial": ViewPartialSum, "bands": ViewBands}[mode]
     vp = cls(lambda sv, **k: ProjectFuse(pm, up, grid, C, slot_views=sv, **k), pm, grid, rank, world, **kw)
+    if mode == "partial":
+        feats = []
+        for v in vp.my_views:
+            x = synthetic.backbone_features(spec["B"], C, [u // 3 for u in up], seed=1000 * cfg + v, device="cuda:0")
+            feats.append(x.half() if half else x.contiguous(memory_format=torch.channels_last))
+    else:
+        feats = _cfg_feats(cfg, spec, up, vp.my_views)
     with torch.no_grad():
-        out = vp.step(vp.workspace(spec["B"], "cuda:0"), _cfg_feats(cfg, spec, up, vp.my_views), mc)
+        out = vp.step(vp.workspace(spec["B"], "cuda:0"), feats, mc)
         torch.cuda.synchronize()
-    torch.save({"map": out.cpu(), "views": vp.my_views, "band": vp.band}, os.path.join(out_dir, f"r{rank}.pt"))
+    torch.save({"map": out.cpu(), "views": vp.my_views, "band": vp.band,
+                "owner": getattr(vp, "owner", None)}, os.path.join(out_dir, f"r{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -239,7 +262,8 @@ def _cfg_worker(rank, world, port, out_dir, cfg, mode):
 @pytest.mark.parametrize("cfg,world", [(3, 7), (5, 8), (4, 6), (2, 8)])
 def test_chosen_mode_at_baseline_size_vs_oracle(cfg, world, tmp_path):
     """The mode ``mp_model.choose_mode`` picks for the config at ``world`` ranks (cfg3 at P = 7: partial;
-    cfg5 at P = 8: bands; cfg4 at P = 6; cfg2 at P = 8), rehearsed with gloo ranks sharing the box's GPU at
+    cfg5 at P = 8: bands; cfg4 at P = 6: partial; cfg2 at P = 8: partial — the partial-sum mode from each rank's
+    owned backbone maps through the slice exchange, round 6), rehearsed with gloo ranks sharing the box's GPU at
     the BASELINE size: every rank's assembled map vs the oracle (warp of every view whole, convs on row
     bands +- 7) on the top and bottom edge bands and on bands across rank boundaries, at 5e-5 normwise."""
     from mvdet_amd import mp_model
@@ -248,7 +272,14 @@ def test_chosen_mode_at_baseline_size_vs_oracle(cfg, world, tmp_path):
     mp.spawn(_cfg_worker, args=(world, _free_port(), str(tmp_path), cfg, mode), nprocs=world, join=True)
     spec, ds, pm, up, grid = _cfg_inputs(cfg)
     H = grid[0]
-    feats = _cfg_feats(cfg, spec, up, range(ds.num_cam))
+    if mode == "partial" and cfg == 4:  # the ranks' inputs: fp16 backbone maps, upsampled inside the warp
+        from mvdet_amd import synthetic
+        feats = [torch.nn.functional.interpolate(
+            synthetic.backbone_features(spec["B"], spec["C"], [u // 3 for u in up], seed=1000 * cfg + v,
+                                        device="cuda:0").half().float(), list(up), mode="bilinear")
+            for v in range(ds.num_cam)]
+    else:
+        feats = _cfg_feats(cfg, spec, up, range(ds.num_cam))
     warped = cpu_path.warp_views([f.float().cpu() for f in feats], [M.numpy() for M in pm], grid)
     del feats
     tp = {k: torch.from_numpy(v) for k, v in fixtures.head_params(ds.num_cam, seed=cfg, C=spec["C"]).items()}
@@ -259,6 +290,8 @@ def test_chosen_mode_at_baseline_size_vs_oracle(cfg, world, tmp_path):
     for r in range(world):
         res = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
         assert res["map"].shape == (spec["B"], 1) + grid
+        if res["owner"] is not None:  # the rank was handed its owned views' maps only (the slice exchange)
+            assert res["views"] == [v for v in range(ds.num_cam) if res["owner"][v] == r]
         for (r0, r1), ref in zip(bands, refs):
             assert_parity_t(res["map"][:, :, r0:r1], ref, f"cfg{cfg} {mode} x{world} rank {r} map rows {r0}:{r1}",
                             normwise_tol=5e-5)

@@ -18,9 +18,8 @@ def main():
     print("| cfg | P | bands ms (x) | partial ms (x) | gather ms (x) | chosen |")
     print("|---|---|---|---|---|---|")
     for cfg in sorted(mp_model.SINGLE_GPU_MS):
-        N, C, grid, B, acts = mp_model.config_inputs(cfg)
         for P in ((2, 4, 6, 7, 8) if cfg == 4 else (2, 4, 7, 8)):
-            pr = mp_model.predict(N, C, grid, B, P, mp_model.SINGLE_GPU_MS[cfg], acts)
+            pr = mp_model.predict_config(cfg, P)
             cells = [f"{pr[m]['frame']:.2f} ({pr[m]['speedup_vs_1gpu']:.1f}x)" for m in ("bands", "partial", "gather")]
             print(f"| {cfg} | {P} | " + " | ".join(cells) + f" | {mp_model.choose_mode(cfg, P)} |")
 

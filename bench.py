@@ -61,11 +61,13 @@ def head_params(num_cam, seed, C):
     return out
 
 
-def cpu_baseline(ds, B, C, pm, params, frames: int, config: int = 2, warmups: int = 2, single_frames: int = 3):
+def cpu_baseline(ds, B, C, pm, params, frames: int, config: int = 2, warmups: int = 2, single_frames: int = 3,
+                 single_warmups: int = 1):
     """The oracle (reference CPU path restated over torch-CPU ops) on the host cores:
     ``warmups`` untimed frames, then the median of ``frames`` timed ones (2 warm-ups,
     >= 5 timed, median); the reference's own one-thread setting (main.py:3) as the median of
-    ``single_frames`` after one warm-up (0 = skipped)."""
+    ``single_frames`` after ``single_warmups`` warm-ups (0 = skipped; the large configs take one frame
+    right after the multi-thread ones, ~60-70 s of one core each)."""
     from mvdet_amd import synthetic
     from oracle import cpu_path
     threads = len(os.sched_getaffinity(0))
@@ -94,12 +96,14 @@ def cpu_baseline(ds, B, C, pm, params, frames: int, config: int = 2, warmups: in
         if single_frames:
             # the reference's own setting (main.py:3, OMP_NUM_THREADS=1)
             torch.set_num_threads(1)
-            frame()
+            for _ in range(single_warmups):
+                frame()
             t1 = [frame() for _ in range(single_frames)]
             torch.set_num_threads(threads)
             single = dict(value=round(B / float(np.median(t1)), 4), unit="frames/s", cores=1,
-                          sample=f"median of {single_frames} frame(s) after 1 warm-up with torch.set_num_threads(1) "
-                                 "(main.py:3 OMP_NUM_THREADS=1)")
+                          sample=f"median of {single_frames} frame(s) after {single_warmups} warm-up(s) with "
+                                 "torch.set_num_threads(1) (main.py:3 OMP_NUM_THREADS=1)"
+                                 + ("" if single_warmups else " (right after the multi-thread frames)"))
     dt = float(np.median(times))
     return dict(value=round(B / dt, 4), unit="frames/s", cores=threads, kind="port", single_thread=single,
                 sample=f"median of {frames} frame(s) (B={B}) of the bench workload after {warmups} warm-up(s) "
@@ -203,11 +207,16 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
     # 2 coord channels are folded into a per-weight-version init term)
     conv1_flop = 2.0 * B * ho * wo * 9 * (N * C) * 512
     conv2_flop = 2.0 * B * ho * wo * 9 * 512 * 512
-    s = 2 if half else 4  # bytes per source element (fp16 features at cfg4)
+    s = 2 if half else 4  # bytes per element (fp16 features at cfg4)
     tv = [touched_footprint(M.numpy(), up, (ho, wo)) for M in pm]
-    warp_bytes = sum(B * C * (s * t + eng.slab_dtype.itemsize * ho * wo) for t in tv)
-    if eng.wino_warp:  # the warp writes conv1's row transform: 5 split-bf16 rows per 3-row tile
-        warp_bytes = sum(B * C * (s * t + 4 * 5 * 4 * -(-ho // 12) * wo) for t in tv)
+    # warp bytes = sum_v s * B * C * (T_v + Ho * Wo) — the touched source pixels and the warped
+    # output at the source's element size, whatever the kernel physically writes (the
+    # dense 5/3-size T is what the fused warp + B^T may write at most, not the algorithm's bytes)
+    warp_bytes = sum(s * B * C * (t + ho * wo) for t in tv)
+    # what the kernel's output buffer would take if dense: the slab, or with the fused B^T conv1's row transform
+    # T (5 split-bf16 rows per 3-row tile, 4 B per element; it writes only the frustum mask's tiles)
+    warp_out_dense = (N * B * C * 4 * 5 * 4 * -(-ho // 12) * wo if eng.wino_warp
+                      else N * B * C * eng.slab_dtype.itemsize * ho * wo)
     # conv3's stage: with conv2 -> conv3 fused (bf16x3) it reads the [B, 8 sets, 9 taps, rows, Wo] fp32
     # partials conv2's epilogue wrote (y2 never reaches HBM) and writes the map; on a stored y2 (fp32
     # path) it reads y2's 512 channels
@@ -297,9 +306,11 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
         },
         "stage_roofline": {
             "warp": {"bound": "hbm", "algorithmic_bytes": warp_bytes,
+                     "algorithmic_basis": "SURVEY §8(d): sum_v s*B*C*(T_v + Ho*Wo), T_v = touched source pixels",
                      # with the Winograd conv1 the warp writes the row transform T (warp_wino_kernel:
                      # 5/3 of the slab's rows, the separate transform gone), so its time includes B^T
                      "output": "row-Winograd T (warp + B^T fused)" if eng.wino_warp else "split-bf16 slab",
+                     "output_dense_bytes": warp_out_dense,
                      "achieved_GBs": round(warp_bytes / (t_warp * 1e-3) / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
                      # PMC bytes (read at 128-B granules: NCHW rows are gathered, not streamed)
                      "traffic": warp_traffic,
@@ -454,13 +465,31 @@ def run_train_step(config: int, precision: str, steps: int, warmup: int, with_to
             out["stages_ms"] = st
         return out
 
-    def native_step():
+    # trainer.py:48: optimizer.step() after every backward — an in-place update of every head parameter, which
+    # bumps the weights' _version, so the next forward re-packs conv1's / conv2's (Winograd) weights and the
+    # backward its data-gradient packs, inside the timed step.  SGD with momentum as the
+    # reference trains (main.py:69,146-147: momentum 0.5, weight decay 5e-4); a small lr keeps the synthetic weights in range.
+    opt = torch.optim.SGD(mc.parameters(), lr=1e-4, momentum=0.5, weight_decay=5e-4)
+
+    def optimizer_step():
+        if autograd._stage_hook is not None:
+            autograd._stage_hook("optimizer")
+        opt.step()
+
+    def native_step(update=True):
         for f in feats:
             f.grad = None
         mc.zero_grad(set_to_none=True)
         autograd.project_fuse(eng, feats, mc).backward(gmap)
+        if update:
+            optimizer_step()
 
     res["native"] = run(native_step, steps, warmup, hook_stages=True)
+    res["native"]["optimizer"] = "SGD(lr=1e-4, momentum=0.5, weight_decay=5e-4).step() per step (weights re-packed every step)"
+    # the same step without the update (packs reused from the cache): the repacking's cost is the difference
+    nu = run(lambda: native_step(update=False), steps, warmup, hook_stages=True)
+    res["native_no_update"] = nu
+    res["weight_update_cost_ms"] = round(res["native"]["ms_per_step"] - nu["ms_per_step"], 3)
     if with_torch:
         ms = [eng.m_norm_cpu[v].to(dev) for v in range(N)]
         cmap = torch.from_numpy(np.stack(np.meshgrid(np.arange(wo) / (wo - 1) * 2 - 1,
@@ -472,6 +501,7 @@ def run_train_step(config: int, precision: str, steps: int, warmup: int, with_to
             mc.zero_grad(set_to_none=True)
             world = [torch_warp(f, m, ho, wo) for f, m in zip(feats, ms)]
             mc(torch.cat(world + [cmap.repeat(B, 1, 1, 1)], 1)).backward(gmap)
+            opt.step()
 
         res["torch_gpu"] = run(torch_step, max(2, steps // 4), 1)
         res["speedup_vs_torch_gpu"] = round(res["native"]["value"] / res["torch_gpu"]["value"], 2)
@@ -487,6 +517,7 @@ def run_train_step(config: int, precision: str, steps: int, warmup: int, with_to
             f.grad = None
         mc.zero_grad(set_to_none=True)
         autograd.project_fuse_backbone(eng, bfeats, mc).backward(gmap)
+        optimizer_step()
 
     a4 = {"native": run(native_a4, steps, warmup, hook_stages=True)}
     if with_torch:
@@ -497,6 +528,7 @@ def run_train_step(config: int, precision: str, steps: int, warmup: int, with_to
             world = [torch_warp(torch.nn.functional.interpolate(f, up, mode="bilinear"), m, ho, wo)
                      for f, m in zip(bfeats, ms)]
             mc(torch.cat(world + [cmap.repeat(B, 1, 1, 1)], 1)).backward(gmap)
+            opt.step()
 
         a4["torch_gpu"] = run(torch_a4, max(2, steps // 4), 1)
         a4["speedup_vs_torch_gpu"] = round(a4["native"]["value"] / a4["torch_gpu"]["value"], 2)
@@ -613,15 +645,15 @@ def main():
         # the size the north star quotes its >= 5x at 1 GPU on (cfg3: 7 views, 480 x 1440 grid): the same
         # path, its roofline, and a CPU baseline on BASELINE.md:26's sample (2 warm-ups + the median of 5
         # frames, ~18 s of CPU work per frame at 16 threads)
-        subs.append((args.north_star_cfg, dict(frames=5, warmups=2, single_frames=0)))
+        subs.append((args.north_star_cfg, dict(frames=5, warmups=2, single_frames=1, single_warmups=0)))
     if args.roofline_cfg and args.roofline_cfg not in (args.config, args.north_star_cfg):
         # BASELINE's "rocprof roofline run" config (8 views at 4K): 1 warm-up + the median of 3 frames
         # (~16 s of CPU work per frame)
-        subs.append((args.roofline_cfg, dict(frames=3, warmups=1, single_frames=0)))
+        subs.append((args.roofline_cfg, dict(frames=3, warmups=1, single_frames=1, single_warmups=0)))
     if args.batch_cfg and args.batch_cfg not in (args.config, args.north_star_cfg, args.roofline_cfg):
         # BASELINE configs[3]: MultiviewX 6 views, B = 8, fp16 features (C = 512, the reference's ResNet-18
         # width); its CPU baseline on B = 1 frames (1 warm-up + the median of 3), frames/s = 1 / median
-        subs.append((args.batch_cfg, dict(frames=3, warmups=1, single_frames=0)))
+        subs.append((args.batch_cfg, dict(frames=3, warmups=1, single_frames=1, single_warmups=0)))
     for cfg, plan in subs:
         sub = run_single(args, args.precision, max(5, args.steps // 4), 2,
                          with_cpu=plan is not None and not args.no_cpu_baseline, config=cfg, cpu_plan=plan)

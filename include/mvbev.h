@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 12100: MVBEV_LAYOUT_SPLIT_BF16_PIX (conv data gradients' output, the warp adjoint's input); 12000: conv1's and conv2's weight gradients from the forward's row-Winograd transforms (mvbev_wino_dy_rows_f32, mvbev_conv3x3_wgrad_wino_bf16x3); 11900: row windows (mvbev_warp_views_split_bf16_rows with the non-finite report, mvbev_warp_views_exact_rows with fp16 sources), mvbev_conv3x3_f32_ex (row-band output), mvbev_bias_relu_nonfinite_f32, mvbev_zero_gated — the non-finite guard of the multi-GPU modes and the banded exact path; 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 12200: the training forward's non-finite guard (mvbev_store_gated_f32, mvbev_pack_conv3x3_weight_f32_gated, mvbev_wino_rows_split_bf16_gated); 12100: MVBEV_LAYOUT_SPLIT_BF16_PIX (conv data gradients' output, the warp adjoint's input); 12000: conv1's and conv2's weight gradients from the forward's row-Winograd transforms (mvbev_wino_dy_rows_f32, mvbev_conv3x3_wgrad_wino_bf16x3); 11900: row windows (mvbev_warp_views_split_bf16_rows with the non-finite report, mvbev_warp_views_exact_rows with fp16 sources), mvbev_conv3x3_f32_ex (row-band output), mvbev_bias_relu_nonfinite_f32, mvbev_zero_gated — the non-finite guard of the multi-GPU modes and the banded exact path; 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -126,6 +126,16 @@ int mvbev_warp_views_split_bf16_rows(const mvbev_warp_view* views, const int32_t
 /* Gated zero fill: bytes (a multiple of 16, 16-B aligned dst) of zeros when *gate == gate_tag, else no
  * write (ABI 11900: re-zeroes the band exchange's send chunks after a frame whose exact path wrote them). */
 int mvbev_zero_gated(void* dst, int64_t bytes, const int32_t* gate, int32_t gate_tag, void* stream);
+/* Gated store (ABI 12200): fp32 src [B][C][H][W] (element strides, src_strides[3] == 1) into dst when
+ * *gate == gate_tag, else no write.  dst_layout MVBEV_LAYOUT_F32: fp32 at element strides (dst_strides[3]
+ * == 1); MVBEV_LAYOUT_SPLIT_BF16: the split-bf16 blocked layout, dst_strides in 32-byte units {batch,
+ * channel group, row, col (1)}, a non-finite value stored as hi = value, lo = 0 (hi + lo keeps it; the
+ * fast path's split gives lo = NaN).  The training forward's non-finite guard stores its exact-path
+ * activations (conv1's input, y1, y2) where the native backward reads them
+ * (persp_trans_detector.py:65-81 under trainer.py:38-47). */
+int mvbev_store_gated_f32(const float* src, const int64_t src_strides[4], void* dst, const int64_t dst_strides[4],
+                          int64_t B, int64_t C, int64_t H, int64_t W, int dst_layout, const int32_t* gate,
+                          int32_t gate_tag, void* stream);
 /* Fused bilinear upsample + warp.  views[i].src is the
  * backbone-resolution map [B][C][h][w] that persp_trans_detector.py:65 upsamples with
  * F.interpolate(size=(H, W), mode='bilinear', align_corners=False) before the warp at :69;
@@ -181,6 +191,12 @@ size_t mvbev_conv3x3_packed_floats(int64_t Cout, int64_t K);
 int mvbev_pack_conv3x3_weight_f32(const float* w, int64_t Cout, int64_t Cin_w,
                                   const int32_t* chan_map, int64_t K, float* w_packed,
                                   void* stream);
+/* The same pack, run only when *gate == gate_tag (ABI 12200): the training forward's non-finite guard
+ * re-packs the exact path's fp32 weights every step (the optimizer changes them) at the cost of a launch
+ * that exits at once when the features are finite. */
+int mvbev_pack_conv3x3_weight_f32_gated(const float* w, int64_t Cout, int64_t Cin_w, const int32_t* chan_map,
+                                        int64_t K, float* w_packed, const int32_t* gate, int32_t gate_tag,
+                                        void* stream);
 
 /* Geometry of one conv launch (all sizes in elements). */
 typedef struct mvbev_conv_desc {
@@ -384,6 +400,11 @@ int mvbev_conv3x3_wino_bf16x3(const void* t, const mvbev_conv_desc* desc, const 
  * dilation 2), conv3's partial sums from the epilogue (_cout1_partials, ABI 11500). */
 int mvbev_wino_rows_split_bf16_dil(const void* x, const mvbev_conv_desc* desc, int dilation,
                                    const uint32_t* group_mask, void* t, size_t t_bytes, void* stream);
+/* The same transform, run only when *gate == gate_tag (gate not NULL; ABI 12200): the training guard's
+ * T / T2 of its exact-path conv1 input / y1 for the native weight gradients. */
+int mvbev_wino_rows_split_bf16_gated(const void* x, const mvbev_conv_desc* desc, int dilation,
+                                     const uint32_t* group_mask, void* t, size_t t_bytes, const int32_t* gate,
+                                     int32_t gate_tag, void* stream);
 int mvbev_conv3x3_wino_bf16x3_dil(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,
                                   int64_t Cout, int dilation, int relu, void* y, int y_layout, void* stream);
 int mvbev_conv3x3_wino_bf16x3_cout1_partials(const void* t, const mvbev_conv_desc* desc, const void* w_packed,

@@ -85,6 +85,9 @@ EXPORTS = (
     "mvbev_wino_dy_rows_f32",
     "mvbev_conv3x3_wgrad_wino_workspace_bytes",
     "mvbev_conv3x3_wgrad_wino_bf16x3",
+    "mvbev_store_gated_f32",
+    "mvbev_pack_conv3x3_weight_f32_gated",
+    "mvbev_wino_rows_split_bf16_gated",
 )
 BEV_SRC_F32, BEV_SRC_F16, BEV_SRC_BACKBONE_F32 = 0, 1, 2  # MVBEV_BEV_SRC_*
 BEV_SRC_CHANNELS_LAST = 16  # MVBEV_BEV_SRC_CHANNELS_LAST (flag)
@@ -243,6 +246,14 @@ def _declare(lib):
                                                   ctypes.c_int32, _p]
     lib.mvbev_zero_gated.restype = ctypes.c_int
     lib.mvbev_zero_gated.argtypes = [_p, _i64, _p, ctypes.c_int32, _p]
+    lib.mvbev_store_gated_f32.restype = ctypes.c_int
+    lib.mvbev_store_gated_f32.argtypes = [_p, _i64x4, _p, _i64x4, _i64, _i64, _i64, _i64, ctypes.c_int, _p,
+                                          ctypes.c_int32, _p]
+    lib.mvbev_pack_conv3x3_weight_f32_gated.restype = ctypes.c_int
+    lib.mvbev_pack_conv3x3_weight_f32_gated.argtypes = [_p, _i64, _i64, _p, _i64, _p, _p, ctypes.c_int32, _p]
+    lib.mvbev_wino_rows_split_bf16_gated.restype = ctypes.c_int
+    lib.mvbev_wino_rows_split_bf16_gated.argtypes = [_p, ctypes.POINTER(ConvDesc), ctypes.c_int, _p, _p,
+                                                     ctypes.c_size_t, _p, ctypes.c_int32, _p]
     lib.mvbev_nchw_to_nhwc_f32.restype = ctypes.c_int
     lib.mvbev_nchw_to_nhwc_f32.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _p]
     lib.mvbev_warp_tile_mask.restype = ctypes.c_int

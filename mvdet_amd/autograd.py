@@ -213,14 +213,21 @@ def _dgrad1_wino(engine: ProjectFuse, st, dy1s: torch.Tensor, w1: torch.Tensor, 
     ops.conv3x3_wino_dgrad(st.t1d, d, st.pack1t.get(w1), nc, dslab, out_mask=cm, cot_per_group=C // ops.BN)
 
 
-def _wgrad1_wino_fits(engine: ProjectFuse, B: int) -> bool:
-    """conv1's Winograd weight gradient takes this geometry (``mvbev_conv3x3_wgrad_wino_bf16x3``'s limits:
-    W % 8, 128-channel slots, B < 128, 32-bit offsets), so the forward may skip the slab."""
-    H, W = engine.grid_hw
-    K, r3, r5 = engine.S * engine.Cs, -(-H // 3), 20 * (-(-H // 12))
-    return (W % 8 == 0 and engine.Cs % 128 == 0 and engine.mid % 128 == 0 and B < 128 and r3 <= 4096
-            and -(-W // 32) <= 4096 and (K // 8) * 2 * r5 * W < 2 ** 31 - 1 and engine.mid * r3 * W < 2 ** 31 - 1
+def _wgrad_wino_fits(K: int, cout: int, H: int, W: int, B: int, dilation: int) -> bool:
+    """``mvbev_conv3x3_wgrad_wino_bf16x3``'s shape limits (backward.hip): W % 8, whole 128-channel output
+    tiles, B < 128, at most 4096 three-row tiles and 32-px segments, 32-bit chunk-invariant offsets."""
+    r3 = -(-H // 3) if dilation == 1 else 4 * (-(-H // 12))
+    r5 = 20 * (-(-H // 12))
+    return (W % 8 == 0 and cout % 128 == 0 and K % 8 == 0 and B < 128 and r3 <= 4096 and -(-W // 32) <= 4096
+            and (K // 8) * 2 * r5 * W < 2 ** 31 - 1 and cout * r3 * W < 2 ** 31 - 1
             and _native.load().mvbev_version() >= 12000)
+
+
+def _wgrad1_wino_fits(engine: ProjectFuse, B: int) -> bool:
+    """conv1's Winograd weight gradient takes this geometry (128-channel slots and the native limits,
+    ``_wgrad_wino_fits``), so the forward may skip the slab."""
+    H, W = engine.grid_hw
+    return engine.Cs % 128 == 0 and _wgrad_wino_fits(engine.S * engine.Cs, engine.mid, H, W, B, 1)
 
 
 def _wgrad1_wino_applies(engine: ProjectFuse, ws: Workspace, dy1: torch.Tensor) -> bool:
@@ -245,7 +252,7 @@ def _wgrad1_wino(engine: ProjectFuse, st, ws: Workspace, d1, dy1: torch.Tensor, 
         if key not in st.lists_wino:
             st.lists_wino[key] = ops.wgrad_wino_chunk_lists(m, engine.S, B, H, W)
         lists = st.lists_wino[key]
-    ops.conv3x3_wgrad_wino(ws.wino_t, d1, ops.wino_dy_rows(dy1), dw1.shape[1], chan_map=engine.pack1._map_dev,
+    ops.conv3x3_wgrad_wino(ws.wino_t, d1, ops.wino_dy_rows(dy1), dw1.shape[1], chan_map=engine.pack1.map_dev(dev),
                            dw=dw1, workspace=_wgrad_wino_ws(st, d1, mid, 1, dev), chunk_lists=lists)
 
 
@@ -338,7 +345,7 @@ class ProjectFuseFunction(torch.autograd.Function):
         if db2 is not None:
             ops.conv3x3_bias_coord_grad(dy2, 2, db=db2)
         d_y1 = ops.conv_desc(B, mid, H, W, group=mid, group_stride=0, batch_stride=mid * H * W)
-        if ws.t2_valid and W % 8 == 0 and mid % 128 == 0 and B < 128 and H <= 12 * 1024:  # from conv2's own T
+        if ws.t2_valid and _wgrad_wino_fits(mid, mid, H, W, B, 2):  # from conv2's own T (the native limits)
             dw2 = ops.conv3x3_wgrad_wino(ws.wino_t2, d_y1, ops.wino_dy_rows(dy2, dilation=2), mid, dilation=2,
                                          workspace=_wgrad_wino_ws(st, d_y1, mid, 2, dev))
         else:  # (the direct form reads the fp32 dy2: at its size the row split costs what it saves)
@@ -363,7 +370,7 @@ class ProjectFuseFunction(torch.autograd.Function):
         dw1 = torch.zeros_like(w1)
         db1 = torch.empty(mid, dtype=torch.float32, device=dev) if b1 is not None else None
         ops.conv3x3_bias_coord_grad(dy1, 1, db=db1, dw=dw1, coord_ch=nc)
-        engine.pack1.get(w1)  # materialises the device channel map
+        chan_map = engine.pack1.map_dev(dev)  # (round 6: no re-pack of the direct conv1 weights it does not use)
         d1 = ops.conv_desc(B, engine.S * engine.Cs, H, W, group=engine.Cs, group_stride=B * engine.Cs * H * W,
                            batch_stride=engine.Cs * H * W)
         if _wgrad1_wino_applies(engine, ws, dy1):
@@ -371,7 +378,7 @@ class ProjectFuseFunction(torch.autograd.Function):
         elif ws.t_from_warp:
             raise RuntimeError("conv1's weight gradient needs the slab, but the fused warp wrote only T")
         else:
-            ops.conv3x3_wgrad(ws.slab, d1, dy1, 1, w1.shape[1], chan_map=engine.pack1._map_dev, dw=dw1,
+            ops.conv3x3_wgrad(ws.slab, d1, dy1, 1, w1.shape[1], chan_map=chan_map, dw=dw1,
                               workspace=_wgrad_ws(st, d1, mid, dev), chunk_lists=_wgrad_lists(engine, st, dev, B),
                               dy_rows=_dy_rows(dy1, ws.slab.dtype == torch.bfloat16))
         grads = [None] * n

@@ -49,7 +49,8 @@ constexpr int TW = 32;             // output cols per workgroup (= MFMA N)
 // map = identity (chan_map == nullptr) or chan_map[k]; unmapped (-1) / k >= K -> 0.
 __global__ void pack_conv3x3_kernel(const float* __restrict__ w, float* __restrict__ wp, int Cout,
                                     int Cin_w, const int32_t* __restrict__ chan_map, int K,
-                                    int K_pad) {
+                                    int K_pad, const int32_t* gate, int32_t gate_tag) {
+  if (gate && *gate != gate_tag) return;  // (ABI 12200) the training guard's per-step pack: gated
   const int64_t total = (int64_t)K_pad * 9 * Cout;
   const int n_cot = Cout / BN;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
@@ -475,9 +476,19 @@ size_t mvbev_conv3x3_packed_floats(int64_t Cout, int64_t K) {
   return (size_t)mvbev::round_up(K, mvbev::KC) * 9 * (size_t)Cout;
 }
 
+int mvbev_pack_conv3x3_weight_f32_gated(const float* w, int64_t Cout, int64_t Cin_w, const int32_t* chan_map,
+                                        int64_t K, float* w_packed, const int32_t* gate, int32_t gate_tag,
+                                        void* stream);
+
 int mvbev_pack_conv3x3_weight_f32(const float* w, int64_t Cout, int64_t Cin_w,
                                   const int32_t* chan_map, int64_t K, float* w_packed,
                                   void* stream) {
+  return mvbev_pack_conv3x3_weight_f32_gated(w, Cout, Cin_w, chan_map, K, w_packed, nullptr, 0, stream);
+}
+
+int mvbev_pack_conv3x3_weight_f32_gated(const float* w, int64_t Cout, int64_t Cin_w, const int32_t* chan_map,
+                                        int64_t K, float* w_packed, const int32_t* gate, int32_t gate_tag,
+                                        void* stream) {
   if (!w || !w_packed) return MVBEV_ERR_NULL;
   if (Cout <= 0 || Cin_w <= 0 || K <= 0) return MVBEV_ERR_RANK;
   if (Cout % mvbev::BN != 0) return MVBEV_ERR_SHAPE;
@@ -487,7 +498,7 @@ int mvbev_pack_conv3x3_weight_f32(const float* w, int64_t Cout, int64_t Cin_w,
   const int blocks = (int)std::min<int64_t>(mvbev::ceil_div(total, 256), 8192);
   hipLaunchKernelGGL(mvbev::pack_conv3x3_kernel, dim3(blocks), dim3(256), 0,
                      mvbev::as_stream(stream), w, w_packed, (int)Cout, (int)Cin_w, chan_map,
-                     (int)K, (int)k_pad);
+                     (int)K, (int)k_pad, gate, gate_tag);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }

@@ -1377,6 +1377,8 @@ struct WinoRowsArgs {
   int64_t group_stride, batch_stride;  // elements, as mvbev_conv_desc
   int K, group, H, W, in_row0, in_rows, out_row0, tiles_x, tiles_y, dil;
   const uint32_t* gmask;
+  const int32_t* gate;  // (ABI 12200) NULL, or run only when *gate == gate_tag (the training guard's exact T)
+  int32_t gate_tag;
 };
 
 __device__ inline void bf16x8_to_f32(const u32x4 v, float (&f)[8]) {
@@ -1398,6 +1400,7 @@ __device__ inline void bf16x8_to_f32(const u32x4 v, float (&f)[8]) {
 // in T (zero-filled, never written) and in the true transform (the mask covers the halo).
 __global__ __launch_bounds__(256) void wino_rows_kernel(const WinoRowsArgs a) {
   constexpr int KB = 8;  // 8-channel blocks per workgroup: 4 x 32 x 8 items, 4 per thread
+  if (a.gate && *a.gate != a.gate_tag) return;
   const int pp = blockIdx.x, b = blockIdx.z;
   const int nbg = (a.group / SB + KB - 1) / KB;
   const int g = blockIdx.y / nbg, kb0 = (blockIdx.y - g * nbg) * KB;
@@ -1748,7 +1751,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
 // MFMA pipe, which the second wave of this kernel keeps fed.  Removed)
 
 static int wino_rows_launch(const void* x, const mvbev_conv_desc* d, int dil, const uint32_t* group_mask, void* t,
-                            size_t t_bytes, void* stream) {
+                            size_t t_bytes, void* stream, const int32_t* gate = nullptr, int32_t gate_tag = 0) {
   if (!x || !d || !t) return MVBEV_ERR_NULL;
   if (dil != 1 && dil != 2) return MVBEV_ERR_DILATION;
   if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || d->in_rows <= 0 || d->out_rows <= 0 || d->group <= 0)
@@ -1770,6 +1773,7 @@ static int wino_rows_launch(const void* x, const mvbev_conv_desc* d, int dil, co
   a.tiles_x = (int)tiles_x, a.tiles_y = (int)tiles_y;
   a.dil = dil;
   a.gmask = group_mask;
+  a.gate = gate, a.gate_tag = gate_tag;
   const int64_t nbg = ceil_div(d->group / SB, 8);  // wino_rows_kernel's KB
   if ((d->K / d->group) * nbg > 65535) return MVBEV_ERR_SHAPE;
   hipLaunchKernelGGL(wino_rows_kernel, dim3((unsigned)(tiles_x * tiles_y), (unsigned)((d->K / d->group) * nbg), (unsigned)d->B),
@@ -2070,6 +2074,13 @@ int mvbev_wino_rows_split_bf16(const void* x, const mvbev_conv_desc* desc, const
 int mvbev_wino_rows_split_bf16_dil(const void* x, const mvbev_conv_desc* desc, int dilation,
                                    const uint32_t* group_mask, void* t, size_t t_bytes, void* stream) {
   return mvbev::b3::wino_rows_launch(x, desc, dilation, group_mask, t, t_bytes, stream);
+}
+
+int mvbev_wino_rows_split_bf16_gated(const void* x, const mvbev_conv_desc* desc, int dilation,
+                                     const uint32_t* group_mask, void* t, size_t t_bytes, const int32_t* gate,
+                                     int32_t gate_tag, void* stream) {
+  if (!gate) return MVBEV_ERR_NULL;
+  return mvbev::b3::wino_rows_launch(x, desc, dilation, group_mask, t, t_bytes, stream, gate, gate_tag);
 }
 
 int mvbev_conv3x3_wino_bf16x3(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,

@@ -613,9 +613,77 @@ __global__ __launch_bounds__(256) void zero_gated_kernel(u32x4_t* dst, int64_t n
     dst[i] = u32x4_t{0u, 0u, 0u, 0u};
 }
 
+// a gated store (ABI 12200): fp32 src [B][C][H][W] (element strides) into dst as fp32 (element strides) or
+// as the split-bf16 blocked layout (32-B units: batch, channel group, row; 8 channels of a pixel per entry),
+// when *gate == tag — the training forward's exact path puts its activations where the native backward
+// reads them.  The split keeps a non-finite value in hi with lo = 0 (hi + lo is the value: inf stays inf,
+// so the backward's ReLU mask hi + lo > 0 is torch's), unlike the fast path's split (lo = v - hi).
+struct StoreArgs {
+  const float* src;
+  int64_t sB, sC, sH;
+  void* dst;
+  int64_t dB, dC, dH;
+  int B, C, H, W, split;
+  const int32_t* gate;
+  int32_t gate_tag;
+};
+__global__ __launch_bounds__(256) void store_gated_kernel(const StoreArgs a) {
+  if (*a.gate != a.gate_tag) return;
+  const int G = a.split ? (a.C + 7) / 8 : a.C;
+  const int64_t n = (int64_t)a.B * G * a.H * a.W;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(i % a.W);
+    int64_t r = i / a.W;
+    const int y = (int)(r % a.H);
+    r /= a.H;
+    const int g = (int)(r % G);
+    const int b = (int)(r / G);
+    const float* s = a.src + (int64_t)b * a.sB + (int64_t)y * a.sH + x;
+    if (!a.split) {
+      static_cast<float*>(a.dst)[(int64_t)b * a.dB + (int64_t)g * a.dC + (int64_t)y * a.dH + x] = s[(int64_t)g * a.sC];
+      continue;
+    }
+    bf16x8_t hi, lo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = 8 * g + j;
+      const float v = c < a.C ? s[(int64_t)c * a.sC] : 0.f;
+      const __bf16 h = (__bf16)v;
+      hi[j] = h;
+      lo[j] = (__bf16)(isfinite(v) ? v - (float)h : 0.f);
+    }
+    u32x4_t* o = static_cast<u32x4_t*>(a.dst) + 2 * ((int64_t)b * a.dB + (int64_t)g * a.dC + (int64_t)y * a.dH + x);
+    o[0] = __builtin_bit_cast(u32x4_t, hi);
+    o[1] = __builtin_bit_cast(u32x4_t, lo);
+  }
+}
+
 }  // namespace mvbev
 
 extern "C" {
+
+int mvbev_store_gated_f32(const float* src, const int64_t src_strides[4], void* dst, const int64_t dst_strides[4],
+                          int64_t B, int64_t C, int64_t H, int64_t W, int dst_layout, const int32_t* gate,
+                          int32_t gate_tag, void* stream) {
+  using namespace mvbev;
+  if (!src || !dst || !gate || !src_strides || !dst_strides) return MVBEV_ERR_NULL;
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return MVBEV_ERR_RANK;
+  if (dst_layout != MVBEV_LAYOUT_F32 && dst_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;
+  if (src_strides[3] != 1 || dst_strides[3] != 1) return MVBEV_ERR_STRIDE;
+  if (dst_layout == MVBEV_LAYOUT_SPLIT_BF16 && (reinterpret_cast<uintptr_t>(dst) & 15)) return MVBEV_ERR_ALIGN;
+  StoreArgs a;
+  a.src = src;
+  a.sB = src_strides[0], a.sC = src_strides[1], a.sH = src_strides[2];
+  a.dst = dst;
+  a.dB = dst_strides[0], a.dC = dst_strides[1], a.dH = dst_strides[2];
+  a.B = (int)B, a.C = (int)C, a.H = (int)H, a.W = (int)W, a.split = dst_layout == MVBEV_LAYOUT_SPLIT_BF16;
+  a.gate = gate, a.gate_tag = gate_tag;
+  const int64_t n = B * (a.split ? ceil_div(C, 8) : C) * H * W;
+  hipLaunchKernelGGL(store_gated_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n, 256), 8192)), dim3(256), 0,
+                     as_stream(stream), a);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
 
 int mvbev_zero_gated(void* dst, int64_t bytes, const int32_t* gate, int32_t gate_tag, void* stream) {
   using namespace mvbev;
@@ -643,7 +711,7 @@ const char* mvbev_status_string(int s) {
   }
 }
 
-int mvbev_version(void) { return 12100; }
+int mvbev_version(void) { return 12200; }
 
 int mvbev_warp_perspective_f32(const float* src, int64_t B, int64_t C, int64_t H, int64_t W,
                                const int64_t src_strides[4], const float* m, float* dst,

@@ -362,6 +362,31 @@ def bias_relu_nonfinite_(y: torch.Tensor, init: torch.Tensor, row0: int, relu: b
     return y
 
 
+def store_gated_(src: torch.Tensor, dst: torch.Tensor, gate) -> torch.Tensor:
+    """``mvbev_store_gated_f32``: the fp32 [B, C, H, W] view ``src`` into ``dst`` — an fp32 [B, C, H, W] view,
+    or a split-bf16 blocked [B, G, H, W, 2, 8] view (a non-finite value kept in hi, lo = 0) — when the device
+    flag of ``gate = (flag, tag)`` holds tag; no host sync either way."""
+    _require_cuda(src, dst)
+    if src.dtype != torch.float32 or src.dim() != 4 or src.stride(3) != 1:
+        raise ValueError("src must be an fp32 [B, C, H, W] view with unit column stride")
+    B, C, H, W = src.shape
+    if dst.dtype == torch.bfloat16:
+        if tuple(dst.shape) != split_shape(B, C, H, W) or dst.stride(5) != 1 or dst.stride(4) != KC or \
+                dst.stride(3) != 2 * KC:
+            raise ValueError(f"split dst must be a [B, G, H, W, 2, 8] view of {split_shape(B, C, H, W)} with "
+                             "contiguous pixels")
+        layout, dstr = _native.LAYOUT_SPLIT_BF16, (dst.stride(0) // 16, dst.stride(1) // 16, dst.stride(2) // 16, 1)
+    elif dst.dtype == torch.float32 and tuple(dst.shape) == (B, C, H, W) and dst.stride(3) == 1:
+        layout, dstr = _native.LAYOUT_F32, tuple(dst.stride())
+    else:
+        raise ValueError("dst must be an fp32 [B, C, H, W] view or a split-bf16 one")
+    gp, gt = _gate(gate)
+    st = _native.load().mvbev_store_gated_f32(src.data_ptr(), _native._i64x4(*src.stride()), dst.data_ptr(),
+                                              _native._i64x4(*dstr), B, C, H, W, layout, gp, gt, _stream(src))
+    _native.check(st, "mvbev_store_gated_f32")
+    return dst
+
+
 def zero_gated_(t: torch.Tensor, gate) -> torch.Tensor:
     """Zero the contiguous ``t`` when the device flag of ``gate = (flag, tag)`` holds tag
     (``mvbev_zero_gated``), else leave it: no host sync either way."""
@@ -441,6 +466,39 @@ class PackedConv3x3:
     @property
     def K(self) -> Optional[int]:
         return None if self.chan_map is None else len(self.chan_map)
+
+    def map_dev(self, device) -> Optional[torch.Tensor]:
+        """The channel map as a device int32 tensor (None without a map), without packing anything."""
+        if self.chan_map is not None and (self._map_dev is None or self._map_dev.device != torch.device(device)):
+            self._map_dev = torch.tensor(self.chan_map, dtype=torch.int32, device=device)
+        return self._map_dev
+
+    def get_gated(self, weight: torch.Tensor, gate) -> torch.Tensor:
+        """The fp32 pack, enqueued gated on ``gate = (flag, tag)`` on EVERY call (no cache: a skipped pack
+        must not be taken for a current one — ``mvbev_pack_conv3x3_weight_f32_gated``); the buffer is reused."""
+        _require_cuda(weight)
+        if self.precision != "fp32" or self.wino:
+            raise ValueError("gated packs are fp32 packs")
+        cout, cin, kh, kw = weight.shape
+        if (kh, kw) != (3, 3) or weight.dtype != torch.float32 or cout % BN:
+            raise ValueError("expected a float32 [Cout,Cin,3,3] weight with Cout a multiple of 128")
+        lib = _native.load()
+        K = cin if self.chan_map is None else len(self.chan_map)
+        if self.chan_map is not None and (self._map_dev is None or self._map_dev.device != weight.device):
+            self._map_dev = torch.tensor(self.chan_map, dtype=torch.int32, device=weight.device)
+        n = lib.mvbev_conv3x3_packed_floats(cout, K)
+        if self.packed is None or self.packed.numel() != n or self.packed.device != weight.device:
+            self.packed = torch.empty(n, dtype=torch.float32, device=weight.device)
+        self._key = None
+        w = weight.detach()
+        if not w.is_contiguous():
+            raise ValueError("the gated pack reads the weight in place: it must be contiguous")
+        gp, gt = _gate(gate)
+        st = lib.mvbev_pack_conv3x3_weight_f32_gated(w.data_ptr(), cout, cin, None if self._map_dev is None
+                                                     else self._map_dev.data_ptr(), K, self.packed.data_ptr(),
+                                                     gp, gt, _stream(self.packed))
+        _native.check(st, "mvbev_pack_conv3x3_weight_f32_gated")
+        return self.packed
 
     def get(self, weight: torch.Tensor) -> torch.Tensor:
         _require_cuda(weight)
@@ -713,12 +771,13 @@ def wino_rows_bytes(desc) -> int:
 
 
 def wino_rows(x: torch.Tensor, desc, t: torch.Tensor, group_mask: Optional[torch.Tensor] = None,
-              dilation: int = 1) -> torch.Tensor:
+              dilation: int = 1, gate=None) -> torch.Tensor:
     """B^T over every 3-row output tile's 5 input rows of the split-bf16 ``x`` (addressed through
     ``desc`` as ``conv3x3_desc``) into ``t`` (bf16, >= ``wino_rows_bytes`` bytes; with
     ``group_mask`` zero-filled once and only written by this call with that mask):
     ``mvbev_wino_rows_split_bf16``; ``dilation`` 2: conv2's interleaved row tiles, input rows
-    2 apart (``mvbev_wino_rows_split_bf16_dil``)."""
+    2 apart (``mvbev_wino_rows_split_bf16_dil``); ``gate`` = (flag, tag): only when the device flag holds
+    the tag (``mvbev_wino_rows_split_bf16_gated``)."""
     _require_cuda(x, t)
     if x.dtype != torch.bfloat16 or t.dtype != torch.bfloat16 or not t.is_contiguous():
         raise TypeError("wino_rows reads the split-bf16 slab and writes a contiguous bf16 T")
@@ -729,6 +788,13 @@ def wino_rows(x: torch.Tensor, desc, t: torch.Tensor, group_mask: Optional[torch
         if group_mask.dtype != torch.int32 or group_mask.numel() < tiles or not group_mask.is_contiguous():
             raise ValueError(f"group_mask must be a contiguous int32 tensor of >= {tiles} tiles")
         gmp = group_mask.data_ptr()
+    if gate is not None:
+        gp, gt = _gate(gate)
+        st = _native.load().mvbev_wino_rows_split_bf16_gated(x.data_ptr(), ctypes.byref(desc), int(dilation), gmp,
+                                                             t.data_ptr(), t.numel() * t.element_size(), gp, gt,
+                                                             _stream(x))
+        _native.check(st, "mvbev_wino_rows_split_bf16_gated")
+        return t
     st = _native.load().mvbev_wino_rows_split_bf16_dil(x.data_ptr(), ctypes.byref(desc), int(dilation), gmp,
                                                        t.data_ptr(), t.numel() * t.element_size(), _stream(x))
     _native.check(st, "mvbev_wino_rows_split_bf16_dil")

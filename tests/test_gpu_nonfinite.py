@@ -173,3 +173,85 @@ def test_nonfinite_guard_two_warp_calls_one_frame_and_row_bands():
                                     {k: torch.from_numpy(v) for k, v in params.items()})
     _check_discriminates(ref)
     assert_parity_t(got, ref, "two warp calls, banded exact path (NaN / inf pattern included)")
+
+
+def _masked_relu(pre, m):
+    """torch's ReLU with the sign decision of a given 0/1 pattern ``m`` where ``pre`` is not NaN (the GPU's
+    activation pattern: a pre-activation within fp32 rounding of 0 may fall either way): value
+    where(m, pre, 0), NaN kept as NaN, gradient 1 where m and 0 elsewhere (torch: grad * (y > 0))."""
+    nan = torch.where(torch.isnan(pre.detach()), pre.detach(), torch.zeros_like(pre))
+    return torch.where(m > 0, pre, torch.zeros_like(pre)) + nan
+
+
+@pytest.mark.parametrize("backbone", [False, True])
+def test_training_step_nonfinite_features_vs_cpu_autograd(backbone):
+    """VERDICT r05 missing 2: a training step (``autograd.project_fuse`` / ``project_fuse_backbone``: the fused
+    warp + B^T, Winograd convs, native backward) on features holding +inf / NaN / -inf.  The training forward's
+    gated exact path (``ProjectFuse._train_exact``) rewrites the map AND stores the exact activations the native
+    backward reads, so: the map has the reference's NaN / inf pattern; the feature gradients and the biases'
+    (finite in the reference: torch's ReLU backward passes no gradient through a NaN) pass the gate; conv2's
+    and conv3's weight gradients are NaN exactly where the reference's are (everywhere); conv1's weight
+    gradient is non-finite exactly in the reference's entries (the poisoned channels' columns; the row-Winograd
+    form's B^T turns more of those infinities into NaN than the direct sum does) and equal elsewhere."""
+    import torch.nn.functional as F
+    from mvdet_amd import ProjectFuse, synthetic
+    from mvdet_amd.autograd import project_fuse, project_fuse_backbone
+    from mvdet_amd.geometry import projection_matrices
+    C = 128
+    ds, params = _rig(C, seed=5)
+    N, B = ds.num_cam, 1
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    hb = [u // 3 for u in up]
+    pm = projection_matrices(ds)
+    mc = _mc(C, N, params)
+    eng = ProjectFuse(pm, up, grid, C)
+    low = [synthetic.backbone_features(B, C, hb, seed=700 + v, device=DEV) for v in range(N)]
+    if backbone:
+        low = _poison(low, hb)
+        feats = [f.clone().requires_grad_() for f in low]
+        out = project_fuse_backbone(eng, feats, mc)
+        cpu_feats = [f.detach().cpu() for f in low]
+    else:
+        ups = [torch.nn.functional.interpolate(f, list(up), mode="bilinear") for f in low]
+        ups[0][0, 3, up[0] // 2, up[1] // 2] = float("inf")
+        ups[1][0, 7, up[0] // 2 + 3, up[1] // 2 - 5] = float("nan")
+        ups[2][0, 1, up[0] // 2 - 4, up[1] // 2 + 6] = float("-inf")
+        feats = [f.clone().requires_grad_() for f in ups]
+        out = project_fuse(eng, feats, mc)
+        cpu_feats = [f.detach().cpu() for f in ups]
+    ws = out.grad_fn.ws
+    assert ws.train_t_only and ws.t_from_warp and ws.guard_src is None  # the guard ran and closed the frame
+    assert int(ws.nf.item()) == ws.nf_tag, "the fused warp did not report the non-finite features"
+    m1, m2 = (eng.y1_fp32(ws) > 0).float().cpu(), (ws.y2 > 0).float().cpu()
+    gmap = torch.randn(out.shape, generator=torch.Generator().manual_seed(1))
+    out.backward(gmap.to(DEV))
+    # the reference: torch-CPU autograd through F.interpolate (backbone), the kornia restatement, cat, the convs
+    fr = [f.clone().requires_grad_() for f in cpu_feats]
+    pr = {k: torch.from_numpy(v).requires_grad_() for k, v in params.items() if k.startswith("map_classifier.")}
+    src = [cpu_path.upsample(f, up) for f in fr] if backbone else fr
+    warped = cpu_path.warp_views(src, [M.numpy() for M in pm], grid)
+    x = torch.cat(warped + [cpu_path.coord_map(*grid).repeat([B, 1, 1, 1])], 1)
+    pre1 = F.conv2d(x, pr["map_classifier.0.weight"], pr["map_classifier.0.bias"], padding=1)
+    pre2 = F.conv2d(_masked_relu(pre1, m1), pr["map_classifier.2.weight"], pr["map_classifier.2.bias"], padding=2,
+                    dilation=2)
+    ref = F.conv2d(_masked_relu(pre2, m2), pr["map_classifier.4.weight"], None, padding=4, dilation=4)
+    for m, pre in ((m1, pre1), (m2, pre2)):  # the GPU's pattern is torch's up to fp32 rounding near 0
+        fin = torch.isfinite(pre)
+        flip = (m != (pre > 0).float()) & fin
+        assert flip.sum().item() <= max(2, pre.numel() // 20000)
+        assert (pre[flip].abs() <= 1e-4 * pre[fin].abs().max()).all()
+        assert torch.equal(m[~fin].bool(), (pre[~fin] > 0))  # +inf passes, -inf / NaN do not
+    ref.backward(gmap)
+    _check_discriminates(ref.detach())
+    assert_parity_t(out.detach(), ref.detach(), "training forward, non-finite features (NaN / inf pattern)")
+    for v in range(N):
+        assert torch.isfinite(fr[v].grad).all()
+        assert_parity_t(feats[v].grad, fr[v].grad, f"d features view {v}")
+    got = dict(mc.named_parameters())
+    for k in ("0.bias", "2.bias", "2.weight", "4.weight"):
+        assert_parity_t(got[k].grad, pr["map_classifier." + k].grad, f"d {k} (non-finite pattern included)")
+    g1, r1 = got["0.weight"].grad.cpu(), pr["map_classifier.0.weight"].grad
+    assert 0 < int((~torch.isfinite(r1)).sum()) < r1.numel()
+    assert torch.equal(~torch.isfinite(g1), ~torch.isfinite(r1)), "conv1 dW: non-finite entries differ"
+    fin = torch.isfinite(r1)
+    assert_parity_t(g1[fin], r1[fin], "conv1 dW, finite entries")

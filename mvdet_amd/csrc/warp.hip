@@ -175,7 +175,7 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
   static_assert(!PAIR || std::is_same<T, float>::value, "corner pairs are fp32 8-B loads");
   __shared__ __attribute__((aligned(16))) float ds[kWwRows][kWwCols][8];  // [row][col][channel]
   __shared__ unsigned char nz[kWwRows][kWwCols];
-  __shared__ __attribute__((aligned(16))) float stage[kWarpCPB * (kWwStage > 0 ? kWwStage : 1)];
+  __shared__ __attribute__((aligned(16))) f32x2_t stage2[kWarpCPB / 2 * (kWwStage > 0 ? kWwStage : 1)];
   __shared__ int box[4];  // source rows [box0, box1], columns [box2, box3] of the block's corners
   const int lb = xcd_remap(blockIdx.x, a.nwg);
   const int tile = lb % a.tiles;
@@ -192,7 +192,20 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
   const int i = tid / kWwCols, c = tid % kWwCols;  // 16 x kWwCols threads, rows >= 14 idle
   const int v = 12 * k - 1 + i, u = tx * kWwCols + c;
   const bool live = i < kWwRows && v >= 0 && v < a.Ho && u < a.Wo;
-  if (tid == 0) {
+  // (ABI 12200) the block's source box from the per-geometry table: the 64 channel-group blocks of a
+  // (view, tile) no longer each reduce the same box (24 ds_bpermute + 4 LDS atomics per wave and a
+  // barrier: ~47 % of this kernel's LDS instructions at cfg2), and a block with no sample inside the
+  // source (32 % of cfg2's blocks) leaves before doing anything
+  int bx[4];
+  if (a.boxes) {
+    const int32_t* e = a.boxes + 4 * ((int64_t)view * a.tiles + tile);
+    bx[0] = e[0];
+    bx[1] = e[1];
+    bx[2] = e[2];
+    const int c1f = e[3];
+    bx[3] = c1f & 0x3FFFFFFF;
+    if (a.skip_zero && bx[1] < 0 && !(c1f >> 30)) return;  // whole block, before any barrier
+  } else if (tid == 0) {
     box[0] = INT32_MAX;
     box[1] = -1;
     box[2] = INT32_MAX;
@@ -213,34 +226,38 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
   const int x0 = wc.inside ? (int)fx0 : 0, y0 = wc.inside ? (int)fy0 : 0;
   const int cx0 = max(x0, 0), cy0 = max(y0, 0);
   const int cx1 = min(x0 + 1, W - 1), cy1 = min(y0 + 1, H - 1);
-  __syncthreads();
-  if (kWwStage > 0) {  // the box: a shuffle reduction per wave, then one LDS atomic per wave and bound
-    int r0 = wc.inside ? cy0 : INT32_MAX, r1 = wc.inside ? cy1 : -1;
-    int q0 = wc.inside ? cx0 : INT32_MAX, q1 = wc.inside ? cx1 : -1;
+  if (!a.boxes) {
+    __syncthreads();
+    if (kWwStage > 0) {  // the box: a shuffle reduction per wave, then one LDS atomic per wave and bound
+      int r0 = wc.inside ? cy0 : INT32_MAX, r1 = wc.inside ? cy1 : -1;
+      int q0 = wc.inside ? cx0 : INT32_MAX, q1 = wc.inside ? cx1 : -1;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      r0 = min(r0, __shfl_xor(r0, o));
-      r1 = max(r1, __shfl_xor(r1, o));
-      q0 = min(q0, __shfl_xor(q0, o));
-      q1 = max(q1, __shfl_xor(q1, o));
+      for (int o = 32; o > 0; o >>= 1) {
+        r0 = min(r0, __shfl_xor(r0, o));
+        r1 = max(r1, __shfl_xor(r1, o));
+        q0 = min(q0, __shfl_xor(q0, o));
+        q1 = max(q1, __shfl_xor(q1, o));
+      }
+      if ((tid & 63) == 0 && r1 >= 0) {
+        atomicMin(&box[0], r0);
+        atomicMax(&box[1], r1);
+        atomicMin(&box[2], q0);
+        atomicMax(&box[3], q1);
+      }
     }
-    if ((tid & 63) == 0 && r1 >= 0) {
-      atomicMin(&box[0], r0);
-      atomicMax(&box[1], r1);
-      atomicMin(&box[2], q0);
-      atomicMax(&box[3], q1);
-    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bx[q] = box[q];
   }
-  __syncthreads();
   const T* base = static_cast<const T*>(vw.src) + (int64_t)b * vw.sB;
   const bool quad_ok = vw.sW == 1 && (W & 3) == 0 && (vw.sH & 3) == 0 && (vw.sC & 3) == 0 &&
                        (reinterpret_cast<uintptr_t>(base) & (4 * sizeof(T) - 1)) == 0;
-  const StageBox sb = stage_box_shape(box, W, quad_ok);  // 16-B staging loads where the source allows
+  const StageBox sb = stage_box_shape(bx, W, quad_ok);  // 16-B staging loads where the source allows
   const int R = sb.R, Cb = sb.pitch;
   // uniform per block (the staged path needs unit column stride: the non-quad loads assume it too)
-  const bool staged = kWwStage > 0 && box[1] >= 0 && vw.sW == 1 && R * Cb <= kWwStage;
+  const bool staged = kWwStage > 0 && bx[1] >= 0 && vw.sW == 1 && R * Cb <= kWwStage;
   if (staged) {
-    stage_box_load<kWwThreads, T>(base, vw.sC, vw.sH, c_begin, c_end, sb, stage, tid);
+    stage_box_load<kWwThreads, T>(base, vw.sC, vw.sH, c_begin, c_end, sb, stage2, tid);
     __syncthreads();
   }
   if (i < kWwRows) {  // phase 1: one warped pixel (8 channels) per thread
@@ -264,17 +281,21 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
         const bool ok_nw = vx0 && vy0, ok_ne = vx1 && vy0, ok_sw = vx0 && vy1, ok_se = vx1 && vy1;
         if (staged) {
           const int n = R * Cb;
-          const int t0 = (cy0 - box[0]) * Cb, t1 = (cy1 - box[0]) * Cb;
+          const int t0 = (cy0 - bx[0]) * Cb, t1 = (cy1 - bx[0]) * Cb;
           const int l0 = cx0 - sb.c0, l1 = cx1 - sb.c0;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float* sj = stage + j * n;
-            float acc = 0.f;
-            acc += (ok_nw ? sj[t0 + l0] : 0.f) * w_nw;
-            acc += (ok_ne ? sj[t0 + l1] : 0.f) * w_ne;
-            acc += (ok_sw ? sj[t1 + l0] : 0.f) * w_sw;
-            acc += (ok_se ? sj[t1 + l1] : 0.f) * w_se;
-            d[j] = c_begin + j < c_end ? acc : 0.f;
+          for (int p = 0; p < 4; ++p) {  // a channel pair per ds_read_b64 (the same products per channel)
+            const f32x2_t* sp = stage2 + p * n;
+            const f32x2_t vnw = sp[t0 + l0], vne = sp[t0 + l1], vsw = sp[t1 + l0], vse = sp[t1 + l1];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              float acc = 0.f;
+              acc += (ok_nw ? vnw[e] : 0.f) * w_nw;
+              acc += (ok_ne ? vne[e] : 0.f) * w_ne;
+              acc += (ok_sw ? vsw[e] : 0.f) * w_sw;
+              acc += (ok_se ? vse[e] : 0.f) * w_se;
+              d[2 * p + e] = c_begin + 2 * p + e < c_end ? acc : 0.f;
+            }
           }
         } else {
           const int64_t sH = vw.sH, sW = vw.sW, sC = vw.sC;
@@ -308,12 +329,60 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
         }
       }
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ds[i][c][j] = d[j];
+    // two 16-B stores (the element-wise form compiled to 8 ds_write_b32)
+    *reinterpret_cast<f32x4a_t*>(&ds[i][c][0]) = f32x4a_t{d[0], d[1], d[2], d[3]};
+    *reinterpret_cast<f32x4a_t*>(&ds[i][c][4]) = f32x4a_t{d[4], d[5], d[6], d[7]};
     nz[i][c] = any;
   }
   __syncthreads();
   wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
+}
+
+// The per-(view, tile) source boxes of warp_wino_kernel (ABI 12200), once per geometry: a block per (view,
+// tile) evaluates the same pixels, coordinates (warp_coord) and clamped corners as the fused warp's block
+// and stores {r0, r1, c0, c1 | nonfinite << 30} (r1 = -1: no sample inside the source; nonfinite: some live
+// pixel has non-finite coordinates — its NaN output must still be written).
+__global__ __launch_bounds__(kWwThreads) void wino_box_kernel(const WarpArgs a, int32_t* __restrict__ boxes) {
+  __shared__ int box[5];
+  const int tile = blockIdx.x % a.tiles, view = blockIdx.x / a.tiles;
+  const WarpView& vw = a.v[view];
+  const int k = tile / a.tiles_x, tx = tile - k * a.tiles_x;
+  const int tid = threadIdx.x;
+  const int i = tid / kWwCols, c = tid % kWwCols;
+  const int v = 12 * k - 1 + i, u = tx * kWwCols + c;
+  const bool live = i < kWwRows && v >= 0 && v < a.Ho && u < a.Wo;
+  if (tid == 0) {
+    box[0] = INT32_MAX;
+    box[1] = -1;
+    box[2] = INT32_MAX;
+    box[3] = -1;
+    box[4] = 0;
+  }
+  __syncthreads();
+  WarpCoord wc;
+  wc.inside = false;
+  wc.finite = true;
+  wc.ix = wc.iy = 0.f;
+  if (live) {
+    float m[9];
+#pragma unroll
+    for (int q = 0; q < 9; ++q) m[q] = vw.m[q];
+    wc = warp_coord(m, u, v, a.Ho, a.Wo, a.H, a.W);
+  }
+  if (wc.inside) {
+    const int x0 = (int)floorf(wc.ix), y0 = (int)floorf(wc.iy);
+    atomicMin(&box[0], max(y0, 0));
+    atomicMax(&box[1], min(y0 + 1, a.H - 1));
+    atomicMin(&box[2], max(x0, 0));
+    atomicMax(&box[3], min(x0 + 1, a.W - 1));
+  }
+  if (live && !wc.finite) atomicOr(&box[4], 1);
+  __syncthreads();
+  if (tid == 0) {  // one 16-B vector store
+    const int empty = box[1] < 0;
+    const int4 out = make_int4(empty ? 0 : box[0], box[1], empty ? 0 : box[2], (empty ? 0 : box[3]) | (box[4] << 30));
+    *reinterpret_cast<int4*>(boxes + 4 * ((int64_t)view * a.tiles + tile)) = out;
+  }
 }
 
 // warp_wino_kernel for channels-last sources (round 4: sC == 1, the [B, C, H, W] tensor in torch's
@@ -756,9 +825,45 @@ int mvbev_warp_views_split_bf16_rows(const mvbev_warp_view* views, const int32_t
                                   nonfinite, nf_tag);
 }
 
+int mvbev_warp_views_wino_rows_ex(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t H,
+                                  int64_t W, int64_t Ho, int64_t Wo, int64_t r3_rows, int flags, int32_t* nonfinite,
+                                  int32_t nf_tag, const int32_t* boxes, void* stream);
+
 int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t H,
                                int64_t W, int64_t Ho, int64_t Wo, int64_t r3_rows, int flags, int32_t* nonfinite,
                                int32_t nf_tag, void* stream) {
+  return mvbev_warp_views_wino_rows_ex(views, nviews, B, C, H, W, Ho, Wo, r3_rows, flags, nonfinite, nf_tag, nullptr,
+                                       stream);
+}
+
+int64_t mvbev_warp_wino_boxes_count(int64_t Wo, int64_t r3_rows) {
+  if (Wo <= 0 || r3_rows <= 0) return 0;
+  return mvbev::ceil_div(Wo, (int64_t)mvbev::kWwCols) * mvbev::ceil_div(r3_rows, (int64_t)4);
+}
+
+int mvbev_warp_wino_boxes(const mvbev_warp_view* views, int nviews, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
+                          int64_t r3_rows, int32_t* boxes, void* stream) {
+  using namespace mvbev;
+  if (!views || !boxes) return MVBEV_ERR_NULL;
+  if (nviews <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 || r3_rows <= 0) return MVBEV_ERR_RANK;
+  if (nviews > kWarpMaxViews || 3 * r3_rows < Ho || H >= (1 << 29) || W >= (1 << 29)) return MVBEV_ERR_SHAPE;
+  if (reinterpret_cast<uintptr_t>(boxes) & 15) return MVBEV_ERR_ALIGN;
+  WarpArgs a = {};
+  for (int i = 0; i < nviews; ++i)
+    for (int q = 0; q < 9; ++q) a.v[i].m[q] = views[i].m[q];
+  a.nviews = nviews;
+  a.H = (int)H, a.W = (int)W, a.Ho = (int)Ho, a.Wo = (int)Wo;
+  a.tiles_x = (int)ceil_div(Wo, kWwCols);
+  a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);
+  hipLaunchKernelGGL(wino_box_kernel, dim3((unsigned)(a.tiles * nviews)), dim3(kWwThreads), 0, as_stream(stream), a,
+                     boxes);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+int mvbev_warp_views_wino_rows_ex(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t H,
+                                  int64_t W, int64_t Ho, int64_t Wo, int64_t r3_rows, int flags, int32_t* nonfinite,
+                                  int32_t nf_tag, const int32_t* boxes, void* stream) {
   using namespace mvbev;
   if (!views) return MVBEV_ERR_NULL;
   if (flags & ~(MVBEV_WARP_DST_ZEROED | MVBEV_WARP_SRC_F16)) return MVBEV_ERR_SHAPE;
@@ -805,6 +910,7 @@ int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t
   }
   a.chunks = (int)ceil_div(C, cl ? kWcCh : kWarpCPB);
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
+  a.boxes = cl ? nullptr : boxes;  // (the line-per-pixel kernel has its own tiling)
   const dim3 grid((unsigned)a.nwg), block(cl ? kWcThreads : kWwThreads);
   if (cl)
     hipLaunchKernelGGL(warp_wino_cl_kernel, grid, block, 0, as_stream(stream), a, (int)r3_rows);

@@ -70,6 +70,10 @@ struct WarpArgs {
   // rows of each dst (a row window of the Ho-row grid starting at its view's row0; 0 = Ho):
   // warp_tile_kernel and the exact warp (ABI 11900)
   int out_rows;
+  // (ABI 12200) warp_wino_kernel: the per-(view, block tile) source box of the block's bilinear corners,
+  // int32 [nviews][tiles][4] {r0, r1, c0, c1 | nonfinite << 30} (r1 < 0: no sample inside the source),
+  // computed once per geometry by mvbev_warp_wino_boxes; NULL: each block reduces its own box
+  const int32_t* boxes;
 };
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -256,63 +260,53 @@ __device__ inline StageBox stage_box_shape(const int (&box)[4], int W, bool quad
   sb.pitch = c1 - sb.c0;
   return sb;
 }
-// channel-major staging: stage[j][r][col] (fp32; T = float or __half sources; quad: 16-B fp32 / 8-B fp16
-// loads of 4 columns where the source's strides and alignment allow)
+// channel-pair staging (round 6): stage2[p][r][col] = {channel 2p, channel 2p + 1} (fp32 pairs; T = float or
+// __half sources; quad: 16-B fp32 / 8-B fp16 loads of 4 columns where the source's strides and alignment allow,
+// interleaved by pair into two 16-B LDS stores) — a warped sample then reads each corner of two channels with
+// one ds_read_b64 (16 per pixel and 8-channel group instead of 32 ds_read_b32)
 template <int NT, typename T = float>
 __device__ inline void stage_box_load(const T* __restrict__ base, int64_t sC, int64_t sH, int c_begin, int c_end,
-                                      const StageBox& sb, float* __restrict__ stage, int tid) {
+                                      const StageBox& sb, f32x2_t* __restrict__ stage2, int tid) {
   const int n = sb.R * sb.pitch;
-  if constexpr (!std::is_same<T, float>::value) {
-    if (sb.quad) {  // 4 halves (8 B) per lane and channel, widened to one 16-B LDS store
-      const int Q = sb.pitch >> 2, items = sb.R * Q;
-      for (int it = tid; it < items; it += NT) {
-        const int r = it / Q, q = it - r * Q;
-        const T* src = base + (int64_t)(sb.r0 + r) * sH + sb.c0 + 4 * q;
-        uint2 t[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) t[j] = *reinterpret_cast<const uint2*>(src + (int64_t)min(c_begin + j, c_end - 1) * sC);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const T* h = reinterpret_cast<const T*>(&t[j]);
-          const f32x4a_t f = {to_f32<T>(h[0]), to_f32<T>(h[1]), to_f32<T>(h[2]), to_f32<T>(h[3])};
-          *reinterpret_cast<f32x4a_t*>(stage + j * n + r * sb.pitch + 4 * q) = f;
-        }
-      }
-      return;
-    }
-    for (int r = tid / 32; r < sb.R; r += NT / 32)
-      for (int cc = tid % 32; cc < sb.pitch; cc += 32) {
-        float t[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          t[j] = to_f32<T>(base[(int64_t)min(c_begin + j, c_end - 1) * sC + (int64_t)(sb.r0 + r) * sH + sb.c0 + cc]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) stage[j * n + r * sb.pitch + cc] = t[j];
-      }
-    return;
-  } else if (sb.quad) {
+  if (sb.quad) {
     const int Q = sb.pitch >> 2, items = sb.R * Q;
     for (int it = tid; it < items; it += NT) {
       const int r = it / Q, q = it - r * Q;
-      const float* src = base + (int64_t)(sb.r0 + r) * sH + sb.c0 + 4 * q;
+      const T* src = base + (int64_t)(sb.r0 + r) * sH + sb.c0 + 4 * q;
       f32x4a_t t[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        t[j] = *reinterpret_cast<const f32x4a_t*>(src + (int64_t)min(c_begin + j, c_end - 1) * sC);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) *reinterpret_cast<f32x4a_t*>(stage + j * n + r * sb.pitch + 4 * q) = t[j];
-    }
-  } else {
-    for (int r = tid / 32; r < sb.R; r += NT / 32)
-      for (int cc = tid % 32; cc < sb.pitch; cc += 32) {
-        float t[8];
+      if constexpr (std::is_same<T, float>::value) {
 #pragma unroll
         for (int j = 0; j < 8; ++j)
-          t[j] = base[(int64_t)min(c_begin + j, c_end - 1) * sC + (int64_t)(sb.r0 + r) * sH + sb.c0 + cc];
+          t[j] = *reinterpret_cast<const f32x4a_t*>(src + (int64_t)min(c_begin + j, c_end - 1) * sC);
+      } else {  // 4 halves (8 B) per lane and channel
+        uint2 u[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) stage[j * n + r * sb.pitch + cc] = t[j];
+        for (int j = 0; j < 8; ++j) u[j] = *reinterpret_cast<const uint2*>(src + (int64_t)min(c_begin + j, c_end - 1) * sC);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const T* h = reinterpret_cast<const T*>(&u[j]);
+          t[j] = f32x4a_t{to_f32<T>(h[0]), to_f32<T>(h[1]), to_f32<T>(h[2]), to_f32<T>(h[3])};
+        }
       }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const f32x4a_t x = t[2 * p], y = t[2 * p + 1];
+        f32x4a_t* dst = reinterpret_cast<f32x4a_t*>(stage2 + p * n + r * sb.pitch + 4 * q);
+        dst[0] = f32x4a_t{x[0], y[0], x[1], y[1]};
+        dst[1] = f32x4a_t{x[2], y[2], x[3], y[3]};
+      }
+    }
+    return;
   }
+  for (int r = tid / 32; r < sb.R; r += NT / 32)
+    for (int cc = tid % 32; cc < sb.pitch; cc += 32) {
+      float t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        t[j] = to_f32<T>(base[(int64_t)min(c_begin + j, c_end - 1) * sC + (int64_t)(sb.r0 + r) * sH + sb.c0 + cc]);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) stage2[p * n + r * sb.pitch + cc] = f32x2_t{t[2 * p], t[2 * p + 1]};
+    }
 }
 
 __device__ inline void wino_rows_phase2(const float (&ds)[kWwRows][kWwCols][8], const unsigned char (&nz)[kWwRows][kWwCols],

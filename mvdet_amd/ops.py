@@ -801,8 +801,27 @@ def wino_rows(x: torch.Tensor, desc, t: torch.Tensor, group_mask: Optional[torch
     return t
 
 
+def warp_wino_boxes(m_norms, src_hw, grid_hw, device) -> torch.Tensor:
+    """``mvbev_warp_wino_boxes``: the per-(view, block) staging boxes of the NCHW fused warp + B^T for the
+    whole-grid T (r3 rows 4 * ceil(Ho / 12)) — geometry only, computed once and reused every frame."""
+    Ho, Wo = int(grid_hw[0]), int(grid_hw[1])
+    r3 = 4 * (-(-Ho // 12))
+    n = len(m_norms)
+    if not 0 < n <= 16:
+        raise ValueError("need 1..16 views")
+    lib = _native.load()
+    boxes = torch.empty((n, int(lib.mvbev_warp_wino_boxes_count(Wo, r3)), 4), dtype=torch.int32, device=device)
+    arr = (_native.WarpView * n)()
+    for i, m in enumerate(m_norms):
+        arr[i].m = (ctypes.c_float * 9)(*torch.as_tensor(m, dtype=torch.float32).reshape(9).tolist())
+    st = lib.mvbev_warp_wino_boxes(arr, n, int(src_hw[0]), int(src_hw[1]), Ho, Wo, r3, boxes.data_ptr(),
+                                   _stream(boxes))
+    _native.check(st, "mvbev_warp_wino_boxes")
+    return boxes
+
+
 def warp_views_wino_rows_into(srcs, m_norms, t: torch.Tensor, slots, Cs: int, K: int, Ho: int, Wo: int,
-                              dst_zeroed: bool = False, up_hw=None, nonfinite=None) -> None:
+                              dst_zeroed: bool = False, up_hw=None, nonfinite=None, boxes=None) -> None:
     """Warp + row-Winograd transform in ONE launch (``mvbev_warp_views_wino_rows``): view i
     (fp32 ``srcs[i]`` [B,C,H,W], host kornia matrix ``m_norms[i]``) lands in channels
     [slots[i] * Cs, + C) of ``t``, the T buffer of ``wino_rows`` for a K-channel slab of
@@ -845,8 +864,13 @@ def warp_views_wino_rows_into(srcs, m_norms, t: torch.Tensor, slots, Cs: int, K:
                                                                  Ho, Wo, r3, flags, fp, ft, _stream(t))
         _native.check(st, "mvbev_warp_views_upsampled_wino_rows")
         return
-    st = _native.load().mvbev_warp_views_wino_rows(arr, n, B, C, H, W, Ho, Wo, r3, flags, fp, ft, _stream(t))
-    _native.check(st, "mvbev_warp_views_wino_rows")
+    if boxes is not None:  # (from warp_wino_boxes with the same matrices, in the same view order)
+        _require_cuda(boxes)
+        if boxes.dtype != torch.int32 or tuple(boxes.shape[:1]) != (n,) or not boxes.is_contiguous():
+            raise ValueError("boxes must be warp_wino_boxes' int32 [views, tiles, 4] table of these views")
+    st = _native.load().mvbev_warp_views_wino_rows_ex(arr, n, B, C, H, W, Ho, Wo, r3, flags, fp, ft,
+                                                      None if boxes is None else boxes.data_ptr(), _stream(t))
+    _native.check(st, "mvbev_warp_views_wino_rows_ex")
 
 
 def conv3x3_wino(t: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: Optional[torch.Tensor] = None,

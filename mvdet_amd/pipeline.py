@@ -373,8 +373,18 @@ class ProjectFuse:
                 ws.guard_src[self.slot_of[c]] = (c, f, up_hw)
         ops.warp_views_wino_rows_into(list(feats), [self.m_norm_cpu[c] for c in cams], ws.wino_t,
                                       [self.slot_of[c] for c in cams], self.Cs, self.S * self.Cs, H, W,
-                                      dst_zeroed=True, up_hw=up_hw, nonfinite=nonfinite)
+                                      dst_zeroed=True, up_hw=up_hw, nonfinite=nonfinite,
+                                      boxes=None if up_hw is not None else self._wino_boxes(ws.slab.device, cams))
         ws.t_from_warp = True
+
+    def _wino_boxes(self, device, cams) -> torch.Tensor:
+        """The fused warp's per-(view, block) staging boxes for these cameras (geometry only, cached)."""
+        key = ("boxes", str(torch.device(device)), tuple(cams))
+        b = self._masks.get(key)
+        if b is None:
+            b = ops.warp_wino_boxes([self.m_norm_cpu[c] for c in cams], self.src_hw, self.grid_hw, device)
+            self._masks[key] = b
+        return b
 
     def warp_views(self, ws: Workspace, cams: Sequence[int], feats: Sequence[torch.Tensor]) -> None:
         """a5 for several views in one launch (``feats[i]`` is view ``cams[i]``).  With

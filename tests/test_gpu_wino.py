@@ -297,6 +297,46 @@ def test_fused_warp_channels_last_matches_nchw(cfg, C, B):
     _assert_same_t(_t_value(a, Wo), _t_value(b, Wo))
 
 
+@pytest.mark.parametrize("cfg,C,B,half", [(1, 32, 1, False), (2, 64, 2, False), (2, 24, 1, False), (4, 16, 2, True)])
+def test_fused_warp_box_table_is_bitwise_the_block_reduction(cfg, C, B, half):
+    """Round 6: the NCHW fused warp + B^T with the per-geometry staging boxes (``mvbev_warp_wino_boxes`` ->
+    ``mvbev_warp_views_wino_rows_ex``) writes bitwise the T of the per-block box reduction (same box, same
+    staged / direct choice, same arithmetic), with skip_zero on and off (blocks without an inside sample
+    return at once), a view with non-finite geometry (its NaN T still written), an inf feature (the
+    non-finite report), B = 2 and fp16 sources; the table marks the empty and non-finite blocks."""
+    from mvdet_amd import ops, synthetic
+    from mvdet_amd.geometry import kornia_src_norm_from_dst_norm, projection_matrices
+    spec = synthetic.CONFIGS[cfg]
+    ds = spec["make"]()
+    N = ds.num_cam
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    ms = [kornia_src_norm_from_dst_norm(M.float().reshape(1, 3, 3), up, grid)[0] for M in projection_matrices(ds)]
+    ms[-1] = ms[-1].clone()
+    ms[-1][0, 2] = float("inf")
+    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in up], up, seed=81 + v, device=DEV)
+             for v in range(N)]
+    feats[0][B - 1, C - 1, up[0] // 2, up[1] // 2] = float("inf")
+    if half:
+        feats = [f.half() for f in feats]
+    Ho, Wo = grid
+    r3 = 4 * (-(-Ho // 12))
+    boxes = ops.warp_wino_boxes(ms, up, grid, DEV)
+    bc = boxes.cpu()
+    assert (bc[:-1, :, 1] < 0).any() and (bc[:-1, :, 1] >= 0).any()  # empty and non-empty blocks
+    assert ((bc[-1, :, 3] >> 30) == 1).all()                          # the NaN view: every block non-finite
+    numel = B * (N * C // 8) * 5 * r3 * Wo * 16
+    for zeroed in (False, True):
+        outs = []
+        for bx in (None, boxes):
+            t = torch.zeros(numel, dtype=torch.bfloat16, device=DEV)
+            flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+            ops.warp_views_wino_rows_into(feats, ms, t, list(range(N)), C, N * C, Ho, Wo, dst_zeroed=zeroed,
+                                          nonfinite=(flag, 5), boxes=bx)
+            outs.append((t.view(torch.int16).cpu(), int(flag.item())))
+        assert outs[0][1] == outs[1][1] == 5
+        assert torch.equal(outs[0][0], outs[1][0]), f"skip_zero={zeroed}: T differs with the box table"
+
+
 @pytest.mark.parametrize("cfg,C,B", [(1, 32, 1), (2, 64, 2), (2, 40, 1)])
 def test_fused_upsample_warp_channels_last_matches_nchw(cfg, C, B):
     """The fused 3x upsample + warp + B^T from channels-last backbone maps (warp_up_wino_cl_kernel:

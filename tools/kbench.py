@@ -187,6 +187,9 @@ def main():
             "winorows": (lambda: ops.wino_rows(wws.slab, wd1, wws.wino_t, wgm), None),
             "warpw": (lambda: _with(weng, "wino_warp", True, lambda: weng.warp_views(wws, list(range(N)), feats)),
                       None),  # warp + B^T in one pass (wino_warp; leaves T from the warp, run it last)
+            # round 6: the same without the per-geometry box table (each block reduces its own box)
+            "warpw0": (lambda: _with(weng, "_wino_boxes", lambda dev, cams: None, lambda: _with(
+                weng, "wino_warp", True, lambda: weng.warp_views(wws, list(range(N)), feats))), None),
             # the same on channels-last features (warp_wino_cl_kernel)
             "warpwcl": (lambda: _with(weng, "wino_warp", True, lambda: weng.warp_views(wws, list(range(N)), cfeats)),
                         None),

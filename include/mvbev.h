@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 12200: the training forward's non-finite guard (mvbev_store_gated_f32, mvbev_pack_conv3x3_weight_f32_gated, mvbev_wino_rows_split_bf16_gated), per-geometry staging boxes of the fused warp (mvbev_warp_wino_boxes, mvbev_warp_views_wino_rows_ex); 12100: MVBEV_LAYOUT_SPLIT_BF16_PIX (conv data gradients' output, the warp adjoint's input); 12000: conv1's and conv2's weight gradients from the forward's row-Winograd transforms (mvbev_wino_dy_rows_f32, mvbev_conv3x3_wgrad_wino_bf16x3); 11900: row windows (mvbev_warp_views_split_bf16_rows with the non-finite report, mvbev_warp_views_exact_rows with fp16 sources), mvbev_conv3x3_f32_ex (row-band output), mvbev_bias_relu_nonfinite_f32, mvbev_zero_gated — the non-finite guard of the multi-GPU modes and the banded exact path; 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 12200: the training forward's non-finite guard (mvbev_store_gated_f32, mvbev_pack_conv3x3_weight_f32_gated, mvbev_wino_rows_split_bf16_gated), per-geometry staging boxes of the fused warps (mvbev_warp_wino_boxes, mvbev_warp_views_wino_rows_ex, mvbev_warp_upsampled_wino_boxes, mvbev_warp_views_upsampled_wino_rows_ex); 12100: MVBEV_LAYOUT_SPLIT_BF16_PIX (conv data gradients' output, the warp adjoint's input); 12000: conv1's and conv2's weight gradients from the forward's row-Winograd transforms (mvbev_wino_dy_rows_f32, mvbev_conv3x3_wgrad_wino_bf16x3); 11900: row windows (mvbev_warp_views_split_bf16_rows with the non-finite report, mvbev_warp_views_exact_rows with fp16 sources), mvbev_conv3x3_f32_ex (row-band output), mvbev_bias_relu_nonfinite_f32, mvbev_zero_gated — the non-finite guard of the multi-GPU modes and the banded exact path; 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -348,7 +348,8 @@ int mvbev_warp_views_wino_rows(const mvbev_warp_view* views, int nviews, int64_t
  * r3_rows)][4], 16-B aligned.  Passed to mvbev_warp_views_wino_rows_ex (same views, sizes and r3_rows), every
  * block of a (view, tile) takes its staging box from the table instead of reducing it, and a block none of
  * whose samples falls inside the source (with MVBEV_WARP_DST_ZEROED) returns at once; boxes = NULL is
- * mvbev_warp_views_wino_rows.  Channels-last sources ignore the table. */
+ * mvbev_warp_views_wino_rows.  Channels-last sources (the line-per-pixel kernel, same block tiles) use it for the
+ * early return only. */
 int64_t mvbev_warp_wino_boxes_count(int64_t Wo, int64_t r3_rows);
 int mvbev_warp_wino_boxes(const mvbev_warp_view* views, int nviews, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
                           int64_t r3_rows, int32_t* boxes, void* stream);
@@ -365,6 +366,18 @@ int mvbev_warp_views_wino_rows_ex(const mvbev_warp_view* views, int nviews, int6
 int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t h,
                                          int64_t w, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int64_t r3_rows,
                                          int flags, int32_t* nonfinite, int32_t nf_tag, void* stream);
+/* (ABI 12200) As mvbev_warp_wino_boxes for the channels-last upsample warp: the per-(view, block) boxes of the
+ * blocks' 3x3 backbone windows (h x w maps, m for the upsampled H x W), once per geometry; passed to
+ * mvbev_warp_views_upsampled_wino_rows_ex (same views, sizes and r3_rows) every block of a (view, tile) takes its
+ * staging box from the table and a block none of whose samples falls inside the source (with
+ * MVBEV_WARP_DST_ZEROED) returns at once.  The table has mvbev_warp_wino_boxes_count(Wo, r3_rows) entries per
+ * view; NCHW maps ignore it. */
+int mvbev_warp_upsampled_wino_boxes(const mvbev_warp_view* views, int nviews, int64_t h, int64_t w, int64_t H,
+                                    int64_t W, int64_t Ho, int64_t Wo, int64_t r3_rows, int32_t* boxes, void* stream);
+int mvbev_warp_views_upsampled_wino_rows_ex(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C, int64_t h,
+                                            int64_t w, int64_t H, int64_t W, int64_t Ho, int64_t Wo, int64_t r3_rows,
+                                            int flags, int32_t* nonfinite, int32_t nf_tag, const int32_t* boxes,
+                                            void* stream);
 /* nonfinite (both fused warps, ABI 11600; NULL = no report): nf_tag is stored into the device int32
  * *nonfinite when a sample reads a NaN / inf feature (conservatively also when finite values overflow).
  * The fused form folds B^T (and the upsample's taps into one 3x3 window), so it cannot keep the

@@ -91,6 +91,8 @@ EXPORTS = (
     "mvbev_warp_wino_boxes_count",
     "mvbev_warp_wino_boxes",
     "mvbev_warp_views_wino_rows_ex",
+    "mvbev_warp_upsampled_wino_boxes",
+    "mvbev_warp_views_upsampled_wino_rows_ex",
 )
 BEV_SRC_F32, BEV_SRC_F16, BEV_SRC_BACKBONE_F32 = 0, 1, 2  # MVBEV_BEV_SRC_*
 BEV_SRC_CHANNELS_LAST = 16  # MVBEV_BEV_SRC_CHANNELS_LAST (flag)
@@ -238,6 +240,12 @@ def _declare(lib):
     lib.mvbev_warp_views_upsampled_wino_rows.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64,
                                                          _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_int, _p,
                                                          ctypes.c_int32, _p]
+    lib.mvbev_warp_views_upsampled_wino_rows_ex.restype = ctypes.c_int
+    lib.mvbev_warp_views_upsampled_wino_rows_ex.argtypes = lib.mvbev_warp_views_upsampled_wino_rows.argtypes[:-1] + [
+        _p, _p]
+    lib.mvbev_warp_upsampled_wino_boxes.restype = ctypes.c_int
+    lib.mvbev_warp_upsampled_wino_boxes.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64,
+                                                    _i64, _i64, _i64, _p, _p]
     lib.mvbev_warp_views_exact_f32.restype = ctypes.c_int
     lib.mvbev_warp_views_exact_f32.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
                                                _i64, _i64, _i64, _p, ctypes.c_int32, _p]

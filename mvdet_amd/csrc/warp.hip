@@ -418,6 +418,12 @@ void warp_wino_cl_kernel(const WarpArgs a, int r3_rows) {
   const WarpView& vw = a.v[view];
   const int k = tile / a.tiles_x, tx = tile - k * a.tiles_x;
   const int tid = threadIdx.x;
+  // (round 6) the per-geometry box table (the same 14 x 16 block tiles as warp_wino_kernel): a block with no
+  // sample inside the source and none non-finite returns at once (T zero-filled, skip_zero)
+  if (a.boxes && a.skip_zero) {
+    const int32_t* e = a.boxes + 4 * ((int64_t)view * a.tiles + tile);
+    if (e[1] < 0 && !(e[3] >> 30)) return;
+  }
   const int H = a.H, W = a.W;
   if (tid < kWcPix) {
     const int i = tid / kWcCols, c = tid % kWcCols;
@@ -910,7 +916,7 @@ int mvbev_warp_views_wino_rows_ex(const mvbev_warp_view* views, int nviews, int6
   }
   a.chunks = (int)ceil_div(C, cl ? kWcCh : kWarpCPB);
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
-  a.boxes = cl ? nullptr : boxes;  // (the line-per-pixel kernel has its own tiling)
+  a.boxes = boxes;  // (the line-per-pixel kernel's 14 x 16 block tiles are warp_wino_kernel's: same table)
   const dim3 grid((unsigned)a.nwg), block(cl ? kWcThreads : kWwThreads);
   if (cl)
     hipLaunchKernelGGL(warp_wino_cl_kernel, grid, block, 0, as_stream(stream), a, (int)r3_rows);

@@ -24,6 +24,10 @@ struct UpArgs {
   WarpArgs w;     // views, sizes of the UPSAMPLED image in w.H/w.W, grid, tiling
   int h, sw;      // source (backbone-resolution) height and width
   float sy, sx;   // upsample source scales in/out (h/H, w/W) as PyTorch computes them
+  // (ABI 12200) warp_up_wino_cl_kernel: the per-(view, block tile) box of the blocks' 3x3 backbone windows,
+  // int32 [nviews][tiles][4] {r0, r1, c0, c1 | nonfinite << 30} (r1 < 0: no sample inside), computed once per
+  // geometry by mvbev_warp_upsampled_wino_boxes; NULL: each block reduces its own box
+  const int32_t* boxes;
 };
 
 // a window row of 4 fp32 source pixels: 16 bytes, 4-byte aligned
@@ -358,13 +362,24 @@ __global__ __launch_bounds__(kUcThreads) void warp_up_wino_cl_kernel(const UpArg
   const int k = tile / a.tiles_x, tx = tile - k * a.tiles_x;
   const int H = a.H, W = a.W, h = ua.h, w = ua.sw;
   const int tid = threadIdx.x;
-  if (tid == 0) {
+  // (round 6) with the per-geometry table the 16 channel-group blocks of a (view, tile) take its box
+  // instead of reducing it, and a block with no sample inside the source returns at once (before any barrier)
+  int bxv[4];
+  if (ua.boxes) {
+    const int32_t* e = ua.boxes + 4 * ((int64_t)view * a.tiles + tile);
+    bxv[0] = e[0];
+    bxv[1] = e[1];
+    bxv[2] = e[2];
+    const int c1f = e[3];
+    bxv[3] = c1f & 0x3FFFFFFF;
+    if (a.skip_zero && bxv[1] < 0 && !(c1f >> 30)) return;
+  } else if (tid == 0) {
     box[0] = INT32_MAX;
     box[1] = -1;
     box[2] = INT32_MAX;
     box[3] = -1;
   }
-  __syncthreads();
+  if (!ua.boxes) __syncthreads();
   float m[9];
 #pragma unroll
   for (int q = 0; q < 9; ++q) m[q] = vw.m[q];
@@ -390,23 +405,29 @@ __global__ __launch_bounds__(kUcThreads) void warp_up_wino_cl_kernel(const UpArg
       q1 = max(q1, min(uw.cb + 2, w - 1));
     }
   }
+  if (!ua.boxes) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    r0 = min(r0, __shfl_xor(r0, o));
-    r1 = max(r1, __shfl_xor(r1, o));
-    q0 = min(q0, __shfl_xor(q0, o));
-    q1 = max(q1, __shfl_xor(q1, o));
+    for (int o = 32; o > 0; o >>= 1) {
+      r0 = min(r0, __shfl_xor(r0, o));
+      r1 = max(r1, __shfl_xor(r1, o));
+      q0 = min(q0, __shfl_xor(q0, o));
+      q1 = max(q1, __shfl_xor(q1, o));
+    }
+    if ((tid & 63) == 0 && r1 >= 0) {
+      atomicMin(&box[0], r0);
+      atomicMax(&box[1], r1);
+      atomicMin(&box[2], q0);
+      atomicMax(&box[3], q1);
+    }
   }
-  if ((tid & 63) == 0 && r1 >= 0) {
-    atomicMin(&box[0], r0);
-    atomicMax(&box[1], r1);
-    atomicMin(&box[2], q0);
-    atomicMax(&box[3], q1);
+  __syncthreads();  // (the windows in LDS; and the reduced box)
+  if (!ua.boxes) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bxv[q] = box[q];
   }
-  __syncthreads();
-  const int br0 = box[0], bc0 = box[2];
-  const int R = box[1] - br0 + 1, Cb = box[3] - bc0 + 1;  // (an all-outside block: R, Cb <= 0)
-  const bool staged = box[1] >= 0 && R * Cb <= kUcStage;  // uniform per block
+  const int br0 = bxv[0], bc0 = bxv[2];
+  const int R = bxv[1] - br0 + 1, Cb = bxv[3] - bc0 + 1;  // (an all-outside block: R, Cb <= 0)
+  const bool staged = bxv[1] >= 0 && R * Cb <= kUcStage;  // uniform per block
   // the batch item's 32-channel group (16-B aligned: host check)
   const float* gbase = static_cast<const float*>(vw.src) + (int64_t)b * vw.sB + (int64_t)grp * kUcCh;
   if (staged) {
@@ -493,6 +514,49 @@ __global__ __launch_bounds__(kUcThreads) void warp_up_wino_cl_kernel(const UpArg
       *reinterpret_cast<u32x2_t*>(o + vw.dH * 4) =
           u32x2_t{pack_bf16x2(t[xi].x - h0, t[xi].y - h1), pack_bf16x2(t[xi].z - h2, t[xi].w - h3)};
     }
+  }
+}
+
+// The per-(view, tile) backbone-window boxes of warp_up_wino_cl_kernel (ABI 12200), once per geometry: the
+// same pixels and up_window as its phase 0, {r0, r1, c0, c1 | nonfinite << 30} (r1 = -1: no sample inside).
+__global__ __launch_bounds__(kUcThreads) void up_box_kernel(const UpArgs ua, int32_t* __restrict__ boxes) {
+  __shared__ int box[5];
+  const WarpArgs& a = ua.w;
+  const int tile = blockIdx.x % a.tiles, view = blockIdx.x / a.tiles;
+  const WarpView& vw = a.v[view];
+  const int k = tile / a.tiles_x, tx = tile - k * a.tiles_x;
+  const int h = ua.h, w = ua.sw;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    box[0] = INT32_MAX;
+    box[1] = -1;
+    box[2] = INT32_MAX;
+    box[3] = -1;
+    box[4] = 0;
+  }
+  __syncthreads();
+  float m[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) m[q] = vw.m[q];
+  for (int p = tid; p < kWcPixUp; p += kUcThreads) {
+    const int i = p / kWcCols, c = p % kWcCols;
+    const int v = 12 * k - 1 + i, u = tx * kWcCols + c;
+    if (v < 0 || v >= a.Ho || u >= a.Wo) continue;
+    const UpWindow uw = up_window(m, u, v, a.Ho, a.Wo, a.H, a.W, h, w, ua.sy, ua.sx);
+    if (uw.inside) {
+      atomicMin(&box[0], uw.rb);
+      atomicMax(&box[1], min(uw.rb + 2, h - 1));
+      atomicMin(&box[2], uw.cb);
+      atomicMax(&box[3], min(uw.cb + 2, w - 1));
+    } else if (!uw.finite) {
+      atomicOr(&box[4], 1);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const int empty = box[1] < 0;
+    const int4 out = make_int4(empty ? 0 : box[0], box[1], empty ? 0 : box[2], (empty ? 0 : box[3]) | (box[4] << 30));
+    *reinterpret_cast<int4*>(boxes + 4 * ((int64_t)view * a.tiles + tile)) = out;
   }
 }
 
@@ -644,10 +708,50 @@ extern "C" int mvbev_warp_views_exact_rows(const mvbev_warp_view* views, const i
   return warp_exact(views, row0s, nviews, src_is_f16, B, C, h, w, H, W, Ho, Wo, out_rows, gate, gate_tag, stream);
 }
 
+extern "C" int mvbev_warp_views_upsampled_wino_rows_ex(const mvbev_warp_view* views, int nviews, int64_t B,
+                                                       int64_t C, int64_t h, int64_t w, int64_t H, int64_t W,
+                                                       int64_t Ho, int64_t Wo, int64_t r3_rows, int flags,
+                                                       int32_t* nonfinite, int32_t nf_tag, const int32_t* boxes,
+                                                       void* stream);
+
 extern "C" int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views, int nviews, int64_t B, int64_t C,
                                                     int64_t h, int64_t w, int64_t H, int64_t W, int64_t Ho,
                                                     int64_t Wo, int64_t r3_rows, int flags, int32_t* nonfinite,
                                                     int32_t nf_tag, void* stream) {
+  return mvbev_warp_views_upsampled_wino_rows_ex(views, nviews, B, C, h, w, H, W, Ho, Wo, r3_rows, flags, nonfinite,
+                                                 nf_tag, nullptr, stream);
+}
+
+extern "C" int mvbev_warp_upsampled_wino_boxes(const mvbev_warp_view* views, int nviews, int64_t h, int64_t w,
+                                               int64_t H, int64_t W, int64_t Ho, int64_t Wo, int64_t r3_rows,
+                                               int32_t* boxes, void* stream) {
+  using namespace mvbev;
+  if (!views || !boxes) return MVBEV_ERR_NULL;
+  if (nviews <= 0 || h <= 0 || w <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 || r3_rows <= 0) return MVBEV_ERR_RANK;
+  if (nviews > kWarpMaxViews || 3 * r3_rows < Ho || H < h || W < w || h >= 32768 || w >= 16384) return MVBEV_ERR_SHAPE;
+  if (reinterpret_cast<uintptr_t>(boxes) & 15) return MVBEV_ERR_ALIGN;
+  UpArgs ua = {};
+  WarpArgs& a = ua.w;
+  for (int i = 0; i < nviews; ++i)
+    for (int q = 0; q < 9; ++q) a.v[i].m[q] = views[i].m[q];
+  a.nviews = nviews;
+  a.H = (int)H, a.W = (int)W, a.Ho = (int)Ho, a.Wo = (int)Wo;
+  a.tiles_x = (int)ceil_div(Wo, kWcCols);
+  a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);
+  ua.h = (int)h, ua.sw = (int)w;
+  ua.sy = (float)h / (float)H;
+  ua.sx = (float)w / (float)W;
+  hipLaunchKernelGGL(up_box_kernel, dim3((unsigned)(a.tiles * nviews)), dim3(kUcThreads), 0, as_stream(stream), ua,
+                     boxes);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+extern "C" int mvbev_warp_views_upsampled_wino_rows_ex(const mvbev_warp_view* views, int nviews, int64_t B,
+                                                       int64_t C, int64_t h, int64_t w, int64_t H, int64_t W,
+                                                       int64_t Ho, int64_t Wo, int64_t r3_rows, int flags,
+                                                       int32_t* nonfinite, int32_t nf_tag, const int32_t* boxes,
+                                                       void* stream) {
   using namespace mvbev;
   if (flags & ~MVBEV_WARP_DST_ZEROED) return MVBEV_ERR_SHAPE;
   if (!views) return MVBEV_ERR_NULL;
@@ -695,6 +799,7 @@ extern "C" int mvbev_warp_views_upsampled_wino_rows(const mvbev_warp_view* views
     a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);
     a.chunks = (int)(C / kUcCh);
     a.nwg = a.tiles * a.chunks * a.B * a.nviews;
+    ua.boxes = boxes;
     hipLaunchKernelGGL(warp_up_wino_cl_kernel, dim3((unsigned)a.nwg), dim3(kUcThreads), 0, as_stream(stream), ua,
                        (int)r3_rows);
     MVBEV_CHECK_LAUNCH();

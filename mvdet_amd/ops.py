@@ -801,9 +801,11 @@ def wino_rows(x: torch.Tensor, desc, t: torch.Tensor, group_mask: Optional[torch
     return t
 
 
-def warp_wino_boxes(m_norms, src_hw, grid_hw, device) -> torch.Tensor:
+def warp_wino_boxes(m_norms, src_hw, grid_hw, device, backbone_hw=None) -> torch.Tensor:
     """``mvbev_warp_wino_boxes``: the per-(view, block) staging boxes of the NCHW fused warp + B^T for the
-    whole-grid T (r3 rows 4 * ceil(Ho / 12)) — geometry only, computed once and reused every frame."""
+    whole-grid T (r3 rows 4 * ceil(Ho / 12)) — geometry only, computed once and reused every frame.
+    ``backbone_hw``: the channels-last fused upsample warp's boxes of its 3x3 windows in the backbone maps
+    (``mvbev_warp_upsampled_wino_boxes``; ``src_hw`` = the upsampled size)."""
     Ho, Wo = int(grid_hw[0]), int(grid_hw[1])
     r3 = 4 * (-(-Ho // 12))
     n = len(m_norms)
@@ -814,6 +816,11 @@ def warp_wino_boxes(m_norms, src_hw, grid_hw, device) -> torch.Tensor:
     arr = (_native.WarpView * n)()
     for i, m in enumerate(m_norms):
         arr[i].m = (ctypes.c_float * 9)(*torch.as_tensor(m, dtype=torch.float32).reshape(9).tolist())
+    if backbone_hw is not None:
+        st = lib.mvbev_warp_upsampled_wino_boxes(arr, n, int(backbone_hw[0]), int(backbone_hw[1]), int(src_hw[0]),
+                                                 int(src_hw[1]), Ho, Wo, r3, boxes.data_ptr(), _stream(boxes))
+        _native.check(st, "mvbev_warp_upsampled_wino_boxes")
+        return boxes
     st = lib.mvbev_warp_wino_boxes(arr, n, int(src_hw[0]), int(src_hw[1]), Ho, Wo, r3, boxes.data_ptr(),
                                    _stream(boxes))
     _native.check(st, "mvbev_warp_wino_boxes")
@@ -859,17 +866,17 @@ def warp_views_wino_rows_into(srcs, m_norms, t: torch.Tensor, slots, Cs: int, K:
         arr[i].m = (ctypes.c_float * 9)(*mm)
     flags = (_native.WARP_DST_ZEROED if dst_zeroed else 0) | (_native.WARP_SRC_F16 if dtype == torch.float16 else 0)
     fp, ft = _gate(nonfinite)
-    if up_hw is not None:
-        st = _native.load().mvbev_warp_views_upsampled_wino_rows(arr, n, B, C, H, W, int(up_hw[0]), int(up_hw[1]),
-                                                                 Ho, Wo, r3, flags, fp, ft, _stream(t))
-        _native.check(st, "mvbev_warp_views_upsampled_wino_rows")
-        return
     if boxes is not None:  # (from warp_wino_boxes with the same matrices, in the same view order)
         _require_cuda(boxes)
         if boxes.dtype != torch.int32 or tuple(boxes.shape[:1]) != (n,) or not boxes.is_contiguous():
             raise ValueError("boxes must be warp_wino_boxes' int32 [views, tiles, 4] table of these views")
-    st = _native.load().mvbev_warp_views_wino_rows_ex(arr, n, B, C, H, W, Ho, Wo, r3, flags, fp, ft,
-                                                      None if boxes is None else boxes.data_ptr(), _stream(t))
+    bp = None if boxes is None else boxes.data_ptr()
+    if up_hw is not None:
+        st = _native.load().mvbev_warp_views_upsampled_wino_rows_ex(arr, n, B, C, H, W, int(up_hw[0]), int(up_hw[1]),
+                                                                    Ho, Wo, r3, flags, fp, ft, bp, _stream(t))
+        _native.check(st, "mvbev_warp_views_upsampled_wino_rows_ex")
+        return
+    st = _native.load().mvbev_warp_views_wino_rows_ex(arr, n, B, C, H, W, Ho, Wo, r3, flags, fp, ft, bp, _stream(t))
     _native.check(st, "mvbev_warp_views_wino_rows_ex")
 
 

@@ -374,15 +374,18 @@ class ProjectFuse:
         ops.warp_views_wino_rows_into(list(feats), [self.m_norm_cpu[c] for c in cams], ws.wino_t,
                                       [self.slot_of[c] for c in cams], self.Cs, self.S * self.Cs, H, W,
                                       dst_zeroed=True, up_hw=up_hw, nonfinite=nonfinite,
-                                      boxes=None if up_hw is not None else self._wino_boxes(ws.slab.device, cams))
+                                      boxes=self._wino_boxes(ws.slab.device, cams, None if up_hw is None else
+                                                             tuple(feats[0].shape[2:])))
         ws.t_from_warp = True
 
-    def _wino_boxes(self, device, cams) -> torch.Tensor:
-        """The fused warp's per-(view, block) staging boxes for these cameras (geometry only, cached)."""
-        key = ("boxes", str(torch.device(device)), tuple(cams))
+    def _wino_boxes(self, device, cams, backbone_hw=None) -> torch.Tensor:
+        """The fused warps' per-(view, block) staging boxes for these cameras (geometry only, cached):
+        ``ops.warp_wino_boxes``; ``backbone_hw``: of the upsample warp's backbone windows."""
+        key = ("boxes", str(torch.device(device)), tuple(cams), backbone_hw)
         b = self._masks.get(key)
         if b is None:
-            b = ops.warp_wino_boxes([self.m_norm_cpu[c] for c in cams], self.src_hw, self.grid_hw, device)
+            b = ops.warp_wino_boxes([self.m_norm_cpu[c] for c in cams], self.src_hw, self.grid_hw, device,
+                                    backbone_hw=backbone_hw)
             self._masks[key] = b
         return b
 

@@ -297,13 +297,15 @@ def test_fused_warp_channels_last_matches_nchw(cfg, C, B):
     _assert_same_t(_t_value(a, Wo), _t_value(b, Wo))
 
 
-@pytest.mark.parametrize("cfg,C,B,half", [(1, 32, 1, False), (2, 64, 2, False), (2, 24, 1, False), (4, 16, 2, True)])
-def test_fused_warp_box_table_is_bitwise_the_block_reduction(cfg, C, B, half):
+@pytest.mark.parametrize("cfg,C,B,half,cl", [(1, 32, 1, False, False), (2, 64, 2, False, False), (2, 24, 1, False, False),
+                                           (4, 16, 2, True, False), (2, 64, 2, False, True), (1, 32, 1, False, True)])
+def test_fused_warp_box_table_is_bitwise_the_block_reduction(cfg, C, B, half, cl):
     """Round 6: the NCHW fused warp + B^T with the per-geometry staging boxes (``mvbev_warp_wino_boxes`` ->
     ``mvbev_warp_views_wino_rows_ex``) writes bitwise the T of the per-block box reduction (same box, same
     staged / direct choice, same arithmetic), with skip_zero on and off (blocks without an inside sample
     return at once), a view with non-finite geometry (its NaN T still written), an inf feature (the
-    non-finite report), B = 2 and fp16 sources; the table marks the empty and non-finite blocks."""
+    non-finite report), B = 2 and fp16 sources; the table marks the empty and non-finite blocks.  ``cl``:
+    channels-last sources (warp_wino_cl_kernel, the same block tiles: the table's early return)."""
     from mvdet_amd import ops, synthetic
     from mvdet_amd.geometry import kornia_src_norm_from_dst_norm, projection_matrices
     spec = synthetic.CONFIGS[cfg]
@@ -318,6 +320,8 @@ def test_fused_warp_box_table_is_bitwise_the_block_reduction(cfg, C, B, half):
     feats[0][B - 1, C - 1, up[0] // 2, up[1] // 2] = float("inf")
     if half:
         feats = [f.half() for f in feats]
+    if cl:  # the line-per-pixel kernel (channels-last sources): the table's early return only
+        feats = [f.contiguous(memory_format=torch.channels_last) for f in feats]
     Ho, Wo = grid
     r3 = 4 * (-(-Ho // 12))
     boxes = ops.warp_wino_boxes(ms, up, grid, DEV)
@@ -334,6 +338,43 @@ def test_fused_warp_box_table_is_bitwise_the_block_reduction(cfg, C, B, half):
                                           nonfinite=(flag, 5), boxes=bx)
             outs.append((t.view(torch.int16).cpu(), int(flag.item())))
         assert outs[0][1] == outs[1][1] == 5
+        assert torch.equal(outs[0][0], outs[1][0]), f"skip_zero={zeroed}: T differs with the box table"
+
+
+@pytest.mark.parametrize("cfg,C,B", [(1, 32, 1), (2, 64, 2), (5, 32, 1)])
+def test_fused_upsample_warp_box_table_is_bitwise_the_block_reduction(cfg, C, B):
+    """Round 6: the channels-last fused upsample warp + B^T (the detector's default path) with the per-geometry
+    backbone-window boxes (``mvbev_warp_upsampled_wino_boxes`` -> ``..._upsampled_wino_rows_ex``) writes bitwise
+    the T of the per-block reduction: skip_zero on and off, a view with non-finite geometry, an inf feature
+    (the non-finite report), B = 2."""
+    from mvdet_amd import ops, synthetic
+    from mvdet_amd.geometry import kornia_src_norm_from_dst_norm, projection_matrices
+    spec = synthetic.CONFIGS[cfg]
+    ds = spec["make"]()
+    N = ds.num_cam
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    hb = tuple(u // 3 for u in up)
+    ms = [kornia_src_norm_from_dst_norm(M.float().reshape(1, 3, 3), up, grid)[0] for M in projection_matrices(ds)]
+    ms[-1] = ms[-1].clone()
+    ms[-1][0, 2] = float("inf")
+    low = [synthetic.backbone_features(B, C, hb, seed=91 + v, device=DEV) for v in range(N)]
+    low[0][B - 1, C - 1, hb[0] // 2, hb[1] // 2] = float("inf")
+    low = [f.contiguous(memory_format=torch.channels_last) for f in low]
+    Ho, Wo = grid
+    r3 = 4 * (-(-Ho // 12))
+    boxes = ops.warp_wino_boxes(ms, up, grid, DEV, backbone_hw=hb)
+    bc = boxes.cpu()
+    assert (bc[:-1, :, 1] < 0).any() and (bc[:-1, :, 1] >= 0).any() and ((bc[-1, :, 3] >> 30) == 1).all()
+    numel = B * (N * C // 8) * 5 * r3 * Wo * 16
+    for zeroed in (False, True):
+        outs = []
+        for bx in (None, boxes):
+            t = torch.zeros(numel, dtype=torch.bfloat16, device=DEV)
+            flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+            ops.warp_views_wino_rows_into(low, ms, t, list(range(N)), C, N * C, Ho, Wo, dst_zeroed=zeroed,
+                                          up_hw=up, nonfinite=(flag, 3), boxes=bx)
+            outs.append((t.view(torch.int16).cpu(), int(flag.item())))
+        assert outs[0][1] == outs[1][1] == 3
         assert torch.equal(outs[0][0], outs[1][0]), f"skip_zero={zeroed}: T differs with the box table"
 
 

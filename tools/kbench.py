@@ -188,8 +188,10 @@ def main():
             "warpw": (lambda: _with(weng, "wino_warp", True, lambda: weng.warp_views(wws, list(range(N)), feats)),
                       None),  # warp + B^T in one pass (wino_warp; leaves T from the warp, run it last)
             # round 6: the same without the per-geometry box table (each block reduces its own box)
-            "warpw0": (lambda: _with(weng, "_wino_boxes", lambda dev, cams: None, lambda: _with(
+            "warpw0": (lambda: _with(weng, "_wino_boxes", lambda dev, cams, bb=None: None, lambda: _with(
                 weng, "wino_warp", True, lambda: weng.warp_views(wws, list(range(N)), feats))), None),
+            "warpwcl0": (lambda: _with(weng, "_wino_boxes", lambda dev, cams, bb=None: None, lambda: _with(
+                weng, "wino_warp", True, lambda: weng.warp_views(wws, list(range(N)), cfeats))), None),
             # the same on channels-last features (warp_wino_cl_kernel)
             "warpwcl": (lambda: _with(weng, "wino_warp", True, lambda: weng.warp_views(wws, list(range(N)), cfeats)),
                         None),
@@ -200,6 +202,8 @@ def main():
             # NCHW maps copied to channels-last first (cl_upsample), then the line-per-pixel kernel
             "warpupwt": (lambda: _with(weng, "cl_upsample", True, lambda: _with(weng, "wino_warp", True,
                          lambda: weng.warp_views_upsampled(wws, list(range(N)), bfeats))), None),
+            "warpupwcl0": (lambda: _with(weng, "_wino_boxes", lambda dev, cams, bb=None: None, lambda: _with(
+                weng, "wino_warp", True, lambda: weng.warp_views_upsampled(wws, list(range(N)), cbfeats))), None),
             "warpupwcl": (lambda: _with(weng, "wino_warp", True,
                                         lambda: weng.warp_views_upsampled(wws, list(range(N)), cbfeats)), None),
             "warpupw": (lambda: _with(weng, "wino_warp", True,

@@ -484,10 +484,14 @@ def run_train_step(config: int, precision: str, steps: int, warmup: int, with_to
         if update:
             optimizer_step()
 
+    # the same step without the update (packs reused from the cache): the repacking's cost is the difference.
+    # Both after warm-up steps of the other (the device's clock drifts over the first seconds of a run:
+    # back to back, the first variant timed runs its MFMA kernels up to ~15 % slower)
+    for _ in range(warmup):
+        native_step()
+    nu = run(lambda: native_step(update=False), steps, warmup, hook_stages=True)
     res["native"] = run(native_step, steps, warmup, hook_stages=True)
     res["native"]["optimizer"] = "SGD(lr=1e-4, momentum=0.5, weight_decay=5e-4).step() per step (weights re-packed every step)"
-    # the same step without the update (packs reused from the cache): the repacking's cost is the difference
-    nu = run(lambda: native_step(update=False), steps, warmup, hook_stages=True)
     res["native_no_update"] = nu
     res["weight_update_cost_ms"] = round(res["native"]["ms_per_step"] - nu["ms_per_step"], 3)
     if with_torch:

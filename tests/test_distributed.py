@@ -326,3 +326,25 @@ def test_owner_affine_part_dealing():
             home = sum(owner[v] == r for r, ps in enumerate(assign) for v, _ in ps)
             plain = mp_model.balanced_parts(w, P, 512, k=k, affinity=0.0)[0]
             assert home >= sum(owner[v] == r for r, ps in enumerate(plain) for v, _ in ps)
+
+
+def test_slice_exchange_cost_model():
+    """mp_model's slice-exchange pricing (round 6): per (sender, receiver) link the bytes of the parts held away
+    from their owner; whole views (k = 1) move nothing; the model's chosen split for the driver's node at cfg2
+    (P = 8) cuts every view into 64-channel parts and each link carries at most one 3.7 MB backbone-map slice."""
+    from mvdet_amd import mp_model
+    w = [0.37, 0.73, 0.82, 0.6, 0.58, 0.9, 0.82]
+    for P in (2, 4, 8):
+        owner = mp_model.view_owners([x + 0.05 for x in w], P)
+        a1, _ = mp_model.balanced_parts(w, P, 512, k=1)
+        assert mp_model.fetch_link_bytes(a1, owner, P, 1.0).sum() == 0
+        a8, cp = mp_model.balanced_parts(w, P, 512, k=8)
+        links = mp_model.fetch_link_bytes(a8, owner, P, 1.0)
+        moved = sum(owner[v] != q for q, ps in enumerate(a8) for v, _ in ps)
+        assert links.sum() == moved and np.all(np.diag(links) == 0)
+    pr = mp_model.predict_config(2, 8)["partial"]
+    assert pr["parts_k"] == 8 and pr["fetch"] > 0
+    part = 4.0 * 1 * 64 * mp_model.backbone_pixels(2)
+    assert abs(part - 64 * 90 * 160 * 4) < 1
+    assert pr["fetch_bytes_max_rank"] <= 8 * part
+    assert mp_model.predict_config(2, 2)["partial"]["fetch"] == 0.0  # k = 1 at P = 2: no slice moves

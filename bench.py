@@ -62,12 +62,17 @@ def head_params(num_cam, seed, C):
 
 
 def cpu_baseline(ds, B, C, pm, params, frames: int, config: int = 2, warmups: int = 2, single_frames: int = 3,
-                 single_warmups: int = 1):
+                 single_warmups: int = 1, single_band: int = 1):
     """The oracle (reference CPU path restated over torch-CPU ops) on the host cores:
     ``warmups`` untimed frames, then the median of ``frames`` timed ones (2 warm-ups,
     >= 5 timed, median); the reference's own one-thread setting (main.py:3) as the median of
-    ``single_frames`` after ``single_warmups`` warm-ups (0 = skipped; the large configs take one frame
-    right after the multi-thread ones, ~60-70 s of one core each)."""
+    ``single_frames`` after ``single_warmups`` warm-ups (0 = skipped).  ``single_band`` > 1 bounds the
+    one-thread sample of the large configs (a whole cfg3 / cfg5 frame is ~100 s of one core): the same
+    frame over the output rows [0, H / single_band) (the warp into that band, the three convs over it with
+    their zero padding), its time x H / band rows; every output row costs the same
+    grid_sample + conv work, so the scaled band is the frame's time less one call's fixed overheads (checked
+    on cfg2 here: the x4 band gave 0.0559 frames/s against 0.0525 for whole frames, i.e. it errs ~6% in the
+    CPU's favour)."""
     from mvdet_amd import synthetic
     from oracle import cpu_path
     threads = len(os.sched_getaffinity(0))
@@ -80,11 +85,15 @@ def cpu_baseline(ds, B, C, pm, params, frames: int, config: int = 2, warmups: in
     mats = [M.numpy() for M in pm]
     grid = tuple(ds.reducedgrid_shape)
 
-    def frame(stages=None):
+    def frame(stages=None, band=1):
+        g, ms = grid, mats
+        if band > 1:  # output rows [0, H / band): the band starts at row 0, so the matrices stay
+            g = (max(1, grid[0] // band), grid[1])
         t = time.perf_counter()
-        cpu_path.project_fuse(feats, mats, grid, tp, timings=stages)
-        dt = time.perf_counter() - t
-        progress(f"cpu baseline cfg{config}: frame {dt:.2f} s ({torch.get_num_threads()} threads)")
+        cpu_path.project_fuse(feats, ms, g, tp, timings=stages)
+        dt = (time.perf_counter() - t) * (grid[0] / g[0])
+        progress(f"cpu baseline cfg{config}: frame {dt:.2f} s ({torch.get_num_threads()} threads"
+                 + (f", rows [0, {g[0]}) x {grid[0] / g[0]:.2f})" if band > 1 else ")"))
         return dt
 
     with torch.no_grad():
@@ -97,13 +106,16 @@ def cpu_baseline(ds, B, C, pm, params, frames: int, config: int = 2, warmups: in
             # the reference's own setting (main.py:3, OMP_NUM_THREADS=1)
             torch.set_num_threads(1)
             for _ in range(single_warmups):
-                frame()
-            t1 = [frame() for _ in range(single_frames)]
+                frame(band=single_band)
+            t1 = [frame(band=single_band) for _ in range(single_frames)]
             torch.set_num_threads(threads)
+            rows = max(1, grid[0] // single_band)
             single = dict(value=round(B / float(np.median(t1)), 4), unit="frames/s", cores=1,
                           sample=f"median of {single_frames} frame(s) after {single_warmups} warm-up(s) with "
                                  "torch.set_num_threads(1) (main.py:3 OMP_NUM_THREADS=1)"
-                                 + ("" if single_warmups else " (right after the multi-thread frames)"))
+                                 + ("" if single_warmups else " (right after the multi-thread frames)")
+                                 + (f"; bounded sample: output rows [0, {rows}) of {grid[0]} (warp + 3 convs over "
+                                    f"the band), time x {grid[0] / rows:.2f}" if rows < grid[0] else ""))
     dt = float(np.median(times))
     return dict(value=round(B / dt, 4), unit="frames/s", cores=threads, kind="port", single_thread=single,
                 sample=f"median of {frames} frame(s) (B={B}) of the bench workload after {warmups} warm-up(s) "
@@ -649,11 +661,11 @@ def main():
         # the size the north star quotes its >= 5x at 1 GPU on (cfg3: 7 views, 480 x 1440 grid): the same
         # path, its roofline, and a CPU baseline on BASELINE.md:26's sample (2 warm-ups + the median of 5
         # frames, ~18 s of CPU work per frame at 16 threads)
-        subs.append((args.north_star_cfg, dict(frames=5, warmups=2, single_frames=1, single_warmups=0)))
+        subs.append((args.north_star_cfg, dict(frames=5, warmups=2, single_frames=1, single_warmups=0, single_band=4)))
     if args.roofline_cfg and args.roofline_cfg not in (args.config, args.north_star_cfg):
         # BASELINE's "rocprof roofline run" config (8 views at 4K): 1 warm-up + the median of 3 frames
         # (~16 s of CPU work per frame)
-        subs.append((args.roofline_cfg, dict(frames=3, warmups=1, single_frames=1, single_warmups=0)))
+        subs.append((args.roofline_cfg, dict(frames=3, warmups=1, single_frames=1, single_warmups=0, single_band=4)))
     if args.batch_cfg and args.batch_cfg not in (args.config, args.north_star_cfg, args.roofline_cfg):
         # BASELINE configs[3]: MultiviewX 6 views, B = 8, fp16 features (C = 512, the reference's ResNet-18
         # width); its CPU baseline on B = 1 frames (1 warm-up + the median of 3), frames/s = 1 / median

@@ -497,13 +497,27 @@ def run_train_step(config: int, precision: str, steps: int, warmup: int, with_to
             optimizer_step()
 
     # the same step without the update (packs reused from the cache): the repacking's cost is the difference.
-    # Both after warm-up steps of the other (the device's clock drifts over the first seconds of a run:
-    # back to back, the first variant timed runs its MFMA kernels up to ~15 % slower)
+    # Three interleaved rounds (no-update / update, update / no-update, no-update / update), each variant's
+    # median run reported: one pair timed back to back swung by ±0.3-0.9 ms between boxes and orders
+    # (round 6: the first-timed variant ran its MFMA kernels up to ~15 % slower on some boxes, on others not)
     for _ in range(warmup):
         native_step()
-    nu = run(lambda: native_step(update=False), steps, warmup, hook_stages=True)
-    res["native"] = run(native_step, steps, warmup, hook_stages=True)
+    runs = {"u": [], "nu": []}
+    fns = {"u": native_step, "nu": lambda: native_step(update=False)}
+    for order in (("nu", "u"), ("u", "nu"), ("nu", "u")):
+        for v in order:
+            runs[v].append(run(fns[v], steps, warmup, hook_stages=True))
+
+    def median_run(rs):
+        return sorted(rs, key=lambda r: r["ms_per_step"])[len(rs) // 2]
+
+    nu = median_run(runs["nu"])
+    nu["runs_ms"] = [r["ms_per_step"] for r in runs["nu"]]
+    res["native"] = median_run(runs["u"])
+    res["native"]["runs_ms"] = [r["ms_per_step"] for r in runs["u"]]
     res["native"]["optimizer"] = "SGD(lr=1e-4, momentum=0.5, weight_decay=5e-4).step() per step (weights re-packed every step)"
+    res["native"]["sample"] = (f"median of 3 runs of {steps} steps, interleaved with the no-update runs "
+                               "(nu/u, u/nu, nu/u)")
     res["native_no_update"] = nu
     res["weight_update_cost_ms"] = round(res["native"]["ms_per_step"] - nu["ms_per_step"], 3)
     if with_torch:

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 12200: the training forward's non-finite guard (mvbev_store_gated_f32, mvbev_pack_conv3x3_weight_f32_gated, mvbev_wino_rows_split_bf16_gated), per-geometry staging boxes of the fused warps (mvbev_warp_wino_boxes, mvbev_warp_views_wino_rows_ex, mvbev_warp_upsampled_wino_boxes, mvbev_warp_views_upsampled_wino_rows_ex); 12100: MVBEV_LAYOUT_SPLIT_BF16_PIX (conv data gradients' output, the warp adjoint's input); 12000: conv1's and conv2's weight gradients from the forward's row-Winograd transforms (mvbev_wino_dy_rows_f32, mvbev_conv3x3_wgrad_wino_bf16x3); 11900: row windows (mvbev_warp_views_split_bf16_rows with the non-finite report, mvbev_warp_views_exact_rows with fp16 sources), mvbev_conv3x3_f32_ex (row-band output), mvbev_bias_relu_nonfinite_f32, mvbev_zero_gated — the non-finite guard of the multi-GPU modes and the banded exact path; 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 12300: mvbev_coord_term_f32 (conv1's coord term as one VALU pass); 12200: the training forward's non-finite guard (mvbev_store_gated_f32, mvbev_pack_conv3x3_weight_f32_gated, mvbev_wino_rows_split_bf16_gated), per-geometry staging boxes of the fused warps (mvbev_warp_wino_boxes, mvbev_warp_views_wino_rows_ex, mvbev_warp_upsampled_wino_boxes, mvbev_warp_views_upsampled_wino_rows_ex); 12100: MVBEV_LAYOUT_SPLIT_BF16_PIX (conv data gradients' output, the warp adjoint's input); 12000: conv1's and conv2's weight gradients from the forward's row-Winograd transforms (mvbev_wino_dy_rows_f32, mvbev_conv3x3_wgrad_wino_bf16x3); 11900: row windows (mvbev_warp_views_split_bf16_rows with the non-finite report, mvbev_warp_views_exact_rows with fp16 sources), mvbev_conv3x3_f32_ex (row-band output), mvbev_bias_relu_nonfinite_f32, mvbev_zero_gated — the non-finite guard of the multi-GPU modes and the banded exact path; 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -236,6 +236,13 @@ int mvbev_conv3x3_f32_ex(const float* x, const mvbev_conv_desc* desc, const floa
  * pre-activation — persp_trans_detector.py:51 — and its non-finite guard). */
 int mvbev_bias_relu_nonfinite_f32(float* y, const float* init, int64_t B, int64_t C, int64_t rows, int64_t W,
                                   int64_t H, int64_t row0, int relu, int32_t* flag, int32_t tag, void* stream);
+/* conv1's coord term (ABI 12300; persp_trans_detector.py:103-112 coord map, :77 its concat, :51 conv1):
+ * out [Cout][H][W] fp32 = bias (NULL: 0) + conv2d over the two coord channels [x = col / (W-1) * 2 - 1,
+ * y = row / (H-1) * 2 - 1] (float64 then float, zero padding 1) with conv1's weights w1 [Cout][cin][3][3]
+ * at input channels coord_c0 (x) and coord_c0 + 1 (y).  The input-independent part of conv1, added as its
+ * accumulators' initial value. */
+int mvbev_coord_term_f32(const float* w1, int64_t cin, int64_t coord_c0, const float* bias, int64_t Cout, int64_t H,
+                         int64_t W, float* out, void* stream);
 /* gate (this entry point, mvbev_conv3x3_cout1_f32, mvbev_warp_views_exact_f32; ABI 11600): a device
  * int32; when non-NULL the launch does its work only if *gate == gate_tag at the time it runs (every
  * workgroup exits at once otherwise) — a decision taken on the device in stream order, so a caller

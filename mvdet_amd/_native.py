@@ -80,6 +80,7 @@ EXPORTS = (
     "mvbev_warp_views_exact_rows",
     "mvbev_conv3x3_f32_ex",
     "mvbev_bias_relu_nonfinite_f32",
+    "mvbev_coord_term_f32",
     "mvbev_zero_gated",
     "mvbev_wino_dy_rows_bytes",
     "mvbev_wino_dy_rows_f32",
@@ -259,6 +260,8 @@ def _declare(lib):
     lib.mvbev_conv3x3_f32_ex.restype = ctypes.c_int
     lib.mvbev_conv3x3_f32_ex.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64, ctypes.c_int,
                                          ctypes.c_int, _p, _i64, _p, ctypes.c_int32, _p]
+    lib.mvbev_coord_term_f32.restype = ctypes.c_int
+    lib.mvbev_coord_term_f32.argtypes = [_p, _i64, _i64, _p, _i64, _i64, _i64, _p, _p]
     lib.mvbev_bias_relu_nonfinite_f32.restype = ctypes.c_int
     lib.mvbev_bias_relu_nonfinite_f32.argtypes = [_p, _p, _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_int, _p,
                                                   ctypes.c_int32, _p]

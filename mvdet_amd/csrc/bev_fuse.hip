@@ -32,7 +32,7 @@ constexpr int64_t kKC = MVBEV_CONV_KC;
 constexpr int64_t kTileW = MVBEV_CONV_TILE_W;
 constexpr size_t kAlign = 256;
 
-enum Region { R_MAP1, R_MAPC, R_PACK1, R_PACK2, R_PACKC, R_CIN, R_INIT, R_MASK, R_ORDER, R_NF, R_BIG, R_Y1, R_T2,
+enum Region { R_MAP1, R_PACK1, R_PACK2, R_INIT, R_MASK, R_ORDER, R_NF, R_BIG, R_Y1, R_T2,
               R_GFLAG, R_GPACK1, R_GPACK2, R_GSLAB, R_P3, R_COUNT };
 static_assert(R_COUNT <= 24, "mvbev_bev_plan.off");
 
@@ -163,11 +163,8 @@ int mvbev_bev_plan_init(const mvbev_bev_geometry* g, mvbev_bev_plan* p) {
   const size_t slab_bytes = (size_t)g->num_views * g->B * p->Cs * g->Ho * g->Wo * 4;
   size_t sz[R_COUNT] = {};
   sz[R_MAP1] = (size_t)K * 4;
-  sz[R_MAPC] = (size_t)kKC * 4;
   sz[R_PACK1] = std::max(mvbev_conv3x3_packed_bytes_wino(kMid, K), mvbev_conv3x3_packed_bytes_bf16x3(kMid, K));
   sz[R_PACK2] = std::max(mvbev_conv3x3_packed_bytes_wino(kMid, kMid), mvbev_conv3x3_packed_bytes_bf16x3(kMid, kMid));
-  sz[R_PACKC] = 4 * mvbev_conv3x3_packed_floats(kMid, kKC);
-  sz[R_CIN] = (size_t)kKC * g->Ho * g->Wo * 4;
   sz[R_INIT] = (size_t)kMid * g->Ho * g->Wo * 4;
   sz[R_MASK] = (size_t)p->tiles * 4;
   sz[R_ORDER] = (size_t)g->B * p->tiles * 4;
@@ -212,15 +209,12 @@ int mvbev_bev_fuse_prepare(mvbev_bev_plan* p, const float* w1, const float* b1, 
   hipStream_t s = static_cast<hipStream_t>(stream);
   const int64_t K = g.num_views * p->Cs, nc = g.num_views * g.C, cin = nc + 2;
   // conv1's channel map: slot s channel c -> module channel s*C + c (view-major concat, :77)
-  std::vector<int32_t> map1((size_t)K), mapc((size_t)kKC, -1);
+  std::vector<int32_t> map1((size_t)K);
   for (int64_t k = 0; k < K; ++k) {
     const int64_t sl = k / p->Cs, c = k % p->Cs;
     map1[(size_t)k] = c < g.C ? (int32_t)(sl * g.C + c) : -1;
   }
-  mapc[0] = (int32_t)nc;
-  mapc[1] = (int32_t)(nc + 1);
-  if (hipMemcpyAsync(at<int32_t>(ws, p, R_MAP1), map1.data(), map1.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess ||
-      hipMemcpyAsync(at<int32_t>(ws, p, R_MAPC), mapc.data(), mapc.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess) {
+  if (hipMemcpyAsync(at<int32_t>(ws, p, R_MAP1), map1.data(), map1.size() * 4, hipMemcpyHostToDevice, s) != hipSuccess) {
     (void)hipStreamSynchronize(s);
     return MVBEV_ERR_HIP;
   }
@@ -279,18 +273,8 @@ int mvbev_bev_fuse_prepare(mvbev_bev_plan* p, const float* w1, const float* b1, 
     if (hipMemsetAsync(at<void>(ws, p, R_GSLAB), 0, p->off[R_GSLAB + 1] - p->off[R_GSLAB], s) != hipSuccess)
       return MVBEV_ERR_HIP;
   }
-  BEV_TRY(mvbev_pack_conv3x3_weight_f32(w1, kMid, cin, at<int32_t>(ws, p, R_MAPC), kKC, at<float>(ws, p, R_PACKC),
-                                        stream));
-  float* cinp = at<float>(ws, p, R_CIN);
-  if (hipMemsetAsync(cinp, 0, (size_t)kKC * g.Ho * g.Wo * 4, s) != hipSuccess) return MVBEV_ERR_HIP;
-  const int64_t cst[4] = {kKC * g.Ho * g.Wo, g.Ho * g.Wo, g.Wo, 1};
-  BEV_TRY(mvbev_fill_coord_map_f32(cinp, 1, g.Ho, g.Wo, cst, stream));
-  mvbev_conv_desc dc;
-  dc.B = 1; dc.K = kKC; dc.H = g.Ho; dc.W = g.Wo; dc.group = kKC; dc.group_stride = 0;
-  dc.batch_stride = kKC * g.Ho * g.Wo; dc.in_row0 = 0; dc.in_rows = g.Ho; dc.out_row0 = 0; dc.out_rows = g.Ho;
-  // coord term = conv1 bias + conv1 over the two coord channels (:21, :77): input-independent
-  BEV_TRY(mvbev_conv3x3_f32(cinp, &dc, at<float>(ws, p, R_PACKC), b1, nullptr, kMid, 1, 0, at<float>(ws, p, R_INIT),
-                            nullptr, 0, stream));
+  // coord term = conv1 bias + conv1 over the two coord channels (:21, :77): input-independent (ABI 12300)
+  BEV_TRY(mvbev_coord_term_f32(w1, cin, nc, b1, kMid, g.Ho, g.Wo, at<float>(ws, p, R_INIT), stream));
   // T / the slab: zero once; later warps skip the pixels whose samples fall outside the source
   if (hipMemsetAsync(at<void>(ws, p, R_BIG), 0, p->off[R_BIG + 1] - p->off[R_BIG], s) != hipSuccess)
     return MVBEV_ERR_HIP;

@@ -249,6 +249,30 @@ def fill_coord_map(dst: torch.Tensor) -> torch.Tensor:
     return dst
 
 
+def coord_term(weight: torch.Tensor, bias: Optional[torch.Tensor], coord_c0: int, hw,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """conv1's coord term [Cout, H, W] (``mvbev_coord_term_f32``): ``bias`` + conv2d of the coord map
+    (``persp_trans_detector.py:103-112``, zero padding 1) with ``weight[:, coord_c0:coord_c0 + 2]`` —
+    the input-independent part of conv1 (``:51`` over ``:77``'s concat)."""
+    _require_cuda(weight)
+    if weight.dim() != 4 or tuple(weight.shape[2:]) != (3, 3) or weight.dtype != torch.float32:
+        raise ValueError("weight must be a float32 [Cout, Cin, 3, 3] tensor")
+    w = weight.detach().contiguous()
+    cout, cin = w.shape[:2]
+    H, W = int(hw[0]), int(hw[1])
+    b = None if bias is None else bias.detach().contiguous()
+    if b is not None and (b.numel() != cout or b.dtype != torch.float32):
+        raise ValueError(f"bias must be float32 [{cout}]")
+    if out is None:
+        out = torch.empty((cout, H, W), dtype=torch.float32, device=w.device)
+    elif tuple(out.shape) != (cout, H, W) or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous float32 [{cout}, {H}, {W}] tensor")
+    st = _native.load().mvbev_coord_term_f32(w.data_ptr(), cin, int(coord_c0), 0 if b is None else b.data_ptr(),
+                                             cout, H, W, out.data_ptr(), _stream(w))
+    _native.check(st, "mvbev_coord_term_f32")
+    return out
+
+
 def _gate(gate):
     """``(flag, tag)`` -> (device pointer, int32 tag) for the ABI (None -> NULL, 0)."""
     if gate is None:

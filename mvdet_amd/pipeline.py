@@ -164,12 +164,11 @@ class ProjectFuse:
                 chan_map.append(base + c if (v is not None and c < self.C) else -1)
         nc = n_views * view_ch
         self.pack1 = ops.PackedConv3x3(chan_map, precision)
-        self.pack_coord = ops.PackedConv3x3([nc, nc + 1] + [-1] * (ops.KC - 2))  # once per weights: fp32
+        self.coord_c0 = nc  # conv1's input channels of the coord map (x, y) after the views' (:77)
         self.pack2 = ops.PackedConv3x3(None, precision)
         self._ws: Dict[tuple, Workspace] = {}
         self._coord_key = None
         self._coord_term: Optional[torch.Tensor] = None
-        self._coord_in: Dict[str, torch.Tensor] = {}
         self._sk: Dict[str, torch.Tensor] = {}  # split-K-tail scratch per device (bf16x3 convs)
         self.split_k = split_k
         # conv1 skips, per output tile, the slots whose warp is exactly zero there (camera
@@ -440,16 +439,8 @@ class ProjectFuse:
         """[512, Ho, Wo]: bias + conv(coord channels) for the current conv1 parameters."""
         w, b = conv1.weight, conv1.bias
         key = (w.data_ptr(), w._version, None if b is None else (b.data_ptr(), b._version))
-        if key != self._coord_key:
-            H, W = self.grid_hw
-            dev = w.device
-            cin = self._coord_in.get(str(dev))
-            if cin is None:
-                cin = torch.zeros((1, ops.KC, H, W), dtype=torch.float32, device=dev)
-                ops.fill_coord_map(cin[:, :2])
-                self._coord_in[str(dev)] = cin
-            packed = self.pack_coord.get(w)
-            self._coord_term = ops.conv3x3(cin, packed, self.mid, bias=b, dilation=1, relu=False)[0]
+        if key != self._coord_key:  # (ABI 12300: one VALU pass; was an fp32-MFMA conv over a padded coord input)
+            self._coord_term = ops.coord_term(w, b, self.coord_c0, self.grid_hw)  # (fresh: in-flight readers)
             self._coord_key = key
         return self._coord_term
 

@@ -546,6 +546,28 @@ def test_fill_coord_map_matches_reference_coord_map():
     assert (dst[:, 0] == 3).all() and (dst[:, 3:] == 3).all()
 
 
+@pytest.mark.parametrize("hw,with_bias", [((120, 360), True), ((37, 70), False), ((2, 5), True)])
+def test_coord_term_matches_conv2d_of_the_coord_map(hw, with_bias):
+    """mvbev_coord_term_f32 (ABI 12300): conv1's bias + conv2d over the two coord channels (zero padding)
+    equals torch's float64 conv2d of the reference's coord map (golden-pinned by
+    test_fill_coord_map_matches_reference_coord_map) with the same weights, to fp32 rounding (1e-6 of
+    the term's scale), on the cfg2 grid, a grid with ragged tiles and a 2-row grid (every row a border)."""
+    import torch.nn.functional as F
+    from mvdet_amd import ops
+    from oracle.cpu_path import coord_map
+    H, W = hw
+    cin, c0, cout = 11, 8, 64
+    gen = torch.Generator().manual_seed(H * W)
+    w = torch.randn((cout, cin, 3, 3), generator=gen)
+    b = torch.randn((cout,), generator=gen) if with_bias else None
+    got = ops.coord_term(w.to(DEV), None if b is None else b.to(DEV), c0, (H, W)).cpu()
+    ref = F.conv2d(coord_map(H, W).double(), w[:, c0:c0 + 2].double(), None if b is None else b.double(), padding=1)[0]
+    err = (got.double() - ref).abs().max().item()
+    assert err <= 1e-6 * max(1.0, ref.abs().max().item()), err
+    with pytest.raises(Exception):
+        ops.coord_term(w.to(DEV), None, cin - 1, (H, W))  # the y channel past the weight's channels
+
+
 @pytest.mark.parametrize("band", [None, (5, 23)])
 def test_conv2_conv3_fused_matches_unfused(band):
     """conv2 -> conv3 without y2 in HBM (conv2's epilogue writes conv3's per-tap partials,

@@ -30,7 +30,7 @@ def test_library_exports_every_header_symbol():
     assert declared == sorted(_native.EXPORTS)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.mvbev_version() == 12200
+    assert lib.mvbev_version() == 12300
     assert lib.mvbev_status_string(0) == b"ok"
     assert lib.mvbev_status_string(-100) == b"HIP launch failed"
 
@@ -208,7 +208,9 @@ def test_bev_fuse_structs_and_plan_match_the_header(tmp_path):
     assert offs == sorted(offs) and all(o % 256 == 0 for o in offs)
     assert plan.Cs == 512 and plan.frustum == 1 and plan.wino == 1 and plan.tiles == 10 * 12
     t_bytes = 1 * (7 * 512 // 8) * 5 * 4 * 10 * 360 * 32  # mvbev_wino_rows_bytes: 5/3 of the slab's rows
-    assert offs[11] - offs[10] >= max(t_bytes, 7 * 512 * 120 * 360 * 4)
+    # R_BIG = region 7 (R_MAP1, R_PACK1, R_PACK2, R_INIT, R_MASK, R_ORDER, R_NF, R_BIG, ...; ABI 12300 dropped
+    # the coord term's padded input and fp32 pack)
+    assert offs[8] - offs[7] >= max(t_bytes, 7 * 512 * 120 * 360 * 4)
     assert lib.mvbev_bev_fuse_workspace_bytes(ctypes.byref(g)) == plan.workspace_bytes
     g.src_kind = _native.BEV_SRC_F16  # fp16 sources: the direct conv1 on the split slab
     assert lib.mvbev_bev_plan_init(ctypes.byref(g), ctypes.byref(plan)) == 0 and plan.wino == 0

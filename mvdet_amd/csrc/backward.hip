@@ -1257,6 +1257,9 @@ struct AdjArgs {
   AdjView v[kWarpMaxViews];
   int nviews, B, C, P, pblocks, chunks, nwg, accumulate;
   int src_cl;  // warp_adjoint_pix_kernel: grad_src channels-last (sC = 1, pixel stride C), else dense planes
+  // warp_adjoint_pix_kernel (round 6): 16-B stores of 4 elements along grad_src's contiguous dimension (every
+  // view's grad_src 16-B aligned, its batch / channel strides and P (planes) or C (channels-last) multiples of 4)
+  int vec4;
 };
 
 __global__ __launch_bounds__(256) void warp_adjoint_kernel(const AdjArgs a) {
@@ -1566,6 +1569,14 @@ __global__ __launch_bounds__(256) void warp_adjoint_pix_kernel(const AdjArgs a) 
 #if MVBEV_ADJ_PIX_EMPTY
   if (vw.rp[p0] == vw.rp[p0 + np]) {  // no entries in the block (rp is monotone): zeros, no LDS pass
     if (a.accumulate) return;
+    if (a.vec4) {  // 16-B stores: a quarter of the store instructions (the TA/TD path binds this kernel)
+      for (int i = threadIdx.x; i < 16 * NPIX; i += 256) {
+        const int cr = a.src_cl ? 4 * (i % 16) : i / (NPIX / 4), pl = a.src_cl ? i / 16 : 4 * (i % (NPIX / 4));
+        if (pl < np && c0 + cr < a.C)
+          *reinterpret_cast<floatx4*>(gs0 + (int64_t)cr * vw.sC + (int64_t)pl * ps) = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+      return;
+    }
     for (int i = threadIdx.x; i < 64 * NPIX; i += 256) {
       // the fastest index along the contiguous dimension: pixels for planes, channels for channels-last
       const int cr = a.src_cl ? i % 64 : i / NPIX, pl = a.src_cl ? i / 64 : i % NPIX;
@@ -1612,6 +1623,19 @@ __global__ __launch_bounds__(256) void warp_adjoint_pix_kernel(const AdjArgs a) 
     for (int k = 0; k < 8; ++k) tr[(gq * 8 + k) * kPitch + pl] = s[k];
   }
   __syncthreads();
+  if (a.vec4) {  // 4 elements along the contiguous dimension per lane: 4 conflict-free LDS reads, one 16-B store
+    for (int i = threadIdx.x; i < 16 * NPIX; i += 256) {
+      const int cr = a.src_cl ? 4 * (i % 16) : i / (NPIX / 4), pl = a.src_cl ? i / 16 : 4 * (i % (NPIX / 4));
+      if (pl < np && c0 + cr < a.C) {
+        floatx4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = a.src_cl ? tr[(cr + e) * kPitch + pl] : tr[cr * kPitch + pl + e];
+        floatx4* d = reinterpret_cast<floatx4*>(gs0 + (int64_t)cr * vw.sC + (int64_t)pl * ps);
+        *d = a.accumulate ? v + *d : v;
+      }
+    }
+    return;
+  }
   for (int i = threadIdx.x; i < 64 * NPIX; i += 256) {
     const int cr = a.src_cl ? i % 64 : i / NPIX, pl = a.src_cl ? i / 64 : i % NPIX;
     if (pl < np && c0 + cr < a.C) {
@@ -2041,6 +2065,12 @@ int mvbev_warp_views_adjoint(const mvbev_warp_adjoint_view* views, int nviews, i
   }
   a.nviews = nviews;
   a.B = (int)B; a.C = (int)C; a.P = (int)(H * W);
+#ifndef MVBEV_ADJ_PIX_VEC4
+#define MVBEV_ADJ_PIX_VEC4 1
+#endif
+  a.vec4 = MVBEV_ADJ_PIX_VEC4 && pixm && (a.src_cl ? C % 4 == 0 : (H * W) % 4 == 0);
+  for (int i = 0; i < nviews && a.vec4; ++i)
+    a.vec4 = (reinterpret_cast<uintptr_t>(a.v[i].gs) & 15) == 0 && a.v[i].sB % 4 == 0 && (a.src_cl || a.v[i].sC % 4 == 0);
   const bool g8 = split && MVBEV_ADJ_G8;
   // many entries per source pixel (a source smaller than the grid: the S.U plan): 16 pixels
   const int pix = H * W < Ho * Wo ? 16 : 32;

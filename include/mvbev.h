@@ -29,7 +29,7 @@
  *       nn.Conv2d(Cin->Cout, 3, padding=d, dilation=d) (+ nn.ReLU) of
  *       map_classifier[0:4]   persp_trans_detector.py:51-53, :81; the conv1 contribution of
  *       the two constant coord channels plus its bias is input-independent and enters as
- *       the `init` term (computed once per weight version with the same kernel).
+ *       the `init` term (once per weight version: mvbev_coord_term_f32, ABI 12300).
  *   mvbev_pack_conv3x3_weight_bf16x3, mvbev_conv3x3_bf16x3
  *       the same convs in 3xbf16 split precision on the bf16 MFMA (5.3x the fp32 rate)
  *   mvbev_conv3x3_cout1_f32

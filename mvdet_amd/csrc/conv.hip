@@ -451,38 +451,44 @@ __global__ __launch_bounds__(256) void bias_relu_nonfinite_kernel(float* __restr
 // conv1's coord term (ABI 12300): init[c][r][q] = bias[c] + sum over the 3 x 3 taps of conv1's two coord-channel
 // weights times the coord map (persp_trans_detector.py:103-112: grid / (n - 1) * 2 - 1 in float64, then
 // .float(); zero outside the grid, conv2d's padding, :51).  Input-independent, recomputed when the weights
-// change (every training step).  A VALU kernel: 18 products per output, one dword store per lane — the fp32
-// MFMA conv over an 8-channel padded coord input it replaces (6 zero channels) took 72 us at cfg2, this
-// writes the 88 MB term at the store rate.  Block = (output channel, 256 pixels); the channel's 18 weights
-// and its bias are uniform per block.
+// change (every training step).  A VALU kernel: a thread per output pixel evaluates its 3 x 3 coord window once
+// (the float64 divisions) and loops over kCtCh output channels — 18 products and one coalesced store each, the
+// channel's weights and bias wave-uniform (scalar loads).  The fp32-MFMA conv over an 8-channel padded coord
+// input it replaces took 72 us at cfg2, this 39 us (one thread per (channel, pixel) with the divisions redone per
+// channel took 108 us; unrolling the channel loop by 8: 42 us).
+constexpr int kCtCh = 32;  // output channels per block
 __global__ __launch_bounds__(256) void coord_term_kernel(const float* __restrict__ w, int64_t w_cout_stride,
                                                          const float* __restrict__ bias, float* __restrict__ out,
-                                                         int H, int W) {
-  const int c = blockIdx.y;
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= H * W) return;
-  const int r = p / W, q = p - r * W;
-  const float* wc = w + (int64_t)c * w_cout_stride;  // [2][3][3]: the x channel, then the y channel
-  float xs[3], ys[3];
-  bool cv[3], rv[3];
+                                                         int Cout, int H, int W) {
+  const int r = blockIdx.y, q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= W) return;
+  float xv[3][3], yv[3][3];  // [ky][kx] the window's coord values, 0 where the tap is padding
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     const int qq = q + k - 1, rr = r + k - 1;
-    cv[k] = qq >= 0 && qq < W;
-    rv[k] = rr >= 0 && rr < H;
-    xs[k] = (float)((double)qq / (double)(W - 1) * 2.0 - 1.0);
-    ys[k] = (float)((double)rr / (double)(H - 1) * 2.0 - 1.0);
-  }
-  float acc = 0.f;
+    const bool cv = qq >= 0 && qq < W, rv = rr >= 0 && rr < H;
+    const float x = (float)((double)qq / (double)(W - 1) * 2.0 - 1.0);
+    const float y = (float)((double)rr / (double)(H - 1) * 2.0 - 1.0);
 #pragma unroll
-  for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {  // a padded tap: both channels read 0
-      const bool in = rv[ky] && cv[kx];
-      acc = fmaf(wc[ky * 3 + kx], in ? xs[kx] : 0.f, acc);
-      acc = fmaf(wc[9 + ky * 3 + kx], in ? ys[ky] : 0.f, acc);
+    for (int j = 0; j < 3; ++j) {
+      xv[j][k] = (cv && r + j - 1 >= 0 && r + j - 1 < H) ? x : 0.f;  // tap (ky = j, kx = k)
+      yv[k][j] = (rv && q + j - 1 >= 0 && q + j - 1 < W) ? y : 0.f;  // tap (ky = k, kx = j)
     }
-  out[(int64_t)c * H * W + p] = acc + (bias ? bias[c] : 0.f);
+  }
+  const int c0 = blockIdx.z * kCtCh, c1 = min(Cout, c0 + kCtCh);
+  float* o = out + (int64_t)r * W + q;
+  for (int c = c0; c < c1; ++c) {
+    const float* wc = w + (int64_t)c * w_cout_stride;  // [2][3][3]: the x channel, then the y channel
+    float acc = 0.f;
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        acc = fmaf(wc[ky * 3 + kx], xv[ky][kx], acc);
+        acc = fmaf(wc[9 + ky * 3 + kx], yv[ky][kx], acc);
+      }
+    o[(int64_t)c * H * W] = acc + (bias ? bias[c] : 0.f);
+  }
 }
 
 }  // namespace mvbev
@@ -494,10 +500,10 @@ int mvbev_coord_term_f32(const float* w1, int64_t cin, int64_t coord_c0, const f
   using namespace mvbev;
   if (!w1 || !out) return MVBEV_ERR_NULL;
   if (cin <= 0 || Cout <= 0 || H <= 1 || W <= 1) return MVBEV_ERR_RANK;
-  if (coord_c0 < 0 || coord_c0 + 2 > cin || Cout > 65535 || H * W > INT32_MAX - 256) return MVBEV_ERR_SHAPE;
-  const dim3 grid((unsigned)ceil_div(H * W, (int64_t)256), (unsigned)Cout);
+  if (coord_c0 < 0 || coord_c0 + 2 > cin || H > 65535 || H * W > INT32_MAX - 256) return MVBEV_ERR_SHAPE;
+  const dim3 grid((unsigned)ceil_div(W, (int64_t)256), (unsigned)H, (unsigned)ceil_div(Cout, (int64_t)kCtCh));
   hipLaunchKernelGGL(coord_term_kernel, grid, dim3(256), 0, as_stream(stream), w1 + coord_c0 * 9, cin * 9, bias, out,
-                     (int)H, (int)W);
+                     (int)Cout, (int)H, (int)W);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }

@@ -810,7 +810,8 @@ def bench_main(args) -> None:
             res["inputs"] = ("each rank: the backbone-resolution maps of the views it owns (mp_model.view_owners; "
                              + ("fp16 NCHW" if s.half else "fp32 channels-last") + "); the channel slices of the "
                              "parts held elsewhere cross in one all-to-all per frame inside the timed region, and "
-                             "the a4 upsample runs fused into the warp (more work than the N = 1 value's step)")
+                             "the a4 upsample runs fused into the warp (more work than the N = 1 value's step, but less time: "
+                             "the like-for-like N = 1 figure is that line's plus_a4.fused_channels_last.value)")
             res["parts"] = dict(k=s.C // vp.part_channels, part_channels=vp.part_channels,
                                 parts_rank0=[list(p) for p in vp.my_parts], owners=vp.owner,
                                 fetched_bytes_rank0=int(sum(map(len, vp.recv_parts))) * fr.part_numel *

@@ -154,8 +154,10 @@ __global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_tile_kernel(const Warp
 }
 
 // Warp + row-Winograd input transform in one pass (inference conv1, csrc/conv_bf16x3.hip
-// "Row-Winograd conv1"): a block = 4 three-row output tiles (12 rows) x 8 columns of one view's
-// 8-channel group.  Phase 1: thread (row i < 14, column) warps input row 12 k - 1 + i like
+// "Row-Winograd conv1"): a block = 4 three-row output tiles (12 rows) x 16 columns of one view's
+// kWwGroups consecutive 8-channel groups, one after the other (round 6: the block decode, box, sample geometry
+// and address setup once per 2 groups; cfg3 4.09 -> 3.43-3.50 ms, cfg5 3.51 -> 3.12-3.14, cfg2 0.441 -> 0.421-0.428;
+// 4 groups spill at any occupancy).  Phase 1: thread (row i < 14, column) warps input row 12 k - 1 + i like
 // warp_tile_kernel (zero outside the grid) into LDS; phase 2: each (tile, column, xi) applies
 // B^T to its 5 rows and stores the transformed row split-bf16 at T row 5 r3 + xi (dst strides
 // in 32-B units: dB per item, dC per 8-channel group, dH per T row).  The slab itself is never
@@ -169,24 +171,28 @@ __global__ __launch_bounds__(kWarpTH * kWarpTW) void warp_tile_kernel(const Warp
 #define MVBEV_WW_STAGE 384  // max staged box pixels per channel (8 channels x 384 x 4 B = 12 KiB); 0 = off
 #endif
 constexpr int kWwStage = MVBEV_WW_STAGE;
+#ifndef MVBEV_WW_GROUPS
+#define MVBEV_WW_GROUPS 2  // 8-channel groups per block of warp_wino_kernel (A/B below)
+#endif
+constexpr int kWwGroups = MVBEV_WW_GROUPS;
 
+#ifndef MVBEV_WW_WAVES
+#define MVBEV_WW_WAVES 7  // waves per SIMD asked of the compiler (7: at most 72 VGPRs; 2 groups fit without spills)
+#endif
 template <bool PAIR, typename T = float>
-__global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(const WarpArgs a, int r3_rows) {
+__global__ __launch_bounds__(kWwThreads) __attribute__((amdgpu_waves_per_eu(MVBEV_WW_WAVES, 8)))
+void warp_wino_kernel(const WarpArgs a, int r3_rows) {
   static_assert(!PAIR || std::is_same<T, float>::value, "corner pairs are fp32 8-B loads");
   __shared__ __attribute__((aligned(16))) float ds[kWwRows][kWwCols][8];  // [row][col][channel]
   __shared__ unsigned char nz[kWwRows][kWwCols];
   __shared__ __attribute__((aligned(16))) f32x2_t stage2[kWarpCPB / 2 * (kWwStage > 0 ? kWwStage : 1)];
   __shared__ int box[4];  // source rows [box0, box1], columns [box2, box3] of the block's corners
-  const int lb = xcd_remap(blockIdx.x, a.nwg);
-  const int tile = lb % a.tiles;
-  const int chunk = (lb / a.tiles) % a.chunks;
-  const int bv = lb / (a.tiles * a.chunks);
-  const int view = bv % a.nviews;
-  const int b = bv / a.nviews;
+  const WarpBlock wb = warp_block_index(a);
+  const int tile = wb.tile, view = wb.view, b = wb.b, k = wb.k, tx = wb.tx;
   const WarpView& vw = a.v[view];
-  const int k = tile / a.tiles_x, tx = tile - k * a.tiles_x;
-  const int c_begin = chunk * kWarpCPB;
-  const int c_end = min(a.C, c_begin + kWarpCPB);
+  // (round 6) kWwGroups consecutive 8-channel groups per block: the block index, box, sample geometry and
+  // address setup are done once for all of them (a.chunks counts group blocks)
+  const int chunk0 = wb.chunk * kWwGroups;
   const int H = a.H, W = a.W;
   const int tid = threadIdx.x;
   const int i = tid / kWwCols, c = tid % kWwCols;  // 16 x kWwCols threads, rows >= 14 idle
@@ -256,86 +262,96 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_wino_kernel(co
   const int R = sb.R, Cb = sb.pitch;
   // uniform per block (the staged path needs unit column stride: the non-quad loads assume it too)
   const bool staged = kWwStage > 0 && bx[1] >= 0 && vw.sW == 1 && R * Cb <= kWwStage;
-  if (staged) {
-    stage_box_load<kWwThreads, T>(base, vw.sC, vw.sH, c_begin, c_end, sb, stage2, tid);
-    __syncthreads();
-  }
-  if (i < kWwRows) {  // phase 1: one warped pixel (8 channels) per thread
-    float d[8];
+  // the sample's geometry, shared by every group (same products, in the same order, as before)
+  const float fx1 = fx0 + 1.f, fy1 = fy0 + 1.f;
+  const float w_nw = (fx1 - ix) * (fy1 - iy), w_ne = (ix - fx0) * (fy1 - iy);
+  const float w_sw = (fx1 - ix) * (iy - fy0), w_se = (ix - fx0) * (iy - fy0);
+  const bool vx0 = x0 >= 0, vx1 = x0 + 1 <= W - 1, vy0 = y0 >= 0, vy1 = y0 + 1 <= H - 1;
+  const bool ok_nw = vx0 && vy0, ok_ne = vx1 && vy0, ok_sw = vx0 && vy1, ok_se = vx1 && vy1;
+  const int n = R * Cb;
+  const int t0 = (cy0 - bx[0]) * Cb, t1 = (cy1 - bx[0]) * Cb;
+  const int l0 = cx0 - sb.c0, l1 = cx1 - sb.c0;
+  for (int g = 0; g < kWwGroups; ++g) {  // uniform (unrolled by the compiler: the rolled loop spills)
+    const int chunk = chunk0 + g;
+    const int c_begin = chunk * kWarpCPB;
+    if (c_begin >= a.C) break;
+    const int c_end = min(a.C, c_begin + kWarpCPB);
+    // before this group's phase 1 writes ds, the previous group's phase 2 must have read it: the staging barrier
+    // below serves (stage2's last readers, the previous phase 1, finished before that group's second barrier)
+    if (g && !staged) __syncthreads();
+    if (staged) {
+      stage_box_load<kWwThreads, T>(base, vw.sC, vw.sH, c_begin, c_end, sb, stage2, tid);
+      __syncthreads();
+    }
+    if (i < kWwRows) {  // phase 1: one warped pixel (8 channels) per thread
+      float d[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) d[j] = 0.f;
-    bool any = false;
-    if (live) {
-      if (!wc.inside) {
-        if (!wc.finite) {
-          any = true;
+      for (int j = 0; j < 8; ++j) d[j] = 0.f;
+      bool any = false;
+      if (live) {
+        if (!wc.inside) {
+          if (!wc.finite) {
+            any = true;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) d[j] = c_begin + j < c_end ? __builtin_nanf("") : 0.f;
-        }
-      } else {
-        any = true;
-        const float fx1 = fx0 + 1.f, fy1 = fy0 + 1.f;
-        const float w_nw = (fx1 - ix) * (fy1 - iy), w_ne = (ix - fx0) * (fy1 - iy);
-        const float w_sw = (fx1 - ix) * (iy - fy0), w_se = (ix - fx0) * (iy - fy0);
-        const bool vx0 = x0 >= 0, vx1 = x0 + 1 <= W - 1, vy0 = y0 >= 0, vy1 = y0 + 1 <= H - 1;
-        const bool ok_nw = vx0 && vy0, ok_ne = vx1 && vy0, ok_sw = vx0 && vy1, ok_se = vx1 && vy1;
-        if (staged) {
-          const int n = R * Cb;
-          const int t0 = (cy0 - bx[0]) * Cb, t1 = (cy1 - bx[0]) * Cb;
-          const int l0 = cx0 - sb.c0, l1 = cx1 - sb.c0;
-#pragma unroll
-          for (int p = 0; p < 4; ++p) {  // a channel pair per ds_read_b64 (the same products per channel)
-            const f32x2_t* sp = stage2 + p * n;
-            const f32x2_t vnw = sp[t0 + l0], vne = sp[t0 + l1], vsw = sp[t1 + l0], vse = sp[t1 + l1];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              float acc = 0.f;
-              acc += (ok_nw ? vnw[e] : 0.f) * w_nw;
-              acc += (ok_ne ? vne[e] : 0.f) * w_ne;
-              acc += (ok_sw ? vsw[e] : 0.f) * w_sw;
-              acc += (ok_se ? vse[e] : 0.f) * w_se;
-              d[2 * p + e] = c_begin + 2 * p + e < c_end ? acc : 0.f;
-            }
+            for (int j = 0; j < 8; ++j) d[j] = c_begin + j < c_end ? __builtin_nanf("") : 0.f;
           }
         } else {
-          const int64_t sH = vw.sH, sW = vw.sW, sC = vw.sC;
-          const int bx = min(max(x0, 0), W - 2);
-          const int64_t o_top = cy0 * sH + bx, o_bot = cy1 * sH + bx;
-          const bool nw_lo = x0 == bx, ne_lo = x0 + 1 == bx;
-          const int64_t o_nw = cy0 * sH + cx0 * sW, o_ne = cy0 * sH + cx1 * sW;
-          const int64_t o_sw = cy1 * sH + cx0 * sW, o_se = cy1 * sH + cx1 * sW;
+          any = true;
+          if (staged) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {  // straight-line (a short last group re-reads its last channel)
-            const int ch = min(c_begin + j, c_end - 1);
-            const T* pc = base + (int64_t)ch * sC;
-            float vnw, vne, vsw, vse;
-            if constexpr (PAIR) {
-              const f32x2u_t top = *reinterpret_cast<const f32x2u_t*>(pc + o_top);
-              const f32x2u_t bot = *reinterpret_cast<const f32x2u_t*>(pc + o_bot);
-              vnw = nw_lo ? top.x : top.y;
-              vne = ne_lo ? top.x : top.y;
-              vsw = nw_lo ? bot.x : bot.y;
-              vse = ne_lo ? bot.x : bot.y;
-            } else {
-              vnw = to_f32<T>(pc[o_nw]); vne = to_f32<T>(pc[o_ne]); vsw = to_f32<T>(pc[o_sw]); vse = to_f32<T>(pc[o_se]);
+            for (int p = 0; p < 4; ++p) {  // a channel pair per ds_read_b64 (the same products per channel)
+              const f32x2_t* sp = stage2 + p * n;
+              const f32x2_t vnw = sp[t0 + l0], vne = sp[t0 + l1], vsw = sp[t1 + l0], vse = sp[t1 + l1];
+#pragma unroll
+              for (int e = 0; e < 2; ++e) {
+                float acc = 0.f;
+                acc += (ok_nw ? vnw[e] : 0.f) * w_nw;
+                acc += (ok_ne ? vne[e] : 0.f) * w_ne;
+                acc += (ok_sw ? vsw[e] : 0.f) * w_sw;
+                acc += (ok_se ? vse[e] : 0.f) * w_se;
+                d[2 * p + e] = c_begin + 2 * p + e < c_end ? acc : 0.f;
+              }
             }
-            float acc = 0.f;
-            acc += (ok_nw ? vnw : 0.f) * w_nw;
-            acc += (ok_ne ? vne : 0.f) * w_ne;
-            acc += (ok_sw ? vsw : 0.f) * w_sw;
-            acc += (ok_se ? vse : 0.f) * w_se;
-            d[j] = c_begin + j < c_end ? acc : 0.f;
+          } else {
+            const int64_t sH = vw.sH, sW = vw.sW, sC = vw.sC;
+            const int bxc = min(max(x0, 0), W - 2);
+            const int64_t o_top = cy0 * sH + bxc, o_bot = cy1 * sH + bxc;
+            const bool nw_lo = x0 == bxc, ne_lo = x0 + 1 == bxc;
+            const int64_t o_nw = cy0 * sH + cx0 * sW, o_ne = cy0 * sH + cx1 * sW;
+            const int64_t o_sw = cy1 * sH + cx0 * sW, o_se = cy1 * sH + cx1 * sW;
+            const T* pc = base + (int64_t)c_begin * sC;  // stepped per channel (no 64-bit multiply per channel)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {  // straight-line (a short last group re-reads its last channel)
+              if (j > 0 && c_begin + j < c_end) pc += sC;
+              float vnw, vne, vsw, vse;
+              if constexpr (PAIR) {
+                const f32x2u_t top = *reinterpret_cast<const f32x2u_t*>(pc + o_top);
+                const f32x2u_t bot = *reinterpret_cast<const f32x2u_t*>(pc + o_bot);
+                vnw = nw_lo ? top.x : top.y;
+                vne = ne_lo ? top.x : top.y;
+                vsw = nw_lo ? bot.x : bot.y;
+                vse = ne_lo ? bot.x : bot.y;
+              } else {
+                vnw = to_f32<T>(pc[o_nw]); vne = to_f32<T>(pc[o_ne]); vsw = to_f32<T>(pc[o_sw]); vse = to_f32<T>(pc[o_se]);
+              }
+              float acc = 0.f;
+              acc += (ok_nw ? vnw : 0.f) * w_nw;
+              acc += (ok_ne ? vne : 0.f) * w_ne;
+              acc += (ok_sw ? vsw : 0.f) * w_sw;
+              acc += (ok_se ? vse : 0.f) * w_se;
+              d[j] = c_begin + j < c_end ? acc : 0.f;
+            }
           }
         }
       }
+      // two 16-B stores (the element-wise form compiled to 8 ds_write_b32)
+      *reinterpret_cast<f32x4a_t*>(&ds[i][c][0]) = f32x4a_t{d[0], d[1], d[2], d[3]};
+      *reinterpret_cast<f32x4a_t*>(&ds[i][c][4]) = f32x4a_t{d[4], d[5], d[6], d[7]};
+      nz[i][c] = any;
     }
-    // two 16-B stores (the element-wise form compiled to 8 ds_write_b32)
-    *reinterpret_cast<f32x4a_t*>(&ds[i][c][0]) = f32x4a_t{d[0], d[1], d[2], d[3]};
-    *reinterpret_cast<f32x4a_t*>(&ds[i][c][4]) = f32x4a_t{d[4], d[5], d[6], d[7]};
-    nz[i][c] = any;
+    __syncthreads();
+    wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
   }
-  __syncthreads();
-  wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
 }
 
 // The per-(view, tile) source boxes of warp_wino_kernel (ABI 12200), once per geometry: a block per (view,
@@ -410,13 +426,9 @@ void warp_wino_cl_kernel(const WarpArgs a, int r3_rows) {
   __shared__ __attribute__((aligned(16))) float ds[kWcPix * kWcPitch];
   __shared__ float2 crd[kWcPix];
   __shared__ unsigned char cls[kWcPix];  // 0: exact zero (outside / off the grid), 1: inside, 2: non-finite
-  const int lb = xcd_remap(blockIdx.x, a.nwg);
-  const int tile = lb % a.tiles;
-  const int grp = (lb / a.tiles) % a.chunks;  // 32-channel group
-  const int bv = lb / (a.tiles * a.chunks);
-  const int view = bv % a.nviews, b = bv / a.nviews;
+  const WarpBlock wb = warp_block_index(a);
+  const int tile = wb.tile, grp = wb.chunk, view = wb.view, b = wb.b, k = wb.k, tx = wb.tx;  // grp: 32-channel group
   const WarpView& vw = a.v[view];
-  const int k = tile / a.tiles_x, tx = tile - k * a.tiles_x;
   const int tid = threadIdx.x;
   // (round 6) the per-geometry box table (the same 14 x 16 block tiles as warp_wino_kernel): a block with no
   // sample inside the source and none non-finite returns at once (T zero-filled, skip_zero)
@@ -914,8 +926,9 @@ int mvbev_warp_views_wino_rows_ex(const mvbev_warp_view* views, int nviews, int6
     a.tiles_x = (int)ceil_div(Wo, kWcCols);
     a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);
   }
-  a.chunks = (int)ceil_div(C, cl ? kWcCh : kWarpCPB);
+  a.chunks = (int)ceil_div(C, cl ? kWcCh : kWarpCPB * kWwGroups);  // (NCHW: blocks of kWwGroups 8-channel groups)
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
+  set_fastdiv(a);
   a.boxes = boxes;  // (the line-per-pixel kernel's 14 x 16 block tiles are warp_wino_kernel's: same table)
   const dim3 grid((unsigned)a.nwg), block(cl ? kWcThreads : kWwThreads);
   if (cl)

@@ -55,6 +55,20 @@ struct WarpView {
   int row0;            // grid row of dst row 0 (a row window of the grid: warp_tile_kernel, the exact warp)
 };
 
+// n / d for 0 <= n < 2^31 as (umulhi(n, m) + n) >> s (round 6: the fused warps' block decomposition took four
+// runtime divisions, ~100 scalar instructions of the ~295 each wave issued at cfg3); m == 0: not set (plain division)
+struct FastDiv {
+  uint32_t m, s;
+};
+inline FastDiv make_fastdiv(int d) {  // host, d >= 1
+  uint32_t s = 0;
+  while ((1ull << s) < (unsigned long long)d) ++s;
+  return FastDiv{(uint32_t)(((1ull << 32) * ((1ull << s) - (unsigned long long)d)) / (unsigned long long)d + 1), s};
+}
+__device__ inline int fdiv(int n, int d, FastDiv f) {
+  return f.m ? (int)((__umulhi((unsigned)n, f.m) + (unsigned)n) >> f.s) : n / d;
+}
+
 struct WarpArgs {
   WarpView v[kWarpMaxViews];
   int nviews, B, C, H, W, Ho, Wo, tiles_x, tiles, chunks, nwg;
@@ -74,7 +88,35 @@ struct WarpArgs {
   // int32 [nviews][tiles][4] {r0, r1, c0, c1 | nonfinite << 30} (r1 < 0: no sample inside the source),
   // computed once per geometry by mvbev_warp_wino_boxes; NULL: each block reduces its own box
   const int32_t* boxes;
+  // (round 6) fast divisors of tiles, chunks, nviews and tiles_x for warp_block_index (set_fastdiv; zero: unset)
+  FastDiv fd_tiles, fd_chunks, fd_nviews, fd_tiles_x;
 };
+
+inline void set_fastdiv(WarpArgs& a) {  // host, after the tiling fields are final
+  a.fd_tiles = make_fastdiv(a.tiles);
+  a.fd_chunks = make_fastdiv(a.chunks);
+  a.fd_nviews = make_fastdiv(a.nviews);
+  a.fd_tiles_x = make_fastdiv(a.tiles_x);
+}
+
+// a fused-warp block's coordinates: lb = xcd_remap(block) = ((b * nviews + view) * chunks + chunk) * tiles + tile,
+// tile = k * tiles_x + tx
+struct WarpBlock {
+  int tile, chunk, view, b, k, tx;
+};
+__device__ inline WarpBlock warp_block_index(const WarpArgs& a) {
+  WarpBlock r;
+  const int lb = xcd_remap(blockIdx.x, a.nwg);
+  const int q1 = fdiv(lb, a.tiles, a.fd_tiles);
+  r.tile = lb - q1 * a.tiles;
+  const int q2 = fdiv(q1, a.chunks, a.fd_chunks);
+  r.chunk = q1 - q2 * a.chunks;
+  r.b = fdiv(q2, a.nviews, a.fd_nviews);
+  r.view = q2 - r.b * a.nviews;
+  r.k = fdiv(r.tile, a.tiles_x, a.fd_tiles_x);
+  r.tx = r.tile - r.k * a.tiles_x;
+  return r;
+}
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 // a horizontally adjacent corner pair (nw,ne) / (sw,se) of an fp32 row: 8 bytes, 4-byte aligned
@@ -268,20 +310,26 @@ template <int NT, typename T = float>
 __device__ inline void stage_box_load(const T* __restrict__ base, int64_t sC, int64_t sH, int c_begin, int c_end,
                                       const StageBox& sb, f32x2_t* __restrict__ stage2, int tid) {
   const int n = sb.R * sb.pitch;
+  // the 8 channels' planes: pointers stepped by sC from channel c_begin (a short last group repeats its last
+  // channel) — the 64-bit min / multiply per channel this replaces was ~160 scalar instructions per wave
+  // (32-bit offsets from one pointer instead: 1-2 % slower at cfg2 / cfg4 / cfg5, 2 % faster at cfg3)
+  const T* pl[8];
+  pl[0] = base + (int64_t)c_begin * sC;
+#pragma unroll
+  for (int j = 1; j < 8; ++j) pl[j] = c_begin + j < c_end ? pl[j - 1] + sC : pl[j - 1];
   if (sb.quad) {
     const int Q = sb.pitch >> 2, items = sb.R * Q;
     for (int it = tid; it < items; it += NT) {
       const int r = it / Q, q = it - r * Q;
-      const T* src = base + (int64_t)(sb.r0 + r) * sH + sb.c0 + 4 * q;
+      const int64_t o = (int64_t)(sb.r0 + r) * sH + sb.c0 + 4 * q;
       f32x4a_t t[8];
       if constexpr (std::is_same<T, float>::value) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          t[j] = *reinterpret_cast<const f32x4a_t*>(src + (int64_t)min(c_begin + j, c_end - 1) * sC);
+        for (int j = 0; j < 8; ++j) t[j] = *reinterpret_cast<const f32x4a_t*>(pl[j] + o);
       } else {  // 4 halves (8 B) per lane and channel
         uint2 u[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) u[j] = *reinterpret_cast<const uint2*>(src + (int64_t)min(c_begin + j, c_end - 1) * sC);
+        for (int j = 0; j < 8; ++j) u[j] = *reinterpret_cast<const uint2*>(pl[j] + o);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const T* h = reinterpret_cast<const T*>(&u[j]);
@@ -301,9 +349,9 @@ __device__ inline void stage_box_load(const T* __restrict__ base, int64_t sC, in
   for (int r = tid / 32; r < sb.R; r += NT / 32)
     for (int cc = tid % 32; cc < sb.pitch; cc += 32) {
       float t[8];
+      const int64_t o = (int64_t)(sb.r0 + r) * sH + sb.c0 + cc;
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        t[j] = to_f32<T>(base[(int64_t)min(c_begin + j, c_end - 1) * sC + (int64_t)(sb.r0 + r) * sH + sb.c0 + cc]);
+      for (int j = 0; j < 8; ++j) t[j] = to_f32<T>(pl[j][o]);
 #pragma unroll
       for (int p = 0; p < 4; ++p) stage2[p * n + r * sb.pitch + cc] = f32x2_t{t[2 * p], t[2 * p + 1]};
     }

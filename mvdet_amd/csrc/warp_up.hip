@@ -353,13 +353,9 @@ __global__ __launch_bounds__(kUcThreads) void warp_up_wino_cl_kernel(const UpArg
   __shared__ int pint[kWcPixUp];  // rb << 16 | cb << 2 | class (0 zero, 1 inside, 2 NaN)
   __shared__ int box[4];
   const WarpArgs& a = ua.w;
-  const int lb = xcd_remap(blockIdx.x, a.nwg);
-  const int tile = lb % a.tiles;
-  const int grp = (lb / a.tiles) % a.chunks;  // 32-channel group
-  const int bv = lb / (a.tiles * a.chunks);
-  const int view = bv % a.nviews, b = bv / a.nviews;
+  const WarpBlock wb = warp_block_index(a);
+  const int tile = wb.tile, grp = wb.chunk, view = wb.view, b = wb.b, k = wb.k, tx = wb.tx;  // grp: 32-channel group
   const WarpView& vw = a.v[view];
-  const int k = tile / a.tiles_x, tx = tile - k * a.tiles_x;
   const int H = a.H, W = a.W, h = ua.h, w = ua.sw;
   const int tid = threadIdx.x;
   // (round 6) with the per-geometry table the 16 channel-group blocks of a (view, tile) take its box
@@ -799,6 +795,7 @@ extern "C" int mvbev_warp_views_upsampled_wino_rows_ex(const mvbev_warp_view* vi
     a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);
     a.chunks = (int)(C / kUcCh);
     a.nwg = a.tiles * a.chunks * a.B * a.nviews;
+    set_fastdiv(a);
     ua.boxes = boxes;
     hipLaunchKernelGGL(warp_up_wino_cl_kernel, dim3((unsigned)a.nwg), dim3(kUcThreads), 0, as_stream(stream), ua,
                        (int)r3_rows);

@@ -65,7 +65,7 @@ extern "C" {
 
 const char* mvbev_status_string(int status);
 /* Library / ABI version, e.g. 10000 for 1.0.0. */
-int mvbev_version(void);  /* 12300: mvbev_coord_term_f32 (conv1's coord term as one VALU pass); 12200: the training forward's non-finite guard (mvbev_store_gated_f32, mvbev_pack_conv3x3_weight_f32_gated, mvbev_wino_rows_split_bf16_gated), per-geometry staging boxes of the fused warps (mvbev_warp_wino_boxes, mvbev_warp_views_wino_rows_ex, mvbev_warp_upsampled_wino_boxes, mvbev_warp_views_upsampled_wino_rows_ex); 12100: MVBEV_LAYOUT_SPLIT_BF16_PIX (conv data gradients' output, the warp adjoint's input); 12000: conv1's and conv2's weight gradients from the forward's row-Winograd transforms (mvbev_wino_dy_rows_f32, mvbev_conv3x3_wgrad_wino_bf16x3); 11900: row windows (mvbev_warp_views_split_bf16_rows with the non-finite report, mvbev_warp_views_exact_rows with fp16 sources), mvbev_conv3x3_f32_ex (row-band output), mvbev_bias_relu_nonfinite_f32, mvbev_zero_gated — the non-finite guard of the multi-GPU modes and the banded exact path; 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
+int mvbev_version(void);  /* 12400: row-Winograd F(4,3) (mvbev_pack_conv3x3_weight_wino43, mvbev_wino43_rows_split_bf16, mvbev_conv3x3_wino43_bf16x3, mvbev_conv3x3_wino43_bf16x3_cout1_partials); 12300: mvbev_coord_term_f32 (conv1's coord term as one VALU pass); 12200: the training forward's non-finite guard (mvbev_store_gated_f32, mvbev_pack_conv3x3_weight_f32_gated, mvbev_wino_rows_split_bf16_gated), per-geometry staging boxes of the fused warps (mvbev_warp_wino_boxes, mvbev_warp_views_wino_rows_ex, mvbev_warp_upsampled_wino_boxes, mvbev_warp_views_upsampled_wino_rows_ex); 12100: MVBEV_LAYOUT_SPLIT_BF16_PIX (conv data gradients' output, the warp adjoint's input); 12000: conv1's and conv2's weight gradients from the forward's row-Winograd transforms (mvbev_wino_dy_rows_f32, mvbev_conv3x3_wgrad_wino_bf16x3); 11900: row windows (mvbev_warp_views_split_bf16_rows with the non-finite report, mvbev_warp_views_exact_rows with fp16 sources), mvbev_conv3x3_f32_ex (row-band output), mvbev_bias_relu_nonfinite_f32, mvbev_zero_gated — the non-finite guard of the multi-GPU modes and the banded exact path; 11800: mvbev_conv3x3_wino_bf16x3_dgrad (row-Winograd data gradient, output-side mask); 11700: channels-last sources for the fused warps (mvbev_warp_views_wino_rows, mvbev_warp_views_upsampled_wino_rows), mvbev_nchw_to_nhwc_f32; 11600: the non-finite-feature guard (mvbev_warp_views_exact_f32; the fused warps' nonfinite report; gate arguments of mvbev_conv3x3_f32 / mvbev_conv3x3_cout1_f32; mvbev_bev_plan.guard); 11500: row-Winograd conv2 -> conv3 partials (mvbev_wino_rows_split_bf16_dil, mvbev_conv3x3_wino_bf16x3_dil, mvbev_conv3x3_wino_bf16x3_cout1_partials); 11400: mvbev_warp_nonfinite_views (non-finite geometry routes to the direct conv1); the NMS candidate order replays torch's CPU sort (ties included), mvbev_point_nms (no workspace) retired; mvbev_conv3x3_bf16x3_sched / _sched3 retired (forward schedules measured slower); 11300: row-Winograd conv1 (mvbev_pack_conv3x3_weight_wino, mvbev_wino_rows_split_bf16, mvbev_conv3x3_wino_bf16x3); 11200: mvbev_conv3x3_bf16x3_sched3 (schedules over the edge-strip tiles); 11100: edge-strip conv tiles (mvbev_conv_ring_tile_space, mvbev_conv3x3_bf16x3_ex3); 11000: ring-kernel schedules (mvbev_conv_schedule, mvbev_conv3x3_bf16x3_sched, mvbev_conv3x3_dgrad_bf16x3_sched); 10900: mvbev_conv3x3_wgrad_bf16x3_ex2 (pre-split dy rows), mvbev_split_rows_bf16; 10800: mvbev_warp_upsampled_adjoint_plan (training from backbone features), mvbev_conv3x3_cout1_backward_ex; 10700: training on split-bf16 y1 (mvbev_relu_backward_split_f32, mvbev_conv3x3_dgrad_bf16x3_ex); 10600: conv2 -> conv3 fused (mvbev_conv3x3_bf16x3_cout1_partials, mvbev_cout1_reduce_partials); 10500: mvbev_point_nms_ws (any K); 10400: MVBEV_WARP_DST_ZEROED warps; 10300: LDS-DMA ring conv (12-row tiles for split-bf16 input); 10200: native backward (10100: frustum masks, split-K tail, fused upsample+warp) */
 
 /* Bilinear homography warp, zero padding, align_corners=True (kornia 0.6.11).
  *   src    : [B][C][H][W] fp32, element strides src_strides[4] (any, >= 0)
@@ -442,6 +442,26 @@ int mvbev_conv3x3_wino_bf16x3_dil(const void* t, const mvbev_conv_desc* desc, co
 int mvbev_conv3x3_wino_bf16x3_cout1_partials(const void* t, const mvbev_conv_desc* desc, const void* w_packed,
                                              const float* bias, int64_t Cout, int dilation, int relu, const float* w3,
                                              void* partials, size_t partials_bytes, void* stream);
+/* Row-Winograd F(4,3) (ABI 12400; persp_trans_detector.py:51 conv1 and :53-54 conv2 -> conv3): the same
+ * convs as mvbev_conv3x3_wino_bf16x3 / _cout1_partials from 6 transformed rows per 4 output rows (points
+ * 0, +-1, +-2, inf) instead of 5 per 3 — 10 % fewer MFMAs, the K sum walked xi-major.  T43 =
+ * [B][K/8][6 * 4 * ceil(out_rows / 16)][hi, lo][W][8] (mvbev_wino43_rows_bytes; dilation 2: row tile q of
+ * a 16-row tile holds rows 8 (q / 2) + q % 2 + 2 pt), written by mvbev_wino43_rows_split_bf16 from the
+ * split-bf16 input; weights from mvbev_pack_conv3x3_weight_wino43 (arguments as
+ * mvbev_pack_conv3x3_weight_wino); group_mask / tile_order over 16 x 32 output tiles
+ * (mvbev_warp_tile_mask with 16-row tiles); y fp32 or split-bf16. */
+size_t mvbev_conv3x3_packed_bytes_wino43(int64_t Cout, int64_t K);
+int mvbev_pack_conv3x3_weight_wino43(const float* w, int64_t Cout, int64_t Cin_w, const int32_t* chan_map, int64_t K,
+                                     void* w_packed, void* stream);
+size_t mvbev_wino43_rows_bytes(const mvbev_conv_desc* desc);
+int mvbev_wino43_rows_split_bf16(const void* x, const mvbev_conv_desc* desc, int dilation, const uint32_t* group_mask,
+                                 void* t, size_t t_bytes, void* stream);
+int mvbev_conv3x3_wino43_bf16x3(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,
+                                const float* init, int64_t Cout, int dilation, int relu, void* y, int y_layout,
+                                const uint32_t* group_mask, const int32_t* tile_order, void* stream);
+int mvbev_conv3x3_wino43_bf16x3_cout1_partials(const void* t, const mvbev_conv_desc* desc, const void* w_packed,
+                                               const float* bias, int64_t Cout, int dilation, int relu,
+                                               const float* w3, void* partials, size_t partials_bytes, void* stream);
 /* A data gradient as the dilation-1 row-Winograd conv (ABI 11800; the training backward's conv1
  * dgrad, persp_trans_detector.py:51 differentiated): t = the row transform of the split-bf16 dy
  * (mvbev_wino_rows_split_bf16), w_packed = mvbev_pack_conv3x3_weight_wino of the weight with its

@@ -94,6 +94,12 @@ EXPORTS = (
     "mvbev_warp_views_wino_rows_ex",
     "mvbev_warp_upsampled_wino_boxes",
     "mvbev_warp_views_upsampled_wino_rows_ex",
+    "mvbev_conv3x3_packed_bytes_wino43",
+    "mvbev_pack_conv3x3_weight_wino43",
+    "mvbev_wino43_rows_bytes",
+    "mvbev_wino43_rows_split_bf16",
+    "mvbev_conv3x3_wino43_bf16x3",
+    "mvbev_conv3x3_wino43_bf16x3_cout1_partials",
 )
 BEV_SRC_F32, BEV_SRC_F16, BEV_SRC_BACKBONE_F32 = 0, 1, 2  # MVBEV_BEV_SRC_*
 BEV_SRC_CHANNELS_LAST = 16  # MVBEV_BEV_SRC_CHANNELS_LAST (flag)
@@ -227,6 +233,21 @@ def _declare(lib):
     lib.mvbev_conv3x3_wino_bf16x3_cout1_partials.restype = ctypes.c_int
     lib.mvbev_conv3x3_wino_bf16x3_cout1_partials.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, _i64, ctypes.c_int,
                                                              ctypes.c_int, _p, _p, ctypes.c_size_t, _p]
+    lib.mvbev_conv3x3_packed_bytes_wino43.restype = ctypes.c_size_t
+    lib.mvbev_conv3x3_packed_bytes_wino43.argtypes = [_i64, _i64]
+    lib.mvbev_pack_conv3x3_weight_wino43.restype = ctypes.c_int
+    lib.mvbev_pack_conv3x3_weight_wino43.argtypes = [_p, _i64, _i64, _p, _i64, _p, _p]
+    lib.mvbev_wino43_rows_bytes.restype = ctypes.c_size_t
+    lib.mvbev_wino43_rows_bytes.argtypes = [ctypes.POINTER(ConvDesc)]
+    lib.mvbev_wino43_rows_split_bf16.restype = ctypes.c_int
+    lib.mvbev_wino43_rows_split_bf16.argtypes = [_p, ctypes.POINTER(ConvDesc), ctypes.c_int, _p, _p, ctypes.c_size_t,
+                                                 _p]
+    lib.mvbev_conv3x3_wino43_bf16x3.restype = ctypes.c_int
+    lib.mvbev_conv3x3_wino43_bf16x3.argtypes = [_p, ctypes.POINTER(ConvDesc), _p, _p, _p, _i64, ctypes.c_int,
+                                                ctypes.c_int, _p, ctypes.c_int, _p, _p, _p]
+    lib.mvbev_conv3x3_wino43_bf16x3_cout1_partials.restype = ctypes.c_int
+    lib.mvbev_conv3x3_wino43_bf16x3_cout1_partials.argtypes = \
+        lib.mvbev_conv3x3_wino_bf16x3_cout1_partials.argtypes
     lib.mvbev_warp_views_wino_rows.restype = ctypes.c_int
     lib.mvbev_warp_views_wino_rows.argtypes = [ctypes.POINTER(WarpView), ctypes.c_int, _i64, _i64, _i64, _i64, _i64,
                                                _i64, _i64, ctypes.c_int, _p, ctypes.c_int32, _p]

@@ -652,10 +652,10 @@ __device__ inline void glds16(const u32x4* src, u32x4* lds_wave_base) {
 // tap, pixel), set = (Cout tile, 64-channel half of the wave).  cout1_reduce_kernel then sums
 // the sets' shifted taps in a fixed order.  w3 is staged in LDS ([tap][128 co] of this Cout
 // tile) after the K loop: 4 consecutive channels = one ds_read_b128 per (tap, 8-channel quad).
-template <bool RELU>
+template <bool RELU, int NPT = 3>
 __device__ __attribute__((always_inline)) inline void cout1_partials(const Args& a, int b, int row_base, int dil,
                                                                     int col, int cot, int cw,
-                                      const floatx16 (&acc)[2][3], u32x4* lds) {
+                                      const floatx16 (&acc)[2][NPT], u32x4* lds) {
   const int tid = threadIdx.x, kh = (tid & 63) >> 5;
   // LDS (the ring buffers, free after the K loop): w3s [9][128] then the bias [128]
   float* w3s = reinterpret_cast<float*>(lds);
@@ -671,7 +671,7 @@ __device__ __attribute__((always_inline)) inline void cout1_partials(const Args&
   // per row: per (Cout block, 4-channel quad) the 4 activations, then the 9 taps' weights one
   // floatx4 at a time (9 sums + 4 activations + 4 weights live; the weights re-read per row)
 #pragma unroll
-  for (int pt = 0; pt < 3; ++pt) {
+  for (int pt = 0; pt < NPT; ++pt) {
     float s[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) s[t] = 0.f;
@@ -1853,6 +1853,463 @@ static int wino_launch(const void* t, const mvbev_conv_desc* d, const void* w_pa
   return MVBEV_OK;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Row-Winograd F(4,3), xi-major (round 6).
+//   B^T = [4 0 -5 0 1 0; 0 -4 -4 1 1 0; 0 4 -4 -1 1 0; 0 -2 -1 2 1 0; 0 2 -1 -2 1 0; 0 4 0 -5 0 1]
+//   G   = [1/4 0 0; -1/6 -1/6 -1/6; -1/6 1/6 -1/6; 1/24 1/12 1/6; 1/24 -1/12 1/6; 0 0 1]
+//   A^T = [1 1 1 1 1 0; 0 1 -1 2 -2 0; 0 1 1 4 4 0; 0 1 -1 8 -8 1]
+// (points 0, +-1, +-2, inf).  A wave's 4 output rows come from 6 transformed rows: 6 x 3 MFMA K-blocks
+// per 16-channel chunk and 4 rows instead of F(3,3)'s 5 per 3 (-10 % of the MFMAs, T at 6/4 instead of
+// 5/3 of the slab).  Accumulating per transformed row as the F(3,3) kernel does would need acc[2][6]
+// (192 registers) beside the fragments — past the 256 a wave has at two waves per SIMD.  This kernel walks
+// K xi-major instead: every (chunk, xi) unit is the F(3,3) kernel's unit (the same weight and T DMAs, the
+// same 18 MFMAs per wave), but the units of one xi run back to back over all chunks into ONE accumulator
+// pair, which is folded into the 4 output rows (y[r] += A^T[r][xi] M_xi, fp32) when the xi's K sum is
+// complete: y[2][4] + acc[2] = 160 accumulator registers, as F(3,3)'s acc[2][5].  Workgroup tile 16 rows
+// (4 row tiles of 4) x 32 columns x 128 Cout; dilation 2: row tile q holds rows base + 2 pt,
+// base = 8 (q / 2) + q % 2.  T43[b][k / 8][6 r4 + xi][hi, lo][W][8], r4 < 4 ceil(out_rows / 16).
+namespace w43 {
+constexpr int NXI = 6;              // transformed rows per 4-row output tile
+constexpr int RT4 = 16;             // output rows per workgroup tile
+constexpr int XH = 4 * NXI;         // T rows of a workgroup tile
+constexpr int NTAP = 3 * NXI;       // packed taps (xi, kw)
+constexpr int WPART = NTAP * KC * BN;
+constexpr int W16 = 2 * WPART * 2 / 16;  // 16-B pieces per (chunk, cout tile)
+template <int DIL>
+__device__ inline int base_row(int rg) {
+  return DIL == 1 ? 4 * rg : (rg >> 1) * 8 + (rg & 1);
+}
+}  // namespace w43
+
+// packed[chunk][cot][part][3 xi + kw][sub][co][j] = split(sum_kh G43[xi][kh] w[co][map(k)][kh][kw])
+__global__ void pack_wino43_kernel(const float* __restrict__ w, __bf16* __restrict__ out, int Cout, int Cin_w,
+                                   const int32_t* __restrict__ chan_map, int K, int K_pad) {
+  const int n_cot = Cout / BN;
+  const int64_t total = (int64_t)(K_pad / KC) * n_cot * 3 * 2 * BN * SB;  // kernel columns
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t r = i;
+    const int j = r % SB; r /= SB;
+    const int co = r % BN; r /= BN;
+    const int sub = r % 2; r /= 2;
+    const int kw = r % 3; r /= 3;
+    const int cot = r % n_cot;
+    const int chunk = (int)(r / n_cot);
+    const int k = chunk * KC + sub * SB + j;
+    int ci = k < K ? (chan_map ? chan_map[k] : k) : -1;
+    if (ci >= Cin_w) ci = -1;
+    double g0 = 0.0, g1 = 0.0, g2 = 0.0;
+    if (ci >= 0) {
+      const float* g = w + ((int64_t)(cot * BN + co) * Cin_w + ci) * 9 + kw;  // g[3 kh]
+      g0 = g[0], g1 = g[3], g2 = g[6];
+    }
+    const double u[w43::NXI] = {0.25 * g0, -(g0 + g1 + g2) / 6.0, (g1 - g0 - g2) / 6.0,
+                                g0 / 24.0 + g1 / 12.0 + g2 / 6.0, g0 / 24.0 - g1 / 12.0 + g2 / 6.0, g2};
+    __bf16* o = out + ((int64_t)chunk * n_cot + cot) * 2 * w43::WPART + ((int64_t)sub * BN + co) * SB + j;
+#pragma unroll
+    for (int xi = 0; xi < w43::NXI; ++xi) {
+      const float v = (float)u[xi];
+      const __bf16 hi = (__bf16)v;
+      const int tap = 3 * xi + kw;
+      o[(int64_t)tap * KC * BN] = hi;
+      o[(int64_t)(w43::NTAP + tap) * KC * BN] = (__bf16)(v - (float)hi);
+    }
+  }
+}
+
+// T43 of a split-bf16 input (the slab, or y1 for conv2): a thread per (column, row tile q of the 16-row
+// tile, 8-channel block pair kq) and 2 blocks; d[m] = x[base + dil (m - 1)], m < 6 (zero outside the image
+// and the input rows).  With a frustum mask the groups it clears for the tile are skipped (as wino_rows).
+__global__ __launch_bounds__(256) void wino43_rows_kernel(const WinoRowsArgs a) {
+  constexpr int KB = 4;  // 8-channel blocks per workgroup: 4 x 32 x 2 threads, 2 blocks each
+  const int pp = blockIdx.x, b = blockIdx.z;
+  const int nbg = (a.group / SB + KB - 1) / KB;
+  const int g = blockIdx.y / nbg, kb0 = (blockIdx.y - g * nbg) * KB;
+  if (a.gmask && !((a.gmask[pp] >> g) & 1u)) return;
+  const int W = a.W;
+  const int ty = pp / a.tiles_x;
+  const int x0 = (pp - ty * a.tiles_x) * TW;
+  const int nb = a.group / SB, K8 = a.K / SB, R6 = w43::NXI * 4 * a.tiles_y;
+  const int64_t plane = (int64_t)a.in_rows * W;
+  const int c = threadIdx.x % TW, q = (threadIdx.x / TW) % 4, kq = threadIdx.x / (4 * TW);  // kq < 2
+  const int col = x0 + c, r4 = 4 * ty + q;
+  if (col >= W) return;
+  const int base = w43::RT4 * ty + (a.dil == 1 ? 4 * q : (q >> 1) * 8 + (q & 1));
+  int64_t roff[6];
+  bool rok[6];
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    const int row = a.out_row0 + base + a.dil * (m - 1), by = row - a.in_row0;
+    rok[m] = row >= 0 && row < a.H && by >= 0 && by < a.in_rows;
+    roff[m] = 2 * ((int64_t)by * W + col);
+  }
+  u32x4 raw[2][6][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int kb = kb0 + kq + 2 * i;
+    const bool kok = kb < nb && g * a.group + kb * SB < a.K;
+    const u32x4* src = a.x + ((int64_t)b * a.batch_stride + (int64_t)g * a.group_stride +
+                              (int64_t)(kok ? kb : 0) * SB * plane) / 4;
+#pragma unroll
+    for (int m = 0; m < 6; ++m)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) raw[i][m][p] = (kok && rok[m]) ? src[roff[m] + p] : u32x4{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int kb = kb0 + kq + 2 * i, k0 = g * a.group + kb * SB;
+    if (kb >= nb || k0 >= a.K) continue;
+    float d[6][8];
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+      float h[8], l[8];
+      bf16x8_to_f32(raw[i][m][0], h);
+      bf16x8_to_f32(raw[i][m][1], l);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d[m][j] = h[j] + l[j];
+    }
+    u32x4* dst = a.t + 2 * (((int64_t)b * K8 + k0 / SB) * R6 * W + (int64_t)w43::NXI * r4 * W) + col;
+#pragma unroll
+    for (int xi = 0; xi < w43::NXI; ++xi) {
+      unsigned hp[4], lp[4];
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4) {
+        unsigned short hs[2], ls[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int j = 2 * e4 + e;
+          const float d0 = d[0][j], d1 = d[1][j], d2 = d[2][j], d3 = d[3][j], d4 = d[4][j], d5 = d[5][j];
+          const float v = xi == 0 ? 4.f * d0 - 5.f * d2 + d4
+                        : xi == 1 ? -4.f * d1 - 4.f * d2 + d3 + d4
+                        : xi == 2 ? 4.f * d1 - 4.f * d2 - d3 + d4
+                        : xi == 3 ? -2.f * d1 - d2 + 2.f * d3 + d4
+                        : xi == 4 ? 2.f * d1 - d2 - 2.f * d3 + d4
+                                  : 4.f * d1 - 5.f * d3 + d5;
+          const __bf16 hv = (__bf16)v, lv = (__bf16)(v - (float)hv);
+          hs[e] = __builtin_bit_cast(unsigned short, hv);
+          ls[e] = __builtin_bit_cast(unsigned short, lv);
+        }
+        hp[e4] = (unsigned)hs[0] | ((unsigned)hs[1] << 16);
+        lp[e4] = (unsigned)ls[0] | ((unsigned)ls[1] << 16);
+      }
+      dst[2 * (int64_t)xi * W] = u32x4{hp[0], hp[1], hp[2], hp[3]};
+      dst[2 * (int64_t)xi * W + W] = u32x4{lp[0], lp[1], lp[2], lp[3]};
+    }
+  }
+}
+
+// The F(4,3) conv: conv_wino_kernel's ring, DMAs, fragment schedule and epilogues, with units walked
+// xi-major (above).  Two walkers of the tile's chunk sequence: the DMA side issues unit u + 4 while the
+// compute side runs unit u; at the end of each xi's K sum the accumulators are folded into y.
+template <bool RELU, int DIL, bool P3>
+__global__ __launch_bounds__(RNT, 1) void conv_wino43_kernel(const Args a) {
+  using namespace wino;  // the ring geometry (NIW, NIT, NWI, Geo, SLOT, NSLOT, LDS) is F(3,3)'s
+  using G = Geo<DIL>;
+  constexpr int XW = G::XW, TROW = G::TROW, NXT = G::NXT;
+  constexpr int NX6 = w43::NXI;
+  __shared__ __attribute__((aligned(16))) u32x4 lds[LDS];
+  const int W = a.W;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l32 = lane & 31, kl = lane >> 5;
+
+  int tile = xcd_remap(blockIdx.x, a.nwg);
+  if (a.gmask) {
+    const int Gq = a.mgroup;
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int q = j / a.n_cot;
+    const int slot = Gq * (8 * (q / Gq) + x) + q % Gq;
+    if (slot >= a.npix) return;
+    tile = (a.tile_order ? a.tile_order[slot] : slot) * a.n_cot + j % a.n_cot;
+  }
+  const int cot = tile % a.n_cot, rest = tile / a.n_cot;
+  const int t_main = a.tiles_y * a.tiles_x;
+  const int pp = rest % t_main, b = rest / t_main;
+  const int ty = pp / a.tiles_x;
+  const int x0 = (pp - ty * a.tiles_x) * TW;
+  const int y0 = a.out_row0 + ty * w43::RT4;
+  const uint32_t gm = a.gmask ? a.gmask[pp] : 0u;
+  const int nch = a.gmask ? __builtin_popcount(gm) * a.cpg : a.nchunks;
+  const int K8 = a.K / SB;
+  const int64_t tplane2 = 2LL * (w43::XH * a.tiles_y) * W;
+  const uint32_t tplane_b = (uint32_t)(tplane2 * 16);
+  constexpr uint32_t kOOB = 0x80000000u;
+  uint32_t wvo[NWI], tvo[NXTMAX];
+#pragma unroll
+  for (int j = 0; j < NWI; ++j) {
+    const int e = (j * NIW + wave) * 64 + lane;
+    wvo[j] = (uint32_t)(((e / RHALF) * (w43::NTAP * 2 * BN) + e % RHALF) * 16);
+    asm volatile("" : "+v"(wvo[j]));
+  }
+#pragma unroll
+  for (int j = 0; j < NXT; ++j) {
+    const int e = (j * NIW + wave) * 64 + lane;
+    const int sub = e / (TROW / 2), part = (e / (TROW / 4)) & 1, rt = (e % (TROW / 4)) / XW, c = e % XW;
+    const int gx = x0 - DIL + c;
+    const bool z = e >= TROW || gx < 0 || gx >= W;
+    tvo[j] = z ? kOOB : (uint32_t)sub * tplane_b + (uint32_t)((2 * (w43::XH * ty + NX6 * rt) * W + part * W + gx) * 16);
+    asm volatile("" : "+v"(tvo[j]));
+  }
+  // the DMA side's walker (issuing waves only; a scalar branch): unit (ixi, iwi-th chunk of the tile's
+  // sequence = chunk ph, index ici of its group), its weight / T bases stepped per chunk (the per-unit
+  // address arithmetic of a walker that multiplies out every base cost 90-130 scalar instructions per
+  // unit on every wave, ~4x the F(3,3) kernel's); past the last unit it stays on it (dummy loads that
+  // keep the vmcnt counts exact)
+  const int cpg = a.gmask ? a.cpg : max(nch, 1);
+  const uint32_t rem0 = a.gmask ? gm : 1u;
+  const int gbase0 = a.gmask ? __builtin_ctz(gm | 0x80000000u) * cpg : 0;
+  const int64_t wstep = (int64_t)a.n_cot * w43::W16 * 16, tstep = 2 * tplane2 * 16;
+  const char* w_first = reinterpret_cast<const char*>(a.wp + (int64_t)cot * w43::W16) + gbase0 * wstep;
+  const char* t_first = reinterpret_cast<const char*>(static_cast<const u32x4*>(a.x) + (int64_t)b * K8 * tplane2) +
+                        gbase0 * tstep;
+  const char* iwp = w_first;
+  const char* itp = t_first;
+  uint32_t irem = rem0;
+  int ph = gbase0, ici = 0, iwi = 0, ixi = 0, irows_b = 0;
+  auto issue_next = [&](int slot) __attribute__((always_inline)) {
+    if (wave >= NIW) return;
+    u32x4* dst = lds + slot * SLOT + wave * 64;
+    const __amdgpu_buffer_rsrc_t rw =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(iwp), (short)0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int j = 0; j < NWI; ++j)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (__attribute__((address_space(3))) void*)(dst + j * NIT), 16,
+                                               wvo[j], 0, 0, 0);
+    const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<char*>(itp), (short)0, 2 * ph + 1 < K8 ? 0x7fffffff : (int)(tplane_b - irows_b), 0x00020000);
+#pragma unroll
+    for (int j = 0; j < NXT; ++j)
+      if ((j * NIW + wave) * 64 < TROW)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rt, (__attribute__((address_space(3))) void*)(dst + RUNIT + j * NIT),
+                                                 16, tvo[j], 0, 0, 0);
+    if (iwi + 1 < nch) {
+      ++iwi;
+      if (++ici == cpg) {  // the next set group of the mask
+        ici = 0;
+        irem &= irem - 1;
+        const int nph = __builtin_ctz(irem | 0x80000000u) * cpg;
+        iwp += (nph - ph) * wstep;
+        itp += (nph - ph) * tstep;
+        ph = nph;
+      } else {
+        ++ph;
+        iwp += wstep;
+        itp += tstep;
+      }
+    } else if (ixi + 1 < NX6) {  // the next xi: the chunk sequence from its start
+      ++ixi;
+      iwi = 0, ici = 0, irem = rem0, ph = gbase0;
+      irows_b = ixi * W * 32;
+      iwp = w_first + ixi * 3 * 2 * BN * 16;
+      itp = t_first + irows_b;
+    }
+  };
+
+  const int rg = wave & 3;
+  const int cw = 64 * (wave >> 2);
+  floatx16 acc[2], y[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    acc[i] = floatx16{0};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[i][r] = floatx16{0};
+  }
+  bf16x8 fb[3][2];
+  bf16x8 fa[2][2][2];
+  auto fetch_b = [&](int kw, int slot) __attribute__((always_inline)) {
+    const u32x4* X = lds + slot * SLOT + RUNIT + kl * (TROW / 2) + rg * XW + l32 + DIL * kw;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) fb[kw][p] = __builtin_bit_cast(bf16x8, X[p * (TROW / 4)]);
+  };
+  auto fetch_a = [&](int st, int slot, int kw) __attribute__((always_inline)) {
+    const u32x4* Wl = lds + slot * SLOT + kw * 2 * BN + kl * BN + cw + l32;
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) fa[st][ct][p] = __builtin_bit_cast(bf16x8, Wl[p * RHALF + 32 * ct]);
+  };
+  auto sched6 = [&](auto nreads) __attribute__((always_inline)) {
+    constexpr int n = decltype(nreads)::value;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      if (i < n) __builtin_amdgcn_sched_group_barrier(0x100, (n + 5) / 6, 0);
+    }
+  };
+  // y[r] += A^T[r][xi] M_xi: A^T column xi = (1, s p, p^2, s p^3), p = (xi + 1) / 2, s = +-1 (xi 1-4);
+  // (1, 0, 0, 0) for xi 0, (0, 0, 0, 1) for xi 5
+  auto fold = [&](int xi) __attribute__((always_inline)) {
+    const float p = (float)((xi + 1) >> 1), sp = (xi & 1) ? p : -p;
+    const bool mid = xi > 0 && xi < 5;
+    const float c0 = xi < 5 ? 1.f : 0.f, c1 = mid ? sp : 0.f, c2 = mid ? p * p : 0.f,
+                c3 = mid ? sp * p * p : (xi == 5 ? 1.f : 0.f);
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct) {
+      y[ct][0] += c0 * acc[ct];
+      y[ct][1] += c1 * acc[ct];
+      y[ct][2] += c2 * acc[ct];
+      y[ct][3] += c3 * acc[ct];
+      acc[ct] = floatx16{0};
+    }
+  };
+
+  constexpr int NXT_LO = TROW / NIT;
+  constexpr int WHI = (TROW % NIT + 63) / 64;
+  static_assert(NXT_LO + (WHI > 0) == NXT, "T pieces");
+  constexpr int NPU_HI = NWI + NXT;
+  constexpr int NPU_LO = NWI + NXT_LO;
+  const bool whi = wave < WHI;
+  if (nch > 0) {
+    const int U = NX6 * nch;
+    int cleft = nch, cxi = 0;  // the compute side: units left in xi cxi
+    issue_next(0);
+    issue_next(1);
+    issue_next(2);
+    issue_next(3);
+    if (whi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPU_HI) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NPU_LO) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    fetch_b(0, 0);
+    fetch_b(1, 0);
+    fetch_a(0, 0, 0);
+#define W43_MFMAS(AS, KW)                                                                              \
+  _Pragma("unroll") for (int ct = 0; ct < 2; ++ct) {                                                   \
+    acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][1], fb[KW][0], acc[ct], 0, 0, 0);     \
+    acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][1], acc[ct], 0, 0, 0);     \
+    acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][0], acc[ct], 0, 0, 0);     \
+  }
+#define W43_UNIT(R)                                                                                    \
+  do {                                                                                                 \
+    constexpr int P = (R) & 1, slot = (R) & 3, nslot = ((R) + 1) & 3; /* u0 % 4 == 0 */               \
+    if (u0 + (R) >= U) break;                                                                          \
+    fetch_a(P ^ 1, slot, 1);                                                                           \
+    fetch_b(2, slot);                                                                                  \
+    W43_MFMAS(P, 0);                                                                                   \
+    sched6(std::integral_constant<int, 6>{});                                                          \
+    fetch_a(P, slot, 2);                                                                               \
+    W43_MFMAS(P ^ 1, 1);                                                                               \
+    sched6(std::integral_constant<int, 4>{});                                                          \
+    if (whi) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU_HI) : "memory");             \
+    else asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * NPU_LO) : "memory");                  \
+    __builtin_amdgcn_s_barrier();                                                                      \
+    asm volatile("" ::: "memory");                                                                     \
+    issue_next(slot); /* unit u + 4 into this slot */                                                  \
+    fetch_b(0, nslot);                                                                                 \
+    fetch_b(1, nslot);                                                                                 \
+    fetch_a(P ^ 1, nslot, 0);                                                                          \
+    W43_MFMAS(P, 2);                                                                                   \
+    sched6(std::integral_constant<int, 8>{});                                                          \
+    if (--cleft == 0) {                                                                                \
+      fold(cxi);                                                                                       \
+      ++cxi;                                                                                           \
+      cleft = nch;                                                                                     \
+    }                                                                                                  \
+  } while (0)
+    for (int u0 = 0; u0 < U; u0 += 4) {
+      W43_UNIT(0); W43_UNIT(1); W43_UNIT(2); W43_UNIT(3);
+    }
+#undef W43_UNIT
+#undef W43_MFMAS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the block exits
+  }
+  const int row_base = y0 + w43::base_row<DIL>(rg), col = x0 + l32;
+  if constexpr (P3) {
+    cout1_partials<RELU, 4>(a, b, row_base, DIL, col, cot, cw, y, lds);
+  } else {
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt)
+        store_block<RELU>(a, b, row_base + pt * DIL, col, cot * BN + cw + 32 * ct, y[ct][pt]);
+  }
+}
+
+static int wino43_rows_launch(const void* x, const mvbev_conv_desc* d, int dil, const uint32_t* group_mask, void* t,
+                              size_t t_bytes, void* stream) {
+  if (!x || !d || !t) return MVBEV_ERR_NULL;
+  if (dil != 1 && dil != 2) return MVBEV_ERR_DILATION;
+  if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || d->in_rows <= 0 || d->out_rows <= 0 || d->group <= 0)
+    return MVBEV_ERR_RANK;
+  if (d->K % SB != 0 || d->group % SB != 0 || d->K % d->group != 0) return MVBEV_ERR_SHAPE;
+  if (d->out_row0 < 0 || d->out_row0 + d->out_rows > d->H || d->K / d->group > 65535 || d->B > 65535)
+    return MVBEV_ERR_SHAPE;
+  const int64_t tiles_y = ceil_div(d->out_rows, w43::RT4), tiles_x = ceil_div(d->W, TW);
+  const int64_t need = d->B * (d->K / SB) * w43::NXI * 4 * tiles_y * d->W * 32;
+  if ((size_t)need > t_bytes || 2 * need / 32 > (int64_t)INT32_MAX * 8) return MVBEV_ERR_SHAPE;
+  if (group_mask && d->K / d->group > 32) return MVBEV_ERR_SHAPE;
+  if (((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(t)) & 15) != 0) return MVBEV_ERR_ALIGN;
+  WinoRowsArgs a{};
+  a.x = static_cast<const u32x4*>(x);
+  a.t = static_cast<u32x4*>(t);
+  a.group_stride = d->group_stride, a.batch_stride = d->batch_stride;
+  a.K = (int)d->K, a.group = (int)d->group, a.H = (int)d->H, a.W = (int)d->W;
+  a.in_row0 = (int)d->in_row0, a.in_rows = (int)d->in_rows, a.out_row0 = (int)d->out_row0;
+  a.tiles_x = (int)tiles_x, a.tiles_y = (int)tiles_y;
+  a.dil = dil;
+  a.gmask = group_mask;
+  const int64_t nbg = ceil_div(d->group / SB, 4);  // wino43_rows_kernel's KB
+  if ((d->K / d->group) * nbg > 65535) return MVBEV_ERR_SHAPE;
+  hipLaunchKernelGGL(wino43_rows_kernel, dim3((unsigned)(tiles_x * tiles_y), (unsigned)((d->K / d->group) * nbg),
+                                              (unsigned)d->B),
+                     dim3(256), 0, as_stream(stream), a);
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+static int wino43_launch(const void* t, const mvbev_conv_desc* d, const void* w_packed, const float* bias,
+                         const float* init, int64_t Cout, int dil, int relu, float* y, int y_layout,
+                         const uint32_t* group_mask, const int32_t* tile_order, const float* w3, float* p3,
+                         void* stream) {
+  if (!t || !d || !w_packed || (!y && !p3)) return MVBEV_ERR_NULL;
+  if (dil != 1 && dil != 2) return MVBEV_ERR_DILATION;
+  if (p3 && (!w3 || group_mask || init || dil != 2 || !relu)) return MVBEV_ERR_SHAPE;
+  if (d->B <= 0 || d->K <= 0 || d->H <= 0 || d->W <= 0 || Cout <= 0 || d->out_rows <= 0 || d->group <= 0)
+    return MVBEV_ERR_RANK;
+  if (Cout % BN != 0 || d->K % SB != 0 || d->group % SB != 0 || d->K % d->group != 0) return MVBEV_ERR_SHAPE;
+  if (d->out_row0 < 0 || d->out_row0 + d->out_rows > d->H || d->H > INT32_MAX / 2 || d->W > INT32_MAX / 2)
+    return MVBEV_ERR_SHAPE;
+  if (y_layout != MVBEV_LAYOUT_F32 && y_layout != MVBEV_LAYOUT_SPLIT_BF16) return MVBEV_ERR_SHAPE;
+  if (((reinterpret_cast<uintptr_t>(w_packed) | reinterpret_cast<uintptr_t>(t)) & 15) != 0) return MVBEV_ERR_ALIGN;
+  Args a{};
+  a.x = t; a.wp = static_cast<const u32x4*>(w_packed); a.bias = bias; a.init = init; a.y = y;
+  a.w3 = w3; a.p3 = p3;
+  a.B = (int)d->B; a.group = (int)d->group; a.K = (int)d->K; a.nchunks = (int)ceil_div(d->K, KC);
+  a.Cout = (int)Cout; a.H = (int)d->H; a.W = (int)d->W;
+  a.in_row0 = 0; a.in_rows = (int)d->H;
+  a.out_row0 = (int)d->out_row0; a.out_rows = (int)d->out_rows;
+  a.tiles_x = (int)ceil_div(d->W, TW); a.tiles_y = (int)ceil_div(d->out_rows, w43::RT4);
+  a.n_cot = (int)(Cout / BN);
+  const int64_t tiles = (int64_t)a.tiles_x * a.tiles_y * a.n_cot * d->B;
+  if (tiles > INT32_MAX / 2 || 2LL * w43::NXI * 4 * a.tiles_y * a.W * (d->K / SB) * d->B > (int64_t)INT32_MAX * 64)
+    return MVBEV_ERR_SHAPE;
+  if (2LL * 32 * w43::XH * a.tiles_y * a.W >= (1LL << 31)) return MVBEV_ERR_SHAPE;
+  if (group_mask) {
+    if (d->group % KC != 0 || d->K / d->group > 32) return MVBEV_ERR_SHAPE;
+    a.gmask = group_mask;
+    a.cpg = (int)(d->group / KC);
+  }
+  a.tile_order = group_mask ? tile_order : nullptr;
+  a.y_split = y_layout == MVBEV_LAYOUT_SPLIT_BF16;
+  a.npix = (int)(tiles / a.n_cot);
+  a.mgroup = (group_mask && tiles >= 8 * (int64_t)std::max(cu_count(), 1)) ? 8 : 1;
+  const int64_t nwg = group_mask ? (int64_t)a.n_cot * round_up(a.npix, 8 * a.mgroup) : tiles;
+  a.nwg = (int)nwg;
+  hipStream_t s = as_stream(stream);
+  const dim3 grid((unsigned)nwg), blk(RNT);
+  if (p3) hipLaunchKernelGGL((conv_wino43_kernel<true, 2, true>), grid, blk, 0, s, a);
+  else if (dil == 2) {
+    if (relu) hipLaunchKernelGGL((conv_wino43_kernel<true, 2, false>), grid, blk, 0, s, a);
+    else hipLaunchKernelGGL((conv_wino43_kernel<false, 2, false>), grid, blk, 0, s, a);
+  } else if (relu) {
+    hipLaunchKernelGGL((conv_wino43_kernel<true, 1, false>), grid, blk, 0, s, a);
+  } else {
+    hipLaunchKernelGGL((conv_wino43_kernel<false, 1, false>), grid, blk, 0, s, a);
+  }
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
 }  // namespace b3
 }  // namespace mvbev
 
@@ -2112,6 +2569,62 @@ int mvbev_conv3x3_wino_bf16x3_cout1_partials(const void* t, const mvbev_conv_des
   if (need == 0 || partials_bytes < need) return MVBEV_ERR_SHAPE;
   return mvbev::b3::wino_launch(t, desc, w_packed, bias, nullptr, Cout, relu, nullptr, MVBEV_LAYOUT_F32, nullptr,
                                 nullptr, stream, dilation, w3, static_cast<float*>(partials));
+}
+
+}  // extern "C"
+
+/* row-Winograd F(4,3) (xi-major; ABI 12400) */
+extern "C" {
+
+size_t mvbev_conv3x3_packed_bytes_wino43(int64_t Cout, int64_t K) {
+  if (Cout <= 0 || K <= 0) return 0;
+  return (size_t)(mvbev::round_up(K, mvbev::b3::KC) / mvbev::b3::KC) * (size_t)(Cout / mvbev::b3::BN) *
+         mvbev::b3::w43::W16 * 16;
+}
+
+int mvbev_pack_conv3x3_weight_wino43(const float* w, int64_t Cout, int64_t Cin_w, const int32_t* chan_map, int64_t K,
+                                     void* w_packed, void* stream) {
+  using namespace mvbev;
+  if (!w || !w_packed) return MVBEV_ERR_NULL;
+  if (Cout <= 0 || Cin_w <= 0 || K <= 0) return MVBEV_ERR_RANK;
+  if (Cout % b3::BN != 0) return MVBEV_ERR_SHAPE;
+  if (!chan_map && K != Cin_w) return MVBEV_ERR_SHAPE;
+  const int64_t total = (int64_t)mvbev_conv3x3_packed_bytes_wino43(Cout, K) / 2 / (2 * b3::w43::NXI);  // threads
+  const int blocks = (int)std::min<int64_t>(ceil_div(total, 256), 8192);
+  hipLaunchKernelGGL(b3::pack_wino43_kernel, dim3(blocks), dim3(256), 0, as_stream(stream), w,
+                     static_cast<__bf16*>(w_packed), (int)Cout, (int)Cin_w, chan_map, (int)K,
+                     (int)round_up(K, b3::KC));
+  MVBEV_CHECK_LAUNCH();
+  return MVBEV_OK;
+}
+
+size_t mvbev_wino43_rows_bytes(const mvbev_conv_desc* d) {
+  using namespace mvbev;
+  if (!d || d->B <= 0 || d->K <= 0 || d->W <= 0 || d->out_rows <= 0) return 0;
+  return (size_t)d->B * (size_t)(ceil_div(d->K, b3::SB)) * b3::w43::NXI * 4 *
+         (size_t)ceil_div(d->out_rows, b3::w43::RT4) * (size_t)d->W * 32;
+}
+
+int mvbev_wino43_rows_split_bf16(const void* x, const mvbev_conv_desc* desc, int dilation, const uint32_t* group_mask,
+                                 void* t, size_t t_bytes, void* stream) {
+  return mvbev::b3::wino43_rows_launch(x, desc, dilation, group_mask, t, t_bytes, stream);
+}
+
+int mvbev_conv3x3_wino43_bf16x3(const void* t, const mvbev_conv_desc* desc, const void* w_packed, const float* bias,
+                                const float* init, int64_t Cout, int dilation, int relu, void* y, int y_layout,
+                                const uint32_t* group_mask, const int32_t* tile_order, void* stream) {
+  return mvbev::b3::wino43_launch(t, desc, w_packed, bias, init, Cout, dilation, relu, static_cast<float*>(y),
+                                  y_layout, group_mask, tile_order, nullptr, nullptr, stream);
+}
+
+int mvbev_conv3x3_wino43_bf16x3_cout1_partials(const void* t, const mvbev_conv_desc* desc, const void* w_packed,
+                                               const float* bias, int64_t Cout, int dilation, int relu,
+                                               const float* w3, void* partials, size_t partials_bytes, void* stream) {
+  if (!desc || !w3 || !partials) return MVBEV_ERR_NULL;
+  const size_t need = mvbev_conv3x3_bf16x3_cout1_partials_bytes(desc, Cout);
+  if (need == 0 || partials_bytes < need) return MVBEV_ERR_SHAPE;
+  return mvbev::b3::wino43_launch(t, desc, w_packed, bias, nullptr, Cout, dilation, relu, nullptr, MVBEV_LAYOUT_F32,
+                                  nullptr, nullptr, w3, static_cast<float*>(partials), stream);
 }
 
 }  // extern "C"

@@ -1116,6 +1116,125 @@ def conv3x3_wino_then_cout1_partials(t: torch.Tensor, desc, packed: torch.Tensor
     _native.check(st, "mvbev_conv3x3_wino_bf16x3_cout1_partials")
 
 
+# -- row-Winograd F(4,3) (ABI 12400: mvbev_*wino43*) ------------------------------------------------
+WINO43_TILE_ROWS = 16  # output rows per F(4,3) conv tile (its frustum-mask / order granule)
+
+
+def wino43_rows_bytes(desc) -> int:
+    """Bytes of the F(4,3) row transform T43 of a conv input (``mvbev_wino43_rows_bytes``)."""
+    return int(_native.load().mvbev_wino43_rows_bytes(ctypes.byref(desc)))
+
+
+def _mask43(mask, desc, what: str):
+    if mask is None:
+        return None
+    _require_cuda(mask)
+    tiles = -(-desc.out_rows // WINO43_TILE_ROWS) * -(-desc.W // _native.TILE_W)
+    if mask.dtype != torch.int32 or mask.numel() < tiles or not mask.is_contiguous():
+        raise ValueError(f"{what} must be a contiguous int32 tensor of >= {tiles} tiles (16 x 32)")
+    return mask.data_ptr()
+
+
+def wino43_rows(x: torch.Tensor, desc, t: torch.Tensor, group_mask: Optional[torch.Tensor] = None,
+                dilation: int = 1) -> torch.Tensor:
+    """B^T of F(4,3) over every 4-row output tile's 6 input rows of the split-bf16 ``x`` into ``t``
+    (``mvbev_wino43_rows_split_bf16``; ``group_mask`` over 16 x 32 tiles, ``t`` zero-filled once)."""
+    _require_cuda(x, t)
+    if x.dtype != torch.bfloat16 or t.dtype != torch.bfloat16 or not t.is_contiguous():
+        raise TypeError("wino43_rows reads the split-bf16 slab and writes a contiguous bf16 T")
+    st = _native.load().mvbev_wino43_rows_split_bf16(x.data_ptr(), ctypes.byref(desc), int(dilation),
+                                                     _mask43(group_mask, desc, "group_mask"), t.data_ptr(),
+                                                     t.numel() * t.element_size(), _stream(x))
+    _native.check(st, "mvbev_wino43_rows_split_bf16")
+    return t
+
+
+def pack_wino43(weight: torch.Tensor, chan_map: Optional[torch.Tensor] = None,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """G w of F(4,3), split hi / lo, in the F(4,3) conv's layout (``mvbev_pack_conv3x3_weight_wino43``);
+    ``chan_map``: device int32 map of the conv input channel k to the weight's input channel."""
+    _require_cuda(weight)
+    cout, cin, kh, kw = weight.shape
+    if (kh, kw) != (3, 3) or weight.dtype != torch.float32 or cout % BN:
+        raise ValueError("expected a float32 [Cout,Cin,3,3] weight with Cout a multiple of 128")
+    K = cin if chan_map is None else chan_map.numel()
+    lib = _native.load()
+    n = int(lib.mvbev_conv3x3_packed_bytes_wino43(cout, K)) // 2
+    if out is None or out.numel() < n:
+        out = torch.empty(n, dtype=torch.bfloat16, device=weight.device)
+    w = weight.detach().contiguous()
+    st = lib.mvbev_pack_conv3x3_weight_wino43(w.data_ptr(), cout, cin, None if chan_map is None else
+                                              chan_map.data_ptr(), K, out.data_ptr(), _stream(out))
+    _native.check(st, "mvbev_pack_conv3x3_weight_wino43")
+    return out
+
+
+def conv3x3_wino43(t: torch.Tensor, desc, packed: torch.Tensor, cout: int, bias: Optional[torch.Tensor] = None,
+                   init: Optional[torch.Tensor] = None, relu: bool = False, out: Optional[torch.Tensor] = None,
+                   group_mask: Optional[torch.Tensor] = None, tile_order: Optional[torch.Tensor] = None,
+                   dilation: int = 1) -> torch.Tensor:
+    """``conv3x3_wino`` in the F(4,3) form: from ``wino43_rows``' T and ``pack_wino43`` weights
+    (``mvbev_conv3x3_wino43_bf16x3``; mask / order over 16 x 32 tiles; ``out`` fp32 or split-bf16)."""
+    _require_cuda(t, packed)
+    B, W, out_rows = desc.B, desc.W, desc.out_rows
+    lib = _native.load()
+    if packed.numel() * packed.element_size() < lib.mvbev_conv3x3_packed_bytes_wino43(cout, desc.K):
+        raise ValueError("packed weights are smaller than the F(4,3) conv needs")
+    if t.numel() * t.element_size() < wino43_rows_bytes(desc):
+        raise ValueError("t is smaller than the descriptor's F(4,3) transform")
+    y_split = out is not None and out.dtype == torch.bfloat16
+    if out is None:
+        out = torch.empty((B, cout, out_rows, W), dtype=torch.float32, device=t.device)
+    elif y_split:
+        if tuple(out.shape) != split_shape(B, cout, out_rows, W) or not out.is_contiguous():
+            raise ValueError(f"a split out must be a contiguous bf16 {split_shape(B, cout, out_rows, W)} tensor")
+    elif tuple(out.shape) != (B, cout, out_rows, W) or not out.is_contiguous() or out.dtype != torch.float32:
+        raise ValueError(f"out must be a contiguous fp32 [{B},{cout},{out_rows},{W}] tensor")
+    if init is not None:
+        _require_cuda(init)
+        if init.numel() != cout * desc.H * W or not init.is_contiguous():
+            raise ValueError("init must be a contiguous [Cout,H,W] tensor")
+    gmp = _mask43(group_mask, desc, "group_mask")
+    top = None
+    if tile_order is not None:
+        tiles = -(-out_rows // WINO43_TILE_ROWS) * -(-W // _native.TILE_W)
+        if group_mask is None or tile_order.dtype != torch.int32 or tile_order.numel() != B * tiles:
+            raise ValueError("tile_order must be an int32 permutation of the B x tiles pixel tiles")
+        top = tile_order.data_ptr()
+    b = bias.detach().contiguous() if bias is not None else None
+    st = lib.mvbev_conv3x3_wino43_bf16x3(t.data_ptr(), ctypes.byref(desc), packed.data_ptr(),
+                                         b.data_ptr() if b is not None else None,
+                                         init.data_ptr() if init is not None else None, cout, int(dilation),
+                                         int(bool(relu)), out.data_ptr(),
+                                         _native.LAYOUT_SPLIT_BF16 if y_split else _native.LAYOUT_F32, gmp, top,
+                                         _stream(t))
+    _native.check(st, "mvbev_conv3x3_wino43_bf16x3")
+    return out
+
+
+def conv3x3_wino43_then_cout1_partials(t: torch.Tensor, desc, packed: torch.Tensor, cout: int,
+                                       bias: Optional[torch.Tensor], relu: bool, weight3: torch.Tensor,
+                                       partials: torch.Tensor) -> None:
+    """``conv3x3_wino_then_cout1_partials`` (dilation 2) in the F(4,3) form: the same partials
+    (``mvbev_conv3x3_wino43_bf16x3_cout1_partials``)."""
+    _require_cuda(t, packed, weight3, partials)
+    if tuple(weight3.shape) != (1, cout, 3, 3):
+        raise ValueError(f"weight3 must be [1,{cout},3,3], got {tuple(weight3.shape)}")
+    if partials.dtype != torch.float32 or not partials.is_contiguous():
+        raise ValueError("partials must be a contiguous float32 tensor")
+    lib = _native.load()
+    if packed.numel() * packed.element_size() < lib.mvbev_conv3x3_packed_bytes_wino43(cout, desc.K):
+        raise ValueError("packed weights are smaller than the F(4,3) conv needs")
+    if t.numel() * t.element_size() < wino43_rows_bytes(desc):
+        raise ValueError("t is smaller than the descriptor's F(4,3) transform")
+    w3 = weight3.detach().contiguous()
+    b = bias.detach().contiguous() if bias is not None else None
+    st = lib.mvbev_conv3x3_wino43_bf16x3_cout1_partials(
+        t.data_ptr(), ctypes.byref(desc), packed.data_ptr(), b.data_ptr() if b is not None else None, int(cout), 2,
+        int(bool(relu)), w3.data_ptr(), partials.data_ptr(), partials.numel() * partials.element_size(), _stream(t))
+    _native.check(st, "mvbev_conv3x3_wino43_bf16x3_cout1_partials")
+
+
 def cout1_from_partials(partials: torch.Tensor, desc, cout: int, dilation3: int, map_row0: int, map_rows: int,
                         out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``conv2d(act(y), weight3, padding=d3, dilation=d3)`` rows ``[map_row0, map_row0+map_rows)``

@@ -30,7 +30,7 @@ def test_library_exports_every_header_symbol():
     assert declared == sorted(_native.EXPORTS)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.mvbev_version() == 12300
+    assert lib.mvbev_version() == 12400
     assert lib.mvbev_status_string(0) == b"ok"
     assert lib.mvbev_status_string(-100) == b"HIP launch failed"
 

@@ -144,6 +144,7 @@ def main():
     ap.add_argument("--libs", default="", help="comma-separated libmvbev variants to A/B (interleaved rounds)")
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--no-frustum", action="store_true", help="dense conv1 (no frustum mask)")
+    ap.add_argument("--check43", action="store_true", help="print the F(4,3) vs F(3,3) difference at full size")
     args = ap.parse_args()
     spec = synthetic.CONFIGS[args.config]
     ds = spec["make"]()
@@ -175,7 +176,34 @@ def main():
         wd1 = ops.conv_desc(B, weng.S * weng.Cs, ho, wo, group=weng.Cs, group_stride=B * weng.Cs * ho * wo,
                             batch_stride=weng.Cs * ho * wo)
         wgm = weng.conv1_mask(dev, 0, ho)
+        # row-Winograd F(4,3) (ABI 12400, xi-major): conv1 from the slab's T43 (16 x 32 mask / order) and
+        # conv2 -> conv3 partials from y1's dilation-2 T43, beside the F(3,3) stages winoconv / conv23w
+        wgm43 = weng.conv1_mask(dev, 0, ho, tile_h=ops.WINO43_TILE_ROWS)
+        word43 = ops.heavy_first_order(wgm43, B) if wgm43 is not None else None
+        t43 = torch.zeros((ops.wino43_rows_bytes(wd1) + 1) // 2, dtype=torch.bfloat16, device=dev)
+        ops.wino43_rows(wws.slab, wd1, t43, wgm43)
+        pk43 = ops.pack_wino43(mc[0].weight, weng.pack1w.map_dev(dev))
+        d2 = weng._conv2_desc(wws)
+        t243 = torch.zeros((ops.wino43_rows_bytes(d2) + 1) // 2, dtype=torch.bfloat16, device=dev)
+        pk243 = ops.pack_wino43(mc[2].weight)
+        p3_43 = torch.empty(ops.conv3x3_cout1_partials_bytes(d2, 512) // 4, dtype=torch.float32, device=dev)
+        y1_43 = torch.empty_like(wws.y1)
+
+        def conv23w43():
+            ops.wino43_rows(wws.y1, d2, t243, dilation=2)
+            ops.conv3x3_wino43_then_cout1_partials(t243, d2, pk243, 512, mc[2].bias, True, mc[4].weight, p3_43)
+            return ops.cout1_from_partials(p3_43, d2, 512, 4, wws.band[0], wws.band[1] - wws.band[0])
+
         stages = {
+            "winorows43": (lambda: ops.wino43_rows(wws.slab, wd1, t43, wgm43), None),
+            "winoconv43": (lambda: ops.conv3x3_wino43(t43, wd1, pk43, 512, init=weng.coord_term(mc[0]), relu=True,
+                                                      out=y1_43, group_mask=wgm43, tile_order=word43),
+                           2.0 * B * ho * wo * 9 * N * C * 512),
+            "conv2w43": (lambda: ops.conv3x3_wino43_then_cout1_partials(t243, d2, pk243, 512, mc[2].bias, True,
+                                                                        mc[4].weight, p3_43),
+                         2.0 * B * ho * wo * 9 * 512 * 512),
+            "winorows2_43": (lambda: ops.wino43_rows(wws.y1, d2, t243, dilation=2), None),
+            "conv23w43": (conv23w43, 2.0 * B * ho * wo * 9 * 512 * 512),
             "warp": (lambda: eng.warp_views(ws, list(range(N)), feats), None),
             "warpup": (lambda: eng.warp_views_upsampled(ws, list(range(N)), bfeats), None),
             "warp1": (lambda: [eng.warp_view(ws, v, feats[v]) for v in range(N)], None),
@@ -242,6 +270,26 @@ def main():
             stages["adjuppix"] = ((lambda: ops.warp_views_adjoint(dpv, plu, gs, pixel_major=True)), None)
         if {"wgrad1", "wgrad1w", "wgrad2w", "wgrad1f", "dgrad1", "dgrad1s", "wgrad2", "wgrad2f", "dgrad2"} & set(args.only.split(",")):
             stages.update(backward_stages(eng, ws, mc, B, ho, wo, N, C, dev))
+        if args.check43:  # F(4,3) vs F(3,3) at this config's full size (normwise over y1 and the map)
+            weng.conv1(wws, mc[0])
+            y1_33 = weng.y1_fp32(wws).clone()
+            ops.conv3x3_wino43(t43, wd1, pk43, 512, init=weng.coord_term(mc[0]), relu=True, out=y1_43,
+                               group_mask=wgm43, tile_order=word43)
+            y1_43f = ops.split_decode(y1_43, 512) if y1_43.dtype == torch.bfloat16 else y1_43
+            m33 = (weng.conv2_partials(wws, mc[2], mc[4]), weng.conv3_from_partials(wws, mc[4]))[1].clone()
+            m43 = conv23w43()
+            def active(m, th):  # fraction of conv1's dense (pixel, slot) work a th x 32 tile mask keeps
+                if m is None:
+                    return 1.0
+                tx = -(-wo // 32)
+                bits = [bin(int(v) & 0xFFFFFFFF).count("1") for v in m.cpu().tolist()]
+                return sum(bb * min(th, ho - (t // tx) * th) * min(32, wo - (t % tx) * 32)
+                           for t, bb in enumerate(bits[:tx * -(-ho // th)])) / (ho * wo * weng.S)
+            print(json.dumps({"check43": "mask_active", "config": args.config, "rows12": active(wgm, 12),
+                              "rows16": active(wgm43, 16)}), flush=True)
+            for name, a_, b_ in (("y1", y1_43f, y1_33), ("map_conv23", m43, m33)):
+                print(json.dumps({"check43": name, "config": args.config, "normwise": float(
+                    (a_.double() - b_.double()).abs().max() / b_.double().abs().max())}), flush=True)
         from mvdet_amd import _native
         libs = [("default", _native.load())]
         for path in filter(None, args.libs.split(",")):

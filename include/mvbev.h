@@ -111,6 +111,11 @@ int mvbev_warp_views_f32(const mvbev_warp_view* views, int nviews, int64_t B, in
 /* flag of mvbev_warp_views_wino_rows (ABI 11900): the sources are fp16 (fp32 math; T split-bf16 as for
  * fp32 sources) — config 4's fp16 features on the fused warp + B^T and the row-Winograd conv1. */
 #define MVBEV_WARP_SRC_F16 2
+/* MVBEV_WARP_WINO43 (ABI 12400; mvbev_warp_views_wino_rows_ex / _upsampled_wino_rows_ex): the fused warp
+ * writes the F(4,3) transform T43 (mvbev_wino43_rows_bytes' layout) instead of T; r3_rows then counts
+ * four-row tiles (4 * ceil(out_rows / 16)), 3 per 14 x 16 block; the block's staging-box table is
+ * mvbev_warp_wino_boxes' with r3_rows = 4 * ceil(r4_rows / 3) (the same 12-row blocks). */
+#define MVBEV_WARP_WINO43 4
 int mvbev_warp_views_split_bf16_ex(const mvbev_warp_view* views, int nviews, int src_is_f16,
                                    int64_t B, int64_t C, int64_t H, int64_t W, int64_t Ho, int64_t Wo,
                                    int flags, void* stream);

@@ -106,6 +106,7 @@ BEV_SRC_CHANNELS_LAST = 16  # MVBEV_BEV_SRC_CHANNELS_LAST (flag)
 BEV_NO_GUARD = 32  # MVBEV_BEV_NO_GUARD (flag, ABI 11900)
 WARP_DST_ZEROED = 1  # MVBEV_WARP_DST_ZEROED
 WARP_SRC_F16 = 2  # MVBEV_WARP_SRC_F16 (mvbev_warp_views_wino_rows, ABI 11900)
+WARP_WINO43 = 4  # MVBEV_WARP_WINO43 (the fused warps write the F(4,3) transform, ABI 12400)
 TILES_GRID, TILES_EDGE_STRIP = 0, 1  # MVBEV_TILES_*
 ERR_SHAPE = -2  # MVBEV_ERR_SHAPE
 ERR_DILATION = -6  # MVBEV_ERR_DILATION

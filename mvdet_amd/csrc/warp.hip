@@ -179,7 +179,7 @@ constexpr int kWwGroups = MVBEV_WW_GROUPS;
 #ifndef MVBEV_WW_WAVES
 #define MVBEV_WW_WAVES 7  // waves per SIMD asked of the compiler (7: at most 72 VGPRs; 2 groups fit without spills)
 #endif
-template <bool PAIR, typename T = float>
+template <bool PAIR, typename T = float, int FORM = 3>
 __global__ __launch_bounds__(kWwThreads) __attribute__((amdgpu_waves_per_eu(MVBEV_WW_WAVES, 8)))
 void warp_wino_kernel(const WarpArgs a, int r3_rows) {
   static_assert(!PAIR || std::is_same<T, float>::value, "corner pairs are fp32 8-B loads");
@@ -350,7 +350,7 @@ void warp_wino_kernel(const WarpArgs a, int r3_rows) {
       nz[i][c] = any;
     }
     __syncthreads();
-    wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
+    wino_rows_phase2<FORM>(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
   }
 }
 
@@ -421,6 +421,7 @@ constexpr int kWcOutside = 0x7fff0000;  // byte offset of "no corner" (sources m
 static_assert(kWcCols == 16 && kWcThreads == 256, "channels-last fused warp: 256 threads, 16 columns");
 static_assert(kWcPix % 32 == 0, "phase 1: 32 pixels per pass");
 
+template <int FORM = 3>
 __global__ __launch_bounds__(kWcThreads) __attribute__((amdgpu_waves_per_eu(4, 8)))
 void warp_wino_cl_kernel(const WarpArgs a, int r3_rows) {
   __shared__ __attribute__((aligned(16))) float ds[kWcPix * kWcPitch];
@@ -496,36 +497,35 @@ void warp_wino_cl_kernel(const WarpArgs a, int r3_rows) {
     *reinterpret_cast<f32x4a_t*>(ds + p * kWcPitch + 4 * qd) = acc;
   }
   __syncthreads();
+  // phase 2 (FORM 4: 3 four-row tiles per block, rows i0 = 4 q .. 4 q + 5, T43 rows 6 r4 + xi; q = 3 idles)
+  constexpr int NT = FORM == 3 ? 4 : 3, NX = FORM + 2;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int it = tid + kWcThreads * h;
     const int half = it & 1, c = (it >> 1) & 15, ch8 = (it >> 5) & 3, q = it >> 7;
-    const int r3 = 4 * k + q, u = tx * kWcCols + c;
-    if (r3 >= r3_rows || u >= a.Wo) continue;
-    const int i0 = 3 * q;
-    if (a.skip_zero && !(cls[i0 * 16 + c] | cls[(i0 + 1) * 16 + c] | cls[(i0 + 2) * 16 + c] |
-                         cls[(i0 + 3) * 16 + c] | cls[(i0 + 4) * 16 + c]))
-      continue;
-    f32x4a_t d[5];
+    const int r3 = NT * k + q, u = tx * kWcCols + c;
+    if (q >= NT || r3 >= r3_rows || u >= a.Wo) continue;
+    const int i0 = FORM * q;
+    int any = 0;
 #pragma unroll
-    for (int m = 0; m < 5; ++m)
+    for (int m = 0; m < NX; ++m) any |= cls[(i0 + m) * 16 + c];
+    if (a.skip_zero && !any) continue;
+    f32x4a_t d[NX];
+#pragma unroll
+    for (int m = 0; m < NX; ++m)
       d[m] = *reinterpret_cast<const f32x4a_t*>(ds + ((i0 + m) * 16 + c) * kWcPitch + 8 * ch8 + 4 * half);
-    f32x4a_t t[5];
-    t[0] = 2.f * d[0] - d[1] - 2.f * d[2] + d[3];
-    t[1] = -2.f * d[1] - d[2] + d[3];
-    t[2] = 2.f * d[1] - 3.f * d[2] + d[3];
-    t[3] = d[3] - d[1];
-    t[4] = 2.f * d[1] - d[2] - 2.f * d[3] + d[4];
+    f32x4a_t t[NX];
+    wino_bt<FORM>(d, t);
     if (a.nonfinite) {  // as wino_rows_phase2
-      const f32x4a_t sum = (t[0] + t[1]) + (t[2] + t[3]) + t[4];
+      const f32x4a_t sum = wino_bt_sum<FORM>(t);
       if (!isfinite((sum.x + sum.y) + (sum.z + sum.w))) *a.nonfinite = a.nf_tag;
     }
     const int chunk = grp * (kWcCh / 8) + ch8;
     unsigned* out = reinterpret_cast<unsigned*>(static_cast<u32x4_t*>(vw.dst) +
                                                 (2 * ((int64_t)b * vw.dB + (int64_t)chunk * vw.dC +
-                                                      (int64_t)(5 * r3) * vw.dH) + u)) + 2 * half;
+                                                      (int64_t)(NX * r3) * vw.dH) + u)) + 2 * half;
 #pragma unroll
-    for (int xi = 0; xi < 5; ++xi) {
+    for (int xi = 0; xi < NX; ++xi) {
       const float h0 = (float)(__bf16)t[xi].x, h1 = (float)(__bf16)t[xi].y;
       const float h2 = (float)(__bf16)t[xi].z, h3 = (float)(__bf16)t[xi].w;
       unsigned* o = out + (int64_t)xi * vw.dH * 8;
@@ -884,13 +884,15 @@ int mvbev_warp_views_wino_rows_ex(const mvbev_warp_view* views, int nviews, int6
                                   int32_t nf_tag, const int32_t* boxes, void* stream) {
   using namespace mvbev;
   if (!views) return MVBEV_ERR_NULL;
-  if (flags & ~(MVBEV_WARP_DST_ZEROED | MVBEV_WARP_SRC_F16)) return MVBEV_ERR_SHAPE;
+  if (flags & ~(MVBEV_WARP_DST_ZEROED | MVBEV_WARP_SRC_F16 | MVBEV_WARP_WINO43)) return MVBEV_ERR_SHAPE;
   const bool f16 = (flags & MVBEV_WARP_SRC_F16) != 0;
+  const bool w43 = (flags & MVBEV_WARP_WINO43) != 0;  // T43: r3_rows counts four-row tiles, 3 per block
+  const int form = w43 ? 4 : 3, tpb = w43 ? 3 : 4;
   int st = check_sizes(B, C, H, W, r3_rows, Wo, nviews);
   if (st != MVBEV_OK) return st;
   st = check_sizes(B, C, H, W, Ho, Wo, nviews);
   if (st != MVBEV_OK) return st;
-  if (3 * r3_rows < Ho || W < 2) return MVBEV_ERR_SHAPE;
+  if (form * r3_rows < Ho || W < 2) return MVBEV_ERR_SHAPE;
   WarpArgs a = {};
   bool pair = true;
   for (int i = 0; i < nviews; ++i) {
@@ -912,7 +914,7 @@ int mvbev_warp_views_wino_rows_ex(const mvbev_warp_view* views, int nviews, int6
   a.nf_tag = nf_tag;
   a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
   a.tiles_x = (int)ceil_div(Wo, kWwCols);
-  a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);  // 4 three-row tiles per block
+  a.tiles = a.tiles_x * (int)ceil_div(r3_rows, tpb);  // 4 three-row (3 four-row) tiles per block
   // channels-last sources (every view: unit channel stride, 16-B aligned pixels of whole 32-channel
   // groups, offsets within 31 bits) take the line-per-pixel kernel
   bool cl = C % kWcCh == 0 && !f16;
@@ -924,21 +926,29 @@ int mvbev_warp_views_wino_rows_ex(const mvbev_warp_view* views, int nviews, int6
   }
   if (cl) {
     a.tiles_x = (int)ceil_div(Wo, kWcCols);
-    a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);
+    a.tiles = a.tiles_x * (int)ceil_div(r3_rows, tpb);
   }
   a.chunks = (int)ceil_div(C, cl ? kWcCh : kWarpCPB * kWwGroups);  // (NCHW: blocks of kWwGroups 8-channel groups)
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
   set_fastdiv(a);
   a.boxes = boxes;  // (the line-per-pixel kernel's 14 x 16 block tiles are warp_wino_kernel's: same table)
   const dim3 grid((unsigned)a.nwg), block(cl ? kWcThreads : kWwThreads);
-  if (cl)
-    hipLaunchKernelGGL(warp_wino_cl_kernel, grid, block, 0, as_stream(stream), a, (int)r3_rows);
-  else if (f16)
-    hipLaunchKernelGGL((warp_wino_kernel<false, __half>), grid, block, 0, as_stream(stream), a, (int)r3_rows);
-  else if (pair)
-    hipLaunchKernelGGL((warp_wino_kernel<true>), grid, block, 0, as_stream(stream), a, (int)r3_rows);
-  else
-    hipLaunchKernelGGL((warp_wino_kernel<false>), grid, block, 0, as_stream(stream), a, (int)r3_rows);
+  hipStream_t s = as_stream(stream);
+  const int r = (int)r3_rows;
+  if (w43) {
+    if (cl) hipLaunchKernelGGL((warp_wino_cl_kernel<4>), grid, block, 0, s, a, r);
+    else if (f16) hipLaunchKernelGGL((warp_wino_kernel<false, __half, 4>), grid, block, 0, s, a, r);
+    else if (pair) hipLaunchKernelGGL((warp_wino_kernel<true, float, 4>), grid, block, 0, s, a, r);
+    else hipLaunchKernelGGL((warp_wino_kernel<false, float, 4>), grid, block, 0, s, a, r);
+  } else if (cl) {
+    hipLaunchKernelGGL((warp_wino_cl_kernel<3>), grid, block, 0, s, a, r);
+  } else if (f16) {
+    hipLaunchKernelGGL((warp_wino_kernel<false, __half>), grid, block, 0, s, a, r);
+  } else if (pair) {
+    hipLaunchKernelGGL((warp_wino_kernel<true>), grid, block, 0, s, a, r);
+  } else {
+    hipLaunchKernelGGL((warp_wino_kernel<false>), grid, block, 0, s, a, r);
+  }
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }

@@ -357,38 +357,68 @@ __device__ inline void stage_box_load(const T* __restrict__ base, int64_t sC, in
     }
 }
 
+// FORM 3: the F(3,3) transform above.  FORM 4 (ABI 12400): the F(4,3) transform of the xi-major F(4,3) conv
+// (conv_bf16x3.hip "Row-Winograd F(4,3)": B^T rows of points 0, +-1, +-2, inf) — the block's 12 output rows are 3
+// four-row tiles r4 = 3 k + q (q < 3), input rows i0 = 4 q .. 4 q + 5 of the same 14-row block, T43 rows 6 r4 + xi
+// (the last thread quarter idles); the same phase 1, boxes and skip rules.
+template <int FORM, typename V>
+__device__ inline void wino_bt(const V (&d)[FORM + 2], V (&t)[FORM + 2]) {
+  if constexpr (FORM == 3) {
+    t[0] = 2.f * d[0] - d[1] - 2.f * d[2] + d[3];
+    t[1] = -2.f * d[1] - d[2] + d[3];
+    t[2] = 2.f * d[1] - 3.f * d[2] + d[3];
+    t[3] = d[3] - d[1];
+    t[4] = 2.f * d[1] - d[2] - 2.f * d[3] + d[4];
+  } else {  // as wino43_rows_kernel (conv_bf16x3.hip), the same fp32 expressions
+    t[0] = 4.f * d[0] - 5.f * d[2] + d[4];
+    t[1] = -4.f * d[1] - 4.f * d[2] + d[3] + d[4];
+    t[2] = 4.f * d[1] - 4.f * d[2] - d[3] + d[4];
+    t[3] = -2.f * d[1] - d[2] + 2.f * d[3] + d[4];
+    t[4] = 2.f * d[1] - d[2] - 2.f * d[3] + d[4];
+    t[5] = 4.f * d[1] - 5.f * d[3] + d[5];
+  }
+}
+// the non-finite report's sum of a thread's T values (F(3,3): the order of rounds 3-6)
+template <int FORM, typename V>
+__device__ inline V wino_bt_sum(const V (&t)[FORM + 2]) {
+  if constexpr (FORM == 3) return (t[0] + t[1]) + (t[2] + t[3]) + t[4];
+  else return ((t[0] + t[1]) + (t[2] + t[3])) + (t[4] + t[5]);
+}
+
+template <int FORM = 3>
 __device__ inline void wino_rows_phase2(const float (&ds)[kWwRows][kWwCols][8], const unsigned char (&nz)[kWwRows][kWwCols],
                                         const WarpView& vw, const WarpArgs& a, int b, int chunk, int k, int tx,
                                         int r3_rows) {
+  static_assert(FORM == 3 || FORM == 4, "row-Winograd form");
+  constexpr int NT = FORM == 3 ? 4 : 3, NX = FORM + 2;  // row tiles per block, transformed rows per tile
   const int it = threadIdx.x;
   const int cp = it & 3, c = (it >> 2) % kWwCols, q = it / (4 * kWwCols);
-  const int r3 = 4 * k + q, u = tx * kWwCols + c;
-  if (r3 >= r3_rows || u >= a.Wo) return;
-  const int i0 = 3 * q;  // rows i0 .. i0 + 4 of the block
-  if (a.skip_zero && !(nz[i0][c] | nz[i0 + 1][c] | nz[i0 + 2][c] | nz[i0 + 3][c] | nz[i0 + 4][c])) return;
-  f32x2_t d[5];
+  const int r3 = NT * k + q, u = tx * kWwCols + c;
+  if (q >= NT || r3 >= r3_rows || u >= a.Wo) return;
+  const int i0 = FORM * q;  // rows i0 .. i0 + NX - 1 of the block
+  bool any = false;
 #pragma unroll
-  for (int m = 0; m < 5; ++m) d[m] = *reinterpret_cast<const f32x2_t*>(&ds[i0 + m][c][2 * cp]);
-  f32x2_t t[5];
-  t[0] = 2.f * d[0] - d[1] - 2.f * d[2] + d[3];
-  t[1] = -2.f * d[1] - d[2] + d[3];
-  t[2] = 2.f * d[1] - 3.f * d[2] + d[3];
-  t[3] = d[3] - d[1];
-  t[4] = 2.f * d[1] - d[2] - 2.f * d[3] + d[4];
+  for (int m = 0; m < NX; ++m) any |= nz[i0 + m][c] != 0;
+  if (a.skip_zero && !any) return;
+  f32x2_t d[NX];
+#pragma unroll
+  for (int m = 0; m < NX; ++m) d[m] = *reinterpret_cast<const f32x2_t*>(&ds[i0 + m][c][2 * cp]);
+  f32x2_t t[NX];
+  wino_bt<FORM>(d, t);
   if (a.nonfinite) {
     // every d row enters some T row with a non-zero coefficient, and a sample is non-finite when a
     // value it reads is (every read value is multiplied by its weight, zero weights included), so
-    // the sum of the 10 T values is non-finite whenever a feature this thread's samples read is
+    // the sum of the T values is non-finite whenever a feature this thread's samples read is
     // (or, conservatively, when finite values overflow): the caller's exact path then runs
-    const f32x2_t sum = (t[0] + t[1]) + (t[2] + t[3]) + t[4];
+    const f32x2_t sum = wino_bt_sum<FORM>(t);
     if (!isfinite(sum.x + sum.y)) *a.nonfinite = a.nf_tag;
   }
   // a T row of dH (= Wo) columns is its hi plane [dH][8 bf16] then its lo plane (16-B units)
   unsigned* out = reinterpret_cast<unsigned*>(static_cast<u32x4_t*>(vw.dst) +
                                               (2 * ((int64_t)b * vw.dB + (int64_t)chunk * vw.dC +
-                                                    (int64_t)(5 * r3) * vw.dH) + u)) + cp;
+                                                    (int64_t)(NX * r3) * vw.dH) + u)) + cp;
 #pragma unroll
-  for (int xi = 0; xi < 5; ++xi) {
+  for (int xi = 0; xi < NX; ++xi) {
     const float h0 = (float)(__bf16)t[xi].x, h1 = (float)(__bf16)t[xi].y;
     unsigned* o = out + (int64_t)xi * vw.dH * 8;  // 8 dwords per 32-B unit
     o[0] = pack_bf16x2(h0, h1);

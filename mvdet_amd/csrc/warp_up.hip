@@ -161,6 +161,7 @@ constexpr int kUpStage = MVBEV_UPW_STAGE;
 // cfg2: 0.39-0.42 ms vs 0.42-0.44 (profiles/r04a_kbench.jsonl).  (Several 8-channel groups per block,
 // the sample geometry computed once for them, spilled and ran 0.64-0.85 ms: removed.)
 constexpr int G = 1;
+template <int FORM = 3>
 __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino2_kernel(const UpArgs ua, int r3_rows,
                                                                                   int cgroups) {
   __shared__ __attribute__((aligned(16))) float ds[kWwRows][kWwCols][8];
@@ -323,7 +324,7 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino2_kerne
       if (gi == 0) nz[i][c] = any;
     }
     __syncthreads();
-    wino_rows_phase2(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
+    wino_rows_phase2<FORM>(ds, nz, vw, a, b, chunk, k, tx, r3_rows);
   }
 }
 
@@ -346,6 +347,7 @@ __global__ __launch_bounds__(kWwThreads) MVBEV_WARP_OCC void warp_up_wino2_kerne
 constexpr int kUcCh = 32, kUcThreads = 128, kUcStage = MVBEV_UPCL_STAGE, kWcPixUp = kWwRows * kWcCols;
 static_assert(kWcCols * 8 == kUcThreads, "thread = (column, channel quad)");
 
+template <int FORM = 3>
 __global__ __launch_bounds__(kUcThreads) void warp_up_wino_cl_kernel(const UpArgs ua, int r3_rows) {
   __shared__ __attribute__((aligned(16))) f32x4a_t box_px[kUcStage * 8];  // [pixel][quad]
   __shared__ __attribute__((aligned(16))) f32x4a_t pax[kWcPixUp];  // ax0, ax1, ax2, ay0
@@ -482,27 +484,30 @@ __global__ __launch_bounds__(kUcThreads) void warp_up_wino_cl_kernel(const UpArg
   }
   if (u >= a.Wo) return;
   const int chunk = grp * (kUcCh / 8) + (q >> 1), half = q & 1;
+  // phase 2: tile qt = rows FORM qt .. FORM qt + FORM + 1 (FORM 4: 3 four-row tiles, T43 rows 6 r4 + xi)
+  constexpr int NT = FORM == 3 ? 4 : 3, NX = FORM + 2;
 #pragma unroll
-  for (int qt = 0; qt < 4; ++qt) {  // phase 2: tile qt = rows 3 qt .. 3 qt + 4
-    const int r3 = 4 * k + qt, i0 = 3 * qt;
+  for (int qt = 0; qt < NT; ++qt) {
+    const int r3 = NT * k + qt, i0 = FORM * qt;
     if (r3 >= r3_rows) break;
-    if (a.skip_zero && !(nzr[i0] | nzr[i0 + 1] | nzr[i0 + 2] | nzr[i0 + 3] | nzr[i0 + 4])) continue;
-    f32x4a_t t[5];
-    t[0] = 2.f * d[i0] - d[i0 + 1] - 2.f * d[i0 + 2] + d[i0 + 3];
-    t[1] = -2.f * d[i0 + 1] - d[i0 + 2] + d[i0 + 3];
-    t[2] = 2.f * d[i0 + 1] - 3.f * d[i0 + 2] + d[i0 + 3];
-    t[3] = d[i0 + 3] - d[i0 + 1];
-    t[4] = 2.f * d[i0 + 1] - d[i0 + 2] - 2.f * d[i0 + 3] + d[i0 + 4];
+    int any = 0;
+#pragma unroll
+    for (int m = 0; m < NX; ++m) any |= nzr[i0 + m];
+    if (a.skip_zero && !any) continue;
+    f32x4a_t dd[NX], t[NX];
+#pragma unroll
+    for (int m = 0; m < NX; ++m) dd[m] = d[i0 + m];
+    wino_bt<FORM>(dd, t);
     if (a.nonfinite) {  // as wino_rows_phase2
-      const f32x4a_t sum = (t[0] + t[1]) + (t[2] + t[3]) + t[4];
+      const f32x4a_t sum = wino_bt_sum<FORM>(t);
       if (!isfinite((sum.x + sum.y) + (sum.z + sum.w))) *a.nonfinite = a.nf_tag;
     }
     unsigned* out = reinterpret_cast<unsigned*>(static_cast<u32x4_t*>(vw.dst) +
                                                 (2 * ((int64_t)b * vw.dB + (int64_t)chunk * vw.dC +
-                                                      (int64_t)(5 * r3) * vw.dH) + u)) + 2 * half;
+                                                      (int64_t)(NX * r3) * vw.dH) + u)) + 2 * half;
     typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int xi = 0; xi < 5; ++xi) {
+    for (int xi = 0; xi < NX; ++xi) {
       const float h0 = (float)(__bf16)t[xi].x, h1 = (float)(__bf16)t[xi].y;
       const float h2 = (float)(__bf16)t[xi].z, h3 = (float)(__bf16)t[xi].w;
       unsigned* o = out + (int64_t)xi * vw.dH * 8;
@@ -749,13 +754,15 @@ extern "C" int mvbev_warp_views_upsampled_wino_rows_ex(const mvbev_warp_view* vi
                                                        int32_t* nonfinite, int32_t nf_tag, const int32_t* boxes,
                                                        void* stream) {
   using namespace mvbev;
-  if (flags & ~MVBEV_WARP_DST_ZEROED) return MVBEV_ERR_SHAPE;
+  if (flags & ~(MVBEV_WARP_DST_ZEROED | MVBEV_WARP_WINO43)) return MVBEV_ERR_SHAPE;
+  const bool w43 = (flags & MVBEV_WARP_WINO43) != 0;  // T43: r3_rows counts four-row tiles, 3 per block
+  const int form = w43 ? 4 : 3, tpb = w43 ? 3 : 4;
   if (!views) return MVBEV_ERR_NULL;
   if (B <= 0 || C <= 0 || h <= 0 || w <= 0 || H <= 0 || W <= 0 || Ho <= 0 || Wo <= 0 || nviews <= 0 || r3_rows <= 0)
     return MVBEV_ERR_RANK;
   if (nviews > kWarpMaxViews || B * nviews > 65535 || C > INT32_MAX || H > INT32_MAX / 2 || W > INT32_MAX / 2 ||
-      Ho > INT32_MAX / 2 || Wo > INT32_MAX / 2 || H < h || W < w || w < 4 || 3 * r3_rows < Ho ||
-      ceil_div(r3_rows, 4) * ceil_div(Wo, kWwCols) * ceil_div(C, kUpCPB) * B * nviews > INT32_MAX)
+      Ho > INT32_MAX / 2 || Wo > INT32_MAX / 2 || H < h || W < w || w < 4 || form * r3_rows < Ho ||
+      ceil_div(r3_rows, tpb) * ceil_div(Wo, kWwCols) * ceil_div(C, kUpCPB) * B * nviews > INT32_MAX)
     return MVBEV_ERR_SHAPE;
   UpArgs ua = {};
   WarpArgs& a = ua.w;
@@ -774,7 +781,7 @@ extern "C" int mvbev_warp_views_upsampled_wino_rows_ex(const mvbev_warp_view* vi
   a.skip_zero = (flags & MVBEV_WARP_DST_ZEROED) != 0;
   a.B = (int)B; a.C = (int)C; a.H = (int)H; a.W = (int)W; a.Ho = (int)Ho; a.Wo = (int)Wo;
   a.tiles_x = (int)ceil_div(Wo, kWwCols);
-  a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);
+  a.tiles = a.tiles_x * (int)ceil_div(r3_rows, tpb);
   a.chunks = (int)ceil_div(C, kUpCPB);
   a.nwg = a.tiles * a.chunks * a.B * a.nviews;
   a.nonfinite = nonfinite;
@@ -792,20 +799,28 @@ extern "C" int mvbev_warp_views_upsampled_wino_rows_ex(const mvbev_warp_view* vi
   }
   if (cl) {
     a.tiles_x = (int)ceil_div(Wo, kWcCols);
-    a.tiles = a.tiles_x * (int)ceil_div(r3_rows, 4);
+    a.tiles = a.tiles_x * (int)ceil_div(r3_rows, tpb);
     a.chunks = (int)(C / kUcCh);
     a.nwg = a.tiles * a.chunks * a.B * a.nviews;
     set_fastdiv(a);
     ua.boxes = boxes;
-    hipLaunchKernelGGL(warp_up_wino_cl_kernel, dim3((unsigned)a.nwg), dim3(kUcThreads), 0, as_stream(stream), ua,
-                       (int)r3_rows);
+    if (w43)
+      hipLaunchKernelGGL((warp_up_wino_cl_kernel<4>), dim3((unsigned)a.nwg), dim3(kUcThreads), 0, as_stream(stream),
+                         ua, (int)r3_rows);
+    else
+      hipLaunchKernelGGL((warp_up_wino_cl_kernel<3>), dim3((unsigned)a.nwg), dim3(kUcThreads), 0, as_stream(stream),
+                         ua, (int)r3_rows);
     MVBEV_CHECK_LAUNCH();
     return MVBEV_OK;
   }
   for (int i = 0; i < nviews; ++i)
     if (a.v[i].sW != 1) return MVBEV_ERR_STRIDE;  // 16-B window rows
-  hipLaunchKernelGGL(warp_up_wino2_kernel, dim3((unsigned)a.nwg), dim3(kWwThreads), 0, as_stream(stream), ua,
-                     (int)r3_rows, a.chunks);
+  if (w43)
+    hipLaunchKernelGGL((warp_up_wino2_kernel<4>), dim3((unsigned)a.nwg), dim3(kWwThreads), 0, as_stream(stream), ua,
+                       (int)r3_rows, a.chunks);
+  else
+    hipLaunchKernelGGL((warp_up_wino2_kernel<3>), dim3((unsigned)a.nwg), dim3(kWwThreads), 0, as_stream(stream), ua,
+                       (int)r3_rows, a.chunks);
   MVBEV_CHECK_LAUNCH();
   return MVBEV_OK;
 }

@@ -474,14 +474,19 @@ class PackedConv3x3:
     ``precision``: "fp32" (fp32 MFMA, exact fp32 products) or "bf16x3" (hi/lo bf16 split,
     three bf16 MFMA passes, fp32 accumulation)."""
 
-    def __init__(self, chan_map: Optional[Sequence[int]] = None, precision: str = "fp32", wino: bool = False):
+    def __init__(self, chan_map: Optional[Sequence[int]] = None, precision: str = "fp32", wino: bool = False,
+                 form: int = 3):
         if precision not in PRECISIONS:
             raise ValueError(f"precision must be one of {PRECISIONS}")
         if wino and precision != "bf16x3":
             raise ValueError("the row-Winograd packing is bf16x3")
+        if form not in (3, 4) or (form == 4 and not wino):
+            raise ValueError("form 4 (F(4,3)) is a row-Winograd packing")
         self.precision = precision
-        # wino: the row-Winograd weights G w of mvbev_pack_conv3x3_weight_wino (conv3x3_wino)
+        # wino: the row-Winograd weights G w of mvbev_pack_conv3x3_weight_wino (conv3x3_wino); form 4: F(4,3)'s
+        # (mvbev_pack_conv3x3_weight_wino43, conv3x3_wino43)
         self.wino = wino
+        self.form = form
         self._key = None
         self.packed: Optional[torch.Tensor] = None
         self.chan_map = None if chan_map is None else [int(c) for c in chan_map]
@@ -546,6 +551,12 @@ class PackedConv3x3:
                 st = lib.mvbev_pack_conv3x3_weight_f32(w.data_ptr(), cout, cin, cmap, K, packed.data_ptr(),
                                                        _stream(packed))
                 _native.check(st, "mvbev_pack_conv3x3_weight_f32")
+            elif self.wino and self.form == 4:
+                n = lib.mvbev_conv3x3_packed_bytes_wino43(cout, K)
+                packed = torch.empty(n // 2, dtype=torch.bfloat16, device=weight.device)
+                st = lib.mvbev_pack_conv3x3_weight_wino43(w.data_ptr(), cout, cin, cmap, K, packed.data_ptr(),
+                                                          _stream(packed))
+                _native.check(st, "mvbev_pack_conv3x3_weight_wino43")
             elif self.wino:
                 n = lib.mvbev_conv3x3_packed_bytes_wino(cout, K)
                 packed = torch.empty(n // 2, dtype=torch.bfloat16, device=weight.device)
@@ -825,13 +836,20 @@ def wino_rows(x: torch.Tensor, desc, t: torch.Tensor, group_mask: Optional[torch
     return t
 
 
-def warp_wino_boxes(m_norms, src_hw, grid_hw, device, backbone_hw=None) -> torch.Tensor:
+def wino_tile_rows(Ho: int, form: int = 3) -> int:
+    """Row tiles of a whole-grid row-Winograd transform: 4 ceil(Ho / 12) three-row tiles (F(3,3)), or
+    4 ceil(Ho / 16) four-row tiles (``form`` 4, F(4,3))."""
+    return 4 * (-(-int(Ho) // (12 if form == 3 else 16)))
+
+
+def warp_wino_boxes(m_norms, src_hw, grid_hw, device, backbone_hw=None, form: int = 3) -> torch.Tensor:
     """``mvbev_warp_wino_boxes``: the per-(view, block) staging boxes of the NCHW fused warp + B^T for the
     whole-grid T (r3 rows 4 * ceil(Ho / 12)) — geometry only, computed once and reused every frame.
     ``backbone_hw``: the channels-last fused upsample warp's boxes of its 3x3 windows in the backbone maps
-    (``mvbev_warp_upsampled_wino_boxes``; ``src_hw`` = the upsampled size)."""
+    (``mvbev_warp_upsampled_wino_boxes``; ``src_hw`` = the upsampled size).  ``form`` 4: the blocks of the
+    F(4,3) fused warp (the same 12-row blocks, ceil(r4 / 3) of them: r3 = 4 ceil(r4 / 3))."""
     Ho, Wo = int(grid_hw[0]), int(grid_hw[1])
-    r3 = 4 * (-(-Ho // 12))
+    r3 = 4 * (-(-wino_tile_rows(Ho, 4) // 3)) if form == 4 else wino_tile_rows(Ho)
     n = len(m_norms)
     if not 0 < n <= 16:
         raise ValueError("need 1..16 views")
@@ -852,7 +870,8 @@ def warp_wino_boxes(m_norms, src_hw, grid_hw, device, backbone_hw=None) -> torch
 
 
 def warp_views_wino_rows_into(srcs, m_norms, t: torch.Tensor, slots, Cs: int, K: int, Ho: int, Wo: int,
-                              dst_zeroed: bool = False, up_hw=None, nonfinite=None, boxes=None) -> None:
+                              dst_zeroed: bool = False, up_hw=None, nonfinite=None, boxes=None,
+                              form: int = 3) -> None:
     """Warp + row-Winograd transform in ONE launch (``mvbev_warp_views_wino_rows``): view i
     (fp32 ``srcs[i]`` [B,C,H,W], host kornia matrix ``m_norms[i]``) lands in channels
     [slots[i] * Cs, + C) of ``t``, the T buffer of ``wino_rows`` for a K-channel slab of
@@ -861,7 +880,8 @@ def warp_views_wino_rows_into(srcs, m_norms, t: torch.Tensor, slots, Cs: int, K:
     (``mvbev_warp_views_upsampled_wino_rows``; ``m_norms`` for the upsampled size).  ``nonfinite``:
     ``(flag, tag)`` — ``tag`` is stored into the device int32 ``flag[0]`` when a sample reads a NaN /
     inf feature (the fused form cannot keep the reference's NaN pattern; ``warp_views_exact_into``
-    and the gated fp32 convs can)."""
+    and the gated fp32 convs can).  ``form`` 4: ``t`` is the F(4,3) transform T43 of ``wino43_rows``
+    (``MVBEV_WARP_WINO43``; ``boxes`` from ``warp_wino_boxes(..., form=4)``)."""
     n = len(srcs)
     if n == 0:
         return
@@ -869,10 +889,12 @@ def warp_views_wino_rows_into(srcs, m_norms, t: torch.Tensor, slots, Cs: int, K:
         raise ValueError("need 1..16 matching srcs / m_norms / slots")
     _require_cuda(t, *srcs)
     B, C, H, W = srcs[0].shape
-    r3 = 4 * (-(-Ho // 12))
+    if form not in (3, 4):
+        raise ValueError("form must be 3 (F(3,3)) or 4 (F(4,3))")
+    r3, nx = wino_tile_rows(Ho, form), form + 2  # row tiles, transformed rows per tile
     K8 = K // KC
-    if t.dtype != torch.bfloat16 or not t.is_contiguous() or t.numel() < B * K8 * 5 * r3 * Wo * 16:
-        raise ValueError("t must be a contiguous bf16 buffer of wino_rows_bytes")
+    if t.dtype != torch.bfloat16 or not t.is_contiguous() or t.numel() < B * K8 * nx * r3 * Wo * 16:
+        raise ValueError("t must be a contiguous bf16 buffer of wino_rows_bytes (form 4: wino43_rows_bytes)")
     if Cs % KC or C > Cs:
         raise ValueError("Cs must be a multiple of 8 holding C")
     arr = (_native.WarpView * n)()
@@ -885,10 +907,11 @@ def warp_views_wino_rows_into(srcs, m_norms, t: torch.Tensor, slots, Cs: int, K:
         mm = torch.as_tensor(m, dtype=torch.float32).reshape(9).tolist()
         arr[i].src = s_.data_ptr()
         arr[i].src_strides = _native._i64x4(*s_.stride())
-        arr[i].dst = t.data_ptr() + 32 * (int(slot) * (Cs // KC)) * 5 * r3 * Wo
-        arr[i].dst_strides = _native._i64x4(K8 * 5 * r3 * Wo, 5 * r3 * Wo, Wo, 1)  # 32-byte units
+        arr[i].dst = t.data_ptr() + 32 * (int(slot) * (Cs // KC)) * nx * r3 * Wo
+        arr[i].dst_strides = _native._i64x4(K8 * nx * r3 * Wo, nx * r3 * Wo, Wo, 1)  # 32-byte units
         arr[i].m = (ctypes.c_float * 9)(*mm)
-    flags = (_native.WARP_DST_ZEROED if dst_zeroed else 0) | (_native.WARP_SRC_F16 if dtype == torch.float16 else 0)
+    flags = ((_native.WARP_DST_ZEROED if dst_zeroed else 0) | (_native.WARP_SRC_F16 if dtype == torch.float16 else 0)
+             | (_native.WARP_WINO43 if form == 4 else 0))
     fp, ft = _gate(nonfinite)
     if boxes is not None:  # (from warp_wino_boxes with the same matrices, in the same view order)
         _require_cuda(boxes)

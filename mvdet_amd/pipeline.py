@@ -69,6 +69,12 @@ class Workspace:
     wino_t: Optional[torch.Tensor] = None
     # wino_t holds the current frame's transform, written by the fused warp (the slab was not)
     t_from_warp: bool = False
+    # the F(4,3) transforms (ABI 12400, inference over the whole grid where ProjectFuse.wino43_pays): T43 of the
+    # slab for conv1 (zero-filled on first use, as wino_t) and of y1 for conv2; t_form = the form of the
+    # current frame's conv1 transform (3: wino_t, 4: wino_t43)
+    wino_t43: Optional[torch.Tensor] = None
+    wino_t2_43: Optional[torch.Tensor] = None
+    t_form: int = 3
     # wino_t holds this forward's transform of the whole grid (conv1 ran row-Winograd over all rows):
     # the training backward's conv1 weight gradient reads it (autograd._wgrad1_wino)
     t1_valid: bool = False
@@ -118,7 +124,8 @@ class ProjectFuse:
                  all_views: bool = True, split_k: bool = True, frustum: bool = True, fuse_conv3: bool = True,
                  edge_strip: bool = True, wino_conv1: bool = True, wino_warp: bool = True,
                  wino_conv2: bool = True, nonfinite_guard: bool = True, cl_upsample: bool = True,
-                 parts: Optional[Sequence[Tuple[int, int]]] = None, part_channels: Optional[int] = None):
+                 parts: Optional[Sequence[Tuple[int, int]]] = None, part_channels: Optional[int] = None,
+                 wino43: Optional[bool] = None):
         if slab_dtype not in (torch.float32, torch.float16):
             raise ValueError("slab_dtype must be float32 or float16")
         if slab_dtype == torch.float16 and precision != "bf16x3":
@@ -224,6 +231,39 @@ class ProjectFuse:
         self._pack1f: Optional[ops.PackedConv3x3] = None
         self._pack2f: Optional[ops.PackedConv3x3] = None
         self._chan_map = chan_map
+        # wino43 (ABI 12400; default: where it pays, ``wino43_pays``): the inference conv1 and conv2 -> conv3 over
+        # the whole grid as row-Winograd F(4,3) (6 transformed rows per 4 output rows, 10 % fewer MFMAs than
+        # F(3,3); 16 x 32 tiles, the K sum walked xi-major) — the fused warp then writes T43.  Not in training
+        # (its backward reads F(3,3)'s T) nor in the partial-sum multi-GPU engines (conv1_partial).
+        # (True: wherever it applies, without the wino43_pays rule — tests and A/B runs)
+        self.wino43 = (self.wino_conv1 and all_views and self.parts is None) if wino43 is None else \
+            (bool(wino43) and self.wino_conv1)
+        self._wino43_forced = wino43 is True
+        self.pack1w43 = ops.PackedConv3x3(chan_map, "bf16x3", wino=True, form=4) if self.wino43 else None
+        self.pack2w43 = ops.PackedConv3x3(None, "bf16x3", wino=True, form=4) if self.wino43 else None
+        self._cus: Dict[str, int] = {}
+
+    def wino43_pays(self, rows: int, B: int, device) -> bool:
+        """F(4,3) over ``rows`` output rows (whole grid): enabled, its 16-row tiles waste at most 3 % of the rows
+        and the launch is at least 8 rounds of workgroups deep (16 x 32 pixel tiles x 4 Cout tiles over the CUs).
+        Measured (``profiles/r06aj_wino43_ab.jsonl``, conv1 / conv2 -> conv3): cfg3 (480 rows, 21 rounds)
+        -9.7 % / -7.5 %, cfg5 (1000 rows, 31 rounds) -8.4 % / -6.4 %, cfg2 (120 rows: 6.7 % waste, 1.5
+        rounds) +1.7 % / +9 %."""
+        if not self.wino43:
+            return False
+        if self._wino43_forced:
+            return True
+        rows = int(rows)
+        h16 = -(-rows // 16) * 16
+        if h16 - rows > 0.03 * rows:
+            return False
+        key = str(torch.device(device))
+        if key not in self._cus:
+            dev = torch.device(device)
+            self._cus[key] = (torch.cuda.get_device_properties(dev).multi_processor_count
+                              if dev.type == "cuda" else 256)
+        tiles = (h16 // 16) * -(-self.grid_hw[1] // 32) * int(B) * max(1, self.mid // ops.BN)
+        return tiles >= 8 * self._cus[key]
 
     # -- buffers ----------------------------------------------------------------------------
     def workspace(self, B: int, device, band: Optional[Tuple[int, int]] = None,
@@ -351,9 +391,15 @@ class ProjectFuse:
         """The warp writing conv1's row transform T (``ops.warp_views_wino_rows_into``)."""
         H, W = self.grid_hw
         B = ws.slab.shape[1]
-        need = ops.wino_rows_bytes(self._conv1_desc(B))
-        if ws.wino_t is None or ws.wino_t.numel() * 2 < need:
-            ws.wino_t = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=ws.slab.device)
+        form = 4 if (not ws.store_y2 and self.wino43_pays(H, B, ws.slab.device)) else 3
+        if form == 4:
+            need = ops.wino43_rows_bytes(self._conv1_desc(B))
+            if ws.wino_t43 is None or ws.wino_t43.numel() * 2 < need:
+                ws.wino_t43 = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=ws.slab.device)
+        else:
+            need = ops.wino_rows_bytes(self._conv1_desc(B))
+            if ws.wino_t is None or ws.wino_t.numel() * 2 < need:
+                ws.wino_t = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=ws.slab.device)
         nonfinite = None
         if self.nonfinite_guard:
             # a training forward's workspace is fresh every step: its flag and tag live on the engine (no
@@ -370,21 +416,24 @@ class ProjectFuse:
             nonfinite = (ws.nf, ws.nf_tag)
             for c, f in zip(cams, feats):  # the frame's views so far (one tag for all its warp calls)
                 ws.guard_src[self.slot_of[c]] = (c, f, up_hw)
-        ops.warp_views_wino_rows_into(list(feats), [self.m_norm_cpu[c] for c in cams], ws.wino_t,
+        ops.warp_views_wino_rows_into(list(feats), [self.m_norm_cpu[c] for c in cams],
+                                      ws.wino_t43 if form == 4 else ws.wino_t,
                                       [self.slot_of[c] for c in cams], self.Cs, self.S * self.Cs, H, W,
                                       dst_zeroed=True, up_hw=up_hw, nonfinite=nonfinite,
                                       boxes=self._wino_boxes(ws.slab.device, cams, None if up_hw is None else
-                                                             tuple(feats[0].shape[2:])))
+                                                             tuple(feats[0].shape[2:]), form=form), form=form)
         ws.t_from_warp = True
+        ws.t_form = form
 
-    def _wino_boxes(self, device, cams, backbone_hw=None) -> torch.Tensor:
+    def _wino_boxes(self, device, cams, backbone_hw=None, form: int = 3) -> torch.Tensor:
         """The fused warps' per-(view, block) staging boxes for these cameras (geometry only, cached):
-        ``ops.warp_wino_boxes``; ``backbone_hw``: of the upsample warp's backbone windows."""
-        key = ("boxes", str(torch.device(device)), tuple(cams), backbone_hw)
+        ``ops.warp_wino_boxes``; ``backbone_hw``: of the upsample warp's backbone windows; ``form`` 4: of the
+        F(4,3) fused warp's blocks."""
+        key = ("boxes", str(torch.device(device)), tuple(cams), backbone_hw, form)
         b = self._masks.get(key)
         if b is None:
             b = ops.warp_wino_boxes([self.m_norm_cpu[c] for c in cams], self.src_hw, self.grid_hw, device,
-                                    backbone_hw=backbone_hw)
+                                    backbone_hw=backbone_hw, form=form)
             self._masks[key] = b
         return b
 
@@ -493,13 +542,15 @@ class ProjectFuse:
             self._masks[key] = r
         return r
 
-    def conv1_order(self, device, row0: int, rows: int, B: int, grid: bool = False) -> Optional[torch.Tensor]:
+    def conv1_order(self, device, row0: int, rows: int, B: int, grid: bool = False,
+                    tile_h: Optional[int] = None) -> Optional[torch.Tensor]:
         """Heavy-first run order of the forward conv1's pixel tiles (``grid``: of the 12 x 32
-        grid even where the forward uses edge strips)."""
-        key = ("order", str(device), row0, rows, B, grid)
+        grid even where the forward uses edge strips; ``tile_h``: of the ``tile_h`` x 32 grid)."""
+        key = ("order", str(device), row0, rows, B, grid, tile_h)
         o = self._masks.get(key)
         if o is None:
-            m = self.conv1_mask(device, row0, rows) if grid else self.conv1_fwd_mask(device, row0, rows)[0]
+            m = (self.conv1_mask(device, row0, rows, tile_h=tile_h) if grid or tile_h
+                 else self.conv1_fwd_mask(device, row0, rows)[0])
             if m is None:
                 return None
             o = ops.heavy_first_order(m, B)
@@ -561,6 +612,26 @@ class ProjectFuse:
         with the G w weights (``ops.conv3x3_wino``); same y1 as ``conv1`` within the 3xbf16 error."""
         a1, b1 = ws.y1_rows
         B = ws.slab.shape[1]
+        if ws.t_from_warp:
+            form = ws.t_form
+        else:
+            form = 4 if (not ws.store_y2 and (a1, b1) == (0, self.grid_hw[0])
+                         and self.wino43_pays(b1 - a1, B, ws.slab.device)) else 3
+        if form == 4:  # F(4,3): T43 (from the fused warp, else of the slab) over 16 x 32 tiles
+            th = ops.WINO43_TILE_ROWS
+            gm = self.conv1_mask(ws.slab.device, a1, b1 - a1, tile_h=th)
+            need = ops.wino43_rows_bytes(d1)
+            if ws.wino_t43 is None or ws.wino_t43.numel() * 2 < need:
+                ws.wino_t43 = torch.zeros((need + 1) // 2, dtype=torch.bfloat16, device=ws.slab.device)
+            if not ws.t_from_warp:
+                ops.wino43_rows(ws.slab, d1, ws.wino_t43, gm)
+            ws.t1_valid = False  # (T43 is not the training backward's T)
+            if mark:
+                mark("conv1_wino")
+            return ops.conv3x3_wino43(ws.wino_t43, d1, self.pack1w43.get(conv1.weight), self.mid, init=init,
+                                      relu=True, out=ws.y1, group_mask=gm,
+                                      tile_order=self.conv1_order(ws.slab.device, a1, b1 - a1, B, grid=True,
+                                                                  tile_h=th))
         gm = self.conv1_mask(ws.slab.device, a1, b1 - a1)
         need = ops.wino_rows_bytes(d1)
         if ws.wino_t is None or ws.wino_t.numel() * 2 < need:
@@ -614,6 +685,14 @@ class ProjectFuse:
         need = ops.conv3x3_cout1_partials_bytes(d2, self.mid)
         if ws.p3 is None or ws.p3.numel() * 4 < need:
             ws.p3 = torch.empty((need + 3) // 4, dtype=torch.float32, device=ws.y1.device)
+        if self.wino_conv2_active(ws) and self.wino43_pays(d2.out_rows, d2.B, ws.y1.device):
+            tneed = ops.wino43_rows_bytes(d2)  # F(4,3) (ABI 12400)
+            if ws.wino_t2_43 is None or ws.wino_t2_43.numel() * 2 < tneed:
+                ws.wino_t2_43 = torch.zeros((tneed + 1) // 2, dtype=torch.bfloat16, device=ws.y1.device)
+            ops.wino43_rows(ws.y1, d2, ws.wino_t2_43, dilation=2)
+            ops.conv3x3_wino43_then_cout1_partials(ws.wino_t2_43, d2, self.pack2w43.get(conv2.weight), self.mid,
+                                                   conv2.bias, True, conv3.weight, ws.p3)
+            return
         if self.wino_conv2_active(ws):
             tneed = ops.wino_rows_bytes(d2)
             if ws.wino_t2 is None or ws.wino_t2.numel() * 2 < tneed:
@@ -660,6 +739,8 @@ class ProjectFuse:
         gm = self.conv1_mask(ws.slab.device, 0, H)  # no ReLU: the grid tiles (edge strips are conv1+ReLU only)
         order = self.conv1_order(ws.slab.device, 0, H, B, grid=True)
         w1 = map_classifier[0].weight
+        if ws.t_from_warp and ws.t_form != 3:
+            raise RuntimeError("conv1_partial reads F(3,3)'s T: this engine's fused warp wrote T43 (wino43)")
         if self.wino_active(ws.slab.device):
             need = ops.wino_rows_bytes(d1)
             if ws.wino_t is None or ws.wino_t.numel() * 2 < need:

@@ -159,3 +159,153 @@ def test_wino43_refusals():
         ops.conv3x3_wino43(small, desc, pk, 128)
     with pytest.raises(_native.NativeError):
         ops.conv3x3_wino43(t, desc, pk, 128, dilation=3)
+
+
+# -- the fused warps writing T43 (MVBEV_WARP_WINO43) and the engine's F(4,3) path -----------------------------
+def _rig(cfg, nan_view=True):
+    from mvdet_amd import synthetic
+    from mvdet_amd.geometry import kornia_src_norm_from_dst_norm, projection_matrices
+    ds = synthetic.CONFIGS[cfg]["make"]()
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    ms = [kornia_src_norm_from_dst_norm(M.float().reshape(1, 3, 3), up, grid)[0] for M in projection_matrices(ds)]
+    if nan_view:
+        ms[-1] = ms[-1].clone()
+        ms[-1][0, 2] = float("inf")  # every sample of the last view is non-finite -> NaN T
+    return ds, up, grid, ms
+
+
+def _t43_numel(B, K, Ho, Wo):
+    from mvdet_amd import ops
+    return B * (K // 8) * 6 * ops.wino_tile_rows(Ho, 4) * Wo * 16
+
+
+@pytest.mark.parametrize("cfg,C,B,kind", [(1, 32, 1, "nchw"), (2, 64, 2, "nchw"), (2, 24, 1, "nchw"), (4, 16, 2, "f16"),
+                                          (2, 64, 2, "cl"), (1, 32, 1, "cl"), (2, 32, 1, "up"), (1, 32, 2, "upcl"),
+                                          (5, 32, 1, "upcl")])
+def test_fused_warp43_matches_slab_transform_and_box_table(cfg, C, B, kind):
+    """The fused warps with MVBEV_WARP_WINO43 (NCHW fp32 / fp16, channels-last, the fused upsample on NCHW and
+    channels-last backbone maps) write the T43 of the two-pass path — the split slab of the plain warp, then
+    mvbev_wino43_rows_split_bf16 — to the split's rounding, with finite geometry; and, with a NaN-geometry view
+    and an inf feature, bitwise the same T43 with and without the per-geometry box table, skip_zero on and off,
+    reporting the non-finite feature."""
+    from mvdet_amd import ops, synthetic
+    ds, up, grid, ms = _rig(cfg, nan_view=False)
+    N = ds.num_cam
+    Ho, Wo = grid
+    hb = tuple(u // 3 for u in up)
+    upk = kind in ("up", "upcl")
+    if upk:
+        feats = [synthetic.backbone_features(B, C, hb, seed=41 + v, device=DEV) for v in range(N)]
+    else:
+        feats = [synthetic.synthetic_features(B, C, hb, up, seed=41 + v, device=DEV) for v in range(N)]
+    if kind == "f16":
+        feats = [f.half() for f in feats]
+    if kind in ("cl", "upcl"):
+        feats = [f.contiguous(memory_format=torch.channels_last) for f in feats]
+    K = N * C
+    kw = dict(up_hw=up) if upk else {}
+    t = torch.zeros(_t43_numel(B, K, Ho, Wo), dtype=torch.bfloat16, device=DEV)
+    ops.warp_views_wino_rows_into(feats, ms, t, list(range(N)), C, K, Ho, Wo, dst_zeroed=True, form=4,
+                                  boxes=ops.warp_wino_boxes(ms, up, grid, DEV, backbone_hw=hb if kind == "upcl" else None,
+                                                            form=4), **kw)
+    # two-pass: the split slab (per view: [B, C/8, Ho, Wo, 2, 8]) and its T43
+    slab = torch.zeros((N,) + ops.split_shape(B, C, Ho, Wo), dtype=torch.bfloat16, device=DEV)
+    src32 = [f.float().contiguous() for f in feats]
+    if upk:
+        ops.warp_views_upsampled_into(src32, up, ms, [slab[v] for v in range(N)], split=True, dst_zeroed=True)
+    else:
+        ops.warp_views_into(src32, ms, [slab[v] for v in range(N)], split=True, dst_zeroed=True)
+    desc = ops.conv_desc(B, K, Ho, Wo, group=C, group_stride=B * C * Ho * Wo, batch_stride=C * Ho * Wo)
+    t2 = torch.zeros(ops.wino43_rows_bytes(desc) // 2, dtype=torch.bfloat16, device=DEV)
+    ops.wino43_rows(slab, desc, t2)
+    a, b = _t43_values(t, B, K, Ho, Wo)[0], _t43_values(t2, B, K, Ho, Wo)[0]
+    assert np.abs(a - b).max() <= 2e-4 * max(1.0, np.abs(b).max())
+    # non-finite geometry and features: the box table changes nothing (bitwise), the report fires
+    ds, up, grid, ms = _rig(cfg)
+    feats = [f.clone() for f in feats]
+    feats[0][B - 1, C - 1, feats[0].shape[2] // 2, feats[0].shape[3] // 2] = float("inf")
+    boxes = ops.warp_wino_boxes(ms, up, grid, DEV, backbone_hw=hb if kind == "upcl" else None, form=4)
+    for zeroed in (False, True):
+        outs = []
+        for bx in ((None, boxes) if kind != "up" else (None,)):
+            t = torch.zeros(_t43_numel(B, K, Ho, Wo), dtype=torch.bfloat16, device=DEV)
+            flag = torch.zeros(1, dtype=torch.int32, device=DEV)
+            ops.warp_views_wino_rows_into(feats, ms, t, list(range(N)), C, K, Ho, Wo, dst_zeroed=zeroed,
+                                          nonfinite=(flag, 9), boxes=bx, form=4, **kw)
+            outs.append((t.view(torch.int16).cpu(), int(flag.item())))
+        assert all(f == 9 for _, f in outs)
+        assert all(torch.equal(outs[0][0], o) for o, _ in outs[1:])
+        v = _t43_values(outs[0][0].view(torch.bfloat16), B, K, Ho, Wo)[0]
+        assert np.isnan(v[:, (N - 1) * C // 8 * 8:]).any()  # the NaN view's T43 is written
+
+
+def _head(N, C, seed):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Conv2d(N * C + 2, 512, 3, padding=1), torch.nn.ReLU(),
+                               torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
+                               torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False)).to(DEV)
+
+
+@pytest.mark.parametrize("cfg,C,B,up", [(1, 32, 1, False), (2, 24, 2, False), (1, 32, 1, True), (4, 16, 2, False)])
+def test_engine_wino43_matches_f33(cfg, C, B, up):
+    """ProjectFuse(wino43=True): the fused warp writes T43, conv1 and conv2 -> conv3 run F(4,3); y1 and the map
+    match the F(3,3) engine (wino43=False) within the 3xbf16 tolerance, and the slab path (wino_warp off:
+    wino43_rows of the slab) gives the fused path's map."""
+    from mvdet_amd import ProjectFuse, synthetic
+    from mvdet_amd.geometry import projection_matrices
+    ds = synthetic.CONFIGS[cfg]["make"]()
+    N = ds.num_cam
+    upsz, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    pm = projection_matrices(ds)
+    hb = [u // 3 for u in upsz]
+    if up:
+        feats = [synthetic.backbone_features(B, C, hb, seed=5 + v, device=DEV) for v in range(N)]
+    else:
+        feats = [synthetic.synthetic_features(B, C, hb, upsz, seed=5 + v, device=DEV) for v in range(N)]
+    if cfg == 4:
+        feats = [f.half() for f in feats]
+    mc = _head(N, C, cfg)
+    e33 = ProjectFuse(pm, upsz, grid, C, wino43=False)
+    e43 = ProjectFuse(pm, upsz, grid, C, wino43=True)
+    e43s = ProjectFuse(pm, upsz, grid, C, wino43=True, wino_warp=False)
+    maps, y1s = [], []
+    with torch.no_grad():
+        for e in ((e33, e43) if cfg == 4 else (e33, e43, e43s)):  # (the slab path takes fp32 features)
+            ws = e.workspace(B, DEV)
+            (e.warp_views_upsampled if up else e.warp_views)(ws, list(range(N)), feats)
+            maps.append(e.fuse(ws, mc).clone())
+            y1s.append(e.y1_fp32(ws).clone())
+            if e is e43:
+                assert ws.t_from_warp and ws.t_form == 4 and ws.wino_t is None
+    assert_parity(y1s[1].cpu(), y1s[0].cpu(), "F(4,3) y1 vs F(3,3)", normwise_tol=TOL)
+    assert_parity(maps[1].cpu(), maps[0].cpu(), "F(4,3) map vs F(3,3)", normwise_tol=TOL)
+    if len(maps) > 2:
+        assert_parity(maps[2].cpu(), maps[1].cpu(), "F(4,3) slab path vs fused", normwise_tol=TOL)
+
+
+def test_engine_wino43_nonfinite_guard_matches_f33():
+    """A NaN / inf feature under the F(4,3) path: the fused warp's report gates the exact path, whose map keeps
+    the reference's NaN / inf pattern — the F(3,3) engine's (pinned to the oracle in test_gpu_nonfinite.py)."""
+    from mvdet_amd import ProjectFuse, synthetic
+    from mvdet_amd.geometry import projection_matrices
+    ds = synthetic.CONFIGS[1]["make"]()
+    N, C, B = ds.num_cam, 32, 1
+    upsz, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    pm = projection_matrices(ds)
+    feats = [synthetic.synthetic_features(B, C, [u // 3 for u in upsz], upsz, seed=61 + v, device=DEV)
+             for v in range(N)]
+    feats[1][0, 3, upsz[0] // 2, upsz[1] // 3] = float("nan")
+    feats[2][0, 5, upsz[0] // 3, upsz[1] // 2] = float("inf")
+    mc = _head(N, C, 7)
+    outs = []
+    with torch.no_grad():
+        for w43 in (False, True):
+            e = ProjectFuse(pm, upsz, grid, C, wino43=w43)
+            ws = e.workspace(B, DEV)
+            e.warp_views(ws, list(range(N)), feats)
+            outs.append(e.fuse(ws, mc).cpu())
+    a, b = outs
+    assert torch.equal(a.isnan(), b.isnan()) and torch.equal(a.isinf(), b.isinf())
+    assert a.isnan().any() or a.isinf().any()
+    fin = a.isfinite()
+    assert_parity(b[fin].view(1, -1), a[fin].view(1, -1), "finite part", normwise_tol=TOL)

@@ -214,6 +214,11 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
     t_c3 = avg(ev["conv3"], ev["guard"] if guarded else end_ev)
     t_guard = avg(ev["guard"], end_ev) if guarded else 0.0
     wino2 = eng.wino_conv2_active(ws)  # conv2 -> conv3 partials as row-Winograd
+    # the row-Winograd forms that ran (F(4,3) where ProjectFuse.wino43_pays: 6 transformed rows per 4 output rows,
+    # 1/2 of the direct MFMA work; F(3,3): 5 per 3, 5/9)
+    f1 = eng.conv1_form(ws) if wino else 0
+    f2 = eng.conv2_form(ws) if wino2 else 0
+    wf = {0: 1.0, 3: 5.0 / 9.0, 4: 0.5}
     value = B * K / dt
     # algorithmic work; conv1 runs over the N*C view channels per step (the
     # 2 coord channels are folded into a per-weight-version init term)
@@ -227,8 +232,8 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
     warp_bytes = sum(s * B * C * (t + ho * wo) for t in tv)
     # what the kernel's output buffer would take if dense: the slab, or with the fused B^T conv1's row transform
     # T (5 split-bf16 rows per 3-row tile, 4 B per element; it writes only the frustum mask's tiles)
-    warp_out_dense = (N * B * C * 4 * 5 * 4 * -(-ho // 12) * wo if eng.wino_warp
-                      else N * B * C * eng.slab_dtype.itemsize * ho * wo)
+    warp_out_dense = ((N * B * C * 4 * 6 * 4 * -(-ho // 16) * wo if f1 == 4 else N * B * C * 4 * 5 * 4 * -(-ho // 12) * wo)
+                      if eng.wino_warp else N * B * C * eng.slab_dtype.itemsize * ho * wo)
     # conv3's stage: with conv2 -> conv3 fused (bf16x3) it reads the [B, 8 sets, 9 taps, rows, Wo] fp32
     # partials conv2's epilogue wrote (y2 never reaches HBM) and writes the map; on a stored y2 (fp32
     # path) it reads y2's 512 channels
@@ -237,12 +242,12 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
     conv3_read = 4.0 * B * (2 * 512 // 128) * 9 * y2rows * wo if fused3 else 4.0 * B * 512 * y2rows * wo
     conv3_bytes = conv3_read + 4.0 * B * ho * wo
     conv1_alg_tfs = conv1_flop / (t_c1k * 1e-3) / 1e12  # over the conv kernel's time
-    active = eng.conv1_active_fraction(dev, *ws.y1_rows[:1], ws.y1_rows[1] - ws.y1_rows[0], grid=wino) \
-        if precision == "bf16x3" else 1.0
+    active = eng.conv1_active_fraction(dev, *ws.y1_rows[:1], ws.y1_rows[1] - ws.y1_rows[0], grid=wino,
+                                       tile_h=16 if f1 == 4 else None) if precision == "bf16x3" else 1.0
     # the end-to-end floor prices the algorithm that executes: conv1's frustum-active products, the
     # row-Winograd forms at 5/9 of the direct MFMA work, 3 bf16 passes (bf16x3) or the fp32 MFMA peak
-    w1 = 5.0 / 9.0 if wino else 1.0
-    w2 = 5.0 / 9.0 if wino2 else 1.0
+    w1 = wf[f1]
+    w2 = wf[f2]
     mfma_s = (3 * (active * w1 * conv1_flop + w2 * conv2_flop) / (BF16_MFMA_PEAK_TFS * 1e12) if precision == "bf16x3"
               else (active * conv1_flop + conv2_flop) / (FP32_MFMA_PEAK_TFS * 1e12))
     hbm_s = (warp_bytes + conv3_bytes) / (HBM_PEAK_GBS * 1e9)
@@ -253,8 +258,10 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
         # Algorithmic = the reference's dense conv; the frustum mask executes `active` of it.
         # Winograd F(3,3) along the rows executes 5 of the direct conv's 9 MFMA K-blocks per
         # (chunk, kernel column): its MFMA work is 5/9 of the direct count
-        achieved, peak = conv1_alg_tfs * 3 * (5.0 / 9.0 if wino else 1.0), BF16_MFMA_PEAK_TFS
-        kname = ("conv_wino_kernel (conv1: row-Winograd F(3,3), 3xbf16 MFMA, LDS-DMA unit ring, frustum-masked)"
+        achieved, peak = conv1_alg_tfs * 3 * w1, BF16_MFMA_PEAK_TFS
+        kname = ("conv_wino43_kernel (conv1: row-Winograd F(4,3) walked xi-major, 3xbf16 MFMA, LDS-DMA unit ring, "
+                 "frustum-masked 16 x 32 tiles)" if f1 == 4 else
+                 "conv_wino_kernel (conv1: row-Winograd F(3,3), 3xbf16 MFMA, LDS-DMA unit ring, frustum-masked)"
                  if wino else "conv_ring_kernel (conv1: 3xbf16 MFMA, LDS-DMA ring, frustum-masked)")
     else:
         achieved, peak = conv1_alg_tfs, FP32_MFMA_PEAK_TFS
@@ -284,8 +291,9 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
         "roofline": {"kernel": kname, "bound": "mfma", "achieved": round(achieved * active, 2), "peak": peak,
                      "unit": "TFLOP/s", "frac": round(achieved * active / peak, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "basis": (("3 bf16 MFMA passes x 5/9 (row Winograd) x 2*B*Ho*Wo*9*(N*C)*512 x "
-                                "frustum_active_fraction over the conv kernel's time" if wino else
+                     "basis": (("3 bf16 MFMA passes x " + ("1/2 (row Winograd F(4,3))" if f1 == 4 else
+                                                               "5/9 (row Winograd F(3,3))") +
+                                " x 2*B*Ho*Wo*9*(N*C)*512 x frustum_active_fraction over the conv kernel's time" if wino else
                                 "3 bf16 MFMA passes x 2*B*Ho*Wo*9*(N*C)*512 x frustum_active_fraction")
                                if precision == "bf16x3" else "2*B*Ho*Wo*9*(N*C)*512 at the fp32 MFMA peak"),
                      "frustum_active_fraction": round(active, 4),
@@ -311,8 +319,8 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
         "e2e_roofline": {
             "floor_ms": round(e2e_floor_ms, 4),
             "frac": round(e2e_floor_ms / (dt * 1e3 / K), 4),
-            "basis": "warp_bytes/8 TB/s + (conv1 flop x frustum_active" + (" x 5/9" if wino else "") +
-                     " + conv2 flop" + (" x 5/9" if wino2 else "") + ") " +
+            "basis": "warp_bytes/8 TB/s + (conv1 flop x frustum_active" + {0: "", 3: " x 5/9", 4: " x 1/2"}[f1] +
+                     " + conv2 flop" + {0: "", 3: " x 5/9", 4: " x 1/2"}[f2] + ") " +
                      ("x3 / 2.5 PF bf16" if precision == "bf16x3" else "/ 157.3 TF fp32") +
                      " + conv3_bytes/8 TB/s (the executed algorithm)",
         },
@@ -321,7 +329,8 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
                      "algorithmic_basis": "SURVEY §8(d): sum_v s*B*C*(T_v + Ho*Wo), T_v = touched source pixels",
                      # with the Winograd conv1 the warp writes the row transform T (warp_wino_kernel:
                      # 5/3 of the slab's rows, the separate transform gone), so its time includes B^T
-                     "output": "row-Winograd T (warp + B^T fused)" if eng.wino_warp else "split-bf16 slab",
+                     "output": (("row-Winograd T43 (warp + F(4,3) B^T fused)" if f1 == 4 else
+                                 "row-Winograd T (warp + B^T fused)") if eng.wino_warp else "split-bf16 slab"),
                      "output_dense_bytes": warp_out_dense,
                      "achieved_GBs": round(warp_bytes / (t_warp * 1e-3) / 1e9, 1), "peak_GBs": HBM_PEAK_GBS,
                      # PMC bytes (read at 128-B granules: NCHW rows are gathered, not streamed)
@@ -330,10 +339,11 @@ def run_single(args, precision, steps, warmup, with_cpu, config=None, cpu_plan=N
             "conv2": {"bound": "mfma", "algorithmic_fp32_TFs": round(conv2_flop / (t_c2 * 1e-3) / 1e12, 2),
                       # executed bf16 MFMA work over conv2's stage time (its dilation-2 row transform
                       # included when row-Winograd: 3 passes x 5/9 of the direct products)
-                      "executed_bf16_frac": (round(3 * conv2_flop * (5.0 / 9.0 if wino2 else 1.0) / (t_c2 * 1e-3)
+                      "executed_bf16_frac": (round(3 * conv2_flop * w2 / (t_c2 * 1e-3)
                                                    / (BF16_MFMA_PEAK_TFS * 1e12), 4)
                                              if precision == "bf16x3" else None),
-                      "form": "row-Winograd F(3,3), dilation 2" if wino2 else "direct"},
+                      "form": {0: "direct", 3: "row-Winograd F(3,3), dilation 2",
+                               4: "row-Winograd F(4,3) xi-major, dilation 2"}[f2]},
             "conv3": {"bound": "hbm", "algorithmic_bytes": conv3_bytes,
                       "reads": "conv2's conv3 partials [B, 8, 9, rows, Wo] fp32" if fused3 else "y2 [B, 512, rows, Wo] fp32",
                       "achieved_GBs": round(conv3_bytes / (t_c3 * 1e-3) / 1e9, 1), "peak_GBs": HBM_PEAK_GBS},

@@ -557,10 +557,21 @@ class ProjectFuse:
             self._masks[key] = o
         return o
 
-    def conv1_active_fraction(self, device, row0: int, rows: int, grid: bool = False) -> float:
+    def conv1_active_fraction(self, device, row0: int, rows: int, grid: bool = False,
+                              tile_h: Optional[int] = None) -> float:
         """Fraction of conv1's dense (pixel, slot) work the forward's frustum mask keeps (1.0 =
         dense): per tile its enabled slots x its pixels inside the grid.  ``grid``: over the
-        12 x 32 grid tiles (the row-Winograd conv1's tile space) instead of the forward's."""
+        12 x 32 grid tiles (the row-Winograd conv1's tile space) instead of the forward's;
+        ``tile_h``: over the ``tile_h`` x 32 grid (16: F(4,3)'s)."""
+        if tile_h:
+            m = self.conv1_mask(device, row0, rows, tile_h=tile_h)
+            if m is None:
+                return 1.0
+            W, S, th = self.grid_hw[1], self.S, int(tile_h)
+            tx = -(-W // 32)
+            bits = [bin(int(v) & 0xFFFFFFFF).count("1") for v in m.cpu().tolist()]
+            return sum(bb * min(th, rows - (t // tx) * th) * min(32, W - (t % tx) * 32)
+                       for t, bb in enumerate(bits[:tx * -(-rows // th)])) / (rows * W * S)
         m, space = ((self.conv1_mask(device, row0, rows), _native.TILES_GRID) if grid
                     else self.conv1_fwd_mask(device, row0, rows))
         if m is None:
@@ -612,12 +623,7 @@ class ProjectFuse:
         with the G w weights (``ops.conv3x3_wino``); same y1 as ``conv1`` within the 3xbf16 error."""
         a1, b1 = ws.y1_rows
         B = ws.slab.shape[1]
-        if ws.t_from_warp:
-            form = ws.t_form
-        else:
-            form = 4 if (not ws.store_y2 and (a1, b1) == (0, self.grid_hw[0])
-                         and self.wino43_pays(b1 - a1, B, ws.slab.device)) else 3
-        if form == 4:  # F(4,3): T43 (from the fused warp, else of the slab) over 16 x 32 tiles
+        if self.conv1_form(ws) == 4:  # F(4,3): T43 (from the fused warp, else of the slab) over 16 x 32 tiles
             th = ops.WINO43_TILE_ROWS
             gm = self.conv1_mask(ws.slab.device, a1, b1 - a1, tile_h=th)
             need = ops.wino43_rows_bytes(d1)
@@ -644,6 +650,22 @@ class ProjectFuse:
         return ops.conv3x3_wino(ws.wino_t, d1, self.pack1w.get(conv1.weight), self.mid, init=init, relu=True,
                                 out=ws.y1, group_mask=gm,
                                 tile_order=self.conv1_order(ws.slab.device, a1, b1 - a1, B, grid=True))
+
+    def conv1_form(self, ws: Workspace) -> int:
+        """The row-Winograd form of ``conv1_wino`` on this workspace: the fused warp's (``ws.t_form``), else 4 for
+        an inference forward over the whole grid where ``wino43_pays``, else 3."""
+        if ws.t_from_warp:
+            return ws.t_form
+        a1, b1 = ws.y1_rows
+        return 4 if (not ws.store_y2 and (a1, b1) == (0, self.grid_hw[0])
+                     and self.wino43_pays(b1 - a1, ws.slab.shape[1], ws.slab.device)) else 3
+
+    def conv2_form(self, ws: Workspace) -> int:
+        """The row-Winograd form of ``conv2_partials`` (0: not row-Winograd)."""
+        if not self.wino_conv2_active(ws):
+            return 0
+        (a2, b2) = ws.y2_rows
+        return 4 if self.wino43_pays(b2 - a2, ws.y1.shape[0], ws.y1.device) else 3
 
     def conv2(self, ws: Workspace, conv2: torch.nn.Conv2d) -> torch.Tensor:
         """a8: y2 = relu(conv3x3_d2(y1) + b2) on y2's rows (row-Winograd where ``wino_conv2_active``:
@@ -685,7 +707,7 @@ class ProjectFuse:
         need = ops.conv3x3_cout1_partials_bytes(d2, self.mid)
         if ws.p3 is None or ws.p3.numel() * 4 < need:
             ws.p3 = torch.empty((need + 3) // 4, dtype=torch.float32, device=ws.y1.device)
-        if self.wino_conv2_active(ws) and self.wino43_pays(d2.out_rows, d2.B, ws.y1.device):
+        if self.conv2_form(ws) == 4:
             tneed = ops.wino43_rows_bytes(d2)  # F(4,3) (ABI 12400)
             if ws.wino_t2_43 is None or ws.wino_t2_43.numel() * 2 < tneed:
                 ws.wino_t2_43 = torch.zeros((tneed + 1) // 2, dtype=torch.bfloat16, device=ws.y1.device)

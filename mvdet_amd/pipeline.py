@@ -243,12 +243,15 @@ class ProjectFuse:
         self.pack2w43 = ops.PackedConv3x3(None, "bf16x3", wino=True, form=4) if self.wino43 else None
         self._cus: Dict[str, int] = {}
 
-    def wino43_pays(self, rows: int, B: int, device) -> bool:
-        """F(4,3) over ``rows`` output rows (whole grid): enabled, its 16-row tiles waste at most 3 % of the rows
-        and the launch is at least 8 rounds of workgroups deep (16 x 32 pixel tiles x 4 Cout tiles over the CUs).
-        Measured (``profiles/r06aj_wino43_ab.jsonl``, conv1 / conv2 -> conv3): cfg3 (480 rows, 21 rounds)
-        -9.7 % / -7.5 %, cfg5 (1000 rows, 31 rounds) -8.4 % / -6.4 %, cfg2 (120 rows: 6.7 % waste, 1.5
-        rounds) +1.7 % / +9 %."""
+    def wino43_pays(self, rows: int, B: int, device, deep: bool = False) -> bool:
+        """F(4,3) over ``rows`` output rows (whole grid): enabled and its 16-row tiles waste at most 3 % of the rows;
+        ``deep`` (conv2 -> conv3, whose workgroups all cost the same): the launch is also at least 8 rounds of
+        workgroups deep (16 x 32 pixel tiles x 4 Cout tiles over the CUs) — a shallow one loses a round to
+        F(4,3)'s 1.2x larger workgroups.  Measured (interleaved kbench, ``profiles/r06aj_wino43_ab.jsonl``,
+        ``r06am_wino43_wide_tiles_ab.jsonl``), conv1 (frustum-masked, workgroups dealt heaviest first) F(3,3) ->
+        F(4,3): cfg1 0.350 -> 0.320 ms, cfg3 19.9 -> 18.0, cfg4 8.02 -> 7.12, cfg5 14.5 -> 13.3, cfg2 (120 rows:
+        6.7 % of the 16-row tiles idle) 1.437 -> 1.438; conv2 -> conv3: cfg3 4.78 -> 4.43, cfg4 2.47 -> 2.18, cfg5
+        7.05 -> 6.60, but cfg1 (1.25 rounds) 0.311 -> 0.343 and cfg2 0.327 -> 0.357."""
         if not self.wino43:
             return False
         if self._wino43_forced:
@@ -257,6 +260,8 @@ class ProjectFuse:
         h16 = -(-rows // 16) * 16
         if h16 - rows > 0.03 * rows:
             return False
+        if not deep:
+            return True
         key = str(torch.device(device))
         if key not in self._cus:
             dev = torch.device(device)
@@ -665,7 +670,7 @@ class ProjectFuse:
         if not self.wino_conv2_active(ws):
             return 0
         (a2, b2) = ws.y2_rows
-        return 4 if self.wino43_pays(b2 - a2, ws.y1.shape[0], ws.y1.device) else 3
+        return 4 if self.wino43_pays(b2 - a2, ws.y1.shape[0], ws.y1.device, deep=True) else 3
 
     def conv2(self, ws: Workspace, conv2: torch.nn.Conv2d) -> torch.Tensor:
         """a8: y2 = relu(conv3x3_d2(y1) + b2) on y2's rows (row-Winograd where ``wino_conv2_active``:

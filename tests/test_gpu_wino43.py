@@ -246,7 +246,8 @@ def _head(N, C, seed):
                                torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False)).to(DEV)
 
 
-@pytest.mark.parametrize("cfg,C,B,up", [(1, 32, 1, False), (2, 24, 2, False), (1, 32, 1, True), (4, 16, 2, False)])
+@pytest.mark.parametrize("cfg,C,B,up", [(1, 32, 1, False), (2, 24, 2, False), (1, 32, 1, True), (4, 16, 2, False),
+                                        (2, 32, 1, True)])
 def test_engine_wino43_matches_f33(cfg, C, B, up):
     """ProjectFuse(wino43=True): the fused warp writes T43, conv1 and conv2 -> conv3 run F(4,3); y1 and the map
     match the F(3,3) engine (wino43=False) within the 3xbf16 tolerance, and the slab path (wino_warp off:

@@ -169,7 +169,7 @@ def main():
         # the slab path (wino_warp off) so the transform stages run on real data; warpw / warpupw
         # switch the fused warp on (and leave T from the warp: run them last)
         weng = ProjectFuse(pm, up, (ho, wo), C, precision=args.precision, frustum=not args.no_frustum,
-                           wino_conv1=True, wino_warp=False)
+                           wino_conv1=True, wino_warp=False, wino43=False)  # (F(3,3): the F(4,3) stages below)
         wws = weng.workspace(B, dev)
         weng.warp_views(wws, list(range(N)), feats)
         weng.conv1(wws, mc[0])

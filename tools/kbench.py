@@ -188,6 +188,7 @@ def main():
         pk243 = ops.pack_wino43(mc[2].weight)
         p3_43 = torch.empty(ops.conv3x3_cout1_partials_bytes(d2, 512) // 4, dtype=torch.float32, device=dev)
         y1_43 = torch.empty_like(wws.y1)
+        t43w = torch.zeros_like(t43)  # (warpw43's T43: its own zero-filled buffer, written only by that geometry)
 
         def conv23w43():
             ops.wino43_rows(wws.y1, d2, t243, dilation=2)
@@ -215,6 +216,10 @@ def main():
             "winorows": (lambda: ops.wino_rows(wws.slab, wd1, wws.wino_t, wgm), None),
             "warpw": (lambda: _with(weng, "wino_warp", True, lambda: weng.warp_views(wws, list(range(N)), feats)),
                       None),  # warp + B^T in one pass (wino_warp; leaves T from the warp, run it last)
+            # the same writing T43 (MVBEV_WARP_WINO43: the F(4,3) engine's fused warp) into its own buffer
+            "warpw43": (lambda: ops.warp_views_wino_rows_into(
+                feats, [weng.m_norm_cpu[c] for c in range(N)], t43w, list(range(N)), weng.Cs, weng.S * weng.Cs, ho, wo,
+                dst_zeroed=True, boxes=weng._wino_boxes(dev, list(range(N)), form=4), form=4), None),
             # round 6: the same without the per-geometry box table (each block reduces its own box)
             "warpw0": (lambda: _with(weng, "_wino_boxes", lambda dev, cams, bb=None: None, lambda: _with(
                 weng, "wino_warp", True, lambda: weng.warp_views(wws, list(range(N)), feats))), None),

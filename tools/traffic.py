@@ -20,7 +20,8 @@ import sys
 
 out_dir, tag, cfg = sys.argv[1], sys.argv[2], int(sys.argv[3])
 precision = sys.argv[4] if len(sys.argv) > 4 else "bf16x3"
-wino = len(sys.argv) > 5 and sys.argv[5] == "wino"  # conv1 = the row-Winograd conv kernel (kbench winoconv)
+wino = len(sys.argv) > 5 and sys.argv[5] in ("wino", "wino43")  # conv1 = the row-Winograd conv kernel (kbench winoconv)
+w43 = len(sys.argv) > 5 and sys.argv[5] == "wino43"  # the F(4,3) kernels (kbench winoconv43, conv2w43, warpw43)
 vals = collections.defaultdict(lambda: collections.defaultdict(dict))
 for f in glob.glob(f"{out_dir}/{tag}_pmc*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
@@ -46,18 +47,20 @@ for name in vals:
 # edge-strip tiles "<1, true, false, EW>"), or the fp32-MFMA kernel
 pat = r"conv_ring_kernel<1, true(, false, \d+)?>" if precision == "bf16x3" else r"conv3x3_mfma_f32_kernel<1, true"
 if wino:
-    pat = r"conv_wino_kernel<true, 1, false>"
-    c2 = [k for k in res["kernels"] if "conv_wino_kernel<true, 2, true>" in k]
+    kn = "conv_wino43_kernel" if w43 else "conv_wino_kernel"
+    pat = kn + r"<true, 1, false>"
+    c2 = [k for k in res["kernels"] if kn + "<true, 2, true>" in k]
     if c2:  # conv2 -> conv3 partials, row-Winograd (ABI 11500)
         res["conv2_hbm_bytes_per_launch"] = res["kernels"][c2[0]]["hbm_bytes_per_launch"]
-    rows = [k for k in res["kernels"] if "wino_rows_kernel" in k]
+    rows = [k for k in res["kernels"] if ("wino43_rows_kernel" if w43 else "wino_rows_kernel") in k]
     if rows:
         res["wino_rows_hbm_bytes_per_launch"] = res["kernels"][rows[0]]["hbm_bytes_per_launch"]
 conv1 = [k for k in res["kernels"] if re.search(pat, k)]
 if conv1:
     res["conv1_hbm_bytes_per_launch"] = res["kernels"][conv1[0]]["hbm_bytes_per_launch"]
 # the all-views warp of the timed "warp" stage: the largest-grid warp_tile_kernel dispatch
-warps = [k for k in res["kernels"] if ("warp_wino_kernel" if wino else "warp_tile_kernel") in k]
+warps = [k for k in res["kernels"] if ("warp_wino_kernel" if wino else "warp_tile_kernel") in k
+         and (not w43 or "float, 4>" in k)]
 if warps:
     k = max(warps, key=lambda n: int(n.rsplit("grid ", 1)[1].rstrip("]")))
     res["warp_hbm_bytes_per_launch"] = res["kernels"][k]["hbm_bytes_per_launch"]

@@ -52,7 +52,8 @@ if wino:
     c2 = [k for k in res["kernels"] if kn + "<true, 2, true>" in k]
     if c2:  # conv2 -> conv3 partials, row-Winograd (ABI 11500)
         res["conv2_hbm_bytes_per_launch"] = res["kernels"][c2[0]]["hbm_bytes_per_launch"]
-    rows = [k for k in res["kernels"] if ("wino43_rows_kernel" if w43 else "wino_rows_kernel") in k]
+    rows = sorted((k for k in res["kernels"] if ("wino43_rows_kernel" if w43 else "wino_rows_kernel") in k),
+                  key=lambda n: int(n.rsplit("grid ", 1)[1].rstrip("]")))  # (the smallest: conv2's y1 transform)
     if rows:
         res["wino_rows_hbm_bytes_per_launch"] = res["kernels"][rows[0]]["hbm_bytes_per_launch"]
 conv1 = [k for k in res["kernels"] if re.search(pat, k)]

@@ -550,12 +550,14 @@ typedef struct mvbev_bev_geometry {
 } mvbev_bev_geometry;
 typedef struct mvbev_bev_plan {     /* host memory, caller-owned; filled by the calls below */
   mvbev_bev_geometry g;
-  int32_t wino;                     /* after prepare: 1 = row-Winograd conv1, 0 = direct (non-finite geometry) */
+  int32_t wino;                     /* after prepare: 1 = row-Winograd conv1, 0 = direct (non-finite geometry);
+                                       ABI 12400: 2 = row-Winograd F(4,3) (grids whose rows fill 16-row tiles) */
   int32_t frustum;                  /* conv1 skips the views a tile's camera frustum excludes (C % 16 == 0 after padding) */
   int32_t prepared;
-  int32_t wino2;                    /* after prepare: 1 = row-Winograd conv2 -> conv3 partials (ABI 11500; finite geometry) */
+  int32_t wino2;                    /* after prepare: 1 = row-Winograd conv2 -> conv3 partials (ABI 11500; finite geometry);
+                                       ABI 12400: 2 = F(4,3) (16-row tiles and a launch >= 8 rounds deep) */
   int32_t guard;                    /* 1 = the non-finite-feature guard runs behind the row-Winograd path (ABI 11600) */
-  int64_t Cs, tiles;                /* channels per view slot (C rounded to 8); conv1's 12 x 32 tiles */
+  int64_t Cs, tiles;                /* channels per view slot (C rounded to 8); conv1's 12 x 32 tiles (16 x 32 with wino 2) */
   size_t off[24];                   /* workspace regions */
   size_t workspace_bytes;           /* >= what mvbev_bev_fuse_workspace_bytes returns, 256-B aligned base */
   const float* b2;

@@ -98,18 +98,36 @@ void slab_views(const mvbev_bev_plan* p, const void* const* views, void* slab, m
   }
 }
 
-// the same writing slot s's channels of T (the Winograd transform of the whole grid)
+// row tiles of the whole grid's row-Winograd transform: 4 ceil(Ho / 12) three-row tiles (F(3,3)), or
+// 4 ceil(Ho / 16) four-row tiles (F(4,3), plan wino 2)
+int64_t t_tile_rows(const mvbev_bev_plan* p) {
+  return p->wino == 2 ? 4 * ((p->g.Ho + 15) / 16) : 4 * ((p->g.Ho + 11) / 12);
+}
+
+// The F(4,3) policy of ProjectFuse.wino43_pays (pipeline.py): 16-row tiles wasting at most 3 % of the grid's
+// rows (conv1, frustum-masked: workgroups of uneven cost dealt heaviest first) and, for conv2 -> conv3
+// (workgroups of equal cost), a launch at least 8 rounds of workgroups deep
+bool w43_rows_ok(int64_t Ho) { return (double)(((Ho + 15) / 16) * 16 - Ho) <= 0.03 * (double)Ho; }
+bool w43_deep(const mvbev_bev_geometry& g) {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  return ((g.Ho + 15) / 16) * ((g.Wo + kTileW - 1) / kTileW) * g.B * (kMid / 128) >= 8 * (int64_t)cus;
+}
+
+// the same writing slot s's channels of T (the Winograd transform of the whole grid; T43 with plan wino 2)
 void t_views(const mvbev_bev_plan* p, const void* const* views, void* t, mvbev_warp_view* out) {
   const mvbev_bev_geometry& g = p->g;
   const bool backbone = kind_of(g) == MVBEV_BEV_SRC_BACKBONE_F32;
   const int64_t sh = backbone ? g.h : g.H, sw = backbone ? g.w : g.W;
-  const int64_t r3 = 4 * ((g.Ho + 11) / 12), K8 = g.num_views * p->Cs / kKC;
+  const int64_t nx = p->wino == 2 ? 6 : 5, r3 = t_tile_rows(p), K8 = g.num_views * p->Cs / kKC;
   for (int s = 0; s < g.num_views; ++s) {
     mvbev_warp_view& v = out[s];
     v.src = views[s];
     src_strides(g, sh, sw, v.src_strides);
-    v.dst = static_cast<char*>(t) + (size_t)32 * (s * (p->Cs / kKC)) * 5 * r3 * g.Wo;
-    v.dst_strides[0] = K8 * 5 * r3 * g.Wo; v.dst_strides[1] = 5 * r3 * g.Wo; v.dst_strides[2] = g.Wo;
+    v.dst = static_cast<char*>(t) + (size_t)32 * (s * (p->Cs / kKC)) * nx * r3 * g.Wo;
+    v.dst_strides[0] = K8 * nx * r3 * g.Wo; v.dst_strides[1] = nx * r3 * g.Wo; v.dst_strides[2] = g.Wo;
     v.dst_strides[3] = 1;
     std::memcpy(v.m, g.m[s], sizeof(v.m));
   }
@@ -156,23 +174,29 @@ int mvbev_bev_plan_init(const mvbev_bev_geometry* g, mvbev_bev_plan* p) {
   // warp + transform kernels); fp16 sources take the direct conv1 on the split slab, as the
   // engine's fp16-storage path does; prepare also falls back for non-finite geometry
   p->wino = (kind != MVBEV_BEV_SRC_F16 && g->W >= 2 && (kind != MVBEV_BEV_SRC_BACKBONE_F32 || g->w >= 4)) ? 1 : 0;
-  const int64_t tiles_y = (g->Ho + 11) / 12, tiles_x = (g->Wo + kTileW - 1) / kTileW;
+  // (ABI 12400) F(4,3) where it pays: conv1 (wino 2) and conv2 -> conv3 (wino2 2, decided in prepare)
+  if (p->wino && w43_rows_ok(g->Ho)) p->wino = 2;
+  const int64_t tiles_y = p->wino == 2 ? (g->Ho + 15) / 16 : (g->Ho + 11) / 12, tiles_x = (g->Wo + kTileW - 1) / kTileW;
   p->tiles = tiles_y * tiles_x;
   mvbev_conv_desc d1 = conv1_desc(p), d2 = conv2_desc(p);
-  const size_t t_bytes = mvbev_wino_rows_bytes(&d1);
+  const size_t t_bytes = std::max(mvbev_wino_rows_bytes(&d1), mvbev_wino43_rows_bytes(&d1));
   const size_t slab_bytes = (size_t)g->num_views * g->B * p->Cs * g->Ho * g->Wo * 4;
   size_t sz[R_COUNT] = {};
   sz[R_MAP1] = (size_t)K * 4;
-  sz[R_PACK1] = std::max(mvbev_conv3x3_packed_bytes_wino(kMid, K), mvbev_conv3x3_packed_bytes_bf16x3(kMid, K));
-  sz[R_PACK2] = std::max(mvbev_conv3x3_packed_bytes_wino(kMid, kMid), mvbev_conv3x3_packed_bytes_bf16x3(kMid, kMid));
+  sz[R_PACK1] = std::max({mvbev_conv3x3_packed_bytes_wino(kMid, K), mvbev_conv3x3_packed_bytes_wino43(kMid, K),
+                          mvbev_conv3x3_packed_bytes_bf16x3(kMid, K)});
+  sz[R_PACK2] = std::max({mvbev_conv3x3_packed_bytes_wino(kMid, kMid), mvbev_conv3x3_packed_bytes_wino43(kMid, kMid),
+                          mvbev_conv3x3_packed_bytes_bf16x3(kMid, kMid)});
   sz[R_INIT] = (size_t)kMid * g->Ho * g->Wo * 4;
-  sz[R_MASK] = (size_t)p->tiles * 4;
-  sz[R_ORDER] = (size_t)g->B * p->tiles * 4;
+  // (sized for the 12 x 32 tiles: prepare falls back to them from F(4,3)'s 16 x 32 for non-finite geometry)
+  const int64_t tiles12 = ((g->Ho + 11) / 12) * tiles_x;
+  sz[R_MASK] = (size_t)tiles12 * 4;
+  sz[R_ORDER] = (size_t)g->B * tiles12 * 4;
   sz[R_NF] = 4;
   sz[R_BIG] = std::max(t_bytes, slab_bytes);  // T (Winograd) or the split slab (direct conv1)
   sz[R_Y1] = (size_t)g->B * kMid * g->Ho * g->Wo * 4;
-  sz[R_T2] = std::max(mvbev_wino_rows_bytes(&d2),  // conv2's row-Winograd transform of y1 (the guard: its y2)
-                      (size_t)g->B * kMid * g->Ho * g->Wo * 4);
+  sz[R_T2] = std::max({mvbev_wino_rows_bytes(&d2), mvbev_wino43_rows_bytes(&d2),  // conv2's row transform of y1
+                       (size_t)g->B * kMid * g->Ho * g->Wo * 4});                     // (the guard: its y2)
   // the non-finite guard (row-Winograd plans): flag, fp32 packs of conv1 / conv2, the fp32 slab; its y1
   // reuses R_Y1 and its y2 R_T2 (both free once the fast path's conv2 has run)
   p->guard = p->wino && !(g->src_kind & MVBEV_BEV_NO_GUARD);
@@ -224,9 +248,9 @@ int mvbev_bev_fuse_prepare(mvbev_bev_plan* p, const float* w1, const float* b1, 
   for (int v = 0; v < g.num_views; ++v) std::memcpy(mv[(size_t)v].m, g.m[v], sizeof(mv[0].m));
   BEV_TRY_SYNC(mvbev_warp_nonfinite_views(mv.data(), g.num_views, g.H, g.W, g.Ho, g.Wo, at<uint32_t>(ws, p, R_NF),
                                           stream), s);
-  if (p->frustum)
-    BEV_TRY_SYNC(mvbev_warp_tile_mask(mv.data(), g.num_views, g.H, g.W, g.Ho, g.Wo, 0, g.Ho, 12, kTileW, 1,
-                                      at<uint32_t>(ws, p, R_MASK), stream), s);
+  if (p->frustum)  // (over F(4,3)'s 16 x 32 tiles with plan wino 2: the transform's and the conv's)
+    BEV_TRY_SYNC(mvbev_warp_tile_mask(mv.data(), g.num_views, g.H, g.W, g.Ho, g.Wo, 0, g.Ho, p->wino == 2 ? 16 : 12,
+                                      kTileW, 1, at<uint32_t>(ws, p, R_MASK), stream), s);
   uint32_t nf = 0;
   std::vector<uint32_t> mask((size_t)p->tiles, 0);
   if (hipMemcpyAsync(&nf, at<uint32_t>(ws, p, R_NF), 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -236,8 +260,20 @@ int mvbev_bev_fuse_prepare(mvbev_bev_plan* p, const float* w1, const float* b1, 
     return MVBEV_ERR_HIP;
   }
   if (hipStreamSynchronize(s) != hipSuccess) return MVBEV_ERR_HIP;
-  p->wino = p->wino && nf == 0 ? 1 : 0;
-  p->wino2 = nf == 0 ? 1 : 0;  // conv2's Winograd form (y1 finite), as the engine's wino_conv2_active
+  if (nf != 0 && p->wino == 2) {  // non-finite geometry: the direct conv1 on 12-row tiles (the mask is rebuilt)
+    p->tiles = ((g.Ho + 11) / 12) * ((g.Wo + kTileW - 1) / kTileW);
+    mask.assign((size_t)p->tiles, 0);
+    if (p->frustum) {
+      BEV_TRY_SYNC(mvbev_warp_tile_mask(mv.data(), g.num_views, g.H, g.W, g.Ho, g.Wo, 0, g.Ho, 12, kTileW, 1,
+                                        at<uint32_t>(ws, p, R_MASK), stream), s);
+      if (hipMemcpyAsync(mask.data(), at<uint32_t>(ws, p, R_MASK), mask.size() * 4, hipMemcpyDeviceToHost, s) !=
+              hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        return MVBEV_ERR_HIP;
+    }
+  }
+  p->wino = nf == 0 ? p->wino : 0;
+  // conv2's Winograd form (y1 finite), as the engine's wino_conv2_active; F(4,3) as its conv2_form
+  p->wino2 = nf == 0 ? (w43_rows_ok(g.Ho) && w43_deep(g) ? 2 : 1) : 0;
   if (p->frustum) {
     // heavy-first run order: most active views first, equal view sets adjacent (ops.heavy_first_order)
     const int64_t T = p->tiles, n = g.B * T;
@@ -255,13 +291,18 @@ int mvbev_bev_fuse_prepare(mvbev_bev_plan* p, const float* w1, const float* b1, 
     if (hipStreamSynchronize(s) != hipSuccess || !ok) return MVBEV_ERR_HIP;  // the host order buffer's lifetime
   }
   // weights: conv1 (G w for the Winograd form, or the direct pack), conv2, and the coord term
-  if (p->wino)
+  if (p->wino == 2)
+    BEV_TRY(mvbev_pack_conv3x3_weight_wino43(w1, kMid, cin, at<int32_t>(ws, p, R_MAP1), K, at<void>(ws, p, R_PACK1),
+                                             stream));
+  else if (p->wino)
     BEV_TRY(mvbev_pack_conv3x3_weight_wino(w1, kMid, cin, at<int32_t>(ws, p, R_MAP1), K, at<void>(ws, p, R_PACK1),
                                            stream));
   else
     BEV_TRY(mvbev_pack_conv3x3_weight_bf16x3(w1, kMid, cin, at<int32_t>(ws, p, R_MAP1), K, at<void>(ws, p, R_PACK1),
                                              stream));
-  if (p->wino2)
+  if (p->wino2 == 2)
+    BEV_TRY(mvbev_pack_conv3x3_weight_wino43(w2, kMid, kMid, nullptr, kMid, at<void>(ws, p, R_PACK2), stream));
+  else if (p->wino2)
     BEV_TRY(mvbev_pack_conv3x3_weight_wino(w2, kMid, kMid, nullptr, kMid, at<void>(ws, p, R_PACK2), stream));
   else
     BEV_TRY(mvbev_pack_conv3x3_weight_bf16x3(w2, kMid, kMid, nullptr, kMid, at<void>(ws, p, R_PACK2), stream));
@@ -304,13 +345,13 @@ int mvbev_bev_fuse(const mvbev_bev_plan* p, const void* const* views, float* map
   // a4 + a5 + a6 (+ conv1's B^T): the warp of every view in one launch
   if (p->wino) {
     t_views(p, views, big, wv);
-    const int64_t r3 = 4 * ((g.Ho + 11) / 12);
+    const int64_t r3 = t_tile_rows(p);
+    const int wf = MVBEV_WARP_DST_ZEROED | (p->wino == 2 ? MVBEV_WARP_WINO43 : 0);
     if (backbone)
-      BEV_TRY(mvbev_warp_views_upsampled_wino_rows(wv, g.num_views, g.B, g.C, g.h, g.w, g.H, g.W, g.Ho, g.Wo, r3,
-                                                   MVBEV_WARP_DST_ZEROED, gflag, 1, stream));
+      BEV_TRY(mvbev_warp_views_upsampled_wino_rows(wv, g.num_views, g.B, g.C, g.h, g.w, g.H, g.W, g.Ho, g.Wo, r3, wf,
+                                                   gflag, 1, stream));
     else
-      BEV_TRY(mvbev_warp_views_wino_rows(wv, g.num_views, g.B, g.C, g.H, g.W, g.Ho, g.Wo, r3, MVBEV_WARP_DST_ZEROED,
-                                         gflag, 1, stream));
+      BEV_TRY(mvbev_warp_views_wino_rows(wv, g.num_views, g.B, g.C, g.H, g.W, g.Ho, g.Wo, r3, wf, gflag, 1, stream));
   } else {
     slab_views(p, views, big, wv);
     if (backbone)
@@ -321,7 +362,10 @@ int mvbev_bev_fuse(const mvbev_bev_plan* p, const void* const* views, float* map
                                              g.W, g.Ho, g.Wo, MVBEV_WARP_DST_ZEROED, stream));
   }
   // a7: conv1 + coord term + bias + ReLU -> y1 (split-bf16, conv2's input)
-  if (p->wino)
+  if (p->wino == 2)
+    BEV_TRY(mvbev_conv3x3_wino43_bf16x3(big, &d1, at<void>(ws, p, R_PACK1), nullptr, at<float>(ws, p, R_INIT), kMid, 1,
+                                        1, y1, MVBEV_LAYOUT_SPLIT_BF16, mask, order, stream));
+  else if (p->wino)
     BEV_TRY(mvbev_conv3x3_wino_bf16x3(big, &d1, at<void>(ws, p, R_PACK1), nullptr, at<float>(ws, p, R_INIT), kMid, 1,
                                       y1, MVBEV_LAYOUT_SPLIT_BF16, 0, mask, order, stream));
   else
@@ -331,7 +375,12 @@ int mvbev_bev_fuse(const mvbev_bev_plan* p, const void* const* views, float* map
   // a8 + a9: conv2 + ReLU with conv3's per-tap partials in its epilogue, then their reduce
   void* p3 = at<void>(ws, p, R_P3);
   static_assert(R_P3 == R_COUNT - 1, "the partials are the workspace's last region");
-  if (p->wino2) {  // the dilation-2 row transform of y1, then the Winograd conv with the partials epilogue
+  if (p->wino2 == 2) {  // F(4,3) (ABI 12400)
+    void* t2 = at<void>(ws, p, R_T2);
+    BEV_TRY(mvbev_wino43_rows_split_bf16(y1, &d2, 2, nullptr, t2, p->off[R_T2 + 1] - p->off[R_T2], stream));
+    BEV_TRY(mvbev_conv3x3_wino43_bf16x3_cout1_partials(t2, &d2, at<void>(ws, p, R_PACK2), p->b2, kMid, 2, 1, p->w3, p3,
+                                                       p->workspace_bytes - p->off[R_P3], stream));
+  } else if (p->wino2) {  // the dilation-2 row transform of y1, then the Winograd conv with the partials epilogue
     void* t2 = at<void>(ws, p, R_T2);
     BEV_TRY(mvbev_wino_rows_split_bf16_dil(y1, &d2, 2, nullptr, t2, p->off[R_T2 + 1] - p->off[R_T2], stream));
     BEV_TRY(mvbev_conv3x3_wino_bf16x3_cout1_partials(t2, &d2, at<void>(ws, p, R_PACK2), p->b2, kMid, 2, 1, p->w3, p3,

@@ -58,6 +58,43 @@ def test_bev_fuse_cfg2_fp32_vs_oracle_and_engine():
         assert_parity_t(got, ref, f"bev_fuse cfg2 frame {frame}", normwise_tol=5e-5)
 
 
+@pytest.mark.parametrize("cfg,C,up_src", [(1, 128, False), (3, 32, False), (1, 64, True)])
+def test_bev_fuse_wino43_vs_engine_and_oracle(cfg, C, up_src):
+    """ABI 12400: grids whose rows fill 16-row tiles run F(4,3) in the one-call path too (plan wino 2: the fused
+    warp writes T43, conv1 F(4,3); wino2 2 where the launch is deep — config 3 — else F(3,3)); bitwise the
+    Python engine's map (the same kernels, masks and order; from backbone maps to fp32 rounding: the engine's
+    upsample warp reads a channels-last copy), within the gate of the oracle."""
+    from mvdet_amd import ProjectFuse, _native, ops, synthetic
+    ds = synthetic.CONFIGS[cfg]["make"]()
+    N = ds.num_cam
+    up, grid = tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    lo = [u // 3 for u in up]
+    pm, mc, tp = _setup(ds, C, seed=cfg)
+    kw = dict(src_kind=_native.BEV_SRC_BACKBONE_F32, backbone_hw=lo) if up_src else {}
+    bev = ops.BevFuse(_engine_mats(pm, up, grid), C, up, grid, **kw)
+    bev.prepare(mc, DEV)
+    eng = ProjectFuse(pm, up, grid, C)
+    assert bev.plan.wino == 2 and bev.plan.wino2 == (2 if cfg == 3 else 1)
+    if up_src:
+        feats = [synthetic.backbone_features(1, C, lo, seed=300 + v, device=DEV) for v in range(N)]
+    else:
+        feats = [synthetic.synthetic_features(1, C, lo, up, seed=300 + v, device=DEV) for v in range(N)]
+    with torch.no_grad():
+        got = bev(feats).clone()
+        ws = eng.workspace(1, DEV)
+        (eng.warp_views_upsampled if up_src else eng.warp_views)(ws, list(range(N)), feats)
+        ref_eng = eng.fuse(ws, mc)
+        assert ws.t_form == 4
+        torch.cuda.synchronize()
+        src = [cpu_path.upsample(f.cpu(), up) for f in feats] if up_src else [f.cpu() for f in feats]
+        ref = cpu_path.project_fuse(src, [M.numpy() for M in pm], grid, tp)
+    if up_src:  # (the engine copies NCHW backbone maps to channels-last for its upsample warp: T to fp32 rounding)
+        assert_parity_t(got, ref_eng, f"bev_fuse F(4,3) cfg{cfg} vs engine", normwise_tol=1e-5)
+    else:
+        assert torch.equal(got, ref_eng)
+    assert_parity_t(got, ref, f"bev_fuse F(4,3) cfg{cfg}", normwise_tol=5e-5)
+
+
 def test_bev_fuse_backbone_sources_vs_oracle():
     """Backbone-resolution sources (the detector's inference path: upsample + warp + B^T in one
     kernel), config 1's rig at C = 512, B = 2."""

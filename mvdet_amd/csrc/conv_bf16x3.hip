@@ -1483,9 +1483,6 @@ __global__ __launch_bounds__(256) void wino_rows_kernel(const WinoRowsArgs a) {
 // counts); the T DMAs keep the default cache policy (nt measured +0.5 % on conv1, +1 % on conv2).
 // DIL 2 (conv2): the wave's row tile is the ring kernel's interleaved rows base + 2 pt; P3: the
 // epilogue forms conv3's partial sums (cout1_partials) instead of storing y
-#ifndef MVBEV_WINO_ILV
-#define MVBEV_WINO_ILV 0  // 1: a kernel column's 6 MFMAs interleaved over the two Cout blocks (the same per-accumulator order)
-#endif
 #ifndef MVBEV_WINO_STAMPS
 #define MVBEV_WINO_STAMPS 0  // diagnostic builds only: per-workgroup start / end clocks and CU of the last launch
 #endif
@@ -1672,22 +1669,12 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     fetch_a(0, 0, 0);
     // unit u = u0 + R, R < 10 compile-time (u0 a multiple of 10): xi = R % 5, fragment set
     // R & 1; ring slot u % 4 (runtime)
-#if MVBEV_WINO_ILV
-#define WINO_MFMAS(AS, KW, XI)                                                                       \
-  _Pragma("unroll") for (int ct = 0; ct < 2; ++ct)                                                   \
-    acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][1], fb[KW][0], acc[ct][XI], 0, 0, 0); \
-  _Pragma("unroll") for (int ct = 0; ct < 2; ++ct)                                                   \
-    acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][1], acc[ct][XI], 0, 0, 0); \
-  _Pragma("unroll") for (int ct = 0; ct < 2; ++ct)                                                   \
-    acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][0], acc[ct][XI], 0, 0, 0);
-#else
 #define WINO_MFMAS(AS, KW, XI)                                                                       \
   _Pragma("unroll") for (int ct = 0; ct < 2; ++ct) {                                                 \
     acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][1], fb[KW][0], acc[ct][XI], 0, 0, 0); \
     acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][1], acc[ct][XI], 0, 0, 0); \
     acc[ct][XI] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][0], acc[ct][XI], 0, 0, 0); \
   }
-#endif
 #define WINO_UNIT(R)                                                                                 \
   do {                                                                                               \
     constexpr int XI = (R) % 5, P = (R) & 1;                                                          \
@@ -2186,22 +2173,12 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino43_kernel(const Args a) {
     fetch_b(0, 0);
     fetch_b(1, 0);
     fetch_a(0, 0, 0);
-#if MVBEV_WINO_ILV
-#define W43_MFMAS(AS, KW)                                                                              \
-  _Pragma("unroll") for (int ct = 0; ct < 2; ++ct)                                                     \
-    acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][1], fb[KW][0], acc[ct], 0, 0, 0);     \
-  _Pragma("unroll") for (int ct = 0; ct < 2; ++ct)                                                     \
-    acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][1], acc[ct], 0, 0, 0);     \
-  _Pragma("unroll") for (int ct = 0; ct < 2; ++ct)                                                     \
-    acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][0], acc[ct], 0, 0, 0);
-#else
 #define W43_MFMAS(AS, KW)                                                                              \
   _Pragma("unroll") for (int ct = 0; ct < 2; ++ct) {                                                   \
     acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][1], fb[KW][0], acc[ct], 0, 0, 0);     \
     acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][1], acc[ct], 0, 0, 0);     \
     acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[AS][ct][0], fb[KW][0], acc[ct], 0, 0, 0);     \
   }
-#endif
 #define W43_UNIT(R)                                                                                    \
   do {                                                                                                 \
     constexpr int P = (R) & 1, slot = (R) & 3, nslot = ((R) + 1) & 3; /* u0 % 4 == 0 */               \

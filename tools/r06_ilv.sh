@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round 6: interleaved MFMA order over the Cout blocks (MVBEV_WINO_ILV=1, bitwise the same sums) vs the default,
+# (MVBEV_WINO_ILV was removed after this measurement: DESIGN.md §4)
 # interleaved kbench at cfg2 / cfg3 (tools/r06_ilv.sh TAG)
 mkdir -p gpurun_out
 export TMPDIR=/tmp

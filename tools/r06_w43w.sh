@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round 6: the F(4,3) conv's 8 x 64 tile mode (MVBEV_W43_TILES_8X64) — parity, then interleaved kbench of conv1 in
+# (the wide-mode stages winoconv43w / conv2w43w and MVBEV_W43_TILES_8X64 were removed after this measurement: DESIGN.md §4)
 # F(3,3), F(4,3) 16 x 32 and F(4,3) 8 x 64 at cfg1 / cfg2 (tools/r06_w43w.sh TAG)
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -190,8 +190,9 @@ def test_fused_warp_transform_matches_two_pass(cfg):
     mc = torch.nn.Sequential(torch.nn.Conv2d(N * C + 2, 512, 3, padding=1), torch.nn.ReLU(),
                              torch.nn.Conv2d(512, 512, 3, padding=2, dilation=2), torch.nn.ReLU(),
                              torch.nn.Conv2d(512, 1, 3, padding=4, dilation=4, bias=False)).to(DEV)
-    fused = ProjectFuse(pm, up, grid, C, wino_conv1=True)
-    two = ProjectFuse(pm, up, grid, C, wino_conv1=True, wino_warp=False)
+    # (F(3,3)'s T: the F(4,3) engines' T43 has its own test, test_gpu_wino43.py)
+    fused = ProjectFuse(pm, up, grid, C, wino_conv1=True, wino43=False)
+    two = ProjectFuse(pm, up, grid, C, wino_conv1=True, wino_warp=False, wino43=False)
     assert fused.wino_warp and not two.wino_warp
     with torch.no_grad():
         got = fused.project_fuse(feats, mc)

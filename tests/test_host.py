@@ -326,3 +326,28 @@ def test_wgrad_chunk_lists_match_brute_force():
             assert lst[off[g]:off[g + 1]] == want, (lister.__name__, g)
     with pytest.raises(ValueError):
         ops.wgrad_wino_chunk_lists(torch.zeros(5, dtype=torch.int32), groups, B, H, W)
+
+
+def test_wino43_policy_per_config():
+    """ProjectFuse.wino43_pays (ABI 12400): conv1 takes F(4,3) where its 16-row tiles waste <= 3 % of the grid's rows
+    (configs 1, 3, 4, 5; config 2's 120 rows leave half a tile idle), conv2 -> conv3 only where the launch is also
+    >= 8 rounds of workgroups deep (configs 3, 4, 5 on 256 CUs); wino43=False / True override; the partial-sum
+    engines (view parts) never take it (conv1_partial reads F(3,3)'s T)."""
+    from mvdet_amd import ProjectFuse, synthetic
+    from mvdet_amd.geometry import projection_matrices
+    want = {1: (True, False), 2: (False, False), 3: (True, True), 4: (True, True), 5: (True, True)}
+    for cfg, (c1, c2) in want.items():
+        spec = synthetic.CONFIGS[cfg]
+        ds = spec["make"]()
+        pm, up, grid = projection_matrices(ds), tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+        e = ProjectFuse(pm, up, grid, 32)
+        e._cus["cpu"] = 256
+        H = grid[0]
+        assert (e.wino43_pays(H, spec["B"], "cpu"), e.wino43_pays(H, spec["B"], "cpu", deep=True)) == (c1, c2), cfg
+        assert not ProjectFuse(pm, up, grid, 32, wino43=False).wino43_pays(H, spec["B"], "cpu")
+        assert ProjectFuse(pm, up, grid, 32, wino43=True).wino43_pays(H, spec["B"], "cpu", deep=True)
+    ds = synthetic.CONFIGS[3]["make"]()
+    pm, up, grid = projection_matrices(ds), tuple(ds.upsample_shape), tuple(ds.reducedgrid_shape)
+    part = ProjectFuse(pm, up, grid, 32, parts=[(0, 0), (1, 0)], part_channels=32, all_views=False)
+    assert not part.wino43 and not part.wino43_pays(grid[0], 1, "cpu")
+

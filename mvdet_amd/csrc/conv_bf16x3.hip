@@ -170,7 +170,8 @@ template <> __device__ inline float ld<_Float16>(const _Float16* p) { return (fl
 
 // One finished 32x32 accumulator block (output channels co0..co0+31 at output pixel
 // (row, col) of this lane): bias, coord-term init, ReLU, store fp32 or split-bf16.
-template <bool RELU>
+// INIT = false: the caller folded the init term into its accumulators already (the row-Winograd convs' prologue)
+template <bool RELU, bool INIT = true>
 __device__ inline void store_block(const Args& a, int b, int row, int col, int co0, const floatx16& acc) {
   const int kh = (threadIdx.x & 63) >> 5;
   const int W = a.W;
@@ -191,7 +192,7 @@ __device__ inline void store_block(const Args& a, int b, int row, int col, int c
       const int co = co0 + (r & 3) + 8 * (r >> 2) + 4 * kh;
       float v = acc[r];
       if (a.bias) v += a.bias[co];
-      if (a.init) v += a.init[co * iplane + (int64_t)row * W + col];
+      if (INIT && a.init) v += a.init[co * iplane + (int64_t)row * W + col];
       if (RELU) v = v < 0.f ? 0.f : v;
       yp[co * cstride] = v;
     }
@@ -213,7 +214,7 @@ __device__ inline void store_block(const Args& a, int b, int row, int col, int c
         const int co = co0 + (r & 3) + 8 * (r >> 2) + 4 * kh;
         float v = acc[r];
         if (a.bias) v += a.bias[co];
-        if (a.init && valid) v += a.init[co * iplane + (int64_t)row * W + col];
+        if (INIT && a.init && valid) v += a.init[co * iplane + (int64_t)row * W + col];
         if (RELU) v = v < 0.f ? 0.f : v;
         v2[e] = v;
       }
@@ -743,7 +744,7 @@ __global__ __launch_bounds__(64 * kC1rGroups) void cout1_reduce_kernel(const flo
 
 // The ring kernel's output of a finished tile: rows row_base + pt * DIL (pt < 3) of this wave,
 // the lane's column, output channels cot * BN + cw + 32 ct (+ the fused Cout-1 partials).
-template <int DIL, bool RELU, bool P3>
+template <int DIL, bool RELU, bool P3, bool INIT = true>
 __device__ __attribute__((always_inline)) inline void ring_epilogue(const Args& a, int b, int row_base, int col,
                                                                    int cot, int cw, const floatx16 (&acc)[2][3],
                                                                    u32x4* lds) {
@@ -754,8 +755,40 @@ __device__ __attribute__((always_inline)) inline void ring_epilogue(const Args& 
     for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
       for (int pt = 0; pt < 3; ++pt)
-        store_block<RELU>(a, b, row_base + pt * DIL, col, cot * BN + cw + 32 * ct, acc[ct][pt]);
+        store_block<RELU, INIT>(a, b, row_base + pt * DIL, col, cot * BN + cw + 32 * ct, acc[ct][pt]);
   }
+}
+
+// The init term (conv1's coord term) of this lane's outputs: rows row_base + pt * DIL (pt < NPT), column col, output
+// channels co0 + 32 ct + (r & 3) + 8 (r >> 2) + 4 kh (store_block's lane layout); 0 outside the image.  Read at a
+// row-Winograd conv's start, beside its first DMAs, and folded into its accumulators: the epilogue's 6-8 rounds of
+// 16 dependent init loads per lane cost 3-4.5 % of conv1 (cfg2 1.37 vs 1.31 ms without them,
+// profiles/r06av_init_epilogue_cost.jsonl)
+template <int NPT, int NA>
+__device__ __attribute__((always_inline)) inline void load_init(const Args& a, int row_base, int dil, int col, int co0,
+                                                                floatx16 (&v)[2][NA]) {
+  static_assert(NPT <= NA, "rows");
+  // 32-bit element offsets from the uniform base (co * H * W < 2^31: the host's shape checks), one channel at a
+  // time over the rows (the 96-128 offsets of all of them at once cost registers the K loop needs)
+  const int kh = (threadIdx.x & 63) >> 5;
+  const uint32_t iplane = (uint32_t)a.H * (uint32_t)a.W;
+  bool ok[NPT];
+  uint32_t roff[NPT];
+#pragma unroll
+  for (int pt = 0; pt < NPT; ++pt) {
+    const int row = row_base + pt * dil;
+    ok[pt] = row < a.H && col < a.W;
+    roff[pt] = ok[pt] ? (uint32_t)row * (uint32_t)a.W + (uint32_t)col : 0u;
+  }
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const uint32_t co = (uint32_t)(co0 + 32 * ct + (r & 3) + 8 * (r >> 2) + 4 * kh);
+      const float* p = a.init + co * iplane;
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt) v[ct][pt][r] = ok[pt] ? p[roff[pt]] : 0.f;
+    }
 }
 
 // split tiles' raw partial sums: slot s = [24 floatx4 of a thread's 96 accumulators][RNT threads]
@@ -1489,6 +1522,20 @@ __global__ __launch_bounds__(256) void wino_rows_kernel(const WinoRowsArgs a) {
 #if MVBEV_WINO_STAMPS
 __device__ long long g_wino_stamps[4 * 65536];
 #endif
+// acc[.][0..2] = the init term (i0, i1, i2) of a wave's 3 rows -> M = (i0 - i2, (i1 + i2) / 2, (i2 - i1) / 2), element
+// by element in place (A^T M = (i0, i1, i2))
+__device__ __attribute__((always_inline)) inline void init_to_m(floatx16 (&acc)[2][wino::NXI]) {
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float i0 = acc[ct][0][r], i1 = acc[ct][1][r], i2 = acc[ct][2][r];
+      acc[ct][0][r] = i0 - i2;
+      acc[ct][1][r] = 0.5f * (i1 + i2);
+      acc[ct][2][r] = 0.5f * (i2 - i1);
+    }
+}
+
 template <bool RELU, int DIL, bool P3>
 __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   using namespace wino;
@@ -1611,6 +1658,13 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < NXI; ++j) acc[i][j] = floatx16{0};
+  // the init term i of the wave's 3 rows, loaded into acc[.][0..2] here (beside the first DMAs: the loads are older
+  // than them, so the prologue's counted wait covers them) and turned after the first barrier into
+  // M = (i0 - i2, (i1 + i2) / 2, (i2 - i1) / 2, 0, 0), whose A^T is exactly (i0, i1, i2): the epilogue adds nothing
+  // (ring_epilogue<..., INIT = false>)
+  if constexpr (!P3) {  // (conv2 -> conv3 partials: no init term)
+    if (a.init) load_init<3>(a, y0 + ring_base_row<DIL>(rg), DIL, x0 + l32, cot * BN + cw, acc);
+  }
   // one B set, refilled per kernel column right after its MFMAs (kw 0, 1 of the next unit after
   // the unit's barrier, kw 2 at the unit's start); two A sets alternating per kernel column
   bf16x8 fb[3][2];     // [kw][hi, lo]
@@ -1664,6 +1718,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if constexpr (!P3) init_to_m(acc);  // (zeros without an init term: no branch)
     fetch_b(0, 0);
     fetch_b(1, 0);
     fetch_a(0, 0, 0);
@@ -1723,6 +1778,8 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
 #undef WINO_UNIT
 #undef WINO_MFMAS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may land after the block exits
+  } else if constexpr (!P3) {  // no chunk in this tile (frustum): M = the init term's transform alone, as above
+    init_to_m(acc);
   }
   // y = A^T M per (Cout block, lane element): the 3 output rows of the wave's row tile
   floatx16 y[2][3];
@@ -1733,7 +1790,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino_kernel(const Args a) {
     y[ct][1] = m1 - m2 + 2.f * m3;
     y[ct][2] = m1 + m2 + 4.f * m3 + m4;
   }
-  ring_epilogue<DIL, RELU, P3>(a, b, y0 + ring_base_row<DIL>(rg), x0 + l32, cot, cw, y, lds);
+  ring_epilogue<DIL, RELU, P3, false>(a, b, y0 + ring_base_row<DIL>(rg), x0 + l32, cot, cw, y, lds);
 #if MVBEV_WINO_STAMPS
   __syncthreads();
   if (threadIdx.x < 4 && blockIdx.x < 65536) {  // lanes 0-3 store one field each (vector stores)
@@ -2114,6 +2171,8 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino43_kernel(const Args a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) y[i][r] = floatx16{0};
   }
+  if (a.init)  // the output rows start at the init term (the epilogue adds nothing: store_block<..., false>)
+    load_init<4>(a, y0 + w43::base_row<DIL>(rg), DIL, x0 + l32, cot * BN + cw, y);  // (y: [2][4])
   bf16x8 fb[3][2];
   bf16x8 fa[2][2][2];
   auto fetch_b = [&](int kw, int slot) __attribute__((always_inline)) {
@@ -2221,7 +2280,7 @@ __global__ __launch_bounds__(RNT, 1) void conv_wino43_kernel(const Args a) {
     for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
       for (int pt = 0; pt < 4; ++pt)
-        store_block<RELU>(a, b, row_base + pt * DIL, col, cot * BN + cw + 32 * ct, y[ct][pt]);
+        store_block<RELU, false>(a, b, row_base + pt * DIL, col, cot * BN + cw + 32 * ct, y[ct][pt]);
   }
 }
 

@@ -200,6 +200,12 @@ def main():
             "winoconv43": (lambda: ops.conv3x3_wino43(t43, wd1, pk43, 512, init=weng.coord_term(mc[0]), relu=True,
                                                       out=y1_43, group_mask=wgm43, tile_order=word43),
                            2.0 * B * ho * wo * 9 * N * C * 512),
+            # the same without the coord-term init in the epilogue (what reading init costs; not a valid conv1)
+            "winoconv_noinit": (lambda: ops.conv3x3_wino(wws.wino_t, wd1, weng.pack1w.get(mc[0].weight), 512,
+                                                         init=None, relu=True, out=wws.y1, group_mask=wgm,
+                                                         tile_order=weng.conv1_order(dev, 0, ho, B, grid=True)), None),
+            "winoconv43_noinit": (lambda: ops.conv3x3_wino43(t43, wd1, pk43, 512, init=None, relu=True, out=y1_43,
+                                                             group_mask=wgm43, tile_order=word43), None),
             "conv2w43": (lambda: ops.conv3x3_wino43_then_cout1_partials(t243, d2, pk243, 512, mc[2].bias, True,
                                                                         mc[4].weight, p3_43),
                          2.0 * B * ho * wo * 9 * 512 * 512),

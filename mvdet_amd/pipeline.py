@@ -116,6 +116,9 @@ class ProjectFuse:
     Its slots, masks, warps and T are those of ``len(parts)`` cameras of ``part_channels``; only conv1's
     channel map (and the module's ``cin``) refer to the views: slot s channel c is module channel
     ``view_s * channels + c0_s + c``.  Callers pass the features' channel slices as the cameras' features.
+
+    ``wino43`` (round 6, ABI 12400): the inference convs as row-Winograd F(4,3) — ``None`` (default) where
+    ``wino43_pays``, ``True`` wherever the whole-grid inference path applies, ``False`` never (F(3,3)).
     """
 
     def __init__(self, proj_mats: Sequence[torch.Tensor], src_hw: Tuple[int, int], grid_hw: Tuple[int, int],

@@ -225,9 +225,12 @@ __device__ inline void store_block(const Args& a, int b, int row, int col, int c
       lp[h] = (unsigned)__builtin_bit_cast(unsigned short, l0) |
               ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
     }
-    const unsigned s0 = kh ? hp[0] : lp[0], s1 = kh ? hp[1] : lp[1];
-    const unsigned r0 = (unsigned)__shfl_xor((int)s0, 32), r1 = (unsigned)__shfl_xor((int)s1, 32);
-    const u32x4 piece = kh ? u32x4{r0, r1, lp[0], lp[1]} : u32x4{hp[0], hp[1], r0, r1};
+    // v_permlane32_swap (the hi dword of the upper half-wave <-> the lo dword of the lower): lanes 0-31 then hold
+    // their hi and the upper lanes' hi (the group's 16-B hi piece), lanes 32-63 the lower lanes' lo and their own lo
+    // (the lo piece) — in VALU, without the two ds_bpermute round trips of a __shfl_xor(.., 32) per dword
+    const auto x0 = __builtin_amdgcn_permlane32_swap(hp[0], lp[0], false, false);
+    const auto x1 = __builtin_amdgcn_permlane32_swap(hp[1], lp[1], false, false);
+    const u32x4 piece = u32x4{x0[0], x1[0], x0[1], x1[1]};
     if (valid) {
       const int64_t g = co0 / 8 + q;
       u32x4* out = reinterpret_cast<u32x4*>(a.y);
